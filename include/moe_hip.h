@@ -1,0 +1,150 @@
+/*
+ * moe_hip.h -- C-ABI of libmoe_hip.so, the MI355X (gfx950) kernels of the
+ * context-aware MoE FFN that sits inside the RT-DETR encoder (AIFI) and
+ * decoder layers.
+ *
+ * Boundary.  The reference (scaleoutsystems/multimodal-MoE @2026-02-20) has no
+ * native code and no FFI: its operator API is the Python module
+ * src/models/vision/rtdetr.py (RtdetrTrainConfig :36-48, train_rtdetr_detector
+ * :77-95, eval_rtdetr_detector :98-128), whose engine (Ultralytics RTDETR,
+ * :58-64, :82-94, :112-127) owns the transformer FFN that this library
+ * replaces.  The MoE itself is planned but unwritten in the reference
+ * (notes/MoE_in_ZOD_Thesis_Proposal_revisedTimeline.txt:214-220: "expert
+ * modules, gating module, routing utilities (e.g., Top-k routing), and
+ * load-balancing terms"), with context as an additive router bias
+ * (notes/related_work.md:64-68) and the context id from
+ * scripts/add_solar_context_bins.py:87-107.  Each entry point below names the
+ * row of SURVEY.md section 8(a) it implements; INTEGRATION.md shows the ctypes
+ * binding the Python side uses.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a DEVICE pointer owned by the caller (torch allocator);
+ *     nothing is allocated, freed or synchronised inside; work is ordered on
+ *     `stream` only, so every call is hipGraph-capturable;
+ *   - bf16 tensors are passed as `const void*` (raw 16-bit storage);
+ *   - return 0 on success, a negative code on failure: -1 bad shape/argument,
+ *     -(1000 + hipError_t) for a HIP launch error; moe_last_error() returns a
+ *     thread-local message for the last failure;
+ *   - no host<->device copies: hist/offsets stay on the device.
+ *
+ * Shapes: T tokens, d model width (multiple of 128, <= 1024), E experts
+ * (1..64), k slots (1..8, k <= E), F expert hidden width (multiple of 128).
+ */
+#ifndef MOE_HIP_H_
+#define MOE_HIP_H_
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Number of 64-token router blocks for T tokens (size of the per-block
+ * workspaces below). */
+int moe_router_num_blocks(int T);
+
+/* a2+a3: router logits, fp32 softmax, top-k, gates, per-block
+ * routing counts and aux-loss partials, fused.
+ *   logits[t,e] = sum_c x[t,c] * wg[e,c] + ctx_bias[ctx_img[t / tokens_per_image], e]
+ *   probs = softmax(logits) (fp32), lse[t] = logsumexp(logits[t])
+ *   topk_idx[t,j], j=0..k-1: experts by descending prob, ties -> lower index
+ *   topk_w[t,j] = probs[t, idx] (normalize==0 or k==1) or renormalised to sum 1
+ *   local_rank[t,j] = #{t' < t in the same 64-token block : idx[t',j] == idx[t,j]}
+ *   block_counts[b, j, e] = #{t in block b : idx[t,j] == e}
+ *   aux_partials[b, e] = sum_{t in b} probs[t,e]; aux_partials[b, E] = sum lse^2
+ * x: bf16 [T,d]; wg: fp32 [E,d]; ctx_bias: fp32 [C,E] or NULL; ctx_img: int32
+ * [T/tokens_per_image] or NULL. Workspaces sized by moe_router_num_blocks(T). */
+int moe_router_topk_fwd(const void* x, const float* wg, const float* ctx_bias,
+                        const int32_t* ctx_img, int tokens_per_image,
+                        int T, int d, int E, int k, int normalize,
+                        int32_t* topk_idx, float* topk_w, float* probs, float* lse,
+                        int32_t* local_rank, int32_t* block_counts,
+                        float* aux_partials, hipStream_t stream);
+
+/* a4, index half: exclusive scans of the block counts.
+ * Assignment (t,j) to expert e has rank r = slot_base[j,e] + sum_{b'<b}
+ * block_counts[b',j,e] + local_rank[t,j] (slot-major, then token order; this
+ * is the capacity priority).  kept_e = min(hist_e, cap) (cap <= 0: no limit).
+ * Outputs: rank_base[b,j,e] (int32 [nblk,k,E]), hist[e] (unclipped counts),
+ * offsets[0..E] = exclusive scan of kept counts (offsets[E] = rows in Xp). */
+int moe_route_scan(const int32_t* block_counts, int nblk, int k, int E, int cap,
+                   int32_t* rank_base, int32_t* hist, int32_t* offsets,
+                   hipStream_t stream);
+
+/* a4, data half: scatter token rows into the expert-contiguous
+ * buffer.  pos[t,j] = offsets[e] + r if r < cap else -1;  xp[pos[t,j]] = x[t].
+ * x: bf16 [T,d]; xp: bf16 [>= offsets[E], d]; pos: int32 [T,k]. */
+int moe_permute_fwd(const void* x, const int32_t* topk_idx, const int32_t* local_rank,
+                    const int32_t* rank_base, const int32_t* offsets,
+                    int T, int d, int E, int k, int cap,
+                    void* xp, int32_t* pos, hipStream_t stream);
+
+/* a6: y[t] = sum_j topk_w[t,j] * yp[pos[t,j]] (pos<0 skipped),
+ * fp32 accumulation, bf16 out. */
+int moe_combine_fwd(const void* yp, const int32_t* pos, const float* topk_w,
+                    int T, int d, int k, void* y, hipStream_t stream);
+
+/* a7, combine transpose: dyp[pos[t,j]] = topk_w[t,j] * dy[t] (bf16)
+ * and dw[t,j] = <dy[t], yp[pos[t,j]]> (fp32; 0 when dropped). */
+int moe_combine_bwd(const void* dy, const void* yp, const int32_t* pos,
+                    const float* topk_w, int T, int d, int k,
+                    void* dyp, float* dw, hipStream_t stream);
+
+/* a7, dispatch transpose + router backward, fused per token:
+ *   dprobs[t,e]  = d(topk gates)/d(probs) applied to dw, plus dprob_bias[e]
+ *   dlogits[t,e] = softmax_bwd(probs[t], dprobs[t]) + zc * lse[t] * probs[t,e]
+ *   dx[t,c]      = sum_j dxp[pos[t,j], c] + sum_e dlogits[t,e] * wg[e,c]
+ * dprob_bias: fp32 [E] or NULL (load-balance grad); zc: one fp32 on the
+ * device (z-loss grad scale, 2 * dL/dz / T) or NULL for 0 -- a device scalar so
+ * that the backward never synchronises with the host.
+ * dx: bf16 [T,d]; dlogits: fp32 [T,E]. */
+int moe_token_bwd(const void* dxp, const int32_t* pos, const float* probs,
+                  const int32_t* topk_idx, const float* topk_w, const float* dw,
+                  const float* lse, const float* dprob_bias, const float* zc,
+                  const float* wg, int T, int d, int E, int k, int normalize,
+                  void* dx, float* dlogits, hipStream_t stream);
+
+/* Grouped GEMM data types / epilogues. */
+enum moe_dtype { MOE_BF16 = 0, MOE_FP8_E4M3 = 1 };
+enum moe_epilogue {
+  MOE_EPI_NONE = 0,      /* C = A.B                                   */
+  MOE_EPI_BIAS = 1,      /* C = A.B + bias[g, n]                      */
+  MOE_EPI_BIAS_RELU = 2, /* C = relu(A.B + bias[g, n])                */
+  MOE_EPI_RELU_MASK = 3  /* C = (A.B) * (aux[row, n] > 0)   (dgrad)   */
+};
+
+/* a5/a7, rows-grouped GEMM (expert FFN forward and dgrad):
+ * for every group g with rows [offsets[g], offsets[g+1]):
+ *   C[r, n] = epi( sum_k A[r, k] * B_g(k, n) ),   r in group g
+ * A: bf16 [rows, K] row-major.  B_g = b + g * K * N:
+ *   trans_b = 1: stored [N][K] (nn.Linear weight; forward),
+ *   trans_b = 0: stored [K][N] (dgrad through the same weight).
+ * bias: fp32 [G, N] (EPI_BIAS*); aux: bf16 [rows, N] (EPI_RELU_MASK).
+ * C: bf16 [rows, N].  K, N multiples of 64; offsets int32 [G+1] on device;
+ * max_rows is a host upper bound of offsets[G] (grid sizing, no sync). */
+int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c,
+                     const int32_t* offsets, int G, int max_rows, int N, int K,
+                     int trans_b, int epilogue, const float* bias, const void* aux,
+                     const float* scales, hipStream_t stream);
+
+/* a7, expert weight gradient (K = the group's rows):
+ *   C_g[m, n] = sum_{r in group g} X[r, m] * Y[r, n]     (fp32 [G, M, N])
+ *   colsum_g[m] = sum_{r in group g} X[r, m]             (fp32 [G, M], optional)
+ * X: bf16 [rows, M]; Y: bf16 [rows, N]; M, N multiples of 64.
+ * (dW2 = dYp^T H with colsum = db2; dW1 = dH^T Xp with colsum = db1.) */
+int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, float* c,
+                           float* colsum, const int32_t* offsets, int G,
+                           int M, int N, hipStream_t stream);
+
+/* Thread-local message for the last non-zero return code. */
+const char* moe_last_error(void);
+
+/* Library build identification ("moe_hip <version> gfx950"). */
+const char* moe_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MOE_HIP_H_ */

@@ -1,0 +1,178 @@
+// Token dispatch / combine kernels for gfx950.
+//
+// Geometry shared by all three: 16 lanes own one token; a lane moves the
+// token row in 16-B chunks (chunk = lane + 16 i), so one wave-instruction
+// touches four contiguous 256-B row segments; 256-thread blocks, 16 tokens
+// per block-iteration, grid-stride over tokens.  All three are HBM-bound
+// row movers: permute reads T rows and writes A rows; combine reads A rows
+// and writes T rows; combine_bwd reads T + A rows and writes A rows.
+#include "moe_common.h"
+
+namespace moe {
+
+__device__ __forceinline__ int assignment_pos(const int32_t* __restrict__ topk_idx,
+                                              const int32_t* __restrict__ local_rank,
+                                              const int32_t* __restrict__ rank_base,
+                                              const int32_t* __restrict__ offsets, int t,
+                                              int j, int E, int k, int cap) {
+  const int e = topk_idx[(size_t)t * k + j];
+  const int blk = t / kRouterBlockTokens;
+  const int r = rank_base[((size_t)blk * k + j) * E + e] + local_rank[(size_t)t * k + j];
+  return (cap <= 0 || r < cap) ? offsets[e] + r : -1;
+}
+
+__global__ __launch_bounds__(256) void permute_fwd_kernel(
+    const uint16_t* __restrict__ x, const int32_t* __restrict__ topk_idx,
+    const int32_t* __restrict__ local_rank, const int32_t* __restrict__ rank_base,
+    const int32_t* __restrict__ offsets, int T, int d, int E, int k, int cap,
+    uint16_t* __restrict__ xp, int32_t* __restrict__ pos) {
+  const int tid = threadIdx.x;
+  const int sub = tid & 15;
+  const int nchunk = d >> 7;
+  for (int tb = blockIdx.x * 16; tb < T; tb += gridDim.x * 16) {
+    const int t = tb + (tid >> 4);
+    if (t >= T) continue;
+    int pj[8];
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+      pj[j] = assignment_pos(topk_idx, local_rank, rank_base, offsets, t, j, E, k, cap);
+      if (sub == j) pos[(size_t)t * k + j] = pj[j];
+    }
+    const uint4* src = reinterpret_cast<const uint4*>(x + (size_t)t * d);
+    for (int c = 0; c < nchunk; ++c) {
+      const int ch = sub + 16 * c;
+      const uint4 v = src[ch];
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k)
+        if (pj[j] >= 0) reinterpret_cast<uint4*>(xp + (size_t)pj[j] * d)[ch] = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void combine_fwd_kernel(
+    const uint16_t* __restrict__ yp, const int32_t* __restrict__ pos,
+    const float* __restrict__ topk_w, int T, int d, int k, uint16_t* __restrict__ y) {
+  const int tid = threadIdx.x;
+  const int sub = tid & 15;
+  const int nchunk = d >> 7;
+  for (int tb = blockIdx.x * 16; tb < T; tb += gridDim.x * 16) {
+    const int t = tb + (tid >> 4);
+    if (t >= T) continue;
+    int pj[8];
+    float wj[8];
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+      pj[j] = pos[(size_t)t * k + j];
+      wj[j] = topk_w[(size_t)t * k + j];
+    }
+    for (int c = 0; c < nchunk; ++c) {
+      const int ch = sub + 16 * c;
+      float acc[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+        if (pj[j] < 0) continue;
+        float v[8];
+        unpack8(reinterpret_cast<const uint4*>(yp + (size_t)pj[j] * d)[ch], v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += wj[j] * v[i];
+      }
+      reinterpret_cast<uint4*>(y + (size_t)t * d)[ch] = pack8(acc);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void combine_bwd_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ yp,
+    const int32_t* __restrict__ pos, const float* __restrict__ topk_w, int T, int d, int k,
+    uint16_t* __restrict__ dyp, float* __restrict__ dw) {
+  const int tid = threadIdx.x;
+  const int sub = tid & 15;
+  const int nchunk = d >> 7;
+  for (int tb = blockIdx.x * 16; tb < T; tb += gridDim.x * 16) {
+    const int t = tb + (tid >> 4);
+    const bool valid = t < T;  // keep all 16 lanes of a group in the shuffles
+    int pj[8];
+    float wj[8], dot[8];
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+      pj[j] = valid ? pos[(size_t)t * k + j] : -1;
+      wj[j] = valid ? topk_w[(size_t)t * k + j] : 0.f;
+      dot[j] = 0.f;
+    }
+    for (int c = 0; c < nchunk; ++c) {
+      const int ch = sub + 16 * c;
+      float g[8];
+      if (valid) {
+        unpack8(reinterpret_cast<const uint4*>(dy + (size_t)t * d)[ch], g);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) g[i] = 0.f;
+      }
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+        if (pj[j] < 0) continue;
+        float v[8], o[8];
+        unpack8(reinterpret_cast<const uint4*>(yp + (size_t)pj[j] * d)[ch], v);
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s += g[i] * v[i];
+          o[i] = wj[j] * g[i];
+        }
+        dot[j] += s;
+        reinterpret_cast<uint4*>(dyp + (size_t)pj[j] * d)[ch] = pack8(o);
+      }
+    }
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+      const float s = group_sum<16>(dot[j]);
+      if (valid && sub == 0) dw[(size_t)t * k + j] = s;
+    }
+  }
+}
+
+}  // namespace moe
+
+using namespace moe;
+
+static int rows_grid(int T) {
+  int g = (T + 15) / 16;
+  return g > 4096 ? 4096 : (g < 1 ? 1 : g);
+}
+
+static int check_row_width(int d, const char* who) {
+  if (d <= 0 || d % 128 != 0 || d > 4096)
+    return fail(std::string(who) + ": d must be a multiple of 128 in [128,4096]");
+  return 0;
+}
+
+extern "C" int moe_permute_fwd(const void* x, const int32_t* topk_idx,
+                               const int32_t* local_rank, const int32_t* rank_base,
+                               const int32_t* offsets, int T, int d, int E, int k, int cap,
+                               void* xp, int32_t* pos, hipStream_t stream) {
+  if (check_row_width(d, "permute")) return -1;
+  if (E < 1 || E > 64 || k < 1 || k > 8) return fail("permute: need 1<=E<=64, 1<=k<=8");
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(permute_fwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
+                     static_cast<const uint16_t*>(x), topk_idx, local_rank, rank_base,
+                     offsets, T, d, E, k, cap, static_cast<uint16_t*>(xp), pos);
+  return check_launch("moe_permute_fwd");
+}
+
+extern "C" int moe_combine_fwd(const void* yp, const int32_t* pos, const float* topk_w,
+                               int T, int d, int k, void* y, hipStream_t stream) {
+  if (check_row_width(d, "combine")) return -1;
+  if (k < 1 || k > 8) return fail("combine: need 1<=k<=8");
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(combine_fwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
+                     static_cast<const uint16_t*>(yp), pos, topk_w, T, d, k,
+                     static_cast<uint16_t*>(y));
+  return check_launch("moe_combine_fwd");
+}
+
+extern "C" int moe_combine_bwd(const void* dy, const void* yp, const int32_t* pos,
+                               const float* topk_w, int T, int d, int k, void* dyp, float* dw,
+                               hipStream_t stream) {
+  if (check_row_width(d, "combine_bwd")) return -1;
+  if (k < 1 || k > 8) return fail("combine_bwd: need 1<=k<=8");
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(combine_bwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
+                     static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(yp), pos,
+                     topk_w, T, d, k, static_cast<uint16_t*>(dyp), dw);
+  return check_launch("moe_combine_bwd");
+}

@@ -1,0 +1,447 @@
+// Router kernels for gfx950.
+//
+//  router_topk_fwd : logits = x.Wg^T + ctx_bias[ctx(t)], fp32 softmax, top-k
+//                    (ties -> lower expert id), gates, per-64-token-block
+//                    routing counts + within-block ranks (wave ballot), aux
+//                    partials.  One 256-thread block = 4 waves = 64 tokens;
+//                    16 lanes per token, each lane owning d/16 channels read as
+//                    16-B chunks (a token row is read by 16 lanes, 4 tokens per
+//                    wave-instruction).
+//  route_scan      : one workgroup; per (slot, expert) column a wave-parallel
+//                    exclusive scan over router blocks, then hist / kept
+//                    offsets (capacity) / slot-major rank bases.
+//  token_bwd       : per token: gather-sum of dXp rows (dispatch transpose,
+//                    no atomics), gate + softmax + z-loss backward, and the
+//                    router's dx term dlogits.Wg, fused.
+#include "moe_common.h"
+
+namespace moe {
+
+// ---------------------------------------------------------------------------
+// router forward
+// ---------------------------------------------------------------------------
+template <int EMAX>
+__global__ __launch_bounds__(256) void router_topk_fwd_kernel(
+    const uint16_t* __restrict__ x, const float* __restrict__ wg,
+    const float* __restrict__ ctx_bias, const int32_t* __restrict__ ctx_img,
+    int tpi, int T, int d, int E, int k, int normalize,
+    int32_t* __restrict__ topk_idx, float* __restrict__ topk_w,
+    float* __restrict__ probs_out, float* __restrict__ lse_out,
+    int32_t* __restrict__ local_rank, int32_t* __restrict__ block_counts,
+    float* __restrict__ aux_partials) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* s_wg = reinterpret_cast<float*>(smem);               // [E][d]
+  int32_t* s_idx = reinterpret_cast<int32_t*>(s_wg + E * d);  // [64][k]
+  float* s_aux = reinterpret_cast<float*>(s_idx + 64 * 8);    // [4][EMAX+1]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int sub = lane & 15;   // lane within the token group
+  const int grp = lane >> 4;   // token group within the wave (0..3)
+  const int blk = blockIdx.x;
+
+  // Stage Wg (fp32 [E][d]) in LDS, 16 B per thread-iteration.
+  {
+    const int n4 = (E * d) >> 2;
+    const float4* src = reinterpret_cast<const float4*>(wg);
+    float4* dst = reinterpret_cast<float4*>(s_wg);
+    for (int i = tid; i < n4; i += 256) dst[i] = src[i];
+  }
+  for (int i = tid; i < 64 * 8; i += 256) s_idx[i] = -1;
+  __syncthreads();
+
+  const int nchunk = d >> 7;  // 16-B chunks per lane (d / 8 / 16)
+  float psum[EMAX + 1];
+#pragma unroll
+  for (int e = 0; e <= EMAX; ++e) psum[e] = 0.f;
+
+  for (int it = 0; it < 4; ++it) {
+    const int tl = wave * 16 + it * 4 + grp;  // token within block
+    const int t = blk * 64 + tl;
+    const bool valid = t < T;
+    float logit[EMAX];
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) logit[e] = 0.f;
+    if (valid) {
+      const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)t * d);
+      for (int c = 0; c < nchunk; ++c) {
+        const int ch = sub + 16 * c;  // chunk index within the row
+        float xv[8];
+        unpack8(xr[ch], xv);
+#pragma unroll
+        for (int e = 0; e < EMAX; ++e) {
+          if (e < E) {
+            const float4* w4 = reinterpret_cast<const float4*>(s_wg + e * d + ch * 8);
+            const float4 w0 = w4[0], w1 = w4[1];
+            logit[e] += xv[0] * w0.x + xv[1] * w0.y + xv[2] * w0.z + xv[3] * w0.w +
+                        xv[4] * w1.x + xv[5] * w1.y + xv[6] * w1.z + xv[7] * w1.w;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) logit[e] = group_sum<16>(logit[e]);
+    if (!valid) continue;  // uniform per 16-lane group; no more shuffles below
+
+    if (ctx_bias != nullptr && ctx_img != nullptr) {
+      const int c = ctx_img[t / tpi];
+      const float* cb = ctx_bias + (size_t)c * E;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e)
+        if (e < E) logit[e] += cb[e];
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e)
+      if (e < E) m = fmaxf(m, logit[e]);
+    float s = 0.f;
+    float p[EMAX];
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) {
+      p[e] = (e < E) ? expf(logit[e] - m) : 0.f;
+      s += p[e];
+    }
+    const float inv = 1.f / s;
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) p[e] *= inv;
+    const float lse = m + logf(s);
+
+    // top-k on logits (monotone in probs); strict '>' keeps the lower index on ties
+    uint64_t taken = 0;
+    int sel[8];
+    float selp[8];
+    float ssum = 0.f;
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+      int best = -1;
+      float bv = -INFINITY;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        if (e < E && !((taken >> e) & 1ull) && (best < 0 || logit[e] > bv)) {
+          bv = logit[e];
+          best = e;
+        }
+      }
+      taken |= 1ull << best;
+      sel[j] = best;
+      float pb = 0.f;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e)
+        if (e == best) pb = p[e];
+      selp[j] = pb;
+      ssum += pb;
+    }
+    const bool renorm = normalize && k > 1;
+    if (sub < k) {
+      int si = 0;
+      float sp = 0.f;
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k)
+        if (j == sub) { si = sel[j]; sp = selp[j]; }
+      topk_idx[(size_t)t * k + sub] = si;
+      topk_w[(size_t)t * k + sub] = renorm ? sp / ssum : sp;
+      s_idx[tl * 8 + sub] = si;
+    }
+    for (int e = sub; e < E; e += 16) {
+      float pv = 0.f;
+#pragma unroll
+      for (int q = 0; q < EMAX; ++q)
+        if (q == e) pv = p[q];
+      probs_out[(size_t)t * E + e] = pv;
+    }
+    if (sub == 0) lse_out[t] = lse;
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) psum[e] += p[e];
+    psum[EMAX] += lse * lse;
+  }
+
+  // Aux partials: every lane of a group holds its tokens' sums; combine the
+  // four groups of the wave, then the four waves, in a fixed order.
+#pragma unroll
+  for (int e = 0; e <= EMAX; ++e) {
+    float v = psum[e];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    psum[e] = v;
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e <= EMAX; ++e) s_aux[wave * (EMAX + 1) + e] = psum[e];
+  }
+  __syncthreads();
+  if (tid <= E) {
+    const int src = (tid == E) ? EMAX : tid;
+    float v = s_aux[src] + s_aux[(EMAX + 1) + src] + s_aux[2 * (EMAX + 1) + src] +
+              s_aux[3 * (EMAX + 1) + src];
+    aux_partials[(size_t)blk * (E + 1) + tid] = v;
+  }
+
+  // Within-block stable ranks: wave 0, lane l = token l of the block.
+  if (wave == 0) {
+    const int t = blk * 64 + lane;
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+      const int e_l = s_idx[lane * 8 + j];
+      int rank = 0;
+      for (int e = 0; e < E; ++e) {
+        const unsigned long long mask = __ballot(e_l == e);
+        if (e_l == e) rank = mbcnt(mask);
+        if (lane == 0) block_counts[((size_t)blk * k + j) * E + e] = __popcll(mask);
+      }
+      if (t < T) local_rank[(size_t)t * k + j] = rank;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// route scan (single workgroup)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void route_scan_kernel(
+    const int32_t* __restrict__ counts, int nblk, int k, int E, int cap,
+    int32_t* __restrict__ rank_base, int32_t* __restrict__ hist,
+    int32_t* __restrict__ offsets) {
+  __shared__ int32_t s_tot[8 * 64];
+  __shared__ int32_t s_slot[8 * 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nwave = blockDim.x >> 6;
+  const int ncol = k * E;
+
+  // Phase 0: column totals.
+  for (int col = wave; col < ncol; col += nwave) {
+    int s = 0;
+    for (int b = lane; b < nblk; b += 64) s += counts[(size_t)b * ncol + col];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) s_tot[col] = s;
+  }
+  __syncthreads();
+  // hist / kept offsets / slot bases (one wave, E <= 64 lanes).
+  if (wave == 0) {
+    int h = 0;
+    if (lane < E)
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+        if (lane < E) s_slot[j * E + lane] = h;
+        h += s_tot[j * E + lane];
+      }
+    const int kept = (lane < E) ? ((cap > 0 && h > cap) ? cap : h) : 0;
+    // inclusive wave scan of kept
+    int inc = kept;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
+    }
+    if (lane < E) {
+      hist[lane] = h;
+      offsets[lane] = inc - kept;
+    }
+    if (lane == E - 1) offsets[E] = inc;
+  }
+  __syncthreads();
+  // Phase 1: exclusive scan over blocks per column, plus the slot base.
+  for (int col = wave; col < ncol; col += nwave) {
+    int carry = s_slot[col];
+    for (int b0 = 0; b0 < nblk; b0 += 64) {
+      const int b = b0 + lane;
+      const int v = (b < nblk) ? counts[(size_t)b * ncol + col] : 0;
+      int inc = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += u;
+      }
+      if (b < nblk) rank_base[(size_t)b * ncol + col] = carry + inc - v;
+      carry += __shfl(inc, 63, 64);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// token backward: dispatch transpose + router backward
+// ---------------------------------------------------------------------------
+template <int EMAX>
+__global__ __launch_bounds__(256) void token_bwd_kernel(
+    const uint16_t* __restrict__ dxp, const int32_t* __restrict__ pos,
+    const float* __restrict__ probs, const int32_t* __restrict__ topk_idx,
+    const float* __restrict__ topk_w, const float* __restrict__ dw,
+    const float* __restrict__ lse, const float* __restrict__ dprob_bias,
+    const float* __restrict__ zc_ptr,
+    const float* __restrict__ wg, int T, int d, int E, int k, int normalize,
+    uint16_t* __restrict__ dx, float* __restrict__ dlogits) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* s_wg = reinterpret_cast<float*>(smem);  // [E][d]
+  const int tid = threadIdx.x;
+  {
+    const int n4 = (E * d) >> 2;
+    const float4* src = reinterpret_cast<const float4*>(wg);
+    float4* dst = reinterpret_cast<float4*>(s_wg);
+    for (int i = tid; i < n4; i += 256) dst[i] = src[i];
+  }
+  __syncthreads();
+
+  const int lane = tid & 63;
+  const int sub = lane & 15;
+  const int grp = lane >> 4;
+  const int nchunk = d >> 7;
+  const float zc = zc_ptr != nullptr ? *zc_ptr : 0.f;
+  // 16 tokens per block-iteration (4 waves x 4 groups); grid-stride.
+  for (int tb = blockIdx.x * 16; tb < T; tb += gridDim.x * 16) {
+    const int t = tb + (tid >> 6) * 4 + grp;
+    if (t >= T) continue;
+    // ---- router backward (every lane of the group, redundantly) ----
+    float p[EMAX], dp[EMAX];
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) {
+      p[e] = (e < E) ? probs[(size_t)t * E + e] : 0.f;
+      dp[e] = (e < E && dprob_bias != nullptr) ? dprob_bias[e] : 0.f;
+    }
+    int sel[8];
+    float selw[8], seldw[8];
+    float S = 0.f, wdw = 0.f;
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+      sel[j] = topk_idx[(size_t)t * k + j];
+      selw[j] = topk_w[(size_t)t * k + j];
+      seldw[j] = dw[(size_t)t * k + j];
+      wdw += selw[j] * seldw[j];
+      float pj = 0.f;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e)
+        if (e == sel[j]) pj = p[e];
+      S += pj;
+    }
+    const bool renorm = normalize && k > 1;
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+      const float g = renorm ? (seldw[j] - wdw) / S : seldw[j];
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e)
+        if (e == sel[j]) dp[e] += g;
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) dot += p[e] * dp[e];
+    const float zt = zc * lse[t];
+    float dl[EMAX];
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) dl[e] = p[e] * (dp[e] - dot) + zt * p[e];
+    for (int e = sub; e < E; e += 16) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < EMAX; ++q)
+        if (q == e) v = dl[q];
+      dlogits[(size_t)t * E + e] = v;
+    }
+    // ---- dx = sum_j dXp[pos] + dlogits . Wg ----
+    int pj[8];
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) pj[j] = pos[(size_t)t * k + j];
+    for (int c = 0; c < nchunk; ++c) {
+      const int ch = sub + 16 * c;
+      float acc[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+        if (pj[j] < 0) continue;
+        float v[8];
+        unpack8(reinterpret_cast<const uint4*>(dxp + (size_t)pj[j] * d)[ch], v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += v[i];
+      }
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        if (e < E) {
+          const float4* w4 = reinterpret_cast<const float4*>(s_wg + e * d + ch * 8);
+          const float4 w0 = w4[0], w1 = w4[1];
+          acc[0] += dl[e] * w0.x; acc[1] += dl[e] * w0.y;
+          acc[2] += dl[e] * w0.z; acc[3] += dl[e] * w0.w;
+          acc[4] += dl[e] * w1.x; acc[5] += dl[e] * w1.y;
+          acc[6] += dl[e] * w1.z; acc[7] += dl[e] * w1.w;
+        }
+      }
+      reinterpret_cast<uint4*>(dx + (size_t)t * d)[ch] = pack8(acc);
+    }
+  }
+}
+
+}  // namespace moe
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+using namespace moe;
+
+extern "C" int moe_router_num_blocks(int T) { return (T + 63) / 64; }
+
+// Raise the dynamic-LDS cap of a kernel when a launch needs more than 64 KiB.
+static void allow_lds(const void* fn, size_t bytes) {
+  if (bytes > 65536) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+static int emax_for(int E) { return E <= 8 ? 8 : E <= 16 ? 16 : E <= 32 ? 32 : 64; }
+
+extern "C" int moe_router_topk_fwd(const void* x, const float* wg, const float* ctx_bias,
+                                   const int32_t* ctx_img, int tokens_per_image, int T,
+                                   int d, int E, int k, int normalize, int32_t* topk_idx,
+                                   float* topk_w, float* probs, float* lse,
+                                   int32_t* local_rank, int32_t* block_counts,
+                                   float* aux_partials, hipStream_t stream) {
+  if (T < 0 || d <= 0 || d % 128 != 0 || d > 1024) return fail("router: d must be a multiple of 128 in [128,1024]");
+  if (E < 1 || E > 64 || k < 1 || k > 8 || k > E) return fail("router: need 1<=E<=64, 1<=k<=min(8,E)");
+  if ((size_t)E * d * 4 > 64 * 1024) return fail("router: E*d*4 must fit 64 KiB of LDS");
+  if (ctx_img != nullptr && tokens_per_image <= 0) return fail("router: tokens_per_image must be > 0");
+  if (T == 0) return 0;
+  const int nblk = moe_router_num_blocks(T);
+  const int em = emax_for(E);
+  const size_t shmem = (size_t)E * d * 4 + 64 * 8 * 4 + 4 * (em + 1) * 4;
+  const uint16_t* xb = static_cast<const uint16_t*>(x);
+#define LAUNCH_R(EM)                                                                       \
+  allow_lds(reinterpret_cast<const void*>(&router_topk_fwd_kernel<EM>), shmem);             \
+  hipLaunchKernelGGL(router_topk_fwd_kernel<EM>, dim3(nblk), dim3(256), shmem, stream, xb, \
+                     wg, ctx_bias, ctx_img, tokens_per_image, T, d, E, k, normalize,       \
+                     topk_idx, topk_w, probs, lse, local_rank, block_counts, aux_partials)
+  switch (em) {
+    case 8: LAUNCH_R(8); break;
+    case 16: LAUNCH_R(16); break;
+    case 32: LAUNCH_R(32); break;
+    default: LAUNCH_R(64); break;
+  }
+#undef LAUNCH_R
+  return check_launch("moe_router_topk_fwd");
+}
+
+extern "C" int moe_route_scan(const int32_t* block_counts, int nblk, int k, int E, int cap,
+                              int32_t* rank_base, int32_t* hist, int32_t* offsets,
+                              hipStream_t stream) {
+  if (E < 1 || E > 64 || k < 1 || k > 8) return fail("route_scan: need 1<=E<=64, 1<=k<=8");
+  if (nblk < 0) return fail("route_scan: nblk < 0");
+  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, stream, block_counts, nblk, k,
+                     E, cap, rank_base, hist, offsets);
+  return check_launch("moe_route_scan");
+}
+
+extern "C" int moe_token_bwd(const void* dxp, const int32_t* pos, const float* probs,
+                             const int32_t* topk_idx, const float* topk_w, const float* dw,
+                             const float* lse, const float* dprob_bias, const float* zc,
+                             const float* wg, int T, int d, int E, int k, int normalize,
+                             void* dx, float* dlogits, hipStream_t stream) {
+  if (d <= 0 || d % 128 != 0 || d > 1024) return fail("token_bwd: d must be a multiple of 128 in [128,1024]");
+  if (E < 1 || E > 64 || k < 1 || k > 8 || k > E) return fail("token_bwd: need 1<=E<=64, 1<=k<=min(8,E)");
+  if ((size_t)E * d * 4 > 64 * 1024) return fail("token_bwd: E*d*4 must fit 64 KiB of LDS");
+  if (T <= 0) return 0;
+  const int em = emax_for(E);
+  int grid = (T + 15) / 16;
+  if (grid > 2048) grid = 2048;
+  const size_t shmem = (size_t)E * d * 4;
+  const uint16_t* dxpb = static_cast<const uint16_t*>(dxp);
+  uint16_t* dxb = static_cast<uint16_t*>(dx);
+#define LAUNCH_B(EM)                                                                          \
+  allow_lds(reinterpret_cast<const void*>(&token_bwd_kernel<EM>), shmem);                    \
+  hipLaunchKernelGGL(token_bwd_kernel<EM>, dim3(grid), dim3(256), shmem, stream, dxpb, pos, \
+                     probs, topk_idx, topk_w, dw, lse, dprob_bias, zc, wg, T, d, E, k,      \
+                     normalize, dxb, dlogits)
+  switch (em) {
+    case 8: LAUNCH_B(8); break;
+    case 16: LAUNCH_B(16); break;
+    case 32: LAUNCH_B(32); break;
+    default: LAUNCH_B(64); break;
+  }
+#undef LAUNCH_B
+  return check_launch("moe_token_bwd");
+}

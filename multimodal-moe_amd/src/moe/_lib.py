@@ -1,0 +1,230 @@
+"""ctypes binding of libmoe_hip.so (C-ABI declared in include/moe_hip.h).
+
+This is the only place Python touches the HIP kernels.  Every wrapper takes
+torch tensors that must already live on the GPU, passes raw device pointers
+plus torch's current HIP stream, and raises ``MoEKernelError`` on a non-zero
+return code.  There is no fallback: if the library is missing or fails to
+load, ``lib()`` raises ``MoELibraryMissing`` (the GPU path fails loudly).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+_PKG = Path(__file__).resolve().parents[2]  # multimodal-moe_amd/
+LIB_PATH = Path(os.environ.get("MOE_HIP_LIB", _PKG / "lib" / "libmoe_hip.so"))
+
+MOE_BF16 = 0
+MOE_FP8_E4M3 = 1
+EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK = 0, 1, 2, 3
+
+# name -> (restype, argtypes); mirrors include/moe_hip.h
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+SIGNATURES = {
+    "moe_router_num_blocks": (_I, [_I]),
+    "moe_router_topk_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "moe_route_scan": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "moe_permute_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "moe_combine_fwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
+    "moe_combine_bwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P]),
+    "moe_token_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "moe_grouped_gemm": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "moe_grouped_gemm_wgrad": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "moe_last_error": (ctypes.c_char_p, []),
+    "moe_version": (ctypes.c_char_p, []),
+}
+
+
+class MoELibraryMissing(RuntimeError):
+    pass
+
+
+class MoEKernelError(RuntimeError):
+    pass
+
+
+_LIB = None
+
+
+def load_library(path: Path | str | None = None) -> ctypes.CDLL:
+    """Load the shared library and bind every exported symbol (no GPU needed)."""
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise MoELibraryMissing(
+            f"{p} not found: build it with `python multimodal-moe_amd/build_ext.py` "
+            "(or __graft_entry__.build()); the GPU MoE path has no fallback."
+        )
+    try:
+        cdll = ctypes.CDLL(str(p), mode=ctypes.RTLD_GLOBAL)
+    except OSError as e:  # pragma: no cover - depends on the box
+        raise MoELibraryMissing(f"failed to load {p}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(cdll, name)  # AttributeError if a symbol is missing
+        fn.restype = res
+        fn.argtypes = args
+    return cdll
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        _LIB = load_library()
+    return _LIB
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().moe_last_error()
+        raise MoEKernelError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def _need(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
+    if not t.is_cuda:
+        raise MoEKernelError(f"{name} must be a GPU tensor (HIP path has no CPU fallback)")
+    if t.dtype != dtype:
+        raise MoEKernelError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise MoEKernelError(f"{name} must be contiguous")
+
+
+# ---------------------------------------------------------------------------
+# thin typed wrappers (tensors in, tensors out; shapes checked on the host)
+# ---------------------------------------------------------------------------
+def router_num_blocks(T: int) -> int:
+    return (T + 63) // 64
+
+
+def router_topk_fwd(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize):
+    """Returns (topk_idx, topk_w, probs, lse, local_rank, block_counts, aux_partials)."""
+    T, d = x.shape
+    E = wg.shape[0]
+    _need(x, torch.bfloat16, "x")
+    _need(wg, torch.float32, "wg")
+    if wg.shape[1] != d:
+        raise MoEKernelError(f"wg shape {tuple(wg.shape)} does not match d={d}")
+    if ctx_bias is not None:
+        _need(ctx_bias, torch.float32, "ctx_bias")
+        if ctx_bias.shape[1] != E:
+            raise MoEKernelError("ctx_bias must be [C, E]")
+        _need(ctx_img, torch.int32, "ctx_img")
+        if tokens_per_image <= 0 or ctx_img.numel() * tokens_per_image < T:
+            raise MoEKernelError("ctx_img does not cover every token")
+    dev = x.device
+    nblk = router_num_blocks(T)
+    topk_idx = torch.empty((T, k), dtype=torch.int32, device=dev)
+    topk_w = torch.empty((T, k), dtype=torch.float32, device=dev)
+    probs = torch.empty((T, E), dtype=torch.float32, device=dev)
+    lse = torch.empty((T,), dtype=torch.float32, device=dev)
+    local_rank = torch.empty((T, k), dtype=torch.int32, device=dev)
+    block_counts = torch.empty((nblk, k, E), dtype=torch.int32, device=dev)
+    aux_partials = torch.empty((nblk, E + 1), dtype=torch.float32, device=dev)
+    rc = lib().moe_router_topk_fwd(
+        _ptr(x), _ptr(wg), _ptr(ctx_bias), _ptr(ctx_img) if ctx_bias is not None else None,
+        int(tokens_per_image), T, d, E, k, int(normalize),
+        _ptr(topk_idx), _ptr(topk_w), _ptr(probs), _ptr(lse), _ptr(local_rank),
+        _ptr(block_counts), _ptr(aux_partials), _stream())
+    _check(rc, "moe_router_topk_fwd")
+    return topk_idx, topk_w, probs, lse, local_rank, block_counts, aux_partials
+
+
+def route_scan(block_counts, cap):
+    nblk, k, E = block_counts.shape
+    _need(block_counts, torch.int32, "block_counts")
+    dev = block_counts.device
+    rank_base = torch.empty_like(block_counts)
+    hist = torch.empty((E,), dtype=torch.int32, device=dev)
+    offsets = torch.empty((E + 1,), dtype=torch.int32, device=dev)
+    rc = lib().moe_route_scan(_ptr(block_counts), nblk, k, E, int(cap), _ptr(rank_base),
+                              _ptr(hist), _ptr(offsets), _stream())
+    _check(rc, "moe_route_scan")
+    return rank_base, hist, offsets
+
+
+def permute_fwd(x, topk_idx, local_rank, rank_base, offsets, E, cap, rows_alloc):
+    T, d = x.shape
+    k = topk_idx.shape[1]
+    _need(x, torch.bfloat16, "x")
+    xp = torch.empty((max(rows_alloc, 1), d), dtype=torch.bfloat16, device=x.device)
+    pos = torch.empty((T, k), dtype=torch.int32, device=x.device)
+    rc = lib().moe_permute_fwd(_ptr(x), _ptr(topk_idx), _ptr(local_rank), _ptr(rank_base),
+                               _ptr(offsets), T, d, E, k, int(cap), _ptr(xp), _ptr(pos), _stream())
+    _check(rc, "moe_permute_fwd")
+    return xp, pos
+
+
+def combine_fwd(yp, pos, topk_w, T):
+    d = yp.shape[1]
+    k = pos.shape[1]
+    _need(yp, torch.bfloat16, "yp")
+    y = torch.empty((T, d), dtype=torch.bfloat16, device=yp.device)
+    rc = lib().moe_combine_fwd(_ptr(yp), _ptr(pos), _ptr(topk_w), T, d, k, _ptr(y), _stream())
+    _check(rc, "moe_combine_fwd")
+    return y
+
+
+def combine_bwd(dy, yp, pos, topk_w):
+    T, d = dy.shape
+    k = pos.shape[1]
+    _need(dy, torch.bfloat16, "dy")
+    _need(yp, torch.bfloat16, "yp")
+    dyp = torch.empty_like(yp)
+    dw = torch.empty((T, k), dtype=torch.float32, device=dy.device)
+    rc = lib().moe_combine_bwd(_ptr(dy), _ptr(yp), _ptr(pos), _ptr(topk_w), T, d, k,
+                               _ptr(dyp), _ptr(dw), _stream())
+    _check(rc, "moe_combine_bwd")
+    return dyp, dw
+
+
+def token_bwd(dxp, pos, probs, topk_idx, topk_w, dw, lse, dprob_bias, zc, wg, normalize):
+    T, k = pos.shape
+    E, d = wg.shape
+    dx = torch.empty((T, d), dtype=torch.bfloat16, device=wg.device)
+    dlogits = torch.empty((T, E), dtype=torch.float32, device=wg.device)
+    rc = lib().moe_token_bwd(_ptr(dxp), _ptr(pos), _ptr(probs), _ptr(topk_idx), _ptr(topk_w),
+                             _ptr(dw), _ptr(lse), _ptr(dprob_bias), _ptr(zc), _ptr(wg),
+                             T, d, E, k, int(normalize), _ptr(dx), _ptr(dlogits), _stream())
+    _check(rc, "moe_token_bwd")
+    return dx, dlogits
+
+
+def grouped_gemm(a, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None, aux=None,
+                 out=None):
+    _need(a, torch.bfloat16, "a")
+    _need(b, torch.bfloat16, "b")
+    if b.numel() != G * N * K:
+        raise MoEKernelError(f"grouped_gemm: b has {b.numel()} elements, want {G}*{N}*{K}")
+    if a.shape[1] != K or a.shape[0] < max_rows:
+        raise MoEKernelError("grouped_gemm: a must be [>=max_rows, K]")
+    c = out if out is not None else torch.empty((a.shape[0], N), dtype=torch.bfloat16, device=a.device)
+    rc = lib().moe_grouped_gemm(MOE_BF16, _ptr(a), _ptr(b), _ptr(c), _ptr(offsets), G, int(max_rows),
+                                N, K, int(trans_b), int(epilogue), _ptr(bias), _ptr(aux), None,
+                                _stream())
+    _check(rc, "moe_grouped_gemm")
+    return c
+
+
+def grouped_gemm_wgrad(x, y, offsets, G, want_colsum=True):
+    _need(x, torch.bfloat16, "x")
+    _need(y, torch.bfloat16, "y")
+    M, N = x.shape[1], y.shape[1]
+    c = torch.empty((G, M, N), dtype=torch.float32, device=x.device)
+    cs = torch.empty((G, M), dtype=torch.float32, device=x.device) if want_colsum else None
+    rc = lib().moe_grouped_gemm_wgrad(MOE_BF16, _ptr(x), _ptr(y), _ptr(c), _ptr(cs), _ptr(offsets),
+                                      G, M, N, _stream())
+    _check(rc, "moe_grouped_gemm_wgrad")
+    return c, cs

@@ -1,0 +1,94 @@
+"""MoE knobs and the ``--model`` spec grammar.
+
+The reference's ``--model`` flag names an Ultralytics hub weight
+(scripts/train_rtdetr.py:40, src/models/vision/rtdetr.py:39).  Here it names a
+local architecture spec (no network fetch), e.g.::
+
+    rtdetr-r50-moe8-top2          C2/C3: R50, 8 experts, top-2, bf16
+    rtdetr-r18-moe4-top1          C1: R18, 4 experts, top-1 (CPU plumbing)
+    rtdetr-r50-moe16-top2-ep8     C4: 16 experts sharded over 8 ranks
+    rtdetr-r50-moe32-top4-cf1.25-fp8   C5: capacity factor 1.25, fp8 experts
+    rtdetr-r50                    dense FFN (no MoE)
+"""
+from __future__ import annotations
+
+import math
+import re
+from dataclasses import dataclass, field
+
+
+@dataclass
+class MoEConfig:
+    num_experts: int = 8
+    top_k: int = 2
+    hidden: int = 1024            # expert FFN width (RT-DETR dim_feedforward)
+    capacity_factor: float = 0.0  # 0 -> no capacity limit (no drops)
+    normalize: bool = True        # renormalise top-k gates to sum 1 (k > 1)
+    expert_dtype: str = "bf16"    # "bf16" | "fp8"
+    lb_coef: float = 1e-2         # load-balance loss coefficient
+    z_coef: float = 1e-3          # router z-loss coefficient
+    num_contexts: int = 6         # solar bins + missing
+    use_context: bool = True
+    ep_size: int = 1              # expert-parallel group size (C4)
+    router_init_std: float = 0.02
+    ctx_init_scale: float = 0.5
+
+    def capacity(self, tokens: int) -> int:
+        if self.capacity_factor <= 0:
+            return 0
+        return int(math.ceil(self.capacity_factor * tokens * self.top_k / self.num_experts))
+
+
+@dataclass
+class ModelSpec:
+    backbone: str = "r50"          # r18 | r34 | r50 | r101
+    moe: MoEConfig | None = field(default_factory=MoEConfig)
+    num_decoder_layers: int | None = None  # default by backbone (6 for r50, 3 for r18)
+    raw: str = ""
+
+
+_SPEC_RE = re.compile(r"^rtdetr-(r18|r34|r50|r101)((?:-[a-z0-9.]+)*)$")
+
+
+def parse_moe_spec(spec: str) -> ModelSpec:
+    """Parse ``rtdetr-<backbone>[-moe<E>][-top<k>][-cf<f>][-fp8][-ep<n>][-dec<L>]``."""
+    s = spec.strip().lower()
+    if s.endswith(".pt") or s.endswith(".pth"):
+        raise ValueError(f"{spec!r} is a weights file, not an architecture spec")
+    m = _SPEC_RE.match(s)
+    if not m:
+        raise ValueError(
+            f"unknown model spec {spec!r}; expected e.g. 'rtdetr-r50-moe8-top2' "
+            "(hub weight names such as 'rtdetr-l.pt' need a network fetch and are not supported)")
+    out = ModelSpec(backbone=m.group(1), moe=None, raw=spec)
+    moe = None
+    for tok in [t for t in m.group(2).split("-") if t]:
+        if tok.startswith("moe"):
+            moe = moe or MoEConfig()
+            moe.num_experts = int(tok[3:])
+        elif tok.startswith("top"):
+            moe = moe or MoEConfig()
+            moe.top_k = int(tok[3:])
+        elif tok.startswith("cf"):
+            moe = moe or MoEConfig()
+            moe.capacity_factor = float(tok[2:])
+        elif tok == "fp8":
+            moe = moe or MoEConfig()
+            moe.expert_dtype = "fp8"
+        elif tok == "noctx":
+            moe = moe or MoEConfig()
+            moe.use_context = False
+        elif tok.startswith("ep"):
+            moe = moe or MoEConfig()
+            moe.ep_size = int(tok[2:])
+        elif tok.startswith("dec"):
+            out.num_decoder_layers = int(tok[3:])
+        else:
+            raise ValueError(f"unknown token {tok!r} in model spec {spec!r}")
+    if moe is not None:
+        if moe.top_k > moe.num_experts:
+            raise ValueError("top_k must be <= num_experts")
+        if moe.num_experts % moe.ep_size:
+            raise ValueError("num_experts must be divisible by ep_size")
+    out.moe = moe
+    return out

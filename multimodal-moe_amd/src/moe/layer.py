@@ -1,0 +1,73 @@
+"""MoEFFN: the routed expert FFN that replaces the dense FFN of the RT-DETR
+AIFI encoder layer and of every decoder layer.
+
+Parameters (fp32 masters; the GPU path computes in bf16 with fp32 accumulate):
+  router.weight wg [E, d]      router.ctx_bias [C, E]  (context as additive logit bias)
+  w1 [E, F, d], b1 [E, F]      w2 [E, d, F], b2 [E, d]  (nn.Linear layout per expert)
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+from .config import MoEConfig
+
+
+class MoEFFN(nn.Module):
+    def __init__(self, d_model: int, cfg: MoEConfig):
+        super().__init__()
+        self.cfg = cfg
+        E, F = cfg.num_experts, cfg.hidden
+        self.d_model = d_model
+        self.ep_size = max(1, cfg.ep_size)
+        self.ep_group = None          # set by parallel.expert_parallel for C4
+        E_local = E // self.ep_size
+        self.wg = nn.Parameter(torch.randn(E, d_model) * cfg.router_init_std)
+        self.ctx_bias = nn.Parameter(torch.randn(cfg.num_contexts, E) * cfg.ctx_init_scale) \
+            if cfg.use_context else None
+        bound1 = 1.0 / math.sqrt(d_model)
+        bound2 = 1.0 / math.sqrt(F)
+        self.w1 = nn.Parameter(torch.empty(E_local, F, d_model).uniform_(-bound1, bound1))
+        self.b1 = nn.Parameter(torch.empty(E_local, F).uniform_(-bound1, bound1))
+        self.w2 = nn.Parameter(torch.empty(E_local, d_model, F).uniform_(-bound2, bound2))
+        self.b2 = nn.Parameter(torch.empty(E_local, d_model).uniform_(-bound2, bound2))
+        for p in (self.w1, self.b1, self.w2, self.b2):
+            p.expert_parallel = self.ep_size > 1  # excluded from the DP all-reduce
+        self.last_aux = None   # (lb_raw, z_raw) of the last forward
+        self.last_hist = None  # int32 [E] expert histogram of the last forward
+
+    def forward(self, x: torch.Tensor, ctx_img: torch.Tensor | None) -> torch.Tensor:
+        """x [B, L, d] (image-major tokens), ctx_img int [B] -> [B, L, d]."""
+        B, L, d = x.shape
+        cfg = self.cfg
+        flat = x.reshape(B * L, d)
+        T = B * L
+        cap = cfg.capacity(T)
+        cb = self.ctx_bias if (self.ctx_bias is not None and ctx_img is not None) else None
+        ci = ctx_img.to(torch.int32).contiguous() if cb is not None else None
+        if flat.is_cuda:
+            if self.ep_size > 1:
+                from .ep import moe_ffn_ep
+                y, lb, z, hist = moe_ffn_ep(self, flat, cb, ci, L, cap)
+            else:
+                from .ops import moe_ffn_hip
+                y, lb, z, hist = moe_ffn_hip(flat, self.wg, cb, self.w1, self.b1, self.w2, self.b2,
+                                             ci, L, cfg.top_k, cfg.normalize, cap)
+            y = y.to(x.dtype)
+        else:
+            if self.ep_size > 1:
+                raise RuntimeError("expert parallelism needs GPU tensors")
+            from .eager import moe_ffn_eager
+            y, lb, z, hist = moe_ffn_eager(flat, self.wg, cb, self.w1, self.b1, self.w2, self.b2,
+                                           ci, L, cfg.top_k, cfg.normalize, cap)
+        self.last_aux = (lb, z)
+        self.last_hist = hist
+        return y.view(B, L, d)
+
+    def aux_loss(self) -> torch.Tensor | None:
+        if self.last_aux is None:
+            return None
+        lb, z = self.last_aux
+        return self.cfg.lb_coef * lb + self.cfg.z_coef * z

@@ -1,0 +1,128 @@
+"""PResNet-vd backbone (RT-DETR's R18/R34/R50/R101 body).
+
+The reference trains RT-DETR through third-party engines that are absent here
+(Ultralytics ``RTDETR``: src/models/vision/rtdetr.py:58-64, :82-94; RT-DETRv2
+``rtdetrv2_r50vd`` configs named at scripts/train_rtdetr_thirdparty.py:30-35).
+This is the build's own body for those configs:
+ResNet-D stem (three 3x3 convs), AvgPool shortcut downsampling, stages
+returning strides 8/16/32.  Runs channels_last under bf16 autocast (MIOpen
+convolutions); nothing here is on the MoE hot path.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+_DEPTHS = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3], 50: [3, 4, 6, 3], 101: [3, 4, 23, 3]}
+
+
+class FrozenBatchNorm2d(nn.Module):
+    """BatchNorm with fixed statistics and affine (RT-DETR ``freeze_norm``)."""
+
+    def __init__(self, n, eps=1e-5):
+        super().__init__()
+        self.register_buffer("weight", torch.ones(n))
+        self.register_buffer("bias", torch.zeros(n))
+        self.register_buffer("running_mean", torch.zeros(n))
+        self.register_buffer("running_var", torch.ones(n))
+        self.eps = eps
+
+    def forward(self, x):
+        scale = self.weight * (self.running_var + self.eps).rsqrt()
+        shift = self.bias - self.running_mean * scale
+        return x * scale.view(1, -1, 1, 1).to(x.dtype) + shift.view(1, -1, 1, 1).to(x.dtype)
+
+
+def _norm(n, frozen):
+    return FrozenBatchNorm2d(n) if frozen else nn.BatchNorm2d(n)
+
+
+class ConvNormLayer(nn.Module):
+    def __init__(self, cin, cout, k, s, act=None, frozen=False):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, k, s, (k - 1) // 2, bias=False)
+        self.norm = _norm(cout, frozen)
+        self.act = nn.ReLU(inplace=True) if act == "relu" else (nn.SiLU(inplace=True) if act == "silu" else nn.Identity())
+
+    def forward(self, x):
+        return self.act(self.norm(self.conv(x)))
+
+
+class _Shortcut(nn.Module):
+    """ResNet-D shortcut: AvgPool(2) then 1x1 conv when downsampling."""
+
+    def __init__(self, cin, cout, stride, frozen):
+        super().__init__()
+        self.pool = nn.AvgPool2d(2, 2, 0, ceil_mode=True) if stride == 2 else nn.Identity()
+        self.conv = ConvNormLayer(cin, cout, 1, 1, frozen=frozen)
+
+    def forward(self, x):
+        return self.conv(self.pool(x))
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin, cout, stride, shortcut, frozen):
+        super().__init__()
+        self.short = None if shortcut else _Shortcut(cin, cout, stride, frozen)
+        self.branch2a = ConvNormLayer(cin, cout, 3, stride, "relu", frozen)
+        self.branch2b = ConvNormLayer(cout, cout, 3, 1, None, frozen)
+
+    def forward(self, x):
+        out = self.branch2b(self.branch2a(x))
+        return F.relu(out + (x if self.short is None else self.short(x)))
+
+
+class BottleNeck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, cout, stride, shortcut, frozen):
+        super().__init__()
+        width = cout
+        self.branch2a = ConvNormLayer(cin, width, 1, 1, "relu", frozen)
+        self.branch2b = ConvNormLayer(width, width, 3, stride, "relu", frozen)
+        self.branch2c = ConvNormLayer(width, cout * 4, 1, 1, None, frozen)
+        self.short = None if shortcut else _Shortcut(cin, cout * 4, stride, frozen)
+
+    def forward(self, x):
+        out = self.branch2c(self.branch2b(self.branch2a(x)))
+        return F.relu(out + (x if self.short is None else self.short(x)))
+
+
+class PResNet(nn.Module):
+    def __init__(self, depth=50, return_idx=(1, 2, 3), freeze_norm=False):
+        super().__init__()
+        block = BottleNeck if depth >= 50 else BasicBlock
+        c = 64
+        self.stem = nn.Sequential(
+            ConvNormLayer(3, c // 2, 3, 2, "relu", freeze_norm),
+            ConvNormLayer(c // 2, c // 2, 3, 1, "relu", freeze_norm),
+            ConvNormLayer(c // 2, c, 3, 1, "relu", freeze_norm),
+        )
+        self.pool = nn.MaxPool2d(3, 2, 1)
+        ch_in = c
+        self.stages = nn.ModuleList()
+        self.out_channels = []
+        for i, (n, cout) in enumerate(zip(_DEPTHS[depth], [64, 128, 256, 512])):
+            stride = 1 if i == 0 else 2
+            blocks = []
+            for b in range(n):
+                shortcut = b > 0 or (i == 0 and block is BasicBlock)
+                blocks.append(block(ch_in, cout, stride if b == 0 else 1, shortcut, freeze_norm))
+                ch_in = cout * block.expansion
+            self.stages.append(nn.Sequential(*blocks))
+            self.out_channels.append(ch_in)
+        self.return_idx = list(return_idx)
+        self.out_channels = [self.out_channels[i] for i in self.return_idx]
+        self.out_strides = [[4, 8, 16, 32][i] for i in self.return_idx]
+
+    def forward(self, x):
+        x = self.pool(self.stem(x))
+        outs = []
+        for i, stage in enumerate(self.stages):
+            x = stage(x)
+            if i in self.return_idx:
+                outs.append(x)
+        return outs

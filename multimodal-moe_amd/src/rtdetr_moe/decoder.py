@@ -1,0 +1,192 @@
+"""RT-DETR transformer decoder: IoU-free query selection (top-300 encoder
+tokens), L decoder layers of {self-attention, multi-scale deformable
+cross-attention, (MoE) FFN} with iterative box refinement.  The FFN of every
+decoder layer is the MoE slot; deformable attention
+samples 4 points x 3 levels x 8 heads with bilinear grid_sample (SURVEY.md
+8(f).1 names it the next HIP-kernel candidate)."""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+from ..moe.config import MoEConfig
+from .encoder import make_ffn
+
+
+def inverse_sigmoid(x, eps=1e-5):
+    x = x.clamp(min=0.0, max=1.0)
+    return torch.log(x.clamp(min=eps) / (1 - x).clamp(min=eps))
+
+
+class MLP(nn.Module):
+    def __init__(self, din, dh, dout, n):
+        super().__init__()
+        dims = [din] + [dh] * (n - 1)
+        self.layers = nn.ModuleList(nn.Linear(a, b) for a, b in zip(dims, dims[1:] + [dout]))
+
+    def forward(self, x):
+        for i, layer in enumerate(self.layers):
+            x = layer(x)
+            if i < len(self.layers) - 1:
+                x = F.relu(x)
+        return x
+
+
+def deformable_attention_core(value, shapes, sampling_locations, attention_weights):
+    """value [B, S, H, Dh]; sampling_locations [B, Q, H, L, P, 2] in [0,1];
+    attention_weights [B, Q, H, L, P] -> [B, Q, H*Dh]."""
+    B, _, H, Dh = value.shape
+    _, Q, _, L, P, _ = sampling_locations.shape
+    splits = [h * w for h, w in shapes]
+    values = value.split(splits, dim=1)
+    grids = 2.0 * sampling_locations - 1.0
+    sampled = []
+    for lvl, (h, w) in enumerate(shapes):
+        v = values[lvl].flatten(2).transpose(1, 2).reshape(B * H, Dh, h, w)
+        g = grids[:, :, :, lvl].transpose(1, 2).flatten(0, 1)            # [B*H, Q, P, 2]
+        sampled.append(F.grid_sample(v, g.to(v.dtype), mode="bilinear", padding_mode="zeros",
+                                     align_corners=False))              # [B*H, Dh, Q, P]
+    aw = attention_weights.transpose(1, 2).reshape(B * H, 1, Q, L * P)
+    out = (torch.stack(sampled, dim=-2).flatten(-2) * aw.to(sampled[0].dtype)).sum(-1)
+    return out.view(B, H * Dh, Q).transpose(1, 2)
+
+
+class MSDeformableAttention(nn.Module):
+    def __init__(self, d=256, nhead=8, nlevels=3, npoints=4, offset_scale=0.5):
+        super().__init__()
+        self.d, self.nhead, self.nlevels, self.npoints = d, nhead, nlevels, npoints
+        self.offset_scale = offset_scale
+        self.sampling_offsets = nn.Linear(d, nhead * nlevels * npoints * 2)
+        self.attention_weights = nn.Linear(d, nhead * nlevels * npoints)
+        self.value_proj = nn.Linear(d, d)
+        self.output_proj = nn.Linear(d, d)
+        self._reset()
+
+    def _reset(self):
+        nn.init.zeros_(self.sampling_offsets.weight)
+        thetas = torch.arange(self.nhead, dtype=torch.float32) * (2.0 * math.pi / self.nhead)
+        grid = torch.stack([thetas.cos(), thetas.sin()], -1)
+        grid = grid / grid.abs().max(-1, keepdim=True).values
+        grid = grid.view(self.nhead, 1, 1, 2).tile(1, self.nlevels, self.npoints, 1)
+        grid *= torch.arange(1, self.npoints + 1, dtype=torch.float32).view(1, 1, -1, 1)
+        with torch.no_grad():
+            self.sampling_offsets.bias.copy_(grid.flatten())
+        nn.init.zeros_(self.attention_weights.weight)
+        nn.init.zeros_(self.attention_weights.bias)
+        nn.init.xavier_uniform_(self.value_proj.weight)
+        nn.init.zeros_(self.value_proj.bias)
+        nn.init.xavier_uniform_(self.output_proj.weight)
+        nn.init.zeros_(self.output_proj.bias)
+
+    def forward(self, query, ref_boxes, value, shapes):
+        """query [B,Q,d]; ref_boxes [B,Q,4] (cx,cy,w,h in [0,1]); value [B,S,d]."""
+        B, Q, _ = query.shape
+        H, L, P = self.nhead, self.nlevels, self.npoints
+        v = self.value_proj(value).view(B, value.shape[1], H, self.d // H)
+        off = self.sampling_offsets(query).view(B, Q, H, L, P, 2)
+        aw = F.softmax(self.attention_weights(query).view(B, Q, H, L * P).float(), -1).view(B, Q, H, L, P)
+        ref = ref_boxes[:, :, None, None, None, :]
+        loc = ref[..., :2] + off / P * ref[..., 2:] * self.offset_scale
+        return self.output_proj(deformable_attention_core(v, shapes, loc, aw))
+
+
+class TransformerDecoderLayer(nn.Module):
+    def __init__(self, d=256, nhead=8, hidden=1024, nlevels=3, npoints=4, moe: MoEConfig | None = None):
+        super().__init__()
+        self.self_attn = nn.MultiheadAttention(d, nhead, batch_first=True)
+        self.norm1 = nn.LayerNorm(d)
+        self.cross_attn = MSDeformableAttention(d, nhead, nlevels, npoints)
+        self.norm2 = nn.LayerNorm(d)
+        self.ffn = make_ffn(d, hidden, moe, act="relu")
+        self.norm3 = nn.LayerNorm(d)
+
+    def forward(self, tgt, ref_boxes, memory, shapes, query_pos, ctx):
+        q = k = tgt + query_pos
+        tgt = self.norm1(tgt + self.self_attn(q, k, tgt, need_weights=False)[0])
+        tgt = self.norm2(tgt + self.cross_attn(tgt + query_pos, ref_boxes, memory, shapes))
+        tgt = self.norm3(tgt + self.ffn(tgt, ctx))
+        return tgt
+
+
+class RTDETRDecoder(nn.Module):
+    def __init__(self, num_classes=1, hidden=256, feat_channels=(256, 256, 256), feat_strides=(8, 16, 32),
+                 num_queries=300, num_layers=6, nhead=8, dim_feedforward=1024, npoints=4,
+                 moe: MoEConfig | None = None):
+        super().__init__()
+        self.hidden = hidden
+        self.num_queries = num_queries
+        self.num_classes = num_classes
+        self.nlevels = len(feat_channels)
+        self.input_proj = nn.ModuleList(
+            [nn.Sequential(nn.Conv2d(c, hidden, 1, bias=False), nn.BatchNorm2d(hidden)) for c in feat_channels])
+        self.layers = nn.ModuleList([
+            TransformerDecoderLayer(hidden, nhead, dim_feedforward, self.nlevels, npoints, moe)
+            for _ in range(num_layers)])
+        self.query_pos_head = MLP(4, 2 * hidden, hidden, 2)
+        self.enc_output = nn.Sequential(nn.Linear(hidden, hidden), nn.LayerNorm(hidden))
+        self.enc_score_head = nn.Linear(hidden, num_classes)
+        self.enc_bbox_head = MLP(hidden, hidden, 4, 3)
+        self.dec_score_head = nn.ModuleList([nn.Linear(hidden, num_classes) for _ in range(num_layers)])
+        self.dec_bbox_head = nn.ModuleList([MLP(hidden, hidden, 4, 3) for _ in range(num_layers)])
+        self._anchor_cache = {}
+        self._reset()
+
+    def _reset(self):
+        bias = -math.log((1 - 0.01) / 0.01)
+        nn.init.constant_(self.enc_score_head.bias, bias)
+        for h in self.dec_score_head:
+            nn.init.constant_(h.bias, bias)
+        for m in [self.enc_bbox_head, *self.dec_bbox_head]:
+            nn.init.zeros_(m.layers[-1].weight)
+            nn.init.zeros_(m.layers[-1].bias)
+
+    def _anchors(self, shapes, device, dtype, grid_size=0.05, eps=1e-2):
+        key = (tuple(shapes), device, dtype)
+        if key not in self._anchor_cache:
+            anchors = []
+            for lvl, (h, w) in enumerate(shapes):
+                gy, gx = torch.meshgrid(torch.arange(h, dtype=torch.float32), torch.arange(w, dtype=torch.float32),
+                                        indexing="ij")
+                xy = torch.stack([(gx + 0.5) / w, (gy + 0.5) / h], -1)
+                wh = torch.full_like(xy, grid_size * 2.0 ** lvl)
+                anchors.append(torch.cat([xy, wh], -1).reshape(-1, 4))
+            a = torch.cat(anchors, 0)[None].to(device)
+            valid = ((a > eps) & (a < 1 - eps)).all(-1, keepdim=True)
+            a = torch.log(a / (1 - a))
+            a = torch.where(valid, a, torch.full_like(a, float("inf")))
+            self._anchor_cache[key] = (a.to(dtype), valid.to(dtype))
+        return self._anchor_cache[key]
+
+    def forward(self, feats, ctx):
+        proj = [p(f) for p, f in zip(self.input_proj, feats)]
+        shapes = [tuple(f.shape[-2:]) for f in proj]
+        memory = torch.cat([f.flatten(2).permute(0, 2, 1) for f in proj], 1).contiguous()  # [B, S, d]
+        B = memory.shape[0]
+        anchors, valid = self._anchors(shapes, memory.device, torch.float32)
+        out_mem = self.enc_output(valid.to(memory.dtype) * memory)
+        enc_logits = self.enc_score_head(out_mem)
+        enc_coord = self.enc_bbox_head(out_mem).float() + anchors
+        topk = torch.topk(enc_logits.detach().float().max(-1).values, self.num_queries, dim=1).indices
+        ref_unact = enc_coord.gather(1, topk[..., None].expand(-1, -1, 4))
+        enc_topk_boxes = ref_unact.sigmoid()
+        enc_topk_logits = enc_logits.gather(1, topk[..., None].expand(-1, -1, enc_logits.shape[-1]))
+        tgt = out_mem.gather(1, topk[..., None].expand(-1, -1, out_mem.shape[-1])).detach()
+        ref_detach = ref_unact.detach().sigmoid()
+        ref = ref_detach
+        dec_logits, dec_boxes = [], []
+        for i, layer in enumerate(self.layers):
+            query_pos = self.query_pos_head(ref_detach.to(tgt.dtype))
+            tgt = layer(tgt, ref_detach, memory, shapes, query_pos, ctx)
+            delta = self.dec_bbox_head[i](tgt).float()
+            inter = (delta + inverse_sigmoid(ref_detach)).sigmoid()
+            dec_logits.append(self.dec_score_head[i](tgt))
+            dec_boxes.append(inter if i == 0 else (delta + inverse_sigmoid(ref)).sigmoid())
+            ref = inter
+            ref_detach = inter.detach()
+        out = {"pred_logits": dec_logits[-1], "pred_boxes": dec_boxes[-1],
+               "aux_outputs": [{"pred_logits": a, "pred_boxes": b} for a, b in zip(dec_logits[:-1], dec_boxes[:-1])],
+               "enc_outputs": {"pred_logits": enc_topk_logits, "pred_boxes": enc_topk_boxes}}
+        return out

@@ -1,0 +1,136 @@
+"""RT-DETR HybridEncoder: AIFI transformer layer on S5 (its FFN is the MoE
+slot) + CCFM cross-scale fusion (FPN + PAN of
+CSPRep layers).  Dimensions follow Appendix A of SURVEY.md (hidden 256, FFN
+1024, 8 heads, one encoder layer on stride 32)."""
+from __future__ import annotations
+
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+from ..moe.config import MoEConfig
+from ..moe.layer import MoEFFN
+from .backbone import ConvNormLayer
+
+
+class DenseFFN(nn.Module):
+    def __init__(self, d, hidden, act="relu"):
+        super().__init__()
+        self.linear1 = nn.Linear(d, hidden)
+        self.linear2 = nn.Linear(hidden, d)
+        self.act = nn.GELU() if act == "gelu" else nn.ReLU()
+
+    def forward(self, x, ctx=None):
+        return self.linear2(self.act(self.linear1(x)))
+
+
+def make_ffn(d, hidden, moe: MoEConfig | None, act="relu"):
+    return MoEFFN(d, moe) if moe is not None else DenseFFN(d, hidden, act)
+
+
+class TransformerEncoderLayer(nn.Module):
+    """Post-norm encoder layer (AIFI): self-attention with 2-D sin-cos position
+    added to q/k, then the (MoE) FFN."""
+
+    def __init__(self, d=256, nhead=8, hidden=1024, moe: MoEConfig | None = None):
+        super().__init__()
+        self.self_attn = nn.MultiheadAttention(d, nhead, batch_first=True)
+        self.ffn = make_ffn(d, hidden, moe, act="relu")
+        self.norm1 = nn.LayerNorm(d)
+        self.norm2 = nn.LayerNorm(d)
+
+    def forward(self, src, pos, ctx):
+        q = k = src + pos
+        src = self.norm1(src + self.self_attn(q, k, src, need_weights=False)[0])
+        src = self.norm2(src + self.ffn(src, ctx))
+        return src
+
+
+class RepVggBlock(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.conv1 = ConvNormLayer(cin, cout, 3, 1)
+        self.conv2 = ConvNormLayer(cin, cout, 1, 1)
+
+    def forward(self, x):
+        return F.silu(self.conv1(x) + self.conv2(x))
+
+
+class CSPRepLayer(nn.Module):
+    def __init__(self, cin, cout, num_blocks=3, expansion=1.0):
+        super().__init__()
+        hidden = int(cout * expansion)
+        self.conv1 = ConvNormLayer(cin, hidden, 1, 1, "silu")
+        self.conv2 = ConvNormLayer(cin, hidden, 1, 1, "silu")
+        self.bottlenecks = nn.Sequential(*[RepVggBlock(hidden, hidden) for _ in range(num_blocks)])
+        self.conv3 = ConvNormLayer(hidden, cout, 1, 1, "silu") if hidden != cout else nn.Identity()
+
+    def forward(self, x):
+        return self.conv3(self.bottlenecks(self.conv1(x)) + self.conv2(x))
+
+
+def sincos_pos_embed_2d(w, h, dim=256, temperature=10000.0, device=None, dtype=torch.float32):
+    gw = torch.arange(w, dtype=torch.float32, device=device)
+    gh = torch.arange(h, dtype=torch.float32, device=device)
+    gw, gh = torch.meshgrid(gw, gh, indexing="ij")
+    pos_dim = dim // 4
+    omega = 1.0 / temperature ** (torch.arange(pos_dim, dtype=torch.float32, device=device) / pos_dim)
+    out_w = gw.flatten()[:, None] @ omega[None]
+    out_h = gh.flatten()[:, None] @ omega[None]
+    # [w*h, dim] in (x-major) order; transpose to row-major (h, w) token order
+    emb = torch.cat([out_w.sin(), out_w.cos(), out_h.sin(), out_h.cos()], dim=1)
+    emb = emb.view(w, h, dim).transpose(0, 1).reshape(h * w, dim)
+    return emb[None].to(dtype)
+
+
+class HybridEncoder(nn.Module):
+    def __init__(self, in_channels=(512, 1024, 2048), strides=(8, 16, 32), hidden=256, nhead=8,
+                 dim_feedforward=1024, use_encoder_idx=(2,), num_encoder_layers=1,
+                 expansion=1.0, depth_mult=1.0, moe: MoEConfig | None = None):
+        super().__init__()
+        self.hidden = hidden
+        self.use_encoder_idx = list(use_encoder_idx)
+        self.strides = list(strides)
+        self.input_proj = nn.ModuleList(
+            [nn.Sequential(nn.Conv2d(c, hidden, 1, bias=False), nn.BatchNorm2d(hidden)) for c in in_channels])
+        self.encoder = nn.ModuleList([
+            nn.ModuleList([TransformerEncoderLayer(hidden, nhead, dim_feedforward, moe)
+                           for _ in range(num_encoder_layers)]) for _ in self.use_encoder_idx])
+        nb = round(3 * depth_mult)
+        n = len(in_channels)
+        self.lateral_convs = nn.ModuleList([ConvNormLayer(hidden, hidden, 1, 1, "silu") for _ in range(n - 1)])
+        self.fpn_blocks = nn.ModuleList([CSPRepLayer(hidden * 2, hidden, nb, expansion) for _ in range(n - 1)])
+        self.downsample_convs = nn.ModuleList([ConvNormLayer(hidden, hidden, 3, 2, "silu") for _ in range(n - 1)])
+        self.pan_blocks = nn.ModuleList([CSPRepLayer(hidden * 2, hidden, nb, expansion) for _ in range(n - 1)])
+        self._pos_cache = {}
+
+    def _pos(self, w, h, device, dtype):
+        key = (w, h, device, dtype)
+        if key not in self._pos_cache:
+            self._pos_cache[key] = sincos_pos_embed_2d(w, h, self.hidden, device=device, dtype=dtype)
+        return self._pos_cache[key]
+
+    def forward(self, feats, ctx):
+        proj = [p(f) for p, f in zip(self.input_proj, feats)]
+        for i, enc_ind in enumerate(self.use_encoder_idx):
+            B, C, h, w = proj[enc_ind].shape
+            src = proj[enc_ind].flatten(2).permute(0, 2, 1).contiguous()   # [B, h*w, C]
+            pos = self._pos(w, h, src.device, src.dtype)
+            for layer in self.encoder[i]:
+                src = layer(src, pos, ctx)
+            proj[enc_ind] = src.permute(0, 2, 1).reshape(B, C, h, w).contiguous(memory_format=torch.channels_last)
+        n = len(proj)
+        inner = [proj[-1]]
+        for idx in range(n - 1, 0, -1):
+            high = self.lateral_convs[n - 1 - idx](inner[0])
+            inner[0] = high
+            up = F.interpolate(high, scale_factor=2.0, mode="nearest")
+            low = proj[idx - 1]
+            if up.shape[-2:] != low.shape[-2:]:
+                up = up[..., : low.shape[-2], : low.shape[-1]]
+            inner.insert(0, self.fpn_blocks[n - 1 - idx](torch.cat([up, low], dim=1)))
+        outs = [inner[0]]
+        for idx in range(n - 1):
+            down = self.downsample_convs[idx](outs[-1])
+            outs.append(self.pan_blocks[idx](torch.cat([down, inner[idx + 1]], dim=1)))
+        return outs

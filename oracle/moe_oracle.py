@@ -1,0 +1,317 @@
+"""CPU oracle for the MoE-gated RT-DETR hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker / CPU baseline.  The product path
+(multimodal-moe_amd/src/moe) never imports it.
+
+What it restates (numpy, float64, explicit loops over experts):
+  a1  solar context bin      scripts/add_solar_context_bins.py:87-107
+      (pd.cut(bins=[-1e9,-6,0,15,45,1e9], include_lowest, right-closed);
+       NaN -> "missing"; duplicate at scripts/analyze_context_frequencies.py:68-83)
+  a2  router                 SURVEY.md 8(a) row a2 (reference: planned only,
+      notes/MoE_in_ZOD_Thesis_Proposal_revisedTimeline.txt:215-216 "Top-k
+      routing"; context as an additive router-logit bias,
+      notes/related_work.md:64-68)
+  a3  aux losses             SURVEY.md 8(a) row a3 (load balance, z-loss:
+      notes/related_work.md:72-75)
+  a4  dispatch               SURVEY.md 8(a) row a4 (slot-major capacity priority)
+  a5  expert FFN             SURVEY.md 8(a) row a5 ("Experts are standard MLP
+      blocks", notes/related_work.md:23)
+  a6  combine                SURVEY.md 8(a) row a6
+  a7  backward               SURVEY.md 8(a) row a7 (hand-derived, checked
+      against torch autograd in tests/test_oracle.py)
+
+Parity status: a1 is PINNED against the reference itself (golden vectors in
+tests/golden/reference_known_answers.json, made by tests/golden/make_golden.py
+importing /root/reference).  a2-a7 are "parity unpinned": the reference has no
+MoE code, so this restatement of the written spec is the
+oracle, cross-checked against an independent torch-autograd formulation.
+
+``emulate_bf16=True`` rounds the tensors the GPU path stores in bf16 (inputs,
+H, Yp, y, dYp, dH, dXp, dx) at the same points, so GPU-vs-oracle differences
+are only fp32-vs-fp64 accumulation order plus one final bf16 rounding.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+# ----------------------------------------------------------------------------
+# a1: solar context bins (scripts/add_solar_context_bins.py:90-107)
+# ----------------------------------------------------------------------------
+SOLAR_BINS = [-1e9, -6.0, 0.0, 15.0, 45.0, 1e9]
+SOLAR_LABELS = [
+    "night(<-6)",
+    "twilight(-6..0)",
+    "low_sun(0..15)",
+    "mid_sun(15..45)",
+    "high_sun(>45)",
+]
+CONTEXT_LABELS = SOLAR_LABELS + ["missing"]
+
+
+def solar_context_bin(angle) -> str:
+    """Label of one solar elevation angle, as pd.cut(..., include_lowest=True)."""
+    try:
+        a = float(angle)
+    except (TypeError, ValueError):
+        return "missing"
+    if math.isnan(a):
+        return "missing"
+    # right-closed intervals (lo, hi]; include_lowest closes the first on the left
+    if SOLAR_BINS[0] <= a <= SOLAR_BINS[1]:
+        return SOLAR_LABELS[0]
+    for i in range(1, len(SOLAR_LABELS)):
+        if SOLAR_BINS[i] < a <= SOLAR_BINS[i + 1]:
+            return SOLAR_LABELS[i]
+    return "missing"  # outside [-1e9, 1e9]: pd.cut gives NaN -> fillna("missing")
+
+
+def solar_context_id(angle) -> int:
+    return CONTEXT_LABELS.index(solar_context_bin(angle))
+
+
+# ----------------------------------------------------------------------------
+# bf16 emulation (round-to-nearest-even, like v_cvt_pk_bf16_f32)
+# ----------------------------------------------------------------------------
+def round_bf16(a) -> np.ndarray:
+    f = np.asarray(a, dtype=np.float32)
+    u = f.view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    out = r.astype(np.uint32).view(np.float32)
+    out = np.where(np.isnan(f), np.float32(np.nan), out)
+    return out.astype(np.float64)
+
+
+def _maybe(a, on):
+    return round_bf16(a) if on else np.asarray(a, dtype=np.float64)
+
+
+# ----------------------------------------------------------------------------
+# a2: router
+# ----------------------------------------------------------------------------
+def router_forward(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize):
+    """logits = x.wg^T + ctx_bias[ctx(t)]; softmax; top-k (ties -> lower id); gates."""
+    x = np.asarray(x, np.float64)
+    wg = np.asarray(wg, np.float64)
+    T = x.shape[0]
+    E = wg.shape[0]
+    logits = x @ wg.T
+    if ctx_bias is not None:
+        img = np.arange(T) // int(tokens_per_image)
+        logits = logits + np.asarray(ctx_bias, np.float64)[np.asarray(ctx_img)[img]]
+    m = logits.max(axis=1, keepdims=True)
+    ex = np.exp(logits - m)
+    s = ex.sum(axis=1, keepdims=True)
+    probs = ex / s
+    lse = (m + np.log(s))[:, 0]
+    # lexsort: last key primary -> by -logit, then by expert id (lowest first)
+    eid = np.broadcast_to(np.arange(E), logits.shape)
+    order = np.lexsort((eid, -logits), axis=1)
+    idx = order[:, :k].astype(np.int64)
+    psel = np.take_along_axis(probs, idx, axis=1)
+    if normalize and k > 1:
+        w = psel / psel.sum(axis=1, keepdims=True)
+    else:
+        w = psel.copy()
+    return logits, probs, lse, idx, w
+
+
+# ----------------------------------------------------------------------------
+# a4: dispatch (slot-major, token order; capacity drop)
+# ----------------------------------------------------------------------------
+def dispatch_indices(idx, E, cap):
+    """Returns (pos [T,k] (-1 = dropped), hist [E], offsets [E+1])."""
+    idx = np.asarray(idx)
+    T, k = idx.shape
+    hist = np.bincount(idx.ravel(), minlength=E).astype(np.int64)
+    kept = np.minimum(hist, cap) if cap and cap > 0 else hist.copy()
+    offsets = np.concatenate([[0], np.cumsum(kept)]).astype(np.int64)
+    rank = np.zeros((T, k), np.int64)
+    seen = np.zeros(E, np.int64)
+    for j in range(k):          # slot-major: every top-1 choice before any top-2
+        for t in range(T):      # then token order
+            e = idx[t, j]
+            rank[t, j] = seen[e]
+            seen[e] += 1
+    if cap and cap > 0:
+        pos = np.where(rank < cap, offsets[idx] + rank, -1)
+    else:
+        pos = offsets[idx] + rank
+    return pos.astype(np.int64), hist, offsets
+
+
+def permute(x, pos, rows):
+    x = np.asarray(x, np.float64)
+    T, k = pos.shape
+    xp = np.zeros((rows, x.shape[1]))
+    for t in range(T):
+        for j in range(k):
+            if pos[t, j] >= 0:
+                xp[pos[t, j]] = x[t]
+    return xp
+
+
+# ----------------------------------------------------------------------------
+# a5: expert FFN
+# ----------------------------------------------------------------------------
+def expert_ffn(xp, offsets, w1, b1, w2, b2, emulate_bf16=False):
+    rows = int(offsets[-1])
+    E = w1.shape[0]
+    d = w2.shape[1]
+    F = w1.shape[1]
+    H = np.zeros((rows, F))
+    Y = np.zeros((rows, d))
+    for e in range(E):
+        a, b = int(offsets[e]), int(offsets[e + 1])
+        if b <= a:
+            continue
+        h = np.maximum(xp[a:b] @ np.asarray(w1[e], np.float64).T + b1[e], 0.0)
+        H[a:b] = _maybe(h, emulate_bf16)
+        Y[a:b] = _maybe(H[a:b] @ np.asarray(w2[e], np.float64).T + b2[e], emulate_bf16)
+    return H, Y
+
+
+# ----------------------------------------------------------------------------
+# a6: combine
+# ----------------------------------------------------------------------------
+def combine(yp, pos, w, emulate_bf16=False):
+    T, k = pos.shape
+    y = np.zeros((T, yp.shape[1]))
+    for j in range(k):
+        keep = pos[:, j] >= 0
+        y[keep] += w[keep, j][:, None] * yp[pos[keep, j]]
+    return _maybe(y, emulate_bf16)
+
+
+# ----------------------------------------------------------------------------
+# a3: aux losses
+# ----------------------------------------------------------------------------
+def aux_losses(probs, lse, hist, k):
+    T, E = probs.shape
+    f = hist / max(T * k, 1)
+    P = probs.mean(axis=0) if T > 0 else np.zeros(E)
+    lb = E * float((f * P).sum())
+    z = float((lse ** 2).mean()) if T > 0 else 0.0
+    return lb, z
+
+
+@dataclass
+class MoEState:
+    logits: np.ndarray
+    probs: np.ndarray
+    lse: np.ndarray
+    idx: np.ndarray
+    w: np.ndarray
+    pos: np.ndarray
+    hist: np.ndarray
+    offsets: np.ndarray
+    xp: np.ndarray
+    H: np.ndarray
+    Yp: np.ndarray
+    y: np.ndarray
+    lb: float
+    z: float
+
+
+def moe_forward(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k,
+                normalize=True, cap=0, emulate_bf16=False) -> MoEState:
+    """Full routed FFN of one layer (a2-a6).  Shapes: x [T,d], wg [E,d],
+    ctx_bias [C,E] | None, w1 [E,F,d], b1 [E,F], w2 [E,d,F], b2 [E,d]."""
+    E = np.asarray(wg).shape[0]
+    x = _maybe(x, emulate_bf16)
+    logits, probs, lse, idx, w = router_forward(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize)
+    pos, hist, offsets = dispatch_indices(idx, E, cap)
+    xp = permute(x, pos, int(offsets[-1]))
+    if emulate_bf16:
+        w1 = round_bf16(w1)
+        w2 = round_bf16(w2)
+    H, Yp = expert_ffn(xp, offsets, w1, b1, w2, b2, emulate_bf16)
+    y = combine(Yp, pos, w, emulate_bf16)
+    lb, z = aux_losses(probs, lse, hist, k)
+    return MoEState(logits, probs, lse, idx, w, pos, hist, offsets, xp, H, Yp, y, lb, z)
+
+
+# ----------------------------------------------------------------------------
+# a7: backward (hand-derived)
+# ----------------------------------------------------------------------------
+def moe_backward(st: MoEState, x, wg, w1, w2, ctx_img, tokens_per_image, n_ctx, dy,
+                 g_lb=0.0, g_z=0.0, normalize=True, emulate_bf16=False):
+    """Gradients of  <dy, y> + g_lb * lb + g_z * z  w.r.t. every input.
+
+    Returns dict(dx, dwg, dctx_bias, dw1, db1, dw2, db2)."""
+    x = _maybe(x, emulate_bf16)
+    dy = _maybe(dy, emulate_bf16)
+    if emulate_bf16:
+        w1 = round_bf16(w1)
+        w2 = round_bf16(w2)
+    w1 = np.asarray(w1, np.float64)
+    w2 = np.asarray(w2, np.float64)
+    wg = np.asarray(wg, np.float64)
+    T, d = x.shape
+    E, F = w1.shape[0], w1.shape[1]
+    k = st.idx.shape[1]
+    rows = int(st.offsets[-1])
+    # combine transpose
+    dYp = np.zeros((rows, d))
+    dw = np.zeros((T, k))
+    for j in range(k):
+        for t in range(T):
+            p = st.pos[t, j]
+            if p >= 0:
+                dYp[p] = st.w[t, j] * dy[t]
+                dw[t, j] = float(dy[t] @ st.Yp[p])
+    dYp = _maybe(dYp, emulate_bf16)
+    # expert FFN backward
+    dH = np.zeros((rows, F))
+    dXp = np.zeros((rows, d))
+    dw1 = np.zeros_like(w1)
+    dw2 = np.zeros_like(w2)
+    db1 = np.zeros((E, F))
+    db2 = np.zeros((E, d))
+    for e in range(E):
+        a, b = int(st.offsets[e]), int(st.offsets[e + 1])
+        if b <= a:
+            continue
+        dh = (dYp[a:b] @ w2[e]) * (st.H[a:b] > 0)
+        dH[a:b] = _maybe(dh, emulate_bf16)
+        dXp[a:b] = _maybe(dH[a:b] @ w1[e], emulate_bf16)
+        dw2[e] = dYp[a:b].T @ st.H[a:b]
+        dw1[e] = dH[a:b].T @ st.xp[a:b]
+        db2[e] = dYp[a:b].sum(axis=0)
+        db1[e] = dH[a:b].sum(axis=0)
+    # router backward
+    dprobs = np.zeros((T, E))
+    psel = np.take_along_axis(st.probs, st.idx, axis=1)
+    if normalize and k > 1:
+        S = psel.sum(axis=1, keepdims=True)
+        wdw = (st.w * dw).sum(axis=1, keepdims=True)
+        dpsel = (dw - wdw) / S
+    else:
+        dpsel = dw
+    for j in range(k):
+        dprobs[np.arange(T), st.idx[:, j]] += dpsel[:, j]
+    if g_lb:
+        f = st.hist / max(T * k, 1)
+        dprobs += g_lb * E * f[None, :] / max(T, 1)
+    dlogits = st.probs * (dprobs - (st.probs * dprobs).sum(axis=1, keepdims=True))
+    if g_z:
+        dlogits += g_z * 2.0 * st.lse[:, None] * st.probs / max(T, 1)
+    # dispatch transpose + router input grad
+    dx = dlogits @ wg
+    for j in range(k):
+        for t in range(T):
+            p = st.pos[t, j]
+            if p >= 0:
+                dx[t] += dXp[p]
+    dx = _maybe(dx, emulate_bf16)
+    dwg = dlogits.T @ x
+    dctx = None
+    if ctx_img is not None and n_ctx:
+        dctx = np.zeros((n_ctx, E))
+        img = np.arange(T) // int(tokens_per_image)
+        np.add.at(dctx, np.asarray(ctx_img)[img], dlogits)
+    return dict(dx=dx, dwg=dwg, dctx_bias=dctx, dw1=dw1, db1=db1, dw2=dw2, db2=db2,
+                dlogits=dlogits, dw=dw)

@@ -1,0 +1,268 @@
+"""GPU parity of the HIP MoE kernels against the CPU oracle (oracle/moe_oracle.py).
+
+Every test calls libmoe_hip.so through its C-ABI (src/moe/_lib.py -> ctypes)
+and compares with the float64 oracle run on the same bf16-representable
+inputs (``emulate_bf16=True`` rounds the same intermediates the GPU stores in
+bf16).  Tolerances (stated per check below):
+  integer outputs (top-k ids, pos, hist, offsets, permuted rows): bit-exact;
+  fp32 router outputs (probs, lse, gates): |err| <= 2e-6;
+  bf16 tensors: |err| <= 1e-2 * max|ref| + 1 bf16 ulp of the value
+  (fp32 accumulation order differs from the fp64 oracle, then one rounding);
+  fp32 weight gradients: relative Frobenius error <= 5e-3.
+Integer-valued GEMM checks are exact (small integers are exact in bf16 and
+their fp32 sums are exact).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import moe_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _bf16(a):
+    return torch.from_numpy(np.asarray(O.round_bf16(a), np.float32)).to(torch.bfloat16)
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy().astype(np.float64)
+
+
+def make_case(T, d, E, F, k, tpi, seed, C=6, wg_std=0.3, ctx_scale=0.5, skew=None):
+    """Random bf16-representable inputs whose top-(k) choice has a margin of
+    at least 1e-3 in fp64 logits (so fp32 vs fp64 cannot flip a selection)."""
+    rng = np.random.default_rng(seed)
+    n_img = (T + tpi - 1) // tpi
+    wg = O.round_bf16(rng.standard_normal((E, d)) * wg_std).astype(np.float32).astype(np.float64)
+    ctx_bias = (rng.standard_normal((C, E)) * ctx_scale).astype(np.float32).astype(np.float64)
+    if skew is not None:
+        ctx_bias[:, :] = 0.0
+        ctx_bias[:, skew] = 60.0  # steer every token to one expert
+    ctx_img = rng.integers(0, C, size=n_img).astype(np.int32)
+    x = O.round_bf16(rng.standard_normal((T, d)))
+    for _ in range(50):
+        logits, *_ = O.router_forward(x, wg, ctx_bias, ctx_img, tpi, k, True)
+        srt = -np.sort(-logits, axis=1)
+        gaps = np.min(np.abs(np.diff(srt[:, : min(k + 1, E)], axis=1)), axis=1) if E > 1 else np.ones(T)
+        bad = gaps < 1e-3
+        if not bad.any():
+            break
+        x[bad] = O.round_bf16(rng.standard_normal((int(bad.sum()), d)))
+    else:
+        raise RuntimeError("could not build a tie-free case")
+    w1 = O.round_bf16(rng.standard_normal((E, F, d)) / np.sqrt(d))
+    b1 = (rng.standard_normal((E, F)) * 0.1).astype(np.float32).astype(np.float64)
+    w2 = O.round_bf16(rng.standard_normal((E, d, F)) / np.sqrt(F))
+    b2 = (rng.standard_normal((E, d)) * 0.1).astype(np.float32).astype(np.float64)
+    return dict(x=x, wg=wg, ctx_bias=ctx_bias, ctx_img=ctx_img, w1=w1, b1=b1, w2=w2, b2=b2, tpi=tpi)
+
+
+def bf16_close(got, ref, what, rel=1e-2):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    scale = max(float(np.abs(ref).max()), 1e-6)
+    ulp = np.abs(ref) * 2.0 ** -7
+    err = np.abs(got - ref)
+    tol = rel * scale + ulp
+    bad = err > tol
+    assert not bad.any(), f"{what}: {bad.sum()} / {bad.size} out of tolerance; max err {err.max():.3e}, scale {scale:.3e}"
+
+
+def rel_fro(got, ref):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    return float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-12))
+
+
+# ---------------------------------------------------------------------------
+# grouped GEMM with exact integer data (layout / indexing checks)
+# ---------------------------------------------------------------------------
+def _int_tensor(rng, shape, lo=-3, hi=4):
+    return rng.integers(lo, hi, size=shape).astype(np.float64)
+
+
+@pytest.mark.parametrize("trans_b", [1, 0])
+@pytest.mark.parametrize("rows_per_group", [[0, 1, 63, 64, 65, 200, 0, 130], [1000, 24, 0, 500]])
+@pytest.mark.parametrize("N,K", [(1024, 256), (256, 1024), (128, 64)])
+def test_grouped_gemm_exact(hip_lib, trans_b, rows_per_group, N, K):
+    from src.moe import _lib as L
+
+    rng = np.random.default_rng(7)
+    G = len(rows_per_group)
+    offsets = np.concatenate([[0], np.cumsum(rows_per_group)]).astype(np.int32)
+    R = int(offsets[-1])
+    A = _int_tensor(rng, (R + 5, K))  # extra rows beyond the groups must be ignored
+    Bw = _int_tensor(rng, (G, N, K) if trans_b else (G, K, N))
+    bias = _int_tensor(rng, (G, N))
+    ref = np.zeros((R, N))
+    for g in range(G):
+        a, b = offsets[g], offsets[g + 1]
+        Bg = Bw[g].T if trans_b else Bw[g]  # logical [K][N]
+        ref[a:b] = A[a:b] @ Bg
+    At = torch.from_numpy(A).to(torch.bfloat16).to(DEV)
+    Bt = torch.from_numpy(Bw).to(torch.bfloat16).to(DEV).contiguous()
+    off_t = torch.from_numpy(offsets).to(DEV)
+    C = L.grouped_gemm(At, Bt, off_t, G, R + 5, N, K, trans_b, L.EPI_NONE)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_np(C)[:R], O.round_bf16(ref))  # exact fp32 sum, one RNE rounding
+    # bias + relu epilogue
+    bias_t = torch.from_numpy(bias).float().to(DEV)
+    C2 = L.grouped_gemm(At, Bt, off_t, G, R + 5, N, K, trans_b, L.EPI_BIAS_RELU, bias=bias_t)
+    gid = np.repeat(np.arange(G), rows_per_group)
+    ref2 = np.maximum(ref + bias[gid], 0)
+    # values are integers up to ~|3*3*K| -> may exceed bf16's exact range: compare in bf16
+    np.testing.assert_array_equal(_np(C2)[:R], O.round_bf16(ref2))
+    # relu-mask epilogue (mask from C2 > 0)
+    C3 = L.grouped_gemm(At, Bt, off_t, G, R + 5, N, K, trans_b, L.EPI_RELU_MASK, aux=C2)
+    np.testing.assert_array_equal(_np(C3)[:R], O.round_bf16(ref * (O.round_bf16(ref2) > 0)))
+
+
+@pytest.mark.parametrize("rows_per_group", [[0, 1, 63, 64, 65, 200, 0, 130], [700, 0, 33]])
+@pytest.mark.parametrize("M,N", [(256, 1024), (1024, 256), (64, 128)])
+def test_grouped_gemm_wgrad_exact(hip_lib, rows_per_group, M, N):
+    from src.moe import _lib as L
+
+    rng = np.random.default_rng(11)
+    G = len(rows_per_group)
+    offsets = np.concatenate([[0], np.cumsum(rows_per_group)]).astype(np.int32)
+    R = int(offsets[-1])
+    X = _int_tensor(rng, (R + 3, M), -2, 3)
+    Y = _int_tensor(rng, (R + 3, N), -2, 3)
+    Xt = torch.from_numpy(X).to(torch.bfloat16).to(DEV)
+    Yt = torch.from_numpy(Y).to(torch.bfloat16).to(DEV)
+    off_t = torch.from_numpy(offsets).to(DEV)
+    C, cs = L.grouped_gemm_wgrad(Xt, Yt, off_t, G)
+    torch.cuda.synchronize()
+    for g in range(G):
+        a, b = offsets[g], offsets[g + 1]
+        np.testing.assert_array_equal(_np(C[g]), X[a:b].T @ Y[a:b])
+        np.testing.assert_array_equal(_np(cs[g]), X[a:b].sum(0))
+
+
+# ---------------------------------------------------------------------------
+# router / dispatch / combine / full layer against the oracle
+# ---------------------------------------------------------------------------
+CASES = [
+    # T, d, E, F, k, tpi, cap_factor, seed
+    (1, 256, 4, 1024, 1, 1, 0.0, 0),
+    (200, 256, 4, 1024, 1, 100, 0.0, 1),
+    (1000, 256, 8, 1024, 2, 250, 0.0, 2),
+    (1300, 256, 8, 1024, 2, 130, 1.25, 3),
+    (777, 256, 16, 1024, 2, 111, 0.0, 4),
+    (640, 256, 32, 1024, 4, 64, 1.25, 5),
+    (333, 128, 8, 256, 3, 333, 0.5, 6),
+]
+
+
+def _cap(T, k, E, cf):
+    import math
+
+    return 0 if cf <= 0 else int(math.ceil(cf * T * k / E))
+
+
+@pytest.mark.parametrize("T,d,E,F,k,tpi,cf,seed", CASES)
+def test_router_dispatch_combine(hip_lib, T, d, E, F, k, tpi, cf, seed):
+    from src.moe import _lib as L
+
+    c = make_case(T, d, E, F, k, tpi, seed)
+    cap = _cap(T, k, E, cf)
+    st = O.moe_forward(c["x"], c["wg"], c["ctx_bias"], c["w1"], c["b1"], c["w2"], c["b2"],
+                       c["ctx_img"], tpi, k, True, cap, emulate_bf16=True)
+    x = _bf16(c["x"]).to(DEV)
+    wg = torch.from_numpy(c["wg"]).float().to(DEV)
+    cb = torch.from_numpy(c["ctx_bias"]).float().to(DEV)
+    ci = torch.from_numpy(c["ctx_img"]).to(DEV)
+    idx, w, probs, lse, lrank, bcnt, auxp = L.router_topk_fwd(x, wg, cb, ci, tpi, k, True)
+    rank_base, hist, offsets = L.route_scan(bcnt, cap)
+    rows = T * k if cap <= 0 else min(T * k, E * cap)
+    xp, pos = L.permute_fwd(x, idx, lrank, rank_base, offsets, E, cap, rows)
+    torch.cuda.synchronize()
+    # integer outputs: exact
+    np.testing.assert_array_equal(idx.cpu().numpy(), st.idx)
+    np.testing.assert_array_equal(hist.cpu().numpy(), st.hist)
+    np.testing.assert_array_equal(offsets.cpu().numpy(), st.offsets)
+    np.testing.assert_array_equal(pos.cpu().numpy(), st.pos)
+    R = int(st.offsets[-1])
+    np.testing.assert_array_equal(_np(xp)[:R], st.xp)
+    # fp32 router outputs
+    np.testing.assert_allclose(_np(probs), st.probs, atol=2e-6, rtol=0)
+    np.testing.assert_allclose(_np(lse), st.lse, atol=2e-6 * max(1, np.abs(st.lse).max()), rtol=0)
+    np.testing.assert_allclose(_np(w), st.w, atol=2e-6, rtol=0)
+    # aux partials
+    np.testing.assert_allclose(_np(auxp[:, :E].sum(0)), st.probs.sum(0), rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(float(auxp[:, E].sum()), float((st.lse ** 2).sum()), rtol=1e-5)
+    # combine with the oracle's Yp (isolates the combine kernel)
+    yp = _bf16(st.Yp if R > 0 else np.zeros((1, d))).to(DEV)
+    y = L.combine_fwd(yp, pos, w, T)
+    torch.cuda.synchronize()
+    bf16_close(_np(y), st.y, "combine y")
+
+
+@pytest.mark.parametrize("T,d,E,F,k,tpi,cf,seed", CASES)
+def test_moe_layer_fwd_bwd(hip_lib, T, d, E, F, k, tpi, cf, seed):
+    from src.moe.ops import moe_ffn_hip
+
+    c = make_case(T, d, E, F, k, tpi, seed)
+    cap = _cap(T, k, E, cf)
+    rng = np.random.default_rng(100 + seed)
+    dy = O.round_bf16(rng.standard_normal((T, d)))
+    g_lb, g_z = 0.7, 0.3
+    st = O.moe_forward(c["x"], c["wg"], c["ctx_bias"], c["w1"], c["b1"], c["w2"], c["b2"],
+                       c["ctx_img"], tpi, k, True, cap, emulate_bf16=True)
+    gr = O.moe_backward(st, c["x"], c["wg"], c["w1"], c["w2"], c["ctx_img"], tpi, 6, dy,
+                        g_lb=g_lb, g_z=g_z, normalize=True, emulate_bf16=True)
+
+    def P(a, dtype=torch.float32):
+        return torch.from_numpy(np.asarray(a)).to(dtype).to(DEV).requires_grad_(True)
+
+    x = P(c["x"], torch.bfloat16)
+    wg, cb = P(c["wg"]), P(c["ctx_bias"])
+    w1, b1, w2, b2 = P(c["w1"]), P(c["b1"]), P(c["w2"]), P(c["b2"])
+    ci = torch.from_numpy(c["ctx_img"]).to(DEV)
+    y, lb, z, hist = moe_ffn_hip(x, wg, cb, w1, b1, w2, b2, ci, tpi, k, True, cap)
+    loss = (y.float() * _bf16(dy).float().to(DEV)).sum() + g_lb * lb + g_z * z
+    loss.backward()
+    torch.cuda.synchronize()
+    bf16_close(_np(y), st.y, "y")
+    assert abs(float(lb.detach()) - st.lb) <= 1e-5 * max(1.0, abs(st.lb))
+    assert abs(float(z.detach()) - st.z) <= 1e-5 * max(1.0, abs(st.z))
+    np.testing.assert_array_equal(hist.cpu().numpy(), st.hist)
+    bf16_close(_np(x.grad), gr["dx"], "dx")
+    for name, t in [("dwg", wg), ("dctx_bias", cb), ("dw1", w1), ("db1", b1), ("dw2", w2), ("db2", b2)]:
+        ref = gr[name]
+        e = rel_fro(_np(t.grad), ref)
+        assert e <= 5e-3, f"{name}: relative Frobenius error {e:.2e}"
+
+
+def test_skewed_routing_and_empty_experts(hip_lib):
+    """Every token forced to one expert (others empty), with capacity drops."""
+    from src.moe.ops import moe_ffn_hip
+
+    T, d, E, F, k, tpi = 500, 256, 8, 1024, 2, 50
+    c = make_case(T, d, E, F, k, tpi, 9, wg_std=0.05, skew=3)
+    cap = _cap(T, k, E, 1.0)
+    st = O.moe_forward(c["x"], c["wg"], c["ctx_bias"], c["w1"], c["b1"], c["w2"], c["b2"],
+                       c["ctx_img"], tpi, k, True, cap, emulate_bf16=True)
+    assert st.hist[3] == T and (st.pos[:, 0] >= 0).sum() == cap  # drops happen
+    x = _bf16(c["x"]).to(DEV)
+    f = lambda a: torch.from_numpy(np.asarray(a)).float().to(DEV)
+    y, lb, z, hist = moe_ffn_hip(x, f(c["wg"]), f(c["ctx_bias"]), f(c["w1"]), f(c["b1"]), f(c["w2"]),
+                                 f(c["b2"]), torch.from_numpy(c["ctx_img"]).to(DEV), tpi, k, True, cap)
+    torch.cuda.synchronize()
+    bf16_close(_np(y), st.y, "y (skewed)")
+    np.testing.assert_array_equal(hist.cpu().numpy(), st.hist)
+
+
+def test_library_reports_bad_shapes(hip_lib):
+    from src.moe import _lib as L
+
+    x = torch.zeros((10, 100), dtype=torch.bfloat16, device=DEV)  # d not a multiple of 128
+    wg = torch.zeros((4, 100), dtype=torch.float32, device=DEV)
+    with pytest.raises(L.MoEKernelError, match="multiple of 128"):
+        L.router_topk_fwd(x, wg, None, None, 10, 1, True)
