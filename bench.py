@@ -1,0 +1,253 @@
+#!/usr/bin/env python
+"""Benchmark: images/sec (fwd+bwd) of RT-DETR-MoE at 1280x720, bs=8/GPU, MI355X.
+
+Metric and configs come from BASELINE.json.  One "step" = one full training
+step of the C2 workload on one batch: RT-DETR-R50 + 8-expert top-2 MoE FFN in
+the AIFI encoder layer and all 6 decoder layers, bf16 autocast, forward,
+Hungarian-matched VFL/L1/GIoU losses + MoE aux losses, backward, grad clip,
+AdamW step.  Synthetic ZOD-shaped batches generated once and
+kept resident in HBM; random-init weights.
+
+  python bench.py                               # N=1, defaults
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N         # DP over RCCL (C3), weak scaling
+
+Rank 0 prints ONE JSON line.  Besides the contract keys it carries
+``roofline`` for the dominant HIP kernel (the grouped expert GEMM, HIP events
+around every launch inside the timed region, algorithmic flops 2*rows*N*K per
+launch), ``roofline_dispatch`` for the HBM-bound row movers, and
+``cpu_baseline``: the same model in fp32 on the host cores with the MoE layers
+computed by the CPU oracle (oracle/moe_oracle.py, kind "port"), timed on a
+bounded sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for p in (str(ROOT / "multimodal-moe_amd"), str(ROOT)):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "images/sec (fwd+bwd) RT-DETR-MoE 1280×720 bs=8/GPU at 1/2/4/8 MI355X"
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec peak
+
+WORKLOADS = {
+    "c2": dict(spec="rtdetr-r50-moe8-top2", batch=8, desc="C2: RT-DETR-R50 + 8-expert top-2 MoE, bs=8/GPU, bf16"),
+    "c4": dict(spec="rtdetr-r50-moe16-top2-ep{N}", batch=8, single_ctx=True,
+               desc="C4: 16-expert top-2, expert-parallel all-to-all, solar-context-binned batches"),
+    "c5": dict(spec="rtdetr-r50-moe32-top4-cf1.25-fp8", batch=16,
+               desc="C5: 32-expert top-4 fp8 experts, capacity factor 1.25, bs=16/GPU"),
+}
+
+
+def parse_args():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the workload's)")
+    ap.add_argument("--img-h", type=int, default=720)
+    ap.add_argument("--img-w", type=int, default=1280)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample length")
+    ap.add_argument("--no-kernel-timing", action="store_true", help="skip per-launch HIP events")
+    return ap.parse_args()
+
+
+def setup_dist(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    if n_gpus != world:
+        print(f"[bench] warning: --gpus {n_gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    return world, rank, local
+
+
+def build_training(spec, device, world, local):
+    from src.rtdetr_moe.criterion import SetCriterion
+    from src.rtdetr_moe.model import RTDETRMoE
+
+    torch.manual_seed(1)
+    model = RTDETRMoE(spec).to(device).to(memory_format=torch.channels_last)
+    if world > 1:
+        from src.rtdetr_moe.engine import wrap_ddp
+
+        model = wrap_ddp(model, local)
+    params = [p for p in model.parameters() if p.requires_grad]
+    opt = torch.optim.AdamW(params, lr=1e-4, weight_decay=1e-4)
+    return model, opt, SetCriterion(num_classes=1)
+
+
+def make_step(model, opt, criterion, images, targets, ctx, num_boxes):
+    core = model.module if hasattr(model, "module") else model
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(images, ctx)
+        losses = criterion(out, targets, num_boxes)
+        loss = sum(losses.values())
+        aux = core.moe_aux_loss()
+        if aux is not None:
+            loss = loss + aux
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 0.1)
+        opt.step()
+        return loss
+
+    return step
+
+
+def cpu_baseline(spec, batch_img, img_h, img_w, target_s):
+    """Same model, fp32 on host cores, MoE layers through the CPU oracle."""
+    from oracle.torch_bridge import use_oracle_moe
+    from src.rtdetr_moe.criterion import SetCriterion
+    from src.rtdetr_moe.data import SyntheticZOD
+    from src.rtdetr_moe.model import RTDETRMoE
+
+    threads = min(torch.get_num_threads(), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    torch.set_num_threads(threads)
+    torch.manual_seed(1)
+    model = RTDETRMoE(spec).to(memory_format=torch.channels_last)
+    n_moe = use_oracle_moe(model)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+    crit = SetCriterion(num_classes=1)
+    data = SyntheticZOD(batch=batch_img, img_h=img_h, img_w=img_w, seed=0)
+    images, targets, ctx = data.sample()
+    images = images.contiguous(memory_format=torch.channels_last)
+    nb = max(1.0, float(sum(len(t["boxes"]) for t in targets)))
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        out = model(images, ctx)
+        loss = sum(crit(out, targets, nb).values()) + model.moe_aux_loss()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 0.1)
+        opt.step()
+
+    t0 = time.perf_counter()
+    step()  # warm-up
+    warm = time.perf_counter() - t0
+    n = max(1, min(5, int(target_s / max(warm, 1e-3))))
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": round(batch_img * n / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"{n} timed fwd+bwd+AdamW steps (+1 warm-up) of {spec} at batch {batch_img}, "
+                      f"{img_w}x{img_h} padded to 32, fp32 on {threads} host threads, {n_moe} MoE layers "
+                      f"computed by oracle/moe_oracle.py (float64 numpy)"}
+
+
+def main():
+    args = parse_args()
+    world, rank, local = setup_dist(args.gpus)
+    device = torch.device("cuda", local)
+    wl = WORKLOADS[args.workload]
+    spec = wl["spec"].format(N=world)
+    batch = args.batch or wl["batch"]
+
+    from src.moe import _lib as L
+    from src.rtdetr_moe.data import SyntheticZOD
+
+    L.lib()  # fail loudly if the HIP extension is missing
+    model, opt, criterion = build_training(spec, device, world, local)
+    data = SyntheticZOD(batch=batch, img_h=args.img_h, img_w=args.img_w, seed=1000 + rank,
+                        single_context=(rank % 5) if wl.get("single_ctx") else None)
+    images, targets, ctx = data.sample()
+    images = images.to(device).contiguous(memory_format=torch.channels_last)
+    ctx = ctx.to(device)
+    targets = [{k: v.to(device) for k, v in t.items()} for t in targets]
+    nb = torch.tensor([float(sum(len(t["boxes"]) for t in targets))], device=device)
+    if world > 1:
+        dist.all_reduce(nb)
+    num_boxes = max(1.0, float(nb.item()) / world)
+    step = make_step(model, opt, criterion, images, targets, ctx, num_boxes)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    if not args.no_kernel_timing:
+        L.TIMER.start()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    L.TIMER.stop()
+    el = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    ksum = L.TIMER.summary() if not args.no_kernel_timing else {}
+
+    result = None
+    if rank == 0:
+        images_total = world * batch * args.steps
+        value = images_total / elapsed
+        roof = None
+        g = ksum.get("grouped_gemm")
+        if g and g["total_ms"] > 0:
+            ach = g["work"] / (g["total_ms"] * 1e-3) / 1e12
+            roof = {"bound": "mfma", "kernel": "grouped_gemm_kernel (all fwd/dgrad/wgrad variants)",
+                    "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                    "launches": g["launches"], "avg_us": round(g["avg_us"], 2),
+                    "flop_per_launch": round(g["work"] / g["launches"], 1),
+                    "share_of_step": round(g["total_ms"] / (elapsed * 1e3), 4)}
+        rd = None
+        dsp = ksum.get("dispatch")
+        if dsp and dsp["total_ms"] > 0:
+            ach = dsp["work"] / (dsp["total_ms"] * 1e-3) / 1e9
+            rd = {"bound": "hbm", "kernel": "permute_fwd/combine_fwd/combine_bwd", "achieved": round(ach, 1),
+                  "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+                  "launches": dsp["launches"], "avg_us": round(dsp["avg_us"], 2),
+                  "bytes_per_launch": round(dsp["work"] / dsp["launches"], 1)}
+        result = {
+            "metric": METRIC, "value": round(value, 3), "unit": "images/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (ZOD-shaped batches resident in HBM, random-init weights)",
+            "config": {"workload": wl["desc"], "arch": spec, "global_batch": world * batch,
+                       "img": f"{args.img_w}x{args.img_h} (padded to {data.pad_w}x{data.pad_h})",
+                       "parallelism": f"dp{world}" if "ep" not in spec else f"dp{world}+ep{world}"},
+            "roofline": roof, "roofline_dispatch": rd,
+        }
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                result["cpu_baseline"] = cpu_baseline(spec, 1, args.img_h, args.img_w, args.cpu_seconds)
+            except Exception as e:  # report, never hide, a failed baseline
+                result["cpu_baseline"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
+        else:
+            result["cpu_baseline"] = None
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -77,6 +77,59 @@ def lib() -> ctypes.CDLL:
     return _LIB
 
 
+class KernelTimer:
+    """Optional per-launch HIP-event timing of the MoE kernels (bench.py).
+
+    When enabled, every wrapped launch records a pair of torch.cuda.Events on
+    the stream it is launched on (torch's current stream -- the same stream
+    the C-ABI call receives) together with its algorithmic work: flops for the
+    grouped GEMMs (2*rows*N*K, rows read from the device offsets after the
+    timed region) and bytes for the row movers.
+    """
+
+    def __init__(self):
+        self.enabled = False
+        self.records = []  # (kind, start_event, end_event, work_fn)
+
+    def start(self):
+        self.records = []
+        self.enabled = True
+
+    def stop(self):
+        self.enabled = False
+
+    def wrap(self, kind, work_fn, launch):
+        if not self.enabled:
+            return launch()
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        out = launch()
+        e.record()
+        self.records.append((kind, s, e, work_fn))
+        return out
+
+    def summary(self):
+        """{kind: dict(launches, total_ms, avg_us, work, unit)} after a sync."""
+        torch.cuda.synchronize()
+        out = {}
+        for kind, s, e, work_fn in self.records:
+            d = out.setdefault(kind, {"launches": 0, "total_ms": 0.0, "work": 0.0})
+            d["launches"] += 1
+            d["total_ms"] += s.elapsed_time(e)
+            d["work"] += float(work_fn())
+        for d in out.values():
+            d["avg_us"] = 1e3 * d["total_ms"] / max(d["launches"], 1)
+        return out
+
+
+TIMER = KernelTimer()
+
+
+def _rows_of(offsets):
+    return lambda: int(offsets[-1].item())
+
+
 def _ptr(t: torch.Tensor | None) -> int | None:
     if t is None:
         return None
@@ -161,8 +214,11 @@ def permute_fwd(x, topk_idx, local_rank, rank_base, offsets, E, cap, rows_alloc)
     _need(x, torch.bfloat16, "x")
     xp = torch.empty((max(rows_alloc, 1), d), dtype=torch.bfloat16, device=x.device)
     pos = torch.empty((T, k), dtype=torch.int32, device=x.device)
-    rc = lib().moe_permute_fwd(_ptr(x), _ptr(topk_idx), _ptr(local_rank), _ptr(rank_base),
-                               _ptr(offsets), T, d, E, k, int(cap), _ptr(xp), _ptr(pos), _stream())
+    rows = _rows_of(offsets)
+    # read T rows + write kept rows + indices (idx, rank, pos: 12 B per assignment)
+    rc = TIMER.wrap("dispatch", lambda: 2.0 * d * (T + rows()) + 12.0 * T * k, lambda: lib().moe_permute_fwd(
+        _ptr(x), _ptr(topk_idx), _ptr(local_rank), _ptr(rank_base), _ptr(offsets), T, d, E, k, int(cap),
+        _ptr(xp), _ptr(pos), _stream()))
     _check(rc, "moe_permute_fwd")
     return xp, pos
 
@@ -172,7 +228,9 @@ def combine_fwd(yp, pos, topk_w, T):
     k = pos.shape[1]
     _need(yp, torch.bfloat16, "yp")
     y = torch.empty((T, d), dtype=torch.bfloat16, device=yp.device)
-    rc = lib().moe_combine_fwd(_ptr(yp), _ptr(pos), _ptr(topk_w), T, d, k, _ptr(y), _stream())
+    # read T*k rows (all kept when cap = 0) + gates/pos (8 B per assignment) + write T rows
+    rc = TIMER.wrap("dispatch", lambda: 2.0 * d * (T * k + T) + 8.0 * T * k, lambda: lib().moe_combine_fwd(
+        _ptr(yp), _ptr(pos), _ptr(topk_w), T, d, k, _ptr(y), _stream()))
     _check(rc, "moe_combine_fwd")
     return y
 
@@ -184,8 +242,9 @@ def combine_bwd(dy, yp, pos, topk_w):
     _need(yp, torch.bfloat16, "yp")
     dyp = torch.empty_like(yp)
     dw = torch.empty((T, k), dtype=torch.float32, device=dy.device)
-    rc = lib().moe_combine_bwd(_ptr(dy), _ptr(yp), _ptr(pos), _ptr(topk_w), T, d, k,
-                               _ptr(dyp), _ptr(dw), _stream())
+    # read dy (T rows) + Yp (T*k rows) + write dYp (T*k rows) + gates/pos/dw (12 B per assignment)
+    rc = TIMER.wrap("dispatch", lambda: 2.0 * d * (T + 2 * T * k) + 12.0 * T * k, lambda: lib().moe_combine_bwd(
+        _ptr(dy), _ptr(yp), _ptr(pos), _ptr(topk_w), T, d, k, _ptr(dyp), _ptr(dw), _stream()))
     _check(rc, "moe_combine_bwd")
     return dyp, dw
 
@@ -211,9 +270,10 @@ def grouped_gemm(a, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None,
     if a.shape[1] != K or a.shape[0] < max_rows:
         raise MoEKernelError("grouped_gemm: a must be [>=max_rows, K]")
     c = out if out is not None else torch.empty((a.shape[0], N), dtype=torch.bfloat16, device=a.device)
-    rc = lib().moe_grouped_gemm(MOE_BF16, _ptr(a), _ptr(b), _ptr(c), _ptr(offsets), G, int(max_rows),
-                                N, K, int(trans_b), int(epilogue), _ptr(bias), _ptr(aux), None,
-                                _stream())
+    rows = _rows_of(offsets)
+    rc = TIMER.wrap("grouped_gemm", lambda: 2.0 * rows() * N * K, lambda: lib().moe_grouped_gemm(
+        MOE_BF16, _ptr(a), _ptr(b), _ptr(c), _ptr(offsets), G, int(max_rows), N, K, int(trans_b),
+        int(epilogue), _ptr(bias), _ptr(aux), None, _stream()))
     _check(rc, "moe_grouped_gemm")
     return c
 
@@ -224,7 +284,8 @@ def grouped_gemm_wgrad(x, y, offsets, G, want_colsum=True):
     M, N = x.shape[1], y.shape[1]
     c = torch.empty((G, M, N), dtype=torch.float32, device=x.device)
     cs = torch.empty((G, M), dtype=torch.float32, device=x.device) if want_colsum else None
-    rc = lib().moe_grouped_gemm_wgrad(MOE_BF16, _ptr(x), _ptr(y), _ptr(c), _ptr(cs), _ptr(offsets),
-                                      G, M, N, _stream())
+    rows = _rows_of(offsets)
+    rc = TIMER.wrap("grouped_gemm", lambda: 2.0 * rows() * M * N, lambda: lib().moe_grouped_gemm_wgrad(
+        MOE_BF16, _ptr(x), _ptr(y), _ptr(c), _ptr(cs), _ptr(offsets), G, M, N, _stream()))
     _check(rc, "moe_grouped_gemm_wgrad")
     return c, cs

@@ -1,0 +1,160 @@
+"""RT-DETR set criterion: Hungarian matching (focal class cost + L1 + GIoU),
+varifocal classification loss, L1 and GIoU box losses, applied to the final
+decoder output, every auxiliary decoder layer and the encoder's top-k
+proposals.  (torchvision is absent in this image: the box ops are local.)"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+try:
+    from scipy.optimize import linear_sum_assignment
+except Exception:  # pragma: no cover
+    linear_sum_assignment = None
+
+
+def box_cxcywh_to_xyxy(b):
+    cx, cy, w, h = b.unbind(-1)
+    return torch.stack([cx - 0.5 * w, cy - 0.5 * h, cx + 0.5 * w, cy + 0.5 * h], -1)
+
+
+def box_area(b):
+    return (b[..., 2] - b[..., 0]).clamp(min=0) * (b[..., 3] - b[..., 1]).clamp(min=0)
+
+
+def box_iou(a, b):
+    """Pairwise IoU of xyxy boxes a [N,4], b [M,4] -> (iou [N,M], union)."""
+    area_a, area_b = box_area(a), box_area(b)
+    lt = torch.max(a[:, None, :2], b[None, :, :2])
+    rb = torch.min(a[:, None, 2:], b[None, :, 2:])
+    wh = (rb - lt).clamp(min=0)
+    inter = wh[..., 0] * wh[..., 1]
+    union = area_a[:, None] + area_b[None, :] - inter
+    return inter / union.clamp(min=1e-9), union
+
+
+def generalized_box_iou(a, b):
+    iou, union = box_iou(a, b)
+    lt = torch.min(a[:, None, :2], b[None, :, :2])
+    rb = torch.max(a[:, None, 2:], b[None, :, 2:])
+    wh = (rb - lt).clamp(min=0)
+    area = wh[..., 0] * wh[..., 1]
+    return iou - (area - union) / area.clamp(min=1e-9)
+
+
+class HungarianMatcher(nn.Module):
+    def __init__(self, cost_class=2.0, cost_bbox=5.0, cost_giou=2.0, alpha=0.25, gamma=2.0):
+        super().__init__()
+        self.cost_class, self.cost_bbox, self.cost_giou = cost_class, cost_bbox, cost_giou
+        self.alpha, self.gamma = alpha, gamma
+
+    @torch.no_grad()
+    def forward(self, outputs, targets):
+        return self.match_many([outputs], targets)[0]
+
+    @torch.no_grad()
+    def match_many(self, output_sets, targets):
+        """Match several prediction sets (final, aux layers, encoder) with ONE
+        device->host transfer of the stacked cost matrices."""
+        sizes = [len(t["boxes"]) for t in targets]
+        if sum(sizes) == 0:
+            e = torch.empty(0, dtype=torch.int64)
+            return [[(e, e) for _ in targets] for _ in output_sets]
+        logits = torch.stack([o["pred_logits"].float() for o in output_sets])  # [S, B, Q, C]
+        boxes = torch.stack([o["pred_boxes"].float() for o in output_sets])
+        S, B, Q, _ = logits.shape
+        prob = logits.flatten(0, 2).sigmoid()
+        out_bbox = boxes.flatten(0, 2)
+        tgt_ids = torch.cat([t["labels"] for t in targets])
+        tgt_bbox = torch.cat([t["boxes"] for t in targets]).float()
+        p = prob[:, tgt_ids]
+        neg = (1 - self.alpha) * p ** self.gamma * (-(1 - p + 1e-8).log())
+        pos = self.alpha * (1 - p) ** self.gamma * (-(p + 1e-8).log())
+        c_class = pos - neg
+        c_bbox = torch.cdist(out_bbox, tgt_bbox, p=1)
+        c_giou = -generalized_box_iou(box_cxcywh_to_xyxy(out_bbox), box_cxcywh_to_xyxy(tgt_bbox))
+        C = (self.cost_bbox * c_bbox + self.cost_class * c_class + self.cost_giou * c_giou)
+        C = C.view(S, B, Q, -1).cpu()  # one host round trip for every set
+        res = []
+        for s in range(S):
+            out = []
+            for i, c in enumerate(C[s].split(sizes, -1)):
+                if sizes[i] == 0:
+                    e = torch.empty(0, dtype=torch.int64)
+                    out.append((e, e))
+                    continue
+                r, col = linear_sum_assignment(c[i].numpy())
+                out.append((torch.as_tensor(r, dtype=torch.int64), torch.as_tensor(col, dtype=torch.int64)))
+            res.append(out)
+        return res
+
+
+class SetCriterion(nn.Module):
+    def __init__(self, num_classes=1, weight_vfl=1.0, weight_bbox=5.0, weight_giou=2.0, alpha=0.75, gamma=2.0):
+        super().__init__()
+        self.num_classes = num_classes
+        self.matcher = HungarianMatcher()
+        self.w = {"loss_vfl": weight_vfl, "loss_bbox": weight_bbox, "loss_giou": weight_giou}
+        self.alpha, self.gamma = alpha, gamma
+
+    def _idx(self, indices, device):
+        b = torch.cat([torch.full_like(s, i) for i, (s, _) in enumerate(indices)]).to(device)
+        s = torch.cat([s for s, _ in indices]).to(device)
+        return b, s
+
+    def _losses(self, out, targets, indices, num_boxes):
+        logits = out["pred_logits"].float()
+        boxes = out["pred_boxes"].float()
+        dev = logits.device
+        bi, si = self._idx(indices, dev)
+        tgt_boxes = torch.cat([t["boxes"][j] for t, (_, j) in zip(targets, indices)]).to(dev).float()
+        tgt_cls = torch.cat([t["labels"][j] for t, (_, j) in zip(targets, indices)]).to(dev)
+        src_boxes = boxes[bi, si]
+        # boxes
+        if tgt_boxes.numel():
+            l1 = F.l1_loss(src_boxes, tgt_boxes, reduction="none").sum() / num_boxes
+            giou = torch.diag(generalized_box_iou(box_cxcywh_to_xyxy(src_boxes), box_cxcywh_to_xyxy(tgt_boxes)))
+            lg = (1 - giou).sum() / num_boxes
+            ious = torch.diag(box_iou(box_cxcywh_to_xyxy(src_boxes.detach()), box_cxcywh_to_xyxy(tgt_boxes))[0])
+        else:
+            l1 = boxes.sum() * 0.0
+            lg = boxes.sum() * 0.0
+            ious = boxes.new_zeros(0)
+        # varifocal
+        target_classes = torch.full(logits.shape[:2], self.num_classes, dtype=torch.int64, device=dev)
+        target_classes[bi, si] = tgt_cls
+        target = F.one_hot(target_classes, self.num_classes + 1)[..., :-1].to(logits.dtype)
+        score = torch.zeros(logits.shape[:2], dtype=logits.dtype, device=dev)
+        score[bi, si] = ious.to(logits.dtype)
+        target_score = score.unsqueeze(-1) * target
+        pred_score = logits.sigmoid().detach()
+        weight = self.alpha * pred_score.pow(self.gamma) * (1 - target) + target_score
+        vfl = F.binary_cross_entropy_with_logits(logits, target_score, weight=weight, reduction="none")
+        vfl = vfl.mean(1).sum() * logits.shape[1] / num_boxes
+        return {"loss_vfl": vfl, "loss_bbox": l1, "loss_giou": lg}
+
+    def forward(self, outputs, targets, num_boxes: float):
+        losses = {}
+        sets = [("", outputs)] + [(f"_aux{i}", a) for i, a in enumerate(outputs.get("aux_outputs", []))]
+        if "enc_outputs" in outputs:
+            sets.append(("_enc", outputs["enc_outputs"]))
+        all_indices = self.matcher.match_many([o for _, o in sets], targets)
+        for (suffix, out), indices in zip(sets, all_indices):
+            for k, v in self._losses(out, targets, indices, num_boxes).items():
+                losses[k + suffix] = v * self.w[k]
+        return losses
+
+
+def targets_to_device(targets, device):
+    return [{k: (v.to(device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in t.items()}
+            for t in targets]
+
+
+def count_boxes(targets) -> int:
+    return int(sum(len(t["boxes"]) for t in targets))
+
+
+def as_numpy_boxes(t):
+    return np.asarray(t["boxes"].detach().cpu().numpy(), dtype=np.float64)
