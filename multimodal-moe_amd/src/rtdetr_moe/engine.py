@@ -1,16 +1,405 @@
-"""Training / validation engine (filled in below the DDP helpers)."""
+"""Training / validation engine behind src/models/vision/rtdetr.py.
+
+Replaces what the reference delegates to Ultralytics (``RTDETR(cfg.model)
+.train(...)`` / ``.val(...)``, src/models/vision/rtdetr.py:82-94, :112-127):
+  * ``train(...)``    -> TrainResults  (.results_dict, .model, .save_dir, .best, .last)
+  * ``validate(...)`` -> DetMetrics    (.results_dict, .box, .speed, .model)
+Devices follow the reference's ``device`` string ("cpu", "0", "0,1,2,3"):
+one process per GPU; a multi-GPU string launches that many local workers
+(torch.multiprocessing) unless the caller is already under torchrun; gradients
+are all-reduced by DDP over RCCL.  bf16 autocast on GPU,
+fp32 on CPU (config C1).
+"""
 from __future__ import annotations
 
+import csv
+import json
+import math
+import os
+import random
+import time
+from dataclasses import asdict, dataclass, field
+from pathlib import Path
+
+import numpy as np
 import torch
+import torch.distributed as dist
 from torch.nn.parallel import DistributedDataParallel as DDP
 
+from ..moe.config import parse_moe_spec
+from .criterion import SetCriterion
+from .data import SyntheticZOD, YoloDataset, collate
+from .metrics import BoxMetrics, DetectionEvaluator
+from .model import RTDETRMoE
 
-def wrap_ddp(model: torch.nn.Module, local_rank: int, bucket_cap_mb: int = 64) -> DDP:
+
+# ---------------------------------------------------------------------------
+# distributed helpers
+# ---------------------------------------------------------------------------
+def wrap_ddp(model: torch.nn.Module, local_rank: int | None, bucket_cap_mb: int = 64) -> DDP:
     """Data-parallel wrapper over RCCL.  Expert weights
     that are sharded over an expert-parallel group (C4) are excluded from the
     gradient all-reduce."""
     ignore = [n for n, p in model.named_parameters() if getattr(p, "expert_parallel", False)]
     if ignore:
         DDP._set_params_and_buffers_to_ignore_for_model(model, ignore)
-    return DDP(model, device_ids=[local_rank], output_device=local_rank, broadcast_buffers=False,
-               gradient_as_bucket_view=True, bucket_cap_mb=bucket_cap_mb)
+    kw = dict(device_ids=[local_rank], output_device=local_rank) if local_rank is not None else {}
+    return DDP(model, broadcast_buffers=False, gradient_as_bucket_view=True, bucket_cap_mb=bucket_cap_mb, **kw)
+
+
+def parse_device(device: str | int | None) -> list:
+    """"cpu" -> ["cpu"]; "0" -> [0]; "0,1" -> [0, 1]; "" / None -> [0] if a GPU else ["cpu"]."""
+    s = "" if device is None else str(device).strip().lower()
+    if s in ("", "auto"):
+        return [0] if torch.cuda.is_available() else ["cpu"]
+    if s == "cpu":
+        return ["cpu"]
+    s = s.replace("cuda:", "")
+    return [int(v) for v in s.split(",") if v.strip() != ""]
+
+
+def _dist_ctx():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+# ---------------------------------------------------------------------------
+# model handle / results objects (the attributes the reference reads)
+# ---------------------------------------------------------------------------
+class ModelHandle:
+    """``.model`` is the nn.Module (yolo.py:108-114 reads .model.parameters()
+    and .model.flops/.GFLOPs)."""
+
+    def __init__(self, module: RTDETRMoE):
+        self.model = module
+
+    def __repr__(self):
+        return f"ModelHandle({self.model.spec.raw})"
+
+
+@dataclass
+class TrainResults:
+    results_dict: dict
+    model: ModelHandle | None
+    save_dir: Path
+    best: Path | None
+    last: Path | None
+    epochs_run: int = 0
+    moe: dict = field(default_factory=dict)
+
+
+@dataclass
+class DetMetrics:
+    results_dict: dict
+    box: BoxMetrics
+    speed: dict
+    model: ModelHandle | None
+    save_dir: Path | None = None
+    moe: dict = field(default_factory=dict)
+
+
+def _results_dict(box: BoxMetrics) -> dict:
+    return {"metrics/precision(B)": box.mp, "metrics/recall(B)": box.mr, "metrics/mAP50(B)": box.map50,
+            "metrics/mAP50-95(B)": box.map, "fitness": 0.1 * box.map50 + 0.9 * box.map}
+
+
+# ---------------------------------------------------------------------------
+# checkpoints: plain dicts of tensors / primitives (torch.load weights_only=True)
+# ---------------------------------------------------------------------------
+def save_checkpoint(path: Path, model: RTDETRMoE, epoch: int, fitness: float, optimizer=None):
+    path.parent.mkdir(parents=True, exist_ok=True)
+    ck = {"spec": model.spec.raw, "num_classes": model.num_classes, "epoch": int(epoch),
+          "fitness": float(fitness), "state_dict": {k: v.detach().cpu() for k, v in model.state_dict().items()}}
+    if model.spec.moe is not None:
+        ck["moe_cfg"] = {k: v for k, v in asdict(model.spec.moe).items()}
+    if optimizer is not None:
+        ck["optimizer"] = optimizer.state_dict()
+    torch.save(ck, path)
+
+
+def load_model(weights: str | Path, device="cpu") -> RTDETRMoE:
+    """A checkpoint written by save_checkpoint, or a bare architecture spec."""
+    p = Path(str(weights))
+    if p.exists():
+        ck = torch.load(p, map_location="cpu", weights_only=True)
+        model = RTDETRMoE(parse_moe_spec(ck["spec"]), num_classes=int(ck.get("num_classes", 1)))
+        model.load_state_dict(ck["state_dict"])
+        return model.to(device)
+    if str(weights).endswith((".pt", ".pth")):
+        raise FileNotFoundError(f"weights file not found: {weights}")
+    return RTDETRMoE(parse_moe_spec(str(weights))).to(device)
+
+
+# ---------------------------------------------------------------------------
+# data
+# ---------------------------------------------------------------------------
+def _is_synthetic(data) -> bool:
+    return str(data).startswith("synthetic")
+
+
+def _synthetic_steps(data, default=4) -> int:
+    s = str(data)
+    return int(s.split(":", 1)[1]) if ":" in s else default
+
+
+def _hw(imgsz):
+    return (imgsz, imgsz) if isinstance(imgsz, int) else (int(imgsz[0]), int(imgsz[1]))
+
+
+def _batches(data, split, imgsz, batch, workers, seed, rank, world, epoch):
+    h, w = _hw(imgsz)
+    if _is_synthetic(data):
+        gen = SyntheticZOD(batch=batch, img_h=h, img_w=w, seed=seed * 1000 + rank + (0 if split == "train" else 777)
+                           + epoch * 7919)
+        for _ in range(_synthetic_steps(data)):
+            yield gen.sample()
+        return
+    ds = YoloDataset(data, split=split, imgsz=(h, w))
+    sampler = torch.utils.data.distributed.DistributedSampler(ds, world, rank, shuffle=split == "train",
+                                                              seed=seed) if world > 1 else None
+    if sampler is not None:
+        sampler.set_epoch(epoch)
+    g = torch.Generator().manual_seed(seed + epoch)
+    dl = torch.utils.data.DataLoader(ds, batch_size=batch, shuffle=(split == "train" and sampler is None),
+                                     sampler=sampler, num_workers=workers, collate_fn=collate,
+                                     generator=g, drop_last=False, persistent_workers=False)
+    yield from dl
+
+
+# ---------------------------------------------------------------------------
+# training
+# ---------------------------------------------------------------------------
+@dataclass
+class TrainArgs:
+    model: str
+    data: str
+    imgsz: object = (704, 1248)
+    epochs: int = 50
+    patience: int = 100
+    batch: int = 16
+    device: str = "0"
+    project: str = "outputs/runs/rtdetr"
+    name: str = "baseline"
+    seed: int = 0
+    workers: int = 8
+    lr: float = 1e-4
+    lr_backbone: float = 1e-5
+    weight_decay: float = 1e-4
+    clip_norm: float = 0.1
+
+
+def _seed_all(seed: int):
+    random.seed(seed)
+    np.random.seed(seed % (2 ** 32))
+    torch.manual_seed(seed)
+
+
+def _optimizer(model: RTDETRMoE, a: TrainArgs):
+    bb = [p for n, p in model.named_parameters() if n.startswith("backbone.") and p.requires_grad]
+    rest = [p for n, p in model.named_parameters() if not n.startswith("backbone.") and p.requires_grad]
+    return torch.optim.AdamW([{"params": bb, "lr": a.lr_backbone}, {"params": rest, "lr": a.lr}],
+                             lr=a.lr, weight_decay=a.weight_decay)
+
+
+def _train_worker(a: TrainArgs, rank: int, world: int, local: int | str) -> TrainResults | None:
+    on_gpu = local != "cpu"
+    device = torch.device("cuda", local) if on_gpu else torch.device("cpu")
+    if on_gpu:
+        torch.cuda.set_device(local)
+        from ..moe import _lib
+
+        _lib.lib()  # the GPU path has no fallback: fail now if libmoe_hip.so is missing
+    _seed_all(a.seed)
+    model = load_model(a.model, device)
+    if on_gpu:
+        model = model.to(memory_format=torch.channels_last)
+    core = model
+    net = wrap_ddp(model, local if on_gpu else None) if world > 1 else model
+    opt = _optimizer(core, a)
+    crit = SetCriterion(num_classes=core.num_classes)
+    save_dir = Path(a.project) / a.name
+    wdir = save_dir / "weights"
+    if rank == 0:
+        wdir.mkdir(parents=True, exist_ok=True)
+    best_fit, best_epoch = -1.0, -1
+    last_metrics = BoxMetrics()
+    csv_rows = []
+    epoch = 0
+    for epoch in range(a.epochs):
+        net.train()
+        t_ep = time.perf_counter()
+        tot, n = 0.0, 0
+        for images, targets, ctx in _batches(a.data, "train", a.imgsz, a.batch, a.workers, a.seed, rank, world,
+                                             epoch):
+            images = images.to(device, non_blocking=True)
+            if on_gpu:
+                images = images.contiguous(memory_format=torch.channels_last)
+            ctx = ctx.to(device)
+            tg = [{"boxes": t["boxes"].to(device), "labels": t["labels"].to(device)} for t in targets]
+            nb = torch.tensor([float(sum(len(t["boxes"]) for t in tg))], device=device)
+            if world > 1:
+                dist.all_reduce(nb)
+            num_boxes = max(1.0, float(nb.item()) / world)
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast(device.type, dtype=torch.bfloat16, enabled=on_gpu):
+                out = net(images, ctx)
+            losses = crit(out, tg, num_boxes)
+            loss = sum(losses.values())
+            aux = core.moe_aux_loss()
+            if aux is not None:
+                loss = loss + aux
+            loss.backward()
+            if a.clip_norm > 0:
+                torch.nn.utils.clip_grad_norm_(net.parameters(), a.clip_norm)
+            opt.step()
+            tot += float(loss.detach())
+            n += 1
+        # validation (rank 0 evaluates the unwrapped model)
+        metrics = None
+        if rank == 0:
+            metrics = _evaluate(core, a.data, "val", a.imgsz, a.batch, device, a.workers, a.seed)
+            last_metrics = metrics
+            fit = _results_dict(metrics)["fitness"]
+            save_checkpoint(wdir / "last.pt", core, epoch, fit)
+            if fit > best_fit:
+                best_fit, best_epoch = fit, epoch
+                save_checkpoint(wdir / "best.pt", core, epoch, fit)
+            row = {"epoch": epoch + 1, "train/loss": tot / max(n, 1), "time_s": time.perf_counter() - t_ep,
+                   **_results_dict(metrics)}
+            row.update(_moe_stats(core))
+            csv_rows.append(row)
+        stop = torch.tensor([0.0], device=device)
+        if rank == 0 and epoch - best_epoch >= a.patience:
+            stop[0] = 1.0
+        if world > 1:
+            dist.broadcast(stop, 0)
+        if float(stop.item()) > 0:
+            break
+    if rank != 0:
+        return None
+    with open(save_dir / "results.csv", "w", newline="") as f:
+        if csv_rows:
+            wr = csv.DictWriter(f, fieldnames=list(csv_rows[0].keys()))
+            wr.writeheader()
+            wr.writerows(csv_rows)
+    return TrainResults(results_dict=_results_dict(last_metrics), model=ModelHandle(core), save_dir=save_dir,
+                        best=wdir / "best.pt", last=wdir / "last.pt", epochs_run=epoch + 1, moe=_moe_stats(core))
+
+
+def _moe_stats(model: RTDETRMoE) -> dict:
+    out = {}
+    layers = model.moe_layers()
+    for i, m in enumerate(layers):
+        if m.last_hist is not None:
+            h = m.last_hist.detach().float().cpu()
+            out[f"moe/l{i}_load_cv"] = float(h.std() / h.mean().clamp(min=1e-9))
+        if m.last_aux is not None:
+            out[f"moe/l{i}_lb"] = float(m.last_aux[0].detach())
+            out[f"moe/l{i}_z"] = float(m.last_aux[1].detach())
+    return out
+
+
+def _mp_entry(local_idx, a, devices, port, out_file):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(local_idx),
+                       "WORLD_SIZE": str(len(devices)), "LOCAL_RANK": str(local_idx)})
+    dev = devices[local_idx]
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    try:
+        res = _train_worker(a, local_idx, len(devices), dev)
+        if local_idx == 0 and res is not None:
+            Path(out_file).write_text(json.dumps({"results_dict": res.results_dict, "epochs_run": res.epochs_run,
+                                                  "moe": res.moe}))
+    finally:
+        dist.destroy_process_group()
+
+
+def train(a: TrainArgs) -> TrainResults:
+    devices = parse_device(a.device)
+    if dist.is_available() and dist.is_initialized():  # already under torchrun
+        rank, world = dist.get_rank(), dist.get_world_size()
+        local = int(os.environ.get("LOCAL_RANK", rank)) if devices != ["cpu"] else "cpu"
+        return _train_worker(a, rank, world, local)
+    if devices == ["cpu"] or len(devices) == 1:
+        return _train_worker(a, 0, 1, devices[0])
+    import socket
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out_file = Path(tempfile.mkdtemp()) / "rank0.json"
+    mp.spawn(_mp_entry, args=(a, devices, port, str(out_file)), nprocs=len(devices), join=True)
+    d = json.loads(out_file.read_text())
+    save_dir = Path(a.project) / a.name
+    model = load_model(save_dir / "weights" / "last.pt", "cpu")
+    return TrainResults(results_dict=d["results_dict"], model=ModelHandle(model), save_dir=save_dir,
+                        best=save_dir / "weights" / "best.pt", last=save_dir / "weights" / "last.pt",
+                        epochs_run=d["epochs_run"], moe=d.get("moe", {}))
+
+
+# ---------------------------------------------------------------------------
+# validation
+# ---------------------------------------------------------------------------
+@torch.no_grad()
+def _evaluate(model: RTDETRMoE, data, split, imgsz, batch, device, workers, seed, speed: dict | None = None):
+    model.eval()
+    on_gpu = device.type == "cuda"
+    ev = DetectionEvaluator()
+    t_pre = t_inf = t_post = 0.0
+    n_img = 0
+    for images, targets, ctx in _batches(data, split, imgsz, batch, workers, seed, 0, 1, 0):
+        t0 = time.perf_counter()
+        images = images.to(device, non_blocking=True)
+        if on_gpu:
+            images = images.contiguous(memory_format=torch.channels_last)
+            torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        with torch.autocast(device.type, dtype=torch.bfloat16, enabled=on_gpu):
+            out = model(images, ctx.to(device))
+        if on_gpu:
+            torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        H, W = images.shape[-2:]
+        dets = model.postprocess(out, [(W, H)] * images.shape[0])
+        for det, t in zip(dets, targets):
+            gt = t["boxes"].numpy().astype(np.float64)
+            gt_xyxy = np.stack([(gt[:, 0] - gt[:, 2] / 2) * W, (gt[:, 1] - gt[:, 3] / 2) * H,
+                                (gt[:, 0] + gt[:, 2] / 2) * W, (gt[:, 1] + gt[:, 3] / 2) * H], 1) \
+                if len(gt) else np.zeros((0, 4))
+            ev.update(det["boxes"].float().cpu().numpy(), det["scores"].float().cpu().numpy(),
+                      det["labels"].cpu().numpy(), gt_xyxy, t["labels"].numpy())
+        t3 = time.perf_counter()
+        t_pre += t1 - t0
+        t_inf += t2 - t1
+        t_post += t3 - t2
+        n_img += images.shape[0]
+    model.train()
+    if speed is not None and n_img:
+        speed.update({"preprocess": 1e3 * t_pre / n_img, "inference": 1e3 * t_inf / n_img,
+                      "loss": 0.0, "postprocess": 1e3 * t_post / n_img})
+    return ev.compute()
+
+
+def validate(weights, data, split="val", imgsz=(704, 1248), batch=16, device="0", project=None, name=None,
+             workers=4, seed=0) -> DetMetrics:
+    devices = parse_device(device)
+    dev = torch.device("cpu") if devices == ["cpu"] else torch.device("cuda", devices[0])
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+        from ..moe import _lib
+
+        _lib.lib()
+    model = load_model(weights, dev)
+    if dev.type == "cuda":
+        model = model.to(memory_format=torch.channels_last)
+    speed = {}
+    box = _evaluate(model, data, split, imgsz, batch, dev, workers, seed, speed)
+    save_dir = Path(project) / name if project and name else None
+    if save_dir is not None:
+        save_dir.mkdir(parents=True, exist_ok=True)
+    return DetMetrics(results_dict=_results_dict(box), box=box, speed=speed, model=ModelHandle(model),
+                      save_dir=save_dir, moe=_moe_stats(model))

@@ -31,6 +31,47 @@ class RTDETRMoE(nn.Module):
         nl = spec.num_decoder_layers or _DEC_LAYERS[spec.backbone]
         self.decoder = RTDETRDecoder(num_classes=num_classes, num_layers=nl, moe=spec.moe)
 
+    @property
+    def GFLOPs(self) -> float | None:
+        """Forward GFLOPs of one 640x640 image (Ultralytics' convention):
+        torch's FlopCounterMode for the dense ops + the routed expert FFNs and
+        routers counted analytically (their HIP kernels are opaque to it)."""
+        if getattr(self, "_gflops", None) is None:
+            try:
+                from torch.utils.flop_counter import FlopCounterMode
+
+                dev = next(self.parameters()).device
+                x = torch.zeros((1, 3, 640, 640), device=dev)
+                saved = [m.__dict__.get("forward") for m in self.moe_layers()]
+                for m in self.moe_layers():  # identity stand-in: count the dense body only
+                    m.forward = (lambda x, ctx=None: x)
+                was = self.training
+                self.eval()
+                try:
+                    with torch.no_grad(), FlopCounterMode(display=False) as fc:
+                        self(x, None)
+                finally:
+                    for m, f in zip(self.moe_layers(), saved):
+                        if f is None:
+                            del m.forward
+                        else:
+                            m.forward = f
+                    self.train(was)
+                dense = fc.get_total_flops()
+                moe = 0.0
+                for i, m in enumerate(self.moe_layers()):
+                    T = 400 if i == 0 else self.decoder.num_queries  # AIFI on S5 (20x20) / decoder queries
+                    c = m.cfg
+                    moe += T * (2 * m.d_model * c.num_experts + c.top_k * 4 * m.d_model * c.hidden)
+                self._gflops = (dense + moe) / 1e9
+            except Exception:
+                return None
+        return self._gflops
+
+    @property
+    def flops(self):
+        return self.GFLOPs
+
     def moe_layers(self):
         return [m for m in self.modules() if isinstance(m, MoEFFN)]
 
