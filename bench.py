@@ -64,6 +64,10 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample length")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip per-launch HIP events")
+    ap.add_argument("--graphs", action=argparse.BooleanOptionalAction, default=False,
+                    help="capture the model forward/backward as hipGraphs (no per-kernel HIP-event timing: "
+                         "ROCm 7.2 does not stamp timing events recorded inside a graph, "
+                         "tools/graph_event_probe.py)")
     return ap.parse_args()
 
 
@@ -81,39 +85,15 @@ def setup_dist(n_gpus):
     return world, rank, local
 
 
-def build_training(spec, device, world, local):
-    from src.rtdetr_moe.criterion import SetCriterion
+def build_model(spec, device, world):
     from src.rtdetr_moe.model import RTDETRMoE
 
     torch.manual_seed(1)
     model = RTDETRMoE(spec).to(device).to(memory_format=torch.channels_last)
-    if world > 1:
-        from src.rtdetr_moe.engine import wrap_ddp
-
-        model = wrap_ddp(model, local)
-    params = [p for p in model.parameters() if p.requires_grad]
-    opt = torch.optim.AdamW(params, lr=1e-4, weight_decay=1e-4)
-    return model, opt, SetCriterion(num_classes=1)
-
-
-def make_step(model, opt, criterion, images, targets, ctx, num_boxes):
-    core = model.module if hasattr(model, "module") else model
-
-    def step():
-        opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            out = model(images, ctx)
-        losses = criterion(out, targets, num_boxes)
-        loss = sum(losses.values())
-        aux = core.moe_aux_loss()
-        if aux is not None:
-            loss = loss + aux
-        loss.backward()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 0.1)
-        opt.step()
-        return loss
-
-    return step
+    if world > 1:  # identical initial weights on every rank (DDP would broadcast them)
+        for t in list(model.parameters()) + list(model.buffers()):
+            dist.broadcast(t.data, 0)
+    return model
 
 
 def cpu_baseline(spec, batch_img, img_h, img_w, target_s):
@@ -169,7 +149,10 @@ def main():
     from src.rtdetr_moe.data import SyntheticZOD
 
     L.lib()  # fail loudly if the HIP extension is missing
-    model, opt, criterion = build_training(spec, device, world, local)
+    from src.rtdetr_moe.criterion import SetCriterion
+    from src.rtdetr_moe.step import TrainStep
+
+    model = build_model(spec, device, world)
     data = SyntheticZOD(batch=batch, img_h=args.img_h, img_w=args.img_w, seed=1000 + rank,
                         single_context=(rank % 5) if wl.get("single_ctx") else None)
     images, targets, ctx = data.sample()
@@ -180,18 +163,27 @@ def main():
     if world > 1:
         dist.all_reduce(nb)
     num_boxes = max(1.0, float(nb.item()) / world)
-    step = make_step(model, opt, criterion, images, targets, ctx, num_boxes)
+
+    timing = not args.no_kernel_timing
+    if timing:  # graph mode: the event pairs are captured as nodes of the hipGraphs
+        L.TIMER.start(mode="graph" if args.graphs else "eager")
+    ddp_local = local if (world > 1 and not args.graphs) else None
+    step = TrainStep(model, SetCriterion(num_classes=1), images, ctx, graphs=args.graphs, world=world,
+                     ddp_local=ddp_local)
 
     for _ in range(args.warmup):
-        step()
+        step(images, ctx, targets, num_boxes)
+    if timing:
+        L.TIMER.harvest()
+        L.TIMER.reset_totals()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if not args.no_kernel_timing:
-        L.TIMER.start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(images, ctx, targets, num_boxes)
+        if timing:
+            L.TIMER.harvest()  # syncs: read this step's kernel events
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -201,7 +193,7 @@ def main():
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    ksum = L.TIMER.summary() if not args.no_kernel_timing else {}
+    ksum = L.TIMER.summary() if timing else {}
 
     result = None
     if rank == 0:
@@ -231,6 +223,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (ZOD-shaped batches resident in HBM, random-init weights)",
             "config": {"workload": wl["desc"], "arch": spec, "global_batch": world * batch,
+                       "execution": "hipGraph fwd/bwd" if args.graphs else "eager",
                        "img": f"{args.img_w}x{args.img_h} (padded to {data.pad_w}x{data.pad_h})",
                        "parallelism": f"dp{world}" if "ep" not in spec else f"dp{world}+ep{world}"},
             "roofline": roof, "roofline_dispatch": rd,

@@ -137,6 +137,12 @@ int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, float* c,
                            float* colsum, const int32_t* offsets, int G,
                            int M, int N, hipStream_t stream);
 
+/* Process-wide tuning knobs (not thread-safe; set before launching):
+ *   "gemm_variant" 1 = register-staged double buffer, 2 = LDS-DMA ring (default)
+ *   "gemm_stages"  3 (default) or 4 ring slots for variant 2
+ * Returns 0, or -1 for an unknown key/value. */
+int moe_set_tuning(const char* key, int value);
+
 /* Thread-local message for the last non-zero return code. */
 const char* moe_last_error(void);
 

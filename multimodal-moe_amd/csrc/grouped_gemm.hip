@@ -1,6 +1,6 @@
 // Grouped expert GEMMs on bf16 MFMA for gfx950.
 //
-// One kernel template covers the five expert contractions of the MoE FFN:
+// One kernel template family covers the five expert contractions of the FFN:
 //   ROWS mode  (rows of group g = tokens routed to expert g, K/N fixed)
 //     fwd   H  = relu(Xp . W1_g^T + b1_g)      A=[rows][K]  B=[N][K]  (trans_b=1)
 //     fwd   Yp = H . W2_g^T + b2_g             A=[rows][K]  B=[N][K]  (trans_b=1)
@@ -9,19 +9,23 @@
 //   WGRAD mode (K = rows of group g, M/N fixed)
 //     dW2_g = dYp^T . H  (+ db2 = colsum dYp), dW1_g = dH^T . Xp (+ db1)
 //
-// Tiling: 256 threads = 4 waves in 2x2, block tile BM x BN (BM in {64,128},
-// BN = 128), K-step 64, v_mfma_f32_16x16x32_bf16 with the operands swapped
-// (D = B^T-frag x A-frag) so that each lane ends with 4 consecutive output
-// columns of one row (8-B bf16 / 16-B fp32 stores).  Operands are staged
-// global -> registers -> LDS (double-buffered, one barrier per K-step, next
-// tile's global loads in flight under the current tile's MFMAs).
-// Two LDS images:
+// Tiling: 256 threads = 4 waves in 2x2, block tile BM x 128, K-step 64,
+// v_mfma_f32_16x16x32_bf16 with the operands swapped (D = B^T-frag x A-frag) so
+// that each lane ends with 4 consecutive output columns of one row.
+// Two LDS images per operand tile:
 //   K-contiguous  [R][64] bf16, 128-B rows, 16-B chunk c of row r stored at
 //                 chunk c ^ ((r>>1)&7): conflict-free ds_read_b128 fragments;
 //   MN-contiguous [64][R] bf16 (weights read for dgrad, activations for
-//                 wgrad), fragments by ds_read_b64_tr_b16 (hardware
-//                 transpose), chunk XOR swizzle chosen so that the two 16-lane
-//                 blocks of each 32-lane half hit 16 distinct 16-B slots.
+//                 wgrad), fragments by ds_read_b64_tr_b16 (hardware transpose),
+//                 XOR swizzle so the two 16-lane blocks of each 32-lane half hit
+//                 16 distinct 16-B slots.
+// Two main loops:
+//   v1 (pipe_kernel<...,1>): global -> registers -> LDS, double buffer, one
+//      tile of lookahead (handles every shape; kept for A/B);
+//   v2 (default): global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
+//      wave-instruction, swizzle applied to the per-lane SOURCE address), an
+//      S-deep ring with S-1 K-tiles in flight, counted `s_waitcnt vmcnt` +
+//      raw s_barrier (no vmcnt(0) drain inside the loop).
 #include "moe_common.h"
 
 namespace moe {
@@ -42,70 +46,28 @@ struct GemmParams {
   int G, M, N, K;
 };
 
+// runtime tuning knobs (moe_set_tuning)
+static int g_gemm_variant = 2;
+static int g_gemm_stages = 3;
+
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 // byte offset of 16-B chunk c of row r in a K-contiguous [R][64] image
 __device__ __forceinline__ int kimg_off(int r, int c) {
   return r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
 }
-// byte offset of 16-B chunk c of k-row r in an MN-contiguous [64][R] image
+// chunk swizzle of an MN-contiguous [64][R] image (R = 128 or 64 bf16 per k-row)
+template <int R>
+__device__ __forceinline__ int mimg_swz(int r) {
+  if constexpr (R == 128) return ((r & 3) << 1) | (((r >> 3) & 1) << 3);
+  else return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2);
+}
 template <int R>
 __device__ __forceinline__ int mimg_off(int r, int c) {
-  if constexpr (R == 128) {
-    const int f = ((r & 3) << 1) | (((r >> 3) & 1) << 3);
-    return r * 256 + ((c ^ f) << 4);
-  } else {
-    const int f = (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2);
-    return r * 128 + ((c ^ f) << 4);
-  }
+  return r * (R * 2) + ((c ^ mimg_swz<R>(r)) << 4);
 }
 
-// Operand loader for one K-step tile: R rows of the operand (m or n) x 64 k.
-// KCONT: storage is [row][k] (row stride ld); else [k][row] (k stride ld).
-template <int R, bool KCONT>
-struct TileLoader {
-  static constexpr int kChunks = R * 64 / 8;  // 16-B chunks per tile
-  static constexpr int kPer = kChunks / 256;  // per thread
-  uint4 reg[kPer];
-
-  // base: pointer to element (row0, k0) of the operand (already group-offset);
-  // row_lim / k_lim: valid extents (rows beyond -> zeros).
-  __device__ __forceinline__ void load(const uint16_t* base, int ld, int row_lim, int k_lim,
-                                       int tid) {
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int q = tid + 256 * i;
-      int r, kk;
-      if constexpr (KCONT) {
-        r = q >> 3;
-        kk = (q & 7) * 8;
-      } else {
-        constexpr int cpr = R / 8;  // chunks per k-row
-        kk = q / cpr;
-        r = (q % cpr) * 8;
-      }
-      const bool ok = KCONT ? (r < row_lim && kk < k_lim) : (kk < k_lim && r < row_lim);
-      const uint16_t* p = KCONT ? base + (size_t)r * ld + kk : base + (size_t)kk * ld + r;
-      reg[i] = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
-    }
-  }
-  __device__ __forceinline__ void store(char* lds, int tid) const {
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int q = tid + 256 * i;
-      int off;
-      if constexpr (KCONT) {
-        off = kimg_off(q >> 3, q & 7);
-      } else {
-        constexpr int cpr = R / 8;
-        off = mimg_off<R>(q / cpr, q % cpr);
-      }
-      *reinterpret_cast<uint4*>(lds + off) = reg[i];
-    }
-  }
-};
-
-// Fragment (8 bf16 along k) for operand row `row` (0..R-1) at k-step ks.
+// Fragment (8 bf16 along k) for operand row block `row_base` (16 rows) at k-step ks.
 template <int R, bool KCONT>
 __device__ __forceinline__ bf16x8 read_frag(const char* lds, int row_base, int ks, int lane) {
   if constexpr (KCONT) {
@@ -138,129 +100,82 @@ __device__ __forceinline__ float sum8(bf16x8 v) {
   return s;
 }
 
-template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM>
-__global__ __launch_bounds__(256) void grouped_gemm_kernel(GemmParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int A_BYTES = BM * 64 * 2;
-  constexpr int B_BYTES = BN * 64 * 2;
-  constexpr int BUF = A_BYTES + B_BYTES;
-  constexpr int TM = BM / 32;  // 16-row sub-tiles per wave
-  constexpr int TN = BN / 32;
+// ---------------------------------------------------------------------------
+// tile schedule + operand addressing shared by both main loops
+// ---------------------------------------------------------------------------
+template <int BM, int BN, bool B_K, int MODE>
+struct Tile {
+  int g, mt, nt, row0, rows_g, m0, n0, a_row_lim, nk;
+  const uint16_t* a_base;  // element (m0 or row0, k=0) of logical A
+  const uint16_t* b_base;  // element (k=0, n0) of logical B
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-
-  // ---- tile -> (group, m-tile, n-tile) ----
-  int g, mt, nt, row0, rows_g;
-  if constexpr (MODE == MODE_ROWS) {
-    int rem = blockIdx.x;
-    g = 0;
-    for (; g < p.G; ++g) {
-      const int n_g = p.offsets[g + 1] - p.offsets[g];
-      const int t_g = (n_g + BM - 1) / BM;
-      if (rem < t_g) break;
-      rem -= t_g;
-    }
-    if (g >= p.G) return;  // beyond the last tile (grid is an upper bound)
-    mt = rem;
-    nt = blockIdx.y;
-    row0 = p.offsets[g] + mt * BM;
-    rows_g = p.offsets[g + 1] - row0;  // valid rows from row0
-  } else {
-    g = blockIdx.y;
-    const int ntn = p.N / BN;
-    mt = blockIdx.x / ntn;
-    nt = blockIdx.x % ntn;
-    row0 = p.offsets[g];
-    rows_g = p.offsets[g + 1] - row0;  // K extent of this group
-  }
-  const int m0 = mt * BM, n0 = nt * BN;
-
-  // ---- operand base pointers and limits ----
-  // A logical [m][k]; B logical [k][n].
-  const uint16_t* a_base;
-  const uint16_t* b_base;
-  int a_row_lim, nk;
-  if constexpr (MODE == MODE_ROWS) {
-    a_base = p.a + (size_t)row0 * p.lda;           // [rows][K]
-    a_row_lim = rows_g < BM ? rows_g : BM;
-    const uint16_t* bg = p.b + (size_t)g * p.stride_b;
-    b_base = B_K ? bg + (size_t)n0 * p.ldb : bg + n0;  // [N][K] or [K][N]
-    nk = p.K / 64;
-  } else {
-    a_base = p.a + (size_t)row0 * p.lda + m0;      // X [rows][M], k = row
-    b_base = p.b + (size_t)row0 * p.ldb + n0;      // Y [rows][N]
-    a_row_lim = BM;
-    nk = (rows_g + 63) / 64;
-  }
-
-  TileLoader<BM, A_K> la;
-  TileLoader<BN, B_K> lb;
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float csum[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) csum[i] = 0.f;
-
-  auto k_lim_of = [&](int kt) -> int {
-    if constexpr (MODE == MODE_ROWS) return 64;
-    else return rows_g - kt * 64;
-  };
-  auto a_ptr = [&](int kt) -> const uint16_t* {
-    return A_K ? a_base + kt * 64 : a_base + (size_t)kt * 64 * p.lda;
-  };
-  auto b_ptr = [&](int kt) -> const uint16_t* {
-    return B_K ? b_base + kt * 64 : b_base + (size_t)kt * 64 * p.ldb;
-  };
-
-  if (nk > 0) {
-    la.load(a_ptr(0), p.lda, a_row_lim, k_lim_of(0), tid);
-    lb.load(b_ptr(0), p.ldb, BN, k_lim_of(0), tid);
-    la.store(smem, tid);
-    lb.store(smem + A_BYTES, tid);
-  }
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * BUF;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      la.load(a_ptr(kt + 1), p.lda, a_row_lim, k_lim_of(kt + 1), tid);
-      lb.load(b_ptr(kt + 1), p.ldb, BN, k_lim_of(kt + 1), tid);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = read_frag<BM, A_K>(cur, wm * (BM / 2) + 16 * i, ks, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[j] = read_frag<BN, B_K>(cur + A_BYTES, wn * (BN / 2) + 16 * j, ks, lane);
-      if constexpr (COLSUM) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) csum[i] += sum8(af[i]);
+  // XCD-aware block -> tile map (speed only; any placement is correct).
+  // Workgroups are dealt round-robin over the 8 XCDs, so blocks b and b+8
+  // share an XCD (and its 4 MiB L2).  ROWS: the N/BN column tiles of one row
+  // tile get consecutive slots on one XCD (they share the 64-128 KiB A panel)
+  // and row tiles rotate over the XCDs.  WGRAD (G >= 8): every tile of group g
+  // runs on XCD g % 8, so the group's activation rows stream through one L2.
+  __device__ __forceinline__ bool init(const GemmParams& p) {
+    const int L = blockIdx.x;
+    const int xcd = L & 7, slot = L >> 3;
+    if constexpr (MODE == MODE_ROWS) {
+      const int ntn = p.N / BN;
+      nt = slot % ntn;
+      int rem = (slot / ntn) * 8 + xcd;  // global row-tile index
+      g = 0;
+      for (; g < p.G; ++g) {
+        const int n_g = p.offsets[g + 1] - p.offsets[g];
+        const int t_g = (n_g + BM - 1) / BM;
+        if (rem < t_g) break;
+        rem -= t_g;
       }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      if (g >= p.G) return false;  // beyond the last tile (grid is an upper bound)
+      mt = rem;
+      row0 = p.offsets[g] + mt * BM;
+      rows_g = p.offsets[g + 1] - row0;
+    } else {
+      const int ntn = p.N / BN;
+      const int tpg = (p.M / BM) * ntn;  // tiles per group
+      int tile;
+      if (p.G >= 8) {
+        g = (slot / tpg) * 8 + xcd;
+        tile = slot % tpg;
+      } else {
+        g = L / tpg;
+        tile = L % tpg;
+      }
+      if (g >= p.G) return false;
+      mt = tile / ntn;
+      nt = tile % ntn;
+      row0 = p.offsets[g];
+      rows_g = p.offsets[g + 1] - row0;
     }
-    if (more) {
-      char* nxt = smem + ((kt + 1) & 1) * BUF;
-      la.store(nxt, tid);
-      lb.store(nxt + A_BYTES, tid);
+    m0 = mt * BM;
+    n0 = nt * BN;
+    if constexpr (MODE == MODE_ROWS) {
+      a_base = p.a + (size_t)row0 * p.lda;
+      a_row_lim = rows_g < BM ? rows_g : BM;
+      const uint16_t* bg = p.b + (size_t)g * p.stride_b;
+      b_base = B_K ? bg + (size_t)n0 * p.ldb : bg + n0;
+      nk = p.K / 64;
+    } else {
+      a_base = p.a + (size_t)row0 * p.lda + m0;
+      b_base = p.b + (size_t)row0 * p.ldb + n0;
+      a_row_lim = BM;
+      nk = (rows_g + 63) / 64;
     }
-    __syncthreads();
+    return true;
   }
+};
 
-  // ---- epilogue: lane holds C[m = .. + (lane&15)][n = .. + 4*(lane>>4) + r] ----
+// ---------------------------------------------------------------------------
+// epilogue: lane holds C[m = .. + (lane&15)][n = .. + 4*(lane>>4) + r]
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int MODE, int EPI, bool COLSUM>
+__device__ __forceinline__ void epilogue(const GemmParams& p, int g, int row0, int a_row_lim, int m0, int n0, int nt,
+                                         f32x4 (&acc)[BM / 32][BN / 32], float (&csum)[BM / 32],
+                                         int lane, int wm, int wn) {
+  constexpr int TM = BM / 32, TN = BN / 32;
   const int lm = lane & 15;
   const int ln = 4 * (lane >> 4);
   if constexpr (MODE == MODE_ROWS) {
@@ -327,16 +242,277 @@ __global__ __launch_bounds__(256) void grouped_gemm_kernel(GemmParams p) {
   }
 }
 
+// MFMA work on one staged K-tile (2 k-steps of 32).
+template <int BM, int BN, bool A_K, bool B_K, bool COLSUM>
+__device__ __forceinline__ void compute_tile(const char* abuf, const char* bbuf,
+                                             f32x4 (&acc)[BM / 32][BN / 32], float (&csum)[BM / 32],
+                                             int lane, int wm, int wn) {
+  constexpr int TM = BM / 32, TN = BN / 32;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    bf16x8 af[TM], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = read_frag<BM, A_K>(abuf, wm * (BM / 2) + 16 * i, ks, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = read_frag<BN, B_K>(bbuf, wn * (BN / 2) + 16 * j, ks, lane);
+    if constexpr (COLSUM) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) csum[i] += sum8(af[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// v1: register-staged double buffer
+// ---------------------------------------------------------------------------
+template <int R, bool KCONT>
+struct RegStage {
+  static constexpr int kPer = R * 64 / 8 / 256;  // 16-B chunks per thread
+  uint4 reg[kPer];
+
+  __device__ __forceinline__ void load(const uint16_t* base, int ld, int row_lim, int k_lim, int tid) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int q = tid + 256 * i;
+      int r, kk;
+      if constexpr (KCONT) {
+        r = q >> 3;
+        kk = (q & 7) * 8;
+      } else {
+        constexpr int cpr = R / 8;
+        kk = q / cpr;
+        r = (q % cpr) * 8;
+      }
+      const bool ok = r < row_lim && kk < k_lim;
+      const uint16_t* p = KCONT ? base + (size_t)r * ld + kk : base + (size_t)kk * ld + r;
+      reg[i] = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int q = tid + 256 * i;
+      int off;
+      if constexpr (KCONT) {
+        off = kimg_off(q >> 3, q & 7);
+      } else {
+        constexpr int cpr = R / 8;
+        off = mimg_off<R>(q / cpr, q % cpr);
+      }
+      *reinterpret_cast<uint4*>(lds + off) = reg[i];
+    }
+  }
+};
+
+template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM>
+__global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int A_BYTES = BM * 64 * 2;
+  constexpr int BUF = (BM + BN) * 64 * 2;
+  constexpr int TM = BM / 32, TN = BN / 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  Tile<BM, BN, B_K, MODE> t;
+  if (!t.init(p)) return;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float csum[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) csum[i] = 0.f;
+
+  auto k_lim = [&](int kt) -> int { return MODE == MODE_ROWS ? 64 : t.rows_g - kt * 64; };
+  auto a_ptr = [&](int kt) { return A_K ? t.a_base + kt * 64 : t.a_base + (size_t)kt * 64 * p.lda; };
+  auto b_ptr = [&](int kt) { return B_K ? t.b_base + kt * 64 : t.b_base + (size_t)kt * 64 * p.ldb; };
+
+  RegStage<BM, A_K> la;
+  RegStage<BN, B_K> lb;
+  if (t.nk > 0) {
+    la.load(a_ptr(0), p.lda, t.a_row_lim, k_lim(0), tid);
+    lb.load(b_ptr(0), p.ldb, BN, k_lim(0), tid);
+    la.store(smem, tid);
+    lb.store(smem + A_BYTES, tid);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < t.nk; ++kt) {
+    char* cur = smem + (kt & 1) * BUF;
+    const bool more = kt + 1 < t.nk;
+    if (more) {
+      la.load(a_ptr(kt + 1), p.lda, t.a_row_lim, k_lim(kt + 1), tid);
+      lb.load(b_ptr(kt + 1), p.ldb, BN, k_lim(kt + 1), tid);
+    }
+    compute_tile<BM, BN, A_K, B_K, COLSUM>(cur, cur + A_BYTES, acc, csum, lane, wm, wn);
+    if (more) {
+      char* nxt = smem + ((kt + 1) & 1) * BUF;
+      la.store(nxt, tid);
+      lb.store(nxt + A_BYTES, tid);
+    }
+    __syncthreads();
+  }
+  epilogue<BM, BN, MODE, EPI, COLSUM>(p, t.g, t.row0,
+                                      t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, lane, wm, wn);
+}
+
+// ---------------------------------------------------------------------------
+// v2: LDS-DMA ring, S stages, S-1 K-tiles in flight
+// ---------------------------------------------------------------------------
+// Issue the LDS-DMA of one operand tile (R rows x 64 k) into `lds` (a
+// wave-uniform base).  1 KiB per wave-instruction, R/32 instructions per wave.
+// Rows / k-rows beyond the valid extent are CLAMPED to the last valid one
+// (never out of bounds); the caller masks rows (ROWS mode) or zeroes k-rows
+// (WGRAD tail) -- a DMA cannot write zeros.
+template <int R, bool KCONT>
+__device__ __forceinline__ void dma_tile(const uint16_t* base, int ld, int row_lim, int k_lim, char* lds,
+                                         int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < R / 32; ++j) {
+    const int ins = wave + 4 * j;  // wave-instruction index within the tile
+    const uint16_t* src;
+    if constexpr (KCONT) {  // [R][64]: 8 rows of 128 B per KiB
+      int r = ins * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);  // source chunk for LDS slot (r, lane&7)
+      r = r < row_lim ? r : row_lim - 1;
+      src = base + (size_t)r * ld + c * 8;
+    } else {  // [64][R]: 1024 / (2R) k-rows per KiB
+      constexpr int cpr = R / 8;            // 16-B chunks per k-row
+      constexpr int rows_per = 64 / cpr;    // k-rows per wave-instruction
+      int kr = ins * rows_per + lane / cpr;
+      const int c = (lane % cpr) ^ mimg_swz<R>(kr);
+      kr = kr < k_lim ? kr : k_lim - 1;
+      src = base + (size_t)kr * ld + c * 8;
+    }
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + ins * 1024), 16, 0, 0);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int S, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM>
+__global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int A_BYTES = BM * 64 * 2;
+  constexpr int BUF = (BM + BN) * 64 * 2;
+  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int GW = BM / 32 + BN / 32;  // LDS-DMA instructions per wave per K-tile
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  Tile<BM, BN, B_K, MODE> t;
+  if (!t.init(p)) return;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float csum[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) csum[i] = 0.f;
+
+  const int nk = t.nk;
+  auto issue = [&](int kt) {
+    char* buf = smem + (kt % S) * BUF;
+    const int klim = MODE == MODE_ROWS ? 64 : t.rows_g - kt * 64;
+    const uint16_t* ap = A_K ? t.a_base + kt * 64 : t.a_base + (size_t)kt * 64 * p.lda;
+    const uint16_t* bp = B_K ? t.b_base + kt * 64 : t.b_base + (size_t)kt * 64 * p.ldb;
+    dma_tile<BM, A_K>(ap, p.lda, t.a_row_lim, klim, buf, wave, lane);
+    dma_tile<BN, B_K>(bp, p.ldb, BN, klim, buf + A_BYTES, wave, lane);
+  };
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(s);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt has landed for this wave once at most min(S-2, nk-1-kt) newer tiles are pending
+    const int newer = nk - 1 - kt;
+    if constexpr (S >= 4) {
+      if (newer >= 2) wait_vm<2 * GW>();
+      else if (newer == 1) wait_vm<GW>();
+      else wait_vm<0>();
+    } else {
+      if (newer >= 1) wait_vm<GW>();
+      else wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for tile kt is visible
+    char* cur = smem + (kt % S) * BUF;
+    if constexpr (MODE == MODE_WGRAD) {
+      const int kvalid = t.rows_g - kt * 64;
+      if (kvalid < 64) {  // tail: zero the clamped k-rows of both operands
+        for (int q = tid; q < (64 - kvalid) * (BM + BN) / 8; q += 256) {
+          const int per = (BM + BN) / 8;  // 16-B chunks per k-row over both images
+          const int kr = kvalid + q / per;
+          const int c = q % per;
+          char* dst = c < BM / 8 ? cur + kr * (BM * 2) + c * 16 : cur + A_BYTES + kr * (BN * 2) + (c - BM / 8) * 16;
+          *reinterpret_cast<uint4*>(dst) = make_uint4(0, 0, 0, 0);
+        }
+        __syncthreads();
+      }
+    }
+    if (kt + S - 1 < nk) issue(kt + S - 1);  // refills the slot read in iteration kt-1
+    compute_tile<BM, BN, A_K, B_K, COLSUM>(cur, cur + A_BYTES, acc, csum, lane, wm, wn);
+  }
+  epilogue<BM, BN, MODE, EPI, COLSUM>(p, t.g, t.row0,
+                                      t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, lane, wm, wn);
+}
+
+// ---------------------------------------------------------------------------
+// host launch helpers
+// ---------------------------------------------------------------------------
+// Raise a kernel's dynamic-LDS cap once (first launch), so that later launches
+// -- including ones captured into a hipGraph -- make no attribute call.
+template <auto FN>
+static void allow_lds(size_t bytes) {
+  static bool done = false;
+  if (!done && bytes > 65536) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(FN), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+  }
+  done = true;
+}
+
 template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM>
 static void launch(const GemmParams& p, dim3 grid, hipStream_t s) {
-  constexpr int BUF = (BM + BN) * 64 * 2;
-  hipLaunchKernelGGL((grouped_gemm_kernel<BM, BN, A_K, B_K, MODE, EPI, COLSUM>), grid,
-                     dim3(256), 2 * BUF, s, p);
+  if (g_gemm_variant == 1) {
+    constexpr size_t lds = 2 * (BM + BN) * 64 * 2;
+    constexpr auto fn = gemm_v1_kernel<BM, BN, A_K, B_K, MODE, EPI, COLSUM>;
+    allow_lds<fn>(lds);
+    hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, p);
+  } else if (g_gemm_stages >= 4) {
+    constexpr size_t lds = 4 * (BM + BN) * 64 * 2;
+    constexpr auto fn = gemm_v2_kernel<BM, BN, 4, A_K, B_K, MODE, EPI, COLSUM>;
+    allow_lds<fn>(lds);
+    hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, p);
+  } else {
+    constexpr size_t lds = 3 * (BM + BN) * 64 * 2;
+    constexpr auto fn = gemm_v2_kernel<BM, BN, 3, A_K, B_K, MODE, EPI, COLSUM>;
+    allow_lds<fn>(lds);
+    hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, p);
+  }
 }
 
 }  // namespace moe
 
 using namespace moe;
+
+extern "C" int moe_set_tuning(const char* key, int value) {
+  const std::string k = key ? key : "";
+  if (k == "gemm_variant" && (value == 1 || value == 2)) { g_gemm_variant = value; return 0; }
+  if (k == "gemm_stages" && (value == 3 || value == 4)) { g_gemm_stages = value; return 0; }
+  return fail("moe_set_tuning: unknown key or value");
+}
 
 extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c,
                                 const int32_t* offsets, int G, int max_rows, int N, int K,
@@ -373,21 +549,21 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
   p.N = N;
   p.K = K;
 
-  // Pick the row tile so the launch has >= ~2 waves of workgroups per chip.
+  // Pick the row tile so the launch has >= ~2 workgroups per CU.
   const int nt = N / 128;
   const int tiles128 = (max_rows + 127) / 128 + G;
   const bool big = (long long)tiles128 * nt >= 512;
   const int BMsel = big ? 128 : 64;
-  const int mtiles = (max_rows + BMsel - 1) / BMsel + G;
-  dim3 grid(mtiles, nt);
+  const int mtiles = ((max_rows + BMsel - 1) / BMsel + G + 7) / 8 * 8;  // padded to the XCD count
+  dim3 grid(mtiles * nt);
 
 #define GG_ROWS(BM, BK_, EPI) launch<BM, 128, true, BK_, MODE_ROWS, EPI, false>(p, grid, stream)
-#define GG_EPI(BM, BK_)                                             \
-  switch (epilogue) {                                              \
-    case MOE_EPI_NONE: GG_ROWS(BM, BK_, MOE_EPI_NONE); break;       \
-    case MOE_EPI_BIAS: GG_ROWS(BM, BK_, MOE_EPI_BIAS); break;       \
-    case MOE_EPI_BIAS_RELU: GG_ROWS(BM, BK_, MOE_EPI_BIAS_RELU); break; \
-    default: GG_ROWS(BM, BK_, MOE_EPI_RELU_MASK); break;            \
+#define GG_EPI(BM, BK_)                                                  \
+  switch (epilogue) {                                                   \
+    case MOE_EPI_NONE: GG_ROWS(BM, BK_, MOE_EPI_NONE); break;            \
+    case MOE_EPI_BIAS: GG_ROWS(BM, BK_, MOE_EPI_BIAS); break;            \
+    case MOE_EPI_BIAS_RELU: GG_ROWS(BM, BK_, MOE_EPI_BIAS_RELU); break;  \
+    default: GG_ROWS(BM, BK_, MOE_EPI_RELU_MASK); break;                 \
   }
   if (BMsel == 128) {
     if (trans_b) { GG_EPI(128, true) } else { GG_EPI(128, false) }
@@ -422,12 +598,13 @@ extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, f
   p.K = 0;
   const int ntn = N / 128;
   const bool big = M % 128 == 0 && (long long)(M / 128) * ntn * G >= 512;
+  const int gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
   if (big) {
-    dim3 grid((M / 128) * ntn, G);
+    dim3 grid((M / 128) * ntn * gpad);
     if (colsum) launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream);
     else launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream);
   } else {
-    dim3 grid((M / 64) * ntn, G);
+    dim3 grid((M / 64) * ntn * gpad);
     if (colsum) launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream);
     else launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream);
   }

@@ -369,9 +369,16 @@ using namespace moe;
 
 extern "C" int moe_router_num_blocks(int T) { return (T + 63) / 64; }
 
-// Raise the dynamic-LDS cap of a kernel when a launch needs more than 64 KiB.
-static void allow_lds(const void* fn, size_t bytes) {
-  if (bytes > 65536) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+// Raise the dynamic-LDS cap of a kernel (once, on its first launch) so a
+// launch needing more than 64 KiB succeeds; later launches make no call.
+template <auto FN>
+static void allow_lds(size_t bytes) {
+  static bool done = false;
+  if (!done)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(FN), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              64 * 1024 + 8192);
+  done = true;
+  (void)bytes;
 }
 
 static int emax_for(int E) { return E <= 8 ? 8 : E <= 16 ? 16 : E <= 32 ? 32 : 64; }
@@ -392,7 +399,7 @@ extern "C" int moe_router_topk_fwd(const void* x, const float* wg, const float* 
   const size_t shmem = (size_t)E * d * 4 + 64 * 8 * 4 + 4 * (em + 1) * 4;
   const uint16_t* xb = static_cast<const uint16_t*>(x);
 #define LAUNCH_R(EM)                                                                       \
-  allow_lds(reinterpret_cast<const void*>(&router_topk_fwd_kernel<EM>), shmem);             \
+  allow_lds<router_topk_fwd_kernel<EM>>(shmem);                                             \
   hipLaunchKernelGGL(router_topk_fwd_kernel<EM>, dim3(nblk), dim3(256), shmem, stream, xb, \
                      wg, ctx_bias, ctx_img, tokens_per_image, T, d, E, k, normalize,       \
                      topk_idx, topk_w, probs, lse, local_rank, block_counts, aux_partials)
@@ -432,7 +439,7 @@ extern "C" int moe_token_bwd(const void* dxp, const int32_t* pos, const float* p
   const uint16_t* dxpb = static_cast<const uint16_t*>(dxp);
   uint16_t* dxb = static_cast<uint16_t*>(dx);
 #define LAUNCH_B(EM)                                                                          \
-  allow_lds(reinterpret_cast<const void*>(&token_bwd_kernel<EM>), shmem);                    \
+  allow_lds<token_bwd_kernel<EM>>(shmem);                                                   \
   hipLaunchKernelGGL(token_bwd_kernel<EM>, dim3(grid), dim3(256), shmem, stream, dxpb, pos, \
                      probs, topk_idx, topk_w, dw, lse, dprob_bias, zc, wg, T, d, E, k,      \
                      normalize, dxb, dlogits)

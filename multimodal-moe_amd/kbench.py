@@ -1,0 +1,140 @@
+"""Kernel microbenchmark for the MoE HIP kernels at the C2 shapes.
+
+Times every kernel of one MoE layer (encoder T = 8*920, decoder T = 8*300;
+E = 8, k = 2, d = 256, F = 1024) back to back on one stream, interleaving the
+tuning variants in one process (median of rounds), and prints one JSON line
+per (kernel, shape, variant) with us / TFLOP/s / GB/s.
+
+  python multimodal-moe_amd/kbench.py [--reps 50] [--rounds 5] [--variants 1,2] [--stages 3,4]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+
+import torch  # noqa: E402
+
+from src.moe import _lib as L  # noqa: E402
+
+
+def timed(fn, reps):
+    """GPU time per call: `reps` calls captured in one hipGraph, replayed and
+    timed with events (no Python/ctypes host overhead in the measurement;
+    includes the ~1-2 us kernel-boundary cost per launch)."""
+    fn()
+    torch.cuda.synchronize()
+    stream = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(stream):
+        fn()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph, stream=stream):
+            for _ in range(reps):
+                fn()
+    graph.replay()
+    torch.cuda.synchronize()
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    graph.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return 1e3 * s.elapsed_time(e) / reps  # us
+
+
+def setup(T, E, k, d, F, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn((T, d), device="cuda", generator=g).to(torch.bfloat16)
+    wg = (torch.randn((E, d), device="cuda", generator=g) * 0.3).float()
+    cb = torch.randn((6, E), device="cuda", generator=g).float() * 0.5
+    ci = torch.randint(0, 6, (T // 920 if T % 920 == 0 else T // 300,), device="cuda", generator=g).int()
+    tpi = 920 if T % 920 == 0 else 300
+    w1 = (torch.randn((E, F, d), device="cuda", generator=g) / 16).to(torch.bfloat16)
+    w2 = (torch.randn((E, d, F), device="cuda", generator=g) / 32).to(torch.bfloat16)
+    b1 = torch.zeros((E, F), device="cuda")
+    b2 = torch.zeros((E, d), device="cuda")
+    idx, w, probs, lse, lrank, bcnt, auxp = L.router_topk_fwd(x, wg, cb, ci, tpi, k, True)
+    rank_base, hist, offsets = L.route_scan(bcnt, 0)
+    rows = T * k
+    xp, pos = L.permute_fwd(x, idx, lrank, rank_base, offsets, E, 0, rows)
+    h = L.grouped_gemm(xp, w1, offsets, E, rows, F, d, 1, L.EPI_BIAS_RELU, bias=b1)
+    yp = L.grouped_gemm(h, w2, offsets, E, rows, d, F, 1, L.EPI_BIAS, bias=b2)
+    dy = torch.randn((T, d), device="cuda", generator=g).to(torch.bfloat16)
+    dyp, dw = L.combine_bwd(dy, yp, pos, w)
+    dh = L.grouped_gemm(dyp, w2, offsets, E, rows, F, d, 0, L.EPI_RELU_MASK, aux=h)
+    dxp = L.grouped_gemm(dh, w1, offsets, E, rows, d, F, 0, L.EPI_NONE)
+    return dict(T=T, E=E, k=k, d=d, F=F, x=x, wg=wg, cb=cb, ci=ci, tpi=tpi, w1=w1, w2=w2, b1=b1, b2=b2, idx=idx,
+                w=w, probs=probs, lse=lse, lrank=lrank, bcnt=bcnt, rank_base=rank_base, offsets=offsets, rows=rows,
+                xp=xp, pos=pos, h=h, yp=yp, dy=dy, dyp=dyp, dw=dw, dh=dh, dxp=dxp)
+
+
+def kernels(c):
+    T, E, k, d, F, rows = c["T"], c["E"], c["k"], c["d"], c["F"], c["rows"]
+    A = rows
+    out = [
+        ("router", lambda: L.router_topk_fwd(c["x"], c["wg"], c["cb"], c["ci"], c["tpi"], k, True), 0,
+         512 * T + T * (4 * (E + 1) + 16 * k)),
+        ("route_scan", lambda: L.route_scan(c["bcnt"], 0), 0, 8 * c["bcnt"].numel()),
+        ("permute", lambda: L.permute_fwd(c["x"], c["idx"], c["lrank"], c["rank_base"], c["offsets"], E, 0, rows),
+         0, 512 * (T + A) + 12 * A),
+        ("gemm1_fwd", lambda: L.grouped_gemm(c["xp"], c["w1"], c["offsets"], E, rows, F, d, 1, L.EPI_BIAS_RELU,
+                                             bias=c["b1"]), 2.0 * A * F * d, 0),
+        ("gemm2_fwd", lambda: L.grouped_gemm(c["h"], c["w2"], c["offsets"], E, rows, d, F, 1, L.EPI_BIAS,
+                                             bias=c["b2"]), 2.0 * A * F * d, 0),
+        ("combine", lambda: L.combine_fwd(c["yp"], c["pos"], c["w"], T), 0, 512 * (A + T) + 8 * A),
+        ("combine_bwd", lambda: L.combine_bwd(c["dy"], c["yp"], c["pos"], c["w"]), 0, 512 * (T + 2 * A) + 12 * A),
+        ("gemm_dgrad2", lambda: L.grouped_gemm(c["dyp"], c["w2"], c["offsets"], E, rows, F, d, 0, L.EPI_RELU_MASK,
+                                               aux=c["h"]), 2.0 * A * F * d, 0),
+        ("gemm_wgrad2", lambda: L.grouped_gemm_wgrad(c["dyp"], c["h"], c["offsets"], E), 2.0 * A * F * d, 0),
+        ("gemm_dgrad1", lambda: L.grouped_gemm(c["dh"], c["w1"], c["offsets"], E, rows, d, F, 0, L.EPI_NONE),
+         2.0 * A * F * d, 0),
+        ("gemm_wgrad1", lambda: L.grouped_gemm_wgrad(c["dh"], c["xp"], c["offsets"], E), 2.0 * A * F * d, 0),
+        ("token_bwd", lambda: L.token_bwd(c["dxp"], c["pos"], c["probs"], c["idx"], c["w"], c["dw"], c["lse"],
+                                          None, None, c["wg"], True), 0, 512 * (A + T) + 4 * (2 * E + 3 * k) * T),
+    ]
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--stages", default="3,4")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    L.lib()
+    configs = [(v, s) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
+               if not (v == 1 and s != int(a.stages.split(",")[0]))]
+    shapes = {"enc": setup(8 * 920, 8, 2, 256, 1024), "dec": setup(8 * 300, 8, 2, 256, 1024, seed=1)}
+    res = {}
+    for _ in range(a.rounds):
+        for (v, s) in configs:
+            L.set_tuning("gemm_variant", v)
+            L.set_tuning("gemm_stages", s)
+            for sname, c in shapes.items():
+                for name, fn, flops, byts in kernels(c):
+                    if a.only and a.only not in name:
+                        continue
+                    if not name.startswith("gemm") and (v, s) != configs[0]:
+                        continue
+                    res.setdefault((name, sname, v, s, flops, byts), []).append(timed(fn, a.reps))
+    for (name, sname, v, s, flops, byts), ts in res.items():
+        us = statistics.median(ts)
+        d = {"kernel": name, "shape": sname, "variant": v, "stages": s, "us": round(us, 2), "min_us": round(min(ts), 2)}
+        if flops:
+            d["tflops"] = round(flops / us / 1e6, 1)
+            d["frac_bf16_peak"] = round(flops / us / 1e6 / 2500.0, 4)
+        if byts:
+            d["gbs"] = round(byts / us / 1e3, 1)
+            d["frac_hbm_peak"] = round(byts / us / 1e3 / 8000.0, 4)
+        print(json.dumps(d))
+
+
+if __name__ == "__main__":
+    main()

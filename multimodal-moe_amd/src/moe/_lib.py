@@ -35,6 +35,7 @@ SIGNATURES = {
     "moe_token_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "moe_grouped_gemm": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_wgrad": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "moe_last_error": (ctypes.c_char_p, []),
     "moe_version": (ctypes.c_char_p, []),
 }
@@ -84,22 +85,37 @@ class KernelTimer:
     the stream it is launched on (torch's current stream -- the same stream
     the C-ABI call receives) together with its algorithmic work: flops for the
     grouped GEMMs (2*rows*N*K, rows read from the device offsets after the
-    timed region) and bytes for the row movers.
+    launch completed) and bytes for the row movers.
+
+    mode "eager": each launch appends a record; ``harvest()`` consumes them.
+    mode "graph": records are made only while a stream is being captured, so
+    the event pairs become event-record nodes of the hipGraph; every replay
+    re-stamps them and ``harvest()`` (after the replay completed) adds that
+    replay's durations without dropping the records.
     """
 
     def __init__(self):
         self.enabled = False
+        self.mode = "eager"
         self.records = []  # (kind, start_event, end_event, work_fn)
+        self.acc = {}
 
-    def start(self):
+    def start(self, mode="eager"):
         self.records = []
+        self.acc = {}
+        self.mode = mode
         self.enabled = True
 
     def stop(self):
         self.enabled = False
 
+    def reset_totals(self):
+        self.acc = {}
+
     def wrap(self, kind, work_fn, launch):
         if not self.enabled:
+            return launch()
+        if self.mode == "graph" and not torch.cuda.is_current_stream_capturing():
             return launch()
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
@@ -109,15 +125,22 @@ class KernelTimer:
         self.records.append((kind, s, e, work_fn))
         return out
 
-    def summary(self):
-        """{kind: dict(launches, total_ms, avg_us, work, unit)} after a sync."""
+    def harvest(self):
+        """Add the completed launches' durations/work to the totals (syncs)."""
         torch.cuda.synchronize()
-        out = {}
         for kind, s, e, work_fn in self.records:
-            d = out.setdefault(kind, {"launches": 0, "total_ms": 0.0, "work": 0.0})
+            d = self.acc.setdefault(kind, {"launches": 0, "total_ms": 0.0, "work": 0.0})
             d["launches"] += 1
             d["total_ms"] += s.elapsed_time(e)
             d["work"] += float(work_fn())
+        if self.mode == "eager":
+            self.records = []
+
+    def summary(self):
+        """{kind: dict(launches, total_ms, avg_us, work)} of the harvested launches."""
+        if self.mode == "eager" and self.records:
+            self.harvest()
+        out = {k: dict(v) for k, v in self.acc.items()}
         for d in out.values():
             d["avg_us"] = 1e3 * d["total_ms"] / max(d["launches"], 1)
         return out
@@ -158,6 +181,10 @@ def _need(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
 # ---------------------------------------------------------------------------
 # thin typed wrappers (tensors in, tensors out; shapes checked on the host)
 # ---------------------------------------------------------------------------
+def set_tuning(key: str, value: int) -> None:
+    _check(lib().moe_set_tuning(key.encode(), int(value)), f"moe_set_tuning({key}={value})")
+
+
 def router_num_blocks(T: int) -> int:
     return (T + 63) // 64
 

@@ -87,10 +87,26 @@ def _int_tensor(rng, shape, lo=-3, hi=4):
     return rng.integers(lo, hi, size=shape).astype(np.float64)
 
 
+GEMM_CFGS = [(1, 3), (2, 3), (2, 4)]  # (gemm_variant, gemm_stages)
+
+
+@pytest.fixture
+def gemm_cfg(request, hip_lib):
+    from src.moe import _lib as L
+
+    v, s = request.param
+    L.set_tuning("gemm_variant", v)
+    L.set_tuning("gemm_stages", s)
+    yield request.param
+    L.set_tuning("gemm_variant", 2)
+    L.set_tuning("gemm_stages", 3)
+
+
+@pytest.mark.parametrize("gemm_cfg", GEMM_CFGS, indirect=True)
 @pytest.mark.parametrize("trans_b", [1, 0])
 @pytest.mark.parametrize("rows_per_group", [[0, 1, 63, 64, 65, 200, 0, 130], [1000, 24, 0, 500]])
 @pytest.mark.parametrize("N,K", [(1024, 256), (256, 1024), (128, 64)])
-def test_grouped_gemm_exact(hip_lib, trans_b, rows_per_group, N, K):
+def test_grouped_gemm_exact(gemm_cfg, trans_b, rows_per_group, N, K):
     from src.moe import _lib as L
 
     rng = np.random.default_rng(7)
@@ -123,9 +139,10 @@ def test_grouped_gemm_exact(hip_lib, trans_b, rows_per_group, N, K):
     np.testing.assert_array_equal(_np(C3)[:R], O.round_bf16(ref * (O.round_bf16(ref2) > 0)))
 
 
+@pytest.mark.parametrize("gemm_cfg", GEMM_CFGS, indirect=True)
 @pytest.mark.parametrize("rows_per_group", [[0, 1, 63, 64, 65, 200, 0, 130], [700, 0, 33]])
 @pytest.mark.parametrize("M,N", [(256, 1024), (1024, 256), (64, 128)])
-def test_grouped_gemm_wgrad_exact(hip_lib, rows_per_group, M, N):
+def test_grouped_gemm_wgrad_exact(gemm_cfg, rows_per_group, M, N):
     from src.moe import _lib as L
 
     rng = np.random.default_rng(11)

@@ -51,3 +51,29 @@ def test_capacity_formula():
 
     c = MoEConfig(num_experts=32, top_k=4, capacity_factor=1.25)
     assert c.capacity(14720) == 2300  # C5 enc cap at cf 1.25
+
+
+def test_batched_criterion_matches_per_set():
+    import torch
+    from src.rtdetr_moe.criterion import SetCriterion
+    from src.rtdetr_moe.data import SyntheticZOD
+
+    torch.manual_seed(0)
+    B, Q, S = 3, 50, 4
+    _, targets, _ = SyntheticZOD(batch=B, img_h=256, img_w=256, seed=3).sample()
+    def mk():
+        return {"pred_logits": torch.randn(B, Q, 1, requires_grad=True),
+                "pred_boxes": torch.rand(B, Q, 4).mul(0.5).add(0.1).requires_grad_(True)}
+    outs = [mk() for _ in range(S)]
+    out = dict(outs[0], aux_outputs=outs[1:-1], enc_outputs=outs[-1])
+    crit = SetCriterion()
+    nb = max(1.0, float(sum(len(t["boxes"]) for t in targets)))
+    a = crit(out, targets, nb)
+    b = crit.forward_per_set(out, targets, nb)
+    assert a.keys() == b.keys()
+    for k in a:
+        torch.testing.assert_close(a[k], b[k], rtol=1e-5, atol=1e-6, msg=k)
+    ga = torch.autograd.grad(sum(a.values()), [o["pred_logits"] for o in outs] + [o["pred_boxes"] for o in outs])
+    gb = torch.autograd.grad(sum(b.values()), [o["pred_logits"] for o in outs] + [o["pred_boxes"] for o in outs])
+    for x, y in zip(ga, gb):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
