@@ -137,6 +137,26 @@ int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, float* c,
                            float* colsum, const int32_t* offsets, int G,
                            int M, int N, hipStream_t stream);
 
+/* ---- SURVEY 8(f).1 (next row): RT-DETR multi-scale deformable attention ----
+ * Sampling core of the decoder's cross-attention (replaces the per-level
+ * grid_sample chain of the reference engine's MSDeformableAttention):
+ *   out[b,q,h,:] = sum_{l,p} attn[b,q,h,l,p] * bilinear(value_l[b,:,:,h,:], loc[b,q,h,l,p,:])
+ * grid_sample conventions: align_corners = 0, zero padding, pixel = loc*size - 0.5.
+ * value: bf16 [B, S, H, D] (levels flattened; level l = rows starts[l] ..
+ * starts[l] + h_l*w_l); shapes: int32 [L, 2] (h, w); starts: int32 [L];
+ * loc: fp32 [B, Q, H, L, P, 2]; attn: fp32 [B, Q, H, L, P]; out: bf16 [B, Q, H*D].
+ * D in {32, 64}; L <= 4; P <= 16. */
+int rtdetr_msda_fwd(const void* value, const int32_t* shapes, const int32_t* starts,
+                    const float* loc, const float* attn, int B, int S, int Q, int H, int D,
+                    int L, int P, void* out, hipStream_t stream);
+
+/* Backward: grad_value fp32 [B, S, H, D] (zeroed here, then accumulated with
+ * fp32 atomics), grad_loc fp32 [B, Q, H, L, P, 2], grad_attn fp32 [B, Q, H, L, P]. */
+int rtdetr_msda_bwd(const void* value, const int32_t* shapes, const int32_t* starts,
+                    const float* loc, const float* attn, const void* grad_out, int B, int S,
+                    int Q, int H, int D, int L, int P, float* grad_value, float* grad_loc,
+                    float* grad_attn, hipStream_t stream);
+
 /* Process-wide tuning knobs (not thread-safe; set before launching):
  *   "gemm_variant" 1 = register-staged double buffer, 2 = LDS-DMA ring (default)
  *   "gemm_stages"  3 (default) or 4 ring slots for variant 2

@@ -1,0 +1,225 @@
+// Multi-scale deformable attention sampling core of the RT-DETR decoder
+// ("Deformable attention via grid_sample is the next
+// HIP-kernel candidate ... HBM-gather-bound").
+//
+//   out[b,q,h,c] = sum_{l,p} attn[b,q,h,l,p] * bilinear(value_l[b,:,:,h,c], loc[b,q,h,l,p])
+//
+// with grid_sample's conventions (align_corners = False, zero padding):
+// pixel = loc * size - 0.5.  value is the flattened multi-level memory
+// [B, S, H, D] (level l occupies rows starts[l] .. starts[l] + h_l*w_l).
+//
+// Geometry: one (b, q, h) per group of D/2 lanes; each lane owns 2 adjacent
+// channels (4-B bf16x2 loads: a group reads a 64-B contiguous row segment per
+// corner), 256-thread blocks.  Forward: registers only.  Backward: per sample,
+// the group reduces <grad_out, value> terms with xor-shuffles for the
+// attention-weight and location gradients; the value gradient is scattered
+// with fp32 atomics into an fp32 buffer (each corner row segment is 64-256 B
+// contiguous per wave-instruction).
+#include "moe_common.h"
+
+namespace moe {
+
+struct MsdaLevels {
+  int h[4], w[4], start[4];
+};
+
+__device__ __forceinline__ MsdaLevels load_levels(const int32_t* shapes, const int32_t* starts, int L) {
+  MsdaLevels lv;
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    lv.h[l] = l < L ? shapes[2 * l] : 0;
+    lv.w[l] = l < L ? shapes[2 * l + 1] : 0;
+    lv.start[l] = l < L ? starts[l] : 0;
+  }
+  return lv;
+}
+
+__device__ __forceinline__ float2 ld_bf16x2(const uint16_t* p) {
+  const uint32_t v = *reinterpret_cast<const uint32_t*>(p);
+  return make_float2(__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u));
+}
+
+template <int LPG>  // lanes per (b,q,h) group = D / 2
+__global__ __launch_bounds__(256) void msda_fwd_kernel(const uint16_t* __restrict__ value,
+                                                       const int32_t* __restrict__ shapes,
+                                                       const int32_t* __restrict__ starts,
+                                                       const float* __restrict__ loc,
+                                                       const float* __restrict__ attn, int B, int S, int Q,
+                                                       int H, int L, int P, uint16_t* __restrict__ out) {
+  constexpr int D = 2 * LPG;
+  const MsdaLevels lv = load_levels(shapes, starts, L);
+  const int groups = B * Q * H;
+  const int sub = threadIdx.x % LPG;
+  for (int gidx = (blockIdx.x * blockDim.x + threadIdx.x) / LPG; gidx < groups;
+       gidx += gridDim.x * blockDim.x / LPG) {
+    const int h = gidx % H;
+    const int b = gidx / (Q * H);
+    const float* lp = loc + (size_t)gidx * L * P * 2;
+    const float* ap = attn + (size_t)gidx * L * P;
+    float acc0 = 0.f, acc1 = 0.f;
+    for (int l = 0; l < L; ++l) {
+      const int Hl = lv.h[l], Wl = lv.w[l];
+      const uint16_t* vb = value + ((size_t)b * S + lv.start[l]) * H * D + h * D + 2 * sub;
+      for (int p = 0; p < P; ++p) {
+        const int sp = l * P + p;
+        const float x = lp[2 * sp] * Wl - 0.5f;
+        const float y = lp[2 * sp + 1] * Hl - 0.5f;
+        const float a = ap[sp];
+        const float xf = floorf(x), yf = floorf(y);
+        const int x0 = (int)xf, y0 = (int)yf;
+        const float fx = x - xf, fy = y - yf;
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int cy = 0; cy < 2; ++cy) {
+#pragma unroll
+          for (int cx = 0; cx < 2; ++cx) {
+            const int xi = x0 + cx, yi = y0 + cy;
+            if (xi < 0 || xi >= Wl || yi < 0 || yi >= Hl) continue;
+            const float wgt = (cx ? fx : 1.f - fx) * (cy ? fy : 1.f - fy);
+            const float2 v = ld_bf16x2(vb + (size_t)(yi * Wl + xi) * H * D);
+            s0 += wgt * v.x;
+            s1 += wgt * v.y;
+          }
+        }
+        acc0 += a * s0;
+        acc1 += a * s1;
+      }
+    }
+    *reinterpret_cast<uint32_t*>(out + (size_t)gidx * D + 2 * sub) = pack2bf(acc0, acc1);
+  }
+}
+
+template <int LPG>
+__global__ __launch_bounds__(256) void msda_bwd_kernel(
+    const uint16_t* __restrict__ value, const int32_t* __restrict__ shapes,
+    const int32_t* __restrict__ starts, const float* __restrict__ loc, const float* __restrict__ attn,
+    const uint16_t* __restrict__ grad_out, int B, int S, int Q, int H, int L, int P,
+    float* __restrict__ grad_value, float* __restrict__ grad_loc, float* __restrict__ grad_attn) {
+  constexpr int D = 2 * LPG;
+  const MsdaLevels lv = load_levels(shapes, starts, L);
+  const int groups = B * Q * H;
+  const int sub = threadIdx.x % LPG;
+  // every lane of a group iterates the same trip counts: shuffles stay convergent
+  const int ngrp_total = (gridDim.x * blockDim.x) / LPG;
+  const int first = (blockIdx.x * blockDim.x + threadIdx.x) / LPG;
+  const int iters = (groups + ngrp_total - 1) / ngrp_total;
+  for (int it = 0; it < iters; ++it) {
+    const int gidx = first + it * ngrp_total;
+    const bool valid = gidx < groups;
+    const int gi = valid ? gidx : 0;
+    const int h = gi % H;
+    const int b = gi / (Q * H);
+    const float* lp = loc + (size_t)gi * L * P * 2;
+    const float* ap = attn + (size_t)gi * L * P;
+    const float2 g = valid ? ld_bf16x2(grad_out + (size_t)gi * D + 2 * sub) : make_float2(0.f, 0.f);
+    for (int l = 0; l < L; ++l) {
+      const int Hl = lv.h[l], Wl = lv.w[l];
+      const size_t row0 = (size_t)b * S + lv.start[l];
+      const uint16_t* vb = value + row0 * H * D + h * D + 2 * sub;
+      float* gvb = grad_value + row0 * H * D + h * D + 2 * sub;
+      for (int p = 0; p < P; ++p) {
+        const int sp = l * P + p;
+        const float x = lp[2 * sp] * Wl - 0.5f;
+        const float y = lp[2 * sp + 1] * Hl - 0.5f;
+        const float a = ap[sp];
+        const float xf = floorf(x), yf = floorf(y);
+        const int x0 = (int)xf, y0 = (int)yf;
+        const float fx = x - xf, fy = y - yf;
+        float2 v[2][2];
+        bool in[2][2];
+#pragma unroll
+        for (int cy = 0; cy < 2; ++cy)
+#pragma unroll
+          for (int cx = 0; cx < 2; ++cx) {
+            const int xi = x0 + cx, yi = y0 + cy;
+            in[cy][cx] = valid && xi >= 0 && xi < Wl && yi >= 0 && yi < Hl;
+            v[cy][cx] = in[cy][cx] ? ld_bf16x2(vb + (size_t)(yi * Wl + xi) * H * D) : make_float2(0.f, 0.f);
+          }
+        // sampled value and its spatial derivatives (per channel)
+        const float w00 = (1.f - fx) * (1.f - fy), w01 = fx * (1.f - fy);
+        const float w10 = (1.f - fx) * fy, w11 = fx * fy;
+        const float sx = w00 * v[0][0].x + w01 * v[0][1].x + w10 * v[1][0].x + w11 * v[1][1].x;
+        const float sy = w00 * v[0][0].y + w01 * v[0][1].y + w10 * v[1][0].y + w11 * v[1][1].y;
+        const float dxa = (1.f - fy) * (v[0][1].x - v[0][0].x) + fy * (v[1][1].x - v[1][0].x);
+        const float dxb = (1.f - fy) * (v[0][1].y - v[0][0].y) + fy * (v[1][1].y - v[1][0].y);
+        const float dya = (1.f - fx) * (v[1][0].x - v[0][0].x) + fx * (v[1][1].x - v[0][1].x);
+        const float dyb = (1.f - fx) * (v[1][0].y - v[0][0].y) + fx * (v[1][1].y - v[0][1].y);
+        float ga = g.x * sx + g.y * sy;           // d out / d attn
+        float gx = g.x * dxa + g.y * dxb;         // d out / d x (per unit attn)
+        float gy = g.x * dya + g.y * dyb;
+        ga = group_sum<LPG>(ga);
+        gx = group_sum<LPG>(gx);
+        gy = group_sum<LPG>(gy);
+        if (valid && sub == 0) {
+          grad_attn[(size_t)gi * L * P + sp] = ga;
+          grad_loc[((size_t)gi * L * P + sp) * 2] = a * gx * Wl;
+          grad_loc[((size_t)gi * L * P + sp) * 2 + 1] = a * gy * Hl;
+        }
+        const float wc[2][2] = {{w00, w01}, {w10, w11}};
+#pragma unroll
+        for (int cy = 0; cy < 2; ++cy)
+#pragma unroll
+          for (int cx = 0; cx < 2; ++cx) {
+            if (!in[cy][cx]) continue;
+            const float s = a * wc[cy][cx];
+            float* dst = gvb + (size_t)((y0 + cy) * Wl + (x0 + cx)) * H * D;
+            atomicAdd(dst, s * g.x);
+            atomicAdd(dst + 1, s * g.y);
+          }
+      }
+    }
+  }
+}
+
+}  // namespace moe
+
+using namespace moe;
+
+static int msda_check(int B, int S, int Q, int H, int D, int L, int P) {
+  if (B <= 0 || S <= 0 || Q < 0 || H <= 0 || L < 1 || L > 4 || P < 1 || P > 16)
+    return fail("msda: bad shape (need L in [1,4], P in [1,16])");
+  if (D != 32 && D != 64) return fail("msda: head dim must be 32 or 64");
+  return 0;
+}
+
+static int msda_grid(long long groups, int lpg) {
+  long long g = (groups * lpg + 255) / 256;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+extern "C" int rtdetr_msda_fwd(const void* value, const int32_t* shapes, const int32_t* starts,
+                               const float* loc, const float* attn, int B, int S, int Q, int H, int D, int L,
+                               int P, void* out, hipStream_t stream) {
+  if (msda_check(B, S, Q, H, D, L, P)) return -1;
+  if (Q == 0) return 0;
+  const long long groups = (long long)B * Q * H;
+  const uint16_t* v = static_cast<const uint16_t*>(value);
+  uint16_t* o = static_cast<uint16_t*>(out);
+  if (D == 32)
+    hipLaunchKernelGGL(msda_fwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
+                       loc, attn, B, S, Q, H, L, P, o);
+  else
+    hipLaunchKernelGGL(msda_fwd_kernel<32>, dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v, shapes, starts,
+                       loc, attn, B, S, Q, H, L, P, o);
+  return check_launch("rtdetr_msda_fwd");
+}
+
+extern "C" int rtdetr_msda_bwd(const void* value, const int32_t* shapes, const int32_t* starts,
+                               const float* loc, const float* attn, const void* grad_out, int B, int S, int Q,
+                               int H, int D, int L, int P, float* grad_value, float* grad_loc, float* grad_attn,
+                               hipStream_t stream) {
+  if (msda_check(B, S, Q, H, D, L, P)) return -1;
+  const hipError_t e = hipMemsetAsync(grad_value, 0, (size_t)B * S * H * D * sizeof(float), stream);
+  if (e != hipSuccess) return fail(std::string("rtdetr_msda_bwd: memset: ") + hipGetErrorString(e));
+  if (Q == 0) return 0;
+  const long long groups = (long long)B * Q * H;
+  const uint16_t* v = static_cast<const uint16_t*>(value);
+  const uint16_t* go = static_cast<const uint16_t*>(grad_out);
+  if (D == 32)
+    hipLaunchKernelGGL(msda_bwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
+                       loc, attn, go, B, S, Q, H, L, P, grad_value, grad_loc, grad_attn);
+  else
+    hipLaunchKernelGGL(msda_bwd_kernel<32>, dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v, shapes, starts,
+                       loc, attn, go, B, S, Q, H, L, P, grad_value, grad_loc, grad_attn);
+  return check_launch("rtdetr_msda_bwd");
+}

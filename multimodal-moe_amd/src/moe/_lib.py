@@ -35,6 +35,8 @@ SIGNATURES = {
     "moe_token_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "moe_grouped_gemm": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_wgrad": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "rtdetr_msda_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "moe_last_error": (ctypes.c_char_p, []),
     "moe_version": (ctypes.c_char_p, []),
@@ -316,3 +318,32 @@ def grouped_gemm_wgrad(x, y, offsets, G, want_colsum=True):
         MOE_BF16, _ptr(x), _ptr(y), _ptr(c), _ptr(cs), _ptr(offsets), G, M, N, _stream()))
     _check(rc, "moe_grouped_gemm_wgrad")
     return c, cs
+
+
+def msda_fwd(value, shapes, starts, loc, attn):
+    """value bf16 [B,S,H,D]; shapes/starts int32 on device; loc fp32 [B,Q,H,L,P,2];
+    attn fp32 [B,Q,H,L,P] -> bf16 [B,Q,H*D]."""
+    B, S, H, D = value.shape
+    Q, L, P = loc.shape[1], loc.shape[3], loc.shape[4]
+    _need(value, torch.bfloat16, "value")
+    _need(loc, torch.float32, "loc")
+    _need(attn, torch.float32, "attn")
+    out = torch.empty((B, Q, H * D), dtype=torch.bfloat16, device=value.device)
+    rc = TIMER.wrap("msda", lambda: 0.0, lambda: lib().rtdetr_msda_fwd(
+        _ptr(value), _ptr(shapes), _ptr(starts), _ptr(loc), _ptr(attn), B, S, Q, H, D, L, P, _ptr(out), _stream()))
+    _check(rc, "rtdetr_msda_fwd")
+    return out
+
+
+def msda_bwd(value, shapes, starts, loc, attn, grad_out):
+    B, S, H, D = value.shape
+    Q, L, P = loc.shape[1], loc.shape[3], loc.shape[4]
+    _need(grad_out, torch.bfloat16, "grad_out")
+    gv = torch.empty((B, S, H, D), dtype=torch.float32, device=value.device)
+    gl = torch.empty_like(loc)
+    ga = torch.empty_like(attn)
+    rc = TIMER.wrap("msda", lambda: 0.0, lambda: lib().rtdetr_msda_bwd(
+        _ptr(value), _ptr(shapes), _ptr(starts), _ptr(loc), _ptr(attn), _ptr(grad_out), B, S, Q, H, D, L, P,
+        _ptr(gv), _ptr(gl), _ptr(ga), _stream()))
+    _check(rc, "rtdetr_msda_bwd")
+    return gv, gl, ga

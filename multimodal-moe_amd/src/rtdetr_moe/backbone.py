@@ -31,7 +31,8 @@ class FrozenBatchNorm2d(nn.Module):
     def forward(self, x):
         scale = self.weight * (self.running_var + self.eps).rsqrt()
         shift = self.bias - self.running_mean * scale
-        return x * scale.view(1, -1, 1, 1).to(x.dtype) + shift.view(1, -1, 1, 1).to(x.dtype)
+        # one fused multiply-add kernel (x * scale + shift)
+        return torch.addcmul(shift.view(1, -1, 1, 1).to(x.dtype), x, scale.view(1, -1, 1, 1).to(x.dtype))
 
 
 def _norm(n, frozen):
@@ -92,7 +93,12 @@ class BottleNeck(nn.Module):
 
 
 class PResNet(nn.Module):
-    def __init__(self, depth=50, return_idx=(1, 2, 3), freeze_norm=False):
+    def __init__(self, depth=50, return_idx=(1, 2, 3), freeze_norm=True, freeze_at=0):
+        """freeze_norm / freeze_at follow the rtdetrv2_r50vd configuration named
+        by the reference (scripts/train_rtdetr_thirdparty.py:30-35): frozen
+        BatchNorm statistics in the backbone and a frozen stem (freeze_at=0),
+        so neither the stem's weight gradient nor its input gradient is
+        computed."""
         super().__init__()
         block = BottleNeck if depth >= 50 else BasicBlock
         c = 64
@@ -114,6 +120,12 @@ class PResNet(nn.Module):
                 ch_in = cout * block.expansion
             self.stages.append(nn.Sequential(*blocks))
             self.out_channels.append(ch_in)
+        if freeze_at >= 0:
+            for prm in self.stem.parameters():
+                prm.requires_grad_(False)
+            for st in self.stages[:freeze_at]:
+                for prm in st.parameters():
+                    prm.requires_grad_(False)
         self.return_idx = list(return_idx)
         self.out_channels = [self.out_channels[i] for i in self.return_idx]
         self.out_strides = [[4, 8, 16, 32][i] for i in self.return_idx]

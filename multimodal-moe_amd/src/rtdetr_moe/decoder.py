@@ -54,6 +54,53 @@ def deformable_attention_core(value, shapes, sampling_locations, attention_weigh
     return out.view(B, H * Dh, Q).transpose(1, 2)
 
 
+class _MSDAHip(torch.autograd.Function):
+    """HIP sampling core (libmoe_hip.so rtdetr_msda_fwd/bwd) for GPU tensors."""
+
+    @staticmethod
+    def forward(ctx, value, shapes_t, starts_t, loc, attn):
+        from ..moe import _lib as L
+
+        v = value.to(torch.bfloat16).contiguous()
+        lo = loc.float().contiguous()
+        at = attn.float().contiguous()
+        out = L.msda_fwd(v, shapes_t, starts_t, lo, at)
+        ctx.save_for_backward(v, shapes_t, starts_t, lo, at)
+        ctx.vdtype = value.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        from ..moe import _lib as L
+
+        v, shapes_t, starts_t, lo, at = ctx.saved_tensors
+        gv, gl, ga = L.msda_bwd(v, shapes_t, starts_t, lo, at, grad_out.to(torch.bfloat16).contiguous())
+        return gv.to(ctx.vdtype), None, None, gl, ga
+
+
+_LEVEL_CACHE = {}
+
+
+def _level_tensors(shapes, device):
+    key = (tuple(shapes), device)
+    if key not in _LEVEL_CACHE:
+        starts, s = [], 0
+        for h, w in shapes:
+            starts.append(s)
+            s += h * w
+        _LEVEL_CACHE[key] = (torch.tensor(shapes, dtype=torch.int32, device=device),
+                             torch.tensor(starts, dtype=torch.int32, device=device))
+    return _LEVEL_CACHE[key]
+
+
+def deformable_attention(value, shapes, sampling_locations, attention_weights):
+    """GPU: HIP kernel; CPU: the grid_sample formulation above."""
+    if value.is_cuda:
+        st, so = _level_tensors(shapes, value.device)
+        return _MSDAHip.apply(value, st, so, sampling_locations, attention_weights)
+    return deformable_attention_core(value, shapes, sampling_locations, attention_weights)
+
+
 class MSDeformableAttention(nn.Module):
     def __init__(self, d=256, nhead=8, nlevels=3, npoints=4, offset_scale=0.5):
         super().__init__()
@@ -90,7 +137,7 @@ class MSDeformableAttention(nn.Module):
         aw = F.softmax(self.attention_weights(query).view(B, Q, H, L * P).float(), -1).view(B, Q, H, L, P)
         ref = ref_boxes[:, :, None, None, None, :]
         loc = ref[..., :2] + off / P * ref[..., 2:] * self.offset_scale
-        return self.output_proj(deformable_attention_core(v, shapes, loc, aw))
+        return self.output_proj(deformable_attention(v, shapes, loc, aw))
 
 
 class TransformerDecoderLayer(nn.Module):

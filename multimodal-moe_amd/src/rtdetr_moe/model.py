@@ -17,7 +17,7 @@ _DEC_LAYERS = {"r18": 3, "r34": 4, "r50": 6, "r101": 6}
 
 
 class RTDETRMoE(nn.Module):
-    def __init__(self, spec: ModelSpec | str, num_classes: int = 1, freeze_norm: bool = False):
+    def __init__(self, spec: ModelSpec | str, num_classes: int = 1, freeze_norm: bool = True):
         super().__init__()
         if isinstance(spec, str):
             spec = parse_moe_spec(spec)

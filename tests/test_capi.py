@@ -13,7 +13,7 @@ HEADER = ROOT / "include" / "moe_hip.h"
 def declared_symbols():
     text = HEADER.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(moe_[a-z0-9_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b((?:moe|rtdetr)_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_header_declares_the_expected_entry_points():
