@@ -2,9 +2,11 @@
 
 BASELINE.json configs[0] is "CPU-only PyTorch (plumbing, no GPU)": the model
 must train on CPU tensors.  This module is that device path, in plain torch
-ops with autograd; it implements the same semantics as the HIP kernels
-(include/moe_hip.h) but is NEVER used for GPU tensors -- MoEFFN sends CUDA
-tensors to ops.moe_ffn_hip, which raises if libmoe_hip.so is missing.
+ops with autograd, split like ops.py (route+dispatch / expert FFN / combine)
+so the expert-parallel composition in ep.py runs on either device.  It
+implements the same semantics as the HIP kernels (include/moe_hip.h) but is
+NEVER used for GPU tensors -- MoEFFN sends CUDA tensors to the HIP path, which
+raises if libmoe_hip.so is missing.
 """
 from __future__ import annotations
 
@@ -45,22 +47,63 @@ def dispatch_positions(idx, E, cap):
     return pos, hist, offsets
 
 
-def moe_ffn_eager(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap):
+def route_dispatch_eager(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap):
+    """-> (xp [rows, d], w [T, k], lb, z, pos [T, k], hist [E], offsets [E+1], rows)."""
     T, d = x.shape
-    E = w1.shape[0]
+    E = wg.shape[0]
     probs, lse, idx, w = route(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize)
     pos, hist, offsets = dispatch_positions(idx, E, cap)
-    y = torch.zeros((T, d), dtype=torch.float32, device=x.device)
-    xf = x.float()
-    for e in range(E):
-        sel = (idx == e) & (pos >= 0)
-        t_idx, j_idx = torch.nonzero(sel, as_tuple=True)
-        if t_idx.numel() == 0:
-            continue
-        h = F.relu(F.linear(xf[t_idx], w1[e].float(), b1[e].float()))
-        ye = F.linear(h, w2[e].float(), b2[e].float())
-        y = y.index_add(0, t_idx, ye * w[t_idx, j_idx].unsqueeze(1))
+    rows = int(offsets[-1])
+    keep = pos >= 0
+    t_idx = torch.arange(T, device=x.device).unsqueeze(1).expand(T, k)[keep]
+    xp = torch.zeros((rows, d), dtype=x.dtype, device=x.device)
+    xp = xp.index_copy(0, pos[keep], x[t_idx]) if rows else xp
     f = hist.float() / float(max(T * k, 1))
     lb = E * (f * probs.mean(0)).sum()
     z = (lse ** 2).mean()
-    return y.to(x.dtype), lb, z, hist.to(torch.int32)
+    return xp, w, lb, z, pos, hist.to(torch.int32), offsets, rows
+
+
+def expert_ffn_eager(xp, w1, b1, w2, b2, offsets, grad_scale=1.0):
+    if grad_scale != 1.0:  # scale the expert-weight gradients only (EP: sum over ranks -> mean)
+        w1, b1, w2, b2 = (_ScaleGrad.apply(t, grad_scale) for t in (w1, b1, w2, b2))
+    out = torch.zeros((xp.shape[0], w2.shape[1]), dtype=torch.float32, device=xp.device)
+    G = w1.shape[0]
+    off = [int(v) for v in offsets.tolist()]
+    for g in range(G):
+        a, b = off[g], off[g + 1]
+        if b <= a:
+            continue
+        h = F.relu(F.linear(xp[a:b].float(), w1[g].float(), b1[g].float()))
+        out = out.index_copy(0, torch.arange(a, b, device=xp.device), F.linear(h, w2[g].float(), b2[g].float()))
+    return out.to(xp.dtype)
+
+
+class _ScaleGrad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, s):
+        ctx.s = s
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g * ctx.s, None
+
+
+def combine_eager(yp, w, pos, T):
+    y = torch.zeros((T, yp.shape[1]), dtype=torch.float32, device=yp.device)
+    for j in range(pos.shape[1]):
+        keep = pos[:, j] >= 0
+        t = torch.nonzero(keep, as_tuple=True)[0]
+        if t.numel():
+            y = y.index_add(0, t, yp[pos[t, j]].float() * w[t, j:j + 1])
+    return y
+
+
+def moe_ffn_eager(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap):
+    T = x.shape[0]
+    xp, w, lb, z, pos, hist, offsets, rows = route_dispatch_eager(x, wg, ctx_bias, ctx_img, tokens_per_image, k,
+                                                                  normalize, cap)
+    yp = expert_ffn_eager(xp, w1, b1, w2, b2, offsets)
+    y = combine_eager(yp, w, pos, T)
+    return y.to(x.dtype), lb, z, hist

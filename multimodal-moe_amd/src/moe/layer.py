@@ -23,16 +23,30 @@ class MoEFFN(nn.Module):
         self.d_model = d_model
         self.ep_size = max(1, cfg.ep_size)
         self.ep_group = None          # set by parallel.expert_parallel for C4
-        E_local = E // self.ep_size
         self.wg = nn.Parameter(torch.randn(E, d_model) * cfg.router_init_std)
         self.ctx_bias = nn.Parameter(torch.randn(cfg.num_contexts, E) * cfg.ctx_init_scale) \
             if cfg.use_context else None
         bound1 = 1.0 / math.sqrt(d_model)
         bound2 = 1.0 / math.sqrt(F)
-        self.w1 = nn.Parameter(torch.empty(E_local, F, d_model).uniform_(-bound1, bound1))
-        self.b1 = nn.Parameter(torch.empty(E_local, F).uniform_(-bound1, bound1))
-        self.w2 = nn.Parameter(torch.empty(E_local, d_model, F).uniform_(-bound2, bound2))
-        self.b2 = nn.Parameter(torch.empty(E_local, d_model).uniform_(-bound2, bound2))
+        # all E experts are initialised on every rank (same RNG stream), then an
+        # expert-parallel rank keeps its slice [r E/W, (r+1) E/W)
+        w1 = torch.empty(E, F, d_model).uniform_(-bound1, bound1)
+        b1 = torch.empty(E, F).uniform_(-bound1, bound1)
+        w2 = torch.empty(E, d_model, F).uniform_(-bound2, bound2)
+        b2 = torch.empty(E, d_model).uniform_(-bound2, bound2)
+        if self.ep_size > 1:
+            import torch.distributed as dist
+
+            if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() != self.ep_size:
+                raise RuntimeError(f"expert parallelism over {self.ep_size} ranks needs torch.distributed "
+                                   f"initialised with world size {self.ep_size} before the model is built")
+            El = E // self.ep_size
+            r = dist.get_rank()
+            w1, b1, w2, b2 = (t[r * El:(r + 1) * El].clone() for t in (w1, b1, w2, b2))
+        self.w1 = nn.Parameter(w1)
+        self.b1 = nn.Parameter(b1)
+        self.w2 = nn.Parameter(w2)
+        self.b2 = nn.Parameter(b2)
         for p in (self.w1, self.b1, self.w2, self.b2):
             p.expert_parallel = self.ep_size > 1  # excluded from the DP all-reduce
         self.last_aux = None   # (lb_raw, z_raw) of the last forward
@@ -47,21 +61,21 @@ class MoEFFN(nn.Module):
         cap = cfg.capacity(T)
         cb = self.ctx_bias if (self.ctx_bias is not None and ctx_img is not None) else None
         ci = ctx_img.to(torch.int32).contiguous() if cb is not None else None
-        if flat.is_cuda:
-            if self.ep_size > 1:
-                from .ep import moe_ffn_ep
-                y, lb, z, hist = moe_ffn_ep(self, flat, cb, ci, L, cap)
-            else:
-                from .ops import moe_ffn_hip
-                y, lb, z, hist = moe_ffn_hip(flat, self.wg, cb, self.w1, self.b1, self.w2, self.b2,
-                                             ci, L, cfg.top_k, cfg.normalize, cap)
-            y = y.to(x.dtype)
+        if self.ep_size > 1:  # C4: experts sharded over ranks, all-to-all token exchange
+            from .ep import moe_ffn_ep
+
+            y, lb, z, hist = moe_ffn_ep(self, flat, cb, ci, L, cap)
+        elif flat.is_cuda:
+            from .ops import moe_ffn_hip
+
+            y, lb, z, hist = moe_ffn_hip(flat, self.wg, cb, self.w1, self.b1, self.w2, self.b2,
+                                         ci, L, cfg.top_k, cfg.normalize, cap)
         else:
-            if self.ep_size > 1:
-                raise RuntimeError("expert parallelism needs GPU tensors")
             from .eager import moe_ffn_eager
+
             y, lb, z, hist = moe_ffn_eager(flat, self.wg, cb, self.w1, self.b1, self.w2, self.b2,
                                            ci, L, cfg.top_k, cfg.normalize, cap)
+        y = y.to(x.dtype)
         self.last_aux = (lb, z)
         self.last_hist = hist
         return y.view(B, L, d)

@@ -1,12 +1,23 @@
-"""autograd wrapper of the HIP MoE FFN.
+"""autograd wrappers of the HIP MoE FFN.
 
-``moe_ffn_hip`` runs the whole routed FFN of one layer on the GPU through
-libmoe_hip.so: 6 launches forward (router, route_scan, permute, GEMM1+bias+
-ReLU, GEMM2+bias, combine) and 7 backward (combine_bwd, dgrad GEMM with the
-ReLU mask, wgrad GEMM (+db2), dgrad GEMM, wgrad GEMM (+db1), token_bwd, and a
-plain GEMM for the router weight gradient).  Nothing is synchronised with the
-host: expert offsets stay on the device and every grid is sized from host
-upper bounds.
+One layer = three autograd Functions over the C-ABI kernels:
+  _RouteDispatch  router + top-k + aux partials (K1), route_scan, permute (K2)
+                  backward: token_bwd (dispatch transpose + router backward)
+  _ExpertFFN      grouped GEMM1 (+b1, ReLU) and GEMM2 (+b2)
+                  backward: dgrad GEMM (ReLU mask), wgrad (+db2), dgrad, wgrad (+db1)
+  _Combine        gate-weighted combine (K3); backward: combine_bwd
+Single GPU: 6 launches forward, 6 (+1 torch GEMM for dWg) backward.  The
+expert-parallel path (ep.py) runs the same Functions with an all-to-all
+before and after _ExpertFFN.  Nothing is synchronised with the host: expert
+offsets stay on the device, grids are sized from host upper bounds, and the
+aux-loss gradients reach the router kernel as device tensors.
+
+Aux losses (row a3), from the router's per-block partials ``auxp``
+[nblk, E+1] (column sums of probs, and of lse^2):
+  lb = E * sum_e f_e * P_e,  f = hist / (T k),  P = colsum(auxp[:, :E]) / T
+  z  = colsum(auxp[:, E]) / T
+Their gradient w.r.t. ``auxp`` is uniform over blocks, so _RouteDispatch's
+backward reads row 0: dprob_bias = d_auxp[0, :E], z-loss scale = 2 d_auxp[0, E].
 """
 from __future__ import annotations
 
@@ -15,65 +26,115 @@ import torch
 from . import _lib as L
 
 
-class _MoEFFNHip(torch.autograd.Function):
+class _RouteDispatch(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap):
+    def forward(ctx, x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, rows):
         T, d = x.shape
-        E, F = w1.shape[0], w1.shape[1]
+        E = wg.shape[0]
         xb = x.to(torch.bfloat16).contiguous()
         wg32 = wg.float().contiguous()
         cb = ctx_bias.float().contiguous() if ctx_bias is not None else None
-        w1b = w1.to(torch.bfloat16).contiguous()
-        w2b = w2.to(torch.bfloat16).contiguous()
-        b1f = b1.float().contiguous()
-        b2f = b2.float().contiguous()
-
-        idx, w, probs, lse, lrank, bcnt, auxp = L.router_topk_fwd(
-            xb, wg32, cb, ctx_img, tokens_per_image, k, normalize)
+        idx, w, probs, lse, lrank, bcnt, auxp = L.router_topk_fwd(xb, wg32, cb, ctx_img, tokens_per_image, k,
+                                                                   normalize)
         rank_base, hist, offsets = L.route_scan(bcnt, cap)
-        rows = T * k if cap <= 0 else min(T * k, E * cap)
         xp, pos = L.permute_fwd(xb, idx, lrank, rank_base, offsets, E, cap, rows)
-        h = L.grouped_gemm(xp, w1b, offsets, E, rows, F, d, 1, L.EPI_BIAS_RELU, bias=b1f)
-        yp = L.grouped_gemm(h, w2b, offsets, E, rows, d, F, 1, L.EPI_BIAS, bias=b2f)
-        y = L.combine_fwd(yp, pos, w, T)
-
-        # aux losses, raw (coefficients applied by the caller)
-        f = hist.float() / float(max(T * k, 1))
-        P = auxp[:, :E].sum(0) / float(max(T, 1))
-        lb = E * (f * P).sum()
-        z = auxp[:, E].sum() / float(max(T, 1))
-
-        ctx.save_for_backward(xb, wg32, w1b, w2b, idx, w, probs, lse, pos, offsets, xp, h, yp, hist,
+        ctx.save_for_backward(xb, wg32, idx, w, probs, lse, pos,
                               ctx_img if ctx_img is not None else torch.empty(0))
-        ctx.meta = (T, d, E, F, k, int(normalize), rows, tokens_per_image, cb is not None,
-                    x.dtype, ctx_bias.shape[0] if ctx_bias is not None else 0)
-        ctx.mark_non_differentiable(hist)
-        return y, lb, z, hist
+        ctx.meta = (T, d, E, int(normalize), tokens_per_image, cb is not None, x.dtype,
+                    ctx_bias.shape[0] if ctx_bias is not None else 0)
+        ctx.mark_non_differentiable(pos, hist, offsets)
+        return xp, w, auxp, pos, hist, offsets
 
     @staticmethod
-    def backward(ctx, dy, g_lb, g_z, _g_hist):
-        (xb, wg32, w1b, w2b, idx, w, probs, lse, pos, offsets, xp, h, yp, hist,
-         ctx_img) = ctx.saved_tensors
-        T, d, E, F, k, normalize, rows, tpi, has_ctx, xdtype, C = ctx.meta
-        dyb = dy.to(torch.bfloat16).contiguous()
-        dyp, dw = L.combine_bwd(dyb, yp, pos, w)
-        dh = L.grouped_gemm(dyp, w2b, offsets, E, rows, F, d, 0, L.EPI_RELU_MASK, aux=h)
-        dW2, db2 = L.grouped_gemm_wgrad(dyp, h, offsets, E)
-        dxp = L.grouped_gemm(dh, w1b, offsets, E, rows, d, F, 0, L.EPI_NONE)
-        dW1, db1 = L.grouped_gemm_wgrad(dh, xp, offsets, E)
-
-        f = hist.float() / float(max(T * k, 1))
-        dprob_bias = (g_lb.float() * E / float(max(T, 1))) * f
-        zc = (g_z.float() * (2.0 / float(max(T, 1)))).reshape(1).contiguous() if g_z is not None else None
-        dx, dlogits = L.token_bwd(dxp, pos, probs, idx, w, dw, lse, dprob_bias.contiguous(), zc,
-                                  wg32, normalize)
+    def backward(ctx, d_xp, d_w, d_auxp, _p, _h, _o):
+        xb, wg32, idx, w, probs, lse, pos, ctx_img = ctx.saved_tensors
+        T, d, E, normalize, tpi, has_ctx, xdtype, C = ctx.meta
+        dev = xb.device
+        if d_xp is None:
+            d_xp = torch.zeros((1, d), dtype=torch.bfloat16, device=dev)
+            pos_use = torch.full_like(pos, -1)
+        else:
+            d_xp = d_xp.to(torch.bfloat16).contiguous()
+            pos_use = pos
+        d_w = torch.zeros_like(w) if d_w is None else d_w.float().contiguous()
+        if d_auxp is not None:
+            dprob_bias = d_auxp[0, :E].float().contiguous()
+            zc = (2.0 * d_auxp[0, E:E + 1]).float().contiguous()
+        else:
+            dprob_bias, zc = None, None
+        dx, dlogits = L.token_bwd(d_xp, pos_use, probs, idx, w, d_w, lse, dprob_bias, zc, wg32, normalize)
         dwg = dlogits.t().mm(xb.float())
         dcb = None
         if has_ctx:
-            per_img = dlogits.view(-1, tpi, E).sum(1)
-            dcb = torch.zeros((C, E), dtype=torch.float32, device=dy.device)
-            dcb.index_add_(0, ctx_img.long(), per_img)
-        return (dx.to(xdtype), dwg, dcb, dW1, db1, dW2, db2, None, None, None, None, None)
+            dcb = torch.zeros((C, E), dtype=torch.float32, device=dev)
+            dcb.index_add_(0, ctx_img.long(), dlogits.view(-1, tpi, E).sum(1))
+        return dx.to(xdtype), dwg, dcb, None, None, None, None, None, None
+
+
+class _ExpertFFN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xp, w1, b1, w2, b2, offsets, rows, grad_scale):
+        G, F, d = w1.shape
+        w1b = w1.to(torch.bfloat16).contiguous()
+        w2b = w2.to(torch.bfloat16).contiguous()
+        h = L.grouped_gemm(xp, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU, bias=b1.float().contiguous())
+        yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=b2.float().contiguous())
+        ctx.save_for_backward(xp, h, w1b, w2b, offsets)
+        ctx.meta = (G, F, d, rows, float(grad_scale))
+        return yp
+
+    @staticmethod
+    def backward(ctx, d_yp):
+        xp, h, w1b, w2b, offsets = ctx.saved_tensors
+        G, F, d, rows, s = ctx.meta
+        dyp = d_yp.to(torch.bfloat16).contiguous()
+        dh = L.grouped_gemm(dyp, w2b, offsets, G, rows, F, d, 0, L.EPI_RELU_MASK, aux=h)
+        dW2, db2 = L.grouped_gemm_wgrad(dyp, h, offsets, G)
+        dxp = L.grouped_gemm(dh, w1b, offsets, G, rows, d, F, 0, L.EPI_NONE)
+        dW1, db1 = L.grouped_gemm_wgrad(dh, xp, offsets, G)
+        if s != 1.0:
+            for t in (dW1, db1, dW2, db2):
+                t.mul_(s)
+        return dxp, dW1, db1, dW2, db2, None, None, None
+
+
+class _Combine(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, yp, w, pos, T):
+        y = L.combine_fwd(yp.to(torch.bfloat16).contiguous(), pos, w, T)
+        ctx.save_for_backward(yp, w, pos)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        yp, w, pos = ctx.saved_tensors
+        dyp, dw = L.combine_bwd(dy.to(torch.bfloat16).contiguous(), yp.to(torch.bfloat16).contiguous(), pos, w)
+        return dyp, dw, None, None
+
+
+def aux_losses(auxp, hist, T, k):
+    E = hist.shape[0]
+    f = hist.float() / float(max(T * k, 1))
+    P = auxp[:, :E].sum(0) / float(max(T, 1))
+    lb = E * (f * P).sum()
+    z = auxp[:, E].sum() / float(max(T, 1))
+    return lb, z
+
+
+def route_dispatch_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap):
+    T = x.shape[0]
+    E = wg.shape[0]
+    rows = T * k if cap <= 0 else min(T * k, E * cap)
+    return _RouteDispatch.apply(x, wg, ctx_bias, ctx_img, int(tokens_per_image), int(k), bool(normalize), int(cap),
+                                rows) + (rows,)
+
+
+def expert_ffn_hip(xp, w1, b1, w2, b2, offsets, rows, grad_scale=1.0):
+    return _ExpertFFN.apply(xp, w1, b1, w2, b2, offsets, int(rows), grad_scale)
+
+
+def combine_hip(yp, w, pos, T):
+    return _Combine.apply(yp, w, pos, int(T))
 
 
 def moe_ffn_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap):
@@ -88,5 +149,10 @@ def moe_ffn_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, n
         raise L.MoEKernelError("moe_ffn_hip needs GPU tensors")
     if ctx_bias is not None and ctx_img is None:
         raise L.MoEKernelError("ctx_bias given without ctx_img")
-    return _MoEFFNHip.apply(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, int(tokens_per_image), int(k),
-                            bool(normalize), int(cap))
+    T = x.shape[0]
+    xp, w, auxp, pos, hist, offsets, rows = route_dispatch_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k,
+                                                               normalize, cap)
+    yp = expert_ffn_hip(xp, w1, b1, w2, b2, offsets, rows)
+    y = combine_hip(yp, w, pos, T)
+    lb, z = aux_losses(auxp, hist, T, k)
+    return y, lb, z, hist

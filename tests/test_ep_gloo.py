@@ -1,0 +1,95 @@
+"""Expert parallelism on CPU (gloo, world size 2, 4 experts -> 2 per rank):
+the EP layer reproduces the single-process layer with all experts -- outputs,
+input gradients, router gradients (after the DP mean) and each rank's expert
+gradients (after the 1/W scaling) -- on skewed, context-binned inputs."""
+from __future__ import annotations
+
+import os
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parents[1]
+E, K, D, F, TPI = 4, 2, 16, 32, 12
+
+
+def _cfg(ep):
+    from src.moe.config import MoEConfig
+
+    return MoEConfig(num_experts=E, top_k=K, hidden=F, ep_size=ep, capacity_factor=0.0)
+
+
+def _inputs(rank):
+    g = torch.Generator().manual_seed(100 + rank)
+    x = torch.randn(3, TPI, D, generator=g)
+    ctx = torch.full((3,), rank % 6, dtype=torch.int32)  # one context bin per rank (C4)
+    dy = torch.randn(3, TPI, D, generator=g)
+    return x, ctx, dy
+
+
+def _worker(rank, world, port, out):
+    for p in (str(ROOT / "multimodal-moe_amd"), str(ROOT)):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from src.moe.layer import MoEFFN
+
+    torch.manual_seed(0)
+    layer = MoEFFN(D, _cfg(world))
+    x, ctx, dy = _inputs(rank)
+    x.requires_grad_(True)
+    y = layer(x, ctx)
+    lb, z = layer.last_aux
+    ((y * dy).sum() + 0.1 * lb + 0.05 * z).backward()
+    res = {"y": y.detach(), "dx": x.grad, "hist": layer.last_hist}
+    for n in ("wg", "ctx_bias"):  # replicated: DP mean over ranks
+        g = getattr(layer, n).grad.clone()
+        dist.all_reduce(g)
+        res["d" + n] = g / world
+    for n in ("w1", "b1", "w2", "b2"):
+        res["d" + n] = getattr(layer, n).grad.clone()
+    torch.save(res, out / f"r{rank}.pt")
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_ep_gloo_world2_matches_single_process(tmp_path):
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    W = 2
+    mp.spawn(_worker, args=(W, port, tmp_path), nprocs=W, join=True)
+    from src.moe.layer import MoEFFN
+
+    torch.manual_seed(0)
+    ref = MoEFFN(D, _cfg(1))
+    El = E // W
+    for r in range(W):
+        got = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
+        x, ctx, dy = _inputs(r)
+        x.requires_grad_(True)
+        ref.zero_grad(set_to_none=True)
+        y = ref(x, ctx)
+        lb, z = ref.last_aux
+        ((y * dy).sum() + 0.1 * lb + 0.05 * z).backward()
+        torch.testing.assert_close(got["y"], y.detach(), rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(got["dx"], x.grad, rtol=1e-5, atol=1e-5)
+        assert torch.equal(got["hist"], ref.last_hist)
+        if r == 0:
+            ref_grads = {n: getattr(ref, n).grad.clone() for n in ("wg", "ctx_bias", "w1", "b1", "w2", "b2")}
+        else:
+            for n in ref_grads:
+                ref_grads[n] += getattr(ref, n).grad
+    for r in range(W):
+        got = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
+        for n in ("wg", "ctx_bias"):
+            torch.testing.assert_close(got["d" + n], ref_grads[n] / W, rtol=1e-4, atol=1e-5)
+        for n in ("w1", "b1", "w2", "b2"):
+            torch.testing.assert_close(got["d" + n], ref_grads[n][r * El:(r + 1) * El] / W, rtol=1e-4, atol=1e-5)
