@@ -163,6 +163,26 @@ int rtdetr_msda_bwd(const void* value, const int32_t* shapes, const int32_t* sta
  * Returns 0, or -1 for an unknown key/value. */
 int moe_set_tuning(const char* key, int value);
 
+/* Launch profiler (measurement only; no reference counterpart).
+ * While enabled, every kernel launch of the library records a hipEvent pair on
+ * its own stream plus its algorithmic work: flops for kind 0 (grouped GEMM,
+ * 2 N K per routed row, the row count read back from offsets[G]); bytes for
+ * kinds 1 (permute/combine row moves), 2 (router), 3 (route scan),
+ * 4 (token backward), 5 (deformable attention).  Not thread-safe, not for
+ * graph capture.  enable(0|1) also clears; get() waits for the record. */
+enum moe_prof_kind {
+  MOE_PROF_GEMM = 0,
+  MOE_PROF_ROWMOVE = 1,
+  MOE_PROF_ROUTER = 2,
+  MOE_PROF_SCAN = 3,
+  MOE_PROF_TOKEN_BWD = 4,
+  MOE_PROF_MSDA = 5
+};
+int moe_profile_enable(int on);
+int moe_profile_count(void);
+int moe_profile_get(int i, int* kind, float* ms, double* work);
+int moe_profile_clear(void);
+
 /* Thread-local message for the last non-zero return code. */
 const char* moe_last_error(void);
 

@@ -1,5 +1,9 @@
-// Error plumbing and identification for the C-ABI (include/moe_hip.h).
+// Error plumbing, identification and the launch profiler of the C-ABI
+// (include/moe_hip.h).
+#include <vector>
+
 #include "moe_common.h"
+#include "prof.h"
 
 namespace moe {
 
@@ -21,8 +25,113 @@ int check_launch(const char* what) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// launch profiler: a hipEvent pair recorded on the launch stream around every
+// kernel launch of the library while enabled (not thread-safe; profiling only)
+// ---------------------------------------------------------------------------
+namespace {
+struct Record {
+  int kind;
+  hipEvent_t start, stop;
+  double work_fixed, work_per_row;
+  int rows_slot;  // index into the pinned rows buffer, or -1
+};
+struct Profiler {
+  bool on = false;
+  std::vector<Record> recs;
+  std::vector<hipEvent_t> pool;  // recycled events
+  int32_t* rows_host = nullptr;  // pinned, one int per record that reads device rows
+  int rows_cap = 0, rows_used = 0;
+
+  hipEvent_t ev() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  void clear() {
+    for (auto& r : recs) {
+      pool.push_back(r.start);
+      pool.push_back(r.stop);
+    }
+    recs.clear();
+    rows_used = 0;
+  }
+};
+Profiler g_prof;
+}  // namespace
+
+ProfScope::ProfScope(hipStream_t s, int kind, double work_fixed, const int32_t* dev_rows, double work_per_row)
+    : stream_(s), active_(g_prof.on), idx_(-1) {
+  if (!active_) return;
+  Record r{kind, g_prof.ev(), g_prof.ev(), work_fixed, work_per_row, -1};
+  if (dev_rows != nullptr) {
+    if (g_prof.rows_used >= g_prof.rows_cap) {
+      const int cap = g_prof.rows_cap ? 2 * g_prof.rows_cap : 4096;
+      int32_t* nb = nullptr;
+      if (hipHostMalloc(reinterpret_cast<void**>(&nb), cap * sizeof(int32_t)) == hipSuccess) {
+        if (g_prof.rows_host) {
+          (void)hipDeviceSynchronize();
+          std::copy(g_prof.rows_host, g_prof.rows_host + g_prof.rows_used, nb);
+          (void)hipHostFree(g_prof.rows_host);
+        }
+        g_prof.rows_host = nb;
+        g_prof.rows_cap = cap;
+      }
+    }
+    if (g_prof.rows_used < g_prof.rows_cap) {
+      r.rows_slot = g_prof.rows_used++;
+      dev_rows_ = dev_rows;
+    }
+  }
+  (void)hipEventRecord(r.start, s);
+  g_prof.recs.push_back(r);
+  idx_ = (int)g_prof.recs.size() - 1;
+}
+
+ProfScope::~ProfScope() {
+  if (!active_ || idx_ < 0) return;
+  Record& r = g_prof.recs[idx_];
+  (void)hipEventRecord(r.stop, stream_);
+  if (r.rows_slot >= 0)  // stream-ordered read of the device row count (after the kernel)
+    (void)hipMemcpyAsync(g_prof.rows_host + r.rows_slot, dev_rows_, sizeof(int32_t), hipMemcpyDeviceToHost,
+                         stream_);
+}
+
 }  // namespace moe
 
 extern "C" const char* moe_last_error(void) { return moe::g_last_error.c_str(); }
 
-extern "C" const char* moe_version(void) { return "moe_hip 0.1.0 gfx950"; }
+extern "C" const char* moe_version(void) { return "moe_hip 0.2.0 gfx950"; }
+
+extern "C" int moe_profile_enable(int on) {
+  moe::g_prof.clear();
+  moe::g_prof.on = on != 0;
+  return 0;
+}
+
+extern "C" int moe_profile_count(void) { return (int)moe::g_prof.recs.size(); }
+
+extern "C" int moe_profile_get(int i, int* kind, float* ms, double* work) {
+  if (i < 0 || i >= (int)moe::g_prof.recs.size()) return moe::fail("moe_profile_get: index out of range");
+  auto& r = moe::g_prof.recs[i];
+  if (hipEventSynchronize(r.stop) != hipSuccess) return moe::fail("moe_profile_get: event sync failed");
+  if (r.rows_slot >= 0) (void)hipDeviceSynchronize();  // the rows copy trails the stop event
+  float t = 0.f;
+  const hipError_t e = hipEventElapsedTime(&t, r.start, r.stop);
+  if (e != hipSuccess) return moe::fail(std::string("moe_profile_get: ") + hipGetErrorString(e));
+  *kind = r.kind;
+  *ms = t;
+  const double rows = r.rows_slot >= 0 ? (double)moe::g_prof.rows_host[r.rows_slot] : 0.0;
+  *work = r.work_fixed + r.work_per_row * rows;
+  return 0;
+}
+
+extern "C" int moe_profile_clear(void) {
+  moe::g_prof.clear();
+  return 0;
+}

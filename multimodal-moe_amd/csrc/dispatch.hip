@@ -7,6 +7,7 @@
 // row movers: permute reads T rows and writes A rows; combine reads A rows
 // and writes T rows; combine_bwd reads T + A rows and writes A rows.
 #include "moe_common.h"
+#include "prof.h"
 
 namespace moe {
 
@@ -148,6 +149,8 @@ extern "C" int moe_permute_fwd(const void* x, const int32_t* topk_idx,
   if (check_row_width(d, "permute")) return -1;
   if (E < 1 || E > 64 || k < 1 || k > 8) return fail("permute: need 1<=E<=64, 1<=k<=8");
   if (T <= 0) return 0;
+  // bytes: x read once, idx/local_rank read, pos written, kept rows written
+  ProfScope prof(stream, PROF_ROWMOVE, 2.0 * T * d + 12.0 * T * k, offsets + E, 2.0 * d);
   hipLaunchKernelGGL(permute_fwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
                      static_cast<const uint16_t*>(x), topk_idx, local_rank, rank_base,
                      offsets, T, d, E, k, cap, static_cast<uint16_t*>(xp), pos);
@@ -159,6 +162,8 @@ extern "C" int moe_combine_fwd(const void* yp, const int32_t* pos, const float* 
   if (check_row_width(d, "combine")) return -1;
   if (k < 1 || k > 8) return fail("combine: need 1<=k<=8");
   if (T <= 0) return 0;
+  // bytes: T*k expert rows + pos/w read, y written
+  ProfScope prof(stream, PROF_ROWMOVE, 2.0 * T * d + 2.0 * T * k * d + 8.0 * T * k);
   hipLaunchKernelGGL(combine_fwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
                      static_cast<const uint16_t*>(yp), pos, topk_w, T, d, k,
                      static_cast<uint16_t*>(y));
@@ -171,6 +176,8 @@ extern "C" int moe_combine_bwd(const void* dy, const void* yp, const int32_t* po
   if (check_row_width(d, "combine_bwd")) return -1;
   if (k < 1 || k > 8) return fail("combine_bwd: need 1<=k<=8");
   if (T <= 0) return 0;
+  // bytes: dy + T*k expert rows + pos/w read, dyp rows + dw written
+  ProfScope prof(stream, PROF_ROWMOVE, 2.0 * T * d + 4.0 * T * k * d + 12.0 * T * k);
   hipLaunchKernelGGL(combine_bwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
                      static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(yp), pos,
                      topk_w, T, d, k, static_cast<uint16_t*>(dyp), dw);

@@ -27,6 +27,7 @@
 //      S-deep ring with S-1 K-tiles in flight, counted `s_waitcnt vmcnt` +
 //      raw s_barrier (no vmcnt(0) drain inside the loop).
 #include "moe_common.h"
+#include "prof.h"
 
 namespace moe {
 
@@ -556,6 +557,7 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
   const int BMsel = big ? 128 : 64;
   const int mtiles = ((max_rows + BMsel - 1) / BMsel + G + 7) / 8 * 8;  // padded to the XCD count
   dim3 grid(mtiles * nt);
+  ProfScope prof(stream, PROF_GEMM, 0.0, offsets + G, 2.0 * N * K);  // flops: 2 N K per routed row
 
 #define GG_ROWS(BM, BK_, EPI) launch<BM, 128, true, BK_, MODE_ROWS, EPI, false>(p, grid, stream)
 #define GG_EPI(BM, BK_)                                                  \
@@ -599,6 +601,7 @@ extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, f
   const int ntn = N / 128;
   const bool big = M % 128 == 0 && (long long)(M / 128) * ntn * G >= 512;
   const int gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
+  ProfScope prof(stream, PROF_GEMM, 0.0, offsets + G, 2.0 * M * N);  // flops: 2 M N per routed row
   if (big) {
     dim3 grid((M / 128) * ntn * gpad);
     if (colsum) launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream);

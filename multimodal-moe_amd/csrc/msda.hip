@@ -16,6 +16,7 @@
 // with fp32 atomics into an fp32 buffer (each corner row segment is 64-256 B
 // contiguous per wave-instruction).
 #include "moe_common.h"
+#include "prof.h"
 
 namespace moe {
 
@@ -195,6 +196,9 @@ extern "C" int rtdetr_msda_fwd(const void* value, const int32_t* shapes, const i
   const long long groups = (long long)B * Q * H;
   const uint16_t* v = static_cast<const uint16_t*>(value);
   uint16_t* o = static_cast<uint16_t*>(out);
+  // bytes: 4 bilinear corners of D bf16 per sample, loc+attn per sample, output rows
+  const double samples = (double)groups * L * P;
+  ProfScope prof(stream, PROF_MSDA, samples * (8.0 * D + 12.0) + 2.0 * groups * D);
   if (D == 32)
     hipLaunchKernelGGL(msda_fwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
                        loc, attn, B, S, Q, H, L, P, o);
@@ -215,6 +219,9 @@ extern "C" int rtdetr_msda_bwd(const void* value, const int32_t* shapes, const i
   const long long groups = (long long)B * Q * H;
   const uint16_t* v = static_cast<const uint16_t*>(value);
   const uint16_t* go = static_cast<const uint16_t*>(grad_out);
+  // bytes: forward's gathers + 4 fp32 corner atomics of D per sample, grad_loc/attn, grad_out
+  const double samples = (double)groups * L * P;
+  ProfScope prof(stream, PROF_MSDA, samples * (8.0 * D + 16.0 * D + 24.0) + 2.0 * groups * D);
   if (D == 32)
     hipLaunchKernelGGL(msda_bwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
                        loc, attn, go, B, S, Q, H, L, P, grad_value, grad_loc, grad_attn);

@@ -14,6 +14,7 @@
 //                    no atomics), gate + softmax + z-loss backward, and the
 //                    router's dx term dlogits.Wg, fused.
 #include "moe_common.h"
+#include "prof.h"
 
 namespace moe {
 
@@ -398,6 +399,9 @@ extern "C" int moe_router_topk_fwd(const void* x, const float* wg, const float* 
   const int em = emax_for(E);
   const size_t shmem = (size_t)E * d * 4 + 64 * 8 * 4 + 4 * (em + 1) * 4;
   const uint16_t* xb = static_cast<const uint16_t*>(x);
+  // bytes: x, Wg once, per-token outputs (idx, w, probs, lse, local rank), per-block partials
+  ProfScope prof(stream, PROF_ROUTER,
+                 2.0 * T * d + 4.0 * E * d + 12.0 * T * k + 4.0 * T * (E + 1) + 4.0 * nblk * (k * E + E + 1));
 #define LAUNCH_R(EM)                                                                       \
   allow_lds<router_topk_fwd_kernel<EM>>(shmem);                                             \
   hipLaunchKernelGGL(router_topk_fwd_kernel<EM>, dim3(nblk), dim3(256), shmem, stream, xb, \
@@ -418,6 +422,7 @@ extern "C" int moe_route_scan(const int32_t* block_counts, int nblk, int k, int 
                               hipStream_t stream) {
   if (E < 1 || E > 64 || k < 1 || k > 8) return fail("route_scan: need 1<=E<=64, 1<=k<=8");
   if (nblk < 0) return fail("route_scan: nblk < 0");
+  ProfScope prof(stream, PROF_SCAN, 8.0 * nblk * k * E + 12.0 * E);
   hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, stream, block_counts, nblk, k,
                      E, cap, rank_base, hist, offsets);
   return check_launch("moe_route_scan");
@@ -438,6 +443,9 @@ extern "C" int moe_token_bwd(const void* dxp, const int32_t* pos, const float* p
   const size_t shmem = (size_t)E * d * 4;
   const uint16_t* dxpb = static_cast<const uint16_t*>(dxp);
   uint16_t* dxb = static_cast<uint16_t*>(dx);
+  // bytes: T*k rows of dXp, per-token routing state, Wg; dx and dlogits written
+  ProfScope prof(stream, PROF_TOKEN_BWD,
+                 2.0 * T * k * d + 2.0 * T * d + 8.0 * T * E + 20.0 * T * k + 4.0 * T + 4.0 * E * d);
 #define LAUNCH_B(EM)                                                                          \
   allow_lds<token_bwd_kernel<EM>>(shmem);                                                   \
   hipLaunchKernelGGL(token_bwd_kernel<EM>, dim3(grid), dim3(256), shmem, stream, dxpb, pos, \

@@ -38,6 +38,10 @@ SIGNATURES = {
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_msda_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
+    "moe_profile_enable": (_I, [_I]),
+    "moe_profile_count": (_I, []),
+    "moe_profile_get": (_I, [_I, _P, _P, _P]),
+    "moe_profile_clear": (_I, []),
     "moe_last_error": (ctypes.c_char_p, []),
     "moe_version": (ctypes.c_char_p, []),
 }
@@ -80,79 +84,63 @@ def lib() -> ctypes.CDLL:
     return _LIB
 
 
-class KernelTimer:
-    """Optional per-launch HIP-event timing of the MoE kernels (bench.py).
+PROF_KINDS = {0: "grouped_gemm", 1: "dispatch", 2: "router", 3: "route_scan", 4: "token_bwd", 5: "msda"}
+PROF_UNITS = {0: "flop"}  # every other kind counts bytes
 
-    When enabled, every wrapped launch records a pair of torch.cuda.Events on
-    the stream it is launched on (torch's current stream -- the same stream
-    the C-ABI call receives) together with its algorithmic work: flops for the
-    grouped GEMMs (2*rows*N*K, rows read from the device offsets after the
-    launch completed) and bytes for the row movers.
 
-    mode "eager": each launch appends a record; ``harvest()`` consumes them.
-    mode "graph": records are made only while a stream is being captured, so
-    the event pairs become event-record nodes of the hipGraph; every replay
-    re-stamps them and ``harvest()`` (after the replay completed) adds that
-    replay's durations without dropping the records.
+class KernelProfiler:
+    """Per-launch kernel timing by the library's own profiler (moe_profile_*).
+
+    While enabled, libmoe_hip records a hipEvent pair on each launch's stream
+    directly around the kernel (no Python between the events) plus its
+    algorithmic work (flops for the grouped GEMMs with the row count read back
+    from the device offsets, bytes for the others; include/moe_hip.h).
+    ``harvest()`` adds the completed records to running totals per kind.
+    Not usable inside hipGraph capture.
     """
 
     def __init__(self):
         self.enabled = False
-        self.mode = "eager"
-        self.records = []  # (kind, start_event, end_event, work_fn)
         self.acc = {}
 
-    def start(self, mode="eager"):
-        self.records = []
+    def start(self):
+        _check(lib().moe_profile_enable(1), "moe_profile_enable")
         self.acc = {}
-        self.mode = mode
         self.enabled = True
 
     def stop(self):
+        lib().moe_profile_enable(0)
         self.enabled = False
 
     def reset_totals(self):
         self.acc = {}
 
-    def wrap(self, kind, work_fn, launch):
-        if not self.enabled:
-            return launch()
-        if self.mode == "graph" and not torch.cuda.is_current_stream_capturing():
-            return launch()
-        s = torch.cuda.Event(enable_timing=True)
-        e = torch.cuda.Event(enable_timing=True)
-        s.record()
-        out = launch()
-        e.record()
-        self.records.append((kind, s, e, work_fn))
-        return out
-
     def harvest(self):
-        """Add the completed launches' durations/work to the totals (syncs)."""
-        torch.cuda.synchronize()
-        for kind, s, e, work_fn in self.records:
-            d = self.acc.setdefault(kind, {"launches": 0, "total_ms": 0.0, "work": 0.0})
+        """Consume the library's records into the totals (waits for them)."""
+        if not self.enabled:
+            return
+        kind, ms, work = ctypes.c_int(), ctypes.c_float(), ctypes.c_double()
+        n = lib().moe_profile_count()
+        for i in range(n):
+            _check(lib().moe_profile_get(i, ctypes.byref(kind), ctypes.byref(ms), ctypes.byref(work)),
+                   "moe_profile_get")
+            name = PROF_KINDS.get(kind.value, str(kind.value))
+            d = self.acc.setdefault(name, {"launches": 0, "total_ms": 0.0, "work": 0.0,
+                                           "unit": PROF_UNITS.get(kind.value, "byte")})
             d["launches"] += 1
-            d["total_ms"] += s.elapsed_time(e)
-            d["work"] += float(work_fn())
-        if self.mode == "eager":
-            self.records = []
+            d["total_ms"] += ms.value
+            d["work"] += work.value
+        lib().moe_profile_clear()
 
     def summary(self):
-        """{kind: dict(launches, total_ms, avg_us, work)} of the harvested launches."""
-        if self.mode == "eager" and self.records:
-            self.harvest()
+        """{kind: dict(launches, total_ms, avg_us, work, unit)} of the harvested launches."""
         out = {k: dict(v) for k, v in self.acc.items()}
         for d in out.values():
             d["avg_us"] = 1e3 * d["total_ms"] / max(d["launches"], 1)
         return out
 
 
-TIMER = KernelTimer()
-
-
-def _rows_of(offsets):
-    return lambda: int(offsets[-1].item())
+TIMER = KernelProfiler()
 
 
 def _ptr(t: torch.Tensor | None) -> int | None:
@@ -243,11 +231,9 @@ def permute_fwd(x, topk_idx, local_rank, rank_base, offsets, E, cap, rows_alloc)
     _need(x, torch.bfloat16, "x")
     xp = torch.empty((max(rows_alloc, 1), d), dtype=torch.bfloat16, device=x.device)
     pos = torch.empty((T, k), dtype=torch.int32, device=x.device)
-    rows = _rows_of(offsets)
-    # read T rows + write kept rows + indices (idx, rank, pos: 12 B per assignment)
-    rc = TIMER.wrap("dispatch", lambda: 2.0 * d * (T + rows()) + 12.0 * T * k, lambda: lib().moe_permute_fwd(
+    rc = lib().moe_permute_fwd(
         _ptr(x), _ptr(topk_idx), _ptr(local_rank), _ptr(rank_base), _ptr(offsets), T, d, E, k, int(cap),
-        _ptr(xp), _ptr(pos), _stream()))
+        _ptr(xp), _ptr(pos), _stream())
     _check(rc, "moe_permute_fwd")
     return xp, pos
 
@@ -257,9 +243,8 @@ def combine_fwd(yp, pos, topk_w, T):
     k = pos.shape[1]
     _need(yp, torch.bfloat16, "yp")
     y = torch.empty((T, d), dtype=torch.bfloat16, device=yp.device)
-    # read T*k rows (all kept when cap = 0) + gates/pos (8 B per assignment) + write T rows
-    rc = TIMER.wrap("dispatch", lambda: 2.0 * d * (T * k + T) + 8.0 * T * k, lambda: lib().moe_combine_fwd(
-        _ptr(yp), _ptr(pos), _ptr(topk_w), T, d, k, _ptr(y), _stream()))
+    rc = lib().moe_combine_fwd(
+        _ptr(yp), _ptr(pos), _ptr(topk_w), T, d, k, _ptr(y), _stream())
     _check(rc, "moe_combine_fwd")
     return y
 
@@ -271,9 +256,8 @@ def combine_bwd(dy, yp, pos, topk_w):
     _need(yp, torch.bfloat16, "yp")
     dyp = torch.empty_like(yp)
     dw = torch.empty((T, k), dtype=torch.float32, device=dy.device)
-    # read dy (T rows) + Yp (T*k rows) + write dYp (T*k rows) + gates/pos/dw (12 B per assignment)
-    rc = TIMER.wrap("dispatch", lambda: 2.0 * d * (T + 2 * T * k) + 12.0 * T * k, lambda: lib().moe_combine_bwd(
-        _ptr(dy), _ptr(yp), _ptr(pos), _ptr(topk_w), T, d, k, _ptr(dyp), _ptr(dw), _stream()))
+    rc = lib().moe_combine_bwd(
+        _ptr(dy), _ptr(yp), _ptr(pos), _ptr(topk_w), T, d, k, _ptr(dyp), _ptr(dw), _stream())
     _check(rc, "moe_combine_bwd")
     return dyp, dw
 
@@ -299,10 +283,9 @@ def grouped_gemm(a, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None,
     if a.shape[1] != K or a.shape[0] < max_rows:
         raise MoEKernelError("grouped_gemm: a must be [>=max_rows, K]")
     c = out if out is not None else torch.empty((a.shape[0], N), dtype=torch.bfloat16, device=a.device)
-    rows = _rows_of(offsets)
-    rc = TIMER.wrap("grouped_gemm", lambda: 2.0 * rows() * N * K, lambda: lib().moe_grouped_gemm(
+    rc = lib().moe_grouped_gemm(
         MOE_BF16, _ptr(a), _ptr(b), _ptr(c), _ptr(offsets), G, int(max_rows), N, K, int(trans_b),
-        int(epilogue), _ptr(bias), _ptr(aux), None, _stream()))
+        int(epilogue), _ptr(bias), _ptr(aux), None, _stream())
     _check(rc, "moe_grouped_gemm")
     return c
 
@@ -313,9 +296,8 @@ def grouped_gemm_wgrad(x, y, offsets, G, want_colsum=True):
     M, N = x.shape[1], y.shape[1]
     c = torch.empty((G, M, N), dtype=torch.float32, device=x.device)
     cs = torch.empty((G, M), dtype=torch.float32, device=x.device) if want_colsum else None
-    rows = _rows_of(offsets)
-    rc = TIMER.wrap("grouped_gemm", lambda: 2.0 * rows() * M * N, lambda: lib().moe_grouped_gemm_wgrad(
-        MOE_BF16, _ptr(x), _ptr(y), _ptr(c), _ptr(cs), _ptr(offsets), G, M, N, _stream()))
+    rc = lib().moe_grouped_gemm_wgrad(
+        MOE_BF16, _ptr(x), _ptr(y), _ptr(c), _ptr(cs), _ptr(offsets), G, M, N, _stream())
     _check(rc, "moe_grouped_gemm_wgrad")
     return c, cs
 
@@ -329,8 +311,8 @@ def msda_fwd(value, shapes, starts, loc, attn):
     _need(loc, torch.float32, "loc")
     _need(attn, torch.float32, "attn")
     out = torch.empty((B, Q, H * D), dtype=torch.bfloat16, device=value.device)
-    rc = TIMER.wrap("msda", lambda: 0.0, lambda: lib().rtdetr_msda_fwd(
-        _ptr(value), _ptr(shapes), _ptr(starts), _ptr(loc), _ptr(attn), B, S, Q, H, D, L, P, _ptr(out), _stream()))
+    rc = lib().rtdetr_msda_fwd(
+        _ptr(value), _ptr(shapes), _ptr(starts), _ptr(loc), _ptr(attn), B, S, Q, H, D, L, P, _ptr(out), _stream())
     _check(rc, "rtdetr_msda_fwd")
     return out
 
@@ -342,8 +324,8 @@ def msda_bwd(value, shapes, starts, loc, attn, grad_out):
     gv = torch.empty((B, S, H, D), dtype=torch.float32, device=value.device)
     gl = torch.empty_like(loc)
     ga = torch.empty_like(attn)
-    rc = TIMER.wrap("msda", lambda: 0.0, lambda: lib().rtdetr_msda_bwd(
+    rc = lib().rtdetr_msda_bwd(
         _ptr(value), _ptr(shapes), _ptr(starts), _ptr(loc), _ptr(attn), _ptr(grad_out), B, S, Q, H, D, L, P,
-        _ptr(gv), _ptr(gl), _ptr(ga), _stream()))
+        _ptr(gv), _ptr(gl), _ptr(ga), _stream())
     _check(rc, "rtdetr_msda_bwd")
     return gv, gl, ga

@@ -283,3 +283,34 @@ def test_library_reports_bad_shapes(hip_lib):
     wg = torch.zeros((4, 100), dtype=torch.float32, device=DEV)
     with pytest.raises(L.MoEKernelError, match="multiple of 128"):
         L.router_topk_fwd(x, wg, None, None, 10, 1, True)
+
+
+def test_library_profiler_records_gemm_work(hip_lib):
+    """moe_profile_*: one record per launch, GEMM work = 2 N K x routed rows read from offsets[G]."""
+    from src.moe import _lib as L
+
+    rows_per_group = [100, 0, 37, 300]
+    G, N, K = len(rows_per_group), 256, 128
+    offsets = torch.tensor(np.concatenate([[0], np.cumsum(rows_per_group)]), dtype=torch.int32, device=DEV)
+    R = int(sum(rows_per_group))
+    A = torch.ones((R + 64, K), dtype=torch.bfloat16, device=DEV)
+    B = torch.ones((G, N, K), dtype=torch.bfloat16, device=DEV)
+    L.TIMER.start()
+    try:
+        L.grouped_gemm(A, B, offsets, G, R + 64, N, K, 1, L.EPI_NONE)
+        L.grouped_gemm_wgrad(A[:R].contiguous(), torch.ones((R, N), dtype=torch.bfloat16, device=DEV), offsets, G)
+        L.TIMER.harvest()
+    finally:
+        L.TIMER.stop()
+    s = L.TIMER.summary()
+    g = s["grouped_gemm"]
+    assert g["launches"] == 2 and g["unit"] == "flop"
+    assert g["work"] == 2.0 * R * N * K + 2.0 * R * K * N
+    assert 0 < g["avg_us"] < 1e5
+    assert lib_count_after_stop() == 0
+
+
+def lib_count_after_stop():
+    from src.moe import _lib as L
+
+    return L.lib().moe_profile_count()
