@@ -13,9 +13,11 @@ kept resident in HBM; random-init weights.
       --master-port P bench.py --gpus N         # DP over RCCL (C3), weak scaling
 
 Rank 0 prints ONE JSON line.  Besides the contract keys it carries
-``roofline`` for the dominant HIP kernel (the grouped expert GEMM, HIP events
-around every launch inside the timed region, algorithmic flops 2*rows*N*K per
-launch), ``roofline_dispatch`` for the HBM-bound row movers, and
+``roofline`` for the dominant HIP kernel (the grouped expert GEMM: kernel
+times from dispatch-stamped HIP events of every launch inside the timed
+region, recorded by libmoe_hip itself; algorithmic bytes and flops per launch;
+bound = HBM, since at d=256, F=1024 every expert GEMM has ~200 flop/B, below
+the MI355X balance of ~312), ``roofline_dispatch`` for the row movers, and
 ``cpu_baseline``: the same model in fp32 on the host cores with the MoE layers
 computed by the CPU oracle (oracle/moe_oracle.py, kind "port"), timed on a
 bounded sample (rank 0, N=1 only).
@@ -50,6 +52,54 @@ WORKLOADS = {
     "c5": dict(spec="rtdetr-r50-moe32-top4-cf1.25-fp8", batch=16,
                desc="C5: 32-expert top-4 fp8 experts, capacity factor 1.25, bs=16/GPU"),
 }
+
+
+def load_pmc_traffic(workload):
+    """HBM bytes per launch per kernel group from the committed PMC summary of
+    the same workload (tools/gpu_round.sh + tools/profile_summary.py:
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected)."""
+    p = ROOT / "profiles" / f"pmc_traffic_{workload}.json"
+    if not p.exists():
+        return {}
+    try:
+        data = json.loads(p.read_text())
+    except ValueError:
+        return {}
+    out = {}
+    for g, e in data.get("groups", {}).items():
+        if "hbm_bytes_per_launch" in e:
+            out[g] = {"bytes": e["hbm_bytes_per_launch"], "source": f"{p.relative_to(ROOT)} ({data.get('source')})"}
+    return out
+
+
+def roofline_entry(d, pmc, elapsed, kernel):
+    """Roofline of one kernel group over the timed region.  Every launch is
+    bounded by max(flops / MFMA peak, algorithmic bytes / HBM peak); the group's
+    bound is the resource with the larger summed time.  achieved = algorithmic
+    work / measured kernel time (dispatch-stamped HIP events)."""
+    if not d or d["total_ms"] <= 0:
+        return None
+    sec = d["total_ms"] * 1e-3
+    hbm = d["t_hbm_ms"] >= d["t_mfma_ms"]
+    ach_gbs = d["bytes"] / sec / 1e9
+    ach_tf = d["flops"] / sec / 1e12
+    e = {"bound": "hbm" if hbm else "mfma",
+         "achieved": round(ach_gbs if hbm else ach_tf, 2),
+         "peak": PEAK_HBM_GBS if hbm else PEAK_BF16_TFLOPS,
+         "unit": "GB/s" if hbm else "TFLOP/s",
+         "frac": round((ach_gbs / PEAK_HBM_GBS) if hbm else (ach_tf / PEAK_BF16_TFLOPS), 4),
+         "traffic": pmc["bytes"] if pmc else None,
+         "kernel": kernel, "launches": d["launches"], "avg_us": round(d["avg_us"], 2),
+         "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
+         "roofline_time_frac": round(d["t_roof_ms"] / d["total_ms"], 4),
+         "share_of_step": round(d["total_ms"] / (elapsed * 1e3), 4)}
+    if d["flops"]:
+        e["flop_per_launch"] = round(d["flops"] / d["launches"])
+        e["mfma"] = {"achieved": round(ach_tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(ach_tf / PEAK_BF16_TFLOPS, 4)}
+    if pmc:
+        e["traffic_source"] = pmc["source"]
+    return e
 
 
 def parse_args():
@@ -197,33 +247,22 @@ def main():
     if rank == 0:
         images_total = world * batch * args.steps
         value = images_total / elapsed
-        roof = None
-        g = ksum.get("grouped_gemm")
-        if g and g["total_ms"] > 0:
-            ach = g["work"] / (g["total_ms"] * 1e-3) / 1e12
-            roof = {"bound": "mfma", "kernel": "grouped_gemm_kernel (all fwd/dgrad/wgrad variants)",
-                    "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                    "launches": g["launches"], "avg_us": round(g["avg_us"], 2),
-                    "flop_per_launch": round(g["work"] / g["launches"], 1),
-                    "share_of_step": round(g["total_ms"] / (elapsed * 1e3), 4)}
-        rd = None
-        dsp = ksum.get("dispatch")
-        if dsp and dsp["total_ms"] > 0:
-            ach = dsp["work"] / (dsp["total_ms"] * 1e-3) / 1e9
-            rd = {"bound": "hbm", "kernel": "permute_fwd/combine_fwd/combine_bwd", "achieved": round(ach, 1),
-                  "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
-                  "launches": dsp["launches"], "avg_us": round(dsp["avg_us"], 2),
-                  "bytes_per_launch": round(dsp["work"] / dsp["launches"], 1)}
+        pmc = load_pmc_traffic(args.workload)
+        roof = roofline_entry(ksum.get("grouped_gemm"), pmc.get("grouped_gemm"), elapsed,
+                              "grouped GEMM (gemm_v2_kernel: expert fwd, dgrad, wgrad)")
+        rd = roofline_entry(ksum.get("dispatch"), pmc.get("dispatch"), elapsed,
+                            "permute_fwd / combine_fwd / combine_bwd")
         kprof = {}
         for name, d in ksum.items():
             if d["total_ms"] <= 0:
                 continue
-            scale = 1e12 if d["unit"] == "flop" else 1e9
+            sec = d["total_ms"] * 1e-3
             kprof[name] = {"launches_per_step": round(d["launches"] / args.steps, 1), "avg_us": round(d["avg_us"], 2),
                            "ms_per_step": round(d["total_ms"] / args.steps, 3),
-                           "achieved": round(d["work"] / (d["total_ms"] * 1e-3) / scale, 1),
-                           "unit": "TFLOP/s" if d["unit"] == "flop" else "GB/s"}
+                           "GB_s": round(d["bytes"] / sec / 1e9, 1),
+                           "roofline_time_frac": round(d["t_roof_ms"] / d["total_ms"], 4)}
+            if d["flops"]:
+                kprof[name]["TFLOP_s"] = round(d["flops"] / sec / 1e12, 1)
         result = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),

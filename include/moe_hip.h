@@ -159,17 +159,20 @@ int rtdetr_msda_bwd(const void* value, const int32_t* shapes, const int32_t* sta
 
 /* Process-wide tuning knobs (not thread-safe; set before launching):
  *   "gemm_variant" 1 = register-staged double buffer, 2 = LDS-DMA ring (default)
- *   "gemm_stages"  3 (default) or 4 ring slots for variant 2
+ *   "gemm_stages"  2 (default), 3 or 4 ring slots for variant 2
  * Returns 0, or -1 for an unknown key/value. */
 int moe_set_tuning(const char* key, int value);
 
 /* Launch profiler (measurement only; no reference counterpart).
- * While enabled, every kernel launch of the library records a hipEvent pair on
- * its own stream plus its algorithmic work: flops for kind 0 (grouped GEMM,
- * 2 N K per routed row, the row count read back from offsets[G]); bytes for
- * kinds 1 (permute/combine row moves), 2 (router), 3 (route scan),
- * 4 (token backward), 5 (deformable attention).  Not thread-safe, not for
- * graph capture.  enable(0|1) also clears; get() waits for the record. */
+ * While enabled, every kernel launch of the library carries a hipEvent pair
+ * stamped by its own dispatch packet (hipExtLaunchKernel: kernel execution
+ * start/end, host gaps excluded) plus its algorithmic work: HBM bytes (every
+ * operand read once, every output written once) and flops (grouped GEMM:
+ * 2 N K per routed row; 0 for the other kinds), with the routed row count read
+ * back from the device offsets.  Kinds: 0 grouped GEMM, 1 permute/combine row
+ * moves, 2 router, 3 route scan, 4 token backward, 5 deformable attention.
+ * Not thread-safe, not for graph capture.  enable(0|1) also clears; get()
+ * waits for the record. */
 enum moe_prof_kind {
   MOE_PROF_GEMM = 0,
   MOE_PROF_ROWMOVE = 1,
@@ -180,7 +183,7 @@ enum moe_prof_kind {
 };
 int moe_profile_enable(int on);
 int moe_profile_count(void);
-int moe_profile_get(int i, int* kind, float* ms, double* work);
+int moe_profile_get(int i, int* kind, float* ms, double* flops, double* bytes);
 int moe_profile_clear(void);
 
 /* Thread-local message for the last non-zero return code. */

@@ -26,14 +26,14 @@ int check_launch(const char* what) {
 }
 
 // ---------------------------------------------------------------------------
-// launch profiler: a hipEvent pair recorded on the launch stream around every
-// kernel launch of the library while enabled (not thread-safe; profiling only)
+// launch profiler: while enabled, every kernel launch of the library carries a
+// hipEvent pair stamped by its dispatch (not thread-safe; profiling only)
 // ---------------------------------------------------------------------------
 namespace {
 struct Record {
   int kind;
   hipEvent_t start, stop;
-  double work_fixed, work_per_row;
+  double bytes_fixed, bytes_per_row, flops_per_row;
   int rows_slot;  // index into the pinned rows buffer, or -1
 };
 struct Profiler {
@@ -65,10 +65,11 @@ struct Profiler {
 Profiler g_prof;
 }  // namespace
 
-ProfScope::ProfScope(hipStream_t s, int kind, double work_fixed, const int32_t* dev_rows, double work_per_row)
+ProfScope::ProfScope(hipStream_t s, int kind, double bytes_fixed, const int32_t* dev_rows, double bytes_per_row,
+                     double flops_per_row)
     : stream_(s), active_(g_prof.on), idx_(-1) {
   if (!active_) return;
-  Record r{kind, g_prof.ev(), g_prof.ev(), work_fixed, work_per_row, -1};
+  Record r{kind, g_prof.ev(), g_prof.ev(), bytes_fixed, bytes_per_row, flops_per_row, -1};
   if (dev_rows != nullptr) {
     if (g_prof.rows_used >= g_prof.rows_cap) {
       const int cap = g_prof.rows_cap ? 2 * g_prof.rows_cap : 4096;
@@ -88,15 +89,16 @@ ProfScope::ProfScope(hipStream_t s, int kind, double work_fixed, const int32_t* 
       dev_rows_ = dev_rows;
     }
   }
-  (void)hipEventRecord(r.start, s);
   g_prof.recs.push_back(r);
   idx_ = (int)g_prof.recs.size() - 1;
 }
 
+hipEvent_t ProfScope::start_event() const { return g_prof.recs[idx_].start; }
+hipEvent_t ProfScope::stop_event() const { return g_prof.recs[idx_].stop; }
+
 ProfScope::~ProfScope() {
   if (!active_ || idx_ < 0) return;
   Record& r = g_prof.recs[idx_];
-  (void)hipEventRecord(r.stop, stream_);
   if (r.rows_slot >= 0)  // stream-ordered read of the device row count (after the kernel)
     (void)hipMemcpyAsync(g_prof.rows_host + r.rows_slot, dev_rows_, sizeof(int32_t), hipMemcpyDeviceToHost,
                          stream_);
@@ -116,7 +118,7 @@ extern "C" int moe_profile_enable(int on) {
 
 extern "C" int moe_profile_count(void) { return (int)moe::g_prof.recs.size(); }
 
-extern "C" int moe_profile_get(int i, int* kind, float* ms, double* work) {
+extern "C" int moe_profile_get(int i, int* kind, float* ms, double* flops, double* bytes) {
   if (i < 0 || i >= (int)moe::g_prof.recs.size()) return moe::fail("moe_profile_get: index out of range");
   auto& r = moe::g_prof.recs[i];
   if (hipEventSynchronize(r.stop) != hipSuccess) return moe::fail("moe_profile_get: event sync failed");
@@ -127,7 +129,8 @@ extern "C" int moe_profile_get(int i, int* kind, float* ms, double* work) {
   *kind = r.kind;
   *ms = t;
   const double rows = r.rows_slot >= 0 ? (double)moe::g_prof.rows_host[r.rows_slot] : 0.0;
-  *work = r.work_fixed + r.work_per_row * rows;
+  *flops = r.flops_per_row * rows;
+  *bytes = r.bytes_fixed + r.bytes_per_row * rows;
   return 0;
 }
 

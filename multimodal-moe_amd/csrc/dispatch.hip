@@ -151,7 +151,7 @@ extern "C" int moe_permute_fwd(const void* x, const int32_t* topk_idx,
   if (T <= 0) return 0;
   // bytes: x read once, idx/local_rank read, pos written, kept rows written
   ProfScope prof(stream, PROF_ROWMOVE, 2.0 * T * d + 12.0 * T * k, offsets + E, 2.0 * d);
-  hipLaunchKernelGGL(permute_fwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
+  MOE_LAUNCH(prof, permute_fwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
                      static_cast<const uint16_t*>(x), topk_idx, local_rank, rank_base,
                      offsets, T, d, E, k, cap, static_cast<uint16_t*>(xp), pos);
   return check_launch("moe_permute_fwd");
@@ -164,7 +164,7 @@ extern "C" int moe_combine_fwd(const void* yp, const int32_t* pos, const float* 
   if (T <= 0) return 0;
   // bytes: T*k expert rows + pos/w read, y written
   ProfScope prof(stream, PROF_ROWMOVE, 2.0 * T * d + 2.0 * T * k * d + 8.0 * T * k);
-  hipLaunchKernelGGL(combine_fwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
+  MOE_LAUNCH(prof, combine_fwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
                      static_cast<const uint16_t*>(yp), pos, topk_w, T, d, k,
                      static_cast<uint16_t*>(y));
   return check_launch("moe_combine_fwd");
@@ -178,7 +178,7 @@ extern "C" int moe_combine_bwd(const void* dy, const void* yp, const int32_t* po
   if (T <= 0) return 0;
   // bytes: dy + T*k expert rows + pos/w read, dyp rows + dw written
   ProfScope prof(stream, PROF_ROWMOVE, 2.0 * T * d + 4.0 * T * k * d + 12.0 * T * k);
-  hipLaunchKernelGGL(combine_bwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
+  MOE_LAUNCH(prof, combine_bwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
                      static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(yp), pos,
                      topk_w, T, d, k, static_cast<uint16_t*>(dyp), dw);
   return check_launch("moe_combine_bwd");

@@ -49,7 +49,7 @@ struct GemmParams {
 
 // runtime tuning knobs (moe_set_tuning)
 static int g_gemm_variant = 2;
-static int g_gemm_stages = 3;
+static int g_gemm_stages = 2;
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
@@ -116,24 +116,44 @@ struct Tile {
   // tile get consecutive slots on one XCD (they share the 64-128 KiB A panel)
   // and row tiles rotate over the XCDs.  WGRAD (G >= 8): every tile of group g
   // runs on XCD g % 8, so the group's activation rows stream through one L2.
-  __device__ __forceinline__ bool init(const GemmParams& p) {
+  // The group of a row tile is found wave-parallel: each lane loads one
+  // group's offsets (one memory round trip per 64 groups, not one per group),
+  // an inclusive lane scan of the tile counts and a ballot pick the group.
+  __device__ __forceinline__ bool init(const GemmParams& p, int lane) {
     const int L = blockIdx.x;
     const int xcd = L & 7, slot = L >> 3;
     if constexpr (MODE == MODE_ROWS) {
       const int ntn = p.N / BN;
       nt = slot % ntn;
-      int rem = (slot / ntn) * 8 + xcd;  // global row-tile index
-      g = 0;
-      for (; g < p.G; ++g) {
-        const int n_g = p.offsets[g + 1] - p.offsets[g];
-        const int t_g = (n_g + BM - 1) / BM;
-        if (rem < t_g) break;
-        rem -= t_g;
+      const int rem = (slot / ntn) * 8 + xcd;  // global row-tile index
+      int before = 0;                          // row tiles of the groups below chunk c0
+      g = -1;
+      for (int c0 = 0; c0 < p.G; c0 += 64) {
+        const int gi = c0 + lane;
+        int lo = 0, hi = 0;
+        if (gi < p.G) {
+          lo = p.offsets[gi];
+          hi = p.offsets[gi + 1];
+        }
+        const int tg = (hi - lo + BM - 1) / BM;
+        int incl = tg;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int v = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += v;
+        }
+        const unsigned long long hit = __ballot(before + incl > rem);
+        if (hit) {
+          const int src = __builtin_ctzll(hit);
+          g = c0 + src;
+          mt = rem - before - __shfl(incl - tg, src, 64);
+          row0 = __shfl(lo, src, 64) + mt * BM;
+          rows_g = __shfl(hi, src, 64) - row0;
+          break;
+        }
+        before += __shfl(incl, 63, 64);
       }
-      if (g >= p.G) return false;  // beyond the last tile (grid is an upper bound)
-      mt = rem;
-      row0 = p.offsets[g] + mt * BM;
-      rows_g = p.offsets[g + 1] - row0;
+      if (g < 0) return false;  // beyond the last tile (grid is an upper bound)
     } else {
       const int ntn = p.N / BN;
       const int tpg = (p.M / BM) * ntn;  // tiles per group
@@ -172,15 +192,42 @@ struct Tile {
 // ---------------------------------------------------------------------------
 // epilogue: lane holds C[m = .. + (lane&15)][n = .. + 4*(lane>>4) + r]
 // ---------------------------------------------------------------------------
+// Bias of this lane's output columns, loaded at kernel start so its latency
+// hides behind the main loop (ROWS mode, EPI_BIAS*).
+template <int BN, int MODE, int EPI>
+__device__ __forceinline__ void prefetch_bias(const GemmParams& p, int g, int n0, int lane, int wn,
+                                              float4 (&bpre)[BN / 32]) {
+  if constexpr (MODE == MODE_ROWS && (EPI == MOE_EPI_BIAS || EPI == MOE_EPI_BIAS_RELU)) {
+    const int ln = 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < BN / 32; ++j)
+      bpre[j] = *reinterpret_cast<const float4*>(p.bias + (size_t)g * p.N + n0 + wn * (BN / 2) + 16 * j + ln);
+  }
+}
+
 template <int BM, int BN, int MODE, int EPI, bool COLSUM>
 __device__ __forceinline__ void epilogue(const GemmParams& p, int g, int row0, int a_row_lim, int m0, int n0, int nt,
                                          f32x4 (&acc)[BM / 32][BN / 32], float (&csum)[BM / 32],
-                                         int lane, int wm, int wn) {
+                                         const float4 (&bpre)[BN / 32], int lane, int wm, int wn) {
   constexpr int TM = BM / 32, TN = BN / 32;
   const int lm = lane & 15;
   const int ln = 4 * (lane >> 4);
   if constexpr (MODE == MODE_ROWS) {
     uint16_t* C = static_cast<uint16_t*>(p.c);
+    // relu-mask operand: every load issued before the first use (rows past the
+    // group clamped to a valid one; their results are never stored)
+    uint2 hv[EPI == MOE_EPI_RELU_MASK ? TM : 1][EPI == MOE_EPI_RELU_MASK ? TN : 1];
+    if constexpr (EPI == MOE_EPI_RELU_MASK) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        int ml = wm * (BM / 2) + 16 * i + lm;
+        ml = ml < a_row_lim ? ml : a_row_lim - 1;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          hv[i][j] = *reinterpret_cast<const uint2*>(p.aux + ((size_t)row0 + ml) * p.ldc + n0 + wn * (BN / 2) +
+                                                     16 * j + ln);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int ml = wm * (BM / 2) + 16 * i + lm;
@@ -191,17 +238,16 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int g, int row0, i
         const int n = n0 + wn * (BN / 2) + 16 * j + ln;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if constexpr (EPI == MOE_EPI_BIAS || EPI == MOE_EPI_BIAS_RELU) {
-          const float4 bv = *reinterpret_cast<const float4*>(p.bias + (size_t)g * p.N + n);
-          v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+          v[0] += bpre[j].x; v[1] += bpre[j].y; v[2] += bpre[j].z; v[3] += bpre[j].w;
         }
         if constexpr (EPI == MOE_EPI_BIAS_RELU) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
         }
         if constexpr (EPI == MOE_EPI_RELU_MASK) {
-          const uint2 hv = *reinterpret_cast<const uint2*>(p.aux + row * p.ldc + n);
-          const uint16_t h[4] = {(uint16_t)(hv.x & 0xffff), (uint16_t)(hv.x >> 16),
-                                 (uint16_t)(hv.y & 0xffff), (uint16_t)(hv.y >> 16)};
+          const uint2 hw = hv[i][j];
+          const uint16_t h[4] = {(uint16_t)(hw.x & 0xffff), (uint16_t)(hw.x >> 16),
+                                 (uint16_t)(hw.y & 0xffff), (uint16_t)(hw.y >> 16)};
 #pragma unroll
           for (int r = 0; r < 4; ++r)  // bf16 > 0: sign clear and not +0
             if ((h[r] & 0x8000u) || h[r] == 0) v[r] = 0.f;
@@ -319,7 +365,9 @@ __global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   Tile<BM, BN, B_K, MODE> t;
-  if (!t.init(p)) return;
+  if (!t.init(p, lane)) return;
+  float4 bpre[TN];
+  prefetch_bias<BN, MODE, EPI>(p, t.g, t.n0, lane, wn, bpre);
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -359,7 +407,7 @@ __global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
     __syncthreads();
   }
   epilogue<BM, BN, MODE, EPI, COLSUM>(p, t.g, t.row0,
-                                      t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, lane, wm, wn);
+                                      t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, lane, wm, wn);
 }
 
 // ---------------------------------------------------------------------------
@@ -411,7 +459,9 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   Tile<BM, BN, B_K, MODE> t;
-  if (!t.init(p)) return;
+  if (!t.init(p, lane)) return;
+  float4 bpre[TN];
+  prefetch_bias<BN, MODE, EPI>(p, t.g, t.n0, lane, wn, bpre);
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -439,7 +489,9 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt has landed for this wave once at most min(S-2, nk-1-kt) newer tiles are pending
     const int newer = nk - 1 - kt;
-    if constexpr (S >= 4) {
+    if constexpr (S == 2) {
+      wait_vm<0>();  // tile kt+1 is issued after this wait
+    } else if constexpr (S >= 4) {
       if (newer >= 2) wait_vm<2 * GW>();
       else if (newer == 1) wait_vm<GW>();
       else wait_vm<0>();
@@ -466,7 +518,7 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
     compute_tile<BM, BN, A_K, B_K, COLSUM>(cur, cur + A_BYTES, acc, csum, lane, wm, wn);
   }
   epilogue<BM, BN, MODE, EPI, COLSUM>(p, t.g, t.row0,
-                                      t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, lane, wm, wn);
+                                      t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, lane, wm, wn);
 }
 
 // ---------------------------------------------------------------------------
@@ -485,22 +537,27 @@ static void allow_lds(size_t bytes) {
 }
 
 template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM>
-static void launch(const GemmParams& p, dim3 grid, hipStream_t s) {
+static void launch(const GemmParams& p, dim3 grid, hipStream_t s, const ProfScope& prof) {
   if (g_gemm_variant == 1) {
     constexpr size_t lds = 2 * (BM + BN) * 64 * 2;
     constexpr auto fn = gemm_v1_kernel<BM, BN, A_K, B_K, MODE, EPI, COLSUM>;
     allow_lds<fn>(lds);
-    hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, p);
+    MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
+  } else if (g_gemm_stages == 2) {
+    constexpr size_t lds = 2 * (BM + BN) * 64 * 2;
+    constexpr auto fn = gemm_v2_kernel<BM, BN, 2, A_K, B_K, MODE, EPI, COLSUM>;
+    allow_lds<fn>(lds);
+    MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
   } else if (g_gemm_stages >= 4) {
     constexpr size_t lds = 4 * (BM + BN) * 64 * 2;
     constexpr auto fn = gemm_v2_kernel<BM, BN, 4, A_K, B_K, MODE, EPI, COLSUM>;
     allow_lds<fn>(lds);
-    hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, p);
+    MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
   } else {
     constexpr size_t lds = 3 * (BM + BN) * 64 * 2;
     constexpr auto fn = gemm_v2_kernel<BM, BN, 3, A_K, B_K, MODE, EPI, COLSUM>;
     allow_lds<fn>(lds);
-    hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, p);
+    MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
   }
 }
 
@@ -511,7 +568,7 @@ using namespace moe;
 extern "C" int moe_set_tuning(const char* key, int value) {
   const std::string k = key ? key : "";
   if (k == "gemm_variant" && (value == 1 || value == 2)) { g_gemm_variant = value; return 0; }
-  if (k == "gemm_stages" && (value == 3 || value == 4)) { g_gemm_stages = value; return 0; }
+  if (k == "gemm_stages" && value >= 2 && value <= 4) { g_gemm_stages = value; return 0; }
   return fail("moe_set_tuning: unknown key or value");
 }
 
@@ -557,9 +614,12 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
   const int BMsel = big ? 128 : 64;
   const int mtiles = ((max_rows + BMsel - 1) / BMsel + G + 7) / 8 * 8;  // padded to the XCD count
   dim3 grid(mtiles * nt);
-  ProfScope prof(stream, PROF_GEMM, 0.0, offsets + G, 2.0 * N * K);  // flops: 2 N K per routed row
+  // algorithmic bytes: weights + bias once; per routed row A (K), C (N) and the relu-mask operand (N)
+  const bool has_bias = epilogue == MOE_EPI_BIAS || epilogue == MOE_EPI_BIAS_RELU;
+  ProfScope prof(stream, PROF_GEMM, 2.0 * G * N * K + (has_bias ? 4.0 * G * N : 0.0), offsets + G,
+                 2.0 * K + 2.0 * N + (epilogue == MOE_EPI_RELU_MASK ? 2.0 * N : 0.0), 2.0 * N * K);
 
-#define GG_ROWS(BM, BK_, EPI) launch<BM, 128, true, BK_, MODE_ROWS, EPI, false>(p, grid, stream)
+#define GG_ROWS(BM, BK_, EPI) launch<BM, 128, true, BK_, MODE_ROWS, EPI, false>(p, grid, stream, prof)
 #define GG_EPI(BM, BK_)                                                  \
   switch (epilogue) {                                                   \
     case MOE_EPI_NONE: GG_ROWS(BM, BK_, MOE_EPI_NONE); break;            \
@@ -601,15 +661,17 @@ extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, f
   const int ntn = N / 128;
   const bool big = M % 128 == 0 && (long long)(M / 128) * ntn * G >= 512;
   const int gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
-  ProfScope prof(stream, PROF_GEMM, 0.0, offsets + G, 2.0 * M * N);  // flops: 2 M N per routed row
+  // algorithmic bytes: fp32 C (+ colsum) once; per routed row one row of X (M) and of Y (N)
+  ProfScope prof(stream, PROF_GEMM, 4.0 * G * M * N + (colsum ? 4.0 * G * M : 0.0), offsets + G, 2.0 * (M + N),
+                 2.0 * M * N);
   if (big) {
     dim3 grid((M / 128) * ntn * gpad);
-    if (colsum) launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream);
-    else launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream);
+    if (colsum) launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream, prof);
+    else launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream, prof);
   } else {
     dim3 grid((M / 64) * ntn * gpad);
-    if (colsum) launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream);
-    else launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream);
+    if (colsum) launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream, prof);
+    else launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream, prof);
   }
   return check_launch("moe_grouped_gemm_wgrad");
 }

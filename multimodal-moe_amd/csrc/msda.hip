@@ -200,10 +200,10 @@ extern "C" int rtdetr_msda_fwd(const void* value, const int32_t* shapes, const i
   const double samples = (double)groups * L * P;
   ProfScope prof(stream, PROF_MSDA, samples * (8.0 * D + 12.0) + 2.0 * groups * D);
   if (D == 32)
-    hipLaunchKernelGGL(msda_fwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
+    MOE_LAUNCH(prof, msda_fwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
                        loc, attn, B, S, Q, H, L, P, o);
   else
-    hipLaunchKernelGGL(msda_fwd_kernel<32>, dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v, shapes, starts,
+    MOE_LAUNCH(prof, msda_fwd_kernel<32>, dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v, shapes, starts,
                        loc, attn, B, S, Q, H, L, P, o);
   return check_launch("rtdetr_msda_fwd");
 }
@@ -223,10 +223,10 @@ extern "C" int rtdetr_msda_bwd(const void* value, const int32_t* shapes, const i
   const double samples = (double)groups * L * P;
   ProfScope prof(stream, PROF_MSDA, samples * (8.0 * D + 16.0 * D + 24.0) + 2.0 * groups * D);
   if (D == 32)
-    hipLaunchKernelGGL(msda_bwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
+    MOE_LAUNCH(prof, msda_bwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
                        loc, attn, go, B, S, Q, H, L, P, grad_value, grad_loc, grad_attn);
   else
-    hipLaunchKernelGGL(msda_bwd_kernel<32>, dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v, shapes, starts,
+    MOE_LAUNCH(prof, msda_bwd_kernel<32>, dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v, shapes, starts,
                        loc, attn, go, B, S, Q, H, L, P, grad_value, grad_loc, grad_attn);
   return check_launch("rtdetr_msda_bwd");
 }

@@ -1,10 +1,14 @@
-// RAII launch profiler scope (see capi.hip): while profiling is enabled
-// (moe_profile_enable), records a hipEvent pair on `stream` around the kernel
-// launched inside the scope, plus the launch's algorithmic work
-// work_fixed + work_per_row * (*dev_rows) (dev_rows: a device int such as
-// offsets[G], copied back stream-ordered after the kernel).
+// RAII launch profiler scope (see capi.hip).  While profiling is enabled
+// (moe_profile_enable) the kernel launched through MOE_LAUNCH inside the scope
+// gets a start/stop hipEvent pair stamped by its own dispatch packet
+// (hipExtLaunchKernel: kernel execution time, no host gaps), and the scope
+// records the launch's algorithmic HBM bytes bytes_fixed + bytes_per_row * R and
+// flops flops_per_row * R, R = *dev_rows (a device int such as offsets[G],
+// copied back stream-ordered after the kernel; 0 without dev_rows).
+// Disabled: MOE_LAUNCH is a plain hipLaunchKernelGGL.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -14,9 +18,12 @@ enum ProfKind { PROF_GEMM = 0, PROF_ROWMOVE = 1, PROF_ROUTER = 2, PROF_SCAN = 3,
 
 class ProfScope {
  public:
-  ProfScope(hipStream_t s, int kind, double work_fixed, const int32_t* dev_rows = nullptr,
-            double work_per_row = 0.0);
+  ProfScope(hipStream_t s, int kind, double bytes_fixed, const int32_t* dev_rows = nullptr,
+            double bytes_per_row = 0.0, double flops_per_row = 0.0);
   ~ProfScope();
+  bool active() const { return active_ && idx_ >= 0; }
+  hipEvent_t start_event() const;
+  hipEvent_t stop_event() const;
   ProfScope(const ProfScope&) = delete;
   ProfScope& operator=(const ProfScope&) = delete;
 
@@ -28,3 +35,12 @@ class ProfScope {
 };
 
 }  // namespace moe
+
+#define MOE_LAUNCH(prof, kern, grid, block, shmem, stream, ...)                                          \
+  do {                                                                                                    \
+    if ((prof).active())                                                                                  \
+      hipExtLaunchKernelGGL(kern, grid, block, shmem, stream, (prof).start_event(), (prof).stop_event(), 0, \
+                            __VA_ARGS__);                                                                 \
+    else                                                                                                  \
+      hipLaunchKernelGGL(kern, grid, block, shmem, stream, __VA_ARGS__);                                  \
+  } while (0)

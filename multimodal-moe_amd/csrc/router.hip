@@ -404,7 +404,7 @@ extern "C" int moe_router_topk_fwd(const void* x, const float* wg, const float* 
                  2.0 * T * d + 4.0 * E * d + 12.0 * T * k + 4.0 * T * (E + 1) + 4.0 * nblk * (k * E + E + 1));
 #define LAUNCH_R(EM)                                                                       \
   allow_lds<router_topk_fwd_kernel<EM>>(shmem);                                             \
-  hipLaunchKernelGGL(router_topk_fwd_kernel<EM>, dim3(nblk), dim3(256), shmem, stream, xb, \
+  MOE_LAUNCH(prof, router_topk_fwd_kernel<EM>, dim3(nblk), dim3(256), shmem, stream, xb, \
                      wg, ctx_bias, ctx_img, tokens_per_image, T, d, E, k, normalize,       \
                      topk_idx, topk_w, probs, lse, local_rank, block_counts, aux_partials)
   switch (em) {
@@ -423,7 +423,7 @@ extern "C" int moe_route_scan(const int32_t* block_counts, int nblk, int k, int 
   if (E < 1 || E > 64 || k < 1 || k > 8) return fail("route_scan: need 1<=E<=64, 1<=k<=8");
   if (nblk < 0) return fail("route_scan: nblk < 0");
   ProfScope prof(stream, PROF_SCAN, 8.0 * nblk * k * E + 12.0 * E);
-  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, stream, block_counts, nblk, k,
+  MOE_LAUNCH(prof, route_scan_kernel, dim3(1), dim3(1024), 0, stream, block_counts, nblk, k,
                      E, cap, rank_base, hist, offsets);
   return check_launch("moe_route_scan");
 }
@@ -448,7 +448,7 @@ extern "C" int moe_token_bwd(const void* dxp, const int32_t* pos, const float* p
                  2.0 * T * k * d + 2.0 * T * d + 8.0 * T * E + 20.0 * T * k + 4.0 * T + 4.0 * E * d);
 #define LAUNCH_B(EM)                                                                          \
   allow_lds<token_bwd_kernel<EM>>(shmem);                                                   \
-  hipLaunchKernelGGL(token_bwd_kernel<EM>, dim3(grid), dim3(256), shmem, stream, dxpb, pos, \
+  MOE_LAUNCH(prof, token_bwd_kernel<EM>, dim3(grid), dim3(256), shmem, stream, dxpb, pos, \
                      probs, topk_idx, topk_w, dw, lse, dprob_bias, zc, wg, T, d, E, k,      \
                      normalize, dxb, dlogits)
   switch (em) {

@@ -23,28 +23,19 @@ from src.moe import _lib as L  # noqa: E402
 
 
 def timed(fn, reps):
-    """GPU time per call: `reps` calls captured in one hipGraph, replayed and
-    timed with events (no Python/ctypes host overhead in the measurement;
-    includes the ~1-2 us kernel-boundary cost per launch)."""
+    """Median kernel execution time (us) of `fn`'s launch over `reps` calls,
+    from the dispatch-stamped event pairs of libmoe_hip's profiler
+    (hipExtLaunchKernel): no host overhead or inter-launch gaps included."""
     fn()
     torch.cuda.synchronize()
-    stream = torch.cuda.Stream()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(stream):
-        fn()
-        torch.cuda.synchronize()
-        with torch.cuda.graph(graph, stream=stream):
-            for _ in range(reps):
-                fn()
-    graph.replay()
-    torch.cuda.synchronize()
-    s = torch.cuda.Event(enable_timing=True)
-    e = torch.cuda.Event(enable_timing=True)
-    s.record()
-    graph.replay()
-    e.record()
-    torch.cuda.synchronize()
-    return 1e3 * s.elapsed_time(e) / reps  # us
+    L.lib().moe_profile_enable(1)
+    try:
+        for _ in range(reps):
+            fn()
+        recs = L.profile_records()
+    finally:
+        L.lib().moe_profile_enable(0)
+    return 1e3 * statistics.median(r[1] for r in recs)
 
 
 def setup(T, E, k, d, F, seed=0):
@@ -105,7 +96,7 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="1,2")
-    ap.add_argument("--stages", default="3,4")
+    ap.add_argument("--stages", default="2,3,4")
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     L.lib()

@@ -40,7 +40,7 @@ SIGNATURES = {
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "moe_profile_enable": (_I, [_I]),
     "moe_profile_count": (_I, []),
-    "moe_profile_get": (_I, [_I, _P, _P, _P]),
+    "moe_profile_get": (_I, [_I, _P, _P, _P, _P]),
     "moe_profile_clear": (_I, []),
     "moe_last_error": (ctypes.c_char_p, []),
     "moe_version": (ctypes.c_char_p, []),
@@ -85,17 +85,18 @@ def lib() -> ctypes.CDLL:
 
 
 PROF_KINDS = {0: "grouped_gemm", 1: "dispatch", 2: "router", 3: "route_scan", 4: "token_bwd", 5: "msda"}
-PROF_UNITS = {0: "flop"}  # every other kind counts bytes
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E
 
 
 class KernelProfiler:
     """Per-launch kernel timing by the library's own profiler (moe_profile_*).
 
-    While enabled, libmoe_hip records a hipEvent pair on each launch's stream
-    directly around the kernel (no Python between the events) plus its
-    algorithmic work (flops for the grouped GEMMs with the row count read back
-    from the device offsets, bytes for the others; include/moe_hip.h).
-    ``harvest()`` adds the completed records to running totals per kind.
+    While enabled, libmoe_hip stamps each launch with a hipEvent pair from its
+    own dispatch packet (hipExtLaunchKernel: kernel execution only) and records
+    its algorithmic HBM bytes and flops (include/moe_hip.h).  ``harvest()``
+    adds the completed records to running totals per kind, including the
+    roofline time sum(max(flops / peak_flops, bytes / peak_bw)) of each launch.
     Not usable inside hipGraph capture.
     """
 
@@ -119,21 +120,22 @@ class KernelProfiler:
         """Consume the library's records into the totals (waits for them)."""
         if not self.enabled:
             return
-        kind, ms, work = ctypes.c_int(), ctypes.c_float(), ctypes.c_double()
-        n = lib().moe_profile_count()
-        for i in range(n):
-            _check(lib().moe_profile_get(i, ctypes.byref(kind), ctypes.byref(ms), ctypes.byref(work)),
-                   "moe_profile_get")
-            name = PROF_KINDS.get(kind.value, str(kind.value))
-            d = self.acc.setdefault(name, {"launches": 0, "total_ms": 0.0, "work": 0.0,
-                                           "unit": PROF_UNITS.get(kind.value, "byte")})
+        for kind, ms, flops, byts in profile_records():
+            name = PROF_KINDS.get(kind, str(kind))
+            d = self.acc.setdefault(name, {"launches": 0, "total_ms": 0.0, "flops": 0.0, "bytes": 0.0,
+                                           "t_mfma_ms": 0.0, "t_hbm_ms": 0.0, "t_roof_ms": 0.0})
+            t_f = flops / (PEAK_BF16_TFLOPS * 1e9)  # ms
+            t_b = byts / (PEAK_HBM_GBS * 1e6)       # ms
             d["launches"] += 1
-            d["total_ms"] += ms.value
-            d["work"] += work.value
-        lib().moe_profile_clear()
+            d["total_ms"] += ms
+            d["flops"] += flops
+            d["bytes"] += byts
+            d["t_mfma_ms"] += t_f
+            d["t_hbm_ms"] += t_b
+            d["t_roof_ms"] += max(t_f, t_b)
 
     def summary(self):
-        """{kind: dict(launches, total_ms, avg_us, work, unit)} of the harvested launches."""
+        """{kind: dict(launches, total_ms, avg_us, flops, bytes, t_*_ms)} of the harvested launches."""
         out = {k: dict(v) for k, v in self.acc.items()}
         for d in out.values():
             d["avg_us"] = 1e3 * d["total_ms"] / max(d["launches"], 1)
@@ -141,6 +143,20 @@ class KernelProfiler:
 
 
 TIMER = KernelProfiler()
+
+
+def profile_records(clear=True):
+    """[(kind, kernel ms, flops, bytes)] of the launches recorded since the
+    profiler was enabled or last cleared (waits for them)."""
+    kind, ms, flops, byts = ctypes.c_int(), ctypes.c_float(), ctypes.c_double(), ctypes.c_double()
+    out = []
+    for i in range(lib().moe_profile_count()):
+        _check(lib().moe_profile_get(i, ctypes.byref(kind), ctypes.byref(ms), ctypes.byref(flops),
+                                     ctypes.byref(byts)), "moe_profile_get")
+        out.append((kind.value, ms.value, flops.value, byts.value))
+    if clear:
+        lib().moe_profile_clear()
+    return out
 
 
 def _ptr(t: torch.Tensor | None) -> int | None:

@@ -87,7 +87,7 @@ def _int_tensor(rng, shape, lo=-3, hi=4):
     return rng.integers(lo, hi, size=shape).astype(np.float64)
 
 
-GEMM_CFGS = [(1, 3), (2, 3), (2, 4)]  # (gemm_variant, gemm_stages)
+GEMM_CFGS = [(1, 3), (2, 2), (2, 3), (2, 4)]  # (gemm_variant, gemm_stages)
 
 
 @pytest.fixture
@@ -99,7 +99,7 @@ def gemm_cfg(request, hip_lib):
     L.set_tuning("gemm_stages", s)
     yield request.param
     L.set_tuning("gemm_variant", 2)
-    L.set_tuning("gemm_stages", 3)
+    L.set_tuning("gemm_stages", 2)
 
 
 @pytest.mark.parametrize("gemm_cfg", GEMM_CFGS, indirect=True)
@@ -304,8 +304,10 @@ def test_library_profiler_records_gemm_work(hip_lib):
         L.TIMER.stop()
     s = L.TIMER.summary()
     g = s["grouped_gemm"]
-    assert g["launches"] == 2 and g["unit"] == "flop"
-    assert g["work"] == 2.0 * R * N * K + 2.0 * R * K * N
+    assert g["launches"] == 2
+    assert g["flops"] == 2.0 * R * N * K + 2.0 * R * K * N
+    # bytes: fwd = weights + R rows of A and C; wgrad = fp32 C + colsum + R rows of X and Y
+    assert g["bytes"] == (2.0 * G * N * K + R * (2 * K + 2 * N)) + (4.0 * G * K * N + 4.0 * G * K + R * 2 * (K + N))
     assert 0 < g["avg_us"] < 1e5
     assert lib_count_after_stop() == 0
 
