@@ -37,6 +37,9 @@ for p in (str(ROOT / "multimodal-moe_amd"), str(ROOT)):
     if p not in sys.path:
         sys.path.insert(0, p)
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+# MIOpen convolution search (torch.backends.cudnn.benchmark, --conv-search) in
+# its fast mode: find-db lookups + quick heuristics, seconds instead of minutes
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -114,6 +117,8 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample length")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip per-launch HIP events")
+    ap.add_argument("--conv-search", action=argparse.BooleanOptionalAction, default=True,
+                    help="let MIOpen benchmark convolution algorithms (torch.backends.cudnn.benchmark)")
     ap.add_argument("--graphs", action=argparse.BooleanOptionalAction, default=False,
                     help="capture the model forward/backward as hipGraphs (no per-kernel HIP-event timing: "
                          "ROCm 7.2 does not stamp timing events recorded inside a graph, "
@@ -193,6 +198,7 @@ def main():
     device = torch.device("cuda", local)
     wl = WORKLOADS[args.workload]
     spec = wl["spec"].format(N=world)
+    torch.backends.cudnn.benchmark = bool(args.conv_search)
     batch = args.batch or wl["batch"]
 
     from src.moe import _lib as L

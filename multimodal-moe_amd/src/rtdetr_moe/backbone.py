@@ -50,16 +50,28 @@ class ConvNormLayer(nn.Module):
         return self.act(self.norm(self.conv(x)))
 
 
+def avg_pool_2x2(x):
+    """AvgPool2d(2, 2, ceil_mode=True).  Even H and W (every RT-DETR input padded
+    to a multiple of 32) take a reshape-mean over the channels_last layout, whose
+    backward is one broadcast kernel (ROCm's NHWC avg_pool2d backward took
+    ~400 us per call at 1280x736, batch 8)."""
+    B, C, H, W = x.shape
+    if H % 2 or W % 2 or not x.is_contiguous(memory_format=torch.channels_last):
+        return F.avg_pool2d(x, 2, 2, 0, ceil_mode=True)
+    y = x.permute(0, 2, 3, 1).reshape(B, H // 2, 2, W // 2, 2, C).mean(dim=(2, 4))
+    return y.permute(0, 3, 1, 2)
+
+
 class _Shortcut(nn.Module):
     """ResNet-D shortcut: AvgPool(2) then 1x1 conv when downsampling."""
 
     def __init__(self, cin, cout, stride, frozen):
         super().__init__()
-        self.pool = nn.AvgPool2d(2, 2, 0, ceil_mode=True) if stride == 2 else nn.Identity()
+        self.down = stride == 2
         self.conv = ConvNormLayer(cin, cout, 1, 1, frozen=frozen)
 
     def forward(self, x):
-        return self.conv(self.pool(x))
+        return self.conv(avg_pool_2x2(x) if self.down else x)
 
 
 class BasicBlock(nn.Module):

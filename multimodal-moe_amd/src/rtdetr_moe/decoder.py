@@ -12,6 +12,7 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
+from .linear import TokenLinear
 from ..moe.config import MoEConfig
 from .encoder import make_ffn
 
@@ -108,7 +109,7 @@ class MSDeformableAttention(nn.Module):
         self.offset_scale = offset_scale
         self.sampling_offsets = nn.Linear(d, nhead * nlevels * npoints * 2)
         self.attention_weights = nn.Linear(d, nhead * nlevels * npoints)
-        self.value_proj = nn.Linear(d, d)
+        self.value_proj = TokenLinear(d, d)  # runs over all B*S memory tokens
         self.output_proj = nn.Linear(d, d)
         self._reset()
 
@@ -213,14 +214,22 @@ class RTDETRDecoder(nn.Module):
         memory = torch.cat([f.flatten(2).permute(0, 2, 1) for f in proj], 1).contiguous()  # [B, S, d]
         B = memory.shape[0]
         anchors, valid = self._anchors(shapes, memory.device, torch.float32)
-        out_mem = self.enc_output(valid.to(memory.dtype) * memory)
-        enc_logits = self.enc_score_head(out_mem)
-        enc_coord = self.enc_bbox_head(out_mem).float() + anchors
-        topk = torch.topk(enc_logits.detach().float().max(-1).values, self.num_queries, dim=1).indices
-        ref_unact = enc_coord.gather(1, topk[..., None].expand(-1, -1, 4))
+        mem_v = valid.to(memory.dtype) * memory
+        # Query selection.  Only the top-k rows of the encoder-output heads are
+        # used downstream (their logits/boxes and the detached decoder targets),
+        # so the heads run over all S tokens once without autograd, to rank
+        # them, and again with autograd on the B*Q selected rows only.  Same
+        # values and gradients as running the heads over all tokens, without
+        # the three [B*S, 256] weight-gradient GEMMs and activation storage.
+        with torch.no_grad():
+            enc_rank = self.enc_score_head(self.enc_output(mem_v)).float().max(-1).values
+        topk = torch.topk(enc_rank, self.num_queries, dim=1).indices
+        sel = self.enc_output(mem_v.gather(1, topk[..., None].expand(-1, -1, mem_v.shape[-1])))
+        enc_topk_logits = self.enc_score_head(sel)
+        ref_unact = self.enc_bbox_head(sel).float() + anchors.expand(B, -1, -1).gather(
+            1, topk[..., None].expand(-1, -1, 4))
         enc_topk_boxes = ref_unact.sigmoid()
-        enc_topk_logits = enc_logits.gather(1, topk[..., None].expand(-1, -1, enc_logits.shape[-1]))
-        tgt = out_mem.gather(1, topk[..., None].expand(-1, -1, out_mem.shape[-1])).detach()
+        tgt = sel.detach()
         ref_detach = ref_unact.detach().sigmoid()
         ref = ref_detach
         dec_logits, dec_boxes = [], []

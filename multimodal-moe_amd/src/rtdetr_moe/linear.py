@@ -1,0 +1,63 @@
+"""Linear layer for inputs with a very large row count (the decoder's value
+projection over all B*S encoder-memory tokens: 154,560 rows at 1280x736,
+batch 8).
+
+The weight gradient dW = dY^T X reduces over all rows.  As one GEMM with a
+256x256 output, hipBLASLt picks a tiling that puts only 16 workgroups on the
+chip (~380 us on MI355X); split into S row chunks as a batched GEMM
+(S independent [256, K/S] x [K/S, 256] products, then a fp32 sum over S) it
+fills the chip (~50 us, tools/mm_probe.py).  Forward and input gradient are
+the usual GEMMs.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+BIG_ROWS = 65536  # below this, the plain GEMM is already well shaped
+
+
+def chunked_wgrad(gy: torch.Tensor, x: torch.Tensor, target_chunk: int = 2560) -> torch.Tensor:
+    """sum_r gy[r, :]^T x[r, :] -> fp32 [m, n] as a batched GEMM over row chunks."""
+    K, m = gy.shape
+    n = x.shape[1]
+    S = max(1, min(256, K // target_chunk))
+    kc = K // S
+    head = S * kc
+    out = torch.bmm(gy[:head].view(S, kc, m).transpose(1, 2), x[:head].view(S, kc, n)).sum(0, dtype=torch.float32)
+    if head < K:
+        out += gy[head:].t().float().mm(x[head:].float())
+    return out
+
+
+class _TokenLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, dtype):
+        xc, wc = x.to(dtype), weight.to(dtype)
+        bc = bias.to(dtype) if bias is not None else None
+        ctx.save_for_backward(xc, wc)
+        ctx.has_bias = bias is not None
+        return F.linear(xc, wc, bc)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xc, wc = ctx.saved_tensors
+        g2 = gy.reshape(-1, gy.shape[-1]).to(wc.dtype).contiguous()
+        x2 = xc.reshape(-1, xc.shape[-1])
+        gx = g2.mm(wc).view(xc.shape) if ctx.needs_input_grad[0] else None
+        gw = chunked_wgrad(g2, x2) if ctx.needs_input_grad[1] else None
+        gb = g2.sum(0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return gx, gw, gb, None
+
+
+class TokenLinear(nn.Linear):
+    """nn.Linear (same parameters and state dict) whose backward splits the
+    weight-gradient reduction over row chunks when the input has many rows."""
+
+    def forward(self, x):
+        if x.is_cuda and x.numel() // x.shape[-1] >= BIG_ROWS:
+            dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+            with torch.autocast("cuda", enabled=False):
+                return _TokenLinear.apply(x, self.weight, self.bias, dtype)
+        return super().forward(x)
