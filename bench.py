@@ -117,6 +117,8 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample length")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip per-launch HIP events")
+    ap.add_argument("--precision", choices=["bf16", "amp"], default="bf16",
+                    help="bf16: bf16 GEMM/conv weights + fp32 master weights; amp: fp32 weights under bf16 autocast")
     ap.add_argument("--conv-search", action=argparse.BooleanOptionalAction, default=True,
                     help="let MIOpen benchmark convolution algorithms (torch.backends.cudnn.benchmark)")
     ap.add_argument("--graphs", action=argparse.BooleanOptionalAction, default=False,
@@ -224,6 +226,7 @@ def main():
     timing = not args.no_kernel_timing and not args.graphs
     ddp_local = local if (world > 1 and not args.graphs) else None
     step = TrainStep(model, SetCriterion(num_classes=1), images, ctx, graphs=args.graphs, world=world,
+                     precision=args.precision,
                      ddp_local=ddp_local)
 
     for _ in range(args.warmup):
@@ -276,6 +279,7 @@ def main():
             "data": "synthetic (ZOD-shaped batches resident in HBM, random-init weights)",
             "config": {"workload": wl["desc"], "arch": spec, "global_batch": world * batch,
                        "execution": "hipGraph fwd/bwd" if args.graphs else "eager",
+                       "precision": "bf16 weights + fp32 master" if args.precision == "bf16" else "bf16 autocast",
                        "img": f"{args.img_w}x{args.img_h} (padded to {data.pad_w}x{data.pad_h})",
                        "parallelism": f"dp{world}" if "ep" not in spec else f"dp{world}+ep{world}"},
             "roofline": roof, "roofline_dispatch": rd, "kernel_profile": kprof,

@@ -34,23 +34,29 @@ struct Record {
   int kind;
   hipEvent_t start, stop;
   double bytes_fixed, bytes_per_row, flops_per_row;
-  int rows_slot;  // index into the pinned rows buffer, or -1
+  int rows_slot;  // index into the device rows buffer, or -1
 };
+constexpr int kRowSlots = 1 << 16;
 struct Profiler {
   bool on = false;
   std::vector<Record> recs;
-  std::vector<hipEvent_t> pool;  // recycled events
-  int32_t* rows_host = nullptr;  // pinned, one int per record that reads device rows
-  int rows_cap = 0, rows_used = 0;
+  std::vector<hipEvent_t> pool;   // free events (created at enable, recycled at clear)
+  int32_t* rows_dev = nullptr;    // kRowSlots device ints the kernels write their row counts to
+  std::vector<int32_t> rows_host;
+  int rows_used = 0;
+  bool rows_fetched = false;
 
-  hipEvent_t ev() {
-    if (!pool.empty()) {
-      hipEvent_t e = pool.back();
-      pool.pop_back();
-      return e;
+  void reserve(int n) {
+    while ((int)pool.size() < n) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) break;
+      pool.push_back(e);
     }
-    hipEvent_t e;
-    (void)hipEventCreate(&e);
+  }
+  hipEvent_t ev() {
+    if (pool.empty()) reserve(256);
+    hipEvent_t e = pool.back();
+    pool.pop_back();
     return e;
   }
   void clear() {
@@ -60,48 +66,29 @@ struct Profiler {
     }
     recs.clear();
     rows_used = 0;
+    rows_fetched = false;
   }
 };
 Profiler g_prof;
 }  // namespace
 
-ProfScope::ProfScope(hipStream_t s, int kind, double bytes_fixed, const int32_t* dev_rows, double bytes_per_row,
+ProfScope::ProfScope(hipStream_t s, int kind, double bytes_fixed, bool per_row, double bytes_per_row,
                      double flops_per_row)
-    : stream_(s), active_(g_prof.on), idx_(-1) {
+    : active_(g_prof.on), idx_(-1) {
+  (void)s;
   if (!active_) return;
   Record r{kind, g_prof.ev(), g_prof.ev(), bytes_fixed, bytes_per_row, flops_per_row, -1};
-  if (dev_rows != nullptr) {
-    if (g_prof.rows_used >= g_prof.rows_cap) {
-      const int cap = g_prof.rows_cap ? 2 * g_prof.rows_cap : 4096;
-      int32_t* nb = nullptr;
-      if (hipHostMalloc(reinterpret_cast<void**>(&nb), cap * sizeof(int32_t)) == hipSuccess) {
-        if (g_prof.rows_host) {
-          (void)hipDeviceSynchronize();
-          std::copy(g_prof.rows_host, g_prof.rows_host + g_prof.rows_used, nb);
-          (void)hipHostFree(g_prof.rows_host);
-        }
-        g_prof.rows_host = nb;
-        g_prof.rows_cap = cap;
-      }
-    }
-    if (g_prof.rows_used < g_prof.rows_cap) {
-      r.rows_slot = g_prof.rows_used++;
-      dev_rows_ = dev_rows;
-    }
-  }
+  if (per_row && g_prof.rows_dev != nullptr && g_prof.rows_used < kRowSlots) r.rows_slot = g_prof.rows_used++;
   g_prof.recs.push_back(r);
   idx_ = (int)g_prof.recs.size() - 1;
 }
 
 hipEvent_t ProfScope::start_event() const { return g_prof.recs[idx_].start; }
 hipEvent_t ProfScope::stop_event() const { return g_prof.recs[idx_].stop; }
-
-ProfScope::~ProfScope() {
-  if (!active_ || idx_ < 0) return;
-  Record& r = g_prof.recs[idx_];
-  if (r.rows_slot >= 0)  // stream-ordered read of the device row count (after the kernel)
-    (void)hipMemcpyAsync(g_prof.rows_host + r.rows_slot, dev_rows_, sizeof(int32_t), hipMemcpyDeviceToHost,
-                         stream_);
+int32_t* ProfScope::rows_slot() const {
+  if (!active()) return nullptr;
+  const int slot = g_prof.recs[idx_].rows_slot;
+  return slot >= 0 ? g_prof.rows_dev + slot : nullptr;
 }
 
 }  // namespace moe
@@ -111,8 +98,17 @@ extern "C" const char* moe_last_error(void) { return moe::g_last_error.c_str(); 
 extern "C" const char* moe_version(void) { return "moe_hip 0.2.0 gfx950"; }
 
 extern "C" int moe_profile_enable(int on) {
-  moe::g_prof.clear();
-  moe::g_prof.on = on != 0;
+  auto& P = moe::g_prof;
+  P.clear();
+  P.on = on != 0;
+  if (P.on) {
+    P.reserve(8192);  // no event creation inside a profiled region of up to 4096 launches
+    if (P.rows_dev == nullptr &&
+        hipMalloc(reinterpret_cast<void**>(&P.rows_dev), moe::kRowSlots * sizeof(int32_t)) != hipSuccess) {
+      P.rows_dev = nullptr;
+      return moe::fail("moe_profile_enable: cannot allocate the row-count slots");
+    }
+  }
   return 0;
 }
 
@@ -120,15 +116,23 @@ extern "C" int moe_profile_count(void) { return (int)moe::g_prof.recs.size(); }
 
 extern "C" int moe_profile_get(int i, int* kind, float* ms, double* flops, double* bytes) {
   if (i < 0 || i >= (int)moe::g_prof.recs.size()) return moe::fail("moe_profile_get: index out of range");
-  auto& r = moe::g_prof.recs[i];
+  auto& P = moe::g_prof;
+  auto& r = P.recs[i];
   if (hipEventSynchronize(r.stop) != hipSuccess) return moe::fail("moe_profile_get: event sync failed");
-  if (r.rows_slot >= 0) (void)hipDeviceSynchronize();  // the rows copy trails the stop event
+  if (r.rows_slot >= 0 && !P.rows_fetched) {  // one copy of every slot written so far
+    P.rows_host.resize(P.rows_used);
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(P.rows_host.data(), P.rows_dev, P.rows_used * sizeof(int32_t), hipMemcpyDeviceToHost) !=
+            hipSuccess)
+      return moe::fail("moe_profile_get: row-count copy failed");
+    P.rows_fetched = true;
+  }
   float t = 0.f;
   const hipError_t e = hipEventElapsedTime(&t, r.start, r.stop);
   if (e != hipSuccess) return moe::fail(std::string("moe_profile_get: ") + hipGetErrorString(e));
   *kind = r.kind;
   *ms = t;
-  const double rows = r.rows_slot >= 0 ? (double)moe::g_prof.rows_host[r.rows_slot] : 0.0;
+  const double rows = r.rows_slot >= 0 ? (double)P.rows_host[r.rows_slot] : 0.0;
   *flops = r.flops_per_row * rows;
   *bytes = r.bytes_fixed + r.bytes_per_row * rows;
   return 0;

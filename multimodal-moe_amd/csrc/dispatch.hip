@@ -26,8 +26,9 @@ __global__ __launch_bounds__(256) void permute_fwd_kernel(
     const uint16_t* __restrict__ x, const int32_t* __restrict__ topk_idx,
     const int32_t* __restrict__ local_rank, const int32_t* __restrict__ rank_base,
     const int32_t* __restrict__ offsets, int T, int d, int E, int k, int cap,
-    uint16_t* __restrict__ xp, int32_t* __restrict__ pos) {
+    uint16_t* __restrict__ xp, int32_t* __restrict__ pos, int32_t* __restrict__ prof_rows) {
   const int tid = threadIdx.x;
+  if (prof_rows != nullptr && blockIdx.x == 0 && tid == 0) *prof_rows = offsets[E];
   const int sub = tid & 15;
   const int nchunk = d >> 7;
   for (int tb = blockIdx.x * 16; tb < T; tb += gridDim.x * 16) {
@@ -150,10 +151,10 @@ extern "C" int moe_permute_fwd(const void* x, const int32_t* topk_idx,
   if (E < 1 || E > 64 || k < 1 || k > 8) return fail("permute: need 1<=E<=64, 1<=k<=8");
   if (T <= 0) return 0;
   // bytes: x read once, idx/local_rank read, pos written, kept rows written
-  ProfScope prof(stream, PROF_ROWMOVE, 2.0 * T * d + 12.0 * T * k, offsets + E, 2.0 * d);
+  ProfScope prof(stream, PROF_ROWMOVE, 2.0 * T * d + 12.0 * T * k, true, 2.0 * d);
   MOE_LAUNCH(prof, permute_fwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
                      static_cast<const uint16_t*>(x), topk_idx, local_rank, rank_base,
-                     offsets, T, d, E, k, cap, static_cast<uint16_t*>(xp), pos);
+                     offsets, T, d, E, k, cap, static_cast<uint16_t*>(xp), pos, prof.rows_slot());
   return check_launch("moe_permute_fwd");
 }
 

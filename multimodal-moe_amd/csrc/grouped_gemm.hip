@@ -41,6 +41,7 @@ struct GemmParams {
   const float* bias;
   const uint16_t* aux;
   float* colsum;
+  int32_t* prof_rows;  // profiler slot for offsets[G] (written by block 0), or nullptr
   long long stride_b;  // elements between groups' B (ROWS mode)
   long long stride_c;  // elements between groups' C (WGRAD mode)
   int lda, ldb, ldc;
@@ -364,6 +365,7 @@ __global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
   constexpr int TM = BM / 32, TN = BN / 32;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  if (p.prof_rows != nullptr && blockIdx.x == 0 && tid == 0) *p.prof_rows = p.offsets[p.G];
   Tile<BM, BN, B_K, MODE> t;
   if (!t.init(p, lane)) return;
   float4 bpre[TN];
@@ -458,6 +460,7 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
+  if (p.prof_rows != nullptr && blockIdx.x == 0 && tid == 0) *p.prof_rows = p.offsets[p.G];
   Tile<BM, BN, B_K, MODE> t;
   if (!t.init(p, lane)) return;
   float4 bpre[TN];
@@ -616,8 +619,9 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
   dim3 grid(mtiles * nt);
   // algorithmic bytes: weights + bias once; per routed row A (K), C (N) and the relu-mask operand (N)
   const bool has_bias = epilogue == MOE_EPI_BIAS || epilogue == MOE_EPI_BIAS_RELU;
-  ProfScope prof(stream, PROF_GEMM, 2.0 * G * N * K + (has_bias ? 4.0 * G * N : 0.0), offsets + G,
+  ProfScope prof(stream, PROF_GEMM, 2.0 * G * N * K + (has_bias ? 4.0 * G * N : 0.0), true,
                  2.0 * K + 2.0 * N + (epilogue == MOE_EPI_RELU_MASK ? 2.0 * N : 0.0), 2.0 * N * K);
+  p.prof_rows = prof.rows_slot();
 
 #define GG_ROWS(BM, BK_, EPI) launch<BM, 128, true, BK_, MODE_ROWS, EPI, false>(p, grid, stream, prof)
 #define GG_EPI(BM, BK_)                                                  \
@@ -662,8 +666,9 @@ extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, f
   const bool big = M % 128 == 0 && (long long)(M / 128) * ntn * G >= 512;
   const int gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
   // algorithmic bytes: fp32 C (+ colsum) once; per routed row one row of X (M) and of Y (N)
-  ProfScope prof(stream, PROF_GEMM, 4.0 * G * M * N + (colsum ? 4.0 * G * M : 0.0), offsets + G, 2.0 * (M + N),
+  ProfScope prof(stream, PROF_GEMM, 4.0 * G * M * N + (colsum ? 4.0 * G * M : 0.0), true, 2.0 * (M + N),
                  2.0 * M * N);
+  p.prof_rows = prof.rows_slot();
   if (big) {
     dim3 grid((M / 128) * ntn * gpad);
     if (colsum) launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream, prof);

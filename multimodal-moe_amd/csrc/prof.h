@@ -3,9 +3,11 @@
 // gets a start/stop hipEvent pair stamped by its own dispatch packet
 // (hipExtLaunchKernel: kernel execution time, no host gaps), and the scope
 // records the launch's algorithmic HBM bytes bytes_fixed + bytes_per_row * R and
-// flops flops_per_row * R, R = *dev_rows (a device int such as offsets[G],
-// copied back stream-ordered after the kernel; 0 without dev_rows).
-// Disabled: MOE_LAUNCH is a plain hipLaunchKernelGGL.
+// flops flops_per_row * R, where R (the routed row count, known only on the
+// device) is written by the kernel itself into rows_slot() -- a device int of
+// the profiler -- so profiling adds no copies or launches.  Events come from a
+// pool created when profiling is enabled.  Disabled: MOE_LAUNCH is a plain
+// hipLaunchKernelGGL and rows_slot() is nullptr.
 #pragma once
 
 #include <hip/hip_ext.h>
@@ -18,20 +20,19 @@ enum ProfKind { PROF_GEMM = 0, PROF_ROWMOVE = 1, PROF_ROUTER = 2, PROF_SCAN = 3,
 
 class ProfScope {
  public:
-  ProfScope(hipStream_t s, int kind, double bytes_fixed, const int32_t* dev_rows = nullptr,
-            double bytes_per_row = 0.0, double flops_per_row = 0.0);
-  ~ProfScope();
+  ProfScope(hipStream_t s, int kind, double bytes_fixed, bool per_row = false, double bytes_per_row = 0.0,
+            double flops_per_row = 0.0);
+  ~ProfScope() = default;
   bool active() const { return active_ && idx_ >= 0; }
   hipEvent_t start_event() const;
   hipEvent_t stop_event() const;
+  int32_t* rows_slot() const;  // device int the kernel sets to its row count, or nullptr
   ProfScope(const ProfScope&) = delete;
   ProfScope& operator=(const ProfScope&) = delete;
 
  private:
-  hipStream_t stream_;
   bool active_;
   int idx_;
-  const int32_t* dev_rows_ = nullptr;
 };
 
 }  // namespace moe

@@ -49,24 +49,74 @@ class FlatOutputs(nn.Module):
         return out, flat[-1]
 
 
+def gemm_params(model: nn.Module):
+    """Parameters that are GEMM / convolution operands: weights and biases of
+    Linear, Conv2d and MultiheadAttention layers and the MoE expert weights.
+    These are held in bf16 (TrainStep precision "bf16"); norms, the MoE router
+    and everything else stay fp32."""
+    from ..moe.layer import MoEFFN
+
+    out, seen = [], set()
+    for mod in model.modules():
+        if isinstance(mod, (nn.Linear, nn.Conv2d)):
+            ps = [mod.weight, mod.bias]
+        elif isinstance(mod, nn.MultiheadAttention):
+            ps = [mod.in_proj_weight, mod.in_proj_bias]
+        elif isinstance(mod, MoEFFN):
+            ps = [mod.w1, mod.b1, mod.w2, mod.b2]
+        else:
+            continue
+        for p in ps:
+            if p is not None and id(p) not in seen:
+                seen.add(id(p))
+                out.append(p)
+    return out
+
+
 class TrainStep:
+    """precision (GPU):
+      "bf16" (default) -- GEMM/conv operands (gemm_params) held in bf16, fp32
+             master copies in the optimizer, no autocast: no per-layer weight
+             casts in the forward nor grad casts in the backward (about 1,700
+             cast ops per C2 step under autocast, most of the host time of an
+             eager step); after backward the bf16 grads are copied into the
+             masters' fp32 grads (multi-tensor copy), AdamW updates the
+             masters, and the masters are copied back into the bf16 weights;
+      "amp"  -- fp32 parameters under bf16 autocast.
+    On CPU the model runs in fp32."""
+
     def __init__(self, model: RTDETRMoE, criterion, images, ctx, *, lr=1e-4, lr_backbone=1e-5,
-                 weight_decay=1e-4, clip_norm=0.1, graphs=True, ddp_local=None, world=1):
+                 weight_decay=1e-4, clip_norm=0.1, graphs=True, ddp_local=None, world=1, precision="bf16"):
         self.model = model
         self.criterion = criterion
         self.clip_norm = clip_norm
         self.world = world
         self.graphs = graphs
-        self.params = [p for p in model.parameters() if p.requires_grad]
-        bb = [p for n, p in model.named_parameters() if n.startswith("backbone.") and p.requires_grad]
-        rest = [p for n, p in model.named_parameters() if not n.startswith("backbone.") and p.requires_grad]
+        self.precision = precision if images.is_cuda else "fp32"
+        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        self.params = [p for _, p in named]
+        self.lowp, self.master = [], []
+        opt_of = {id(p): p for p in self.params}  # model param -> tensor the optimizer updates
+        if self.precision == "bf16":
+            for p in gemm_params(model):
+                p.data = p.data.to(torch.bfloat16)
+                if p.requires_grad:
+                    m = p.detach().float().clone()
+                    m.grad = torch.zeros_like(m)
+                    self.lowp.append(p)
+                    self.master.append(m)
+                    opt_of[id(p)] = m
+        bb = [opt_of[id(p)] for n, p in named if n.startswith("backbone.")]
+        rest = [opt_of[id(p)] for n, p in named if not n.startswith("backbone.")]
+        self.opt_params = bb + rest
         fused = images.is_cuda
         self.opt = torch.optim.AdamW([{"params": bb, "lr": lr_backbone}, {"params": rest, "lr": lr}], lr=lr,
                                      weight_decay=weight_decay, fused=fused)
         self.flat = FlatOutputs(model)
         self.dp_params = [p for p in self.params if not getattr(p, "expert_parallel", False)]
+        images = self._cast_in(images)
         if graphs:
-            with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False, enabled=self.precision == "amp"):
                 self.fn = torch.cuda.make_graphed_callables(self.flat, (images, ctx), num_warmup_iters=3,
                                                             allow_unused_input=True)
             self.ddp = None
@@ -78,6 +128,20 @@ class TrainStep:
         else:
             self.fn = self.flat
             self.ddp = None
+
+    def _cast_in(self, images):
+        return images.to(torch.bfloat16) if self.precision == "bf16" else images
+
+    def _grads_to_master(self):
+        src, dst = [], []
+        for p, m in zip(self.lowp, self.master):
+            if p.grad is None:
+                m.grad.zero_()
+            else:
+                src.append(p.grad)
+                dst.append(m.grad)
+        if src:
+            torch._foreach_copy_(dst, src)
 
     def _allreduce_grads(self):
         grads = [p.grad for p in self.dp_params if p.grad is not None]
@@ -93,17 +157,23 @@ class TrainStep:
             off += n
 
     def __call__(self, images, ctx, targets, num_boxes):
-        self.opt.zero_grad(set_to_none=True)
-        with torch.autocast(images.device.type, dtype=torch.bfloat16, enabled=images.is_cuda,
+        for p in self.params:
+            p.grad = None
+        with torch.autocast(images.device.type, dtype=torch.bfloat16, enabled=self.precision == "amp",
                             cache_enabled=not self.graphs):
-            flat = self.fn(images, ctx)
+            flat = self.fn(self._cast_in(images), ctx)
         out, aux = FlatOutputs.unflatten(flat)
         losses = self.criterion(out, targets, num_boxes)
         loss = sum(losses.values()) + aux
         loss.backward()
         if self.graphs and self.world > 1:
             self._allreduce_grads()
+        if self.lowp:
+            self._grads_to_master()
         if self.clip_norm > 0:
-            torch.nn.utils.clip_grad_norm_(self.params, self.clip_norm, foreach=True)
+            torch.nn.utils.clip_grad_norm_(self.opt_params, self.clip_norm, foreach=True)
         self.opt.step()
+        if self.lowp:
+            with torch.no_grad():
+                torch._foreach_copy_(self.lowp, self.master)
         return loss.detach()
