@@ -119,6 +119,8 @@ def parse_args():
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--precision", choices=["bf16", "amp"], default="bf16",
                     help="bf16: bf16 GEMM/conv weights + fp32 master weights; amp: fp32 weights under bf16 autocast")
+    ap.add_argument("--phase-timing", action="store_true",
+                    help="report per-phase GPU/host ms (forward, criterion, backward, optimizer)")
     ap.add_argument("--conv-search", action=argparse.BooleanOptionalAction, default=True,
                     help="let MIOpen benchmark convolution algorithms (torch.backends.cudnn.benchmark)")
     ap.add_argument("--graphs", action=argparse.BooleanOptionalAction, default=False,
@@ -246,6 +248,13 @@ def main():
     if timing:
         L.TIMER.harvest()  # the K steps' launch records, read after the timed region
         L.TIMER.stop()
+    phases = None
+    if args.phase_timing:  # extra steps after the timed region
+        step.phases = []
+        for _ in range(3):
+            step(images, ctx, targets, num_boxes)
+        phases = step.phase_summary()
+        step.phases = None
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -283,6 +292,7 @@ def main():
                        "img": f"{args.img_w}x{args.img_h} (padded to {data.pad_w}x{data.pad_h})",
                        "parallelism": f"dp{world}" if "ep" not in spec else f"dp{world}+ep{world}"},
             "roofline": roof, "roofline_dispatch": rd, "kernel_profile": kprof,
+            **({"phases_gpu_host_ms": phases} if phases else {}),
         }
     if world > 1:
         dist.barrier()

@@ -1,19 +1,25 @@
 """One RT-DETR-MoE training step, optionally with the model's forward and
-backward captured as hipGraphs (torch.cuda.make_graphed_callables).
+backward captured as hipGraphs.
 
-Why graphs: a step launches ~6,000 kernels (MIOpen convolutions + BatchNorm,
-~80 layers of small element-wise ops, 13 MoE launches x 7 layers, loss
-terms); launched eagerly from Python the GPU idles ~40 % of the step waiting
-for the host.  Captured, the model's forward and backward are one replay each.
-What stays eager: the Hungarian matching (host linear_sum_assignment, one
-device->host copy of all cost matrices), the batched set criterion, the
-gradient all-reduce (one flat RCCL all_reduce over xGMI when world > 1),
-gradient clipping and the fused AdamW update.
+Why graphs: the model's forward + backward launch ~4,000 kernels (MIOpen
+convolutions + BatchNorm, element-wise ops, 13 MoE launches x 7 layers);
+issued eagerly from Python and the autograd engine, the host takes longer to
+enqueue the backward than the GPU takes to run it.  Captured (GraphedModel),
+the forward and the backward are one hipGraph replay each.  The backward graph
+computes torch.autograd.grad of the forward outputs w.r.t. every trainable
+parameter into static gradient buffers that the optimizer reads directly (no
+per-parameter AccumulateGrad copies).  What stays eager: the Hungarian
+matching (host linear_sum_assignment, one device->host copy of all cost
+matrices), the batched set criterion, the gradient all-reduce (one flat RCCL
+all_reduce over xGMI when world > 1), gradient clipping and the fused AdamW
+update.
 
 The captured forward keeps the MoE aux losses as an explicit graph output so
 their gradients reach the router through the captured backward.
 """
 from __future__ import annotations
+
+import time
 
 import torch
 import torch.distributed as dist
@@ -49,16 +55,90 @@ class FlatOutputs(nn.Module):
         return out, flat[-1]
 
 
+class _ReplayFn(torch.autograd.Function):
+    """Forward = replay of the captured forward graph; backward = copy the
+    incoming output gradients into the static buffers and replay the captured
+    backward graph (parameter grads land in the runner's static buffers)."""
+
+    @staticmethod
+    def forward(ctx, runner, anchor):
+        runner.g_fwd.replay()
+        ctx.runner = runner
+        return tuple(o.detach() for o in runner.static_out)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        r = ctx.runner
+        for buf, g in zip(r.static_gout, grads):
+            if g is None:
+                buf.zero_()
+            else:
+                buf.copy_(g)
+        r.g_bwd.replay()
+        return None, None
+
+
+class GraphedModel:
+    """Capture ``fn(images, ctx) -> tuple of tensors`` forward and backward as
+    two hipGraphs (see the module docstring).  After ``loss.backward()`` the
+    parameter gradients are in ``static_grads`` (one per ``params`` entry)."""
+
+    def __init__(self, fn, params, images, ctx, warmup=3, autocast=False):
+        self.fn = fn
+        self.params = params
+        self.autocast = autocast
+        self.static_images = images.clone()
+        self.static_ctx = ctx.clone()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up: convolution search, library attributes, allocator
+            for _ in range(warmup):
+                out = self._run()
+                grads = torch.autograd.grad([o for o in out if o.requires_grad],
+                                            params, [torch.ones_like(o) for o in out if o.requires_grad],
+                                            allow_unused=True)
+                del out, grads
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.pool = torch.cuda.graph_pool_handle()
+        self.g_fwd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_fwd, pool=self.pool):
+            out = self._run()
+        self.static_out = out
+        self.diff = [i for i, o in enumerate(out) if o.requires_grad]
+        self.static_gout = [torch.zeros_like(o) for o in out]
+        self.g_bwd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_bwd, pool=self.pool):
+            grads = torch.autograd.grad([out[i] for i in self.diff], params,
+                                        [self.static_gout[i] for i in self.diff], allow_unused=True)
+        self.static_grads = [g if g is not None else torch.zeros_like(p) for g, p in zip(grads, params)]
+        self.anchor = torch.zeros((), device=images.device, requires_grad=True)
+        torch.cuda.synchronize()
+
+    def _run(self):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.autocast, cache_enabled=False):
+            return self.fn(self.static_images, self.static_ctx)
+
+    def __call__(self, images, ctx):
+        if images.data_ptr() != self.static_images.data_ptr():
+            self.static_images.copy_(images)
+        if ctx.data_ptr() != self.static_ctx.data_ptr():
+            self.static_ctx.copy_(ctx)
+        return _ReplayFn.apply(self, self.anchor)
+
+
 def gemm_params(model: nn.Module):
     """Parameters that are GEMM / convolution operands: weights and biases of
-    Linear, Conv2d and MultiheadAttention layers and the MoE expert weights.
-    These are held in bf16 (TrainStep precision "bf16"); norms, the MoE router
-    and everything else stay fp32."""
+    Linear, Conv2d and MultiheadAttention layers and the MoE expert weights,
+    plus LayerNorm affines (the HIP layer_norm kernel wants them in the input
+    dtype).  These are held in bf16 (TrainStep precision "bf16"); BatchNorm
+    (mixed bf16-input / fp32-affine kernels), the MoE router and everything
+    else stay fp32."""
     from ..moe.layer import MoEFFN
 
     out, seen = [], set()
     for mod in model.modules():
-        if isinstance(mod, (nn.Linear, nn.Conv2d)):
+        if isinstance(mod, (nn.Linear, nn.Conv2d, nn.LayerNorm)):  # layer_norm on HIP needs weight dtype == input
             ps = [mod.weight, mod.bias]
         elif isinstance(mod, nn.MultiheadAttention):
             ps = [mod.in_proj_weight, mod.in_proj_bias]
@@ -90,6 +170,7 @@ class TrainStep:
         self.model = model
         self.criterion = criterion
         self.clip_norm = clip_norm
+        self.phases = None  # list to enable per-phase event marks (phase_summary)
         self.world = world
         self.graphs = graphs
         self.precision = precision if images.is_cuda else "fp32"
@@ -115,11 +196,14 @@ class TrainStep:
         self.flat = FlatOutputs(model)
         self.dp_params = [p for p in self.params if not getattr(p, "expert_parallel", False)]
         images = self._cast_in(images)
+        self.runner = None
         if graphs:
-            with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False, enabled=self.precision == "amp"):
-                self.fn = torch.cuda.make_graphed_callables(self.flat, (images, ctx), num_warmup_iters=3,
-                                                            allow_unused_input=True)
+            self.runner = GraphedModel(self.flat, self.params, images, ctx, autocast=self.precision == "amp")
+            self.fn = self.runner
             self.ddp = None
+            # the optimizer reads the static gradient buffers of the backward graph
+            for p, g in zip(self.params, self.runner.static_grads):
+                p.grad = g
         elif world > 1:
             from .engine import wrap_ddp
 
@@ -156,16 +240,26 @@ class TrainStep:
             g.copy_(flat[off:off + n].view_as(g))
             off += n
 
+    def _mark(self, name):
+        if self.phases is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.phases.append((name, e, time.perf_counter()))
+
     def __call__(self, images, ctx, targets, num_boxes):
-        for p in self.params:
-            p.grad = None
-        with torch.autocast(images.device.type, dtype=torch.bfloat16, enabled=self.precision == "amp",
-                            cache_enabled=not self.graphs):
+        self._mark("start")
+        if self.runner is None:
+            for p in self.params:
+                p.grad = None
+        with torch.autocast(images.device.type, dtype=torch.bfloat16, enabled=self.precision == "amp"):
             flat = self.fn(self._cast_in(images), ctx)
+        self._mark("forward")
         out, aux = FlatOutputs.unflatten(flat)
         losses = self.criterion(out, targets, num_boxes)
         loss = sum(losses.values()) + aux
+        self._mark("criterion")
         loss.backward()
+        self._mark("backward")
         if self.graphs and self.world > 1:
             self._allreduce_grads()
         if self.lowp:
@@ -176,4 +270,21 @@ class TrainStep:
         if self.lowp:
             with torch.no_grad():
                 torch._foreach_copy_(self.lowp, self.master)
+        self._mark("optimizer")
         return loss.detach()
+
+    def phase_summary(self):
+        """{phase: (gpu ms, host ms)} averaged over the marked steps (syncs)."""
+        torch.cuda.synchronize()
+        acc, n = {}, 0
+        ph = self.phases or []
+        for i in range(1, len(ph)):
+            name, e, t = ph[i]
+            if name == "start":
+                n += 1
+                continue
+            pe, pt = ph[i - 1][1], ph[i - 1][2]
+            g, h = acc.get(name, (0.0, 0.0))
+            acc[name] = (g + pe.elapsed_time(e), h + 1e3 * (t - pt))
+        n = max(n + 1, 1)
+        return {k: (round(g / n, 3), round(h / n, 3)) for k, (g, h) in acc.items()}
