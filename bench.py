@@ -123,10 +123,13 @@ def parse_args():
                     help="report per-phase GPU/host ms (forward, criterion, backward, optimizer)")
     ap.add_argument("--conv-search", action=argparse.BooleanOptionalAction, default=True,
                     help="let MIOpen benchmark convolution algorithms (torch.backends.cudnn.benchmark)")
-    ap.add_argument("--graphs", action=argparse.BooleanOptionalAction, default=False,
-                    help="capture the model forward/backward as hipGraphs (no per-kernel HIP-event timing: "
-                         "ROCm 7.2 does not stamp timing events recorded inside a graph, "
-                         "tools/graph_event_probe.py)")
+    ap.add_argument("--graphs", action=argparse.BooleanOptionalAction, default=True,
+                    help="capture the model forward/backward as hipGraphs (default; not with expert parallelism). "
+                         "ROCm 7.2 does not stamp timing events inside a graph (tools/graph_event_probe.py), so "
+                         "with graphs the per-kernel roofline comes from --profile-steps eager steps run right "
+                         "after the timed region")
+    ap.add_argument("--profile-steps", type=int, default=3,
+                    help="graph mode: eager steps after the timed region that carry the kernel events")
     return ap.parse_args()
 
 
@@ -224,16 +227,17 @@ def main():
         dist.all_reduce(nb)
     num_boxes = max(1.0, float(nb.item()) / world)
 
-    # library-side HIP-event pairs around each MoE/MSDA launch (not capturable in hipGraphs)
-    timing = not args.no_kernel_timing and not args.graphs
-    ddp_local = local if (world > 1 and not args.graphs) else None
-    step = TrainStep(model, SetCriterion(num_classes=1), images, ctx, graphs=args.graphs, world=world,
-                     precision=args.precision,
-                     ddp_local=ddp_local)
+    graphs = args.graphs and "ep" not in spec  # the EP all-to-all sizes its buffers on the host
+    # library-side kernel events around each MoE/MSDA launch: inside the timed
+    # region when eager; in eager steps right after it when graphed
+    timing = not args.no_kernel_timing
+    ddp_local = local if (world > 1 and not graphs) else None
+    step = TrainStep(model, SetCriterion(num_classes=1), images, ctx, graphs=graphs, world=world,
+                     precision=args.precision, ddp_local=ddp_local)
 
     for _ in range(args.warmup):
         step(images, ctx, targets, num_boxes)
-    if timing:
+    if timing and not graphs:
         L.TIMER.start()
     if world > 1:
         dist.barrier()
@@ -245,9 +249,20 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if timing:
+    prof_steps = args.steps
+    if timing and not graphs:
         L.TIMER.harvest()  # the K steps' launch records, read after the timed region
         L.TIMER.stop()
+    elif timing:
+        step.use_eager()
+        step(images, ctx, targets, num_boxes)  # untimed: first eager step allocates
+        torch.cuda.synchronize()
+        L.TIMER.start()
+        for _ in range(args.profile_steps):
+            step(images, ctx, targets, num_boxes)
+        L.TIMER.harvest()
+        L.TIMER.stop()
+        prof_steps = args.profile_steps
     phases = None
     if args.phase_timing:  # extra steps after the timed region
         step.phases = []
@@ -266,17 +281,18 @@ def main():
         images_total = world * batch * args.steps
         value = images_total / elapsed
         pmc = load_pmc_traffic(args.workload)
-        roof = roofline_entry(ksum.get("grouped_gemm"), pmc.get("grouped_gemm"), elapsed,
+        prof_elapsed = elapsed * prof_steps / args.steps  # share_of_step: per-step kernel time / step time
+        roof = roofline_entry(ksum.get("grouped_gemm"), pmc.get("grouped_gemm"), prof_elapsed,
                               "grouped GEMM (gemm_v2_kernel: expert fwd, dgrad, wgrad)")
-        rd = roofline_entry(ksum.get("dispatch"), pmc.get("dispatch"), elapsed,
+        rd = roofline_entry(ksum.get("dispatch"), pmc.get("dispatch"), prof_elapsed,
                             "permute_fwd / combine_fwd / combine_bwd")
         kprof = {}
         for name, d in ksum.items():
             if d["total_ms"] <= 0:
                 continue
             sec = d["total_ms"] * 1e-3
-            kprof[name] = {"launches_per_step": round(d["launches"] / args.steps, 1), "avg_us": round(d["avg_us"], 2),
-                           "ms_per_step": round(d["total_ms"] / args.steps, 3),
+            kprof[name] = {"launches_per_step": round(d["launches"] / prof_steps, 1), "avg_us": round(d["avg_us"], 2),
+                           "ms_per_step": round(d["total_ms"] / prof_steps, 3),
                            "GB_s": round(d["bytes"] / sec / 1e9, 1),
                            "roofline_time_frac": round(d["t_roof_ms"] / d["total_ms"], 4)}
             if d["flops"]:
@@ -287,11 +303,15 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (ZOD-shaped batches resident in HBM, random-init weights)",
             "config": {"workload": wl["desc"], "arch": spec, "global_batch": world * batch,
-                       "execution": "hipGraph fwd/bwd" if args.graphs else "eager",
+                       "execution": "hipGraph fwd/bwd" if graphs else "eager",
                        "precision": "bf16 weights + fp32 master" if args.precision == "bf16" else "bf16 autocast",
                        "img": f"{args.img_w}x{args.img_h} (padded to {data.pad_w}x{data.pad_h})",
                        "parallelism": f"dp{world}" if "ep" not in spec else f"dp{world}+ep{world}"},
             "roofline": roof, "roofline_dispatch": rd, "kernel_profile": kprof,
+            "kernel_timing": None if not timing else (
+                f"libmoe_hip dispatch-stamped events over the {args.steps} timed steps" if not graphs else
+                f"libmoe_hip dispatch-stamped events over {args.profile_steps} eager steps right after the "
+                f"timed region (same shapes; the timed steps replay hipGraphs, which carry no timing events)"),
             **({"phases_gpu_host_ms": phases} if phases else {}),
         }
     if world > 1:

@@ -227,18 +227,38 @@ class TrainStep:
         if src:
             torch._foreach_copy_(dst, src)
 
+    def use_eager(self):
+        """Leave graph mode (bench.py's kernel-profiling steps): later steps run
+        the model eagerly; parameter grads go back to autograd allocation."""
+        if self.runner is not None:
+            self.runner = None
+            self.fn = self.flat
+            self.graphs = False
+            self._flat_grads = None
+            for p in self.params:
+                p.grad = None
+
     def _allreduce_grads(self):
-        grads = [p.grad for p in self.dp_params if p.grad is not None]
-        if not grads:
-            return
-        flat = torch.cat([g.reshape(-1) for g in grads])
-        dist.all_reduce(flat)
-        flat.div_(self.world)
-        off = 0
-        for g in grads:
-            n = g.numel()
-            g.copy_(flat[off:off + n].view_as(g))
-            off += n
+        """Data-parallel mean of the static gradient buffers (graph mode, world >
+        1): one flat buffer per dtype, gathered and scattered by multi-tensor
+        copies, one RCCL all_reduce each."""
+        if getattr(self, "_flat_grads", None) is None:
+            groups = {}
+            for p in self.dp_params:
+                groups.setdefault(p.grad.dtype, []).append(p.grad)
+            self._flat_grads = []
+            for dt, gs in groups.items():
+                flat = torch.empty(sum(g.numel() for g in gs), dtype=dt, device=gs[0].device)
+                views, off = [], 0
+                for g in gs:
+                    views.append(flat[off:off + g.numel()].view_as(g))
+                    off += g.numel()
+                self._flat_grads.append((flat, views, gs))
+        for flat, views, gs in self._flat_grads:
+            torch._foreach_copy_(views, gs)
+            dist.all_reduce(flat)
+            flat.div_(self.world)
+            torch._foreach_copy_(gs, views)
 
     def _mark(self, name):
         if self.phases is not None:
