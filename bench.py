@@ -249,6 +249,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    phases = None
+    if args.phase_timing:  # extra steps after the timed region, same execution mode
+        step.phases = []
+        for _ in range(3):
+            step(images, ctx, targets, num_boxes)
+        phases = step.phase_summary()
+        step.phases = None
     prof_steps = args.steps
     if timing and not graphs:
         L.TIMER.harvest()  # the K steps' launch records, read after the timed region
@@ -263,13 +270,6 @@ def main():
         L.TIMER.harvest()
         L.TIMER.stop()
         prof_steps = args.profile_steps
-    phases = None
-    if args.phase_timing:  # extra steps after the timed region
-        step.phases = []
-        for _ in range(3):
-            step(images, ctx, targets, num_boxes)
-        phases = step.phase_summary()
-        step.phases = None
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)

@@ -46,11 +46,13 @@ struct GemmParams {
   long long stride_c;  // elements between groups' C (WGRAD mode)
   int lda, ldb, ldc;
   int G, M, N, K;
+  int dbg;  // measurement only (moe_set_tuning "gemm_debug"): 1 = no C stores, 2 = no main loop
 };
 
 // runtime tuning knobs (moe_set_tuning)
 static int g_gemm_variant = 2;
 static int g_gemm_stages = 2;
+static int g_gemm_debug = 0;
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
@@ -256,7 +258,7 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int g, int row0, i
         uint2 o;
         o.x = pack2bf(v[0], v[1]);
         o.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(C + row * p.ldc + n) = o;
+        if (!(p.dbg & 1)) *reinterpret_cast<uint2*>(C + row * p.ldc + n) = o;
       }
     }
   } else {
@@ -267,9 +269,113 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int g, int row0, i
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * (BN / 2) + 16 * j + ln;
-        *reinterpret_cast<float4*>(C + (size_t)m * p.ldc + n) =
+        if (!(p.dbg & 1)) *reinterpret_cast<float4*>(C + (size_t)m * p.ldc + n) =
             make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
       }
+    }
+    if constexpr (COLSUM) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        float s = csum[i];
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        csum[i] = s;
+      }
+      if (nt == 0 && wn == 0 && (lane >> 4) == 0) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = m0 + wm * (BM / 2) + 16 * i + lm;
+          p.colsum[(size_t)g * p.M + m] = csum[i];
+        }
+      }
+    }
+  }
+}
+
+// Epilogue through LDS (v2): each wave writes its accumulators (after bias /
+// ReLU) into a row-major [BM][BN] image over the drained stage buffers, then
+// the block stores whole rows with 16-B-per-lane global stores (full 128-B
+// lines; the register-direct path issues 8-B pieces, which the store path
+// handles at half the rate).  The relu-mask operand is read the same way.
+// Images: 16-B chunk c of row r at c ^ (r % chunks_per_row).
+template <int BM, int BN, int MODE, int EPI, bool COLSUM>
+__device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row0, int a_row_lim, int m0, int n0,
+                                             int nt, f32x4 (&acc)[BM / 32][BN / 32], float (&csum)[BM / 32],
+                                             const float4 (&bpre)[BN / 32], char* smem, int tid, int lane, int wm,
+                                             int wn) {
+  constexpr int TM = BM / 32, TN = BN / 32;
+  const int lm = lane & 15;
+  const int ln = 4 * (lane >> 4);
+  __syncthreads();  // every wave is done with the stage buffers
+  if constexpr (MODE == MODE_ROWS) {
+    constexpr int CPR = BN / 8;  // 16-B chunks per bf16 row
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wm * (BM / 2) + 16 * i + lm;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nl = wn * (BN / 2) + 16 * j + ln;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (EPI == MOE_EPI_BIAS || EPI == MOE_EPI_BIAS_RELU) {
+          v[0] += bpre[j].x; v[1] += bpre[j].y; v[2] += bpre[j].z; v[3] += bpre[j].w;
+        }
+        if constexpr (EPI == MOE_EPI_BIAS_RELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        uint2 o;
+        o.x = pack2bf(v[0], v[1]);
+        o.y = pack2bf(v[2], v[3]);
+        const int off = ml * (BN * 2) + (((nl >> 3) ^ (ml & (CPR - 1))) << 4) + (nl & 7) * 2;
+        *reinterpret_cast<uint2*>(smem + off) = o;
+      }
+    }
+    __syncthreads();
+    uint16_t* C = static_cast<uint16_t*>(p.c);
+    constexpr int RPP = 256 / CPR;  // rows per pass
+    const int c = tid % CPR;
+#pragma unroll
+    for (int r0 = 0; r0 < BM; r0 += RPP) {
+      const int r = r0 + tid / CPR;
+      if (r >= a_row_lim) continue;
+      uint4 v = *reinterpret_cast<const uint4*>(smem + r * (BN * 2) + ((c ^ (r & (CPR - 1))) << 4));
+      const size_t gofs = ((size_t)row0 + r) * p.ldc + n0 + c * 8;
+      if constexpr (EPI == MOE_EPI_RELU_MASK) {  // keep where the forward activation is > 0
+        const uint4 h = *reinterpret_cast<const uint4*>(p.aux + gofs);
+        uint32_t hw[4] = {h.x, h.y, h.z, h.w};
+        uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t lo = hw[q] & 0xffffu, hi = hw[q] >> 16;
+          const uint32_t keep_lo = ((lo & 0x8000u) || lo == 0) ? 0u : 0xffffu;
+          const uint32_t keep_hi = ((hi & 0x8000u) || hi == 0) ? 0u : 0xffff0000u;
+          vw[q] &= keep_lo | keep_hi;
+        }
+        v = make_uint4(vw[0], vw[1], vw[2], vw[3]);
+      }
+      if (!(p.dbg & 1)) *reinterpret_cast<uint4*>(C + gofs) = v;
+    }
+  } else {
+    constexpr int CPR = BN / 4;  // 16-B chunks per fp32 row
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wm * (BM / 2) + 16 * i + lm;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nl = wn * (BN / 2) + 16 * j + ln;
+        const int off = ml * (BN * 4) + (((nl >> 2) ^ (ml & (CPR - 1))) << 4);
+        *reinterpret_cast<float4*>(smem + off) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    __syncthreads();
+    float* C = static_cast<float*>(p.c) + (size_t)g * p.stride_c;
+    constexpr int RPP = 256 / CPR;
+    const int c = tid % CPR;
+#pragma unroll 4
+    for (int r0 = 0; r0 < BM; r0 += RPP) {
+      const int r = r0 + tid / CPR;
+      const float4 v = *reinterpret_cast<const float4*>(smem + r * (BN * 4) + ((c ^ (r & (CPR - 1))) << 4));
+      if (!(p.dbg & 1)) *reinterpret_cast<float4*>(C + (size_t)(m0 + r) * p.ldc + n0 + c * 4) = v;
     }
     if constexpr (COLSUM) {
 #pragma unroll
@@ -393,7 +499,7 @@ __global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
     lb.store(smem + A_BYTES, tid);
   }
   __syncthreads();
-  for (int kt = 0; kt < t.nk; ++kt) {
+  for (int kt = 0; kt < ((p.dbg & 2) ? 0 : t.nk); ++kt) {
     char* cur = smem + (kt & 1) * BUF;
     const bool more = kt + 1 < t.nk;
     if (more) {
@@ -475,7 +581,7 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
 #pragma unroll
   for (int i = 0; i < TM; ++i) csum[i] = 0.f;
 
-  const int nk = t.nk;
+  const int nk = (p.dbg & 2) ? 0 : t.nk;
   auto issue = [&](int kt) {
     char* buf = smem + (kt % S) * BUF;
     const int klim = MODE == MODE_ROWS ? 64 : t.rows_g - kt * 64;
@@ -520,8 +626,9 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
     if (kt + S - 1 < nk) issue(kt + S - 1);  // refills the slot read in iteration kt-1
     compute_tile<BM, BN, A_K, B_K, COLSUM>(cur, cur + A_BYTES, acc, csum, lane, wm, wn);
   }
-  epilogue<BM, BN, MODE, EPI, COLSUM>(p, t.g, t.row0,
-                                      t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, lane, wm, wn);
+  static_assert(S * (BM + BN) * 64 * 2 >= BM * BN * (MODE == MODE_ROWS ? 2 : 4), "epilogue image exceeds LDS");
+  epilogue_lds<BM, BN, MODE, EPI, COLSUM>(p, t.g, t.row0, t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, smem,
+                                          tid, lane, wm, wn);
 }
 
 // ---------------------------------------------------------------------------
@@ -572,6 +679,7 @@ extern "C" int moe_set_tuning(const char* key, int value) {
   const std::string k = key ? key : "";
   if (k == "gemm_variant" && (value == 1 || value == 2)) { g_gemm_variant = value; return 0; }
   if (k == "gemm_stages" && value >= 2 && value <= 4) { g_gemm_stages = value; return 0; }
+  if (k == "gemm_debug" && value >= 0 && value <= 3) { g_gemm_debug = value; return 0; }
   return fail("moe_set_tuning: unknown key or value");
 }
 
@@ -593,6 +701,7 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
   if (max_rows == 0) return 0;
 
   GemmParams p{};
+  p.dbg = g_gemm_debug;
   p.a = static_cast<const uint16_t*>(a);
   p.b = static_cast<const uint16_t*>(b);
   p.c = c;
@@ -649,6 +758,7 @@ extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, f
   if (M <= 0 || N <= 0 || M % 64 != 0 || N % 128 != 0)
     return fail("grouped_gemm_wgrad: need M % 64 == 0 and N % 128 == 0");
   GemmParams p{};
+  p.dbg = g_gemm_debug;
   p.a = static_cast<const uint16_t*>(x);
   p.b = static_cast<const uint16_t*>(y);
   p.c = c;

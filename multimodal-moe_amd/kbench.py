@@ -98,26 +98,31 @@ def main():
     ap.add_argument("--variants", default="1,2")
     ap.add_argument("--stages", default="2,3,4")
     ap.add_argument("--only", default="")
+    ap.add_argument("--debug", default="0", help="comma list of gemm_debug modes (1 no C stores, 2 no main loop)")
     a = ap.parse_args()
     L.lib()
-    configs = [(v, s) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
+    configs = [(v, s, dbg) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
+               for dbg in map(int, a.debug.split(","))
                if not (v == 1 and s != int(a.stages.split(",")[0]))]
     shapes = {"enc": setup(8 * 920, 8, 2, 256, 1024), "dec": setup(8 * 300, 8, 2, 256, 1024, seed=1)}
     res = {}
     for _ in range(a.rounds):
-        for (v, s) in configs:
+        for (v, s, dbg) in configs:
             L.set_tuning("gemm_variant", v)
             L.set_tuning("gemm_stages", s)
+            L.set_tuning("gemm_debug", dbg)
             for sname, c in shapes.items():
                 for name, fn, flops, byts in kernels(c):
                     if a.only and a.only not in name:
                         continue
-                    if not name.startswith("gemm") and (v, s) != configs[0]:
+                    if not name.startswith("gemm") and (v, s, dbg) != configs[0]:
                         continue
-                    res.setdefault((name, sname, v, s, flops, byts), []).append(timed(fn, a.reps))
-    for (name, sname, v, s, flops, byts), ts in res.items():
+                    res.setdefault((name, sname, v, s, dbg, flops, byts), []).append(timed(fn, a.reps))
+    L.set_tuning("gemm_debug", 0)
+    for (name, sname, v, s, dbg, flops, byts), ts in res.items():
         us = statistics.median(ts)
-        d = {"kernel": name, "shape": sname, "variant": v, "stages": s, "us": round(us, 2), "min_us": round(min(ts), 2)}
+        d = {"kernel": name, "shape": sname, "variant": v, "stages": s, "debug": dbg, "us": round(us, 2),
+             "min_us": round(min(ts), 2)}
         if flops:
             d["tflops"] = round(flops / us / 1e6, 1)
             d["frac_bf16_peak"] = round(flops / us / 1e6 / 2500.0, 4)
