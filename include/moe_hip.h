@@ -157,9 +157,13 @@ int rtdetr_msda_bwd(const void* value, const int32_t* shapes, const int32_t* sta
                     int Q, int H, int D, int L, int P, float* grad_value, float* grad_loc,
                     float* grad_attn, hipStream_t stream);
 
-/* Process-wide tuning knobs (not thread-safe; set before launching):
- *   "gemm_variant" 1 = register-staged double buffer, 2 = LDS-DMA ring (default)
- *   "gemm_stages"  2 (default), 3 or 4 ring slots for variant 2
+/* Process-wide tuning overrides (not thread-safe; set before launching).  By
+ * default (0) every launch picks its own kernel variant, ring depth and tile
+ * height from its shape; these force one (kernel benchmarks and tests):
+ *   "gemm_variant" 0 auto, 1 register-staged double buffer, 2 LDS-DMA ring
+ *   "gemm_stages"  0 auto, 2..4 ring slots for variant 2
+ *   "rows_bm", "wgrad_bm"  0 auto, 64 or 128 row-tile height
+ *   "gemm_debug"   0; 1 = skip C stores, 2 = skip the main loop (time attribution only)
  * Returns 0, or -1 for an unknown key/value. */
 int moe_set_tuning(const char* key, int value);
 

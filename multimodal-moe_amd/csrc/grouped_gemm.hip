@@ -50,9 +50,12 @@ struct GemmParams {
 };
 
 // runtime tuning knobs (moe_set_tuning)
-static int g_gemm_variant = 2;
-static int g_gemm_stages = 2;
+// runtime tuning overrides (moe_set_tuning); 0 = the per-shape choice below
+static int g_gemm_variant = 0;
+static int g_gemm_stages = 0;
 static int g_gemm_debug = 0;
+static int g_rows_bm = 0;   // 0 = by tile count, else 64 or 128
+static int g_wgrad_bm = 0;  // 0 = by tile count, else 64 or 128
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
@@ -647,18 +650,18 @@ static void allow_lds(size_t bytes) {
 }
 
 template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM>
-static void launch(const GemmParams& p, dim3 grid, hipStream_t s, const ProfScope& prof) {
-  if (g_gemm_variant == 1) {
+static void launch(const GemmParams& p, dim3 grid, hipStream_t s, const ProfScope& prof, int variant, int stages) {
+  if (variant == 1) {
     constexpr size_t lds = 2 * (BM + BN) * 64 * 2;
     constexpr auto fn = gemm_v1_kernel<BM, BN, A_K, B_K, MODE, EPI, COLSUM>;
     allow_lds<fn>(lds);
     MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
-  } else if (g_gemm_stages == 2) {
+  } else if (stages == 2) {
     constexpr size_t lds = 2 * (BM + BN) * 64 * 2;
     constexpr auto fn = gemm_v2_kernel<BM, BN, 2, A_K, B_K, MODE, EPI, COLSUM>;
     allow_lds<fn>(lds);
     MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
-  } else if (g_gemm_stages >= 4) {
+  } else if (stages >= 4) {
     constexpr size_t lds = 4 * (BM + BN) * 64 * 2;
     constexpr auto fn = gemm_v2_kernel<BM, BN, 4, A_K, B_K, MODE, EPI, COLSUM>;
     allow_lds<fn>(lds);
@@ -677,9 +680,11 @@ using namespace moe;
 
 extern "C" int moe_set_tuning(const char* key, int value) {
   const std::string k = key ? key : "";
-  if (k == "gemm_variant" && (value == 1 || value == 2)) { g_gemm_variant = value; return 0; }
-  if (k == "gemm_stages" && value >= 2 && value <= 4) { g_gemm_stages = value; return 0; }
+  if (k == "gemm_variant" && value >= 0 && value <= 2) { g_gemm_variant = value; return 0; }
+  if (k == "gemm_stages" && (value == 0 || (value >= 2 && value <= 4))) { g_gemm_stages = value; return 0; }
   if (k == "gemm_debug" && value >= 0 && value <= 3) { g_gemm_debug = value; return 0; }
+  if (k == "rows_bm" && (value == 0 || value == 64 || value == 128)) { g_rows_bm = value; return 0; }
+  if (k == "wgrad_bm" && (value == 0 || value == 64 || value == 128)) { g_wgrad_bm = value; return 0; }
   return fail("moe_set_tuning: unknown key or value");
 }
 
@@ -719,20 +724,24 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
   p.N = N;
   p.K = K;
 
-  // Pick the row tile so the launch has >= ~2 workgroups per CU.
+  // Per-shape choice (kbench.py sweeps at the C2 shapes, MI355X): 64-row
+  // tiles (two 48-64 KiB workgroups per CU, one's epilogue overlapping the
+  // other's main loop); LDS-DMA ring of 2 stages, 3 for K >= 1024 on grids
+  // under one tile per CU (the deeper ring covers the longer K loop).
   const int nt = N / 128;
-  const int tiles128 = (max_rows + 127) / 128 + G;
-  const bool big = (long long)tiles128 * nt >= 512;
-  const int BMsel = big ? 128 : 64;
+  const int BMsel = g_rows_bm ? g_rows_bm : 64;
   const int mtiles = ((max_rows + BMsel - 1) / BMsel + G + 7) / 8 * 8;  // padded to the XCD count
   dim3 grid(mtiles * nt);
+  const int variant = g_gemm_variant ? g_gemm_variant : 2;
+  const int stages = g_gemm_stages ? g_gemm_stages : ((K >= 1024 && (long long)mtiles * nt < 256) ? 3 : 2);
   // algorithmic bytes: weights + bias once; per routed row A (K), C (N) and the relu-mask operand (N)
   const bool has_bias = epilogue == MOE_EPI_BIAS || epilogue == MOE_EPI_BIAS_RELU;
   ProfScope prof(stream, PROF_GEMM, 2.0 * G * N * K + (has_bias ? 4.0 * G * N : 0.0), true,
                  2.0 * K + 2.0 * N + (epilogue == MOE_EPI_RELU_MASK ? 2.0 * N : 0.0), 2.0 * N * K);
   p.prof_rows = prof.rows_slot();
 
-#define GG_ROWS(BM, BK_, EPI) launch<BM, 128, true, BK_, MODE_ROWS, EPI, false>(p, grid, stream, prof)
+#define GG_ROWS(BM, BK_, EPI) \
+  launch<BM, 128, true, BK_, MODE_ROWS, EPI, false>(p, grid, stream, prof, variant, stages)
 #define GG_EPI(BM, BK_)                                                  \
   switch (epilogue) {                                                   \
     case MOE_EPI_NONE: GG_ROWS(BM, BK_, MOE_EPI_NONE); break;            \
@@ -773,7 +782,11 @@ extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, f
   p.N = N;
   p.K = 0;
   const int ntn = N / 128;
-  const bool big = M % 128 == 0 && (long long)(M / 128) * ntn * G >= 512;
+  // Per-shape choice (kbench.py): 64-row tiles, register-staged double buffer
+  // (its global_load_dwordx4 path streams these k-row gathers faster than LDS-DMA)
+  const bool big = M % 128 == 0 && g_wgrad_bm == 128;
+  const int variant = g_gemm_variant ? g_gemm_variant : 1;
+  const int stages = g_gemm_stages ? g_gemm_stages : 2;
   const int gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
   // algorithmic bytes: fp32 C (+ colsum) once; per routed row one row of X (M) and of Y (N)
   ProfScope prof(stream, PROF_GEMM, 4.0 * G * M * N + (colsum ? 4.0 * G * M : 0.0), true, 2.0 * (M + N),
@@ -781,12 +794,12 @@ extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, f
   p.prof_rows = prof.rows_slot();
   if (big) {
     dim3 grid((M / 128) * ntn * gpad);
-    if (colsum) launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream, prof);
-    else launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream, prof);
+    if (colsum) launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream, prof, variant, stages);
+    else launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream, prof, variant, stages);
   } else {
     dim3 grid((M / 64) * ntn * gpad);
-    if (colsum) launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream, prof);
-    else launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream, prof);
+    if (colsum) launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream, prof, variant, stages);
+    else launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream, prof, variant, stages);
   }
   return check_launch("moe_grouped_gemm_wgrad");
 }

@@ -95,19 +95,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="1,2")
-    ap.add_argument("--stages", default="2,3,4")
+    ap.add_argument("--variants", default="0")
+    ap.add_argument("--stages", default="0")
     ap.add_argument("--only", default="")
     ap.add_argument("--debug", default="0", help="comma list of gemm_debug modes (1 no C stores, 2 no main loop)")
+    ap.add_argument("--bm", default="0", help="comma list of forced row-tile heights (0 = auto) for rows and wgrad")
     a = ap.parse_args()
     L.lib()
-    configs = [(v, s, dbg) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
-               for dbg in map(int, a.debug.split(","))
+    configs = [(v, s, dbg, bm) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
+               for dbg in map(int, a.debug.split(",")) for bm in map(int, a.bm.split(","))
                if not (v == 1 and s != int(a.stages.split(",")[0]))]
     shapes = {"enc": setup(8 * 920, 8, 2, 256, 1024), "dec": setup(8 * 300, 8, 2, 256, 1024, seed=1)}
     res = {}
     for _ in range(a.rounds):
-        for (v, s, dbg) in configs:
+        for (v, s, dbg, bm) in configs:
+            L.set_tuning("rows_bm", bm)
+            L.set_tuning("wgrad_bm", bm)
             L.set_tuning("gemm_variant", v)
             L.set_tuning("gemm_stages", s)
             L.set_tuning("gemm_debug", dbg)
@@ -115,13 +118,15 @@ def main():
                 for name, fn, flops, byts in kernels(c):
                     if a.only and a.only not in name:
                         continue
-                    if not name.startswith("gemm") and (v, s, dbg) != configs[0]:
+                    if not name.startswith("gemm") and (v, s, dbg, bm) != configs[0]:
                         continue
-                    res.setdefault((name, sname, v, s, dbg, flops, byts), []).append(timed(fn, a.reps))
+                    res.setdefault((name, sname, v, s, dbg, bm, flops, byts), []).append(timed(fn, a.reps))
     L.set_tuning("gemm_debug", 0)
-    for (name, sname, v, s, dbg, flops, byts), ts in res.items():
+    L.set_tuning("rows_bm", 0)
+    L.set_tuning("wgrad_bm", 0)
+    for (name, sname, v, s, dbg, bm, flops, byts), ts in res.items():
         us = statistics.median(ts)
-        d = {"kernel": name, "shape": sname, "variant": v, "stages": s, "debug": dbg, "us": round(us, 2),
+        d = {"kernel": name, "shape": sname, "variant": v, "stages": s, "debug": dbg, "bm": bm, "us": round(us, 2),
              "min_us": round(min(ts), 2)}
         if flops:
             d["tflops"] = round(flops / us / 1e6, 1)

@@ -87,7 +87,7 @@ def _int_tensor(rng, shape, lo=-3, hi=4):
     return rng.integers(lo, hi, size=shape).astype(np.float64)
 
 
-GEMM_CFGS = [(1, 3), (2, 2), (2, 3), (2, 4)]  # (gemm_variant, gemm_stages)
+GEMM_CFGS = [(0, 0), (1, 2), (2, 2), (2, 3), (2, 4)]  # (gemm_variant, gemm_stages); 0 = per-shape choice
 
 
 @pytest.fixture
@@ -98,8 +98,8 @@ def gemm_cfg(request, hip_lib):
     L.set_tuning("gemm_variant", v)
     L.set_tuning("gemm_stages", s)
     yield request.param
-    L.set_tuning("gemm_variant", 2)
-    L.set_tuning("gemm_stages", 2)
+    L.set_tuning("gemm_variant", 0)  # back to the per-shape choice
+    L.set_tuning("gemm_stages", 0)
 
 
 @pytest.mark.parametrize("gemm_cfg", GEMM_CFGS, indirect=True)
