@@ -16,7 +16,7 @@ cd $R
 timeout -k 10 420 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1; rc=$?
 echo "PYTEST $rc"; tail -3 $O/pytest_gpu.log
 ok $rc || exit $rc
-timeout -k 10 420 python bench.py > $O/bench.json 2> $O/bench.err; rc=$?
+timeout -k 10 420 python bench.py --phase-timing > $O/bench.json 2> $O/bench.err; rc=$?
 echo "BENCH $rc"; cat $O/bench.json
 [ $rc -eq 0 ] || exit $rc
 
@@ -27,10 +27,14 @@ echo "ROCPROF $rc"; cat $O/prof/bench.json
 [ $rc -eq 0 ] || exit $rc
 KRE="gemm_v|permute_fwd|combine_fwd|combine_bwd|router_topk|token_bwd|msda_"
 timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" --output-format csv -d $O/pmc_fetch -o p -- \
-  python3 $R/bench.py --no-cpu-baseline --no-kernel-timing --steps 3 --warmup 1 > $O/pmc_fetch/bench.json 2> $O/pmc_fetch/bench.err; rc=$?
+  python3 $R/bench.py --no-cpu-baseline --no-kernel-timing --no-graphs --steps 3 --warmup 1 > $O/pmc_fetch/bench.json 2> $O/pmc_fetch/bench.err; rc=$?
 echo "PMC_FETCH $rc"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" --output-format csv -d $O/pmc_write -o p -- \
-  python3 $R/bench.py --no-cpu-baseline --no-kernel-timing --steps 3 --warmup 1 > $O/pmc_write/bench.json 2> $O/pmc_write/bench.err; rc=$?
+  python3 $R/bench.py --no-cpu-baseline --no-kernel-timing --no-graphs --steps 3 --warmup 1 > $O/pmc_write/bench.json 2> $O/pmc_write/bench.err; rc=$?
 echo "PMC_WRITE $rc"
+[ $rc -eq 0 ] || exit $rc
+cd $R
+timeout -k 10 300 python multimodal-moe_amd/kbench.py --rounds 3 --reps 20 > $O/kbench.jsonl 2> $O/kbench.err; rc=$?
+echo "KBENCH $rc"
 exit $rc
