@@ -111,7 +111,8 @@ enum moe_epilogue {
   MOE_EPI_NONE = 0,      /* C = A.B                                   */
   MOE_EPI_BIAS = 1,      /* C = A.B + bias[g, n]                      */
   MOE_EPI_BIAS_RELU = 2, /* C = relu(A.B + bias[g, n])                */
-  MOE_EPI_RELU_MASK = 3  /* C = (A.B) * (aux[row, n] > 0)   (dgrad)   */
+  MOE_EPI_RELU_MASK = 3, /* C = (A.B) * (aux[row, n] > 0)   (dgrad)   */
+  MOE_EPI_RELU_MASK_MX = 4 /* same, aux is e4m3 [rows, N] (byte > +0)  */
 };
 
 /* a5/a7, rows-grouped GEMM (expert FFN forward and dgrad):
@@ -120,10 +121,11 @@ enum moe_epilogue {
  * A: bf16 [rows, K] row-major.  B_g = b + g * K * N:
  *   trans_b = 1: stored [N][K] (nn.Linear weight; forward),
  *   trans_b = 0: stored [K][N] (dgrad through the same weight).
- * bias: fp32 [G, N] (EPI_BIAS*); aux: bf16 [rows, N] (EPI_RELU_MASK).
+ * bias: fp32 [G, N] (EPI_BIAS*); aux: bf16 [rows, N] (EPI_RELU_MASK) or e4m3
+ * [rows, N] (EPI_RELU_MASK_MX; sign/zero only, no exponents needed).
  * C: bf16 [rows, N].  K, N multiples of 64; offsets int32 [G+1] on device;
  * max_rows is a host upper bound of offsets[G] (grid sizing, no sync). */
-int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c,
+int moe_grouped_gemm(int dtype /* MOE_BF16; fp8: moe_grouped_gemm_mx */, const void* a, const void* b, void* c,
                      const int32_t* offsets, int G, int max_rows, int N, int K,
                      int trans_b, int epilogue, const float* bias, const void* aux,
                      const float* scales, hipStream_t stream);
@@ -136,6 +138,42 @@ int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c,
 int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, float* c,
                            float* colsum, const int32_t* offsets, int G,
                            int M, int N, hipStream_t stream);
+
+/* ---- MXFP8 expert path (config C5: 32-expert top-4 fp8 expert GEMMs) ----
+ * Format: OCP e4m3 elements with one E8M0 exponent byte per 32 consecutive
+ * elements of a row ("MXFP8"); the block exponent e is the smallest with
+ * amax <= 448 * 2^e (nothing saturates), stored as e + 127.  Forward GEMMs
+ * run on v_mfma_scale_f32_16x16x128_f8f6f4 (hardware-applied block scales);
+ * the backward keeps the e4m3 activations (ReLU mask from the e4m3 H, wgrad
+ * operands dequantised exactly to bf16) and the bf16 weights for dgrad. */
+
+/* Row quantizer: x bf16 [R, K] -> q e4m3 [R, K], scales uint8 [R, K/32].
+ * K multiple of 128 (<= 8192).  Used for the expert weights (R = G*N). */
+int moe_quantize_mx(const void* x, long long R, int K, void* q, void* scales, hipStream_t stream);
+
+/* a4 in MXFP8: as moe_permute_fwd, but each token row is quantized
+ * once and written to its kept destinations as e4m3 xq [rows, d] with
+ * exponents xs [rows, d/32]. */
+int moe_permute_fwd_mx(const void* x, const int32_t* topk_idx, const int32_t* local_rank,
+                       const int32_t* rank_base, const int32_t* offsets, int T, int d, int E, int k,
+                       int cap, void* xq, void* xs, int32_t* pos, hipStream_t stream);
+
+/* a5 in MXFP8, rows-grouped, B stored [N][K] per group (nn.Linear):
+ *   C[r, n] = epi( sum_k deq(A)[r, k] * deq(B_g)[n, k] )
+ * a e4m3 [rows, K] + a_scales [rows, K/32]; b e4m3 [G, N, K] + b_scales
+ * [G, N, K/32]; epilogue NONE / BIAS / BIAS_RELU (bias fp32 [G, N]).
+ * c_scales == NULL: C is bf16 [rows, N]; else C is e4m3 [rows, N] with
+ * exponents c_scales [rows, N/32] (quantized from the bf16-rounded result).
+ * N % 128 == 0, K % 128 == 0. */
+int moe_grouped_gemm_mx(const void* a, const void* a_scales, const void* b, const void* b_scales,
+                        void* c, void* c_scales, const int32_t* offsets, int G, int max_rows, int N,
+                        int K, int epilogue, const float* bias, hipStream_t stream);
+
+/* a7: moe_grouped_gemm_wgrad with Y in MXFP8 (e4m3 [rows, N] +
+ * y_scales [rows, N/32]); X stays bf16 (colsum over X as before). */
+int moe_grouped_gemm_wgrad_mx(const void* x, const void* y, const void* y_scales, float* c,
+                              float* colsum, const int32_t* offsets, int G, int M, int N,
+                              hipStream_t stream);
 
 /* ---- SURVEY 8(f).1 (next row): RT-DETR multi-scale deformable attention ----
  * Sampling core of the decoder's cross-attention (replaces the per-level

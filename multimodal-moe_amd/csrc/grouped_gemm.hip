@@ -33,6 +33,14 @@ namespace moe {
 
 enum { MODE_ROWS = 0, MODE_WGRAD = 1 };
 
+// Operand-format flags (template parameter FL of the kernels)
+enum {
+  FL_MX = 1,    // ROWS: A and B are MXFP8 (e4m3 + E8M0 per 32 along K): v_mfma_scale_f32_16x16x128_f8f6f4
+  FL_CQ = 2,    // ROWS: C is written as MXFP8 (e4m3 [rows][N] + exponents [rows][N/32])
+  FL_AUX8 = 4,  // ROWS, EPI_RELU_MASK: the mask operand is e4m3 (keep where the byte is > +0)
+  FL_Y8 = 8     // WGRAD: Y is MXFP8, dequantised to bf16 while staging (v1)
+};
+
 struct GemmParams {
   const uint16_t* a;
   const uint16_t* b;
@@ -42,6 +50,10 @@ struct GemmParams {
   const uint16_t* aux;
   float* colsum;
   int32_t* prof_rows;  // profiler slot for offsets[G] (written by block 0), or nullptr
+  const uint8_t* as;   // MX: E8M0 block exponents of A [rows][ksb] (ROWS) or of Y [rows][N/32] (WGRAD Y8)
+  const uint8_t* bs;   // MX: E8M0 block exponents of B [G][N][ksb]
+  uint8_t* cs;         // CQ: E8M0 block exponents of C [rows][N/32]
+  int ksb;             // MX: scale bytes per A/B row (= K / 32)
   long long stride_b;  // elements between groups' B (ROWS mode)
   long long stride_c;  // elements between groups' C (WGRAD mode)
   int lda, ldb, ldc;
@@ -301,7 +313,7 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int g, int row0, i
 // lines; the register-direct path issues 8-B pieces, which the store path
 // handles at half the rate).  The relu-mask operand is read the same way.
 // Images: 16-B chunk c of row r at c ^ (r % chunks_per_row).
-template <int BM, int BN, int MODE, int EPI, bool COLSUM>
+template <int BM, int BN, int MODE, int EPI, bool COLSUM, int FL>
 __device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row0, int a_row_lim, int m0, int n0,
                                              int nt, f32x4 (&acc)[BM / 32][BN / 32], float (&csum)[BM / 32],
                                              const float4 (&bpre)[BN / 32], char* smem, int tid, int lane, int wm,
@@ -343,7 +355,19 @@ __device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row
       if (r >= a_row_lim) continue;
       uint4 v = *reinterpret_cast<const uint4*>(smem + r * (BN * 2) + ((c ^ (r & (CPR - 1))) << 4));
       const size_t gofs = ((size_t)row0 + r) * p.ldc + n0 + c * 8;
-      if constexpr (EPI == MOE_EPI_RELU_MASK) {  // keep where the forward activation is > 0
+      if constexpr (EPI == MOE_EPI_RELU_MASK && (FL & FL_AUX8)) {  // e4m3 activation: keep where byte > +0
+        const uint2 h = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(p.aux) + gofs);
+        uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t hw = q < 2 ? h.x : h.y;
+          const uint32_t lo = (hw >> (16 * (q & 1))) & 0xffu, hi = (hw >> (16 * (q & 1) + 8)) & 0xffu;
+          const uint32_t keep_lo = (lo == 0 || lo >= 0x80u) ? 0u : 0xffffu;
+          const uint32_t keep_hi = (hi == 0 || hi >= 0x80u) ? 0u : 0xffff0000u;
+          vw[q] &= keep_lo | keep_hi;
+        }
+        v = make_uint4(vw[0], vw[1], vw[2], vw[3]);
+      } else if constexpr (EPI == MOE_EPI_RELU_MASK) {  // keep where the forward activation is > 0
         const uint4 h = *reinterpret_cast<const uint4*>(p.aux + gofs);
         uint32_t hw[4] = {h.x, h.y, h.z, h.w};
         uint32_t vw[4] = {v.x, v.y, v.z, v.w};
@@ -356,7 +380,16 @@ __device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row
         }
         v = make_uint4(vw[0], vw[1], vw[2], vw[3]);
       }
-      if (!(p.dbg & 1)) *reinterpret_cast<uint4*>(C + gofs) = v;
+      if constexpr (FL & FL_CQ) {  // MXFP8 out: 4 consecutive lanes (same row) hold one 32-column block
+        int e;
+        const uint2 o = mx_quant_chunk(v, e);
+        if (!(p.dbg & 1)) {
+          *reinterpret_cast<uint2*>(static_cast<uint8_t*>(p.c) + gofs) = o;
+          if ((c & 3) == 0) p.cs[((size_t)row0 + r) * (p.ldc / 32) + (n0 + c * 8) / 32] = (uint8_t)(e + 127);
+        }
+      } else {
+        if (!(p.dbg & 1)) *reinterpret_cast<uint4*>(C + gofs) = v;
+      }
     }
   } else {
     constexpr int CPR = BN / 4;  // 16-B chunks per fp32 row
@@ -424,6 +457,45 @@ __device__ __forceinline__ void compute_tile(const char* abuf, const char* bbuf,
   }
 }
 
+// MFMA work on one staged MXFP8 K-tile (128 e4m3 per row = one 128-B LDS row,
+// the same image as a bf16 K-tile): one v_mfma_scale_f32_16x16x128_f8f6f4 per
+// (i, j).  Operand map (measured with tools/mx_probe.hip, exact integer data):
+// lane l = 16 q + i supplies row i, k = 16q..16q+15 in its first 16 bytes and
+// k = 64+16q..64+16q+15 in its last 16 (16-B chunks q and q + 4), and the E8M0
+// exponent of k-block q (k = 32q..32q+31) of row i -- a block's data is spread
+// over two lane groups, its scale comes from one lane.  sA / sB hold each tile
+// row's exponents for the whole K as dwords (4 k-blocks = one K-tile each).
+template <int BM, int BN>
+__device__ __forceinline__ void compute_tile_mx(const char* abuf, const char* bbuf, const uint32_t* sA,
+                                                const uint32_t* sB, int ksw, int kt,
+                                                f32x4 (&acc)[BM / 32][BN / 32], int lane, int wm, int wn) {
+  constexpr int TM = BM / 32, TN = BN / 32;
+  const int rl = lane & 15, kb = lane >> 4;
+  i32x8 af[TM], bfr[TN];
+  int sa[TM], sb[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * (BM / 2) + 16 * i + rl;
+    const uint4 lo = *reinterpret_cast<const uint4*>(abuf + kimg_off(r, kb));
+    const uint4 hi = *reinterpret_cast<const uint4*>(abuf + kimg_off(r, kb + 4));
+    af[i] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    sa[i] = (int)(sA[r * ksw + kt] >> (8 * kb));
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int r = wn * (BN / 2) + 16 * j + rl;
+    const uint4 lo = *reinterpret_cast<const uint4*>(bbuf + kimg_off(r, kb));
+    const uint4 hi = *reinterpret_cast<const uint4*>(bbuf + kimg_off(r, kb + 4));
+    bfr[j] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    sb[j] = (int)(sB[r * ksw + kt] >> (8 * kb));
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af[i], acc[i][j], 0, 0, 0, sb[j], 0, sa[i]);
+}
+
 // ---------------------------------------------------------------------------
 // v1: register-staged double buffer
 // ---------------------------------------------------------------------------
@@ -466,7 +538,34 @@ struct RegStage {
   }
 };
 
-template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM>
+// WGRAD Y operand in MXFP8 (FL_Y8): an MN-contiguous [64][128] tile of e4m3
+// rows (8 bytes + one exponent per thread-chunk), dequantised to bf16 (exact)
+// when stored, so the LDS image and the MFMA loop are the bf16 ones.
+struct RegStageY8 {
+  static constexpr int kPer = 128 * 64 / 8 / 256;
+  uint2 reg[kPer];
+  int ex[kPer];
+
+  __device__ __forceinline__ void load(const uint8_t* base, const uint8_t* sbase, int ld, int k_lim, int tid) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int q = tid + 256 * i;
+      const int kk = q / 16, r = (q % 16) * 8;
+      const bool ok = kk < k_lim;
+      reg[i] = ok ? *reinterpret_cast<const uint2*>(base + (size_t)kk * ld + r) : make_uint2(0, 0);
+      ex[i] = ok ? (int)sbase[(size_t)kk * (ld / 32) + (r >> 5)] - 127 : 0;
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int q = tid + 256 * i;
+      *reinterpret_cast<uint4*>(lds + mimg_off<128>(q / 16, q % 16)) = mx_unpack8_bf16(reg[i], ex[i]);
+    }
+  }
+};
+
+template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>
 __global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int A_BYTES = BM * 64 * 2;
@@ -493,13 +592,28 @@ __global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
   auto a_ptr = [&](int kt) { return A_K ? t.a_base + kt * 64 : t.a_base + (size_t)kt * 64 * p.lda; };
   auto b_ptr = [&](int kt) { return B_K ? t.b_base + kt * 64 : t.b_base + (size_t)kt * 64 * p.ldb; };
 
+  constexpr bool Y8 = (FL & FL_Y8) != 0;
+  static_assert(!Y8 || (MODE == MODE_WGRAD && BN == 128), "Y8 staging is for WGRAD 128-wide tiles");
+  // Y8: byte pointers of Y (e4m3 [rows][N]) and of its exponents ([rows][N/32]) at (row0, n0)
+  const uint8_t* yq = Y8 ? reinterpret_cast<const uint8_t*>(p.b) + (size_t)t.row0 * p.N + t.n0 : nullptr;
+  const uint8_t* ys = Y8 ? p.as + (size_t)t.row0 * (p.N / 32) + t.n0 / 32 : nullptr;
+
   RegStage<BM, A_K> la;
   RegStage<BN, B_K> lb;
+  RegStageY8 ly;
+  auto load_b = [&](int kt) {
+    if constexpr (Y8) ly.load(yq + (size_t)kt * 64 * p.N, ys + (size_t)kt * 64 * (p.N / 32), p.N, k_lim(kt), tid);
+    else lb.load(b_ptr(kt), p.ldb, BN, k_lim(kt), tid);
+  };
+  auto store_b = [&](char* dst) {
+    if constexpr (Y8) ly.store(dst, tid);
+    else lb.store(dst, tid);
+  };
   if (t.nk > 0) {
     la.load(a_ptr(0), p.lda, t.a_row_lim, k_lim(0), tid);
-    lb.load(b_ptr(0), p.ldb, BN, k_lim(0), tid);
+    load_b(0);
     la.store(smem, tid);
-    lb.store(smem + A_BYTES, tid);
+    store_b(smem + A_BYTES);
   }
   __syncthreads();
   for (int kt = 0; kt < ((p.dbg & 2) ? 0 : t.nk); ++kt) {
@@ -507,13 +621,13 @@ __global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
     const bool more = kt + 1 < t.nk;
     if (more) {
       la.load(a_ptr(kt + 1), p.lda, t.a_row_lim, k_lim(kt + 1), tid);
-      lb.load(b_ptr(kt + 1), p.ldb, BN, k_lim(kt + 1), tid);
+      load_b(kt + 1);
     }
     compute_tile<BM, BN, A_K, B_K, COLSUM>(cur, cur + A_BYTES, acc, csum, lane, wm, wn);
     if (more) {
       char* nxt = smem + ((kt + 1) & 1) * BUF;
       la.store(nxt, tid);
-      lb.store(nxt + A_BYTES, tid);
+      store_b(nxt + A_BYTES);
     }
     __syncthreads();
   }
@@ -559,7 +673,7 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int S, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM>
+template <int BM, int BN, int S, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>
 __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int A_BYTES = BM * 64 * 2;
@@ -598,6 +712,28 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) issue(s);
 
+  // MX: stage the tile rows' E8M0 exponents for the whole K (dwords) behind the
+  // ring while the prologue DMA is in flight.
+  constexpr bool MX = (FL & FL_MX) != 0;
+  static_assert(!MX || (MODE == MODE_ROWS && A_K && B_K), "MX operands: ROWS mode, K-contiguous A and B");
+  const int ksw = p.ksb / 4;
+  uint32_t* sA = reinterpret_cast<uint32_t*>(smem + S * BUF);
+  uint32_t* sB = sA + BM * ksw;
+  if constexpr (MX) {
+    for (int q = tid; q < (BM + BN) * ksw; q += 256) {
+      const int r = q / ksw, w = q - r * ksw;
+      uint32_t v;
+      if (r < BM) {
+        const int rr = r < t.a_row_lim ? r : t.a_row_lim - 1;
+        v = reinterpret_cast<const uint32_t*>(p.as + ((size_t)t.row0 + rr) * p.ksb)[w];
+      } else {
+        v = reinterpret_cast<const uint32_t*>(p.bs + ((size_t)t.g * p.N + t.n0 + (r - BM)) * p.ksb)[w];
+      }
+      sA[q] = v;
+    }
+    __syncthreads();
+  }
+
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt has landed for this wave once at most min(S-2, nk-1-kt) newer tiles are pending
     const int newer = nk - 1 - kt;
@@ -627,11 +763,12 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
       }
     }
     if (kt + S - 1 < nk) issue(kt + S - 1);  // refills the slot read in iteration kt-1
-    compute_tile<BM, BN, A_K, B_K, COLSUM>(cur, cur + A_BYTES, acc, csum, lane, wm, wn);
+    if constexpr (MX) compute_tile_mx<BM, BN>(cur, cur + A_BYTES, sA, sB, ksw, kt, acc, lane, wm, wn);
+    else compute_tile<BM, BN, A_K, B_K, COLSUM>(cur, cur + A_BYTES, acc, csum, lane, wm, wn);
   }
   static_assert(S * (BM + BN) * 64 * 2 >= BM * BN * (MODE == MODE_ROWS ? 2 : 4), "epilogue image exceeds LDS");
-  epilogue_lds<BM, BN, MODE, EPI, COLSUM>(p, t.g, t.row0, t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, smem,
-                                          tid, lane, wm, wn);
+  epilogue_lds<BM, BN, MODE, EPI, COLSUM, FL>(p, t.g, t.row0, t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, smem,
+                                              tid, lane, wm, wn);
 }
 
 // ---------------------------------------------------------------------------
@@ -641,34 +778,37 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
 // -- including ones captured into a hipGraph -- make no attribute call.
 template <auto FN>
 static void allow_lds(size_t bytes) {
+  // (raised to the whole 160 KiB at once: the MX exponent stage makes the size depend on K)
   static bool done = false;
   if (!done && bytes > 65536) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(FN), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)bytes);
+                              160 * 1024);
+    done = true;
   }
-  done = true;
 }
 
-template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM>
+template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL = 0>
 static void launch(const GemmParams& p, dim3 grid, hipStream_t s, const ProfScope& prof, int variant, int stages) {
-  if (variant == 1) {
+  // MX: the exponent stage behind the ring ((BM + BN) rows x K/32 bytes)
+  const size_t xs = (FL & FL_MX) ? (size_t)(BM + BN) * p.ksb : 0;
+  if (variant == 1 && !(FL & (FL_MX | FL_CQ | FL_AUX8))) {
     constexpr size_t lds = 2 * (BM + BN) * 64 * 2;
-    constexpr auto fn = gemm_v1_kernel<BM, BN, A_K, B_K, MODE, EPI, COLSUM>;
+    constexpr auto fn = gemm_v1_kernel<BM, BN, A_K, B_K, MODE, EPI, COLSUM, FL & FL_Y8>;
     allow_lds<fn>(lds);
     MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
   } else if (stages == 2) {
-    constexpr size_t lds = 2 * (BM + BN) * 64 * 2;
-    constexpr auto fn = gemm_v2_kernel<BM, BN, 2, A_K, B_K, MODE, EPI, COLSUM>;
+    const size_t lds = 2 * (BM + BN) * 64 * 2 + xs;
+    constexpr auto fn = gemm_v2_kernel<BM, BN, 2, A_K, B_K, MODE, EPI, COLSUM, FL & ~FL_Y8>;
     allow_lds<fn>(lds);
     MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
   } else if (stages >= 4) {
-    constexpr size_t lds = 4 * (BM + BN) * 64 * 2;
-    constexpr auto fn = gemm_v2_kernel<BM, BN, 4, A_K, B_K, MODE, EPI, COLSUM>;
+    const size_t lds = 4 * (BM + BN) * 64 * 2 + xs;
+    constexpr auto fn = gemm_v2_kernel<BM, BN, 4, A_K, B_K, MODE, EPI, COLSUM, FL & ~FL_Y8>;
     allow_lds<fn>(lds);
     MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
   } else {
-    constexpr size_t lds = 3 * (BM + BN) * 64 * 2;
-    constexpr auto fn = gemm_v2_kernel<BM, BN, 3, A_K, B_K, MODE, EPI, COLSUM>;
+    const size_t lds = 3 * (BM + BN) * 64 * 2 + xs;
+    constexpr auto fn = gemm_v2_kernel<BM, BN, 3, A_K, B_K, MODE, EPI, COLSUM, FL & ~FL_Y8>;
     allow_lds<fn>(lds);
     MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
   }
@@ -700,9 +840,9 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
   if (max_rows < 0) return fail("grouped_gemm: max_rows < 0");
   if ((epilogue == MOE_EPI_BIAS || epilogue == MOE_EPI_BIAS_RELU) && bias == nullptr)
     return fail("grouped_gemm: bias epilogue without bias");
-  if (epilogue == MOE_EPI_RELU_MASK && aux == nullptr)
+  if ((epilogue == MOE_EPI_RELU_MASK || epilogue == MOE_EPI_RELU_MASK_MX) && aux == nullptr)
     return fail("grouped_gemm: relu-mask epilogue without aux");
-  if (epilogue < 0 || epilogue > 3) return fail("grouped_gemm: bad epilogue");
+  if (epilogue < 0 || epilogue > 4) return fail("grouped_gemm: bad epilogue");
   if (max_rows == 0) return 0;
 
   GemmParams p{};
@@ -736,18 +876,20 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
   const int stages = g_gemm_stages ? g_gemm_stages : ((K >= 1024 && (long long)mtiles * nt < 256) ? 3 : 2);
   // algorithmic bytes: weights + bias once; per routed row A (K), C (N) and the relu-mask operand (N)
   const bool has_bias = epilogue == MOE_EPI_BIAS || epilogue == MOE_EPI_BIAS_RELU;
+  const double mask_bytes = epilogue == MOE_EPI_RELU_MASK ? 2.0 * N : (epilogue == MOE_EPI_RELU_MASK_MX ? 1.0 * N : 0.0);
   ProfScope prof(stream, PROF_GEMM, 2.0 * G * N * K + (has_bias ? 4.0 * G * N : 0.0), true,
-                 2.0 * K + 2.0 * N + (epilogue == MOE_EPI_RELU_MASK ? 2.0 * N : 0.0), 2.0 * N * K);
+                 2.0 * K + 2.0 * N + mask_bytes, 2.0 * N * K);
   p.prof_rows = prof.rows_slot();
 
-#define GG_ROWS(BM, BK_, EPI) \
-  launch<BM, 128, true, BK_, MODE_ROWS, EPI, false>(p, grid, stream, prof, variant, stages)
-#define GG_EPI(BM, BK_)                                                  \
-  switch (epilogue) {                                                   \
-    case MOE_EPI_NONE: GG_ROWS(BM, BK_, MOE_EPI_NONE); break;            \
-    case MOE_EPI_BIAS: GG_ROWS(BM, BK_, MOE_EPI_BIAS); break;            \
-    case MOE_EPI_BIAS_RELU: GG_ROWS(BM, BK_, MOE_EPI_BIAS_RELU); break;  \
-    default: GG_ROWS(BM, BK_, MOE_EPI_RELU_MASK); break;                 \
+#define GG_ROWS(BM, BK_, EPI, FL) \
+  launch<BM, 128, true, BK_, MODE_ROWS, EPI, false, FL>(p, grid, stream, prof, variant, stages)
+#define GG_EPI(BM, BK_)                                                           \
+  switch (epilogue) {                                                            \
+    case MOE_EPI_NONE: GG_ROWS(BM, BK_, MOE_EPI_NONE, 0); break;                  \
+    case MOE_EPI_BIAS: GG_ROWS(BM, BK_, MOE_EPI_BIAS, 0); break;                  \
+    case MOE_EPI_BIAS_RELU: GG_ROWS(BM, BK_, MOE_EPI_BIAS_RELU, 0); break;        \
+    case MOE_EPI_RELU_MASK: GG_ROWS(BM, BK_, MOE_EPI_RELU_MASK, 0); break;        \
+    default: GG_ROWS(BM, BK_, MOE_EPI_RELU_MASK, FL_AUX8); break;                 \
   }
   if (BMsel == 128) {
     if (trans_b) { GG_EPI(128, true) } else { GG_EPI(128, false) }
@@ -802,4 +944,104 @@ extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, f
     else launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream, prof, variant, stages);
   }
   return check_launch("moe_grouped_gemm_wgrad");
+}
+
+// ---------------------------------------------------------------------------
+// MXFP8 expert GEMMs (config C5; SURVEY 8a rows a5/a7 with the fp8 expert path)
+// ---------------------------------------------------------------------------
+extern "C" int moe_grouped_gemm_mx(const void* a, const void* a_scales, const void* b, const void* b_scales,
+                                   void* c, void* c_scales, const int32_t* offsets, int G, int max_rows, int N,
+                                   int K, int epilogue, const float* bias, hipStream_t stream) {
+  if (G < 1 || G > 1024) return fail("grouped_gemm_mx: G out of range");
+  if (N <= 0 || K <= 0 || N % 128 != 0 || K % 128 != 0 || K > 8192)
+    return fail("grouped_gemm_mx: need N % 128 == 0 and K % 128 == 0 (K <= 8192)");
+  if (max_rows < 0) return fail("grouped_gemm_mx: max_rows < 0");
+  if (epilogue < 0 || epilogue > 2) return fail("grouped_gemm_mx: epilogue must be NONE, BIAS or BIAS_RELU");
+  if (epilogue != MOE_EPI_NONE && bias == nullptr) return fail("grouped_gemm_mx: bias epilogue without bias");
+  if (a_scales == nullptr || b_scales == nullptr) return fail("grouped_gemm_mx: missing operand scales");
+  if (max_rows == 0) return 0;
+  GemmParams p{};
+  p.dbg = g_gemm_debug;
+  // e4m3 rows addressed as 16-bit pairs: the bf16 tile machinery moves [R][128 B] K-tiles
+  p.a = static_cast<const uint16_t*>(a);
+  p.b = static_cast<const uint16_t*>(b);
+  p.c = c;
+  p.cs = static_cast<uint8_t*>(c_scales);
+  p.as = static_cast<const uint8_t*>(a_scales);
+  p.bs = static_cast<const uint8_t*>(b_scales);
+  p.ksb = K / 32;
+  p.offsets = offsets;
+  p.bias = bias;
+  p.stride_b = (long long)N * K / 2;
+  p.lda = K / 2;
+  p.ldb = K / 2;
+  p.ldc = N;
+  p.G = G;
+  p.N = N;
+  p.K = K / 2;
+  const int nt = N / 128;
+  const int BMsel = g_rows_bm ? g_rows_bm : 64;
+  const int mtiles = ((max_rows + BMsel - 1) / BMsel + G + 7) / 8 * 8;
+  dim3 grid(mtiles * nt);
+  const int stages = g_gemm_stages ? g_gemm_stages : ((K >= 2048 && (long long)mtiles * nt < 256) ? 3 : 2);
+  const bool cq = c_scales != nullptr;
+  const bool has_bias = epilogue != MOE_EPI_NONE;
+  // algorithmic bytes: e4m3 weights + exponents (+ bias) once; per routed row A (K + K/32), C (2N or N + N/32)
+  ProfScope prof(stream, PROF_GEMM, G * N * (K + K / 32.0) + (has_bias ? 4.0 * G * N : 0.0), true,
+                 K + K / 32.0 + (cq ? N + N / 32.0 : 2.0 * N), 2.0 * N * K);
+  p.prof_rows = prof.rows_slot();
+#define GM_ROWS(BM, EPI)                                                                                     \
+  do {                                                                                                       \
+    if (cq) launch<BM, 128, true, true, MODE_ROWS, EPI, false, FL_MX | FL_CQ>(p, grid, stream, prof, 2, stages); \
+    else launch<BM, 128, true, true, MODE_ROWS, EPI, false, FL_MX>(p, grid, stream, prof, 2, stages);       \
+  } while (0)
+#define GM_EPI(BM)                                                \
+  switch (epilogue) {                                            \
+    case MOE_EPI_NONE: GM_ROWS(BM, MOE_EPI_NONE); break;          \
+    case MOE_EPI_BIAS: GM_ROWS(BM, MOE_EPI_BIAS); break;          \
+    default: GM_ROWS(BM, MOE_EPI_BIAS_RELU); break;               \
+  }
+  if (BMsel == 128) {
+    GM_EPI(128)
+  } else {
+    GM_EPI(64)
+  }
+#undef GM_EPI
+#undef GM_ROWS
+  return check_launch("moe_grouped_gemm_mx");
+}
+
+extern "C" int moe_grouped_gemm_wgrad_mx(const void* x, const void* y, const void* y_scales, float* c,
+                                         float* colsum, const int32_t* offsets, int G, int M, int N,
+                                         hipStream_t stream) {
+  if (G < 1 || G > 1024) return fail("grouped_gemm_wgrad_mx: G out of range");
+  if (M <= 0 || N <= 0 || M % 64 != 0 || N % 128 != 0)
+    return fail("grouped_gemm_wgrad_mx: need M % 64 == 0 and N % 128 == 0");
+  if (y_scales == nullptr) return fail("grouped_gemm_wgrad_mx: missing Y scales");
+  GemmParams p{};
+  p.dbg = g_gemm_debug;
+  p.a = static_cast<const uint16_t*>(x);
+  p.b = static_cast<const uint16_t*>(y);
+  p.as = static_cast<const uint8_t*>(y_scales);
+  p.c = c;
+  p.offsets = offsets;
+  p.colsum = colsum;
+  p.stride_c = (long long)M * N;
+  p.lda = M;
+  p.ldb = N;
+  p.ldc = N;
+  p.G = G;
+  p.M = M;
+  p.N = N;
+  p.K = 0;
+  const int ntn = N / 128;
+  const int gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
+  // algorithmic bytes: fp32 C (+ colsum) once; per routed row one bf16 row of X (M) and one MXFP8 row of Y
+  ProfScope prof(stream, PROF_GEMM, 4.0 * G * M * N + (colsum ? 4.0 * G * M : 0.0), true,
+                 2.0 * M + N + N / 32.0, 2.0 * M * N);
+  p.prof_rows = prof.rows_slot();
+  dim3 grid((M / 64) * ntn * gpad);
+  if (colsum) launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true, FL_Y8>(p, grid, stream, prof, 1, 2);
+  else launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false, FL_Y8>(p, grid, stream, prof, 1, 2);
+  return check_launch("moe_grouped_gemm_wgrad_mx");
 }

@@ -47,6 +47,53 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return v;
 }
 
+// ---- MXFP8 (OCP e4m3 elements, one E8M0 scale per 32 consecutive elements) ----
+// Block scale: the smallest power of two 2^e with amax <= 448 * 2^e (no element
+// saturates), found from amax's exponent and mantissa bits (1.75 = 448 / 2^8),
+// clamped to the E8M0 range; the stored byte is e + 127.  The oracle
+// (oracle/moe_oracle.py: mx_exponent) restates the same integer rule.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int mx_exponent(float amax) {
+  const uint32_t u = __float_as_uint(amax);
+  if (amax == 0.f) return -127;
+  int e = (int)((u >> 23) & 0xff) - 127 - 8 + ((u & 0x7fffffu) > 0x600000u ? 1 : 0);
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+// Four floats already scaled into [-448, 448] -> four e4m3 bytes (RNE, v_cvt_pk_fp8_f32).
+__device__ __forceinline__ uint32_t pack4fp8(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+// Quantize 8 floats of one 32-element block whose exponent is e: two dwords of e4m3.
+__device__ __forceinline__ uint2 mx_pack8(const float* f, int e) {
+  uint2 o;
+  o.x = pack4fp8(ldexpf(f[0], -e), ldexpf(f[1], -e), ldexpf(f[2], -e), ldexpf(f[3], -e));
+  o.y = pack4fp8(ldexpf(f[4], -e), ldexpf(f[5], -e), ldexpf(f[6], -e), ldexpf(f[7], -e));
+  return o;
+}
+// e4m3 byte i (0..3) of w, times 2^e, as a float (exact).
+__device__ __forceinline__ float fp8_at(uint32_t w, int i, int e) {
+  float v;
+  switch (i) {
+    case 0: v = __builtin_amdgcn_cvt_f32_fp8((int)w, 0); break;
+    case 1: v = __builtin_amdgcn_cvt_f32_fp8((int)w, 1); break;
+    case 2: v = __builtin_amdgcn_cvt_f32_fp8((int)w, 2); break;
+    default: v = __builtin_amdgcn_cvt_f32_fp8((int)w, 3); break;
+  }
+  return ldexpf(v, e);
+}
+// 8 e4m3 bytes of one block with exponent e -> 8 bf16 (exact: 4-bit significands).
+__device__ __forceinline__ uint4 mx_unpack8_bf16(uint2 q, int e) {
+  uint4 o;
+  o.x = (__float_as_uint(fp8_at(q.x, 0, e)) >> 16) | (__float_as_uint(fp8_at(q.x, 1, e)) & 0xffff0000u);
+  o.y = (__float_as_uint(fp8_at(q.x, 2, e)) >> 16) | (__float_as_uint(fp8_at(q.x, 3, e)) & 0xffff0000u);
+  o.z = (__float_as_uint(fp8_at(q.y, 0, e)) >> 16) | (__float_as_uint(fp8_at(q.y, 1, e)) & 0xffff0000u);
+  o.w = (__float_as_uint(fp8_at(q.y, 2, e)) >> 16) | (__float_as_uint(fp8_at(q.y, 3, e)) & 0xffff0000u);
+  return o;
+}
+
 // Number of set bits of `mask` at lanes below this lane (v_mbcnt).
 __device__ __forceinline__ int mbcnt(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
@@ -59,6 +106,26 @@ __device__ __forceinline__ float group_sum(float v) {
 #pragma unroll
   for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+template <int W>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// MX-quantize one 16-B chunk (8 bf16) held by each lane, where 4 consecutive
+// lanes hold one 32-element block: the block amax by a 4-lane butterfly, then
+// e4m3 bytes and the block exponent.
+__device__ __forceinline__ uint2 mx_quant_chunk(const uint4 v, int& e) {
+  float f[8];
+  unpack8(v, f);
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m = fmaxf(m, fabsf(f[i]));
+  m = group_max<4>(m);
+  e = mx_exponent(m);
+  return mx_pack8(f, e);
 }
 
 }  // namespace moe

@@ -19,7 +19,8 @@ LIB_PATH = Path(os.environ.get("MOE_HIP_LIB", _PKG / "lib" / "libmoe_hip.so"))
 
 MOE_BF16 = 0
 MOE_FP8_E4M3 = 1
-EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK = 0, 1, 2, 3
+EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK, EPI_RELU_MASK_MX = 0, 1, 2, 3, 4
+MX_BLOCK = 32  # MXFP8: one E8M0 exponent byte per 32 e4m3 elements of a row
 
 # name -> (restype, argtypes); mirrors include/moe_hip.h
 _P = ctypes.c_void_p
@@ -35,6 +36,10 @@ SIGNATURES = {
     "moe_token_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "moe_grouped_gemm": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_wgrad": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "moe_quantize_mx": (_I, [_P, ctypes.c_longlong, _I, _P, _P, _P]),
+    "moe_permute_fwd_mx": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "moe_grouped_gemm_mx": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "moe_grouped_gemm_wgrad_mx": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_msda_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
@@ -294,6 +299,8 @@ def grouped_gemm(a, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None,
                  out=None):
     _need(a, torch.bfloat16, "a")
     _need(b, torch.bfloat16, "b")
+    if aux is not None:
+        _need(aux, torch.uint8 if epilogue == EPI_RELU_MASK_MX else torch.bfloat16, "aux")
     if b.numel() != G * N * K:
         raise MoEKernelError(f"grouped_gemm: b has {b.numel()} elements, want {G}*{N}*{K}")
     if a.shape[1] != K or a.shape[0] < max_rows:
@@ -315,6 +322,72 @@ def grouped_gemm_wgrad(x, y, offsets, G, want_colsum=True):
     rc = lib().moe_grouped_gemm_wgrad(
         MOE_BF16, _ptr(x), _ptr(y), _ptr(c), _ptr(cs), _ptr(offsets), G, M, N, _stream())
     _check(rc, "moe_grouped_gemm_wgrad")
+    return c, cs
+
+
+# ---------------------------------------------------------------------------
+# MXFP8 (config C5): e4m3 data as torch.uint8, E8M0 exponents as torch.uint8
+# ---------------------------------------------------------------------------
+def quantize_mx(x):
+    """x bf16 [..., K] -> (q uint8 [..., K] e4m3, s uint8 [..., K/32] E8M0)."""
+    _need(x, torch.bfloat16, "x")
+    K = x.shape[-1]
+    R = x.numel() // max(K, 1)
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    sc = torch.empty((*x.shape[:-1], K // MX_BLOCK), dtype=torch.uint8, device=x.device)
+    _check(lib().moe_quantize_mx(_ptr(x), R, K, _ptr(q), _ptr(sc), _stream()), "moe_quantize_mx")
+    return q, sc
+
+
+def permute_fwd_mx(x, topk_idx, local_rank, rank_base, offsets, E, cap, rows_alloc):
+    T, d = x.shape
+    k = topk_idx.shape[1]
+    _need(x, torch.bfloat16, "x")
+    n = max(rows_alloc, 1)
+    xq = torch.empty((n, d), dtype=torch.uint8, device=x.device)
+    xs = torch.empty((n, d // MX_BLOCK), dtype=torch.uint8, device=x.device)
+    pos = torch.empty((T, k), dtype=torch.int32, device=x.device)
+    rc = lib().moe_permute_fwd_mx(
+        _ptr(x), _ptr(topk_idx), _ptr(local_rank), _ptr(rank_base), _ptr(offsets), T, d, E, k, int(cap),
+        _ptr(xq), _ptr(xs), _ptr(pos), _stream())
+    _check(rc, "moe_permute_fwd_mx")
+    return xq, xs, pos
+
+
+def grouped_gemm_mx(aq, as_, bq, bs, offsets, G, max_rows, N, K, epilogue, bias=None, out_mx=False):
+    """MXFP8 rows-grouped GEMM, B stored [G, N, K].  Returns bf16 C [rows, N], or
+    (e4m3 C uint8 [rows, N], exponents uint8 [rows, N/32]) when out_mx."""
+    for t, n in ((aq, "a"), (as_, "a_scales"), (bq, "b"), (bs, "b_scales")):
+        _need(t, torch.uint8, n)
+    if bq.numel() != G * N * K or bs.numel() != G * N * K // MX_BLOCK:
+        raise MoEKernelError(f"grouped_gemm_mx: b must be [{G}, {N}, {K}] with [{G}, {N}, {K // MX_BLOCK}] scales")
+    if aq.shape[1] != K or aq.shape[0] < max_rows or as_.shape != (aq.shape[0], K // MX_BLOCK):
+        raise MoEKernelError("grouped_gemm_mx: a must be [>=max_rows, K] with [rows, K/32] scales")
+    rows = aq.shape[0]
+    if out_mx:
+        c = torch.empty((rows, N), dtype=torch.uint8, device=aq.device)
+        cs = torch.empty((rows, N // MX_BLOCK), dtype=torch.uint8, device=aq.device)
+    else:
+        c = torch.empty((rows, N), dtype=torch.bfloat16, device=aq.device)
+        cs = None
+    rc = lib().moe_grouped_gemm_mx(
+        _ptr(aq), _ptr(as_), _ptr(bq), _ptr(bs), _ptr(c), _ptr(cs), _ptr(offsets), G, int(max_rows), N, K,
+        int(epilogue), _ptr(bias), _stream())
+    _check(rc, "moe_grouped_gemm_mx")
+    return (c, cs) if out_mx else c
+
+
+def grouped_gemm_wgrad_mx(x, yq, ys, offsets, G, want_colsum=True):
+    """C_g = X_g^T deq(Y_g): x bf16 [rows, M], yq/ys MXFP8 [rows, N] -> fp32 [G, M, N] (+ colsum of x)."""
+    _need(x, torch.bfloat16, "x")
+    _need(yq, torch.uint8, "y")
+    _need(ys, torch.uint8, "y_scales")
+    M, N = x.shape[1], yq.shape[1]
+    c = torch.empty((G, M, N), dtype=torch.float32, device=x.device)
+    cs = torch.empty((G, M), dtype=torch.float32, device=x.device) if want_colsum else None
+    rc = lib().moe_grouped_gemm_wgrad_mx(
+        _ptr(x), _ptr(yq), _ptr(ys), _ptr(c), _ptr(cs), _ptr(offsets), G, M, N, _stream())
+    _check(rc, "moe_grouped_gemm_wgrad_mx")
     return c, cs
 
 

@@ -79,6 +79,54 @@ def expert_ffn_eager(xp, w1, b1, w2, b2, offsets, grad_scale=1.0):
     return out.to(xp.dtype)
 
 
+def mx_round(x: torch.Tensor) -> torch.Tensor:
+    """Quantize-dequantize through MXFP8 along the last dim (OCP e4m3, one E8M0
+    exponent per 32 elements; exponent rule of include/moe_hip.h), in fp32."""
+    K = x.shape[-1]
+    xb = x.float().reshape(*x.shape[:-1], K // 32, 32)
+    amax = xb.abs().amax(-1)
+    u = amax.view(torch.int32).long()
+    e = ((u >> 23) & 0xFF) - 127 - 8 + ((u & 0x7FFFFF) > 0x600000).long()
+    e = torch.where(amax == 0, torch.full_like(e, -127), e).clamp(-127, 127)
+    sc = torch.exp2(e.float()).unsqueeze(-1)
+    return ((xb / sc).to(torch.float8_e4m3fn).float() * sc).reshape(x.shape)
+
+
+class _ExpertMX(torch.autograd.Function):
+    """One expert's MXFP8 FFN on CPU tensors, with the HIP path's semantics
+    (ops._ExpertFFNMX): e4m3 operands forward, ReLU mask from the e4m3 H,
+    dgrad through the unquantized weights, weight grads on the e4m3 operands."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        xq = mx_round(x)
+        h = torch.relu(xq @ mx_round(w1).t() + b1.float()).to(torch.bfloat16).float()
+        hq = mx_round(h)
+        y = hq @ mx_round(w2).t() + b2.float()
+        ctx.save_for_backward(xq, hq, w1, w2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xq, hq, w1, w2 = ctx.saved_tensors
+        dy = dy.float()
+        dh = (dy @ w2.float()) * (hq > 0)
+        return dh @ w1.float(), dh.t() @ xq, dh.sum(0), dy.t() @ hq, dy.sum(0)
+
+
+def expert_ffn_mx_eager(xp, w1, b1, w2, b2, offsets, grad_scale=1.0):
+    if grad_scale != 1.0:
+        w1, b1, w2, b2 = (_ScaleGrad.apply(t, grad_scale) for t in (w1, b1, w2, b2))
+    out = torch.zeros((xp.shape[0], w2.shape[1]), dtype=torch.float32, device=xp.device)
+    off = [int(v) for v in offsets.tolist()]
+    for g in range(w1.shape[0]):
+        a, b = off[g], off[g + 1]
+        if b > a:
+            out = out.index_copy(0, torch.arange(a, b, device=xp.device),
+                                 _ExpertMX.apply(xp[a:b].float(), w1[g], b1[g], w2[g], b2[g]))
+    return out.to(xp.dtype)
+
+
 class _ScaleGrad(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, s):
@@ -100,10 +148,14 @@ def combine_eager(yp, w, pos, T):
     return y
 
 
-def moe_ffn_eager(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap):
+def moe_ffn_eager(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap,
+                  expert_dtype="bf16"):
     T = x.shape[0]
     xp, w, lb, z, pos, hist, offsets, rows = route_dispatch_eager(x, wg, ctx_bias, ctx_img, tokens_per_image, k,
                                                                   normalize, cap)
-    yp = expert_ffn_eager(xp, w1, b1, w2, b2, offsets)
+    if expert_dtype == "fp8":
+        yp = expert_ffn_mx_eager(xp, w1, b1, w2, b2, offsets)
+    else:
+        yp = expert_ffn_eager(xp, w1, b1, w2, b2, offsets)
     y = combine_eager(yp, w, pos, T)
     return y.to(x.dtype), lb, z, hist

@@ -39,6 +39,38 @@ class _AllToAll(torch.autograd.Function):
         return gi, None, None, None
 
 
+class _DispatchMX(torch.autograd.Function):
+    """MXFP8 dispatch exchange (config C5): the e4m3 rows and their exponents
+    cross the all-to-all (d + d/32 bytes per row instead of 2d) and are
+    reordered expert-major; the bf16 gradient of the rows (dXp) takes the
+    reverse path in backward.  ``carrier`` is the zero-stride autograd stand-in
+    of the rows (ops._RouteDispatchMX)."""
+
+    @staticmethod
+    def forward(ctx, carrier, xq, xs, send, recv, perm, inv, group):
+        n_send, R = sum(send), sum(recv)
+        qr = xq.new_empty((R, xq.shape[1]))
+        sr = xs.new_empty((R, xs.shape[1]))
+        dist.all_to_all_single(qr, xq[:n_send].contiguous(), output_split_sizes=recv, input_split_sizes=send,
+                               group=group)
+        dist.all_to_all_single(sr, xs[:n_send].contiguous(), output_split_sizes=recv, input_split_sizes=send,
+                               group=group)
+        ctx.send, ctx.recv, ctx.group, ctx.rows = send, recv, group, carrier.shape[0]
+        ctx.save_for_backward(inv)
+        ce = torch.zeros((1, 1), dtype=carrier.dtype, device=carrier.device).expand(R, carrier.shape[1])
+        ctx.mark_non_differentiable(qr, sr)
+        return ce, qr.index_select(0, perm), sr.index_select(0, perm)
+
+    @staticmethod
+    def backward(ctx, g, _q, _s):
+        (inv,) = ctx.saved_tensors
+        gr = g.index_select(0, inv).contiguous()
+        gi = g.new_zeros((ctx.rows, g.shape[1]))
+        dist.all_to_all_single(gi[:sum(ctx.send)], gr, output_split_sizes=ctx.send, input_split_sizes=ctx.recv,
+                               group=ctx.group)
+        return gi, None, None, None, None, None, None, None
+
+
 def expert_major_order(recv_mat: torch.Tensor):
     """recv_mat [W, El] (host) rows received from each source for each local
     expert, laid out source-major.  Returns (perm, offsets) with
@@ -68,14 +100,23 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap):
     group = layer.ep_group
     T = x.shape[0]
     dev = x.device
-    if x.is_cuda:
+    mx = x.is_cuda and cfg.expert_dtype == "fp8"
+    if mx:
+        from .ops import aux_losses, combine_hip as combine, expert_ffn_mx_hip, route_dispatch_mx_hip
+
+        xp, w, auxp, pos, hist, offsets, xq, xs, rows = route_dispatch_mx_hip(
+            x, layer.wg, ctx_bias, ctx_img, tokens_per_image, k, cfg.normalize, cap)
+        lb, z = aux_losses(auxp, hist, T, k)
+    elif x.is_cuda:
         from .ops import aux_losses, combine_hip as combine, expert_ffn_hip as expert_ffn, route_dispatch_hip
 
         xp, w, auxp, pos, hist, offsets, rows = route_dispatch_hip(x, layer.wg, ctx_bias, ctx_img, tokens_per_image,
                                                                    k, cfg.normalize, cap)
         lb, z = aux_losses(auxp, hist, T, k)
     else:
-        from .eager import combine_eager as combine, expert_ffn_eager as expert_ffn, route_dispatch_eager
+        from .eager import combine_eager as combine, expert_ffn_eager, expert_ffn_mx_eager, route_dispatch_eager
+
+        expert_ffn = expert_ffn_mx_eager if cfg.expert_dtype == "fp8" else expert_ffn_eager
 
         xp, w, lb, z, pos, hist, offsets, rows = route_dispatch_eager(x, layer.wg, ctx_bias, ctx_img,
                                                                       tokens_per_image, k, cfg.normalize, cap)
@@ -88,13 +129,20 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap):
     recv = [int(v) for v in recv_h.sum(1).tolist()]
     n_send, R = sum(send), sum(recv)
 
-    xr = _AllToAll.apply(xp[:n_send], send, recv, group)
     perm, offs_l = expert_major_order(recv_h)
     perm = perm.to(dev, non_blocking=True)
     inv = torch.empty_like(perm)
     inv[perm] = torch.arange(perm.numel(), device=dev)
-    xe = xr.index_select(0, perm)
     offs_l = offs_l.to(dev, non_blocking=True)
+    if mx:
+        ce, qe, se = _DispatchMX.apply(xp, xq, xs, send, recv, perm, inv, group)
+        ye = expert_ffn_mx_hip(ce, qe, se, layer.w1, layer.b1, layer.w2, layer.b2, offs_l, R, 1.0 / W) if R else \
+            x.new_zeros((0, x.shape[1]), dtype=torch.bfloat16)
+        yr = ye.index_select(0, inv)
+        yp = _AllToAll.apply(yr, recv, send, group)
+        return combine(yp, w, pos, T), lb, z, hist
+    xr = _AllToAll.apply(xp[:n_send], send, recv, group)
+    xe = xr.index_select(0, perm)
     if x.is_cuda:
         ye = expert_ffn(xe, layer.w1, layer.b1, layer.w2, layer.b2, offs_l, R, 1.0 / W) if R else \
             xe.new_zeros((0, x.shape[1]))

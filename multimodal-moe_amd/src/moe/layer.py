@@ -69,12 +69,12 @@ class MoEFFN(nn.Module):
             from .ops import moe_ffn_hip
 
             y, lb, z, hist = moe_ffn_hip(flat, self.wg, cb, self.w1, self.b1, self.w2, self.b2,
-                                         ci, L, cfg.top_k, cfg.normalize, cap)
+                                         ci, L, cfg.top_k, cfg.normalize, cap, cfg.expert_dtype)
         else:
             from .eager import moe_ffn_eager
 
             y, lb, z, hist = moe_ffn_eager(flat, self.wg, cb, self.w1, self.b1, self.w2, self.b2,
-                                           ci, L, cfg.top_k, cfg.normalize, cap)
+                                           ci, L, cfg.top_k, cfg.normalize, cap, cfg.expert_dtype)
         y = y.to(x.dtype)
         self.last_aux = (lb, z)
         self.last_hist = hist

@@ -71,6 +71,36 @@ class _RouteDispatch(torch.autograd.Function):
         return dx.to(xdtype), dwg, dcb, None, None, None, None, None, None
 
 
+class _RouteDispatchMX(torch.autograd.Function):
+    """_RouteDispatch with the MXFP8 permute (config C5): the routed rows leave
+    as e4m3 ``xq`` + E8M0 ``xs`` (non-differentiable), and a zero-stride bf16
+    ``carrier`` [rows, d] stands for the permuted rows in the autograd graph so
+    that dXp (from _ExpertFFNMX.backward) reaches the dispatch transpose."""
+
+    @staticmethod
+    def forward(ctx, x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, rows):
+        T, d = x.shape
+        E = wg.shape[0]
+        xb = x.to(torch.bfloat16).contiguous()
+        wg32 = wg.float().contiguous()
+        cb = ctx_bias.float().contiguous() if ctx_bias is not None else None
+        idx, w, probs, lse, lrank, bcnt, auxp = L.router_topk_fwd(xb, wg32, cb, ctx_img, tokens_per_image, k,
+                                                                   normalize)
+        rank_base, hist, offsets = L.route_scan(bcnt, cap)
+        xq, xs, pos = L.permute_fwd_mx(xb, idx, lrank, rank_base, offsets, E, cap, rows)
+        carrier = torch.zeros((1, 1), dtype=torch.bfloat16, device=x.device).expand(xq.shape[0], d)
+        ctx.save_for_backward(xb, wg32, idx, w, probs, lse, pos,
+                              ctx_img if ctx_img is not None else torch.empty(0))
+        ctx.meta = (T, d, E, int(normalize), tokens_per_image, cb is not None, x.dtype,
+                    ctx_bias.shape[0] if ctx_bias is not None else 0)
+        ctx.mark_non_differentiable(pos, hist, offsets, xq, xs)
+        return carrier, w, auxp, pos, hist, offsets, xq, xs
+
+    @staticmethod
+    def backward(ctx, d_xp, d_w, d_auxp, _p, _h, _o, _q, _s):
+        return _RouteDispatch.backward(ctx, d_xp, d_w, d_auxp, _p, _h, _o)
+
+
 class _ExpertFFN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xp, w1, b1, w2, b2, offsets, rows, grad_scale):
@@ -96,6 +126,42 @@ class _ExpertFFN(torch.autograd.Function):
             for t in (dW1, db1, dW2, db2):
                 t.mul_(s)
         return dxp, dW1, db1, dW2, db2, None, None, None
+
+
+class _ExpertFFNMX(torch.autograd.Function):
+    """MXFP8 expert FFN (config C5; include/moe_hip.h "MXFP8 expert path").
+    Forward: W1/W2 quantized per call; GEMM1 (e4m3 xq x e4m3 W1, +b1, ReLU)
+    writes H as MXFP8; GEMM2 (e4m3 H x e4m3 W2, +b2) writes bf16 Yp.
+    Backward: ReLU mask from the e4m3 H, dgrad through the bf16 weights,
+    weight gradients against the dequantised (exact) e4m3 H and xq."""
+
+    @staticmethod
+    def forward(ctx, carrier, xq, xs, w1, b1, w2, b2, offsets, rows, grad_scale):
+        G, F, d = w1.shape
+        w1b = w1.to(torch.bfloat16).contiguous()
+        w2b = w2.to(torch.bfloat16).contiguous()
+        w1q, w1s = L.quantize_mx(w1b)
+        w2q, w2s = L.quantize_mx(w2b)
+        hq, hs = L.grouped_gemm_mx(xq, xs, w1q, w1s, offsets, G, rows, F, d, L.EPI_BIAS_RELU,
+                                   bias=b1.float().contiguous(), out_mx=True)
+        yp = L.grouped_gemm_mx(hq, hs, w2q, w2s, offsets, G, rows, d, F, L.EPI_BIAS, bias=b2.float().contiguous())
+        ctx.save_for_backward(xq, xs, hq, hs, w1b, w2b, offsets)
+        ctx.meta = (G, F, d, rows, float(grad_scale))
+        return yp
+
+    @staticmethod
+    def backward(ctx, d_yp):
+        xq, xs, hq, hs, w1b, w2b, offsets = ctx.saved_tensors
+        G, F, d, rows, s = ctx.meta
+        dyp = d_yp.to(torch.bfloat16).contiguous()
+        dh = L.grouped_gemm(dyp, w2b, offsets, G, rows, F, d, 0, L.EPI_RELU_MASK_MX, aux=hq)
+        dW2, db2 = L.grouped_gemm_wgrad_mx(dyp, hq, hs, offsets, G)
+        dxp = L.grouped_gemm(dh, w1b, offsets, G, rows, d, F, 0, L.EPI_NONE)
+        dW1, db1 = L.grouped_gemm_wgrad_mx(dh, xq, xs, offsets, G)
+        if s != 1.0:
+            for t in (dW1, db1, dW2, db2):
+                t.mul_(s)
+        return dxp, None, None, dW1, db1, dW2, db2, None, None, None
 
 
 class _Combine(torch.autograd.Function):
@@ -129,30 +195,52 @@ def route_dispatch_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize,
                                 rows) + (rows,)
 
 
+def route_dispatch_mx_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap):
+    """-> (carrier, w, auxp, pos, hist, offsets, xq, xs, rows): MXFP8 dispatch."""
+    T = x.shape[0]
+    E = wg.shape[0]
+    rows = T * k if cap <= 0 else min(T * k, E * cap)
+    return _RouteDispatchMX.apply(x, wg, ctx_bias, ctx_img, int(tokens_per_image), int(k), bool(normalize),
+                                  int(cap), rows) + (rows,)
+
+
 def expert_ffn_hip(xp, w1, b1, w2, b2, offsets, rows, grad_scale=1.0):
     return _ExpertFFN.apply(xp, w1, b1, w2, b2, offsets, int(rows), grad_scale)
+
+
+def expert_ffn_mx_hip(carrier, xq, xs, w1, b1, w2, b2, offsets, rows, grad_scale=1.0):
+    return _ExpertFFNMX.apply(carrier, xq, xs, w1, b1, w2, b2, offsets, int(rows), grad_scale)
 
 
 def combine_hip(yp, w, pos, T):
     return _Combine.apply(yp, w, pos, int(T))
 
 
-def moe_ffn_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap):
+def moe_ffn_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap,
+                expert_dtype="bf16"):
     """Routed expert FFN of one layer on the GPU.
 
     x [T, d] (tokens of ``T // tokens_per_image`` images, image-major),
     wg [E, d], ctx_bias [C, E] or None, w1 [E, F, d], b1 [E, F], w2 [E, d, F],
-    b2 [E, d], ctx_img int32 [T // tokens_per_image].
+    b2 [E, d], ctx_img int32 [T // tokens_per_image].  expert_dtype "bf16" or
+    "fp8" (MXFP8 dispatch rows and expert GEMMs, config C5).
     Returns (y bf16 [T, d], lb_raw, z_raw, hist int32 [E]).
     """
     if not x.is_cuda:
         raise L.MoEKernelError("moe_ffn_hip needs GPU tensors")
     if ctx_bias is not None and ctx_img is None:
         raise L.MoEKernelError("ctx_bias given without ctx_img")
+    if expert_dtype not in ("bf16", "fp8"):
+        raise L.MoEKernelError(f"unknown expert_dtype {expert_dtype!r}")
     T = x.shape[0]
-    xp, w, auxp, pos, hist, offsets, rows = route_dispatch_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k,
-                                                               normalize, cap)
-    yp = expert_ffn_hip(xp, w1, b1, w2, b2, offsets, rows)
+    if expert_dtype == "fp8":
+        carrier, w, auxp, pos, hist, offsets, xq, xs, rows = route_dispatch_mx_hip(
+            x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap)
+        yp = expert_ffn_mx_hip(carrier, xq, xs, w1, b1, w2, b2, offsets, rows)
+    else:
+        xp, w, auxp, pos, hist, offsets, rows = route_dispatch_hip(x, wg, ctx_bias, ctx_img, tokens_per_image,
+                                                                   k, normalize, cap)
+        yp = expert_ffn_hip(xp, w1, b1, w2, b2, offsets, rows)
     y = combine_hip(yp, w, pos, T)
     lb, z = aux_losses(auxp, hist, T, k)
     return y, lb, z, hist

@@ -85,6 +85,72 @@ def round_bf16(a) -> np.ndarray:
     return out.astype(np.float64)
 
 
+# ----------------------------------------------------------------------------
+# MXFP8 emulation (config C5 fp8 experts; include/moe_hip.h "MXFP8 expert path")
+# OCP e4m3 elements, one E8M0 exponent per 32 consecutive elements of a row.
+# ----------------------------------------------------------------------------
+E4M3_MAX = 448.0
+MX_BLOCK = 32
+
+
+def mx_exponent(amax) -> np.ndarray:
+    """Smallest e with amax <= 448 * 2^e, from amax's fp32 bits (1.75 = 448/2^8),
+    clamped to the E8M0 range [-127, 127]; amax == 0 -> -127."""
+    a = np.asarray(amax, dtype=np.float32)
+    u = a.view(np.uint32).astype(np.int64)
+    e = ((u >> 23) & 0xFF) - 127 - 8 + ((u & 0x7FFFFF) > 0x600000).astype(np.int64)
+    e = np.where(a == 0, -127, e)
+    return np.clip(e, -127, 127)
+
+
+def e4m3_round(v) -> np.ndarray:
+    """Round |v| <= 448 to the nearest OCP e4m3 value (ties to even; subnormal
+    quantum 2^-9 below 2^-6)."""
+    v = np.asarray(v, np.float64)
+    a = np.abs(v)
+    _, ex = np.frexp(np.where(a > 0, a, 1.0))   # a = m 2^ex, m in [0.5, 1)
+    E = np.maximum(ex - 1, -6)
+    q = np.exp2(E - 3)
+    return np.round(v / q) * q
+
+
+def mx_quantize(x):
+    """x [..., K] (bf16-exact values) -> (e4m3 values [..., K] in block units,
+    exponents int [..., K/32]).  Dequantised value = q * 2^e."""
+    x = np.asarray(x, np.float64)
+    K = x.shape[-1]
+    xb = x.reshape(*x.shape[:-1], K // MX_BLOCK, MX_BLOCK)
+    e = mx_exponent(np.abs(xb).max(axis=-1))
+    q = e4m3_round(xb * np.exp2(-e)[..., None].astype(np.float64))
+    return q.reshape(x.shape), e
+
+
+def mx_dequantize(q, e) -> np.ndarray:
+    q = np.asarray(q, np.float64)
+    K = q.shape[-1]
+    qb = q.reshape(*q.shape[:-1], K // MX_BLOCK, MX_BLOCK)
+    return (qb * np.exp2(np.asarray(e, np.float64))[..., None]).reshape(q.shape)
+
+
+def mx_round(x) -> np.ndarray:
+    """Quantize-dequantize through MXFP8."""
+    return mx_dequantize(*mx_quantize(x))
+
+
+def e4m3_bytes(q) -> np.ndarray:
+    """OCP e4m3 encoding (uint8) of e4m3-exact values (|q| <= 448)."""
+    q = np.asarray(q, np.float64)
+    sign = (q < 0) | ((q == 0) & np.signbit(q))
+    a = np.abs(q)
+    _, ex = np.frexp(np.where(a > 0, a, 1.0))
+    E = ex - 1
+    normal = (a >= 2.0 ** -6)
+    exp_field = np.where(normal, E + 7, 0)
+    mant = np.where(normal, a / np.exp2(E) - 1.0, a / 2.0 ** -6) * 8.0
+    out = (sign.astype(np.int64) << 7) | (exp_field.astype(np.int64) << 3) | np.rint(mant).astype(np.int64)
+    return np.where(a == 0, sign.astype(np.int64) << 7, out).astype(np.uint8)
+
+
 def _maybe(a, on):
     return round_bf16(a) if on else np.asarray(a, dtype=np.float64)
 
@@ -157,19 +223,31 @@ def permute(x, pos, rows):
 # ----------------------------------------------------------------------------
 # a5: expert FFN
 # ----------------------------------------------------------------------------
-def expert_ffn(xp, offsets, w1, b1, w2, b2, emulate_bf16=False):
+def expert_ffn(xp, offsets, w1, b1, w2, b2, emulate_bf16=False, mx=False):
+    """Per expert H = relu(xp W1^T + b1), Yp = H W2^T + b2.
+
+    mx=True is the MXFP8 expert path (include/moe_hip.h): xp, W1, W2 and the
+    bf16-rounded H enter the GEMMs quantize-dequantized through MXFP8 (blocks
+    of 32 along each GEMM's K); the returned H is that MXFP8 H (what the
+    backward reads)."""
     rows = int(offsets[-1])
     E = w1.shape[0]
     d = w2.shape[1]
     F = w1.shape[1]
     H = np.zeros((rows, F))
     Y = np.zeros((rows, d))
+    if mx:
+        xp = mx_round(xp)
+        w1 = mx_round(w1)
+        w2 = mx_round(w2)
     for e in range(E):
         a, b = int(offsets[e]), int(offsets[e + 1])
         if b <= a:
             continue
         h = np.maximum(xp[a:b] @ np.asarray(w1[e], np.float64).T + b1[e], 0.0)
-        H[a:b] = _maybe(h, emulate_bf16)
+        H[a:b] = _maybe(h, emulate_bf16 or mx)
+        if mx:
+            H[a:b] = mx_round(H[a:b])
         Y[a:b] = _maybe(H[a:b] @ np.asarray(w2[e], np.float64).T + b2[e], emulate_bf16)
     return H, Y
 
@@ -217,9 +295,11 @@ class MoEState:
 
 
 def moe_forward(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k,
-                normalize=True, cap=0, emulate_bf16=False) -> MoEState:
+                normalize=True, cap=0, emulate_bf16=False, mx=False) -> MoEState:
     """Full routed FFN of one layer (a2-a6).  Shapes: x [T,d], wg [E,d],
-    ctx_bias [C,E] | None, w1 [E,F,d], b1 [E,F], w2 [E,d,F], b2 [E,d]."""
+    ctx_bias [C,E] | None, w1 [E,F,d], b1 [E,F], w2 [E,d,F], b2 [E,d].
+    mx=True: MXFP8 expert GEMMs (st.xp and st.H are then the MXFP8 values the
+    backward uses)."""
     E = np.asarray(wg).shape[0]
     x = _maybe(x, emulate_bf16)
     logits, probs, lse, idx, w = router_forward(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize)
@@ -228,7 +308,9 @@ def moe_forward(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k,
     if emulate_bf16:
         w1 = round_bf16(w1)
         w2 = round_bf16(w2)
-    H, Yp = expert_ffn(xp, offsets, w1, b1, w2, b2, emulate_bf16)
+    H, Yp = expert_ffn(xp, offsets, w1, b1, w2, b2, emulate_bf16, mx)
+    if mx:
+        xp = mx_round(xp)
     y = combine(Yp, pos, w, emulate_bf16)
     lb, z = aux_losses(probs, lse, hist, k)
     return MoEState(logits, probs, lse, idx, w, pos, hist, offsets, xp, H, Yp, y, lb, z)

@@ -19,7 +19,8 @@ def declared_symbols():
 def test_header_declares_the_expected_entry_points():
     syms = declared_symbols()
     for s in ["moe_router_topk_fwd", "moe_route_scan", "moe_permute_fwd", "moe_combine_fwd", "moe_combine_bwd",
-              "moe_token_bwd", "moe_grouped_gemm", "moe_grouped_gemm_wgrad", "moe_last_error"]:
+              "moe_token_bwd", "moe_grouped_gemm", "moe_grouped_gemm_wgrad", "moe_last_error",
+              "moe_quantize_mx", "moe_permute_fwd_mx", "moe_grouped_gemm_mx", "moe_grouped_gemm_wgrad_mx"]:
         assert s in syms
 
 
