@@ -49,10 +49,11 @@ PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec peak
 
 WORKLOADS = {
-    "c2": dict(spec="rtdetr-r50-moe8-top2", batch=8, desc="C2: RT-DETR-R50 + 8-expert top-2 MoE, bs=8/GPU, bf16"),
+    "c2": dict(spec="rtdetr-r50-moe8-top2", batch=8, desc="C2: RT-DETR-R50 + 8-expert top-2 MoE, bs=8/GPU, bf16",
+               dtype="bf16"),
     "c4": dict(spec="rtdetr-r50-moe16-top2-ep{N}", batch=8, single_ctx=True,
                desc="C4: 16-expert top-2, expert-parallel all-to-all, solar-context-binned batches"),
-    "c5": dict(spec="rtdetr-r50-moe32-top4-cf1.25-fp8", batch=16,
+    "c5": dict(spec="rtdetr-r50-moe32-top4-cf1.25-fp8", batch=16, dtype="bf16 + MXFP8 (e4m3) expert GEMMs",
                desc="C5: 32-expert top-4 fp8 experts, capacity factor 1.25, bs=16/GPU"),
 }
 
@@ -196,7 +197,8 @@ def cpu_baseline(spec, batch_img, img_h, img_w, target_s):
     return {"value": round(batch_img * n / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
             "sample": f"{n} timed fwd+bwd+AdamW steps (+1 warm-up) of {spec} at batch {batch_img}, "
                       f"{img_w}x{img_h} padded to 32, fp32 on {threads} host threads, {n_moe} MoE layers "
-                      f"computed by oracle/moe_oracle.py (float64 numpy)"}
+                      f"computed by oracle/moe_oracle.py (float64 numpy"
+                      f"{', MXFP8 expert GEMMs emulated' if 'fp8' in spec else ''})"}
 
 
 def main():
@@ -300,7 +302,7 @@ def main():
         result = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": wl.get("dtype", "bf16"),
             "data": "synthetic (ZOD-shaped batches resident in HBM, random-init weights)",
             "config": {"workload": wl["desc"], "arch": spec, "global_batch": world * batch,
                        "execution": "hipGraph fwd/bwd" if graphs else "eager",

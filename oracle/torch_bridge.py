@@ -14,10 +14,10 @@ from . import moe_oracle as O
 
 class _OracleMoE(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tpi, k, normalize, cap):
+    def forward(ctx, x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tpi, k, normalize, cap, mx=False):
         n = lambda t: None if t is None else t.detach().double().numpy()  # noqa: E731
         ci = None if ctx_img is None else ctx_img.numpy()
-        st = O.moe_forward(n(x), n(wg), n(ctx_bias), n(w1), n(b1), n(w2), n(b2), ci, tpi, k, normalize, cap)
+        st = O.moe_forward(n(x), n(wg), n(ctx_bias), n(w1), n(b1), n(w2), n(b2), ci, tpi, k, normalize, cap, mx=mx)
         ctx.st = st
         ctx.args = (n(x), n(wg), n(w1), n(w2), ci, tpi, 0 if ctx_bias is None else ctx_bias.shape[0], normalize)
         ctx.has_ctx = ctx_bias is not None
@@ -31,7 +31,7 @@ class _OracleMoE(torch.autograd.Function):
                            normalize)
         f = lambda a: None if a is None else torch.from_numpy(np.asarray(a)).to(dy.dtype)  # noqa: E731
         return (f(g["dx"]), f(g["dwg"]), f(g["dctx_bias"]) if ctx.has_ctx else None, f(g["dw1"]), f(g["db1"]),
-                f(g["dw2"]), f(g["db2"]), None, None, None, None, None)
+                f(g["dw2"]), f(g["db2"]), None, None, None, None, None, None)
 
 
 def _oracle_forward(self, x, ctx_img):
@@ -40,7 +40,7 @@ def _oracle_forward(self, x, ctx_img):
     cb = self.ctx_bias if (self.ctx_bias is not None and ctx_img is not None) else None
     y, lb, z = _OracleMoE.apply(x.reshape(B * L, d), self.wg, cb, self.w1, self.b1, self.w2, self.b2,
                                 ctx_img if cb is not None else None, L, cfg.top_k, cfg.normalize,
-                                cfg.capacity(B * L))
+                                cfg.capacity(B * L), cfg.expert_dtype == "fp8")
     self.last_aux = (lb, z)
     return y.view(B, L, d)
 

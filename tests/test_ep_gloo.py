@@ -1,7 +1,8 @@
 """Expert parallelism on CPU (gloo, world size 2, 4 experts -> 2 per rank):
 the EP layer reproduces the single-process layer with all experts -- outputs,
 input gradients, router gradients (after the DP mean) and each rank's expert
-gradients (after the 1/W scaling) -- on skewed, context-binned inputs."""
+gradients (after the 1/W scaling) -- on skewed, context-binned inputs, with
+bf16-path and fp8 (MXFP8-emulating, src/moe/eager.py) experts."""
 from __future__ import annotations
 
 import os
@@ -14,13 +15,13 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 ROOT = Path(__file__).resolve().parents[1]
-E, K, D, F, TPI = 4, 2, 16, 32, 12
+E, K, D, F, TPI = 4, 2, 32, 64, 12  # D, F multiples of the 32-element MX block
 
 
-def _cfg(ep):
+def _cfg(ep, dtype="bf16"):
     from src.moe.config import MoEConfig
 
-    return MoEConfig(num_experts=E, top_k=K, hidden=F, ep_size=ep, capacity_factor=0.0)
+    return MoEConfig(num_experts=E, top_k=K, hidden=F, ep_size=ep, capacity_factor=0.0, expert_dtype=dtype)
 
 
 def _inputs(rank):
@@ -31,7 +32,7 @@ def _inputs(rank):
     return x, ctx, dy
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, dtype):
     for p in (str(ROOT / "multimodal-moe_amd"), str(ROOT)):
         sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -40,7 +41,7 @@ def _worker(rank, world, port, out):
     from src.moe.layer import MoEFFN
 
     torch.manual_seed(0)
-    layer = MoEFFN(D, _cfg(world))
+    layer = MoEFFN(D, _cfg(world, dtype))
     x, ctx, dy = _inputs(rank)
     x.requires_grad_(True)
     y = layer(x, ctx)
@@ -58,18 +59,19 @@ def _worker(rank, world, port, out):
 
 
 @pytest.mark.slow
-def test_ep_gloo_world2_matches_single_process(tmp_path):
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_ep_gloo_world2_matches_single_process(tmp_path, dtype):
     import socket
 
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     W = 2
-    mp.spawn(_worker, args=(W, port, tmp_path), nprocs=W, join=True)
+    mp.spawn(_worker, args=(W, port, tmp_path, dtype), nprocs=W, join=True)
     from src.moe.layer import MoEFFN
 
     torch.manual_seed(0)
-    ref = MoEFFN(D, _cfg(1))
+    ref = MoEFFN(D, _cfg(1, dtype))
     El = E // W
     for r in range(W):
         got = torch.load(tmp_path / f"r{r}.pt", weights_only=True)

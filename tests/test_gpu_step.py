@@ -7,13 +7,13 @@ import torch
 DEV = "cuda"
 
 
-def _setup():
+def _setup(spec="rtdetr-r18-moe4-top2"):
     from src.rtdetr_moe.criterion import SetCriterion
     from src.rtdetr_moe.data import SyntheticZOD
     from src.rtdetr_moe.model import RTDETRMoE
 
     torch.manual_seed(0)
-    model = RTDETRMoE("rtdetr-r18-moe4-top2").to(DEV).to(memory_format=torch.channels_last)
+    model = RTDETRMoE(spec).to(DEV).to(memory_format=torch.channels_last)
     images, targets, ctx = SyntheticZOD(batch=2, img_h=256, img_w=320, seed=3).sample(DEV)
     images = images.contiguous(memory_format=torch.channels_last)
     targets = [{k: v.to(DEV) for k, v in t.items()} for t in targets]
@@ -56,3 +56,66 @@ def test_graphed_step_matches_eager(hip_lib):
     assert min(graph[1:]) < graph[0], graph
     for a, b in zip(eager, graph):
         assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (eager, graph)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graphs", [False, True])
+def test_fp8_experts_train_step(hip_lib, graphs):
+    """Config C5's expert path (32 experts, top-4, capacity factor 1.25, MXFP8
+    expert GEMMs) trains inside the full model, eager and as hipGraphs."""
+    from src.rtdetr_moe.step import TrainStep
+
+    model, crit, images, targets, ctx = _setup("rtdetr-r18-moe32-top4-cf1.25-fp8")
+    assert all(m.cfg.expert_dtype == "fp8" for m in model.moe_layers())
+    step = TrainStep(model, crit, images, ctx, graphs=graphs, world=1, precision="bf16", lr=1e-3)
+    losses = [float(step(images, ctx, targets, 4.0)) for _ in range(4)]
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(torch.tensor(losses))), losses
+    assert min(losses[1:]) < losses[0], losses
+    for m in model.moe_layers():
+        assert int(m.last_hist.sum()) > 0
+
+
+@pytest.mark.gpu
+def test_ep_fp8_exchange_world1(hip_lib, tmp_path):
+    """The expert-parallel MXFP8 dispatch (ep._DispatchMX: e4m3 rows + exponents
+    over all_to_all, bf16 dXp back) over a world-1 RCCL group reproduces the
+    single-GPU fp8 layer (same kernels, identity exchange)."""
+    import socket
+
+    import torch.distributed as dist
+
+    from src.moe.config import MoEConfig
+    from src.moe.ep import moe_ffn_ep
+    from src.moe.layer import MoEFFN
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        torch.manual_seed(0)
+        cfg = MoEConfig(num_experts=16, top_k=2, capacity_factor=1.25, expert_dtype="fp8")
+        layer = MoEFFN(256, cfg).to(DEV)
+        layer.ep_size = 1
+        x = torch.randn(4, 150, 256, device=DEV).to(torch.bfloat16)
+        ctx = torch.tensor([0, 1, 2, 3], dtype=torch.int32, device=DEV)
+        dy = torch.randn(4, 150, 256, device=DEV)
+        res = []
+        for ep in (False, True):
+            layer.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_(True)
+            if ep:
+                flat = xi.reshape(-1, 256)
+                y, lb, z, hist = moe_ffn_ep(layer, flat, layer.ctx_bias, ctx, 150, cfg.capacity(600))
+                y = y.view(4, 150, 256)
+            else:
+                y = layer(xi, ctx)
+                lb, z = layer.last_aux
+            ((y.float() * dy).sum() + 0.1 * lb + 0.01 * z).backward()
+            res.append((y.detach().float(), xi.grad.float(), layer.w1.grad.clone(), layer.wg.grad.clone()))
+        torch.cuda.synchronize()
+        for a, b in zip(res[0], res[1]):
+            torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3)
+    finally:
+        dist.destroy_process_group()
