@@ -148,6 +148,27 @@ def setup_dist(n_gpus):
     return world, rank, local
 
 
+def heartbeat(period=30.0):
+    """A daemon thread that prints to stderr every `period` s, so a long MIOpen
+    convolution search in the first steps is not mistaken for a hang."""
+    import threading
+
+    t0 = time.perf_counter()
+
+    def run():
+        while True:
+            time.sleep(period)
+            print(f"[bench] alive {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+
+
+def log(rank, msg):
+    """Progress to stderr (rank 0): long warm-ups stay visibly alive."""
+    if rank == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def build_model(spec, device, world):
     from src.rtdetr_moe.model import RTDETRMoE
 
@@ -204,6 +225,8 @@ def cpu_baseline(spec, batch_img, img_h, img_w, target_s):
 def main():
     args = parse_args()
     world, rank, local = setup_dist(args.gpus)
+    if rank == 0:
+        heartbeat()
     device = torch.device("cuda", local)
     wl = WORKLOADS[args.workload]
     spec = wl["spec"].format(N=world)
@@ -237,8 +260,11 @@ def main():
     step = TrainStep(model, SetCriterion(num_classes=1), images, ctx, graphs=graphs, world=world,
                      precision=args.precision, ddp_local=ddp_local)
 
-    for _ in range(args.warmup):
+    t_w = time.perf_counter()
+    for i in range(args.warmup):  # the first steps run MIOpen's convolution search (can take minutes)
         step(images, ctx, targets, num_boxes)
+        torch.cuda.synchronize()
+        log(rank, f"warm-up step {i + 1}/{args.warmup} done ({time.perf_counter() - t_w:.1f} s)")
     if timing and not graphs:
         L.TIMER.start()
     if world > 1:
@@ -251,6 +277,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    log(rank, f"timed {args.steps} steps: {1e3 * elapsed / args.steps:.2f} ms/step")
     phases = None
     if args.phase_timing:  # extra steps after the timed region, same execution mode
         step.phases = []
@@ -321,6 +348,7 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
+            log(rank, "timing the CPU baseline")
             try:
                 result["cpu_baseline"] = cpu_baseline(spec, 1, args.img_h, args.img_w, args.cpu_seconds)
             except Exception as e:  # report, never hide, a failed baseline

@@ -59,6 +59,7 @@ struct GemmParams {
   int lda, ldb, ldc;
   int G, M, N, K;
   int dbg;  // measurement only (moe_set_tuning "gemm_debug"): 1 = no C stores, 2 = no main loop
+  int xmap; // ROWS tile -> XCD map: 0 = row tiles round-robin over XCDs, 1 = contiguous chunk per XCD
 };
 
 // runtime tuning knobs (moe_set_tuning)
@@ -68,6 +69,7 @@ static int g_gemm_stages = 0;
 static int g_gemm_debug = 0;
 static int g_rows_bm = 0;   // 0 = by tile count, else 64 or 128
 static int g_wgrad_bm = 0;  // 0 = by tile count, else 64 or 128
+static int g_xcd_map = 0;   // 0 = per-shape choice, 1 = round-robin, 2 = contiguous chunks
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
@@ -143,7 +145,24 @@ struct Tile {
     if constexpr (MODE == MODE_ROWS) {
       const int ntn = p.N / BN;
       nt = slot % ntn;
-      const int rem = (slot / ntn) * 8 + xcd;  // global row-tile index
+      int rem = (slot / ntn) * 8 + xcd;  // global row-tile index (round-robin map)
+      if (p.xmap == 1) {
+        // contiguous map: XCD x owns row tiles [x C, (x+1) C), C = ceil(total / 8), so
+        // its L2 sees the weights of ~1-2 experts instead of all of them
+        int total = 0;
+        for (int c0 = 0; c0 < p.G; c0 += 64) {
+          const int gi = c0 + lane;
+          int tg = 0;
+          if (gi < p.G) tg = (p.offsets[gi + 1] - p.offsets[gi] + BM - 1) / BM;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) tg += __shfl_xor(tg, o, 64);
+          total += tg;
+        }
+        const int C = (total + 7) / 8;
+        const int r = slot / ntn;
+        if (r >= C) return false;
+        rem = xcd * C + r;
+      }
       int before = 0;                          // row tiles of the groups below chunk c0
       g = -1;
       for (int c0 = 0; c0 < p.G; c0 += 64) {
@@ -825,6 +844,7 @@ extern "C" int moe_set_tuning(const char* key, int value) {
   if (k == "gemm_debug" && value >= 0 && value <= 3) { g_gemm_debug = value; return 0; }
   if (k == "rows_bm" && (value == 0 || value == 64 || value == 128)) { g_rows_bm = value; return 0; }
   if (k == "wgrad_bm" && (value == 0 || value == 64 || value == 128)) { g_wgrad_bm = value; return 0; }
+  if (k == "xcd_map" && value >= 0 && value <= 2) { g_xcd_map = value; return 0; }
   return fail("moe_set_tuning: unknown key or value");
 }
 
@@ -847,6 +867,7 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
 
   GemmParams p{};
   p.dbg = g_gemm_debug;
+  p.xmap = g_xcd_map == 2 ? 1 : 0;
   p.a = static_cast<const uint16_t*>(a);
   p.b = static_cast<const uint16_t*>(b);
   p.c = c;
@@ -962,6 +983,7 @@ extern "C" int moe_grouped_gemm_mx(const void* a, const void* a_scales, const vo
   if (max_rows == 0) return 0;
   GemmParams p{};
   p.dbg = g_gemm_debug;
+  p.xmap = g_xcd_map == 2 ? 1 : 0;
   // e4m3 rows addressed as 16-bit pairs: the bf16 tile machinery moves [R][128 B] K-tiles
   p.a = static_cast<const uint16_t*>(a);
   p.b = static_cast<const uint16_t*>(b);

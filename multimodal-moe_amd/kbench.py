@@ -59,9 +59,15 @@ def setup(T, E, k, d, F, seed=0):
     dyp, dw = L.combine_bwd(dy, yp, pos, w)
     dh = L.grouped_gemm(dyp, w2, offsets, E, rows, F, d, 0, L.EPI_RELU_MASK, aux=h)
     dxp = L.grouped_gemm(dh, w1, offsets, E, rows, d, F, 0, L.EPI_NONE)
+    # MXFP8 expert path (C5 kernels) on the same routing
+    xq, xs, _ = L.permute_fwd_mx(x, idx, lrank, rank_base, offsets, E, 0, rows)
+    w1q, w1s = L.quantize_mx(w1)
+    w2q, w2s = L.quantize_mx(w2)
+    hq, hs = L.grouped_gemm_mx(xq, xs, w1q, w1s, offsets, E, rows, F, d, L.EPI_BIAS_RELU, bias=b1, out_mx=True)
     return dict(T=T, E=E, k=k, d=d, F=F, x=x, wg=wg, cb=cb, ci=ci, tpi=tpi, w1=w1, w2=w2, b1=b1, b2=b2, idx=idx,
                 w=w, probs=probs, lse=lse, lrank=lrank, bcnt=bcnt, rank_base=rank_base, offsets=offsets, rows=rows,
-                xp=xp, pos=pos, h=h, yp=yp, dy=dy, dyp=dyp, dw=dw, dh=dh, dxp=dxp)
+                xp=xp, pos=pos, h=h, yp=yp, dy=dy, dyp=dyp, dw=dw, dh=dh, dxp=dxp,
+                xq=xq, xs=xs, w1q=w1q, w1s=w1s, w2q=w2q, w2s=w2s, hq=hq, hs=hs)
 
 
 def kernels(c):
@@ -85,6 +91,20 @@ def kernels(c):
         ("gemm_dgrad1", lambda: L.grouped_gemm(c["dh"], c["w1"], c["offsets"], E, rows, d, F, 0, L.EPI_NONE),
          2.0 * A * F * d, 0),
         ("gemm_wgrad1", lambda: L.grouped_gemm_wgrad(c["dh"], c["xp"], c["offsets"], E), 2.0 * A * F * d, 0),
+        # MXFP8 (C5) variants: bytes are the algorithmic ones of the fp8 operands
+        ("permute_mx", lambda: L.permute_fwd_mx(c["x"], c["idx"], c["lrank"], c["rank_base"], c["offsets"], E, 0,
+                                                rows), 0, 512 * T + (256 + 8) * A + 12 * A),
+        ("quantize_w1_mx", lambda: L.quantize_mx(c["w1"]), 0, E * F * d * (2 + 1 + 1 / 32)),
+        ("gemm1_fwd_mx", lambda: L.grouped_gemm_mx(c["xq"], c["xs"], c["w1q"], c["w1s"], c["offsets"], E, rows, F, d,
+                                                   L.EPI_BIAS_RELU, bias=c["b1"], out_mx=True), 2.0 * A * F * d, 0),
+        ("gemm2_fwd_mx", lambda: L.grouped_gemm_mx(c["hq"], c["hs"], c["w2q"], c["w2s"], c["offsets"], E, rows, d, F,
+                                                   L.EPI_BIAS, bias=c["b2"]), 2.0 * A * F * d, 0),
+        ("gemm_dgrad2_mx", lambda: L.grouped_gemm(c["dyp"], c["w2"], c["offsets"], E, rows, F, d, 0,
+                                                  L.EPI_RELU_MASK_MX, aux=c["hq"]), 2.0 * A * F * d, 0),
+        ("gemm_wgrad2_mx", lambda: L.grouped_gemm_wgrad_mx(c["dyp"], c["hq"], c["hs"], c["offsets"], E),
+         2.0 * A * F * d, 0),
+        ("gemm_wgrad1_mx", lambda: L.grouped_gemm_wgrad_mx(c["dh"], c["xq"], c["xs"], c["offsets"], E),
+         2.0 * A * F * d, 0),
         ("token_bwd", lambda: L.token_bwd(c["dxp"], c["pos"], c["probs"], c["idx"], c["w"], c["dw"], c["lse"],
                                           None, None, c["wg"], True), 0, 512 * (A + T) + 4 * (2 * E + 3 * k) * T),
     ]
@@ -98,17 +118,24 @@ def main():
     ap.add_argument("--variants", default="0")
     ap.add_argument("--stages", default="0")
     ap.add_argument("--only", default="")
+    ap.add_argument("--config", choices=["c2", "c5"], default="c2", help="layer shapes (C2: E8 k2 bs8; C5: E32 k4 bs16)")
     ap.add_argument("--debug", default="0", help="comma list of gemm_debug modes (1 no C stores, 2 no main loop)")
     ap.add_argument("--bm", default="0", help="comma list of forced row-tile heights (0 = auto) for rows and wgrad")
+    ap.add_argument("--xcd", default="0", help="comma list of ROWS tile->XCD maps (0 auto, 1 round-robin, 2 contiguous)")
     a = ap.parse_args()
     L.lib()
-    configs = [(v, s, dbg, bm) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
+    configs = [(v, s, dbg, bm, xm) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
                for dbg in map(int, a.debug.split(",")) for bm in map(int, a.bm.split(","))
+               for xm in map(int, a.xcd.split(","))
                if not (v == 1 and s != int(a.stages.split(",")[0]))]
-    shapes = {"enc": setup(8 * 920, 8, 2, 256, 1024), "dec": setup(8 * 300, 8, 2, 256, 1024, seed=1)}
+    if a.config == "c5":  # 32 experts, top-4, bs 16 (no capacity drops here: cf only trims the tail)
+        shapes = {"enc": setup(16 * 920, 32, 4, 256, 1024), "dec": setup(16 * 300, 32, 4, 256, 1024, seed=1)}
+    else:
+        shapes = {"enc": setup(8 * 920, 8, 2, 256, 1024), "dec": setup(8 * 300, 8, 2, 256, 1024, seed=1)}
     res = {}
     for _ in range(a.rounds):
-        for (v, s, dbg, bm) in configs:
+        for (v, s, dbg, bm, xm) in configs:
+            L.set_tuning("xcd_map", xm)
             L.set_tuning("rows_bm", bm)
             L.set_tuning("wgrad_bm", bm)
             L.set_tuning("gemm_variant", v)
@@ -118,15 +145,17 @@ def main():
                 for name, fn, flops, byts in kernels(c):
                     if a.only and a.only not in name:
                         continue
-                    if not name.startswith("gemm") and (v, s, dbg, bm) != configs[0]:
+                    if not name.startswith("gemm") and (v, s, dbg, bm, xm) != configs[0]:
                         continue
-                    res.setdefault((name, sname, v, s, dbg, bm, flops, byts), []).append(timed(fn, a.reps))
+                    res.setdefault((name, sname, v, s, dbg, bm, xm, flops, byts), []).append(timed(fn, a.reps))
     L.set_tuning("gemm_debug", 0)
     L.set_tuning("rows_bm", 0)
     L.set_tuning("wgrad_bm", 0)
-    for (name, sname, v, s, dbg, bm, flops, byts), ts in res.items():
+    L.set_tuning("xcd_map", 0)
+    for (name, sname, v, s, dbg, bm, xm, flops, byts), ts in res.items():
         us = statistics.median(ts)
-        d = {"kernel": name, "shape": sname, "variant": v, "stages": s, "debug": dbg, "bm": bm, "us": round(us, 2),
+        d = {"kernel": name, "config": a.config, "shape": sname, "variant": v, "stages": s, "debug": dbg, "bm": bm,
+             "xcd": xm, "us": round(us, 2),
              "min_us": round(min(ts), 2)}
         if flops:
             d["tflops"] = round(flops / us / 1e6, 1)

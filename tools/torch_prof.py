@@ -36,6 +36,8 @@ def main():
     from src.rtdetr_moe.step import TrainStep
 
     L.lib()
+    bench.heartbeat()
+    torch.backends.cudnn.benchmark = True  # as bench.py (--conv-search)
     dev = torch.device("cuda", 0)
     model = bench.build_model(a.spec, dev, 1)
     data = SyntheticZOD(batch=a.batch, img_h=720, img_w=1280, seed=1000)
