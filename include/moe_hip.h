@@ -195,6 +195,18 @@ int rtdetr_msda_bwd(const void* value, const int32_t* shapes, const int32_t* sta
                     int Q, int H, int D, int L, int P, float* grad_value, float* grad_loc,
                     float* grad_attn, hipStream_t stream);
 
+/* ---- frozen-BatchNorm convolution epilogues of the backbone ----
+ * With frozen BN statistics, conv + BN = conv with per-channel scaled weights
+ * + a channel bias; these apply the bias with what follows it, in one pass
+ * over bf16 NHWC (channels_last) activations viewed as [M = B*H*W, C]:
+ *   rtdetr_bias_act_nhwc:      y = act(x + bias[c]), act 0 none / 1 ReLU (x == y allowed)
+ *   rtdetr_add_bias_relu_nhwc: y = relu(a + b + bias[c]) (bias may be NULL)
+ * bias fp32 [C]; C % 8 == 0. */
+int rtdetr_bias_act_nhwc(const void* x, const float* bias, long long M, int C, int act, void* y,
+                         hipStream_t stream);
+int rtdetr_add_bias_relu_nhwc(const void* a, const void* b, const float* bias, long long M, int C,
+                              void* y, hipStream_t stream);
+
 /* Process-wide tuning overrides (not thread-safe; set before launching).  By
  * default (0) every launch picks its own kernel variant, ring depth and tile
  * height from its shape; these force one (kernel benchmarks and tests):
@@ -212,7 +224,8 @@ int moe_set_tuning(const char* key, int value);
  * operand read once, every output written once) and flops (grouped GEMM:
  * 2 N K per routed row; 0 for the other kinds), with the routed row count read
  * back from the device offsets.  Kinds: 0 grouped GEMM, 1 permute/combine row
- * moves, 2 router, 3 route scan, 4 token backward, 5 deformable attention.
+ * moves, 2 router, 3 route scan, 4 token backward, 5 deformable attention,
+ * 6 MXFP8 weight quantizer, 7 backbone convolution epilogues.
  * Not thread-safe, not for graph capture.  enable(0|1) also clears; get()
  * waits for the record. */
 enum moe_prof_kind {
@@ -221,7 +234,9 @@ enum moe_prof_kind {
   MOE_PROF_ROUTER = 2,
   MOE_PROF_SCAN = 3,
   MOE_PROF_TOKEN_BWD = 4,
-  MOE_PROF_MSDA = 5
+  MOE_PROF_MSDA = 5,
+  MOE_PROF_QUANT = 6,
+  MOE_PROF_CONV_EPI = 7
 };
 int moe_profile_enable(int on);
 int moe_profile_count(void);

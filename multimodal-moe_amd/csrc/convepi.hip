@@ -1,0 +1,93 @@
+// Fused epilogues of the frozen-BatchNorm convolutions of the RT-DETR backbone
+// (the dense body around the MoE path).  With the BatchNorm
+// statistics frozen (rtdetrv2_r50vd `freeze_norm`), conv + BN is a convolution
+// with per-output-channel scaled weights plus a channel bias; these kernels
+// apply that bias together with what follows it in one pass over the NHWC
+// (channels_last) activation:
+//   bias_act:      y = act(x + bias[c])                  (branch2a / 2b: ReLU)
+//   add_bias_relu: y = relu(a + b + bias[c])             (block output: branch2c + shortcut)
+// bf16 storage, fp32 arithmetic, one rounding.  Each thread moves 16-B chunks
+// (8 channels); C is a multiple of 8, so a chunk never straddles a pixel.
+#include "moe_common.h"
+#include "prof.h"
+
+namespace moe {
+
+template <int ACT>
+__global__ __launch_bounds__(256) void bias_act_kernel(const uint4* __restrict__ x, const float* __restrict__ bias,
+                                                       long long nchunk, int cchunks, uint4* __restrict__ y) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nchunk; i += (long long)gridDim.x * 256) {
+    const int c0 = (int)(i % cchunks) * 8;
+    float v[8];
+    unpack8(x[i], v);
+    const float4 b0 = *reinterpret_cast<const float4*>(bias + c0);
+    const float4 b1 = *reinterpret_cast<const float4*>(bias + c0 + 4);
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+    v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    if constexpr (ACT == 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+    }
+    y[i] = pack8(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void add_bias_relu_kernel(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                            const float* __restrict__ bias, long long nchunk,
+                                                            int cchunks, uint4* __restrict__ y) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nchunk; i += (long long)gridDim.x * 256) {
+    const int c0 = (int)(i % cchunks) * 8;
+    float va[8], vb[8];
+    unpack8(a[i], va);
+    unpack8(b[i], vb);
+    float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (bias != nullptr) {
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + c0);
+      const float4 b1 = *reinterpret_cast<const float4*>(bias + c0 + 4);
+      bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+      bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) va[j] = fmaxf(va[j] + vb[j] + bb[j], 0.f);
+    y[i] = pack8(va);
+  }
+}
+
+}  // namespace moe
+
+using namespace moe;
+
+static int epi_grid(long long nchunk) {
+  // enough waves to fill 256 CUs several times over; grid-stride beyond that
+  long long g = (nchunk + 255) / 256;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+extern "C" int rtdetr_bias_act_nhwc(const void* x, const float* bias, long long M, int C, int act, void* y,
+                                    hipStream_t stream) {
+  if (C <= 0 || C % 8 != 0) return fail("bias_act: C must be a positive multiple of 8");
+  if (act < 0 || act > 1) return fail("bias_act: act must be 0 (none) or 1 (relu)");
+  if (bias == nullptr) return fail("bias_act: bias is required");
+  if (M <= 0) return 0;
+  const long long nchunk = M * (C / 8);
+  ProfScope prof(stream, PROF_CONV_EPI, 4.0 * M * C);
+  if (act == 1)
+    MOE_LAUNCH(prof, bias_act_kernel<1>, dim3(epi_grid(nchunk)), dim3(256), 0, stream,
+               static_cast<const uint4*>(x), bias, nchunk, C / 8, static_cast<uint4*>(y));
+  else
+    MOE_LAUNCH(prof, bias_act_kernel<0>, dim3(epi_grid(nchunk)), dim3(256), 0, stream,
+               static_cast<const uint4*>(x), bias, nchunk, C / 8, static_cast<uint4*>(y));
+  return check_launch("rtdetr_bias_act_nhwc");
+}
+
+extern "C" int rtdetr_add_bias_relu_nhwc(const void* a, const void* b, const float* bias, long long M, int C,
+                                         void* y, hipStream_t stream) {
+  if (C <= 0 || C % 8 != 0) return fail("add_bias_relu: C must be a positive multiple of 8");
+  if (M <= 0) return 0;
+  const long long nchunk = M * (C / 8);
+  ProfScope prof(stream, PROF_CONV_EPI, 6.0 * M * C);
+  MOE_LAUNCH(prof, add_bias_relu_kernel, dim3(epi_grid(nchunk)), dim3(256), 0, stream,
+             static_cast<const uint4*>(a), static_cast<const uint4*>(b), bias, nchunk, C / 8,
+             static_cast<uint4*>(y));
+  return check_launch("rtdetr_add_bias_relu_nhwc");
+}

@@ -83,7 +83,7 @@ extern "C" int moe_quantize_mx(const void* x, long long R, int K, void* q, void*
   if (R < 0) return fail("quantize_mx: R < 0");
   if (R == 0) return 0;
   // bytes: bf16 read, e4m3 + one scale byte per 32 written
-  ProfScope prof(stream, PROF_ROWMOVE, (double)R * K * (2.0 + 1.0 + 1.0 / 32.0));
+  ProfScope prof(stream, PROF_QUANT, (double)R * K * (2.0 + 1.0 + 1.0 / 32.0));
   MOE_LAUNCH(prof, quantize_mx_kernel, dim3(mx_grid(R)), dim3(256), 0, stream, static_cast<const uint16_t*>(x), R,
              K, static_cast<uint8_t*>(q), static_cast<uint8_t*>(scales));
   return check_launch("moe_quantize_mx");

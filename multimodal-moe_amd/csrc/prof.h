@@ -16,7 +16,16 @@
 
 namespace moe {
 
-enum ProfKind { PROF_GEMM = 0, PROF_ROWMOVE = 1, PROF_ROUTER = 2, PROF_SCAN = 3, PROF_TOKEN_BWD = 4, PROF_MSDA = 5 };
+enum ProfKind {
+  PROF_GEMM = 0,
+  PROF_ROWMOVE = 1,
+  PROF_ROUTER = 2,
+  PROF_SCAN = 3,
+  PROF_TOKEN_BWD = 4,
+  PROF_MSDA = 5,
+  PROF_QUANT = 6,
+  PROF_CONV_EPI = 7
+};
 
 class ProfScope {
  public:

@@ -40,6 +40,8 @@ SIGNATURES = {
     "moe_permute_fwd_mx": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_mx": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "moe_grouped_gemm_wgrad_mx": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "rtdetr_bias_act_nhwc": (_I, [_P, _P, ctypes.c_longlong, _I, _I, _P, _P]),
+    "rtdetr_add_bias_relu_nhwc": (_I, [_P, _P, _P, ctypes.c_longlong, _I, _P, _P]),
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_msda_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
@@ -89,7 +91,8 @@ def lib() -> ctypes.CDLL:
     return _LIB
 
 
-PROF_KINDS = {0: "grouped_gemm", 1: "dispatch", 2: "router", 3: "route_scan", 4: "token_bwd", 5: "msda"}
+PROF_KINDS = {0: "grouped_gemm", 1: "dispatch", 2: "router", 3: "route_scan", 4: "token_bwd", 5: "msda",
+              6: "mx_quant", 7: "conv_epilogue"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E
 
@@ -389,6 +392,49 @@ def grouped_gemm_wgrad_mx(x, yq, ys, offsets, G, want_colsum=True):
         _ptr(x), _ptr(yq), _ptr(ys), _ptr(c), _ptr(cs), _ptr(offsets), G, M, N, _stream())
     _check(rc, "moe_grouped_gemm_wgrad_mx")
     return c, cs
+
+
+def _nhwc_rows(t, name):
+    """[B, C, H, W] channels_last (or [M, C] contiguous) bf16 -> (M, C)."""
+    _need_dtype_dev(t, torch.bfloat16, name)
+    if t.dim() == 4:
+        if not t.is_contiguous(memory_format=torch.channels_last):
+            raise MoEKernelError(f"{name} must be channels_last")
+        B, C, H, W = t.shape
+        return B * H * W, C
+    if not t.is_contiguous():
+        raise MoEKernelError(f"{name} must be contiguous")
+    return t.shape[0], t.shape[1]
+
+
+def _need_dtype_dev(t, dtype, name):
+    if not t.is_cuda:
+        raise MoEKernelError(f"{name} must be a GPU tensor (HIP path has no CPU fallback)")
+    if t.dtype != dtype:
+        raise MoEKernelError(f"{name}: expected {dtype}, got {t.dtype}")
+
+
+def bias_act_nhwc(x, bias, relu, out=None):
+    """y = act(x + bias[c]) over a channels_last bf16 activation (out may be x)."""
+    M, C = _nhwc_rows(x, "x")
+    _need(bias, torch.float32, "bias")
+    y = out if out is not None else torch.empty_like(x)
+    _check(lib().rtdetr_bias_act_nhwc(_ptr(x), _ptr(bias), M, C, 1 if relu else 0, _ptr(y), _stream()),
+           "rtdetr_bias_act_nhwc")
+    return y
+
+
+def add_bias_relu_nhwc(a, b, bias):
+    """y = relu(a + b + bias[c]) over channels_last bf16 activations (bias may be None)."""
+    M, C = _nhwc_rows(a, "a")
+    if _nhwc_rows(b, "b") != (M, C):
+        raise MoEKernelError("add_bias_relu: a and b differ in shape")
+    if bias is not None:
+        _need(bias, torch.float32, "bias")
+    y = torch.empty_like(a)
+    _check(lib().rtdetr_add_bias_relu_nhwc(_ptr(a), _ptr(b), _ptr(bias), M, C, _ptr(y), _stream()),
+           "rtdetr_add_bias_relu_nhwc")
+    return y
 
 
 def msda_fwd(value, shapes, starts, loc, attn):

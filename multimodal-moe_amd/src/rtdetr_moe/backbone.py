@@ -14,6 +14,8 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
+from .fused import AddBiasReLU, BiasReLU
+
 _DEPTHS = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3], 50: [3, 4, 6, 3], 101: [3, 4, 23, 3]}
 
 
@@ -28,9 +30,12 @@ class FrozenBatchNorm2d(nn.Module):
         self.register_buffer("running_var", torch.ones(n))
         self.eps = eps
 
-    def forward(self, x):
+    def scale_shift(self):
         scale = self.weight * (self.running_var + self.eps).rsqrt()
-        shift = self.bias - self.running_mean * scale
+        return scale, self.bias - self.running_mean * scale
+
+    def forward(self, x):
+        scale, shift = self.scale_shift()
         # one fused multiply-add kernel (x * scale + shift)
         return torch.addcmul(shift.view(1, -1, 1, 1).to(x.dtype), x, scale.view(1, -1, 1, 1).to(x.dtype))
 
@@ -40,13 +45,32 @@ def _norm(n, frozen):
 
 
 class ConvNormLayer(nn.Module):
+    """Conv + BN + act.  With a frozen BN the BN folds into the convolution
+    (scaled weights) and its shift is applied with the activation by one fused
+    kernel (fused.BiasReLU); ``conv_shift`` leaves the shift to the caller
+    (the block output adds it together with the shortcut, fused.AddBiasReLU)."""
+
     def __init__(self, cin, cout, k, s, act=None, frozen=False):
         super().__init__()
         self.conv = nn.Conv2d(cin, cout, k, s, (k - 1) // 2, bias=False)
         self.norm = _norm(cout, frozen)
+        self.act_name = act
         self.act = nn.ReLU(inplace=True) if act == "relu" else (nn.SiLU(inplace=True) if act == "silu" else nn.Identity())
+        self.fold = frozen and act in (None, "relu")
+
+    def conv_shift(self, x):
+        """Frozen BN: (conv(x, W * scale), shift) -- the BN output minus its shift."""
+        scale, shift = self.norm.scale_shift()
+        w = self.conv.weight
+        w = (w.float() * scale.view(-1, 1, 1, 1)).to(w.dtype)  # one rounding of the folded weight
+        return F.conv2d(x, w, None, self.conv.stride, self.conv.padding), shift
 
     def forward(self, x):
+        if self.fold:
+            y, shift = self.conv_shift(x)
+            if self.act_name == "relu":
+                return BiasReLU.apply(y, shift)
+            return y + shift.view(1, -1, 1, 1).to(y.dtype)
         return self.act(self.norm(self.conv(x)))
 
 
@@ -73,6 +97,21 @@ class _Shortcut(nn.Module):
     def forward(self, x):
         return self.conv(avg_pool_2x2(x) if self.down else x)
 
+    def conv_shift(self, x):
+        return self.conv.conv_shift(avg_pool_2x2(x) if self.down else x)
+
+
+def _block_out(last, short, h, x):
+    """relu(last(h) + shortcut(x)).  With frozen BNs the two BN shifts join
+    the residual add and the ReLU in one fused kernel (fused.AddBiasReLU)."""
+    if last.fold and (short is None or short.conv.fold):
+        a, sa = last.conv_shift(h)
+        if short is None:
+            return AddBiasReLU.apply(a, x, sa)
+        b, sb = short.conv_shift(x)
+        return AddBiasReLU.apply(a, b, sa + sb)
+    return F.relu(last(h) + (x if short is None else short(x)))
+
 
 class BasicBlock(nn.Module):
     expansion = 1
@@ -84,8 +123,7 @@ class BasicBlock(nn.Module):
         self.branch2b = ConvNormLayer(cout, cout, 3, 1, None, frozen)
 
     def forward(self, x):
-        out = self.branch2b(self.branch2a(x))
-        return F.relu(out + (x if self.short is None else self.short(x)))
+        return _block_out(self.branch2b, self.short, self.branch2a(x), x)
 
 
 class BottleNeck(nn.Module):
@@ -100,8 +138,7 @@ class BottleNeck(nn.Module):
         self.short = None if shortcut else _Shortcut(cin, cout * 4, stride, frozen)
 
     def forward(self, x):
-        out = self.branch2c(self.branch2b(self.branch2a(x)))
-        return F.relu(out + (x if self.short is None else self.short(x)))
+        return _block_out(self.branch2c, self.short, self.branch2b(self.branch2a(x)), x)
 
 
 class PResNet(nn.Module):

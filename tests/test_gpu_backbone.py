@@ -1,0 +1,85 @@
+"""Frozen-BN convolution epilogues of the backbone (fused.BiasReLU /
+AddBiasReLU over libmoe_hip's rtdetr_*_nhwc kernels) on the GPU.
+Tolerances: the kernels are bit-exact against the same fp32 formula rounded
+once to bf16; the fused backbone (BN folded into the weights, bf16) follows
+the unfused one (conv, then frozen BN): its error against the same network
+in fp32 is no larger than the unfused bf16 network's (relative Frobenius:
+features x 1.5 + 2e-3; weight gradients, median over layers x 1.5 + 2e-3 and
+every layer x 3 + 5e-3) -- the two
+bf16 paths round at different points, so they are compared through the fp32
+reference rather than with each other."""
+from __future__ import annotations
+
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _cl(t):
+    return t.to(DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+
+def test_bias_act_and_add_bias_relu_exact(hip_lib):
+    from src.moe import _lib as L
+
+    g = torch.Generator().manual_seed(0)
+    a = _cl(torch.randn(3, 64, 17, 23, generator=g))
+    b = _cl(torch.randn(3, 64, 17, 23, generator=g))
+    bias = torch.randn(64, generator=g).to(DEV)
+    bc = bias.view(1, -1, 1, 1)
+    y = L.bias_act_nhwc(a, bias, True)
+    torch.testing.assert_close(y, (a.float() + bc).relu().to(torch.bfloat16), rtol=0, atol=0)
+    y0 = L.bias_act_nhwc(a, bias, False)
+    torch.testing.assert_close(y0, (a.float() + bc).to(torch.bfloat16), rtol=0, atol=0)
+    z = L.add_bias_relu_nhwc(a, b, bias)
+    torch.testing.assert_close(z, (a.float() + b.float() + bc).relu().to(torch.bfloat16), rtol=0, atol=0)
+    z0 = L.add_bias_relu_nhwc(a, b, None)
+    torch.testing.assert_close(z0, (a.float() + b.float()).relu().to(torch.bfloat16), rtol=0, atol=0)
+    xi = a.clone()
+    L.bias_act_nhwc(xi, bias, True, out=xi)  # in place
+    torch.testing.assert_close(xi, y, rtol=0, atol=0)
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("depth", [18, 50])
+def test_folded_backbone_matches_unfolded(hip_lib, depth):
+    from src.rtdetr_moe.backbone import ConvNormLayer, FrozenBatchNorm2d, PResNet
+
+    torch.manual_seed(0)
+    m = PResNet(depth)
+    for mod in m.modules():
+        if isinstance(mod, FrozenBatchNorm2d):
+            mod.weight.uniform_(0.5, 1.5)
+            mod.bias.normal_(0, 0.1)
+            mod.running_mean.normal_(0, 0.1)
+            mod.running_var.uniform_(0.5, 2.0)
+    m32 = copy.deepcopy(m).to(DEV).to(memory_format=torch.channels_last)  # fp32, unfused
+    for mod in m32.modules():
+        if isinstance(mod, ConvNormLayer):
+            mod.fold = False
+    m = m.to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    ref = copy.deepcopy(m)
+    for mod in ref.modules():
+        if isinstance(mod, ConvNormLayer):
+            mod.fold = False
+    x = _cl(torch.randn(2, 3, 256, 320))
+    outs, outs_r, outs_32 = m(x), ref(x), m32(x.float())
+    for a, b, c in zip(outs, outs_r, outs_32):
+        assert _rel(a, c) <= 1.5 * _rel(b, c) + 2e-3
+    for o in (outs, outs_r, outs_32):
+        sum(t.float().square().mean() for t in o).backward()
+    ef, eu = [], []
+    for (n, p), (_, q), (_, r) in zip(m.named_parameters(), ref.named_parameters(), m32.named_parameters()):
+        if p.grad is not None:
+            ef.append(_rel(p.grad, r.grad))
+            eu.append(_rel(q.grad, r.grad))
+            assert ef[-1] <= 3.0 * eu[-1] + 5e-3, (n, ef[-1], eu[-1])  # no layer grossly off
+    ef, eu = torch.tensor(ef), torch.tensor(eu)
+    assert float(ef.median()) <= 1.5 * float(eu.median()) + 2e-3, (float(ef.median()), float(eu.median()))
