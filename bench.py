@@ -129,6 +129,8 @@ def parse_args():
                          "ROCm 7.2 does not stamp timing events inside a graph (tools/graph_event_probe.py), so "
                          "with graphs the per-kernel roofline comes from --profile-steps eager steps run right "
                          "after the timed region")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="libmoe_hip tuning override (moe_set_tuning), repeatable; for A/B runs")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="graph mode: eager steps after the timed region that carry the kernel events")
     return ap.parse_args()
@@ -237,6 +239,9 @@ def main():
     from src.rtdetr_moe.data import SyntheticZOD
 
     L.lib()  # fail loudly if the HIP extension is missing
+    for kv in args.tune:
+        key, val = kv.split("=", 1)
+        L.set_tuning(key, int(val))
     from src.rtdetr_moe.criterion import SetCriterion
     from src.rtdetr_moe.step import TrainStep
 

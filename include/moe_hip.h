@@ -214,8 +214,55 @@ int rtdetr_add_bias_relu_nhwc(const void* a, const void* b, const float* bias, l
  *   "gemm_stages"  0 auto, 2..4 ring slots for variant 2
  *   "rows_bm", "wgrad_bm"  0 auto, 64 or 128 row-tile height
  *   "gemm_debug"   0; 1 = skip C stores, 2 = skip the main loop (time attribution only)
+ *   "xcd_map"      0 auto, 1 row tiles round-robin over XCDs, 2 contiguous chunk per XCD
+ *   "ksplit"       0 auto, 1 no split-K, 2..8 forced split-K factor (needs the workspace below)
  * Returns 0, or -1 for an unknown key/value. */
 int moe_set_tuning(const char* key, int value);
+
+/* Split-K workspace of the grouped GEMMs for the CURRENT device (caller-owned,
+ * kept alive while any launch or captured graph may use it).  When a launch's
+ * grid would leave CUs idle (ROWS: < 256 tiles with K >= 512; WGRAD: <= 512
+ * tiles), its K range is cut into slices run by separate workgroups of one
+ * XCD; each writes fp32 partials to `ws` and the last to arrive per tile
+ * (arrival counter in `counters`, which must be zero on registration and are
+ * left zero after every launch) sums them in slice order (deterministic) and
+ * applies the epilogue.  A launch whose slices do not fit `ws_bytes` or whose
+ * tile count exceeds n_counters runs unsplit; NULL/NULL unregisters.  Launches
+ * sharing one workspace must be stream-ordered.  "ksplit" in moe_set_tuning
+ * forces the factor (1 = off). */
+int moe_set_splitk_workspace(void* ws, size_t ws_bytes, int32_t* counters, int n_counters);
+
+/* Training-step optimizer (the bench step's AdamW; reference: Ultralytics'
+ * AdamW inside RTDETR.train, src/models/vision/rtdetr.py:82-94, with
+ * torch.optim.AdamW + torch.nn.utils.clip_grad_norm_ semantics) over flat
+ * fp32 master / exp_avg / exp_avg_sq buffers, reading each gradient where
+ * autograd left it.  `tensors`: device array of 48-B records
+ *   { const void* grad; uint16_t* bf16_weight_or_NULL; int64 numel;
+ *     int64 flat_offset (multiple of 8); int32 grad_dtype (0 bf16, 1 fp32,
+ *     2 no gradient: tensor skipped as torch.optim does);
+ *     int32 lr_group; int32 pad[2]; }
+ * `chunks`: device int32 pairs {tensor, chunk} covering every tensor in
+ * 2048-element chunks; `tensor_steps`: device int32 per tensor, the AdamW
+ * step count (zero-initialised; counted per tensor like torch.optim, so a
+ * tensor without a gradient neither moves nor advances).  Per step:
+ *   train_grad_sqnorm        partials[c] = sum of squares of chunk c
+ *   train_grad_norm_finalize coef[0] = ||g|| * inv_world,
+ *                            coef[1] = inv_world * min(1, max_norm / (coef[0] + 1e-6))
+ *                            (max_norm <= 0: no clip); fixed summation order;
+ *                            tensor_steps[i] += 1 for tensors with a gradient
+ *   train_adamw_step         g *= coef[1]; w *= 1 - lr wd; m = b1 m + (1-b1) g;
+ *                            v = b2 v + (1-b2) g^2; with t = tensor_steps[i]:
+ *                            w -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps);
+ *                            bf16 weight (if any) = RNE(w)
+ * lrs: HOST array of n_groups (1..4) learning rates. */
+int train_grad_sqnorm(const void* tensors, const int32_t* chunks, int n_chunks, float* partials,
+                      hipStream_t stream);
+int train_grad_norm_finalize(const float* partials, int n, float max_norm, float inv_world, float* coef,
+                             const void* tensors, int n_tensors, int32_t* tensor_steps, hipStream_t stream);
+int train_adamw_step(const void* tensors, const int32_t* chunks, int n_chunks, const float* coef,
+                     float* master, float* exp_avg, float* exp_avg_sq, const int32_t* tensor_steps,
+                     const float* lrs, int n_groups, float weight_decay, float beta1, float beta2, float eps,
+                     hipStream_t stream);
 
 /* Launch profiler (measurement only; no reference counterpart).
  * While enabled, every kernel launch of the library carries a hipEvent pair
@@ -225,7 +272,7 @@ int moe_set_tuning(const char* key, int value);
  * 2 N K per routed row; 0 for the other kinds), with the routed row count read
  * back from the device offsets.  Kinds: 0 grouped GEMM, 1 permute/combine row
  * moves, 2 router, 3 route scan, 4 token backward, 5 deformable attention,
- * 6 MXFP8 weight quantizer, 7 backbone convolution epilogues.
+ * 6 MXFP8 weight quantizer, 7 backbone convolution epilogues, 8 optimizer.
  * Not thread-safe, not for graph capture.  enable(0|1) also clears; get()
  * waits for the record. */
 enum moe_prof_kind {
@@ -236,7 +283,8 @@ enum moe_prof_kind {
   MOE_PROF_TOKEN_BWD = 4,
   MOE_PROF_MSDA = 5,
   MOE_PROF_QUANT = 6,
-  MOE_PROF_CONV_EPI = 7
+  MOE_PROF_CONV_EPI = 7,
+  MOE_PROF_OPTIM = 8
 };
 int moe_profile_enable(int on);
 int moe_profile_count(void);

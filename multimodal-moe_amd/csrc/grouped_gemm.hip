@@ -60,6 +60,17 @@ struct GemmParams {
   int G, M, N, K;
   int dbg;  // measurement only (moe_set_tuning "gemm_debug"): 1 = no C stores, 2 = no main loop
   int xmap; // ROWS tile -> XCD map: 0 = row tiles round-robin over XCDs, 1 = contiguous chunk per XCD
+  // split-K (ksplit > 1): the K range of every output tile is cut into ksplit
+  // slices run by ksplit workgroups on one XCD; each writes its fp32
+  // accumulators to ws, and the last to arrive (per-tile arrival counter in
+  // cnt, reset by that block) sums the slices in slice order -- deterministic
+  // -- and runs the normal epilogue.
+  // WGRAD: groups with fewer than split_min_kt K-tiles (64 rows) are not
+  // split -- slice 0 runs the whole group, the other slices exit at once.
+  int ksplit;
+  int split_min_kt;
+  float* ws;
+  int32_t* cnt;
 };
 
 // runtime tuning knobs (moe_set_tuning)
@@ -70,6 +81,16 @@ static int g_gemm_debug = 0;
 static int g_rows_bm = 0;   // 0 = by tile count, else 64 or 128
 static int g_wgrad_bm = 0;  // 0 = by tile count, else 64 or 128
 static int g_xcd_map = 0;   // 0 = per-shape choice, 1 = round-robin, 2 = contiguous chunks
+static int g_ksplit = 0;    // 0 = per-shape choice, else forced split-K factor (1 = off)
+
+// split-K workspace registered per device by the caller (moe_set_splitk_workspace)
+struct SplitWs {
+  float* ws = nullptr;
+  size_t ws_bytes = 0;
+  int32_t* cnt = nullptr;
+  int n_cnt = 0;
+};
+static SplitWs g_split_ws[64];
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
@@ -127,6 +148,7 @@ __device__ __forceinline__ float sum8(bf16x8 v) {
 template <int BM, int BN, bool B_K, int MODE>
 struct Tile {
   int g, mt, nt, row0, rows_g, m0, n0, a_row_lim, nk;
+  int split, nsplit, tile_id;  // split-K slice of this workgroup, slices of its tile, tile index
   const uint16_t* a_base;  // element (m0 or row0, k=0) of logical A
   const uint16_t* b_base;  // element (k=0, n0) of logical B
 
@@ -140,8 +162,16 @@ struct Tile {
   // group's offsets (one memory round trip per 64 groups, not one per group),
   // an inclusive lane scan of the tile counts and a ballot pick the group.
   __device__ __forceinline__ bool init(const GemmParams& p, int lane) {
-    const int L = blockIdx.x;
-    const int xcd = L & 7, slot = L >> 3;
+    // split-K: the ksplit slices of one tile are consecutive slots of one XCD
+    const int xcd = blockIdx.x & 7;
+    int slot = blockIdx.x >> 3;
+    split = 0;
+    nsplit = p.ksplit > 1 ? p.ksplit : 1;
+    if (p.ksplit > 1) {
+      split = slot % p.ksplit;
+      slot /= p.ksplit;
+    }
+    const int L = (slot << 3) | xcd;
     if constexpr (MODE == MODE_ROWS) {
       const int ntn = p.N / BN;
       nt = slot % ntn;
@@ -191,6 +221,7 @@ struct Tile {
         before += __shfl(incl, 63, 64);
       }
       if (g < 0) return false;  // beyond the last tile (grid is an upper bound)
+      tile_id = rem * ntn + nt;
     } else {
       const int ntn = p.N / BN;
       const int tpg = (p.M / BM) * ntn;  // tiles per group
@@ -207,6 +238,18 @@ struct Tile {
       nt = tile % ntn;
       row0 = p.offsets[g];
       rows_g = p.offsets[g + 1] - row0;
+      tile_id = g * tpg + tile;
+      if (nsplit > 1 && (rows_g + 63) / 64 < p.split_min_kt) {  // short group: slice 0 alone
+        if (split != 0) return false;
+        nsplit = 1;
+      }
+      if (nsplit > 1) {  // this slice's k-rows (the group's rows) start at row0
+        const int nkt = (rows_g + 63) / 64;
+        const int chunk = (nkt + p.ksplit - 1) / p.ksplit;
+        const int r0 = min(split * chunk, nkt) * 64;
+        row0 += r0;
+        rows_g = max(0, min(rows_g - r0, chunk * 64));
+      }
     }
     m0 = mt * BM;
     n0 = nt * BN;
@@ -216,6 +259,13 @@ struct Tile {
       const uint16_t* bg = p.b + (size_t)g * p.stride_b;
       b_base = B_K ? bg + (size_t)n0 * p.ldb : bg + n0;
       nk = p.K / 64;
+      if (p.ksplit > 1) {
+        const int chunk = (nk + p.ksplit - 1) / p.ksplit;
+        const int kt0 = min(split * chunk, nk);
+        nk = min(chunk, nk - kt0);
+        a_base += kt0 * 64;
+        b_base += B_K ? (size_t)kt0 * 64 : (size_t)kt0 * 64 * p.ldb;
+      }
     } else {
       a_base = p.a + (size_t)row0 * p.lda + m0;
       b_base = p.b + (size_t)row0 * p.ldb + n0;
@@ -451,6 +501,96 @@ __device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row
   }
 }
 
+// ---------------------------------------------------------------------------
+// split-K merge (p.ksplit > 1).  Every slice stores its accumulators (and
+// column-sum partials) as fp32 with agent-coherent stores (sc1: written
+// through to the coherence point, never parked dirty in one XCD's L2),
+// waits for them to complete, and bumps the tile's arrival counter; the last
+// slice to arrive resets the counter and replaces its registers by the sum of
+// all slices taken in slice order (its own from registers; the others by
+// agent-coherent loads), so the result does not depend on arrival order.
+// Returns true in that block only (it then runs the epilogue).
+// No __threadfence: its agent-scope release writes back the whole L2
+// (buffer_wbl2), which made every split launch 5-20x slower on MI355X.
+// Layout: component c of accumulator q at [(4 q + c) * 256 + tid] -- every
+// dword instruction of the block covers 1 KiB contiguous.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int TM, int TN, bool COLSUM>
+__device__ __forceinline__ bool splitk_merge(const GemmParams& p, int tile_id, int split,
+                                             f32x4 (&acc)[TM][TN], float (&csum)[TM], int tid) {
+  constexpr int NQ = TM * TN;
+  constexpr size_t PART = 256 * (NQ * 4 + (COLSUM ? TM : 0));  // floats per slice
+  __shared__ int s_arrived;
+  float* base = p.ws + (size_t)tile_id * p.ksplit * PART;
+  {
+    float* mine = base + (size_t)split * PART;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) st_agent(mine + ((i * TN + j) * 4 + c) * 256 + tid, acc[i][j][c]);
+    if constexpr (COLSUM) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) st_agent(mine + (NQ * 4 + i) * 256 + tid, csum[i]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slice stores have completed
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(p.cnt + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == p.ksplit - 1)  // ready for the next launch
+      __hip_atomic_store(p.cnt + tile_id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_arrived = old;
+  }
+  __syncthreads();
+  if (s_arrived != p.ksplit - 1) return false;
+  f32x4 tot[TM][TN];
+  float ctot[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    ctot[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int sl = 0; sl < p.ksplit; ++sl) {
+    if (sl == split) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if constexpr (COLSUM) ctot[i] += csum[i];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) tot[i][j] += acc[i][j];
+      }
+    } else {
+      const float* other = base + (size_t)sl * PART;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) tot[i][j][c] += ld_agent(other + ((i * TN + j) * 4 + c) * 256 + tid);
+      if constexpr (COLSUM) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) ctot[i] += ld_agent(other + (NQ * 4 + i) * 256 + tid);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    csum[i] = ctot[i];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = tot[i][j];
+  }
+  return true;
+}
+
 // MFMA work on one staged K-tile (2 k-steps of 32).
 template <int BM, int BN, bool A_K, bool B_K, bool COLSUM>
 __device__ __forceinline__ void compute_tile(const char* abuf, const char* bbuf,
@@ -650,6 +790,7 @@ __global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
     }
     __syncthreads();
   }
+  if (t.nsplit > 1 && !splitk_merge<TM, TN, COLSUM>(p, t.tile_id, t.split, acc, csum, tid)) return;
   epilogue<BM, BN, MODE, EPI, COLSUM>(p, t.g, t.row0,
                                       t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, lane, wm, wn);
 }
@@ -786,6 +927,7 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
     else compute_tile<BM, BN, A_K, B_K, COLSUM>(cur, cur + A_BYTES, acc, csum, lane, wm, wn);
   }
   static_assert(S * (BM + BN) * 64 * 2 >= BM * BN * (MODE == MODE_ROWS ? 2 : 4), "epilogue image exceeds LDS");
+  if (t.nsplit > 1 && !splitk_merge<TM, TN, COLSUM>(p, t.tile_id, t.split, acc, csum, tid)) return;
   epilogue_lds<BM, BN, MODE, EPI, COLSUM, FL>(p, t.g, t.row0, t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, smem,
                                               tid, lane, wm, wn);
 }
@@ -797,11 +939,12 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
 // -- including ones captured into a hipGraph -- make no attribute call.
 template <auto FN>
 static void allow_lds(size_t bytes) {
-  // (raised to the whole 160 KiB at once: the MX exponent stage makes the size depend on K)
+  // (raised to 159 KiB at once -- the MX exponent stage makes the size depend
+  // on K; 1 KiB is left for the kernels' static LDS, e.g. the split-K flag)
   static bool done = false;
   if (!done && bytes > 65536) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(FN), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+                              159 * 1024);
     done = true;
   }
 }
@@ -833,9 +976,46 @@ static void launch(const GemmParams& p, dim3 grid, hipStream_t s, const ProfScop
   }
 }
 
+// Split-K factor for a launch of `tiles` output tiles (grid before splitting,
+// a multiple of 8) with `nk` K-tiles per tile, when the caller registered a
+// workspace large enough for `part_floats` per slice; 1 = no split.
+static int pick_split(int want, long long tiles, long long part_floats) {
+  if (want <= 1) return 1;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
+  const SplitWs& w = g_split_ws[dev];
+  if (w.ws == nullptr || w.cnt == nullptr || tiles > w.n_cnt) return 1;
+  while (want > 1 && (size_t)tiles * want * part_floats * 4 > w.ws_bytes) --want;
+  return want;
+}
+
+static void bind_split(GemmParams& p, int S) {
+  p.ksplit = S;
+  if (S > 1) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    p.ws = g_split_ws[dev].ws;
+    p.cnt = g_split_ws[dev].cnt;
+  }
+}
+
 }  // namespace moe
 
 using namespace moe;
+
+extern "C" int moe_set_splitk_workspace(void* ws, size_t ws_bytes, int32_t* counters, int n_counters) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail("set_splitk_workspace: no device");
+  if ((ws == nullptr) != (counters == nullptr) || n_counters < 0)
+    return fail("set_splitk_workspace: ws and counters must both be set or both NULL");
+  if (ws != nullptr && (reinterpret_cast<uintptr_t>(ws) & 15) != 0)
+    return fail("set_splitk_workspace: ws must be 16-B aligned");
+  g_split_ws[dev].ws = static_cast<float*>(ws);
+  g_split_ws[dev].ws_bytes = ws ? ws_bytes : 0;
+  g_split_ws[dev].cnt = counters;
+  g_split_ws[dev].n_cnt = counters ? n_counters : 0;
+  return 0;
+}
 
 extern "C" int moe_set_tuning(const char* key, int value) {
   const std::string k = key ? key : "";
@@ -845,6 +1025,7 @@ extern "C" int moe_set_tuning(const char* key, int value) {
   if (k == "rows_bm" && (value == 0 || value == 64 || value == 128)) { g_rows_bm = value; return 0; }
   if (k == "wgrad_bm" && (value == 0 || value == 64 || value == 128)) { g_wgrad_bm = value; return 0; }
   if (k == "xcd_map" && value >= 0 && value <= 2) { g_xcd_map = value; return 0; }
+  if (k == "ksplit" && value >= 0 && value <= 8) { g_ksplit = value; return 0; }
   return fail("moe_set_tuning: unknown key or value");
 }
 
@@ -867,7 +1048,6 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
 
   GemmParams p{};
   p.dbg = g_gemm_debug;
-  p.xmap = g_xcd_map == 2 ? 1 : 0;
   p.a = static_cast<const uint16_t*>(a);
   p.b = static_cast<const uint16_t*>(b);
   p.c = c;
@@ -892,9 +1072,21 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
   const int nt = N / 128;
   const int BMsel = g_rows_bm ? g_rows_bm : 64;
   const int mtiles = ((max_rows + BMsel - 1) / BMsel + G + 7) / 8 * 8;  // padded to the XCD count
-  dim3 grid(mtiles * nt);
+  const long long tiles = (long long)mtiles * nt;
+  // tile -> XCD map: contiguous row-tile chunks per XCD (each L2 then holds
+  // ~1 expert's weights) for the decoder-sized dgrads (kbench: dH 11.3 -> 9.1
+  // us, dX 15.0 -> 12.0); round-robin elsewhere (the encoder shapes prefer it)
+  p.xmap = g_xcd_map ? (g_xcd_map == 2 ? 1 : 0) : ((!trans_b && mtiles <= 128) ? 1 : 0);
+  // split-K when the grid leaves CUs idle and K is long, for the dgrads
+  // (MN-contiguous B; kbench: decoder dX 15.0 -> 11.5 us with the map below;
+  // the K-contiguous forward GEMM2 only loses to the merge latency)
+  int want = g_ksplit ? g_ksplit : ((!trans_b && tiles < 256 && K / 64 >= 16) ? 2 : 1);
+  if (want > K / 64) want = K / 64;
+  const int S = pick_split(want, tiles, 256LL * (BMsel / 32) * (128 / 32) * 4);
+  bind_split(p, S);
+  dim3 grid(tiles * S);
   const int variant = g_gemm_variant ? g_gemm_variant : 2;
-  const int stages = g_gemm_stages ? g_gemm_stages : ((K >= 1024 && (long long)mtiles * nt < 256) ? 3 : 2);
+  const int stages = g_gemm_stages ? g_gemm_stages : ((K >= 1024 && tiles * S < 256) ? 3 : 2);
   // algorithmic bytes: weights + bias once; per routed row A (K), C (N) and the relu-mask operand (N)
   const bool has_bias = epilogue == MOE_EPI_BIAS || epilogue == MOE_EPI_BIAS_RELU;
   const double mask_bytes = epilogue == MOE_EPI_RELU_MASK ? 2.0 * N : (epilogue == MOE_EPI_RELU_MASK_MX ? 1.0 * N : 0.0);
@@ -950,17 +1142,35 @@ extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, f
   const bool big = M % 128 == 0 && g_wgrad_bm == 128;
   const int variant = g_gemm_variant ? g_gemm_variant : 1;
   const int stages = g_gemm_stages ? g_gemm_stages : 2;
-  const int gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
+  int gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
+  const int bmw = big ? 128 : 64;
+  // split-K over each group's rows: the output (G M N) is too small a grid to
+  // fill the chip with K = the whole group
+  {
+    const long long tpg = (long long)(M / bmw) * ntn;
+    long long tiles = tpg * gpad;
+    // (kbench: encoder dW 30.0 -> 25.6 us; decoder groups of ~600 rows are
+    // not split -- split_min_kt, 1536 rows -- the merge latency outweighs the overlap)
+    const int want = g_ksplit ? g_ksplit : (tiles <= 512 ? 2 : 1);
+    p.split_min_kt = g_ksplit ? 0 : 24;
+    if (want > 1 && tiles % 8 != 0) {  // split grids map 8-slot XCD rows: pad the group count
+      gpad = (G + 7) / 8 * 8;
+      tiles = tpg * gpad;
+    }
+    const int S = pick_split(want, tiles, 256LL * (bmw / 32) * 4 * 4 + 256LL * (bmw / 32));
+    bind_split(p, S);
+    if (S == 1) gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
+  }
   // algorithmic bytes: fp32 C (+ colsum) once; per routed row one row of X (M) and of Y (N)
   ProfScope prof(stream, PROF_GEMM, 4.0 * G * M * N + (colsum ? 4.0 * G * M : 0.0), true, 2.0 * (M + N),
                  2.0 * M * N);
   p.prof_rows = prof.rows_slot();
   if (big) {
-    dim3 grid((M / 128) * ntn * gpad);
+    dim3 grid((M / 128) * ntn * gpad * p.ksplit);
     if (colsum) launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream, prof, variant, stages);
     else launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream, prof, variant, stages);
   } else {
-    dim3 grid((M / 64) * ntn * gpad);
+    dim3 grid((M / 64) * ntn * gpad * p.ksplit);
     if (colsum) launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream, prof, variant, stages);
     else launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream, prof, variant, stages);
   }

@@ -24,7 +24,8 @@ enum ProfKind {
   PROF_TOKEN_BWD = 4,
   PROF_MSDA = 5,
   PROF_QUANT = 6,
-  PROF_CONV_EPI = 7
+  PROF_CONV_EPI = 7,
+  PROF_OPTIM = 8
 };
 
 class ProfScope {

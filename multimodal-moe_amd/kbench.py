@@ -122,11 +122,12 @@ def main():
     ap.add_argument("--debug", default="0", help="comma list of gemm_debug modes (1 no C stores, 2 no main loop)")
     ap.add_argument("--bm", default="0", help="comma list of forced row-tile heights (0 = auto) for rows and wgrad")
     ap.add_argument("--xcd", default="0", help="comma list of ROWS tile->XCD maps (0 auto, 1 round-robin, 2 contiguous)")
+    ap.add_argument("--ksplit", default="0", help="comma list of split-K factors (0 auto, 1 off, 2..8 forced)")
     a = ap.parse_args()
     L.lib()
-    configs = [(v, s, dbg, bm, xm) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
+    configs = [(v, s, dbg, bm, xm, ks) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
                for dbg in map(int, a.debug.split(",")) for bm in map(int, a.bm.split(","))
-               for xm in map(int, a.xcd.split(","))
+               for xm in map(int, a.xcd.split(",")) for ks in map(int, a.ksplit.split(","))
                if not (v == 1 and s != int(a.stages.split(",")[0]))]
     if a.config == "c5":  # 32 experts, top-4, bs 16 (no capacity drops here: cf only trims the tail)
         shapes = {"enc": setup(16 * 920, 32, 4, 256, 1024), "dec": setup(16 * 300, 32, 4, 256, 1024, seed=1)}
@@ -134,7 +135,8 @@ def main():
         shapes = {"enc": setup(8 * 920, 8, 2, 256, 1024), "dec": setup(8 * 300, 8, 2, 256, 1024, seed=1)}
     res = {}
     for _ in range(a.rounds):
-        for (v, s, dbg, bm, xm) in configs:
+        for (v, s, dbg, bm, xm, ks) in configs:
+            L.set_tuning("ksplit", ks)
             L.set_tuning("xcd_map", xm)
             L.set_tuning("rows_bm", bm)
             L.set_tuning("wgrad_bm", bm)
@@ -145,17 +147,18 @@ def main():
                 for name, fn, flops, byts in kernels(c):
                     if a.only and a.only not in name:
                         continue
-                    if not name.startswith("gemm") and (v, s, dbg, bm, xm) != configs[0]:
+                    if not name.startswith("gemm") and (v, s, dbg, bm, xm, ks) != configs[0]:
                         continue
-                    res.setdefault((name, sname, v, s, dbg, bm, xm, flops, byts), []).append(timed(fn, a.reps))
+                    res.setdefault((name, sname, v, s, dbg, bm, xm, ks, flops, byts), []).append(timed(fn, a.reps))
+    L.set_tuning("ksplit", 0)
     L.set_tuning("gemm_debug", 0)
     L.set_tuning("rows_bm", 0)
     L.set_tuning("wgrad_bm", 0)
     L.set_tuning("xcd_map", 0)
-    for (name, sname, v, s, dbg, bm, xm, flops, byts), ts in res.items():
+    for (name, sname, v, s, dbg, bm, xm, ks, flops, byts), ts in res.items():
         us = statistics.median(ts)
         d = {"kernel": name, "config": a.config, "shape": sname, "variant": v, "stages": s, "debug": dbg, "bm": bm,
-             "xcd": xm, "us": round(us, 2),
+             "xcd": xm, "ksplit": ks, "us": round(us, 2),
              "min_us": round(min(ts), 2)}
         if flops:
             d["tflops"] = round(flops / us / 1e6, 1)

@@ -45,6 +45,10 @@ SIGNATURES = {
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_msda_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
+    "moe_set_splitk_workspace": (_I, [_P, ctypes.c_size_t, _P, _I]),
+    "train_grad_sqnorm": (_I, [_P, _P, _I, _P, _P]),
+    "train_grad_norm_finalize": (_I, [_P, _I, _F, _F, _P, _P, _I, _P, _P]),
+    "train_adamw_step": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _P]),
     "moe_profile_enable": (_I, [_I]),
     "moe_profile_count": (_I, []),
     "moe_profile_get": (_I, [_I, _P, _P, _P, _P]),
@@ -92,7 +96,7 @@ def lib() -> ctypes.CDLL:
 
 
 PROF_KINDS = {0: "grouped_gemm", 1: "dispatch", 2: "router", 3: "route_scan", 4: "token_bwd", 5: "msda",
-              6: "mx_quant", 7: "conv_epilogue"}
+              6: "mx_quant", 7: "conv_epilogue", 8: "optimizer"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E
 
@@ -197,6 +201,28 @@ def _need(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
 # ---------------------------------------------------------------------------
 def set_tuning(key: str, value: int) -> None:
     _check(lib().moe_set_tuning(key.encode(), int(value)), f"moe_set_tuning({key}={value})")
+
+
+# Split-K workspace of the grouped GEMMs (moe_set_splitk_workspace), one per
+# device, registered on first use outside graph capture and kept alive for the
+# process (captured graphs bake its address in).  64 MiB of fp32 slices covers
+# every C2-C5 split launch; a launch whose slices do not fit runs unsplit.
+SPLITK_WS_BYTES = 64 << 20
+SPLITK_COUNTERS = 1 << 16
+_SPLIT_WS: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
+
+
+def ensure_splitk_workspace(device: torch.device) -> None:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx in _SPLIT_WS or torch.cuda.is_current_stream_capturing():
+        return
+    with torch.cuda.device(idx):
+        ws = torch.empty(SPLITK_WS_BYTES // 4, dtype=torch.float32, device=f"cuda:{idx}")
+        cnt = torch.zeros(SPLITK_COUNTERS, dtype=torch.int32, device=f"cuda:{idx}")
+        torch.cuda.current_stream().synchronize()  # counters are zero before any launch reads them
+        _check(lib().moe_set_splitk_workspace(_ptr(ws), SPLITK_WS_BYTES, _ptr(cnt), SPLITK_COUNTERS),
+               "moe_set_splitk_workspace")
+    _SPLIT_WS[idx] = (ws, cnt)
 
 
 def router_num_blocks(T: int) -> int:
@@ -309,6 +335,7 @@ def grouped_gemm(a, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None,
     if a.shape[1] != K or a.shape[0] < max_rows:
         raise MoEKernelError("grouped_gemm: a must be [>=max_rows, K]")
     c = out if out is not None else torch.empty((a.shape[0], N), dtype=torch.bfloat16, device=a.device)
+    ensure_splitk_workspace(a.device)
     rc = lib().moe_grouped_gemm(
         MOE_BF16, _ptr(a), _ptr(b), _ptr(c), _ptr(offsets), G, int(max_rows), N, K, int(trans_b),
         int(epilogue), _ptr(bias), _ptr(aux), None, _stream())
@@ -322,6 +349,7 @@ def grouped_gemm_wgrad(x, y, offsets, G, want_colsum=True):
     M, N = x.shape[1], y.shape[1]
     c = torch.empty((G, M, N), dtype=torch.float32, device=x.device)
     cs = torch.empty((G, M), dtype=torch.float32, device=x.device) if want_colsum else None
+    ensure_splitk_workspace(x.device)
     rc = lib().moe_grouped_gemm_wgrad(
         MOE_BF16, _ptr(x), _ptr(y), _ptr(c), _ptr(cs), _ptr(offsets), G, M, N, _stream())
     _check(rc, "moe_grouped_gemm_wgrad")

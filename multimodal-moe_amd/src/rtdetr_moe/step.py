@@ -159,11 +159,12 @@ class TrainStep:
              master copies in the optimizer, no autocast: no per-layer weight
              casts in the forward nor grad casts in the backward (about 1,700
              cast ops per C2 step under autocast, most of the host time of an
-             eager step); after backward the bf16 grads are copied into the
-             masters' fp32 grads (multi-tensor copy), AdamW updates the
-             masters, and the masters are copied back into the bf16 weights;
-      "amp"  -- fp32 parameters under bf16 autocast.
-    On CPU the model runs in fp32."""
+             eager step); the optimizer (optim.FlatAdamW: gradient clip +
+             AdamW in three HIP launches) reads the bf16 grads, updates the
+             flat fp32 masters and rewrites the bf16 weights;
+      "amp"  -- fp32 parameters under bf16 autocast (same optimizer).
+    On CPU the model runs in fp32 with torch.optim.AdamW and
+    clip_grad_norm_ (the semantics FlatAdamW restates)."""
 
     def __init__(self, model: RTDETRMoE, criterion, images, ctx, *, lr=1e-4, lr_backbone=1e-5,
                  weight_decay=1e-4, clip_norm=0.1, graphs=True, ddp_local=None, world=1, precision="bf16"):
@@ -176,23 +177,23 @@ class TrainStep:
         self.precision = precision if images.is_cuda else "fp32"
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
         self.params = [p for _, p in named]
-        self.lowp, self.master = [], []
-        opt_of = {id(p): p for p in self.params}  # model param -> tensor the optimizer updates
         if self.precision == "bf16":
             for p in gemm_params(model):
                 p.data = p.data.to(torch.bfloat16)
-                if p.requires_grad:
-                    m = p.detach().float().clone()
-                    m.grad = torch.zeros_like(m)
-                    self.lowp.append(p)
-                    self.master.append(m)
-                    opt_of[id(p)] = m
-        bb = [opt_of[id(p)] for n, p in named if n.startswith("backbone.")]
-        rest = [opt_of[id(p)] for n, p in named if not n.startswith("backbone.")]
-        self.opt_params = bb + rest
-        fused = images.is_cuda
-        self.opt = torch.optim.AdamW([{"params": bb, "lr": lr_backbone}, {"params": rest, "lr": lr}], lr=lr,
-                                     weight_decay=weight_decay, fused=fused)
+        bb = [p for n, p in named if n.startswith("backbone.")]
+        rest = [p for n, p in named if not n.startswith("backbone.")]
+        if images.is_cuda:
+            # flat fp32 masters + moments, clip + AdamW + bf16 weight refresh in
+            # three HIP launches (optim.py); fp32 parameters become views of
+            # their master segment -- before any graph capture bakes addresses
+            from .optim import FlatAdamW
+
+            self.opt = FlatAdamW([(bb, lr_backbone), (rest, lr)], weight_decay=weight_decay, clip_norm=clip_norm)
+            self.opt_params = None
+        else:
+            self.opt_params = bb + rest
+            self.opt = torch.optim.AdamW([{"params": bb, "lr": lr_backbone}, {"params": rest, "lr": lr}], lr=lr,
+                                         weight_decay=weight_decay)
         self.flat = FlatOutputs(model)
         self.dp_params = [p for p in self.params if not getattr(p, "expert_parallel", False)]
         images = self._cast_in(images)
@@ -216,17 +217,6 @@ class TrainStep:
     def _cast_in(self, images):
         return images.to(torch.bfloat16) if self.precision == "bf16" else images
 
-    def _grads_to_master(self):
-        src, dst = [], []
-        for p, m in zip(self.lowp, self.master):
-            if p.grad is None:
-                m.grad.zero_()
-            else:
-                src.append(p.grad)
-                dst.append(m.grad)
-        if src:
-            torch._foreach_copy_(dst, src)
-
     def use_eager(self):
         """Leave graph mode (bench.py's kernel-profiling steps): later steps run
         the model eagerly; parameter grads go back to autograd allocation."""
@@ -239,26 +229,31 @@ class TrainStep:
                 p.grad = None
 
     def _allreduce_grads(self):
-        """Data-parallel mean of the static gradient buffers (graph mode, world >
-        1): one flat buffer per dtype, gathered and scattered by multi-tensor
-        copies, one RCCL all_reduce each."""
+        """Data-parallel gradient sum (graph mode, world > 1): the static
+        gradient buffers are gathered into one flat buffer per dtype by
+        multi-tensor copies and summed with one RCCL all_reduce each; the
+        optimizer reads the flat buffers (views, in parameter order) and divides
+        by the world size inside its kernels.  Returns the gradient list."""
         if getattr(self, "_flat_grads", None) is None:
             groups = {}
-            for p in self.dp_params:
-                groups.setdefault(p.grad.dtype, []).append(p.grad)
+            for i, p in enumerate(self.dp_params):
+                groups.setdefault(p.grad.dtype, []).append(i)
             self._flat_grads = []
-            for dt, gs in groups.items():
+            self._reduced = [None] * len(self.dp_params)
+            for dt, idx in groups.items():
+                gs = [self.dp_params[i].grad for i in idx]
                 flat = torch.empty(sum(g.numel() for g in gs), dtype=dt, device=gs[0].device)
                 views, off = [], 0
-                for g in gs:
-                    views.append(flat[off:off + g.numel()].view_as(g))
+                for i, g in zip(idx, gs):
+                    v = flat[off:off + g.numel()].view_as(g)
+                    views.append(v)
+                    self._reduced[i] = v
                     off += g.numel()
                 self._flat_grads.append((flat, views, gs))
         for flat, views, gs in self._flat_grads:
             torch._foreach_copy_(views, gs)
             dist.all_reduce(flat)
-            flat.div_(self.world)
-            torch._foreach_copy_(gs, views)
+        return self._reduced
 
     def _mark(self, name):
         if self.phases is not None:
@@ -280,16 +275,15 @@ class TrainStep:
         self._mark("criterion")
         loss.backward()
         self._mark("backward")
-        if self.graphs and self.world > 1:
-            self._allreduce_grads()
-        if self.lowp:
-            self._grads_to_master()
-        if self.clip_norm > 0:
-            torch.nn.utils.clip_grad_norm_(self.opt_params, self.clip_norm, foreach=True)
-        self.opt.step()
-        if self.lowp:
-            with torch.no_grad():
-                torch._foreach_copy_(self.lowp, self.master)
+        if self.opt_params is None:  # GPU: FlatAdamW (clip inside)
+            if self.graphs and self.world > 1:
+                self.opt.step(self._allreduce_grads(), inv_world=1.0 / self.world)
+            else:
+                self.opt.step()
+        else:
+            if self.clip_norm > 0:
+                torch.nn.utils.clip_grad_norm_(self.opt_params, self.clip_norm, foreach=True)
+            self.opt.step()
         self._mark("optimizer")
         return loss.detach()
 

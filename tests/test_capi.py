@@ -13,14 +13,15 @@ HEADER = ROOT / "include" / "moe_hip.h"
 def declared_symbols():
     text = HEADER.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b((?:moe|rtdetr)_[a-z0-9_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b((?:moe|rtdetr|train)_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_header_declares_the_expected_entry_points():
     syms = declared_symbols()
     for s in ["moe_router_topk_fwd", "moe_route_scan", "moe_permute_fwd", "moe_combine_fwd", "moe_combine_bwd",
               "moe_token_bwd", "moe_grouped_gemm", "moe_grouped_gemm_wgrad", "moe_last_error",
-              "moe_quantize_mx", "moe_permute_fwd_mx", "moe_grouped_gemm_mx", "moe_grouped_gemm_wgrad_mx"]:
+              "moe_quantize_mx", "moe_permute_fwd_mx", "moe_grouped_gemm_mx", "moe_grouped_gemm_wgrad_mx",
+              "moe_set_splitk_workspace", "train_grad_sqnorm", "train_grad_norm_finalize", "train_adamw_step"]:
         assert s in syms
 
 

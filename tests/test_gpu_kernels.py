@@ -87,19 +87,27 @@ def _int_tensor(rng, shape, lo=-3, hi=4):
     return rng.integers(lo, hi, size=shape).astype(np.float64)
 
 
-GEMM_CFGS = [(0, 0), (1, 2), (2, 2), (2, 3), (2, 4)]  # (gemm_variant, gemm_stages); 0 = per-shape choice
+# (gemm_variant, gemm_stages, ksplit); 0 = per-shape choice, ksplit 1 = no split-K
+GEMM_CFGS = [(0, 0, 0), (0, 0, 1), (1, 2, 1), (2, 2, 1), (2, 3, 1), (2, 4, 1),
+             (1, 2, 2), (2, 2, 3), (2, 3, 4), (1, 2, 5)]
 
 
 @pytest.fixture
 def gemm_cfg(request, hip_lib):
     from src.moe import _lib as L
 
-    v, s = request.param
+    v, s, ks = request.param
     L.set_tuning("gemm_variant", v)
     L.set_tuning("gemm_stages", s)
+    L.set_tuning("ksplit", ks)
     yield request.param
     L.set_tuning("gemm_variant", 0)  # back to the per-shape choice
     L.set_tuning("gemm_stages", 0)
+    L.set_tuning("ksplit", 0)
+    # split-K arrival counters are left at zero by every launch
+    torch.cuda.synchronize()
+    for _ws, cnt in L._SPLIT_WS.values():
+        assert int(cnt.abs().sum()) == 0
 
 
 @pytest.mark.parametrize("gemm_cfg", GEMM_CFGS, indirect=True)
@@ -140,7 +148,7 @@ def test_grouped_gemm_exact(gemm_cfg, trans_b, rows_per_group, N, K):
 
 
 @pytest.mark.parametrize("gemm_cfg", GEMM_CFGS, indirect=True)
-@pytest.mark.parametrize("rows_per_group", [[0, 1, 63, 64, 65, 200, 0, 130], [700, 0, 33]])
+@pytest.mark.parametrize("rows_per_group", [[0, 1, 63, 64, 65, 200, 0, 130], [700, 0, 33], [1500, 40, 0, 1100]])
 @pytest.mark.parametrize("M,N", [(256, 1024), (1024, 256), (64, 128)])
 def test_grouped_gemm_wgrad_exact(gemm_cfg, rows_per_group, M, N):
     from src.moe import _lib as L

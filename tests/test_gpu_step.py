@@ -34,10 +34,19 @@ def test_train_step_precisions(hip_lib, precision):
     assert min(losses[1:]) < losses[0], losses  # same batch: the loss must go down
     w1 = model.decoder.dec_score_head[0].weight
     assert not torch.equal(w1.detach().float(), w0)
+    from src.rtdetr_moe.optim import _storage_flat
+
+    n_bf16 = 0
+    for p in step.opt.params:
+        m = step.opt.master_of(p)
+        if p.dtype == torch.bfloat16:  # bf16 weights are the rounded masters
+            n_bf16 += 1
+            assert torch.equal(_storage_flat(p.detach()), m.to(torch.bfloat16))
+        else:  # fp32 weights are their masters
+            assert _storage_flat(p.detach()).data_ptr() == m.data_ptr()
+    assert (n_bf16 > 0) == (precision == "bf16")
     if precision == "bf16":
         assert w1.dtype == torch.bfloat16
-        for p, m in zip(step.lowp, step.master):  # bf16 weights are the rounded masters
-            assert torch.equal(p.detach(), m.to(torch.bfloat16))
 
 
 @pytest.mark.gpu
