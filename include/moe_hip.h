@@ -232,6 +232,19 @@ int moe_set_tuning(const char* key, int value);
  * forces the factor (1 = off). */
 int moe_set_splitk_workspace(void* ws, size_t ws_bytes, int32_t* counters, int n_counters);
 
+/* Hungarian matching of the set criterion on the device (the reference's
+ * RT-DETR loss matches with scipy.optimize.linear_sum_assignment on the host).
+ * cost fp32 [S][B][Q][M]: S prediction sets, B images, Q queries, M padded
+ * targets of which the first n_valid[b] are real (n_valid int32 [B], <= Q).
+ * assign int32 [S][B][M] <- query matched to each real target, -1 for the
+ * padding: the assignment scipy 1.15's linear_sum_assignment returns for
+ * cost[s][b][:, :n] (same algorithm, arithmetic and tie rule).  *status is
+ * set to 1 (n_valid > Q or > M) or 2 (non-finite costs) on failure, else left
+ * untouched (zero it before the first launch).  One 64-lane workgroup per
+ * (s, b); Q <= 4096, M <= 1024 within 64 KiB of LDS. */
+int rtdetr_hungarian_match(const float* cost, const int32_t* n_valid, int S, int B, int Q, int M,
+                           int32_t* assign, int32_t* status, hipStream_t stream);
+
 /* Training-step optimizer (the bench step's AdamW; reference: Ultralytics'
  * AdamW inside RTDETR.train, src/models/vision/rtdetr.py:82-94, with
  * torch.optim.AdamW + torch.nn.utils.clip_grad_norm_ semantics) over flat
@@ -272,7 +285,8 @@ int train_adamw_step(const void* tensors, const int32_t* chunks, int n_chunks, c
  * 2 N K per routed row; 0 for the other kinds), with the routed row count read
  * back from the device offsets.  Kinds: 0 grouped GEMM, 1 permute/combine row
  * moves, 2 router, 3 route scan, 4 token backward, 5 deformable attention,
- * 6 MXFP8 weight quantizer, 7 backbone convolution epilogues, 8 optimizer.
+ * 6 MXFP8 weight quantizer, 7 backbone convolution epilogues, 8 optimizer,
+ * 9 Hungarian matching.
  * Not thread-safe, not for graph capture.  enable(0|1) also clears; get()
  * waits for the record. */
 enum moe_prof_kind {
@@ -284,7 +298,8 @@ enum moe_prof_kind {
   MOE_PROF_MSDA = 5,
   MOE_PROF_QUANT = 6,
   MOE_PROF_CONV_EPI = 7,
-  MOE_PROF_OPTIM = 8
+  MOE_PROF_OPTIM = 8,
+  MOE_PROF_MATCH = 9
 };
 int moe_profile_enable(int on);
 int moe_profile_count(void);

@@ -25,7 +25,8 @@ enum ProfKind {
   PROF_MSDA = 5,
   PROF_QUANT = 6,
   PROF_CONV_EPI = 7,
-  PROF_OPTIM = 8
+  PROF_OPTIM = 8,
+  PROF_MATCH = 9
 };
 
 class ProfScope {

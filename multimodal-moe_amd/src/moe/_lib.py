@@ -46,6 +46,7 @@ SIGNATURES = {
     "rtdetr_msda_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "moe_set_splitk_workspace": (_I, [_P, ctypes.c_size_t, _P, _I]),
+    "rtdetr_hungarian_match": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "train_grad_sqnorm": (_I, [_P, _P, _I, _P, _P]),
     "train_grad_norm_finalize": (_I, [_P, _I, _F, _F, _P, _P, _I, _P, _P]),
     "train_adamw_step": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _P]),
@@ -96,7 +97,7 @@ def lib() -> ctypes.CDLL:
 
 
 PROF_KINDS = {0: "grouped_gemm", 1: "dispatch", 2: "router", 3: "route_scan", 4: "token_bwd", 5: "msda",
-              6: "mx_quant", 7: "conv_epilogue", 8: "optimizer"}
+              6: "mx_quant", 7: "conv_epilogue", 8: "optimizer", 9: "matcher"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E
 
@@ -341,6 +342,22 @@ def grouped_gemm(a, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None,
         int(epilogue), _ptr(bias), _ptr(aux), None, _stream())
     _check(rc, "moe_grouped_gemm")
     return c
+
+
+def hungarian_match(cost, n_valid, status=None):
+    """cost fp32 [S, B, Q, M] (queries x padded targets), n_valid int32 [B] ->
+    assign int32 [S, B, M]: the query scipy's linear_sum_assignment matches to
+    each real target, -1 for padding.  ``status`` (int32 [1], zeroed by the
+    caller) records failures without a host sync."""
+    _need(cost, torch.float32, "cost")
+    _need(n_valid, torch.int32, "n_valid")
+    S, B, Q, M = cost.shape
+    assign = torch.empty((S, B, M), dtype=torch.int32, device=cost.device)
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=cost.device)
+    rc = lib().rtdetr_hungarian_match(_ptr(cost), _ptr(n_valid), S, B, Q, M, _ptr(assign), _ptr(status), _stream())
+    _check(rc, "rtdetr_hungarian_match")
+    return assign
 
 
 def grouped_gemm_wgrad(x, y, offsets, G, want_colsum=True):
