@@ -131,6 +131,10 @@ def parse_args():
                          "after the timed region")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="libmoe_hip tuning override (moe_set_tuning), repeatable; for A/B runs")
+    ap.add_argument("--step-graph", action=argparse.BooleanOptionalAction, default=True,
+                    help="graph mode: capture forward + criterion (GPU Hungarian matcher) + backward as ONE "
+                         "hipGraph (default); --no-step-graph: forward and backward graphs around a host-matched "
+                         "criterion")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="graph mode: eager steps after the timed region that carry the kernel events")
     return ap.parse_args()
@@ -263,7 +267,8 @@ def main():
     timing = not args.no_kernel_timing
     ddp_local = local if (world > 1 and not graphs) else None
     step = TrainStep(model, SetCriterion(num_classes=1), images, ctx, graphs=graphs, world=world,
-                     precision=args.precision, ddp_local=ddp_local)
+                     precision=args.precision, ddp_local=ddp_local,
+                     targets=targets if args.step_graph else None, num_boxes=num_boxes)
 
     t_w = time.perf_counter()
     for i in range(args.warmup):  # the first steps run MIOpen's convolution search (can take minutes)
@@ -337,7 +342,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": wl.get("dtype", "bf16"),
             "data": "synthetic (ZOD-shaped batches resident in HBM, random-init weights)",
             "config": {"workload": wl["desc"], "arch": spec, "global_batch": world * batch,
-                       "execution": "hipGraph fwd/bwd" if graphs else "eager",
+                       "execution": ("hipGraph: forward + criterion (GPU matcher) + backward" if args.step_graph
+                                     else "hipGraph fwd/bwd") if graphs else "eager",
                        "precision": "bf16 weights + fp32 master" if args.precision == "bf16" else "bf16 autocast",
                        "img": f"{args.img_w}x{args.img_h} (padded to {data.pad_w}x{data.pad_h})",
                        "parallelism": f"dp{world}" if "ep" not in spec else f"dp{world}+ep{world}"},

@@ -209,6 +209,111 @@ class SetCriterion(nn.Module):
         return losses
 
 
+    def forward_padded(self, outputs, tgt_boxes, tgt_labels, n_valid, num_boxes, status=None):
+        """The same losses as ``forward`` with fixed shapes and no host round
+        trip, so the whole training step can be one hipGraph: targets padded to
+        M per image (``tgt_boxes`` [B, M, 4] cxcywh, ``tgt_labels`` [B, M],
+        ``n_valid`` int32 [B]; padding must be finite boxes), ``num_boxes`` a
+        device scalar, and the Hungarian matching on the GPU
+        (``rtdetr_hungarian_match``: scipy's linear_sum_assignment restated,
+        same pairs).  ``status`` (int32 [1]) collects matcher failures."""
+        from ..moe import _lib as L
+
+        sets = self._sets(outputs)
+        logits = torch.stack([o["pred_logits"] for _, o in sets]).float()  # [S, B, Q, C]
+        boxes = torch.stack([o["pred_boxes"] for _, o in sets]).float()    # [S, B, Q, 4]
+        S, B, Q, C = logits.shape
+        M = tgt_boxes.shape[1]
+        dev = logits.device
+        tb = tgt_boxes.float()
+        lab = tgt_labels.long().clamp(0, C - 1)
+        valid = torch.arange(M, device=dev)[None, :] < n_valid[:, None]  # [B, M]
+        m = self.matcher
+        with torch.no_grad():  # matching cost (HungarianMatcher.match_many's, per image)
+            p = logits.sigmoid().gather(3, lab[None, :, None, :].expand(S, B, Q, M))
+            neg = (1 - m.alpha) * p ** m.gamma * (-(1 - p + 1e-8).log())
+            pos = m.alpha * (1 - p) ** m.gamma * (-(p + 1e-8).log())
+            c_bbox = (boxes[:, :, :, None, :] - tb[None, :, None, :, :]).abs().sum(-1)
+            c_giou = -_pairwise_giou(box_cxcywh_to_xyxy(boxes)[:, :, :, None, :],
+                                     box_cxcywh_to_xyxy(tb)[None, :, None, :, :])
+            cost = m.cost_bbox * c_bbox + m.cost_class * (pos - neg) + m.cost_giou * c_giou
+            assign = L.hungarian_match(cost.contiguous(), n_valid.to(torch.int32).contiguous(), status)
+        q = assign.clamp(min=0).long()  # [S, B, M]
+        mask = valid[None].expand(S, B, M).to(logits.dtype)
+        src = boxes.gather(2, q[..., None].expand(S, B, M, 4))
+        tgt = tb[None].expand(S, B, M, 4)
+        iou, giou = _paired_iou_giou(box_cxcywh_to_xyxy(src).reshape(-1, 4), box_cxcywh_to_xyxy(tgt).reshape(-1, 4))
+        iou, giou = iou.view(S, B, M), giou.view(S, B, M)
+        l1 = ((src - tgt).abs().sum(-1) * mask).sum((1, 2)) / num_boxes
+        lg = ((1.0 - giou) * mask).sum((1, 2)) / num_boxes
+        # VFL targets: the padding writes into an extra query slot, sliced away
+        qe = torch.where(valid[None], q, torch.full_like(q, Q))
+        si = torch.arange(S, device=dev)[:, None, None].expand(S, B, M)
+        bi = torch.arange(B, device=dev)[None, :, None].expand(S, B, M)
+        ci = lab[None].expand(S, B, M)
+        score = torch.zeros((S, B, Q + 1, C), dtype=logits.dtype, device=dev)
+        onehot = torch.zeros_like(score)
+        score.index_put_((si, bi, qe, ci), iou.detach() * mask)
+        onehot.index_put_((si, bi, qe, ci), mask)
+        score, onehot = score[:, :, :Q], onehot[:, :, :Q]
+        pred = logits.sigmoid().detach()
+        weight = self.alpha * pred.pow(self.gamma) * (1 - onehot) + score
+        vfl = F.binary_cross_entropy_with_logits(logits, score, weight=weight, reduction="none")
+        vfl = vfl.mean(2).sum((1, 2)) * Q / num_boxes  # [S]
+        losses = {}
+        for s_, (suffix, _) in enumerate(sets):
+            losses["loss_vfl" + suffix] = vfl[s_] * self.w["loss_vfl"]
+            losses["loss_bbox" + suffix] = l1[s_] * self.w["loss_bbox"]
+            losses["loss_giou" + suffix] = lg[s_] * self.w["loss_giou"]
+        return losses
+
+
+PAD_BOX = (0.5, 0.5, 0.1, 0.1)  # finite stand-in for padded target slots (masked out of every loss)
+
+
+def pad_targets(targets, M, boxes_out=None, labels_out=None, n_valid_out=None):
+    """Targets (list of {"boxes" [n,4], "labels" [n]}) -> padded device tensors
+    ([B, M, 4], [B, M], int32 [B]) for ``SetCriterion.forward_padded``; writes
+    into the given static buffers when passed (graph replay)."""
+    B = len(targets)
+    dev = targets[0]["boxes"].device if B else torch.device("cpu")
+    if boxes_out is None:
+        boxes_out = torch.empty((B, M, 4), dtype=torch.float32, device=dev)
+        labels_out = torch.empty((B, M), dtype=torch.int64, device=dev)
+        n_valid_out = torch.empty(B, dtype=torch.int32, device=dev)
+    counts = [len(t["boxes"]) for t in targets]
+    if max(counts, default=0) > M:
+        raise ValueError(f"pad_targets: {max(counts)} boxes in one image exceed the padded capacity {M}")
+    boxes_out[..., :2] = PAD_BOX[0]
+    boxes_out[..., 2:] = PAD_BOX[2]
+    labels_out.zero_()
+    for b, t in enumerate(targets):
+        n = counts[b]
+        if n:
+            boxes_out[b, :n].copy_(t["boxes"])
+            labels_out[b, :n].copy_(t["labels"])
+    host = torch.tensor(counts, dtype=torch.int32)
+    if n_valid_out.is_cuda:  # pinned staging: the copy does not wait for the stream
+        host = host.pin_memory()
+    n_valid_out.copy_(host, non_blocking=True)
+    return boxes_out, labels_out, n_valid_out
+
+
+def _pairwise_giou(a, b):
+    """GIoU of broadcast xyxy boxes a[..., 4], b[..., 4]."""
+    lt = torch.max(a[..., :2], b[..., :2])
+    rb = torch.min(a[..., 2:], b[..., 2:])
+    wh = (rb - lt).clamp(min=0)
+    inter = wh[..., 0] * wh[..., 1]
+    union = box_area(a) + box_area(b) - inter
+    iou = inter / union.clamp(min=1e-9)
+    lt2 = torch.min(a[..., :2], b[..., :2])
+    rb2 = torch.max(a[..., 2:], b[..., 2:])
+    wh2 = (rb2 - lt2).clamp(min=0)
+    area = wh2[..., 0] * wh2[..., 1]
+    return iou - (area - union) / area.clamp(min=1e-9)
+
+
 def _paired_iou_giou(a, b):
     """IoU and GIoU of paired xyxy boxes a[i], b[i]."""
     lt = torch.max(a[:, :2], b[:, :2])

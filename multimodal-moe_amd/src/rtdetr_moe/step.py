@@ -127,6 +127,78 @@ class GraphedModel:
         return _ReplayFn.apply(self, self.anchor)
 
 
+class GraphedStep:
+    """The whole differentiable step -- model forward, set criterion with the
+    GPU Hungarian matcher (``SetCriterion.forward_padded``), backward to every
+    parameter -- captured as ONE hipGraph.  Inputs (images, context ids,
+    padded targets, box count) live in static buffers refreshed by device
+    copies before each replay; gradients land in ``static_grads``.  No host
+    round trip inside the step: the host only refreshes inputs, replays, and
+    launches the optimizer.  Targets are padded to ``max_boxes`` per image;
+    a batch with more boxes re-captures at the next multiple of 16."""
+
+    def __init__(self, fn, criterion, params, images, ctx, targets, num_boxes, *, warmup=3, autocast=False,
+                 max_boxes=None):
+        from .criterion import pad_targets
+
+        self.fn, self.criterion, self.params, self.autocast = fn, criterion, params, autocast
+        dev = images.device
+        self.static_images = images.clone()
+        self.static_ctx = ctx.clone()
+        need = max((len(t["boxes"]) for t in targets), default=0)
+        self.M = max_boxes or max(16, (need + 15) // 16 * 16)
+        self.tb, self.tl, self.nv = pad_targets(targets, self.M)
+        self.nb = torch.full((), float(num_boxes), dtype=torch.float32, device=dev)
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.warmup = warmup
+        self._capture()
+
+    def _loss(self):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.autocast, cache_enabled=False):
+            flat = self.fn(self.static_images, self.static_ctx)
+        out, aux = FlatOutputs.unflatten(flat)
+        losses = self.criterion.forward_padded(out, self.tb, self.tl, self.nv, self.nb, self.status)
+        return sum(losses.values()) + aux, losses
+
+    def _capture(self):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up: convolution search, library attributes, allocator
+            for _ in range(self.warmup):
+                loss, _ = self._loss()
+                grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+                del loss, grads
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, pool=self.pool):
+            loss, losses = self._loss()
+            grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+            self.static_loss = loss.detach()
+            self.static_losses = {k: v.detach() for k, v in losses.items()}
+        self.static_grads = [g if g is not None else torch.zeros_like(p) for g, p in zip(grads, self.params)]
+        torch.cuda.synchronize()
+
+    def __call__(self, images, ctx, targets, num_boxes):
+        from .criterion import pad_targets
+
+        need = max((len(t["boxes"]) for t in targets), default=0)
+        if need > self.M:  # larger than the captured padding: re-capture (rare)
+            self.M = (need + 15) // 16 * 16
+            self.tb, self.tl, self.nv = pad_targets(targets, self.M)
+            self.graph = None
+            self._capture()
+        if images.data_ptr() != self.static_images.data_ptr():
+            self.static_images.copy_(images)
+        if ctx.data_ptr() != self.static_ctx.data_ptr():
+            self.static_ctx.copy_(ctx)
+        pad_targets(targets, self.M, self.tb, self.tl, self.nv)
+        self.nb.fill_(float(num_boxes))
+        self.graph.replay()
+        return self.static_loss
+
+
 def gemm_params(model: nn.Module):
     """Parameters that are GEMM / convolution operands: weights and biases of
     Linear, Conv2d and MultiheadAttention layers and the MoE expert weights,
@@ -167,7 +239,8 @@ class TrainStep:
     clip_grad_norm_ (the semantics FlatAdamW restates)."""
 
     def __init__(self, model: RTDETRMoE, criterion, images, ctx, *, lr=1e-4, lr_backbone=1e-5,
-                 weight_decay=1e-4, clip_norm=0.1, graphs=True, ddp_local=None, world=1, precision="bf16"):
+                 weight_decay=1e-4, clip_norm=0.1, graphs=True, ddp_local=None, world=1, precision="bf16",
+                 targets=None, num_boxes=1.0):
         self.model = model
         self.criterion = criterion
         self.clip_norm = clip_norm
@@ -198,7 +271,15 @@ class TrainStep:
         self.dp_params = [p for p in self.params if not getattr(p, "expert_parallel", False)]
         images = self._cast_in(images)
         self.runner = None
-        if graphs:
+        self.stepper = None
+        if graphs and targets is not None:  # whole step as one graph (GPU matcher)
+            self.stepper = GraphedStep(self.flat, criterion, self.params, images, ctx, targets, num_boxes,
+                                       autocast=self.precision == "amp")
+            self.fn = None
+            self.ddp = None
+            for p, g in zip(self.params, self.stepper.static_grads):
+                p.grad = g
+        elif graphs:
             self.runner = GraphedModel(self.flat, self.params, images, ctx, autocast=self.precision == "amp")
             self.fn = self.runner
             self.ddp = None
@@ -220,8 +301,9 @@ class TrainStep:
     def use_eager(self):
         """Leave graph mode (bench.py's kernel-profiling steps): later steps run
         the model eagerly; parameter grads go back to autograd allocation."""
-        if self.runner is not None:
+        if self.runner is not None or self.stepper is not None:
             self.runner = None
+            self.stepper = None
             self.fn = self.flat
             self.graphs = False
             self._flat_grads = None
@@ -263,6 +345,12 @@ class TrainStep:
 
     def __call__(self, images, ctx, targets, num_boxes):
         self._mark("start")
+        if self.stepper is not None:
+            loss = self.stepper(self._cast_in(images), ctx, targets, num_boxes)
+            self._mark("step_graph")
+            self._optimizer_step()
+            self._mark("optimizer")
+            return loss
         if self.runner is None:
             for p in self.params:
                 p.grad = None
@@ -275,6 +363,11 @@ class TrainStep:
         self._mark("criterion")
         loss.backward()
         self._mark("backward")
+        self._optimizer_step()
+        self._mark("optimizer")
+        return loss.detach()
+
+    def _optimizer_step(self):
         if self.opt_params is None:  # GPU: FlatAdamW (clip inside)
             if self.graphs and self.world > 1:
                 self.opt.step(self._allreduce_grads(), inv_world=1.0 / self.world)
@@ -284,8 +377,6 @@ class TrainStep:
             if self.clip_norm > 0:
                 torch.nn.utils.clip_grad_norm_(self.opt_params, self.clip_norm, foreach=True)
             self.opt.step()
-        self._mark("optimizer")
-        return loss.detach()
 
     def phase_summary(self):
         """{phase: (gpu ms, host ms)} averaged over the marked steps (syncs)."""

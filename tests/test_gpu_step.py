@@ -7,14 +7,14 @@ import torch
 DEV = "cuda"
 
 
-def _setup(spec="rtdetr-r18-moe4-top2"):
+def _setup(spec="rtdetr-r18-moe4-top2", seed=3):
     from src.rtdetr_moe.criterion import SetCriterion
     from src.rtdetr_moe.data import SyntheticZOD
     from src.rtdetr_moe.model import RTDETRMoE
 
     torch.manual_seed(0)
     model = RTDETRMoE(spec).to(DEV).to(memory_format=torch.channels_last)
-    images, targets, ctx = SyntheticZOD(batch=2, img_h=256, img_w=320, seed=3).sample(DEV)
+    images, targets, ctx = SyntheticZOD(batch=2, img_h=256, img_w=320, seed=seed).sample(DEV)
     images = images.contiguous(memory_format=torch.channels_last)
     targets = [{k: v.to(DEV) for k, v in t.items()} for t in targets]
     return model, SetCriterion(num_classes=1), images, targets, ctx
@@ -128,3 +128,59 @@ def test_ep_fp8_exchange_world1(hip_lib, tmp_path):
             torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_whole_step_graph_matches_eager(hip_lib):
+    """GraphedStep (forward + padded criterion with the GPU Hungarian matcher +
+    backward as one hipGraph) follows the eager step with host matching."""
+    from src.rtdetr_moe.step import TrainStep
+
+    runs = {}
+    for whole in (False, True):
+        model, crit, images, targets, ctx = _setup(seed=6)  # 6 + 0 boxes: matching and an empty image
+        nb = max(1.0, float(sum(len(t["boxes"]) for t in targets)))
+        step = TrainStep(model, crit, images, ctx, graphs=whole, world=1, precision="bf16", lr=1e-3,
+                         targets=targets if whole else None, num_boxes=nb)
+        assert (step.stepper is not None) == whole
+        runs[whole] = [float(step(images, ctx, targets, nb)) for _ in range(3)]
+        if whole:
+            assert int(step.stepper.status.item()) == 0
+    torch.cuda.synchronize()
+    eager, graph = runs[False], runs[True]
+    assert min(graph[1:]) < graph[0], graph
+    assert min(eager[1:]) < eager[0], eager
+    # Same initial weights: the first losses agree.  Later steps are not
+    # compared: on a random-init model the 300 queries are near-tied, so bf16
+    # rounding differences between the eager and captured kernels flip
+    # individual matches (host or GPU matcher alike) and the trajectories
+    # drift apart; exact criterion parity on identical outputs is
+    # test_padded_criterion_matches_host_matching.
+    assert abs(eager[0] - graph[0]) <= 3e-2 * max(1.0, abs(eager[0])), (eager, graph)
+
+
+@pytest.mark.gpu
+def test_padded_criterion_matches_host_matching(hip_lib):
+    """SetCriterion.forward_padded (GPU matcher, fixed shapes) gives the losses
+    of SetCriterion.forward (scipy matching on the host) on the same outputs."""
+    from src.rtdetr_moe.criterion import SetCriterion, pad_targets
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    S, B, Q = 7, 4, 300
+
+    def o():
+        return {"pred_logits": torch.randn(B, Q, 1, device=DEV, generator=g),
+                "pred_boxes": torch.rand(B, Q, 4, device=DEV, generator=g) * 0.5 + 0.2}
+    out = o()
+    out["aux_outputs"] = [o() for _ in range(S - 2)]
+    out["enc_outputs"] = o()
+    counts = [0, 3, 11, 1]
+    targets = [{"boxes": torch.rand(n, 4, device=DEV, generator=g) * 0.4 + 0.3,
+                "labels": torch.zeros(n, dtype=torch.int64, device=DEV)} for n in counts]
+    crit = SetCriterion(num_classes=1)
+    ref = crit(out, targets, float(sum(counts)))
+    tb, tl, nv = pad_targets(targets, 16)
+    got = crit.forward_padded(out, tb, tl, nv, torch.tensor(float(sum(counts)), device=DEV))
+    assert set(ref) == set(got)
+    for k in ref:
+        torch.testing.assert_close(got[k], ref[k], rtol=1e-5, atol=1e-6, msg=k)
