@@ -40,6 +40,10 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 # MIOpen convolution search (torch.backends.cudnn.benchmark, --conv-search) in
 # its fast mode: find-db lookups + quick heuristics, seconds instead of minutes
 os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+# ...starting from the find/perf databases measured on MI355X and shipped with
+# the package (multimodal-moe_amd/miopen_db/README.md): same algorithm choices
+# on every fresh box
+os.environ.setdefault("MIOPEN_USER_DB_PATH", str(ROOT / "multimodal-moe_amd" / "miopen_db"))
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
