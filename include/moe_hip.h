@@ -138,6 +138,12 @@ int moe_grouped_gemm(int dtype /* MOE_BF16; fp8: moe_grouped_gemm_mx */, const v
 int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, float* c,
                            float* colsum, const int32_t* offsets, int G,
                            int M, int N, hipStream_t stream);
+/* Same, with rows_hint = a host upper bound of offsets[G] (0: unknown).  The
+ * launch splits each group's K range over 2 workgroups (split-K, see
+ * moe_set_splitk_workspace) when the groups average >= 1024 rows. */
+int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, float* c,
+                                float* colsum, const int32_t* offsets, int G, int M,
+                                int N, int rows_hint, hipStream_t stream);
 
 /* ---- MXFP8 expert path (config C5: 32-expert top-4 fp8 expert GEMMs) ----
  * Format: OCP e4m3 elements with one E8M0 exponent byte per 32 consecutive
@@ -206,6 +212,11 @@ int rtdetr_bias_act_nhwc(const void* x, const float* bias, long long M, int C, i
                          hipStream_t stream);
 int rtdetr_add_bias_relu_nhwc(const void* a, const void* b, const float* bias, long long M, int C,
                               void* y, hipStream_t stream);
+/* Backward of a block output feeding two consumers:
+ *   out = (g1 + g2) * (y > 0)   (bf16 NHWC [M, C]; g2 may be NULL)
+ * the gradient accumulation and the ReLU mask in one pass. */
+int rtdetr_relu_grad2_nhwc(const void* g1, const void* g2, const void* y, long long M, int C, void* out,
+                           hipStream_t stream);
 
 /* Process-wide tuning overrides (not thread-safe; set before launching).  By
  * default (0) every launch picks its own kernel variant, ring depth and tile

@@ -53,6 +53,30 @@ __global__ __launch_bounds__(256) void add_bias_relu_kernel(const uint4* __restr
   }
 }
 
+// Backward of a block output y = relu(...) whose activation feeds two
+// consumers (the next block's branch2a and its shortcut): the two incoming
+// gradients are summed and masked in one pass -- what autograd would do as an
+// accumulate (add_) plus a ReLU backward (threshold_backward), two passes
+// more over the largest activations of the network.  g2 may be null.
+__global__ __launch_bounds__(256) void relu_grad2_kernel(const uint4* __restrict__ g1, const uint4* __restrict__ g2,
+                                                         const uint4* __restrict__ y, long long nchunk,
+                                                         uint4* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nchunk; i += (long long)gridDim.x * 256) {
+    float v1[8], v2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    unpack8(g1[i], v1);
+    if (g2 != nullptr) unpack8(g2[i], v2);
+    const uint4 yv = y[i];
+    const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t h = (yw[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+      const bool pos = !(h & 0x8000u) && h != 0;  // bf16 y > 0
+      v1[j] = pos ? v1[j] + v2[j] : 0.f;
+    }
+    out[i] = pack8(v1);
+  }
+}
+
 }  // namespace moe
 
 using namespace moe;
@@ -90,4 +114,16 @@ extern "C" int rtdetr_add_bias_relu_nhwc(const void* a, const void* b, const flo
              static_cast<const uint4*>(a), static_cast<const uint4*>(b), bias, nchunk, C / 8,
              static_cast<uint4*>(y));
   return check_launch("rtdetr_add_bias_relu_nhwc");
+}
+
+extern "C" int rtdetr_relu_grad2_nhwc(const void* g1, const void* g2, const void* y, long long M, int C, void* out,
+                                      hipStream_t stream) {
+  if (C <= 0 || C % 8 != 0) return fail("relu_grad2: C must be a positive multiple of 8");
+  if (g1 == nullptr || y == nullptr || out == nullptr) return fail("relu_grad2: g1, y and out are required");
+  if (M <= 0) return 0;
+  const long long nchunk = M * (C / 8);
+  ProfScope prof(stream, PROF_CONV_EPI, (g2 ? 8.0 : 6.0) * M * C);
+  MOE_LAUNCH(prof, relu_grad2_kernel, dim3(epi_grid(nchunk)), dim3(256), 0, stream, static_cast<const uint4*>(g1),
+             static_cast<const uint4*>(g2), static_cast<const uint4*>(y), nchunk, static_cast<uint4*>(out));
+  return check_launch("rtdetr_relu_grad2_nhwc");
 }

@@ -1114,9 +1114,19 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
   return check_launch("moe_grouped_gemm");
 }
 
+extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, float* c,
+                                           float* colsum, const int32_t* offsets, int G, int M,
+                                           int N, int rows_hint, hipStream_t stream);
+
 extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, float* c,
                                       float* colsum, const int32_t* offsets, int G, int M,
                                       int N, hipStream_t stream) {
+  return moe_grouped_gemm_wgrad_rows(dtype, x, y, c, colsum, offsets, G, M, N, 0, stream);
+}
+
+extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, float* c,
+                                           float* colsum, const int32_t* offsets, int G, int M,
+                                           int N, int rows_hint, hipStream_t stream) {
   if (dtype != MOE_BF16) return fail("grouped_gemm_wgrad: only MOE_BF16 is implemented");
   if (G < 1 || G > 1024) return fail("grouped_gemm_wgrad: G out of range");
   if (M <= 0 || N <= 0 || M % 64 != 0 || N % 128 != 0)
@@ -1149,10 +1159,11 @@ extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, f
   {
     const long long tpg = (long long)(M / bmw) * ntn;
     long long tiles = tpg * gpad;
-    // (kbench: encoder dW 30.0 -> 25.6 us; decoder groups of ~600 rows are
-    // not split -- split_min_kt, 1536 rows -- the merge latency outweighs the overlap)
-    const int want = g_ksplit ? g_ksplit : (tiles <= 512 ? 2 : 1);
-    p.split_min_kt = g_ksplit ? 0 : 24;
+    // only for long groups: rows_hint / G >= 1024 (kbench: encoder dW, 1,840
+    // rows per expert, 30.0 -> 26.6 us; decoder groups of ~600 rows lose to
+    // the merge latency, 11.5 -> 15.5 us)
+    const int want = g_ksplit ? g_ksplit : ((tiles <= 512 && rows_hint >= 1024LL * G) ? 2 : 1);
+    p.split_min_kt = 0;
     if (want > 1 && tiles % 8 != 0) {  // split grids map 8-slot XCD rows: pad the group count
       gpad = (G + 7) / 8 * 8;
       tiles = tpg * gpad;

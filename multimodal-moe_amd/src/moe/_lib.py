@@ -36,12 +36,14 @@ SIGNATURES = {
     "moe_token_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "moe_grouped_gemm": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_wgrad": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "moe_grouped_gemm_wgrad_rows": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "moe_quantize_mx": (_I, [_P, ctypes.c_longlong, _I, _P, _P, _P]),
     "moe_permute_fwd_mx": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_mx": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "moe_grouped_gemm_wgrad_mx": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "rtdetr_bias_act_nhwc": (_I, [_P, _P, ctypes.c_longlong, _I, _I, _P, _P]),
     "rtdetr_add_bias_relu_nhwc": (_I, [_P, _P, _P, ctypes.c_longlong, _I, _P, _P]),
+    "rtdetr_relu_grad2_nhwc": (_I, [_P, _P, _P, ctypes.c_longlong, _I, _P, _P]),
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_msda_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
@@ -367,9 +369,9 @@ def grouped_gemm_wgrad(x, y, offsets, G, want_colsum=True):
     c = torch.empty((G, M, N), dtype=torch.float32, device=x.device)
     cs = torch.empty((G, M), dtype=torch.float32, device=x.device) if want_colsum else None
     ensure_splitk_workspace(x.device)
-    rc = lib().moe_grouped_gemm_wgrad(
-        MOE_BF16, _ptr(x), _ptr(y), _ptr(c), _ptr(cs), _ptr(offsets), G, M, N, _stream())
-    _check(rc, "moe_grouped_gemm_wgrad")
+    rc = lib().moe_grouped_gemm_wgrad_rows(
+        MOE_BF16, _ptr(x), _ptr(y), _ptr(c), _ptr(cs), _ptr(offsets), G, M, N, int(x.shape[0]), _stream())
+    _check(rc, "moe_grouped_gemm_wgrad_rows")
     return c, cs
 
 
@@ -480,6 +482,17 @@ def add_bias_relu_nhwc(a, b, bias):
     _check(lib().rtdetr_add_bias_relu_nhwc(_ptr(a), _ptr(b), _ptr(bias), M, C, _ptr(y), _stream()),
            "rtdetr_add_bias_relu_nhwc")
     return y
+
+
+def relu_grad2_nhwc(g1, g2, y):
+    """(g1 + g2) * (y > 0) over channels_last bf16 tensors (g2 may be None)."""
+    M, C = _nhwc_rows(y, "y")
+    if _nhwc_rows(g1, "g1") != (M, C) or (g2 is not None and _nhwc_rows(g2, "g2") != (M, C)):
+        raise MoEKernelError("relu_grad2: shapes differ")
+    out = torch.empty_like(y)
+    _check(lib().rtdetr_relu_grad2_nhwc(_ptr(g1), _ptr(g2), _ptr(y), M, C, _ptr(out), _stream()),
+           "rtdetr_relu_grad2_nhwc")
+    return out
 
 
 def msda_fwd(value, shapes, starts, loc, attn):

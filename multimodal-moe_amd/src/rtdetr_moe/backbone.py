@@ -10,11 +10,13 @@ convolutions); nothing here is on the MoE hot path.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 import torch.nn.functional as F
 
-from .fused import AddBiasReLU, BiasReLU
+from .fused import AddBiasReLU, AddBiasReLUFork, BiasReLU
 
 _DEPTHS = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3], 50: [3, 4, 6, 3], 101: [3, 4, 23, 3]}
 
@@ -101,16 +103,24 @@ class _Shortcut(nn.Module):
         return self.conv.conv_shift(avg_pool_2x2(x) if self.down else x)
 
 
+_NO_FORK = os.environ.get("MOE_BACKBONE_FORK", "1") == "0"
+
+
 def _block_out(last, short, h, x):
-    """relu(last(h) + shortcut(x)).  With frozen BNs the two BN shifts join
-    the residual add and the ReLU in one fused kernel (fused.AddBiasReLU)."""
+    """relu(last(h) + shortcut(x)) as a (main, shortcut) pair of handles on the
+    same activation (see fused.AddBiasReLUFork).  With frozen BNs the two BN
+    shifts join the residual add and the ReLU in one fused kernel."""
     if last.fold and (short is None or short.conv.fold):
         a, sa = last.conv_shift(h)
-        if short is None:
-            return AddBiasReLU.apply(a, x, sa)
-        b, sb = short.conv_shift(x)
-        return AddBiasReLU.apply(a, b, sa + sb)
-    return F.relu(last(h) + (x if short is None else short(x)))
+        b, bias = (x, sa) if short is None else short.conv_shift(x)
+        if short is not None:
+            bias = sa + bias
+        if _NO_FORK:  # A/B switch (MOE_BACKBONE_FORK=0): autograd accumulate + mask
+            y = AddBiasReLU.apply(a, b, bias)
+            return y, y
+        return AddBiasReLUFork.apply(a, b, bias)
+    y = F.relu(last(h) + (x if short is None else short(x)))
+    return y, y
 
 
 class BasicBlock(nn.Module):
@@ -122,8 +132,10 @@ class BasicBlock(nn.Module):
         self.branch2a = ConvNormLayer(cin, cout, 3, stride, "relu", frozen)
         self.branch2b = ConvNormLayer(cout, cout, 3, 1, None, frozen)
 
-    def forward(self, x):
-        return _block_out(self.branch2b, self.short, self.branch2a(x), x)
+    def forward(self, x, x_short=None):
+        """x feeds branch2a, x_short (default x) the shortcut; returns the
+        (main, shortcut) handles of the output."""
+        return _block_out(self.branch2b, self.short, self.branch2a(x), x if x_short is None else x_short)
 
 
 class BottleNeck(nn.Module):
@@ -137,8 +149,11 @@ class BottleNeck(nn.Module):
         self.branch2c = ConvNormLayer(width, cout * 4, 1, 1, None, frozen)
         self.short = None if shortcut else _Shortcut(cin, cout * 4, stride, frozen)
 
-    def forward(self, x):
-        return _block_out(self.branch2c, self.short, self.branch2b(self.branch2a(x)), x)
+    def forward(self, x, x_short=None):
+        """x feeds branch2a, x_short (default x) the shortcut; returns the
+        (main, shortcut) handles of the output."""
+        return _block_out(self.branch2c, self.short, self.branch2b(self.branch2a(x)),
+                          x if x_short is None else x_short)
 
 
 class PResNet(nn.Module):
@@ -181,9 +196,11 @@ class PResNet(nn.Module):
 
     def forward(self, x):
         x = self.pool(self.stem(x))
+        xs = None
         outs = []
         for i, stage in enumerate(self.stages):
-            x = stage(x)
+            for blk in stage:
+                x, xs = blk(x, xs)
             if i in self.return_idx:
                 outs.append(x)
         return outs

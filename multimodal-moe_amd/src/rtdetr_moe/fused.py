@@ -11,6 +11,10 @@ the HIP kernels of libmoe_hip (include/moe_hip.h, rtdetr_*_nhwc):
 
 Backward is one mask of the incoming gradient (threshold_backward on y),
 shared by both inputs of AddBiasReLU; the bias carries no gradient (frozen).
+AddBiasReLUFork returns the block output twice -- one handle for the next
+block's branch2a, one for its shortcut -- so that its backward receives the
+two gradients separately and sums + masks them in one pass
+(rtdetr_relu_grad2_nhwc) instead of autograd's accumulate + threshold.
 CPU tensors (config C1 plumbing) take the same math in torch ops.
 """
 from __future__ import annotations
@@ -66,4 +70,31 @@ class AddBiasReLU(torch.autograd.Function):
     def backward(ctx, dy):
         (y,) = ctx.saved_tensors
         g = torch.ops.aten.threshold_backward(dy, y, 0)
+        return g, g, None
+
+
+def _nhwc_ok(*ts) -> bool:
+    return all(t is None or _gpu_ok(t) for t in ts)
+
+
+class AddBiasReLUFork(torch.autograd.Function):
+    """(y, y') with y = relu(a + b + bias[c]); y' aliases y.  Backward:
+    g = (dy + dy') * (y > 0) for both a and b, one pass."""
+
+    @staticmethod
+    def forward(ctx, a, b, bias):
+        y = AddBiasReLU.forward(ctx, a, b, bias)
+        return y, y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, dy1, dy2):
+        (y,) = ctx.saved_tensors
+        if dy1 is None and dy2 is None:
+            return None, None, None
+        if dy1 is None:
+            dy1, dy2 = dy2, None
+        if y.is_cuda and _nhwc_ok(dy1, dy2):
+            g = L.relu_grad2_nhwc(dy1, dy2, y)
+        else:
+            g = torch.ops.aten.threshold_backward(dy1 if dy2 is None else dy1 + dy2, y, 0)
         return g, g, None

@@ -83,3 +83,35 @@ def test_folded_backbone_matches_unfolded(hip_lib, depth):
             assert ef[-1] <= 3.0 * eu[-1] + 5e-3, (n, ef[-1], eu[-1])  # no layer grossly off
     ef, eu = torch.tensor(ef), torch.tensor(eu)
     assert float(ef.median()) <= 1.5 * float(eu.median()) + 2e-3, (float(ef.median()), float(eu.median()))
+
+
+@pytest.mark.gpu
+def test_relu_grad2_and_fork_backward_exact(hip_lib):
+    """rtdetr_relu_grad2_nhwc == threshold_backward(g1 + g2, y) bit for bit
+    (bf16 add rounds once either way), and AddBiasReLUFork's two-handle
+    backward equals autograd's accumulate + mask of AddBiasReLU."""
+    from src.moe import _lib as L
+    from src.rtdetr_moe.fused import AddBiasReLU, AddBiasReLUFork
+
+    g = torch.Generator().manual_seed(4)
+    y = _cl(torch.randn(2, 64, 9, 13, generator=g))
+    g1 = _cl(torch.randn(2, 64, 9, 13, generator=g))
+    g2 = _cl(torch.randn(2, 64, 9, 13, generator=g))
+    assert torch.equal(L.relu_grad2_nhwc(g1, g2, y), torch.ops.aten.threshold_backward(g1 + g2, y, 0))
+    assert torch.equal(L.relu_grad2_nhwc(g1, None, y), torch.ops.aten.threshold_backward(g1, y, 0))
+    a0 = _cl(torch.randn(2, 64, 9, 13, generator=g))
+    b0 = _cl(torch.randn(2, 64, 9, 13, generator=g))
+    bias = torch.randn(64, generator=g).to(DEV)
+    w1 = _cl(torch.randn(2, 64, 9, 13, generator=g))
+    w2 = _cl(torch.randn(2, 64, 9, 13, generator=g))
+    grads = []
+    for fork in (False, True):
+        a = a0.clone().requires_grad_(True)
+        b = b0.clone().requires_grad_(True)
+        if fork:
+            y1, y2 = AddBiasReLUFork.apply(a, b, bias)
+        else:
+            y1 = y2 = AddBiasReLU.apply(a, b, bias)
+        ((y1 * w1).float().sum() + (y2 * w2).float().sum()).backward()
+        grads.append((a.grad, b.grad))
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])

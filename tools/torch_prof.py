@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--out", default="gpurun_out/tprof.txt")
     ap.add_argument("--spec", default="rtdetr-r50-moe8-top2")
     ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--stacks", action="store_true",
+                    help="also attribute glue ops (casts, adds, fills, ReLU backward) to source lines")
     a = ap.parse_args()
 
     import bench
@@ -51,7 +53,9 @@ def main():
         step(images, ctx, targets, nb)
     torch.cuda.synchronize()
     acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
-    with torch.profiler.profile(activities=acts, record_shapes=True) as prof:
+    cfg = torch._C._profiler._ExperimentalConfig(verbose=True) if a.stacks else None
+    with torch.profiler.profile(activities=acts, record_shapes=not a.stacks, with_stack=a.stacks,
+                                experimental_config=cfg) as prof:
         for _ in range(a.steps):
             step(images, ctx, targets, nb)
         torch.cuda.synchronize()
@@ -64,7 +68,27 @@ def main():
                          max_shapes_column_width=100))
         f.write("\n\n# by op name\n")
         f.write(prof.key_averages().table(sort_by="device_time_total", row_limit=80, max_name_column_width=60))
+        if a.stacks:
+            f.write("\n\n# glue ops by source line (count per step, device ms per step)\n")
+            f.write(glue_by_line(prof, a.steps))
     print(f"wrote {out}")
+
+
+GLUE = {"aten::_to_copy", "aten::copy_", "aten::add", "aten::add_", "aten::fill_", "aten::zero_", "aten::zeros",
+        "aten::threshold_backward", "aten::mul", "aten::mul_", "aten::sum", "aten::cat", "aten::clone",
+        "aten::contiguous", "aten::div", "aten::sub", "aten::where", "aten::index", "aten::index_put_"}
+
+
+def glue_by_line(prof, steps):
+    rows = []
+    for e in prof.key_averages(group_by_stack_n=12):
+        if e.key not in GLUE:
+            continue
+        frames = [fr for fr in (e.stack or []) if "multimodal-moe_amd" in fr]
+        src = " <- ".join(fr.split("multimodal-moe_amd/")[-1] for fr in frames[:3]) or "(autograd engine)"
+        rows.append((e.device_time_total / 1e3 / steps, e.count / steps, e.key, src))
+    rows.sort(key=lambda r: -r[0])
+    return "\n".join(f"{t:8.3f} ms {c:7.1f}/step  {n:26s} {src}" for t, c, n, src in rows[:80]) + "\n"
 
 
 if __name__ == "__main__":

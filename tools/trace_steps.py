@@ -37,7 +37,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--marker", default="FusedAdamMathFunctor")
+    ap.add_argument("--marker", default="adamw_step_kernel", help="kernel launched once per step (torch fused AdamW: FusedAdamMathFunctor)")
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
