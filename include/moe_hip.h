@@ -200,6 +200,12 @@ int rtdetr_msda_bwd(const void* value, const int32_t* shapes, const int32_t* sta
                     const float* loc, const float* attn, const void* grad_out, int B, int S,
                     int Q, int H, int D, int L, int P, float* grad_value, float* grad_loc,
                     float* grad_attn, hipStream_t stream);
+/* Same with grad_value bf16 [B,S,H,D], accumulated by packed bf16 atomics
+ * (global_atomic_pk_add_bf16) -- the training step's variant. */
+int rtdetr_msda_bwd_bf16(const void* value, const int32_t* shapes, const int32_t* starts,
+                         const float* loc, const float* attn, const void* grad_out, int B, int S, int Q,
+                         int H, int D, int L, int P, void* grad_value, float* grad_loc, float* grad_attn,
+                         hipStream_t stream);
 
 /* ---- frozen-BatchNorm convolution epilogues of the backbone ----
  * With frozen BN statistics, conv + BN = conv with per-channel scaled weights

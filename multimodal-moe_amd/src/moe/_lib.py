@@ -46,6 +46,7 @@ SIGNATURES = {
     "rtdetr_relu_grad2_nhwc": (_I, [_P, _P, _P, ctypes.c_longlong, _I, _P, _P]),
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_msda_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "rtdetr_msda_bwd_bf16": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "moe_set_splitk_workspace": (_I, [_P, ctypes.c_size_t, _P, _I]),
     "rtdetr_hungarian_match": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
@@ -510,15 +511,16 @@ def msda_fwd(value, shapes, starts, loc, attn):
     return out
 
 
-def msda_bwd(value, shapes, starts, loc, attn, grad_out):
+def msda_bwd(value, shapes, starts, loc, attn, grad_out, bf16_grad_value=False):
+    """grad_value fp32 (fp32 atomics) or, with bf16_grad_value, bf16 (packed bf16 atomics)."""
     B, S, H, D = value.shape
     Q, L, P = loc.shape[1], loc.shape[3], loc.shape[4]
     _need(grad_out, torch.bfloat16, "grad_out")
-    gv = torch.empty((B, S, H, D), dtype=torch.float32, device=value.device)
+    gv = torch.empty((B, S, H, D), dtype=torch.bfloat16 if bf16_grad_value else torch.float32, device=value.device)
     gl = torch.empty_like(loc)
     ga = torch.empty_like(attn)
-    rc = lib().rtdetr_msda_bwd(
-        _ptr(value), _ptr(shapes), _ptr(starts), _ptr(loc), _ptr(attn), _ptr(grad_out), B, S, Q, H, D, L, P,
-        _ptr(gv), _ptr(gl), _ptr(ga), _stream())
+    fn = lib().rtdetr_msda_bwd_bf16 if bf16_grad_value else lib().rtdetr_msda_bwd
+    rc = fn(_ptr(value), _ptr(shapes), _ptr(starts), _ptr(loc), _ptr(attn), _ptr(grad_out), B, S, Q, H, D, L, P,
+            _ptr(gv), _ptr(gl), _ptr(ga), _stream())
     _check(rc, "rtdetr_msda_bwd")
     return gv, gl, ga

@@ -75,7 +75,10 @@ class _MSDAHip(torch.autograd.Function):
         from ..moe import _lib as L
 
         v, shapes_t, starts_t, lo, at = ctx.saved_tensors
-        gv, gl, ga = L.msda_bwd(v, shapes_t, starts_t, lo, at, grad_out.to(torch.bfloat16).contiguous())
+        # bf16 values (the training step): packed bf16 atomics give grad_value in
+        # the value's dtype directly; an fp32 value keeps fp32 accumulation
+        gv, gl, ga = L.msda_bwd(v, shapes_t, starts_t, lo, at, grad_out.to(torch.bfloat16).contiguous(),
+                                bf16_grad_value=ctx.vdtype == torch.bfloat16)
         return gv.to(ctx.vdtype), None, None, gl, ga
 
 

@@ -1,7 +1,8 @@
 """GPU parity of the HIP multi-scale deformable attention (rtdetr_msda_fwd/bwd)
 against the grid_sample formulation in float64 on the CPU (same inputs).
 Tolerance: output |err| <= 1e-2 * max|ref| + 1 bf16 ulp (bf16 output);
-gradients (fp32 accumulation) relative Frobenius error <= 2e-3."""
+gradients relative Frobenius error <= 2e-3 (loc, attn: fp32) and <= 1e-2
+for the value gradient of a bf16 value (packed bf16 atomics)."""
 from __future__ import annotations
 
 import numpy as np
@@ -47,3 +48,28 @@ def test_msda_matches_grid_sample(hip_lib, B, Q, H, D, P, shapes):
         got = got.double().cpu()
         rel = (got - want).norm() / want.norm().clamp(min=1e-12)
         assert rel < 2e-3 if name != "value" else rel < 1e-2, f"{name}: rel err {rel:.3e}"
+
+
+def test_msda_bwd_bf16_atomics_vs_fp32(hip_lib):
+    """The bf16-accumulated value gradient (rtdetr_msda_bwd_bf16) against the
+    fp32-accumulated one (rtdetr_msda_bwd) on the C2 decoder shapes; the
+    location / attention gradients do not depend on the accumulation."""
+    from src.moe import _lib as L
+    from src.rtdetr_moe.decoder import _level_tensors
+
+    g = torch.Generator().manual_seed(1)
+    shapes = [(92, 160), (46, 80), (23, 40)]
+    B, Q, H, D, P = 8, 300, 8, 32, 4
+    S = sum(h * w for h, w in shapes)
+    dev = "cuda"
+    value = torch.randn(B, S, H, D, generator=g).to(torch.bfloat16).to(dev)
+    loc = torch.rand(B, Q, H, 3, P, 2, generator=g).to(dev)
+    attn = torch.softmax(torch.randn(B, Q, H, 3 * P, generator=g), -1).view(B, Q, H, 3, P).to(dev)
+    gout = torch.randn(B, Q, H * D, generator=g).to(torch.bfloat16).to(dev)
+    st, so = _level_tensors(shapes, torch.device(dev))
+    gv32, gl32, ga32 = L.msda_bwd(value, st, so, loc, attn, gout)
+    gv16, gl16, ga16 = L.msda_bwd(value, st, so, loc, attn, gout, bf16_grad_value=True)
+    assert gv16.dtype == torch.bfloat16
+    assert torch.equal(gl16, gl32) and torch.equal(ga16, ga32)
+    rel = float((gv16.float() - gv32).norm() / gv32.norm())
+    assert rel < 4e-3, rel
