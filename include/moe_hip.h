@@ -138,12 +138,14 @@ int moe_grouped_gemm(int dtype /* MOE_BF16; fp8: moe_grouped_gemm_mx */, const v
 int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, float* c,
                            float* colsum, const int32_t* offsets, int G,
                            int M, int N, hipStream_t stream);
-/* Same, with rows_hint = a host upper bound of offsets[G] (0: unknown).  The
- * launch splits each group's K range over 2 workgroups (split-K, see
+/* Same, with rows_hint = a host upper bound of offsets[G] (0: unknown) and
+ * out_bf16 = 1 to write C and colsum as bf16 (RNE of the fp32 sums; the
+ * gradients of bf16 expert weights, no separate cast pass).  The launch splits
+ * each group's K range over 2 workgroups (split-K, see
  * moe_set_splitk_workspace) when the groups average >= 1024 rows. */
-int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, float* c,
-                                float* colsum, const int32_t* offsets, int G, int M,
-                                int N, int rows_hint, hipStream_t stream);
+int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, void* c,
+                                void* colsum, const int32_t* offsets, int G, int M,
+                                int N, int rows_hint, int out_bf16, hipStream_t stream);
 
 /* ---- MXFP8 expert path (config C5: 32-expert top-4 fp8 expert GEMMs) ----
  * Format: OCP e4m3 elements with one E8M0 exponent byte per 32 consecutive

@@ -69,6 +69,7 @@ struct GemmParams {
   // split -- slice 0 runs the whole group, the other slices exit at once.
   int ksplit;
   int split_min_kt;
+  int c_bf16;  // WGRAD: C and colsum written as bf16 (RNE of the fp32 sums) instead of fp32
   float* ws;
   int32_t* cnt;
 };
@@ -346,15 +347,23 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int g, int row0, i
       }
     }
   } else {
-    float* C = static_cast<float*>(p.c) + (size_t)g * p.stride_c;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wm * (BM / 2) + 16 * i + lm;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * (BN / 2) + 16 * j + ln;
-        if (!(p.dbg & 1)) *reinterpret_cast<float4*>(C + (size_t)m * p.ldc + n) =
-            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        const size_t off = (size_t)g * p.stride_c + (size_t)m * p.ldc + n;
+        if (p.dbg & 1) continue;
+        if (p.c_bf16) {
+          uint2 o;
+          o.x = pack2bf(acc[i][j][0], acc[i][j][1]);
+          o.y = pack2bf(acc[i][j][2], acc[i][j][3]);
+          *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p.c) + off) = o;
+        } else {
+          *reinterpret_cast<float4*>(static_cast<float*>(p.c) + off) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
       }
     }
     if constexpr (COLSUM) {
@@ -369,7 +378,8 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int g, int row0, i
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int m = m0 + wm * (BM / 2) + 16 * i + lm;
-          p.colsum[(size_t)g * p.M + m] = csum[i];
+          if (p.c_bf16) reinterpret_cast<uint16_t*>(p.colsum)[(size_t)g * p.M + m] = f2bf(csum[i]);
+          else p.colsum[(size_t)g * p.M + m] = csum[i];
         }
       }
     }
@@ -473,14 +483,22 @@ __device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row
       }
     }
     __syncthreads();
-    float* C = static_cast<float*>(p.c) + (size_t)g * p.stride_c;
     constexpr int RPP = 256 / CPR;
     const int c = tid % CPR;
 #pragma unroll 4
     for (int r0 = 0; r0 < BM; r0 += RPP) {
       const int r = r0 + tid / CPR;
       const float4 v = *reinterpret_cast<const float4*>(smem + r * (BN * 4) + ((c ^ (r & (CPR - 1))) << 4));
-      if (!(p.dbg & 1)) *reinterpret_cast<float4*>(C + (size_t)(m0 + r) * p.ldc + n0 + c * 4) = v;
+      const size_t off = (size_t)g * p.stride_c + (size_t)(m0 + r) * p.ldc + n0 + c * 4;
+      if (p.dbg & 1) continue;
+      if (p.c_bf16) {
+        uint2 o;
+        o.x = pack2bf(v.x, v.y);
+        o.y = pack2bf(v.z, v.w);
+        *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p.c) + off) = o;
+      } else {
+        *reinterpret_cast<float4*>(static_cast<float*>(p.c) + off) = v;
+      }
     }
     if constexpr (COLSUM) {
 #pragma unroll
@@ -494,7 +512,8 @@ __device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int m = m0 + wm * (BM / 2) + 16 * i + lm;
-          p.colsum[(size_t)g * p.M + m] = csum[i];
+          if (p.c_bf16) reinterpret_cast<uint16_t*>(p.colsum)[(size_t)g * p.M + m] = f2bf(csum[i]);
+          else p.colsum[(size_t)g * p.M + m] = csum[i];
         }
       }
     }
@@ -1114,19 +1133,19 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
   return check_launch("moe_grouped_gemm");
 }
 
-extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, float* c,
-                                           float* colsum, const int32_t* offsets, int G, int M,
-                                           int N, int rows_hint, hipStream_t stream);
+extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, void* c,
+                                           void* colsum, const int32_t* offsets, int G, int M,
+                                           int N, int rows_hint, int out_bf16, hipStream_t stream);
 
 extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, float* c,
                                       float* colsum, const int32_t* offsets, int G, int M,
                                       int N, hipStream_t stream) {
-  return moe_grouped_gemm_wgrad_rows(dtype, x, y, c, colsum, offsets, G, M, N, 0, stream);
+  return moe_grouped_gemm_wgrad_rows(dtype, x, y, c, colsum, offsets, G, M, N, 0, 0, stream);
 }
 
-extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, float* c,
-                                           float* colsum, const int32_t* offsets, int G, int M,
-                                           int N, int rows_hint, hipStream_t stream) {
+extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, void* c,
+                                           void* colsum, const int32_t* offsets, int G, int M,
+                                           int N, int rows_hint, int out_bf16, hipStream_t stream) {
   if (dtype != MOE_BF16) return fail("grouped_gemm_wgrad: only MOE_BF16 is implemented");
   if (G < 1 || G > 1024) return fail("grouped_gemm_wgrad: G out of range");
   if (M <= 0 || N <= 0 || M % 64 != 0 || N % 128 != 0)
@@ -1137,7 +1156,8 @@ extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void*
   p.b = static_cast<const uint16_t*>(y);
   p.c = c;
   p.offsets = offsets;
-  p.colsum = colsum;
+  p.colsum = static_cast<float*>(colsum);
+  p.c_bf16 = out_bf16 ? 1 : 0;
   p.stride_c = (long long)M * N;
   p.lda = M;
   p.ldb = N;
@@ -1173,7 +1193,7 @@ extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void*
     if (S == 1) gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
   }
   // algorithmic bytes: fp32 C (+ colsum) once; per routed row one row of X (M) and of Y (N)
-  ProfScope prof(stream, PROF_GEMM, 4.0 * G * M * N + (colsum ? 4.0 * G * M : 0.0), true, 2.0 * (M + N),
+  ProfScope prof(stream, PROF_GEMM, (out_bf16 ? 2.0 : 4.0) * G * M * N + (colsum ? (out_bf16 ? 2.0 : 4.0) * G * M : 0.0), true, 2.0 * (M + N),
                  2.0 * M * N);
   p.prof_rows = prof.rows_slot();
   if (big) {

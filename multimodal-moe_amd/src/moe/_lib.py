@@ -36,7 +36,7 @@ SIGNATURES = {
     "moe_token_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "moe_grouped_gemm": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_wgrad": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
-    "moe_grouped_gemm_wgrad_rows": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "moe_grouped_gemm_wgrad_rows": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "moe_quantize_mx": (_I, [_P, ctypes.c_longlong, _I, _P, _P, _P]),
     "moe_permute_fwd_mx": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_mx": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
@@ -363,15 +363,19 @@ def hungarian_match(cost, n_valid, status=None):
     return assign
 
 
-def grouped_gemm_wgrad(x, y, offsets, G, want_colsum=True):
+def grouped_gemm_wgrad(x, y, offsets, G, want_colsum=True, out_dtype=torch.float32):
+    """(C [G, M, N], colsum [G, M]) in out_dtype (float32 or bfloat16)."""
     _need(x, torch.bfloat16, "x")
     _need(y, torch.bfloat16, "y")
+    if out_dtype not in (torch.float32, torch.bfloat16):
+        raise MoEKernelError("grouped_gemm_wgrad: out_dtype must be float32 or bfloat16")
     M, N = x.shape[1], y.shape[1]
-    c = torch.empty((G, M, N), dtype=torch.float32, device=x.device)
-    cs = torch.empty((G, M), dtype=torch.float32, device=x.device) if want_colsum else None
+    c = torch.empty((G, M, N), dtype=out_dtype, device=x.device)
+    cs = torch.empty((G, M), dtype=out_dtype, device=x.device) if want_colsum else None
     ensure_splitk_workspace(x.device)
     rc = lib().moe_grouped_gemm_wgrad_rows(
-        MOE_BF16, _ptr(x), _ptr(y), _ptr(c), _ptr(cs), _ptr(offsets), G, M, N, int(x.shape[0]), _stream())
+        MOE_BF16, _ptr(x), _ptr(y), _ptr(c), _ptr(cs), _ptr(offsets), G, M, N, int(x.shape[0]),
+        int(out_dtype == torch.bfloat16), _stream())
     _check(rc, "moe_grouped_gemm_wgrad_rows")
     return c, cs
 

@@ -111,6 +111,7 @@ class _ExpertFFN(torch.autograd.Function):
         yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=b2.float().contiguous())
         ctx.save_for_backward(xp, h, w1b, w2b, offsets)
         ctx.meta = (G, F, d, rows, float(grad_scale))
+        ctx.wdtype = w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32
         return yp
 
     @staticmethod
@@ -119,9 +120,12 @@ class _ExpertFFN(torch.autograd.Function):
         G, F, d, rows, s = ctx.meta
         dyp = d_yp.to(torch.bfloat16).contiguous()
         dh = L.grouped_gemm(dyp, w2b, offsets, G, rows, F, d, 0, L.EPI_RELU_MASK, aux=h)
-        dW2, db2 = L.grouped_gemm_wgrad(dyp, h, offsets, G)
+        # weight gradients written in the parameters' dtype by the kernel (bf16
+        # weights: no fp32 copy + autograd cast pass)
+        odt = torch.bfloat16 if ctx.wdtype == torch.bfloat16 else torch.float32
+        dW2, db2 = L.grouped_gemm_wgrad(dyp, h, offsets, G, out_dtype=odt)
         dxp = L.grouped_gemm(dh, w1b, offsets, G, rows, d, F, 0, L.EPI_NONE)
-        dW1, db1 = L.grouped_gemm_wgrad(dh, xp, offsets, G)
+        dW1, db1 = L.grouped_gemm_wgrad(dh, xp, offsets, G, out_dtype=odt)
         if s != 1.0:
             for t in (dW1, db1, dW2, db2):
                 t.mul_(s)

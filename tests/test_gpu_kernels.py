@@ -163,11 +163,14 @@ def test_grouped_gemm_wgrad_exact(gemm_cfg, rows_per_group, M, N):
     Yt = torch.from_numpy(Y).to(torch.bfloat16).to(DEV)
     off_t = torch.from_numpy(offsets).to(DEV)
     C, cs = L.grouped_gemm_wgrad(Xt, Yt, off_t, G)
+    Cb, csb = L.grouped_gemm_wgrad(Xt, Yt, off_t, G, out_dtype=torch.bfloat16)  # bf16 out: RNE of the sums
     torch.cuda.synchronize()
     for g in range(G):
         a, b = offsets[g], offsets[g + 1]
         np.testing.assert_array_equal(_np(C[g]), X[a:b].T @ Y[a:b])
         np.testing.assert_array_equal(_np(cs[g]), X[a:b].sum(0))
+        np.testing.assert_array_equal(_np(Cb[g]), O.round_bf16(X[a:b].T @ Y[a:b]))
+        np.testing.assert_array_equal(_np(csb[g]), O.round_bf16(X[a:b].sum(0)))
 
 
 # ---------------------------------------------------------------------------
