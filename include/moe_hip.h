@@ -251,6 +251,16 @@ int moe_set_tuning(const char* key, int value);
  * forces the factor (1 = off). */
 int moe_set_splitk_workspace(void* ws, size_t ws_bytes, int32_t* counters, int n_counters);
 
+/* a3: the layer's aux losses from the router's partials, one block:
+ *   P_e = sum_b aux_partials[b][e] / T, f_e = hist[e] / (T k),
+ *   out3 = {lb = E sum_e f_e P_e, z = sum_b aux_partials[b][E] / T,
+ *           lb_coef lb + z_coef z}
+ *   wcoef[E+1] = d out3[2] / d aux_partials[b][.] (same for every b):
+ *           lb_coef E f_e / T (e < E), z_coef / T (e = E)
+ * (the backward is g * wcoef broadcast over the blocks). */
+int moe_aux_loss_fwd(const float* aux_partials, int nblk, int E, const int32_t* hist, int T, int k,
+                     float lb_coef, float z_coef, float* out3, float* wcoef, hipStream_t stream);
+
 /* Hungarian matching of the set criterion on the device (the reference's
  * RT-DETR loss matches with scipy.optimize.linear_sum_assignment on the host).
  * cost fp32 [S][B][Q][M]: S prediction sets, B images, Q queries, M padded

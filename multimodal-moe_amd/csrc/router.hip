@@ -257,6 +257,45 @@ __global__ __launch_bounds__(1024) void route_scan_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// aux losses from the router's per-block partials, one block:
+//   P_e = sum_b partials[b][e] / T, f_e = hist[e] / (T k), lb = E sum_e f_e P_e,
+//   z = sum_b partials[b][E] / T;  out = {lb, z, lb_coef lb + z_coef z}
+//   wcoef = d out[2] / d partials[b][.] (the same for every b):
+//           lb_coef E f_e / T (e < E), z_coef / T (e = E)
+// Replaces ~12 tiny torch launches forward and ~8 backward per MoE layer.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void aux_loss_fwd_kernel(const float* __restrict__ partials, int nblk, int E,
+                                                           const int32_t* __restrict__ hist, int T, int k,
+                                                           float lb_coef, float z_coef, float* __restrict__ out,
+                                                           float* __restrict__ wcoef) {
+  __shared__ float s_term[65];
+  const int e = threadIdx.x;
+  const float invT = 1.f / (float)(T > 0 ? T : 1);
+  const float invA = 1.f / (float)(T * k > 0 ? T * k : 1);
+  if (e <= E) {
+    float colsum = 0.f;
+    for (int b = 0; b < nblk; ++b) colsum += partials[(size_t)b * (E + 1) + e];  // fixed order
+    if (e < E) {
+      const float f = (float)hist[e] * invA;
+      s_term[e] = f * (colsum * invT);
+      wcoef[e] = lb_coef * (float)E * f * invT;
+    } else {
+      s_term[E] = colsum * invT;
+      wcoef[E] = z_coef * invT;
+    }
+  }
+  __syncthreads();
+  if (e == 0) {
+    float acc = 0.f;
+    for (int i = 0; i < E; ++i) acc += s_term[i];
+    const float lb = (float)E * acc, z = s_term[E];
+    out[0] = lb;
+    out[1] = z;
+    out[2] = lb_coef * lb + z_coef * z;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // token backward: dispatch transpose + router backward
 // ---------------------------------------------------------------------------
 template <int EMAX>
@@ -459,4 +498,15 @@ extern "C" int moe_token_bwd(const void* dxp, const int32_t* pos, const float* p
   }
 #undef LAUNCH_B
   return check_launch("moe_token_bwd");
+}
+
+extern "C" int moe_aux_loss_fwd(const float* aux_partials, int nblk, int E, const int32_t* hist, int T, int k,
+                                float lb_coef, float z_coef, float* out3, float* wcoef, hipStream_t stream) {
+  if (E < 1 || E > 64 || nblk < 0 || k < 1) return fail("aux_loss_fwd: need 1 <= E <= 64, nblk >= 0, k >= 1");
+  if (aux_partials == nullptr || hist == nullptr || out3 == nullptr || wcoef == nullptr)
+    return fail("aux_loss_fwd: NULL pointer");
+  ProfScope prof(stream, PROF_ROUTER, 4.0 * nblk * (E + 1) + 4.0 * E + 12.0 + 4.0 * (E + 1));
+  MOE_LAUNCH(prof, aux_loss_fwd_kernel, dim3(1), dim3(256), 0, stream, aux_partials, nblk, E, hist, T, k, lb_coef,
+             z_coef, out3, wcoef);
+  return check_launch("moe_aux_loss_fwd");
 }

@@ -50,6 +50,7 @@ SIGNATURES = {
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "moe_set_splitk_workspace": (_I, [_P, ctypes.c_size_t, _P, _I]),
     "rtdetr_hungarian_match": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "moe_aux_loss_fwd": (_I, [_P, _I, _I, _P, _I, _I, _F, _F, _P, _P, _P]),
     "train_grad_sqnorm": (_I, [_P, _P, _I, _P, _P]),
     "train_grad_norm_finalize": (_I, [_P, _I, _F, _F, _P, _P, _I, _P, _P]),
     "train_adamw_step": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _P]),
@@ -345,6 +346,18 @@ def grouped_gemm(a, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None,
         int(epilogue), _ptr(bias), _ptr(aux), None, _stream())
     _check(rc, "moe_grouped_gemm")
     return c
+
+
+def aux_loss_fwd(auxp, hist, T, k, lb_coef, z_coef):
+    """-> (out fp32 [3] = (lb, z, lb_coef lb + z_coef z), wcoef fp32 [E+1])."""
+    _need(auxp, torch.float32, "aux_partials")
+    _need(hist, torch.int32, "hist")
+    nblk, E1 = auxp.shape
+    out = torch.empty(3, dtype=torch.float32, device=auxp.device)
+    wcoef = torch.empty(E1, dtype=torch.float32, device=auxp.device)
+    _check(lib().moe_aux_loss_fwd(_ptr(auxp), nblk, E1 - 1, _ptr(hist), int(T), int(k), float(lb_coef),
+                                  float(z_coef), _ptr(out), _ptr(wcoef), _stream()), "moe_aux_loss_fwd")
+    return out, wcoef
 
 
 def hungarian_match(cost, n_valid, status=None):

@@ -50,6 +50,7 @@ class MoEFFN(nn.Module):
         for p in (self.w1, self.b1, self.w2, self.b2):
             p.expert_parallel = self.ep_size > 1  # excluded from the DP all-reduce
         self.last_aux = None   # (lb_raw, z_raw) of the last forward
+        self.last_aux_weighted = None  # lb_coef lb + z_coef z (GPU path: fused kernel, differentiable)
         self.last_hist = None  # int32 [E] expert histogram of the last forward
 
     def forward(self, x: torch.Tensor, ctx_img: torch.Tensor | None) -> torch.Tensor:
@@ -68,8 +69,13 @@ class MoEFFN(nn.Module):
         elif flat.is_cuda:
             from .ops import moe_ffn_hip
 
-            y, lb, z, hist = moe_ffn_hip(flat, self.wg, cb, self.w1, self.b1, self.w2, self.b2,
-                                         ci, L, cfg.top_k, cfg.normalize, cap, cfg.expert_dtype)
+            y, aux, raw, hist = moe_ffn_hip(flat, self.wg, cb, self.w1, self.b1, self.w2, self.b2,
+                                            ci, L, cfg.top_k, cfg.normalize, cap, cfg.expert_dtype,
+                                            aux_coefs=(cfg.lb_coef, cfg.z_coef))
+            self.last_aux = (raw[0], raw[1])
+            self.last_aux_weighted = aux
+            self.last_hist = hist
+            return y.to(x.dtype).view(B, L, d)
         else:
             from .eager import moe_ffn_eager
 
@@ -77,11 +83,14 @@ class MoEFFN(nn.Module):
                                            ci, L, cfg.top_k, cfg.normalize, cap, cfg.expert_dtype)
         y = y.to(x.dtype)
         self.last_aux = (lb, z)
+        self.last_aux_weighted = None
         self.last_hist = hist
         return y.view(B, L, d)
 
     def aux_loss(self) -> torch.Tensor | None:
         if self.last_aux is None:
             return None
+        if self.last_aux_weighted is not None:  # fused kernel (GPU path)
+            return self.last_aux_weighted
         lb, z = self.last_aux
         return self.cfg.lb_coef * lb + self.cfg.z_coef * z

@@ -182,6 +182,30 @@ class _Combine(torch.autograd.Function):
         return dyp, dw, None, None
 
 
+class _AuxLoss(torch.autograd.Function):
+    """lb_coef lb + z_coef z of one layer in one HIP launch (moe_aux_loss_fwd);
+    backward = g * wcoef broadcast over the router blocks (one launch).  The
+    raw (lb, z) ride along, detached, for logging."""
+
+    @staticmethod
+    def forward(ctx, auxp, hist, T, k, lb_coef, z_coef):
+        out, wcoef = L.aux_loss_fwd(auxp.contiguous(), hist, T, k, lb_coef, z_coef)
+        ctx.save_for_backward(wcoef)
+        ctx.nblk = auxp.shape[0]
+        ctx.mark_non_differentiable(out)
+        return out[2].clone(), out[:2]
+
+    @staticmethod
+    def backward(ctx, g, _raw):
+        (wcoef,) = ctx.saved_tensors
+        return (g * wcoef).view(1, -1).expand(ctx.nblk, -1), None, None, None, None, None
+
+
+def aux_loss_weighted(auxp, hist, T, k, lb_coef, z_coef):
+    """-> (lb_coef lb + z_coef z (differentiable), detached (lb, z) [2])."""
+    return _AuxLoss.apply(auxp, hist, int(T), int(k), float(lb_coef), float(z_coef))
+
+
 def aux_losses(auxp, hist, T, k):
     E = hist.shape[0]
     f = hist.float() / float(max(T * k, 1))
@@ -221,14 +245,16 @@ def combine_hip(yp, w, pos, T):
 
 
 def moe_ffn_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap,
-                expert_dtype="bf16"):
+                expert_dtype="bf16", aux_coefs=None):
     """Routed expert FFN of one layer on the GPU.
 
     x [T, d] (tokens of ``T // tokens_per_image`` images, image-major),
     wg [E, d], ctx_bias [C, E] or None, w1 [E, F, d], b1 [E, F], w2 [E, d, F],
     b2 [E, d], ctx_img int32 [T // tokens_per_image].  expert_dtype "bf16" or
     "fp8" (MXFP8 dispatch rows and expert GEMMs, config C5).
-    Returns (y bf16 [T, d], lb_raw, z_raw, hist int32 [E]).
+    Returns (y bf16 [T, d], lb_raw, z_raw, hist int32 [E]); with
+    aux_coefs = (lb_coef, z_coef) it returns (y, aux, (lb, z) detached, hist)
+    instead, aux = lb_coef lb + z_coef z from the fused aux-loss kernel.
     """
     if not x.is_cuda:
         raise L.MoEKernelError("moe_ffn_hip needs GPU tensors")
@@ -246,5 +272,8 @@ def moe_ffn_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, n
                                                                    k, normalize, cap)
         yp = expert_ffn_hip(xp, w1, b1, w2, b2, offsets, rows)
     y = combine_hip(yp, w, pos, T)
+    if aux_coefs is not None:
+        aux, raw = aux_loss_weighted(auxp, hist, T, k, *aux_coefs)
+        return y, aux, raw, hist
     lb, z = aux_losses(auxp, hist, T, k)
     return y, lb, z, hist

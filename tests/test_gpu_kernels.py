@@ -327,3 +327,24 @@ def lib_count_after_stop():
     from src.moe import _lib as L
 
     return L.lib().moe_profile_count()
+
+
+@pytest.mark.gpu
+def test_fused_aux_loss_matches_torch(hip_lib):
+    """moe_aux_loss_fwd (one launch) == ops.aux_losses (torch ops) in value
+    and in its gradient w.r.t. the router partials."""
+    from src.moe.ops import aux_loss_weighted, aux_losses
+
+    g = torch.Generator(device=DEV).manual_seed(2)
+    nblk, E, T, k = 37, 8, 2300, 2
+    auxp = (torch.rand(nblk, E + 1, device=DEV, generator=g) * 10).requires_grad_(True)
+    hist = torch.randint(0, 600, (E,), device=DEV, generator=g).int()
+    lbc, zc = 1e-2, 1e-3
+    lb, z = aux_losses(auxp, hist, T, k)
+    ref = lbc * lb + zc * z
+    (ga_ref,) = torch.autograd.grad(ref, auxp)
+    aux, raw = aux_loss_weighted(auxp, hist, T, k, lbc, zc)
+    (ga,) = torch.autograd.grad(aux * 3.0, auxp)
+    torch.testing.assert_close(aux, ref, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(raw, torch.stack([lb, z]).detach(), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(ga, 3.0 * ga_ref, rtol=1e-5, atol=1e-9)

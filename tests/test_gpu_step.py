@@ -118,10 +118,11 @@ def test_ep_fp8_exchange_world1(hip_lib, tmp_path):
                 flat = xi.reshape(-1, 256)
                 y, lb, z, hist = moe_ffn_ep(layer, flat, layer.ctx_bias, ctx, 150, cfg.capacity(600))
                 y = y.view(4, 150, 256)
+                aux = cfg.lb_coef * lb + cfg.z_coef * z
             else:
                 y = layer(xi, ctx)
-                lb, z = layer.last_aux
-            ((y.float() * dy).sum() + 0.1 * lb + 0.01 * z).backward()
+                aux = layer.aux_loss()  # fused aux-loss kernel
+            ((y.float() * dy).sum() + 10.0 * aux).backward()
             res.append((y.detach().float(), xi.grad.float(), layer.w1.grad.clone(), layer.wg.grad.clone()))
         torch.cuda.synchronize()
         for a, b in zip(res[0], res[1]):
