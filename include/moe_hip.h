@@ -220,6 +220,14 @@ int rtdetr_bias_act_nhwc(const void* x, const float* bias, long long M, int C, i
                          hipStream_t stream);
 int rtdetr_add_bias_relu_nhwc(const void* a, const void* b, const float* bias, long long M, int C,
                               void* y, hipStream_t stream);
+/* Frozen-BN weight fold of many convolutions in one launch (forward
+ * W' = W * scale[c_out], backward dW = dW' * scale[c_out]): `records` is a
+ * device array of 32-B {const bf16* w; const float* scale; bf16* out;
+ * int32 rows; int32 inner} (rows = output channels, inner = elements per
+ * output channel, a multiple of 8; 16-B aligned tensors); `chunks` device
+ * int32 pairs {record, chunk of 2048 elements}.  out = RNE(float(w) * scale). */
+int rtdetr_fold_scale_multi(const void* records, const int32_t* chunks, int n_chunks, hipStream_t stream);
+
 /* Backward of a block output feeding two consumers:
  *   out = (g1 + g2) * (y > 0)   (bf16 NHWC [M, C]; g2 may be NULL)
  * the gradient accumulation and the ReLU mask in one pass. */

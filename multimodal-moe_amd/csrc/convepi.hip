@@ -77,6 +77,32 @@ __global__ __launch_bounds__(256) void relu_grad2_kernel(const uint4* __restrict
   }
 }
 
+// Frozen-BN weight fold for many convolutions in one launch:
+//   out_t[r][i] = bf16(float(w_t[r][i]) * scale_t[r])   (r = output channel)
+// over a table of tensors (forward: W' = W * s; backward: dW = dW' * s).
+struct FoldRec {      // 32 B, mirrored by src/rtdetr_moe/backbone.py
+  const uint16_t* w;  // bf16 [rows][inner] (any dense layout with the output channel outermost)
+  const float* scale; // fp32 [rows]
+  uint16_t* out;      // bf16, same layout as w
+  int rows, inner;    // inner = elements per output channel (multiple of 8)
+};
+static_assert(sizeof(FoldRec) == 32, "FoldRec layout");
+
+__global__ __launch_bounds__(256) void fold_scale_multi_kernel(const FoldRec* __restrict__ recs,
+                                                               const int2* __restrict__ chunks) {
+  const int2 ch = chunks[blockIdx.x];  // (tensor, chunk of 2048 elements)
+  const FoldRec r = recs[ch.x];
+  const long long e = (long long)ch.y * 2048 + threadIdx.x * 8;
+  const long long n = (long long)r.rows * r.inner;
+  if (e >= n) return;
+  const float s = r.scale[e / r.inner];  // 8 consecutive elements share a row (inner % 8 == 0)
+  float v[8];
+  unpack8(*reinterpret_cast<const uint4*>(r.w + e), v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] *= s;
+  *reinterpret_cast<uint4*>(r.out + e) = pack8(v);
+}
+
 }  // namespace moe
 
 using namespace moe;
@@ -126,4 +152,14 @@ extern "C" int rtdetr_relu_grad2_nhwc(const void* g1, const void* g2, const void
   MOE_LAUNCH(prof, relu_grad2_kernel, dim3(epi_grid(nchunk)), dim3(256), 0, stream, static_cast<const uint4*>(g1),
              static_cast<const uint4*>(g2), static_cast<const uint4*>(y), nchunk, static_cast<uint4*>(out));
   return check_launch("rtdetr_relu_grad2_nhwc");
+}
+
+extern "C" int rtdetr_fold_scale_multi(const void* records, const int32_t* chunks, int n_chunks, hipStream_t stream) {
+  if (n_chunks < 0 || (n_chunks > 0 && (records == nullptr || chunks == nullptr)))
+    return fail("fold_scale_multi: bad arguments");
+  if (n_chunks == 0) return 0;
+  ProfScope prof(stream, PROF_CONV_EPI, 4.0 * 2048 * n_chunks);
+  MOE_LAUNCH(prof, fold_scale_multi_kernel, dim3(n_chunks), dim3(256), 0, stream,
+             static_cast<const FoldRec*>(records), reinterpret_cast<const int2*>(chunks));
+  return check_launch("rtdetr_fold_scale_multi");
 }

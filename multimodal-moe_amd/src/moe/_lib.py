@@ -44,6 +44,7 @@ SIGNATURES = {
     "rtdetr_bias_act_nhwc": (_I, [_P, _P, ctypes.c_longlong, _I, _I, _P, _P]),
     "rtdetr_add_bias_relu_nhwc": (_I, [_P, _P, _P, ctypes.c_longlong, _I, _P, _P]),
     "rtdetr_relu_grad2_nhwc": (_I, [_P, _P, _P, ctypes.c_longlong, _I, _P, _P]),
+    "rtdetr_fold_scale_multi": (_I, [_P, _P, _I, _P]),
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_msda_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "rtdetr_msda_bwd_bf16": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),

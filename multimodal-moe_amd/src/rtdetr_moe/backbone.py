@@ -84,6 +84,85 @@ class _FoldScale(torch.autograd.Function):
         return gw, None
 
 
+class _FoldAll(torch.autograd.Function):
+    """Every frozen-BN fold of the backbone (W'_l = W_l * scale_l) in ONE
+    launch (rtdetr_fold_scale_multi) instead of one per convolution.  The
+    folded weights live in buffers owned by the plan (fixed addresses: the
+    device table is built once, outside any graph capture) and are returned
+    as fresh views; the backward (dW_l = dW'_l * scale_l) is one kernel per
+    tensor (the incoming gradients are new allocations)."""
+
+    @staticmethod
+    def forward(ctx, plan, *weights):
+        plan.run()
+        ctx.plan = plan
+        outs = tuple(o.view_as(o) for o in plan.outs)
+        frozen = [o for o, w in zip(outs, weights) if not w.requires_grad]
+        if frozen:  # e.g. the frozen stem: no weight gradient is computed for it
+            ctx.mark_non_differentiable(*frozen)
+        return outs
+
+    @staticmethod
+    def backward(ctx, *grads):
+        plan = ctx.plan
+        out = []
+        for g, sc in zip(grads, plan.scales):
+            if g is None:
+                out.append(None)
+                continue
+            gw = torch.empty_like(g)
+            torch.mul(g, sc.view(-1, *([1] * (g.dim() - 1))), out=gw)
+            out.append(gw)
+        return (None, *out)
+
+
+class FoldPlan:
+    """Device table of the backbone's folds (see _FoldAll)."""
+
+    def __init__(self, layers):
+        self.layers = layers
+        self.outs = None
+        self.key = None
+
+    def _build(self):
+        import numpy as np
+
+        from ..moe import _lib as L
+
+        ws = [l.conv.weight for l in self.layers]
+        self.scales = [l.norm.scale_shift()[0].float().contiguous() for l in self.layers]
+        self.outs = [torch.empty_like(w) for w in ws]
+        rec = np.zeros(len(ws), dtype=[("w", "<u8"), ("s", "<u8"), ("o", "<u8"), ("rows", "<i4"), ("inner", "<i4")])
+        chunks = []
+        for i, (w, sc, o) in enumerate(zip(ws, self.scales, self.outs)):
+            rec[i] = (w.data_ptr(), sc.data_ptr(), o.data_ptr(), w.shape[0], w.numel() // w.shape[0])
+            chunks += [(i, c) for c in range((w.numel() + 2047) // 2048)]
+        dev = ws[0].device
+        self.table = torch.from_numpy(rec.view(np.uint8).copy()).to(dev)
+        self.chunks = torch.tensor(chunks, dtype=torch.int32, device=dev)
+        self.n_chunks = len(chunks)
+        self.lib = L
+
+    def usable(self):
+        ws = [l.conv.weight for l in self.layers]
+        return (len(ws) > 0 and all(w.is_cuda and w.dtype == torch.bfloat16 and (w.numel() // w.shape[0]) % 8 == 0
+                                    and w.data_ptr() % 16 == 0 and
+                                    (w.is_contiguous() or w.is_contiguous(memory_format=torch.channels_last))
+                                    for w in ws))
+
+    def run(self):
+        key = tuple((l.conv.weight.data_ptr(), l.conv.weight.dtype, l.norm.scale_shift()[0].data_ptr())
+                    for l in self.layers)
+        if key != self.key:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("FoldPlan: first use inside a graph capture (run one eager step first)")
+            self._build()
+            self.key = key
+        L = self.lib
+        L._check(L.lib().rtdetr_fold_scale_multi(self.table.data_ptr(), self.chunks.data_ptr(), self.n_chunks,
+                                                 L._stream()), "rtdetr_fold_scale_multi")
+
+
 class ConvNormLayer(nn.Module):
     """Conv + BN + act.  With a frozen BN the BN folds into the convolution
     (scaled weights) and its shift is applied with the activation by one fused
@@ -101,7 +180,10 @@ class ConvNormLayer(nn.Module):
     def conv_shift(self, x):
         """Frozen BN: (conv(x, W * scale), shift) -- the BN output minus its shift."""
         scale, shift = self.norm.scale_shift()
-        w = _FoldScale.apply(self.conv.weight, scale)
+        w = getattr(self, "_w_folded", None)  # set by PResNet.forward (one launch for all)
+        self._w_folded = None
+        if w is None:
+            w = _FoldScale.apply(self.conv.weight, scale)
         return F.conv2d(x, w, None, self.conv.stride, self.conv.padding), shift
 
     def forward(self, x):
@@ -141,6 +223,7 @@ class _Shortcut(nn.Module):
 
 
 _NO_FORK = os.environ.get("MOE_BACKBONE_FORK", "1") == "0"
+_NO_FOLD_ALL = os.environ.get("MOE_FOLD_ALL", "1") == "0"
 
 
 def _block_out(last, short, h, x):
@@ -231,7 +314,24 @@ class PResNet(nn.Module):
         self.out_channels = [self.out_channels[i] for i in self.return_idx]
         self.out_strides = [[4, 8, 16, 32][i] for i in self.return_idx]
 
+    def _fold_all(self):
+        """Fold every frozen BN of the stages (and stem) in one launch when all
+        the folded weights are GPU bf16 (TrainStep precision "bf16")."""
+        plan = getattr(self, "_fold_plan", None)
+        if plan is None:  # the 16-B vector kernel needs whole 8-element groups per output channel
+            layers = [m for m in self.modules() if isinstance(m, ConvNormLayer) and m.fold
+                      and (m.conv.weight.numel() // m.conv.weight.shape[0]) % 8 == 0]
+            plan = self._fold_plan = FoldPlan(layers)
+        if _NO_FOLD_ALL or not plan.usable():  # A/B switch MOE_FOLD_ALL=0: one fold kernel per layer
+            return
+        need = torch.is_grad_enabled() and any(l.conv.weight.requires_grad for l in plan.layers)
+        ws = [l.conv.weight for l in plan.layers]
+        outs = _FoldAll.apply(plan, *ws) if need else (plan.run() or tuple(plan.outs))
+        for l, w in zip(plan.layers, outs):
+            l._w_folded = w
+
     def forward(self, x):
+        self._fold_all()
         x = self.pool(self.stem(x))
         xs = None
         outs = []

@@ -115,3 +115,38 @@ def test_relu_grad2_and_fork_backward_exact(hip_lib):
         ((y1 * w1).float().sum() + (y2 * w2).float().sum()).backward()
         grads.append((a.grad, b.grad))
     assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+
+
+def test_fold_all_matches_per_layer_fold(hip_lib):
+    """PResNet's one-launch fold of the frozen BNs (rtdetr_fold_scale_multi)
+    gives the per-layer fold's outputs and weight gradients, and no gradient
+    for the frozen stem."""
+    from src.rtdetr_moe.backbone import PResNet
+
+    torch.manual_seed(0)
+    m = PResNet(18).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for mod in m.modules():  # non-trivial frozen statistics
+        if hasattr(mod, "running_var") and not isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_var.uniform_(0.5, 2.0)
+            mod.weight.uniform_(0.5, 1.5)
+    x = torch.randn(2, 3, 64, 96, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    for use_plan in (False, True):
+        m.zero_grad(set_to_none=True)
+        if not use_plan:
+            m._fold_plan = type("Off", (), {"usable": lambda self: False})()
+        else:
+            m._fold_plan = None
+        outs = m(x)
+        sum(o.float().square().mean() for o in outs).backward()
+        res.append(([o.detach().clone() for o in outs],
+                    {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}))
+    # (MIOpen's convolution kernels are not bit-reproducible call to call --
+    # weight gradients use atomics -- so compare at bf16 noise level)
+    assert m._fold_plan.usable() and len(m._fold_plan.layers) > 0
+    for a, b in zip(res[0][0], res[1][0]):
+        assert _rel(b, a) < 2e-3
+    assert res[0][1].keys() == res[1][1].keys()
+    assert not any(k.startswith("stem") for k in res[1][1])
+    for k in res[0][1]:
+        assert _rel(res[1][1][k], res[0][1][k]) < 2e-2, k
