@@ -43,7 +43,7 @@ class FrozenBatchNorm2d(nn.Module):
             with torch.no_grad():
                 scale = self.weight * (self.running_var + self.eps).rsqrt()
                 shift = self.bias - self.running_mean * scale
-            if torch.cuda.is_current_stream_capturing():
+            if scale.is_cuda and torch.cuda.is_current_stream_capturing():
                 return scale, shift  # first computed inside a capture: graph-owned, not cached
             cache = (key, scale, shift)
             self._ss_cache = cache
