@@ -209,6 +209,22 @@ int rtdetr_msda_bwd_bf16(const void* value, const int32_t* shapes, const int32_t
                          int H, int D, int L, int P, void* grad_value, float* grad_loc, float* grad_attn,
                          hipStream_t stream);
 
+/* Fused decoder cross-attention core: the sampling locations and attention
+ * weights are formed in the kernel from the raw linear outputs
+ *   loc[.., l, p, :] = ref[b, q, :2] + bf16(off[.., l, p, :] / P) * ref[b, q, 2:] * offset_scale
+ *   attn[b, q, h, :] = softmax(logits[b, q, h, :])   (over the L*P samples, fp32)
+ * off bf16 [B,Q,H,L,P,2], ref fp32 [B,Q,4] (cx, cy, w, h; no gradient),
+ * logits bf16 [B,Q,H,L*P], L*P <= 16.  Backward: grad_value bf16 (packed bf16
+ * atomics), grad_off bf16 (same shape as off), grad_logits bf16 (softmax
+ * backward fused). */
+int rtdetr_msda_fused_fwd(const void* value, const int32_t* shapes, const int32_t* starts, const void* off,
+                          const float* ref, const void* logits, float offset_scale, int B, int S, int Q,
+                          int H, int D, int L, int P, void* out, hipStream_t stream);
+int rtdetr_msda_fused_bwd(const void* value, const int32_t* shapes, const int32_t* starts, const void* off,
+                          const float* ref, const void* logits, float offset_scale, const void* grad_out,
+                          int B, int S, int Q, int H, int D, int L, int P, void* grad_value,
+                          void* grad_off, void* grad_logits, hipStream_t stream);
+
 /* ---- frozen-BatchNorm convolution epilogues of the backbone ----
  * With frozen BN statistics, conv + BN = conv with per-channel scaled weights
  * + a channel bias; these apply the bias with what follows it, in one pass

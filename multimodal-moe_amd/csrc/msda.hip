@@ -189,6 +189,209 @@ __global__ __launch_bounds__(256) void msda_bwd_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused variant (decoder cross-attention, TrainStep): the sampling locations
+// and attention weights are formed inside the kernel from the raw linear
+// outputs -- loc = ref.xy + bf16(off / P) * ref.wh * offset_scale and
+// attn = softmax over the L*P logits of the (b, q, h) group -- and the
+// backward returns the gradients of those linear outputs (softmax backward
+// and the location chain rule fused).  Replaces ~14 element-wise launches per
+// decoder layer.  ref carries no gradient (RT-DETR detaches the reference
+// boxes).  L*P <= 16.
+// ---------------------------------------------------------------------------
+constexpr int MSDA_LP_MAX = 16;
+
+struct MsdaPrep {
+  float a[MSDA_LP_MAX];
+  float rx, ry, rw, rh;
+};
+
+__device__ __forceinline__ void msda_prep(const uint16_t* __restrict__ logits, const float* __restrict__ ref,
+                                          int gi, int H, int LP, MsdaPrep& pr) {
+  const uint16_t* lg = logits + (size_t)gi * LP;
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < MSDA_LP_MAX; ++i) {
+    pr.a[i] = i < LP ? bf2f(lg[i]) : -INFINITY;
+    m = fmaxf(m, pr.a[i]);
+  }
+  float ssum = 0.f;
+#pragma unroll
+  for (int i = 0; i < MSDA_LP_MAX; ++i) {
+    pr.a[i] = i < LP ? expf(pr.a[i] - m) : 0.f;
+    ssum += pr.a[i];
+  }
+  const float inv = 1.f / ssum;
+#pragma unroll
+  for (int i = 0; i < MSDA_LP_MAX; ++i) pr.a[i] *= inv;
+  const float4 r = *reinterpret_cast<const float4*>(ref + (size_t)(gi / H) * 4);
+  pr.rx = r.x; pr.ry = r.y; pr.rw = r.z; pr.rh = r.w;
+}
+
+__device__ __forceinline__ float msda_pick(const float (&v)[MSDA_LP_MAX], int i) {
+  float r = 0.f;
+#pragma unroll
+  for (int j = 0; j < MSDA_LP_MAX; ++j)
+    if (j == i) r = v[j];
+  return r;
+}
+
+template <int LPG>
+__global__ __launch_bounds__(256) void msda_fused_fwd_kernel(
+    const uint16_t* __restrict__ value, const int32_t* __restrict__ shapes, const int32_t* __restrict__ starts,
+    const uint16_t* __restrict__ off, const float* __restrict__ ref, const uint16_t* __restrict__ logits,
+    float offset_scale, int B, int S, int Q, int H, int L, int P, uint16_t* __restrict__ out) {
+  constexpr int D = 2 * LPG;
+  const MsdaLevels lv = load_levels(shapes, starts, L);
+  const int groups = B * Q * H;
+  const int sub = threadIdx.x % LPG;
+  const int LP = L * P;
+  const float invP = 1.f / (float)P;
+  for (int gidx = (blockIdx.x * blockDim.x + threadIdx.x) / LPG; gidx < groups;
+       gidx += gridDim.x * blockDim.x / LPG) {
+    const int h = gidx % H;
+    const int b = gidx / (Q * H);
+    MsdaPrep pr;
+    msda_prep(logits, ref, gidx, H, LP, pr);
+    const uint16_t* op = off + (size_t)gidx * LP * 2;
+    float acc0 = 0.f, acc1 = 0.f;
+    for (int l = 0; l < L; ++l) {
+      const int Hl = lv.h[l], Wl = lv.w[l];
+      const size_t row0 = (size_t)b * S + lv.start[l];
+      const uint16_t* vb = value + row0 * H * D + h * D + 2 * sub;
+      for (int p = 0; p < P; ++p) {
+        const int sp = l * P + p;
+        const float ox = bf2f(f2bf(bf2f(op[2 * sp]) * invP)), oy = bf2f(f2bf(bf2f(op[2 * sp + 1]) * invP));
+        const float lx = pr.rx + ox * pr.rw * offset_scale;
+        const float ly = pr.ry + oy * pr.rh * offset_scale;
+        const float a = msda_pick(pr.a, sp);
+        const float x = lx * Wl - 0.5f, y = ly * Hl - 0.5f;
+        const float xf = floorf(x), yf = floorf(y);
+        const int x0 = (int)xf, y0 = (int)yf;
+        const float fx = x - xf, fy = y - yf;
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int cy = 0; cy < 2; ++cy) {
+#pragma unroll
+          for (int cx = 0; cx < 2; ++cx) {
+            const int xi = x0 + cx, yi = y0 + cy;
+            if (xi < 0 || xi >= Wl || yi < 0 || yi >= Hl) continue;
+            const float wgt = (cx ? fx : 1.f - fx) * (cy ? fy : 1.f - fy);
+            const float2 v = ld_bf16x2(vb + (size_t)(yi * Wl + xi) * H * D);
+            s0 += wgt * v.x;
+            s1 += wgt * v.y;
+          }
+        }
+        acc0 += a * s0;
+        acc1 += a * s1;
+      }
+    }
+    *reinterpret_cast<uint32_t*>(out + (size_t)gidx * D + 2 * sub) = pack2bf(acc0, acc1);
+  }
+}
+
+template <int LPG>
+__global__ __launch_bounds__(256) void msda_fused_bwd_kernel(
+    const uint16_t* __restrict__ value, const int32_t* __restrict__ shapes, const int32_t* __restrict__ starts,
+    const uint16_t* __restrict__ off, const float* __restrict__ ref, const uint16_t* __restrict__ logits,
+    float offset_scale, const uint16_t* __restrict__ grad_out, int B, int S, int Q, int H, int L, int P,
+    uint16_t* __restrict__ grad_value, uint16_t* __restrict__ grad_off, uint16_t* __restrict__ grad_logits) {
+  constexpr int D = 2 * LPG;
+  const MsdaLevels lv = load_levels(shapes, starts, L);
+  const int groups = B * Q * H;
+  const int sub = threadIdx.x % LPG;
+  const int LP = L * P;
+  const float invP = 1.f / (float)P;
+  const int ngrp_total = (gridDim.x * blockDim.x) / LPG;
+  const int first = (blockIdx.x * blockDim.x + threadIdx.x) / LPG;
+  const int iters = (groups + ngrp_total - 1) / ngrp_total;
+  for (int it = 0; it < iters; ++it) {  // uniform trip count: shuffles stay convergent
+    const int gidx = first + it * ngrp_total;
+    const bool valid = gidx < groups;
+    const int gi = valid ? gidx : 0;
+    const int h = gi % H;
+    const int b = gi / (Q * H);
+    MsdaPrep pr;
+    msda_prep(logits, ref, gi, H, LP, pr);
+    const uint16_t* op = off + (size_t)gi * LP * 2;
+    const float2 g = valid ? ld_bf16x2(grad_out + (size_t)gi * D + 2 * sub) : make_float2(0.f, 0.f);
+    float gaa[MSDA_LP_MAX];
+#pragma unroll
+    for (int i = 0; i < MSDA_LP_MAX; ++i) gaa[i] = 0.f;
+    float dot = 0.f;  // sum_sp a_sp ga_sp (softmax backward)
+    for (int l = 0; l < L; ++l) {
+      const int Hl = lv.h[l], Wl = lv.w[l];
+      const size_t row0 = (size_t)b * S + lv.start[l];
+      const uint16_t* vb = value + row0 * H * D + h * D + 2 * sub;
+      const size_t gofs = row0 * H * D + h * D + 2 * sub;
+      for (int p = 0; p < P; ++p) {
+        const int sp = l * P + p;
+        const float ox = bf2f(f2bf(bf2f(op[2 * sp]) * invP)), oy = bf2f(f2bf(bf2f(op[2 * sp + 1]) * invP));
+        const float lx = pr.rx + ox * pr.rw * offset_scale;
+        const float ly = pr.ry + oy * pr.rh * offset_scale;
+        const float a = msda_pick(pr.a, sp);
+        const float x = lx * Wl - 0.5f, y = ly * Hl - 0.5f;
+        const float xf = floorf(x), yf = floorf(y);
+        const int x0 = (int)xf, y0 = (int)yf;
+        const float fx = x - xf, fy = y - yf;
+        float2 v[2][2];
+        bool in[2][2];
+#pragma unroll
+        for (int cy = 0; cy < 2; ++cy)
+#pragma unroll
+          for (int cx = 0; cx < 2; ++cx) {
+            const int xi = x0 + cx, yi = y0 + cy;
+            in[cy][cx] = valid && xi >= 0 && xi < Wl && yi >= 0 && yi < Hl;
+            v[cy][cx] = in[cy][cx] ? ld_bf16x2(vb + (size_t)(yi * Wl + xi) * H * D) : make_float2(0.f, 0.f);
+          }
+        const float w00 = (1.f - fx) * (1.f - fy), w01 = fx * (1.f - fy);
+        const float w10 = (1.f - fx) * fy, w11 = fx * fy;
+        const float sx = w00 * v[0][0].x + w01 * v[0][1].x + w10 * v[1][0].x + w11 * v[1][1].x;
+        const float sy = w00 * v[0][0].y + w01 * v[0][1].y + w10 * v[1][0].y + w11 * v[1][1].y;
+        const float dxa = (1.f - fy) * (v[0][1].x - v[0][0].x) + fy * (v[1][1].x - v[1][0].x);
+        const float dxb = (1.f - fy) * (v[0][1].y - v[0][0].y) + fy * (v[1][1].y - v[1][0].y);
+        const float dya = (1.f - fx) * (v[1][0].x - v[0][0].x) + fx * (v[1][1].x - v[0][1].x);
+        const float dyb = (1.f - fx) * (v[1][0].y - v[0][0].y) + fx * (v[1][1].y - v[0][1].y);
+        float ga = g.x * sx + g.y * sy;
+        float gx = g.x * dxa + g.y * dxb;
+        float gy = g.x * dya + g.y * dyb;
+        ga = group_sum<LPG>(ga);
+        gx = group_sum<LPG>(gx);
+        gy = group_sum<LPG>(gy);
+#pragma unroll
+        for (int i = 0; i < MSDA_LP_MAX; ++i)
+          if (i == sp) gaa[i] = ga;
+        dot += a * ga;
+        if (valid && sub == 0) {  // d loc / d off = wh * offset_scale / P (straight through the bf16 rounding)
+          const float glx = a * gx * Wl, gly = a * gy * Hl;
+          const uint32_t o = pack2bf(glx * pr.rw * offset_scale * invP, gly * pr.rh * offset_scale * invP);
+          *reinterpret_cast<uint32_t*>(grad_off + ((size_t)gi * LP + sp) * 2) = o;
+        }
+        const float wc[2][2] = {{w00, w01}, {w10, w11}};
+#pragma unroll
+        for (int cy = 0; cy < 2; ++cy)
+#pragma unroll
+          for (int cx = 0; cx < 2; ++cx) {
+            if (!in[cy][cx]) continue;
+            const float s = a * wc[cy][cx];
+            bf16x2_t pv;
+            pv.x = (__bf16)(s * g.x);
+            pv.y = (__bf16)(s * g.y);
+            __builtin_amdgcn_global_atomic_fadd_v2bf16(
+                (__attribute__((address_space(1))) bf16x2_t*)(grad_value + gofs +
+                                                              (size_t)((y0 + cy) * Wl + (x0 + cx)) * H * D),
+                pv);
+          }
+      }
+    }
+    // softmax backward: d logit_sp = a_sp (ga_sp - sum_j a_j ga_j); lane `sub` writes sample sub
+    if (valid && sub < LP) {
+      const float a = msda_pick(pr.a, sub);
+      grad_logits[(size_t)gi * LP + sub] = f2bf(a * (msda_pick(gaa, sub) - dot));
+    }
+  }
+}
+
 }  // namespace moe
 
 using namespace moe;
@@ -265,4 +468,54 @@ extern "C" int rtdetr_msda_bwd_bf16(const void* value, const int32_t* shapes, co
                                     hipStream_t stream) {
   return msda_bwd_impl(value, shapes, starts, loc, attn, grad_out, B, S, Q, H, D, L, P, grad_value, true, grad_loc,
                        grad_attn, stream);
+}
+
+extern "C" int rtdetr_msda_fused_fwd(const void* value, const int32_t* shapes, const int32_t* starts, const void* off,
+                                     const float* ref, const void* logits, float offset_scale, int B, int S, int Q,
+                                     int H, int D, int L, int P, void* out, hipStream_t stream) {
+  if (msda_check(B, S, Q, H, D, L, P)) return -1;
+  if (L * P > MSDA_LP_MAX) return fail("msda_fused: L * P must be <= 16");
+  if (Q == 0) return 0;
+  const long long groups = (long long)B * Q * H;
+  const double samples = (double)groups * L * P;
+  ProfScope prof(stream, PROF_MSDA, samples * (8.0 * D + 6.0) + groups * (2.0 * D + 16.0 / H));
+  const uint16_t* v = static_cast<const uint16_t*>(value);
+  const uint16_t* o = static_cast<const uint16_t*>(off);
+  const uint16_t* lg = static_cast<const uint16_t*>(logits);
+  uint16_t* y = static_cast<uint16_t*>(out);
+  if (D == 32)
+    MOE_LAUNCH(prof, msda_fused_fwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
+               o, ref, lg, offset_scale, B, S, Q, H, L, P, y);
+  else
+    MOE_LAUNCH(prof, msda_fused_fwd_kernel<32>, dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v, shapes, starts,
+               o, ref, lg, offset_scale, B, S, Q, H, L, P, y);
+  return check_launch("rtdetr_msda_fused_fwd");
+}
+
+extern "C" int rtdetr_msda_fused_bwd(const void* value, const int32_t* shapes, const int32_t* starts, const void* off,
+                                     const float* ref, const void* logits, float offset_scale, const void* grad_out,
+                                     int B, int S, int Q, int H, int D, int L, int P, void* grad_value,
+                                     void* grad_off, void* grad_logits, hipStream_t stream) {
+  if (msda_check(B, S, Q, H, D, L, P)) return -1;
+  if (L * P > MSDA_LP_MAX) return fail("msda_fused: L * P must be <= 16");
+  const hipError_t e = hipMemsetAsync(grad_value, 0, (size_t)B * S * H * D * 2, stream);
+  if (e != hipSuccess) return fail(std::string("rtdetr_msda_fused_bwd: memset: ") + hipGetErrorString(e));
+  if (Q == 0) return 0;
+  const long long groups = (long long)B * Q * H;
+  const double samples = (double)groups * L * P;
+  ProfScope prof(stream, PROF_MSDA, samples * (16.0 * D + 10.0) + groups * (2.0 * D + 16.0 / H));
+  const uint16_t* v = static_cast<const uint16_t*>(value);
+  const uint16_t* o = static_cast<const uint16_t*>(off);
+  const uint16_t* lg = static_cast<const uint16_t*>(logits);
+  const uint16_t* go = static_cast<const uint16_t*>(grad_out);
+  uint16_t* gv = static_cast<uint16_t*>(grad_value);
+  uint16_t* gof = static_cast<uint16_t*>(grad_off);
+  uint16_t* glg = static_cast<uint16_t*>(grad_logits);
+  if (D == 32)
+    MOE_LAUNCH(prof, msda_fused_bwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
+               o, ref, lg, offset_scale, go, B, S, Q, H, L, P, gv, gof, glg);
+  else
+    MOE_LAUNCH(prof, msda_fused_bwd_kernel<32>, dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v, shapes, starts,
+               o, ref, lg, offset_scale, go, B, S, Q, H, L, P, gv, gof, glg);
+  return check_launch("rtdetr_msda_fused_bwd");
 }

@@ -48,6 +48,8 @@ SIGNATURES = {
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_msda_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "rtdetr_msda_bwd_bf16": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "rtdetr_msda_fused_fwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "rtdetr_msda_fused_bwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "moe_set_splitk_workspace": (_I, [_P, ctypes.c_size_t, _P, _I]),
     "rtdetr_hungarian_match": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
@@ -527,6 +529,36 @@ def msda_fwd(value, shapes, starts, loc, attn):
         _ptr(value), _ptr(shapes), _ptr(starts), _ptr(loc), _ptr(attn), B, S, Q, H, D, L, P, _ptr(out), _stream())
     _check(rc, "rtdetr_msda_fwd")
     return out
+
+
+def msda_fused_fwd(value, shapes, starts, off, ref, logits, offset_scale, L, P):
+    """value bf16 [B,S,H,D]; off bf16 [B,Q,H*L*P*2]; ref fp32 [B,Q,4]; logits bf16 [B,Q,H*L*P] -> bf16 [B,Q,H*D]."""
+    B, S, H, D = value.shape
+    Q = off.shape[1]
+    for t, n, dt in ((value, "value", torch.bfloat16), (off, "off", torch.bfloat16), (ref, "ref", torch.float32),
+                     (logits, "logits", torch.bfloat16)):
+        _need(t, dt, n)
+    if off.numel() != B * Q * H * L * P * 2 or logits.numel() != B * Q * H * L * P or ref.numel() != B * Q * 4:
+        raise MoEKernelError("msda_fused: shape mismatch")
+    out = torch.empty((B, Q, H * D), dtype=torch.bfloat16, device=value.device)
+    _check(lib().rtdetr_msda_fused_fwd(_ptr(value), _ptr(shapes), _ptr(starts), _ptr(off), _ptr(ref), _ptr(logits),
+                                       float(offset_scale), B, S, Q, H, D, L, P, _ptr(out), _stream()),
+           "rtdetr_msda_fused_fwd")
+    return out
+
+
+def msda_fused_bwd(value, shapes, starts, off, ref, logits, offset_scale, L, P, grad_out):
+    """-> (grad_value bf16 [B,S,H,D], grad_off bf16 like off, grad_logits bf16 like logits)."""
+    B, S, H, D = value.shape
+    Q = off.shape[1]
+    _need(grad_out, torch.bfloat16, "grad_out")
+    gv = torch.empty_like(value)
+    go = torch.empty_like(off)
+    gl = torch.empty_like(logits)
+    _check(lib().rtdetr_msda_fused_bwd(_ptr(value), _ptr(shapes), _ptr(starts), _ptr(off), _ptr(ref), _ptr(logits),
+                                       float(offset_scale), _ptr(grad_out), B, S, Q, H, D, L, P, _ptr(gv), _ptr(go),
+                                       _ptr(gl), _stream()), "rtdetr_msda_fused_bwd")
+    return gv, go, gl
 
 
 def msda_bwd(value, shapes, starts, loc, attn, grad_out, bf16_grad_value=False):

@@ -7,6 +7,7 @@ samples 4 points x 3 levels x 8 heads with bilinear grid_sample (SURVEY.md
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 from torch import nn
@@ -82,7 +83,36 @@ class _MSDAHip(torch.autograd.Function):
         return gv.to(ctx.vdtype), None, None, gl, ga
 
 
+class _MSDAFusedHip(torch.autograd.Function):
+    """Decoder cross-attention core with the location / softmax prep fused
+    into the HIP kernels (rtdetr_msda_fused_fwd/bwd): inputs are the raw
+    sampling-offset and attention-weight linear outputs and the (detached)
+    reference boxes."""
+
+    @staticmethod
+    def forward(ctx, value, shapes_t, starts_t, off, ref, logits, offset_scale, L, P):
+        from ..moe import _lib as L_
+
+        v, o, lg = value.contiguous(), off.contiguous(), logits.contiguous()
+        r = ref.float().contiguous()
+        out = L_.msda_fused_fwd(v, shapes_t, starts_t, o, r, lg, offset_scale, L, P)
+        ctx.save_for_backward(v, shapes_t, starts_t, o, r, lg)
+        ctx.cfg = (offset_scale, L, P)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        from ..moe import _lib as L_
+
+        v, shapes_t, starts_t, o, r, lg = ctx.saved_tensors
+        offset_scale, L, P = ctx.cfg
+        gv, go, gl = L_.msda_fused_bwd(v, shapes_t, starts_t, o, r, lg, offset_scale, L, P,
+                                       grad_out.to(torch.bfloat16).contiguous())
+        return gv, None, None, go, None, gl, None, None, None
+
+
 _LEVEL_CACHE = {}
+_FUSED_MSDA = os.environ.get("MOE_FUSED_MSDA", "1") != "0"  # A/B switch
 
 
 def _level_tensors(shapes, device):
@@ -137,8 +167,15 @@ class MSDeformableAttention(nn.Module):
         B, Q, _ = query.shape
         H, L, P = self.nhead, self.nlevels, self.npoints
         v = self.value_proj(value).view(B, value.shape[1], H, self.d // H)
-        off = self.sampling_offsets(query).view(B, Q, H, L, P, 2)
-        aw = F.softmax(self.attention_weights(query).view(B, Q, H, L * P).float(), -1).view(B, Q, H, L, P)
+        off = self.sampling_offsets(query)
+        logits = self.attention_weights(query)
+        if (_FUSED_MSDA and v.is_cuda and v.dtype == off.dtype == logits.dtype == torch.bfloat16
+                and not ref_boxes.requires_grad and L * P <= 16):
+            st, so = _level_tensors(shapes, v.device)
+            out = _MSDAFusedHip.apply(v, st, so, off, ref_boxes, logits, float(self.offset_scale), L, P)
+            return self.output_proj(out)
+        off = off.view(B, Q, H, L, P, 2)
+        aw = F.softmax(logits.view(B, Q, H, L * P).float(), -1).view(B, Q, H, L, P)
         ref = ref_boxes[:, :, None, None, None, :]
         loc = ref[..., :2] + off / P * ref[..., 2:] * self.offset_scale
         return self.output_proj(deformable_attention(v, shapes, loc, aw))

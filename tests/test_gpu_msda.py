@@ -73,3 +73,42 @@ def test_msda_bwd_bf16_atomics_vs_fp32(hip_lib):
     assert torch.equal(gl16, gl32) and torch.equal(ga16, ga32)
     rel = float((gv16.float() - gv32).norm() / gv32.norm())
     assert rel < 4e-3, rel
+
+
+def test_msda_fused_prep_matches_unfused(hip_lib):
+    """rtdetr_msda_fused_fwd/bwd (locations + softmax formed in the kernel)
+    against the unfused decoder formulation (torch prep + rtdetr_msda_*) on the
+    C2 decoder shapes: output and the gradients of value, sampling offsets and
+    attention logits."""
+    import torch.nn.functional as F
+
+    from src.rtdetr_moe.decoder import _MSDAFusedHip, _level_tensors, deformable_attention
+
+    g = torch.Generator().manual_seed(2)
+    shapes = [(92, 160), (46, 80), (23, 40)]
+    B, Q, H, D, L, P = 4, 300, 8, 32, 3, 4
+    S = sum(h * w for h, w in shapes)
+    dev = "cuda"
+    value = torch.randn(B, S, H, D, generator=g).to(torch.bfloat16).to(dev)
+    off = (torch.randn(B, Q, H * L * P * 2, generator=g) * 2).to(torch.bfloat16).to(dev)
+    logits = torch.randn(B, Q, H * L * P, generator=g).to(torch.bfloat16).to(dev)
+    ref = torch.cat([torch.rand(B, Q, 2, generator=g) * 0.8 + 0.1, torch.rand(B, Q, 2, generator=g) * 0.3 + 0.02],
+                    -1).to(dev)
+    gout = torch.randn(B, Q, H * D, generator=g).to(torch.bfloat16).to(dev)
+    scale = 0.5
+    res = []
+    for fused in (False, True):
+        v, o, lg = (t.clone().requires_grad_(True) for t in (value, off, logits))
+        if fused:
+            st, so = _level_tensors(shapes, torch.device(dev))
+            out = _MSDAFusedHip.apply(v, st, so, o, ref, lg, scale, L, P)
+        else:
+            aw = F.softmax(lg.view(B, Q, H, L * P).float(), -1).view(B, Q, H, L, P)
+            r = ref[:, :, None, None, None, :]
+            loc = r[..., :2] + o.view(B, Q, H, L, P, 2) / P * r[..., 2:] * scale
+            out = deformable_attention(v, shapes, loc, aw)
+        (out.float() * gout.float()).sum().backward()
+        res.append((out.detach().float(), v.grad.float(), o.grad.float(), lg.grad.float()))
+    for name, a, b in zip(("out", "value", "off", "logits"), res[0], res[1]):
+        rel = float((b - a).norm() / a.norm().clamp_min(1e-12))
+        assert rel < 1e-2, f"{name}: rel err {rel:.3e}"
