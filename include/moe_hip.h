@@ -244,6 +244,17 @@ int rtdetr_add_bias_relu_nhwc(const void* a, const void* b, const float* bias, l
  * int32 pairs {record, chunk of 2048 elements}.  out = RNE(float(w) * scale). */
 int rtdetr_fold_scale_multi(const void* records, const int32_t* chunks, int n_chunks, hipStream_t stream);
 
+/* Decoder box refinement (one launch each way), over n = B*Q*4 elements:
+ *   y = sigmoid(delta + log(max(x', eps) / max(1 - x', eps))), x' = clamp(ref, 0, 1)
+ * delta bf16 (delta_bf16 = 1) or fp32; ref, y fp32.  Backward:
+ *   g_delta = (g_boxes + g_inter) y (1 - y)          (either gradient may be NULL)
+ *   g_ref   = g_boxes y (1 - y) d inverse_sigmoid / d ref   (g_ref NULL: not needed) */
+int rtdetr_box_refine_fwd(const void* delta, int delta_bf16, const float* ref, long long n, float eps, float* y,
+                          hipStream_t stream);
+int rtdetr_box_refine_bwd(const float* g_boxes, const float* g_inter, const float* y, const float* ref,
+                          long long n, float eps, void* g_delta, int delta_bf16, float* g_ref,
+                          hipStream_t stream);
+
 /* Backward of a block output feeding two consumers:
  *   out = (g1 + g2) * (y > 0)   (bf16 NHWC [M, C]; g2 may be NULL)
  * the gradient accumulation and the ReLU mask in one pass. */

@@ -45,6 +45,8 @@ SIGNATURES = {
     "rtdetr_add_bias_relu_nhwc": (_I, [_P, _P, _P, ctypes.c_longlong, _I, _P, _P]),
     "rtdetr_relu_grad2_nhwc": (_I, [_P, _P, _P, ctypes.c_longlong, _I, _P, _P]),
     "rtdetr_fold_scale_multi": (_I, [_P, _P, _I, _P]),
+    "rtdetr_box_refine_fwd": (_I, [_P, _I, _P, ctypes.c_longlong, _F, _P, _P]),
+    "rtdetr_box_refine_bwd": (_I, [_P, _P, _P, _P, ctypes.c_longlong, _F, _P, _I, _P, _P]),
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_msda_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "rtdetr_msda_bwd_bf16": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),

@@ -23,6 +23,55 @@ def inverse_sigmoid(x, eps=1e-5):
     return torch.log(x.clamp(min=eps) / (1 - x).clamp(min=eps))
 
 
+class _BoxRefineHip(torch.autograd.Function):
+    """(boxes, inter) = sigmoid(delta + inverse_sigmoid(ref)) twice over: the
+    same values, ``boxes`` with a gradient to ``ref`` (the loss term) and
+    ``inter`` without (the next layer's reference) -- the upstream decoder's
+    two sigmoid(delta + inverse_sigmoid(.)) evaluations on ref and on
+    ref.detach().  One HIP launch each way (rtdetr_box_refine_fwd/bwd)."""
+
+    @staticmethod
+    def forward(ctx, delta, ref, eps):
+        from ..moe import _lib as L
+
+        d = delta.contiguous()
+        r = ref.float().contiguous()
+        y = torch.empty(r.shape, dtype=torch.float32, device=r.device)
+        L._check(L.lib().rtdetr_box_refine_fwd(d.data_ptr(), int(d.dtype == torch.bfloat16), r.data_ptr(), r.numel(),
+                                               float(eps), y.data_ptr(), L._stream()), "rtdetr_box_refine_fwd")
+        ctx.save_for_backward(y, r)
+        ctx.eps, ctx.ddt, ctx.rdt = float(eps), d.dtype, ref.dtype
+        return y, y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, g_boxes, g_inter):
+        from ..moe import _lib as L
+
+        y, r = ctx.saved_tensors
+        gb = g_boxes.float().contiguous() if g_boxes is not None else None
+        gi = g_inter.float().contiguous() if g_inter is not None else None
+        gd = torch.empty(y.shape, dtype=ctx.ddt, device=y.device)
+        need_ref = ctx.needs_input_grad[1] and gb is not None
+        gr = torch.empty_like(y) if need_ref else None
+        L._check(L.lib().rtdetr_box_refine_bwd(None if gb is None else gb.data_ptr(),
+                                               None if gi is None else gi.data_ptr(), y.data_ptr(), r.data_ptr(),
+                                               y.numel(), ctx.eps, gd.data_ptr(), int(ctx.ddt == torch.bfloat16),
+                                               None if gr is None else gr.data_ptr(), L._stream()),
+                 "rtdetr_box_refine_bwd")
+        return gd, (gr.to(ctx.rdt) if gr is not None else None), None
+
+
+def box_refine(delta, ref, eps=1e-5):
+    """-> (boxes, inter): sigmoid(delta + inverse_sigmoid(ref)), boxes with a
+    gradient to ref, inter without (see _BoxRefineHip)."""
+    if delta.is_cuda and delta.dtype in (torch.bfloat16, torch.float32) and _FUSED_BOXES:
+        return _BoxRefineHip.apply(delta, ref, eps)
+    d = delta.float()
+    boxes = (d + inverse_sigmoid(ref, eps)).sigmoid()
+    inter = (d + inverse_sigmoid(ref.detach(), eps)).sigmoid()
+    return boxes, inter
+
+
 class MLP(nn.Module):
     def __init__(self, din, dh, dout, n):
         super().__init__()
@@ -113,6 +162,7 @@ class _MSDAFusedHip(torch.autograd.Function):
 
 _LEVEL_CACHE = {}
 _FUSED_MSDA = os.environ.get("MOE_FUSED_MSDA", "1") != "0"  # A/B switch
+_FUSED_BOXES = os.environ.get("MOE_FUSED_BOXES", "1") != "0"  # A/B switch
 
 
 def _level_tensors(shapes, device):
@@ -276,10 +326,12 @@ class RTDETRDecoder(nn.Module):
         for i, layer in enumerate(self.layers):
             query_pos = self.query_pos_head(ref_detach.to(tgt.dtype))
             tgt = layer(tgt, ref_detach, memory, shapes, query_pos, ctx)
-            delta = self.dec_bbox_head[i](tgt).float()
-            inter = (delta + inverse_sigmoid(ref_detach)).sigmoid()
+            # boxes_i = sigmoid(delta_i + inverse_sigmoid(ref)) with a gradient to
+            # the previous layer's boxes; the next reference is the same value
+            # without it (upstream: inter on ref_detach, boxes on ref)
+            boxes, inter = box_refine(self.dec_bbox_head[i](tgt), ref)
             dec_logits.append(self.dec_score_head[i](tgt))
-            dec_boxes.append(inter if i == 0 else (delta + inverse_sigmoid(ref)).sigmoid())
+            dec_boxes.append(boxes)
             ref = inter
             ref_detach = inter.detach()
         out = {"pred_logits": dec_logits[-1], "pred_boxes": dec_boxes[-1],

@@ -112,3 +112,36 @@ def test_msda_fused_prep_matches_unfused(hip_lib):
     for name, a, b in zip(("out", "value", "off", "logits"), res[0], res[1]):
         rel = float((b - a).norm() / a.norm().clamp_min(1e-12))
         assert rel < 1e-2, f"{name}: rel err {rel:.3e}"
+
+
+def test_box_refine_matches_torch(hip_lib):
+    """rtdetr_box_refine_fwd/bwd against the upstream decoder's two
+    sigmoid(delta + inverse_sigmoid(.)) evaluations (on ref and ref.detach()),
+    including references at and beyond the clamp edges."""
+    from src.rtdetr_moe.decoder import _BoxRefineHip, inverse_sigmoid
+
+    g = torch.Generator().manual_seed(3)
+    dev = "cuda"
+    delta0 = torch.randn(4, 300, 4, generator=g).to(torch.bfloat16).to(dev)
+    ref0 = torch.rand(4, 300, 4, generator=g).to(dev)
+    ref0[0, :4, 0] = torch.tensor([0.0, 1.0, 1e-7, 1.0 - 1e-7], device=dev)
+    gb = torch.randn(4, 300, 4, generator=g).to(dev)
+    gi = torch.randn(4, 300, 4, generator=g).to(dev)
+    res = []
+    for fused in (False, True):
+        d = delta0.clone().requires_grad_(True)
+        r = ref0.clone().requires_grad_(True)
+        if fused:
+            boxes, inter = _BoxRefineHip.apply(d, r, 1e-5)
+        else:
+            boxes = (d.float() + inverse_sigmoid(r)).sigmoid()
+            inter = (d.float() + inverse_sigmoid(r.detach())).sigmoid()
+        ((boxes * gb).sum() + (inter * gi).sum()).backward()
+        res.append((boxes.detach(), inter.detach(), d.grad.float(), r.grad))
+    for name, a, b in zip(("boxes", "inter", "d_ref"), (res[0][0], res[0][1], res[0][3]),
+                          (res[1][0], res[1][1], res[1][3])):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-5, msg=name)
+    # d_delta is bf16: torch rounds each path's gradient to bf16 and adds them
+    # (two roundings), the kernel rounds their fp32 sum once
+    rel = float((res[1][2] - res[0][2]).norm() / res[0][2].norm())
+    assert rel < 5e-3, rel
