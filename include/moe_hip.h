@@ -309,6 +309,29 @@ int moe_aux_loss_fwd(const float* aux_partials, int nblk, int E, const int32_t* 
 int rtdetr_hungarian_match(const float* cost, const int32_t* n_valid, int S, int B, int Q, int M,
                            int32_t* assign, int32_t* status, hipStream_t stream);
 
+/* RT-DETR set criterion fused (SetCriterion.loss_padded): S prediction sets,
+ * B images, Q queries, C classes, M padded targets (first n_valid[b] real);
+ * logits fp32 [S,B,Q,C], boxes fp32 [S,B,Q,4] cxcywh, tgt_boxes fp32 [B,M,4],
+ * tgt_labels int32 [B,M].
+ *   _match: Hungarian matching with the matching cost (2 focal class + 5 L1 +
+ *           2 GIoU) evaluated inside the solver; assign int32 [S,B,M] as
+ *           rtdetr_hungarian_match.
+ *   _loss:  one workgroup per set: comps[S][3] = {VFL, L1, GIoU} / num_boxes
+ *           (num_boxes: device scalar; VFL weight alpha p^2 (1 - onehot) + IoU),
+ *           and their gradients d_logits [S,B,Q,C], d_l1 / d_giou [S,B,Q,4].
+ *           B*Q*C*4 bytes must fit 64 KiB (LDS score map).
+ *   _loss_bwd: g_logits = g[s,0] d_logits, g_boxes = g[s,1] d_l1 + g[s,2] d_giou. */
+int rtdetr_set_criterion_match(const float* logits, const float* boxes, const float* tgt_boxes,
+                               const int32_t* tgt_labels, const int32_t* n_valid, int S, int B, int Q,
+                               int C, int M, int32_t* assign, int32_t* status, hipStream_t stream);
+int rtdetr_set_criterion_loss(const float* logits, const float* boxes, const float* tgt_boxes,
+                              const int32_t* tgt_labels, const int32_t* n_valid, const int32_t* assign,
+                              const float* num_boxes, float vfl_alpha, int S, int B, int Q, int C, int M,
+                              float* comps, float* d_logits, float* d_l1, float* d_giou, hipStream_t stream);
+int rtdetr_set_criterion_loss_bwd(const float* g_comps, int S, int B, int Q, int C, const float* d_logits,
+                                  const float* d_l1, const float* d_giou, float* g_logits, float* g_boxes,
+                                  hipStream_t stream);
+
 /* Training-step optimizer (the bench step's AdamW; reference: Ultralytics'
  * AdamW inside RTDETR.train, src/models/vision/rtdetr.py:82-94, with
  * torch.optim.AdamW + torch.nn.utils.clip_grad_norm_ semantics) over flat

@@ -55,6 +55,9 @@ SIGNATURES = {
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "moe_set_splitk_workspace": (_I, [_P, ctypes.c_size_t, _P, _I]),
     "rtdetr_hungarian_match": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "rtdetr_set_criterion_match": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "rtdetr_set_criterion_loss": (_I, [_P, _P, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "rtdetr_set_criterion_loss_bwd": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "moe_aux_loss_fwd": (_I, [_P, _I, _I, _P, _I, _I, _F, _F, _P, _P, _P]),
     "train_grad_sqnorm": (_I, [_P, _P, _I, _P, _P]),
     "train_grad_norm_finalize": (_I, [_P, _I, _F, _F, _P, _P, _I, _P, _P]),

@@ -209,6 +209,33 @@ class SetCriterion(nn.Module):
         return losses
 
 
+    def loss_padded(self, outputs, tgt_boxes, tgt_labels, n_valid, num_boxes, status):
+        """Total weighted loss (differentiable scalar) and the per-set components
+        {name: detached value} of ``forward_padded``, with the matching and the
+        losses fused into HIP kernels (_SetLossHip).  GPU only; needs
+        gamma == 2 and B*Q*C*4 bytes <= 64 KiB."""
+        sets = self._sets(outputs)
+        logits = torch.stack([o["pred_logits"] for _, o in sets]).float()
+        boxes = torch.stack([o["pred_boxes"] for _, o in sets]).float()
+        comps, _ = _SetLossHip.apply(logits, boxes, tgt_boxes, tgt_labels, n_valid, num_boxes, status, self.alpha)
+        key = (comps.device, tuple(self.w.values()))
+        w = getattr(self, "_wvec", None)
+        if w is None or w[0] != key:
+            w = (key, torch.tensor([self.w["loss_vfl"], self.w["loss_bbox"], self.w["loss_giou"]],
+                                   dtype=torch.float32, device=comps.device))
+            self._wvec = w
+        weighted = comps * w[1]
+        total = weighted.sum()
+        det = weighted.detach()
+        names = ["loss_vfl", "loss_bbox", "loss_giou"]
+        parts = {n + suffix: det[s_, k] for s_, (suffix, _) in enumerate(sets) for k, n in enumerate(names)}
+        return total, parts
+
+    def fused_ok(self, outputs, M):
+        lg = outputs["pred_logits"]
+        B, Q, C = lg.shape
+        return lg.is_cuda and self.gamma == 2.0 and B * Q * C * 4 <= 64 * 1024 and M <= 1024 and Q <= 4096
+
     def forward_padded(self, outputs, tgt_boxes, tgt_labels, n_valid, num_boxes, status=None):
         """The same losses as ``forward`` with fixed shapes and no host round
         trip, so the whole training step can be one hipGraph: targets padded to
@@ -266,6 +293,52 @@ class SetCriterion(nn.Module):
             losses["loss_bbox" + suffix] = l1[s_] * self.w["loss_bbox"]
             losses["loss_giou" + suffix] = lg[s_] * self.w["loss_giou"]
         return losses
+
+
+class _SetLossHip(torch.autograd.Function):
+    """Matching + VFL/L1/GIoU losses of all prediction sets in three HIP
+    launches (rtdetr_set_criterion_match / _loss), their gradients computed in
+    the same pass and scaled in the backward (rtdetr_set_criterion_loss_bwd)."""
+
+    @staticmethod
+    def forward(ctx, logits, boxes, tgt_boxes, tgt_labels, n_valid, num_boxes, status, vfl_alpha):
+        from ..moe import _lib as L
+
+        S, B, Q, C = logits.shape
+        M = tgt_boxes.shape[1]
+        lg, bx = logits.contiguous(), boxes.contiguous()
+        tb, tl, nv = tgt_boxes.float().contiguous(), tgt_labels.to(torch.int32).contiguous(), n_valid.contiguous()
+        nb = num_boxes.float().reshape(1).contiguous()
+        assign = torch.empty((S, B, M), dtype=torch.int32, device=lg.device)
+        s = L._stream()
+        L._check(L.lib().rtdetr_set_criterion_match(lg.data_ptr(), bx.data_ptr(), tb.data_ptr(), tl.data_ptr(),
+                                                    nv.data_ptr(), S, B, Q, C, M, assign.data_ptr(),
+                                                    status.data_ptr(), s), "rtdetr_set_criterion_match")
+        comps = torch.empty((S, 3), dtype=torch.float32, device=lg.device)
+        d_lg = torch.empty_like(lg)
+        d_l1 = torch.empty_like(bx)
+        d_gi = torch.empty_like(bx)
+        L._check(L.lib().rtdetr_set_criterion_loss(lg.data_ptr(), bx.data_ptr(), tb.data_ptr(), tl.data_ptr(),
+                                                   nv.data_ptr(), assign.data_ptr(), nb.data_ptr(), float(vfl_alpha),
+                                                   S, B, Q, C, M, comps.data_ptr(), d_lg.data_ptr(),
+                                                   d_l1.data_ptr(), d_gi.data_ptr(), s), "rtdetr_set_criterion_loss")
+        ctx.save_for_backward(d_lg, d_l1, d_gi)
+        ctx.mark_non_differentiable(assign)
+        return comps, assign
+
+    @staticmethod
+    def backward(ctx, g_comps, _g_assign):
+        from ..moe import _lib as L
+
+        d_lg, d_l1, d_gi = ctx.saved_tensors
+        S, B, Q, C = d_lg.shape
+        g = g_comps.float().contiguous()
+        g_lg = torch.empty_like(d_lg)
+        g_bx = torch.empty_like(d_l1)
+        L._check(L.lib().rtdetr_set_criterion_loss_bwd(g.data_ptr(), S, B, Q, C, d_lg.data_ptr(), d_l1.data_ptr(),
+                                                       d_gi.data_ptr(), g_lg.data_ptr(), g_bx.data_ptr(),
+                                                       L._stream()), "rtdetr_set_criterion_loss_bwd")
+        return g_lg, g_bx, None, None, None, None, None, None
 
 
 PAD_BOX = (0.5, 0.5, 0.1, 0.1)  # finite stand-in for padded target slots (masked out of every loss)

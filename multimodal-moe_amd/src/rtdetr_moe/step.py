@@ -19,6 +19,7 @@ their gradients reach the router through the captured backward.
 """
 from __future__ import annotations
 
+import os
 import time
 
 import torch
@@ -26,6 +27,8 @@ import torch.distributed as dist
 from torch import nn
 
 from .model import RTDETRMoE
+
+_FUSED_CRIT = os.environ.get("MOE_FUSED_CRITERION", "1") != "0"  # A/B switch
 
 
 class FlatOutputs(nn.Module):
@@ -157,6 +160,9 @@ class GraphedStep:
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.autocast, cache_enabled=False):
             flat = self.fn(self.static_images, self.static_ctx)
         out, aux = FlatOutputs.unflatten(flat)
+        if _FUSED_CRIT and self.criterion.fused_ok(out, self.M):  # matching + losses in 3 HIP launches
+            total, losses = self.criterion.loss_padded(out, self.tb, self.tl, self.nv, self.nb, self.status)
+            return total + aux, losses
         losses = self.criterion.forward_padded(out, self.tb, self.tl, self.nv, self.nb, self.status)
         return sum(losses.values()) + aux, losses
 

@@ -185,3 +185,45 @@ def test_padded_criterion_matches_host_matching(hip_lib):
     assert set(ref) == set(got)
     for k in ref:
         torch.testing.assert_close(got[k], ref[k], rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C", [1, 3])
+def test_fused_criterion_matches_padded(hip_lib, C):
+    """SetCriterion.loss_padded (matching cost evaluated inside the GPU
+    Hungarian solver; VFL/L1/GIoU and their gradients in one HIP pass per
+    set) gives forward_padded's losses and the same gradients w.r.t. every
+    set's logits and boxes.  fp32 tolerance: rtol 1e-4 on the losses, 1e-4
+    relative (atol 1e-6) on the gradients (expf/logf vs torch's sigmoid/log)."""
+    from src.rtdetr_moe.criterion import SetCriterion, pad_targets
+
+    g = torch.Generator(device=DEV).manual_seed(11 + C)
+    S, B, Q, M = 7, 4, 300, 16
+
+    def o():
+        return {"pred_logits": torch.randn(B, Q, C, device=DEV, generator=g).requires_grad_(True),
+                "pred_boxes": (torch.rand(B, Q, 4, device=DEV, generator=g) * 0.5 + 0.2).requires_grad_(True)}
+    out = o()
+    out["aux_outputs"] = [o() for _ in range(S - 2)]
+    out["enc_outputs"] = o()
+    leaves = [t for s in [out] + out["aux_outputs"] + [out["enc_outputs"]]
+              for t in (s["pred_logits"], s["pred_boxes"])]
+    counts = [0, 3, 16, 1]
+    targets = [{"boxes": torch.rand(n, 4, device=DEV, generator=g) * 0.4 + 0.3,
+                "labels": torch.randint(0, C, (n,), device=DEV, generator=g)} for n in counts]
+    crit = SetCriterion(num_classes=C)
+    tb, tl, nv = pad_targets(targets, M)
+    nb = torch.tensor(float(sum(counts)), device=DEV)
+    assert crit.fused_ok(out, M)
+    ref = crit.forward_padded(out, tb, tl, nv, nb)
+    ref_grads = torch.autograd.grad(sum(ref.values()), leaves)
+    status = torch.zeros(1, dtype=torch.int32, device=DEV)
+    total, got = crit.loss_padded(out, tb, tl, nv, nb, status)
+    got_grads = torch.autograd.grad(total, leaves)
+    assert int(status.item()) == 0
+    assert set(ref) == set(got)
+    for k in ref:
+        torch.testing.assert_close(got[k], ref[k].detach(), rtol=1e-4, atol=1e-6, msg=k)
+    torch.testing.assert_close(total.detach(), sum(ref.values()).detach(), rtol=1e-4, atol=1e-6)
+    for i, (a, b) in enumerate(zip(got_grads, ref_grads)):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6, msg=f"grad of leaf {i}")

@@ -84,8 +84,8 @@ def glue_by_line(prof, steps):
     for e in prof.key_averages(group_by_stack_n=12):
         if e.key not in GLUE:
             continue
-        frames = [fr for fr in (e.stack or []) if "multimodal-moe_amd" in fr]
-        src = " <- ".join(fr.split("multimodal-moe_amd/")[-1] for fr in frames[:3]) or "(autograd engine)"
+        frames = [fr for fr in (e.stack or []) if "rtdetr_moe" in fr or "/moe/" in fr or "models/" in fr]
+        src = " <- ".join(fr.split("src/")[-1] for fr in frames[:3]) or "(autograd engine)"
         rows.append((e.device_time_total / 1e3 / steps, e.count / steps, e.key, src))
     rows.sort(key=lambda r: -r[0])
     return "\n".join(f"{t:8.3f} ms {c:7.1f}/step  {n:26s} {src}" for t, c, n, src in rows[:80]) + "\n"
