@@ -13,6 +13,12 @@
   ``class xc yc w h``), plus an optional per-image ``solar_context_bin`` taken
   from a COCO export (scripts/export_coco_dataset.py:146-148) or a
   ``contexts.json`` {image stem: bin label} next to dataset.yaml.
+* ``CocoDataset``: the COCO export (scripts/export_coco_dataset.py:120-195:
+  ``images[]`` with ``file_name`` and ``solar_context_bin``, ``annotations[]``
+  with pixel ``bbox`` [x, y, w, h] and ``category_id``), the input of the
+  RT-DETRv2 adapter (src/models/vision/rtdetr_thirdparty.py:81-108
+  img_folder + ann_file).  Category ids map to contiguous labels in id order
+  (the export's single pedestrian id 1 -> label 0).
 Box helpers restate src/data/bboxes.py (clamp to [0,W-1]x[0,H-1], min 2 px).
 """
 from __future__ import annotations
@@ -188,6 +194,55 @@ class YoloDataset(torch.utils.data.Dataset):
         t = {"boxes": torch.tensor(boxes, dtype=torch.float32).reshape(-1, 4),
              "labels": torch.tensor(labels, dtype=torch.int64), "orig_size": (self.pad_w, self.pad_h)}
         return img, t, self.contexts.get(p.stem, MISSING_ID)
+
+
+class CocoDataset(torch.utils.data.Dataset):
+    def __init__(self, img_folder: str | Path, ann_file: str | Path, imgsz=(704, 1248), pad_to=32):
+        self.img_folder = Path(img_folder)
+        d = json.loads(Path(ann_file).read_text())
+        cats = sorted(int(c["id"]) for c in d.get("categories", []))
+        if not cats:
+            cats = sorted({int(a["category_id"]) for a in d.get("annotations", [])}) or [1]
+        self.cat_to_label = {c: i for i, c in enumerate(cats)}
+        self.num_classes = len(cats)
+        self.images = sorted(d.get("images", []), key=lambda im: im["id"])
+        self.anns = {im["id"]: [] for im in self.images}
+        for a in d.get("annotations", []):
+            if a.get("iscrowd", 0) or a["image_id"] not in self.anns:
+                continue
+            self.anns[a["image_id"]].append(a)
+        self.h, self.w = (imgsz, imgsz) if isinstance(imgsz, int) else imgsz
+        self.pad_h = int(math.ceil(self.h / pad_to) * pad_to)
+        self.pad_w = int(math.ceil(self.w / pad_to) * pad_to)
+
+    def __len__(self):
+        return len(self.images)
+
+    def __getitem__(self, i):
+        from PIL import Image
+
+        im = self.images[i]
+        pil = Image.open(self.img_folder / im["file_name"]).convert("RGB")
+        ow, oh = int(im.get("width", pil.width)), int(im.get("height", pil.height))
+        pil = pil.resize((self.w, self.h), Image.BILINEAR)
+        arr = torch.from_numpy(np.asarray(pil, dtype=np.uint8).copy()).permute(2, 0, 1).float() / 255.0
+        img = torch.zeros((3, self.pad_h, self.pad_w))
+        img[:, : self.h, : self.w] = arr
+        boxes, labels = [], []
+        for a in self.anns[im["id"]]:
+            x, y, w, h = map(float, a["bbox"])
+            x0, y0 = max(x, 0.0), max(y, 0.0)  # SanitizeBoundingBoxes: clip, drop < 1 px
+            x1, y1 = min(x + w, ow), min(y + h, oh)
+            if x1 - x0 < 1 or y1 - y0 < 1:
+                continue
+            # normalised to the content area, then rescaled to the padded tensor
+            boxes.append([(x0 + x1) / 2 / ow * self.w / self.pad_w, (y0 + y1) / 2 / oh * self.h / self.pad_h,
+                          (x1 - x0) / ow * self.w / self.pad_w, (y1 - y0) / oh * self.h / self.pad_h])
+            labels.append(self.cat_to_label[int(a["category_id"])])
+        t = {"boxes": torch.tensor(boxes, dtype=torch.float32).reshape(-1, 4),
+             "labels": torch.tensor(labels, dtype=torch.int64), "orig_size": (self.pad_w, self.pad_h)}
+        ctx = im.get("solar_context_bin")
+        return img, t, MISSING_ID if ctx is None else context_id_from_label(ctx)
 
 
 def collate(batch):

@@ -28,7 +28,7 @@ from torch.nn.parallel import DistributedDataParallel as DDP
 
 from ..moe.config import parse_moe_spec
 from .criterion import SetCriterion
-from .data import SyntheticZOD, YoloDataset, collate
+from .data import CocoDataset, SyntheticZOD, YoloDataset, collate
 from .metrics import BoxMetrics, DetectionEvaluator
 from .model import RTDETRMoE
 
@@ -118,8 +118,9 @@ def save_checkpoint(path: Path, model: RTDETRMoE, epoch: int, fitness: float, op
     torch.save(ck, path)
 
 
-def load_model(weights: str | Path, device="cpu") -> RTDETRMoE:
-    """A checkpoint written by save_checkpoint, or a bare architecture spec."""
+def load_model(weights: str | Path, device="cpu", num_classes: int = 1) -> RTDETRMoE:
+    """A checkpoint written by save_checkpoint, or a bare architecture spec
+    (``num_classes`` applies to the spec only; a checkpoint carries its own)."""
     p = Path(str(weights))
     if p.exists():
         ck = torch.load(p, map_location="cpu", weights_only=True)
@@ -128,7 +129,7 @@ def load_model(weights: str | Path, device="cpu") -> RTDETRMoE:
         return model.to(device)
     if str(weights).endswith((".pt", ".pth")):
         raise FileNotFoundError(f"weights file not found: {weights}")
-    return RTDETRMoE(parse_moe_spec(str(weights))).to(device)
+    return RTDETRMoE(parse_moe_spec(str(weights)), num_classes=num_classes).to(device)
 
 
 # ---------------------------------------------------------------------------
@@ -155,7 +156,10 @@ def _batches(data, split, imgsz, batch, workers, seed, rank, world, epoch):
         for _ in range(_synthetic_steps(data)):
             yield gen.sample()
         return
-    ds = YoloDataset(data, split=split, imgsz=(h, w))
+    if isinstance(data, dict):  # COCO export: {"train"/"val": {"img_folder", "ann_file"}}
+        ds = CocoDataset(data[split]["img_folder"], data[split]["ann_file"], imgsz=(h, w))
+    else:
+        ds = YoloDataset(data, split=split, imgsz=(h, w))
     sampler = torch.utils.data.distributed.DistributedSampler(ds, world, rank, shuffle=split == "train",
                                                               seed=seed) if world > 1 else None
     if sampler is not None:
@@ -187,6 +191,7 @@ class TrainArgs:
     lr_backbone: float = 1e-5
     weight_decay: float = 1e-4
     clip_norm: float = 0.1
+    num_classes: int = 1
 
 
 def _seed_all(seed: int):
@@ -215,7 +220,7 @@ def _train_worker(a: TrainArgs, rank: int, world: int, local: int | str) -> Trai
         os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
         torch.backends.cudnn.benchmark = True
     _seed_all(a.seed)
-    model = load_model(a.model, device)
+    model = load_model(a.model, device, a.num_classes)
     if on_gpu:
         model = model.to(memory_format=torch.channels_last)
     core = model
@@ -349,10 +354,13 @@ def train(a: TrainArgs) -> TrainResults:
 # validation
 # ---------------------------------------------------------------------------
 @torch.no_grad()
-def _evaluate(model: RTDETRMoE, data, split, imgsz, batch, device, workers, seed, speed: dict | None = None):
+def _evaluate(model: RTDETRMoE, data, split, imgsz, batch, device, workers, seed, speed: dict | None = None,
+              ev_out: list | None = None):
     model.eval()
     on_gpu = device.type == "cuda"
     ev = DetectionEvaluator()
+    if ev_out is not None:
+        ev_out.append(ev)
     t_pre = t_inf = t_post = 0.0
     n_img = 0
     for images, targets, ctx in _batches(data, split, imgsz, batch, workers, seed, 0, 1, 0):

@@ -124,6 +124,25 @@ class DetectionEvaluator:
         self.pred_cls.append(pl)
         self.target_cls.append(gt_labels)
 
+    def average_recall(self, max_det: int = 100) -> float:
+        """COCO AR@max_det (all classes, area "all"): per image the max_det
+        highest-scoring detections, recall at each IoU threshold of
+        IOU_THRESHOLDS, averaged over thresholds (and classes present)."""
+        n_gt = {}
+        for tc in self.target_cls:
+            for c in np.asarray(tc).reshape(-1).tolist():
+                n_gt[int(c)] = n_gt.get(int(c), 0) + 1
+        if not n_gt:
+            return -1.0
+        hits = {c: np.zeros(len(IOU_THRESHOLDS)) for c in n_gt}
+        for tp, conf, pc in zip(self.tp, self.conf, self.pred_cls):
+            order = np.argsort(-np.asarray(conf), kind="stable")[:max_det]
+            for j in order:
+                c = int(pc[j])
+                if c in hits:
+                    hits[c] += np.asarray(tp[j], dtype=np.float64)
+        return float(np.mean([(hits[c] / n_gt[c]).mean() for c in n_gt]))
+
     def compute(self) -> BoxMetrics:
         cat = lambda xs, d: np.concatenate(xs, 0) if xs else np.zeros((0,) + d)  # noqa: E731
         tp = cat(self.tp, (len(IOU_THRESHOLDS),))
