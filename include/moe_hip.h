@@ -261,6 +261,25 @@ int rtdetr_box_refine_bwd(const float* g_boxes, const float* g_inter, const floa
 int rtdetr_relu_grad2_nhwc(const void* g1, const void* g2, const void* y, long long M, int C, void* out,
                            hipStream_t stream);
 
+/* Training-mode BatchNorm (batch statistics) of nb = 1 or 2 NHWC bf16 branches
+ * x[i] [M, C] (C a power of two in [8, 2048], M >= 2), summed and activated
+ * (encoder ConvNormLayer act="silu" / RepVggBlock; torch.nn.BatchNorm2d
+ * semantics, reference engine: RT-DETR HybridEncoder):
+ *   y = act(sum_i (x_i - mean_i) invstd_i gamma_i + beta_i), act 0 none / 1 silu.
+ * Host arrays of nb pointers; gamma/beta/running stats fp32 [C] (running
+ * arrays may be NULL: no update; else momentum update, unbiased variance).
+ * saved fp32 [nb][4][C] = mean, invstd, scale, shift (kept for backward);
+ * ws: rtdetr_bn_act_workspace(M, C, nb) bytes of device scratch.
+ * Backward: dx[i] bf16 [M, C]; coef fp32 [nb][3][C] scratch; dgb fp32
+ * [nb][2][C] = dgamma, dbeta.  Deterministic (no atomics). */
+size_t rtdetr_bn_act_workspace(long long M, int C, int nb);
+int rtdetr_bn_act_fwd(const void* const* x, const float* const* gamma, const float* const* beta,
+                      float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act, float eps,
+                      float momentum, float* saved, float* ws, void* y, hipStream_t stream);
+int rtdetr_bn_act_bwd(const void* dy, const void* const* x, const float* const* gamma, int nb, long long M, int C,
+                      int act, const float* saved, float* ws, float* coef, void* const* dx, float* dgb,
+                      hipStream_t stream);
+
 /* Process-wide tuning overrides (not thread-safe; set before launching).  By
  * default (0) every launch picks its own kernel variant, ring depth and tile
  * height from its shape; these force one (kernel benchmarks and tests):

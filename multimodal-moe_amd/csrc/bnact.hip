@@ -1,0 +1,412 @@
+// Training-mode BatchNorm (batch statistics) fused with what follows it in the
+// RT-DETR HybridEncoder (the dense body around the MoE path):
+//   ConvNormLayer(act="silu"):  y = silu(BN(x))
+//   RepVggBlock:                y = silu(BN1(x1) + BN2(x2))
+// over NHWC (channels_last) bf16 activations x_i [M = N*H*W, C], fp32 affine /
+// statistics.  torch runs each BN as three MIOpen kernels forward and three
+// backward plus separate add / silu / silu_backward passes; here:
+//   forward:  bn_stats (per-block partial sums of x and x^2, both branches in
+//             one launch) -> bn_finalize (mean, invstd, scale/shift, running
+//             stats) -> bn_apply (normalise, sum branches, activate; one pass)
+//   backward: bn_bwd_reduce (g = dy * act'(z) recomputed from x, partial sums
+//             of g and g * xhat_i) -> bn_bwd_finalize (dgamma, dbeta and the
+//             per-channel coefficients of dx) -> bn_bwd_dx (every branch's dx
+//             in one pass).
+// Deterministic: fixed partition of rows into blocks, fixed reduction trees,
+// no atomics.  Rows per block are fixed by M alone, so eager and graph runs
+// agree bit for bit.  Each thread moves 16-B chunks (8 channels); C is a power
+// of two in [8, 2048] so a block's 256 threads tile whole rows.
+#include "moe_common.h"
+#include "prof.h"
+
+namespace moe {
+
+struct BnArgs {
+  const uint4* x[2];
+  const float* gamma[2];
+  const float* beta[2];
+  float* run_mean[2];
+  float* run_var[2];
+  int nb;  // branches: 1 or 2
+};
+
+constexpr int BN_MAX_BLOCKS = 256;
+
+__device__ __forceinline__ void load8f(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+__device__ __forceinline__ float sigmoidf_(float z) { return 1.f / (1.f + __expf(-z)); }
+
+// partial sums of x and x^2: part[br][blk][2][C]
+__global__ __launch_bounds__(256) void bn_stats_kernel(BnArgs a, long long M, int C, int rpb,
+                                                       float* __restrict__ part) {
+  extern __shared__ float sm[];  // [2][groups][C] = 2 * 256 * 8 floats
+  const int br = blockIdx.y, cch = C >> 3, groups = 256 / cch;
+  const int t = threadIdx.x, cc = t % cch, g = t / cch;
+  const long long r0 = (long long)blockIdx.x * rpb;
+  const long long r1 = r0 + rpb < M ? r0 + rpb : M;
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+  const uint4* x = a.x[br];
+  long long r = r0 + g;
+  for (; r + 3 * groups < r1; r += 4 * groups) {  // 4 rows in flight per thread
+    uint4 u[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[k] = x[(r + (long long)k * groups) * cch + cc];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float v[8];
+      unpack8(u[k], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += v[j];
+        q[j] = fmaf(v[j], v[j], q[j]);
+      }
+    }
+  }
+  for (; r < r1; r += groups) {
+    float v[8];
+    unpack8(x[r * cch + cc], v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] += v[j];
+      q[j] = fmaf(v[j], v[j], q[j]);
+    }
+  }
+  float* ss = sm;
+  float* sq = sm + groups * C;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ss[g * C + cc * 8 + j] = s[j];
+    sq[g * C + cc * 8 + j] = q[j];
+  }
+  __syncthreads();
+  float* p = part + ((size_t)br * gridDim.x + blockIdx.x) * 2 * C;
+  for (int c = t; c < C; c += 256) {
+    float a1 = 0.f, a2 = 0.f;
+    for (int k = 0; k < groups; ++k) {
+      a1 += ss[k * C + c];
+      a2 += sq[k * C + c];
+    }
+    p[c] = a1;
+    p[C + c] = a2;
+  }
+}
+
+// Sum of nblk partial rows of `width` floats for 8 channels per block: thread
+// (k, c) adds blocks k, k+32, ...; a fixed tree over k in LDS.  Result for
+// channel c0 + c, slot w, in red[w][c] (w < width).
+__device__ __forceinline__ void reduce_partials(const float* __restrict__ part, int nblk, int width, int C, int c0,
+                                                double* red /*[width][32][8]*/) {
+  const int t = threadIdx.x, c = t & 7, k = t >> 3;  // 32 k-lanes x 8 channels
+  for (int w = 0; w < width; ++w) {
+    double acc = 0.0;
+    for (int b = k; b < nblk; b += 32) acc += (double)part[((size_t)b * width + w) * C + c0 + c];
+    red[(w * 32 + k) * 8 + c] = acc;
+  }
+  __syncthreads();
+  for (int h = 16; h > 0; h >>= 1) {
+    if (k < h)
+      for (int w = 0; w < width; ++w) red[(w * 32 + k) * 8 + c] += red[(w * 32 + k + h) * 8 + c];
+    __syncthreads();
+  }
+}
+
+// saved[br][4][C] = mean, invstd, scale = gamma * invstd, shift = beta - mean * scale;
+// running stats: (1 - m) r + m stat, unbiased variance (torch.nn.BatchNorm2d)
+__global__ __launch_bounds__(256) void bn_finalize_kernel(BnArgs a, const float* __restrict__ part, int nblk,
+                                                          long long M, int C, float eps, float momentum,
+                                                          float* __restrict__ saved) {
+  __shared__ double red[2 * 32 * 8];
+  const int br = blockIdx.y, c0 = blockIdx.x * 8;
+  reduce_partials(part + (size_t)br * nblk * 2 * C, nblk, 2, C, c0, red);
+  const int t = threadIdx.x;
+  if (t < 8) {
+    const int c = c0 + t;
+    const double mean = red[t] / (double)M;
+    const double var = fmax(red[32 * 8 + t] / (double)M - mean * mean, 0.0);
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = a.gamma[br][c] * invstd;
+    float* sv = saved + (size_t)br * 4 * C;
+    sv[c] = (float)mean;
+    sv[C + c] = invstd;
+    sv[2 * C + c] = sc;
+    sv[3 * C + c] = a.beta[br][c] - (float)mean * sc;
+    if (a.run_mean[br] != nullptr) {
+      a.run_mean[br][c] = (1.f - momentum) * a.run_mean[br][c] + momentum * (float)mean;
+      a.run_var[br][c] = (1.f - momentum) * a.run_var[br][c] + momentum * (float)(var * (double)M / (double)(M - 1));
+    }
+  }
+}
+
+// z = sum_i x_i * scale_i + shift_i for one 8-channel chunk (NB branches,
+// compile-time so that xs stays in registers)
+template <int NB>
+__device__ __forceinline__ void bn_z(const BnArgs& a, const float* __restrict__ saved, int C, long long i, int c0,
+                                     float* z, float (*xs)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = 0.f;
+#pragma unroll
+  for (int br = 0; br < NB; ++br) {
+    float sc[8], sh[8];
+    unpack8(a.x[br][i], xs[br]);
+    load8f(saved + (size_t)br * 4 * C + 2 * C + c0, sc);
+    load8f(saved + (size_t)br * 4 * C + 3 * C + c0, sh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] += fmaf(xs[br][j], sc[j], sh[j]);
+  }
+}
+
+template <int ACT, int NB>
+__global__ __launch_bounds__(256) void bn_apply_kernel(BnArgs a, const float* __restrict__ saved, long long nchunk,
+                                                       int C, uint4* __restrict__ y) {
+  const int cch = C >> 3;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nchunk; i += (long long)gridDim.x * 256) {
+    const int c0 = (int)(i % cch) * 8;
+    float z[8], xs[NB][8];
+    bn_z<NB>(a, saved, C, i, c0, z, xs);
+    if constexpr (ACT == 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = z[j] * sigmoidf_(z[j]);
+    }
+    y[i] = pack8(z);
+  }
+}
+
+// g = dy * act'(z)
+template <int ACT>
+__device__ __forceinline__ void bn_grad_in(const uint4* __restrict__ dy, long long i, const float* z, float* g) {
+  unpack8(dy[i], g);
+  if constexpr (ACT == 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float s = sigmoidf_(z[j]);
+      g[j] *= s * (1.f + z[j] * (1.f - s));
+    }
+  }
+}
+
+// partials part[blk][1 + nb][C]: sum g, sum g * xhat_i
+template <int ACT, int NB>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, const uint4* __restrict__ dy,
+                                                            const float* __restrict__ saved, long long M, int C,
+                                                            int rpb, float* __restrict__ part) {
+  extern __shared__ float sm[];  // [3][groups][C]
+  const int cch = C >> 3, groups = 256 / cch, width = 1 + NB;
+  const int t = threadIdx.x, cc = t % cch, g = t / cch, c0 = cc * 8;
+  const long long r0 = (long long)blockIdx.x * rpb;
+  const long long r1 = r0 + rpb < M ? r0 + rpb : M;
+  float mean[NB][8], inv[NB][8];
+#pragma unroll
+  for (int br = 0; br < NB; ++br) {
+    load8f(saved + (size_t)br * 4 * C + c0, mean[br]);
+    load8f(saved + (size_t)br * 4 * C + C + c0, inv[br]);
+  }
+  float sg[8], sgx[NB][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sg[j] = 0.f;
+#pragma unroll
+    for (int br = 0; br < NB; ++br) sgx[br][j] = 0.f;
+  }
+  for (long long r = r0 + g; r < r1; r += groups) {
+    const long long i = r * cch + cc;
+    float z[8], xs[NB][8], gv[8];
+    bn_z<NB>(a, saved, C, i, c0, z, xs);
+    bn_grad_in<ACT>(dy, i, z, gv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sg[j] += gv[j];
+#pragma unroll
+    for (int br = 0; br < NB; ++br) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sgx[br][j] = fmaf(gv[j], (xs[br][j] - mean[br][j]) * inv[br][j], sgx[br][j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sm[g * C + c0 + j] = sg[j];
+#pragma unroll
+    for (int br = 0; br < NB; ++br) sm[((1 + br) * groups + g) * C + c0 + j] = sgx[br][j];
+  }
+  __syncthreads();
+  float* p = part + (size_t)blockIdx.x * width * C;
+  for (int c = t; c < C; c += 256) {
+    for (int w = 0; w < width; ++w) {
+      float acc = 0.f;
+      for (int k = 0; k < groups; ++k) acc += sm[(w * groups + k) * C + c];
+      p[w * C + c] = acc;
+    }
+  }
+}
+
+// dgb[br][2][C] = dgamma, dbeta; coef[br][3][C] = (A, B, D) with
+// dx_i = A g + B x_i + D:  A = scale, B = -scale * invstd * Sgx / M,
+// D = -scale * Sg / M - B * mean
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(BnArgs a, const float* __restrict__ part, int nblk,
+                                                              long long M, int C, const float* __restrict__ saved,
+                                                              float* __restrict__ coef, float* __restrict__ dgb) {
+  __shared__ double red[3 * 32 * 8];
+  const int c0 = blockIdx.x * 8, width = 1 + a.nb;
+  reduce_partials(part, nblk, width, C, c0, red);
+  const int t = threadIdx.x;
+  if (t < 8 * a.nb) {
+    const int br = t >> 3, c = c0 + (t & 7);
+    const double sg = red[t & 7], sgx = red[((1 + br) * 32) * 8 + (t & 7)];
+    const float* sv = saved + (size_t)br * 4 * C;
+    const double mean = sv[c], inv = sv[C + c], sc = sv[2 * C + c];
+    const double B = -sc * inv * sgx / (double)M;
+    float* cf = coef + (size_t)br * 3 * C;
+    cf[c] = (float)sc;
+    cf[C + c] = (float)B;
+    cf[2 * C + c] = (float)(-sc * sg / (double)M - B * mean);
+    dgb[(size_t)br * 2 * C + c] = (float)sgx;
+    dgb[(size_t)br * 2 * C + C + c] = (float)sg;
+  }
+}
+
+template <int ACT, int NB>
+__global__ __launch_bounds__(256) void bn_bwd_dx_kernel(BnArgs a, const uint4* __restrict__ dy,
+                                                        const float* __restrict__ saved,
+                                                        const float* __restrict__ coef, long long nchunk, int C,
+                                                        uint4* __restrict__ dx0, uint4* __restrict__ dx1) {
+  const int cch = C >> 3;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nchunk; i += (long long)gridDim.x * 256) {
+    const int c0 = (int)(i % cch) * 8;
+    float z[8], xs[NB][8], gv[8];
+    bn_z<NB>(a, saved, C, i, c0, z, xs);
+    bn_grad_in<ACT>(dy, i, z, gv);
+#pragma unroll
+    for (int br = 0; br < NB; ++br) {
+      float A[8], B[8], D[8], o[8];
+      const float* cf = coef + (size_t)br * 3 * C;
+      load8f(cf + c0, A);
+      load8f(cf + C + c0, B);
+      load8f(cf + 2 * C + c0, D);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = fmaf(A[j], gv[j], fmaf(B[j], xs[br][j], D[j]));
+      (br == 0 ? dx0 : dx1)[i] = pack8(o);
+    }
+  }
+}
+
+static int bn_grid(long long nchunk) {
+  long long g = (nchunk + 255) / 256;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+// rows per block and block count of the reductions: a function of M only
+static void bn_blocks(long long M, int* nblk, int* rpb) {
+  long long n = (M + 127) / 128;
+  if (n > BN_MAX_BLOCKS) n = BN_MAX_BLOCKS;
+  if (n < 1) n = 1;
+  *rpb = (int)((M + n - 1) / n);
+  *nblk = (int)((M + *rpb - 1) / *rpb);
+}
+
+static int bn_check(int nb, long long M, int C, int act) {
+  if (nb < 1 || nb > 2) return fail("bn_act: 1 or 2 branches");
+  if (C < 8 || C > 2048 || (C & (C - 1))) return fail("bn_act: C must be a power of two in [8, 2048]");
+  if (M < 2) return fail("bn_act: need at least 2 rows (unbiased running variance)");
+  if (act < 0 || act > 1) return fail("bn_act: act must be 0 (none) or 1 (silu)");
+  return 0;
+}
+
+}  // namespace moe
+
+using namespace moe;
+
+extern "C" size_t rtdetr_bn_act_workspace(long long M, int C, int nb) {
+  (void)M;
+  return (size_t)BN_MAX_BLOCKS * 3 * C * (nb > 1 ? 2 : 1) * sizeof(float);
+}
+
+extern "C" int rtdetr_bn_act_fwd(const void* const* x, const float* const* gamma, const float* const* beta,
+                                 float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act,
+                                 float eps, float momentum, float* saved, float* ws, void* y, hipStream_t stream) {
+  if (int rc = bn_check(nb, M, C, act)) return rc;
+  if (!x || !gamma || !beta || !saved || !ws || !y) return fail("bn_act_fwd: NULL argument");
+  BnArgs a{};
+  a.nb = nb;
+  for (int i = 0; i < nb; ++i) {
+    if (!x[i] || !gamma[i] || !beta[i]) return fail("bn_act_fwd: NULL branch pointer");
+    a.x[i] = static_cast<const uint4*>(x[i]);
+    a.gamma[i] = gamma[i];
+    a.beta[i] = beta[i];
+    a.run_mean[i] = run_mean ? run_mean[i] : nullptr;
+    a.run_var[i] = run_var ? run_var[i] : nullptr;
+    if ((a.run_mean[i] == nullptr) != (a.run_var[i] == nullptr)) return fail("bn_act_fwd: running mean without var");
+  }
+  int nblk, rpb;
+  bn_blocks(M, &nblk, &rpb);
+  const long long nchunk = M * (C / 8);
+  {
+    ProfScope prof(stream, PROF_CONV_EPI, 2.0 * nb * M * C);
+    MOE_LAUNCH(prof, bn_stats_kernel, dim3(nblk, nb), dim3(256), 2 * 2048 * sizeof(float), stream, a, M, C, rpb, ws);
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8, nb), dim3(256), 0, stream, a, ws, nblk, M, C, eps, momentum,
+                   saved);
+  {
+    ProfScope prof(stream, PROF_CONV_EPI, 2.0 * (nb + 1) * M * C);
+#define BN_APPLY(A, N)                                                                                  \
+  MOE_LAUNCH(prof, (bn_apply_kernel<A, N>), dim3(bn_grid(nchunk)), dim3(256), 0, stream, a, saved, nchunk, C, \
+             static_cast<uint4*>(y))
+    if (act == 1) {
+      if (nb == 2) BN_APPLY(1, 2); else BN_APPLY(1, 1);
+    } else {
+      if (nb == 2) BN_APPLY(0, 2); else BN_APPLY(0, 1);
+    }
+#undef BN_APPLY
+  }
+  return check_launch("rtdetr_bn_act_fwd");
+}
+
+extern "C" int rtdetr_bn_act_bwd(const void* dy, const void* const* x, const float* const* gamma, int nb,
+                                 long long M, int C, int act, const float* saved, float* ws, float* coef,
+                                 void* const* dx, float* dgb, hipStream_t stream) {
+  if (int rc = bn_check(nb, M, C, act)) return rc;
+  if (!dy || !x || !gamma || !saved || !ws || !coef || !dx || !dgb) return fail("bn_act_bwd: NULL argument");
+  BnArgs a{};
+  a.nb = nb;
+  for (int i = 0; i < nb; ++i) {
+    if (!x[i] || !dx[i]) return fail("bn_act_bwd: NULL branch pointer");
+    a.x[i] = static_cast<const uint4*>(x[i]);
+    a.gamma[i] = gamma[i];
+  }
+  int nblk, rpb;
+  bn_blocks(M, &nblk, &rpb);
+  const long long nchunk = M * (C / 8);
+  const size_t shm = 3 * 2048 * sizeof(float);
+  {
+    ProfScope prof(stream, PROF_CONV_EPI, 2.0 * (nb + 1) * M * C);
+#define BN_RED(A, N)                                                                                 \
+  MOE_LAUNCH(prof, (bn_bwd_reduce_kernel<A, N>), dim3(nblk), dim3(256), shm, stream, a,              \
+             static_cast<const uint4*>(dy), saved, M, C, rpb, ws)
+    if (act == 1) {
+      if (nb == 2) BN_RED(1, 2); else BN_RED(1, 1);
+    } else {
+      if (nb == 2) BN_RED(0, 2); else BN_RED(0, 1);
+    }
+#undef BN_RED
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(256), 0, stream, a, ws, nblk, M, C, saved, coef, dgb);
+  {
+    ProfScope prof(stream, PROF_CONV_EPI, 2.0 * (2 * nb + 1) * M * C);
+    uint4* d0 = static_cast<uint4*>(dx[0]);
+    uint4* d1 = nb > 1 ? static_cast<uint4*>(dx[1]) : nullptr;
+#define BN_DX(A, N)                                                                                   \
+  MOE_LAUNCH(prof, (bn_bwd_dx_kernel<A, N>), dim3(bn_grid(nchunk)), dim3(256), 0, stream, a,           \
+             static_cast<const uint4*>(dy), saved, coef, nchunk, C, d0, d1)
+    if (act == 1) {
+      if (nb == 2) BN_DX(1, 2); else BN_DX(1, 1);
+    } else {
+      if (nb == 2) BN_DX(0, 2); else BN_DX(0, 1);
+    }
+#undef BN_DX
+  }
+  return check_launch("rtdetr_bn_act_bwd");
+}

@@ -45,6 +45,9 @@ SIGNATURES = {
     "rtdetr_add_bias_relu_nhwc": (_I, [_P, _P, _P, ctypes.c_longlong, _I, _P, _P]),
     "rtdetr_relu_grad2_nhwc": (_I, [_P, _P, _P, ctypes.c_longlong, _I, _P, _P]),
     "rtdetr_fold_scale_multi": (_I, [_P, _P, _I, _P]),
+    "rtdetr_bn_act_workspace": (ctypes.c_size_t, [ctypes.c_longlong, _I, _I]),
+    "rtdetr_bn_act_fwd": (_I, [_P, _P, _P, _P, _P, _I, ctypes.c_longlong, _I, _I, _F, _F, _P, _P, _P, _P]),
+    "rtdetr_bn_act_bwd": (_I, [_P, _P, _P, _I, ctypes.c_longlong, _I, _I, _P, _P, _P, _P, _P, _P]),
     "rtdetr_box_refine_fwd": (_I, [_P, _I, _P, ctypes.c_longlong, _F, _P, _P]),
     "rtdetr_box_refine_bwd": (_I, [_P, _P, _P, _P, ctypes.c_longlong, _F, _P, _I, _P, _P]),
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
@@ -519,6 +522,58 @@ def relu_grad2_nhwc(g1, g2, y):
     _check(lib().rtdetr_relu_grad2_nhwc(_ptr(g1), _ptr(g2), _ptr(y), M, C, _ptr(out), _stream()),
            "rtdetr_relu_grad2_nhwc")
     return out
+
+
+def _ptrs(ts):
+    arr = (ctypes.c_void_p * len(ts))(*[_ptr(t) for t in ts])
+    return ctypes.cast(arr, ctypes.c_void_p), arr  # keep arr alive with the call
+
+
+def _bn_ws(M, C, nb, dev):
+    n = int(lib().rtdetr_bn_act_workspace(M, C, nb)) // 4
+    return torch.empty(n, dtype=torch.float32, device=dev)
+
+
+def bn_act_fwd(xs, gammas, betas, run_means, run_vars, act, eps, momentum):
+    """Training BatchNorm of 1-2 channels_last bf16 branches, summed, act
+    (0 none / 1 silu) -> (y, saved fp32 [nb, 4, C])."""
+    M, C = _nhwc_rows(xs[0], "x0")
+    nb = len(xs)
+    for i, x in enumerate(xs[1:], 1):
+        if _nhwc_rows(x, f"x{i}") != (M, C):
+            raise MoEKernelError("bn_act: branches differ in shape")
+    for t in list(gammas) + list(betas) + [r for r in run_means + run_vars if r is not None]:
+        _need(t, torch.float32, "bn affine/statistics")
+    y = torch.empty_like(xs[0])
+    saved = torch.empty((nb, 4, C), dtype=torch.float32, device=y.device)
+    ws = _bn_ws(M, C, nb, y.device)
+    px, kx = _ptrs(xs)
+    pg, kg = _ptrs(gammas)
+    pb, kb = _ptrs(betas)
+    has_run = all(r is not None for r in run_means + run_vars)
+    pm, km = _ptrs(run_means) if has_run else (None, None)
+    pv, kv = _ptrs(run_vars) if has_run else (None, None)
+    _check(lib().rtdetr_bn_act_fwd(px, pg, pb, pm, pv, nb, M, C, int(act), float(eps), float(momentum),
+                                   _ptr(saved), _ptr(ws), _ptr(y), _stream()), "rtdetr_bn_act_fwd")
+    return y, saved
+
+
+def bn_act_bwd(dy, xs, gammas, saved, act):
+    """-> ([dx_i bf16], dgb fp32 [nb, 2, C] = dgamma, dbeta)."""
+    M, C = _nhwc_rows(xs[0], "x0")
+    if _nhwc_rows(dy, "dy") != (M, C):
+        raise MoEKernelError("bn_act_bwd: dy shape")
+    nb = len(xs)
+    dxs = [torch.empty_like(x) for x in xs]
+    coef = torch.empty((nb, 3, C), dtype=torch.float32, device=dy.device)
+    dgb = torch.empty((nb, 2, C), dtype=torch.float32, device=dy.device)
+    ws = _bn_ws(M, C, nb, dy.device)
+    px, kx = _ptrs(xs)
+    pg, kg = _ptrs(gammas)
+    pd, kd = _ptrs(dxs)
+    _check(lib().rtdetr_bn_act_bwd(_ptr(dy), px, pg, nb, M, C, int(act), _ptr(saved), _ptr(ws), _ptr(coef), pd,
+                                   _ptr(dgb), _stream()), "rtdetr_bn_act_bwd")
+    return dxs, dgb
 
 
 def msda_fwd(value, shapes, starts, loc, attn):

@@ -16,7 +16,9 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
-from .fused import AddBiasReLU, AddBiasReLUFork, BiasReLU
+from .fused import AddBiasReLU, AddBiasReLUFork, BiasReLU, bn_act, bn_act_ok
+
+_FUSED_BN = os.environ.get("MOE_FUSED_BN", "1") != "0"  # A/B switch: training BN + SiLU in HIP
 
 _DEPTHS = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3], 50: [3, 4, 6, 3], 101: [3, 4, 23, 3]}
 
@@ -192,7 +194,10 @@ class ConvNormLayer(nn.Module):
             if self.act_name == "relu":
                 return BiasReLU.apply(y, shift)
             return y + shift.view(1, -1, 1, 1).to(y.dtype)
-        return self.act(self.norm(self.conv(x)))
+        y = self.conv(x)
+        if self.act_name in (None, "silu") and _FUSED_BN and bn_act_ok([y], [self.norm]):
+            return bn_act([y], [self.norm], self.act_name)  # BN + SiLU in HIP (training statistics)
+        return self.act(self.norm(y))
 
 
 def avg_pool_2x2(x):

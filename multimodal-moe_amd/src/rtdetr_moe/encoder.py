@@ -10,7 +10,8 @@ import torch.nn.functional as F
 
 from ..moe.config import MoEConfig
 from ..moe.layer import MoEFFN
-from .backbone import ConvNormLayer
+from .backbone import _FUSED_BN, ConvNormLayer
+from .fused import bn_act, bn_act_ok
 
 
 class DenseFFN(nn.Module):
@@ -53,6 +54,11 @@ class RepVggBlock(nn.Module):
         self.conv2 = ConvNormLayer(cin, cout, 1, 1)
 
     def forward(self, x):
+        if _FUSED_BN:
+            y1, y2 = self.conv1.conv(x), self.conv2.conv(x)
+            if bn_act_ok([y1, y2], [self.conv1.norm, self.conv2.norm]):  # both BNs + sum + SiLU in HIP
+                return bn_act([y1, y2], [self.conv1.norm, self.conv2.norm], "silu")
+            return F.silu(self.conv1.norm(y1) + self.conv2.norm(y2))
         return F.silu(self.conv1(x) + self.conv2(x))
 
 

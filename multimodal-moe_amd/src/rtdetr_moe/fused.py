@@ -98,3 +98,60 @@ class AddBiasReLUFork(torch.autograd.Function):
         else:
             g = torch.ops.aten.threshold_backward(dy1 if dy2 is None else dy1 + dy2, y, 0)
         return g, g, None
+
+
+# ---------------------------------------------------------------------------
+# Training-mode BatchNorm + activation of the HybridEncoder (not frozen):
+# ConvNormLayer(act="silu") is silu(BN(conv)), RepVggBlock is
+# silu(BN1(conv3x3) + BN2(conv1x1)).  libmoe_hip's rtdetr_bn_act_fwd/_bwd do
+# the batch statistics, the normalisation of both branches, their sum and the
+# SiLU in three launches each way (torch: three MIOpen kernels per BN each way
+# plus add / silu / silu_backward passes).
+# ---------------------------------------------------------------------------
+class _BatchNormAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, act, eps, momentum, bns, *args):
+        nb = len(bns)
+        xs, gammas, betas = args[:nb], args[nb:2 * nb], args[2 * nb:3 * nb]
+        rms = [bn.running_mean for bn in bns]
+        rvs = [bn.running_var for bn in bns]
+        y, saved = L.bn_act_fwd(list(xs), list(gammas), list(betas), rms, rvs, act, eps, momentum)
+        ctx.act, ctx.nb = act, nb
+        ctx.save_for_backward(*xs, *gammas, saved)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        nb = ctx.nb
+        t = ctx.saved_tensors
+        xs, gammas, saved = list(t[:nb]), list(t[nb:2 * nb]), t[2 * nb]
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dxs, dgb = L.bn_act_bwd(dy, xs, gammas, saved, ctx.act)
+        return (None, None, None, None, *dxs, *[dgb[i, 0] for i in range(nb)], *[dgb[i, 1] for i in range(nb)])
+
+
+def bn_act_ok(xs, bns) -> bool:
+    """The fused kernels apply: GPU channels_last bf16 branches of one shape,
+    training-mode affine BatchNorm2d with running statistics and a momentum,
+    C a power of two in [8, 2048]."""
+    x = xs[0]
+    if not (x.is_cuda and x.dim() == 4 and all(_gpu_ok(t) and t.shape == x.shape for t in xs)):
+        return False
+    C = x.shape[1]
+    if C < 8 or C > 2048 or C & (C - 1) or x.numel() // C < 2:
+        return False
+    for bn in bns:
+        if not (isinstance(bn, torch.nn.BatchNorm2d) and bn.training and bn.affine and bn.track_running_stats
+                and bn.momentum is not None and bn.running_mean is not None
+                and bn.weight.dtype == torch.float32 and bn.eps == bns[0].eps and bn.momentum == bns[0].momentum):
+            return False
+    return True
+
+
+def bn_act(xs, bns, act: str | None):
+    """act(sum_i BN_i(x_i)) through libmoe_hip (callers check bn_act_ok).
+    num_batches_tracked is not advanced (it only matters with momentum=None)."""
+    bns = list(bns)
+    a = 1 if act == "silu" else 0
+    return _BatchNormAct.apply(a, float(bns[0].eps), float(bns[0].momentum), bns, *xs,
+                               *[bn.weight for bn in bns], *[bn.bias for bn in bns])
