@@ -30,7 +30,8 @@ struct BnArgs {
   int nb;  // branches: 1 or 2
 };
 
-constexpr int BN_MAX_BLOCKS = 256;
+constexpr int BN_MAX_BLOCKS = 1024;  // partial-sum blocks of a reduction (4 per CU)
+constexpr int BN_FIN_T = 1024;        // finalize threads: 8 channels x 128 block lanes
 
 __device__ __forceinline__ void load8f(const float* p, float* v) {
   const float4 a = *reinterpret_cast<const float4*>(p);
@@ -98,38 +99,52 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(BnArgs a, long long M, in
   }
 }
 
-// Sum of nblk partial rows of `width` floats for 8 channels per block: thread
-// (k, c) adds blocks k, k+32, ...; a fixed tree over k in LDS.  Result for
-// channel c0 + c, slot w, in red[w][c] (w < width).
-__device__ __forceinline__ void reduce_partials(const float* __restrict__ part, int nblk, int width, int C, int c0,
-                                                double* red /*[width][32][8]*/) {
-  const int t = threadIdx.x, c = t & 7, k = t >> 3;  // 32 k-lanes x 8 channels
-  for (int w = 0; w < width; ++w) {
+// Sum of nblk (<= BN_MAX_BLOCKS) partial rows of `width` floats for 8
+// channels per block: thread (k, c) adds blocks k, k+128, ... (all loads issued
+// before the adds), then a fixed tree over k in LDS.  Result for channel
+// c0 + c, slot w, in red[w][0][c].
+template <int WIDTH>
+__device__ __forceinline__ void reduce_partials(const float* __restrict__ part, int nblk, int C, int c0,
+                                                double* red /*[WIDTH][128][8]*/) {
+  constexpr int KL = BN_FIN_T / 8, PER = BN_MAX_BLOCKS / KL;
+  const int t = threadIdx.x, c = t & 7, k = t >> 3;
+  float v[WIDTH][PER];
+#pragma unroll
+  for (int w = 0; w < WIDTH; ++w)
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int b = k + u * KL;
+      v[w][u] = b < nblk ? part[((size_t)b * WIDTH + w) * C + c0 + c] : 0.f;
+    }
+#pragma unroll
+  for (int w = 0; w < WIDTH; ++w) {
     double acc = 0.0;
-    for (int b = k; b < nblk; b += 32) acc += (double)part[((size_t)b * width + w) * C + c0 + c];
-    red[(w * 32 + k) * 8 + c] = acc;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) acc += (double)v[w][u];
+    red[(w * KL + k) * 8 + c] = acc;
   }
   __syncthreads();
-  for (int h = 16; h > 0; h >>= 1) {
+  for (int h = KL / 2; h > 0; h >>= 1) {
     if (k < h)
-      for (int w = 0; w < width; ++w) red[(w * 32 + k) * 8 + c] += red[(w * 32 + k + h) * 8 + c];
+#pragma unroll
+      for (int w = 0; w < WIDTH; ++w) red[(w * KL + k) * 8 + c] += red[(w * KL + k + h) * 8 + c];
     __syncthreads();
   }
 }
 
 // saved[br][4][C] = mean, invstd, scale = gamma * invstd, shift = beta - mean * scale;
 // running stats: (1 - m) r + m stat, unbiased variance (torch.nn.BatchNorm2d)
-__global__ __launch_bounds__(256) void bn_finalize_kernel(BnArgs a, const float* __restrict__ part, int nblk,
-                                                          long long M, int C, float eps, float momentum,
-                                                          float* __restrict__ saved) {
-  __shared__ double red[2 * 32 * 8];
+__global__ __launch_bounds__(BN_FIN_T) void bn_finalize_kernel(BnArgs a, const float* __restrict__ part, int nblk,
+                                                               long long M, int C, float eps, float momentum,
+                                                               float* __restrict__ saved) {
+  __shared__ double red[2 * (BN_FIN_T / 8) * 8];
   const int br = blockIdx.y, c0 = blockIdx.x * 8;
-  reduce_partials(part + (size_t)br * nblk * 2 * C, nblk, 2, C, c0, red);
+  reduce_partials<2>(part + (size_t)br * nblk * 2 * C, nblk, C, c0, red);
   const int t = threadIdx.x;
   if (t < 8) {
     const int c = c0 + t;
     const double mean = red[t] / (double)M;
-    const double var = fmax(red[32 * 8 + t] / (double)M - mean * mean, 0.0);
+    const double var = fmax(red[(BN_FIN_T / 8) * 8 + t] / (double)M - mean * mean, 0.0);
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     const float sc = a.gamma[br][c] * invstd;
     float* sv = saved + (size_t)br * 4 * C;
@@ -191,7 +206,23 @@ __device__ __forceinline__ void bn_grad_in(const uint4* __restrict__ dy, long lo
   }
 }
 
-// partials part[blk][1 + nb][C]: sum g, sum g * xhat_i
+// partials part[blk][1 + nb][C]: sum g, sum g * x_i (xhat applied in the
+// finalize: sum g xhat = invstd (sum g x - mean sum g))
+template <int ACT, int NB>
+__device__ __forceinline__ void bn_bwd_row(const BnArgs& a, const uint4* __restrict__ dy,
+                                           const float* __restrict__ saved, int C, long long i, int c0, float* sg,
+                                           float (*sgx)[8]) {
+  float z[8], xs[NB][8], gv[8];
+  bn_z<NB>(a, saved, C, i, c0, z, xs);
+  bn_grad_in<ACT>(dy, i, z, gv);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sg[j] += gv[j];
+#pragma unroll
+  for (int br = 0; br < NB; ++br)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sgx[br][j] = fmaf(gv[j], xs[br][j], sgx[br][j]);
+}
+
 template <int ACT, int NB>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, const uint4* __restrict__ dy,
                                                             const float* __restrict__ saved, long long M, int C,
@@ -201,12 +232,6 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, const uint
   const int t = threadIdx.x, cc = t % cch, g = t / cch, c0 = cc * 8;
   const long long r0 = (long long)blockIdx.x * rpb;
   const long long r1 = r0 + rpb < M ? r0 + rpb : M;
-  float mean[NB][8], inv[NB][8];
-#pragma unroll
-  for (int br = 0; br < NB; ++br) {
-    load8f(saved + (size_t)br * 4 * C + c0, mean[br]);
-    load8f(saved + (size_t)br * 4 * C + C + c0, inv[br]);
-  }
   float sg[8], sgx[NB][8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -214,19 +239,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, const uint
 #pragma unroll
     for (int br = 0; br < NB; ++br) sgx[br][j] = 0.f;
   }
-  for (long long r = r0 + g; r < r1; r += groups) {
-    const long long i = r * cch + cc;
-    float z[8], xs[NB][8], gv[8];
-    bn_z<NB>(a, saved, C, i, c0, z, xs);
-    bn_grad_in<ACT>(dy, i, z, gv);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sg[j] += gv[j];
-#pragma unroll
-    for (int br = 0; br < NB; ++br) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sgx[br][j] = fmaf(gv[j], (xs[br][j] - mean[br][j]) * inv[br][j], sgx[br][j]);
-    }
+  long long r = r0 + g;
+  for (; r + groups < r1; r += 2 * groups) {
+    bn_bwd_row<ACT, NB>(a, dy, saved, C, r * cch + cc, c0, sg, sgx);
+    bn_bwd_row<ACT, NB>(a, dy, saved, C, (r + groups) * cch + cc, c0, sg, sgx);
   }
+  if (r < r1) bn_bwd_row<ACT, NB>(a, dy, saved, C, r * cch + cc, c0, sg, sgx);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sm[g * C + c0 + j] = sg[j];
@@ -247,18 +265,22 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, const uint
 // dgb[br][2][C] = dgamma, dbeta; coef[br][3][C] = (A, B, D) with
 // dx_i = A g + B x_i + D:  A = scale, B = -scale * invstd * Sgx / M,
 // D = -scale * Sg / M - B * mean
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(BnArgs a, const float* __restrict__ part, int nblk,
-                                                              long long M, int C, const float* __restrict__ saved,
-                                                              float* __restrict__ coef, float* __restrict__ dgb) {
-  __shared__ double red[3 * 32 * 8];
-  const int c0 = blockIdx.x * 8, width = 1 + a.nb;
-  reduce_partials(part, nblk, width, C, c0, red);
+template <int NB>
+__global__ __launch_bounds__(BN_FIN_T) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk,
+                                                                   long long M, int C,
+                                                                   const float* __restrict__ saved,
+                                                                   float* __restrict__ coef, float* __restrict__ dgb) {
+  constexpr int KL = BN_FIN_T / 8;
+  __shared__ double red[(1 + NB) * KL * 8];
+  const int c0 = blockIdx.x * 8;
+  reduce_partials<1 + NB>(part, nblk, C, c0, red);
   const int t = threadIdx.x;
-  if (t < 8 * a.nb) {
+  if (t < 8 * NB) {
     const int br = t >> 3, c = c0 + (t & 7);
-    const double sg = red[t & 7], sgx = red[((1 + br) * 32) * 8 + (t & 7)];
     const float* sv = saved + (size_t)br * 4 * C;
     const double mean = sv[c], inv = sv[C + c], sc = sv[2 * C + c];
+    const double sg = red[t & 7];
+    const double sgx = inv * (red[((1 + br) * KL) * 8 + (t & 7)] - mean * sg);  // sum g * xhat
     const double B = -sc * inv * sgx / (double)M;
     float* cf = coef + (size_t)br * 3 * C;
     cf[c] = (float)sc;
@@ -301,7 +323,7 @@ static int bn_grid(long long nchunk) {
 
 // rows per block and block count of the reductions: a function of M only
 static void bn_blocks(long long M, int* nblk, int* rpb) {
-  long long n = (M + 127) / 128;
+  long long n = (M + 63) / 64;
   if (n > BN_MAX_BLOCKS) n = BN_MAX_BLOCKS;
   if (n < 1) n = 1;
   *rpb = (int)((M + n - 1) / n);
@@ -348,7 +370,7 @@ extern "C" int rtdetr_bn_act_fwd(const void* const* x, const float* const* gamma
     ProfScope prof(stream, PROF_CONV_EPI, 2.0 * nb * M * C);
     MOE_LAUNCH(prof, bn_stats_kernel, dim3(nblk, nb), dim3(256), 2 * 2048 * sizeof(float), stream, a, M, C, rpb, ws);
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8, nb), dim3(256), 0, stream, a, ws, nblk, M, C, eps, momentum,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8, nb), dim3(BN_FIN_T), 0, stream, a, ws, nblk, M, C, eps, momentum,
                    saved);
   {
     ProfScope prof(stream, PROF_CONV_EPI, 2.0 * (nb + 1) * M * C);
@@ -393,7 +415,12 @@ extern "C" int rtdetr_bn_act_bwd(const void* dy, const void* const* x, const flo
     }
 #undef BN_RED
   }
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(256), 0, stream, a, ws, nblk, M, C, saved, coef, dgb);
+  if (nb == 2)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<2>, dim3(C / 8), dim3(BN_FIN_T), 0, stream, ws, nblk, M, C, saved, coef,
+                       dgb);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3(C / 8), dim3(BN_FIN_T), 0, stream, ws, nblk, M, C, saved, coef,
+                       dgb);
   {
     ProfScope prof(stream, PROF_CONV_EPI, 2.0 * (2 * nb + 1) * M * C);
     uint4* d0 = static_cast<uint4*>(dx[0]);

@@ -116,8 +116,16 @@ class HybridEncoder(nn.Module):
             self._pos_cache[key] = sincos_pos_embed_2d(w, h, self.hidden, device=device, dtype=dtype)
         return self._pos_cache[key]
 
+    @staticmethod
+    def _proj(p, f):
+        conv, bn = p[0], p[1]
+        if _FUSED_BN:
+            y = conv(f)
+            return bn_act([y], [bn], None) if bn_act_ok([y], [bn]) else bn(y)
+        return p(f)
+
     def forward(self, feats, ctx):
-        proj = [p(f) for p, f in zip(self.input_proj, feats)]
+        proj = [self._proj(p, f) for p, f in zip(self.input_proj, feats)]
         for i, enc_ind in enumerate(self.use_encoder_idx):
             B, C, h, w = proj[enc_ind].shape
             src = proj[enc_ind].flatten(2).permute(0, 2, 1).contiguous()   # [B, h*w, C]

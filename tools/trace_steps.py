@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--marker", default="adamw_step_kernel", help="kernel launched once per step (torch fused AdamW: FusedAdamMathFunctor)")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--full", default=None, help="regex over categories: list those kernels by full name + grid")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -60,6 +61,19 @@ def main():
           f"{len(win) / a.steps:.0f} launches/step")
     for c, v in sorted(busy.items(), key=lambda x: -x[1])[: a.top]:
         print(f"{v:7.3f} ms {100 * v / tot:5.1f}%  {cnt[c] / a.steps:6.1f}/step  {c}")
+    if a.full:
+        gcol = next((k for k in ("Grid_Size", "Grid_Size_X", "Grid_X") if k in win[0]), None)
+        fb, fc = defaultdict(float), defaultdict(int)
+        for r in win:
+            if not re.search(a.full, category(r["Kernel_Name"])):
+                continue
+            key = (r["Kernel_Name"][:140], r.get(gcol, "?") if gcol else "?")
+            fb[key] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 / a.steps
+            fc[key] += 1
+        print(f"# kernels of categories /{a.full}/ by full name and grid ({gcol})")
+        for (n, gsz), v in sorted(fb.items(), key=lambda x: -x[1])[:80]:
+            k = fc[(n, gsz)] / a.steps
+            print(f"{v:7.3f} ms {k:6.1f}/step {1e3 * v / max(k, 1e-9):8.1f} us  grid {gsz:>9}  {n}")
 
 
 if __name__ == "__main__":
