@@ -3,7 +3,7 @@
 //  router_topk_fwd : logits = x.Wg^T + ctx_bias[ctx(t)], fp32 softmax, top-k
 //                    (ties -> lower expert id), gates, per-64-token-block
 //                    routing counts + within-block ranks (wave ballot), aux
-//                    partials.  One 256-thread block = 4 waves = 64 tokens;
+//                    partials.  One block = 64 tokens (16 waves; 4 for E > 32);
 //                    16 lanes per token, each lane owning d/16 channels read as
 //                    16-B chunks (a token row is read by 16 lanes, 4 tokens per
 //                    wave-instruction).
@@ -21,8 +21,8 @@ namespace moe {
 // ---------------------------------------------------------------------------
 // router forward
 // ---------------------------------------------------------------------------
-template <int EMAX>
-__global__ __launch_bounds__(256) void router_topk_fwd_kernel(
+template <int EMAX, int NW>
+__global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
     const uint16_t* __restrict__ x, const float* __restrict__ wg,
     const float* __restrict__ ctx_bias, const int32_t* __restrict__ ctx_img,
     int tpi, int T, int d, int E, int k, int normalize,
@@ -33,7 +33,8 @@ __global__ __launch_bounds__(256) void router_topk_fwd_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_wg = reinterpret_cast<float*>(smem);               // [E][d]
   int32_t* s_idx = reinterpret_cast<int32_t*>(s_wg + E * d);  // [64][k]
-  float* s_aux = reinterpret_cast<float*>(s_idx + 64 * 8);    // [4][EMAX+1]
+  float* s_aux = reinterpret_cast<float*>(s_idx + 64 * 8);    // [NW][EMAX+1]
+  float* s_cb = s_aux + NW * (EMAX + 1);                       // [64][E] context bias rows
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -42,23 +43,54 @@ __global__ __launch_bounds__(256) void router_topk_fwd_kernel(
   const int grp = lane >> 4;   // token group within the wave (0..3)
   const int blk = blockIdx.x;
 
+  // One token per 16-lane group, 4 per wave per iteration; NW waves cover the
+  // block's 64 tokens in 16/NW iterations.  The per-token softmax / top-k is
+  // serial VALU work, so it is spread over 16 waves (one iteration) where the
+  // registers allow (EMAX <= 32).  The x loads (up to PF chunks of the row per
+  // lane; d=256 is fully covered) are issued first, overlapped with the Wg
+  // staging.
+  constexpr int NT = NW * 64;
+  constexpr int ITERS = 16 / NW;
+  constexpr int PF = 2;
+  const int nchunk = d >> 7;  // 16-B chunks per lane (d / 8 / 16)
+  uint4 xpre[ITERS][PF];
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
+    const int t = blk * 64 + it * NW * 4 + wave * 4 + grp;
+    const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)t * d);
+#pragma unroll
+    for (int c = 0; c < PF; ++c)
+      xpre[it][c] = (t < T && c < nchunk) ? xr[sub + 16 * c] : make_uint4(0u, 0u, 0u, 0u);
+  }
+
   // Stage Wg (fp32 [E][d]) in LDS, 16 B per thread-iteration.
   {
     const int n4 = (E * d) >> 2;
     const float4* src = reinterpret_cast<const float4*>(wg);
     float4* dst = reinterpret_cast<float4*>(s_wg);
-    for (int i = tid; i < n4; i += 256) dst[i] = src[i];
+    for (int i = tid; i < n4; i += NT) dst[i] = src[i];
   }
-  for (int i = tid; i < 64 * 8; i += 256) s_idx[i] = -1;
+  for (int i = tid; i < 64 * 8; i += NT) s_idx[i] = -1;
+  // Context-bias row of each of the block's 64 tokens, gathered here so the
+  // token loop below issues no global loads: on gfx9 vmcnt also counts the
+  // loop's stores, so a load inside the loop would wait for them.
+  const bool has_ctx = ctx_bias != nullptr && ctx_img != nullptr;
+  if (has_ctx) {
+    for (int i = tid; i < 64 * E; i += NT) {
+      const int tl = i / E, e = i - tl * E;
+      const int t = blk * 64 + tl;
+      s_cb[i] = (t < T) ? ctx_bias[(size_t)ctx_img[t / tpi] * E + e] : 0.f;
+    }
+  }
   __syncthreads();
 
-  const int nchunk = d >> 7;  // 16-B chunks per lane (d / 8 / 16)
   float psum[EMAX + 1];
 #pragma unroll
   for (int e = 0; e <= EMAX; ++e) psum[e] = 0.f;
 
-  for (int it = 0; it < 4; ++it) {
-    const int tl = wave * 16 + it * 4 + grp;  // token within block
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
+    const int tl = it * NW * 4 + wave * 4 + grp;  // token within block
     const int t = blk * 64 + tl;
     const bool valid = t < T;
     float logit[EMAX];
@@ -69,7 +101,11 @@ __global__ __launch_bounds__(256) void router_topk_fwd_kernel(
       for (int c = 0; c < nchunk; ++c) {
         const int ch = sub + 16 * c;  // chunk index within the row
         float xv[8];
-        unpack8(xr[ch], xv);
+        uint4 raw;
+        if (c == 0) raw = xpre[it][0];
+        else if (c == 1) raw = xpre[it][1];
+        else raw = xr[ch];
+        unpack8(raw, xv);
 #pragma unroll
         for (int e = 0; e < EMAX; ++e) {
           if (e < E) {
@@ -85,9 +121,8 @@ __global__ __launch_bounds__(256) void router_topk_fwd_kernel(
     for (int e = 0; e < EMAX; ++e) logit[e] = group_sum<16>(logit[e]);
     if (!valid) continue;  // uniform per 16-lane group; no more shuffles below
 
-    if (ctx_bias != nullptr && ctx_img != nullptr) {
-      const int c = ctx_img[t / tpi];
-      const float* cb = ctx_bias + (size_t)c * E;
+    if (has_ctx) {
+      const float* cb = s_cb + tl * E;
 #pragma unroll
       for (int e = 0; e < EMAX; ++e)
         if (e < E) logit[e] += cb[e];
@@ -156,7 +191,7 @@ __global__ __launch_bounds__(256) void router_topk_fwd_kernel(
   }
 
   // Aux partials: every lane of a group holds its tokens' sums; combine the
-  // four groups of the wave, then the four waves, in a fixed order.
+  // four groups of the wave, then the NW waves, in a fixed order.
 #pragma unroll
   for (int e = 0; e <= EMAX; ++e) {
     float v = psum[e];
@@ -171,8 +206,9 @@ __global__ __launch_bounds__(256) void router_topk_fwd_kernel(
   __syncthreads();
   if (tid <= E) {
     const int src = (tid == E) ? EMAX : tid;
-    float v = s_aux[src] + s_aux[(EMAX + 1) + src] + s_aux[2 * (EMAX + 1) + src] +
-              s_aux[3 * (EMAX + 1) + src];
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += s_aux[w * (EMAX + 1) + src];
     aux_partials[(size_t)blk * (E + 1) + tid] = v;
   }
 
@@ -334,6 +370,8 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
       p[e] = (e < E) ? probs[(size_t)t * E + e] : 0.f;
       dp[e] = (e < E && dprob_bias != nullptr) ? dprob_bias[e] : 0.f;
     }
+    int pj[8];
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) pj[j] = pos[(size_t)t * k + j];
     int sel[8];
     float selw[8], seldw[8];
     float S = 0.f, wdw = 0.f;
@@ -362,16 +400,9 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
     float dl[EMAX];
 #pragma unroll
     for (int e = 0; e < EMAX; ++e) dl[e] = p[e] * (dp[e] - dot) + zt * p[e];
-    for (int e = sub; e < E; e += 16) {
-      float v = 0.f;
-#pragma unroll
-      for (int q = 0; q < EMAX; ++q)
-        if (q == e) v = dl[q];
-      dlogits[(size_t)t * E + e] = v;
-    }
     // ---- dx = sum_j dXp[pos] + dlogits . Wg ----
-    int pj[8];
-    _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) pj[j] = pos[(size_t)t * k + j];
+    // (dlogits is stored after dx: on gfx9 vmcnt also counts stores, so a
+    // store issued before the dXp gathers would delay their wait)
     for (int c = 0; c < nchunk; ++c) {
       const int ch = sub + 16 * c;
       float acc[8];
@@ -397,6 +428,13 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
       }
       reinterpret_cast<uint4*>(dx + (size_t)t * d)[ch] = pack8(acc);
     }
+    for (int e = sub; e < E; e += 16) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < EMAX; ++q)
+        if (q == e) v = dl[q];
+      dlogits[(size_t)t * E + e] = v;
+    }
   }
 }
 
@@ -416,7 +454,7 @@ static void allow_lds(size_t bytes) {
   static bool done = false;
   if (!done)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(FN), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              64 * 1024 + 8192);
+                              96 * 1024);
   done = true;
   (void)bytes;
 }
@@ -436,21 +474,22 @@ extern "C" int moe_router_topk_fwd(const void* x, const float* wg, const float* 
   if (T == 0) return 0;
   const int nblk = moe_router_num_blocks(T);
   const int em = emax_for(E);
-  const size_t shmem = (size_t)E * d * 4 + 64 * 8 * 4 + 4 * (em + 1) * 4;
+  const int nw = em <= 32 ? 16 : 4;
+  const size_t shmem = (size_t)E * d * 4 + 64 * 8 * 4 + nw * (em + 1) * 4 + 64 * (size_t)E * 4;
   const uint16_t* xb = static_cast<const uint16_t*>(x);
   // bytes: x, Wg once, per-token outputs (idx, w, probs, lse, local rank), per-block partials
   ProfScope prof(stream, PROF_ROUTER,
                  2.0 * T * d + 4.0 * E * d + 12.0 * T * k + 4.0 * T * (E + 1) + 4.0 * nblk * (k * E + E + 1));
-#define LAUNCH_R(EM)                                                                       \
-  allow_lds<router_topk_fwd_kernel<EM>>(shmem);                                             \
-  MOE_LAUNCH(prof, router_topk_fwd_kernel<EM>, dim3(nblk), dim3(256), shmem, stream, xb, \
+#define LAUNCH_R(EM, NW)                                                                       \
+  allow_lds<router_topk_fwd_kernel<EM, NW>>(shmem);                                             \
+  MOE_LAUNCH(prof, (router_topk_fwd_kernel<EM, NW>), dim3(nblk), dim3(NW * 64), shmem, stream, xb, \
                      wg, ctx_bias, ctx_img, tokens_per_image, T, d, E, k, normalize,       \
                      topk_idx, topk_w, probs, lse, local_rank, block_counts, aux_partials)
   switch (em) {
-    case 8: LAUNCH_R(8); break;
-    case 16: LAUNCH_R(16); break;
-    case 32: LAUNCH_R(32); break;
-    default: LAUNCH_R(64); break;
+    case 8: LAUNCH_R(8, 16); break;
+    case 16: LAUNCH_R(16, 16); break;
+    case 32: LAUNCH_R(32, 16); break;
+    default: LAUNCH_R(64, 4); break;
   }
 #undef LAUNCH_R
   return check_launch("moe_router_topk_fwd");
