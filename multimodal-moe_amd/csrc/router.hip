@@ -7,9 +7,10 @@
 //                    16 lanes per token, each lane owning d/16 channels read as
 //                    16-B chunks (a token row is read by 16 lanes, 4 tokens per
 //                    wave-instruction).
-//  route_scan      : one workgroup; per (slot, expert) column a wave-parallel
-//                    exclusive scan over router blocks, then hist / kept
-//                    offsets (capacity) / slot-major rank bases.
+//  route_scan      : one workgroup; each (slot, expert) column split into
+//                    1024/(k*E) block segments (coalesced row reads), segment
+//                    sums -> exclusive prefixes, then hist / kept offsets
+//                    (capacity) / slot-major rank bases.
 //  token_bwd       : per token: gather-sum of dXp rows (dispatch transpose,
 //                    no atomics), gate + softmax + z-loss backward, and the
 //                    router's dx term dlogits.Wg, fused.
@@ -235,20 +236,45 @@ __global__ __launch_bounds__(1024) void route_scan_kernel(
     const int32_t* __restrict__ counts, int nblk, int k, int E, int cap,
     int32_t* __restrict__ rank_base, int32_t* __restrict__ hist,
     int32_t* __restrict__ offsets) {
+  // Thread = (segment, column): consecutive threads read consecutive columns
+  // of a counts row (coalesced), and the router blocks are split into nseg
+  // contiguous segments so every column is scanned by 1024/ncol threads.
+  __shared__ int32_t s_seg[1024];  // per (segment, column) sums -> exclusive prefixes
   __shared__ int32_t s_tot[8 * 64];
   __shared__ int32_t s_slot[8 * 64];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int nwave = blockDim.x >> 6;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
   const int ncol = k * E;
+  const int nseg = 1024 / ncol;  // ncol <= 512 -> nseg >= 2
+  const int bs = (nblk + nseg - 1) / nseg;
+  const int col = tid % ncol;
+  const int seg = tid / ncol;
+  const bool active = seg < nseg;
+  const int b_lo = active ? min(seg * bs, nblk) : nblk;
+  const int b_hi = active ? min(b_lo + bs, nblk) : nblk;
+  constexpr int CH = 8;  // loads issued together before their use
 
-  // Phase 0: column totals.
-  for (int col = wave; col < ncol; col += nwave) {
-    int s = 0;
-    for (int b = lane; b < nblk; b += 64) s += counts[(size_t)b * ncol + col];
+  // Phase 0: per-segment column sums.
+  int s = 0;
+  for (int b0 = b_lo; b0 < b_hi; b0 += CH) {
+    int v[CH];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (lane == 0) s_tot[col] = s;
+    for (int i = 0; i < CH; ++i) v[i] = (b0 + i < b_hi) ? counts[(size_t)(b0 + i) * ncol + col] : 0;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) s += v[i];
+  }
+  if (active) s_seg[seg * ncol + col] = s;
+  __syncthreads();
+  // Column totals and per-segment exclusive prefixes (fixed order).
+  if (tid < ncol) {
+    int acc = 0;
+    for (int g = 0; g < nseg; ++g) {
+      const int t = s_seg[g * ncol + tid];
+      s_seg[g * ncol + tid] = acc;
+      acc += t;
+    }
+    s_tot[tid] = acc;
   }
   __syncthreads();
   // hist / kept offsets / slot bases (one wave, E <= 64 lanes).
@@ -274,20 +300,17 @@ __global__ __launch_bounds__(1024) void route_scan_kernel(
     if (lane == E - 1) offsets[E] = inc;
   }
   __syncthreads();
-  // Phase 1: exclusive scan over blocks per column, plus the slot base.
-  for (int col = wave; col < ncol; col += nwave) {
-    int carry = s_slot[col];
-    for (int b0 = 0; b0 < nblk; b0 += 64) {
-      const int b = b0 + lane;
-      const int v = (b < nblk) ? counts[(size_t)b * ncol + col] : 0;
-      int inc = v;
+  // Phase 1: running exclusive sum over the segment's blocks, plus the slot base.
+  if (!active) return;
+  int carry = s_slot[col] + s_seg[seg * ncol + col];
+  for (int b0 = b_lo; b0 < b_hi; b0 += CH) {
+    int v[CH];
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += u;
-      }
-      if (b < nblk) rank_base[(size_t)b * ncol + col] = carry + inc - v;
-      carry += __shfl(inc, 63, 64);
+    for (int i = 0; i < CH; ++i) v[i] = (b0 + i < b_hi) ? counts[(size_t)(b0 + i) * ncol + col] : 0;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      if (b0 + i < b_hi) rank_base[(size_t)(b0 + i) * ncol + col] = carry;
+      carry += v[i];
     }
   }
 }
