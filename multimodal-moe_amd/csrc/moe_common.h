@@ -114,6 +114,37 @@ __device__ __forceinline__ float group_max(float v) {
   return v;
 }
 
+// Cross-lane moves inside a 16-lane DPP row (no LDS round trip, unlike
+// __shfl_xor's ds_bpermute).  row_xor<H> reads the lane whose index differs in
+// bit H and in every lower bit (xor 2H-1: quad_perm for H <= 2, row_half_mirror
+// for H = 4, row_mirror for H = 8).  The four masks 15, 7, 3, 1 are a basis of
+// the row's lane-index space, so a butterfly over H = 8, 4, 2, 1 all-reduces
+// the row, and stage H pairs every lane with one of the opposite bit H.
+template <int H>
+__device__ __forceinline__ int row_xor_i(int v) {
+  constexpr int ctrl = H == 1 ? 0xB1 : H == 2 ? 0x1B : H == 4 ? 0x141 : 0x140;
+  static_assert(H == 1 || H == 2 || H == 4 || H == 8, "row_xor: H in {1,2,4,8}");
+  return __builtin_amdgcn_update_dpp(0, v, ctrl, 0xF, 0xF, false);
+}
+template <int H>
+__device__ __forceinline__ float row_xor(float v) {
+  return __int_as_float(row_xor_i<H>(__float_as_int(v)));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += row_xor<8>(v);
+  v += row_xor<4>(v);
+  v += row_xor<2>(v);
+  v += row_xor<1>(v);
+  return v;
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, row_xor<8>(v));
+  v = fmaxf(v, row_xor<4>(v));
+  v = fmaxf(v, row_xor<2>(v));
+  v = fmaxf(v, row_xor<1>(v));
+  return v;
+}
+
 // MX-quantize one 16-B chunk (8 bf16) held by each lane, where 4 consecutive
 // lanes hold one 32-element block: the block amax by a 4-lane butterfly, then
 // e4m3 bytes and the block exponent.

@@ -22,6 +22,28 @@ namespace moe {
 // ---------------------------------------------------------------------------
 // router forward
 // ---------------------------------------------------------------------------
+// Reduce-scatter stage H of the router's 16-lane expert ownership: position
+// e0 (bit H and all higher in-row bits clear) ends holding the pair sum for
+// expert e0 | (sub & H).
+template <int H, int EP>
+__device__ __forceinline__ void rs_stage(float (&v)[EP], int sub) {
+  const bool hi = (sub & H) != 0;
+#pragma unroll
+  for (int e0 = 0; e0 < EP; ++e0) {
+    if ((e0 & (16 - 2 * H)) != 0 || (e0 & H) != 0) continue;
+    const float keep = hi ? v[e0 | H] : v[e0];
+    const float send = hi ? v[e0] : v[e0 | H];
+    v[e0] = keep + row_xor<H>(send);
+  }
+}
+// Arg-max stage H: larger logit wins, ties -> lower expert id.
+template <int H>
+__device__ __forceinline__ void argmax_stage(float& bv, int& best) {
+  const float ov = row_xor<H>(bv);
+  const int oi = row_xor_i<H>(best);
+  if (ov > bv || (ov == bv && oi < best)) { bv = ov; best = oi; }
+}
+
 template <int EMAX, int NW>
 __global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
     const uint16_t* __restrict__ x, const float* __restrict__ wg,
@@ -85,18 +107,26 @@ __global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
   }
   __syncthreads();
 
-  float psum[EMAX + 1];
+  // Expert ownership inside a 16-lane token group: lane `sub` owns experts
+  // e = 16 q + sub (q < Q).  The partial dot products are reduce-scattered to
+  // their owners (15/16 EP DPP row moves instead of 4 EMAX), and softmax /
+  // top-k run on Q values per lane with DPP row butterflies for the max, the
+  // sum and the arg-max of each top-k round.
+  constexpr int EP = EMAX < 16 ? 16 : EMAX;
+  constexpr int Q = EP / 16;
+  float psum[Q];
 #pragma unroll
-  for (int e = 0; e <= EMAX; ++e) psum[e] = 0.f;
+  for (int q = 0; q < Q; ++q) psum[q] = 0.f;
+  float pz = 0.f;
 
 #pragma unroll
   for (int it = 0; it < ITERS; ++it) {
     const int tl = it * NW * 4 + wave * 4 + grp;  // token within block
     const int t = blk * 64 + tl;
     const bool valid = t < T;
-    float logit[EMAX];
+    float v[EP];
 #pragma unroll
-    for (int e = 0; e < EMAX; ++e) logit[e] = 0.f;
+    for (int e = 0; e < EP; ++e) v[e] = 0.f;
     if (valid) {
       const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)t * d);
       for (int c = 0; c < nchunk; ++c) {
@@ -112,61 +142,68 @@ __global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
           if (e < E) {
             const float4* w4 = reinterpret_cast<const float4*>(s_wg + e * d + ch * 8);
             const float4 w0 = w4[0], w1 = w4[1];
-            logit[e] += xv[0] * w0.x + xv[1] * w0.y + xv[2] * w0.z + xv[3] * w0.w +
-                        xv[4] * w1.x + xv[5] * w1.y + xv[6] * w1.z + xv[7] * w1.w;
+            v[e] += xv[0] * w0.x + xv[1] * w0.y + xv[2] * w0.z + xv[3] * w0.w +
+                    xv[4] * w1.x + xv[5] * w1.y + xv[6] * w1.z + xv[7] * w1.w;
           }
         }
       }
     }
-#pragma unroll
-    for (int e = 0; e < EMAX; ++e) logit[e] = group_sum<16>(logit[e]);
-    if (!valid) continue;  // uniform per 16-lane group; no more shuffles below
+    // reduce-scatter: after the stage with mask m, position e0 (bit m clear)
+    // holds the pair sum for expert e0 | (sub & m)
+    rs_stage<8>(v, sub);
+    rs_stage<4>(v, sub);
+    rs_stage<2>(v, sub);
+    rs_stage<1>(v, sub);
+    if (!valid) continue;  // uniform per 16-lane group; group shuffles only below
 
-    if (has_ctx) {
-      const float* cb = s_cb + tl * E;
+    float logit[Q];
+    bool own[Q];
 #pragma unroll
-      for (int e = 0; e < EMAX; ++e)
-        if (e < E) logit[e] += cb[e];
+    for (int q = 0; q < Q; ++q) {
+      const int e = 16 * q + sub;
+      own[q] = e < E;
+      logit[q] = v[16 * q] + ((own[q] && has_ctx) ? s_cb[tl * E + e] : 0.f);
     }
     float m = -INFINITY;
 #pragma unroll
-    for (int e = 0; e < EMAX; ++e)
-      if (e < E) m = fmaxf(m, logit[e]);
-    float s = 0.f;
-    float p[EMAX];
+    for (int q = 0; q < Q; ++q)
+      if (own[q]) m = fmaxf(m, logit[q]);
+    m = row16_max(m);
+    float p[Q];
+    float sl = 0.f;
 #pragma unroll
-    for (int e = 0; e < EMAX; ++e) {
-      p[e] = (e < E) ? expf(logit[e] - m) : 0.f;
-      s += p[e];
+    for (int q = 0; q < Q; ++q) {
+      p[q] = own[q] ? expf(logit[q] - m) : 0.f;
+      sl += p[q];
     }
-    const float inv = 1.f / s;
+    const float ssm = row16_sum(sl);
+    const float inv = 1.f / ssm;
 #pragma unroll
-    for (int e = 0; e < EMAX; ++e) p[e] *= inv;
-    const float lse = m + logf(s);
+    for (int q = 0; q < Q; ++q) p[q] *= inv;
+    const float lse = m + logf(ssm);
 
-    // top-k on logits (monotone in probs); strict '>' keeps the lower index on ties
-    uint64_t taken = 0;
+    // top-k on logits (monotone in probs); ties -> lower expert id
+    uint32_t taken = 0;  // bit q: owned expert 16q+sub already selected
     int sel[8];
     float selp[8];
     float ssum = 0.f;
     _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
-      int best = -1;
+      int best = 0x7fffffff;
       float bv = -INFINITY;
 #pragma unroll
-      for (int e = 0; e < EMAX; ++e) {
-        if (e < E && !((taken >> e) & 1ull) && (best < 0 || logit[e] > bv)) {
-          bv = logit[e];
-          best = e;
+      for (int q = 0; q < Q; ++q)
+        if (own[q] && !((taken >> q) & 1u) && (best == 0x7fffffff || logit[q] > bv)) {
+          bv = logit[q];
+          best = 16 * q + sub;
         }
-      }
-      taken |= 1ull << best;
+      argmax_stage<8>(bv, best);
+      argmax_stage<4>(bv, best);
+      argmax_stage<2>(bv, best);
+      argmax_stage<1>(bv, best);
+      if ((best & 15) == sub) taken |= 1u << (best >> 4);
       sel[j] = best;
-      float pb = 0.f;
-#pragma unroll
-      for (int e = 0; e < EMAX; ++e)
-        if (e == best) pb = p[e];
-      selp[j] = pb;
-      ssum += pb;
+      selp[j] = expf(bv - m) * inv;  // bit-identical to the owner's p
+      ssum += selp[j];
     }
     const bool renorm = normalize && k > 1;
     if (sub < k) {
@@ -178,39 +215,39 @@ __global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
       topk_w[(size_t)t * k + sub] = renorm ? sp / ssum : sp;
       s_idx[tl * 8 + sub] = si;
     }
-    for (int e = sub; e < E; e += 16) {
-      float pv = 0.f;
 #pragma unroll
-      for (int q = 0; q < EMAX; ++q)
-        if (q == e) pv = p[q];
-      probs_out[(size_t)t * E + e] = pv;
-    }
+    for (int q = 0; q < Q; ++q)
+      if (own[q]) probs_out[(size_t)t * E + 16 * q + sub] = p[q];
     if (sub == 0) lse_out[t] = lse;
 #pragma unroll
-    for (int e = 0; e < EMAX; ++e) psum[e] += p[e];
-    psum[EMAX] += lse * lse;
+    for (int q = 0; q < Q; ++q) psum[q] += p[q];
+    pz += lse * lse;
   }
 
-  // Aux partials: every lane of a group holds its tokens' sums; combine the
-  // four groups of the wave, then the NW waves, in a fixed order.
+  // Aux partials: lane sub of each group holds its owned experts' sums;
+  // combine the four groups of the wave, then the NW waves, in a fixed order.
 #pragma unroll
-  for (int e = 0; e <= EMAX; ++e) {
-    float v = psum[e];
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    psum[e] = v;
+  for (int q = 0; q < Q; ++q) {
+    float u = psum[q];
+    u += __shfl_xor(u, 16, 64);
+    u += __shfl_xor(u, 32, 64);
+    psum[q] = u;
   }
-  if (lane == 0) {
+  pz += __shfl_xor(pz, 16, 64);
+  pz += __shfl_xor(pz, 32, 64);
+  if (lane < 16) {
 #pragma unroll
-    for (int e = 0; e <= EMAX; ++e) s_aux[wave * (EMAX + 1) + e] = psum[e];
+    for (int q = 0; q < Q; ++q)
+      if (16 * q + lane < E) s_aux[wave * (EMAX + 1) + 16 * q + lane] = psum[q];
+    if (lane == 0) s_aux[wave * (EMAX + 1) + EMAX] = pz;
   }
   __syncthreads();
   if (tid <= E) {
     const int src = (tid == E) ? EMAX : tid;
-    float v = 0.f;
+    float u = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) v += s_aux[w * (EMAX + 1) + src];
-    aux_partials[(size_t)blk * (E + 1) + tid] = v;
+    for (int w = 0; w < NW; ++w) u += s_aux[w * (EMAX + 1) + src];
+    aux_partials[(size_t)blk * (E + 1) + tid] = u;
   }
 
   // Within-block stable ranks: wave 0, lane l = token l of the block.

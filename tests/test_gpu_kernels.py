@@ -185,6 +185,8 @@ CASES = [
     (777, 256, 16, 1024, 2, 111, 0.0, 4),
     (640, 256, 32, 1024, 4, 64, 1.25, 5),
     (333, 128, 8, 256, 3, 333, 0.5, 6),
+    (500, 384, 5, 256, 2, 100, 0.0, 7),  # d/128 = 3 row chunks, E not a power of two
+    (300, 256, 64, 256, 8, 300, 0.0, 8),  # E = 64: 4-wave router blocks, 4 experts per lane
 ]
 
 
