@@ -244,6 +244,18 @@ int rtdetr_add_bias_relu_nhwc(const void* a, const void* b, const float* bias, l
  * int32 pairs {record, chunk of 2048 elements}.  out = RNE(float(w) * scale). */
 int rtdetr_fold_scale_multi(const void* records, const int32_t* chunks, int n_chunks, hipStream_t stream);
 
+/* Bias gradient of a linear layer: out[n] = sum_m dy[m, n] over bf16 dy [M, N]
+ * (row-major), fp32 accumulation in a fixed order (deterministic, no atomics),
+ * out fp32 (out_bf16 = 0) or bf16.  Two launches: P row-block partials into
+ * `partials` (fp32 [P, N], caller-owned), then the column totals.
+ * rtdetr_bias_grad_parts(M, N) returns the P the caller should allocate for.
+ * N a multiple of 8 (<= 2048, 16-B aligned dy) or N <= 256.
+ * Replaces AddmmBackward's torch column sum (reference engine: Ultralytics
+ * RT-DETR linear layers, rtdetr.py:82-94). */
+int rtdetr_bias_grad_parts(long long M, int N);
+int rtdetr_bias_grad(const void* dy, long long M, int N, float* partials, int P, void* out, int out_bf16,
+                     hipStream_t stream);
+
 /* Decoder box refinement (one launch each way), over n = B*Q*4 elements:
  *   y = sigmoid(delta + log(max(x', eps) / max(1 - x', eps))), x' = clamp(ref, 0, 1)
  * delta bf16 (delta_bf16 = 1) or fp32; ref, y fp32.  Backward:

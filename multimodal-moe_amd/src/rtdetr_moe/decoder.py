@@ -76,7 +76,7 @@ class MLP(nn.Module):
     def __init__(self, din, dh, dout, n):
         super().__init__()
         dims = [din] + [dh] * (n - 1)
-        self.layers = nn.ModuleList(nn.Linear(a, b) for a, b in zip(dims, dims[1:] + [dout]))
+        self.layers = nn.ModuleList(TokenLinear(a, b) for a, b in zip(dims, dims[1:] + [dout]))
 
     def forward(self, x):
         for i, layer in enumerate(self.layers):
@@ -190,10 +190,10 @@ class MSDeformableAttention(nn.Module):
         super().__init__()
         self.d, self.nhead, self.nlevels, self.npoints = d, nhead, nlevels, npoints
         self.offset_scale = offset_scale
-        self.sampling_offsets = nn.Linear(d, nhead * nlevels * npoints * 2)
-        self.attention_weights = nn.Linear(d, nhead * nlevels * npoints)
+        self.sampling_offsets = TokenLinear(d, nhead * nlevels * npoints * 2)
+        self.attention_weights = TokenLinear(d, nhead * nlevels * npoints)
         self.value_proj = TokenLinear(d, d)  # runs over all B*S memory tokens
-        self.output_proj = nn.Linear(d, d)
+        self.output_proj = TokenLinear(d, d)
         self._reset()
 
     def _reset(self):
@@ -264,10 +264,10 @@ class RTDETRDecoder(nn.Module):
             TransformerDecoderLayer(hidden, nhead, dim_feedforward, self.nlevels, npoints, moe)
             for _ in range(num_layers)])
         self.query_pos_head = MLP(4, 2 * hidden, hidden, 2)
-        self.enc_output = nn.Sequential(nn.Linear(hidden, hidden), nn.LayerNorm(hidden))
-        self.enc_score_head = nn.Linear(hidden, num_classes)
+        self.enc_output = nn.Sequential(TokenLinear(hidden, hidden), nn.LayerNorm(hidden))
+        self.enc_score_head = TokenLinear(hidden, num_classes)
         self.enc_bbox_head = MLP(hidden, hidden, 4, 3)
-        self.dec_score_head = nn.ModuleList([nn.Linear(hidden, num_classes) for _ in range(num_layers)])
+        self.dec_score_head = nn.ModuleList([TokenLinear(hidden, num_classes) for _ in range(num_layers)])
         self.dec_bbox_head = nn.ModuleList([MLP(hidden, hidden, 4, 3) for _ in range(num_layers)])
         self._anchor_cache = {}
         self._reset()

@@ -12,13 +12,14 @@ from ..moe.config import MoEConfig
 from ..moe.layer import MoEFFN
 from .backbone import _FUSED_BN, ConvNormLayer
 from .fused import bn_act, bn_act_ok
+from .linear import TokenLinear
 
 
 class DenseFFN(nn.Module):
     def __init__(self, d, hidden, act="relu"):
         super().__init__()
-        self.linear1 = nn.Linear(d, hidden)
-        self.linear2 = nn.Linear(hidden, d)
+        self.linear1 = TokenLinear(d, hidden)
+        self.linear2 = TokenLinear(hidden, d)
         self.act = nn.GELU() if act == "gelu" else nn.ReLU()
 
     def forward(self, x, ctx=None):

@@ -7,7 +7,9 @@ The weight gradient dW = dY^T X reduces over all rows.  As one GEMM with a
 chip (~380 us on MI355X); split into S row chunks as a batched GEMM
 (S independent [256, K/S] x [K/S, 256] products, then a fp32 sum over S) it
 fills the chip (~50 us, tools/mm_probe.py).  Forward and input gradient are
-the usual GEMMs.
+the usual GEMMs.  Every linear layer of the RT-DETR body is a TokenLinear on
+the GPU: its bias gradient comes from rtdetr_bias_grad (deterministic
+two-launch column sum) instead of torch's reduce kernel.
 """
 from __future__ import annotations
 
@@ -31,6 +33,27 @@ def chunked_wgrad(gy: torch.Tensor, x: torch.Tensor, target_chunk: int = 2560) -
     return out
 
 
+def bias_grad(g2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """Column sum of the bf16 output gradient [M, N] in the bias dtype: the HIP
+    kernel pair rtdetr_bias_grad (fixed-order fp32 accumulation, two launches)
+    on bf16 CUDA gradients; torch's sum elsewhere (fp32 layers)."""
+    M, N = g2.shape
+    if not (g2.is_cuda and g2.dtype == torch.bfloat16 and dtype in (torch.bfloat16, torch.float32)
+            and M > 0 and (N % 8 == 0 and N <= 2048 or N <= 256)):
+        return g2.sum(0, dtype=torch.float32).to(dtype)
+    from ..moe import _lib as L
+
+    if N % 8 == 0 and g2.data_ptr() % 16 != 0:
+        g2 = g2.clone()  # 16-B row vectors
+    lib = L.lib()
+    P = int(lib.rtdetr_bias_grad_parts(M, N))
+    parts = torch.empty((P, N), dtype=torch.float32, device=g2.device)
+    out = torch.empty((N,), dtype=dtype, device=g2.device)
+    L._check(lib.rtdetr_bias_grad(g2.data_ptr(), M, N, parts.data_ptr(), P, out.data_ptr(),
+                                  int(dtype == torch.bfloat16), L._stream()), "rtdetr_bias_grad")
+    return out
+
+
 class _TokenLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, dtype):
@@ -38,6 +61,7 @@ class _TokenLinear(torch.autograd.Function):
         bc = bias.to(dtype) if bias is not None else None
         ctx.save_for_backward(xc, wc)
         ctx.has_bias = bias is not None
+        ctx.bias_dtype = bias.dtype if bias is not None else None
         return F.linear(xc, wc, bc)
 
     @staticmethod
@@ -46,17 +70,20 @@ class _TokenLinear(torch.autograd.Function):
         g2 = gy.reshape(-1, gy.shape[-1]).to(wc.dtype).contiguous()
         x2 = xc.reshape(-1, xc.shape[-1])
         gx = g2.mm(wc).view(xc.shape) if ctx.needs_input_grad[0] else None
-        gw = chunked_wgrad(g2, x2) if ctx.needs_input_grad[1] else None
-        gb = g2.sum(0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            gw = chunked_wgrad(g2, x2) if x2.shape[0] >= BIG_ROWS else g2.t().mm(x2)
+        gb = bias_grad(g2, ctx.bias_dtype) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return gx, gw, gb, None
 
 
 class TokenLinear(nn.Linear):
     """nn.Linear (same parameters and state dict) whose backward splits the
-    weight-gradient reduction over row chunks when the input has many rows."""
+    weight-gradient reduction over row chunks when the input has many rows and
+    takes the bias gradient from the HIP column-sum kernels (bias_grad)."""
 
     def forward(self, x):
-        if x.is_cuda and x.numel() // x.shape[-1] >= BIG_ROWS:
+        if x.is_cuda and x.numel() > 0:
             dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
             with torch.autocast("cuda", enabled=False):
                 return _TokenLinear.apply(x, self.weight, self.bias, dtype)

@@ -1,0 +1,76 @@
+"""GPU parity of the linear-layer bias gradient (rtdetr_bias_grad) and of
+TokenLinear against nn.Linear.
+
+Bias gradient: fp32 accumulation of bf16 gradients in a fixed order vs torch's
+fp64 column sum of the same bf16 values: |err| <= 1e-5 * sum|dy| per column
+(fp32 rounding of M terms), bf16 output within 1 bf16 ulp of the fp32 result.
+Deterministic: two runs are bit-identical.  TokenLinear: output bit-identical
+to nn.Linear (same F.linear call); input and weight gradients within 1e-2
+relative Frobenius error (the same GEMMs, possibly another operand
+orientation, bf16 outputs); bias gradient within the tolerance above plus its
+bf16 rounding.
+"""
+from __future__ import annotations
+
+import pytest
+import torch
+from torch import nn
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,N", [(1, 1), (37, 4), (300, 1), (2400, 256), (2400, 192), (2400, 96),
+                                 (7360, 1024), (154560, 256), (1000, 8), (513, 2048), (100, 200)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_bias_grad(hip_lib, M, N, out_dtype):
+    from src.rtdetr_moe.linear import bias_grad
+
+    g = torch.Generator().manual_seed(M * 31 + N)
+    dy = torch.randn(M, N, generator=g).to(torch.bfloat16).cuda()
+    ref = dy.double().sum(0)
+    tol = 1e-5 * dy.double().abs().sum(0) + 1e-30
+    got = bias_grad(dy, out_dtype)
+    assert got.dtype == out_dtype and got.shape == (N,)
+    if out_dtype == torch.float32:
+        err = (got.double() - ref).abs()
+        assert bool((err <= tol).all()), float((err - tol).max())
+        got2 = bias_grad(dy, out_dtype)
+        assert torch.equal(got, got2)  # deterministic
+    else:
+        f32 = bias_grad(dy, torch.float32)
+        assert torch.equal(got, f32.to(torch.bfloat16))
+
+
+def test_bias_grad_unaligned_view(hip_lib):
+    from src.rtdetr_moe.linear import bias_grad
+
+    base = torch.randn(257 * 256 + 3, dtype=torch.bfloat16, device="cuda")
+    dy = base[3:].view(257, 256)  # 6-B offset: not 16-B aligned
+    got = bias_grad(dy, torch.float32)
+    ref = dy.double().sum(0)
+    assert bool(((got.double() - ref).abs() <= 1e-5 * dy.double().abs().sum(0) + 1e-30).all())
+
+
+@pytest.mark.parametrize("shape,din,dout", [((8, 300, 256), 256, 256), ((2400, 256), 256, 1), ((4, 77, 256), 256, 4),
+                                            ((8, 920, 256), 256, 1024)])
+def test_token_linear_matches_linear(hip_lib, shape, din, dout):
+    from src.rtdetr_moe.linear import TokenLinear
+
+    torch.manual_seed(0)
+    ref = nn.Linear(din, dout).cuda().to(torch.bfloat16)
+    tl = TokenLinear(din, dout).cuda().to(torch.bfloat16)
+    tl.load_state_dict(ref.state_dict())
+    x = torch.randn(*shape, device="cuda", dtype=torch.bfloat16)
+    x1 = x.clone().requires_grad_(True)
+    x2 = x.clone().requires_grad_(True)
+    y1, y2 = ref(x1), tl(x2)
+    assert torch.equal(y1, y2)
+    gy = torch.randn_like(y1)
+    y1.backward(gy)
+    y2.backward(gy)
+    for a, b in ((x1.grad, x2.grad), (ref.weight.grad, tl.weight.grad)):  # same GEMMs, bf16 outputs
+        assert float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)) <= 1e-2
+    gb_ref = gy.reshape(-1, dout).double().sum(0)
+    tol = 1e-5 * gy.reshape(-1, dout).double().abs().sum(0) + 2.0 ** -8 * gb_ref.abs() + 1e-30
+    assert tl.bias.grad.dtype == torch.bfloat16
+    assert bool(((tl.bias.grad.double() - gb_ref).abs() <= tol).all())
