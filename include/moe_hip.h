@@ -244,6 +244,14 @@ int rtdetr_add_bias_relu_nhwc(const void* a, const void* b, const float* bias, l
  * int32 pairs {record, chunk of 2048 elements}.  out = RNE(float(w) * scale). */
 int rtdetr_fold_scale_multi(const void* records, const int32_t* chunks, int n_chunks, hipStream_t stream);
 
+/* ResNet-D shortcut AvgPool2d(2, 2) over channels_last bf16 [B, H, W, C]
+ * (even H, W; C % 8 == 0; 16-B aligned): y = RNE(0.25 * window sum, fp32);
+ * backward gx = RNE(0.25 * gy) broadcast to the 2x2 window (H, W = input
+ * dims in both calls).  Reference engine: Ultralytics/RT-DETR PResNet
+ * (rtdetr.py:82-94, upstream resnet-d variant). */
+int rtdetr_avgpool2x2_nhwc_fwd(const void* x, int B, int H, int W, int C, void* y, hipStream_t stream);
+int rtdetr_avgpool2x2_nhwc_bwd(const void* gy, int B, int H, int W, int C, void* gx, hipStream_t stream);
+
 /* Bias gradient of a linear layer: out[n] = sum_m dy[m, n] over bf16 dy [M, N]
  * (row-major), fp32 accumulation in a fixed order (deterministic, no atomics),
  * out fp32 (out_bf16 = 0) or bf16.  Two launches: P row-block partials into

@@ -1,0 +1,92 @@
+// ResNet-D shortcut downsampling of the RT-DETR backbone:
+// AvgPool2d(2, 2) over channels_last (NHWC) bf16 activations with even H, W.
+//   forward : y[b, i, j, c] = RNE(0.25 * sum of the 2x2 window, fp32)
+//   backward: gx[b, 2i+di, 2j+dj, c] = RNE(0.25 * gy[b, i, j, c])
+// One thread per 8-channel (16-B) vector of an output pixel.  Replaces the
+// reshape-mean forward (torch reduce kernel) and its broadcast-multiply
+// backward (~1.8 TB/s on the stage-2 shortcut, 120 M elements).
+#include "moe_common.h"
+#include "prof.h"
+
+namespace moe {
+
+__global__ __launch_bounds__(256) void avgpool2x2_fwd_kernel(const uint16_t* __restrict__ x, int H, int W, int C8,
+                                                             long long n, uint16_t* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int W2 = W >> 1, H2 = H >> 1;
+  const int cv = (int)(i % C8);
+  long long p = i / C8;
+  const int ow = (int)(p % W2);
+  p /= W2;
+  const int oh = (int)(p % H2);
+  const long long b = p / H2;
+  const uint4* xr = reinterpret_cast<const uint4*>(x);
+  const long long row0 = ((b * H + 2 * oh) * W + 2 * ow) * C8 + cv;
+  const long long row1 = row0 + (long long)W * C8;
+  const uint4 a = xr[row0], bq = xr[row0 + C8], c = xr[row1], d = xr[row1 + C8];
+  float va[8], vb[8], vc[8], vd[8], o[8];
+  unpack8(a, va);
+  unpack8(bq, vb);
+  unpack8(c, vc);
+  unpack8(d, vd);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = (((va[k] + vb[k]) + vc[k]) + vd[k]) * 0.25f;
+  reinterpret_cast<uint4*>(y)[i] = pack8(o);
+}
+
+__global__ __launch_bounds__(256) void avgpool2x2_bwd_kernel(const uint16_t* __restrict__ gy, int H, int W, int C8,
+                                                             long long n, uint16_t* __restrict__ gx) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int W2 = W >> 1, H2 = H >> 1;
+  const int cv = (int)(i % C8);
+  long long p = i / C8;
+  const int ow = (int)(p % W2);
+  p /= W2;
+  const int oh = (int)(p % H2);
+  const long long b = p / H2;
+  float v[8];
+  unpack8(reinterpret_cast<const uint4*>(gy)[i], v);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] *= 0.25f;
+  const uint4 q = pack8(v);
+  uint4* xr = reinterpret_cast<uint4*>(gx);
+  const long long row0 = ((b * H + 2 * oh) * W + 2 * ow) * C8 + cv;
+  const long long row1 = row0 + (long long)W * C8;
+  xr[row0] = q;
+  xr[row0 + C8] = q;
+  xr[row1] = q;
+  xr[row1 + C8] = q;
+}
+
+}  // namespace moe
+
+using namespace moe;
+
+static int pool_args_ok(const void* a, const void* b, int B, int H, int W, int C) {
+  if (a == nullptr || b == nullptr || B < 0 || H <= 0 || W <= 0 || C <= 0) return 0;
+  if ((H & 1) || (W & 1) || (C & 7)) return 0;
+  if ((reinterpret_cast<uintptr_t>(a) & 15) || (reinterpret_cast<uintptr_t>(b) & 15)) return 0;
+  return 1;
+}
+
+extern "C" int rtdetr_avgpool2x2_nhwc_fwd(const void* x, int B, int H, int W, int C, void* y, hipStream_t stream) {
+  if (!pool_args_ok(x, y, B, H, W, C)) return fail("avgpool2x2_fwd: need even H, W, C % 8 == 0, 16-B aligned");
+  const long long n = (long long)B * (H / 2) * (W / 2) * (C / 8);
+  if (n == 0) return 0;
+  ProfScope prof(stream, PROF_CONV_EPI, 2.0 * B * H * W * C * 1.25);
+  MOE_LAUNCH(prof, avgpool2x2_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+             static_cast<const uint16_t*>(x), H, W, C / 8, n, static_cast<uint16_t*>(y));
+  return check_launch("rtdetr_avgpool2x2_nhwc_fwd");
+}
+
+extern "C" int rtdetr_avgpool2x2_nhwc_bwd(const void* gy, int B, int H, int W, int C, void* gx, hipStream_t stream) {
+  if (!pool_args_ok(gy, gx, B, H, W, C)) return fail("avgpool2x2_bwd: need even H, W, C % 8 == 0, 16-B aligned");
+  const long long n = (long long)B * (H / 2) * (W / 2) * (C / 8);
+  if (n == 0) return 0;
+  ProfScope prof(stream, PROF_CONV_EPI, 2.0 * B * H * W * C * 1.25);
+  MOE_LAUNCH(prof, avgpool2x2_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+             static_cast<const uint16_t*>(gy), H, W, C / 8, n, static_cast<uint16_t*>(gx));
+  return check_launch("rtdetr_avgpool2x2_nhwc_bwd");
+}

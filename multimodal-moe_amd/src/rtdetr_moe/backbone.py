@@ -200,14 +200,46 @@ class ConvNormLayer(nn.Module):
         return self.act(self.norm(y))
 
 
+class _AvgPool2x2(torch.autograd.Function):
+    """AvgPool2d(2, 2) on channels_last bf16 through rtdetr_avgpool2x2_nhwc_fwd
+    / _bwd (one launch each way, 16-B channel vectors)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        from ..moe import _lib as L
+
+        B, C, H, W = x.shape
+        y = torch.empty((B, C, H // 2, W // 2), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        L._check(L.lib().rtdetr_avgpool2x2_nhwc_fwd(x.data_ptr(), B, H, W, C, y.data_ptr(), L._stream()),
+                 "rtdetr_avgpool2x2_nhwc_fwd")
+        ctx.shape = (B, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from ..moe import _lib as L
+
+        B, C, H, W = ctx.shape
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        if gy.data_ptr() % 16:
+            gy = gy.clone(memory_format=torch.channels_last)
+        gx = torch.empty((B, C, H, W), dtype=gy.dtype, device=gy.device, memory_format=torch.channels_last)
+        L._check(L.lib().rtdetr_avgpool2x2_nhwc_bwd(gy.data_ptr(), B, H, W, C, gx.data_ptr(), L._stream()),
+                 "rtdetr_avgpool2x2_nhwc_bwd")
+        return gx
+
+
 def avg_pool_2x2(x):
     """AvgPool2d(2, 2, ceil_mode=True).  Even H and W (every RT-DETR input padded
     to a multiple of 32) take a reshape-mean over the channels_last layout, whose
     backward is one broadcast kernel (ROCm's NHWC avg_pool2d backward took
-    ~400 us per call at 1280x736, batch 8)."""
+    ~400 us per call at 1280x736, batch 8); bf16 GPU activations take the
+    HIP kernel pair (_AvgPool2x2), one 16-B-vector launch each way."""
     B, C, H, W = x.shape
     if H % 2 or W % 2 or not x.is_contiguous(memory_format=torch.channels_last):
         return F.avg_pool2d(x, 2, 2, 0, ceil_mode=True)
+    if x.is_cuda and x.dtype == torch.bfloat16 and C % 8 == 0 and x.data_ptr() % 16 == 0:
+        return _AvgPool2x2.apply(x)
     y = x.permute(0, 2, 3, 1).reshape(B, H // 2, 2, W // 2, 2, C).mean(dim=(2, 4))
     return y.permute(0, 3, 1, 2)
 

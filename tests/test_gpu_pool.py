@@ -1,0 +1,35 @@
+"""GPU parity of the ResNet-D shortcut pooling (rtdetr_avgpool2x2_nhwc_fwd/_bwd)
+against torch's AvgPool2d(2, 2) on the same channels_last bf16 input.
+
+Bar: forward within 1 bf16 ulp of torch (fp32 window sum x 0.25, one rounding;
+torch may sum the four terms in another order), backward bit-exact (0.25 * g is
+exact in bf16)."""
+from __future__ import annotations
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("B,C,H,W", [(1, 8, 2, 2), (2, 64, 6, 10), (8, 256, 184, 320), (3, 1024, 46, 80), (1, 24, 4, 2)])
+def test_avgpool2x2_matches_torch(hip_lib, B, C, H, W):
+    from src.rtdetr_moe.backbone import _AvgPool2x2, avg_pool_2x2
+
+    g = torch.Generator().manual_seed(B * C + H)
+    x = torch.randn(B, C, H, W, generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=torch.channels_last)
+    x1 = x.clone().requires_grad_(True)
+    x2 = x.clone().requires_grad_(True)
+    ref = F.avg_pool2d(x1.float(), 2, 2, 0, ceil_mode=True)
+    got = avg_pool_2x2(x2)
+    assert got.grad_fn is not None and "AvgPool2x2" in type(got.grad_fn).__name__
+    assert got.is_contiguous(memory_format=torch.channels_last) and got.shape == ref.shape
+    ulp = ref.abs() * 2.0 ** -8 + 1e-30
+    assert bool(((got.float() - ref).abs() <= ulp).all())
+    gy = torch.randn(got.shape, generator=g).to(torch.bfloat16).cuda()
+    got.backward(gy)
+    gref = (gy.float().repeat_interleave(2, 2).repeat_interleave(2, 3) * 0.25).to(torch.bfloat16)
+    assert torch.equal(x2.grad, gref)
+    assert x2.grad.is_contiguous(memory_format=torch.channels_last)
+    _ = _AvgPool2x2  # the HIP path, not the reshape-mean fallback
