@@ -394,6 +394,17 @@ __global__ __launch_bounds__(256) void aux_loss_fwd_kernel(const float* __restri
 // ---------------------------------------------------------------------------
 // token backward: dispatch transpose + router backward
 // ---------------------------------------------------------------------------
+// dl[e] = the value lane (e mod 16) of this 16-lane row holds in dlq[e / 16]
+// (DPP row_newbcast, no LDS round trip).
+template <int EP, int E0, int Q>
+__device__ __forceinline__ void row_bcast_all(const float (&dlq)[Q], float (&dl)[EP]) {
+  if constexpr (E0 < EP) {
+    dl[E0] = __int_as_float(
+        __builtin_amdgcn_update_dpp(0, __float_as_int(dlq[E0 >> 4]), 0x150 + (E0 & 15), 0xF, 0xF, false));
+    row_bcast_all<EP, E0 + 1, Q>(dlq, dl);
+  }
+}
+
 template <int EMAX>
 __global__ __launch_bounds__(256) void token_bwd_kernel(
     const uint16_t* __restrict__ dxp, const int32_t* __restrict__ pos,
@@ -423,43 +434,54 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
   for (int tb = blockIdx.x * 16; tb < T; tb += gridDim.x * 16) {
     const int t = tb + (tid >> 6) * 4 + grp;
     if (t >= T) continue;
-    // ---- router backward (every lane of the group, redundantly) ----
-    float p[EMAX], dp[EMAX];
+    // ---- router backward: lane sub owns experts 16 q + sub (as in the forward) ----
+    constexpr int EP = EMAX < 16 ? 16 : EMAX;
+    constexpr int Q = EP / 16;
+    float p[Q], dp[Q];
+    bool own[Q];
 #pragma unroll
-    for (int e = 0; e < EMAX; ++e) {
-      p[e] = (e < E) ? probs[(size_t)t * E + e] : 0.f;
-      dp[e] = (e < E && dprob_bias != nullptr) ? dprob_bias[e] : 0.f;
+    for (int q = 0; q < Q; ++q) {
+      const int e = 16 * q + sub;
+      own[q] = e < E;
+      p[q] = own[q] ? probs[(size_t)t * E + e] : 0.f;
+      dp[q] = (own[q] && dprob_bias != nullptr) ? dprob_bias[e] : 0.f;
     }
     int pj[8];
     _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) pj[j] = pos[(size_t)t * k + j];
     int sel[8];
     float selw[8], seldw[8];
-    float S = 0.f, wdw = 0.f;
+    float Sl = 0.f, wdw = 0.f;
     _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
       sel[j] = topk_idx[(size_t)t * k + j];
       selw[j] = topk_w[(size_t)t * k + j];
       seldw[j] = dw[(size_t)t * k + j];
       wdw += selw[j] * seldw[j];
-      float pj = 0.f;
+      if ((sel[j] & 15) == sub) {
 #pragma unroll
-      for (int e = 0; e < EMAX; ++e)
-        if (e == sel[j]) pj = p[e];
-      S += pj;
+        for (int q = 0; q < Q; ++q)
+          if (q == (sel[j] >> 4)) Sl += p[q];
+      }
     }
+    const float S = row16_sum(Sl);  // sum of the selected probabilities
     const bool renorm = normalize && k > 1;
     _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
       const float g = renorm ? (seldw[j] - wdw) / S : seldw[j];
+      if ((sel[j] & 15) == sub) {
 #pragma unroll
-      for (int e = 0; e < EMAX; ++e)
-        if (e == sel[j]) dp[e] += g;
+        for (int q = 0; q < Q; ++q)
+          if (q == (sel[j] >> 4)) dp[q] += g;
+      }
     }
-    float dot = 0.f;
+    float dotl = 0.f;
 #pragma unroll
-    for (int e = 0; e < EMAX; ++e) dot += p[e] * dp[e];
+    for (int q = 0; q < Q; ++q) dotl += p[q] * dp[q];
+    const float dot = row16_sum(dotl);
     const float zt = zc * lse[t];
-    float dl[EMAX];
+    float dlq[Q];
 #pragma unroll
-    for (int e = 0; e < EMAX; ++e) dl[e] = p[e] * (dp[e] - dot) + zt * p[e];
+    for (int q = 0; q < Q; ++q) dlq[q] = own[q] ? p[q] * (dp[q] - dot) + zt * p[q] : 0.f;
+    float dl[EP];  // every expert's dlogit, broadcast from its owner (DPP row_newbcast)
+    row_bcast_all<EP, 0, Q>(dlq, dl);
     // ---- dx = sum_j dXp[pos] + dlogits . Wg ----
     // (dlogits is stored after dx: on gfx9 vmcnt also counts stores, so a
     // store issued before the dXp gathers would delay their wait)
@@ -485,16 +507,15 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
           acc[4] += dl[e] * w1.x; acc[5] += dl[e] * w1.y;
           acc[6] += dl[e] * w1.z; acc[7] += dl[e] * w1.w;
         }
+        // keep the compiler from hoisting every expert's Wg reads at once
+        // (E x 8 registers: occupancy 1 wave/SIMD at E = 32)
+        if ((e & 7) == 7) asm volatile("" ::: "memory");
       }
       reinterpret_cast<uint4*>(dx + (size_t)t * d)[ch] = pack8(acc);
     }
-    for (int e = sub; e < E; e += 16) {
-      float v = 0.f;
 #pragma unroll
-      for (int q = 0; q < EMAX; ++q)
-        if (q == e) v = dl[q];
-      dlogits[(size_t)t * E + e] = v;
-    }
+    for (int q = 0; q < Q; ++q)
+      if (own[q]) dlogits[(size_t)t * E + 16 * q + sub] = dlq[q];
   }
 }
 
