@@ -9,16 +9,89 @@ The reference's RT-DETR adapter reuses these from its YOLO module
   run_metadata.{json,csv}, train_summary.{json,csv}
 scripts/report_detector_benchmarks.py reads them back, so key names, key
 order and fallbacks match the reference (pinned by tests/golden/
-reference_known_answers.json).  Only the artifact half of the reference's
-module is here; YOLO training itself is out of scope.
+reference_known_answers.json).  The YOLO train/eval half of the reference's
+module (yolo.py:19-182, 379-388) is a different model family and out of scope;
+its names are exported with the reference's lazy-import behaviour (an
+ImportError naming Ultralytics when called), so the reference's unchanged
+callers -- scripts/eval_detector.py:28-35 imports eval_yolo_detector and
+get_yolo_model_size_stats_from_weights at module load -- import this module.
 """
 from __future__ import annotations
 
 import csv
 import json
+from dataclasses import dataclass
 from pathlib import Path
+from typing import Union
 
 import numpy as np
+
+
+@dataclass
+class YoloTrainConfig:
+    """Field-for-field the reference's YoloTrainConfig (yolo.py:19-37)."""
+    data_yaml: str
+    model: str = "yolo26s.pt"
+    imgsz: Union[int, tuple[int, int]] = (704, 1248)
+    rect: bool = True
+    epochs: int = 50
+    patience: int = 100
+    batch: int = 16
+    device: str = "0"
+    project: str = "outputs/runs/yolo"
+    name: str = "baseline"
+    seed: int = 0
+    workers: int = 8
+    scale: float = 0.0
+    translate: float = 0.0
+    mosaic: float = 0.0
+    close_mosaic: int = 0
+
+
+def _import_ultralytics_yolo():
+    """The reference's lazy import (yolo.py:40-60): YOLO runs need Ultralytics,
+    which this MI355X build does not ship (YOLO is out of its scope)."""
+    try:
+        from ultralytics import YOLO  # type: ignore
+    except Exception as e:
+        raise ImportError(
+            "Ultralytics is required for YOLO adapter. Install with `pip install ultralytics`. "
+            "(The MI355X build implements the RT-DETR-MoE backend only: use --backend rtdetr.)") from e
+    return YOLO
+
+
+def _format_ultralytics_imgsz(imgsz: Union[int, tuple[int, int]]):
+    """(h, w) -> [h, w]; int -> int (reference yolo.py:175-182)."""
+    if isinstance(imgsz, tuple):
+        return [int(imgsz[0]), int(imgsz[1])]
+    return int(imgsz)
+
+
+def train_yolo_detector(cfg: YoloTrainConfig):
+    """Reference yolo.py:63-95 (Ultralytics YOLO.train)."""
+    YOLO = _import_ultralytics_yolo()
+    model = YOLO(cfg.model)
+    return model.train(data=cfg.data_yaml, imgsz=_format_ultralytics_imgsz(cfg.imgsz), rect=cfg.rect,
+                       epochs=cfg.epochs, patience=cfg.patience, batch=cfg.batch, device=cfg.device,
+                       project=cfg.project, name=cfg.name, seed=cfg.seed, workers=cfg.workers, scale=cfg.scale,
+                       translate=cfg.translate, mosaic=cfg.mosaic, close_mosaic=cfg.close_mosaic)
+
+
+def eval_yolo_detector(data_yaml: str, weights_path: str, split: str = "val",
+                       imgsz: Union[int, tuple[int, int]] = (704, 1248), rect: bool = True, batch: int = 16,
+                       device: str = "0", project: str | None = None, name: str | None = None):
+    """Reference yolo.py:128-172 (Ultralytics YOLO.val)."""
+    YOLO = _import_ultralytics_yolo()
+    model = YOLO(weights_path)
+    kw = {k: v for k, v in (("project", project), ("name", name)) if v}
+    return model.val(data=data_yaml, split=split, imgsz=_format_ultralytics_imgsz(imgsz), rect=rect, batch=batch,
+                     device=device, **kw)
+
+
+def get_yolo_model_size_stats_from_weights(weights_path: str) -> dict:
+    """Reference yolo.py:379-388: params/FLOPs of YOLO weights (needs Ultralytics)."""
+    YOLO = _import_ultralytics_yolo()
+    return _size_stats(YOLO(weights_path))
 
 _RESULT_KEYS = (  # output key, Ultralytics results_dict key
     ("map50", "metrics/mAP50(B)"),

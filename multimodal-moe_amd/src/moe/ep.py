@@ -101,6 +101,7 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap):
     T = x.shape[0]
     dev = x.device
     mx = x.is_cuda and cfg.expert_dtype == "fp8"
+    gs = getattr(layer, "ep_grad_scale", 1.0 / W)  # 1.0 when the optimizer applies 1/W (graph-mode TrainStep)
     if mx:
         from .ops import aux_losses, combine_hip as combine, expert_ffn_mx_hip, route_dispatch_mx_hip
 
@@ -136,7 +137,7 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap):
     offs_l = offs_l.to(dev, non_blocking=True)
     if mx:
         ce, qe, se = _DispatchMX.apply(xp, xq, xs, send, recv, perm, inv, group)
-        ye = expert_ffn_mx_hip(ce, qe, se, layer.w1, layer.b1, layer.w2, layer.b2, offs_l, R, 1.0 / W) if R else \
+        ye = expert_ffn_mx_hip(ce, qe, se, layer.w1, layer.b1, layer.w2, layer.b2, offs_l, R, gs) if R else \
             x.new_zeros((0, x.shape[1]), dtype=torch.bfloat16)
         yr = ye.index_select(0, inv)
         yp = _AllToAll.apply(yr, recv, send, group)
@@ -144,10 +145,10 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap):
     xr = _AllToAll.apply(xp[:n_send], send, recv, group)
     xe = xr.index_select(0, perm)
     if x.is_cuda:
-        ye = expert_ffn(xe, layer.w1, layer.b1, layer.w2, layer.b2, offs_l, R, 1.0 / W) if R else \
+        ye = expert_ffn(xe, layer.w1, layer.b1, layer.w2, layer.b2, offs_l, R, gs) if R else \
             xe.new_zeros((0, x.shape[1]))
     else:
-        ye = expert_ffn(xe, layer.w1, layer.b1, layer.w2, layer.b2, offs_l, 1.0 / W)
+        ye = expert_ffn(xe, layer.w1, layer.b1, layer.w2, layer.b2, offs_l, gs)
     yr = ye.index_select(0, inv)
     yp = _AllToAll.apply(yr, recv, send, group)
     y = combine(yp, w, pos, T)

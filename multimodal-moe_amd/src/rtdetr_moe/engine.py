@@ -6,9 +6,10 @@ Replaces what the reference delegates to Ultralytics (``RTDETR(cfg.model)
   * ``validate(...)`` -> DetMetrics    (.results_dict, .box, .speed, .model)
 Devices follow the reference's ``device`` string ("cpu", "0", "0,1,2,3"):
 one process per GPU; a multi-GPU string launches that many local workers
-(torch.multiprocessing) unless the caller is already under torchrun; gradients
-are all-reduced by DDP over RCCL.  bf16 autocast on GPU,
-fp32 on CPU (config C1).
+(torch.multiprocessing) unless the caller is already under torchrun.  Every
+training batch is one ``step.TrainStep`` -- the same step bench.py times: on
+the GPU a whole-step hipGraph with bf16 weights + fp32 masters and the flat
+RCCL gradient all-reduce; fp32 eager on CPU (config C1).
 """
 from __future__ import annotations
 
@@ -107,10 +108,12 @@ def _results_dict(box: BoxMetrics) -> dict:
 # ---------------------------------------------------------------------------
 # checkpoints: plain dicts of tensors / primitives (torch.load weights_only=True)
 # ---------------------------------------------------------------------------
-def save_checkpoint(path: Path, model: RTDETRMoE, epoch: int, fitness: float, optimizer=None):
+def save_checkpoint(path: Path, model: RTDETRMoE, epoch: int, fitness: float, optimizer=None, state_dict=None):
     path.parent.mkdir(parents=True, exist_ok=True)
+    sd = model.state_dict() if state_dict is None else state_dict
     ck = {"spec": model.spec.raw, "num_classes": model.num_classes, "epoch": int(epoch),
-          "fitness": float(fitness), "state_dict": {k: v.detach().cpu() for k, v in model.state_dict().items()}}
+          "fitness": float(fitness), "state_dict": {k: v.detach().float().cpu() if v.is_floating_point() else
+                                                    v.detach().cpu() for k, v in sd.items()}}
     if model.spec.moe is not None:
         ck["moe_cfg"] = {k: v for k, v in asdict(model.spec.moe).items()}
     if optimizer is not None:
@@ -148,7 +151,7 @@ def _hw(imgsz):
     return (imgsz, imgsz) if isinstance(imgsz, int) else (int(imgsz[0]), int(imgsz[1]))
 
 
-def _batches(data, split, imgsz, batch, workers, seed, rank, world, epoch):
+def _batches(data, split, imgsz, batch, workers, seed, rank, world, epoch, drop_last=False):
     h, w = _hw(imgsz)
     if _is_synthetic(data):
         gen = SyntheticZOD(batch=batch, img_h=h, img_w=w, seed=seed * 1000 + rank + (0 if split == "train" else 777)
@@ -167,7 +170,8 @@ def _batches(data, split, imgsz, batch, workers, seed, rank, world, epoch):
     g = torch.Generator().manual_seed(seed + epoch)
     dl = torch.utils.data.DataLoader(ds, batch_size=batch, shuffle=(split == "train" and sampler is None),
                                      sampler=sampler, num_workers=workers, collate_fn=collate,
-                                     generator=g, drop_last=False, persistent_workers=False)
+                                     generator=g, drop_last=drop_last and len(ds) >= batch * world,
+                                     persistent_workers=False)
     yield from dl
 
 
@@ -200,14 +204,33 @@ def _seed_all(seed: int):
     torch.manual_seed(seed)
 
 
-def _optimizer(model: RTDETRMoE, a: TrainArgs):
-    bb = [p for n, p in model.named_parameters() if n.startswith("backbone.") and p.requires_grad]
-    rest = [p for n, p in model.named_parameters() if not n.startswith("backbone.") and p.requires_grad]
-    return torch.optim.AdamW([{"params": bb, "lr": a.lr_backbone}, {"params": rest, "lr": a.lr}],
-                             lr=a.lr, weight_decay=a.weight_decay)
+def _master_state_dict(core: RTDETRMoE, step) -> dict:
+    """The model's state dict with every bf16 GEMM/conv weight replaced by its
+    fp32 master from the optimizer (TrainStep precision "bf16"), so a
+    checkpoint carries the exact training state."""
+    sd = core.state_dict()
+    opt = getattr(step, "opt", None)
+    if opt is None or not hasattr(opt, "master_of"):
+        return sd
+    names = {id(p): n for n, p in core.named_parameters()}
+    for p in opt.params:
+        if p.dtype == torch.bfloat16 and id(p) in names:
+            sd[names[id(p)]] = opt.master_of(p).as_strided(p.shape, p.stride()).detach()
+    return sd
 
 
 def _train_worker(a: TrainArgs, rank: int, world: int, local: int | str) -> TrainResults | None:
+    """One rank's training loop.  Each batch is one ``TrainStep`` -- the step
+    bench.py measures: on the GPU bf16 GEMM/conv weights with fp32 masters, the
+    whole differentiable step (forward, set criterion with the GPU Hungarian
+    matcher, backward) replayed as ONE hipGraph, the flat gradient all-reduce
+    over RCCL when world > 1, and the fused clip + AdamW (FlatAdamW); on the
+    CPU (config C1) fp32 eager with torch.optim.AdamW + clip_grad_norm_ (DDP
+    over gloo when world > 1).  The graph has static shapes, so on the GPU the
+    train loader drops a last partial batch (every step sees ``batch`` images);
+    the loss is accumulated on the device and read once per epoch."""
+    from .step import TrainStep
+
     on_gpu = local != "cpu"
     device = torch.device("cuda", local) if on_gpu else torch.device("cpu")
     if on_gpu:
@@ -224,8 +247,6 @@ def _train_worker(a: TrainArgs, rank: int, world: int, local: int | str) -> Trai
     if on_gpu:
         model = model.to(memory_format=torch.channels_last)
     core = model
-    net = wrap_ddp(model, local if on_gpu else None) if world > 1 else model
-    opt = _optimizer(core, a)
     crit = SetCriterion(num_classes=core.num_classes)
     save_dir = Path(a.project) / a.name
     wdir = save_dir / "weights"
@@ -235,34 +256,35 @@ def _train_worker(a: TrainArgs, rank: int, world: int, local: int | str) -> Trai
     last_metrics = BoxMetrics()
     csv_rows = []
     epoch = 0
+    step = None
+    shape = None
     for epoch in range(a.epochs):
-        net.train()
+        core.train()
         t_ep = time.perf_counter()
-        tot, n = 0.0, 0
+        tot = torch.zeros((), dtype=torch.float64, device=device)
+        n = 0
         for images, targets, ctx in _batches(a.data, "train", a.imgsz, a.batch, a.workers, a.seed, rank, world,
-                                             epoch):
+                                             epoch, drop_last=on_gpu):
             images = images.to(device, non_blocking=True)
             if on_gpu:
                 images = images.contiguous(memory_format=torch.channels_last)
             ctx = ctx.to(device)
             tg = [{"boxes": t["boxes"].to(device), "labels": t["labels"].to(device)} for t in targets]
-            nb = torch.tensor([float(sum(len(t["boxes"]) for t in tg))], device=device)
+            nb = torch.tensor([float(sum(len(t["boxes"]) for t in targets))], device=device)
             if world > 1:
                 dist.all_reduce(nb)
-            num_boxes = max(1.0, float(nb.item()) / world)
-            opt.zero_grad(set_to_none=True)
-            with torch.autocast(device.type, dtype=torch.bfloat16, enabled=on_gpu):
-                out = net(images, ctx)
-            losses = crit(out, tg, num_boxes)
-            loss = sum(losses.values())
-            aux = core.moe_aux_loss()
-            if aux is not None:
-                loss = loss + aux
-            loss.backward()
-            if a.clip_norm > 0:
-                torch.nn.utils.clip_grad_norm_(net.parameters(), a.clip_norm)
-            opt.step()
-            tot += float(loss.detach())
+            num_boxes = (nb / world).clamp_(min=1.0).reshape(())
+            if step is None:
+                step = TrainStep(core, crit, images, ctx, lr=a.lr, lr_backbone=a.lr_backbone,
+                                 weight_decay=a.weight_decay, clip_norm=a.clip_norm, graphs=on_gpu, world=world,
+                                 precision="bf16" if on_gpu else "fp32",
+                                 ddp_local=None, targets=tg if on_gpu else None,
+                                 num_boxes=float(num_boxes))
+                shape = tuple(images.shape)
+            if on_gpu and tuple(images.shape) != shape:
+                raise RuntimeError(f"batch shape {tuple(images.shape)} differs from the captured {shape}")
+            loss = step(images, ctx, tg, num_boxes if on_gpu else float(num_boxes))
+            tot += loss.detach().double()
             n += 1
         # validation (rank 0 evaluates the unwrapped model)
         metrics = None
@@ -270,11 +292,12 @@ def _train_worker(a: TrainArgs, rank: int, world: int, local: int | str) -> Trai
             metrics = _evaluate(core, a.data, "val", a.imgsz, a.batch, device, a.workers, a.seed)
             last_metrics = metrics
             fit = _results_dict(metrics)["fitness"]
-            save_checkpoint(wdir / "last.pt", core, epoch, fit)
+            sd = _master_state_dict(core, step)
+            save_checkpoint(wdir / "last.pt", core, epoch, fit, state_dict=sd)
             if fit > best_fit:
                 best_fit, best_epoch = fit, epoch
-                save_checkpoint(wdir / "best.pt", core, epoch, fit)
-            row = {"epoch": epoch + 1, "train/loss": tot / max(n, 1), "time_s": time.perf_counter() - t_ep,
+                save_checkpoint(wdir / "best.pt", core, epoch, fit, state_dict=sd)
+            row = {"epoch": epoch + 1, "train/loss": float(tot) / max(n, 1), "time_s": time.perf_counter() - t_ep,
                    **_results_dict(metrics)}
             row.update(_moe_stats(core))
             csv_rows.append(row)

@@ -138,13 +138,17 @@ class GraphedStep:
     copies before each replay; gradients land in ``static_grads``.  No host
     round trip inside the step: the host only refreshes inputs, replays, and
     launches the optimizer.  Targets are padded to ``max_boxes`` per image;
-    a batch with more boxes re-captures at the next multiple of 16."""
+    a batch with more boxes re-captures at the next multiple of 16; the new
+    capture allocates new gradient buffers, announced through ``on_capture``
+    (TrainStep re-points ``p.grad`` and drops its flat all-reduce views)."""
 
     def __init__(self, fn, criterion, params, images, ctx, targets, num_boxes, *, warmup=3, autocast=False,
-                 max_boxes=None):
+                 max_boxes=None, on_capture=None):
         from .criterion import pad_targets
 
         self.fn, self.criterion, self.params, self.autocast = fn, criterion, params, autocast
+        self.on_capture = on_capture  # called with static_grads after every (re-)capture
+        self.captures = 0
         dev = images.device
         self.static_images = images.clone()
         self.static_ctx = ctx.clone()
@@ -185,6 +189,9 @@ class GraphedStep:
             self.static_losses = {k: v.detach() for k, v in losses.items()}
         self.static_grads = [g if g is not None else torch.zeros_like(p) for g, p in zip(grads, self.params)]
         torch.cuda.synchronize()
+        self.captures += 1
+        if self.on_capture is not None:
+            self.on_capture(self.static_grads)
 
     def __call__(self, images, ctx, targets, num_boxes):
         from .criterion import pad_targets
@@ -200,7 +207,10 @@ class GraphedStep:
         if ctx.data_ptr() != self.static_ctx.data_ptr():
             self.static_ctx.copy_(ctx)
         pad_targets(targets, self.M, self.tb, self.tl, self.nv)
-        self.nb.fill_(float(num_boxes))
+        if torch.is_tensor(num_boxes):  # device scalar (e.g. all-reduced box count): no host sync
+            self.nb.copy_(num_boxes.reshape(()))
+        else:
+            self.nb.fill_(float(num_boxes))
         self.graph.replay()
         return self.static_loss
 
@@ -275,16 +285,24 @@ class TrainStep:
                                          weight_decay=weight_decay)
         self.flat = FlatOutputs(model)
         self.dp_params = [p for p in self.params if not getattr(p, "expert_parallel", False)]
+        self._flat_grads = None
+        if graphs and world > 1 and images.is_cuda:
+            # graph mode sums gradients over ranks and the optimizer applies 1/world
+            # to EVERY gradient (FlatAdamW inv_world); expert-parallel weights are
+            # not all-reduced, so their layers must not pre-scale by 1/world
+            from ..moe.layer import MoEFFN
+
+            for m in model.modules():
+                if isinstance(m, MoEFFN) and m.ep_size > 1:
+                    m.ep_grad_scale = 1.0
         images = self._cast_in(images)
         self.runner = None
         self.stepper = None
         if graphs and targets is not None:  # whole step as one graph (GPU matcher)
             self.stepper = GraphedStep(self.flat, criterion, self.params, images, ctx, targets, num_boxes,
-                                       autocast=self.precision == "amp")
+                                       autocast=self.precision == "amp", on_capture=self._bind_grads)
             self.fn = None
             self.ddp = None
-            for p, g in zip(self.params, self.stepper.static_grads):
-                p.grad = g
         elif graphs:
             self.runner = GraphedModel(self.flat, self.params, images, ctx, autocast=self.precision == "amp")
             self.fn = self.runner
@@ -300,6 +318,13 @@ class TrainStep:
         else:
             self.fn = self.flat
             self.ddp = None
+
+    def _bind_grads(self, static_grads):
+        """Point every parameter's .grad at the (new) static gradient buffers of
+        a capture and forget flat views built on the previous ones."""
+        for p, g in zip(self.params, static_grads):
+            p.grad = g
+        self._flat_grads = None
 
     def _cast_in(self, images):
         return images.to(torch.bfloat16) if self.precision == "bf16" else images
@@ -321,8 +346,10 @@ class TrainStep:
         gradient buffers are gathered into one flat buffer per dtype by
         multi-tensor copies and summed with one RCCL all_reduce each; the
         optimizer reads the flat buffers (views, in parameter order) and divides
-        by the world size inside its kernels.  Returns the gradient list."""
-        if getattr(self, "_flat_grads", None) is None:
+        by the world size inside its kernels.  Returns the gradient list in the
+        optimizer's parameter order: the reduced views for data-parallel
+        parameters, the local gradients for expert-parallel ones."""
+        if self._flat_grads is None:
             groups = {}
             for i, p in enumerate(self.dp_params):
                 groups.setdefault(p.grad.dtype, []).append(i)
@@ -338,10 +365,12 @@ class TrainStep:
                     self._reduced[i] = v
                     off += g.numel()
                 self._flat_grads.append((flat, views, gs))
+            red = {id(p): v for p, v in zip(self.dp_params, self._reduced)}
+            self._opt_grads = [red.get(id(p), p.grad) for p in self.opt.params]
         for flat, views, gs in self._flat_grads:
             torch._foreach_copy_(views, gs)
             dist.all_reduce(flat)
-        return self._reduced
+        return self._opt_grads
 
     def _mark(self, name):
         if self.phases is not None:

@@ -60,7 +60,7 @@ def test_cli_flags_match_reference():
 def test_config_c1_train_then_eval_on_cpu(tmp_path):
     """BASELINE.json configs[0]: train_rtdetr.py R18 + 4-expert top-1 MoE, 2 frames, CPU only."""
     env = dict(os.environ, OUTPUTS_DIR=str(tmp_path), OMP_NUM_THREADS="4")
-    common = ["--img-h", "256", "--img-w", "256", "--device", "cpu", "--data-yaml", "synthetic:1"]
+    common = ["--img-h", "640", "--img-w", "640", "--device", "cpu", "--data-yaml", "synthetic:1"]
     r = subprocess.run([sys.executable, str(PKG / "scripts/train_rtdetr.py"), "--model", "rtdetr-r18-moe4-top1",
                         "--batch", "2", "--epochs", "1", "--workers", "0", "--run-name", "c1", *common],
                        capture_output=True, text=True, env=env, timeout=600)

@@ -227,3 +227,41 @@ def test_fused_criterion_matches_padded(hip_lib, C):
     torch.testing.assert_close(total.detach(), sum(ref.values()).detach(), rtol=1e-4, atol=1e-6)
     for i, (a, b) in enumerate(zip(got_grads, ref_grads)):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6, msg=f"grad of leaf {i}")
+
+
+@pytest.mark.gpu
+def test_whole_step_recapture_rebinds_gradients(hip_lib):
+    """A batch with more boxes than the captured padding (16 per image)
+    re-captures GraphedStep with NEW gradient buffers: every parameter's .grad
+    and the optimizer's gradient table must follow them (the old
+    buffers, never written again, kept feeding the optimizer), and the update
+    written by the recaptured graph move the parameters."""
+    from src.rtdetr_moe.step import TrainStep
+
+    model, crit, images, targets, ctx = _setup(seed=6)
+    nb = max(1.0, float(sum(len(t["boxes"]) for t in targets)))
+    step = TrainStep(model, crit, images, ctx, graphs=True, world=1, precision="bf16", lr=1e-3,
+                     targets=targets, num_boxes=nb)
+    step(images, ctx, targets, nb)
+    old = [g.data_ptr() for g in step.stepper.static_grads]
+    g = torch.Generator(device=DEV).manual_seed(9)
+    big = [{"boxes": torch.rand(20, 4, device=DEV, generator=g) * 0.2 + 0.3,
+            "labels": torch.zeros(20, dtype=torch.int64, device=DEV)},
+           {"boxes": torch.rand(2, 4, device=DEV, generator=g) * 0.2 + 0.3,
+            "labels": torch.zeros(2, dtype=torch.int64, device=DEV)}]
+    p = model.decoder.dec_score_head[0].bias
+    m0 = step.opt.master_of(p).clone()
+    loss = float(step(images, ctx, big, 22.0))
+    torch.cuda.synchronize()
+    assert step.stepper.captures == 2 and step.stepper.M == 32
+    assert torch.isfinite(torch.tensor(loss))
+    new = step.stepper.static_grads
+    assert [x.data_ptr() for x in new] != old
+    assert all(q.grad is x for q, x in zip(step.params, new))
+    for i, q in enumerate(step.opt.params):  # the optimizer's table reads the new buffers (or their staged copy)
+        st = step.opt._staged.get(i)
+        assert step.opt._ptrs[i] in (q.grad.data_ptr(), st.data_ptr() if st is not None else -1), i
+    # the recaptured graph wrote the new buffers and the optimizer applied them
+    d = step.opt.master_of(p) - m0
+    gr = p.grad.float().reshape(-1)
+    assert float(gr.abs().max()) > 0 and float(d.abs().max()) > 0
