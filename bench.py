@@ -18,9 +18,12 @@ times from dispatch-stamped HIP events of every launch inside the timed
 region, recorded by libmoe_hip itself; algorithmic bytes and flops per launch;
 bound = HBM, since at d=256, F=1024 every expert GEMM has ~200 flop/B, below
 the MI355X balance of ~312), ``roofline_dispatch`` for the row movers, and
-``cpu_baseline``: the same model in fp32 on the host cores with the MoE layers
-computed by the CPU oracle (oracle/moe_oracle.py, kind "port"), timed on a
-bounded sample (rank 0, N=1 only).
+``cpu_baseline``: the same model and step in fp32 on the host cores at the
+workload's batch (MoE layers through the package's CPU device path,
+src/moe/eager.py, in fp32 torch ops; kind "port"), timed on a bounded sample
+(rank 0, N=1 only), and ``roofline_e2e``: images/s x measured model FLOP per
+image (FlopCounterMode over one fp32 CPU fwd+bwd at the workload's resolution)
+/ the bf16 MFMA peak.
 """
 from __future__ import annotations
 
@@ -50,6 +53,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "images/sec (fwd+bwd) RT-DETR-MoE 1280×720 bs=8/GPU at 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_FP8_TFLOPS = 5000.0    # MI355X dense fp8 MFMA (the MXFP8 expert GEMMs of C5)
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec peak
 
 WORKLOADS = {
@@ -80,22 +84,39 @@ def load_pmc_traffic(workload):
     return out
 
 
+def merge_groups(*ds):
+    """Sum the profiler totals of several kinds (e.g. the bf16 and fp8 launches
+    of the grouped GEMM) into one group."""
+    ds = [d for d in ds if d]
+    if not ds:
+        return None
+    out = {k: sum(d[k] for d in ds) for k in ("launches", "total_ms", "flops", "bytes", "t_mfma_ms", "t_hbm_ms",
+                                               "t_roof_ms")}
+    out["avg_us"] = 1e3 * out["total_ms"] / max(out["launches"], 1)
+    return out
+
+
 def roofline_entry(d, pmc, elapsed, kernel):
     """Roofline of one kernel group over the timed region.  Every launch is
-    bounded by max(flops / MFMA peak, algorithmic bytes / HBM peak); the group's
-    bound is the resource with the larger summed time.  achieved = algorithmic
-    work / measured kernel time (dispatch-stamped HIP events)."""
+    bounded by max(flops / MFMA peak of its dtype, algorithmic bytes / HBM
+    peak); the group's bound is the resource with the larger summed time.
+    achieved = algorithmic work / measured kernel time (dispatch-stamped HIP
+    events).  The MFMA fraction is sum(flops_i / peak_i) / time, i.e. bf16
+    launches priced at the bf16 peak and MXFP8 launches at the fp8 peak; the
+    reported MFMA ``peak`` is the effective (flop-weighted) one."""
     if not d or d["total_ms"] <= 0:
         return None
     sec = d["total_ms"] * 1e-3
     hbm = d["t_hbm_ms"] >= d["t_mfma_ms"]
     ach_gbs = d["bytes"] / sec / 1e9
     ach_tf = d["flops"] / sec / 1e12
+    peak_tf = d["flops"] / (d["t_mfma_ms"] * 1e-3) / 1e12 if d["t_mfma_ms"] > 0 else PEAK_BF16_TFLOPS
+    mfma_frac = d["t_mfma_ms"] / d["total_ms"]
     e = {"bound": "hbm" if hbm else "mfma",
          "achieved": round(ach_gbs if hbm else ach_tf, 2),
-         "peak": PEAK_HBM_GBS if hbm else PEAK_BF16_TFLOPS,
+         "peak": PEAK_HBM_GBS if hbm else round(peak_tf, 1),
          "unit": "GB/s" if hbm else "TFLOP/s",
-         "frac": round((ach_gbs / PEAK_HBM_GBS) if hbm else (ach_tf / PEAK_BF16_TFLOPS), 4),
+         "frac": round((ach_gbs / PEAK_HBM_GBS) if hbm else mfma_frac, 4),
          "traffic": pmc["bytes"] if pmc else None,
          "kernel": kernel, "launches": d["launches"], "avg_us": round(d["avg_us"], 2),
          "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
@@ -103,10 +124,11 @@ def roofline_entry(d, pmc, elapsed, kernel):
          "share_of_step": round(d["total_ms"] / (elapsed * 1e3), 4)}
     if d["flops"]:
         e["flop_per_launch"] = round(d["flops"] / d["launches"])
-        e["mfma"] = {"achieved": round(ach_tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(ach_tf / PEAK_BF16_TFLOPS, 4)}
+        e["mfma"] = {"achieved": round(ach_tf, 2), "peak": round(peak_tf, 1), "unit": "TFLOP/s",
+                     "frac": round(mfma_frac, 4)}
     if pmc:
         e["traffic_source"] = pmc["source"]
+        e["traffic_over_algorithmic"] = round(pmc["bytes"] / (d["bytes"] / d["launches"]), 3)
     return e
 
 
@@ -120,7 +142,8 @@ def parse_args():
     ap.add_argument("--img-h", type=int, default=720)
     ap.add_argument("--img-w", type=int, default=1280)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample length")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU baseline sample length")
+    ap.add_argument("--no-e2e-roofline", action="store_true", help="skip the model-FLOP count (roofline_e2e)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--precision", choices=["bf16", "amp"], default="bf16",
                     help="bf16: bf16 GEMM/conv weights + fp32 master weights; amp: fp32 weights under bf16 autocast")
@@ -190,23 +213,30 @@ def build_model(spec, device, world):
     return model
 
 
-def cpu_baseline(spec, batch_img, img_h, img_w, target_s):
-    """Same model, fp32 on host cores, MoE layers through the CPU oracle."""
-    from oracle.torch_bridge import use_oracle_moe
+def host_threads():
+    """(threads used, CPUs in this process's affinity set): the affinity set,
+    capped by OMP_NUM_THREADS when the box sets it (the GPU box exports the
+    process's CPU share there; its affinity set is the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    n = min(aff, int(omp)) if omp.isdigit() and int(omp) > 0 else aff
+    return max(1, n), aff
+
+
+def _cpu_step_fn(spec, batch_img, img_h, img_w):
+    """The workload's training step on the host, fp32: same model (MoE layers
+    through src/moe/eager.py), same Hungarian-matched criterion, backward,
+    clip_grad_norm_ + torch.optim.AdamW (what TrainStep runs on CPU)."""
     from src.rtdetr_moe.criterion import SetCriterion
     from src.rtdetr_moe.data import SyntheticZOD
     from src.rtdetr_moe.model import RTDETRMoE
 
-    threads = min(torch.get_num_threads(), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    torch.set_num_threads(threads)
     torch.manual_seed(1)
-    model = RTDETRMoE(spec).to(memory_format=torch.channels_last)
-    n_moe = use_oracle_moe(model)
+    model = RTDETRMoE(spec)
     opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
     crit = SetCriterion(num_classes=1)
     data = SyntheticZOD(batch=batch_img, img_h=img_h, img_w=img_w, seed=0)
     images, targets, ctx = data.sample()
-    images = images.contiguous(memory_format=torch.channels_last)
     nb = max(1.0, float(sum(len(t["boxes"]) for t in targets)))
 
     def step():
@@ -217,6 +247,27 @@ def cpu_baseline(spec, batch_img, img_h, img_w, target_s):
         torch.nn.utils.clip_grad_norm_(model.parameters(), 0.1)
         opt.step()
 
+    return step, len(model.moe_layers())
+
+
+def model_flop_per_image(spec, img_h, img_w):
+    """Measured FLOP of one fwd+bwd per image: torch.utils.flop_counter over
+    one fp32 CPU training step of the same model at batch 1 (GEMMs, convolutions
+    and attention; the deformable-attention sampling and element-wise work are
+    not counted -- they are not MFMA work)."""
+    from torch.utils.flop_counter import FlopCounterMode
+
+    step, _ = _cpu_step_fn(spec, 1, img_h, img_w)
+    with FlopCounterMode(display=False) as fc:
+        step()
+    return float(fc.get_total_flops())
+
+
+def cpu_baseline(spec, batch_img, img_h, img_w, target_s):
+    """The same training step in fp32 on the host cores at the workload's batch."""
+    threads, aff = host_threads()
+    torch.set_num_threads(threads)
+    step, n_moe = _cpu_step_fn(spec, batch_img, img_h, img_w)
     t0 = time.perf_counter()
     step()  # warm-up
     warm = time.perf_counter() - t0
@@ -226,10 +277,11 @@ def cpu_baseline(spec, batch_img, img_h, img_w, target_s):
         step()
     dt = time.perf_counter() - t0
     return {"value": round(batch_img * n / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"{n} timed fwd+bwd+AdamW steps (+1 warm-up) of {spec} at batch {batch_img}, "
-                      f"{img_w}x{img_h} padded to 32, fp32 on {threads} host threads, {n_moe} MoE layers "
-                      f"computed by oracle/moe_oracle.py (float64 numpy"
-                      f"{', MXFP8 expert GEMMs emulated' if 'fp8' in spec else ''})"}
+            "affinity_cpus": aff,
+            "sample": f"{n} timed fwd+bwd+AdamW steps (+1 warm-up, {warm:.1f} s) of {spec} at batch {batch_img}, "
+                      f"{img_w}x{img_h} padded to 32, fp32 torch on {threads} host threads "
+                      f"(torch.set_num_threads; {aff} CPUs in the affinity set), {n_moe} MoE layers through "
+                      f"src/moe/eager.py (fp32 torch ops{', MXFP8 expert GEMMs emulated' if 'fp8' in spec else ''})"}
 
 
 def main():
@@ -325,7 +377,8 @@ def main():
         value = images_total / elapsed
         pmc = load_pmc_traffic(args.workload)
         prof_elapsed = elapsed * prof_steps / args.steps  # share_of_step: per-step kernel time / step time
-        roof = roofline_entry(ksum.get("grouped_gemm"), pmc.get("grouped_gemm"), prof_elapsed,
+        roof = roofline_entry(merge_groups(ksum.get("grouped_gemm"), ksum.get("grouped_gemm_fp8")),
+                              pmc.get("grouped_gemm"), prof_elapsed,
                               "grouped GEMM (gemm_v2_kernel: expert fwd, dgrad, wgrad)")
         rd = roofline_entry(ksum.get("dispatch"), pmc.get("dispatch"), prof_elapsed,
                             "permute_fwd / combine_fwd / combine_bwd")
@@ -362,10 +415,24 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
+        if not args.no_e2e_roofline:
+            log(rank, "counting model FLOP per image (fp32 CPU fwd+bwd under FlopCounterMode)")
+            try:
+                threads, _ = host_threads()
+                torch.set_num_threads(threads)
+                fpi = model_flop_per_image(spec, args.img_h, args.img_w)
+                ach = result["value"] * fpi / 1e12
+                result["roofline_e2e"] = {
+                    "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / PEAK_BF16_TFLOPS, 4), "model_gflop_per_image": round(fpi / 1e9, 2),
+                    "source": "images/s x FlopCounterMode FLOP of one fp32 CPU fwd+bwd per image (same model, "
+                              f"{args.img_w}x{args.img_h}) / dense bf16 MFMA peak"}
+            except Exception as e:  # report, never hide
+                result["roofline_e2e"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
         if world == 1 and not args.no_cpu_baseline:
             log(rank, "timing the CPU baseline")
             try:
-                result["cpu_baseline"] = cpu_baseline(spec, 1, args.img_h, args.img_w, args.cpu_seconds)
+                result["cpu_baseline"] = cpu_baseline(spec, batch, args.img_h, args.img_w, args.cpu_seconds)
             except Exception as e:  # report, never hide, a failed baseline
                 result["cpu_baseline"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
         else:

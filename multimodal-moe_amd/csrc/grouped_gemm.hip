@@ -1250,7 +1250,7 @@ extern "C" int moe_grouped_gemm_mx(const void* a, const void* a_scales, const vo
   const bool cq = c_scales != nullptr;
   const bool has_bias = epilogue != MOE_EPI_NONE;
   // algorithmic bytes: e4m3 weights + exponents (+ bias) once; per routed row A (K + K/32), C (2N or N + N/32)
-  ProfScope prof(stream, PROF_GEMM, G * N * (K + K / 32.0) + (has_bias ? 4.0 * G * N : 0.0), true,
+  ProfScope prof(stream, PROF_GEMM_FP8, G * N * (K + K / 32.0) + (has_bias ? 4.0 * G * N : 0.0), true,
                  K + K / 32.0 + (cq ? N + N / 32.0 : 2.0 * N), 2.0 * N * K);
   p.prof_rows = prof.rows_slot();
 #define GM_ROWS(BM, EPI)                                                                                     \

@@ -26,7 +26,8 @@ enum ProfKind {
   PROF_QUANT = 6,
   PROF_CONV_EPI = 7,
   PROF_OPTIM = 8,
-  PROF_MATCH = 9
+  PROF_MATCH = 9,
+  PROF_GEMM_FP8 = 10  // grouped GEMM on the fp8 (MXFP8 e4m3) MFMA: priced against the fp8 peak
 };
 
 class ProfScope {

@@ -116,9 +116,12 @@ def lib() -> ctypes.CDLL:
 
 
 PROF_KINDS = {0: "grouped_gemm", 1: "dispatch", 2: "router", 3: "route_scan", 4: "token_bwd", 5: "msda",
-              6: "mx_quant", 7: "conv_epilogue", 8: "optimizer", 9: "matcher"}
+              6: "mx_quant", 7: "conv_epilogue", 8: "optimizer", 9: "matcher", 10: "grouped_gemm_fp8"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP8_TFLOPS = 5000.0   # MI355X dense fp8 / MXFP8 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E
+# dense MFMA peak each profiled kind's flops are priced against
+PEAK_TFLOPS_OF = {"grouped_gemm_fp8": PEAK_FP8_TFLOPS}
 
 
 class KernelProfiler:
@@ -156,7 +159,7 @@ class KernelProfiler:
             name = PROF_KINDS.get(kind, str(kind))
             d = self.acc.setdefault(name, {"launches": 0, "total_ms": 0.0, "flops": 0.0, "bytes": 0.0,
                                            "t_mfma_ms": 0.0, "t_hbm_ms": 0.0, "t_roof_ms": 0.0})
-            t_f = flops / (PEAK_BF16_TFLOPS * 1e9)  # ms
+            t_f = flops / (PEAK_TFLOPS_OF.get(name, PEAK_BF16_TFLOPS) * 1e9)  # ms
             t_b = byts / (PEAK_HBM_GBS * 1e6)       # ms
             d["launches"] += 1
             d["total_ms"] += ms
