@@ -15,7 +15,7 @@ import torch.nn.functional as F
 
 from .linear import TokenLinear
 from ..moe.config import MoEConfig
-from .encoder import make_ffn
+from .encoder import HybridEncoder, make_ffn
 
 
 def inverse_sigmoid(x, eps=1e-5):
@@ -270,6 +270,11 @@ class RTDETRDecoder(nn.Module):
         self.dec_score_head = nn.ModuleList([TokenLinear(hidden, num_classes) for _ in range(num_layers)])
         self.dec_bbox_head = nn.ModuleList([MLP(hidden, hidden, 4, 3) for _ in range(num_layers)])
         self._anchor_cache = {}
+        # query selection of the last forward ([B, Q] token indices), and an
+        # optional override replayed instead of the top-k (tests/test_gpu_model_parity.py
+        # feeds the CPU run's selection to the GPU run so both decode the same queries)
+        self.last_topk = None
+        self.query_override = None
         self._reset()
 
     def _reset(self):
@@ -299,7 +304,10 @@ class RTDETRDecoder(nn.Module):
         return self._anchor_cache[key]
 
     def forward(self, feats, ctx):
-        proj = [p(f) for p, f in zip(self.input_proj, feats)]
+        # conv + training BatchNorm through libmoe_hip's bn_act (as the encoder's
+        # input projections): MIOpen's BN backward at batch 1 lost the gradient
+        # (relative error 1.4 vs 0.09 for a bf16 CPU run, tools/grad_flow_diag.py)
+        proj = [HybridEncoder._proj(p, f) for p, f in zip(self.input_proj, feats)]
         shapes = [tuple(f.shape[-2:]) for f in proj]
         memory = torch.cat([f.flatten(2).permute(0, 2, 1) for f in proj], 1).contiguous()  # [B, S, d]
         B = memory.shape[0]
@@ -311,9 +319,13 @@ class RTDETRDecoder(nn.Module):
         # them, and again with autograd on the B*Q selected rows only.  Same
         # values and gradients as running the heads over all tokens, without
         # the three [B*S, 256] weight-gradient GEMMs and activation storage.
-        with torch.no_grad():
-            enc_rank = self.enc_score_head(self.enc_output(mem_v)).float().max(-1).values
-        topk = torch.topk(enc_rank, self.num_queries, dim=1).indices
+        if self.query_override is not None:  # parity checks: replay another run's query selection
+            topk = self.query_override.to(memory.device)
+        else:
+            with torch.no_grad():
+                enc_rank = self.enc_score_head(self.enc_output(mem_v)).float().max(-1).values
+            topk = torch.topk(enc_rank, self.num_queries, dim=1).indices
+        self.last_topk = topk
         sel = self.enc_output(mem_v.gather(1, topk[..., None].expand(-1, -1, mem_v.shape[-1])))
         enc_topk_logits = self.enc_score_head(sel)
         ref_unact = self.enc_bbox_head(sel).float() + anchors.expand(B, -1, -1).gather(
