@@ -80,6 +80,15 @@ int moe_permute_fwd(const void* x, const int32_t* topk_idx, const int32_t* local
                     int T, int d, int E, int k, int cap,
                     void* xp, int32_t* pos, hipStream_t stream);
 
+/* a4, index half without the row copy: pos[t,j] as
+ * moe_permute_fwd, and src_tok[pos[t,j]] = t for every kept assignment
+ * (int32 [>= offsets[E]]).  The bf16 expert GEMMs read routed row r as token
+ * row src_tok[r] (moe_grouped_gemm_gather / _wgrad_gather): the permuted copy
+ * of x never exists in HBM. */
+int moe_route_index(const int32_t* topk_idx, const int32_t* local_rank, const int32_t* rank_base,
+                    const int32_t* offsets, int T, int E, int k, int cap, int32_t* pos, int32_t* src_tok,
+                    hipStream_t stream);
+
 /* a6: y[t] = sum_j topk_w[t,j] * yp[pos[t,j]] (pos<0 skipped),
  * fp32 accumulation, bf16 out. */
 int moe_combine_fwd(const void* yp, const int32_t* pos, const float* topk_w,
@@ -146,6 +155,30 @@ int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, float* c,
 int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, void* c,
                                 void* colsum, const int32_t* offsets, int G, int M,
                                 int N, int rows_hint, int out_bf16, hipStream_t stream);
+
+/* moe_grouped_gemm with routed row r of A read as a[a_gather[r]] (a: bf16
+ * [T, K] token rows; a_gather: int32 [>= offsets[G]], moe_route_index's
+ * src_tok); a_gather == NULL is moe_grouped_gemm. */
+int moe_grouped_gemm_gather(int dtype, const void* a, const int32_t* a_gather, const void* b, void* c,
+                            const int32_t* offsets, int G, int max_rows, int N, int K, int trans_b,
+                            int epilogue, const float* bias, const void* aux, hipStream_t stream);
+/* moe_grouped_gemm_wgrad_rows with k-row r of Y read as y[y_gather[r]]
+ * (dW1 = dH^T Xp from the token rows); y_gather == NULL: contiguous. */
+int moe_grouped_gemm_wgrad_gather(int dtype, const void* x, const void* y, const int32_t* y_gather, void* c,
+                                  void* colsum, const int32_t* offsets, int G, int M, int N, int rows_hint,
+                                  int out_bf16, hipStream_t stream);
+/* a7: one backward step of an expert weight in ONE launch --
+ *   dgrad: C[r, n] = epi( sum_k A[r, k] B_g[k][n] )   (moe_grouped_gemm, trans_b = 0,
+ *          epilogue NONE / RELU_MASK / RELU_MASK_MX with aux)
+ *   wgrad: WC_g[m, n] = sum_r WX[r, m] WY[r, n], wcolsum_g[m] = sum_r WX[r, m]
+ *          (moe_grouped_gemm_wgrad_gather, WY optionally gathered)
+ * The two are independent (same offsets, M2 x N2 the weight's shape); sharing
+ * the launch fills the chip with both grids and removes a kernel boundary.
+ * bf16 operands; C bf16 [rows, N]; WC/wcolsum bf16 (out_bf16) or fp32. */
+int moe_grouped_gemm_bwd_pair(const void* a, const void* b, void* c, const int32_t* offsets, int G, int max_rows,
+                              int N, int K, int epilogue, const void* aux, const void* wx, const void* wy,
+                              const int32_t* wy_gather, void* wc, void* wcolsum, int M2, int N2, int out_bf16,
+                              hipStream_t stream);
 
 /* ---- MXFP8 expert path (config C5: 32-expert top-4 fp8 expert GEMMs) ----
  * Format: OCP e4m3 elements with one E8M0 exponent byte per 32 consecutive
@@ -309,6 +342,7 @@ int rtdetr_bn_act_bwd(const void* dy, const void* const* x, const float* const* 
  *   "gemm_debug"   0; 1 = skip C stores, 2 = skip the main loop (time attribution only)
  *   "xcd_map"      0 auto, 1 row tiles round-robin over XCDs, 2 contiguous chunk per XCD
  *   "ksplit"       0 auto, 1 no split-K, 2..8 forced split-K factor (needs the workspace below)
+ *   "gemm_pair"    1 (default) one launch per moe_grouped_gemm_bwd_pair, 0 two launches (A/B)
  * Returns 0, or -1 for an unknown key/value. */
 int moe_set_tuning(const char* key, int value);
 
@@ -425,7 +459,8 @@ enum moe_prof_kind {
   MOE_PROF_QUANT = 6,
   MOE_PROF_CONV_EPI = 7,
   MOE_PROF_OPTIM = 8,
-  MOE_PROF_MATCH = 9
+  MOE_PROF_MATCH = 9,
+  MOE_PROF_GEMM_FP8 = 10 /* grouped GEMM on the fp8 (MXFP8) MFMA: priced at the fp8 peak */
 };
 int moe_profile_enable(int on);
 int moe_profile_count(void);

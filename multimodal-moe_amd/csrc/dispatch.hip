@@ -49,6 +49,23 @@ __global__ __launch_bounds__(256) void permute_fwd_kernel(
   }
 }
 
+// Index half of the dispatch without moving rows: pos[t,j] and the inverse
+// map src_tok[pos] = t, which the grouped GEMMs use to gather the token rows
+// straight into their LDS tiles (no permuted copy in HBM).  One thread per
+// assignment (t, j).
+__global__ __launch_bounds__(256) void route_index_kernel(
+    const int32_t* __restrict__ topk_idx, const int32_t* __restrict__ local_rank,
+    const int32_t* __restrict__ rank_base, const int32_t* __restrict__ offsets, int T, int E, int k, int cap,
+    int32_t* __restrict__ pos, int32_t* __restrict__ src_tok, int32_t* __restrict__ prof_rows) {
+  const int a = blockIdx.x * 256 + threadIdx.x;
+  if (prof_rows != nullptr && a == 0) *prof_rows = offsets[E];
+  if (a >= T * k) return;
+  const int t = a / k, j = a - t * k;
+  const int pj = assignment_pos(topk_idx, local_rank, rank_base, offsets, t, j, E, k, cap);
+  pos[a] = pj;
+  if (pj >= 0) src_tok[pj] = t;
+}
+
 __global__ __launch_bounds__(256) void combine_fwd_kernel(
     const uint16_t* __restrict__ yp, const int32_t* __restrict__ pos,
     const float* __restrict__ topk_w, int T, int d, int k, uint16_t* __restrict__ y) {
@@ -156,6 +173,19 @@ extern "C" int moe_permute_fwd(const void* x, const int32_t* topk_idx,
                      static_cast<const uint16_t*>(x), topk_idx, local_rank, rank_base,
                      offsets, T, d, E, k, cap, static_cast<uint16_t*>(xp), pos, prof.rows_slot());
   return check_launch("moe_permute_fwd");
+}
+
+extern "C" int moe_route_index(const int32_t* topk_idx, const int32_t* local_rank, const int32_t* rank_base,
+                               const int32_t* offsets, int T, int E, int k, int cap, int32_t* pos,
+                               int32_t* src_tok, hipStream_t stream) {
+  if (E < 1 || E > 64 || k < 1 || k > 8) return fail("route_index: need 1<=E<=64, 1<=k<=8");
+  if (T <= 0) return 0;
+  // bytes: idx / local_rank / rank_base reads and pos writes per assignment, src_tok per kept row
+  ProfScope prof(stream, PROF_ROWMOVE, 16.0 * T * k, true, 4.0);
+  const long long A = (long long)T * k;
+  MOE_LAUNCH(prof, route_index_kernel, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, stream, topk_idx,
+             local_rank, rank_base, offsets, T, E, k, cap, pos, src_tok, prof.rows_slot());
+  return check_launch("moe_route_index");
 }
 
 extern "C" int moe_combine_fwd(const void* yp, const int32_t* pos, const float* topk_w,

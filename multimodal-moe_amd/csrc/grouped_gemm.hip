@@ -72,6 +72,12 @@ struct GemmParams {
   int c_bf16;  // WGRAD: C and colsum written as bf16 (RNE of the fp32 sums) instead of fp32
   float* ws;
   int32_t* cnt;
+  // row gathers (no permuted copy of the routed rows in HBM):
+  //   ROWS:  routed row r of A is a[a_gather[r]] (GEMM1 reads the token rows x[t]
+  //          straight into the LDS ring), variant 2 only;
+  //   WGRAD: k-row r of Y is y[b_gather[r]] (dW1 = dH^T Xp from the token rows), variant 1 only.
+  const int32_t* a_gather;
+  const int32_t* b_gather;
 };
 
 // runtime tuning knobs (moe_set_tuning)
@@ -83,6 +89,7 @@ static int g_rows_bm = 0;   // 0 = by tile count, else 64 or 128
 static int g_wgrad_bm = 0;  // 0 = by tile count, else 64 or 128
 static int g_xcd_map = 0;   // 0 = per-shape choice, 1 = round-robin, 2 = contiguous chunks
 static int g_ksplit = 0;    // 0 = per-shape choice, else forced split-K factor (1 = off)
+static int g_gemm_pair_off = 0;  // 1: moe_grouped_gemm_bwd_pair issues two launches (A/B)
 
 // split-K workspace registered per device by the caller (moe_set_splitk_workspace)
 struct SplitWs {
@@ -162,10 +169,12 @@ struct Tile {
   // The group of a row tile is found wave-parallel: each lane loads one
   // group's offsets (one memory round trip per 64 groups, not one per group),
   // an inclusive lane scan of the tile counts and a ballot pick the group.
-  __device__ __forceinline__ bool init(const GemmParams& p, int lane) {
+  __device__ __forceinline__ bool init(const GemmParams& p, int lane, int bid) {
     // split-K: the ksplit slices of one tile are consecutive slots of one XCD
-    const int xcd = blockIdx.x & 7;
-    int slot = blockIdx.x >> 3;
+    // (bid: the workgroup's index within its problem; a multiple-of-8 offset
+    // keeps bid & 7 == the XCD when two problems share a launch)
+    const int xcd = bid & 7;
+    int slot = bid >> 3;
     split = 0;
     nsplit = p.ksplit > 1 ? p.ksplit : 1;
     if (p.ksplit > 1) {
@@ -682,7 +691,25 @@ struct RegStage {
   static constexpr int kPer = R * 64 / 8 / 256;  // 16-B chunks per thread
   uint4 reg[kPer];
 
-  __device__ __forceinline__ void load(const uint16_t* base, int ld, int row_lim, int k_lim, int tid) {
+  // MN-contiguous tile with gathered k-rows: k-row kk of this thread's chunk i
+  // is row gi[i] of gbase (the indices were loaded a tile ahead: load_index).
+  __device__ __forceinline__ void load_index(const int32_t* gk, int k_lim, int tid, int (&gi)[kPer]) const {
+    static_assert(!KCONT, "gathered k-rows: MN-contiguous tiles");
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int kk = (tid + 256 * i) / (R / 8);
+      gi[i] = kk < k_lim ? gk[kk] : -1;
+    }
+  }
+  __device__ __forceinline__ void load_gathered(const uint16_t* gbase, int ld, const int (&gi)[kPer], int tid) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int r = ((tid + 256 * i) % (R / 8)) * 8;
+      reg[i] = gi[i] >= 0 ? *reinterpret_cast<const uint4*>(gbase + (size_t)gi[i] * ld + r) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void load(const uint16_t* base, int ld, int row_lim, int k_lim, int tid,
+                                       const int32_t* gk = nullptr, const uint16_t* gbase = nullptr) {
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int q = tid + 256 * i;
@@ -697,6 +724,9 @@ struct RegStage {
       }
       const bool ok = r < row_lim && kk < k_lim;
       const uint16_t* p = KCONT ? base + (size_t)r * ld + kk : base + (size_t)kk * ld + r;
+      if constexpr (!KCONT) {
+        if (gk != nullptr) p = gbase + (size_t)(ok ? gk[kk] : 0) * ld + r;
+      }
       reg[i] = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
     }
   }
@@ -744,16 +774,15 @@ struct RegStageY8 {
 };
 
 template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>
-__global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void gemm_v1_body(const GemmParams& p, int bid, char* smem) {
   constexpr int A_BYTES = BM * 64 * 2;
   constexpr int BUF = (BM + BN) * 64 * 2;
   constexpr int TM = BM / 32, TN = BN / 32;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  if (p.prof_rows != nullptr && blockIdx.x == 0 && tid == 0) *p.prof_rows = p.offsets[p.G];
+  if (p.prof_rows != nullptr && bid == 0 && tid == 0) *p.prof_rows = p.offsets[p.G];
   Tile<BM, BN, B_K, MODE> t;
-  if (!t.init(p, lane)) return;
+  if (!t.init(p, lane, bid)) return;
   float4 bpre[TN];
   prefetch_bias<BN, MODE, EPI>(p, t.g, t.n0, lane, wn, bpre);
 
@@ -779,10 +808,29 @@ __global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
   RegStage<BM, A_K> la;
   RegStage<BN, B_K> lb;
   RegStageY8 ly;
+  // WGRAD with b_gather: k-row r of Y is y[b_gather[row0 + r]] (columns from
+  // n0); the row indices of tile kt+1 are loaded while tile kt computes, so
+  // the data loads of a tile never wait on their index loads
+  constexpr bool BG = MODE == MODE_WGRAD && !B_K && !Y8;
+  const int32_t* bgk = (BG && p.b_gather != nullptr) ? p.b_gather + t.row0 : nullptr;
+  int gi[BG ? RegStage<BN, B_K>::kPer : 1];
+  auto load_index = [&](int kt) {
+    if constexpr (BG) {
+      if (bgk != nullptr && kt < t.nk) lb.load_index(bgk + kt * 64, k_lim(kt), tid, gi);
+    }
+  };
   auto load_b = [&](int kt) {
     if constexpr (Y8) ly.load(yq + (size_t)kt * 64 * p.N, ys + (size_t)kt * 64 * (p.N / 32), p.N, k_lim(kt), tid);
-    else lb.load(b_ptr(kt), p.ldb, BN, k_lim(kt), tid);
+    else if constexpr (BG) {
+      if (bgk != nullptr) {
+        lb.load_gathered(p.b + t.n0, p.ldb, gi, tid);
+        load_index(kt + 1);
+      } else {
+        lb.load(b_ptr(kt), p.ldb, BN, k_lim(kt), tid);
+      }
+    } else lb.load(b_ptr(kt), p.ldb, BN, k_lim(kt), tid);
   };
+  load_index(0);
   auto store_b = [&](char* dst) {
     if constexpr (Y8) ly.store(dst, tid);
     else lb.store(dst, tid);
@@ -812,6 +860,12 @@ __global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
   if (t.nsplit > 1 && !splitk_merge<TM, TN, COLSUM>(p, t.tile_id, t.split, acc, csum, tid)) return;
   epilogue<BM, BN, MODE, EPI, COLSUM>(p, t.g, t.row0,
                                       t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, lane, wm, wn);
+}
+
+template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>
+__global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  gemm_v1_body<BM, BN, A_K, B_K, MODE, EPI, COLSUM, FL>(p, blockIdx.x, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -847,14 +901,28 @@ __device__ __forceinline__ void dma_tile(const uint16_t* base, int ld, int row_l
   }
 }
 
+// The same for a K-contiguous A tile whose rows are gathered: rowp[j] is the
+// (clamped, gathered) row of wave-instruction j of this lane, sw[j] its chunk
+// swizzle; kofs the K-tile's element offset.
+template <int R>
+__device__ __forceinline__ void dma_tile_rows(const uint16_t* const (&rowp)[R / 32], const int (&sw)[R / 32],
+                                              int kofs, char* lds, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < R / 32; ++j) {
+    const int ins = wave + 4 * j;
+    const uint16_t* src = rowp[j] + kofs + sw[j] * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + ins * 1024), 16, 0, 0);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 template <int BM, int BN, int S, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>
-__global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void gemm_v2_body(const GemmParams& p, int bid, char* smem) {
   constexpr int A_BYTES = BM * 64 * 2;
   constexpr int BUF = (BM + BN) * 64 * 2;
   constexpr int TM = BM / 32, TN = BN / 32;
@@ -862,9 +930,9 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  if (p.prof_rows != nullptr && blockIdx.x == 0 && tid == 0) *p.prof_rows = p.offsets[p.G];
+  if (p.prof_rows != nullptr && bid == 0 && tid == 0) *p.prof_rows = p.offsets[p.G];
   Tile<BM, BN, B_K, MODE> t;
-  if (!t.init(p, lane)) return;
+  if (!t.init(p, lane, bid)) return;
   float4 bpre[TN];
   prefetch_bias<BN, MODE, EPI>(p, t.g, t.n0, lane, wn, bpre);
 
@@ -877,13 +945,37 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
 #pragma unroll
   for (int i = 0; i < TM; ++i) csum[i] = 0.f;
 
+  // ROWS with a_gather: this lane's source row of every A wave-instruction,
+  // found once (the rows are the same for every K-tile)
+  constexpr bool GATHER_OK = MODE == MODE_ROWS && A_K && !(FL & FL_MX);
+  const bool gather = GATHER_OK && p.a_gather != nullptr;
+  const uint16_t* rowp[BM / 32];
+  int sw[BM / 32];
+  if constexpr (GATHER_OK) {
+    if (gather) {
+      const int kofs0 = (int)(t.a_base - (p.a + (size_t)t.row0 * p.lda));  // split-K slice offset
+#pragma unroll
+      for (int j = 0; j < BM / 32; ++j) {
+        const int r = (wave + 4 * j) * 8 + (lane >> 3);
+        sw[j] = (lane & 7) ^ ((r >> 1) & 7);
+        const int rc = r < t.a_row_lim ? r : t.a_row_lim - 1;
+        rowp[j] = p.a + (size_t)p.a_gather[t.row0 + rc] * p.lda + kofs0;
+      }
+    }
+  }
+
   const int nk = (p.dbg & 2) ? 0 : t.nk;
   auto issue = [&](int kt) {
     char* buf = smem + (kt % S) * BUF;
     const int klim = MODE == MODE_ROWS ? 64 : t.rows_g - kt * 64;
     const uint16_t* ap = A_K ? t.a_base + kt * 64 : t.a_base + (size_t)kt * 64 * p.lda;
     const uint16_t* bp = B_K ? t.b_base + kt * 64 : t.b_base + (size_t)kt * 64 * p.ldb;
-    dma_tile<BM, A_K>(ap, p.lda, t.a_row_lim, klim, buf, wave, lane);
+    if constexpr (GATHER_OK) {
+      if (gather) dma_tile_rows<BM>(rowp, sw, kt * 64, buf, wave, lane);
+      else dma_tile<BM, A_K>(ap, p.lda, t.a_row_lim, klim, buf, wave, lane);
+    } else {
+      dma_tile<BM, A_K>(ap, p.lda, t.a_row_lim, klim, buf, wave, lane);
+    }
     dma_tile<BN, B_K>(bp, p.ldb, BN, klim, buf + A_BYTES, wave, lane);
   };
 
@@ -951,6 +1043,35 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
                                               tid, lane, wm, wn);
 }
 
+template <int BM, int BN, int S, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>
+__global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  gemm_v2_body<BM, BN, S, A_K, B_K, MODE, EPI, COLSUM, FL>(p, blockIdx.x, smem);
+}
+
+// Two independent grouped GEMMs in ONE launch (the backward's dgrad and wgrad
+// of the same weight: their grids fill the chip together and one kernel
+// boundary disappears): workgroups [0, n1) run problem 1, the rest problem 2.
+// n1 is a multiple of 8, so each problem keeps its XCD-aware tile map.
+template <class P1, class P2>
+__global__ __launch_bounds__(256) void gemm_pair_kernel(GemmParams p1, GemmParams p2, int n1) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if ((int)blockIdx.x < n1) P1::run(p1, blockIdx.x, smem);
+  else P2::run(p2, (int)blockIdx.x - n1, smem);
+}
+template <int BM, int BN, int S, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>
+struct BodyV2 {
+  static __device__ __forceinline__ void run(const GemmParams& p, int bid, char* smem) {
+    gemm_v2_body<BM, BN, S, A_K, B_K, MODE, EPI, COLSUM, FL>(p, bid, smem);
+  }
+};
+template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>
+struct BodyV1 {
+  static __device__ __forceinline__ void run(const GemmParams& p, int bid, char* smem) {
+    gemm_v1_body<BM, BN, A_K, B_K, MODE, EPI, COLSUM, FL>(p, bid, smem);
+  }
+};
+
 // ---------------------------------------------------------------------------
 // host launch helpers
 // ---------------------------------------------------------------------------
@@ -995,27 +1116,261 @@ static void launch(const GemmParams& p, dim3 grid, hipStream_t s, const ProfScop
   }
 }
 
-// Split-K factor for a launch of `tiles` output tiles (grid before splitting,
-// a multiple of 8) with `nk` K-tiles per tile, when the caller registered a
-// workspace large enough for `part_floats` per slice; 1 = no split.
-static int pick_split(int want, long long tiles, long long part_floats) {
-  if (want <= 1) return 1;
+// Split-K workspace window: the device's registered workspace, or what a
+// first problem of a paired launch left of it.
+struct WsWin {
+  float* ws = nullptr;
+  size_t bytes = 0;
+  int32_t* cnt = nullptr;
+  int n_cnt = 0;
+};
+static WsWin device_ws() {
+  WsWin w;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
-  const SplitWs& w = g_split_ws[dev];
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return w;
+  w.ws = g_split_ws[dev].ws;
+  w.bytes = g_split_ws[dev].ws_bytes;
+  w.cnt = g_split_ws[dev].cnt;
+  w.n_cnt = g_split_ws[dev].n_cnt;
+  return w;
+}
+
+// Split-K factor for a launch of `tiles` output tiles (grid before splitting,
+// a multiple of 8) when the window holds `part_floats` per slice; 1 = no split.
+static int pick_split(int want, long long tiles, long long part_floats, const WsWin& w) {
+  if (want <= 1) return 1;
   if (w.ws == nullptr || w.cnt == nullptr || tiles > w.n_cnt) return 1;
-  while (want > 1 && (size_t)tiles * want * part_floats * 4 > w.ws_bytes) --want;
+  while (want > 1 && (size_t)tiles * want * part_floats * 4 > w.bytes) --want;
   return want;
 }
 
-static void bind_split(GemmParams& p, int S) {
+// Bind the chosen split to p; returns the window left after this problem.
+static WsWin bind_split(GemmParams& p, int S, long long tiles, long long part_floats, const WsWin& w) {
   p.ksplit = S;
-  if (S > 1) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    p.ws = g_split_ws[dev].ws;
-    p.cnt = g_split_ws[dev].cnt;
+  if (S <= 1) return w;
+  p.ws = w.ws;
+  p.cnt = w.cnt;
+  WsWin rest = w;
+  const size_t used = (size_t)tiles * S * part_floats;
+  rest.ws = w.ws + used;
+  rest.bytes = w.bytes - used * 4;
+  rest.cnt = w.cnt + tiles;
+  rest.n_cnt = w.n_cnt - (int)tiles;
+  return rest;
+}
+
+// ---------------------------------------------------------------------------
+// launch plans: the per-shape choices of one grouped GEMM (kbench.py sweeps at
+// the C2 shapes, MI355X; profiles/r01/kbench_*.jsonl)
+// ---------------------------------------------------------------------------
+struct RowsPlan {
+  GemmParams p{};
+  long long grid = 0;  // workgroups (tiles x split)
+  int bm = 64, variant = 2, stages = 2, epi = 0;
+  bool trans_b = true;
+  double bytes_fixed = 0, bytes_row = 0, flops_row = 0;
+};
+struct WgradPlan {
+  GemmParams p{};
+  long long grid = 0;
+  int bm = 64, variant = 1, stages = 2;
+  bool colsum = false;
+  double bytes_fixed = 0, bytes_row = 0, flops_row = 0;
+};
+
+static int plan_rows(RowsPlan& pl, const void* a, const void* b, void* c, const int32_t* offsets, int G, int max_rows,
+                     int N, int K, int trans_b, int epilogue, const float* bias, const void* aux,
+                     const int32_t* a_gather, WsWin& win) {
+  if (G < 1 || G > 1024) return fail("grouped_gemm: G out of range");
+  if (N <= 0 || K <= 0 || N % 128 != 0 || K % 64 != 0) return fail("grouped_gemm: need N % 128 == 0 and K % 64 == 0");
+  if (max_rows < 0) return fail("grouped_gemm: max_rows < 0");
+  if ((epilogue == MOE_EPI_BIAS || epilogue == MOE_EPI_BIAS_RELU) && bias == nullptr)
+    return fail("grouped_gemm: bias epilogue without bias");
+  if ((epilogue == MOE_EPI_RELU_MASK || epilogue == MOE_EPI_RELU_MASK_MX) && aux == nullptr)
+    return fail("grouped_gemm: relu-mask epilogue without aux");
+  if (epilogue < 0 || epilogue > 4) return fail("grouped_gemm: bad epilogue");
+  GemmParams& p = pl.p;
+  p = GemmParams{};
+  p.dbg = g_gemm_debug;
+  p.a = static_cast<const uint16_t*>(a);
+  p.b = static_cast<const uint16_t*>(b);
+  p.c = c;
+  p.offsets = offsets;
+  p.bias = bias;
+  p.aux = static_cast<const uint16_t*>(aux);
+  p.a_gather = a_gather;
+  p.stride_b = (long long)N * K;
+  p.lda = K;
+  p.ldb = trans_b ? K : N;
+  p.ldc = N;
+  p.G = G;
+  p.N = N;
+  p.K = K;
+  pl.trans_b = trans_b != 0;
+  pl.epi = epilogue;
+  // 64-row tiles (two 48-64 KiB workgroups per CU, one's epilogue overlapping
+  // the other's main loop); LDS-DMA ring of 2 stages, 3 for K >= 1024 on grids
+  // under one tile per CU (the deeper ring covers the longer K loop)
+  const int nt = N / 128;
+  pl.bm = g_rows_bm ? g_rows_bm : 64;
+  const int mtiles = ((max_rows + pl.bm - 1) / pl.bm + G + 7) / 8 * 8;  // padded to the XCD count
+  const long long tiles = (long long)mtiles * nt;
+  // tile -> XCD map: contiguous row-tile chunks per XCD (each L2 then holds
+  // ~1 expert's weights) for the decoder-sized dgrads (kbench: dH 11.3 -> 9.1
+  // us, dX 15.0 -> 12.0); round-robin elsewhere (the encoder shapes prefer it)
+  p.xmap = g_xcd_map ? (g_xcd_map == 2 ? 1 : 0) : ((!trans_b && mtiles <= 128) ? 1 : 0);
+  // split-K when the grid leaves CUs idle and K is long, for the dgrads
+  // (MN-contiguous B; kbench: decoder dX 15.0 -> 11.5 us with the map above;
+  // the K-contiguous forward GEMM2 only loses to the merge latency)
+  int want = g_ksplit ? g_ksplit : ((!trans_b && tiles < 256 && K / 64 >= 16) ? 2 : 1);
+  if (want > K / 64) want = K / 64;
+  const long long part = 256LL * (pl.bm / 32) * (128 / 32) * 4;
+  const int S = pick_split(want, tiles, part, win);
+  win = bind_split(p, S, tiles, part, win);
+  pl.grid = tiles * S;
+  pl.variant = (g_gemm_variant && !a_gather) ? g_gemm_variant : 2;  // the row gather needs the LDS-DMA ring
+  pl.stages = g_gemm_stages ? g_gemm_stages : ((K >= 1024 && pl.grid < 256) ? 3 : 2);
+  // algorithmic bytes: weights + bias once; per routed row A (K), C (N) and the relu-mask operand (N)
+  const bool has_bias = epilogue == MOE_EPI_BIAS || epilogue == MOE_EPI_BIAS_RELU;
+  const double mask_bytes = epilogue == MOE_EPI_RELU_MASK ? 2.0 * N : (epilogue == MOE_EPI_RELU_MASK_MX ? 1.0 * N : 0.0);
+  pl.bytes_fixed = 2.0 * G * N * K + (has_bias ? 4.0 * G * N : 0.0);
+  pl.bytes_row = 2.0 * K + 2.0 * N + mask_bytes;
+  pl.flops_row = 2.0 * N * K;
+  return 0;
+}
+
+static int plan_wgrad(WgradPlan& pl, const void* x, const void* y, void* c, void* colsum, const int32_t* offsets,
+                      int G, int M, int N, int rows_hint, int out_bf16, const int32_t* b_gather, WsWin& win) {
+  if (G < 1 || G > 1024) return fail("grouped_gemm_wgrad: G out of range");
+  if (M <= 0 || N <= 0 || M % 64 != 0 || N % 128 != 0)
+    return fail("grouped_gemm_wgrad: need M % 64 == 0 and N % 128 == 0");
+  GemmParams& p = pl.p;
+  p = GemmParams{};
+  p.dbg = g_gemm_debug;
+  p.a = static_cast<const uint16_t*>(x);
+  p.b = static_cast<const uint16_t*>(y);
+  p.c = c;
+  p.offsets = offsets;
+  p.colsum = static_cast<float*>(colsum);
+  p.c_bf16 = out_bf16 ? 1 : 0;
+  p.b_gather = b_gather;
+  p.stride_c = (long long)M * N;
+  p.lda = M;
+  p.ldb = N;
+  p.ldc = N;
+  p.G = G;
+  p.M = M;
+  p.N = N;
+  p.K = 0;
+  pl.colsum = colsum != nullptr;
+  const int ntn = N / 128;
+  // 64-row tiles, register-staged double buffer (its global_load_dwordx4 path
+  // streams these k-row gathers faster than LDS-DMA)
+  const bool big = M % 128 == 0 && g_wgrad_bm == 128 && !b_gather;
+  pl.bm = big ? 128 : 64;
+  pl.variant = (g_gemm_variant && !b_gather) ? g_gemm_variant : 1;  // the k-row gather is in the register path
+  pl.stages = g_gemm_stages ? g_gemm_stages : 2;
+  int gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
+  // split-K over each group's rows: the output (G M N) is too small a grid to
+  // fill the chip with K = the whole group; only for long groups: rows_hint / G
+  // >= 1024 (kbench: encoder dW, 1,840 rows per expert, 30.0 -> 26.6 us;
+  // decoder groups of ~600 rows lose to the merge latency, 11.5 -> 15.5 us)
+  const long long tpg = (long long)(M / pl.bm) * ntn;
+  long long tiles = tpg * gpad;
+  const int want = g_ksplit ? g_ksplit : ((tiles <= 512 && rows_hint >= 1024LL * G) ? 2 : 1);
+  p.split_min_kt = 0;
+  if (want > 1 && tiles % 8 != 0) {  // split grids map 8-slot XCD rows: pad the group count
+    gpad = (G + 7) / 8 * 8;
+    tiles = tpg * gpad;
   }
+  const long long part = 256LL * (pl.bm / 32) * 4 * 4 + 256LL * (pl.bm / 32);
+  const int S = pick_split(want, tiles, part, win);
+  if (S == 1) {
+    gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
+    tiles = tpg * gpad;
+  }
+  win = bind_split(p, S, tiles, part, win);
+  pl.grid = tiles * S;
+  // algorithmic bytes: C (+ colsum) once; per routed row one row of X (M) and of Y (N)
+  const double osz = out_bf16 ? 2.0 : 4.0;
+  pl.bytes_fixed = osz * G * M * N + (colsum ? osz * G * M : 0.0);
+  pl.bytes_row = 2.0 * (M + N);
+  pl.flops_row = 2.0 * M * N;
+  return 0;
+}
+
+// kernel instantiation of a rows plan (callers check the plan's fields)
+template <int BM, int EPI, bool BK, int FL>
+static void launch_rows_bm(const RowsPlan& pl, hipStream_t s, const ProfScope& prof) {
+  launch<BM, 128, true, BK, MODE_ROWS, EPI, false, FL>(pl.p, dim3(pl.grid), s, prof, pl.variant, pl.stages);
+}
+template <int BM, bool BK>
+static void launch_rows_epi(const RowsPlan& pl, hipStream_t s, const ProfScope& prof) {
+  switch (pl.epi) {
+    case MOE_EPI_NONE: launch_rows_bm<BM, MOE_EPI_NONE, BK, 0>(pl, s, prof); break;
+    case MOE_EPI_BIAS: launch_rows_bm<BM, MOE_EPI_BIAS, BK, 0>(pl, s, prof); break;
+    case MOE_EPI_BIAS_RELU: launch_rows_bm<BM, MOE_EPI_BIAS_RELU, BK, 0>(pl, s, prof); break;
+    case MOE_EPI_RELU_MASK: launch_rows_bm<BM, MOE_EPI_RELU_MASK, BK, 0>(pl, s, prof); break;
+    default: launch_rows_bm<BM, MOE_EPI_RELU_MASK, BK, FL_AUX8>(pl, s, prof); break;
+  }
+}
+static void launch_rows(const RowsPlan& pl, hipStream_t s, const ProfScope& prof) {
+  if (pl.bm == 128) {
+    if (pl.trans_b) launch_rows_epi<128, true>(pl, s, prof);
+    else launch_rows_epi<128, false>(pl, s, prof);
+  } else {
+    if (pl.trans_b) launch_rows_epi<64, true>(pl, s, prof);
+    else launch_rows_epi<64, false>(pl, s, prof);
+  }
+}
+template <int FL>
+static void launch_wgrad(const WgradPlan& pl, hipStream_t s, const ProfScope& prof) {
+  if (pl.bm == 128) {
+    if (pl.colsum) launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true, FL>(pl.p, dim3(pl.grid), s, prof, pl.variant, pl.stages);
+    else launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false, FL>(pl.p, dim3(pl.grid), s, prof, pl.variant, pl.stages);
+  } else {
+    if (pl.colsum) launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true, FL>(pl.p, dim3(pl.grid), s, prof, pl.variant, pl.stages);
+    else launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false, FL>(pl.p, dim3(pl.grid), s, prof, pl.variant, pl.stages);
+  }
+}
+
+// Paired launch: a dgrad (ROWS, trans_b = 0, BM 64, ring of 2 or 3 stages)
+// and a weight gradient (WGRAD, BM 64, register-staged, colsum) of the same
+// expert weight.  Other plans fall back to two launches.
+// The weight gradient's workgroups come FIRST: they are few (one per output
+// tile) and each runs the group's whole K loop; dispatched ahead of the
+// dgrad's many short workgroups they overlap them instead of trailing them
+// (kbench: the reverse order ran the two back to back inside the launch).
+template <int S, int EPI, int FLR, int FLW>
+static void launch_pair_k(const RowsPlan& r, const WgradPlan& w, hipStream_t s, const ProfScope& prof) {
+  using R = BodyV2<64, 128, S, true, false, MODE_ROWS, EPI, false, FLR>;
+  using W = BodyV1<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true, FLW>;
+  constexpr auto fn = gemm_pair_kernel<W, R>;
+  const size_t lds_r = (size_t)S * (64 + 128) * 64 * 2;
+  const size_t lds_w = 2 * (64 + 128) * 64 * 2;
+  const size_t lds = lds_r > lds_w ? lds_r : lds_w;
+  allow_lds<fn>(lds);
+  MOE_LAUNCH(prof, fn, dim3(r.grid + w.grid), dim3(256), lds, s, w.p, r.p, (int)w.grid);
+}
+static bool pair_ok(const RowsPlan& r, const WgradPlan& w) {
+  return r.bm == 64 && !r.trans_b && r.variant == 2 && (r.stages == 2 || r.stages == 3) && w.grid % 8 == 0 &&
+         w.bm == 64 && w.variant == 1 && w.colsum &&
+         (r.epi == MOE_EPI_NONE || r.epi == MOE_EPI_RELU_MASK || r.epi == MOE_EPI_RELU_MASK_MX);
+}
+template <int FLW>
+static void launch_pair(const RowsPlan& r, const WgradPlan& w, hipStream_t s, const ProfScope& prof) {
+#define GG_PAIR(S_)                                                                     \
+  switch (r.epi) {                                                                       \
+    case MOE_EPI_NONE: launch_pair_k<S_, MOE_EPI_NONE, 0, FLW>(r, w, s, prof); break;    \
+    case MOE_EPI_RELU_MASK: launch_pair_k<S_, MOE_EPI_RELU_MASK, 0, FLW>(r, w, s, prof); break; \
+    default: launch_pair_k<S_, MOE_EPI_RELU_MASK, FL_AUX8, FLW>(r, w, s, prof); break;   \
+  }
+  if (r.stages == 3) {
+    GG_PAIR(3)
+  } else {
+    GG_PAIR(2)
+  }
+#undef GG_PAIR
 }
 
 }  // namespace moe
@@ -1045,7 +1400,22 @@ extern "C" int moe_set_tuning(const char* key, int value) {
   if (k == "wgrad_bm" && (value == 0 || value == 64 || value == 128)) { g_wgrad_bm = value; return 0; }
   if (k == "xcd_map" && value >= 0 && value <= 2) { g_xcd_map = value; return 0; }
   if (k == "ksplit" && value >= 0 && value <= 8) { g_ksplit = value; return 0; }
+  if (k == "gemm_pair" && value >= 0 && value <= 1) { g_gemm_pair_off = value ? 0 : 1; return 0; }
   return fail("moe_set_tuning: unknown key or value");
+}
+
+extern "C" int moe_grouped_gemm_gather(int dtype, const void* a, const int32_t* a_gather, const void* b, void* c,
+                                       const int32_t* offsets, int G, int max_rows, int N, int K, int trans_b,
+                                       int epilogue, const float* bias, const void* aux, hipStream_t stream) {
+  if (dtype != MOE_BF16) return fail("grouped_gemm: only MOE_BF16 is implemented");
+  RowsPlan pl;
+  WsWin win = device_ws();
+  if (plan_rows(pl, a, b, c, offsets, G, max_rows, N, K, trans_b, epilogue, bias, aux, a_gather, win)) return -1;
+  if (max_rows == 0) return 0;
+  ProfScope prof(stream, PROF_GEMM, pl.bytes_fixed, true, pl.bytes_row, pl.flops_row);
+  pl.p.prof_rows = prof.rows_slot();
+  launch_rows(pl, stream, prof);
+  return check_launch("moe_grouped_gemm");
 }
 
 extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c,
@@ -1053,84 +1423,8 @@ extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c
                                 int trans_b, int epilogue, const float* bias, const void* aux,
                                 const float* scales, hipStream_t stream) {
   (void)scales;
-  if (dtype != MOE_BF16) return fail("grouped_gemm: only MOE_BF16 is implemented");
-  if (G < 1 || G > 1024) return fail("grouped_gemm: G out of range");
-  if (N <= 0 || K <= 0 || N % 128 != 0 || K % 64 != 0)
-    return fail("grouped_gemm: need N % 128 == 0 and K % 64 == 0");
-  if (max_rows < 0) return fail("grouped_gemm: max_rows < 0");
-  if ((epilogue == MOE_EPI_BIAS || epilogue == MOE_EPI_BIAS_RELU) && bias == nullptr)
-    return fail("grouped_gemm: bias epilogue without bias");
-  if ((epilogue == MOE_EPI_RELU_MASK || epilogue == MOE_EPI_RELU_MASK_MX) && aux == nullptr)
-    return fail("grouped_gemm: relu-mask epilogue without aux");
-  if (epilogue < 0 || epilogue > 4) return fail("grouped_gemm: bad epilogue");
-  if (max_rows == 0) return 0;
-
-  GemmParams p{};
-  p.dbg = g_gemm_debug;
-  p.a = static_cast<const uint16_t*>(a);
-  p.b = static_cast<const uint16_t*>(b);
-  p.c = c;
-  p.offsets = offsets;
-  p.bias = bias;
-  p.aux = static_cast<const uint16_t*>(aux);
-  p.colsum = nullptr;
-  p.stride_b = (long long)N * K;
-  p.stride_c = 0;
-  p.lda = K;
-  p.ldb = trans_b ? K : N;
-  p.ldc = N;
-  p.G = G;
-  p.M = 0;
-  p.N = N;
-  p.K = K;
-
-  // Per-shape choice (kbench.py sweeps at the C2 shapes, MI355X): 64-row
-  // tiles (two 48-64 KiB workgroups per CU, one's epilogue overlapping the
-  // other's main loop); LDS-DMA ring of 2 stages, 3 for K >= 1024 on grids
-  // under one tile per CU (the deeper ring covers the longer K loop).
-  const int nt = N / 128;
-  const int BMsel = g_rows_bm ? g_rows_bm : 64;
-  const int mtiles = ((max_rows + BMsel - 1) / BMsel + G + 7) / 8 * 8;  // padded to the XCD count
-  const long long tiles = (long long)mtiles * nt;
-  // tile -> XCD map: contiguous row-tile chunks per XCD (each L2 then holds
-  // ~1 expert's weights) for the decoder-sized dgrads (kbench: dH 11.3 -> 9.1
-  // us, dX 15.0 -> 12.0); round-robin elsewhere (the encoder shapes prefer it)
-  p.xmap = g_xcd_map ? (g_xcd_map == 2 ? 1 : 0) : ((!trans_b && mtiles <= 128) ? 1 : 0);
-  // split-K when the grid leaves CUs idle and K is long, for the dgrads
-  // (MN-contiguous B; kbench: decoder dX 15.0 -> 11.5 us with the map below;
-  // the K-contiguous forward GEMM2 only loses to the merge latency)
-  int want = g_ksplit ? g_ksplit : ((!trans_b && tiles < 256 && K / 64 >= 16) ? 2 : 1);
-  if (want > K / 64) want = K / 64;
-  const int S = pick_split(want, tiles, 256LL * (BMsel / 32) * (128 / 32) * 4);
-  bind_split(p, S);
-  dim3 grid(tiles * S);
-  const int variant = g_gemm_variant ? g_gemm_variant : 2;
-  const int stages = g_gemm_stages ? g_gemm_stages : ((K >= 1024 && tiles * S < 256) ? 3 : 2);
-  // algorithmic bytes: weights + bias once; per routed row A (K), C (N) and the relu-mask operand (N)
-  const bool has_bias = epilogue == MOE_EPI_BIAS || epilogue == MOE_EPI_BIAS_RELU;
-  const double mask_bytes = epilogue == MOE_EPI_RELU_MASK ? 2.0 * N : (epilogue == MOE_EPI_RELU_MASK_MX ? 1.0 * N : 0.0);
-  ProfScope prof(stream, PROF_GEMM, 2.0 * G * N * K + (has_bias ? 4.0 * G * N : 0.0), true,
-                 2.0 * K + 2.0 * N + mask_bytes, 2.0 * N * K);
-  p.prof_rows = prof.rows_slot();
-
-#define GG_ROWS(BM, BK_, EPI, FL) \
-  launch<BM, 128, true, BK_, MODE_ROWS, EPI, false, FL>(p, grid, stream, prof, variant, stages)
-#define GG_EPI(BM, BK_)                                                           \
-  switch (epilogue) {                                                            \
-    case MOE_EPI_NONE: GG_ROWS(BM, BK_, MOE_EPI_NONE, 0); break;                  \
-    case MOE_EPI_BIAS: GG_ROWS(BM, BK_, MOE_EPI_BIAS, 0); break;                  \
-    case MOE_EPI_BIAS_RELU: GG_ROWS(BM, BK_, MOE_EPI_BIAS_RELU, 0); break;        \
-    case MOE_EPI_RELU_MASK: GG_ROWS(BM, BK_, MOE_EPI_RELU_MASK, 0); break;        \
-    default: GG_ROWS(BM, BK_, MOE_EPI_RELU_MASK, FL_AUX8); break;                 \
-  }
-  if (BMsel == 128) {
-    if (trans_b) { GG_EPI(128, true) } else { GG_EPI(128, false) }
-  } else {
-    if (trans_b) { GG_EPI(64, true) } else { GG_EPI(64, false) }
-  }
-#undef GG_EPI
-#undef GG_ROWS
-  return check_launch("moe_grouped_gemm");
+  return moe_grouped_gemm_gather(dtype, a, nullptr, b, c, offsets, G, max_rows, N, K, trans_b, epilogue, bias, aux,
+                                 stream);
 }
 
 extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, void* c,
@@ -1143,69 +1437,56 @@ extern "C" int moe_grouped_gemm_wgrad(int dtype, const void* x, const void* y, f
   return moe_grouped_gemm_wgrad_rows(dtype, x, y, c, colsum, offsets, G, M, N, 0, 0, stream);
 }
 
+extern "C" int moe_grouped_gemm_wgrad_gather(int dtype, const void* x, const void* y, const int32_t* y_gather,
+                                             void* c, void* colsum, const int32_t* offsets, int G, int M, int N,
+                                             int rows_hint, int out_bf16, hipStream_t stream) {
+  if (dtype != MOE_BF16) return fail("grouped_gemm_wgrad: only MOE_BF16 is implemented");
+  WgradPlan pl;
+  WsWin win = device_ws();
+  if (plan_wgrad(pl, x, y, c, colsum, offsets, G, M, N, rows_hint, out_bf16, y_gather, win)) return -1;
+  ProfScope prof(stream, PROF_GEMM, pl.bytes_fixed, true, pl.bytes_row, pl.flops_row);
+  pl.p.prof_rows = prof.rows_slot();
+  launch_wgrad<0>(pl, stream, prof);
+  return check_launch("moe_grouped_gemm_wgrad");
+}
+
 extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, void* c,
                                            void* colsum, const int32_t* offsets, int G, int M,
                                            int N, int rows_hint, int out_bf16, hipStream_t stream) {
-  if (dtype != MOE_BF16) return fail("grouped_gemm_wgrad: only MOE_BF16 is implemented");
-  if (G < 1 || G > 1024) return fail("grouped_gemm_wgrad: G out of range");
-  if (M <= 0 || N <= 0 || M % 64 != 0 || N % 128 != 0)
-    return fail("grouped_gemm_wgrad: need M % 64 == 0 and N % 128 == 0");
-  GemmParams p{};
-  p.dbg = g_gemm_debug;
-  p.a = static_cast<const uint16_t*>(x);
-  p.b = static_cast<const uint16_t*>(y);
-  p.c = c;
-  p.offsets = offsets;
-  p.colsum = static_cast<float*>(colsum);
-  p.c_bf16 = out_bf16 ? 1 : 0;
-  p.stride_c = (long long)M * N;
-  p.lda = M;
-  p.ldb = N;
-  p.ldc = N;
-  p.G = G;
-  p.M = M;
-  p.N = N;
-  p.K = 0;
-  const int ntn = N / 128;
-  // Per-shape choice (kbench.py): 64-row tiles, register-staged double buffer
-  // (its global_load_dwordx4 path streams these k-row gathers faster than LDS-DMA)
-  const bool big = M % 128 == 0 && g_wgrad_bm == 128;
-  const int variant = g_gemm_variant ? g_gemm_variant : 1;
-  const int stages = g_gemm_stages ? g_gemm_stages : 2;
-  int gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
-  const int bmw = big ? 128 : 64;
-  // split-K over each group's rows: the output (G M N) is too small a grid to
-  // fill the chip with K = the whole group
-  {
-    const long long tpg = (long long)(M / bmw) * ntn;
-    long long tiles = tpg * gpad;
-    // only for long groups: rows_hint / G >= 1024 (kbench: encoder dW, 1,840
-    // rows per expert, 30.0 -> 26.6 us; decoder groups of ~600 rows lose to
-    // the merge latency, 11.5 -> 15.5 us)
-    const int want = g_ksplit ? g_ksplit : ((tiles <= 512 && rows_hint >= 1024LL * G) ? 2 : 1);
-    p.split_min_kt = 0;
-    if (want > 1 && tiles % 8 != 0) {  // split grids map 8-slot XCD rows: pad the group count
-      gpad = (G + 7) / 8 * 8;
-      tiles = tpg * gpad;
+  return moe_grouped_gemm_wgrad_gather(dtype, x, y, nullptr, c, colsum, offsets, G, M, N, rows_hint, out_bf16,
+                                       stream);
+}
+
+extern "C" int moe_grouped_gemm_bwd_pair(const void* a, const void* b, void* c, const int32_t* offsets, int G,
+                                         int max_rows, int N, int K, int epilogue, const void* aux, const void* wx,
+                                         const void* wy, const int32_t* wy_gather, void* wc, void* wcolsum, int M2,
+                                         int N2, int out_bf16, hipStream_t stream) {
+  RowsPlan r;
+  WgradPlan w;
+  WsWin win = device_ws();
+  if (plan_rows(r, a, b, c, offsets, G, max_rows, N, K, 0, epilogue, nullptr, aux, nullptr, win)) return -1;
+  if (plan_wgrad(w, wx, wy, wc, wcolsum, offsets, G, M2, N2, max_rows, out_bf16, wy_gather, win)) return -1;
+  if (max_rows == 0) {  // no routed rows: the weight gradient is zero (the unpaired call writes it)
+    return moe_grouped_gemm_wgrad_gather(MOE_BF16, wx, wy, wy_gather, wc, wcolsum, offsets, G, M2, N2, 0, out_bf16,
+                                         stream);
+  }
+  if (g_gemm_pair_off || !pair_ok(r, w)) {  // two launches
+    {
+      ProfScope prof(stream, PROF_GEMM, r.bytes_fixed, true, r.bytes_row, r.flops_row);
+      r.p.prof_rows = prof.rows_slot();
+      launch_rows(r, stream, prof);
     }
-    const int S = pick_split(want, tiles, 256LL * (bmw / 32) * 4 * 4 + 256LL * (bmw / 32));
-    bind_split(p, S);
-    if (S == 1) gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
+    if (check_launch("moe_grouped_gemm_bwd_pair (dgrad)")) return -1;
+    ProfScope prof(stream, PROF_GEMM, w.bytes_fixed, true, w.bytes_row, w.flops_row);
+    w.p.prof_rows = prof.rows_slot();
+    launch_wgrad<0>(w, stream, prof);
+    return check_launch("moe_grouped_gemm_bwd_pair (wgrad)");
   }
-  // algorithmic bytes: fp32 C (+ colsum) once; per routed row one row of X (M) and of Y (N)
-  ProfScope prof(stream, PROF_GEMM, (out_bf16 ? 2.0 : 4.0) * G * M * N + (colsum ? (out_bf16 ? 2.0 : 4.0) * G * M : 0.0), true, 2.0 * (M + N),
-                 2.0 * M * N);
-  p.prof_rows = prof.rows_slot();
-  if (big) {
-    dim3 grid((M / 128) * ntn * gpad * p.ksplit);
-    if (colsum) launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream, prof, variant, stages);
-    else launch<128, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream, prof, variant, stages);
-  } else {
-    dim3 grid((M / 64) * ntn * gpad * p.ksplit);
-    if (colsum) launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true>(p, grid, stream, prof, variant, stages);
-    else launch<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, false>(p, grid, stream, prof, variant, stages);
-  }
-  return check_launch("moe_grouped_gemm_wgrad");
+  ProfScope prof(stream, PROF_GEMM, r.bytes_fixed + w.bytes_fixed, true, r.bytes_row + w.bytes_row,
+                 r.flops_row + w.flops_row);
+  r.p.prof_rows = prof.rows_slot();
+  launch_pair<0>(r, w, stream, prof);
+  return check_launch("moe_grouped_gemm_bwd_pair");
 }
 
 // ---------------------------------------------------------------------------

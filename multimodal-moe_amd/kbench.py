@@ -23,19 +23,23 @@ from src.moe import _lib as L  # noqa: E402
 
 
 def timed(fn, reps):
-    """Median kernel execution time (us) of `fn`'s launch over `reps` calls,
-    from the dispatch-stamped event pairs of libmoe_hip's profiler
-    (hipExtLaunchKernel): no host overhead or inter-launch gaps included."""
+    """Median kernel execution time (us) of `fn` over `reps` calls (the sum of
+    its launches when it makes several), from the dispatch-stamped event pairs
+    of libmoe_hip's profiler (hipExtLaunchKernel): no host overhead or
+    inter-launch gaps included."""
     fn()
     torch.cuda.synchronize()
     L.lib().moe_profile_enable(1)
     try:
+        fn()
+        per = max(1, len(L.profile_records()))
         for _ in range(reps):
             fn()
         recs = L.profile_records()
     finally:
         L.lib().moe_profile_enable(0)
-    return 1e3 * statistics.median(r[1] for r in recs)
+    ms = [r[1] for r in recs]
+    return 1e3 * statistics.median(sum(ms[i:i + per]) for i in range(0, len(ms) - per + 1, per))
 
 
 def setup(T, E, k, d, F, seed=0):
@@ -53,6 +57,7 @@ def setup(T, E, k, d, F, seed=0):
     rank_base, hist, offsets = L.route_scan(bcnt, 0)
     rows = T * k
     xp, pos = L.permute_fwd(x, idx, lrank, rank_base, offsets, E, 0, rows)
+    _, tok = L.route_index(idx, lrank, rank_base, offsets, E, 0, rows)
     h = L.grouped_gemm(xp, w1, offsets, E, rows, F, d, 1, L.EPI_BIAS_RELU, bias=b1)
     yp = L.grouped_gemm(h, w2, offsets, E, rows, d, F, 1, L.EPI_BIAS, bias=b2)
     dy = torch.randn((T, d), device="cuda", generator=g).to(torch.bfloat16)
@@ -66,7 +71,7 @@ def setup(T, E, k, d, F, seed=0):
     hq, hs = L.grouped_gemm_mx(xq, xs, w1q, w1s, offsets, E, rows, F, d, L.EPI_BIAS_RELU, bias=b1, out_mx=True)
     return dict(T=T, E=E, k=k, d=d, F=F, x=x, wg=wg, cb=cb, ci=ci, tpi=tpi, w1=w1, w2=w2, b1=b1, b2=b2, idx=idx,
                 w=w, probs=probs, lse=lse, lrank=lrank, bcnt=bcnt, rank_base=rank_base, offsets=offsets, rows=rows,
-                xp=xp, pos=pos, h=h, yp=yp, dy=dy, dyp=dyp, dw=dw, dh=dh, dxp=dxp,
+                xp=xp, pos=pos, tok=tok, h=h, yp=yp, dy=dy, dyp=dyp, dw=dw, dh=dh, dxp=dxp,
                 xq=xq, xs=xs, w1q=w1q, w1s=w1s, w2q=w2q, w2s=w2s, hq=hq, hs=hs)
 
 
@@ -83,6 +88,14 @@ def kernels(c):
                                              bias=c["b1"]), 2.0 * A * F * d, 0),
         ("gemm2_fwd", lambda: L.grouped_gemm(c["h"], c["w2"], c["offsets"], E, rows, d, F, 1, L.EPI_BIAS,
                                              bias=c["b2"]), 2.0 * A * F * d, 0),
+        ("route_index", lambda: L.route_index(c["idx"], c["lrank"], c["rank_base"], c["offsets"], E, 0, rows), 0,
+         16 * A + 4 * A),
+        ("gemm1_fwd_gather", lambda: L.grouped_gemm_gather(c["x"], c["tok"], c["w1"], c["offsets"], E, rows, F, d, 1,
+                                                           L.EPI_BIAS_RELU, bias=c["b1"]), 2.0 * A * F * d, 0),
+        ("gemm_pair2", lambda: L.grouped_gemm_bwd_pair(c["dyp"], c["w2"], c["offsets"], E, rows, F, d, L.EPI_RELU_MASK,
+                                                       c["h"], c["dyp"], c["h"]), 4.0 * A * F * d, 0),
+        ("gemm_pair1", lambda: L.grouped_gemm_bwd_pair(c["dh"], c["w1"], c["offsets"], E, rows, d, F, L.EPI_NONE,
+                                                       None, c["dh"], c["x"], c["tok"]), 4.0 * A * F * d, 0),
         ("combine", lambda: L.combine_fwd(c["yp"], c["pos"], c["w"], T), 0, 512 * (A + T) + 8 * A),
         ("combine_bwd", lambda: L.combine_bwd(c["dy"], c["yp"], c["pos"], c["w"]), 0, 512 * (T + 2 * A) + 12 * A),
         ("gemm_dgrad2", lambda: L.grouped_gemm(c["dyp"], c["w2"], c["offsets"], E, rows, F, d, 0, L.EPI_RELU_MASK,
@@ -123,11 +136,13 @@ def main():
     ap.add_argument("--bm", default="0", help="comma list of forced row-tile heights (0 = auto) for rows and wgrad")
     ap.add_argument("--xcd", default="0", help="comma list of ROWS tile->XCD maps (0 auto, 1 round-robin, 2 contiguous)")
     ap.add_argument("--ksplit", default="0", help="comma list of split-K factors (0 auto, 1 off, 2..8 forced)")
+    ap.add_argument("--pair", default="1", help="comma list of gemm_pair modes (1 one launch, 0 two launches)")
     a = ap.parse_args()
     L.lib()
-    configs = [(v, s, dbg, bm, xm, ks) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
+    configs = [(v, s, dbg, bm, xm, ks, pr) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
                for dbg in map(int, a.debug.split(",")) for bm in map(int, a.bm.split(","))
                for xm in map(int, a.xcd.split(",")) for ks in map(int, a.ksplit.split(","))
+               for pr in map(int, a.pair.split(","))
                if not (v == 1 and s != int(a.stages.split(",")[0]))]
     if a.config == "c5":  # 32 experts, top-4, bs 16 (no capacity drops here: cf only trims the tail)
         shapes = {"enc": setup(16 * 920, 32, 4, 256, 1024), "dec": setup(16 * 300, 32, 4, 256, 1024, seed=1)}
@@ -135,7 +150,8 @@ def main():
         shapes = {"enc": setup(8 * 920, 8, 2, 256, 1024), "dec": setup(8 * 300, 8, 2, 256, 1024, seed=1)}
     res = {}
     for _ in range(a.rounds):
-        for (v, s, dbg, bm, xm, ks) in configs:
+        for (v, s, dbg, bm, xm, ks, pr) in configs:
+            L.set_tuning("gemm_pair", pr)
             L.set_tuning("ksplit", ks)
             L.set_tuning("xcd_map", xm)
             L.set_tuning("rows_bm", bm)
@@ -147,18 +163,21 @@ def main():
                 for name, fn, flops, byts in kernels(c):
                     if a.only and a.only not in name:
                         continue
-                    if not name.startswith("gemm") and (v, s, dbg, bm, xm, ks) != configs[0]:
+                    if not name.startswith("gemm") and (v, s, dbg, bm, xm, ks, pr) != configs[0]:
                         continue
-                    res.setdefault((name, sname, v, s, dbg, bm, xm, ks, flops, byts), []).append(timed(fn, a.reps))
+                    if pr != 1 and "pair" not in name:
+                        continue
+                    res.setdefault((name, sname, v, s, dbg, bm, xm, ks, pr, flops, byts), []).append(timed(fn, a.reps))
     L.set_tuning("ksplit", 0)
+    L.set_tuning("gemm_pair", 1)
     L.set_tuning("gemm_debug", 0)
     L.set_tuning("rows_bm", 0)
     L.set_tuning("wgrad_bm", 0)
     L.set_tuning("xcd_map", 0)
-    for (name, sname, v, s, dbg, bm, xm, ks, flops, byts), ts in res.items():
+    for (name, sname, v, s, dbg, bm, xm, ks, pr, flops, byts), ts in res.items():
         us = statistics.median(ts)
         d = {"kernel": name, "config": a.config, "shape": sname, "variant": v, "stages": s, "debug": dbg, "bm": bm,
-             "xcd": xm, "ksplit": ks, "us": round(us, 2),
+             "xcd": xm, "ksplit": ks, "pair": pr, "us": round(us, 2),
              "min_us": round(min(ts), 2)}
         if flops:
             d["tflops"] = round(flops / us / 1e6, 1)

@@ -37,6 +37,10 @@ SIGNATURES = {
     "moe_grouped_gemm": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_wgrad": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "moe_grouped_gemm_wgrad_rows": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "moe_route_index": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "moe_grouped_gemm_gather": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "moe_grouped_gemm_wgrad_gather": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "moe_grouped_gemm_bwd_pair": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "moe_quantize_mx": (_I, [_P, ctypes.c_longlong, _I, _P, _P, _P]),
     "moe_permute_fwd_mx": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_mx": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
@@ -364,6 +368,60 @@ def grouped_gemm(a, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None,
         int(epilogue), _ptr(bias), _ptr(aux), None, _stream())
     _check(rc, "moe_grouped_gemm")
     return c
+
+
+def route_index(topk_idx, local_rank, rank_base, offsets, E, cap, rows_alloc):
+    """-> (pos int32 [T, k], src_tok int32 [max(rows_alloc, 1)]): the dispatch's
+    index half; the GEMMs gather token rows through src_tok (moe_route_index)."""
+    T, k = topk_idx.shape
+    dev = topk_idx.device
+    pos = torch.empty((T, k), dtype=torch.int32, device=dev)
+    tok = torch.empty((max(rows_alloc, 1),), dtype=torch.int32, device=dev)
+    _check(lib().moe_route_index(_ptr(topk_idx), _ptr(local_rank), _ptr(rank_base), _ptr(offsets), T, E, k,
+                                 int(cap), _ptr(pos), _ptr(tok), _stream()), "moe_route_index")
+    return pos, tok
+
+
+def grouped_gemm_gather(x, src_tok, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None, aux=None):
+    """grouped_gemm with routed row r of A = x[src_tok[r]] (x: bf16 token rows [T, K])."""
+    _need(x, torch.bfloat16, "x")
+    _need(b, torch.bfloat16, "b")
+    _need(src_tok, torch.int32, "src_tok")
+    if b.numel() != G * N * K or x.shape[1] != K or src_tok.numel() < max_rows:
+        raise MoEKernelError("grouped_gemm_gather: shapes")
+    c = torch.empty((max(max_rows, 1), N), dtype=torch.bfloat16, device=x.device)
+    ensure_splitk_workspace(x.device)
+    _check(lib().moe_grouped_gemm_gather(MOE_BF16, _ptr(x), _ptr(src_tok), _ptr(b), _ptr(c), _ptr(offsets), G,
+                                         int(max_rows), N, K, int(trans_b), int(epilogue), _ptr(bias), _ptr(aux),
+                                         _stream()), "moe_grouped_gemm_gather")
+    return c
+
+
+def grouped_gemm_bwd_pair(a, b, offsets, G, max_rows, N, K, epilogue, aux, wx, wy, wy_gather=None,
+                          out_dtype=torch.bfloat16):
+    """One launch: C = epi(A . B_g) (dgrad, B stored [K][N] per group) and the
+    weight gradient WC_g = WX_g^T WY_g with colsum (WY rows gathered through
+    wy_gather when given).  -> (C bf16 [rows, N], WC [G, M2, N2], colsum [G, M2])."""
+    _need(a, torch.bfloat16, "a")
+    _need(b, torch.bfloat16, "b")
+    _need(wx, torch.bfloat16, "wx")
+    _need(wy, torch.bfloat16, "wy")
+    if aux is not None:
+        _need(aux, torch.uint8 if epilogue == EPI_RELU_MASK_MX else torch.bfloat16, "aux")
+    if b.numel() != G * N * K or a.shape[1] != K or a.shape[0] < max_rows:
+        raise MoEKernelError("grouped_gemm_bwd_pair: dgrad shapes")
+    M2, N2 = wx.shape[1], wy.shape[1]
+    if wy_gather is None and wy.shape[0] < max_rows:
+        raise MoEKernelError("grouped_gemm_bwd_pair: wgrad shapes")
+    c = torch.empty((a.shape[0], N), dtype=torch.bfloat16, device=a.device)
+    wc = torch.empty((G, M2, N2), dtype=out_dtype, device=a.device)
+    cs = torch.empty((G, M2), dtype=out_dtype, device=a.device)
+    ensure_splitk_workspace(a.device)
+    _check(lib().moe_grouped_gemm_bwd_pair(_ptr(a), _ptr(b), _ptr(c), _ptr(offsets), G, int(max_rows), N, K,
+                                           int(epilogue), _ptr(aux), _ptr(wx), _ptr(wy), _ptr(wy_gather), _ptr(wc),
+                                           _ptr(cs), M2, N2, int(out_dtype == torch.bfloat16), _stream()),
+           "moe_grouped_gemm_bwd_pair")
+    return c, wc, cs
 
 
 def aux_loss_fwd(auxp, hist, T, k, lb_coef, z_coef):

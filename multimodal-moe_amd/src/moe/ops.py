@@ -1,14 +1,20 @@
 """autograd wrappers of the HIP MoE FFN.
 
 One layer = three autograd Functions over the C-ABI kernels:
-  _RouteDispatch  router + top-k + aux partials (K1), route_scan, permute (K2)
+  _RouteIndex     router + top-k + aux partials (K1), route_scan, route_index
+                  (K2's index half: pos and the row -> token map; the routed
+                  rows are never copied)
                   backward: token_bwd (dispatch transpose + router backward)
-  _ExpertFFN      grouped GEMM1 (+b1, ReLU) and GEMM2 (+b2)
-                  backward: dgrad GEMM (ReLU mask), wgrad (+db2), dgrad, wgrad (+db1)
+  _ExpertFFNGather grouped GEMM1 (+b1, ReLU) reading the token rows through
+                  the row map, GEMM2 (+b2)
+                  backward: two paired launches (moe_grouped_gemm_bwd_pair):
+                  {dH = dgrad (ReLU mask), dW2 + db2} and {dXp = dgrad, dW1 + db1
+                  with the token rows gathered}
   _Combine        gate-weighted combine (K3); backward: combine_bwd
-Single GPU: 6 launches forward, 6 (+1 torch GEMM for dWg) backward.  The
-expert-parallel path (ep.py) runs the same Functions with an all-to-all
-before and after _ExpertFFN.  Nothing is synchronised with the host: expert
+Single GPU: 6 launches forward (router, scan, index, GEMM1, GEMM2, combine),
+4 backward (combine_bwd, 2 pairs, token_bwd) + 1 torch GEMM for dWg.  The
+expert-parallel path (ep.py) moves real rows through its all-to-alls and runs
+_RouteDispatch (permute) + _ExpertFFN (rows in, same paired backward).  Nothing is synchronised with the host: expert
 offsets stay on the device, grids are sized from host upper bounds, and the
 aux-loss gradients reach the router kernel as device tensors.
 
@@ -101,6 +107,79 @@ class _RouteDispatchMX(torch.autograd.Function):
         return _RouteDispatch.backward(ctx, d_xp, d_w, d_auxp, _p, _h, _o)
 
 
+class _RouteIndex(torch.autograd.Function):
+    """_RouteDispatch without the row copy: the dispatch writes pos and the row
+    -> token map ``tok`` (moe_route_index); a zero-stride bf16 ``carrier``
+    [rows, d] stands for the routed rows in the autograd graph so that dXp
+    (from _ExpertFFNGather.backward) reaches the dispatch transpose."""
+
+    @staticmethod
+    def forward(ctx, x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, rows):
+        T, d = x.shape
+        E = wg.shape[0]
+        xb = x.to(torch.bfloat16).contiguous()
+        wg32 = wg.float().contiguous()
+        cb = ctx_bias.float().contiguous() if ctx_bias is not None else None
+        idx, w, probs, lse, lrank, bcnt, auxp = L.router_topk_fwd(xb, wg32, cb, ctx_img, tokens_per_image, k,
+                                                                   normalize)
+        rank_base, hist, offsets = L.route_scan(bcnt, cap)
+        pos, tok = L.route_index(idx, lrank, rank_base, offsets, E, cap, rows)
+        carrier = torch.zeros((1, 1), dtype=torch.bfloat16, device=x.device).expand(max(rows, 1), d)
+        ctx.save_for_backward(xb, wg32, idx, w, probs, lse, pos,
+                              ctx_img if ctx_img is not None else torch.empty(0))
+        ctx.meta = (T, d, E, int(normalize), tokens_per_image, cb is not None, x.dtype,
+                    ctx_bias.shape[0] if ctx_bias is not None else 0)
+        ctx.mark_non_differentiable(pos, hist, offsets, tok)
+        return carrier, w, auxp, pos, hist, offsets, tok
+
+    @staticmethod
+    def backward(ctx, d_xp, d_w, d_auxp, _p, _h, _o, _t):
+        return _RouteDispatch.backward(ctx, d_xp, d_w, d_auxp, _p, _h, _o)
+
+
+def _ffn_backward(dyp, h, w1b, w2b, offsets, G, rows, xrows, tok, wdtype, s):
+    """The expert FFN's backward in two paired launches:
+    {dH = (dYp W2) * (H > 0), dW2 = dYp^T H, db2} then {dXp = dH W1, dW1 = dH^T Xp, db1},
+    Xp = xrows (the routed rows) or xrows[tok] (token rows gathered)."""
+    F, d = w1b.shape[1], w1b.shape[2]
+    odt = torch.bfloat16 if wdtype == torch.bfloat16 else torch.float32
+    dh, dW2, db2 = L.grouped_gemm_bwd_pair(dyp, w2b, offsets, G, rows, F, d, L.EPI_RELU_MASK, h, dyp, h,
+                                           out_dtype=odt)
+    dxp, dW1, db1 = L.grouped_gemm_bwd_pair(dh, w1b, offsets, G, rows, d, F, L.EPI_NONE, None, dh, xrows, tok,
+                                            out_dtype=odt)
+    if s != 1.0:
+        for t in (dW1, db1, dW2, db2):
+            t.mul_(s)
+    return dxp, dW1, db1, dW2, db2
+
+
+class _ExpertFFNGather(torch.autograd.Function):
+    """Expert FFN whose GEMM1 reads routed row r as token row xb[tok[r]]
+    (moe_grouped_gemm_gather); ``carrier`` is _RouteIndex's stand-in for the
+    routed rows (its gradient is dXp)."""
+
+    @staticmethod
+    def forward(ctx, carrier, xb, tok, w1, b1, w2, b2, offsets, rows, grad_scale):
+        G, F, d = w1.shape
+        w1b = w1.to(torch.bfloat16).contiguous()
+        w2b = w2.to(torch.bfloat16).contiguous()
+        h = L.grouped_gemm_gather(xb, tok, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU,
+                                  bias=b1.float().contiguous())
+        yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=b2.float().contiguous())
+        ctx.save_for_backward(xb, tok, h, w1b, w2b, offsets)
+        ctx.meta = (G, rows, float(grad_scale))
+        ctx.wdtype = w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32
+        return yp
+
+    @staticmethod
+    def backward(ctx, d_yp):
+        xb, tok, h, w1b, w2b, offsets = ctx.saved_tensors
+        G, rows, s = ctx.meta
+        dyp = d_yp.to(torch.bfloat16).contiguous()
+        dxp, dW1, db1, dW2, db2 = _ffn_backward(dyp, h, w1b, w2b, offsets, G, rows, xb, tok, ctx.wdtype, s)
+        return dxp, None, None, dW1, db1, dW2, db2, None, None, None
+
+
 class _ExpertFFN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xp, w1, b1, w2, b2, offsets, rows, grad_scale):
@@ -119,16 +198,9 @@ class _ExpertFFN(torch.autograd.Function):
         xp, h, w1b, w2b, offsets = ctx.saved_tensors
         G, F, d, rows, s = ctx.meta
         dyp = d_yp.to(torch.bfloat16).contiguous()
-        dh = L.grouped_gemm(dyp, w2b, offsets, G, rows, F, d, 0, L.EPI_RELU_MASK, aux=h)
         # weight gradients written in the parameters' dtype by the kernel (bf16
         # weights: no fp32 copy + autograd cast pass)
-        odt = torch.bfloat16 if ctx.wdtype == torch.bfloat16 else torch.float32
-        dW2, db2 = L.grouped_gemm_wgrad(dyp, h, offsets, G, out_dtype=odt)
-        dxp = L.grouped_gemm(dh, w1b, offsets, G, rows, d, F, 0, L.EPI_NONE)
-        dW1, db1 = L.grouped_gemm_wgrad(dh, xp, offsets, G, out_dtype=odt)
-        if s != 1.0:
-            for t in (dW1, db1, dW2, db2):
-                t.mul_(s)
+        dxp, dW1, db1, dW2, db2 = _ffn_backward(dyp, h, w1b, w2b, offsets, G, rows, xp, None, ctx.wdtype, s)
         return dxp, dW1, db1, dW2, db2, None, None, None
 
 
@@ -232,6 +304,19 @@ def route_dispatch_mx_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normali
                                   int(cap), rows) + (rows,)
 
 
+def route_index_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap):
+    """-> (carrier, w, auxp, pos, hist, offsets, tok, rows): dispatch without the row copy."""
+    T = x.shape[0]
+    E = wg.shape[0]
+    rows = T * k if cap <= 0 else min(T * k, E * cap)
+    return _RouteIndex.apply(x, wg, ctx_bias, ctx_img, int(tokens_per_image), int(k), bool(normalize), int(cap),
+                             rows) + (rows,)
+
+
+def expert_ffn_gather_hip(carrier, xb, tok, w1, b1, w2, b2, offsets, rows, grad_scale=1.0):
+    return _ExpertFFNGather.apply(carrier, xb, tok, w1, b1, w2, b2, offsets, int(rows), grad_scale)
+
+
 def expert_ffn_hip(xp, w1, b1, w2, b2, offsets, rows, grad_scale=1.0):
     return _ExpertFFN.apply(xp, w1, b1, w2, b2, offsets, int(rows), grad_scale)
 
@@ -268,9 +353,10 @@ def moe_ffn_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, n
             x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap)
         yp = expert_ffn_mx_hip(carrier, xq, xs, w1, b1, w2, b2, offsets, rows)
     else:
-        xp, w, auxp, pos, hist, offsets, rows = route_dispatch_hip(x, wg, ctx_bias, ctx_img, tokens_per_image,
-                                                                   k, normalize, cap)
-        yp = expert_ffn_hip(xp, w1, b1, w2, b2, offsets, rows)
+        carrier, w, auxp, pos, hist, offsets, tok, rows = route_index_hip(x, wg, ctx_bias, ctx_img, tokens_per_image,
+                                                                          k, normalize, cap)
+        xb = x.detach().to(torch.bfloat16).contiguous()
+        yp = expert_ffn_gather_hip(carrier, xb, tok, w1, b1, w2, b2, offsets, rows)
     y = combine_hip(yp, w, pos, T)
     if aux_coefs is not None:
         aux, raw = aux_loss_weighted(auxp, hist, T, k, *aux_coefs)

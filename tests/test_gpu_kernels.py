@@ -350,3 +350,97 @@ def test_fused_aux_loss_matches_torch(hip_lib):
     torch.testing.assert_close(aux, ref, rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(raw, torch.stack([lb, z]).detach(), rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(ga, 3.0 * ga_ref, rtol=1e-5, atol=1e-9)
+
+
+# ---------------------------------------------------------------------------
+# round 2: row gathers (no permuted copy) and paired backward launches
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("rows_per_group", [[0, 1, 63, 64, 65, 200, 0, 130], [1000, 24, 0, 500]])
+@pytest.mark.parametrize("ksplit", [0, 1, 2])
+def test_grouped_gemm_gather_exact(hip_lib, rows_per_group, ksplit):
+    """GEMM1 reading routed row r as token row x[tok[r]] == the GEMM on the
+    permuted copy, bit for bit (integer data)."""
+    from src.moe import _lib as L
+
+    rng = np.random.default_rng(17)
+    G, N, K = len(rows_per_group), 1024, 256
+    offsets = np.concatenate([[0], np.cumsum(rows_per_group)]).astype(np.int32)
+    R = int(offsets[-1])
+    T = max(R // 2, 1) + 7
+    X = _int_tensor(rng, (T, K))
+    tok = rng.integers(0, T, size=R + 5).astype(np.int32)
+    Bw = _int_tensor(rng, (G, N, K))
+    bias = _int_tensor(rng, (G, N))
+    Xt = torch.from_numpy(X).to(torch.bfloat16).to(DEV)
+    tok_t = torch.from_numpy(tok).to(DEV)
+    Bt = torch.from_numpy(Bw).to(torch.bfloat16).to(DEV)
+    off_t = torch.from_numpy(offsets).to(DEV)
+    bias_t = torch.from_numpy(bias).float().to(DEV)
+    L.set_tuning("ksplit", ksplit)
+    try:
+        got = L.grouped_gemm_gather(Xt, tok_t, Bt, off_t, G, R + 5, N, K, 1, L.EPI_BIAS_RELU, bias=bias_t)
+        ref = L.grouped_gemm(Xt[tok_t.long()].contiguous(), Bt, off_t, G, R + 5, N, K, 1, L.EPI_BIAS_RELU,
+                             bias=bias_t)
+        torch.cuda.synchronize()
+    finally:
+        L.set_tuning("ksplit", 0)
+    assert torch.equal(got[:R], ref[:R])
+
+
+@pytest.mark.parametrize("rows_per_group", [[0, 1, 63, 64, 65, 200, 0, 130], [1500, 40, 0, 1100]])
+@pytest.mark.parametrize("epi", ["mask", "none"])
+@pytest.mark.parametrize("pair", [1, 0])
+def test_grouped_gemm_bwd_pair_exact(hip_lib, rows_per_group, epi, pair):
+    """moe_grouped_gemm_bwd_pair (one launch, or two with gemm_pair=0) ==
+    the separate dgrad and wgrad launches, bit for bit, including the wgrad
+    operand gathered through a row map and split-K in both halves."""
+    from src.moe import _lib as L
+
+    rng = np.random.default_rng(23)
+    G = len(rows_per_group)
+    offsets = np.concatenate([[0], np.cumsum(rows_per_group)]).astype(np.int32)
+    R = int(offsets[-1])
+    N, K = (1024, 256) if epi == "mask" else (256, 1024)  # dH = dYp W2 (mask) / dXp = dH W1
+    A = torch.from_numpy(_int_tensor(rng, (R + 3, K))).to(torch.bfloat16).to(DEV)
+    Bw = torch.from_numpy(_int_tensor(rng, (G, K, N))).to(torch.bfloat16).to(DEV)
+    aux = torch.from_numpy(_int_tensor(rng, (R + 3, N))).to(torch.bfloat16).to(DEV) if epi == "mask" else None
+    Tt = max(R, 1) + 11
+    Y = torch.from_numpy(_int_tensor(rng, (Tt, 256 if epi == "none" else N), -2, 3)).to(torch.bfloat16).to(DEV)
+    tok = torch.from_numpy(rng.integers(0, Tt, size=R + 3).astype(np.int32)).to(DEV) if epi == "none" else None
+    off_t = torch.from_numpy(offsets).to(DEV)
+    e = L.EPI_RELU_MASK if epi == "mask" else L.EPI_NONE
+    L.set_tuning("gemm_pair", pair)
+    try:
+        c, wc, cs = L.grouped_gemm_bwd_pair(A, Bw, off_t, G, R + 3, N, K, e, aux, A, Y, tok, out_dtype=torch.float32)
+    finally:
+        L.set_tuning("gemm_pair", 1)
+    ref_c = L.grouped_gemm(A, Bw, off_t, G, R + 3, N, K, 0, e, aux=aux)
+    Yr = Y[tok.long()].contiguous() if tok is not None else Y
+    ref_wc, ref_cs = L.grouped_gemm_wgrad(A, Yr[:R + 3].contiguous() if tok is None else Yr, off_t, G)
+    torch.cuda.synchronize()
+    assert torch.equal(c[:R], ref_c[:R])
+    assert torch.equal(wc, ref_wc) and torch.equal(cs, ref_cs)
+    for _ws, cnt in L._SPLIT_WS.values():  # split-K arrival counters left at zero
+        assert int(cnt.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("T,E,k,cf", [(1000, 8, 2, 0.0), (777, 16, 2, 0.0), (640, 32, 4, 1.25), (1, 4, 1, 0.0)])
+def test_route_index_matches_permute(hip_lib, T, E, k, cf):
+    """route_index's pos equals permute_fwd's, and src_tok inverts it: the
+    gathered token rows are exactly the permuted copy."""
+    from src.moe import _lib as L
+
+    c = make_case(T, 256, E, 1024, k, max(T // 4, 1), 31)
+    cap = _cap(T, k, E, cf)
+    x = _bf16(c["x"]).to(DEV)
+    idx, w, probs, lse, lrank, bcnt, auxp = L.router_topk_fwd(
+        x, torch.from_numpy(c["wg"]).float().to(DEV), torch.from_numpy(c["ctx_bias"]).float().to(DEV),
+        torch.from_numpy(c["ctx_img"]).to(DEV), max(T // 4, 1), k, True)
+    rank_base, hist, offsets = L.route_scan(bcnt, cap)
+    rows = T * k if cap <= 0 else min(T * k, E * cap)
+    xp, pos = L.permute_fwd(x, idx, lrank, rank_base, offsets, E, cap, rows)
+    pos2, tok = L.route_index(idx, lrank, rank_base, offsets, E, cap, rows)
+    torch.cuda.synchronize()
+    assert torch.equal(pos, pos2)
+    R = int(offsets[-1])
+    assert torch.equal(x[tok[:R].long()], xp[:R])
