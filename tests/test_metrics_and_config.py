@@ -24,6 +24,76 @@ def test_map_perfect_and_shifted():
     assert b.map < m.map
 
 
+def _ev(images):
+    """images: list of (pred_boxes, scores, labels, gt_boxes, gt_labels)."""
+    from src.rtdetr_moe.metrics import DetectionEvaluator
+
+    ev = DetectionEvaluator()
+    for pb, ps, pl, gb, gl in images:
+        ev.update(np.asarray(pb, float).reshape(-1, 4), np.asarray(ps, float), np.asarray(pl, np.int64),
+                  np.asarray(gb, float).reshape(-1, 4), np.asarray(gl, np.int64))
+    return ev.compute()
+
+
+# Known answers worked by hand with the COCO rules (pycocotools evaluateImg /
+# accumulate): detections sorted by score (stable, image order breaks ties),
+# each matched to the best-IoU unmatched GT of its class at IoU >= t, AP the
+# mean over 101 recall points of the precision envelope, classes without GT
+# excluded and classes with GT but no detections scoring 0.
+GT = [0.0, 0.0, 10.0, 10.0]
+
+
+def test_map_duplicate_detection():
+    # 0.9: IoU 0.625 with the GT (TP at t <= 0.6, FP above); 0.8: exact (FP while
+    # the GT is taken, TP once the first one misses) -> AP 1 at 3 thresholds, 0.5 at 7
+    m = _ev([([[0, 0, 10, 6.25], GT], [0.9, 0.8], [0, 0], [GT], [0])])
+    assert m.map50 == pytest.approx(1.0)
+    assert m.map == pytest.approx((3 * 1.0 + 7 * 0.5) / 10)
+
+
+def test_map_score_ties_break_in_image_order():
+    far = [50.0, 50.0, 60.0, 60.0]
+    # image 0: FP at 0.7 and TP at 0.5; image 1: TP at 0.7 (ties the FP)
+    # sorted: FP, TP, TP -> precision [0, .5, .667], recall [0, .5, 1] -> AP 2/3
+    a = _ev([([far, GT], [0.7, 0.5], [0, 0], [GT], [0]), ([GT], [0.7], [0], [GT], [0])])
+    assert a.map50 == pytest.approx(2 / 3) and a.map == pytest.approx(2 / 3)
+    # images swapped: TP, FP, TP -> envelope 1 up to recall .5 (51 points), 2/3 after (50)
+    b = _ev([([GT], [0.7], [0], [GT], [0]), ([far, GT], [0.7, 0.5], [0, 0], [GT], [0])])
+    assert b.map50 == pytest.approx((51 + 50 * 2 / 3) / 101)
+
+
+def test_map_crowded_duplicate_ground_truth():
+    # two identical GT boxes, one detection: recall caps at 0.5 -> 51 of 101 points
+    m = _ev([([GT], [0.9], [0], [GT, GT], [0, 0])])
+    assert m.map50 == pytest.approx(51 / 101) and m.map == pytest.approx(51 / 101)
+    assert m.mr == pytest.approx(0.5)
+
+
+def test_map_multi_class_multi_image():
+    g2 = [20.0, 20.0, 40.0, 30.0]
+    imgs = [
+        # class 0 perfect over two images
+        ([GT], [0.9], [0], [GT], [0]),
+        ([g2, g2], [0.8, 0.6], [0, 1], [g2, g2], [0, 1]),
+        # class 1: a higher-scored FP before its TP -> AP 0.5; class 2: GT, no detections -> 0
+        ([[70, 70, 80, 80], [100, 0, 110, 10]], [0.95, 0.3], [1, 1], [[100, 0, 110, 10]], [2]),
+        # class 3: detections but no GT -> excluded from the mean
+        ([[0, 50, 10, 60]], [0.99], [3], [], []),
+    ]
+    m = _ev(imgs)
+    # class 1: 0.95 FP (no class-1 GT in image 2), 0.6 TP -> precision [0, .5], recall [0, 1]
+    # class 2 in image 2 gets no class-2 detection -> AP 0
+    assert m.map50 == pytest.approx((1.0 + 0.5 + 0.0) / 3)
+    assert m.map == pytest.approx((1.0 + 0.5 + 0.0) / 3)
+
+
+def test_map_empty_inputs():
+    m = _ev([([], [], [], [GT], [0])])
+    assert m.map == 0.0 and m.map50 == 0.0 and len(m.curves_results) == 4
+    m = _ev([([GT], [0.9], [0], [], [])])  # no ground truth anywhere
+    assert m.map == 0.0 and m.mp == 0.0
+
+
 @pytest.mark.parametrize("spec,E,k,cf,bb", [
     ("rtdetr-r50-moe8-top2", 8, 2, 0.0, "r50"),
     ("rtdetr-r18-moe4-top1", 4, 1, 0.0, "r18"),
