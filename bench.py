@@ -33,6 +33,7 @@ import math
 import os
 import sys
 import time
+from datetime import timedelta
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
@@ -173,7 +174,9 @@ def setup_dist(n_gpus):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # a rank that never arrives fails the job instead of hanging it
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                timeout=timedelta(seconds=float(os.environ.get("MOE_DIST_TIMEOUT_S", "600"))))
     else:
         torch.cuda.set_device(0)
     if n_gpus != world:
@@ -317,7 +320,7 @@ def main():
         dist.all_reduce(nb)
     num_boxes = max(1.0, float(nb.item()) / world)
 
-    graphs = args.graphs and "ep" not in spec  # the EP all-to-all sizes its buffers on the host
+    graphs = args.graphs  # the EP layer's all-to-alls are fixed-capacity: capturable too
     # library-side kernel events around each MoE/MSDA launch: inside the timed
     # region when eager; in eager steps right after it when graphed
     timing = not args.no_kernel_timing

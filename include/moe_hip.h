@@ -89,6 +89,18 @@ int moe_route_index(const int32_t* topk_idx, const int32_t* local_rank, const in
                     const int32_t* offsets, int T, int E, int k, int cap, int32_t* pos, int32_t* src_tok,
                     hipStream_t stream);
 
+/* a3 + a4 in ONE launch, from the router's outputs: the
+ * moe_route_scan totals and prefixes (recomputed per 64-token router block
+ * from block_counts, so no second pass), hist / offsets, pos and src_tok as
+ * moe_route_index, optionally row_gate[pos[t,j]] = topk_w[t,j] (fp32 [>=
+ * offsets[E]]) and the aux losses of moe_aux_loss_fwd (aux_out3 / wcoef /
+ * aux_partials non-NULL together).  nblk = moe_router_num_blocks(T). */
+int moe_route_dispatch(const int32_t* block_counts, int nblk, int T, int k, int E, int cap,
+                       const int32_t* topk_idx, const int32_t* local_rank, const float* topk_w,
+                       const float* aux_partials, float lb_coef, float z_coef, int32_t* hist, int32_t* offsets,
+                       int32_t* pos, int32_t* src_tok, float* row_gate, float* aux_out3, float* wcoef,
+                       hipStream_t stream);
+
 /* a6: y[t] = sum_j topk_w[t,j] * yp[pos[t,j]] (pos<0 skipped),
  * fp32 accumulation, bf16 out. */
 int moe_combine_fwd(const void* yp, const int32_t* pos, const float* topk_w,
@@ -113,6 +125,16 @@ int moe_token_bwd(const void* dxp, const int32_t* pos, const float* probs,
                   const float* lse, const float* dprob_bias, const float* zc,
                   const float* wg, int T, int d, int E, int k, int normalize,
                   void* dx, float* dlogits, hipStream_t stream);
+/* Same, with the combine transpose's gate gradient formed here when dw is
+ * NULL: dw[t,j] = <dy[t], yp[pos[t,j]]> (dy bf16 [T,d], yp bf16 [rows,d]),
+ * optionally stored to dw_out fp32 [T,k] -- the single-GPU backward then has
+ * no combine_bwd launch (dYp is formed inside moe_grouped_gemm_bwd_pair). */
+int moe_token_bwd_dw(const void* dxp, const int32_t* pos, const float* probs,
+                     const int32_t* topk_idx, const float* topk_w, const float* dw,
+                     const void* dy, const void* yp, float* dw_out,
+                     const float* lse, const float* dprob_bias, const float* zc,
+                     const float* wg, int T, int d, int E, int k, int normalize,
+                     void* dx, float* dlogits, hipStream_t stream);
 
 /* Grouped GEMM data types / epilogues. */
 enum moe_dtype { MOE_BF16 = 0, MOE_FP8_E4M3 = 1 };
@@ -168,17 +190,23 @@ int moe_grouped_gemm_wgrad_gather(int dtype, const void* x, const void* y, const
                                   void* colsum, const int32_t* offsets, int G, int M, int N, int rows_hint,
                                   int out_bf16, hipStream_t stream);
 /* a7: one backward step of an expert weight in ONE launch --
- *   dgrad: C[r, n] = epi( sum_k A[r, k] B_g[k][n] )   (moe_grouped_gemm, trans_b = 0,
- *          epilogue NONE / RELU_MASK / RELU_MASK_MX with aux)
- *   wgrad: WC_g[m, n] = sum_r WX[r, m] WY[r, n], wcolsum_g[m] = sum_r WX[r, m]
- *          (moe_grouped_gemm_wgrad_gather, WY optionally gathered)
- * The two are independent (same offsets, M2 x N2 the weight's shape); sharing
- * the launch fills the chip with both grids and removes a kernel boundary.
- * bf16 operands; C bf16 [rows, N]; WC/wcolsum bf16 (out_bf16) or fp32. */
-int moe_grouped_gemm_bwd_pair(const void* a, const void* b, void* c, const int32_t* offsets, int G, int max_rows,
-                              int N, int K, int epilogue, const void* aux, const void* wx, const void* wy,
-                              const int32_t* wy_gather, void* wc, void* wcolsum, int M2, int N2, int out_bf16,
-                              hipStream_t stream);
+ *   dgrad: C[r, n] = epi( s_r sum_k A(r, k) B_g[k][n] )   (trans_b = 0; epilogue
+ *          NONE / RELU_MASK / RELU_MASK_MX with aux); A(r, .) = a[a_gather[r]]
+ *          (or a[r] when a_gather is NULL); s_r = row_scale[r] (or 1);
+ *   wgrad: WC_g[m, n] = sum_r WX(r, m) WY(r, n), wcolsum_g[m] = sum_r WX(r, m),
+ *          WX(r, .) = bf16(wx_scale[r] * wx[wx_gather[r]]) (or wx[r]),
+ *          WY(r, .) = wy[wy_gather[r]] (or wy[r]).
+ * With a = wx = dy, the gathers = src_tok and the scales = the row gates,
+ * this is the combine transpose (dYp = gate * dy[token]) fused into the
+ * dH / dW2 step.  The two halves are independent (same offsets, M2 x N2 the
+ * weight's shape); sharing the launch fills the chip with both grids and
+ * removes a kernel boundary.  bf16 operands; C bf16 [rows, N]; WC/wcolsum bf16
+ * (out_bf16) or fp32. */
+int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather, const float* row_scale, const void* b,
+                              void* c, const int32_t* offsets, int G, int max_rows, int N, int K, int epilogue,
+                              const void* aux, const void* wx, const int32_t* wx_gather, const float* wx_scale,
+                              const void* wy, const int32_t* wy_gather, void* wc, void* wcolsum, int M2, int N2,
+                              int out_bf16, hipStream_t stream);
 
 /* ---- MXFP8 expert path (config C5: 32-expert top-4 fp8 expert GEMMs) ----
  * Format: OCP e4m3 elements with one E8M0 exponent byte per 32 consecutive

@@ -78,6 +78,12 @@ struct GemmParams {
   //   WGRAD: k-row r of Y is y[b_gather[r]] (dW1 = dH^T Xp from the token rows), variant 1 only.
   const int32_t* a_gather;
   const int32_t* b_gather;
+  // gate scaling (the combine transpose folded into the backward GEMMs):
+  //   ROWS:  output row r is multiplied by row_scale[r] before the epilogue;
+  //   WGRAD: k-row r of X is bf16(x_scale[r] * x[x_gather[r]]) (dYp formed while staging).
+  const float* row_scale;
+  const int32_t* x_gather;
+  const float* x_scale;
 };
 
 // runtime tuning knobs (moe_set_tuning)
@@ -330,10 +336,11 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int g, int row0, i
       const int ml = wm * (BM / 2) + 16 * i + lm;
       if (ml >= a_row_lim) continue;
       const size_t row = (size_t)row0 + ml;
+      const float rs = p.row_scale != nullptr ? p.row_scale[row] : 1.f;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * (BN / 2) + 16 * j + ln;
-        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        float v[4] = {acc[i][j][0] * rs, acc[i][j][1] * rs, acc[i][j][2] * rs, acc[i][j][3] * rs};
         if constexpr (EPI == MOE_EPI_BIAS || EPI == MOE_EPI_BIAS_RELU) {
           v[0] += bpre[j].x; v[1] += bpre[j].y; v[2] += bpre[j].z; v[3] += bpre[j].w;
         }
@@ -412,13 +419,19 @@ __device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row
   __syncthreads();  // every wave is done with the stage buffers
   if constexpr (MODE == MODE_ROWS) {
     constexpr int CPR = BN / 8;  // 16-B chunks per bf16 row
+    float rs[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wm * (BM / 2) + 16 * i + lm;
+      rs[i] = (p.row_scale != nullptr && ml < a_row_lim) ? p.row_scale[(size_t)row0 + ml] : 1.f;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int ml = wm * (BM / 2) + 16 * i + lm;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int nl = wn * (BN / 2) + 16 * j + ln;
-        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        float v[4] = {acc[i][j][0] * rs[i], acc[i][j][1] * rs[i], acc[i][j][2] * rs[i], acc[i][j][3] * rs[i]};
         if constexpr (EPI == MOE_EPI_BIAS || EPI == MOE_EPI_BIAS_RELU) {
           v[0] += bpre[j].x; v[1] += bpre[j].y; v[2] += bpre[j].z; v[3] += bpre[j].w;
         }
@@ -708,6 +721,25 @@ struct RegStage {
       reg[i] = gi[i] >= 0 ? *reinterpret_cast<const uint4*>(gbase + (size_t)gi[i] * ld + r) : make_uint4(0, 0, 0, 0);
     }
   }
+  // scale factors of the k-rows named by load_index (gathered with the same index)
+  __device__ __forceinline__ void load_scale(const float* sk, int k_lim, int tid, float (&gs)[kPer]) const {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int kk = (tid + 256 * i) / (R / 8);
+      gs[i] = kk < k_lim ? sk[kk] : 0.f;
+    }
+  }
+  // reg[i] = bf16(gs[i] * reg[i]) (RNE, as the combine transpose rounds dYp)
+  __device__ __forceinline__ void scale(const float (&gs)[kPer]) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      float f[8];
+      unpack8(reg[i], f);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) f[c] *= gs[i];
+      reg[i] = pack8(f);
+    }
+  }
   __device__ __forceinline__ void load(const uint16_t* base, int ld, int row_lim, int k_lim, int tid,
                                        const int32_t* gk = nullptr, const uint16_t* gbase = nullptr) {
 #pragma unroll
@@ -808,6 +840,33 @@ __device__ __forceinline__ void gemm_v1_body(const GemmParams& p, int bid, char*
   RegStage<BM, A_K> la;
   RegStage<BN, B_K> lb;
   RegStageY8 ly;
+  // WGRAD with x_gather: k-row r of X is bf16(x_scale[r] * x[x_gather[row0 + r]]); the
+  // indices and scales of tile kt+1 are loaded while tile kt computes
+  constexpr bool AG = MODE == MODE_WGRAD && !A_K;
+  const int32_t* agk = (AG && p.x_gather != nullptr) ? p.x_gather + t.row0 : nullptr;
+  const float* ask = (AG && p.x_scale != nullptr) ? p.x_scale + t.row0 : nullptr;
+  int ai[AG ? RegStage<BM, A_K>::kPer : 1];
+  float as_[AG ? RegStage<BM, A_K>::kPer : 1];
+  auto load_a_index = [&](int kt) {
+    if constexpr (AG) {
+      if (agk != nullptr && kt < t.nk) {
+        la.load_index(agk + kt * 64, k_lim(kt), tid, ai);
+        if (ask != nullptr) la.load_scale(ask + kt * 64, k_lim(kt), tid, as_);
+      }
+    }
+  };
+  auto load_a = [&](int kt) {
+    if constexpr (AG) {
+      if (agk != nullptr) {
+        la.load_gathered(p.a + t.m0, p.lda, ai, tid);
+        if (ask != nullptr) la.scale(as_);
+        load_a_index(kt + 1);
+        return;
+      }
+    }
+    la.load(a_ptr(kt), p.lda, t.a_row_lim, k_lim(kt), tid);
+  };
+  load_a_index(0);
   // WGRAD with b_gather: k-row r of Y is y[b_gather[row0 + r]] (columns from
   // n0); the row indices of tile kt+1 are loaded while tile kt computes, so
   // the data loads of a tile never wait on their index loads
@@ -836,7 +895,7 @@ __device__ __forceinline__ void gemm_v1_body(const GemmParams& p, int bid, char*
     else lb.store(dst, tid);
   };
   if (t.nk > 0) {
-    la.load(a_ptr(0), p.lda, t.a_row_lim, k_lim(0), tid);
+    load_a(0);
     load_b(0);
     la.store(smem, tid);
     store_b(smem + A_BYTES);
@@ -846,7 +905,7 @@ __device__ __forceinline__ void gemm_v1_body(const GemmParams& p, int bid, char*
     char* cur = smem + (kt & 1) * BUF;
     const bool more = kt + 1 < t.nk;
     if (more) {
-      la.load(a_ptr(kt + 1), p.lda, t.a_row_lim, k_lim(kt + 1), tid);
+      load_a(kt + 1);
       load_b(kt + 1);
     }
     compute_tile<BM, BN, A_K, B_K, COLSUM>(cur, cur + A_BYTES, acc, csum, lane, wm, wn);
@@ -862,8 +921,12 @@ __device__ __forceinline__ void gemm_v1_body(const GemmParams& p, int bid, char*
                                       t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, lane, wm, wn);
 }
 
+// 64-row tiles fit three workgroups per CU (512 unified VGPRs per lane: <= 168
+// arch + acc registers each); pin that so the register allocator never tips a
+// variant over the cliff to two.
 template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>
-__global__ __launch_bounds__(256) void gemm_v1_kernel(GemmParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM <= 64 ? 3 : 1)))
+void gemm_v1_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   gemm_v1_body<BM, BN, A_K, B_K, MODE, EPI, COLSUM, FL>(p, blockIdx.x, smem);
 }
@@ -1053,8 +1116,10 @@ __global__ __launch_bounds__(256) void gemm_v2_kernel(GemmParams p) {
 // of the same weight: their grids fill the chip together and one kernel
 // boundary disappears): workgroups [0, n1) run problem 1, the rest problem 2.
 // n1 is a multiple of 8, so each problem keeps its XCD-aware tile map.
+// Both bodies are 64-row tiles: three workgroups per CU (see gemm_v1_kernel).
 template <class P1, class P2>
-__global__ __launch_bounds__(256) void gemm_pair_kernel(GemmParams p1, GemmParams p2, int n1) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+void gemm_pair_kernel(GemmParams p1, GemmParams p2, int n1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if ((int)blockIdx.x < n1) P1::run(p1, blockIdx.x, smem);
   else P2::run(p2, (int)blockIdx.x - n1, smem);
@@ -1180,7 +1245,7 @@ struct WgradPlan {
 
 static int plan_rows(RowsPlan& pl, const void* a, const void* b, void* c, const int32_t* offsets, int G, int max_rows,
                      int N, int K, int trans_b, int epilogue, const float* bias, const void* aux,
-                     const int32_t* a_gather, WsWin& win) {
+                     const int32_t* a_gather, WsWin& win, const float* row_scale = nullptr) {
   if (G < 1 || G > 1024) return fail("grouped_gemm: G out of range");
   if (N <= 0 || K <= 0 || N % 128 != 0 || K % 64 != 0) return fail("grouped_gemm: need N % 128 == 0 and K % 64 == 0");
   if (max_rows < 0) return fail("grouped_gemm: max_rows < 0");
@@ -1199,6 +1264,7 @@ static int plan_rows(RowsPlan& pl, const void* a, const void* b, void* c, const 
   p.bias = bias;
   p.aux = static_cast<const uint16_t*>(aux);
   p.a_gather = a_gather;
+  p.row_scale = row_scale;
   p.stride_b = (long long)N * K;
   p.lda = K;
   p.ldb = trans_b ? K : N;
@@ -1240,7 +1306,8 @@ static int plan_rows(RowsPlan& pl, const void* a, const void* b, void* c, const 
 }
 
 static int plan_wgrad(WgradPlan& pl, const void* x, const void* y, void* c, void* colsum, const int32_t* offsets,
-                      int G, int M, int N, int rows_hint, int out_bf16, const int32_t* b_gather, WsWin& win) {
+                      int G, int M, int N, int rows_hint, int out_bf16, const int32_t* b_gather, WsWin& win,
+                      const int32_t* x_gather = nullptr, const float* x_scale = nullptr) {
   if (G < 1 || G > 1024) return fail("grouped_gemm_wgrad: G out of range");
   if (M <= 0 || N <= 0 || M % 64 != 0 || N % 128 != 0)
     return fail("grouped_gemm_wgrad: need M % 64 == 0 and N % 128 == 0");
@@ -1254,6 +1321,8 @@ static int plan_wgrad(WgradPlan& pl, const void* x, const void* y, void* c, void
   p.colsum = static_cast<float*>(colsum);
   p.c_bf16 = out_bf16 ? 1 : 0;
   p.b_gather = b_gather;
+  p.x_gather = x_gather;
+  p.x_scale = x_gather != nullptr ? x_scale : nullptr;
   p.stride_c = (long long)M * N;
   p.lda = M;
   p.ldb = N;
@@ -1266,9 +1335,10 @@ static int plan_wgrad(WgradPlan& pl, const void* x, const void* y, void* c, void
   const int ntn = N / 128;
   // 64-row tiles, register-staged double buffer (its global_load_dwordx4 path
   // streams these k-row gathers faster than LDS-DMA)
-  const bool big = M % 128 == 0 && g_wgrad_bm == 128 && !b_gather;
+  const bool gath = b_gather != nullptr || x_gather != nullptr;
+  const bool big = M % 128 == 0 && g_wgrad_bm == 128 && !gath;
   pl.bm = big ? 128 : 64;
-  pl.variant = (g_gemm_variant && !b_gather) ? g_gemm_variant : 1;  // the k-row gather is in the register path
+  pl.variant = (g_gemm_variant && !gath) ? g_gemm_variant : 1;  // the k-row gathers are in the register path
   pl.stages = g_gemm_stages ? g_gemm_stages : 2;
   int gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
   // split-K over each group's rows: the output (G M N) is too small a grid to
@@ -1457,18 +1527,25 @@ extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void*
                                        stream);
 }
 
-extern "C" int moe_grouped_gemm_bwd_pair(const void* a, const void* b, void* c, const int32_t* offsets, int G,
-                                         int max_rows, int N, int K, int epilogue, const void* aux, const void* wx,
-                                         const void* wy, const int32_t* wy_gather, void* wc, void* wcolsum, int M2,
-                                         int N2, int out_bf16, hipStream_t stream) {
+extern "C" int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather, const float* row_scale,
+                                         const void* b, void* c, const int32_t* offsets, int G, int max_rows, int N,
+                                         int K, int epilogue, const void* aux, const void* wx,
+                                         const int32_t* wx_gather, const float* wx_scale, const void* wy,
+                                         const int32_t* wy_gather, void* wc, void* wcolsum, int M2, int N2,
+                                         int out_bf16, hipStream_t stream) {
   RowsPlan r;
   WgradPlan w;
   WsWin win = device_ws();
-  if (plan_rows(r, a, b, c, offsets, G, max_rows, N, K, 0, epilogue, nullptr, aux, nullptr, win)) return -1;
-  if (plan_wgrad(w, wx, wy, wc, wcolsum, offsets, G, M2, N2, max_rows, out_bf16, wy_gather, win)) return -1;
-  if (max_rows == 0) {  // no routed rows: the weight gradient is zero (the unpaired call writes it)
-    return moe_grouped_gemm_wgrad_gather(MOE_BF16, wx, wy, wy_gather, wc, wcolsum, offsets, G, M2, N2, 0, out_bf16,
-                                         stream);
+  if (plan_rows(r, a, b, c, offsets, G, max_rows, N, K, 0, epilogue, nullptr, aux, a_gather, win, row_scale))
+    return -1;
+  if (plan_wgrad(w, wx, wy, wc, wcolsum, offsets, G, M2, N2, max_rows, out_bf16, wy_gather, win, wx_gather,
+                 wx_scale))
+    return -1;
+  if (max_rows == 0) {  // no routed rows: the weight gradient is zero
+    ProfScope prof(stream, PROF_GEMM, w.bytes_fixed, true, w.bytes_row, w.flops_row);
+    w.p.prof_rows = prof.rows_slot();
+    launch_wgrad<0>(w, stream, prof);
+    return check_launch("moe_grouped_gemm_bwd_pair (wgrad)");
   }
   if (g_gemm_pair_off || !pair_ok(r, w)) {  // two launches
     {

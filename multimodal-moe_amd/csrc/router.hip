@@ -352,6 +352,189 @@ __global__ __launch_bounds__(1024) void route_scan_kernel(
   }
 }
 
+// Column sums of the router's aux partials [nblk, E+1] by one 256-thread
+// workgroup: 256 / (E+1) strided block segments (coalesced rows), combined in
+// segment order -- a fixed summation order shared by route_dispatch and
+// aux_loss_fwd, so both give bit-identical losses.  Valid for tid <= E.
+__device__ __forceinline__ float aux_colsum(const float* __restrict__ partials, int nblk, int E, float* s_aux,
+                                            int tid) {
+  const int nc = E + 1, nseg = 256 / nc;
+  const int c = tid % nc, seg = tid / nc;
+  if (seg < nseg) {
+    float acc = 0.f;
+    for (int bb = seg; bb < nblk; bb += nseg) acc += partials[(size_t)bb * nc + c];
+    s_aux[tid] = acc;
+  }
+  __syncthreads();
+  float colsum = 0.f;
+  if (tid <= E)
+    for (int sg = 0; sg < nseg; ++sg) colsum += s_aux[sg * nc + tid];
+  return colsum;
+}
+
+// ---------------------------------------------------------------------------
+// route dispatch: scan + index + aux loss in one launch (replaces route_scan,
+// route_index and aux_loss_fwd).  Workgroup b owns
+// router block b (64 tokens): it sums the counts of every router block into
+// column totals and its own exclusive prefix (coalesced rows, a few KiB read
+// per workgroup from L2: no second launch, no inter-workgroup hand-off),
+// forms the slot bases / hist / kept offsets (one wave), and writes pos,
+// the row -> token map and the row gates of its 64 tokens.  Workgroup 0 also
+// writes hist / offsets and the layer's aux losses.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void route_dispatch_kernel(
+    const int32_t* __restrict__ counts, int nblk, int T, int k, int E, int cap,
+    const int32_t* __restrict__ topk_idx, const int32_t* __restrict__ local_rank, const float* __restrict__ topk_w,
+    const float* __restrict__ aux_partials, float lb_coef, float z_coef,
+    int32_t* __restrict__ hist, int32_t* __restrict__ offsets, int32_t* __restrict__ pos,
+    int32_t* __restrict__ src_tok, float* __restrict__ row_gate, float* __restrict__ aux_out,
+    float* __restrict__ wcoef, int32_t* __restrict__ prof_rows) {
+  __shared__ int32_t s_pre[256];      // per (segment, column): prefix sums
+  __shared__ int32_t s_tot[256];      // ... and totals
+  __shared__ int32_t s_col_pre[512];  // column prefix over blocks < b
+  __shared__ int32_t s_base[512];     // slot base + prefix per column
+  __shared__ int32_t s_off[65];
+  __shared__ float s_term[65];
+  __shared__ float s_aux[256];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int b = blockIdx.x;
+  const int ncol = k * E;  // <= 512
+  // Phase A: column totals and this block's prefix over all router blocks.
+  // ncol <= 256: 256 / ncol block segments per column, every thread busy, one
+  // or two 8-deep load batches each (the workgroup's latency is a couple of L2
+  // round trips, not nblk of them); combined in LDS in segment order.
+  // ncol > 256: one segment, columns tid and tid + 256.
+  constexpr int CH = 8;
+  if (ncol <= 256) {
+    const int nseg = 256 / ncol;
+    const int col = tid % ncol, seg = tid / ncol;
+    int pre = 0, tot = 0;
+    if (seg < nseg) {
+      const int bs = (nblk + nseg - 1) / nseg;
+      const int lo = seg * bs, hi = min(lo + bs, nblk);
+      for (int b0 = lo; b0 < hi; b0 += CH) {
+        int v[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) v[i] = (b0 + i < hi) ? counts[(size_t)(b0 + i) * ncol + col] : 0;
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          tot += v[i];
+          pre += (b0 + i < b) ? v[i] : 0;
+        }
+      }
+      s_pre[tid] = pre;
+      s_tot[tid] = tot;
+    }
+    __syncthreads();
+    if (tid < ncol) {
+      int p = 0, t = 0;
+      for (int sg = 0; sg < nseg; ++sg) {
+        p += s_pre[sg * ncol + tid];
+        t += s_tot[sg * ncol + tid];
+      }
+      s_col_pre[tid] = p;
+      s_base[tid] = t;  // column total, for now
+    }
+  } else {
+    for (int pass = 0; pass < 2; ++pass) {
+      const int col = tid + 256 * pass;
+      if (col < ncol) {
+        int pre = 0, tot = 0;
+        for (int b0 = 0; b0 < nblk; b0 += CH) {
+          int v[CH];
+#pragma unroll
+          for (int i = 0; i < CH; ++i) v[i] = (b0 + i < nblk) ? counts[(size_t)(b0 + i) * ncol + col] : 0;
+#pragma unroll
+          for (int i = 0; i < CH; ++i) {
+            tot += v[i];
+            pre += (b0 + i < b) ? v[i] : 0;
+          }
+        }
+        s_col_pre[col] = pre;
+        s_base[col] = tot;
+      }
+    }
+  }
+  __syncthreads();
+  // Phase B (wave 0, lane e): hist, kept offsets, slot bases (slot-major priority)
+  if (wave == 0) {
+    int h = 0;
+    int sb[8];
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+      sb[j] = h;
+      if (lane < E) h += s_base[j * E + lane];
+    }
+    const int kept = (lane < E) ? ((cap > 0 && h > cap) ? cap : h) : 0;
+    int inc = kept;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
+    }
+    if (lane < E) {
+      s_off[lane] = inc - kept;
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k)
+        s_base[j * E + lane] = sb[j] + s_col_pre[j * E + lane];
+      if (b == 0) {
+        hist[lane] = h;
+        offsets[lane] = inc - kept;
+      }
+    }
+    if (lane == E - 1) {
+      s_off[E] = inc;
+      if (b == 0) offsets[E] = inc;
+      if (b == 0 && prof_rows != nullptr) *prof_rows = inc;
+    }
+    if (b == 0 && aux_out != nullptr && lane < E) s_term[lane] = (float)h;  // hist, for the aux loss
+  }
+  __syncthreads();
+  // aux losses (workgroup 0): lb = E sum_e f_e P_e, z = mean lse^2 (aux_colsum order)
+  if (b == 0 && aux_out != nullptr) {
+    const float invT = 1.f / (float)(T > 0 ? T : 1);
+    const float invA = 1.f / (float)(T * k > 0 ? T * k : 1);
+    const float colsum = aux_colsum(aux_partials, nblk, E, s_aux, tid);
+    float term = 0.f;
+    if (tid <= E) {
+      if (tid < E) {
+        const float f = s_term[tid] * invA;
+        term = f * (colsum * invT);
+        wcoef[tid] = lb_coef * (float)E * f * invT;
+      } else {
+        term = colsum * invT;
+        wcoef[E] = z_coef * invT;
+      }
+    }
+    __syncthreads();
+    if (tid <= E) s_term[tid] = term;
+    __syncthreads();
+    if (tid == 0) {
+      float acc = 0.f;
+      for (int i = 0; i < E; ++i) acc += s_term[i];
+      const float lb = (float)E * acc, z = s_term[E];
+      aux_out[0] = lb;
+      aux_out[1] = z;
+      aux_out[2] = lb_coef * lb + z_coef * z;
+    }
+  }
+  // Phase C: this block's assignments
+  for (int a = tid; a < 64 * k; a += 256) {
+    const int t = b * 64 + a / k;
+    if (t >= T) break;
+    const int j = a - (a / k) * k;
+    const size_t ai = (size_t)t * k + j;
+    const int e = topk_idx[ai];
+    const int r = s_base[j * E + e] + local_rank[ai];
+    const int p = (cap <= 0 || r < cap) ? s_off[e] + r : -1;
+    pos[ai] = p;
+    if (p >= 0) {
+      src_tok[p] = t;
+      if (row_gate != nullptr) row_gate[p] = topk_w[ai];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // aux losses from the router's per-block partials, one block:
 //   P_e = sum_b partials[b][e] / T, f_e = hist[e] / (T k), lb = E sum_e f_e P_e,
@@ -365,12 +548,12 @@ __global__ __launch_bounds__(256) void aux_loss_fwd_kernel(const float* __restri
                                                            float lb_coef, float z_coef, float* __restrict__ out,
                                                            float* __restrict__ wcoef) {
   __shared__ float s_term[65];
+  __shared__ float s_aux[256];
   const int e = threadIdx.x;
   const float invT = 1.f / (float)(T > 0 ? T : 1);
   const float invA = 1.f / (float)(T * k > 0 ? T * k : 1);
+  const float colsum = aux_colsum(partials, nblk, E, s_aux, e);
   if (e <= E) {
-    float colsum = 0.f;
-    for (int b = 0; b < nblk; ++b) colsum += partials[(size_t)b * (E + 1) + e];  // fixed order
     if (e < E) {
       const float f = (float)hist[e] * invA;
       s_term[e] = f * (colsum * invT);
@@ -413,7 +596,8 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
     const float* __restrict__ lse, const float* __restrict__ dprob_bias,
     const float* __restrict__ zc_ptr,
     const float* __restrict__ wg, int T, int d, int E, int k, int normalize,
-    uint16_t* __restrict__ dx, float* __restrict__ dlogits) {
+    uint16_t* __restrict__ dx, float* __restrict__ dlogits,
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ yp, float* __restrict__ dw_out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_wg = reinterpret_cast<float*>(smem);  // [E][d]
   const int tid = threadIdx.x;
@@ -450,11 +634,33 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
     _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) pj[j] = pos[(size_t)t * k + j];
     int sel[8];
     float selw[8], seldw[8];
+    if (dw == nullptr) {
+      // the combine transpose's gate gradient, here: dw[t,j] = <dy[t], Yp[pos[t,j]]>
+      // (16 lanes per token, 16-B chunks, fixed-order row sum)
+      float part[8];
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) part[j] = 0.f;
+      for (int c = 0; c < nchunk; ++c) {
+        const int ch = sub + 16 * c;
+        float g[8];
+        unpack8(reinterpret_cast<const uint4*>(dy + (size_t)t * d)[ch], g);
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+          if (pj[j] < 0) continue;
+          float v[8];
+          unpack8(reinterpret_cast<const uint4*>(yp + (size_t)pj[j] * d)[ch], v);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) part[j] += g[i] * v[i];
+        }
+      }
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
+        seldw[j] = row16_sum(part[j]);
+        if (dw_out != nullptr && sub == j) dw_out[(size_t)t * k + j] = seldw[j];
+      }
+    }
     float Sl = 0.f, wdw = 0.f;
     _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
       sel[j] = topk_idx[(size_t)t * k + j];
       selw[j] = topk_w[(size_t)t * k + j];
-      seldw[j] = dw[(size_t)t * k + j];
+      if (dw != nullptr) seldw[j] = dw[(size_t)t * k + j];
       wdw += selw[j] * seldw[j];
       if ((sel[j] & 15) == sub) {
 #pragma unroll
@@ -587,11 +793,51 @@ extern "C" int moe_route_scan(const int32_t* block_counts, int nblk, int k, int 
   return check_launch("moe_route_scan");
 }
 
+extern "C" int moe_route_dispatch(const int32_t* block_counts, int nblk, int T, int k, int E, int cap,
+                                  const int32_t* topk_idx, const int32_t* local_rank, const float* topk_w,
+                                  const float* aux_partials, float lb_coef, float z_coef, int32_t* hist,
+                                  int32_t* offsets, int32_t* pos, int32_t* src_tok, float* row_gate,
+                                  float* aux_out3, float* wcoef, hipStream_t stream) {
+  if (E < 1 || E > 64 || k < 1 || k > 8 || k > E) return fail("route_dispatch: need 1<=E<=64, 1<=k<=min(8,E)");
+  if (nblk != moe_router_num_blocks(T)) return fail("route_dispatch: nblk must be moe_router_num_blocks(T)");
+  if ((aux_out3 == nullptr) != (wcoef == nullptr) || (aux_out3 != nullptr && aux_partials == nullptr))
+    return fail("route_dispatch: aux_out3, wcoef and aux_partials go together");
+  if (row_gate != nullptr && topk_w == nullptr) return fail("route_dispatch: row_gate needs topk_w");
+  if (T <= 0) return 0;
+  // bytes: every workgroup reads the block counts (L2), per assignment idx/rank/gate read and pos written,
+  // per kept row src_tok (+ gate) written
+  ProfScope prof(stream, PROF_SCAN, 4.0 * nblk * k * E + 16.0 * T * k + 4.0 * nblk * (E + 1), true,
+                 row_gate ? 8.0 : 4.0);
+  MOE_LAUNCH(prof, route_dispatch_kernel, dim3(nblk), dim3(256), 0, stream, block_counts, nblk, T, k, E, cap,
+             topk_idx, local_rank, topk_w, aux_partials, lb_coef, z_coef, hist, offsets, pos, src_tok, row_gate,
+             aux_out3, wcoef, prof.rows_slot());
+  return check_launch("moe_route_dispatch");
+}
+
+extern "C" int moe_token_bwd_dw(const void* dxp, const int32_t* pos, const float* probs,
+                                const int32_t* topk_idx, const float* topk_w, const float* dw,
+                                const void* dy, const void* yp, float* dw_out,
+                                const float* lse, const float* dprob_bias, const float* zc,
+                                const float* wg, int T, int d, int E, int k, int normalize,
+                                void* dx, float* dlogits, hipStream_t stream);
+
 extern "C" int moe_token_bwd(const void* dxp, const int32_t* pos, const float* probs,
                              const int32_t* topk_idx, const float* topk_w, const float* dw,
                              const float* lse, const float* dprob_bias, const float* zc,
                              const float* wg, int T, int d, int E, int k, int normalize,
                              void* dx, float* dlogits, hipStream_t stream) {
+  if (dw == nullptr) return fail("token_bwd: dw is NULL (moe_token_bwd_dw computes it from dy and yp)");
+  return moe_token_bwd_dw(dxp, pos, probs, topk_idx, topk_w, dw, nullptr, nullptr, nullptr, lse, dprob_bias, zc,
+                          wg, T, d, E, k, normalize, dx, dlogits, stream);
+}
+
+extern "C" int moe_token_bwd_dw(const void* dxp, const int32_t* pos, const float* probs,
+                                const int32_t* topk_idx, const float* topk_w, const float* dw,
+                                const void* dy, const void* yp, float* dw_out,
+                                const float* lse, const float* dprob_bias, const float* zc,
+                                const float* wg, int T, int d, int E, int k, int normalize,
+                                void* dx, float* dlogits, hipStream_t stream) {
+  if (dw == nullptr && (dy == nullptr || yp == nullptr)) return fail("token_bwd: need dw, or dy and yp");
   if (d <= 0 || d % 128 != 0 || d > 1024) return fail("token_bwd: d must be a multiple of 128 in [128,1024]");
   if (E < 1 || E > 64 || k < 1 || k > 8 || k > E) return fail("token_bwd: need 1<=E<=64, 1<=k<=min(8,E)");
   if ((size_t)E * d * 4 > 64 * 1024) return fail("token_bwd: E*d*4 must fit 64 KiB of LDS");
@@ -603,13 +849,17 @@ extern "C" int moe_token_bwd(const void* dxp, const int32_t* pos, const float* p
   const uint16_t* dxpb = static_cast<const uint16_t*>(dxp);
   uint16_t* dxb = static_cast<uint16_t*>(dx);
   // bytes: T*k rows of dXp, per-token routing state, Wg; dx and dlogits written
+  // (+ dy and the T*k rows of Yp when dw is formed here)
   ProfScope prof(stream, PROF_TOKEN_BWD,
-                 2.0 * T * k * d + 2.0 * T * d + 8.0 * T * E + 20.0 * T * k + 4.0 * T + 4.0 * E * d);
+                 2.0 * T * k * d + 2.0 * T * d + 8.0 * T * E + 20.0 * T * k + 4.0 * T + 4.0 * E * d +
+                     (dw == nullptr ? 2.0 * T * d + 2.0 * T * k * d : 0.0));
+  const uint16_t* dyb = static_cast<const uint16_t*>(dy);
+  const uint16_t* ypb = static_cast<const uint16_t*>(yp);
 #define LAUNCH_B(EM)                                                                          \
   allow_lds<token_bwd_kernel<EM>>(shmem);                                                   \
   MOE_LAUNCH(prof, token_bwd_kernel<EM>, dim3(grid), dim3(256), shmem, stream, dxpb, pos, \
                      probs, topk_idx, topk_w, dw, lse, dprob_bias, zc, wg, T, d, E, k,      \
-                     normalize, dxb, dlogits)
+                     normalize, dxb, dlogits, dyb, ypb, dw_out)
   switch (em) {
     case 8: LAUNCH_B(8); break;
     case 16: LAUNCH_B(16); break;

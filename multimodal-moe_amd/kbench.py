@@ -70,9 +70,20 @@ def setup(T, E, k, d, F, seed=0):
     w2q, w2s = L.quantize_mx(w2)
     hq, hs = L.grouped_gemm_mx(xq, xs, w1q, w1s, offsets, E, rows, F, d, L.EPI_BIAS_RELU, bias=b1, out_mx=True)
     return dict(T=T, E=E, k=k, d=d, F=F, x=x, wg=wg, cb=cb, ci=ci, tpi=tpi, w1=w1, w2=w2, b1=b1, b2=b2, idx=idx,
+                auxp=auxp,
                 w=w, probs=probs, lse=lse, lrank=lrank, bcnt=bcnt, rank_base=rank_base, offsets=offsets, rows=rows,
                 xp=xp, pos=pos, tok=tok, h=h, yp=yp, dy=dy, dyp=dyp, dw=dw, dh=dh, dxp=dxp,
                 xq=xq, xs=xs, w1q=w1q, w1s=w1s, w2q=w2q, w2s=w2s, hq=hq, hs=hs)
+
+
+def layer_fwd_bwd(c):
+    """One MoE layer forward + backward through ops._MoELayer (all its HIP launches)."""
+    from src.moe.ops import moe_layer_hip
+
+    x = c["x"].detach().requires_grad_(True)
+    y, aux, raw, hist = moe_layer_hip(x, c["wg"], c["cb"], c["w1"], c["b1"], c["w2"], c["b2"], c["ci"], c["tpi"],
+                                      c["k"], True, 0, aux_coefs=(1e-2, 1e-3))
+    torch.autograd.backward([y, aux], [c["dy"], torch.ones_like(aux)])
 
 
 def kernels(c):
@@ -96,6 +107,9 @@ def kernels(c):
                                                        c["h"], c["dyp"], c["h"]), 4.0 * A * F * d, 0),
         ("gemm_pair1", lambda: L.grouped_gemm_bwd_pair(c["dh"], c["w1"], c["offsets"], E, rows, d, F, L.EPI_NONE,
                                                        None, c["dh"], c["x"], c["tok"]), 4.0 * A * F * d, 0),
+        ("route_dispatch", lambda: L.route_dispatch(c["bcnt"], c["idx"], c["lrank"], c["w"], c["auxp"], T, E, 0,
+                                                    rows, 1e-2, 1e-3, row_gate=True), 0, 24 * A),
+        ("moe_layer_fwd_bwd", lambda: layer_fwd_bwd(c), 6.0 * A * F * d, 0),
         ("combine", lambda: L.combine_fwd(c["yp"], c["pos"], c["w"], T), 0, 512 * (A + T) + 8 * A),
         ("combine_bwd", lambda: L.combine_bwd(c["dy"], c["yp"], c["pos"], c["w"]), 0, 512 * (T + 2 * A) + 12 * A),
         ("gemm_dgrad2", lambda: L.grouped_gemm(c["dyp"], c["w2"], c["offsets"], E, rows, F, d, 0, L.EPI_RELU_MASK,

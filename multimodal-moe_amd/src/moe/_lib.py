@@ -38,9 +38,12 @@ SIGNATURES = {
     "moe_grouped_gemm_wgrad": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "moe_grouped_gemm_wgrad_rows": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "moe_route_index": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "moe_route_dispatch": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P]),
     "moe_grouped_gemm_gather": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "moe_grouped_gemm_wgrad_gather": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
-    "moe_grouped_gemm_bwd_pair": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "moe_grouped_gemm_bwd_pair": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
+                                       _I, _I, _I, _P]),
+    "moe_token_bwd_dw": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "moe_quantize_mx": (_I, [_P, ctypes.c_longlong, _I, _P, _P, _P]),
     "moe_permute_fwd_mx": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_mx": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
@@ -382,6 +385,28 @@ def route_index(topk_idx, local_rank, rank_base, offsets, E, cap, rows_alloc):
     return pos, tok
 
 
+def route_dispatch(block_counts, topk_idx, local_rank, topk_w, aux_partials, T, E, cap, rows, lb_coef=None,
+                   z_coef=None, row_gate=False):
+    """Scan + index (+ aux losses) in one launch (moe_route_dispatch).
+    -> (pos, src_tok, hist, offsets, row_gate or None, aux_out3 or None, wcoef or None)."""
+    nblk, k, E_ = block_counts.shape
+    dev = block_counts.device
+    pos = torch.empty((T, k), dtype=torch.int32, device=dev)
+    tok = torch.empty((max(rows, 1),), dtype=torch.int32, device=dev)
+    hist = torch.empty((E,), dtype=torch.int32, device=dev)
+    offsets = torch.empty((E + 1,), dtype=torch.int32, device=dev)
+    gate = torch.empty((max(rows, 1),), dtype=torch.float32, device=dev) if row_gate else None
+    aux = lb_coef is not None
+    out3 = torch.empty(3, dtype=torch.float32, device=dev) if aux else None
+    wcoef = torch.empty(E + 1, dtype=torch.float32, device=dev) if aux else None
+    _check(lib().moe_route_dispatch(_ptr(block_counts), nblk, T, k, E, int(cap), _ptr(topk_idx), _ptr(local_rank),
+                                    _ptr(topk_w), _ptr(aux_partials) if aux else None,
+                                    float(lb_coef or 0.0), float(z_coef or 0.0), _ptr(hist), _ptr(offsets),
+                                    _ptr(pos), _ptr(tok), _ptr(gate), _ptr(out3), _ptr(wcoef), _stream()),
+           "moe_route_dispatch")
+    return pos, tok, hist, offsets, gate, out3, wcoef
+
+
 def grouped_gemm_gather(x, src_tok, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None, aux=None):
     """grouped_gemm with routed row r of A = x[src_tok[r]] (x: bf16 token rows [T, K])."""
     _need(x, torch.bfloat16, "x")
@@ -398,30 +423,55 @@ def grouped_gemm_gather(x, src_tok, b, offsets, G, max_rows, N, K, trans_b, epil
 
 
 def grouped_gemm_bwd_pair(a, b, offsets, G, max_rows, N, K, epilogue, aux, wx, wy, wy_gather=None,
-                          out_dtype=torch.bfloat16):
-    """One launch: C = epi(A . B_g) (dgrad, B stored [K][N] per group) and the
-    weight gradient WC_g = WX_g^T WY_g with colsum (WY rows gathered through
-    wy_gather when given).  -> (C bf16 [rows, N], WC [G, M2, N2], colsum [G, M2])."""
+                          out_dtype=torch.bfloat16, a_gather=None, row_scale=None, wx_gather=None, wx_scale=None):
+    """One launch: C = epi(s_r A(r) . B_g) (dgrad, B stored [K][N] per group;
+    A(r) = a[a_gather[r]] when given, s_r = row_scale[r]) and the weight
+    gradient WC_g = WX_g^T WY_g with colsum (WX(r) = bf16(wx_scale[r] *
+    wx[wx_gather[r]]), WY(r) = wy[wy_gather[r]] when given).
+    -> (C bf16 [rows, N], WC [G, M2, N2], colsum [G, M2])."""
     _need(a, torch.bfloat16, "a")
     _need(b, torch.bfloat16, "b")
     _need(wx, torch.bfloat16, "wx")
     _need(wy, torch.bfloat16, "wy")
+    for t, n in ((a_gather, "a_gather"), (wx_gather, "wx_gather"), (wy_gather, "wy_gather")):
+        if t is not None:
+            _need(t, torch.int32, n)
+    for t, n in ((row_scale, "row_scale"), (wx_scale, "wx_scale")):
+        if t is not None:
+            _need(t, torch.float32, n)
     if aux is not None:
         _need(aux, torch.uint8 if epilogue == EPI_RELU_MASK_MX else torch.bfloat16, "aux")
-    if b.numel() != G * N * K or a.shape[1] != K or a.shape[0] < max_rows:
+    if b.numel() != G * N * K or a.shape[1] != K or (a_gather is None and a.shape[0] < max_rows):
         raise MoEKernelError("grouped_gemm_bwd_pair: dgrad shapes")
     M2, N2 = wx.shape[1], wy.shape[1]
-    if wy_gather is None and wy.shape[0] < max_rows:
+    if (wy_gather is None and wy.shape[0] < max_rows) or (wx_gather is None and wx.shape[0] < max_rows):
         raise MoEKernelError("grouped_gemm_bwd_pair: wgrad shapes")
-    c = torch.empty((a.shape[0], N), dtype=torch.bfloat16, device=a.device)
+    rows_out = max(max_rows, 1) if a_gather is not None else a.shape[0]
+    c = torch.empty((rows_out, N), dtype=torch.bfloat16, device=a.device)
     wc = torch.empty((G, M2, N2), dtype=out_dtype, device=a.device)
     cs = torch.empty((G, M2), dtype=out_dtype, device=a.device)
     ensure_splitk_workspace(a.device)
-    _check(lib().moe_grouped_gemm_bwd_pair(_ptr(a), _ptr(b), _ptr(c), _ptr(offsets), G, int(max_rows), N, K,
-                                           int(epilogue), _ptr(aux), _ptr(wx), _ptr(wy), _ptr(wy_gather), _ptr(wc),
+    _check(lib().moe_grouped_gemm_bwd_pair(_ptr(a), _ptr(a_gather), _ptr(row_scale), _ptr(b), _ptr(c), _ptr(offsets),
+                                           G, int(max_rows), N, K, int(epilogue), _ptr(aux), _ptr(wx),
+                                           _ptr(wx_gather), _ptr(wx_scale), _ptr(wy), _ptr(wy_gather), _ptr(wc),
                                            _ptr(cs), M2, N2, int(out_dtype == torch.bfloat16), _stream()),
            "moe_grouped_gemm_bwd_pair")
     return c, wc, cs
+
+
+def token_bwd_dw(dxp, pos, probs, topk_idx, topk_w, dy, yp, lse, dprob_bias, zc, wg, normalize, want_dw=False):
+    """token_bwd forming dw = <dy[t], yp[pos]> itself (no combine_bwd): -> (dx, dlogits, dw or None)."""
+    T, k = pos.shape
+    E, d = wg.shape
+    _need(dy, torch.bfloat16, "dy")
+    _need(yp, torch.bfloat16, "yp")
+    dx = torch.empty((T, d), dtype=torch.bfloat16, device=wg.device)
+    dlogits = torch.empty((T, E), dtype=torch.float32, device=wg.device)
+    dw = torch.empty((T, k), dtype=torch.float32, device=wg.device) if want_dw else None
+    _check(lib().moe_token_bwd_dw(_ptr(dxp), _ptr(pos), _ptr(probs), _ptr(topk_idx), _ptr(topk_w), None, _ptr(dy),
+                                  _ptr(yp), _ptr(dw), _ptr(lse), _ptr(dprob_bias), _ptr(zc), _ptr(wg), T, d, E, k,
+                                  int(normalize), _ptr(dx), _ptr(dlogits), _stream()), "moe_token_bwd_dw")
+    return dx, dlogits, dw
 
 
 def aux_loss_fwd(auxp, hist, T, k, lb_coef, z_coef):

@@ -7,6 +7,7 @@ local architecture spec (no network fetch), e.g.::
     rtdetr-r50-moe8-top2          C2/C3: R50, 8 experts, top-2, bf16
     rtdetr-r18-moe4-top1          C1: R18, 4 experts, top-1 (CPU plumbing)
     rtdetr-r50-moe16-top2-ep8     C4: 16 experts sharded over 8 ranks
+    rtdetr-r50-moe16-top2-ep8-epcf4    same, all-to-all slots at 4x the mean load
     rtdetr-r50-moe32-top4-cf1.25-fp8   C5: capacity factor 1.25, fp8 experts
     rtdetr-r50                    dense FFN (no MoE)
 """
@@ -30,6 +31,11 @@ class MoEConfig:
     num_contexts: int = 6         # solar bins + missing
     use_context: bool = True
     ep_size: int = 1              # expert-parallel group size (C4)
+    expert_parallel: bool = False  # route through ep.py (set by an -ep<n> spec token, n >= 1)
+    # rows each rank may send to one expert in the fixed-capacity all-to-all, as
+    # a factor of the mean T k / E (layers with capacity_factor > 0 use their
+    # own capacity instead); >= E / k never drops
+    ep_capacity_factor: float = 2.0
     router_init_std: float = 0.02
     ctx_init_scale: float = 0.5
 
@@ -37,6 +43,18 @@ class MoEConfig:
         if self.capacity_factor <= 0:
             return 0
         return int(math.ceil(self.capacity_factor * tokens * self.top_k / self.num_experts))
+
+    def ep_slot_rows(self, tokens: int) -> int:
+        """Rows per (source rank, expert) of the expert-parallel exchange: the
+        layer capacity when it has one, else ceil(ep_capacity_factor T k / E),
+        never more than T (a token sends at most one row to an expert)."""
+        cap = self.capacity(tokens)
+        if cap > 0:
+            return cap
+        f = self.ep_capacity_factor
+        if f <= 0 or f * self.top_k >= self.num_experts:
+            return max(1, tokens)
+        return max(1, min(tokens, int(math.ceil(f * tokens * self.top_k / self.num_experts))))
 
 
 @dataclass
@@ -51,7 +69,7 @@ _SPEC_RE = re.compile(r"^rtdetr-(r18|r34|r50|r101)((?:-[a-z0-9.]+)*)$")
 
 
 def parse_moe_spec(spec: str) -> ModelSpec:
-    """Parse ``rtdetr-<backbone>[-moe<E>][-top<k>][-cf<f>][-fp8][-ep<n>][-dec<L>]``."""
+    """Parse ``rtdetr-<backbone>[-moe<E>][-top<k>][-cf<f>][-fp8][-ep<n>][-epcf<f>][-dec<L>]``."""
     s = spec.strip().lower()
     if s.endswith(".pt") or s.endswith(".pth"):
         raise ValueError(f"{spec!r} is a weights file, not an architecture spec")
@@ -78,9 +96,13 @@ def parse_moe_spec(spec: str) -> ModelSpec:
         elif tok == "noctx":
             moe = moe or MoEConfig()
             moe.use_context = False
+        elif tok.startswith("epcf"):
+            moe = moe or MoEConfig()
+            moe.ep_capacity_factor = float(tok[4:])
         elif tok.startswith("ep"):
             moe = moe or MoEConfig()
             moe.ep_size = int(tok[2:])
+            moe.expert_parallel = True
         elif tok.startswith("dec"):
             out.num_decoder_layers = int(tok[3:])
         else:

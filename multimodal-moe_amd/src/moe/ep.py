@@ -1,21 +1,41 @@
-"""Expert parallelism (BASELINE config C4).
+"""Expert parallelism (BASELINE config C4; SURVEY.md 8(e), 2.2 M9, 7 "EP needs
+per-step variable splits").
 
 E experts are sharded over the W ranks of the expert-parallel group (rank r
 owns experts [r*E/W, (r+1)*E/W)), every rank keeps its own tokens and
 replicated router / non-expert weights (data-parallel, all-reduced by DDP or
-the flat all-reduce of TrainStep).  Per MoE layer:
+the flat all-reduce of TrainStep).
 
-  route + dispatch (all E experts, local tokens)   HIP kernels / eager on CPU
-  counts exchange    all_to_all of the per-expert kept counts (W x E/W ints),
-                     then ONE device->host copy of the split sizes
-  dispatch a2a       all_to_all_single(Xp rows, variable splits) over RCCL/xGMI
-  reorder            src-major -> expert-major rows (one gather)
-  expert FFN         grouped GEMMs on the E/W local experts
-  reorder back, combine a2a (reverse splits), gate-weighted combine
-Backward mirrors it (the a2a Function's backward is the reverse a2a); the
-split sizes of the forward are reused, so the backward never syncs.
+The exchange is FIXED-CAPACITY: every (source rank, expert) pair owns S rows
+of the all-to-all buffers (S = ``MoEConfig.ep_slot_rows(T)``: the layer's
+capacity when it has one, else ceil(ep_capacity_factor T k / E), never more
+than T), so every split size is static and nothing about the routing is read
+on the host.  Per MoE layer:
+
+  route + dispatch      router + scan + permute into the padded send layout:
+                        expert e's kept rows at [e S, e S + min(hist_e, S));
+                        assignments ranked >= S are dropped exactly like
+                        capacity drops (for capacity layers S IS the capacity,
+                        so nothing changes)
+  counts exchange       all_to_all of the kept counts [W, E/W] (device ints)
+  dispatch a2a          all_to_all_single of the [E S, d] rows, equal splits
+  compaction map        on the device from the received counts: compact
+                        expert-major row -> received row (``gather``), its
+                        inverse (``inv``) and the local expert offsets
+  expert FFN            grouped GEMM1 reads the received rows through
+                        ``gather`` (no compaction copy), GEMM2; the output is
+                        put back in the received layout (one row gather)
+  combine a2a           the reverse all_to_all_single, then the gate-weighted
+                        combine at the padded positions
+Backward mirrors it; the transposes of the two row maps are the maps
+themselves (bijections on the valid rows; padding rows are never read).
+With no host sync and static shapes the layer captures into a hipGraph.
+W = 1 (``-ep1``) runs the same code with identity exchanges.
 Expert-weight gradients arrive summed over all ranks' tokens; they are scaled
-by 1/W to match the data-parallel mean of the replicated weights.
+by 1/W (``ep_grad_scale``) to match the data-parallel mean of the replicated
+weights.  Assignments beyond S when the layer has no capacity are counted in
+``layer.last_ep_overflow`` (device scalar; 0 means the result equals the
+single-process layer).
 """
 from __future__ import annotations
 
@@ -23,133 +43,218 @@ import torch
 import torch.distributed as dist
 
 
-class _AllToAll(torch.autograd.Function):
+def _a2a(out, x, group, W):
+    if W == 1 and group is None:  # -ep1 without a process group: identity exchange
+        out.copy_(x)
+    else:
+        dist.all_to_all_single(out, x.contiguous(), group=group)
+    return out
+
+
+class _Exchange(torch.autograd.Function):
+    """Equal-split all_to_all_single of [W * n, ...] rows; its transpose is
+    itself."""
+
     @staticmethod
-    def forward(ctx, x, send, recv, group):
-        out = x.new_empty((sum(recv),) + tuple(x.shape[1:]))
-        dist.all_to_all_single(out, x.contiguous(), output_split_sizes=recv, input_split_sizes=send, group=group)
-        ctx.send, ctx.recv, ctx.group = send, recv, group
-        return out
+    def forward(ctx, x, group, W):
+        ctx.group, ctx.W = group, W
+        return _a2a(torch.empty_like(x), x, group, W)
 
     @staticmethod
     def backward(ctx, g):
-        gi = g.new_empty((sum(ctx.send),) + tuple(g.shape[1:]))
-        dist.all_to_all_single(gi, g.contiguous(), output_split_sizes=ctx.send, input_split_sizes=ctx.recv,
-                               group=ctx.group)
-        return gi, None, None, None
+        return _a2a(torch.empty_like(g), g, ctx.group, ctx.W), None, None
 
 
-class _DispatchMX(torch.autograd.Function):
-    """MXFP8 dispatch exchange (config C5): the e4m3 rows and their exponents
-    cross the all-to-all (d + d/32 bytes per row instead of 2d) and are
-    reordered expert-major; the bf16 gradient of the rows (dXp) takes the
-    reverse path in backward.  ``carrier`` is the zero-stride autograd stand-in
-    of the rows (ops._RouteDispatchMX)."""
+class _RowMap(torch.autograd.Function):
+    """out = x[fwd]; backward dx = dout[bwd].  fwd and bwd are mutually inverse
+    on the valid rows; padding rows carry don't-care values both ways (a
+    scatter-add transpose would fold them into row 0)."""
 
     @staticmethod
-    def forward(ctx, carrier, xq, xs, send, recv, perm, inv, group):
-        n_send, R = sum(send), sum(recv)
-        qr = xq.new_empty((R, xq.shape[1]))
-        sr = xs.new_empty((R, xs.shape[1]))
-        dist.all_to_all_single(qr, xq[:n_send].contiguous(), output_split_sizes=recv, input_split_sizes=send,
-                               group=group)
-        dist.all_to_all_single(sr, xs[:n_send].contiguous(), output_split_sizes=recv, input_split_sizes=send,
-                               group=group)
-        ctx.send, ctx.recv, ctx.group, ctx.rows = send, recv, group, carrier.shape[0]
+    def forward(ctx, x, fwd, bwd):
+        ctx.save_for_backward(bwd)
+        return x.index_select(0, fwd)
+
+    @staticmethod
+    def backward(ctx, g):
+        (bwd,) = ctx.saved_tensors
+        return g.index_select(0, bwd), None, None
+
+
+def compaction_map(recv_cnt: torch.Tensor, S: int):
+    """recv_cnt [W, El] rows received from each source for each local expert,
+    held at received row (src El + e) S + j, j < recv_cnt[src, e].
+    Returns (gather int32 [W El S]: compact expert-major row -> received row,
+    inv int64 [W El S]: received row -> compact row (0 for padding),
+    offsets int32 [El + 1]); static shapes, device ops only."""
+    W, El = recv_cnt.shape
+    dev = recv_cnt.device
+    cnt = recv_cnt.to(torch.int64)
+    per_e = cnt.sum(0)
+    offs = torch.zeros(El + 1, dtype=torch.int64, device=dev)
+    offs[1:] = torch.cumsum(per_e, 0)
+    start = offs[:-1].unsqueeze(0) + torch.cumsum(cnt, 0) - cnt          # [W, El]
+    j = torch.arange(S, device=dev)
+    valid = j.view(1, 1, S) < cnt.unsqueeze(-1)                          # [W, El, S]
+    comp = start.unsqueeze(-1) + j.view(1, 1, S)
+    R = W * El * S
+    dst = torch.where(valid, comp, torch.full_like(comp, R)).reshape(-1)
+    gather = torch.zeros(R + 1, dtype=torch.int64, device=dev)
+    gather.scatter_(0, dst, torch.arange(R, device=dev))
+    inv = torch.where(valid, comp, torch.zeros_like(comp)).reshape(-1)
+    return gather[:R].to(torch.int32).contiguous(), inv.contiguous(), offs.to(torch.int32).contiguous()
+
+
+def _exchange_counts(kept, group, W):
+    """kept [W, El] rows this rank sends to each (peer, expert) -> what it
+    receives, device-resident."""
+    kept = kept.to(torch.int64).contiguous()
+    return _a2a(torch.empty_like(kept), kept, group, W)
+
+
+class _EPExpertFFN(torch.autograd.Function):
+    """The local experts over the received rows, in the received layout.
+    Forward: GEMM1 gathers xr[gather] (+b1, ReLU), GEMM2 (+b2), then the
+    output rows are put back at their received positions (row gather by inv).
+    Backward: the first paired launch reads dYp = dyr[gather] inside the
+    GEMMs, the second gathers xr[gather] for dW1; dxr = dXp[inv]."""
+
+    @staticmethod
+    def forward(ctx, xr, gather, inv, w1, b1, w2, b2, offsets, grad_scale):
+        from . import _lib as L
+
+        G, F, d = w1.shape
+        R = xr.shape[0]
+        xb = xr.to(torch.bfloat16).contiguous()
+        w1b = w1.to(torch.bfloat16).contiguous()
+        w2b = w2.to(torch.bfloat16).contiguous()
+        h = L.grouped_gemm_gather(xb, gather, w1b, offsets, G, R, F, d, 1, L.EPI_BIAS_RELU,
+                                  bias=b1.float().contiguous())
+        ye = L.grouped_gemm(h, w2b, offsets, G, R, d, F, 1, L.EPI_BIAS, bias=b2.float().contiguous())
+        ctx.save_for_backward(xb, gather, inv, h, w1b, w2b, offsets)
+        ctx.meta = (G, R, float(grad_scale), xr.dtype)
+        ctx.wdtype = w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32
+        return ye.index_select(0, inv)
+
+    @staticmethod
+    def backward(ctx, dyr):
+        from . import _lib as L
+
+        xb, gather, inv, h, w1b, w2b, offsets = ctx.saved_tensors
+        G, R, s, xdtype = ctx.meta
+        F, d = w1b.shape[1], w1b.shape[2]
+        odt = torch.bfloat16 if ctx.wdtype == torch.bfloat16 else torch.float32
+        dyb = dyr.to(torch.bfloat16).contiguous()
+        dh, dW2, db2 = L.grouped_gemm_bwd_pair(dyb, w2b, offsets, G, R, F, d, L.EPI_RELU_MASK, h, dyb, h,
+                                               out_dtype=odt, a_gather=gather, wx_gather=gather)
+        dxe, dW1, db1 = L.grouped_gemm_bwd_pair(dh, w1b, offsets, G, R, d, F, L.EPI_NONE, None, dh, xb, gather,
+                                                out_dtype=odt)
+        if s != 1.0:
+            for t in (dW1, db1, dW2, db2):
+                t.mul_(s)
+        return dxe.index_select(0, inv).to(xdtype), None, None, dW1, db1, dW2, db2, None, None
+
+
+class _CarrierExchange(torch.autograd.Function):
+    """MXFP8 path: the routed rows cross as e4m3 + exponents (non-differentiable
+    uint8); this node stands for them in the autograd graph.  Forward: a
+    zero-stride bf16 carrier of the compact rows; backward: the compact dXp is
+    put back in the received layout (inv), then sent home by the reverse
+    exchange as the gradient of the sender's padded carrier."""
+
+    @staticmethod
+    def forward(ctx, carrier, inv, group, W):
         ctx.save_for_backward(inv)
-        ce = torch.zeros((1, 1), dtype=carrier.dtype, device=carrier.device).expand(R, carrier.shape[1])
-        ctx.mark_non_differentiable(qr, sr)
-        return ce, qr.index_select(0, perm), sr.index_select(0, perm)
+        ctx.group, ctx.W = group, W
+        return torch.zeros((1, 1), dtype=carrier.dtype, device=carrier.device).expand(inv.shape[0],
+                                                                                      carrier.shape[1])
 
     @staticmethod
-    def backward(ctx, g, _q, _s):
+    def backward(ctx, g):
         (inv,) = ctx.saved_tensors
         gr = g.index_select(0, inv).contiguous()
-        gi = g.new_zeros((ctx.rows, g.shape[1]))
-        dist.all_to_all_single(gi[:sum(ctx.send)], gr, output_split_sizes=ctx.send, input_split_sizes=ctx.recv,
-                               group=ctx.group)
-        return gi, None, None, None, None, None, None, None
+        return _a2a(torch.empty_like(gr), gr, ctx.group, ctx.W), None, None, None
 
 
-def expert_major_order(recv_mat: torch.Tensor):
-    """recv_mat [W, El] (host) rows received from each source for each local
-    expert, laid out source-major.  Returns (perm, offsets) with
-    rows_expert_major = rows_src_major[perm] and offsets [El+1]."""
-    W, El = recv_mat.shape
-    cnt = recv_mat.tolist()
-    start = [[0] * El for _ in range(W)]
-    s = 0
-    for src in range(W):
-        for e in range(El):
-            start[src][e] = s
-            s += cnt[src][e]
-    segs, offs = [], [0]
-    for e in range(El):
-        for src in range(W):
-            if cnt[src][e]:
-                segs.append(torch.arange(start[src][e], start[src][e] + cnt[src][e]))
-        offs.append(offs[-1] + sum(cnt[src][e] for src in range(W)))
-    perm = torch.cat(segs) if segs else torch.zeros(0, dtype=torch.int64)
-    return perm, torch.tensor(offs, dtype=torch.int32)
+def _padded_positions(idx, E, S):
+    """CPU dispatch into the fixed-capacity layout: pos = e S + rank (slot-major,
+    token-ordered rank inside expert e, as eager.dispatch_positions), -1 when
+    rank >= S; and the full histogram."""
+    T, k = idx.shape
+    flat = idx.t().reshape(-1)
+    order = torch.sort(flat, stable=True).indices
+    hist = torch.bincount(flat, minlength=E)
+    starts = torch.cumsum(hist, 0) - hist
+    rank_sorted = torch.arange(flat.numel(), device=idx.device) - starts[flat[order]]
+    rank = torch.empty_like(flat)
+    rank[order] = rank_sorted
+    rank = rank.view(k, T).t()
+    pos = torch.where(rank < S, idx * S + rank, torch.full_like(rank, -1))
+    return pos, hist
+
+
+def _route_padded_eager(x, wg, ctx_bias, ctx_img, tpi, k, normalize, S):
+    from .eager import route
+
+    T, d = x.shape
+    E = wg.shape[0]
+    probs, lse, idx, w = route(x, wg, ctx_bias, ctx_img, tpi, k, normalize)
+    pos, hist = _padded_positions(idx, E, S)
+    keep = pos >= 0
+    t_idx = torch.arange(T, device=x.device).unsqueeze(1).expand(T, k)[keep]
+    xp = torch.zeros((E * S, d), dtype=x.dtype, device=x.device).index_copy(0, pos[keep], x[t_idx])
+    f = hist.float() / float(max(T * k, 1))
+    lb = E * (f * probs.mean(0)).sum()
+    z = (lse ** 2).mean()
+    return xp, w, lb, z, pos, hist.to(torch.int32)
 
 
 def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap):
+    """-> (y [T, d], lb, z, hist [E]) of one expert-parallel MoE layer."""
     cfg = layer.cfg
     E, W, k = cfg.num_experts, layer.ep_size, cfg.top_k
     El = E // W
     group = layer.ep_group
-    T = x.shape[0]
-    dev = x.device
-    mx = x.is_cuda and cfg.expert_dtype == "fp8"
+    T, d = x.shape
+    S = cfg.ep_slot_rows(T)
+    if cap > 0 and S != cap:
+        raise ValueError(f"EP slot rows {S} must equal the layer capacity {cap}")
+    fp8 = cfg.expert_dtype == "fp8"
     gs = getattr(layer, "ep_grad_scale", 1.0 / W)  # 1.0 when the optimizer applies 1/W (graph-mode TrainStep)
-    if mx:
-        from .ops import aux_losses, combine_hip as combine, expert_ffn_mx_hip, route_dispatch_mx_hip
-
-        xp, w, auxp, pos, hist, offsets, xq, xs, rows = route_dispatch_mx_hip(
-            x, layer.wg, ctx_bias, ctx_img, tokens_per_image, k, cfg.normalize, cap)
-        lb, z = aux_losses(auxp, hist, T, k)
-    elif x.is_cuda:
-        from .ops import aux_losses, combine_hip as combine, expert_ffn_hip as expert_ffn, route_dispatch_hip
-
-        xp, w, auxp, pos, hist, offsets, rows = route_dispatch_hip(x, layer.wg, ctx_bias, ctx_img, tokens_per_image,
-                                                                   k, cfg.normalize, cap)
-        lb, z = aux_losses(auxp, hist, T, k)
-    else:
-        from .eager import combine_eager as combine, expert_ffn_eager, expert_ffn_mx_eager, route_dispatch_eager
-
-        expert_ffn = expert_ffn_mx_eager if cfg.expert_dtype == "fp8" else expert_ffn_eager
-
-        xp, w, lb, z, pos, hist, offsets, rows = route_dispatch_eager(x, layer.wg, ctx_bias, ctx_img,
-                                                                      tokens_per_image, k, cfg.normalize, cap)
-    kept = (offsets[1:] - offsets[:-1]).to(torch.int64).view(W, El).contiguous()
-    recv_mat = torch.empty_like(kept)
-    dist.all_to_all_single(recv_mat, kept, group=group)
-    host = torch.cat([kept.sum(1), recv_mat.reshape(-1)]).cpu()  # the one host sync of the layer
-    send = [int(v) for v in host[:W].tolist()]
-    recv_h = host[W:].view(W, El)
-    recv = [int(v) for v in recv_h.sum(1).tolist()]
-    n_send, R = sum(send), sum(recv)
-
-    perm, offs_l = expert_major_order(recv_h)
-    perm = perm.to(dev, non_blocking=True)
-    inv = torch.empty_like(perm)
-    inv[perm] = torch.arange(perm.numel(), device=dev)
-    offs_l = offs_l.to(dev, non_blocking=True)
-    if mx:
-        ce, qe, se = _DispatchMX.apply(xp, xq, xs, send, recv, perm, inv, group)
-        ye = expert_ffn_mx_hip(ce, qe, se, layer.w1, layer.b1, layer.w2, layer.b2, offs_l, R, gs) if R else \
-            x.new_zeros((0, x.shape[1]), dtype=torch.bfloat16)
-        yr = ye.index_select(0, inv)
-        yp = _AllToAll.apply(yr, recv, send, group)
-        return combine(yp, w, pos, T), lb, z, hist
-    xr = _AllToAll.apply(xp[:n_send], send, recv, group)
-    xe = xr.index_select(0, perm)
     if x.is_cuda:
-        ye = expert_ffn(xe, layer.w1, layer.b1, layer.w2, layer.b2, offs_l, R, gs) if R else \
-            xe.new_zeros((0, x.shape[1]))
+        from .ops import aux_losses, combine_hip as combine
+        from .ops import expert_ffn_mx_hip, route_dispatch_hip, route_dispatch_mx_hip
+
+        if fp8:
+            carrier, w, auxp, pos, hist, _, xq, xs, _ = route_dispatch_mx_hip(
+                x, layer.wg, ctx_bias, ctx_img, tokens_per_image, k, cfg.normalize, cap, pad=S)
+        else:
+            xp, w, auxp, pos, hist, _, _ = route_dispatch_hip(x, layer.wg, ctx_bias, ctx_img, tokens_per_image, k,
+                                                              cfg.normalize, cap, pad=S)
+        lb, z = aux_losses(auxp, hist, T, k)
     else:
-        ye = expert_ffn(xe, layer.w1, layer.b1, layer.w2, layer.b2, offs_l, gs)
-    yr = ye.index_select(0, inv)
-    yp = _AllToAll.apply(yr, recv, send, group)
-    y = combine(yp, w, pos, T)
-    return y, lb, z, hist
+        from .eager import combine_eager as combine, expert_ffn_eager, expert_ffn_mx_eager
+
+        xp, w, lb, z, pos, hist = _route_padded_eager(x, layer.wg, ctx_bias, ctx_img, tokens_per_image, k,
+                                                      cfg.normalize, S)
+    recv_cnt = _exchange_counts(hist.clamp(max=S).view(W, El), group, W)
+    gather, inv, offs = compaction_map(recv_cnt, S)
+    layer.last_ep_overflow = (hist.to(torch.int64) - S).clamp(min=0).sum() if cap <= 0 else None
+    if x.is_cuda and fp8:
+        qr = _a2a(torch.empty_like(xq), xq, group, W)
+        sr = _a2a(torch.empty_like(xs), xs, group, W)
+        ce = _CarrierExchange.apply(carrier, inv, group, W)
+        ye = expert_ffn_mx_hip(ce, qr.index_select(0, gather), sr.index_select(0, gather), layer.w1, layer.b1,
+                               layer.w2, layer.b2, offs, W * El * S, gs)
+        yr = _RowMap.apply(ye, inv, gather)
+    elif x.is_cuda:
+        xr = _Exchange.apply(xp, group, W)
+        yr = _EPExpertFFN.apply(xr, gather, inv, layer.w1, layer.b1, layer.w2, layer.b2, offs, gs)
+    else:
+        xr = _Exchange.apply(xp, group, W)
+        xe = _RowMap.apply(xr, gather, inv)
+        ffn = expert_ffn_mx_eager if fp8 else expert_ffn_eager
+        ye = ffn(xe, layer.w1, layer.b1, layer.w2, layer.b2, offs, gs)
+        yr = _RowMap.apply(ye, inv, gather)
+    yp = _Exchange.apply(yr, group, W)
+    return combine(yp, w, pos, T), lb, z, hist

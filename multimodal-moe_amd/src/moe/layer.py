@@ -52,6 +52,7 @@ class MoEFFN(nn.Module):
         self.last_aux = None   # (lb_raw, z_raw) of the last forward
         self.last_aux_weighted = None  # lb_coef lb + z_coef z (GPU path: fused kernel, differentiable)
         self.last_hist = None  # int32 [E] expert histogram of the last forward
+        self.last_ep_overflow = None  # EP without capacity: assignments beyond the a2a slots (device)
 
     def forward(self, x: torch.Tensor, ctx_img: torch.Tensor | None) -> torch.Tensor:
         """x [B, L, d] (image-major tokens), ctx_img int [B] -> [B, L, d]."""
@@ -62,7 +63,7 @@ class MoEFFN(nn.Module):
         cap = cfg.capacity(T)
         cb = self.ctx_bias if (self.ctx_bias is not None and ctx_img is not None) else None
         ci = ctx_img.to(torch.int32).contiguous() if cb is not None else None
-        if self.ep_size > 1:  # C4: experts sharded over ranks, all-to-all token exchange
+        if self.ep_size > 1 or cfg.expert_parallel:  # C4: experts sharded over ranks, all-to-all exchange
             from .ep import moe_ffn_ep
 
             y, lb, z, hist = moe_ffn_ep(self, flat, cb, ci, L, cap)

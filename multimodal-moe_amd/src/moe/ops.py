@@ -1,9 +1,11 @@
 """autograd wrappers of the HIP MoE FFN.
 
-One layer = three autograd Functions over the C-ABI kernels:
-  _RouteIndex     router + top-k + aux partials (K1), route_scan, route_index
-                  (K2's index half: pos and the row -> token map; the routed
-                  rows are never copied)
+Single-GPU bf16 layers run as ONE autograd node, _MoELayer (8 HIP launches
+forward + backward, see its docstring).  The building blocks below remain
+for the MXFP8 (C5) and expert-parallel (C4) compositions:
+  _RouteIndex     router + top-k + aux partials (K1), then route_dispatch: the
+                  scan, K2's index half (pos and the row -> token map; the
+                  routed rows are never copied) and the aux losses, one launch
                   backward: token_bwd (dispatch transpose + router backward)
   _ExpertFFNGather grouped GEMM1 (+b1, ReLU) reading the token rows through
                   the row map, GEMM2 (+b2)
@@ -11,8 +13,8 @@ One layer = three autograd Functions over the C-ABI kernels:
                   {dH = dgrad (ReLU mask), dW2 + db2} and {dXp = dgrad, dW1 + db1
                   with the token rows gathered}
   _Combine        gate-weighted combine (K3); backward: combine_bwd
-Single GPU: 6 launches forward (router, scan, index, GEMM1, GEMM2, combine),
-4 backward (combine_bwd, 2 pairs, token_bwd) + 1 torch GEMM for dWg.  The
+Single GPU: 5 launches forward (router, route_dispatch, GEMM1, GEMM2,
+combine), 4 backward (combine_bwd, 2 pairs, token_bwd) + 1 torch GEMM for dWg.  The
 expert-parallel path (ep.py) moves real rows through its all-to-alls and runs
 _RouteDispatch (permute) + _ExpertFFN (rows in, same paired backward).  Nothing is synchronised with the host: expert
 offsets stay on the device, grids are sized from host upper bounds, and the
@@ -32,9 +34,18 @@ import torch
 from . import _lib as L
 
 
+def _padded_offsets(E, pad, device):
+    """Expert e's rows start at e * pad (the fixed-capacity layout of ep.py)."""
+    return (torch.arange(E + 1, dtype=torch.int32, device=device) * int(pad)).contiguous()
+
+
 class _RouteDispatch(torch.autograd.Function):
+    """Router + scan + permute (rows copied).  ``pad`` > 0: the fixed-capacity
+    layout of the expert-parallel send buffer -- expert e's kept rows at
+    [e pad, e pad + min(hist_e, pad)), assignments ranked >= pad dropped."""
+
     @staticmethod
-    def forward(ctx, x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, rows):
+    def forward(ctx, x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, rows, pad=0):
         T, d = x.shape
         E = wg.shape[0]
         xb = x.to(torch.bfloat16).contiguous()
@@ -43,6 +54,8 @@ class _RouteDispatch(torch.autograd.Function):
         idx, w, probs, lse, lrank, bcnt, auxp = L.router_topk_fwd(xb, wg32, cb, ctx_img, tokens_per_image, k,
                                                                    normalize)
         rank_base, hist, offsets = L.route_scan(bcnt, cap)
+        if pad:
+            offsets, cap = _padded_offsets(E, pad, x.device), pad
         xp, pos = L.permute_fwd(xb, idx, lrank, rank_base, offsets, E, cap, rows)
         ctx.save_for_backward(xb, wg32, idx, w, probs, lse, pos,
                               ctx_img if ctx_img is not None else torch.empty(0))
@@ -74,7 +87,7 @@ class _RouteDispatch(torch.autograd.Function):
         if has_ctx:
             dcb = torch.zeros((C, E), dtype=torch.float32, device=dev)
             dcb.index_add_(0, ctx_img.long(), dlogits.view(-1, tpi, E).sum(1))
-        return dx.to(xdtype), dwg, dcb, None, None, None, None, None, None
+        return dx.to(xdtype), dwg, dcb, None, None, None, None, None, None, None
 
 
 class _RouteDispatchMX(torch.autograd.Function):
@@ -84,7 +97,7 @@ class _RouteDispatchMX(torch.autograd.Function):
     that dXp (from _ExpertFFNMX.backward) reaches the dispatch transpose."""
 
     @staticmethod
-    def forward(ctx, x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, rows):
+    def forward(ctx, x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, rows, pad=0):
         T, d = x.shape
         E = wg.shape[0]
         xb = x.to(torch.bfloat16).contiguous()
@@ -93,6 +106,8 @@ class _RouteDispatchMX(torch.autograd.Function):
         idx, w, probs, lse, lrank, bcnt, auxp = L.router_topk_fwd(xb, wg32, cb, ctx_img, tokens_per_image, k,
                                                                    normalize)
         rank_base, hist, offsets = L.route_scan(bcnt, cap)
+        if pad:
+            offsets, cap = _padded_offsets(E, pad, x.device), pad
         xq, xs, pos = L.permute_fwd_mx(xb, idx, lrank, rank_base, offsets, E, cap, rows)
         carrier = torch.zeros((1, 1), dtype=torch.bfloat16, device=x.device).expand(xq.shape[0], d)
         ctx.save_for_backward(xb, wg32, idx, w, probs, lse, pos,
@@ -114,7 +129,7 @@ class _RouteIndex(torch.autograd.Function):
     (from _ExpertFFNGather.backward) reaches the dispatch transpose."""
 
     @staticmethod
-    def forward(ctx, x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, rows):
+    def forward(ctx, x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, rows, lb_coef, z_coef):
         T, d = x.shape
         E = wg.shape[0]
         xb = x.to(torch.bfloat16).contiguous()
@@ -122,19 +137,42 @@ class _RouteIndex(torch.autograd.Function):
         cb = ctx_bias.float().contiguous() if ctx_bias is not None else None
         idx, w, probs, lse, lrank, bcnt, auxp = L.router_topk_fwd(xb, wg32, cb, ctx_img, tokens_per_image, k,
                                                                    normalize)
-        rank_base, hist, offsets = L.route_scan(bcnt, cap)
-        pos, tok = L.route_index(idx, lrank, rank_base, offsets, E, cap, rows)
+        # scan + index (+ aux losses) in one launch (moe_route_dispatch)
+        pos, tok, hist, offsets, _, out3, wcoef = L.route_dispatch(bcnt, idx, lrank, w, auxp, T, E, cap, rows,
+                                                                   lb_coef, z_coef)
+        if out3 is None:
+            out3 = torch.zeros(3, dtype=torch.float32, device=x.device)
+            wcoef = torch.zeros(E + 1, dtype=torch.float32, device=x.device)
         carrier = torch.zeros((1, 1), dtype=torch.bfloat16, device=x.device).expand(max(rows, 1), d)
         ctx.save_for_backward(xb, wg32, idx, w, probs, lse, pos,
                               ctx_img if ctx_img is not None else torch.empty(0))
         ctx.meta = (T, d, E, int(normalize), tokens_per_image, cb is not None, x.dtype,
                     ctx_bias.shape[0] if ctx_bias is not None else 0)
-        ctx.mark_non_differentiable(pos, hist, offsets, tok)
-        return carrier, w, auxp, pos, hist, offsets, tok
+        ctx.mark_non_differentiable(pos, hist, offsets, tok, out3, wcoef)
+        return carrier, w, auxp, pos, hist, offsets, tok, out3, wcoef
 
     @staticmethod
-    def backward(ctx, d_xp, d_w, d_auxp, _p, _h, _o, _t):
-        return _RouteDispatch.backward(ctx, d_xp, d_w, d_auxp, _p, _h, _o)
+    def backward(ctx, d_xp, d_w, d_auxp, _p, _h, _o, _t, _a, _c):
+        return _RouteDispatch.backward(ctx, d_xp, d_w, d_auxp, _p, _h, _o)[:9] + (None, None)
+
+
+class _AuxFused(torch.autograd.Function):
+    """The layer's weighted aux loss computed by moe_route_dispatch (out3 =
+    (lb, z, lb_coef lb + z_coef z), wcoef = its gradient w.r.t. one router
+    block's partials); backward = g * wcoef broadcast over the blocks."""
+
+    @staticmethod
+    def forward(ctx, auxp, out3, wcoef):
+        ctx.save_for_backward(wcoef)
+        ctx.nblk = auxp.shape[0]
+        raw = out3[:2].clone()
+        ctx.mark_non_differentiable(raw)
+        return out3[2].clone(), raw
+
+    @staticmethod
+    def backward(ctx, g, _raw):
+        (wcoef,) = ctx.saved_tensors
+        return (g * wcoef).view(1, -1).expand(ctx.nblk, -1), None, None
 
 
 def _ffn_backward(dyp, h, w1b, w2b, offsets, G, rows, xrows, tok, wdtype, s):
@@ -287,30 +325,127 @@ def aux_losses(auxp, hist, T, k):
     return lb, z
 
 
-def route_dispatch_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap):
+def route_dispatch_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, pad=0):
+    """-> (xp, w, auxp, pos, hist, offsets, rows); pad > 0: fixed-capacity
+    layout (rows = E pad, offsets = e pad; see _RouteDispatch)."""
     T = x.shape[0]
     E = wg.shape[0]
-    rows = T * k if cap <= 0 else min(T * k, E * cap)
+    rows = E * pad if pad else (T * k if cap <= 0 else min(T * k, E * cap))
     return _RouteDispatch.apply(x, wg, ctx_bias, ctx_img, int(tokens_per_image), int(k), bool(normalize), int(cap),
-                                rows) + (rows,)
+                                rows, int(pad)) + (rows,)
 
 
-def route_dispatch_mx_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap):
+def route_dispatch_mx_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, pad=0):
     """-> (carrier, w, auxp, pos, hist, offsets, xq, xs, rows): MXFP8 dispatch."""
     T = x.shape[0]
     E = wg.shape[0]
-    rows = T * k if cap <= 0 else min(T * k, E * cap)
+    rows = E * pad if pad else (T * k if cap <= 0 else min(T * k, E * cap))
     return _RouteDispatchMX.apply(x, wg, ctx_bias, ctx_img, int(tokens_per_image), int(k), bool(normalize),
-                                  int(cap), rows) + (rows,)
+                                  int(cap), rows, int(pad)) + (rows,)
 
 
-def route_index_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap):
-    """-> (carrier, w, auxp, pos, hist, offsets, tok, rows): dispatch without the row copy."""
+class _MoELayer(torch.autograd.Function):
+    """The whole single-GPU bf16 routed FFN of one layer as ONE autograd node
+    (SURVEY 8(a) rows a2-a7), 8 HIP launches forward + backward:
+      forward  router_topk_fwd; route_dispatch (scan, index, row gates, aux
+               losses); GEMM1 reading token rows through the row map (+b1,
+               ReLU); GEMM2 (+b2); combine
+      backward bwd_pair {dH = gate * (dy[token] W2) * (H > 0), dW2 = dYp^T H,
+               db2} with dYp = gate * dy[token] formed inside the GEMMs (no
+               combine transpose launch); bwd_pair {dXp = dH W1, dW1 = dH^T
+               x[token], db1}; token_bwd_dw (gate gradient <dy, Yp>, router
+               softmax / top-k / aux / z-loss backward, dx)
+    plus the router weight gradient dlogits^T x (one torch GEMM) and the
+    context-bias gradient (index_add).  Outputs: y, then (weighted=True) the
+    layer's lb_coef lb + z_coef z and the detached raw (lb, z), or
+    (weighted=False) lb and z as separate differentiable outputs; hist."""
+
+    @staticmethod
+    def forward(ctx, x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tpi, k, normalize, cap, lb_coef, z_coef, weighted):
+        T, d = x.shape
+        E = wg.shape[0]
+        G, F, _ = w1.shape
+        rows = T * k if cap <= 0 else min(T * k, E * cap)
+        xb = x.to(torch.bfloat16).contiguous()
+        wg32 = wg.float().contiguous()
+        cb = ctx_bias.float().contiguous() if ctx_bias is not None else None
+        idx, w, probs, lse, lrank, bcnt, auxp = L.router_topk_fwd(xb, wg32, cb, ctx_img, tpi, k, normalize)
+        pos, tok, hist, offsets, gate, out3, wcoef = L.route_dispatch(bcnt, idx, lrank, w, auxp, T, E, cap, rows,
+                                                                      lb_coef, z_coef, row_gate=True)
+        w1b = w1.to(torch.bfloat16).contiguous()
+        w2b = w2.to(torch.bfloat16).contiguous()
+        h = L.grouped_gemm_gather(xb, tok, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU,
+                                  bias=b1.float().contiguous())
+        yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=b2.float().contiguous())
+        y = L.combine_fwd(yp, pos, w, T)
+        ctx.save_for_backward(xb, wg32, idx, w, probs, lse, pos, tok, gate, h, yp, w1b, w2b, offsets, wcoef,
+                              ctx_img if ctx_img is not None else torch.empty(0))
+        ctx.meta = (T, d, E, G, rows, int(normalize), tpi, cb is not None,
+                    ctx_bias.shape[0] if ctx_bias is not None else 0, weighted)
+        ctx.dtypes = (x.dtype, w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32)
+        ctx.mark_non_differentiable(hist)
+        if weighted:
+            raw = out3[:2].clone()
+            ctx.mark_non_differentiable(raw)
+            return y.to(x.dtype), out3[2].clone(), raw, hist
+        return y.to(x.dtype), out3[0].clone(), out3[1].clone(), hist
+
+    @staticmethod
+    def backward(ctx, dy, g_a, g_b, _h):
+        (xb, wg32, idx, w, probs, lse, pos, tok, gate, h, yp, w1b, w2b, offsets, wcoef,
+         ctx_img) = ctx.saved_tensors
+        T, d, E, G, rows, normalize, tpi, has_ctx, C, weighted = ctx.meta
+        xdtype, wdtype = ctx.dtypes
+        F = w1b.shape[1]
+        odt = torch.bfloat16 if wdtype == torch.bfloat16 else torch.float32
+        if dy is None:
+            dy = torch.zeros((T, d), dtype=torch.bfloat16, device=xb.device)
+        dyb = dy.to(torch.bfloat16).contiguous()
+        dh, dW2, db2 = L.grouped_gemm_bwd_pair(dyb, w2b, offsets, G, rows, F, d, L.EPI_RELU_MASK, h, dyb, h,
+                                               out_dtype=odt, a_gather=tok, row_scale=gate, wx_gather=tok,
+                                               wx_scale=gate)
+        dxp, dW1, db1 = L.grouped_gemm_bwd_pair(dh, w1b, offsets, G, rows, d, F, L.EPI_NONE, None, dh, xb, tok,
+                                                out_dtype=odt)
+        # aux-loss gradients as device tensors (no host sync): the router
+        # partials' gradient is uniform over blocks (moe_route_dispatch wcoef)
+        if weighted:
+            if g_a is not None:
+                coef = g_a.float() * wcoef
+                dprob_bias, zc = coef[:E].contiguous(), (2.0 * coef[E:E + 1]).contiguous()
+            else:
+                dprob_bias, zc = None, None
+        else:
+            # wcoef holds d lb / d partials (lb_coef = 1) and d z / d partials (z_coef = 1)
+            dprob_bias = (g_a.float() * wcoef[:E]).contiguous() if g_a is not None else None
+            zc = (2.0 * g_b.float() * wcoef[E:E + 1]).contiguous() if g_b is not None else None
+        dx, dlogits, _ = L.token_bwd_dw(dxp, pos, probs, idx, w, dyb, yp, lse, dprob_bias, zc, wg32, normalize)
+        dwg = dlogits.t().mm(xb.float())
+        dcb = None
+        if has_ctx:
+            dcb = torch.zeros((C, E), dtype=torch.float32, device=dy.device)
+            dcb.index_add_(0, ctx_img.long(), dlogits.view(-1, tpi, E).sum(1))
+        return (dx.to(xdtype), dwg, dcb, dW1, db1, dW2, db2) + (None,) * 8
+
+
+def moe_layer_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap, aux_coefs=None):
+    """_MoELayer: -> (y, lb_coef lb + z_coef z, raw (lb, z), hist) with aux_coefs,
+    else (y, lb, z, hist)."""
+    if aux_coefs is not None:
+        return _MoELayer.apply(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, int(tokens_per_image), int(k),
+                               bool(normalize), int(cap), float(aux_coefs[0]), float(aux_coefs[1]), True)
+    return _MoELayer.apply(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, int(tokens_per_image), int(k), bool(normalize),
+                           int(cap), 1.0, 1.0, False)
+
+
+def route_index_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, aux_coefs=None):
+    """-> (carrier, w, auxp, pos, hist, offsets, tok, out3, wcoef, rows): dispatch
+    without the row copy; out3 / wcoef are the fused aux loss (aux_coefs given)."""
     T = x.shape[0]
     E = wg.shape[0]
     rows = T * k if cap <= 0 else min(T * k, E * cap)
+    lb, z = aux_coefs if aux_coefs is not None else (None, None)
     return _RouteIndex.apply(x, wg, ctx_bias, ctx_img, int(tokens_per_image), int(k), bool(normalize), int(cap),
-                             rows) + (rows,)
+                             rows, lb, z) + (rows,)
 
 
 def expert_ffn_gather_hip(carrier, xb, tok, w1, b1, w2, b2, offsets, rows, grad_scale=1.0):
@@ -353,10 +488,8 @@ def moe_ffn_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, n
             x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap)
         yp = expert_ffn_mx_hip(carrier, xq, xs, w1, b1, w2, b2, offsets, rows)
     else:
-        carrier, w, auxp, pos, hist, offsets, tok, rows = route_index_hip(x, wg, ctx_bias, ctx_img, tokens_per_image,
-                                                                          k, normalize, cap)
-        xb = x.detach().to(torch.bfloat16).contiguous()
-        yp = expert_ffn_gather_hip(carrier, xb, tok, w1, b1, w2, b2, offsets, rows)
+        return moe_layer_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap,
+                             aux_coefs)
     y = combine_hip(yp, w, pos, T)
     if aux_coefs is not None:
         aux, raw = aux_loss_weighted(auxp, hist, T, k, *aux_coefs)

@@ -20,6 +20,7 @@ import os
 import random
 import time
 from dataclasses import asdict, dataclass, field
+from datetime import timedelta
 from pathlib import Path
 
 import numpy as np
@@ -326,6 +327,8 @@ def _moe_stats(model: RTDETRMoE) -> dict:
         if m.last_hist is not None:
             h = m.last_hist.detach().float().cpu()
             out[f"moe/l{i}_load_cv"] = float(h.std() / h.mean().clamp(min=1e-9))
+        if getattr(m, "last_ep_overflow", None) is not None:
+            out[f"moe/l{i}_ep_overflow"] = int(m.last_ep_overflow)
         if m.last_aux is not None:
             out[f"moe/l{i}_lb"] = float(m.last_aux[0].detach())
             out[f"moe/l{i}_z"] = float(m.last_aux[1].detach())
@@ -337,7 +340,9 @@ def _mp_entry(local_idx, a, devices, port, out_file):
                        "WORLD_SIZE": str(len(devices)), "LOCAL_RANK": str(local_idx)})
     dev = devices[local_idx]
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    # collective timeout: a dead rank fails the run instead of hanging it
+    dist.init_process_group("nccl", device_id=torch.device("cuda", dev),
+                            timeout=timedelta(seconds=float(os.environ.get("MOE_DIST_TIMEOUT_S", "1800"))))
     try:
         res = _train_worker(a, local_idx, len(devices), dev)
         if local_idx == 0 and res is not None:

@@ -444,3 +444,41 @@ def test_route_index_matches_permute(hip_lib, T, E, k, cf):
     assert torch.equal(pos, pos2)
     R = int(offsets[-1])
     assert torch.equal(x[tok[:R].long()], xp[:R])
+
+
+@pytest.mark.parametrize("T,E,k,cf", [(1000, 8, 2, 0.0), (777, 16, 2, 0.0), (640, 32, 4, 1.25), (1, 4, 1, 0.0),
+                                      (14720, 32, 4, 1.25), (300, 64, 8, 0.0), (1300, 8, 2, 1.25)])
+def test_route_dispatch_matches_scan_index_aux(hip_lib, T, E, k, cf):
+    """moe_route_dispatch (one launch) == route_scan + route_index +
+    aux_loss_fwd: integer outputs bit-exact, aux losses and their gradient
+    coefficients equal (same fixed-order sums), row gates = topk_w at pos."""
+    from src.moe import _lib as L
+
+    tpi = max(T // 4, 1)
+    c = make_case(T, 256, E, 1024, k, tpi, 37) if T <= 2000 else None
+    if c is None:  # C5 encoder size: unfiltered random inputs
+        g = torch.Generator(device=DEV).manual_seed(3)
+        x = torch.randn((T, 256), device=DEV, generator=g).to(torch.bfloat16)
+        wg = torch.randn((E, 256), device=DEV, generator=g) * 0.02
+        cb = torch.randn((6, E), device=DEV, generator=g) * 0.5
+        ci = torch.randint(0, 6, ((T + tpi - 1) // tpi,), device=DEV, generator=g).int()
+    else:
+        x = _bf16(c["x"]).to(DEV)
+        wg = torch.from_numpy(c["wg"]).float().to(DEV)
+        cb = torch.from_numpy(c["ctx_bias"]).float().to(DEV)
+        ci = torch.from_numpy(c["ctx_img"]).to(DEV)
+    cap = _cap(T, k, E, cf)
+    idx, w, probs, lse, lrank, bcnt, auxp = L.router_topk_fwd(x, wg, cb, ci, tpi, k, True)
+    rank_base, hist, offsets = L.route_scan(bcnt, cap)
+    rows = T * k if cap <= 0 else min(T * k, E * cap)
+    pos, tok = L.route_index(idx, lrank, rank_base, offsets, E, cap, rows)
+    out, wcoef = L.aux_loss_fwd(auxp, hist, T, k, 1e-2, 1e-3)
+    pos2, tok2, hist2, off2, gate2, out2, wcoef2 = L.route_dispatch(bcnt, idx, lrank, w, auxp, T, E, cap, rows,
+                                                                    1e-2, 1e-3, row_gate=True)
+    torch.cuda.synchronize()
+    R = int(offsets[-1])
+    assert torch.equal(hist, hist2) and torch.equal(offsets, off2) and torch.equal(pos, pos2)
+    assert torch.equal(tok[:R], tok2[:R])
+    assert torch.equal(out, out2) and torch.equal(wcoef, wcoef2)
+    keep = pos2 >= 0
+    assert torch.equal(gate2[pos2[keep].long()], w[keep])

@@ -35,10 +35,16 @@ run; losses: relative error):
     err_GPU(q) <= FLOOR_X * err_CPU-bf16(q) + ATOL[q]
 for the pred_logits / pred_boxes of every decoder layer and the encoder
 output, every loss term and the total, and the router / expert gradients of
-every MoE layer.  Routing: the router kernel agrees with the fp64 oracle on
-the GPU's own activations (>= 0.999), and per layer the CPU-vs-GPU routing
-DISagreement on tokens with margin > EPS_MARGIN is at most 4x the
-CPU-vs-CPU-bf16 disagreement + 0.03.
+every MoE layer, and the router INPUT of every MoE layer.  Routing: the router
+kernel agrees with the fp64 oracle on the GPU's own activations (>= 0.999),
+and every CPU-vs-GPU routing flip is explained by the router-input difference:
+a token whose top-k set differs has a CPU top-(k+1) logit gap no larger than
+2 max_e |logit_GPU - logit_CPU| (fp64 logits of each path's own input; at most
+1e-3 of the tokens may be unexplained).  With the router inputs inside the
+floor bound, routing then differs only where bf16 noise may move it.  The
+agreement rates (all tokens, and tokens with CPU margin > EPS_MARGIN, next to
+the CPU-bf16 run's) are reported, not bounded: the R50 detector's logit
+perturbations exceed EPS_MARGIN on a few percent of its tokens.
 Measured (profiles/r02/parity_model.json): the GPU's deviations are ~2x the
 CPU-bf16 floor on activations (the GPU path stores EVERY activation and, in
 "bf16" precision, every GEMM/conv weight in bf16; CPU autocast rounds only the
@@ -66,7 +72,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 EPS_MARGIN = 5e-2
 FLOOR_X = 4.0                                        # GPU error <= FLOOR_X x the bf16 noise floor + ATOL
-ATOL = {"logits": 2e-2, "boxes": 1e-3, "loss": 5e-2, "grad": 1e-1}
+ATOL = {"logits": 2e-2, "boxes": 1e-3, "loss": 5e-2, "grad": 1e-1, "act": 1e-2}
 _REPORT = {}
 
 
@@ -193,8 +199,6 @@ def test_detector_gpu_vs_cpu(hip_lib, spec, B, h, w, precision):
             continue
         gg = pg.grad.detach().float().contiguous().cpu().reshape(gc.shape)
         checks.append((f"grad/{n}", "grad", rel(gg, gc), rel(gf, gc)))
-    rep["checks"] = {w: {"gpu": round(e, 5), "cpu_bf16_floor": round(f, 5),
-                         "limit": round(FLOOR_X * f + ATOL[kind], 5)} for w, kind, e, f in checks}
 
     # routing agreement per MoE layer
     ragree = []
@@ -213,19 +217,29 @@ def test_detector_gpu_vs_cpu(hip_lib, spec, B, h, w, precision):
         _, _, idx_c, _ = eager.route(xc, mc.wg.detach(), mc.ctx_bias.detach(), ci, tpi, cfg.top_k, cfg.normalize)
         _, _, idx_f, _ = eager.route(xf.float(), mc.wg.detach(), mc.ctx_bias.detach(), ci, tpi, cfg.top_k,
                                      cfg.normalize)
-        logits_c = (xc.double() @ mc.wg.detach().double().t() +
-                    mc.ctx_bias.detach().double()[ci.long()].repeat_interleave(tpi, 0)).numpy()
+        bias = mc.ctx_bias.detach().double()[ci.long()].repeat_interleave(tpi, 0)
+        logits_c = (xc.double() @ mc.wg.detach().double().t() + bias).numpy()
+        logits_g = (xg.double().cpu() @ mg.wg.detach().double().cpu().t() +
+                    mg.ctx_bias.detach().double().cpu()[ci.long()].repeat_interleave(tpi, 0)).numpy()
+        delta = np.abs(logits_g - logits_c).max(1)
+        checks.append((f"router_in/l{li}", "act", rel(xg, xc), rel(xf, xc)))
         srt = -np.sort(-logits_c, axis=1)[:, : min(cfg.top_k + 1, cfg.num_experts)]
         margin = np.min(np.abs(np.diff(srt, axis=1)), axis=1)
         s_g, s_o, s_c, s_f = (np.sort(a, 1) for a in (idx_g, idx_o, idx_c.numpy(), idx_f.numpy()))
         wide = margin > EPS_MARGIN
         e2e, flr = np.all(s_g == s_c, 1), np.all(s_f == s_c, 1)
+        kth_gap = srt[:, cfg.top_k - 1] - srt[:, min(cfg.top_k, srt.shape[1] - 1)]
+        unexplained = ~e2e & (kth_gap > 2 * delta + 1e-4)  # fp32-kernel slack
         ragree.append({"layer": li, "tokens": T, "kernel_vs_fp64_oracle": float(np.all(s_g == s_o, 1).mean()),
+                       "flips_unexplained": float(unexplained.mean()),
+                       "median_logit_delta": float(np.median(delta)), "median_kth_gap": float(np.median(kth_gap)),
                        "cpu_vs_gpu_all": float(e2e.mean()), "cpu_vs_cpu_bf16_all": float(flr.mean()),
                        "cpu_vs_gpu_margin_gt_eps": float(e2e[wide].mean()) if wide.any() else 1.0,
                        "cpu_vs_cpu_bf16_margin_gt_eps": float(flr[wide].mean()) if wide.any() else 1.0,
                        "frac_margin_gt_eps": float(wide.mean())})
     rep["routing_agreement"] = ragree
+    rep["checks"] = {w: {"gpu": round(e, 5), "cpu_bf16_floor": round(f, 5),
+                         "limit": round(FLOOR_X * f + ATOL[kind], 5)} for w, kind, e, f in checks}
     _REPORT[f"{spec}/{precision}"] = rep
 
     bad = [(w, round(e, 4), round(FLOOR_X * f + ATOL[kind], 4)) for w, kind, e, f in checks
@@ -233,8 +247,7 @@ def test_detector_gpu_vs_cpu(hip_lib, spec, B, h, w, precision):
     assert not bad, f"{len(bad)} of {len(checks)} quantities beyond {FLOOR_X} x the bf16 floor + atol: {bad[:8]}"
     for r in ragree:
         assert r["kernel_vs_fp64_oracle"] >= 0.999, r
-        # disagreement on confidently routed tokens within 4x the bf16 floor's (+ 3 points)
-        assert 1 - r["cpu_vs_gpu_margin_gt_eps"] <= 4 * (1 - r["cpu_vs_cpu_bf16_margin_gt_eps"]) + 0.03, r
+        assert r["flips_unexplained"] <= 1e-3, r
 
 
 def teardown_module(module):
