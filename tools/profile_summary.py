@@ -23,10 +23,11 @@ import sys
 from pathlib import Path
 
 GROUPS = [
-    ("grouped_gemm", re.compile(r"gemm_v\d_kernel")),
-    ("dispatch", re.compile(r"permute_fwd_kernel|combine_fwd_kernel|combine_bwd_kernel")),
+    ("grouped_gemm", re.compile(r"gemm_v\d_kernel|gemm_pair_kernel")),
+    ("dispatch", re.compile(r"permute_fwd(_mx)?_kernel|combine_fwd_kernel|combine_bwd_kernel")),
     ("router", re.compile(r"router_topk_fwd_kernel")),
-    ("route_scan", re.compile(r"route_scan_kernel")),
+    ("route_scan", re.compile(r"route_scan_kernel|route_dispatch_kernel|route_index_kernel")),
+    ("quantize_mx", re.compile(r"quantize_mx_kernel")),
     ("token_bwd", re.compile(r"token_bwd_kernel")),
     ("msda", re.compile(r"msda_(fwd|bwd)_kernel")),
 ]
