@@ -75,6 +75,37 @@ def gpu_layer(c: MC.LayerCase, inp: dict):
                 db2=_np(b2.grad))
 
 
+def gpu_layer_ep(c: MC.LayerCase, inp: dict):
+    """The expert-parallel layer (src/moe/ep.py: fixed-capacity padded dispatch,
+    device row maps, GEMM1 over the gathered received rows) at W = 1 (identity
+    exchange), slots covering the worst case (no overflow drops)."""
+    from types import SimpleNamespace
+
+    from src.moe.config import MoEConfig
+    from src.moe.ep import moe_ffn_ep
+
+    def P(a):
+        return torch.from_numpy(np.asarray(a)).float().to(DEV).requires_grad_(True)
+
+    cfg = MoEConfig(num_experts=c.E, top_k=c.k, capacity_factor=0.0 if c.cap <= 0 else 1.25,
+                    expert_dtype="fp8" if c.mx else "bf16", ep_capacity_factor=float(c.E) / c.k,
+                    expert_parallel=True)
+    assert cfg.capacity(c.T) == c.cap
+    layer = SimpleNamespace(cfg=cfg, ep_size=1, ep_group=None, wg=P(inp["wg"]), w1=P(inp["w1"]), b1=P(inp["b1"]),
+                            w2=P(inp["w2"]), b2=P(inp["b2"]))
+    cb = P(inp["ctx_bias"])
+    x = torch.from_numpy(np.asarray(inp["x"], np.float32)).to(torch.bfloat16).to(DEV).requires_grad_(True)
+    ci = torch.from_numpy(inp["ctx_img"]).to(DEV)
+    y, lb, z, hist = moe_ffn_ep(layer, x, cb, ci, c.tpi, c.cap)
+    dy = torch.from_numpy(np.asarray(inp["dy"], np.float32)).to(torch.bfloat16).to(DEV)
+    ((y.float() * dy.float()).sum() + MC.G_LB * lb + MC.G_Z * z).backward()
+    torch.cuda.synchronize()
+    assert layer.last_ep_overflow is None or int(layer.last_ep_overflow) == 0
+    return dict(hist=hist.cpu().numpy(), y=_np(y), lb=float(lb.detach()), z=float(z.detach()), dx=_np(x.grad),
+                dwg=_np(layer.wg.grad), dctx_bias=_np(cb.grad), dw1=_np(layer.w1.grad), db1=_np(layer.b1.grad),
+                dw2=_np(layer.w2.grad), db2=_np(layer.b2.grad))
+
+
 def _rel_fro(got, ref):
     return float(np.linalg.norm(np.asarray(got) - ref) / max(np.linalg.norm(ref), 1e-12))
 
@@ -132,6 +163,28 @@ def test_full_size_layer_vs_oracle(hip_lib, name):
     if name == "c5_enc":  # the multi-chunk route_scan path: > 8 router blocks per segment
         assert (c.T + 63) // 64 > 8 * 8
     _REPORT[f"full/{name}"] = rep
+
+
+@pytest.mark.parametrize("name", ["c4_enc", "c4_dec", "c5_enc_fp8"])
+def test_full_size_ep_layer_vs_oracle(hip_lib, name):
+    """C4 (and the C5 MXFP8 encoder) through the expert-parallel layer at full
+    size vs the oracle: same tolerances as the single-GPU layer (routing is the
+    same router kernel; per-element outputs on tokens whose routing agrees)."""
+    c = MC.FULL[name]
+    inp = MC.make_inputs(c)
+    st, gr = MC.run_oracle(c, inp)
+    g = gpu_layer_ep(c, inp)
+    np.testing.assert_array_equal(g["hist"], st.hist)
+    frac = 1e-3 if c.mx else 0.0
+    y_err = _elem_check(g["y"], st.y, f"{name} ep y", frac)
+    dx_err = _elem_check(g["dx"], gr["dx"], f"{name} ep dx", frac)
+    assert abs(g["lb"] - st.lb) <= 1e-5 * max(1.0, abs(st.lb))
+    assert abs(g["z"] - st.z) <= 1e-5 * max(1.0, abs(st.z))
+    gtol = 1e-2 if c.mx else 5e-3
+    gerr = {k: _rel_fro(g[k], gr[k]) for k in ("dwg", "dctx_bias", "dw1", "db1", "dw2", "db2")}
+    assert all(v <= gtol for v in gerr.values()), gerr
+    _REPORT[f"ep/{name}"] = dict(T=c.T, E=c.E, k=c.k, cap=c.cap, mx=c.mx, y_max_err_over_scale=y_err,
+                                 dx_max_err_over_scale=dx_err, grad_rel_fro=gerr)
 
 
 @pytest.mark.parametrize("name", list(MC.GOLDEN))
