@@ -285,6 +285,18 @@ int rtdetr_msda_fused_bwd(const void* value, const int32_t* shapes, const int32_
                           const float* ref, const void* logits, float offset_scale, const void* grad_out,
                           int B, int S, int Q, int H, int D, int L, int P, void* grad_value,
                           void* grad_off, void* grad_logits, hipStream_t stream);
+/* The same with a strided value: token (b, s) starts ldv elements after token
+ * (b, s-1) (ldv >= H*D) -- one [B*S, 6*H*D] value projection shared by the six
+ * decoder layers, each reading its column slice; grad_value has the same
+ * stride and is accumulated into (zeroed first only when zero_grad_value and
+ * ldv == H*D). */
+int rtdetr_msda_fused_fwd_ld(const void* value, long long ldv, const int32_t* shapes, const int32_t* starts,
+                             const void* off, const float* ref, const void* logits, float offset_scale, int B, int S,
+                             int Q, int H, int D, int L, int P, void* out, hipStream_t stream);
+int rtdetr_msda_fused_bwd_ld(const void* value, long long ldv, const int32_t* shapes, const int32_t* starts,
+                             const void* off, const float* ref, const void* logits, float offset_scale,
+                             const void* grad_out, int B, int S, int Q, int H, int D, int L, int P, void* grad_value,
+                             int zero_grad_value, void* grad_off, void* grad_logits, hipStream_t stream);
 
 /* ---- frozen-BatchNorm convolution epilogues of the backbone ----
  * With frozen BN statistics, conv + BN = conv with per-channel scaled weights

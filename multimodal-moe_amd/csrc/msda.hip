@@ -240,7 +240,7 @@ template <int LPG>
 __global__ __launch_bounds__(256) void msda_fused_fwd_kernel(
     const uint16_t* __restrict__ value, const int32_t* __restrict__ shapes, const int32_t* __restrict__ starts,
     const uint16_t* __restrict__ off, const float* __restrict__ ref, const uint16_t* __restrict__ logits,
-    float offset_scale, int B, int S, int Q, int H, int L, int P, uint16_t* __restrict__ out) {
+    float offset_scale, int B, int S, int Q, int H, int L, int P, long long ldv, uint16_t* __restrict__ out) {
   constexpr int D = 2 * LPG;
   const MsdaLevels lv = load_levels(shapes, starts, L);
   const int groups = B * Q * H;
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void msda_fused_fwd_kernel(
     for (int l = 0; l < L; ++l) {
       const int Hl = lv.h[l], Wl = lv.w[l];
       const size_t row0 = (size_t)b * S + lv.start[l];
-      const uint16_t* vb = value + row0 * H * D + h * D + 2 * sub;
+      const uint16_t* vb = value + row0 * ldv + h * D + 2 * sub;
       for (int p = 0; p < P; ++p) {
         const int sp = l * P + p;
         const float ox = bf2f(f2bf(bf2f(op[2 * sp]) * invP)), oy = bf2f(f2bf(bf2f(op[2 * sp + 1]) * invP));
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256) void msda_fused_fwd_kernel(
             const int xi = x0 + cx, yi = y0 + cy;
             if (xi < 0 || xi >= Wl || yi < 0 || yi >= Hl) continue;
             const float wgt = (cx ? fx : 1.f - fx) * (cy ? fy : 1.f - fy);
-            const float2 v = ld_bf16x2(vb + (size_t)(yi * Wl + xi) * H * D);
+            const float2 v = ld_bf16x2(vb + (size_t)(yi * Wl + xi) * ldv);
             s0 += wgt * v.x;
             s1 += wgt * v.y;
           }
@@ -295,7 +295,8 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_kernel(
     const uint16_t* __restrict__ value, const int32_t* __restrict__ shapes, const int32_t* __restrict__ starts,
     const uint16_t* __restrict__ off, const float* __restrict__ ref, const uint16_t* __restrict__ logits,
     float offset_scale, const uint16_t* __restrict__ grad_out, int B, int S, int Q, int H, int L, int P,
-    uint16_t* __restrict__ grad_value, uint16_t* __restrict__ grad_off, uint16_t* __restrict__ grad_logits) {
+    long long ldv, uint16_t* __restrict__ grad_value, uint16_t* __restrict__ grad_off,
+    uint16_t* __restrict__ grad_logits) {
   constexpr int D = 2 * LPG;
   const MsdaLevels lv = load_levels(shapes, starts, L);
   const int groups = B * Q * H;
@@ -322,8 +323,8 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_kernel(
     for (int l = 0; l < L; ++l) {
       const int Hl = lv.h[l], Wl = lv.w[l];
       const size_t row0 = (size_t)b * S + lv.start[l];
-      const uint16_t* vb = value + row0 * H * D + h * D + 2 * sub;
-      const size_t gofs = row0 * H * D + h * D + 2 * sub;
+      const uint16_t* vb = value + row0 * ldv + h * D + 2 * sub;
+      const size_t gofs = row0 * ldv + h * D + 2 * sub;
       for (int p = 0; p < P; ++p) {
         const int sp = l * P + p;
         const float ox = bf2f(f2bf(bf2f(op[2 * sp]) * invP)), oy = bf2f(f2bf(bf2f(op[2 * sp + 1]) * invP));
@@ -342,7 +343,7 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_kernel(
           for (int cx = 0; cx < 2; ++cx) {
             const int xi = x0 + cx, yi = y0 + cy;
             in[cy][cx] = valid && xi >= 0 && xi < Wl && yi >= 0 && yi < Hl;
-            v[cy][cx] = in[cy][cx] ? ld_bf16x2(vb + (size_t)(yi * Wl + xi) * H * D) : make_float2(0.f, 0.f);
+            v[cy][cx] = in[cy][cx] ? ld_bf16x2(vb + (size_t)(yi * Wl + xi) * ldv) : make_float2(0.f, 0.f);
           }
         const float w00 = (1.f - fx) * (1.f - fy), w01 = fx * (1.f - fy);
         const float w10 = (1.f - fx) * fy, w11 = fx * fy;
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_kernel(
             pv.y = (__bf16)(s * g.y);
             __builtin_amdgcn_global_atomic_fadd_v2bf16(
                 (__attribute__((address_space(1))) bf16x2_t*)(grad_value + gofs +
-                                                              (size_t)((y0 + cy) * Wl + (x0 + cx)) * H * D),
+                                                              (size_t)((y0 + cy) * Wl + (x0 + cx)) * ldv),
                 pv);
           }
       }
@@ -470,11 +471,18 @@ extern "C" int rtdetr_msda_bwd_bf16(const void* value, const int32_t* shapes, co
                        grad_attn, stream);
 }
 
-extern "C" int rtdetr_msda_fused_fwd(const void* value, const int32_t* shapes, const int32_t* starts, const void* off,
-                                     const float* ref, const void* logits, float offset_scale, int B, int S, int Q,
-                                     int H, int D, int L, int P, void* out, hipStream_t stream) {
+// Strided-value entry points: token (b, s) of the value starts ldv elements
+// after token (b, s-1) -- the decoder's six value projections computed as one
+// [B*S, 6*H*D] GEMM, each layer reading (and its backward accumulating into)
+// its own column slice.  zero_grad_value = 0 leaves grad_value as it is (the
+// caller zeroed the shared buffer once).
+extern "C" int rtdetr_msda_fused_fwd_ld(const void* value, long long ldv, const int32_t* shapes,
+                                        const int32_t* starts, const void* off, const float* ref, const void* logits,
+                                        float offset_scale, int B, int S, int Q, int H, int D, int L, int P, void* out,
+                                        hipStream_t stream) {
   if (msda_check(B, S, Q, H, D, L, P)) return -1;
   if (L * P > MSDA_LP_MAX) return fail("msda_fused: L * P must be <= 16");
+  if (ldv < (long long)H * D || ldv % 2 != 0) return fail("msda_fused: ldv must be >= H * D and even");
   if (Q == 0) return 0;
   const long long groups = (long long)B * Q * H;
   const double samples = (double)groups * L * P;
@@ -485,21 +493,26 @@ extern "C" int rtdetr_msda_fused_fwd(const void* value, const int32_t* shapes, c
   uint16_t* y = static_cast<uint16_t*>(out);
   if (D == 32)
     MOE_LAUNCH(prof, msda_fused_fwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
-               o, ref, lg, offset_scale, B, S, Q, H, L, P, y);
+               o, ref, lg, offset_scale, B, S, Q, H, L, P, ldv, y);
   else
     MOE_LAUNCH(prof, msda_fused_fwd_kernel<32>, dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v, shapes, starts,
-               o, ref, lg, offset_scale, B, S, Q, H, L, P, y);
+               o, ref, lg, offset_scale, B, S, Q, H, L, P, ldv, y);
   return check_launch("rtdetr_msda_fused_fwd");
 }
 
-extern "C" int rtdetr_msda_fused_bwd(const void* value, const int32_t* shapes, const int32_t* starts, const void* off,
-                                     const float* ref, const void* logits, float offset_scale, const void* grad_out,
-                                     int B, int S, int Q, int H, int D, int L, int P, void* grad_value,
-                                     void* grad_off, void* grad_logits, hipStream_t stream) {
+extern "C" int rtdetr_msda_fused_bwd_ld(const void* value, long long ldv, const int32_t* shapes,
+                                        const int32_t* starts, const void* off, const float* ref, const void* logits,
+                                        float offset_scale, const void* grad_out, int B, int S, int Q, int H, int D,
+                                        int L, int P, void* grad_value, int zero_grad_value, void* grad_off,
+                                        void* grad_logits, hipStream_t stream) {
   if (msda_check(B, S, Q, H, D, L, P)) return -1;
   if (L * P > MSDA_LP_MAX) return fail("msda_fused: L * P must be <= 16");
-  const hipError_t e = hipMemsetAsync(grad_value, 0, (size_t)B * S * H * D * 2, stream);
-  if (e != hipSuccess) return fail(std::string("rtdetr_msda_fused_bwd: memset: ") + hipGetErrorString(e));
+  if (ldv < (long long)H * D || ldv % 2 != 0) return fail("msda_fused: ldv must be >= H * D and even");
+  if (zero_grad_value) {
+    if (ldv != (long long)H * D) return fail("msda_fused: zero_grad_value needs a dense grad_value (ldv == H * D)");
+    const hipError_t e = hipMemsetAsync(grad_value, 0, (size_t)B * S * H * D * 2, stream);
+    if (e != hipSuccess) return fail(std::string("rtdetr_msda_fused_bwd: memset: ") + hipGetErrorString(e));
+  }
   if (Q == 0) return 0;
   const long long groups = (long long)B * Q * H;
   const double samples = (double)groups * L * P;
@@ -513,9 +526,24 @@ extern "C" int rtdetr_msda_fused_bwd(const void* value, const int32_t* shapes, c
   uint16_t* glg = static_cast<uint16_t*>(grad_logits);
   if (D == 32)
     MOE_LAUNCH(prof, msda_fused_bwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
-               o, ref, lg, offset_scale, go, B, S, Q, H, L, P, gv, gof, glg);
+               o, ref, lg, offset_scale, go, B, S, Q, H, L, P, ldv, gv, gof, glg);
   else
     MOE_LAUNCH(prof, msda_fused_bwd_kernel<32>, dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v, shapes, starts,
-               o, ref, lg, offset_scale, go, B, S, Q, H, L, P, gv, gof, glg);
+               o, ref, lg, offset_scale, go, B, S, Q, H, L, P, ldv, gv, gof, glg);
   return check_launch("rtdetr_msda_fused_bwd");
+}
+
+extern "C" int rtdetr_msda_fused_fwd(const void* value, const int32_t* shapes, const int32_t* starts, const void* off,
+                                     const float* ref, const void* logits, float offset_scale, int B, int S, int Q,
+                                     int H, int D, int L, int P, void* out, hipStream_t stream) {
+  return rtdetr_msda_fused_fwd_ld(value, (long long)H * D, shapes, starts, off, ref, logits, offset_scale, B, S, Q, H,
+                                  D, L, P, out, stream);
+}
+
+extern "C" int rtdetr_msda_fused_bwd(const void* value, const int32_t* shapes, const int32_t* starts, const void* off,
+                                     const float* ref, const void* logits, float offset_scale, const void* grad_out,
+                                     int B, int S, int Q, int H, int D, int L, int P, void* grad_value,
+                                     void* grad_off, void* grad_logits, hipStream_t stream) {
+  return rtdetr_msda_fused_bwd_ld(value, (long long)H * D, shapes, starts, off, ref, logits, offset_scale, grad_out,
+                                  B, S, Q, H, D, L, P, grad_value, 1, grad_off, grad_logits, stream);
 }

@@ -66,6 +66,10 @@ SIGNATURES = {
     "rtdetr_msda_bwd_bf16": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "rtdetr_msda_fused_fwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_msda_fused_bwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "rtdetr_msda_fused_fwd_ld": (_I, [_P, ctypes.c_longlong, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _I, _I,
+                                      _P, _P]),
+    "rtdetr_msda_fused_bwd_ld": (_I, [_P, ctypes.c_longlong, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _I, _I,
+                                      _P, _I, _P, _P, _P]),
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "moe_set_splitk_workspace": (_I, [_P, ctypes.c_size_t, _P, _I]),
     "rtdetr_hungarian_match": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
@@ -734,6 +738,42 @@ def msda_fused_bwd(value, shapes, starts, off, ref, logits, offset_scale, L, P, 
                                        float(offset_scale), _ptr(grad_out), B, S, Q, H, D, L, P, _ptr(gv), _ptr(go),
                                        _ptr(gl), _stream()), "rtdetr_msda_fused_bwd")
     return gv, go, gl
+
+
+def msda_fused_fwd_slice(value_all, col0, H, D, shapes, starts, off, ref, logits, offset_scale, L, P):
+    """MSDA on the column slice [col0, col0 + H*D) of value_all bf16 [B, S, C]
+    (rtdetr_msda_fused_fwd_ld: row stride C) -> bf16 [B, Q, H*D]."""
+    B, S, C = value_all.shape
+    Q = off.shape[1]
+    _need(value_all, torch.bfloat16, "value_all")
+    if col0 < 0 or col0 + H * D > C or off.numel() != B * Q * H * L * P * 2 or logits.numel() != B * Q * H * L * P:
+        raise MoEKernelError("msda_fused_slice: shape mismatch")
+    out = torch.empty((B, Q, H * D), dtype=torch.bfloat16, device=value_all.device)
+    base = value_all.data_ptr() + 2 * col0
+    _check(lib().rtdetr_msda_fused_fwd_ld(base, C, _ptr(shapes), _ptr(starts), _ptr(off), _ptr(ref), _ptr(logits),
+                                          float(offset_scale), B, S, Q, H, D, L, P, _ptr(out), _stream()),
+           "rtdetr_msda_fused_fwd_ld")
+    return out
+
+
+def msda_fused_bwd_slice(value_all, grad_all, col0, H, D, shapes, starts, off, ref, logits, offset_scale, L, P,
+                         grad_out):
+    """Backward of msda_fused_fwd_slice: the value gradient is ACCUMULATED into
+    the same column slice of grad_all (bf16 [B, S, C], zeroed by the caller);
+    -> (grad_off, grad_logits)."""
+    B, S, C = value_all.shape
+    Q = off.shape[1]
+    _need(grad_out, torch.bfloat16, "grad_out")
+    _need(grad_all, torch.bfloat16, "grad_all")
+    if grad_all.shape != value_all.shape:
+        raise MoEKernelError("msda_fused_slice: grad_all must match value_all")
+    go = torch.empty_like(off)
+    gl = torch.empty_like(logits)
+    _check(lib().rtdetr_msda_fused_bwd_ld(value_all.data_ptr() + 2 * col0, C, _ptr(shapes), _ptr(starts), _ptr(off),
+                                          _ptr(ref), _ptr(logits), float(offset_scale), _ptr(grad_out), B, S, Q, H, D,
+                                          L, P, grad_all.data_ptr() + 2 * col0, 0, _ptr(go), _ptr(gl), _stream()),
+           "rtdetr_msda_fused_bwd_ld")
+    return go, gl
 
 
 def msda_bwd(value, shapes, starts, loc, attn, grad_out, bf16_grad_value=False):

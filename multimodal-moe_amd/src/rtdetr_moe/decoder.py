@@ -13,7 +13,7 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
-from .linear import TokenLinear
+from .linear import TokenLinear, bias_grad, chunked_wgrad
 from ..moe.config import MoEConfig
 from .encoder import HybridEncoder, make_ffn
 
@@ -160,8 +160,81 @@ class _MSDAFusedHip(torch.autograd.Function):
         return gv, None, None, go, None, gl, None, None, None
 
 
+class _ValueProjAll(torch.autograd.Function):
+    """The decoder layers' value projections over the encoder memory as ONE
+    GEMM, [B*S, d] x [d, n d] with the n layers' weights concatenated per call
+    (the parameters stay per layer).  Forward returns the values v_all
+    [B, S, n d] (layer i reads columns [i d, (i+1) d) through the strided MSDA
+    kernels), a zeroed gradient buffer of the same shape into which the layers'
+    MSDA backward kernels ACCUMULATE their value gradients, and a scalar
+    `token` every layer takes as an input (its zero gradient makes autograd run
+    this backward after all of them).  Backward: d memory = G W (one GEMM, no
+    per-layer gradient adds), dW = G^T memory (one row-chunked GEMM), db = the
+    column sums of G, split back per layer."""
+
+    @staticmethod
+    def forward(ctx, memory, dtype, *wb):
+        n = len(wb) // 2
+        ws, bs = wb[0::2], wb[1::2]
+        B, S, d = memory.shape
+        m2 = memory.reshape(B * S, d).to(dtype)
+        W = torch.cat([w.to(dtype) for w in ws], 0)  # [n d, d]
+        bias = torch.cat([b.to(dtype) for b in bs], 0)
+        v_all = F.linear(m2, W, bias).view(B, S, n * d)
+        grad_all = torch.zeros_like(v_all)
+        token = torch.zeros((), dtype=torch.float32, device=memory.device)
+        ctx.save_for_backward(m2, W)
+        ctx.grad_all = grad_all
+        ctx.meta = (B, S, d, n, memory.dtype, [w.dtype for w in ws], [b.dtype for b in bs])
+        ctx.mark_non_differentiable(v_all, grad_all)
+        return v_all, grad_all, token
+
+    @staticmethod
+    def backward(ctx, _gv, _gg, _gt):
+        m2, W = ctx.saved_tensors
+        B, S, d, n, mdtype, wdt, bdt = ctx.meta
+        G = ctx.grad_all.view(B * S, n * d)
+        ctx.grad_all = None
+        dmem = G.mm(W).view(B, S, d).to(mdtype) if ctx.needs_input_grad[0] else None
+        dW = chunked_wgrad(G, m2)  # fp32 [n d, d]
+        db = bias_grad(G, torch.float32)
+        grads = []
+        for i in range(n):
+            grads += [dW[i * d:(i + 1) * d].to(wdt[i]), db[i * d:(i + 1) * d].to(bdt[i])]
+        return (dmem, None, *grads)
+
+
+class _MSDAFusedSlot(torch.autograd.Function):
+    """_MSDAFusedHip on a column slice of _ValueProjAll's v_all; the value
+    gradient is accumulated into the same slice of its shared buffer."""
+
+    @staticmethod
+    def forward(ctx, token, v_all, grad_all, col0, H, D, shapes_t, starts_t, off, ref, logits, offset_scale, L, P):
+        from ..moe import _lib as L_
+
+        o, lg = off.contiguous(), logits.contiguous()
+        r = ref.float().contiguous()
+        out = L_.msda_fused_fwd_slice(v_all, col0, H, D, shapes_t, starts_t, o, r, lg, offset_scale, L, P)
+        ctx.save_for_backward(v_all, shapes_t, starts_t, o, r, lg)
+        ctx.grad_all = grad_all
+        ctx.cfg = (col0, H, D, offset_scale, L, P)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        from ..moe import _lib as L_
+
+        v_all, shapes_t, starts_t, o, r, lg = ctx.saved_tensors
+        col0, H, D, offset_scale, L, P = ctx.cfg
+        go, gl = L_.msda_fused_bwd_slice(v_all, ctx.grad_all, col0, H, D, shapes_t, starts_t, o, r, lg, offset_scale,
+                                         L, P, grad_out.to(torch.bfloat16).contiguous())
+        ctx.grad_all = None
+        return (torch.zeros((), dtype=torch.float32, device=go.device),) + (None,) * 7 + (go, None, gl) + (None,) * 3
+
+
 _LEVEL_CACHE = {}
 _FUSED_MSDA = os.environ.get("MOE_FUSED_MSDA", "1") != "0"  # A/B switch
+_BATCHED_VALUE = os.environ.get("MOE_BATCHED_VALUE", "1") != "0"  # A/B switch: one value projection for all layers
 _FUSED_BOXES = os.environ.get("MOE_FUSED_BOXES", "1") != "0"  # A/B switch
 
 
@@ -212,10 +285,22 @@ class MSDeformableAttention(nn.Module):
         nn.init.xavier_uniform_(self.output_proj.weight)
         nn.init.zeros_(self.output_proj.bias)
 
-    def forward(self, query, ref_boxes, value, shapes):
-        """query [B,Q,d]; ref_boxes [B,Q,4] (cx,cy,w,h in [0,1]); value [B,S,d]."""
+    def forward(self, query, ref_boxes, value, shapes, vslot=None):
+        """query [B,Q,d]; ref_boxes [B,Q,4] (cx,cy,w,h in [0,1]); value [B,S,d].
+        vslot = (v_all, grad_all, token, col0): the projected values come from
+        the decoder's batched value projection (_ValueProjAll) instead."""
         B, Q, _ = query.shape
         H, L, P = self.nhead, self.nlevels, self.npoints
+        if vslot is not None:
+            v_all, g_all, token, col0 = vslot
+            off = self.sampling_offsets(query)
+            logits = self.attention_weights(query)
+            if not (off.dtype == logits.dtype == torch.bfloat16 and not ref_boxes.requires_grad and L * P <= 16):
+                raise RuntimeError("the batched value projection needs the fused bf16 MSDA path")
+            st, so = _level_tensors(shapes, v_all.device)
+            out = _MSDAFusedSlot.apply(token, v_all, g_all, col0, H, self.d // H, st, so, off, ref_boxes, logits,
+                                       float(self.offset_scale), L, P)
+            return self.output_proj(out)
         v = self.value_proj(value).view(B, value.shape[1], H, self.d // H)
         off = self.sampling_offsets(query)
         logits = self.attention_weights(query)
@@ -241,10 +326,10 @@ class TransformerDecoderLayer(nn.Module):
         self.ffn = make_ffn(d, hidden, moe, act="relu")
         self.norm3 = nn.LayerNorm(d)
 
-    def forward(self, tgt, ref_boxes, memory, shapes, query_pos, ctx):
+    def forward(self, tgt, ref_boxes, memory, shapes, query_pos, ctx, vslot=None):
         q = k = tgt + query_pos
         tgt = self.norm1(tgt + self.self_attn(q, k, tgt, need_weights=False)[0])
-        tgt = self.norm2(tgt + self.cross_attn(tgt + query_pos, ref_boxes, memory, shapes))
+        tgt = self.norm2(tgt + self.cross_attn(tgt + query_pos, ref_boxes, memory, shapes, vslot))
         tgt = self.norm3(tgt + self.ffn(tgt, ctx))
         return tgt
 
@@ -303,6 +388,18 @@ class RTDETRDecoder(nn.Module):
             self._anchor_cache[key] = (a.to(dtype), valid.to(dtype))
         return self._anchor_cache[key]
 
+    def _value_slots(self, memory):
+        """GPU bf16 path: all layers' value projections as one GEMM
+        (_ValueProjAll); elsewhere each layer projects its own values."""
+        n = len(self.layers)
+        dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else memory.dtype
+        if not (_BATCHED_VALUE and _FUSED_MSDA and memory.is_cuda and dtype == torch.bfloat16 and n > 1):
+            return [None] * n
+        vps = [layer.cross_attn.value_proj for layer in self.layers]
+        with torch.autocast("cuda", enabled=False):
+            v_all, g_all, token = _ValueProjAll.apply(memory, dtype, *[t for m in vps for t in (m.weight, m.bias)])
+        return [(v_all, g_all, token, i * self.hidden) for i in range(n)]
+
     def forward(self, feats, ctx):
         # conv + training BatchNorm through libmoe_hip's bn_act (as the encoder's
         # input projections): MIOpen's BN backward at batch 1 lost the gradient
@@ -334,10 +431,11 @@ class RTDETRDecoder(nn.Module):
         tgt = sel.detach()
         ref_detach = ref_unact.detach().sigmoid()
         ref = ref_detach
+        vslots = self._value_slots(memory)
         dec_logits, dec_boxes = [], []
         for i, layer in enumerate(self.layers):
             query_pos = self.query_pos_head(ref_detach.to(tgt.dtype))
-            tgt = layer(tgt, ref_detach, memory, shapes, query_pos, ctx)
+            tgt = layer(tgt, ref_detach, memory, shapes, query_pos, ctx, vslots[i])
             # boxes_i = sigmoid(delta_i + inverse_sigmoid(ref)) with a gradient to
             # the previous layer's boxes; the next reference is the same value
             # without it (upstream: inter on ref_detach, boxes on ref)

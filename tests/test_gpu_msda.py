@@ -145,3 +145,52 @@ def test_box_refine_matches_torch(hip_lib):
     # (two roundings), the kernel rounds their fp32 sum once
     rel = float((res[1][2] - res[0][2]).norm() / res[0][2].norm())
     assert rel < 5e-3, rel
+
+
+@pytest.mark.parametrize("precision", ["bf16", "amp"])
+def test_batched_value_projection_matches_per_layer(hip_lib, precision, monkeypatch):
+    """The decoder's six value projections as one [B*S, 6d] GEMM
+    (decoder._ValueProjAll + strided MSDA slices, value gradients accumulated in
+    one shared buffer) give the per-layer path's outputs and gradients (memory,
+    value_proj weights and biases, the other decoder weights) within bf16
+    rounding."""
+    import src.rtdetr_moe.decoder as dec
+    from src.rtdetr_moe.decoder import RTDETRDecoder
+
+    torch.manual_seed(0)
+    dev = "cuda"
+    shapes = [(20, 32), (10, 16), (5, 8)]
+    B = 2
+    from src.rtdetr_moe.step import gemm_params
+
+    model = RTDETRDecoder(num_queries=50, num_layers=3).to(dev)
+    if precision == "bf16":  # TrainStep's "bf16" precision: GEMM operands in bf16, BN / router fp32
+        for p in gemm_params(model):
+            p.data = p.data.to(torch.bfloat16)
+    dt = torch.bfloat16 if precision == "bf16" else torch.float32
+    g = torch.Generator(device=dev).manual_seed(1)
+    feats = [torch.randn(B, 256, h, w, device=dev, generator=g).to(dt).requires_grad_(True) for h, w in shapes]
+    ctx = torch.zeros(B, dtype=torch.int32, device=dev)
+    res = []
+    for batched in (False, True):
+        monkeypatch.setattr(dec, "_BATCHED_VALUE", batched)
+        model.zero_grad(set_to_none=True)
+        for f in feats:
+            f.grad = None
+        model.query_override = None if not batched else model.last_topk
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=precision == "amp"):
+            out = model(feats, ctx)
+        loss = out["pred_logits"].float().square().sum() + out["pred_boxes"].float().sum() + sum(
+            a["pred_boxes"].float().sum() for a in out["aux_outputs"])
+        loss.backward()
+        grads = {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None}
+        res.append((out["pred_logits"].detach().float(), [f.grad.float().clone() for f in feats], grads))
+    torch.cuda.synchronize()
+    assert "layers.0.cross_attn.value_proj.weight" in res[1][2]
+    rel = lambda a, b: float((a - b).norm() / b.norm().clamp_min(1e-12))  # noqa: E731
+    assert rel(res[1][0], res[0][0]) < 2e-2
+    for a, b in zip(res[1][1], res[0][1]):
+        assert rel(a, b) < 3e-2
+    for n, gref in res[0][2].items():
+        assert n in res[1][2], n
+        assert rel(res[1][2][n], gref) < 5e-2, (n, rel(res[1][2][n], gref))
