@@ -26,6 +26,8 @@
 //      wave-instruction, swizzle applied to the per-lane SOURCE address), an
 //      S-deep ring with S-1 K-tiles in flight, counted `s_waitcnt vmcnt` +
 //      raw s_barrier (no vmcnt(0) drain inside the loop).
+#include <algorithm>
+
 #include "moe_common.h"
 #include "prof.h"
 
@@ -1347,7 +1349,14 @@ static int plan_wgrad(WgradPlan& pl, const void* x, const void* y, void* c, void
   // decoder groups of ~600 rows lose to the merge latency, 11.5 -> 15.5 us)
   const long long tpg = (long long)(M / pl.bm) * ntn;
   long long tiles = tpg * gpad;
-  const int want = g_ksplit ? g_ksplit : ((tiles <= 512 && rows_hint >= 1024LL * G) ? 2 : 1);
+  // G = 1 (a dense linear layer's weight gradient, rtdetr TokenLinear): a
+  // 256 x 256 output is only 8 tiles, so cut the rows over up to 8 slices
+  // (>= 4 K-tiles each); tools/mm_probe_small.py, 2,400 rows: 21.9 -> 14.0 us,
+  // against 21.1 us for hipBLASLt's dY^T X without the bias column sum
+  const long long nkt = (rows_hint + 63) / 64;
+  const int dense_want = (int)std::max(1LL, std::min({8LL, 256 / std::max(1LL, tiles), nkt / 4}));
+  const int want = g_ksplit ? g_ksplit
+                            : (G == 1 ? dense_want : ((tiles <= 512 && rows_hint >= 1024LL * G) ? 2 : 1));
   p.split_min_kt = 0;
   if (want > 1 && tiles % 8 != 0) {  // split grids map 8-slot XCD rows: pad the group count
     gpad = (G + 7) / 8 * 8;

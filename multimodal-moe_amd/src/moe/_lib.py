@@ -523,6 +523,24 @@ def grouped_gemm_wgrad(x, y, offsets, G, want_colsum=True, out_dtype=torch.float
     return c, cs
 
 
+_DENSE_OFFSETS = {}
+
+
+def linear_wgrad(gy, x, out_dtype):
+    """A dense linear layer's weight and bias gradients in one launch: the
+    grouped wgrad kernel with G = 1 (rows split over up to 8 workgroup slices),
+    dW = gy^T x [M, N] and db = colsum(gy) [M], both in out_dtype.  gy bf16
+    [K, M], x bf16 [K, N]; M % 64 == 0 and N % 128 == 0."""
+    K = int(gy.shape[0])
+    key = (K, gy.device)
+    off = _DENSE_OFFSETS.get(key)
+    if off is None:  # built on the device (capture-safe: no host copy)
+        off = torch.arange(2, dtype=torch.int32, device=gy.device) * K
+        _DENSE_OFFSETS[key] = off
+    c, cs = grouped_gemm_wgrad(gy, x, off, 1, want_colsum=True, out_dtype=out_dtype)
+    return c[0], cs[0]
+
+
 # ---------------------------------------------------------------------------
 # MXFP8 (config C5): e4m3 data as torch.uint8, E8M0 exponents as torch.uint8
 # ---------------------------------------------------------------------------

@@ -18,6 +18,7 @@ import torch.nn.functional as F
 from torch import nn
 
 BIG_ROWS = 65536  # below this, the plain GEMM is already well shaped
+DENSE_WGRAD_ROWS = [512]  # from this many rows, conforming shapes use libmoe_hip's wgrad (list: A/B switch)
 
 
 def chunked_wgrad(gy: torch.Tensor, x: torch.Tensor, target_chunk: int = 2560) -> torch.Tensor:
@@ -62,6 +63,7 @@ class _TokenLinear(torch.autograd.Function):
         ctx.save_for_backward(xc, wc)
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.weight_dtype = weight.dtype
         return F.linear(xc, wc, bc)
 
     @staticmethod
@@ -70,7 +72,20 @@ class _TokenLinear(torch.autograd.Function):
         g2 = gy.reshape(-1, gy.shape[-1]).to(wc.dtype).contiguous()
         x2 = xc.reshape(-1, xc.shape[-1])
         gx = g2.mm(wc).view(xc.shape) if ctx.needs_input_grad[0] else None
-        gw = None
+        gw = gb = None
+        K, M = g2.shape
+        N = x2.shape[1]
+        if (ctx.needs_input_grad[1] and ctx.has_bias and ctx.needs_input_grad[2] and g2.is_cuda
+                and g2.dtype == x2.dtype == torch.bfloat16 and M % 64 == 0 and N % 128 == 0
+                and DENSE_WGRAD_ROWS[0] <= K < BIG_ROWS and x2.is_contiguous()):
+            # weight + bias gradient in one libmoe_hip launch (split over rows):
+            # hipBLASLt's dY^T X on these few-tile outputs plus the bias column
+            # sum took ~31 us at 2,400 rows, this ~14 us (tools/mm_probe_small.py)
+            from ..moe import _lib as L
+
+            odt = torch.bfloat16 if ctx.weight_dtype == torch.bfloat16 else torch.float32
+            gw, gb = L.linear_wgrad(g2, x2, odt)
+            return gx, gw, gb.to(ctx.bias_dtype), None
         if ctx.needs_input_grad[1]:
             gw = chunked_wgrad(g2, x2) if x2.shape[0] >= BIG_ROWS else g2.t().mm(x2)
         gb = bias_grad(g2, ctx.bias_dtype) if ctx.has_bias and ctx.needs_input_grad[2] else None

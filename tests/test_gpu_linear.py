@@ -52,7 +52,8 @@ def test_bias_grad_unaligned_view(hip_lib):
 
 
 @pytest.mark.parametrize("shape,din,dout", [((8, 300, 256), 256, 256), ((2400, 256), 256, 1), ((4, 77, 256), 256, 4),
-                                            ((8, 920, 256), 256, 1024)])
+                                            ((8, 920, 256), 256, 1024), ((8, 300, 512), 512, 256),
+                                            ((8, 300, 256), 256, 192), ((3, 190, 256), 256, 768)])
 def test_token_linear_matches_linear(hip_lib, shape, din, dout):
     from src.rtdetr_moe.linear import TokenLinear
 
@@ -74,3 +75,22 @@ def test_token_linear_matches_linear(hip_lib, shape, din, dout):
     tol = 1e-5 * gy.reshape(-1, dout).double().abs().sum(0) + 2.0 ** -8 * gb_ref.abs() + 1e-30
     assert tl.bias.grad.dtype == torch.bfloat16
     assert bool(((tl.bias.grad.double() - gb_ref).abs() <= tol).all())
+
+
+def test_token_linear_fp32_weights_under_autocast(hip_lib):
+    """amp precision: fp32 parameters, bf16 compute; the fused weight + bias
+    gradient (libmoe_hip wgrad, G = 1) comes back in fp32."""
+    from src.rtdetr_moe.linear import TokenLinear
+
+    torch.manual_seed(1)
+    tl = TokenLinear(256, 256).cuda()
+    x = torch.randn(8, 300, 256, device="cuda", requires_grad=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = tl(x)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xb, wb, gb = x.detach().to(torch.bfloat16).double(), tl.weight.detach(), gy.to(torch.bfloat16).double()
+    gw_ref = gb.reshape(-1, 256).t() @ xb.reshape(-1, 256)
+    assert tl.weight.grad.dtype == torch.float32 and tl.bias.grad.dtype == torch.float32
+    assert float((tl.weight.grad.double() - gw_ref).norm() / gw_ref.norm()) <= 1e-5
+    torch.testing.assert_close(tl.bias.grad.double(), gb.reshape(-1, 256).sum(0), rtol=1e-5, atol=1e-4)
