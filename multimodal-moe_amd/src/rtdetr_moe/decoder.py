@@ -13,7 +13,7 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
-from .linear import TokenLinear, bias_grad, chunked_wgrad
+from .linear import TokenLinear, TokenSelfAttention, bias_grad, chunked_wgrad
 from ..moe.config import MoEConfig
 from .encoder import HybridEncoder, make_ffn
 
@@ -319,7 +319,7 @@ class MSDeformableAttention(nn.Module):
 class TransformerDecoderLayer(nn.Module):
     def __init__(self, d=256, nhead=8, hidden=1024, nlevels=3, npoints=4, moe: MoEConfig | None = None):
         super().__init__()
-        self.self_attn = nn.MultiheadAttention(d, nhead, batch_first=True)
+        self.self_attn = TokenSelfAttention(d, nhead)
         self.norm1 = nn.LayerNorm(d)
         self.cross_attn = MSDeformableAttention(d, nhead, nlevels, npoints)
         self.norm2 = nn.LayerNorm(d)
@@ -327,8 +327,7 @@ class TransformerDecoderLayer(nn.Module):
         self.norm3 = nn.LayerNorm(d)
 
     def forward(self, tgt, ref_boxes, memory, shapes, query_pos, ctx, vslot=None):
-        q = k = tgt + query_pos
-        tgt = self.norm1(tgt + self.self_attn(q, k, tgt, need_weights=False)[0])
+        tgt = self.norm1(tgt + self.self_attn(tgt + query_pos, tgt))
         tgt = self.norm2(tgt + self.cross_attn(tgt + query_pos, ref_boxes, memory, shapes, vslot))
         tgt = self.norm3(tgt + self.ffn(tgt, ctx))
         return tgt

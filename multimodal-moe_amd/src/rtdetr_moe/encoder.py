@@ -12,7 +12,7 @@ from ..moe.config import MoEConfig
 from ..moe.layer import MoEFFN
 from .backbone import _FUSED_BN, ConvNormLayer
 from .fused import bn_act, bn_act_ok
-from .linear import TokenLinear
+from .linear import TokenLinear, TokenSelfAttention
 
 
 class DenseFFN(nn.Module):
@@ -36,14 +36,13 @@ class TransformerEncoderLayer(nn.Module):
 
     def __init__(self, d=256, nhead=8, hidden=1024, moe: MoEConfig | None = None):
         super().__init__()
-        self.self_attn = nn.MultiheadAttention(d, nhead, batch_first=True)
+        self.self_attn = TokenSelfAttention(d, nhead)
         self.ffn = make_ffn(d, hidden, moe, act="relu")
         self.norm1 = nn.LayerNorm(d)
         self.norm2 = nn.LayerNorm(d)
 
     def forward(self, src, pos, ctx):
-        q = k = src + pos
-        src = self.norm1(src + self.self_attn(q, k, src, need_weights=False)[0])
+        src = self.norm1(src + self.self_attn(src + pos, src))
         src = self.norm2(src + self.ffn(src, ctx))
         return src
 

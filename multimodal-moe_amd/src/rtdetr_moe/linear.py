@@ -103,3 +103,43 @@ class TokenLinear(nn.Linear):
             with torch.autocast("cuda", enabled=False):
                 return _TokenLinear.apply(x, self.weight, self.bias, dtype)
         return super().forward(x)
+
+
+class TokenSelfAttention(nn.Module):
+    """Self-attention with nn.MultiheadAttention(batch_first=True)'s parameters
+    and state-dict keys (in_proj_weight [3d, d], in_proj_bias, out_proj), for
+    the RT-DETR layers' q = k = x + pos, v = x pattern: q and k come from ONE
+    [d -> 2d] GEMM on x + pos and v from one [d -> d] GEMM on x (MHA's packed
+    path needs q, k and v from one tensor and otherwise issues three), every
+    projection through TokenLinear's backward (fused weight + bias gradient),
+    then scaled-dot-product attention and the output projection.  Same math as
+    nn.MultiheadAttention (dropout 0)."""
+
+    def __init__(self, d: int, nhead: int):
+        super().__init__()
+        self.embed_dim, self.num_heads = d, nhead
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * d, d))
+        self.in_proj_bias = nn.Parameter(torch.empty(3 * d))
+        self.out_proj = TokenLinear(d, d)
+        nn.init.xavier_uniform_(self.in_proj_weight)
+        nn.init.zeros_(self.in_proj_bias)
+        nn.init.zeros_(self.out_proj.bias)
+
+    def _proj(self, x, lo, hi):
+        w, b = self.in_proj_weight[lo:hi], self.in_proj_bias[lo:hi]
+        if x.is_cuda and x.numel() > 0:
+            dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+            with torch.autocast("cuda", enabled=False):
+                return _TokenLinear.apply(x, w, b, dtype)
+        return F.linear(x, w, b)
+
+    def forward(self, qk_in: torch.Tensor, v_in: torch.Tensor) -> torch.Tensor:
+        """qk_in = x + pos, v_in = x, both [B, L, d] -> [B, L, d]."""
+        B, L, d = qk_in.shape
+        H = self.num_heads
+        qk = self._proj(qk_in, 0, 2 * d)
+        v = self._proj(v_in, 2 * d, 3 * d)
+        q, k = qk.split(d, -1)
+        heads = lambda t: t.reshape(B, L, H, d // H).transpose(1, 2)  # noqa: E731
+        o = F.scaled_dot_product_attention(heads(q), heads(k), heads(v))
+        return self.out_proj(o.transpose(1, 2).reshape(B, L, d))

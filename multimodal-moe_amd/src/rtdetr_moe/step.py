@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
+from .linear import TokenSelfAttention
 from .model import RTDETRMoE
 
 _FUSED_CRIT = os.environ.get("MOE_FUSED_CRITERION", "1") != "0"  # A/B switch
@@ -228,7 +229,7 @@ def gemm_params(model: nn.Module):
     for mod in model.modules():
         if isinstance(mod, (nn.Linear, nn.Conv2d, nn.LayerNorm)):  # layer_norm on HIP needs weight dtype == input
             ps = [mod.weight, mod.bias]
-        elif isinstance(mod, nn.MultiheadAttention):
+        elif isinstance(mod, (nn.MultiheadAttention, TokenSelfAttention)):
             ps = [mod.in_proj_weight, mod.in_proj_bias]
         elif isinstance(mod, MoEFFN):
             ps = [mod.w1, mod.b1, mod.w2, mod.b2]
