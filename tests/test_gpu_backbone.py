@@ -44,6 +44,28 @@ def test_bias_act_and_add_bias_relu_exact(hip_lib):
     torch.testing.assert_close(xi, y, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("shape", [(3, 72, 17, 23), (8, 264, 160, 160)])
+def test_epilogues_channel_walk_exact(hip_lib, shape):
+    """Channel counts whose chunk count does not divide the grid stride (the
+    kernels advance the channel incrementally) and a tensor large enough for
+    the capped grid's multi-iteration stride, incl. relu_grad2."""
+    from src.moe import _lib as L
+
+    g = torch.Generator().manual_seed(1)
+    a = _cl(torch.randn(*shape, generator=g))
+    b = _cl(torch.randn(*shape, generator=g))
+    bias = torch.randn(shape[1], generator=g).to(DEV)
+    bc = bias.view(1, -1, 1, 1)
+    torch.testing.assert_close(L.bias_act_nhwc(a, bias, True), (a.float() + bc).relu().to(torch.bfloat16),
+                               rtol=0, atol=0)
+    torch.testing.assert_close(L.add_bias_relu_nhwc(a, b, bias),
+                               (a.float() + b.float() + bc).relu().to(torch.bfloat16), rtol=0, atol=0)
+    y = L.add_bias_relu_nhwc(a, b, bias)
+    got = L.relu_grad2_nhwc(a, b, y)
+    ref = torch.where(y > 0, a.float() + b.float(), torch.zeros((), device=DEV)).to(torch.bfloat16)
+    torch.testing.assert_close(got, ref, rtol=0, atol=0)
+
+
 def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
 
