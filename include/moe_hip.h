@@ -189,6 +189,15 @@ int moe_grouped_gemm_gather(int dtype, const void* a, const int32_t* a_gather, c
 int moe_grouped_gemm_wgrad_gather(int dtype, const void* x, const void* y, const int32_t* y_gather, void* c,
                                   void* colsum, const int32_t* offsets, int G, int M, int N, int rows_hint,
                                   int out_bf16, hipStream_t stream);
+/* A dense linear layer's weight and bias gradients in one launch (the
+ * decoder/encoder TokenLinear backward; replaces the two torch ops
+ * dW = dy^T x, db = dy.sum(0) of nn.Linear's autograd):
+ *   dw[m, n] = sum_r gy[r, m] x[r, n],  db[m] = sum_r gy[r, m],  r < K.
+ * gy bf16 [K, M], x bf16 [K, N] row-major; dw [M, N], db [M] fp32 or bf16
+ * (out_bf16); offsets: a device int32 {0, K}.  M % 64 == 0, N % 128 == 0.
+ * K is split over up to 8 workgroup slices (split-K workspace). */
+int rtdetr_linear_wgrad(const void* gy, const void* x, void* dw, void* db, const int32_t* offsets,
+                        int K, int M, int N, int out_bf16, hipStream_t stream);
 /* a7: one backward step of an expert weight in ONE launch --
  *   dgrad: C[r, n] = epi( s_r sum_k A(r, k) B_g[k][n] )   (trans_b = 0; epilogue
  *          NONE / RELU_MASK / RELU_MASK_MX with aux); A(r, .) = a[a_gather[r]]
@@ -486,7 +495,7 @@ int train_adamw_step(const void* tensors, const int32_t* chunks, int n_chunks, c
  * back from the device offsets.  Kinds: 0 grouped GEMM, 1 permute/combine row
  * moves, 2 router, 3 route scan, 4 token backward, 5 deformable attention,
  * 6 MXFP8 weight quantizer, 7 backbone convolution epilogues, 8 optimizer,
- * 9 Hungarian matching.
+ * 9 Hungarian matching, 10 fp8 grouped GEMM, 11 dense linear weight gradients.
  * Not thread-safe, not for graph capture.  enable(0|1) also clears; get()
  * waits for the record. */
 enum moe_prof_kind {
@@ -500,7 +509,8 @@ enum moe_prof_kind {
   MOE_PROF_CONV_EPI = 7,
   MOE_PROF_OPTIM = 8,
   MOE_PROF_MATCH = 9,
-  MOE_PROF_GEMM_FP8 = 10 /* grouped GEMM on the fp8 (MXFP8) MFMA: priced at the fp8 peak */
+  MOE_PROF_GEMM_FP8 = 10, /* grouped GEMM on the fp8 (MXFP8) MFMA: priced at the fp8 peak */
+  MOE_PROF_LINEAR = 11    /* dense linear weight + bias gradients (rtdetr_linear_wgrad) */
 };
 int moe_profile_enable(int on);
 int moe_profile_count(void);

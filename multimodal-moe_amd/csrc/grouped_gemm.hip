@@ -550,8 +550,8 @@ __device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row
 // through to the coherence point, never parked dirty in one XCD's L2),
 // waits for them to complete, and bumps the tile's arrival counter; the last
 // slice to arrive resets the counter and replaces its registers by the sum of
-// all slices taken in slice order (its own from registers; the others by
-// agent-coherent loads), so the result does not depend on arrival order.
+// all slices taken in slice order (agent-coherent loads, several slices per
+// round trip), so the result does not depend on arrival order.
 // Returns true in that block only (it then runs the epilogue).
 // No __threadfence: its agent-scope release writes back the whole L2
 // (buffer_wbl2), which made every split launch 5-20x slower on MI355X.
@@ -565,7 +565,7 @@ __device__ __forceinline__ float ld_agent(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int TM, int TN, bool COLSUM>
+template <int TM, int TN, bool COLSUM, int NB = 1>
 __device__ __forceinline__ bool splitk_merge(const GemmParams& p, int tile_id, int split,
                                              f32x4 (&acc)[TM][TN], float (&csum)[TM], int tid) {
   constexpr int NQ = TM * TN;
@@ -595,6 +595,13 @@ __device__ __forceinline__ bool splitk_merge(const GemmParams& p, int tile_id, i
   }
   __syncthreads();
   if (s_arrived != p.ksplit - 1) return false;
+  // Sum in slice order from the workspace (this block's own slice included:
+  // its stores are this thread's own, already complete), NB slices per memory
+  // round trip -- one round trip per slice made the 8-slice merge of the dense
+  // weight gradients ~7 us.  NB > 1 costs (NB - 1) x NV registers: only the
+  // register-staged WGRAD body (whose staging registers are dead here) has them
+  // without dropping below three workgroups per CU.
+  constexpr int NV = NQ * 4 + (COLSUM ? TM : 0);  // floats per thread per slice
   f32x4 tot[TM][TN];
   float ctot[TM];
 #pragma unroll
@@ -603,25 +610,25 @@ __device__ __forceinline__ bool splitk_merge(const GemmParams& p, int tile_id, i
 #pragma unroll
     for (int j = 0; j < TN; ++j) tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  for (int sl = 0; sl < p.ksplit; ++sl) {
-    if (sl == split) {
+  for (int s0 = 0; s0 < p.ksplit; s0 += NB) {
+    float v[NB][NV];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (s0 + b >= p.ksplit) break;  // (uniform) the last batch may be short
+      const float* src = base + (size_t)(s0 + b) * PART;
+#pragma unroll
+      for (int e = 0; e < NV; ++e) v[b][e] = ld_agent(src + e * 256 + tid);
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (s0 + b >= p.ksplit) break;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        if constexpr (COLSUM) ctot[i] += csum[i];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) tot[i][j] += acc[i][j];
-      }
-    } else {
-      const float* other = base + (size_t)sl * PART;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-          for (int c = 0; c < 4; ++c) tot[i][j][c] += ld_agent(other + ((i * TN + j) * 4 + c) * 256 + tid);
-      if constexpr (COLSUM) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) ctot[i] += ld_agent(other + (NQ * 4 + i) * 256 + tid);
+          for (int c = 0; c < 4; ++c) tot[i][j][c] += v[b][(i * TN + j) * 4 + c];
+        if constexpr (COLSUM) ctot[i] += v[b][NQ * 4 + i];
       }
     }
   }
@@ -918,7 +925,8 @@ __device__ __forceinline__ void gemm_v1_body(const GemmParams& p, int bid, char*
     }
     __syncthreads();
   }
-  if (t.nsplit > 1 && !splitk_merge<TM, TN, COLSUM>(p, t.tile_id, t.split, acc, csum, tid)) return;
+  constexpr int MERGE_NB = (MODE == MODE_WGRAD && TM * TN <= 8) ? 3 : 1;
+  if (t.nsplit > 1 && !splitk_merge<TM, TN, COLSUM, MERGE_NB>(p, t.tile_id, t.split, acc, csum, tid)) return;
   epilogue<BM, BN, MODE, EPI, COLSUM>(p, t.g, t.row0,
                                       t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, lane, wm, wn);
 }
@@ -931,6 +939,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM <= 64 ? 
 void gemm_v1_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   gemm_v1_body<BM, BN, A_K, B_K, MODE, EPI, COLSUM, FL>(p, blockIdx.x, smem);
+}
+
+// A dense linear layer's weight + bias gradients (G = 1, rtdetr_linear_wgrad):
+// the same register-staged WGRAD body with colsum, under its own symbol so a
+// kernel trace / PMC pass tells it apart from the MoE expert GEMMs.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+void linear_wgrad_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  gemm_v1_body<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true, 0>(p, blockIdx.x, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -1534,6 +1551,23 @@ extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void*
                                            int N, int rows_hint, int out_bf16, hipStream_t stream) {
   return moe_grouped_gemm_wgrad_gather(dtype, x, y, nullptr, c, colsum, offsets, G, M, N, rows_hint, out_bf16,
                                        stream);
+}
+
+extern "C" int rtdetr_linear_wgrad(const void* gy, const void* x, void* dw, void* db, const int32_t* offsets,
+                                   int K, int M, int N, int out_bf16, hipStream_t stream) {
+  WgradPlan pl;
+  WsWin win = device_ws();
+  if (db == nullptr) return fail("rtdetr_linear_wgrad: db (the bias gradient) is required");
+  if (plan_wgrad(pl, gy, x, dw, db, offsets, 1, M, N, K, out_bf16, nullptr, win)) return -1;
+  ProfScope prof(stream, PROF_LINEAR, pl.bytes_fixed, true, pl.bytes_row, pl.flops_row);
+  pl.p.prof_rows = prof.rows_slot();
+  if (pl.bm == 64 && pl.variant == 1) {
+    constexpr size_t lds = 2 * (64 + 128) * 64 * 2;
+    MOE_LAUNCH(prof, linear_wgrad_kernel, dim3(pl.grid), dim3(256), lds, stream, pl.p);
+  } else {  // a tuning knob (bm 128 / the DMA ring) asked for another body
+    launch_wgrad<0>(pl, stream, prof);
+  }
+  return check_launch("rtdetr_linear_wgrad");
 }
 
 extern "C" int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather, const float* row_scale,

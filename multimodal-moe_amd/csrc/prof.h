@@ -27,7 +27,8 @@ enum ProfKind {
   PROF_CONV_EPI = 7,
   PROF_OPTIM = 8,
   PROF_MATCH = 9,
-  PROF_GEMM_FP8 = 10  // grouped GEMM on the fp8 (MXFP8 e4m3) MFMA: priced against the fp8 peak
+  PROF_GEMM_FP8 = 10,  // grouped GEMM on the fp8 (MXFP8 e4m3) MFMA: priced against the fp8 peak
+  PROF_LINEAR = 11     // dense linear weight + bias gradients (rtdetr_linear_wgrad)
 };
 
 class ProfScope {

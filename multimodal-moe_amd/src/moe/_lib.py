@@ -37,6 +37,7 @@ SIGNATURES = {
     "moe_grouped_gemm": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_wgrad": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "moe_grouped_gemm_wgrad_rows": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "rtdetr_linear_wgrad": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "moe_route_index": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "moe_route_dispatch": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P]),
     "moe_grouped_gemm_gather": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
@@ -127,7 +128,8 @@ def lib() -> ctypes.CDLL:
 
 
 PROF_KINDS = {0: "grouped_gemm", 1: "dispatch", 2: "router", 3: "route_scan", 4: "token_bwd", 5: "msda",
-              6: "mx_quant", 7: "conv_epilogue", 8: "optimizer", 9: "matcher", 10: "grouped_gemm_fp8"}
+              6: "mx_quant", 7: "conv_epilogue", 8: "optimizer", 9: "matcher", 10: "grouped_gemm_fp8",
+              11: "linear_wgrad"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_FP8_TFLOPS = 5000.0   # MI355X dense fp8 / MXFP8 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E
@@ -537,8 +539,18 @@ def linear_wgrad(gy, x, out_dtype):
     if off is None:  # built on the device (capture-safe: no host copy)
         off = torch.arange(2, dtype=torch.int32, device=gy.device) * K
         _DENSE_OFFSETS[key] = off
-    c, cs = grouped_gemm_wgrad(gy, x, off, 1, want_colsum=True, out_dtype=out_dtype)
-    return c[0], cs[0]
+    _need(gy, torch.bfloat16, "gy")
+    _need(x, torch.bfloat16, "x")
+    if out_dtype not in (torch.float32, torch.bfloat16):
+        raise MoEKernelError("linear_wgrad: out_dtype must be float32 or bfloat16")
+    M, N = int(gy.shape[1]), int(x.shape[1])
+    dw = torch.empty((M, N), dtype=out_dtype, device=gy.device)
+    db = torch.empty((M,), dtype=out_dtype, device=gy.device)
+    ensure_splitk_workspace(gy.device)
+    rc = lib().rtdetr_linear_wgrad(_ptr(gy), _ptr(x), _ptr(dw), _ptr(db), _ptr(off), K, M, N,
+                                   int(out_dtype == torch.bfloat16), _stream())
+    _check(rc, "rtdetr_linear_wgrad")
+    return dw, db
 
 
 # ---------------------------------------------------------------------------

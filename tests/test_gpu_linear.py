@@ -94,3 +94,32 @@ def test_token_linear_fp32_weights_under_autocast(hip_lib):
     assert tl.weight.grad.dtype == torch.float32 and tl.bias.grad.dtype == torch.float32
     assert float((tl.weight.grad.double() - gw_ref).norm() / gw_ref.norm()) <= 1e-5
     torch.testing.assert_close(tl.bias.grad.double(), gb.reshape(-1, 256).sum(0), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("K,M,N", [(512, 64, 128), (2400, 256, 256), (2400, 512, 256), (4800, 256, 256),
+                                   (777, 128, 384), (65535, 64, 128)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_linear_wgrad_dense(hip_lib, K, M, N, out_dtype):
+    """rtdetr_linear_wgrad (dense dW = gy^T x and db = colsum(gy) in one launch,
+    the TokenLinear backward for conforming shapes) vs torch fp64 of the same
+    bf16 operands: dW within 1e-5 * sum_r |gy_rm x_rn| per element (fp32 split-K
+    accumulation), db within the bias tolerance above; bf16 outputs within one
+    bf16 ulp of that; deterministic (bit-identical reruns)."""
+    from src.moe import _lib as L
+
+    g = torch.Generator().manual_seed(K + 7 * M + N)
+    gy = torch.randn(K, M, generator=g).to(torch.bfloat16).cuda()
+    x = torch.randn(K, N, generator=g).to(torch.bfloat16).cuda()
+    dw, db = L.linear_wgrad(gy, x, out_dtype)
+    assert dw.shape == (M, N) and db.shape == (M,) and dw.dtype == db.dtype == out_dtype
+    ref_w = gy.double().t().mm(x.double())
+    tol_w = 1e-5 * gy.double().abs().t().mm(x.double().abs()) + 1e-30
+    ref_b = gy.double().sum(0)
+    tol_b = 1e-5 * gy.double().abs().sum(0) + 1e-30
+    if out_dtype == torch.bfloat16:  # + half a bf16 ulp of the result
+        tol_w = tol_w + ref_w.abs() * 2.0 ** -8
+        tol_b = tol_b + ref_b.abs() * 2.0 ** -8
+    assert bool(((dw.double() - ref_w).abs() <= tol_w).all()), float(((dw.double() - ref_w).abs() - tol_w).max())
+    assert bool(((db.double() - ref_b).abs() <= tol_b).all()), float(((db.double() - ref_b).abs() - tol_b).max())
+    dw2, db2 = L.linear_wgrad(gy, x, out_dtype)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)

@@ -6,29 +6,31 @@
 #   bash tools/gpu_prof.sh <tag> c2 c5 ...
 # Summarise afterwards with: python tools/profile_summary.py gpurun_out/<tag>/<wl> profiles/<round>/<wl> <wl>
 # Every GPU step has its own time limit; the script stops at the first failure.
+# BENCH_EXTRA (env) is appended to every bench command (e.g. "--tune xcd_map=2").
 set -u
+X=${BENCH_EXTRA:-}
 TAG=${1:-prof}; shift
 R=$GRAFT_REPO_ROOT
-KRE="gemm_v|gemm_pair|permute_fwd|combine_fwd|combine_bwd|router_topk|route_dispatch|route_index|route_scan|token_bwd|quantize_mx|msda_"
+KRE="gemm_v|gemm_pair|permute_fwd|combine_fwd|combine_bwd|router_topk|route_dispatch|route_index|route_scan|token_bwd|quantize_mx|msda_|linear_wgrad"
 for WL in "$@"; do
   O=$R/gpurun_out/$TAG/$WL
   mkdir -p $O/prof $O/pmc_fetch $O/pmc_write
   cd $R
-  timeout -k 10 420 python bench.py --workload $WL > $O/bench.json 2> $O/bench.err; rc=$?
+  timeout -k 10 420 python bench.py --workload $WL $X > $O/bench.json 2> $O/bench.err; rc=$?
   echo "BENCH $WL $rc"; tail -c 400 $O/bench.json
   [ $rc -eq 0 ] || exit $rc
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
-    python3 $R/bench.py --workload $WL --no-cpu-baseline > $O/prof/bench.json 2> $O/prof/bench.err; rc=$?
+    python3 $R/bench.py --workload $WL --no-cpu-baseline $X > $O/prof/bench.json 2> $O/prof/bench.err; rc=$?
   echo "ROCPROF $WL $rc"
   [ $rc -eq 0 ] || exit $rc
   timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" --output-format csv -d $O/pmc_fetch -o p -- \
-    python3 $R/bench.py --workload $WL --no-cpu-baseline --no-kernel-timing --no-graphs --steps 3 --warmup 1 \
+    python3 $R/bench.py --workload $WL --no-cpu-baseline --no-kernel-timing --no-graphs --steps 3 --warmup 1 $X \
     > $O/pmc_fetch/bench.json 2> $O/pmc_fetch/bench.err; rc=$?
   echo "PMC_FETCH $WL $rc"
   [ $rc -eq 0 ] || exit $rc
   timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" --output-format csv -d $O/pmc_write -o p -- \
-    python3 $R/bench.py --workload $WL --no-cpu-baseline --no-kernel-timing --no-graphs --steps 3 --warmup 1 \
+    python3 $R/bench.py --workload $WL --no-cpu-baseline --no-kernel-timing --no-graphs --steps 3 --warmup 1 $X \
     > $O/pmc_write/bench.json 2> $O/pmc_write/bench.err; rc=$?
   echo "PMC_WRITE $WL $rc"
   [ $rc -eq 0 ] || exit $rc

@@ -24,6 +24,7 @@ from pathlib import Path
 
 GROUPS = [
     ("grouped_gemm", re.compile(r"gemm_v\d_kernel|gemm_pair_kernel")),
+    ("linear_wgrad", re.compile(r"linear_wgrad_kernel")),
     ("dispatch", re.compile(r"permute_fwd(_mx)?_kernel|combine_fwd_kernel|combine_bwd_kernel")),
     ("router", re.compile(r"router_topk_fwd_kernel")),
     ("route_scan", re.compile(r"route_scan_kernel|route_dispatch_kernel|route_index_kernel")),
