@@ -95,7 +95,7 @@ static int g_gemm_stages = 0;
 static int g_gemm_debug = 0;
 static int g_rows_bm = 0;   // 0 = by tile count, else 64 or 128
 static int g_wgrad_bm = 0;  // 0 = by tile count, else 64 or 128
-static int g_xcd_map = 0;   // 0 = per-shape choice, 1 = round-robin, 2 = contiguous chunks
+static int g_xcd_map = 0;   // 0 = default (contiguous chunks), 1 = round-robin, 2 = contiguous chunks
 static int g_ksplit = 0;    // 0 = per-shape choice, else forced split-K factor (1 = off)
 static int g_gemm_pair_off = 0;  // 1: moe_grouped_gemm_bwd_pair issues two launches (A/B)
 
@@ -1300,10 +1300,12 @@ static int plan_rows(RowsPlan& pl, const void* a, const void* b, void* c, const 
   pl.bm = g_rows_bm ? g_rows_bm : 64;
   const int mtiles = ((max_rows + pl.bm - 1) / pl.bm + G + 7) / 8 * 8;  // padded to the XCD count
   const long long tiles = (long long)mtiles * nt;
-  // tile -> XCD map: contiguous row-tile chunks per XCD (each L2 then holds
-  // ~1 expert's weights) for the decoder-sized dgrads (kbench: dH 11.3 -> 9.1
-  // us, dX 15.0 -> 12.0); round-robin elsewhere (the encoder shapes prefer it)
-  p.xmap = g_xcd_map ? (g_xcd_map == 2 ? 1 : 0) : ((!trans_b && mtiles <= 128) ? 1 : 0);
+  // tile -> XCD map: contiguous row-tile chunks per XCD, so each L2 holds the
+  // weights of ~1-2 experts instead of all of them (kbench: decoder dH 11.3 ->
+  // 9.1 us, dX 15.0 -> 12.0, the rest unchanged; C2 step PMC: 52.9 -> 41.1 MB
+  // of HBM traffic per grouped-GEMM launch at the same speed,
+  // profiles/r02/xcd_map_ab.json).  xcd_map 1 forces round-robin (A/B).
+  p.xmap = g_xcd_map == 1 ? 0 : 1;
   // split-K when the grid leaves CUs idle and K is long, for the dgrads
   // (MN-contiguous B; kbench: decoder dX 15.0 -> 11.5 us with the map above;
   // the K-contiguous forward GEMM2 only loses to the merge latency)
@@ -1625,7 +1627,7 @@ extern "C" int moe_grouped_gemm_mx(const void* a, const void* a_scales, const vo
   if (max_rows == 0) return 0;
   GemmParams p{};
   p.dbg = g_gemm_debug;
-  p.xmap = g_xcd_map == 2 ? 1 : 0;
+  p.xmap = g_xcd_map == 1 ? 0 : 1;  // contiguous row-tile chunks per XCD (see plan_rows)
   // e4m3 rows addressed as 16-bit pairs: the bf16 tile machinery moves [R][128 B] K-tiles
   p.a = static_cast<const uint16_t*>(a);
   p.b = static_cast<const uint16_t*>(b);
