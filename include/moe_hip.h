@@ -194,10 +194,20 @@ int moe_grouped_gemm_wgrad_gather(int dtype, const void* x, const void* y, const
  * dW = dy^T x, db = dy.sum(0) of nn.Linear's autograd):
  *   dw[m, n] = sum_r gy[r, m] x[r, n],  db[m] = sum_r gy[r, m],  r < K.
  * gy bf16 [K, M], x bf16 [K, N] row-major; dw [M, N], db [M] fp32 or bf16
- * (out_bf16); offsets: a device int32 {0, K}.  M % 64 == 0, N % 128 == 0.
+ * (out_bf16); offsets: unused (may be NULL; kept for the ABI: the kernel takes
+ * the rows [0, K) from its parameters).  M % 64 == 0, N % 128 == 0.
  * K is split over up to 8 workgroup slices (split-K workspace). */
 int rtdetr_linear_wgrad(const void* gy, const void* x, void* dw, void* db, const int32_t* offsets,
                         int K, int M, int N, int out_bf16, hipStream_t stream);
+/* n <= 24 such gradients of mixed shapes in ONE launch (the dense layers'
+ * weight gradients deferred to the end of the backward): problem q is
+ * (gy[q] [K[q], M[q]], x[q] [K[q], N[q]]) -> dw[q] [M[q], N[q]], db[q] [M[q]];
+ * outputs may be row slices of larger buffers (contiguous).  Each problem's
+ * rows are split so the whole batch is ~3 workgroups per CU.  The problem
+ * table travels as the kernel argument (host arrays, read at the call). */
+int rtdetr_linear_wgrad_batch(int n, const void* const* gy, const void* const* x, void* const* dw,
+                              void* const* db, const int* K, const int* M, const int* N, int out_bf16,
+                              hipStream_t stream);
 /* a7: one backward step of an expert weight in ONE launch --
  *   dgrad: C[r, n] = epi( s_r sum_k A(r, k) B_g[k][n] )   (trans_b = 0; epilogue
  *          NONE / RELU_MASK / RELU_MASK_MX with aux); A(r, .) = a[a_gather[r]]

@@ -35,6 +35,7 @@ struct Record {
   hipEvent_t start, stop;
   double bytes_fixed, bytes_per_row, flops_per_row;
   int rows_slot;  // index into the device rows buffer, or -1
+  bool per_row;   // false: flops_per_row is the launch's total flops
 };
 constexpr int kRowSlots = 1 << 16;
 struct Profiler {
@@ -77,7 +78,7 @@ ProfScope::ProfScope(hipStream_t s, int kind, double bytes_fixed, bool per_row, 
     : active_(g_prof.on), idx_(-1) {
   (void)s;
   if (!active_) return;
-  Record r{kind, g_prof.ev(), g_prof.ev(), bytes_fixed, bytes_per_row, flops_per_row, -1};
+  Record r{kind, g_prof.ev(), g_prof.ev(), bytes_fixed, bytes_per_row, flops_per_row, -1, per_row};
   if (per_row && g_prof.rows_dev != nullptr && g_prof.rows_used < kRowSlots) r.rows_slot = g_prof.rows_used++;
   g_prof.recs.push_back(r);
   idx_ = (int)g_prof.recs.size() - 1;
@@ -133,7 +134,7 @@ extern "C" int moe_profile_get(int i, int* kind, float* ms, double* flops, doubl
   *kind = r.kind;
   *ms = t;
   const double rows = r.rows_slot >= 0 ? (double)P.rows_host[r.rows_slot] : 0.0;
-  *flops = r.flops_per_row * rows;
+  *flops = r.per_row ? r.flops_per_row * rows : r.flops_per_row;
   *bytes = r.bytes_fixed + r.bytes_per_row * rows;
   return 0;
 }

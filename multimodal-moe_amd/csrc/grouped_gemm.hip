@@ -86,6 +86,9 @@ struct GemmParams {
   const float* row_scale;
   const int32_t* x_gather;
   const float* x_scale;
+  // WGRAD, G = 1 with offsets == nullptr: the group's rows are [0, dense_rows)
+  // (a dense linear layer's weight gradient; no device offsets to load)
+  int dense_rows;
 };
 
 // runtime tuning knobs (moe_set_tuning)
@@ -254,8 +257,13 @@ struct Tile {
       if (g >= p.G) return false;
       mt = tile / ntn;
       nt = tile % ntn;
-      row0 = p.offsets[g];
-      rows_g = p.offsets[g + 1] - row0;
+      if (p.offsets != nullptr) {
+        row0 = p.offsets[g];
+        rows_g = p.offsets[g + 1] - row0;
+      } else {
+        row0 = 0;
+        rows_g = p.dense_rows;
+      }
       tile_id = g * tpg + tile;
       if (nsplit > 1 && (rows_g + 63) / 64 < p.split_min_kt) {  // short group: slice 0 alone
         if (split != 0) return false;
@@ -821,7 +829,8 @@ __device__ __forceinline__ void gemm_v1_body(const GemmParams& p, int bid, char*
   constexpr int TM = BM / 32, TN = BN / 32;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  if (p.prof_rows != nullptr && bid == 0 && tid == 0) *p.prof_rows = p.offsets[p.G];
+  if (p.prof_rows != nullptr && bid == 0 && tid == 0)
+    *p.prof_rows = p.offsets != nullptr ? p.offsets[p.G] : p.dense_rows;
   Tile<BM, BN, B_K, MODE> t;
   if (!t.init(p, lane, bid)) return;
   float4 bpre[TN];
@@ -950,6 +959,54 @@ void linear_wgrad_kernel(GemmParams p) {
   gemm_v1_body<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true, 0>(p, blockIdx.x, smem);
 }
 
+// Several dense weight gradients of different shapes in ONE launch
+// (rtdetr_linear_wgrad_batch): problem q owns workgroups [base[q], base[q+1])
+// (multiples of 8, so each keeps its XCD-aware slice placement) and its own
+// split-K workspace window.  The table travels as the kernel argument.
+constexpr int MAX_DENSE_BATCH = 24;
+struct DenseProb {
+  const uint16_t* gy;
+  const uint16_t* x;
+  void* dw;
+  void* db;
+  float* ws;
+  int32_t* cnt;
+  int K, M, N, ksplit;
+};
+struct DenseBatch {
+  int n, c_bf16, dbg, pad_;
+  int base[MAX_DENSE_BATCH + 1];
+  DenseProb p[MAX_DENSE_BATCH];
+};
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+void linear_wgrad_batch_kernel(DenseBatch b) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int bid = blockIdx.x;
+  int q = 0;
+  while (q + 1 < b.n && bid >= b.base[q + 1]) ++q;  // uniform: a few scalar compares
+  const DenseProb d = b.p[q];
+  GemmParams p{};
+  p.dbg = b.dbg;
+  p.a = d.gy;
+  p.b = d.x;
+  p.c = d.dw;
+  p.colsum = static_cast<float*>(d.db);
+  p.c_bf16 = b.c_bf16;
+  p.lda = d.M;
+  p.ldb = d.N;
+  p.ldc = d.N;
+  p.stride_c = (long long)d.M * d.N;
+  p.G = 1;
+  p.M = d.M;
+  p.N = d.N;
+  p.dense_rows = d.K;
+  p.ksplit = d.ksplit;
+  p.ws = d.ws;
+  p.cnt = d.cnt;
+  gemm_v1_body<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true, 0>(p, bid - b.base[q], smem);
+}
+
 // ---------------------------------------------------------------------------
 // v2: LDS-DMA ring, S stages, S-1 K-tiles in flight
 // ---------------------------------------------------------------------------
@@ -1012,7 +1069,8 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p, int bid, char*
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  if (p.prof_rows != nullptr && bid == 0 && tid == 0) *p.prof_rows = p.offsets[p.G];
+  if (p.prof_rows != nullptr && bid == 0 && tid == 0)
+    *p.prof_rows = p.offsets != nullptr ? p.offsets[p.G] : p.dense_rows;
   Tile<BM, BN, B_K, MODE> t;
   if (!t.init(p, lane, bid)) return;
   float4 bpre[TN];
@@ -1557,12 +1615,14 @@ extern "C" int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void*
 
 extern "C" int rtdetr_linear_wgrad(const void* gy, const void* x, void* dw, void* db, const int32_t* offsets,
                                    int K, int M, int N, int out_bf16, hipStream_t stream) {
+  (void)offsets;  // rows are [0, K): the kernel takes them from its parameters
   WgradPlan pl;
   WsWin win = device_ws();
   if (db == nullptr) return fail("rtdetr_linear_wgrad: db (the bias gradient) is required");
-  if (plan_wgrad(pl, gy, x, dw, db, offsets, 1, M, N, K, out_bf16, nullptr, win)) return -1;
-  ProfScope prof(stream, PROF_LINEAR, pl.bytes_fixed, true, pl.bytes_row, pl.flops_row);
-  pl.p.prof_rows = prof.rows_slot();
+  if (K <= 0) return fail("rtdetr_linear_wgrad: K must be positive");
+  if (plan_wgrad(pl, gy, x, dw, db, nullptr, 1, M, N, K, out_bf16, nullptr, win)) return -1;
+  pl.p.dense_rows = K;
+  ProfScope prof(stream, PROF_LINEAR, pl.bytes_fixed + pl.bytes_row * K, false, 0.0, pl.flops_row * K);
   if (pl.bm == 64 && pl.variant == 1) {
     constexpr size_t lds = 2 * (64 + 128) * 64 * 2;
     MOE_LAUNCH(prof, linear_wgrad_kernel, dim3(pl.grid), dim3(256), lds, stream, pl.p);
@@ -1570,6 +1630,61 @@ extern "C" int rtdetr_linear_wgrad(const void* gy, const void* x, void* dw, void
     launch_wgrad<0>(pl, stream, prof);
   }
   return check_launch("rtdetr_linear_wgrad");
+}
+
+extern "C" int rtdetr_linear_wgrad_batch(int n, const void* const* gy, const void* const* x, void* const* dw,
+                                         void* const* db, const int* K, const int* M, const int* N, int out_bf16,
+                                         hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (n > MAX_DENSE_BATCH) return fail("rtdetr_linear_wgrad_batch: at most 24 problems per launch");
+  WsWin win = device_ws();
+  DenseBatch b{};
+  b.n = n;
+  b.c_bf16 = out_bf16 ? 1 : 0;
+  b.dbg = g_gemm_debug;
+  constexpr long long part = 256LL * 2 * 4 * 4 + 256LL * 2;  // fp32 floats per slice of a 64 x 128 tile
+  // Split each problem's rows so that the whole batch is ~3 workgroups per CU
+  // of about equal K-loop length: slices of >= 4 K-tiles, at most 8 per tile.
+  long long iters = 0;
+  for (int q = 0; q < n; ++q) {
+    if (gy[q] == nullptr || x[q] == nullptr || dw[q] == nullptr || db[q] == nullptr)
+      return fail("rtdetr_linear_wgrad_batch: null operand");
+    if (K[q] <= 0 || M[q] <= 0 || N[q] <= 0 || M[q] % 64 != 0 || N[q] % 128 != 0)
+      return fail("rtdetr_linear_wgrad_batch: need K > 0, M % 64 == 0 and N % 128 == 0");
+    iters += (long long)(M[q] / 64) * (N[q] / 128) * ((K[q] + 63) / 64);
+  }
+  const long long per_wg = std::max(4LL, (iters + 767) / 768);  // K-tiles per workgroup
+  double bytes = 0.0, flops = 0.0;
+  long long grid = 0;
+  for (int q = 0; q < n; ++q) {
+    DenseProb& d = b.p[q];
+    d.gy = static_cast<const uint16_t*>(gy[q]);
+    d.x = static_cast<const uint16_t*>(x[q]);
+    d.dw = dw[q];
+    d.db = db[q];
+    d.K = K[q];
+    d.M = M[q];
+    d.N = N[q];
+    const long long tiles = ((long long)(M[q] / 64) * (N[q] / 128) + 7) / 8 * 8;
+    const long long nkt = (K[q] + 63) / 64;
+    int want = (int)std::min(8LL, std::max(1LL, (nkt + per_wg - 1) / per_wg));
+    want = pick_split(want, tiles, part, win);
+    GemmParams tmp{};
+    win = bind_split(tmp, want, tiles, part, win);
+    d.ksplit = tmp.ksplit;
+    d.ws = tmp.ws;
+    d.cnt = tmp.cnt;
+    b.base[q] = (int)grid;
+    grid += tiles * d.ksplit;
+    const double osz = out_bf16 ? 2.0 : 4.0;
+    bytes += osz * ((double)M[q] * N[q] + M[q]) + 2.0 * K[q] * (M[q] + N[q]);
+    flops += 2.0 * M[q] * N[q] * K[q];
+  }
+  b.base[n] = (int)grid;
+  ProfScope prof(stream, PROF_LINEAR, bytes, false, 0.0, flops);
+  constexpr size_t lds = 2 * (64 + 128) * 64 * 2;
+  MOE_LAUNCH(prof, linear_wgrad_batch_kernel, dim3((unsigned)grid), dim3(256), lds, stream, b);
+  return check_launch("rtdetr_linear_wgrad_batch");
 }
 
 extern "C" int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather, const float* row_scale,

@@ -3,7 +3,8 @@
 // gets a start/stop hipEvent pair stamped by its own dispatch packet
 // (hipExtLaunchKernel: kernel execution time, no host gaps), and the scope
 // records the launch's algorithmic HBM bytes bytes_fixed + bytes_per_row * R and
-// flops flops_per_row * R, where R (the routed row count, known only on the
+// flops flops_per_row * R (per_row = false: bytes_fixed and flops_per_row are
+// the launch's totals), where R (the routed row count, known only on the
 // device) is written by the kernel itself into rows_slot() -- a device int of
 // the profiler -- so profiling adds no copies or launches.  Events come from a
 // pool created when profiling is enabled.  Disabled: MOE_LAUNCH is a plain

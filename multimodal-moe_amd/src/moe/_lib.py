@@ -38,6 +38,7 @@ SIGNATURES = {
     "moe_grouped_gemm_wgrad": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "moe_grouped_gemm_wgrad_rows": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "rtdetr_linear_wgrad": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "rtdetr_linear_wgrad_batch": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "moe_route_index": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "moe_route_dispatch": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P]),
     "moe_grouped_gemm_gather": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
@@ -551,6 +552,38 @@ def linear_wgrad(gy, x, out_dtype):
                                    int(out_dtype == torch.bfloat16), _stream())
     _check(rc, "rtdetr_linear_wgrad")
     return dw, db
+
+
+LINEAR_WGRAD_BATCH = 24  # problems per rtdetr_linear_wgrad_batch launch
+
+
+def linear_wgrad_batch(jobs, out_dtype):
+    """Several dense weight + bias gradients in ceil(n / 24) launches:
+    jobs = [(gy bf16 [K, M], x bf16 [K, N], dw [M, N], db [M])] with dw / db
+    contiguous out_dtype outputs (views into larger buffers allowed); dw =
+    gy^T x, db = colsum(gy).  M % 64 == 0, N % 128 == 0."""
+    if out_dtype not in (torch.float32, torch.bfloat16):
+        raise MoEKernelError("linear_wgrad_batch: out_dtype must be float32 or bfloat16")
+    ensure_splitk_workspace(jobs[0][0].device)
+    for i in range(0, len(jobs), LINEAR_WGRAD_BATCH):
+        part = jobs[i:i + LINEAR_WGRAD_BATCH]
+        n = len(part)
+        ptrs = [(ctypes.c_void_p * n)() for _ in range(4)]
+        dims = [(ctypes.c_int * n)() for _ in range(3)]
+        for q, (gy, x, dw, db) in enumerate(part):
+            _need(gy, torch.bfloat16, "gy")
+            _need(x, torch.bfloat16, "x")
+            if dw.dtype != out_dtype or db.dtype != out_dtype or not (dw.is_contiguous() and db.is_contiguous()):
+                raise MoEKernelError("linear_wgrad_batch: dw / db must be contiguous out_dtype tensors")
+            K, M, N = int(gy.shape[0]), int(gy.shape[1]), int(x.shape[1])
+            if x.shape[0] != K or dw.shape != (M, N) or db.shape != (M,):
+                raise MoEKernelError("linear_wgrad_batch: shape mismatch")
+            for arr, t in zip(ptrs, (gy, x, dw, db)):
+                arr[q] = t.data_ptr()
+            dims[0][q], dims[1][q], dims[2][q] = K, M, N
+        args = [ctypes.cast(a, ctypes.c_void_p) for a in (*ptrs, *dims)]
+        rc = lib().rtdetr_linear_wgrad_batch(n, *args, int(out_dtype == torch.bfloat16), _stream())
+        _check(rc, "rtdetr_linear_wgrad_batch")
 
 
 # ---------------------------------------------------------------------------

@@ -13,12 +13,131 @@ two-launch column sum) instead of torch's reduce kernel.
 """
 from __future__ import annotations
 
+import contextlib
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
 
 BIG_ROWS = 65536  # below this, the plain GEMM is already well shaped
 DENSE_WGRAD_ROWS = [512]  # from this many rows, conforming shapes use libmoe_hip's wgrad (list: A/B switch)
+# GraphedStep defers conforming dense weight gradients to one batched launch
+# after the backward (MOE_DEFER_WGRAD=0: one launch per layer, as before)
+DEFER_WGRAD = [os.environ.get("MOE_DEFER_WGRAD", "1") != "0"]
+_ACTIVE: list = [None]  # the DeferredWgrad collecting during a backward, or None
+
+
+def _row_target(t: torch.Tensor):
+    """(leaf parameter, first row) of a weight / bias that is the parameter
+    itself or a contiguous row slice of it (TokenSelfAttention's in_proj
+    slices); None otherwise."""
+    if t.is_leaf:
+        return t, 0
+    base = t._base
+    if base is None or not base.is_leaf or not t.is_contiguous() or not base.is_contiguous():
+        return None
+    if t.dim() != base.dim() or t.shape[1:] != base.shape[1:]:
+        return None
+    row = t[0].numel() if t.dim() > 1 else 1
+    off = t.storage_offset() - base.storage_offset()
+    if off % row != 0:
+        return None
+    return base, off // row
+
+
+class DeferredWgrad:
+    """Dense weight + bias gradients collected during one backward and computed
+    afterwards in as few launches as possible (rtdetr_linear_wgrad_batch: up to
+    24 layers of mixed shapes per launch, each with its rows split so that the
+    batch fills the chip).  One at a time, every such gradient is a short
+    split-K GEMM whose fixed cost -- launch, first tile, split-K merge -- is most
+    of its ~15 us (54 per C2 step); batched, the fixed cost is paid twice.
+    ``flush()`` returns {id(parameter): gradient} for the leaf parameters."""
+
+    def __init__(self):
+        self.items = []  # (gy, x, out dtype, (weight leaf, row), (bias leaf, row))
+
+    def add(self, gy, x, odt, wt, bt):
+        self.items.append((gy, x, odt, wt, bt))
+
+    def flush(self):
+        from ..moe import _lib as L
+
+        if not self.items:
+            return {}
+        # a parameter whose rows receive more than one layer's gradient (a
+        # layer applied several times, e.g. a shared head) is summed in fp32
+        # and rounded once; the others are written in place, in their dtype
+        seen, shared = set(), set()
+        for gy, x, odt, wt, bt in self.items:
+            for p_, r0 in (wt, bt):
+                if (id(p_), r0) in seen:
+                    shared.add(id(p_))
+                seen.add((id(p_), r0))
+        grads, acc = {}, {}
+        direct = {torch.bfloat16: [], torch.float32: []}
+        summed = []
+        for gy, x, odt, (wp, wr), (bp, br) in self.items:
+            M, N = gy.shape[1], x.shape[1]
+            for p_ in (wp, bp):
+                if id(p_) in shared:
+                    if id(p_) not in acc:
+                        acc[id(p_)] = (torch.zeros(p_.shape, dtype=torch.float32, device=gy.device), odt)
+                elif id(p_) not in grads:
+                    grads[id(p_)] = torch.zeros(p_.shape, dtype=odt, device=gy.device)
+            if id(wp) in shared or id(bp) in shared:
+                dw = torch.empty((M, N), dtype=torch.float32, device=gy.device)
+                db = torch.empty((M,), dtype=torch.float32, device=gy.device)
+                direct[torch.float32].append((gy, x, dw, db))
+                summed.append((dw, db, wp, wr, bp, br, odt))
+            else:
+                direct[odt].append((gy, x, grads[id(wp)][wr:wr + M], grads[id(bp)][br:br + M]))
+        for dt, batch in direct.items():
+            if batch:
+                L.linear_wgrad_batch(batch, dt)
+        for dw, db, wp, wr, bp, br, odt in summed:
+            for p_, r0, part in ((wp, wr, dw), (bp, br, db)):
+                if id(p_) in acc:
+                    acc[id(p_)][0][r0:r0 + part.shape[0]] += part
+                else:
+                    grads[id(p_)][r0:r0 + part.shape[0]] += part.to(odt)
+        for k, (a, odt) in acc.items():
+            grads[k] = a.to(odt)
+        self.items.clear()
+        return grads
+
+
+@contextlib.contextmanager
+def deferred_weight_grads():
+    """Collect conforming TokenLinear weight gradients during the backward run
+    inside this context (the collector's ``flush()`` computes them)."""
+    d = DeferredWgrad() if DEFER_WGRAD[0] else None
+    prev = _ACTIVE[0]
+    _ACTIVE[0] = d
+    try:
+        yield d
+    finally:
+        _ACTIVE[0] = prev
+
+
+def merge_deferred(params, grads, deferred: DeferredWgrad | None):
+    """grads (torch.autograd.grad's output for params) with the deferred
+    gradients flushed in: substituted where autograd had none, added where a
+    parameter also received a regular gradient."""
+    if deferred is None:
+        return list(grads)
+    extra = deferred.flush()
+    out = []
+    for p, g in zip(params, grads):
+        e = extra.get(id(p))
+        if e is None:
+            out.append(g)
+        elif g is None:
+            out.append(e.to(p.dtype) if e.dtype != p.dtype else e)
+        else:
+            out.append(g + e.to(g.dtype))
+    return out
 
 
 def chunked_wgrad(gy: torch.Tensor, x: torch.Tensor, target_chunk: int = 2560) -> torch.Tensor:
@@ -64,6 +183,14 @@ class _TokenLinear(torch.autograd.Function):
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.weight_dtype = weight.dtype
+        # where a deferred weight gradient would land (the leaf parameters; the
+        # backward decides whether to defer: GraphedStep's forward runs outside
+        # the collecting context)
+        ctx.targets = None
+        if DEFER_WGRAD[0] and bias is not None and bias.dtype == weight.dtype and x.is_cuda:
+            wt, bt = _row_target(weight), _row_target(bias)
+            if wt is not None and bt is not None:
+                ctx.targets = (wt, bt)
         return F.linear(xc, wc, bc)
 
     @staticmethod
@@ -84,6 +211,9 @@ class _TokenLinear(torch.autograd.Function):
             from ..moe import _lib as L
 
             odt = torch.bfloat16 if ctx.weight_dtype == torch.bfloat16 else torch.float32
+            if _ACTIVE[0] is not None and ctx.targets is not None and ctx.weight_dtype == odt:
+                _ACTIVE[0].add(g2, x2, odt, *ctx.targets)  # computed after the backward, batched
+                return gx, None, None, None
             gw, gb = L.linear_wgrad(g2, x2, odt)
             return gx, gw, gb.to(ctx.bias_dtype), None
         if ctx.needs_input_grad[1]:

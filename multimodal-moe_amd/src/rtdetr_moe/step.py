@@ -26,7 +26,7 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
-from .linear import TokenSelfAttention
+from .linear import TokenSelfAttention, deferred_weight_grads, merge_deferred
 from .model import RTDETRMoE
 
 _FUSED_CRIT = os.environ.get("MOE_FUSED_CRITERION", "1") != "0"  # A/B switch
@@ -171,13 +171,21 @@ class GraphedStep:
         losses = self.criterion.forward_padded(out, self.tb, self.tl, self.nv, self.nb, self.status)
         return sum(losses.values()) + aux, losses
 
+    def _grads(self, loss):
+        """Gradients of every parameter: autograd for most, the conforming dense
+        layers' weight + bias gradients batched after it (linear.DeferredWgrad)."""
+        with deferred_weight_grads() as deferred:
+            grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+        self.deferred_layers = 0 if deferred is None else len(deferred.items)
+        return merge_deferred(self.params, grads, deferred)
+
     def _capture(self):
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up: convolution search, library attributes, allocator
             for _ in range(self.warmup):
                 loss, _ = self._loss()
-                grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+                grads = self._grads(loss)
                 del loss, grads
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
@@ -185,7 +193,7 @@ class GraphedStep:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, pool=self.pool):
             loss, losses = self._loss()
-            grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+            grads = self._grads(loss)
             self.static_loss = loss.detach()
             self.static_losses = {k: v.detach() for k, v in losses.items()}
         self.static_grads = [g if g is not None else torch.zeros_like(p) for g, p in zip(grads, self.params)]

@@ -123,3 +123,73 @@ def test_linear_wgrad_dense(hip_lib, K, M, N, out_dtype):
     assert bool(((db.double() - ref_b).abs() <= tol_b).all()), float(((db.double() - ref_b).abs() - tol_b).max())
     dw2, db2 = L.linear_wgrad(gy, x, out_dtype)
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_linear_wgrad_batch_mixed_shapes(hip_lib, out_dtype):
+    """rtdetr_linear_wgrad_batch: 30 problems of mixed shapes (two launches of
+    <= 24), outputs written into row slices of shared buffers, vs fp64 under
+    the tolerance of test_linear_wgrad_dense; untouched rows stay untouched;
+    deterministic."""
+    from src.moe import _lib as L
+
+    g = torch.Generator().manual_seed(11)
+    shapes = [(2400, 256, 256), (2400, 512, 256), (2400, 192, 256), (7360, 256, 256), (777, 64, 128),
+              (4800, 1024, 256), (512, 128, 384)] * 4 + [(2400, 256, 256), (65535, 64, 128)]
+    jobs, refs = [], []
+    for K, M, N in shapes:
+        gy = torch.randn(K, M, generator=g).to(torch.bfloat16).cuda()
+        x = torch.randn(K, N, generator=g).to(torch.bfloat16).cuda()
+        big_w = torch.full((M + 64, N), 7.0, dtype=out_dtype, device="cuda")  # rows [32, 32 + M) are the target
+        big_b = torch.full((M + 64,), 7.0, dtype=out_dtype, device="cuda")
+        jobs.append((gy, x, big_w[32:32 + M], big_b[32:32 + M]))
+        refs.append((big_w, big_b))
+    L.linear_wgrad_batch(jobs, out_dtype)
+    first = [(w.clone(), b.clone()) for w, b in refs]
+    for (gy, x, dw, db), (big_w, big_b) in zip(jobs, refs):
+        ref_w = gy.double().t().mm(x.double())
+        tol_w = 1e-5 * gy.double().abs().t().mm(x.double().abs()) + 1e-30
+        ref_b = gy.double().sum(0)
+        tol_b = 1e-5 * gy.double().abs().sum(0) + 1e-30
+        if out_dtype == torch.bfloat16:
+            tol_w = tol_w + ref_w.abs() * 2.0 ** -8
+            tol_b = tol_b + ref_b.abs() * 2.0 ** -8
+        assert bool(((dw.double() - ref_w).abs() <= tol_w).all())
+        assert bool(((db.double() - ref_b).abs() <= tol_b).all())
+        assert bool((big_w[:32] == 7).all() and (big_w[32 + dw.shape[0]:] == 7).all())
+        assert bool((big_b[:32] == 7).all() and (big_b[32 + db.shape[0]:] == 7).all())
+    L.linear_wgrad_batch(jobs, out_dtype)
+    for (w0, b0), (w1, b1) in zip(first, refs):
+        assert torch.equal(w0, w1) and torch.equal(b0, b1)
+
+
+def test_deferred_weight_grads_match_autograd(hip_lib):
+    """Inside deferred_weight_grads(), TokenLinear / TokenSelfAttention weight
+    and bias gradients (incl. in_proj row slices and a layer applied twice) are
+    collected and computed after the backward; merged, they equal the
+    per-layer path's gradients within the dense-wgrad tolerance."""
+    from src.rtdetr_moe.linear import TokenLinear, TokenSelfAttention, deferred_weight_grads, merge_deferred
+
+    torch.manual_seed(0)
+    lin1 = TokenLinear(256, 512).cuda().to(torch.bfloat16)
+    lin2 = TokenLinear(512, 256).cuda().to(torch.bfloat16)
+    attn = TokenSelfAttention(256, 8).cuda().to(torch.bfloat16)
+    params = list(lin1.parameters()) + list(lin2.parameters()) + list(attn.parameters())
+    x = torch.randn(8, 300, 256, device="cuda", dtype=torch.bfloat16)
+    pos = torch.randn(8, 300, 256, device="cuda", dtype=torch.bfloat16)
+
+    def loss_fn():
+        h = lin2(torch.relu(lin1(x)))
+        h = lin2(torch.relu(lin1(h)))  # the same layers twice
+        y = attn(h + pos, h)
+        return (y.float() ** 2).mean()
+
+    ref = torch.autograd.grad(loss_fn(), params)
+    with deferred_weight_grads() as d:
+        got = torch.autograd.grad(loss_fn(), params, allow_unused=True)
+    assert d is not None and len(d.items) > 0
+    got = merge_deferred(params, got, d)
+    for p, r, gg in zip(params, ref, got):
+        assert gg is not None and gg.shape == p.shape and gg.dtype == r.dtype
+        err = (gg.float() - r.float()).norm() / r.float().norm().clamp_min(1e-12)
+        assert float(err) < 1e-2, float(err)

@@ -301,3 +301,53 @@ def test_whole_step_recapture_rebinds_gradients(hip_lib):
     d = step.opt.master_of(p) - m0
     gr = p.grad.float().reshape(-1)
     assert float(gr.abs().max()) > 0 and float(d.abs().max()) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16", "amp"])
+def test_whole_step_deferred_weight_grads(hip_lib, precision):
+    """GraphedStep defers the dense layers' weight + bias gradients to batched
+    launches after the backward (linear.DeferredWgrad).  On the detector's own
+    layers (TokenLinear, TokenSelfAttention in_proj row slices): the merged
+    gradients of the deferred parameters equal the fp64 sum of gy^T x / colsum
+    over the collected (gy, x) pairs, placed at their rows (dense-wgrad
+    tolerance), every other parameter keeps autograd's gradient object, and
+    the captured step did defer layers.  (Two captures cannot be compared
+    tensor by tensor: the value gradient's bf16 atomics make even identical
+    captures differ by up to ~20 % on this random-init model's small deep
+    gradients.)"""
+    from src.rtdetr_moe import linear
+    from src.rtdetr_moe.step import TrainStep
+
+    model, crit, images, targets, ctx = _setup(seed=6)
+    nb = max(1.0, float(sum(len(t["boxes"]) for t in targets)))
+    step = TrainStep(model, crit, images, ctx, graphs=True, world=1, precision=precision, lr=1e-3,
+                     targets=targets, num_boxes=nb)
+    gs = step.stepper
+    assert gs.deferred_layers >= 6, gs.deferred_layers
+    loss, _ = gs._loss()
+    with linear.deferred_weight_grads() as d:
+        grads = torch.autograd.grad(loss, gs.params, allow_unused=True)
+    items = list(d.items)
+    assert len(items) == gs.deferred_layers
+    merged = linear.merge_deferred(gs.params, grads, d)
+    # per element: fp32 accumulation (1e-5 of sum |terms|) plus, for bf16
+    # outputs, one rounding of each layer's partial and one of their sum (a
+    # layer applied twice is added after both partials are rounded)
+    ref, tol, mag = {}, {}, {}
+    z = lambda p_, dev: torch.zeros(p_.shape, dtype=torch.float64, device=dev)  # noqa: E731
+    for gy, x, odt, (wp, wr), (bp, br) in items:
+        M = gy.shape[1]
+        for p_, r0, val, bound in ((wp, wr, gy.double().t().mm(x.double()), gy.double().abs().t().mm(x.double().abs())),
+                                   (bp, br, gy.double().sum(0), gy.double().abs().sum(0))):
+            ref.setdefault(id(p_), z(p_, gy.device))[r0:r0 + M] += val
+            tol.setdefault(id(p_), z(p_, gy.device))[r0:r0 + M] += bound
+            mag.setdefault(id(p_), z(p_, gy.device))[r0:r0 + M] += val.abs()
+    for p, g, m in zip(gs.params, grads, merged):
+        if id(p) not in ref:
+            assert m is g
+            continue
+        assert g is None and m is not None and m.shape == p.shape and m.dtype == p.dtype
+        r = ref[id(p)]
+        t = 1e-5 * tol[id(p)] + (2.0 ** -8 * (mag[id(p)] + r.abs()) if m.dtype == torch.bfloat16 else 0.0) + 1e-30
+        assert bool(((m.double() - r).abs() <= t).all()), (tuple(p.shape), float(((m.double() - r).abs() - t).max()))
