@@ -111,6 +111,9 @@ def _rel_fro(got, ref):
 
 
 def _elem_check(got, ref, what, frac=0.0):
+    from _tolreport import report
+
+    report(what, got, ref)
     scale = max(float(np.abs(ref).max()), 1e-6)
     err = np.abs(got - ref)
     bad = err > 1e-2 * scale + np.abs(ref) * 2.0 ** -7

@@ -71,6 +71,9 @@ def bf16_close(got, ref, what, rel=1e-2):
     err = np.abs(got - ref)
     tol = rel * scale + ulp
     bad = err > tol
+    from _tolreport import report
+
+    report(what, got, ref)
     assert not bad.any(), f"{what}: {bad.sum()} / {bad.size} out of tolerance; max err {err.max():.3e}, scale {scale:.3e}"
 
 

@@ -181,6 +181,9 @@ def _bf16_close(got, ref, what, rel=1e-2, frac=1e-3):
     moves the few outputs that read it by a discrete step."""
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)
+    from _tolreport import report
+
+    report(what, got, ref)
     scale = max(float(np.abs(ref).max()), 1e-6)
     err = np.abs(got - ref)
     bad = err > rel * scale + np.abs(ref) * 2.0 ** -7
