@@ -110,15 +110,10 @@ def _rel_fro(got, ref):
     return float(np.linalg.norm(np.asarray(got) - ref) / max(np.linalg.norm(ref), 1e-12))
 
 
-def _elem_check(got, ref, what, frac=0.0):
-    from _tolreport import report
+def _elem_check(got, ref, what, mx=False):
+    from _tolreport import check_layer_output
 
-    report(what, got, ref)
-    scale = max(float(np.abs(ref).max()), 1e-6)
-    err = np.abs(got - ref)
-    bad = err > 1e-2 * scale + np.abs(ref) * 2.0 ** -7
-    assert bad.sum() <= frac * bad.size, f"{what}: {bad.sum()} / {bad.size} out of tolerance; max err {err.max():.3e}"
-    return float(err.max() / scale)
+    return check_layer_output(got, ref, what, "mxfp8" if mx else "bf16")
 
 
 def _compare(c, g, ref_idx, ref_pos, ref_hist, ref_offsets, ref_y, ref_dx, ref_lb, ref_z, grads, margin, tok):
@@ -134,9 +129,8 @@ def _compare(c, g, ref_idx, ref_pos, ref_hist, ref_offsets, ref_y, ref_dx, ref_l
         np.testing.assert_array_equal(g["offsets"], ref_offsets)
     ok = same & np.all((g["pos"] >= 0) == (ref_pos >= 0), axis=1)
     sel = ok[tok]
-    frac = 1e-3 if c.mx else 0.0
-    y_err = _elem_check(g["y"][tok][sel], ref_y[sel], f"{c.name} y", frac)
-    dx_err = _elem_check(g["dx"][tok][sel], ref_dx[sel], f"{c.name} dx", frac)
+    y_err = _elem_check(g["y"][tok][sel], ref_y[sel], f"{c.name} y", c.mx)
+    dx_err = _elem_check(g["dx"][tok][sel], ref_dx[sel], f"{c.name} dx", c.mx)
     if c.mx:
         assert _rel_fro(g["y"][tok][sel], ref_y[sel]) <= 1e-2
         assert _rel_fro(g["dx"][tok][sel], ref_dx[sel]) <= 1e-2
@@ -178,9 +172,8 @@ def test_full_size_ep_layer_vs_oracle(hip_lib, name):
     st, gr = MC.run_oracle(c, inp)
     g = gpu_layer_ep(c, inp)
     np.testing.assert_array_equal(g["hist"], st.hist)
-    frac = 1e-3 if c.mx else 0.0
-    y_err = _elem_check(g["y"], st.y, f"{name} ep y", frac)
-    dx_err = _elem_check(g["dx"], gr["dx"], f"{name} ep dx", frac)
+    y_err = _elem_check(g["y"], st.y, f"{name} ep y", c.mx)
+    dx_err = _elem_check(g["dx"], gr["dx"], f"{name} ep dx", c.mx)
     assert abs(g["lb"] - st.lb) <= 1e-5 * max(1.0, abs(st.lb))
     assert abs(g["z"] - st.z) <= 1e-5 * max(1.0, abs(st.z))
     gtol = 1e-2 if c.mx else 5e-3

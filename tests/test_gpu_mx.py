@@ -174,20 +174,15 @@ def test_permute_mx_matches_oracle(hip_lib):
     np.testing.assert_array_equal(xs.cpu().numpy()[:Rk], (er + 127).astype(np.uint8))
 
 
-def _bf16_close(got, ref, what, rel=1e-2, frac=1e-3):
-    """bf16 tolerance on all but a fraction `frac` of the elements, and relative
-    Frobenius error <= 1e-2: an H element on an e4m3 rounding boundary (or at the
-    ReLU edge) can land on the other side after fp32 vs fp64 accumulation, which
-    moves the few outputs that read it by a discrete step."""
-    got = np.asarray(got, np.float64)
-    ref = np.asarray(ref, np.float64)
-    from _tolreport import report
+def _bf16_close(got, ref, what):
+    """MXFP8 layer outputs vs the oracle's MX emulation:
+    tests/_tolreport.check_layer_output with the mxfp8 limits (an H element on
+    an e4m3 rounding boundary, or at the ReLU edge, can land on the other side
+    after fp32 vs fp64 accumulation, moving the outputs that read it by an e4m3
+    step), and relative Frobenius error <= 1e-2."""
+    from _tolreport import check_layer_output
 
-    report(what, got, ref)
-    scale = max(float(np.abs(ref).max()), 1e-6)
-    err = np.abs(got - ref)
-    bad = err > rel * scale + np.abs(ref) * 2.0 ** -7
-    assert bad.sum() <= frac * bad.size, f"{what}: {bad.sum()} / {bad.size} out of tolerance; max err {err.max():.3e}"
+    check_layer_output(got, ref, what, "mxfp8")
     assert _rel_fro(got, ref) <= 1e-2, f"{what}: relative Frobenius error {_rel_fro(got, ref):.2e}"
 
 
