@@ -405,7 +405,17 @@ class TrainStep:
         losses = self.criterion(out, targets, num_boxes)
         loss = sum(losses.values()) + aux
         self._mark("criterion")
-        loss.backward()
+        if self.ddp is None and self.runner is None and images.is_cuda:
+            # dense weight gradients batched after the backward (DDP's reducer
+            # needs every gradient during the backward, so not under DDP)
+            with deferred_weight_grads() as deferred:
+                loss.backward()
+            if deferred is not None:
+                grads = merge_deferred(self.params, [p.grad for p in self.params], deferred)
+                for p, g in zip(self.params, grads):
+                    p.grad = g
+        else:
+            loss.backward()
         self._mark("backward")
         self._optimizer_step()
         self._mark("optimizer")
