@@ -75,6 +75,22 @@ class DeferredWgrad:
                 if (id(p_), r0) in seen:
                     shared.add(id(p_))
                 seen.add((id(p_), r0))
+        # rows each parameter receives: a buffer whose rows are all written by
+        # the kernel needs no zero fill
+        rows = {}
+        for gy, x, odt, (wp, wr), (bp, br) in self.items:
+            for p_, r0 in ((wp, wr), (bp, br)):
+                rows.setdefault(id(p_), []).append((r0, r0 + gy.shape[1]))
+
+        def covered(p_):
+            spans = sorted(rows[id(p_)])
+            end = 0
+            for a, b in spans:
+                if a != end:
+                    return False
+                end = b
+            return end == p_.shape[0]
+
         grads, acc = {}, {}
         direct = {torch.bfloat16: [], torch.float32: []}
         summed = []
@@ -85,7 +101,8 @@ class DeferredWgrad:
                     if id(p_) not in acc:
                         acc[id(p_)] = (torch.zeros(p_.shape, dtype=torch.float32, device=gy.device), odt)
                 elif id(p_) not in grads:
-                    grads[id(p_)] = torch.zeros(p_.shape, dtype=odt, device=gy.device)
+                    alloc = torch.empty if covered(p_) else torch.zeros
+                    grads[id(p_)] = alloc(p_.shape, dtype=odt, device=gy.device)
             if id(wp) in shared or id(bp) in shared:
                 dw = torch.empty((M, N), dtype=torch.float32, device=gy.device)
                 db = torch.empty((M,), dtype=torch.float32, device=gy.device)
