@@ -1557,6 +1557,7 @@ extern "C" int moe_set_tuning(const char* key, int value) {
   if (k == "xcd_map" && value >= 0 && value <= 2) { g_xcd_map = value; return 0; }
   if (k == "ksplit" && value >= 0 && value <= 8) { g_ksplit = value; return 0; }
   if (k == "gemm_pair" && value >= 0 && value <= 1) { g_gemm_pair_off = value ? 0 : 1; return 0; }
+  if (k == "msda_generic" && value >= 0 && value <= 3) { g_msda_generic = value; return 0; }
   return fail("moe_set_tuning: unknown key or value");
 }
 

@@ -9,6 +9,8 @@
 
 namespace moe {
 
+extern int g_msda_generic;  // msda.hip: 1 = generic fused MSDA kernels (moe_set_tuning "msda_generic")
+
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));

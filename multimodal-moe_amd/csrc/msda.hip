@@ -393,6 +393,215 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Level-batched fused kernels for the RT-DETR decoder's fixed L = LL, P = PP
+// (3 x 4): the loops are unrolled, the group's sampling offsets are loaded
+// once, and the 4 PP corner loads of a level are issued together -- the
+// generic kernels above issue one sample's offsets and corners per dependent
+// round trip (24 per (b, q, h) group).  The backward also issues level l+1's
+// corner loads BEFORE level l's value-gradient atomics: on gfx9 `vmcnt` counts
+// stores and atomics too, so loads issued after the atomics would wait for
+// them.  Same arithmetic, per sample and in the same order, as the generic
+// kernels (the location / offset gradients are written by lane `sample`
+// instead of lane 0).
+// ---------------------------------------------------------------------------
+int g_msda_generic = 0;  // moe_set_tuning("msda_generic", bits): 1 generic forward, 2 generic backward (A/B)
+
+template <int PP>
+struct MsdaLevelGeo {
+  uint32_t raw[PP][4];  // the 4 corners' bf16x2 channel pairs (0 outside the map)
+  float fx[PP], fy[PP];
+  int x0[PP], y0[PP];
+  uint32_t in;          // bit 4 p + c: corner c of sample p inside the map
+};
+
+template <int LPG, int LL, int PP>
+__device__ __forceinline__ void msda_level_geo(const MsdaLevels& lv, int l, const MsdaPrep& pr,
+                                               const uint32_t (&offw)[LL * PP], float offset_scale,
+                                               const uint16_t* vb, long long ldv, bool valid, MsdaLevelGeo<PP>& g) {
+  constexpr float invP = 1.f / (float)PP;
+  const int Hl = lv.h[l], Wl = lv.w[l];
+  g.in = 0u;
+#pragma unroll
+  for (int p = 0; p < PP; ++p) {
+    const int sp = l * PP + p;
+    const uint32_t ow = offw[sp];
+    const float ox = bf2f(f2bf(bf2f((uint16_t)(ow & 0xffffu)) * invP));
+    const float oy = bf2f(f2bf(bf2f((uint16_t)(ow >> 16)) * invP));
+    const float lx = pr.rx + ox * pr.rw * offset_scale;
+    const float ly = pr.ry + oy * pr.rh * offset_scale;
+    const float x = lx * Wl - 0.5f, y = ly * Hl - 0.5f;
+    const float xf = floorf(x), yf = floorf(y);
+    g.x0[p] = (int)xf;
+    g.y0[p] = (int)yf;
+    g.fx[p] = x - xf;
+    g.fy[p] = y - yf;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int xi = g.x0[p] + (c & 1), yi = g.y0[p] + (c >> 1);
+      const bool in = valid && xi >= 0 && xi < Wl && yi >= 0 && yi < Hl;
+      g.in |= in ? (1u << (4 * p + c)) : 0u;
+      g.raw[p][c] = in ? *reinterpret_cast<const uint32_t*>(vb + (size_t)(yi * Wl + xi) * ldv) : 0u;
+    }
+  }
+}
+
+__device__ __forceinline__ float2 unpack_bf16x2(uint32_t v) {
+  return make_float2(__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u));
+}
+
+template <int LPG, int LL, int PP>
+__global__ __launch_bounds__(256) void msda_fused_fwd_lp_kernel(
+    const uint16_t* __restrict__ value, const int32_t* __restrict__ shapes, const int32_t* __restrict__ starts,
+    const uint16_t* __restrict__ off, const float* __restrict__ ref, const uint16_t* __restrict__ logits,
+    float offset_scale, int B, int S, int Q, int H, long long ldv, uint16_t* __restrict__ out) {
+  constexpr int D = 2 * LPG;
+  constexpr int LP = LL * PP;
+  const MsdaLevels lv = load_levels(shapes, starts, LL);
+  const int groups = B * Q * H;
+  const int sub = threadIdx.x % LPG;
+  for (int gidx = (blockIdx.x * blockDim.x + threadIdx.x) / LPG; gidx < groups;
+       gidx += gridDim.x * blockDim.x / LPG) {
+    const int h = gidx % H;
+    const int b = gidx / (Q * H);
+    uint32_t offw[LP];
+    const uint32_t* op = reinterpret_cast<const uint32_t*>(off + (size_t)gidx * LP * 2);
+#pragma unroll
+    for (int i = 0; i < LP; ++i) offw[i] = op[i];
+    MsdaPrep pr;
+    msda_prep(logits, ref, gidx, H, LP, pr);
+    float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+    for (int l = 0; l < LL; ++l) {
+      const uint16_t* vb = value + ((size_t)b * S + lv.start[l]) * ldv + h * D + 2 * sub;
+      MsdaLevelGeo<PP> g;
+      msda_level_geo<LPG, LL, PP>(lv, l, pr, offw, offset_scale, vb, ldv, true, g);
+#pragma unroll
+      for (int p = 0; p < PP; ++p) {
+        const float fx = g.fx[p], fy = g.fy[p];
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (!(g.in & (1u << (4 * p + c)))) continue;
+          const float wgt = ((c & 1) ? fx : 1.f - fx) * ((c >> 1) ? fy : 1.f - fy);
+          const float2 v = unpack_bf16x2(g.raw[p][c]);
+          s0 += wgt * v.x;
+          s1 += wgt * v.y;
+        }
+        const float a = pr.a[l * PP + p];
+        acc0 += a * s0;
+        acc1 += a * s1;
+      }
+    }
+    *reinterpret_cast<uint32_t*>(out + (size_t)gidx * D + 2 * sub) = pack2bf(acc0, acc1);
+  }
+}
+
+template <int LPG, int LL, int PP>
+__global__ __launch_bounds__(256) void msda_fused_bwd_lp_kernel(
+    const uint16_t* __restrict__ value, const int32_t* __restrict__ shapes, const int32_t* __restrict__ starts,
+    const uint16_t* __restrict__ off, const float* __restrict__ ref, const uint16_t* __restrict__ logits,
+    float offset_scale, const uint16_t* __restrict__ grad_out, int B, int S, int Q, int H, long long ldv,
+    uint16_t* __restrict__ grad_value, uint16_t* __restrict__ grad_off, uint16_t* __restrict__ grad_logits) {
+  constexpr int D = 2 * LPG;
+  constexpr int LP = LL * PP;
+  constexpr float invP = 1.f / (float)PP;
+  const MsdaLevels lv = load_levels(shapes, starts, LL);
+  const int groups = B * Q * H;
+  const int sub = threadIdx.x % LPG;
+  const int ngrp_total = (gridDim.x * blockDim.x) / LPG;
+  const int first = (blockIdx.x * blockDim.x + threadIdx.x) / LPG;
+  const int iters = (groups + ngrp_total - 1) / ngrp_total;
+  for (int it = 0; it < iters; ++it) {  // uniform trip count: shuffles stay convergent
+    const int gidx = first + it * ngrp_total;
+    const bool valid = gidx < groups;
+    const int gi = valid ? gidx : 0;
+    const int h = gi % H;
+    const int b = gi / (Q * H);
+    uint32_t offw[LP];
+    const uint32_t* op = reinterpret_cast<const uint32_t*>(off + (size_t)gi * LP * 2);
+#pragma unroll
+    for (int i = 0; i < LP; ++i) offw[i] = op[i];
+    MsdaPrep pr;
+    msda_prep(logits, ref, gi, H, LP, pr);
+    const float2 g = valid ? ld_bf16x2(grad_out + (size_t)gi * D + 2 * sub) : make_float2(0.f, 0.f);
+    float my_ga = 0.f;        // ga of sample `sub`
+    uint32_t my_goff = 0u;    // packed offset gradient of sample `sub`
+    float dot = 0.f;          // sum_sp a_sp ga_sp (softmax backward)
+    MsdaLevelGeo<PP> geo[2];
+    {
+      const uint16_t* vb0 = value + ((size_t)b * S + lv.start[0]) * ldv + h * D + 2 * sub;
+      msda_level_geo<LPG, LL, PP>(lv, 0, pr, offw, offset_scale, vb0, ldv, valid, geo[0]);
+    }
+#pragma unroll
+    for (int l = 0; l < LL; ++l) {
+      MsdaLevelGeo<PP>& cur = geo[l & 1];
+      const int Hl = lv.h[l], Wl = lv.w[l];
+      const size_t gofs = ((size_t)b * S + lv.start[l]) * ldv + h * D + 2 * sub;
+      uint32_t pv[PP][4];
+#pragma unroll
+      for (int p = 0; p < PP; ++p) {
+        const int sp = l * PP + p;
+        const float fx = cur.fx[p], fy = cur.fy[p];
+        float2 v[2][2];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c >> 1][c & 1] = unpack_bf16x2(cur.raw[p][c]);
+        const float w00 = (1.f - fx) * (1.f - fy), w01 = fx * (1.f - fy);
+        const float w10 = (1.f - fx) * fy, w11 = fx * fy;
+        const float sx = w00 * v[0][0].x + w01 * v[0][1].x + w10 * v[1][0].x + w11 * v[1][1].x;
+        const float sy = w00 * v[0][0].y + w01 * v[0][1].y + w10 * v[1][0].y + w11 * v[1][1].y;
+        const float dxa = (1.f - fy) * (v[0][1].x - v[0][0].x) + fy * (v[1][1].x - v[1][0].x);
+        const float dxb = (1.f - fy) * (v[0][1].y - v[0][0].y) + fy * (v[1][1].y - v[1][0].y);
+        const float dya = (1.f - fx) * (v[1][0].x - v[0][0].x) + fx * (v[1][1].x - v[0][1].x);
+        const float dyb = (1.f - fx) * (v[1][0].y - v[0][0].y) + fx * (v[1][1].y - v[0][1].y);
+        float ga = g.x * sx + g.y * sy;
+        float gx = g.x * dxa + g.y * dxb;
+        float gy = g.x * dya + g.y * dyb;
+        ga = group_sum<LPG>(ga);
+        gx = group_sum<LPG>(gx);
+        gy = group_sum<LPG>(gy);
+        const float a = pr.a[sp];
+        dot += a * ga;
+        if (sub == sp) {  // d loc / d off = wh * offset_scale / P (straight through the bf16 rounding)
+          my_ga = ga;
+          const float glx = a * gx * Wl, gly = a * gy * Hl;
+          my_goff = pack2bf(glx * pr.rw * offset_scale * invP, gly * pr.rh * offset_scale * invP);
+        }
+        const float wc[4] = {w00, w01, w10, w11};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float s = a * wc[c];
+          bf16x2_t t;
+          t.x = (__bf16)(s * g.x);
+          t.y = (__bf16)(s * g.y);
+          pv[p][c] = *reinterpret_cast<uint32_t*>(&t);
+        }
+      }
+      if (l + 1 < LL) {  // next level's corner loads go out before this level's atomics
+        const uint16_t* vbn = value + ((size_t)b * S + lv.start[l + 1]) * ldv + h * D + 2 * sub;
+        msda_level_geo<LPG, LL, PP>(lv, l + 1, pr, offw, offset_scale, vbn, ldv, valid, geo[(l + 1) & 1]);
+      }
+#pragma unroll
+      for (int p = 0; p < PP; ++p)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (!(cur.in & (1u << (4 * p + c)))) continue;
+          const int xi = cur.x0[p] + (c & 1), yi = cur.y0[p] + (c >> 1);
+          bf16x2_t t = *reinterpret_cast<const bf16x2_t*>(&pv[p][c]);
+          __builtin_amdgcn_global_atomic_fadd_v2bf16(
+              (__attribute__((address_space(1))) bf16x2_t*)(grad_value + gofs + (size_t)(yi * Wl + xi) * ldv), t);
+        }
+    }
+    // softmax backward: d logit_sp = a_sp (ga_sp - sum_j a_j ga_j); lane `sub` writes sample sub
+    if (valid && sub < LP) {
+      const float a = msda_pick(pr.a, sub);
+      grad_logits[(size_t)gi * LP + sub] = f2bf(a * (my_ga - dot));
+      *reinterpret_cast<uint32_t*>(grad_off + ((size_t)gi * LP + sub) * 2) = my_goff;
+    }
+  }
+}
+
 }  // namespace moe
 
 using namespace moe;
@@ -491,7 +700,14 @@ extern "C" int rtdetr_msda_fused_fwd_ld(const void* value, long long ldv, const 
   const uint16_t* o = static_cast<const uint16_t*>(off);
   const uint16_t* lg = static_cast<const uint16_t*>(logits);
   uint16_t* y = static_cast<uint16_t*>(out);
-  if (D == 32)
+  const bool lp34 = L == 3 && P == 4 && !(g_msda_generic & 1);
+  if (D == 32 && lp34)
+    MOE_LAUNCH(prof, (msda_fused_fwd_lp_kernel<16, 3, 4>), dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v,
+               shapes, starts, o, ref, lg, offset_scale, B, S, Q, H, ldv, y);
+  else if (D == 64 && lp34)
+    MOE_LAUNCH(prof, (msda_fused_fwd_lp_kernel<32, 3, 4>), dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v,
+               shapes, starts, o, ref, lg, offset_scale, B, S, Q, H, ldv, y);
+  else if (D == 32)
     MOE_LAUNCH(prof, msda_fused_fwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
                o, ref, lg, offset_scale, B, S, Q, H, L, P, ldv, y);
   else
@@ -524,7 +740,14 @@ extern "C" int rtdetr_msda_fused_bwd_ld(const void* value, long long ldv, const 
   uint16_t* gv = static_cast<uint16_t*>(grad_value);
   uint16_t* gof = static_cast<uint16_t*>(grad_off);
   uint16_t* glg = static_cast<uint16_t*>(grad_logits);
-  if (D == 32)
+  const bool lp34 = L == 3 && P == 4 && !(g_msda_generic & 2);
+  if (D == 32 && lp34)
+    MOE_LAUNCH(prof, (msda_fused_bwd_lp_kernel<16, 3, 4>), dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v,
+               shapes, starts, o, ref, lg, offset_scale, go, B, S, Q, H, ldv, gv, gof, glg);
+  else if (D == 64 && lp34)
+    MOE_LAUNCH(prof, (msda_fused_bwd_lp_kernel<32, 3, 4>), dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v,
+               shapes, starts, o, ref, lg, offset_scale, go, B, S, Q, H, ldv, gv, gof, glg);
+  else if (D == 32)
     MOE_LAUNCH(prof, msda_fused_bwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
                o, ref, lg, offset_scale, go, B, S, Q, H, L, P, ldv, gv, gof, glg);
   else

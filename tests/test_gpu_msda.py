@@ -194,3 +194,51 @@ def test_batched_value_projection_matches_per_layer(hip_lib, precision, monkeypa
     for n, gref in res[0][2].items():
         assert n in res[1][2], n
         assert rel(res[1][2][n], gref) < 5e-2, (n, rel(res[1][2][n], gref))
+
+
+@pytest.mark.parametrize("D", [32, 64])
+def test_msda_level_batched_kernels_match_generic(hip_lib, D):
+    """The level-batched fused kernels (L = 3, P = 4: unrolled samples, one
+    offsets load per group, a level's corner loads issued together) against the
+    generic fused kernels (moe_set_tuning msda_generic) on the strided value
+    slice the decoder uses: forward bit-identical (same arithmetic in the same
+    order); offset / logit gradients within 1e-5 relative Frobenius (their
+    group reductions are identical, the stores move to other lanes); the value
+    gradient -- bf16 atomics, whose summation order differs -- within 1e-2."""
+    from src.moe import _lib as L
+    from src.rtdetr_moe.decoder import _level_tensors
+
+    g = torch.Generator().manual_seed(5)
+    shapes = [(46, 80), (23, 40), (12, 20)]
+    B, Q, H, Lv, P = 2, 300, 8, 3, 4
+    S = sum(h * w for h, w in shapes)
+    C = 3 * H * D
+    dev = "cuda"
+    value_all = torch.randn(B, S, C, generator=g).to(torch.bfloat16).to(dev)
+    off = (torch.randn(B, Q, H * Lv * P * 2, generator=g) * 2).to(torch.bfloat16).to(dev)
+    logits = torch.randn(B, Q, H * Lv * P, generator=g).to(torch.bfloat16).to(dev)
+    ref = torch.cat([torch.rand(B, Q, 2, generator=g) * 1.2 - 0.1, torch.rand(B, Q, 2, generator=g) * 0.3 + 0.02],
+                    -1).to(dev)  # some locations off the map: the zero-padding corners
+    gout = torch.randn(B, Q, H * D, generator=g).to(torch.bfloat16).to(dev)
+    st, so = _level_tensors(shapes, torch.device(dev))
+    col0 = H * D
+    res = {}
+    try:
+        for generic in (3, 0):
+            L.set_tuning("msda_generic", generic)
+            out = L.msda_fused_fwd_slice(value_all, col0, H, D, st, so, off, ref, logits, 0.5, Lv, P)
+            grad_all = torch.zeros(B, S, C, dtype=torch.bfloat16, device=dev)
+            go, gl = L.msda_fused_bwd_slice(value_all, grad_all, col0, H, D, st, so, off, ref, logits, 0.5, Lv, P, gout)
+            torch.cuda.synchronize()
+            res[generic] = (out, grad_all, go, gl)
+    finally:
+        L.set_tuning("msda_generic", 0)
+    (o3, gv3, go3, gl3), (o0, gv0, go0, gl0) = res[3], res[0]
+    assert torch.equal(o3, o0)
+    assert bool((gv0[..., :col0] == 0).all() and (gv0[..., col0 + H * D:] == 0).all())  # only this slice written
+
+    def rel(a, b):
+        return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+    assert rel(go0, go3) < 1e-5 and rel(gl0, gl3) < 1e-5, (rel(go0, go3), rel(gl0, gl3))
+    assert rel(gv0, gv3) < 1e-2, rel(gv0, gv3)
