@@ -106,6 +106,13 @@ int moe_route_dispatch(const int32_t* block_counts, int nblk, int T, int k, int 
 int moe_combine_fwd(const void* yp, const int32_t* pos, const float* topk_w,
                     int T, int d, int k, void* y, hipStream_t stream);
 
+/* a6 + the caller's residual branch (the AIFI and
+ * decoder layers compute norm(x + FFN(x))): y[t] = resid[t] + sum_j ...,
+ * summed in fp32 and rounded to bf16 once; resid bf16 [T,d] or NULL (then
+ * moe_combine_fwd).  Removes the separate residual add of every MoE layer. */
+int moe_combine_res_fwd(const void* yp, const int32_t* pos, const float* topk_w, const void* resid,
+                        int T, int d, int k, void* y, hipStream_t stream);
+
 /* a7, combine transpose: dyp[pos[t,j]] = topk_w[t,j] * dy[t] (bf16)
  * and dw[t,j] = <dy[t], yp[pos[t,j]]> (fp32; 0 when dropped). */
 int moe_combine_bwd(const void* dy, const void* yp, const int32_t* pos,
@@ -135,6 +142,17 @@ int moe_token_bwd_dw(const void* dxp, const int32_t* pos, const float* probs,
                      const float* lse, const float* dprob_bias, const float* zc,
                      const float* wg, int T, int d, int E, int k, int normalize,
                      void* dx, float* dlogits, hipStream_t stream);
+
+/* moe_token_bwd_dw plus a residual gradient: dx[t] += dres[t] (bf16 [T,d]
+ * or NULL), inside the same fp32 sum -- with moe_combine_res_fwd the layer's
+ * dx = dy + dispatch transpose + router term, so autograd never accumulates
+ * the residual branch's gradient with a separate add. */
+int moe_token_bwd_res(const void* dxp, const int32_t* pos, const float* probs,
+                      const int32_t* topk_idx, const float* topk_w, const float* dw,
+                      const void* dy, const void* yp, float* dw_out, const void* dres,
+                      const float* lse, const float* dprob_bias, const float* zc,
+                      const float* wg, int T, int d, int E, int k, int normalize,
+                      void* dx, float* dlogits, hipStream_t stream);
 
 /* Grouped GEMM data types / epilogues. */
 enum moe_dtype { MOE_BF16 = 0, MOE_FP8_E4M3 = 1 };
@@ -355,6 +373,26 @@ int rtdetr_avgpool2x2_nhwc_bwd(const void* gy, int B, int H, int W, int C, void*
 int rtdetr_bias_grad_parts(long long M, int N);
 int rtdetr_bias_grad(const void* dy, long long M, int N, float* partials, int P, void* out, int out_bf16,
                      hipStream_t stream);
+
+/* Residual add + LayerNorm over the last dim of bf16 rows (the post-norm
+ * sites of the AIFI / decoder layers, norm(x + sublayer(x)), incl. the MoE
+ * layers' norm(x + MoEFFN(x)); reference engine: Ultralytics RT-DETR
+ * transformer layers, rtdetr.py:82-94):
+ *   out = (s - mean) * rstd * gamma + beta,  s = a + b (b may be NULL),
+ * fp32 statistics (biased variance), bf16 out, mean / rstd fp32 [T] saved for
+ * the backward.  d = 128, 256 or 512; gamma / beta bf16 (w_bf16 = 1) or fp32.
+ * Backward: ds = d out / d s (bf16 [T, d]; the gradient of a and of b) and
+ * [dgamma; dbeta] (2 x d, the parameter dtype) from P block partials
+ * (fp32 [P, 2d], caller-owned, P = rtdetr_add_layer_norm_parts(T)), summed
+ * in a fixed order (deterministic, no atomics).  Replaces the residual add
+ * and torch's native_layer_norm / native_layer_norm_backward. */
+int rtdetr_add_layer_norm_parts(long long T);
+int rtdetr_add_layer_norm_fwd(const void* a, const void* b, const void* gamma, const void* beta, int w_bf16,
+                              long long T, int d, float eps, void* out, float* mean, float* rstd,
+                              hipStream_t stream);
+int rtdetr_add_layer_norm_bwd(const void* dout, const void* a, const void* b, const void* gamma, int w_bf16,
+                              const float* mean, const float* rstd, long long T, int d, void* ds, float* partials,
+                              int P, void* dgamma_dbeta, hipStream_t stream);
 
 /* Decoder box refinement (one launch each way), over n = B*Q*4 elements:
  *   y = sigmoid(delta + log(max(x', eps) / max(1 - x', eps))), x' = clamp(ref, 0, 1)

@@ -68,7 +68,8 @@ __global__ __launch_bounds__(256) void route_index_kernel(
 
 __global__ __launch_bounds__(256) void combine_fwd_kernel(
     const uint16_t* __restrict__ yp, const int32_t* __restrict__ pos,
-    const float* __restrict__ topk_w, int T, int d, int k, uint16_t* __restrict__ y) {
+    const float* __restrict__ topk_w, int T, int d, int k, uint16_t* __restrict__ y,
+    const uint16_t* __restrict__ resid) {
   const int tid = threadIdx.x;
   const int sub = tid & 15;
   const int nchunk = d >> 7;
@@ -84,8 +85,12 @@ __global__ __launch_bounds__(256) void combine_fwd_kernel(
     for (int c = 0; c < nchunk; ++c) {
       const int ch = sub + 16 * c;
       float acc[8];
+      if (resid != nullptr) {  // the layer's residual: y = x + sum (one bf16 rounding)
+        unpack8(reinterpret_cast<const uint4*>(resid + (size_t)t * d)[ch], acc);
+      } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+        for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+      }
       _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
         if (pj[j] < 0) continue;
         float v[8];
@@ -188,17 +193,23 @@ extern "C" int moe_route_index(const int32_t* topk_idx, const int32_t* local_ran
   return check_launch("moe_route_index");
 }
 
-extern "C" int moe_combine_fwd(const void* yp, const int32_t* pos, const float* topk_w,
-                               int T, int d, int k, void* y, hipStream_t stream) {
+extern "C" int moe_combine_res_fwd(const void* yp, const int32_t* pos, const float* topk_w, const void* resid,
+                                   int T, int d, int k, void* y, hipStream_t stream) {
   if (check_row_width(d, "combine")) return -1;
   if (k < 1 || k > 8) return fail("combine: need 1<=k<=8");
   if (T <= 0) return 0;
-  // bytes: T*k expert rows + pos/w read, y written
-  ProfScope prof(stream, PROF_ROWMOVE, 2.0 * T * d + 2.0 * T * k * d + 8.0 * T * k);
+  // bytes: T*k expert rows + pos/w (+ the residual rows) read, y written
+  ProfScope prof(stream, PROF_ROWMOVE,
+                 2.0 * T * d + 2.0 * T * k * d + 8.0 * T * k + (resid != nullptr ? 2.0 * T * d : 0.0));
   MOE_LAUNCH(prof, combine_fwd_kernel, dim3(rows_grid(T)), dim3(256), 0, stream,
                      static_cast<const uint16_t*>(yp), pos, topk_w, T, d, k,
-                     static_cast<uint16_t*>(y));
+                     static_cast<uint16_t*>(y), static_cast<const uint16_t*>(resid));
   return check_launch("moe_combine_fwd");
+}
+
+extern "C" int moe_combine_fwd(const void* yp, const int32_t* pos, const float* topk_w,
+                               int T, int d, int k, void* y, hipStream_t stream) {
+  return moe_combine_res_fwd(yp, pos, topk_w, nullptr, T, d, k, y, stream);
 }
 
 extern "C" int moe_combine_bwd(const void* dy, const void* yp, const int32_t* pos,

@@ -197,6 +197,37 @@ struct Tile {
       const int ntn = p.N / BN;
       nt = slot % ntn;
       int rem = (slot / ntn) * 8 + xcd;  // global row-tile index (round-robin map)
+      if (p.G <= 64) {
+        // one load of the offsets and one lane scan give both the total (for
+        // the contiguous map) and the group: every workgroup's first
+        // dependent chain (the generic path below loads and reduces twice)
+        int lo = 0, hi = 0;
+        if (lane < p.G) {
+          lo = p.offsets[lane];
+          hi = p.offsets[lane + 1];
+        }
+        const int tg = (hi - lo + BM - 1) / BM;
+        int incl = tg;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int v = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += v;
+        }
+        if (p.xmap == 1) {
+          const int C = (__shfl(incl, 63, 64) + 7) / 8;
+          const int r = slot / ntn;
+          if (r >= C) return false;
+          rem = xcd * C + r;
+        }
+        const unsigned long long hit = __ballot(incl > rem);
+        if (!hit) return false;  // beyond the last tile (grid is an upper bound)
+        const int src = __builtin_ctzll(hit);
+        g = src;
+        mt = rem - __shfl(incl - tg, src, 64);
+        row0 = __shfl(lo, src, 64) + mt * BM;
+        rows_g = __shfl(hi, src, 64) - row0;
+        tile_id = rem * ntn + nt;
+      } else {
       if (p.xmap == 1) {
         // contiguous map: XCD x owns row tiles [x C, (x+1) C), C = ceil(total / 8), so
         // its L2 sees the weights of ~1-2 experts instead of all of them
@@ -243,6 +274,7 @@ struct Tile {
       }
       if (g < 0) return false;  // beyond the last tile (grid is an upper bound)
       tile_id = rem * ntn + nt;
+      }  // G > 64
     } else {
       const int ntn = p.N / BN;
       const int tpg = (p.M / BM) * ntn;  // tiles per group
@@ -865,6 +897,7 @@ __device__ __forceinline__ void gemm_v1_body(const GemmParams& p, int bid, char*
   const float* ask = (AG && p.x_scale != nullptr) ? p.x_scale + t.row0 : nullptr;
   int ai[AG ? RegStage<BM, A_K>::kPer : 1];
   float as_[AG ? RegStage<BM, A_K>::kPer : 1];
+  float dsc[AG ? RegStage<BM, A_K>::kPer : 1];  // scales of the tile in flight (applied at the LDS store)
   auto load_a_index = [&](int kt) {
     if constexpr (AG) {
       if (agk != nullptr && kt < t.nk) {
@@ -877,7 +910,13 @@ __device__ __forceinline__ void gemm_v1_body(const GemmParams& p, int bid, char*
     if constexpr (AG) {
       if (agk != nullptr) {
         la.load_gathered(p.a + t.m0, p.lda, ai, tid);
-        if (ask != nullptr) la.scale(as_);
+        // the scale is applied when the tile is written to LDS: multiplying
+        // here would wait on these loads before the tile in LDS is computed
+        // and before the B loads are issued (two round trips per K-tile)
+        if (ask != nullptr) {
+#pragma unroll
+          for (int i = 0; i < RegStage<BM, A_K>::kPer; ++i) dsc[i] = as_[i];
+        }
         load_a_index(kt + 1);
         return;
       }
@@ -912,10 +951,16 @@ __device__ __forceinline__ void gemm_v1_body(const GemmParams& p, int bid, char*
     if constexpr (Y8) ly.store(dst, tid);
     else lb.store(dst, tid);
   };
+  auto store_a = [&](char* dst) {
+    if constexpr (AG) {
+      if (ask != nullptr) la.scale(dsc);
+    }
+    la.store(dst, tid);
+  };
   if (t.nk > 0) {
     load_a(0);
     load_b(0);
-    la.store(smem, tid);
+    store_a(smem);
     store_b(smem + A_BYTES);
   }
   __syncthreads();
@@ -929,7 +974,7 @@ __device__ __forceinline__ void gemm_v1_body(const GemmParams& p, int bid, char*
     compute_tile<BM, BN, A_K, B_K, COLSUM>(cur, cur + A_BYTES, acc, csum, lane, wm, wn);
     if (more) {
       char* nxt = smem + ((kt + 1) & 1) * BUF;
-      la.store(nxt, tid);
+      store_a(nxt);
       store_b(nxt + A_BYTES);
     }
     __syncthreads();

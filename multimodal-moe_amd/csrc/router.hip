@@ -597,7 +597,8 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
     const float* __restrict__ zc_ptr,
     const float* __restrict__ wg, int T, int d, int E, int k, int normalize,
     uint16_t* __restrict__ dx, float* __restrict__ dlogits,
-    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ yp, float* __restrict__ dw_out) {
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ yp, float* __restrict__ dw_out,
+    const uint16_t* __restrict__ dres) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_wg = reinterpret_cast<float*>(smem);  // [E][d]
   const int tid = threadIdx.x;
@@ -694,8 +695,12 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
     for (int c = 0; c < nchunk; ++c) {
       const int ch = sub + 16 * c;
       float acc[8];
+      if (dres != nullptr) {  // the residual branch's gradient (combine with resid: dres = dy)
+        unpack8(reinterpret_cast<const uint4*>(dres + (size_t)t * d)[ch], acc);
+      } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+        for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+      }
       _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
         if (pj[j] < 0) continue;
         float v[8];
@@ -814,12 +819,22 @@ extern "C" int moe_route_dispatch(const int32_t* block_counts, int nblk, int T, 
   return check_launch("moe_route_dispatch");
 }
 
+extern "C" int moe_token_bwd_res(const void* dxp, const int32_t* pos, const float* probs,
+                                 const int32_t* topk_idx, const float* topk_w, const float* dw,
+                                 const void* dy, const void* yp, float* dw_out, const void* dres,
+                                 const float* lse, const float* dprob_bias, const float* zc,
+                                 const float* wg, int T, int d, int E, int k, int normalize,
+                                 void* dx, float* dlogits, hipStream_t stream);
+
 extern "C" int moe_token_bwd_dw(const void* dxp, const int32_t* pos, const float* probs,
                                 const int32_t* topk_idx, const float* topk_w, const float* dw,
                                 const void* dy, const void* yp, float* dw_out,
                                 const float* lse, const float* dprob_bias, const float* zc,
                                 const float* wg, int T, int d, int E, int k, int normalize,
-                                void* dx, float* dlogits, hipStream_t stream);
+                                void* dx, float* dlogits, hipStream_t stream) {
+  return moe_token_bwd_res(dxp, pos, probs, topk_idx, topk_w, dw, dy, yp, dw_out, nullptr, lse, dprob_bias, zc,
+                           wg, T, d, E, k, normalize, dx, dlogits, stream);
+}
 
 extern "C" int moe_token_bwd(const void* dxp, const int32_t* pos, const float* probs,
                              const int32_t* topk_idx, const float* topk_w, const float* dw,
@@ -831,12 +846,12 @@ extern "C" int moe_token_bwd(const void* dxp, const int32_t* pos, const float* p
                           wg, T, d, E, k, normalize, dx, dlogits, stream);
 }
 
-extern "C" int moe_token_bwd_dw(const void* dxp, const int32_t* pos, const float* probs,
-                                const int32_t* topk_idx, const float* topk_w, const float* dw,
-                                const void* dy, const void* yp, float* dw_out,
-                                const float* lse, const float* dprob_bias, const float* zc,
-                                const float* wg, int T, int d, int E, int k, int normalize,
-                                void* dx, float* dlogits, hipStream_t stream) {
+extern "C" int moe_token_bwd_res(const void* dxp, const int32_t* pos, const float* probs,
+                                 const int32_t* topk_idx, const float* topk_w, const float* dw,
+                                 const void* dy, const void* yp, float* dw_out, const void* dres,
+                                 const float* lse, const float* dprob_bias, const float* zc,
+                                 const float* wg, int T, int d, int E, int k, int normalize,
+                                 void* dx, float* dlogits, hipStream_t stream) {
   if (dw == nullptr && (dy == nullptr || yp == nullptr)) return fail("token_bwd: need dw, or dy and yp");
   if (d <= 0 || d % 128 != 0 || d > 1024) return fail("token_bwd: d must be a multiple of 128 in [128,1024]");
   if (E < 1 || E > 64 || k < 1 || k > 8 || k > E) return fail("token_bwd: need 1<=E<=64, 1<=k<=min(8,E)");
@@ -852,14 +867,15 @@ extern "C" int moe_token_bwd_dw(const void* dxp, const int32_t* pos, const float
   // (+ dy and the T*k rows of Yp when dw is formed here)
   ProfScope prof(stream, PROF_TOKEN_BWD,
                  2.0 * T * k * d + 2.0 * T * d + 8.0 * T * E + 20.0 * T * k + 4.0 * T + 4.0 * E * d +
-                     (dw == nullptr ? 2.0 * T * d + 2.0 * T * k * d : 0.0));
+                     (dw == nullptr ? 2.0 * T * d + 2.0 * T * k * d : 0.0) +
+                     (dres != nullptr && dres != dy ? 2.0 * T * d : 0.0));
   const uint16_t* dyb = static_cast<const uint16_t*>(dy);
   const uint16_t* ypb = static_cast<const uint16_t*>(yp);
 #define LAUNCH_B(EM)                                                                          \
   allow_lds<token_bwd_kernel<EM>>(shmem);                                                   \
   MOE_LAUNCH(prof, token_bwd_kernel<EM>, dim3(grid), dim3(256), shmem, stream, dxpb, pos, \
                      probs, topk_idx, topk_w, dw, lse, dprob_bias, zc, wg, T, d, E, k,      \
-                     normalize, dxb, dlogits, dyb, ypb, dw_out)
+                     normalize, dxb, dlogits, dyb, ypb, dw_out, static_cast<const uint16_t*>(dres))
   switch (em) {
     case 8: LAUNCH_B(8); break;
     case 16: LAUNCH_B(16); break;

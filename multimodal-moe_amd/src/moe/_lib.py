@@ -46,6 +46,9 @@ SIGNATURES = {
     "moe_grouped_gemm_bwd_pair": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                        _I, _I, _I, _P]),
     "moe_token_bwd_dw": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "moe_token_bwd_res": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P,
+                               _P]),
+    "moe_combine_res_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "moe_quantize_mx": (_I, [_P, ctypes.c_longlong, _I, _P, _P, _P]),
     "moe_permute_fwd_mx": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_mx": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
@@ -61,6 +64,9 @@ SIGNATURES = {
     "rtdetr_avgpool2x2_nhwc_bwd": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "rtdetr_bias_grad_parts": (_I, [ctypes.c_longlong, _I]),
     "rtdetr_bias_grad": (_I, [_P, ctypes.c_longlong, _I, _P, _I, _P, _I, _P]),
+    "rtdetr_add_layer_norm_parts": (_I, [ctypes.c_longlong]),
+    "rtdetr_add_layer_norm_fwd": (_I, [_P, _P, _P, _P, _I, ctypes.c_longlong, _I, _F, _P, _P, _P, _P]),
+    "rtdetr_add_layer_norm_bwd": (_I, [_P, _P, _P, _P, _I, _P, _P, ctypes.c_longlong, _I, _P, _P, _I, _P, _P]),
     "rtdetr_box_refine_fwd": (_I, [_P, _I, _P, ctypes.c_longlong, _F, _P, _P]),
     "rtdetr_box_refine_bwd": (_I, [_P, _P, _P, _P, ctypes.c_longlong, _F, _P, _I, _P, _P]),
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
@@ -325,13 +331,21 @@ def permute_fwd(x, topk_idx, local_rank, rank_base, offsets, E, cap, rows_alloc)
     return xp, pos
 
 
-def combine_fwd(yp, pos, topk_w, T):
+def combine_fwd(yp, pos, topk_w, T, resid=None):
+    """y = sum_j topk_w[t,j] yp[pos[t,j]] (+ resid[t] when given: the layer's residual, one rounding)."""
     d = yp.shape[1]
     k = pos.shape[1]
     _need(yp, torch.bfloat16, "yp")
     y = torch.empty((T, d), dtype=torch.bfloat16, device=yp.device)
-    rc = lib().moe_combine_fwd(
-        _ptr(yp), _ptr(pos), _ptr(topk_w), T, d, k, _ptr(y), _stream())
+    if resid is not None:
+        _need(resid, torch.bfloat16, "resid")
+        if tuple(resid.shape) != (T, d):
+            raise MoEKernelError(f"combine_fwd: resid shape {tuple(resid.shape)} != {(T, d)}")
+        rc = lib().moe_combine_res_fwd(
+            _ptr(yp), _ptr(pos), _ptr(topk_w), _ptr(resid), T, d, k, _ptr(y), _stream())
+    else:
+        rc = lib().moe_combine_fwd(
+            _ptr(yp), _ptr(pos), _ptr(topk_w), T, d, k, _ptr(y), _stream())
     _check(rc, "moe_combine_fwd")
     return y
 
@@ -466,8 +480,10 @@ def grouped_gemm_bwd_pair(a, b, offsets, G, max_rows, N, K, epilogue, aux, wx, w
     return c, wc, cs
 
 
-def token_bwd_dw(dxp, pos, probs, topk_idx, topk_w, dy, yp, lse, dprob_bias, zc, wg, normalize, want_dw=False):
-    """token_bwd forming dw = <dy[t], yp[pos]> itself (no combine_bwd): -> (dx, dlogits, dw or None)."""
+def token_bwd_dw(dxp, pos, probs, topk_idx, topk_w, dy, yp, lse, dprob_bias, zc, wg, normalize, want_dw=False,
+                 dres=None):
+    """token_bwd forming dw = <dy[t], yp[pos]> itself (no combine_bwd): -> (dx, dlogits, dw or None).
+    dres (bf16 [T, d]): a residual gradient added into dx (moe_token_bwd_res)."""
     T, k = pos.shape
     E, d = wg.shape
     _need(dy, torch.bfloat16, "dy")
@@ -475,6 +491,15 @@ def token_bwd_dw(dxp, pos, probs, topk_idx, topk_w, dy, yp, lse, dprob_bias, zc,
     dx = torch.empty((T, d), dtype=torch.bfloat16, device=wg.device)
     dlogits = torch.empty((T, E), dtype=torch.float32, device=wg.device)
     dw = torch.empty((T, k), dtype=torch.float32, device=wg.device) if want_dw else None
+    if dres is not None:
+        _need(dres, torch.bfloat16, "dres")
+        if tuple(dres.shape) != (T, d):
+            raise MoEKernelError(f"token_bwd: dres shape {tuple(dres.shape)} != {(T, d)}")
+        _check(lib().moe_token_bwd_res(_ptr(dxp), _ptr(pos), _ptr(probs), _ptr(topk_idx), _ptr(topk_w), None,
+                                       _ptr(dy), _ptr(yp), _ptr(dw), _ptr(dres), _ptr(lse), _ptr(dprob_bias),
+                                       _ptr(zc), _ptr(wg), T, d, E, k, int(normalize), _ptr(dx), _ptr(dlogits),
+                                       _stream()), "moe_token_bwd_res")
+        return dx, dlogits, dw
     _check(lib().moe_token_bwd_dw(_ptr(dxp), _ptr(pos), _ptr(probs), _ptr(topk_idx), _ptr(topk_w), None, _ptr(dy),
                                   _ptr(yp), _ptr(dw), _ptr(lse), _ptr(dprob_bias), _ptr(zc), _ptr(wg), T, d, E, k,
                                   int(normalize), _ptr(dx), _ptr(dlogits), _stream()), "moe_token_bwd_dw")

@@ -54,8 +54,10 @@ class MoEFFN(nn.Module):
         self.last_hist = None  # int32 [E] expert histogram of the last forward
         self.last_ep_overflow = None  # EP without capacity: assignments beyond the a2a slots (device)
 
-    def forward(self, x: torch.Tensor, ctx_img: torch.Tensor | None) -> torch.Tensor:
-        """x [B, L, d] (image-major tokens), ctx_img int [B] -> [B, L, d]."""
+    def forward(self, x: torch.Tensor, ctx_img: torch.Tensor | None, residual: bool = False) -> torch.Tensor:
+        """x [B, L, d] (image-major tokens), ctx_img int [B] -> [B, L, d].
+        residual=True returns x + FFN(x) (the caller's residual branch; on the
+        single-GPU bf16 path fused into the combine and token_bwd kernels)."""
         B, L, d = x.shape
         cfg = self.cfg
         flat = x.reshape(B * L, d)
@@ -72,7 +74,7 @@ class MoEFFN(nn.Module):
 
             y, aux, raw, hist = moe_ffn_hip(flat, self.wg, cb, self.w1, self.b1, self.w2, self.b2,
                                             ci, L, cfg.top_k, cfg.normalize, cap, cfg.expert_dtype,
-                                            aux_coefs=(cfg.lb_coef, cfg.z_coef))
+                                            aux_coefs=(cfg.lb_coef, cfg.z_coef), residual=residual)
             self.last_aux = (raw[0], raw[1])
             self.last_aux_weighted = aux
             self.last_hist = hist
@@ -83,6 +85,8 @@ class MoEFFN(nn.Module):
             y, lb, z, hist = moe_ffn_eager(flat, self.wg, cb, self.w1, self.b1, self.w2, self.b2,
                                            ci, L, cfg.top_k, cfg.normalize, cap, cfg.expert_dtype)
         y = y.to(x.dtype)
+        if residual:
+            y = flat + y
         self.last_aux = (lb, z)
         self.last_aux_weighted = None
         self.last_hist = hist

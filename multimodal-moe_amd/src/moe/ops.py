@@ -29,6 +29,8 @@ backward reads row 0: dprob_bias = d_auxp[0, :E], z-loss scale = 2 d_auxp[0, E].
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -344,6 +346,10 @@ def route_dispatch_mx_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normali
                                   int(cap), rows, int(pad)) + (rows,)
 
 
+# MOE_FUSE_RESIDUAL=0: the residual add stays a torch add (A/B switch)
+_FUSE_RESIDUAL = os.environ.get("MOE_FUSE_RESIDUAL", "1") != "0"
+
+
 class _MoELayer(torch.autograd.Function):
     """The whole single-GPU bf16 routed FFN of one layer as ONE autograd node
     (SURVEY 8(a) rows a2-a7), 8 HIP launches forward + backward:
@@ -358,10 +364,15 @@ class _MoELayer(torch.autograd.Function):
     plus the router weight gradient dlogits^T x (one torch GEMM) and the
     context-bias gradient (index_add).  Outputs: y, then (weighted=True) the
     layer's lb_coef lb + z_coef z and the detached raw (lb, z), or
-    (weighted=False) lb and z as separate differentiable outputs; hist."""
+    (weighted=False) lb and z as separate differentiable outputs; hist.
+    residual=True (x in bf16): y = x + FFN(x) -- the caller's residual add
+    folded into combine (one bf16 rounding) and its gradient into token_bwd
+    (dx = dy + ...), so neither the forward add nor autograd's gradient
+    accumulation for x runs as a separate launch."""
 
     @staticmethod
-    def forward(ctx, x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tpi, k, normalize, cap, lb_coef, z_coef, weighted):
+    def forward(ctx, x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tpi, k, normalize, cap, lb_coef, z_coef, weighted,
+                residual=False):
         T, d = x.shape
         E = wg.shape[0]
         G, F, _ = w1.shape
@@ -377,7 +388,8 @@ class _MoELayer(torch.autograd.Function):
         h = L.grouped_gemm_gather(xb, tok, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU,
                                   bias=b1.float().contiguous())
         yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=b2.float().contiguous())
-        y = L.combine_fwd(yp, pos, w, T)
+        y = L.combine_fwd(yp, pos, w, T, resid=xb if residual else None)
+        ctx.residual = bool(residual)
         ctx.save_for_backward(xb, wg32, idx, w, probs, lse, pos, tok, gate, h, yp, w1b, w2b, offsets, wcoef,
                               ctx_img if ctx_img is not None else torch.empty(0))
         ctx.meta = (T, d, E, G, rows, int(normalize), tpi, cb is not None,
@@ -418,23 +430,30 @@ class _MoELayer(torch.autograd.Function):
             # wcoef holds d lb / d partials (lb_coef = 1) and d z / d partials (z_coef = 1)
             dprob_bias = (g_a.float() * wcoef[:E]).contiguous() if g_a is not None else None
             zc = (2.0 * g_b.float() * wcoef[E:E + 1]).contiguous() if g_b is not None else None
-        dx, dlogits, _ = L.token_bwd_dw(dxp, pos, probs, idx, w, dyb, yp, lse, dprob_bias, zc, wg32, normalize)
+        dx, dlogits, _ = L.token_bwd_dw(dxp, pos, probs, idx, w, dyb, yp, lse, dprob_bias, zc, wg32, normalize,
+                                        dres=dyb if ctx.residual else None)
         dwg = dlogits.t().mm(xb.float())
         dcb = None
         if has_ctx:
             dcb = torch.zeros((C, E), dtype=torch.float32, device=dy.device)
             dcb.index_add_(0, ctx_img.long(), dlogits.view(-1, tpi, E).sum(1))
-        return (dx.to(xdtype), dwg, dcb, dW1, db1, dW2, db2) + (None,) * 8
+        return (dx.to(xdtype), dwg, dcb, dW1, db1, dW2, db2) + (None,) * 9
 
 
-def moe_layer_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap, aux_coefs=None):
+def moe_layer_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap, aux_coefs=None,
+                  residual=False):
     """_MoELayer: -> (y, lb_coef lb + z_coef z, raw (lb, z), hist) with aux_coefs,
-    else (y, lb, z, hist)."""
+    else (y, lb, z, hist); residual=True returns x + y (fused for bf16 x)."""
+    fuse = bool(residual) and x.dtype == torch.bfloat16 and _FUSE_RESIDUAL
     if aux_coefs is not None:
-        return _MoELayer.apply(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, int(tokens_per_image), int(k),
-                               bool(normalize), int(cap), float(aux_coefs[0]), float(aux_coefs[1]), True)
-    return _MoELayer.apply(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, int(tokens_per_image), int(k), bool(normalize),
-                           int(cap), 1.0, 1.0, False)
+        out = _MoELayer.apply(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, int(tokens_per_image), int(k),
+                              bool(normalize), int(cap), float(aux_coefs[0]), float(aux_coefs[1]), True, fuse)
+    else:
+        out = _MoELayer.apply(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, int(tokens_per_image), int(k),
+                              bool(normalize), int(cap), 1.0, 1.0, False, fuse)
+    if residual and not fuse:  # fp32 activations (amp): keep the residual add in x's precision
+        out = (x + out[0],) + tuple(out[1:])
+    return out
 
 
 def route_index_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize, cap, aux_coefs=None):
@@ -465,7 +484,7 @@ def combine_hip(yp, w, pos, T):
 
 
 def moe_ffn_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap,
-                expert_dtype="bf16", aux_coefs=None):
+                expert_dtype="bf16", aux_coefs=None, residual=False):
     """Routed expert FFN of one layer on the GPU.
 
     x [T, d] (tokens of ``T // tokens_per_image`` images, image-major),
@@ -475,6 +494,8 @@ def moe_ffn_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, n
     Returns (y bf16 [T, d], lb_raw, z_raw, hist int32 [E]); with
     aux_coefs = (lb_coef, z_coef) it returns (y, aux, (lb, z) detached, hist)
     instead, aux = lb_coef lb + z_coef z from the fused aux-loss kernel.
+    residual=True: the first output is x + y (the layer's residual branch;
+    fused into combine / token_bwd on the bf16 path).
     """
     if not x.is_cuda:
         raise L.MoEKernelError("moe_ffn_hip needs GPU tensors")
@@ -489,8 +510,10 @@ def moe_ffn_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, n
         yp = expert_ffn_mx_hip(carrier, xq, xs, w1, b1, w2, b2, offsets, rows)
     else:
         return moe_layer_hip(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k, normalize, cap,
-                             aux_coefs)
+                             aux_coefs, residual=residual)
     y = combine_hip(yp, w, pos, T)
+    if residual:
+        y = x + y.to(x.dtype)
     if aux_coefs is not None:
         aux, raw = aux_loss_weighted(auxp, hist, T, k, *aux_coefs)
         return y, aux, raw, hist

@@ -16,6 +16,7 @@ import torch.nn.functional as F
 from .linear import TokenLinear, TokenSelfAttention, bias_grad, chunked_wgrad
 from ..moe.config import MoEConfig
 from .encoder import HybridEncoder, make_ffn
+from .norm import AddLayerNorm
 
 
 def inverse_sigmoid(x, eps=1e-5):
@@ -320,16 +321,16 @@ class TransformerDecoderLayer(nn.Module):
     def __init__(self, d=256, nhead=8, hidden=1024, nlevels=3, npoints=4, moe: MoEConfig | None = None):
         super().__init__()
         self.self_attn = TokenSelfAttention(d, nhead)
-        self.norm1 = nn.LayerNorm(d)
+        self.norm1 = AddLayerNorm(d)  # LayerNorm(a + b), fused on the GPU (norm.py)
         self.cross_attn = MSDeformableAttention(d, nhead, nlevels, npoints)
-        self.norm2 = nn.LayerNorm(d)
+        self.norm2 = AddLayerNorm(d)
         self.ffn = make_ffn(d, hidden, moe, act="relu")
-        self.norm3 = nn.LayerNorm(d)
+        self.norm3 = AddLayerNorm(d)
 
     def forward(self, tgt, ref_boxes, memory, shapes, query_pos, ctx, vslot=None):
-        tgt = self.norm1(tgt + self.self_attn(tgt + query_pos, tgt))
-        tgt = self.norm2(tgt + self.cross_attn(tgt + query_pos, ref_boxes, memory, shapes, vslot))
-        tgt = self.norm3(tgt + self.ffn(tgt, ctx))
+        tgt = self.norm1(tgt, self.self_attn(tgt + query_pos, tgt))
+        tgt = self.norm2(tgt, self.cross_attn(tgt + query_pos, ref_boxes, memory, shapes, vslot))
+        tgt = self.norm3(self.ffn(tgt, ctx, residual=True))  # tgt + FFN(tgt)
         return tgt
 
 
@@ -348,7 +349,7 @@ class RTDETRDecoder(nn.Module):
             TransformerDecoderLayer(hidden, nhead, dim_feedforward, self.nlevels, npoints, moe)
             for _ in range(num_layers)])
         self.query_pos_head = MLP(4, 2 * hidden, hidden, 2)
-        self.enc_output = nn.Sequential(TokenLinear(hidden, hidden), nn.LayerNorm(hidden))
+        self.enc_output = nn.Sequential(TokenLinear(hidden, hidden), AddLayerNorm(hidden))
         self.enc_score_head = TokenLinear(hidden, num_classes)
         self.enc_bbox_head = MLP(hidden, hidden, 4, 3)
         self.dec_score_head = nn.ModuleList([TokenLinear(hidden, num_classes) for _ in range(num_layers)])

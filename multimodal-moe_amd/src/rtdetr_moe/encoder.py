@@ -10,6 +10,7 @@ import torch.nn.functional as F
 
 from ..moe.config import MoEConfig
 from ..moe.layer import MoEFFN
+from .norm import AddLayerNorm
 from .backbone import _FUSED_BN, ConvNormLayer
 from .fused import bn_act, bn_act_ok
 from .linear import TokenLinear, TokenSelfAttention
@@ -22,8 +23,9 @@ class DenseFFN(nn.Module):
         self.linear2 = TokenLinear(hidden, d)
         self.act = nn.GELU() if act == "gelu" else nn.ReLU()
 
-    def forward(self, x, ctx=None):
-        return self.linear2(self.act(self.linear1(x)))
+    def forward(self, x, ctx=None, residual=False):
+        y = self.linear2(self.act(self.linear1(x)))
+        return x + y if residual else y
 
 
 def make_ffn(d, hidden, moe: MoEConfig | None, act="relu"):
@@ -38,12 +40,12 @@ class TransformerEncoderLayer(nn.Module):
         super().__init__()
         self.self_attn = TokenSelfAttention(d, nhead)
         self.ffn = make_ffn(d, hidden, moe, act="relu")
-        self.norm1 = nn.LayerNorm(d)
-        self.norm2 = nn.LayerNorm(d)
+        self.norm1 = AddLayerNorm(d)  # LayerNorm(a + b), fused on the GPU (norm.py)
+        self.norm2 = AddLayerNorm(d)
 
     def forward(self, src, pos, ctx):
-        src = self.norm1(src + self.self_attn(src + pos, src))
-        src = self.norm2(src + self.ffn(src, ctx))
+        src = self.norm1(src, self.self_attn(src + pos, src))
+        src = self.norm2(self.ffn(src, ctx, residual=True))  # src + FFN(src)
         return src
 
 

@@ -44,7 +44,7 @@ class RTDETRMoE(nn.Module):
                 x = torch.zeros((1, 3, 640, 640), device=dev)
                 saved = [m.__dict__.get("forward") for m in self.moe_layers()]
                 for m in self.moe_layers():  # identity stand-in: count the dense body only
-                    m.forward = (lambda x, ctx=None: x)
+                    m.forward = (lambda x, ctx=None, residual=False: x)
                 was = self.training
                 self.eval()
                 try:

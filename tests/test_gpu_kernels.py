@@ -266,6 +266,57 @@ def test_moe_layer_fwd_bwd(hip_lib, T, d, E, F, k, tpi, cf, seed):
         assert e <= 5e-3, f"{name}: relative Frobenius error {e:.2e}"
 
 
+@pytest.mark.parametrize("T,d,E,F,k,tpi,cf,seed", [CASES[0], CASES[2], CASES[5]])
+def test_moe_layer_residual_fused(hip_lib, T, d, E, F, k, tpi, cf, seed):
+    """residual=True (moe_combine_res_fwd + moe_token_bwd_res): y = x + FFN(x)
+    and dx = dy + the layer's dx, against the oracle (x + y, dx + dy) and
+    against the unfused GPU path (x + y in torch, autograd's accumulation):
+    outputs within one bf16 rounding of the unfused ones, every parameter
+    gradient bit-identical (they see the same dy)."""
+    from src.moe.ops import moe_ffn_hip
+
+    c = make_case(T, d, E, F, k, tpi, seed)
+    cap = _cap(T, k, E, cf)
+    rng = np.random.default_rng(200 + seed)
+    dy = O.round_bf16(rng.standard_normal((T, d)))
+    st = O.moe_forward(c["x"], c["wg"], c["ctx_bias"], c["w1"], c["b1"], c["w2"], c["b2"],
+                       c["ctx_img"], tpi, k, True, cap, emulate_bf16=True)
+    gr = O.moe_backward(st, c["x"], c["wg"], c["w1"], c["w2"], c["ctx_img"], tpi, 6, dy,
+                        g_lb=0.0, g_z=0.0, normalize=True, emulate_bf16=True)
+    runs = {}
+    for fused in (True, False):
+        def P(a, dtype=torch.float32):
+            return torch.from_numpy(np.asarray(a)).to(dtype).to(DEV).requires_grad_(True)
+
+        x = P(c["x"], torch.bfloat16)
+        ps = [P(c["wg"]), P(c["ctx_bias"]), P(c["w1"]), P(c["b1"]), P(c["w2"]), P(c["b2"])]
+        ci = torch.from_numpy(c["ctx_img"]).to(DEV)
+        if fused:
+            out, *_ = moe_ffn_hip(x, *ps[:2], *ps[2:], ci, tpi, k, True, cap, residual=True)
+        else:
+            y, *_ = moe_ffn_hip(x, *ps[:2], *ps[2:], ci, tpi, k, True, cap)
+            out = x + y
+        (out.float() * _bf16(dy).float().to(DEV)).sum().backward()
+        torch.cuda.synchronize()
+        runs[fused] = (out, x.grad, [p.grad for p in ps])
+    out, dx, grads = runs[True]
+    out_u, dx_u, grads_u = runs[False]
+    bf16_close(_np(out), c["x"] + st.y, "x + y")
+    bf16_close(_np(dx), gr["dx"] + dy, "dx + dy")
+    # the unfused path rounds the branch sum to bf16 before the add: the two
+    # differ by at most half an ulp of the addends' scale plus one final rounding
+    def ulp(m):
+        return np.exp2(np.floor(np.log2(np.maximum(m, 1e-30))) - 7)
+
+    x64, dy64 = c["x"], dy
+    for name, a, b, addend in [("out", out, out_u, x64), ("dx", dx, dx_u, dy64)]:
+        a, b = _np(a), _np(b)
+        bound = ulp(np.abs(addend) + np.abs(b)) + ulp(np.maximum(np.abs(a), np.abs(b)))
+        assert np.all(np.abs(a - b) <= bound), f"{name}: fused vs unfused beyond one bf16 rounding"
+    for name, g, gu in zip(["dwg", "dctx_bias", "dw1", "db1", "dw2", "db2"], grads, grads_u):
+        assert torch.equal(g, gu), f"{name}: fused residual changed a parameter gradient"
+
+
 def test_skewed_routing_and_empty_experts(hip_lib):
     """Every token forced to one expert (others empty), with capacity drops."""
     from src.moe.ops import moe_ffn_hip

@@ -187,13 +187,16 @@ def test_whole_step_graph_matches_eager(hip_lib):
     eager, graph = runs[False], runs[True]
     assert min(graph[1:]) < graph[0], graph
     assert min(eager[1:]) < eager[0], eager
-    # Same initial weights: the first losses agree.  Later steps are not
-    # compared: on a random-init model the 300 queries are near-tied, so bf16
-    # rounding differences between the eager and captured kernels flip
-    # individual matches (host or GPU matcher alike) and the trajectories
-    # drift apart; exact criterion parity on identical outputs is
+    # Same initial weights: the first losses agree up to the model's own
+    # run-to-run spread.  On this random-init model the encoder scores that
+    # select the 300 queries are near-tied, so even two EAGER forwards of the
+    # same weights and images differ (max logit difference 2.6 between
+    # consecutive calls; first eager losses 13.87-14.36 over processes, i.e.
+    # 3.5 %: tools/graph_eager_diag.py, profiles/r02/graph_eager_diag.jsonl),
+    # hence 6 %.  Later steps are not compared (the trajectories drift apart);
+    # exact criterion parity on identical outputs is
     # test_padded_criterion_matches_host_matching.
-    assert abs(eager[0] - graph[0]) <= 3e-2 * max(1.0, abs(eager[0])), (eager, graph)
+    assert abs(eager[0] - graph[0]) <= 6e-2 * max(1.0, abs(eager[0])), (eager, graph)
 
 
 @pytest.mark.gpu
