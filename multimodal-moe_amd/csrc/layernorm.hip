@@ -168,21 +168,29 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(const uint16_t* __restr
   }
 }
 
-// out[n] = sum_p partials[p][n] (fixed order), n < N; fp32 or bf16 out
+// out[n] = sum_p partials[p][n] (fixed order), n < N; fp32 or bf16 out.
+// 16 columns x 16 partial lanes per block; each lane issues all its loads
+// (P <= 256: at most 16) before summing -- one memory round trip, not P / 8
 __global__ __launch_bounds__(256) void add_ln_final_kernel(const float* __restrict__ partials, int P, int N,
                                                            void* __restrict__ out, int out_bf16) {
-  __shared__ float s_acc[8][32];
-  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
-  const int n = blockIdx.x * 32 + cl;
+  __shared__ float s_acc[16][17];
+  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  const int n = blockIdx.x * 16 + cl;
+  float v[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int p = pl + 16 * u;
+    v[u] = (n < N && p < P) ? partials[(size_t)p * N + n] : 0.f;
+  }
   float s = 0.f;
-  if (n < N)
-    for (int p = pl; p < P; p += 8) s += partials[(size_t)p * N + n];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) s += v[u];
   s_acc[pl][cl] = s;
   __syncthreads();
   if (pl == 0 && n < N) {
     float t = 0.f;
 #pragma unroll
-    for (int l = 0; l < 8; ++l) t += s_acc[l][cl];
+    for (int l = 0; l < 16; ++l) t += s_acc[l][cl];
     if (out_bf16) static_cast<uint16_t*>(out)[n] = f2bf(t);
     else static_cast<float*>(out)[n] = t;
   }
@@ -260,7 +268,7 @@ extern "C" int rtdetr_add_layer_norm_bwd(const void* dout, const void* a, const 
 #undef LNB
   int rc = check_launch("rtdetr_add_layer_norm_bwd");
   if (rc != 0) return rc;
-  hipLaunchKernelGGL(add_ln_final_kernel, dim3((2 * d + 31) / 32), dim3(256), 0, stream, partials, P, 2 * d,
+  hipLaunchKernelGGL(add_ln_final_kernel, dim3((2 * d + 15) / 16), dim3(256), 0, stream, partials, P, 2 * d,
                      dgamma_dbeta, w_bf16);
   return check_launch("rtdetr_add_layer_norm_bwd(final)");
 }
