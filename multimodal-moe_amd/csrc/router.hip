@@ -86,6 +86,19 @@ __global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
       xpre[it][c] = (t < T && c < nchunk) ? xr[sub + 16 * c] : make_uint4(0u, 0u, 0u, 0u);
   }
 
+  // The context id of each (token, expert) element this thread stages below,
+  // loaded together with the x rows: the context-bias gather then waits on
+  // one round trip instead of two (ctx_img, then ctx_bias) after the Wg copy.
+  const bool has_ctx = ctx_bias != nullptr && ctx_img != nullptr;
+  constexpr int CBP = (64 * EMAX + NT - 1) / NT;
+  int cimg[CBP];
+#pragma unroll
+  for (int u = 0; u < CBP; ++u) {
+    const int i = tid + u * NT;
+    const int t = blk * 64 + i / (E > 0 ? E : 1);
+    cimg[u] = (has_ctx && i < 64 * E && t < T) ? ctx_img[t / tpi] : -1;
+  }
+
   // Stage Wg (fp32 [E][d]) in LDS, 16 B per thread-iteration.
   {
     const int n4 = (E * d) >> 2;
@@ -97,12 +110,11 @@ __global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
   // Context-bias row of each of the block's 64 tokens, gathered here so the
   // token loop below issues no global loads: on gfx9 vmcnt also counts the
   // loop's stores, so a load inside the loop would wait for them.
-  const bool has_ctx = ctx_bias != nullptr && ctx_img != nullptr;
   if (has_ctx) {
-    for (int i = tid; i < 64 * E; i += NT) {
-      const int tl = i / E, e = i - tl * E;
-      const int t = blk * 64 + tl;
-      s_cb[i] = (t < T) ? ctx_bias[(size_t)ctx_img[t / tpi] * E + e] : 0.f;
+#pragma unroll
+    for (int u = 0; u < CBP; ++u) {
+      const int i = tid + u * NT;
+      if (i < 64 * E) s_cb[i] = cimg[u] >= 0 ? ctx_bias[(size_t)cimg[u] * E + (i - (i / E) * E)] : 0.f;
     }
   }
   __syncthreads();
