@@ -57,15 +57,41 @@ class DeferredWgrad:
 
     def __init__(self):
         self.items = []  # (gy, x, out dtype, (weight leaf, row), (bias leaf, row))
+        # MoE expert weight gradients (src/moe/ops.py _MoELayer): dicts for
+        # _lib.grouped_gemm_wgrad_batch plus the weight / bias leaves they fill
+        self.moe_items = []
 
     def add(self, gy, x, odt, wt, bt):
         self.items.append((gy, x, odt, wt, bt))
 
+    def add_moe(self, job, odt, w_leaf, b_leaf):
+        self.moe_items.append((job, odt, w_leaf, b_leaf))
+
+    def _flush_moe(self):
+        """All collected expert weight gradients in one batched launch per
+        dtype (every MoE layer's W1 and W2 of the step)."""
+        from ..moe import _lib as L
+
+        grads, by_dt = {}, {}
+        for job, odt, wp, bp in self.moe_items:
+            if id(wp) in grads or id(bp) in grads:
+                raise RuntimeError("DeferredWgrad: an expert weight applied twice in one step")
+            G, M, N = int(job["G"]), int(job["x"].shape[1]), int(job["y"].shape[1])
+            job = dict(job, wc=torch.empty((G, M, N), dtype=odt, device=job["x"].device),
+                       cs=torch.empty((G, M), dtype=odt, device=job["x"].device))
+            grads[id(wp)], grads[id(bp)] = job["wc"], job["cs"]
+            by_dt.setdefault(odt, []).append(job)
+        for dt, jobs in by_dt.items():
+            L.grouped_gemm_wgrad_batch(jobs, dt)
+        self.moe_items.clear()
+        return grads
+
     def flush(self):
         from ..moe import _lib as L
 
+        moe = self._flush_moe() if self.moe_items else {}
         if not self.items:
-            return {}
+            return moe
         # a parameter whose rows receive more than one layer's gradient (a
         # layer applied several times, e.g. a shared head) is summed in fp32
         # and rounded once; the others are written in place, in their dtype
@@ -122,6 +148,7 @@ class DeferredWgrad:
         for k, (a, odt) in acc.items():
             grads[k] = a.to(odt)
         self.items.clear()
+        grads.update(moe)
         return grads
 
 
