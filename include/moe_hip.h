@@ -258,12 +258,13 @@ int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather, const floa
  * split-K over the batch.  Outputs bf16 (out_bf16 = 1) or fp32.  Arrays are
  * host arrays of n entries.  Replaces the weight-gradient halves of 2 n / 2
  * moe_grouped_gemm_bwd_pair launches on the backward's critical path by one
- * launch that fills the chip. */
+ * launch that fills the chip.  allow_split = 0: no split-K (for a launch on a
+ * second stream concurrent with split GEMMs: the workspace is per device). */
 int moe_grouped_gemm_wgrad_batch(int n, const void* const* x, const int32_t* const* x_gather,
                                  const float* const* x_scale, const void* const* y, const int32_t* const* y_gather,
                                  const int32_t* const* offsets, const int* G, const int* M, const int* N,
                                  const int* rows, void* const* c, void* const* colsum, int out_bf16,
-                                 hipStream_t stream);
+                                 int allow_split, hipStream_t stream);
 
 /* ---- MXFP8 expert path (config C5: 32-expert top-4 fp8 expert GEMMs) ----
  * Format: OCP e4m3 elements with one E8M0 exponent byte per 32 consecutive

@@ -1794,11 +1794,13 @@ extern "C" int moe_grouped_gemm_wgrad_batch(int n, const void* const* x, const i
                                             const float* const* x_scale, const void* const* y,
                                             const int32_t* const* y_gather, const int32_t* const* offsets,
                                             const int* G, const int* M, const int* N, const int* rows,
-                                            void* const* c, void* const* colsum, int out_bf16,
+                                            void* const* c, void* const* colsum, int out_bf16, int allow_split,
                                             hipStream_t stream) {
   if (n <= 0) return 0;
   if (n > MAX_MOE_WGRAD_BATCH) return fail("moe_grouped_gemm_wgrad_batch: at most 16 problems per launch");
-  WsWin win = device_ws();
+  // allow_split = 0: no split-K (the workspace is per device: a launch on a
+  // second stream, concurrent with split GEMMs, must not bind it)
+  WsWin win = allow_split ? device_ws() : WsWin{};
   MoeWgBatch b{};
   b.n = n;
   b.c_bf16 = out_bf16 ? 1 : 0;

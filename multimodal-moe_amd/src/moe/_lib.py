@@ -49,7 +49,7 @@ SIGNATURES = {
     "moe_token_bwd_res": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P,
                                _P]),
     "moe_combine_res_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P]),
-    "moe_grouped_gemm_wgrad_batch": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "moe_grouped_gemm_wgrad_batch": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
     "moe_quantize_mx": (_I, [_P, ctypes.c_longlong, _I, _P, _P, _P]),
     "moe_permute_fwd_mx": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_mx": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
@@ -588,7 +588,7 @@ LINEAR_WGRAD_BATCH = 24  # problems per rtdetr_linear_wgrad_batch launch
 MOE_WGRAD_BATCH = 16  # problems per moe_grouped_gemm_wgrad_batch launch
 
 
-def grouped_gemm_wgrad_batch(jobs, out_dtype):
+def grouped_gemm_wgrad_batch(jobs, out_dtype, allow_split=True):
     """Expert weight gradients of several grouped GEMMs in ceil(n / 16) launches:
     jobs = [dict(x, x_gather, x_scale, y, y_gather, offsets, G, rows, wc, cs)]
     with wc [G, M, N] = WX^T WY per expert and cs [G, M] = colsum(WX) written
@@ -598,7 +598,8 @@ def grouped_gemm_wgrad_batch(jobs, out_dtype):
         raise MoEKernelError("grouped_gemm_wgrad_batch: out_dtype must be float32 or bfloat16")
     if not jobs:
         return
-    ensure_splitk_workspace(jobs[0]["x"].device)
+    if allow_split:
+        ensure_splitk_workspace(jobs[0]["x"].device)
     for i in range(0, len(jobs), MOE_WGRAD_BATCH):
         part = jobs[i:i + MOE_WGRAD_BATCH]
         n = len(part)
@@ -626,7 +627,8 @@ def grouped_gemm_wgrad_batch(jobs, out_dtype):
         a = [ctypes.cast(p, ctypes.c_void_p) for p in ptrs]
         d = [ctypes.cast(p, ctypes.c_void_p) for p in dims]
         rc = lib().moe_grouped_gemm_wgrad_batch(n, a[0], a[1], a[2], a[3], a[4], a[5], d[0], d[1], d[2], d[3],
-                                                a[7], a[8], int(out_dtype == torch.bfloat16), _stream())
+                                                a[7], a[8], int(out_dtype == torch.bfloat16), int(bool(allow_split)),
+                                                _stream())
         _check(rc, "moe_grouped_gemm_wgrad_batch")
 
 

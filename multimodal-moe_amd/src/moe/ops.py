@@ -354,7 +354,19 @@ _FUSE_RESIDUAL = os.environ.get("MOE_FUSE_RESIDUAL", "1") != "0"
 # takes ~206 us for the step's 14 grouped weight gradients -- run together,
 # their per-expert operands overflow each XCD's L2 -- about what the pairs'
 # weight-gradient halves cost; profiles/r02/defer_ab/)
+# MOE_DEFER_MOE_WGRAD=2: each layer's two weight gradients as one 2-problem
+# batch launched right away on a side stream (overlapping the rest of the
+# backward), joined when the step flushes its deferred gradients
 _DEFER_MOE_WGRAD = os.environ.get("MOE_DEFER_MOE_WGRAD", "0") != "0"
+_SIDE_WGRAD = os.environ.get("MOE_DEFER_MOE_WGRAD", "0") == "2"
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(dev):
+    s = _SIDE_STREAMS.get(dev)
+    if s is None:
+        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 class _MoELayer(torch.autograd.Function):
@@ -438,10 +450,22 @@ class _MoELayer(torch.autograd.Function):
                                                 out_dtype=odt, want_wgrad=defer is None)
         if defer is not None:
             w1l, b1l, w2l, b2l = ctx.leaves
-            defer.add_moe(dict(x=dyb, x_gather=tok, x_scale=gate, y=h, y_gather=None, offsets=offsets, G=G,
-                               rows=rows), odt, w2l, b2l)
-            defer.add_moe(dict(x=dh, x_gather=None, x_scale=None, y=xb, y_gather=tok, offsets=offsets, G=G,
-                               rows=rows), odt, w1l, b1l)
+            j2 = dict(x=dyb, x_gather=tok, x_scale=gate, y=h, y_gather=None, offsets=offsets, G=G, rows=rows)
+            j1 = dict(x=dh, x_gather=None, x_scale=None, y=xb, y_gather=tok, offsets=offsets, G=G, rows=rows)
+            if _SIDE_WGRAD:
+                # outputs allocated on this stream; every operand stays referenced by
+                # the collector until its flush joins the side stream
+                for j, wl in ((j2, w2l), (j1, w1l)):
+                    j["wc"] = torch.empty((G,) + tuple(wl.shape[1:]), dtype=odt, device=dyb.device)
+                    j["cs"] = torch.empty((G, j["x"].shape[1]), dtype=odt, device=dyb.device)
+                side = _side_stream(dyb.device)
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    L.grouped_gemm_wgrad_batch([j2, j1], odt, allow_split=False)
+                defer.add_moe_done(side, [(j2, w2l, b2l), (j1, w1l, b1l)])
+            else:
+                defer.add_moe(j2, odt, w2l, b2l)
+                defer.add_moe(j1, odt, w1l, b1l)
         # aux-loss gradients as device tensors (no host sync): the router
         # partials' gradient is uniform over blocks (moe_route_dispatch wcoef)
         if weighted:

@@ -60,12 +60,19 @@ class DeferredWgrad:
         # MoE expert weight gradients (src/moe/ops.py _MoELayer): dicts for
         # _lib.grouped_gemm_wgrad_batch plus the weight / bias leaves they fill
         self.moe_items = []
+        self.moe_done = []  # (side stream, [(job, weight leaf, bias leaf)]) launched during the backward
 
     def add(self, gy, x, odt, wt, bt):
         self.items.append((gy, x, odt, wt, bt))
 
     def add_moe(self, job, odt, w_leaf, b_leaf):
         self.moe_items.append((job, odt, w_leaf, b_leaf))
+
+    def add_moe_done(self, stream, outs):
+        """Expert weight gradients already launched on `stream` (outs: (job
+        with its wc / cs outputs, weight leaf, bias leaf)); the flush makes
+        the current stream wait for it."""
+        self.moe_done.append((stream, outs))
 
     def _flush_moe(self):
         """All collected expert weight gradients in one batched launch per
@@ -90,6 +97,13 @@ class DeferredWgrad:
         from ..moe import _lib as L
 
         moe = self._flush_moe() if self.moe_items else {}
+        if self.moe_done:
+            cur = torch.cuda.current_stream()
+            for stream, outs in self.moe_done:
+                cur.wait_stream(stream)
+                for job, wp, bp in outs:
+                    moe[id(wp)], moe[id(bp)] = job["wc"], job["cs"]
+            self.moe_done.clear()
         if not self.items:
             return moe
         # a parameter whose rows receive more than one layer's gradient (a

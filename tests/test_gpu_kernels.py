@@ -531,8 +531,9 @@ def test_route_dispatch_matches_scan_index_aux(hip_lib, T, E, k, cf):
     assert torch.equal(gate2[pos2[keep].long()], w[keep])
 
 
+@pytest.mark.parametrize("side", [False, True])
 @pytest.mark.parametrize("T,E,k", [(1300, 8, 2), (2400, 8, 2), (640, 32, 4)])
-def test_deferred_expert_wgrads_match_paired(hip_lib, monkeypatch, T, E, k):
+def test_deferred_expert_wgrads_match_paired(hip_lib, monkeypatch, T, E, k, side):
     """Expert weight / bias gradients deferred out of the backward (dgrad-only
     paired launches, then ONE moe_grouped_gemm_wgrad_batch launch for two
     layers at the step's end: rtdetr_moe.linear.DeferredWgrad) equal the
@@ -543,6 +544,7 @@ def test_deferred_expert_wgrads_match_paired(hip_lib, monkeypatch, T, E, k):
     from src.rtdetr_moe.linear import deferred_weight_grads, merge_deferred
 
     monkeypatch.setattr(ops, "_DEFER_MOE_WGRAD", True)
+    monkeypatch.setattr(ops, "_SIDE_WGRAD", side)  # side: one 2-problem launch per layer on a second stream
     d, F, tpi = 256, 1024, T // 2
     cases = [make_case(T, d, E, F, k, tpi, seed) for seed in (11, 12)]
     rng = np.random.default_rng(5)
@@ -567,7 +569,8 @@ def test_deferred_expert_wgrads_match_paired(hip_lib, monkeypatch, T, E, k):
         if defer:
             with deferred_weight_grads() as dw:
                 grads = torch.autograd.grad(loss, every, allow_unused=True)
-            assert dw is not None and len(dw.moe_items) == 2 * len(cases)
+            assert dw is not None
+            assert (len(dw.moe_done), len(dw.moe_items)) == ((len(cases), 0) if side else (0, 2 * len(cases)))
             grads = merge_deferred(every, grads, dw)
         else:
             grads = torch.autograd.grad(loss, every)

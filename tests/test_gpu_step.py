@@ -332,11 +332,15 @@ def test_whole_step_deferred_weight_grads(hip_lib, precision):
     with linear.deferred_weight_grads() as d:
         grads = torch.autograd.grad(loss, gs.params, allow_unused=True)
     items = list(d.items)
-    moe_items = list(d.moe_items)  # the MoE layers' expert weight gradients (ops._MoELayer)
+    # the MoE layers' expert weight gradients (ops._MoELayer): batched at the
+    # flush (moe_items) or already launched on a side stream (moe_done)
+    moe_items = list(d.moe_items) + [(job, job["wc"].dtype, wp, bp) for _, outs in d.moe_done
+                                     for job, wp, bp in outs]
     assert len(items) == gs.deferred_layers
     from src.moe import ops
 
-    assert len(moe_items) == (2 * len(model.moe_layers()) if ops._DEFER_MOE_WGRAD else 0), len(moe_items)
+    want = 2 * len(model.moe_layers()) if ops._DEFER_MOE_WGRAD else 0
+    assert len(moe_items) == want, len(moe_items)
     merged = linear.merge_deferred(gs.params, grads, d)
     # per element: fp32 accumulation (1e-5 of sum |terms|) plus, for bf16
     # outputs, one rounding of each layer's partial and one of their sum (a
