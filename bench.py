@@ -82,6 +82,8 @@ def load_pmc_traffic(workload):
     for g, e in data.get("groups", {}).items():
         if "hbm_bytes_per_launch" in e:
             out[g] = {"bytes": e["hbm_bytes_per_launch"], "source": f"{p.relative_to(ROOT)} ({data.get('source')})"}
+            if "mfma_counter_frac" in e:  # rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)
+                out[g]["mfma_counter_frac"] = e["mfma_counter_frac"]
     return out
 
 
@@ -127,6 +129,11 @@ def roofline_entry(d, pmc, elapsed, kernel):
         e["flop_per_launch"] = round(d["flops"] / d["launches"])
         e["mfma"] = {"achieved": round(ach_tf, 2), "peak": round(peak_tf, 1), "unit": "TFLOP/s",
                      "frac": round(mfma_frac, 4)}
+        if pmc and "mfma_counter_frac" in pmc:
+            # matrix-core busy fraction from PMC counters over the same kernels
+            # (SQ_VALU_MFMA_BUSY_CYCLES / SIMD-cycles of the kernels' lifetime)
+            e["mfma"]["counter_frac"] = pmc["mfma_counter_frac"]
+            e["mfma"]["counter_source"] = pmc["source"]
     if pmc:
         e["traffic_source"] = pmc["source"]
         e["traffic_over_algorithmic"] = round(pmc["bytes"] / (d["bytes"] / d["launches"]), 3)

@@ -545,7 +545,13 @@ int rtdetr_set_criterion_loss_bwd(const float* g_comps, int S, int B, int Q, int
  *                            v = b2 v + (1-b2) g^2; with t = tensor_steps[i]:
  *                            w -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps);
  *                            bf16 weight (if any) = RNE(w)
- * lrs: HOST array of n_groups (1..4) learning rates. */
+ * lrs: HOST array of n_groups (1..4) learning rates.
+ *   train_grad_pack          data-parallel staging: every
+ *                            record's gradient widened to fp32 at
+ *                            flat[flat_offset ...] (zeros for grad_dtype 2),
+ *                            so the ranks' gradient sum is one fp32
+ *                            all-reduce; flat must be 16-B aligned. */
+int train_grad_pack(const void* tensors, const int32_t* chunks, int n_chunks, float* flat, hipStream_t stream);
 int train_grad_sqnorm(const void* tensors, const int32_t* chunks, int n_chunks, float* partials,
                       hipStream_t stream);
 int train_grad_norm_finalize(const float* partials, int n, float max_norm, float inv_world, float* coef,

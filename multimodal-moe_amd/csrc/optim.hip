@@ -59,6 +59,35 @@ __device__ __forceinline__ void load_grad8(const OptTensor& t, long long e, bool
   }
 }
 
+// Data-parallel gradient staging: every tensor's gradient (bf16 or fp32; a
+// tensor without one contributes zeros) widened to fp32 into one flat buffer
+// at the record's offset, so the ranks' sum is ONE fp32 all-reduce (no bf16
+// rounding per ring hop) and the optimizer reads the reduced sums in place.
+__global__ __launch_bounds__(256) void grad_pack_kernel(const OptTensor* __restrict__ tens,
+                                                        const int2* __restrict__ chunks, float* __restrict__ flat) {
+  const int2 ch = chunks[blockIdx.x];
+  const OptTensor t = tens[ch.x];
+  const long long e = (long long)ch.y * OPT_CHUNK + threadIdx.x * 8;
+  if (e >= t.numel) return;
+  const bool full = e + 8 <= t.numel;
+  float g[8];
+  if (t.gdtype == 2) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = 0.f;
+  } else {
+    load_grad8(t, e, full, g);
+  }
+  float* dst = flat + t.moff + e;
+  if (full) {
+    reinterpret_cast<float4*>(dst)[0] = make_float4(g[0], g[1], g[2], g[3]);
+    reinterpret_cast<float4*>(dst)[1] = make_float4(g[4], g[5], g[6], g[7]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (e + i < t.numel) dst[i] = g[i];
+  }
+}
+
 __global__ __launch_bounds__(256) void grad_sqnorm_kernel(const OptTensor* __restrict__ tens,
                                                           const int2* __restrict__ chunks,
                                                           float* __restrict__ partials) {
@@ -206,6 +235,19 @@ extern "C" int train_grad_sqnorm(const void* tensors, const int32_t* chunks, int
   MOE_LAUNCH(prof, grad_sqnorm_kernel, dim3(n_chunks), dim3(256), 0, stream,
              static_cast<const OptTensor*>(tensors), reinterpret_cast<const int2*>(chunks), partials);
   return check_launch("train_grad_sqnorm");
+}
+
+extern "C" int train_grad_pack(const void* tensors, const int32_t* chunks, int n_chunks, float* flat,
+                               hipStream_t stream) {
+  if (n_chunks < 0 || (n_chunks > 0 && (tensors == nullptr || chunks == nullptr || flat == nullptr)))
+    return fail("train_grad_pack: bad arguments");
+  if (reinterpret_cast<uintptr_t>(flat) % 16) return fail("train_grad_pack: flat buffer must be 16-B aligned");
+  if (n_chunks == 0) return 0;
+  // bytes: <= 4 read + 4 written per element
+  ProfScope prof(stream, PROF_OPTIM, 8.0 * OPT_CHUNK * n_chunks);
+  MOE_LAUNCH(prof, grad_pack_kernel, dim3(n_chunks), dim3(256), 0, stream, static_cast<const OptTensor*>(tensors),
+             reinterpret_cast<const int2*>(chunks), flat);
+  return check_launch("train_grad_pack");
 }
 
 extern "C" int train_grad_norm_finalize(const float* partials, int n, float max_norm, float inv_world, float* coef,

@@ -86,6 +86,7 @@ SIGNATURES = {
     "rtdetr_set_criterion_loss": (_I, [_P, _P, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "rtdetr_set_criterion_loss_bwd": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "moe_aux_loss_fwd": (_I, [_P, _I, _I, _P, _I, _I, _F, _F, _P, _P, _P]),
+    "train_grad_pack": (_I, [_P, _P, _I, _P, _P]),
     "train_grad_sqnorm": (_I, [_P, _P, _I, _P, _P]),
     "train_grad_norm_finalize": (_I, [_P, _I, _F, _F, _P, _P, _I, _P, _P]),
     "train_adamw_step": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _P]),

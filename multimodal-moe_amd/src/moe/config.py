@@ -6,8 +6,8 @@ local architecture spec (no network fetch), e.g.::
 
     rtdetr-r50-moe8-top2          C2/C3: R50, 8 experts, top-2, bf16
     rtdetr-r18-moe4-top1          C1: R18, 4 experts, top-1 (CPU plumbing)
-    rtdetr-r50-moe16-top2-ep8     C4: 16 experts sharded over 8 ranks
-    rtdetr-r50-moe16-top2-ep8-epcf4    same, all-to-all slots at 4x the mean load
+    rtdetr-r50-moe16-top2-ep8     C4: 16 experts sharded over 8 ranks (lossless exchange)
+    rtdetr-r50-moe16-top2-ep8-epcf2    same, all-to-all slots at 2x the mean load (overflow dropped + counted)
     rtdetr-r50-moe32-top4-cf1.25-fp8   C5: capacity factor 1.25, fp8 experts
     rtdetr-r50                    dense FFN (no MoE)
 """
@@ -34,8 +34,10 @@ class MoEConfig:
     expert_parallel: bool = False  # route through ep.py (set by an -ep<n> spec token, n >= 1)
     # rows each rank may send to one expert in the fixed-capacity all-to-all, as
     # a factor of the mean T k / E (layers with capacity_factor > 0 use their
-    # own capacity instead); >= E / k never drops
-    ep_capacity_factor: float = 2.0
+    # own capacity instead).  0 (default) = lossless: T slots, the worst case,
+    # so the EP layer equals the single-process layer; an explicit -epcf<f>
+    # spec token opts into smaller exchanges that drop (and count) overflow
+    ep_capacity_factor: float = 0.0
     router_init_std: float = 0.02
     ctx_init_scale: float = 0.5
 

@@ -8,9 +8,9 @@ the flat all-reduce of TrainStep).
 
 The exchange is FIXED-CAPACITY: every (source rank, expert) pair owns S rows
 of the all-to-all buffers (S = ``MoEConfig.ep_slot_rows(T)``: the layer's
-capacity when it has one, else ceil(ep_capacity_factor T k / E), never more
-than T), so every split size is static and nothing about the routing is read
-on the host.  Per MoE layer:
+capacity when it has one, else T -- lossless, the default -- or, with an
+explicit ep_capacity_factor f > 0, ceil(f T k / E)), so every split size is
+static and nothing about the routing is read on the host.  Per MoE layer:
 
   route + dispatch      router + scan + permute into the padded send layout:
                         expert e's kept rows at [e S, e S + min(hist_e, S));
@@ -46,6 +46,15 @@ import torch.distributed as dist
 def _a2a(out, x, group, W):
     if W == 1 and group is None:  # -ep1 without a process group: identity exchange
         out.copy_(x)
+    elif x.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo moves host memory only (several ranks sharing one GPU in the
+        # multi-rank tests): stage through the host; not graph-capturable
+        xs = x.detach().contiguous().cpu()
+        if xs.element_size() == 2:  # bf16 rows as int16 bit patterns
+            xs = xs.view(torch.int16)
+        o = torch.empty(xs.shape, dtype=xs.dtype)
+        dist.all_to_all_single(o, xs, group=group)
+        out.copy_(o.view(out.dtype).to(out.device))
     else:
         dist.all_to_all_single(out, x.contiguous(), group=group)
     return out

@@ -109,6 +109,70 @@ def _results_dict(box: BoxMetrics) -> dict:
 # ---------------------------------------------------------------------------
 # checkpoints: plain dicts of tensors / primitives (torch.load weights_only=True)
 # ---------------------------------------------------------------------------
+def _expert_shard_names(model: RTDETRMoE) -> dict:
+    """{state-dict key: (MoEFFN, attribute)} of the expert weights that an
+    expert-parallel model holds as [E/W, ...] shards."""
+    from ..moe.layer import MoEFFN
+
+    out = {}
+    for name, mod in model.named_modules():
+        if isinstance(mod, MoEFFN) and mod.ep_size > 1:
+            for a in ("w1", "b1", "w2", "b2"):
+                out[f"{name}.{a}" if name else a] = (mod, a)
+    return out
+
+
+def gather_expert_shards(model: RTDETRMoE, sd: dict) -> dict:
+    """Collective over the expert-parallel group (every rank must call it):
+    replace each [E/W, ...] expert shard in ``sd`` by the stacked [E, ...]
+    tensor of all ranks (expert weights are saved stacked so EP
+    shards re-assemble).  Identity for a model without EP layers."""
+    names = _expert_shard_names(model)
+    if not names:
+        return sd
+    out = dict(sd)
+    for key, (mod, _) in names.items():
+        t = sd[key].detach().contiguous()
+        W = mod.ep_size
+        parts = [torch.empty_like(t) for _ in range(W)]
+        dist.all_gather(parts, t, group=mod.ep_group)
+        out[key] = torch.cat(parts, 0)
+    return out
+
+
+def shard_expert_state(model: RTDETRMoE, sd: dict) -> dict:
+    """Inverse of gather_expert_shards for loading: stacked [E, ...] expert
+    tensors are cut to this rank's [r E/W, (r+1) E/W) slice when the model is
+    expert-parallel."""
+    names = _expert_shard_names(model)
+    if not names:
+        return sd
+    out = dict(sd)
+    for key, (mod, attr) in names.items():
+        full = sd.get(key)
+        local = getattr(mod, attr)
+        if full is None or full.shape[0] == local.shape[0]:
+            continue
+        El = local.shape[0]
+        r = dist.get_rank(mod.ep_group)
+        out[key] = full[r * El:(r + 1) * El]
+    return out
+
+
+def resolve_spec(raw: str):
+    """Parse a model spec for THIS process: an expert-parallel spec (-ep<W>)
+    outside a process group of W ranks builds the same model with all experts
+    local (e.g. single-process evaluation of an EP-trained checkpoint)."""
+    spec = parse_moe_spec(raw)
+    m = spec.moe
+    if m is not None and m.ep_size > 1:
+        world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
+        if world != m.ep_size:
+            m.ep_size = 1
+            m.expert_parallel = False
+    return spec
+
+
 def save_checkpoint(path: Path, model: RTDETRMoE, epoch: int, fitness: float, optimizer=None, state_dict=None):
     path.parent.mkdir(parents=True, exist_ok=True)
     sd = model.state_dict() if state_dict is None else state_dict
@@ -128,12 +192,12 @@ def load_model(weights: str | Path, device="cpu", num_classes: int = 1) -> RTDET
     p = Path(str(weights))
     if p.exists():
         ck = torch.load(p, map_location="cpu", weights_only=True)
-        model = RTDETRMoE(parse_moe_spec(ck["spec"]), num_classes=int(ck.get("num_classes", 1)))
-        model.load_state_dict(ck["state_dict"])
+        model = RTDETRMoE(resolve_spec(ck["spec"]), num_classes=int(ck.get("num_classes", 1)))
+        model.load_state_dict(shard_expert_state(model, ck["state_dict"]))
         return model.to(device)
     if str(weights).endswith((".pt", ".pth")):
         raise FileNotFoundError(f"weights file not found: {weights}")
-    return RTDETRMoE(parse_moe_spec(str(weights)), num_classes=num_classes).to(device)
+    return RTDETRMoE(resolve_spec(str(weights)), num_classes=num_classes).to(device)
 
 
 # ---------------------------------------------------------------------------
@@ -248,6 +312,7 @@ def _train_worker(a: TrainArgs, rank: int, world: int, local: int | str) -> Trai
     if on_gpu:
         model = model.to(memory_format=torch.channels_last)
     core = model
+    ep = bool(_expert_shard_names(core))
     crit = SetCriterion(num_classes=core.num_classes)
     save_dir = Path(a.project) / a.name
     wdir = save_dir / "weights"
@@ -287,13 +352,17 @@ def _train_worker(a: TrainArgs, rank: int, world: int, local: int | str) -> Trai
             loss = step(images, ctx, tg, num_boxes if on_gpu else float(num_boxes))
             tot += loss.detach().double()
             n += 1
-        # validation (rank 0 evaluates the unwrapped model)
+        # validation: rank 0 evaluates the unwrapped model; an expert-parallel
+        # model's forward holds all-to-alls, so every rank runs the same
+        # validation batches in lockstep (rank 0 keeps the metrics)
         metrics = None
-        if rank == 0:
+        if rank == 0 or ep:
             metrics = _evaluate(core, a.data, "val", a.imgsz, a.batch, device, a.workers, a.seed)
+        # checkpoint state: fp32 masters; expert shards gathered to [E, ...] (collective)
+        sd = gather_expert_shards(core, _master_state_dict(core, step)) if (rank == 0 or ep) else None
+        if rank == 0:
             last_metrics = metrics
             fit = _results_dict(metrics)["fitness"]
-            sd = _master_state_dict(core, step)
             save_checkpoint(wdir / "last.pt", core, epoch, fit, state_dict=sd)
             if fit > best_fit:
                 best_fit, best_epoch = fit, epoch

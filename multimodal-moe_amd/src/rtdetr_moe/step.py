@@ -224,6 +224,40 @@ class GraphedStep:
         return self.static_loss
 
 
+def _ep_group(model: nn.Module):
+    """The process group the expert-parallel layers shard their experts over
+    (None = the default group; every EP layer uses the same one)."""
+    from ..moe.layer import MoEFFN
+
+    groups = {id(m.ep_group): m.ep_group for m in model.modules() if isinstance(m, MoEFFN) and m.ep_size > 1}
+    if len(groups) > 1:
+        raise ValueError("expert-parallel layers over different process groups are not supported")
+    return next(iter(groups.values()), None)
+
+
+@torch.no_grad()
+def clip_grad_norm_sharded(rep_params, shard_params, max_norm, shard_group=None):
+    """torch.nn.utils.clip_grad_norm_ over a model whose ``shard_params`` are
+    sharded across ``shard_group`` (expert parallelism): the global norm is
+    sqrt(|g_rep|^2 + sum over ranks |g_shard|^2), identical on every rank, so
+    the clip coefficient -- and hence the replicated weights -- stay in lockstep.
+    Returns the total norm."""
+    rep = [p.grad for p in rep_params if p.grad is not None]
+    shard = [p.grad for p in shard_params if p.grad is not None]
+    dev = (rep or shard)[0].device if (rep or shard) else torch.device("cpu")
+    sq_rep = torch.stack([g.float().pow(2).sum() for g in rep]).sum() if rep else torch.zeros((), device=dev)
+    sq_sh = torch.stack([g.float().pow(2).sum() for g in shard]).sum() if shard else torch.zeros((), device=dev)
+    if shard_params and dist.is_available() and dist.is_initialized() and dist.get_world_size(shard_group) > 1:
+        sq_sh = sq_sh.reshape(1)
+        dist.all_reduce(sq_sh, group=shard_group)
+        sq_sh = sq_sh.reshape(())
+    total = (sq_rep + sq_sh).sqrt()
+    coef = (max_norm / (total + 1e-6)).clamp(max=1.0)
+    for g in rep + shard:
+        g.mul_(coef.to(g.dtype))
+    return total
+
+
 def gemm_params(model: nn.Module):
     """Parameters that are GEMM / convolution operands: weights and biases of
     Linear, Conv2d and MultiheadAttention layers and the MoE expert weights,
@@ -280,27 +314,37 @@ class TrainStep:
                 p.data = p.data.to(torch.bfloat16)
         bb = [p for n, p in named if n.startswith("backbone.")]
         rest = [p for n, p in named if not n.startswith("backbone.")]
+        self.ep_params = [p for p in self.params if getattr(p, "expert_parallel", False)]
+        self.dp_params = [p for p in self.params if not getattr(p, "expert_parallel", False)]
+        self.ep_group = _ep_group(model)
         if images.is_cuda:
             # flat fp32 masters + moments, clip + AdamW + bf16 weight refresh in
             # three HIP launches (optim.py); fp32 parameters become views of
-            # their master segment -- before any graph capture bakes addresses
+            # their master segment -- before any graph capture bakes addresses.
+            # Expert-parallel shards enter the clip norm through a sum over the
+            # EP group (the same global norm on every rank)
             from .optim import FlatAdamW
 
-            self.opt = FlatAdamW([(bb, lr_backbone), (rest, lr)], weight_decay=weight_decay, clip_norm=clip_norm)
+            self.opt = FlatAdamW([(bb, lr_backbone), (rest, lr)], weight_decay=weight_decay, clip_norm=clip_norm,
+                                 sharded=self.ep_params, shard_group=self.ep_group)
             self.opt_params = None
         else:
             self.opt_params = bb + rest
             self.opt = torch.optim.AdamW([{"params": bb, "lr": lr_backbone}, {"params": rest, "lr": lr}], lr=lr,
                                          weight_decay=weight_decay)
         self.flat = FlatOutputs(model)
-        self.dp_params = [p for p in self.params if not getattr(p, "expert_parallel", False)]
-        self._flat_grads = None
-        if graphs and world > 1 and images.is_cuda:
-            # graph mode sums gradients over ranks and the optimizer applies 1/world
-            # to EVERY gradient (FlatAdamW inv_world); expert-parallel weights are
-            # not all-reduced, so their layers must not pre-scale by 1/world
+        self.reducer = None
+        if world > 1 and images.is_cuda:
+            # GPU data parallelism (graph or eager): the replicated gradients are
+            # summed in fp32 by ONE all-reduce after the backward
+            # (optim.DPGradReducer) and the optimizer applies 1/world to EVERY
+            # gradient (FlatAdamW inv_world); expert-parallel weights are not
+            # all-reduced (their gradients already hold every rank's tokens), so
+            # their layers must not pre-scale by 1/world
             from ..moe.layer import MoEFFN
+            from .optim import DPGradReducer
 
+            self.reducer = DPGradReducer(self.dp_params)
             for m in model.modules():
                 if isinstance(m, MoEFFN) and m.ep_size > 1:
                     m.ep_grad_scale = 1.0
@@ -319,7 +363,7 @@ class TrainStep:
             # the optimizer reads the static gradient buffers of the backward graph
             for p, g in zip(self.params, self.runner.static_grads):
                 p.grad = g
-        elif world > 1:
+        elif world > 1 and not images.is_cuda:  # CPU (gloo): DDP buckets overlapped with the backward
             from .engine import wrap_ddp
 
             self.ddp = wrap_ddp(self.flat, ddp_local)
@@ -330,10 +374,9 @@ class TrainStep:
 
     def _bind_grads(self, static_grads):
         """Point every parameter's .grad at the (new) static gradient buffers of
-        a capture and forget flat views built on the previous ones."""
+        a capture (the reducer rebuilds its table when the addresses change)."""
         for p, g in zip(self.params, static_grads):
             p.grad = g
-        self._flat_grads = None
 
     def _cast_in(self, images):
         return images.to(torch.bfloat16) if self.precision == "bf16" else images
@@ -346,40 +389,18 @@ class TrainStep:
             self.stepper = None
             self.fn = self.flat
             self.graphs = False
-            self._flat_grads = None
             for p in self.params:
                 p.grad = None
 
     def _allreduce_grads(self):
-        """Data-parallel gradient sum (graph mode, world > 1): the static
-        gradient buffers are gathered into one flat buffer per dtype by
-        multi-tensor copies and summed with one RCCL all_reduce each; the
-        optimizer reads the flat buffers (views, in parameter order) and divides
-        by the world size inside its kernels.  Returns the gradient list in the
-        optimizer's parameter order: the reduced views for data-parallel
-        parameters, the local gradients for expert-parallel ones."""
-        if self._flat_grads is None:
-            groups = {}
-            for i, p in enumerate(self.dp_params):
-                groups.setdefault(p.grad.dtype, []).append(i)
-            self._flat_grads = []
-            self._reduced = [None] * len(self.dp_params)
-            for dt, idx in groups.items():
-                gs = [self.dp_params[i].grad for i in idx]
-                flat = torch.empty(sum(g.numel() for g in gs), dtype=dt, device=gs[0].device)
-                views, off = [], 0
-                for i, g in zip(idx, gs):
-                    v = flat[off:off + g.numel()].view_as(g)
-                    views.append(v)
-                    self._reduced[i] = v
-                    off += g.numel()
-                self._flat_grads.append((flat, views, gs))
-            red = {id(p): v for p, v in zip(self.dp_params, self._reduced)}
-            self._opt_grads = [red.get(id(p), p.grad) for p in self.opt.params]
-        for flat, views, gs in self._flat_grads:
-            torch._foreach_copy_(views, gs)
-            dist.all_reduce(flat)
-        return self._opt_grads
+        """Data-parallel gradient sum (GPU, world > 1): the replicated
+        parameters' gradients summed in fp32 by one all-reduce
+        (optim.DPGradReducer).  Returns the gradient list in the optimizer's
+        parameter order: the summed fp32 views for replicated parameters, the
+        local gradients for expert-parallel ones; the optimizer divides by the
+        world size inside its kernels."""
+        red = {id(p): v for p, v in zip(self.dp_params, self.reducer([p.grad for p in self.dp_params]))}
+        return [red.get(id(p), p.grad) for p in self.opt.params]
 
     def _mark(self, name):
         if self.phases is not None:
@@ -423,13 +444,13 @@ class TrainStep:
 
     def _optimizer_step(self):
         if self.opt_params is None:  # GPU: FlatAdamW (clip inside)
-            if self.graphs and self.world > 1:
+            if self.reducer is not None:
                 self.opt.step(self._allreduce_grads(), inv_world=1.0 / self.world)
             else:
                 self.opt.step()
         else:
             if self.clip_norm > 0:
-                torch.nn.utils.clip_grad_norm_(self.opt_params, self.clip_norm, foreach=True)
+                clip_grad_norm_sharded(self.dp_params, self.ep_params, self.clip_norm, self.ep_group)
             self.opt.step()
 
     def phase_summary(self):

@@ -72,12 +72,62 @@ def pmc(path: Path, counter: str):
     return out
 
 
+def pmc_multi(path: Path, counters):
+    """{group: {counter: summed value, "launches": n}} over the listed counters."""
+    out = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            c = row["Counter_Name"]
+            if c not in counters:
+                continue
+            g = group_of(row["Kernel_Name"])
+            if g is None:
+                continue
+            d = out.setdefault(g, {"dispatches": set()})
+            d[c] = d.get(c, 0.0) + float(row["Counter_Value"])
+            d["dispatches"].add(row.get("Dispatch_Id", row.get("Correlation_Id", len(d["dispatches"]))))
+    for d in out.values():
+        d["launches"] = len(d.pop("dispatches"))
+    return out
+
+
+# MI355X: 256 CUs x 4 SIMDs; rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs
+# (MI355X_MICROARCH.md, DVFS note), so the kernel's active cycles are GRBM / 8
+N_CU, N_SIMD, N_XCD = 256, 4, 8
+FLOP_PER_MFMA = 2 * 16 * 16 * 32  # v_mfma_f32_16x16x32_bf16, the grouped GEMM's instruction
+
+
+def mfma_summary(path: Path):
+    cs = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_MFMA", "GRBM_GUI_ACTIVE")
+    out = {}
+    for g, d in pmc_multi(path, cs).items():
+        if "SQ_VALU_MFMA_BUSY_CYCLES" not in d or "GRBM_GUI_ACTIVE" not in d:
+            continue
+        n = d["launches"]
+        active = d["GRBM_GUI_ACTIVE"] / N_XCD
+        e = {"pmc_launches": n,
+             "mfma_busy_cycles_per_launch": round(d["SQ_VALU_MFMA_BUSY_CYCLES"] / n),
+             "gui_active_cycles_per_launch": round(active / n),
+             # fraction of all SIMD-cycles of the kernel's lifetime the matrix cores were busy
+             "mfma_counter_frac": round(d["SQ_VALU_MFMA_BUSY_CYCLES"] / (active * N_CU * N_SIMD), 4)}
+        if "SQ_INSTS_MFMA" in d:
+            e["mfma_insts_per_launch"] = round(d["SQ_INSTS_MFMA"] / n)
+            e["mfma_busy_cycles_per_inst"] = round(d["SQ_VALU_MFMA_BUSY_CYCLES"] / max(d["SQ_INSTS_MFMA"], 1), 2)
+            e["mfma_inst_flops_per_launch"] = round(d["SQ_INSTS_MFMA"] * FLOP_PER_MFMA / n)
+        if "SQ_BUSY_CYCLES" in d:
+            e["sq_busy_cycles_per_launch"] = round(d["SQ_BUSY_CYCLES"] / n)
+        out[g] = e
+    return out
+
+
 def main(src: str, dst: str):
     src_p, dst_p = Path(src), Path(dst)
     dst_p.mkdir(parents=True, exist_ok=True)
     stats, total_ns = kernel_stats(src_p / "prof" / "run_kernel_stats.csv")
     fetch = pmc(src_p / "pmc_fetch" / "p_counter_collection.csv", "FETCH_SIZE")
     write = pmc(src_p / "pmc_write" / "p_counter_collection.csv", "WRITE_SIZE")
+    mp = src_p / "pmc_mfma" / "p_counter_collection.csv"
+    mfma = mfma_summary(mp) if mp.exists() else {}
     res = {"source": str(src_p), "all_kernels_total_ms": round(total_ns / 1e6, 3), "groups": {}}
     for g, _ in GROUPS:
         e = dict(stats.get(g, {}))
@@ -86,6 +136,8 @@ def main(src: str, dst: str):
             wr = write[g]["kib"] * 1024 / write[g]["launches"]
             e.update({"hbm_read_bytes_per_launch": round(rd), "hbm_write_bytes_per_launch": round(wr),
                       "hbm_bytes_per_launch": round(rd + wr), "pmc_launches": fetch[g]["launches"]})
+        if g in mfma:
+            e.update(mfma[g])
         if e:
             e.pop("total_ns", None)
             res["groups"][g] = e
