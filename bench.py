@@ -159,6 +159,8 @@ def parse_args():
                     help="report per-phase GPU/host ms (forward, criterion, backward, optimizer)")
     ap.add_argument("--conv-search", action=argparse.BooleanOptionalAction, default=True,
                     help="let MIOpen benchmark convolution algorithms (torch.backends.cudnn.benchmark)")
+    ap.add_argument("--deterministic", action=argparse.BooleanOptionalAction, default=False,
+                    help="MIOpen deterministic convolution solvers only (torch.backends.cudnn.deterministic)")
     ap.add_argument("--graphs", action=argparse.BooleanOptionalAction, default=True,
                     help="capture the model forward/backward as hipGraphs (default; not with expert parallelism). "
                          "ROCm 7.2 does not stamp timing events inside a graph (tools/graph_event_probe.py), so "
@@ -303,6 +305,7 @@ def main():
     wl = WORKLOADS[args.workload]
     spec = wl["spec"].format(N=world)
     torch.backends.cudnn.benchmark = bool(args.conv_search)
+    torch.backends.cudnn.deterministic = bool(args.deterministic)
     batch = args.batch or wl["batch"]
 
     from src.moe import _lib as L

@@ -523,6 +523,26 @@ int rtdetr_set_criterion_loss_bwd(const float* g_comps, int S, int B, int Q, int
                                   const float* d_l1, const float* d_giou, float* g_logits, float* g_boxes,
                                   hipStream_t stream);
 
+/* Multi-head self-attention of the encoder (AIFI) and decoder layers on the
+ * bf16 MFMA, head_dim 32 (replaces torch's scaled_dot_product_attention, i.e.
+ * AOTriton kernels, inside nn.MultiheadAttention; the reference's engine runs
+ * it inside RTDETR.train, src/models/vision/rtdetr.py:82-94).  bf16 operands
+ * addressed in place: row of (image b, token t, head h) at ptr + (b L + t) ld
+ * + 32 h, ld in elements (multiple of 8, >= 32 H), pointers 16-B aligned.
+ * Scores are scaled by `scale`; softmax over all L keys (no mask).
+ *   rtdetr_attn_fwd: o = softmax(scale q k^T) v; lse [B, H, L] fp32 =
+ *     per-row max + log2(sum) of the base-2 softmax (for the backward).
+ *   rtdetr_attn_bwd: dq, dk, dv from dout, the forward's o and lse; delta
+ *     [B, H, L] fp32 scratch (rowsum(dout * o)).  Two launches (dQ, then dK and
+ *     dV), no atomics: bitwise repeatable. */
+int rtdetr_attn_fwd(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,
+                    void* o, long long ldo, float* lse, int B, int H, int L, int head_dim, float scale,
+                    hipStream_t stream);
+int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,
+                    const void* o, long long ldo, const void* dout, long long lddo, const float* lse, float* delta,
+                    void* dq, long long lddq, void* dk, long long lddk, void* dv, long long lddv, int B, int H,
+                    int L, int head_dim, float scale, hipStream_t stream);
+
 /* Training-step optimizer (the bench step's AdamW; reference: Ultralytics'
  * AdamW inside RTDETR.train, src/models/vision/rtdetr.py:82-94, with
  * torch.optim.AdamW + torch.nn.utils.clip_grad_norm_ semantics) over flat
@@ -585,7 +605,8 @@ enum moe_prof_kind {
   MOE_PROF_OPTIM = 8,
   MOE_PROF_MATCH = 9,
   MOE_PROF_GEMM_FP8 = 10, /* grouped GEMM on the fp8 (MXFP8) MFMA: priced at the fp8 peak */
-  MOE_PROF_LINEAR = 11    /* dense linear weight + bias gradients (rtdetr_linear_wgrad) */
+  MOE_PROF_LINEAR = 11,   /* dense linear weight + bias gradients (rtdetr_linear_wgrad) */
+  MOE_PROF_ATTN = 12      /* multi-head self-attention (rtdetr_attn_fwd / rtdetr_attn_bwd) */
 };
 int moe_profile_enable(int on);
 int moe_profile_count(void);

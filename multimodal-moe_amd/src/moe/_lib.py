@@ -26,6 +26,7 @@ MX_BLOCK = 32  # MXFP8: one E8M0 exponent byte per 32 e4m3 elements of a row
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
+_LL = ctypes.c_longlong
 SIGNATURES = {
     "moe_router_num_blocks": (_I, [_I]),
     "moe_router_topk_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -86,6 +87,9 @@ SIGNATURES = {
     "rtdetr_set_criterion_loss": (_I, [_P, _P, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "rtdetr_set_criterion_loss_bwd": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "moe_aux_loss_fwd": (_I, [_P, _I, _I, _P, _I, _I, _F, _F, _P, _P, _P]),
+    "rtdetr_attn_fwd": (_I, [_P, _LL, _P, _LL, _P, _LL, _P, _LL, _P, _I, _I, _I, _I, _F, _P]),
+    "rtdetr_attn_bwd": (_I, [_P, _LL, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _P, _P, _P, _LL, _P, _LL, _P, _LL,
+                             _I, _I, _I, _I, _F, _P]),
     "train_grad_pack": (_I, [_P, _P, _I, _P, _P]),
     "train_grad_sqnorm": (_I, [_P, _P, _I, _P, _P]),
     "train_grad_norm_finalize": (_I, [_P, _I, _F, _F, _P, _P, _I, _P, _P]),
@@ -138,7 +142,7 @@ def lib() -> ctypes.CDLL:
 
 PROF_KINDS = {0: "grouped_gemm", 1: "dispatch", 2: "router", 3: "route_scan", 4: "token_bwd", 5: "msda",
               6: "mx_quant", 7: "conv_epilogue", 8: "optimizer", 9: "matcher", 10: "grouped_gemm_fp8",
-              11: "linear_wgrad"}
+              11: "linear_wgrad", 12: "attention"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_FP8_TFLOPS = 5000.0   # MI355X dense fp8 / MXFP8 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E

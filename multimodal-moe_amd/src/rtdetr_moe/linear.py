@@ -14,6 +14,7 @@ two-launch column sum) instead of torch's reduce kernel.
 from __future__ import annotations
 
 import contextlib
+import math
 import os
 
 import torch
@@ -293,6 +294,59 @@ class TokenLinear(nn.Linear):
         return super().forward(x)
 
 
+class _SelfAttentionHIP(torch.autograd.Function):
+    """softmax(q k^T / sqrt(32)) v per head on the bf16 MFMA
+    (rtdetr_attn_fwd / rtdetr_attn_bwd, csrc/attn.hip), reading q and k in
+    place from the fused [q | k] projection output [B, L, 2d] and v from
+    [B, L, d]; o comes back as [B, L, d] (heads concatenated), so no head
+    transposes in either direction.  Head dim 32 only (RT-DETR: d 256, 8 heads)."""
+
+    @staticmethod
+    def forward(ctx, qk, v, H):
+        from ..moe import _lib as L
+
+        B, T, d2 = qk.shape
+        d = d2 // 2
+        if d % H or d // H != 32:
+            raise ValueError(f"rtdetr_attn: head dim must be 32 (d {d}, {H} heads)")
+        ctx.in_dtypes = (qk.dtype, v.dtype)
+        qk = qk.to(torch.bfloat16).contiguous()
+        v = v.to(torch.bfloat16).contiguous()
+        o = torch.empty((B, T, d), dtype=torch.bfloat16, device=qk.device)
+        lse = torch.empty((B, H, T), dtype=torch.float32, device=qk.device)
+        scale = 1.0 / math.sqrt(d // H)
+        L._check(L.lib().rtdetr_attn_fwd(qk.data_ptr(), d2, qk.data_ptr() + 2 * d, d2, v.data_ptr(), d,
+                                         o.data_ptr(), d, lse.data_ptr(), B, H, T, d // H, scale, L._stream()),
+                 "rtdetr_attn_fwd")
+        ctx.save_for_backward(qk, v, o, lse)
+        ctx.H, ctx.scale = H, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        from ..moe import _lib as L
+
+        qk, v, o, lse = ctx.saved_tensors
+        B, T, d2 = qk.shape
+        d = d2 // 2
+        H = ctx.H
+        do = do.to(torch.bfloat16).contiguous()
+        dqk = torch.empty_like(qk)
+        dv = torch.empty_like(v)
+        delta = torch.empty_like(lse)
+        L._check(L.lib().rtdetr_attn_bwd(qk.data_ptr(), d2, qk.data_ptr() + 2 * d, d2, v.data_ptr(), d,
+                                         o.data_ptr(), d, do.data_ptr(), d, lse.data_ptr(), delta.data_ptr(),
+                                         dqk.data_ptr(), d2, dqk.data_ptr() + 2 * d, d2, dv.data_ptr(), d,
+                                         B, H, T, d // H, ctx.scale, L._stream()), "rtdetr_attn_bwd")
+        return dqk.to(ctx.in_dtypes[0]), dv.to(ctx.in_dtypes[1]), None
+
+
+def self_attention_hip(qk: torch.Tensor, v: torch.Tensor, num_heads: int) -> torch.Tensor:
+    """Multi-head self-attention of [B, L, 2d] fused q|k and [B, L, d] v on the
+    GPU (HIP kernels; no scaled_dot_product_attention)."""
+    return _SelfAttentionHIP.apply(qk, v, num_heads)
+
+
 class TokenSelfAttention(nn.Module):
     """Self-attention with nn.MultiheadAttention(batch_first=True)'s parameters
     and state-dict keys (in_proj_weight [3d, d], in_proj_bias, out_proj), for
@@ -300,8 +354,9 @@ class TokenSelfAttention(nn.Module):
     [d -> 2d] GEMM on x + pos and v from one [d -> d] GEMM on x (MHA's packed
     path needs q, k and v from one tensor and otherwise issues three), every
     projection through TokenLinear's backward (fused weight + bias gradient),
-    then scaled-dot-product attention and the output projection.  Same math as
-    nn.MultiheadAttention (dropout 0)."""
+    then the attention (on the GPU the HIP kernels of csrc/attn.hip, reading
+    q / k / v in place; on the CPU scaled_dot_product_attention) and the
+    output projection.  Same math as nn.MultiheadAttention (dropout 0)."""
 
     def __init__(self, d: int, nhead: int):
         super().__init__()
@@ -327,6 +382,8 @@ class TokenSelfAttention(nn.Module):
         H = self.num_heads
         qk = self._proj(qk_in, 0, 2 * d)
         v = self._proj(v_in, 2 * d, 3 * d)
+        if qk.is_cuda:  # HIP attention (csrc/attn.hip): no Triton-generated SDPA kernels in the step
+            return self.out_proj(self_attention_hip(qk, v, H))
         q, k = qk.split(d, -1)
         heads = lambda t: t.reshape(B, L, H, d // H).transpose(1, 2)  # noqa: E731
         o = F.scaled_dot_product_attention(heads(q), heads(k), heads(v))

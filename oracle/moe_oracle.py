@@ -320,8 +320,15 @@ def moe_forward(x, wg, ctx_bias, w1, b1, w2, b2, ctx_img, tokens_per_image, k,
 # a7: backward (hand-derived)
 # ----------------------------------------------------------------------------
 def moe_backward(st: MoEState, x, wg, w1, w2, ctx_img, tokens_per_image, n_ctx, dy,
-                 g_lb=0.0, g_z=0.0, normalize=True, emulate_bf16=False):
+                 g_lb=0.0, g_z=0.0, normalize=True, emulate_bf16=False, fused_dgrad=False):
     """Gradients of  <dy, y> + g_lb * lb + g_z * z  w.r.t. every input.
+
+    fused_dgrad (with emulate_bf16): emulate the single-GPU bf16 path's fused
+    combine transpose, whose dgrad GEMM reads the UNSCALED bf16 dy rows and
+    applies the gate as an fp32 epilogue row scale, dH = relu'(H) * w (dy W2^T),
+    instead of multiplying by a bf16-rounded dYp = w dy; the weight gradient
+    dW2 = H^T dYp and db2 still see the rounded dYp (the MFMA operand).  Same
+    value in exact arithmetic; only the rounding point moves.
 
     Returns dict(dx, dwg, dctx_bias, dw1, db1, dw2, db2)."""
     x = _maybe(x, emulate_bf16)
@@ -345,7 +352,9 @@ def moe_backward(st: MoEState, x, wg, w1, w2, ctx_img, tokens_per_image, n_ctx, 
             if p >= 0:
                 dYp[p] = st.w[t, j] * dy[t]
                 dw[t, j] = float(dy[t] @ st.Yp[p])
+    dYp_exact = dYp
     dYp = _maybe(dYp, emulate_bf16)
+    dYp_dgrad = dYp_exact if fused_dgrad else dYp
     # expert FFN backward
     dH = np.zeros((rows, F))
     dXp = np.zeros((rows, d))
@@ -357,7 +366,7 @@ def moe_backward(st: MoEState, x, wg, w1, w2, ctx_img, tokens_per_image, n_ctx, 
         a, b = int(st.offsets[e]), int(st.offsets[e + 1])
         if b <= a:
             continue
-        dh = (dYp[a:b] @ w2[e]) * (st.H[a:b] > 0)
+        dh = (dYp_dgrad[a:b] @ w2[e]) * (st.H[a:b] > 0)
         dH[a:b] = _maybe(dh, emulate_bf16)
         dXp[a:b] = _maybe(dH[a:b] @ w1[e], emulate_bf16)
         dw2[e] = dYp[a:b].T @ st.H[a:b]

@@ -116,7 +116,8 @@ def test_whole_step_graph_dp_equals_single_process_mean(hip_lib, tmp_path, preci
         step.stepper(step._cast_in(images), ctx, targets, NB)
         torch.cuda.synchronize()
         per_rank.append([g.float().clone() for g in step.stepper.static_grads])
-    names = [n for n, _ in model.named_parameters()]
+    names = [n for n, p in model.named_parameters() if p.requires_grad]  # TrainStep.params order
+    assert len(names) == len(per_rank[0])
     ref = {n: ((a + b) / 2).cpu() for n, a, b in zip(names, *per_rank)}
     # tolerance: the step is not bitwise repeatable (deformable-attention value
     # gradients are accumulated with bf16 atomics in arrival order), so two

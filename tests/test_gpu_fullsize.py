@@ -18,7 +18,10 @@ Tolerances (stated here, summarized in DESIGN.md 5):
     flips of H move a few outputs by one e4m3 step) and relative Frobenius <= 1e-2;
   lb, z: relative 1e-5;
   weight gradients (dWg, dctx_bias, dW1, db1, dW2, db2): relative Frobenius
-    error <= 5e-3 (bf16 experts) / 1e-2 (MXFP8 experts).
+    error <= 5e-4 for the single-GPU bf16 layer against the oracle emulating its
+    fused dgrad (gate applied as an fp32 epilogue row scale,
+    moe_oracle.moe_backward(fused_dgrad=True)); 5e-3 for the expert-parallel
+    layer and the golden fixtures (bf16-rounded dYp); 1e-2 for MXFP8 experts.
 Set MOE_PARITY_REPORT=<path> to write the measured agreement rates, margins and
 errors as JSON (profiles/r02/parity_fullsize.json).
 """
@@ -116,7 +119,8 @@ def _elem_check(got, ref, what, mx=False):
     return check_layer_output(got, ref, what, "mxfp8" if mx else "bf16")
 
 
-def _compare(c, g, ref_idx, ref_pos, ref_hist, ref_offsets, ref_y, ref_dx, ref_lb, ref_z, grads, margin, tok):
+def _compare(c, g, ref_idx, ref_pos, ref_hist, ref_offsets, ref_y, ref_dx, ref_lb, ref_z, grads, margin, tok,
+             gtol=None):
     """Shared assertions; ``tok`` selects the token rows ref_y / ref_dx hold."""
     same = np.all(np.sort(g["idx"], 1) == np.sort(ref_idx, 1), axis=1)
     agree = float(same.mean())
@@ -136,7 +140,8 @@ def _compare(c, g, ref_idx, ref_pos, ref_hist, ref_offsets, ref_y, ref_dx, ref_l
         assert _rel_fro(g["dx"][tok][sel], ref_dx[sel]) <= 1e-2
     assert abs(g["lb"] - ref_lb) <= 1e-5 * max(1.0, abs(ref_lb)), (g["lb"], ref_lb)
     assert abs(g["z"] - ref_z) <= 1e-5 * max(1.0, abs(ref_z)), (g["z"], ref_z)
-    gtol = 1e-2 if c.mx else 5e-3
+    if gtol is None:
+        gtol = 1e-2 if c.mx else 5e-3
     gerr = {}
     for name, (got, ref) in grads.items():
         gerr[name] = _rel_fro(got, ref)
@@ -151,12 +156,12 @@ def _compare(c, g, ref_idx, ref_pos, ref_hist, ref_offsets, ref_y, ref_dx, ref_l
 def test_full_size_layer_vs_oracle(hip_lib, name):
     c = MC.FULL[name]
     inp = MC.make_inputs(c)
-    st, gr = MC.run_oracle(c, inp)
+    st, gr = MC.run_oracle(c, inp, fused_dgrad=not c.mx)
     g = gpu_layer(c, inp)
     grads = {k: (g[k], gr[k]) for k in ("dwg", "dctx_bias", "dw1", "db1", "dw2", "db2")}
     tok = np.arange(c.T)
     rep = _compare(c, g, st.idx, st.pos, st.hist, st.offsets, st.y, gr["dx"], st.lb, st.z, grads,
-                   MC.topk_margin(st.logits, c.k), tok)
+                   MC.topk_margin(st.logits, c.k), tok, gtol=1e-2 if c.mx else 5e-4)
     if name == "c5_enc":  # the multi-chunk route_scan path: > 8 router blocks per segment
         assert (c.T + 63) // 64 > 8 * 8
     _REPORT[f"full/{name}"] = rep

@@ -98,12 +98,15 @@ def main():
     ap.add_argument("--w", type=int, default=320)
     ap.add_argument("--repeats", type=int, default=3)
     ap.add_argument("--benchmark", action="store_true", help="torch.backends.cudnn.benchmark (bench.py's setting)")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="torch.backends.cudnn.deterministic: MIOpen's deterministic convolution solvers only")
     a = ap.parse_args()
     from src.rtdetr_moe.data import SyntheticZOD
     from src.rtdetr_moe.model import RTDETRMoE
     from src.rtdetr_moe.step import FlatOutputs, gemm_params
 
     torch.backends.cudnn.benchmark = a.benchmark
+    torch.backends.cudnn.deterministic = a.deterministic
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     model = RTDETRMoE(a.spec).to(dev).to(memory_format=torch.channels_last)
@@ -124,7 +127,7 @@ def main():
         runs.append(calls)
     for i in range(1, a.repeats):
         first, culprits = compare(runs[0], runs[i])
-        print(json.dumps({"probe": "forward", "spec": a.spec, "repeat": i, "n_calls": len(runs[0]),
+        print(json.dumps({"probe": "forward", "spec": a.spec, "deterministic": a.deterministic, "repeat": i, "n_calls": len(runs[0]),
                           "first_diff": first, "nondeterministic_modules": culprits}), flush=True)
     runs = None
     for h in rec.handles:
@@ -151,7 +154,7 @@ def main():
                 continue
             rel = float((g0.float() - g1.float()).norm() / g0.float().norm().clamp(min=1e-30))
             diff.append((n, rel))
-        print(json.dumps({"probe": "backward", "spec": a.spec, "repeat": i, "n_params": len(names),
+        print(json.dumps({"probe": "backward", "spec": a.spec, "deterministic": a.deterministic, "repeat": i, "n_params": len(names),
                           "n_differ": len(diff), "differ_in_backward_order": diff[::-1][:40],
                           "max_rel": max((r for _, r in diff), default=0.0)}), flush=True)
 

@@ -36,7 +36,7 @@ for WL in "$@"; do
   [ $rc -eq 0 ] || exit $rc
   # MFMA utilisation of the expert GEMMs from counters (one pass, no trace domains)
   mkdir -p $O/pmc_mfma
-  timeout -k 10 420 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE \
+  timeout -k 10 420 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE \
     --kernel-include-regex "gemm_v|gemm_pair" --output-format csv -d $O/pmc_mfma -o p -- \
     python3 $R/bench.py --workload $WL --no-cpu-baseline --no-kernel-timing --no-graphs --steps 3 --warmup 1 $X \
     > $O/pmc_mfma/bench.json 2> $O/pmc_mfma/bench.err; rc=$?

@@ -98,7 +98,8 @@ FLOP_PER_MFMA = 2 * 16 * 16 * 32  # v_mfma_f32_16x16x32_bf16, the grouped GEMM's
 
 
 def mfma_summary(path: Path):
-    cs = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_MFMA", "GRBM_GUI_ACTIVE")
+    cs = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_MFMA", "SQ_INSTS_VALU_MFMA_MOPS_BF16",
+          "GRBM_GUI_ACTIVE")
     out = {}
     for g, d in pmc_multi(path, cs).items():
         if "SQ_VALU_MFMA_BUSY_CYCLES" not in d or "GRBM_GUI_ACTIVE" not in d:
@@ -114,6 +115,8 @@ def mfma_summary(path: Path):
             e["mfma_insts_per_launch"] = round(d["SQ_INSTS_MFMA"] / n)
             e["mfma_busy_cycles_per_inst"] = round(d["SQ_VALU_MFMA_BUSY_CYCLES"] / max(d["SQ_INSTS_MFMA"], 1), 2)
             e["mfma_inst_flops_per_launch"] = round(d["SQ_INSTS_MFMA"] * FLOP_PER_MFMA / n)
+        if "SQ_INSTS_VALU_MFMA_MOPS_BF16" in d:  # rocprofv3's MfmaFlopsBF16 = MOPS x 512
+            e["mfma_bf16_flops_per_launch"] = round(d["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 / n)
         if "SQ_BUSY_CYCLES" in d:
             e["sq_busy_cycles_per_launch"] = round(d["SQ_BUSY_CYCLES"] / n)
         out[g] = e
