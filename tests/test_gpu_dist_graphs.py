@@ -110,33 +110,34 @@ def test_whole_step_graph_dp_equals_single_process_mean(hip_lib, tmp_path, preci
     images, targets, ctx = _data(0, dev)
     step = TrainStep(model, SetCriterion(num_classes=1), images, ctx, graphs=True, world=1, lr=1e-3,
                      precision=precision, targets=targets, num_boxes=NB)
-    per_rank = []
-    for r in range(2):
-        images, targets, ctx = _data(r, dev)
-        step.stepper(step._cast_in(images), ctx, targets, NB)
-        torch.cuda.synchronize()
-        per_rank.append([g.float().clone() for g in step.stepper.static_grads])
     names = [n for n, p in model.named_parameters() if p.requires_grad]  # TrainStep.params order
-    assert len(names) == len(per_rank[0])
-    ref = {n: ((a + b) / 2).cpu() for n, a, b in zip(names, *per_rank)}
-    # tolerance: the step is not bitwise repeatable (deformable-attention value
-    # gradients are accumulated with bf16 atomics in arrival order), so two
-    # replays of the same graph differ by bf16 ulps that the backward carries;
-    # measured worst tensor relative error is reported in the failure message
-    worst, tot_d, tot_r = ("", 0.0), 0.0, 0.0
-    for n, g in r0["g"].items():
-        d = float((g - ref[n]).norm())
-        rn = float(ref[n].norm())
-        tot_d += d * d
-        tot_r += rn * rn
-        rel = d / max(rn, 1e-12)
-        if rn > 1e-8 and rel > worst[1]:
-            worst = (n, rel)
-    tot = (tot_d ** 0.5) / max(tot_r ** 0.5, 1e-12)
-    assert tot <= 2e-2, f"whole-gradient relative error {tot:.3e} (worst tensor {worst})"
-    assert worst[1] <= 1e-1, f"worst tensor {worst}, whole-gradient {tot:.3e}"
-    norm_ref = tot_r ** 0.5
-    assert abs(float(r0["coef"][0]) - norm_ref) <= 2e-2 * norm_ref, (float(r0["coef"][0]), norm_ref)
+    means = []
+    for _ in range(2):  # two independent replays of both images: the backward's own run-to-run spread
+        per_rank = []
+        for r in range(2):
+            images, targets, ctx = _data(r, dev)
+            step.stepper(step._cast_in(images), ctx, targets, NB)
+            torch.cuda.synchronize()
+            per_rank.append([g.float().clone() for g in step.stepper.static_grads])
+        assert len(names) == len(per_rank[0])
+        means.append({n: ((a + b) / 2).cpu() for n, a, b in zip(names, *per_rank)})
+    ref, ref2 = means
+
+    def rel_err(got):
+        d2 = sum(float((got[n] - ref[n]).norm()) ** 2 for n in got)
+        return d2 ** 0.5 / sum(float(ref[n].norm()) ** 2 for n in got) ** 0.5
+
+    # Tolerance: the forward is bitwise repeatable, the backward is not (the
+    # deformable-attention value gradients are bf16 atomics and MIOpen's
+    # backward-data / weight convolution solvers sum split-K slices with fp32
+    # atomics, both in arrival order), so two single-process
+    # replays of the same images already differ.  The data-parallel mean must
+    # sit within 3x that measured spread (+1e-3) of the single-process mean.
+    floor = rel_err({n: ref2[n] for n in r0["g"]})
+    tot = rel_err(r0["g"])
+    assert tot <= 3.0 * floor + 1e-3, f"DP vs single-process mean {tot:.3e}, replay spread {floor:.3e}"
+    norm_ref = sum(float(ref[n].norm()) ** 2 for n in r0["g"]) ** 0.5
+    assert abs(float(r0["coef"][0]) - norm_ref) <= (3.0 * floor + 1e-3) * norm_ref, (float(r0["coef"][0]), norm_ref)
 
 
 # ---------------------------------------------------------------------------
