@@ -244,27 +244,7 @@ int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather, const floa
                               const void* aux, const void* wx, const int32_t* wx_gather, const float* wx_scale,
                               const void* wy, const int32_t* wy_gather, void* wc, void* wcolsum, int M2, int N2,
                               int out_bf16, hipStream_t stream);
-/* (wc = wcolsum = NULL: the dgrad alone -- its weight gradient is deferred to
- * moe_grouped_gemm_wgrad_batch.) */
-
-/* a7: the expert weight gradients of up to 16 grouped GEMMs (e.g.
- * W1 and W2 of every MoE layer of a training step) in ONE launch, computed
- * after the backward pass: problem q is WC_q[g] = WX_q(g)^T WY_q(g) and
- * colsum_q[g] = column sums of WX_q(g) over the rows of expert g
- * (offsets[q], G[q] experts, M[q] % 64 == 0, N[q] % 128 == 0), with the
- * paired kernel's operand forms: WX(r) = bf16(x_scale[r] x[x_gather[r]]) when
- * x_gather is given, WY(r) = y[y_gather[r]] when y_gather is given.  rows[q]
- * = the routed rows (T k, or the capacity bound) -- used to balance the
- * split-K over the batch.  Outputs bf16 (out_bf16 = 1) or fp32.  Arrays are
- * host arrays of n entries.  Replaces the weight-gradient halves of 2 n / 2
- * moe_grouped_gemm_bwd_pair launches on the backward's critical path by one
- * launch that fills the chip.  allow_split = 0: no split-K (for a launch on a
- * second stream concurrent with split GEMMs: the workspace is per device). */
-int moe_grouped_gemm_wgrad_batch(int n, const void* const* x, const int32_t* const* x_gather,
-                                 const float* const* x_scale, const void* const* y, const int32_t* const* y_gather,
-                                 const int32_t* const* offsets, const int* G, const int* M, const int* N,
-                                 const int* rows, void* const* c, void* const* colsum, int out_bf16,
-                                 int allow_split, hipStream_t stream);
+/* (wc = wcolsum = NULL: the dgrad alone.) */
 
 /* ---- MXFP8 expert path (config C5: 32-expert top-4 fp8 expert GEMMs) ----
  * Format: OCP e4m3 elements with one E8M0 exponent byte per 32 consecutive

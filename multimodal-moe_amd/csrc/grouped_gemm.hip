@@ -1052,63 +1052,6 @@ void linear_wgrad_batch_kernel(DenseBatch b) {
   gemm_v1_body<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true, 0>(p, bid - b.base[q], smem);
 }
 
-// The expert weight gradients of several MoE layers in ONE launch
-// (moe_grouped_gemm_wgrad_batch): problem q is one grouped weight gradient
-// WC_g = WX_g^T WY_g + colsum over the rows of expert g (gathered / gate-scaled
-// k-rows as in the paired backward) and owns workgroups [base[q], base[q+1])
-// (multiples of 8: each keeps its XCD-aware tile map and split-K window).
-// The table travels as the kernel argument.
-constexpr int MAX_MOE_WGRAD_BATCH = 16;
-struct MoeWgProb {
-  const uint16_t* x;
-  const uint16_t* y;
-  void* c;
-  void* colsum;
-  const int32_t* offsets;
-  const int32_t* x_gather;
-  const float* x_scale;
-  const int32_t* y_gather;
-  float* ws;
-  int32_t* cnt;
-  int G, M, N, ksplit;
-};
-struct MoeWgBatch {
-  int n, c_bf16, dbg, pad_;
-  int base[MAX_MOE_WGRAD_BATCH + 1];
-  MoeWgProb p[MAX_MOE_WGRAD_BATCH];
-};
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
-void moe_wgrad_batch_kernel(MoeWgBatch b) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int bid = blockIdx.x;
-  int q = 0;
-  while (q + 1 < b.n && bid >= b.base[q + 1]) ++q;  // uniform: a few scalar compares
-  const MoeWgProb d = b.p[q];
-  GemmParams p{};
-  p.dbg = b.dbg;
-  p.a = d.x;
-  p.b = d.y;
-  p.c = d.c;
-  p.colsum = static_cast<float*>(d.colsum);
-  p.c_bf16 = b.c_bf16;
-  p.offsets = d.offsets;
-  p.b_gather = d.y_gather;
-  p.x_gather = d.x_gather;
-  p.x_scale = d.x_gather != nullptr ? d.x_scale : nullptr;
-  p.stride_c = (long long)d.M * d.N;
-  p.lda = d.M;
-  p.ldb = d.N;
-  p.ldc = d.N;
-  p.G = d.G;
-  p.M = d.M;
-  p.N = d.N;
-  p.ksplit = d.ksplit;
-  p.ws = d.ws;
-  p.cnt = d.cnt;
-  gemm_v1_body<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true, 0>(p, bid - b.base[q], smem);
-}
-
 // ---------------------------------------------------------------------------
 // v2: LDS-DMA ring, S stages, S-1 K-tiles in flight
 // ---------------------------------------------------------------------------
@@ -1790,77 +1733,6 @@ extern "C" int rtdetr_linear_wgrad_batch(int n, const void* const* gy, const voi
   return check_launch("rtdetr_linear_wgrad_batch");
 }
 
-extern "C" int moe_grouped_gemm_wgrad_batch(int n, const void* const* x, const int32_t* const* x_gather,
-                                            const float* const* x_scale, const void* const* y,
-                                            const int32_t* const* y_gather, const int32_t* const* offsets,
-                                            const int* G, const int* M, const int* N, const int* rows,
-                                            void* const* c, void* const* colsum, int out_bf16, int allow_split,
-                                            hipStream_t stream) {
-  if (n <= 0) return 0;
-  if (n > MAX_MOE_WGRAD_BATCH) return fail("moe_grouped_gemm_wgrad_batch: at most 16 problems per launch");
-  // allow_split = 0: no split-K (the workspace is per device: a launch on a
-  // second stream, concurrent with split GEMMs, must not bind it)
-  WsWin win = allow_split ? device_ws() : WsWin{};
-  MoeWgBatch b{};
-  b.n = n;
-  b.c_bf16 = out_bf16 ? 1 : 0;
-  b.dbg = g_gemm_debug;
-  constexpr long long part = 256LL * 2 * 4 * 4 + 256LL * 2;  // fp32 floats per slice of a 64 x 128 tile (+ colsum)
-  // K-tiles (64 rows) of the whole batch, from each problem's mean rows per
-  // expert; problems are split over their rows so that the batch is ~3
-  // workgroups per CU of about equal K-loop length (slices >= 4 K-tiles, <= 8)
-  long long iters = 0;
-  for (int q = 0; q < n; ++q) {
-    if (x[q] == nullptr || y[q] == nullptr || c[q] == nullptr || colsum[q] == nullptr || offsets[q] == nullptr)
-      return fail("moe_grouped_gemm_wgrad_batch: null operand");
-    if (G[q] < 1 || G[q] > 1024 || M[q] <= 0 || N[q] <= 0 || M[q] % 64 != 0 || N[q] % 128 != 0 || rows[q] < 0)
-      return fail("moe_grouped_gemm_wgrad_batch: need 1 <= G <= 1024, M % 64 == 0, N % 128 == 0, rows >= 0");
-    if (x_scale[q] != nullptr && x_gather[q] == nullptr)
-      return fail("moe_grouped_gemm_wgrad_batch: x_scale needs x_gather");
-    iters += (long long)G[q] * (M[q] / 64) * (N[q] / 128) * std::max(1LL, ((long long)rows[q] / G[q] + 63) / 64);
-  }
-  const long long per_wg = std::max(4LL, (iters + 767) / 768);
-  double bytes = 0.0, flops = 0.0;
-  long long grid = 0;
-  for (int q = 0; q < n; ++q) {
-    MoeWgProb& d = b.p[q];
-    d.x = static_cast<const uint16_t*>(x[q]);
-    d.y = static_cast<const uint16_t*>(y[q]);
-    d.c = c[q];
-    d.colsum = colsum[q];
-    d.offsets = offsets[q];
-    d.x_gather = x_gather[q];
-    d.x_scale = x_scale[q];
-    d.y_gather = y_gather[q];
-    d.G = G[q];
-    d.M = M[q];
-    d.N = N[q];
-    const long long tpg = (long long)(M[q] / 64) * (N[q] / 128);
-    const long long nkt = std::max(1LL, ((long long)rows[q] / G[q] + 63) / 64);
-    int want = (int)std::min(8LL, std::max(1LL, (nkt + per_wg - 1) / per_wg));
-    const long long gpad = (G[q] + 7) / 8 * 8;  // every problem maps 8-slot XCD rows (Tile::init, WGRAD)
-    const long long tiles = tpg * (G[q] >= 8 ? gpad : G[q]);
-    const long long tiles8 = (tiles + 7) / 8 * 8;
-    if (G[q] < 8 && want > 1) want = 1;  // split grids of G < 8 would need the padded map
-    want = pick_split(want, tiles8, part, win);
-    GemmParams tmp{};
-    win = bind_split(tmp, want, tiles8, part, win);
-    d.ksplit = tmp.ksplit;
-    d.ws = tmp.ws;
-    d.cnt = tmp.cnt;
-    b.base[q] = (int)grid;
-    grid += tiles8 * d.ksplit;
-    const double osz = out_bf16 ? 2.0 : 4.0;
-    bytes += osz * ((double)G[q] * M[q] * N[q] + (double)G[q] * M[q]) + 2.0 * rows[q] * (M[q] + N[q]);
-    flops += 2.0 * (double)rows[q] * M[q] * N[q];
-  }
-  b.base[n] = (int)grid;
-  ProfScope prof(stream, PROF_GEMM, bytes, false, 0.0, flops);
-  constexpr size_t lds = 2 * (64 + 128) * 64 * 2;
-  MOE_LAUNCH(prof, moe_wgrad_batch_kernel, dim3((unsigned)grid), dim3(256), lds, stream, b);
-  return check_launch("moe_grouped_gemm_wgrad_batch");
-}
-
 extern "C" int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather, const float* row_scale,
                                          const void* b, void* c, const int32_t* offsets, int G, int max_rows, int N,
                                          int K, int epilogue, const void* aux, const void* wx,
@@ -1872,7 +1744,7 @@ extern "C" int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather,
   WsWin win = device_ws();
   if (plan_rows(r, a, b, c, offsets, G, max_rows, N, K, 0, epilogue, nullptr, aux, a_gather, win, row_scale))
     return -1;
-  if (wc == nullptr) {  // dgrad only: the weight gradient is computed elsewhere (moe_grouped_gemm_wgrad_batch)
+  if (wc == nullptr) {  // dgrad only (the caller computes the weight gradient elsewhere)
     if (wcolsum != nullptr) return fail("grouped_gemm_bwd_pair: wcolsum without wc");
     if (max_rows == 0) return 0;
     ProfScope prof(stream, PROF_GEMM, r.bytes_fixed, true, r.bytes_row, r.flops_row);

@@ -200,12 +200,17 @@ __global__ __launch_bounds__(256) void add_ln_final_kernel(const float* __restri
 
 using namespace moe;
 
-static int add_ln_check(const void* a, const void* b, const void* gamma, long long T, int d, const char* what) {
+// every operand read or written with 16-B vector accesses (row loads, pack8
+// stores, float4 weight loads, partial / dgamma_dbeta vectors) must be 16-B
+// aligned; NULL optional operands pass (0 has no low bits)
+static int add_ln_check(const void* a, const void* b, const void* gamma, long long T, int d, const char* what,
+                        const void* const* more = nullptr, int n_more = 0) {
   if (T < 0 || T > (1LL << 30)) return fail(std::string(what) + ": T out of range");
   if (d != 128 && d != 256 && d != 512) return fail(std::string(what) + ": d must be 128, 256 or 512");
   if (a == nullptr || gamma == nullptr) return fail(std::string(what) + ": a and gamma are required");
-  if ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) | reinterpret_cast<uintptr_t>(gamma)) & 15)
-    return fail(std::string(what) + ": rows and weights must be 16-B aligned");
+  uintptr_t bits = reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) | reinterpret_cast<uintptr_t>(gamma);
+  for (int i = 0; i < n_more; ++i) bits |= reinterpret_cast<uintptr_t>(more[i]);
+  if (bits & 15) return fail(std::string(what) + ": rows, weights and outputs must be 16-B aligned");
   return 0;
 }
 
@@ -217,7 +222,8 @@ extern "C" int rtdetr_add_layer_norm_parts(long long T) {
 extern "C" int rtdetr_add_layer_norm_fwd(const void* a, const void* b, const void* gamma, const void* beta,
                                          int w_bf16, long long T, int d, float eps, void* out, float* mean,
                                          float* rstd, hipStream_t stream) {
-  if (add_ln_check(a, b, gamma, T, d, "add_layer_norm_fwd")) return -1;
+  const void* fwd_ops[2] = {beta, out};
+  if (add_ln_check(a, b, gamma, T, d, "add_layer_norm_fwd", fwd_ops, 2)) return -1;
   if (beta == nullptr || out == nullptr || mean == nullptr || rstd == nullptr)
     return fail("add_layer_norm_fwd: beta, out, mean and rstd are required");
   if (T == 0) return 0;
@@ -245,7 +251,8 @@ extern "C" int rtdetr_add_layer_norm_bwd(const void* dout, const void* a, const 
                                          int w_bf16, const float* mean, const float* rstd, long long T, int d,
                                          void* ds, float* partials, int P, void* dgamma_dbeta,
                                          hipStream_t stream) {
-  if (add_ln_check(a, b, gamma, T, d, "add_layer_norm_bwd")) return -1;
+  const void* bwd_ops[4] = {dout, ds, partials, dgamma_dbeta};
+  if (add_ln_check(a, b, gamma, T, d, "add_layer_norm_bwd", bwd_ops, 4)) return -1;
   if (dout == nullptr || mean == nullptr || rstd == nullptr || ds == nullptr || partials == nullptr ||
       dgamma_dbeta == nullptr)
     return fail("add_layer_norm_bwd: dout, mean, rstd, ds, partials and dgamma_dbeta are required");

@@ -50,7 +50,6 @@ SIGNATURES = {
     "moe_token_bwd_res": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P,
                                _P]),
     "moe_combine_res_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P]),
-    "moe_grouped_gemm_wgrad_batch": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
     "moe_quantize_mx": (_I, [_P, ctypes.c_longlong, _I, _P, _P, _P]),
     "moe_permute_fwd_mx": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_grouped_gemm_mx": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
@@ -450,8 +449,7 @@ def grouped_gemm_gather(x, src_tok, b, offsets, G, max_rows, N, K, trans_b, epil
 
 
 def grouped_gemm_bwd_pair(a, b, offsets, G, max_rows, N, K, epilogue, aux, wx, wy, wy_gather=None,
-                          out_dtype=torch.bfloat16, a_gather=None, row_scale=None, wx_gather=None, wx_scale=None,
-                          want_wgrad=True):
+                          out_dtype=torch.bfloat16, a_gather=None, row_scale=None, wx_gather=None, wx_scale=None):
     """One launch: C = epi(s_r A(r) . B_g) (dgrad, B stored [K][N] per group;
     A(r) = a[a_gather[r]] when given, s_r = row_scale[r]) and the weight
     gradient WC_g = WX_g^T WY_g with colsum (WX(r) = bf16(wx_scale[r] *
@@ -476,9 +474,8 @@ def grouped_gemm_bwd_pair(a, b, offsets, G, max_rows, N, K, epilogue, aux, wx, w
         raise MoEKernelError("grouped_gemm_bwd_pair: wgrad shapes")
     rows_out = max(max_rows, 1) if a_gather is not None else a.shape[0]
     c = torch.empty((rows_out, N), dtype=torch.bfloat16, device=a.device)
-    # want_wgrad=False: the dgrad alone (the weight gradient is deferred to grouped_gemm_wgrad_batch)
-    wc = torch.empty((G, M2, N2), dtype=out_dtype, device=a.device) if want_wgrad else None
-    cs = torch.empty((G, M2), dtype=out_dtype, device=a.device) if want_wgrad else None
+    wc = torch.empty((G, M2, N2), dtype=out_dtype, device=a.device)
+    cs = torch.empty((G, M2), dtype=out_dtype, device=a.device)
     ensure_splitk_workspace(a.device)
     _check(lib().moe_grouped_gemm_bwd_pair(_ptr(a), _ptr(a_gather), _ptr(row_scale), _ptr(b), _ptr(c), _ptr(offsets),
                                            G, int(max_rows), N, K, int(epilogue), _ptr(aux), _ptr(wx),
@@ -588,53 +585,6 @@ def linear_wgrad(gy, x, out_dtype):
 
 
 LINEAR_WGRAD_BATCH = 24  # problems per rtdetr_linear_wgrad_batch launch
-
-
-MOE_WGRAD_BATCH = 16  # problems per moe_grouped_gemm_wgrad_batch launch
-
-
-def grouped_gemm_wgrad_batch(jobs, out_dtype, allow_split=True):
-    """Expert weight gradients of several grouped GEMMs in ceil(n / 16) launches:
-    jobs = [dict(x, x_gather, x_scale, y, y_gather, offsets, G, rows, wc, cs)]
-    with wc [G, M, N] = WX^T WY per expert and cs [G, M] = colsum(WX) written
-    in out_dtype (WX(r) = bf16(x_scale[r] x[x_gather[r]]) / WY(r) = y[y_gather[r]]
-    when the gathers are given, as in grouped_gemm_bwd_pair)."""
-    if out_dtype not in (torch.float32, torch.bfloat16):
-        raise MoEKernelError("grouped_gemm_wgrad_batch: out_dtype must be float32 or bfloat16")
-    if not jobs:
-        return
-    if allow_split:
-        ensure_splitk_workspace(jobs[0]["x"].device)
-    for i in range(0, len(jobs), MOE_WGRAD_BATCH):
-        part = jobs[i:i + MOE_WGRAD_BATCH]
-        n = len(part)
-        ptrs = [(ctypes.c_void_p * n)() for _ in range(9)]
-        dims = [(ctypes.c_int * n)() for _ in range(4)]
-        for q, j in enumerate(part):
-            _need(j["x"], torch.bfloat16, "x")
-            _need(j["y"], torch.bfloat16, "y")
-            _need(j["offsets"], torch.int32, "offsets")
-            for t, nm in ((j.get("x_gather"), "x_gather"), (j.get("y_gather"), "y_gather")):
-                if t is not None:
-                    _need(t, torch.int32, nm)
-            if j.get("x_scale") is not None:
-                _need(j["x_scale"], torch.float32, "x_scale")
-            G, M, N = int(j["G"]), int(j["x"].shape[1]), int(j["y"].shape[1])
-            wc, cs = j["wc"], j["cs"]
-            if wc.dtype != out_dtype or cs.dtype != out_dtype or not (wc.is_contiguous() and cs.is_contiguous()):
-                raise MoEKernelError("grouped_gemm_wgrad_batch: wc / cs must be contiguous out_dtype tensors")
-            if tuple(wc.shape) != (G, M, N) or tuple(cs.shape) != (G, M) or j["offsets"].numel() < G + 1:
-                raise MoEKernelError("grouped_gemm_wgrad_batch: shape mismatch")
-            for arr, t in zip(ptrs, (j["x"], j.get("x_gather"), j.get("x_scale"), j["y"], j.get("y_gather"),
-                                     j["offsets"], None, wc, cs)):
-                arr[q] = t.data_ptr() if t is not None else None
-            dims[0][q], dims[1][q], dims[2][q], dims[3][q] = G, M, N, int(j["rows"])
-        a = [ctypes.cast(p, ctypes.c_void_p) for p in ptrs]
-        d = [ctypes.cast(p, ctypes.c_void_p) for p in dims]
-        rc = lib().moe_grouped_gemm_wgrad_batch(n, a[0], a[1], a[2], a[3], a[4], a[5], d[0], d[1], d[2], d[3],
-                                                a[7], a[8], int(out_dtype == torch.bfloat16), int(bool(allow_split)),
-                                                _stream())
-        _check(rc, "moe_grouped_gemm_wgrad_batch")
 
 
 def linear_wgrad_batch(jobs, out_dtype):

@@ -348,25 +348,6 @@ def route_dispatch_mx_hip(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normali
 
 # MOE_FUSE_RESIDUAL=0: the residual add stays a torch add (A/B switch)
 _FUSE_RESIDUAL = os.environ.get("MOE_FUSE_RESIDUAL", "1") != "0"
-# MOE_DEFER_MOE_WGRAD=1: expert weight gradients deferred to one batched launch
-# after the backward (moe_grouped_gemm_wgrad_batch) instead of inside the
-# paired backward launches.  Off by default: measured neutral at C2 (the batch
-# takes ~206 us for the step's 14 grouped weight gradients -- run together,
-# their per-expert operands overflow each XCD's L2 -- about what the pairs'
-# weight-gradient halves cost; profiles/r02/defer_ab/)
-# MOE_DEFER_MOE_WGRAD=2: each layer's two weight gradients as one 2-problem
-# batch launched right away on a side stream (overlapping the rest of the
-# backward), joined when the step flushes its deferred gradients
-_DEFER_MOE_WGRAD = os.environ.get("MOE_DEFER_MOE_WGRAD", "0") != "0"
-_SIDE_WGRAD = os.environ.get("MOE_DEFER_MOE_WGRAD", "0") == "2"
-_SIDE_STREAMS: dict = {}
-
-
-def _side_stream(dev):
-    s = _SIDE_STREAMS.get(dev)
-    if s is None:
-        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
-    return s
 
 
 class _MoELayer(torch.autograd.Function):
@@ -414,9 +395,6 @@ class _MoELayer(torch.autograd.Function):
         ctx.meta = (T, d, E, G, rows, int(normalize), tpi, cb is not None,
                     ctx_bias.shape[0] if ctx_bias is not None else 0, weighted)
         ctx.dtypes = (x.dtype, w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32)
-        # the expert weights as leaf parameters of one dtype: their gradients can be deferred
-        ctx.leaves = (w1, b1, w2, b2) if (all(t.is_leaf and t.requires_grad for t in (w1, b1, w2, b2))
-                                          and ctx.dtypes[1] == w1.dtype) else None
         ctx.mark_non_differentiable(hist)
         if weighted:
             raw = out3[:2].clone()
@@ -435,37 +413,11 @@ class _MoELayer(torch.autograd.Function):
         if dy is None:
             dy = torch.zeros((T, d), dtype=torch.bfloat16, device=xb.device)
         dyb = dy.to(torch.bfloat16).contiguous()
-        # inside a training step's deferral context (TrainStep / GraphedStep,
-        # not under DDP) the expert weight gradients leave the critical path:
-        # only the dgrads run here and the step computes every layer's dW1 /
-        # dW2 / db1 / db2 after the backward in one batched launch
-        # (rtdetr_moe.linear.DeferredWgrad -> moe_grouped_gemm_wgrad_batch)
-        from ..rtdetr_moe import linear as _lin
-
-        defer = _lin._ACTIVE[0] if (_DEFER_MOE_WGRAD and ctx.leaves is not None) else None
         dh, dW2, db2 = L.grouped_gemm_bwd_pair(dyb, w2b, offsets, G, rows, F, d, L.EPI_RELU_MASK, h, dyb, h,
                                                out_dtype=odt, a_gather=tok, row_scale=gate, wx_gather=tok,
-                                               wx_scale=gate, want_wgrad=defer is None)
+                                               wx_scale=gate)
         dxp, dW1, db1 = L.grouped_gemm_bwd_pair(dh, w1b, offsets, G, rows, d, F, L.EPI_NONE, None, dh, xb, tok,
-                                                out_dtype=odt, want_wgrad=defer is None)
-        if defer is not None:
-            w1l, b1l, w2l, b2l = ctx.leaves
-            j2 = dict(x=dyb, x_gather=tok, x_scale=gate, y=h, y_gather=None, offsets=offsets, G=G, rows=rows)
-            j1 = dict(x=dh, x_gather=None, x_scale=None, y=xb, y_gather=tok, offsets=offsets, G=G, rows=rows)
-            if _SIDE_WGRAD:
-                # outputs allocated on this stream; every operand stays referenced by
-                # the collector until its flush joins the side stream
-                for j, wl in ((j2, w2l), (j1, w1l)):
-                    j["wc"] = torch.empty((G,) + tuple(wl.shape[1:]), dtype=odt, device=dyb.device)
-                    j["cs"] = torch.empty((G, j["x"].shape[1]), dtype=odt, device=dyb.device)
-                side = _side_stream(dyb.device)
-                side.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(side):
-                    L.grouped_gemm_wgrad_batch([j2, j1], odt, allow_split=False)
-                defer.add_moe_done(side, [(j2, w2l, b2l), (j1, w1l, b1l)])
-            else:
-                defer.add_moe(j2, odt, w2l, b2l)
-                defer.add_moe(j1, odt, w1l, b1l)
+                                                out_dtype=odt)
         # aux-loss gradients as device tensors (no host sync): the router
         # partials' gradient is uniform over blocks (moe_route_dispatch wcoef)
         if weighted:

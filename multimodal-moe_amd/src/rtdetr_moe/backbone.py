@@ -19,61 +19,6 @@ import torch.nn.functional as F
 from .fused import AddBiasReLU, AddBiasReLUFork, BiasReLU, bn_act, bn_act_ok
 
 _FUSED_BN = os.environ.get("MOE_FUSED_BN", "1") != "0"  # A/B switch: training BN + SiLU in HIP
-# A/B switch (default off): 1x1 stride-1 convolutions over at most this many
-# NHWC rows (B*H*W) as GEMMs on the channels_last view.  The isolated probe
-# favoured them at R50 stages 2-4, but the whole C2 step ran slower with them
-# (MOE_CONV1X1_GEMM_ROWS=131072: 243.7 vs 246.2 images/s, same box), so MIOpen
-# keeps every convolution.
-_CONV1X1_GEMM_ROWS = int(os.environ.get("MOE_CONV1X1_GEMM_ROWS", "0"))
-
-
-class _Conv1x1(torch.autograd.Function):
-    """A 1x1, stride-1, bias-free convolution on a channels_last tensor as the
-    GEMM it is: the NHWC activation is a [B*H*W, Cin] row-major matrix, so
-    y = x W^T (hipBLASLt), dX = dY W, and dW = dY^T X reduced over the rows in
-    chunks (linear.chunked_wgrad: a row-chunk bmm + fp32 sum).  No copies: the
-    output is written by the GEMM into a channels_last tensor.  Isolated, at
-    the R50 stage 2-4 shapes (1280x736, batch 8), forward + backward beat
-    MIOpen (tools/conv1x1_probe.py, profiles/r02/conv1x1_probe.jsonl); stage 1
-    (64 channels at 184x320) did not; in the whole step it lost (see
-    _CONV1X1_GEMM_ROWS)."""
-
-    @staticmethod
-    def forward(ctx, x, w):
-        B, C, H, W = x.shape
-        x2 = x.permute(0, 2, 3, 1).reshape(-1, C)
-        w2 = w.reshape(w.shape[0], C)
-        # the output is a fresh channels_last tensor (not a view: the block
-        # epilogues may update it in place), written by the GEMM directly
-        y = torch.empty((B, w2.shape[0], H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-        torch.mm(x2, w2.t(), out=y.permute(0, 2, 3, 1).view(-1, w2.shape[0]))
-        ctx.save_for_backward(x2, w2)
-        ctx.dims = (B, C, H, W)
-        ctx.w_shape = w.shape
-        return y
-
-    @staticmethod
-    def backward(ctx, gy):
-        from .linear import chunked_wgrad
-
-        x2, w2 = ctx.saved_tensors
-        B, C, H, W = ctx.dims
-        gy = gy.contiguous(memory_format=torch.channels_last)
-        gy2 = gy.permute(0, 2, 3, 1).reshape(-1, w2.shape[0])
-        gx = gw = None
-        if ctx.needs_input_grad[0]:
-            gx = gy2.mm(w2).view(B, H, W, C).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1]:
-            gw = chunked_wgrad(gy2, x2).to(w2.dtype).view(ctx.w_shape)
-        return gx, gw
-
-
-def conv1x1_as_gemm(x: torch.Tensor, w: torch.Tensor) -> bool:
-    """Whether _Conv1x1 takes this 1x1 stride-1 convolution."""
-    B, C, H, W = x.shape
-    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.shape[2:] == (1, 1)
-            and 0 < B * H * W <= _CONV1X1_GEMM_ROWS and C % 8 == 0 and w.shape[0] % 8 == 0
-            and x.is_contiguous(memory_format=torch.channels_last))
 
 _DEPTHS = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3], 50: [3, 4, 6, 3], 101: [3, 4, 23, 3]}
 
@@ -241,8 +186,6 @@ class ConvNormLayer(nn.Module):
         self._w_folded = None
         if w is None:
             w = _FoldScale.apply(self.conv.weight, scale)
-        if self.conv.kernel_size == (1, 1) and self.conv.stride == (1, 1) and conv1x1_as_gemm(x, w):
-            return _Conv1x1.apply(x, w), shift
         return F.conv2d(x, w, None, self.conv.stride, self.conv.padding), shift
 
     def forward(self, x):

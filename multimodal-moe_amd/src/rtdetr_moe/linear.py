@@ -58,55 +58,15 @@ class DeferredWgrad:
 
     def __init__(self):
         self.items = []  # (gy, x, out dtype, (weight leaf, row), (bias leaf, row))
-        # MoE expert weight gradients (src/moe/ops.py _MoELayer): dicts for
-        # _lib.grouped_gemm_wgrad_batch plus the weight / bias leaves they fill
-        self.moe_items = []
-        self.moe_done = []  # (side stream, [(job, weight leaf, bias leaf)]) launched during the backward
 
     def add(self, gy, x, odt, wt, bt):
         self.items.append((gy, x, odt, wt, bt))
 
-    def add_moe(self, job, odt, w_leaf, b_leaf):
-        self.moe_items.append((job, odt, w_leaf, b_leaf))
-
-    def add_moe_done(self, stream, outs):
-        """Expert weight gradients already launched on `stream` (outs: (job
-        with its wc / cs outputs, weight leaf, bias leaf)); the flush makes
-        the current stream wait for it."""
-        self.moe_done.append((stream, outs))
-
-    def _flush_moe(self):
-        """All collected expert weight gradients in one batched launch per
-        dtype (every MoE layer's W1 and W2 of the step)."""
-        from ..moe import _lib as L
-
-        grads, by_dt = {}, {}
-        for job, odt, wp, bp in self.moe_items:
-            if id(wp) in grads or id(bp) in grads:
-                raise RuntimeError("DeferredWgrad: an expert weight applied twice in one step")
-            G, M, N = int(job["G"]), int(job["x"].shape[1]), int(job["y"].shape[1])
-            job = dict(job, wc=torch.empty((G, M, N), dtype=odt, device=job["x"].device),
-                       cs=torch.empty((G, M), dtype=odt, device=job["x"].device))
-            grads[id(wp)], grads[id(bp)] = job["wc"], job["cs"]
-            by_dt.setdefault(odt, []).append(job)
-        for dt, jobs in by_dt.items():
-            L.grouped_gemm_wgrad_batch(jobs, dt)
-        self.moe_items.clear()
-        return grads
-
     def flush(self):
         from ..moe import _lib as L
 
-        moe = self._flush_moe() if self.moe_items else {}
-        if self.moe_done:
-            cur = torch.cuda.current_stream()
-            for stream, outs in self.moe_done:
-                cur.wait_stream(stream)
-                for job, wp, bp in outs:
-                    moe[id(wp)], moe[id(bp)] = job["wc"], job["cs"]
-            self.moe_done.clear()
         if not self.items:
-            return moe
+            return {}
         # a parameter whose rows receive more than one layer's gradient (a
         # layer applied several times, e.g. a shared head) is summed in fp32
         # and rounded once; the others are written in place, in their dtype
@@ -163,7 +123,6 @@ class DeferredWgrad:
         for k, (a, odt) in acc.items():
             grads[k] = a.to(odt)
         self.items.clear()
-        grads.update(moe)
         return grads
 
 

@@ -529,61 +529,3 @@ def test_route_dispatch_matches_scan_index_aux(hip_lib, T, E, k, cf):
     assert torch.equal(out, out2) and torch.equal(wcoef, wcoef2)
     keep = pos2 >= 0
     assert torch.equal(gate2[pos2[keep].long()], w[keep])
-
-
-@pytest.mark.parametrize("side", [False, True])
-@pytest.mark.parametrize("T,E,k", [(1300, 8, 2), (2400, 8, 2), (640, 32, 4)])
-def test_deferred_expert_wgrads_match_paired(hip_lib, monkeypatch, T, E, k, side):
-    """Expert weight / bias gradients deferred out of the backward (dgrad-only
-    paired launches, then ONE moe_grouped_gemm_wgrad_batch launch for two
-    layers at the step's end: rtdetr_moe.linear.DeferredWgrad) equal the
-    paired launches' gradients up to the fp32 summation order (split-K
-    slices differ), and every other gradient is bit-identical."""
-    from src.moe import ops
-    from src.moe.ops import moe_ffn_hip
-    from src.rtdetr_moe.linear import deferred_weight_grads, merge_deferred
-
-    monkeypatch.setattr(ops, "_DEFER_MOE_WGRAD", True)
-    monkeypatch.setattr(ops, "_SIDE_WGRAD", side)  # side: one 2-problem launch per layer on a second stream
-    d, F, tpi = 256, 1024, T // 2
-    cases = [make_case(T, d, E, F, k, tpi, seed) for seed in (11, 12)]
-    rng = np.random.default_rng(5)
-    dy = _bf16(rng.standard_normal((T, d))).float().to(DEV)
-
-    def run(defer):
-        params, xs = [], []
-        loss = 0.0
-        for c in cases:
-            def P(a, dtype=torch.bfloat16):
-                return torch.from_numpy(np.asarray(a)).to(dtype).to(DEV).requires_grad_(True)
-
-            x = P(c["x"])
-            ps = [P(c["wg"], torch.float32), P(c["ctx_bias"], torch.float32), P(c["w1"]), P(c["b1"]), P(c["w2"]),
-                  P(c["b2"])]
-            ci = torch.from_numpy(c["ctx_img"]).to(DEV)
-            y, lb, z, _ = moe_ffn_hip(x, *ps, ci, tpi, k, True, 0, residual=True)
-            loss = loss + (y.float() * dy).sum() + 0.3 * lb + 0.1 * z
-            params += ps
-            xs.append(x)
-        every = params + xs
-        if defer:
-            with deferred_weight_grads() as dw:
-                grads = torch.autograd.grad(loss, every, allow_unused=True)
-            assert dw is not None
-            assert (len(dw.moe_done), len(dw.moe_items)) == ((len(cases), 0) if side else (0, 2 * len(cases)))
-            grads = merge_deferred(every, grads, dw)
-        else:
-            grads = torch.autograd.grad(loss, every)
-        torch.cuda.synchronize()
-        return grads
-
-    ref = run(False)
-    got = run(True)
-    names = ["wg", "ctx_bias", "w1", "b1", "w2", "b2"] * len(cases) + ["x"] * len(cases)
-    for name, g, r in zip(names, got, ref):
-        assert g is not None and g.dtype == r.dtype and g.shape == r.shape, name
-        if name in ("w1", "b1", "w2", "b2"):
-            e = rel_fro(_np(g), _np(r))
-            assert e <= 4e-3, f"{name}: deferred vs paired relative Frobenius {e:.2e}"
-        else:
-            assert torch.equal(g, r), f"{name}: changed by the deferral"
