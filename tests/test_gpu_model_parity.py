@@ -54,8 +54,12 @@ one 23x40 map) has near-constant channels whose 1/sigma amplifies ANY
 perturbation of the incoming gradient (on the CPU alone, 1 % noise on it moves
 its input gradient by 140 %; tools/grad_flow_diag.py), which no precision
 comparison survives.
+Per-stage report: the same relative errors for the backbone outputs (S3-S5),
+the AIFI layer, the encoder outputs (P3-P5), the selected memory projection and
+every decoder layer, in forward order, with the first stage whose GPU error
+exceeds 1.5x the CPU-bf16 floor (also bounded by FLOOR_X x floor + ATOL).
 Set MOE_PARITY_REPORT=<path> to write the measured numbers as JSON
-(profiles/r02/parity_model.json).
+(profiles/r03/parity_model.json).
 """
 from __future__ import annotations
 
@@ -87,10 +91,34 @@ class _ReplayMatcher(torch.nn.Module):
         return self.recorded
 
 
-def _run(model, crit, images, ctx, targets, nb, autocast=False, matcher_record=None):
+def _stage_names(model):
+    """Module names of the per-stage report, in forward order: backbone S3-S5,
+    the AIFI layer, the encoder outputs P3-P5, the selected memory projection
+    and every decoder layer."""
+    names = ["backbone", "encoder.encoder.0.0", "encoder", "decoder.enc_output"]
+    return names + [f"decoder.layers.{i}" for i in range(len(model.decoder.layers))]
+
+
+def _stage_hooks(model, store):
+    """Forward hooks that record the stage outputs (detached fp32 CPU copies)."""
+    mods = dict(model.named_modules())
+    hooks = []
+    for n in _stage_names(model):
+        def f(mod, inp, out, n=n):
+            outs = list(out) if isinstance(out, (list, tuple)) else [out]
+            for i, o in enumerate(outs):
+                key = n if len(outs) == 1 else f"{n}[{i}]"
+                store[key] = o.detach().float().cpu()
+        hooks.append(mods[n].register_forward_hook(f))
+    return hooks
+
+
+def _run(model, crit, images, ctx, targets, nb, autocast=False, matcher_record=None, stages=None):
     captured = []
     hooks = [m.register_forward_hook(lambda mod, inp, out: captured.append(inp[0].detach().reshape(-1, inp[0].shape[-1])))
              for m in model.moe_layers()]
+    if stages is not None:
+        hooks += _stage_hooks(model, stages)
     try:
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
             out = model(images, ctx)
@@ -142,7 +170,8 @@ def test_detector_gpu_vs_cpu(hip_lib, spec, B, h, w, precision):
     # CPU fp32 reference path (records the query selection and the matching)
     crit_c = SetCriterion(num_classes=1)
     pairs = []
-    out_c, loss_c, tot_c, xs_c = _run(cpu, crit_c, images, ctx, targets, nb, matcher_record=pairs)
+    st_c, st_g, st_f = {}, {}, {}
+    out_c, loss_c, tot_c, xs_c = _run(cpu, crit_c, images, ctx, targets, nb, matcher_record=pairs, stages=st_c)
 
     # GPU path, replaying the two discrete choices
     crit_g = SetCriterion(num_classes=1)
@@ -152,7 +181,8 @@ def test_detector_gpu_vs_cpu(hip_lib, spec, B, h, w, precision):
     if precision == "bf16":
         img_g = img_g.to(torch.bfloat16)
     tg = [{k: v.to(DEV) for k, v in t.items()} for t in targets]
-    out_g, loss_g, tot_g, xs_g = _run(gpu, crit_g, img_g, ctx.to(DEV), tg, nb, autocast=precision == "amp")
+    out_g, loss_g, tot_g, xs_g = _run(gpu, crit_g, img_g, ctx.to(DEV), tg, nb, autocast=precision == "amp",
+                                      stages=st_g)
     torch.cuda.synchronize()
     assert torch.equal(gpu.decoder.last_topk.cpu(), cpu.decoder.last_topk)
 
@@ -160,8 +190,11 @@ def test_detector_gpu_vs_cpu(hip_lib, spec, B, h, w, precision):
     flo.decoder.query_override = cpu.decoder.last_topk
     crit_f = SetCriterion(num_classes=1)
     crit_f.matcher = _ReplayMatcher(pairs)
+    fh = _stage_hooks(flo, st_f)
     with torch.autocast("cpu", dtype=torch.bfloat16):
         out_f = flo(images, ctx)
+    for hk in fh:
+        hk.remove()
     loss_f = crit_f(out_f, targets, nb)
     tot_f = sum(loss_f.values()) + flo.moe_aux_loss()
     tot_f.backward()
@@ -237,6 +270,16 @@ def test_detector_gpu_vs_cpu(hip_lib, spec, B, h, w, precision):
                        "cpu_vs_gpu_margin_gt_eps": float(e2e[wide].mean()) if wide.any() else 1.0,
                        "cpu_vs_cpu_bf16_margin_gt_eps": float(flr[wide].mean()) if wide.any() else 1.0,
                        "frac_margin_gt_eps": float(wide.mean())})
+    # per-stage activations in forward order: where does the GPU's deviation
+    # from fp32 first exceed 1.5x the CPU-bf16 floor?
+    stages = []
+    for key in st_c:
+        e, f = rel(st_g[key], st_c[key]), rel(st_f[key], st_c[key])
+        stages.append({"stage": key, "gpu": round(e, 5), "cpu_bf16_floor": round(f, 5),
+                       "ratio": round(e / max(f, 1e-12), 3)})
+        checks.append((f"stage/{key}", "act", e, f))
+    rep["stages"] = stages
+    rep["first_stage_over_1.5x_floor"] = next((s_["stage"] for s_ in stages if s_["ratio"] > 1.5), None)
     rep["routing_agreement"] = ragree
     rep["checks"] = {w: {"gpu": round(e, 5), "cpu_bf16_floor": round(f, 5),
                          "limit": round(FLOOR_X * f + ATOL[kind], 5)} for w, kind, e, f in checks}
