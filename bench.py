@@ -150,7 +150,9 @@ def parse_args():
     ap.add_argument("--img-h", type=int, default=720)
     ap.add_argument("--img-w", type=int, default=1280)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU baseline sample length")
+    ap.add_argument("--cpu-seconds", type=float, default=100.0,
+                    help="target length of the CPU baseline's timed sample (at least 5 steps when a step takes "
+                         "<= 20 s, BASELINE.md 2)")
     ap.add_argument("--no-e2e-roofline", action="store_true", help="skip the model-FLOP count (roofline_e2e)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--precision", choices=["bf16", "amp"], default="bf16",
@@ -281,15 +283,20 @@ def cpu_baseline(spec, batch_img, img_h, img_w, target_s):
     torch.set_num_threads(threads)
     step, n_moe = _cpu_step_fn(spec, batch_img, img_h, img_w)
     t0 = time.perf_counter()
-    step()  # warm-up
+    step()  # warm-up: allocator and thread-pool start-up (no search or JIT on the CPU path)
     warm = time.perf_counter() - t0
+    # BASELINE.md 2 plans 2 warm-up + 5 timed steps: one warm-up suffices here
+    # (the per-step times below show no drift after it), and n = 5 timed steps
+    # whenever a step takes <= target_s / 5
     n = max(1, min(5, int(target_s / max(warm, 1e-3))))
-    t0 = time.perf_counter()
+    times = []
     for _ in range(n):
+        t1 = time.perf_counter()
         step()
-    dt = time.perf_counter() - t0
+        times.append(time.perf_counter() - t1)
+    dt = sum(times)
     return {"value": round(batch_img * n / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "affinity_cpus": aff,
+            "affinity_cpus": aff, "step_s": [round(t, 2) for t in times], "warmup_s": round(warm, 2),
             "sample": f"{n} timed fwd+bwd+AdamW steps (+1 warm-up, {warm:.1f} s) of {spec} at batch {batch_img}, "
                       f"{img_w}x{img_h} padded to 32, fp32 torch on {threads} host threads "
                       f"(torch.set_num_threads; {aff} CPUs in the affinity set), {n_moe} MoE layers through "

@@ -50,11 +50,11 @@ def _a2a(out, x, group, W):
         # gloo moves host memory only (several ranks sharing one GPU in the
         # multi-rank tests): stage through the host; not graph-capturable
         xs = x.detach().contiguous().cpu()
-        if xs.element_size() == 2:  # bf16 rows as int16 bit patterns
-            xs = xs.view(torch.int16)
+        if xs.dtype in (torch.bfloat16, torch.float16):  # gloo has no 16-bit a2a: widen (exact) and narrow back
+            xs = xs.float()
         o = torch.empty(xs.shape, dtype=xs.dtype)
         dist.all_to_all_single(o, xs, group=group)
-        out.copy_(o.view(out.dtype).to(out.device))
+        out.copy_(o.to(out.device))
     else:
         dist.all_to_all_single(out, x.contiguous(), group=group)
     return out

@@ -5,7 +5,9 @@ own float64 oracle (oracle/moe_oracle.py; the reference has no MoE code, so a2-a
 parity is "unpinned" -- these fixtures pin the GPU path and the oracle against
 the same numbers over time).  Inputs are NOT stored: tests/moe_cases.py
 regenerates them from each case's seed.  Per case, tests/golden/moe_<name>.npz
-holds the oracle's outputs for loss = <dy, y> + 0.7 lb + 0.3 z:
+holds the oracle's outputs for loss = <dy, y> + 0.7 lb + 0.3 z (bf16-expert
+cases with the single-GPU layer's fused-dgrad rounding points,
+moe_oracle.moe_backward(fused_dgrad=True); MXFP8 cases without):
 
   idx int8 [T,k], pos int32 [T,k] (-1 = dropped), hist int32 [E], offsets int32 [E+1]
   margin fp32 [T]          top-(k+1) logit gap per token (routing tie distance)
@@ -39,7 +41,7 @@ def main(names):
     for name in names or list(MC.GOLDEN):
         c = MC.GOLDEN[name]
         t0 = time.perf_counter()
-        st, gr = MC.run_oracle(c, MC.make_inputs(c))
+        st, gr = MC.run_oracle(c, MC.make_inputs(c), fused_dgrad=not c.mx)
         out = HERE / f"moe_{name}.npz"
         np.savez_compressed(out, **MC.summarize(c, st, gr))
         print(f"{out.name}: {out.stat().st_size / 1e6:.2f} MB, {time.perf_counter() - t0:.1f} s")

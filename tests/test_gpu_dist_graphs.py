@@ -84,10 +84,11 @@ def _dp_worker(rank, world, port, out, precision):
     torch.cuda.synchronize()
     names = {id(p): n for n, p in model.named_parameters()}
     mean = {names[id(p)]: (v.float() / world).cpu() for p, v in zip(step.dp_params, step.reducer.views)}
+    coef = step.opt.coef.cpu().clone()  # [norm of the mean gradient, applied scale] of step 1
     losses = [float(step(images, ctx, targets, NB))]
     torch.cuda.synchronize()
     w = torch.cat([p.detach().float().reshape(-1) for p in model.parameters()]).cpu()
-    torch.save({"g": mean, "coef": step.opt.coef.cpu().clone(), "w": w, "losses": losses}, out / f"r{rank}.pt")
+    torch.save({"g": mean, "coef": coef, "w": w, "losses": losses}, out / f"r{rank}.pt")
     dist.destroy_process_group()
 
 

@@ -20,8 +20,8 @@ Tolerances (stated here, summarized in DESIGN.md 5):
   weight gradients (dWg, dctx_bias, dW1, db1, dW2, db2): relative Frobenius
     error <= 5e-4 for the single-GPU bf16 layer against the oracle emulating its
     fused dgrad (gate applied as an fp32 epilogue row scale,
-    moe_oracle.moe_backward(fused_dgrad=True)); 5e-3 for the expert-parallel
-    layer and the golden fixtures (bf16-rounded dYp); 1e-2 for MXFP8 experts.
+    moe_oracle.moe_backward(fused_dgrad=True); the golden fixtures are made the
+    same way); 5e-3 for the expert-parallel layer; 1e-2 for MXFP8 experts.
 Set MOE_PARITY_REPORT=<path> to write the measured agreement rates, margins and
 errors as JSON (profiles/r02/parity_fullsize.json).
 """
@@ -201,7 +201,7 @@ def test_layer_vs_golden_fixture(hip_lib, name):
              "dw1_rows": (g["dw1"][:, ::step[0]], fx["dw1_rows"]), "dw2_rows": (g["dw2"][:, ::step[1]], fx["dw2_rows"])}
     rep = _compare(c, g, fx["idx"].astype(np.int64), fx["pos"], fx["hist"], fx["offsets"],
                    MC.from_bf16_bits(fx["y"]), MC.from_bf16_bits(fx["dx"]), float(fx["lb"]), float(fx["z"]), grads,
-                   fx["margin"], tok)
+                   fx["margin"], tok, gtol=1e-2 if c.mx else 5e-4)
     # size-independent checksums of the full expert-weight gradients
     for key, arr in (("dw1", g["dw1"]), ("dw2", g["dw2"])):
         ref = float(fx[f"{key}_sumsq"])
