@@ -150,7 +150,7 @@ def parse_args():
     ap.add_argument("--img-h", type=int, default=720)
     ap.add_argument("--img-w", type=int, default=1280)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=100.0,
+    ap.add_argument("--cpu-seconds", type=float, default=125.0,
                     help="target length of the CPU baseline's timed sample (at least 5 steps when a step takes "
                          "<= 20 s, BASELINE.md 2)")
     ap.add_argument("--no-e2e-roofline", action="store_true", help="skip the model-FLOP count (roofline_e2e)")

@@ -523,6 +523,29 @@ int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, 
                     void* dq, long long lddq, void* dk, long long lddk, void* dv, long long lddv, int B, int H,
                     int L, int head_dim, float scale, hipStream_t stream);
 
+/* Implicit-GEMM convolutions of the RT-DETR body (the
+ * backbone and the HybridEncoder's RepVGG / CSP convolutions, which the
+ * reference's engine trains inside RTDETR.train, src/models/vision/rtdetr.py:
+ * 82-94), bf16 MFMA, stride 1, padding (KS - 1) / 2, KS in {1, 3}, no bias.
+ * x / dy / y: NHWC bf16 [B, H, W, channels]; w: [N][KS][KS][C] bf16 (a
+ * channels_last [N, C, KS, KS] weight); C and N multiples of 128; zero: >= 256
+ * zero bytes on the device (read for padding neighbours); pointers 16-B aligned.
+ *   rtdetr_conv_fwd         y[B,H,W,N] = conv(x[B,H,W,C], w)   (no im2col buffer)
+ *   rtdetr_conv_weight_flip wt[C][KS][KS][N] = w[N][KS-1-ky][KS-1-kx][C]: the
+ *                           data gradient is then rtdetr_conv_fwd(dy, wt) with
+ *                           C and N exchanged
+ *   rtdetr_conv_wgrad       dw[N][KS][KS][C] = sum over pixels dy (x) x[neighbour]:
+ *                           nsplit pixel slices write fp32 partials to part
+ *                           [nsplit][N KS KS C], summed in slice order
+ *                           (deterministic) into dw (bf16 if out_bf16 else fp32);
+ *                           nsplit from rtdetr_conv_wgrad_splits. */
+int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void* zero, int B, int H, int W, int C, int N,
+                    int KS, hipStream_t stream);
+int rtdetr_conv_weight_flip(const void* w, void* wt, int N, int C, int KS, hipStream_t stream);
+int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS);
+int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
+                      const void* zero, int B, int H, int W, int C, int N, int KS, hipStream_t stream);
+
 /* Training-step optimizer (the bench step's AdamW; reference: Ultralytics'
  * AdamW inside RTDETR.train, src/models/vision/rtdetr.py:82-94, with
  * torch.optim.AdamW + torch.nn.utils.clip_grad_norm_ semantics) over flat
@@ -586,7 +609,8 @@ enum moe_prof_kind {
   MOE_PROF_MATCH = 9,
   MOE_PROF_GEMM_FP8 = 10, /* grouped GEMM on the fp8 (MXFP8) MFMA: priced at the fp8 peak */
   MOE_PROF_LINEAR = 11,   /* dense linear weight + bias gradients (rtdetr_linear_wgrad) */
-  MOE_PROF_ATTN = 12      /* multi-head self-attention (rtdetr_attn_fwd / rtdetr_attn_bwd) */
+  MOE_PROF_ATTN = 12,     /* multi-head self-attention (rtdetr_attn_fwd / rtdetr_attn_bwd) */
+  MOE_PROF_CONV = 13      /* implicit-GEMM convolutions (rtdetr_conv_*) */
 };
 int moe_profile_enable(int on);
 int moe_profile_count(void);

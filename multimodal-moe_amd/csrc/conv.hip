@@ -1,0 +1,384 @@
+// Implicit-GEMM convolutions of the RT-DETR body on the bf16 MFMA (gfx950):
+// stride 1, "same" padding (KS - 1) / 2, KS in {1, 3}, NHWC (channels_last)
+// activations and [Cout][KS][KS][Cin] (channels_last) weights.  They replace
+// MIOpen for the convolutions that dominate the training step (SURVEY.md 8(f)
+// row 1: "the backbone ... dominate images/sec"; the HybridEncoder's
+// RepVGG 3x3 / 1x1 pairs and the ResNet 3x3 / 1x1 layers): the reference
+// engine trains them inside RTDETR.train (src/models/vision/rtdetr.py:82-94).
+//
+//   conv_fwd_kernel    Y[p, n] = sum_{tap, c} X[nbr(p, tap), c] W[n, tap, c]
+//                      GEMM M = pixels (B H W), N = Cout, K = KS^2 Cin.  The A
+//                      tile's rows are the 64-channel slices of each pixel's
+//                      neighbour for the K-tile's tap, fetched by LDS-DMA with a
+//                      per-row source address (a padding neighbour reads a zero
+//                      row), so no im2col buffer exists.  Used for the data
+//                      gradient too: dX = conv(dY, W') with W' the flipped,
+//                      channel-transposed weight (conv_weight_flip_kernel).
+//   conv_wgrad_kernel  dW[n, tap, c] = sum_p dY[p, n] X[nbr(p, tap), c]
+//                      GEMM M = Cout, N = KS^2 Cin, K = pixels, split over S
+//                      slices of the pixels (fp32 partials) and summed in slice
+//                      order by conv_wgrad_reduce_kernel (deterministic).
+// Tiles 128 x 128 x 64, 4 waves (2 x 2), an S-deep LDS-DMA ring (one
+// global_load_lds_dwordx4 per lane per 1 KiB, counted vmcnt waits, raw
+// s_barrier), K-contiguous operand images (fwd) or MN-contiguous ones read by
+// ds_read_b64_tr_b16 (wgrad), v_mfma_f32_16x16x32_bf16.
+#include <algorithm>
+
+#include "mfma_lds.h"
+#include "moe_common.h"
+#include "prof.h"
+
+namespace moe {
+
+constexpr int CV_BM = 128, CV_BN = 128;
+constexpr int CV_TILE = (CV_BM + CV_BN) * 64 * 2;  // bytes of one ring stage
+
+struct ConvArgs {
+  const uint16_t* x;     // [B H W, C] (fwd: X; dgrad: dY)
+  const uint16_t* w;     // [N][KS][KS][C] (fwd: W; dgrad: W')
+  uint16_t* y;           // [B H W, N]
+  const uint16_t* zero;  // >= 256 zero bytes (padding rows)
+  int B, H, W, C, N;
+  int P;                 // B H W
+  int mt_n;              // M tiles
+};
+
+__device__ __forceinline__ void dma16(const uint16_t* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// ---------------------------------------------------------------------------
+// forward / data gradient
+// ---------------------------------------------------------------------------
+template <int KS, int S>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TM = CV_BM / 32, TN = CV_BN / 32;
+  constexpr int GW = CV_BM / 32 + CV_BN / 32;  // DMA instructions per wave per K-tile
+  constexpr int PAD = (KS - 1) / 2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware map: the N tiles of one M tile run on one XCD (they share the A panel)
+  const int NT = a.N / CV_BN;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int nt = slot % NT;
+  const int mt = (slot / NT) * 8 + xcd;
+  if (mt >= a.mt_n) return;
+  const int m0 = mt * CV_BM, n0 = nt * CV_BN;
+  const int cpt = a.C / 64;        // K-tiles per tap
+  const int nk = KS * KS * cpt;
+  const int HW = a.H * a.W;
+  // this lane's A rows (one per DMA instruction j): pixel, coordinates, source chunk
+  int py[TM], px[TM], pb[TM], ach[TM];
+  bool pv[TM];
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int r = (wave + 4 * j) * 8 + (lane >> 3);
+    const int p = m0 + r;
+    pv[j] = p < a.P;
+    const int pp = pv[j] ? p : 0;
+    pb[j] = pp / HW;
+    const int rem = pp - pb[j] * HW;
+    py[j] = rem / a.W;
+    px[j] = rem - py[j] * a.W;
+    ach[j] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+  }
+  const uint16_t* wrow[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int r = (wave + 4 * j) * 8 + (lane >> 3);
+    wrow[j] = a.w + (size_t)(n0 + r) * (KS * KS * a.C) + ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+  }
+  auto issue = [&](int kt) {
+    char* buf = smem + (kt % S) * CV_TILE;
+    const int tap = kt / cpt, c0 = (kt - tap * cpt) * 64;
+    const int dy = tap / KS - PAD, dx = tap % KS - PAD;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int yy = py[j] + dy, xx = px[j] + dx;
+      const bool ok = pv[j] && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+      const uint16_t* src = ok ? a.x + ((size_t)(pb[j] * HW + yy * a.W + xx)) * a.C + c0 + ach[j] : a.zero + ach[j];
+      dma16(src, buf + (wave + 4 * j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) dma16(wrow[j] + tap * a.C + c0, buf + CV_BM * 128 + (wave + 4 * j) * 1024);
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float csum[TM];
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(s);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int newer = nk - 1 - kt;
+    if constexpr (S == 2) {
+      wait_vm<0>();
+    } else {
+      if (newer >= 1) wait_vm<GW>();
+      else wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
+    if (kt + S - 1 < nk) issue(kt + S - 1);  // refills the slot consumed in iteration kt - 1
+    const char* cur = smem + (kt % S) * CV_TILE;
+    compute_tile<CV_BM, CV_BN, true, true, false>(cur, cur + CV_BM * 128, acc, csum, lane, wm, wn);
+  }
+  // lane holds Y[m0 + wm 64 + 16 i + (lane & 15)][n0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3]
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int p = m0 + wm * (CV_BM / 2) + 16 * i + (lane & 15);
+    if (p >= a.P) continue;
+    uint16_t* yrow = a.y + (size_t)p * a.N + n0 + wn * (CV_BN / 2) + 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      uint2 v;
+      v.x = pack2bf(acc[i][j][0], acc[i][j][1]);
+      v.y = pack2bf(acc[i][j][2], acc[i][j][3]);
+      *reinterpret_cast<uint2*>(yrow + 16 * j) = v;
+    }
+  }
+}
+
+// W'[c][ky][kx][n] = W[n][KS-1-ky][KS-1-kx][c]: the data gradient's weight
+__global__ __launch_bounds__(256) void conv_weight_flip_kernel(const uint16_t* __restrict__ w,
+                                                               uint16_t* __restrict__ wt, int N, int C, int KS) {
+  const long long total = (long long)N * C * KS * KS;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    // i indexes the OUTPUT [c][tap'][n] (writes coalesced)
+    const int n = (int)(i % N);
+    const long long q = i / N;
+    const int tap = (int)(q % (KS * KS));
+    const int c = (int)(q / (KS * KS));
+    const int ftap = KS * KS - 1 - tap;
+    wt[i] = w[((long long)n * KS * KS + ftap) * C + c];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient
+// ---------------------------------------------------------------------------
+struct ConvWgArgs {
+  const uint16_t* dy;    // [P][N]
+  const uint16_t* x;     // [P][C]
+  float* part;           // [S][N][KS KS C]
+  const uint16_t* zero;
+  int B, H, W, C, N, P;
+  int nsplit, kt_per;    // pixel K-tiles per slice
+};
+
+template <int KS, int S>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TM = CV_BM / 32, TN = CV_BN / 32;
+  constexpr int GW = 64 * 2 * (CV_BM + CV_BN) / 1024 / 4;  // DMA instructions per wave per K-tile
+  constexpr int PAD = (KS - 1) / 2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int NN = KS * KS * a.C;      // GEMM N
+  const int MT = a.N / CV_BM, NT = NN / CV_BN;
+  // slices of one output tile on one XCD: bid = ((tile / 8) * nsplit + split) * 8 + tile % 8
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int split = slot % a.nsplit;
+  const int tile = (slot / a.nsplit) * 8 + xcd;
+  if (tile >= MT * NT) return;
+  const int mt = tile % MT, nt = tile / MT;
+  const int m0 = mt * CV_BM, nn0 = nt * CV_BN;
+  const int tap = nn0 / a.C, c0 = nn0 - tap * a.C;
+  const int dy_ = tap / KS - PAD, dx_ = tap % KS - PAD;
+  const int ktot = (a.P + 63) / 64;
+  const int kt0 = split * a.kt_per;
+  const int nk = max(0, min(a.kt_per, ktot - kt0));
+  const int HW = a.H * a.W;
+  // k-row (pixel) of this lane in DMA instruction j: kr = (wave + 4 j) * 4 + lane / 16 (256-B rows)
+  int ach[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int kr = (wave + 4 * j) * 4 + (lane >> 4);
+    ach[j] = ((lane & 15) ^ mimg_swz<128>(kr)) * 8;
+  }
+  auto issue = [&](int kt) {
+    char* buf = smem + (kt % S) * CV_TILE;
+    const int kb = (kt0 + kt) * 64;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kr = (wave + 4 * j) * 4 + (lane >> 4);
+      const int p = kb + kr;
+      const bool pv = p < a.P;
+      const int pp = pv ? p : 0;
+      const int b = pp / HW;
+      const int rem = pp - b * HW;
+      const int y = rem / a.W;
+      const int x = rem - y * a.W;
+      const int yy = y + dy_, xx = x + dx_;
+      const bool ok = pv && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+      const uint16_t* sa = pv ? a.dy + (size_t)p * a.N + m0 + ach[j] : a.zero + ach[j];
+      const uint16_t* sb = ok ? a.x + ((size_t)(b * HW + yy * a.W + xx)) * a.C + c0 + ach[j] : a.zero + ach[j];
+      dma16(sa, buf + (wave + 4 * j) * 1024);
+      dma16(sb, buf + CV_BM * 128 + (wave + 4 * j) * 1024);
+    }
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float csum[TM];
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(s);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int newer = nk - 1 - kt;
+    if constexpr (S == 2) {
+      wait_vm<0>();
+    } else {
+      if (newer >= 1) wait_vm<GW>();
+      else wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + S - 1 < nk) issue(kt + S - 1);
+    const char* cur = smem + (kt % S) * CV_TILE;
+    compute_tile<CV_BM, CV_BN, false, false, false>(cur, cur + CV_BM * 128, acc, csum, lane, wm, wn);
+  }
+  // lane holds dW[m0 + wm 64 + 16 i + (lane & 15)][nn0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3]
+  float* out = a.part + (size_t)split * a.N * NN;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * (CV_BM / 2) + 16 * i + (lane & 15);
+    float* row = out + (size_t)m * NN + nn0 + wn * (CV_BN / 2) + 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      *reinterpret_cast<float4*>(row + 16 * j) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+  }
+}
+
+// dW = sum over slices in slice order (fp32), written as bf16 or fp32
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part, int nsplit,
+                                                                long long n, void* __restrict__ dw, int out_bf16) {
+  const long long i = (blockIdx.x * 256ll + threadIdx.x) * 4;
+  if (i >= n) return;
+  float4 s = *reinterpret_cast<const float4*>(part + i);
+  for (int k = 1; k < nsplit; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (size_t)k * n + i);
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  if (out_bf16) {
+    uint2 o;
+    o.x = pack2bf(s.x, s.y);
+    o.y = pack2bf(s.z, s.w);
+    *reinterpret_cast<uint2*>(static_cast<uint16_t*>(dw) + i) = o;
+  } else {
+    *reinterpret_cast<float4*>(static_cast<float*>(dw) + i) = s;
+  }
+}
+
+template <auto FN>
+static void allow_lds_once(size_t bytes) {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(FN), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    done = true;
+  }
+}
+
+static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int C, int N, int KS, const char* what) {
+  if (KS != 1 && KS != 3) return fail(std::string(what) + ": kernel size must be 1 or 3");
+  if (B < 0 || H <= 0 || W <= 0) return fail(std::string(what) + ": bad B / H / W");
+  if (C % 128 || N % 128 || C <= 0 || N <= 0)
+    return fail(std::string(what) + ": channels must be positive multiples of 128");
+  if ((long long)B * H * W * (C > N ? C : N) >= (1ll << 31)) return fail(std::string(what) + ": tensor too large");
+  for (int i = 0; i < np; ++i)
+    if (ptrs[i] == nullptr || reinterpret_cast<uintptr_t>(ptrs[i]) % 16)
+      return fail(std::string(what) + ": operands must be non-NULL and 16-B aligned");
+  return 0;
+}
+
+constexpr int CV_STAGES = 2;
+
+template <int KS>
+static void launch_fwd(const ConvArgs& a, hipStream_t stream, ProfScope& prof) {
+  constexpr size_t lds = CV_STAGES * CV_TILE;
+  allow_lds_once<conv_fwd_kernel<KS, CV_STAGES>>(lds);
+  const int NT = a.N / CV_BN;
+  const int grid = ((a.mt_n + 7) / 8) * 8 * NT;
+  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, CV_STAGES>), dim3(grid), dim3(256), lds, stream, a);
+}
+
+template <int KS>
+static void launch_wgrad(const ConvWgArgs& a, hipStream_t stream, ProfScope& prof) {
+  constexpr size_t lds = CV_STAGES * CV_TILE;
+  allow_lds_once<conv_wgrad_kernel<KS, CV_STAGES>>(lds);
+  const int tiles = (a.N / CV_BM) * (KS * KS * a.C / CV_BN);
+  const int grid = ((tiles + 7) / 8) * a.nsplit * 8;
+  MOE_LAUNCH(prof, (conv_wgrad_kernel<KS, CV_STAGES>), dim3(grid), dim3(256), lds, stream, a);
+}
+
+}  // namespace moe
+
+using namespace moe;
+
+extern "C" int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void* zero, int B, int H, int W, int C,
+                               int N, int KS, hipStream_t stream) {
+  const void* ptrs[4] = {x, w, y, zero};
+  if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, "rtdetr_conv_fwd")) return rc;
+  if (B == 0) return 0;
+  ConvArgs a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(y),
+             static_cast<const uint16_t*>(zero), B, H, W, C, N, B * H * W, 0};
+  a.mt_n = (a.P + CV_BM - 1) / CV_BM;
+  const double P = a.P;
+  ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N) + 2.0 * N * KS * KS * C, false, 0.0,
+                 2.0 * P * N * KS * KS * C);
+  if (KS == 3) launch_fwd<3>(a, stream, prof);
+  else launch_fwd<1>(a, stream, prof);
+  return check_launch("rtdetr_conv_fwd");
+}
+
+extern "C" int rtdetr_conv_weight_flip(const void* w, void* wt, int N, int C, int KS, hipStream_t stream) {
+  if (w == nullptr || wt == nullptr || N <= 0 || C <= 0 || (KS != 1 && KS != 3))
+    return fail("rtdetr_conv_weight_flip: bad arguments");
+  const long long total = (long long)N * C * KS * KS;
+  const int grid = (int)std::min<long long>((total + 255) / 256, 4096);
+  ProfScope prof(stream, PROF_CONV, 4.0 * total);
+  MOE_LAUNCH(prof, conv_weight_flip_kernel, dim3(grid), dim3(256), 0, stream, static_cast<const uint16_t*>(w),
+             static_cast<uint16_t*>(wt), N, C, KS);
+  return check_launch("rtdetr_conv_weight_flip");
+}
+
+extern "C" int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS) {
+  // slices so that the grid is ~2 workgroups per CU, each slice >= 8 pixel K-tiles
+  const long long tiles = (long long)(N / CV_BM) * (KS * KS * C / CV_BN);
+  const long long ktot = ((long long)B * H * W + 63) / 64;
+  long long s = (512 + tiles - 1) / std::max(1ll, tiles);
+  s = std::min(s, std::max(1ll, ktot / 8));
+  return (int)std::max(1ll, std::min(s, 64ll));
+}
+
+extern "C" int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
+                                 const void* zero, int B, int H, int W, int C, int N, int KS, hipStream_t stream) {
+  const void* ptrs[5] = {dy, x, part, dw, zero};
+  if (int rc = conv_check(ptrs, 5, B, H, W, C, N, KS, "rtdetr_conv_wgrad")) return rc;
+  if (nsplit < 1 || nsplit > 64) return fail("rtdetr_conv_wgrad: nsplit must be 1..64");
+  ConvWgArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(x), part,
+               static_cast<const uint16_t*>(zero), B, H, W, C, N, B * H * W, nsplit, 0};
+  const int ktot = (a.P + 63) / 64;
+  a.kt_per = (ktot + nsplit - 1) / nsplit;
+  const long long nw = (long long)N * KS * KS * C;
+  {
+    const double P = a.P;
+    ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N) + 4.0 * nsplit * nw, false, 0.0, 2.0 * P * nw);
+    if (KS == 3) launch_wgrad<3>(a, stream, prof);
+    else launch_wgrad<1>(a, stream, prof);
+    if (int rc = check_launch("rtdetr_conv_wgrad")) return rc;
+  }
+  ProfScope prof(stream, PROF_CONV, 4.0 * nsplit * nw + (out_bf16 ? 2.0 : 4.0) * nw);
+  MOE_LAUNCH(prof, conv_wgrad_reduce_kernel, dim3((unsigned)((nw / 4 + 255) / 256)), dim3(256), 0, stream, part,
+             nsplit, nw, dw, out_bf16);
+  return check_launch("rtdetr_conv_wgrad (reduce)");
+}

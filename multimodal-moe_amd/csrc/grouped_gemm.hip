@@ -28,6 +28,7 @@
 //      raw s_barrier (no vmcnt(0) drain inside the loop).
 #include <algorithm>
 
+#include "mfma_lds.h"
 #include "moe_common.h"
 #include "prof.h"
 
@@ -110,56 +111,6 @@ struct SplitWs {
   int n_cnt = 0;
 };
 static SplitWs g_split_ws[64];
-
-typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-
-// byte offset of 16-B chunk c of row r in a K-contiguous [R][64] image
-__device__ __forceinline__ int kimg_off(int r, int c) {
-  return r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
-}
-// chunk swizzle of an MN-contiguous [64][R] image (R = 128 or 64 bf16 per k-row)
-template <int R>
-__device__ __forceinline__ int mimg_swz(int r) {
-  if constexpr (R == 128) return ((r & 3) << 1) | (((r >> 3) & 1) << 3);
-  else return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2);
-}
-template <int R>
-__device__ __forceinline__ int mimg_off(int r, int c) {
-  return r * (R * 2) + ((c ^ mimg_swz<R>(r)) << 4);
-}
-
-// Fragment (8 bf16 along k) for operand row block `row_base` (16 rows) at k-step ks.
-template <int R, bool KCONT>
-__device__ __forceinline__ bf16x8 read_frag(const char* lds, int row_base, int ks, int lane) {
-  if constexpr (KCONT) {
-    const int r = row_base + (lane & 15);
-    const int c = ks * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8*>(lds + kimg_off(r, c));
-  } else {
-    const int i = lane & 15;
-    const int q = i >> 2, p = i & 3;
-    const int kr = ks * 32 + 8 * (lane >> 4) + q;
-    const int col = row_base + 4 * p;
-    const int c = col >> 3;
-    const int half = (col & 7) * 2;  // 0 or 8 bytes
-    char* base = const_cast<char*>(lds);
-    lds_bf16x4* p0 = (lds_bf16x4*)(base + mimg_off<R>(kr, c) + half);
-    lds_bf16x4* p1 = (lds_bf16x4*)(base + mimg_off<R>(kr + 4, c) + half);
-    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(p0);
-    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(p1);
-    bf16x8 v;
-    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-    v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-    return v;
-  }
-}
-
-__device__ __forceinline__ float sum8(bf16x8 v) {
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) s += bf2f((uint16_t)v[i]);
-  return s;
-}
 
 // ---------------------------------------------------------------------------
 // tile schedule + operand addressing shared by both main loops
@@ -681,31 +632,6 @@ __device__ __forceinline__ bool splitk_merge(const GemmParams& p, int tile_id, i
   return true;
 }
 
-// MFMA work on one staged K-tile (2 k-steps of 32).
-template <int BM, int BN, bool A_K, bool B_K, bool COLSUM>
-__device__ __forceinline__ void compute_tile(const char* abuf, const char* bbuf,
-                                             f32x4 (&acc)[BM / 32][BN / 32], float (&csum)[BM / 32],
-                                             int lane, int wm, int wn) {
-  constexpr int TM = BM / 32, TN = BN / 32;
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    bf16x8 af[TM], bfr[TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) af[i] = read_frag<BM, A_K>(abuf, wm * (BM / 2) + 16 * i, ks, lane);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bfr[j] = read_frag<BN, B_K>(bbuf, wn * (BN / 2) + 16 * j, ks, lane);
-    if constexpr (COLSUM) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i) csum[i] += sum8(af[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-  }
-}
-
 // MFMA work on one staged MXFP8 K-tile (128 e4m3 per row = one 128-B LDS row,
 // the same image as a bf16 K-tile): one v_mfma_scale_f32_16x16x128_f8f6f4 per
 // (i, j).  Operand map (measured with tools/mx_probe.hip, exact integer data):
@@ -1098,11 +1024,6 @@ __device__ __forceinline__ void dma_tile_rows(const uint16_t* const (&rowp)[R / 
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)(lds + ins * 1024), 16, 0, 0);
   }
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 template <int BM, int BN, int S, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>

@@ -89,6 +89,10 @@ SIGNATURES = {
     "rtdetr_attn_fwd": (_I, [_P, _LL, _P, _LL, _P, _LL, _P, _LL, _P, _I, _I, _I, _I, _F, _P]),
     "rtdetr_attn_bwd": (_I, [_P, _LL, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _P, _P, _P, _LL, _P, _LL, _P, _LL,
                              _I, _I, _I, _I, _F, _P]),
+    "rtdetr_conv_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "rtdetr_conv_weight_flip": (_I, [_P, _P, _I, _I, _I, _P]),
+    "rtdetr_conv_wgrad_splits": (_I, [_I, _I, _I, _I, _I, _I]),
+    "rtdetr_conv_wgrad": (_I, [_P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P]),
     "train_grad_pack": (_I, [_P, _P, _I, _P, _P]),
     "train_grad_sqnorm": (_I, [_P, _P, _I, _P, _P]),
     "train_grad_norm_finalize": (_I, [_P, _I, _F, _F, _P, _P, _I, _P, _P]),
@@ -141,7 +145,7 @@ def lib() -> ctypes.CDLL:
 
 PROF_KINDS = {0: "grouped_gemm", 1: "dispatch", 2: "router", 3: "route_scan", 4: "token_bwd", 5: "msda",
               6: "mx_quant", 7: "conv_epilogue", 8: "optimizer", 9: "matcher", 10: "grouped_gemm_fp8",
-              11: "linear_wgrad", 12: "attention"}
+              11: "linear_wgrad", 12: "attention", 13: "conv"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_FP8_TFLOPS = 5000.0   # MI355X dense fp8 / MXFP8 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E

@@ -16,6 +16,7 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
+from .conv import conv2d, conv_module
 from .fused import AddBiasReLU, AddBiasReLUFork, BiasReLU, bn_act, bn_act_ok
 
 _FUSED_BN = os.environ.get("MOE_FUSED_BN", "1") != "0"  # A/B switch: training BN + SiLU in HIP
@@ -186,7 +187,7 @@ class ConvNormLayer(nn.Module):
         self._w_folded = None
         if w is None:
             w = _FoldScale.apply(self.conv.weight, scale)
-        return F.conv2d(x, w, None, self.conv.stride, self.conv.padding), shift
+        return conv2d(x, w, self.conv.stride, self.conv.padding), shift
 
     def forward(self, x):
         if self.fold:
@@ -194,7 +195,7 @@ class ConvNormLayer(nn.Module):
             if self.act_name == "relu":
                 return BiasReLU.apply(y, shift)
             return y + shift.view(1, -1, 1, 1).to(y.dtype)
-        y = self.conv(x)
+        y = conv_module(self.conv, x)
         if self.act_name in (None, "silu") and _FUSED_BN and bn_act_ok([y], [self.norm]):
             return bn_act([y], [self.norm], self.act_name)  # BN + SiLU in HIP (training statistics)
         return self.act(self.norm(y))

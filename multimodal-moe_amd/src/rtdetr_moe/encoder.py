@@ -12,6 +12,7 @@ from ..moe.config import MoEConfig
 from ..moe.layer import MoEFFN
 from .norm import AddLayerNorm
 from .backbone import _FUSED_BN, ConvNormLayer
+from .conv import conv_module
 from .fused import bn_act, bn_act_ok
 from .linear import TokenLinear, TokenSelfAttention
 
@@ -57,7 +58,7 @@ class RepVggBlock(nn.Module):
 
     def forward(self, x):
         if _FUSED_BN:
-            y1, y2 = self.conv1.conv(x), self.conv2.conv(x)
+            y1, y2 = conv_module(self.conv1.conv, x), conv_module(self.conv2.conv, x)
             if bn_act_ok([y1, y2], [self.conv1.norm, self.conv2.norm]):  # both BNs + sum + SiLU in HIP
                 return bn_act([y1, y2], [self.conv1.norm, self.conv2.norm], "silu")
             return F.silu(self.conv1.norm(y1) + self.conv2.norm(y2))
@@ -122,7 +123,7 @@ class HybridEncoder(nn.Module):
     def _proj(p, f):
         conv, bn = p[0], p[1]
         if _FUSED_BN:
-            y = conv(f)
+            y = conv_module(conv, f)
             return bn_act([y], [bn], None) if bn_act_ok([y], [bn]) else bn(y)
         return p(f)
 

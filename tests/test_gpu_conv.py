@@ -1,0 +1,71 @@
+"""HIP implicit-GEMM convolutions (csrc/conv.hip) vs a plain PyTorch fp32
+reference of the same op (F.conv2d on the same bf16 operands, upcast):
+forward, data gradient and weight gradient, 1x1 and 3x3, stride 1 with
+"same" padding, NHWC bf16.
+
+Shapes: the C2 encoder's RepVGG convolutions (256 -> 256 at 23x40, batch 8),
+a ResNet bottleneck shape (128 channels), channel-asymmetric layers
+(512 -> 128, 128 -> 256), odd spatial sizes (7 x 9: the partial 128-pixel
+tile and every padding case) and a single image.
+
+Tolerance (stated): bf16 outputs of fp32 accumulations over K = KS^2 Cin
+(up to 4,608 terms), so relative Frobenius error <= 1e-2 and per element
+|err| <= 2e-2 max|ref|; the weight gradient's pixel slices are summed in a
+fixed order, so repeated launches are bitwise identical."""
+from __future__ import annotations
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _check(got, ref, what):
+    got, ref = got.float(), ref.float()
+    assert torch.isfinite(got).all(), what
+    err = (got - ref).abs().max().item()
+    rel = ((got - ref).norm() / ref.norm().clamp(min=1e-30)).item()
+    assert err <= 2e-2 * ref.abs().max().item() + 1e-6, f"{what}: max err {err:.3e}"
+    assert rel <= 1e-2, f"{what}: relative Frobenius {rel:.3e}"
+
+
+@pytest.mark.parametrize("B,C,N,H,W,ks", [(8, 256, 256, 23, 40, 3), (8, 256, 256, 23, 40, 1), (2, 128, 128, 46, 80, 3),
+                                          (2, 512, 128, 7, 9, 1), (2, 128, 256, 7, 9, 3), (1, 256, 512, 5, 3, 3)])
+def test_conv_fwd_bwd_vs_fp32(hip_lib, B, C, N, H, W, ks):
+    from src.rtdetr_moe.conv import _ConvHIP, hip_conv_ok
+
+    g = torch.Generator(device=DEV).manual_seed(B + C + N + H + ks)
+    x = torch.randn(B, C, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(N, C, ks, ks, device=DEV, generator=g) * (C * ks * ks) ** -0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(B, N, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert hip_conv_ok(x, w, 1, (ks - 1) // 2)
+    xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y = _ConvHIP.apply(xa, wa)
+    assert y.shape == (B, N, H, W) and y.is_contiguous(memory_format=torch.channels_last)
+    gx, gw = torch.autograd.grad(y, (xa, wa), gy)
+    xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, 1, (ks - 1) // 2)
+    gxr, gwr = torch.autograd.grad(yr, (xr, wr), gy.float())
+    torch.cuda.synchronize()
+    _check(y, yr, "y")
+    _check(gx, gxr, "dx")
+    _check(gw, gwr, "dw")
+    y2 = _ConvHIP.apply(xa, wa)
+    gx2, gw2 = torch.autograd.grad(y2, (xa, wa), gy)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2) and torch.equal(gx, gx2) and torch.equal(gw, gw2)
+
+
+def test_conv_dispatch_rules(hip_lib):
+    """Only the covered convolutions take the HIP kernels."""
+    from src.rtdetr_moe.conv import hip_conv_ok
+
+    x = torch.zeros(1, 256, 8, 8, device=DEV, dtype=torch.bfloat16)
+    w3 = torch.zeros(256, 256, 3, 3, device=DEV, dtype=torch.bfloat16)
+    assert hip_conv_ok(x, w3, 1, 1) and not hip_conv_ok(x, w3, 2, 1) and not hip_conv_ok(x, w3, 1, 0)
+    assert not hip_conv_ok(x.float(), w3.float(), 1, 1)
+    assert not hip_conv_ok(torch.zeros(1, 64, 8, 8, device=DEV, dtype=torch.bfloat16),
+                           torch.zeros(64, 64, 3, 3, device=DEV, dtype=torch.bfloat16), 1, 1)
