@@ -30,8 +30,9 @@
 
 namespace moe {
 
-constexpr int CV_BM = 128, CV_BN = 128;
-constexpr int CV_TILE = (CV_BM + CV_BN) * 64 * 2;  // bytes of one ring stage
+constexpr int CV_BM = 128, CV_BN = 128;             // weight-gradient tile
+constexpr int CV_TILE = (CV_BM + CV_BN) * 64 * 2;  // bytes of one weight-gradient ring stage
+static int g_conv_bm = 0;  // moe_set_tuning "conv_bm": 0 = by problem size, else 128 or 256 (forward)
 
 struct ConvArgs {
   const uint16_t* x;     // [B H W, C] (fwd: X; dgrad: dY)
@@ -51,22 +52,24 @@ __device__ __forceinline__ void dma16(const uint16_t* src, char* lds) {
 // ---------------------------------------------------------------------------
 // forward / data gradient
 // ---------------------------------------------------------------------------
-template <int KS, int S>
+template <int KS, int S, int BM>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TM = CV_BM / 32, TN = CV_BN / 32;
-  constexpr int GW = CV_BM / 32 + CV_BN / 32;  // DMA instructions per wave per K-tile
+  constexpr int BN = 128;
+  constexpr int TILE = (BM + BN) * 128;  // bytes of one ring stage
+  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int GW = BM / 32 + BN / 32;  // DMA instructions per wave per K-tile
   constexpr int PAD = (KS - 1) / 2;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   // XCD-aware map: the N tiles of one M tile run on one XCD (they share the A panel)
-  const int NT = a.N / CV_BN;
+  const int NT = a.N / BN;
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
   const int nt = slot % NT;
   const int mt = (slot / NT) * 8 + xcd;
   if (mt >= a.mt_n) return;
-  const int m0 = mt * CV_BM, n0 = nt * CV_BN;
+  const int m0 = mt * BM, n0 = nt * BN;
   const int cpt = a.C / 64;        // K-tiles per tap
   const int nk = KS * KS * cpt;
   const int HW = a.H * a.W;
@@ -92,7 +95,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     wrow[j] = a.w + (size_t)(n0 + r) * (KS * KS * a.C) + ((lane & 7) ^ ((r >> 1) & 7)) * 8;
   }
   auto issue = [&](int kt) {
-    char* buf = smem + (kt % S) * CV_TILE;
+    char* buf = smem + (kt % S) * TILE;
     const int tap = kt / cpt, c0 = (kt - tap * cpt) * 64;
     const int dy = tap / KS - PAD, dx = tap % KS - PAD;
 #pragma unroll
@@ -103,7 +106,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
       dma16(src, buf + (wave + 4 * j) * 1024);
     }
 #pragma unroll
-    for (int j = 0; j < TN; ++j) dma16(wrow[j] + tap * a.C + c0, buf + CV_BM * 128 + (wave + 4 * j) * 1024);
+    for (int j = 0; j < TN; ++j) dma16(wrow[j] + tap * a.C + c0, buf + BM * 128 + (wave + 4 * j) * 1024);
   };
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -124,15 +127,15 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     }
     __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
     if (kt + S - 1 < nk) issue(kt + S - 1);  // refills the slot consumed in iteration kt - 1
-    const char* cur = smem + (kt % S) * CV_TILE;
-    compute_tile<CV_BM, CV_BN, true, true, false>(cur, cur + CV_BM * 128, acc, csum, lane, wm, wn);
+    const char* cur = smem + (kt % S) * TILE;
+    compute_tile<BM, BN, true, true, false>(cur, cur + BM * 128, acc, csum, lane, wm, wn);
   }
   // lane holds Y[m0 + wm 64 + 16 i + (lane & 15)][n0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3]
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int p = m0 + wm * (CV_BM / 2) + 16 * i + (lane & 15);
+    const int p = m0 + wm * (BM / 2) + 16 * i + (lane & 15);
     if (p >= a.P) continue;
-    uint16_t* yrow = a.y + (size_t)p * a.N + n0 + wn * (CV_BN / 2) + 4 * (lane >> 4);
+    uint16_t* yrow = a.y + (size_t)p * a.N + n0 + wn * (BN / 2) + 4 * (lane >> 4);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       uint2 v;
@@ -302,13 +305,14 @@ static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int 
 
 constexpr int CV_STAGES = 2;
 
-template <int KS>
-static void launch_fwd(const ConvArgs& a, hipStream_t stream, ProfScope& prof) {
-  constexpr size_t lds = CV_STAGES * CV_TILE;
-  allow_lds_once<conv_fwd_kernel<KS, CV_STAGES>>(lds);
-  const int NT = a.N / CV_BN;
+template <int KS, int BM>
+static void launch_fwd(ConvArgs a, hipStream_t stream, ProfScope& prof) {
+  constexpr size_t lds = CV_STAGES * (BM + 128) * 128;
+  allow_lds_once<conv_fwd_kernel<KS, CV_STAGES, BM>>(lds);
+  a.mt_n = (a.P + BM - 1) / BM;
+  const int NT = a.N / 128;
   const int grid = ((a.mt_n + 7) / 8) * 8 * NT;
-  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, CV_STAGES>), dim3(grid), dim3(256), lds, stream, a);
+  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, CV_STAGES, BM>), dim3(grid), dim3(256), lds, stream, a);
 }
 
 template <int KS>
@@ -331,12 +335,20 @@ extern "C" int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void
   if (B == 0) return 0;
   ConvArgs a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(y),
              static_cast<const uint16_t*>(zero), B, H, W, C, N, B * H * W, 0};
-  a.mt_n = (a.P + CV_BM - 1) / CV_BM;
   const double P = a.P;
   ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N) + 2.0 * N * KS * KS * C, false, 0.0,
                  2.0 * P * N * KS * KS * C);
-  if (KS == 3) launch_fwd<3>(a, stream, prof);
-  else launch_fwd<1>(a, stream, prof);
+  // 256-pixel tiles halve the weight-tile DMA per flop; only with enough
+  // tiles to fill the chip (>= ~2 rounds of workgroups on 256 CUs)
+  int bm = g_conv_bm;
+  if (bm != 128 && bm != 256) bm = (long long)((a.P + 255) / 256) * (N / 128) >= 512 ? 256 : 128;
+  if (KS == 3) {
+    if (bm == 256) launch_fwd<3, 256>(a, stream, prof);
+    else launch_fwd<3, 128>(a, stream, prof);
+  } else {
+    if (bm == 256) launch_fwd<1, 256>(a, stream, prof);
+    else launch_fwd<1, 128>(a, stream, prof);
+  }
   return check_launch("rtdetr_conv_fwd");
 }
 
@@ -381,4 +393,13 @@ extern "C" int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int
   MOE_LAUNCH(prof, conv_wgrad_reduce_kernel, dim3((unsigned)((nw / 4 + 255) / 256)), dim3(256), 0, stream, part,
              nsplit, nw, dw, out_bf16);
   return check_launch("rtdetr_conv_wgrad (reduce)");
+}
+
+extern "C" int rtdetr_conv_set_tuning(const char* key, int value) {
+  if (key == nullptr) return fail("rtdetr_conv_set_tuning: key is NULL");
+  if (std::string(key) == "conv_bm") {
+    g_conv_bm = value;
+    return 0;
+  }
+  return fail(std::string("rtdetr_conv_set_tuning: unknown key ") + key);
 }

@@ -92,6 +92,7 @@ SIGNATURES = {
     "rtdetr_conv_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "rtdetr_conv_weight_flip": (_I, [_P, _P, _I, _I, _I, _P]),
     "rtdetr_conv_wgrad_splits": (_I, [_I, _I, _I, _I, _I, _I]),
+    "rtdetr_conv_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "rtdetr_conv_wgrad": (_I, [_P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P]),
     "train_grad_pack": (_I, [_P, _P, _I, _P, _P]),
     "train_grad_sqnorm": (_I, [_P, _P, _I, _P, _P]),

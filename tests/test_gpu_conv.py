@@ -3,7 +3,8 @@ reference of the same op (F.conv2d on the same bf16 operands, upcast):
 forward, data gradient and weight gradient, 1x1 and 3x3, stride 1 with
 "same" padding, NHWC bf16.
 
-Shapes: the C2 encoder's RepVGG convolutions (256 -> 256 at 23x40, batch 8),
+Forward tiles of 128 and 256 pixels (rtdetr_conv_set_tuning "conv_bm") and the
+automatic choice.  Shapes: the C2 encoder's RepVGG convolutions (256 -> 256 at 23x40, batch 8),
 a ResNet bottleneck shape (128 channels), channel-asymmetric layers
 (512 -> 128, 128 -> 256), odd spatial sizes (7 x 9: the partial 128-pixel
 tile and every padding case) and a single image.
@@ -31,9 +32,20 @@ def _check(got, ref, what):
     assert rel <= 1e-2, f"{what}: relative Frobenius {rel:.3e}"
 
 
+@pytest.mark.parametrize("bm", [0, 128, 256], ids=["bm_auto", "bm128", "bm256"])
 @pytest.mark.parametrize("B,C,N,H,W,ks", [(8, 256, 256, 23, 40, 3), (8, 256, 256, 23, 40, 1), (2, 128, 128, 46, 80, 3),
                                           (2, 512, 128, 7, 9, 1), (2, 128, 256, 7, 9, 3), (1, 256, 512, 5, 3, 3)])
-def test_conv_fwd_bwd_vs_fp32(hip_lib, B, C, N, H, W, ks):
+def test_conv_fwd_bwd_vs_fp32(hip_lib, B, C, N, H, W, ks, bm):
+    from src.rtdetr_moe.conv import _ConvHIP, hip_conv_ok
+
+    assert hip_lib.rtdetr_conv_set_tuning(b"conv_bm", bm) == 0
+    try:
+        _conv_case(B, C, N, H, W, ks)
+    finally:
+        hip_lib.rtdetr_conv_set_tuning(b"conv_bm", 0)
+
+
+def _conv_case(B, C, N, H, W, ks):
     from src.rtdetr_moe.conv import _ConvHIP, hip_conv_ok
 
     g = torch.Generator(device=DEV).manual_seed(B + C + N + H + ks)

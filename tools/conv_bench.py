@@ -1,0 +1,107 @@
+"""Per-shape timing of the body's convolutions: MIOpen (F.conv2d, with the
+bench's find-db and benchmark mode) against the HIP implicit-GEMM kernels
+(csrc/conv.hip), forward, data gradient and weight gradient separately.
+
+    python tools/conv_bench.py > gpurun_out/conv_bench.jsonl
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+for p in (str(ROOT / "multimodal-moe_amd"), str(ROOT)):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+os.environ.setdefault("MIOPEN_USER_DB_PATH", str(ROOT / "multimodal-moe_amd" / "miopen_db"))
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+# (B, Cin, Cout, H, W, KS): the C2 step's stride-1 convolutions with 128-multiple channels
+SHAPES = [(8, 256, 256, 46, 80, 3), (8, 256, 256, 92, 160, 3), (8, 256, 256, 23, 40, 3), (8, 128, 128, 92, 160, 3),
+          (8, 512, 512, 23, 40, 3), (8, 256, 256, 46, 80, 1), (8, 256, 256, 92, 160, 1), (8, 1024, 256, 46, 80, 1),
+          (8, 256, 1024, 46, 80, 1), (8, 512, 128, 92, 160, 1), (8, 128, 512, 92, 160, 1), (8, 2048, 512, 23, 40, 1),
+          (8, 512, 2048, 23, 40, 1), (8, 512, 256, 92, 160, 1)]
+
+
+def timeit(fn, reps=20):
+    """GPU time per call of fn replayed from a hipGraph (as the training step
+    runs): no host launch gaps between a library's kernels."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    g.replay()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1e3 / reps  # us
+
+
+def main():
+    from src.moe import _lib as L
+    from src.rtdetr_moe import conv as C
+
+    L.lib()
+    torch.backends.cudnn.benchmark = True
+    dev = torch.device("cuda", 0)
+    shapes = SHAPES
+    args = [a for a in sys.argv[1:] if "=" not in a]
+    for kv in [a for a in sys.argv[1:] if "=" in a]:  # e.g. conv_bm=256
+        k, v = kv.split("=")
+        L._check(L.lib().rtdetr_conv_set_tuning(k.encode(), int(v)), "rtdetr_conv_set_tuning")
+    if args:
+        shapes = [tuple(int(v) for v in s.split(",")) for s in args]
+    for B, Ci, Co, H, W, ks in shapes:
+        x = torch.randn(B, Ci, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        w = (torch.randn(Co, Ci, ks, ks, device=dev) * 0.05).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        gy = torch.randn(B, Co, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        pad = (ks - 1) // 2
+        flop = 2.0 * B * H * W * Ci * Co * ks * ks
+        t_mf = timeit(lambda: F.conv2d(x, w, None, 1, pad))
+        t_md = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [pad, pad], [1, 1], False,
+                                                                  [0, 0], 1, [True, False, False]))
+        t_mw = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [pad, pad], [1, 1], False,
+                                                                  [0, 0], 1, [False, True, False]))
+        z = C._zero(dev).data_ptr()
+        s = L._stream()
+        lib = L.lib()
+        yh = torch.empty_like(gy)
+        t_hf = timeit(lambda: lib.rtdetr_conv_fwd(x.data_ptr(), w.data_ptr(), yh.data_ptr(), z, B, H, W, Ci, Co, ks, s))
+        wt = torch.empty((Ci, ks, ks, Co), dtype=torch.bfloat16, device=dev)
+        gx = torch.empty_like(x)
+
+        def dgrad():
+            lib.rtdetr_conv_weight_flip(w.data_ptr(), wt.data_ptr(), Co, Ci, ks, s)
+            lib.rtdetr_conv_fwd(gy.data_ptr(), wt.data_ptr(), gx.data_ptr(), z, B, H, W, Co, Ci, ks, s)
+        t_hd = timeit(dgrad)
+        ns = lib.rtdetr_conv_wgrad_splits(B, H, W, Ci, Co, ks)
+        part = torch.empty(ns * Co * Ci * ks * ks, dtype=torch.float32, device=dev)
+        gw = torch.empty_like(w)
+        t_hw = timeit(lambda: lib.rtdetr_conv_wgrad(gy.data_ptr(), x.data_ptr(), part.data_ptr(), ns, gw.data_ptr(), 1,
+                                                    z, B, H, W, Ci, Co, ks, s))
+        tf = lambda t: round(flop / t / 1e6, 1)  # noqa: E731  TFLOP/s
+        print(json.dumps({"shape": [B, Ci, Co, H, W, ks], "gflop": round(flop / 1e9, 2), "wgrad_splits": ns,
+                          "miopen_us": [round(t_mf, 1), round(t_md, 1), round(t_mw, 1)],
+                          "hip_us": [round(t_hf, 1), round(t_hd, 1), round(t_hw, 1)],
+                          "miopen_tflops": [tf(t_mf), tf(t_md), tf(t_mw)], "hip_tflops": [tf(t_hf), tf(t_hd), tf(t_hw)]}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
