@@ -184,11 +184,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
   const int wm = wave >> 1, wn = wave & 1;
   const int NN = KS * KS * a.C;      // GEMM N
   const int MT = a.N / CV_BM, NT = NN / CV_BN;
-  // slices of one output tile on one XCD: bid = ((tile / 8) * nsplit + split) * 8 + tile % 8
+  // every tile of one pixel slice on one XCD: the slice's dY and X rows are
+  // read by all its output tiles, so they stream through that XCD's L2 once
+  // (slices of one tile spread over XCDs instead made every XCD read all rows)
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-  const int split = slot % a.nsplit;
-  const int tile = (slot / a.nsplit) * 8 + xcd;
-  if (tile >= MT * NT) return;
+  const int tiles = MT * NT;
+  const int tile = slot % tiles;
+  const int split = (slot / tiles) * 8 + xcd;
+  if (split >= a.nsplit) return;
   const int mt = tile % MT, nt = tile / MT;
   const int m0 = mt * CV_BM, nn0 = nt * CV_BN;
   const int tap = nn0 / a.C, c0 = nn0 - tap * a.C;
@@ -197,32 +200,42 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
   const int kt0 = split * a.kt_per;
   const int nk = max(0, min(a.kt_per, ktot - kt0));
   const int HW = a.H * a.W;
-  // k-row (pixel) of this lane in DMA instruction j: kr = (wave + 4 j) * 4 + lane / 16 (256-B rows)
-  int ach[4];
+  // k-row (pixel) of this lane in DMA instruction j: kr = (wave + 4 j) * 4 + lane / 16 (256-B rows);
+  // its (image, y, x) is kept and advanced by 64 pixels per K-tile (no divisions in the loop)
+  int ach[4], pp[4], py[4], px[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int kr = (wave + 4 * j) * 4 + (lane >> 4);
     ach[j] = ((lane & 15) ^ mimg_swz<128>(kr)) * 8;
+    const int p = kt0 * 64 + kr;
+    pp[j] = p;
+    const int q = p < a.P ? p : 0;
+    const int rem = q % HW;
+    py[j] = rem / a.W;
+    px[j] = rem - py[j] * a.W;
   }
   auto issue = [&](int kt) {
     char* buf = smem + (kt % S) * CV_TILE;
-    const int kb = (kt0 + kt) * 64;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int kr = (wave + 4 * j) * 4 + (lane >> 4);
-      const int p = kb + kr;
+      const int p = pp[j];
       const bool pv = p < a.P;
-      const int pp = pv ? p : 0;
-      const int b = pp / HW;
-      const int rem = pp - b * HW;
-      const int y = rem / a.W;
-      const int x = rem - y * a.W;
-      const int yy = y + dy_, xx = x + dx_;
+      const int yy = py[j] + dy_, xx = px[j] + dx_;
       const bool ok = pv && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+      const long long nb = (long long)p + (long long)dy_ * a.W + dx_;  // the neighbour's flat pixel index
       const uint16_t* sa = pv ? a.dy + (size_t)p * a.N + m0 + ach[j] : a.zero + ach[j];
-      const uint16_t* sb = ok ? a.x + ((size_t)(b * HW + yy * a.W + xx)) * a.C + c0 + ach[j] : a.zero + ach[j];
+      const uint16_t* sb = ok ? a.x + (size_t)nb * a.C + c0 + ach[j] : a.zero + ach[j];
       dma16(sa, buf + (wave + 4 * j) * 1024);
       dma16(sb, buf + CV_BM * 128 + (wave + 4 * j) * 1024);
+      // next K-tile: 64 pixels on (row-major within the image; images are contiguous)
+      pp[j] = p + 64;
+      int x = px[j] + 64, y = py[j];
+      while (x >= a.W) {
+        x -= a.W;
+        if (++y == a.H) y = 0;
+      }
+      px[j] = x;
+      py[j] = y;
     }
   };
   f32x4 acc[TM][TN];
@@ -320,7 +333,7 @@ static void launch_wgrad(const ConvWgArgs& a, hipStream_t stream, ProfScope& pro
   constexpr size_t lds = CV_STAGES * CV_TILE;
   allow_lds_once<conv_wgrad_kernel<KS, CV_STAGES>>(lds);
   const int tiles = (a.N / CV_BM) * (KS * KS * a.C / CV_BN);
-  const int grid = ((tiles + 7) / 8) * a.nsplit * 8;
+  const int grid = tiles * ((a.nsplit + 7) / 8) * 8;
   MOE_LAUNCH(prof, (conv_wgrad_kernel<KS, CV_STAGES>), dim3(grid), dim3(256), lds, stream, a);
 }
 
@@ -338,10 +351,8 @@ extern "C" int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void
   const double P = a.P;
   ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N) + 2.0 * N * KS * KS * C, false, 0.0,
                  2.0 * P * N * KS * KS * C);
-  // 256-pixel tiles halve the weight-tile DMA per flop; only with enough
-  // tiles to fill the chip (>= ~2 rounds of workgroups on 256 CUs)
   int bm = g_conv_bm;
-  if (bm != 128 && bm != 256) bm = (long long)((a.P + 255) / 256) * (N / 128) >= 512 ? 256 : 128;
+  if (bm != 128 && bm != 256) bm = 128;  // 256 rows: one workgroup per CU, measured slower at every C2 shape
   if (KS == 3) {
     if (bm == 256) launch_fwd<3, 256>(a, stream, prof);
     else launch_fwd<3, 128>(a, stream, prof);
@@ -364,12 +375,15 @@ extern "C" int rtdetr_conv_weight_flip(const void* w, void* wt, int N, int C, in
 }
 
 extern "C" int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS) {
-  // slices so that the grid is ~2 workgroups per CU, each slice >= 8 pixel K-tiles
+  // a multiple of 8 slices (one set per XCD) so that the grid is ~2 workgroups
+  // per CU, each slice >= 8 pixel K-tiles
   const long long tiles = (long long)(N / CV_BM) * (KS * KS * C / CV_BN);
   const long long ktot = ((long long)B * H * W + 63) / 64;
   long long s = (512 + tiles - 1) / std::max(1ll, tiles);
   s = std::min(s, std::max(1ll, ktot / 8));
-  return (int)std::max(1ll, std::min(s, 64ll));
+  s = std::min(s, 64ll);
+  if (s >= 8) s = s / 8 * 8;
+  return (int)std::max(1ll, s);
 }
 
 extern "C" int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,

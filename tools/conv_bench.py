@@ -79,14 +79,15 @@ def main():
         t_mw = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [pad, pad], [1, 1], False,
                                                                   [0, 0], 1, [False, True, False]))
         z = C._zero(dev).data_ptr()
-        s = L._stream()
         lib = L.lib()
         yh = torch.empty_like(gy)
-        t_hf = timeit(lambda: lib.rtdetr_conv_fwd(x.data_ptr(), w.data_ptr(), yh.data_ptr(), z, B, H, W, Ci, Co, ks, s))
+        t_hf = timeit(lambda: lib.rtdetr_conv_fwd(x.data_ptr(), w.data_ptr(), yh.data_ptr(), z, B, H, W, Ci, Co, ks,
+                                                  L._stream()))
         wt = torch.empty((Ci, ks, ks, Co), dtype=torch.bfloat16, device=dev)
         gx = torch.empty_like(x)
 
         def dgrad():
+            s = L._stream()  # the capture stream
             lib.rtdetr_conv_weight_flip(w.data_ptr(), wt.data_ptr(), Co, Ci, ks, s)
             lib.rtdetr_conv_fwd(gy.data_ptr(), wt.data_ptr(), gx.data_ptr(), z, B, H, W, Co, Ci, ks, s)
         t_hd = timeit(dgrad)
@@ -94,7 +95,7 @@ def main():
         part = torch.empty(ns * Co * Ci * ks * ks, dtype=torch.float32, device=dev)
         gw = torch.empty_like(w)
         t_hw = timeit(lambda: lib.rtdetr_conv_wgrad(gy.data_ptr(), x.data_ptr(), part.data_ptr(), ns, gw.data_ptr(), 1,
-                                                    z, B, H, W, Ci, Co, ks, s))
+                                                    z, B, H, W, Ci, Co, ks, L._stream()))
         tf = lambda t: round(flop / t / 1e6, 1)  # noqa: E731  TFLOP/s
         print(json.dumps({"shape": [B, Ci, Co, H, W, ks], "gflop": round(flop / 1e9, 2), "wgrad_splits": ns,
                           "miopen_us": [round(t_mf, 1), round(t_md, 1), round(t_mw, 1)],
