@@ -380,6 +380,7 @@ extern "C" int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int K
   const long long tiles = (long long)(N / CV_BM) * (KS * KS * C / CV_BN);
   const long long ktot = ((long long)B * H * W + 63) / 64;
   long long s = (512 + tiles - 1) / std::max(1ll, tiles);
+  s = std::max(s, 8ll);  // every XCD takes slices
   s = std::min(s, std::max(1ll, ktot / 8));
   s = std::min(s, 64ll);
   if (s >= 8) s = s / 8 * 8;
