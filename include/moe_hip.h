@@ -546,7 +546,7 @@ int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
                       const void* zero, int B, int H, int W, int C, int N, int KS, hipStream_t stream);
 /* Measurement / A-B knob: "conv_bm" = forward pixel-tile rows (0: by problem
- * size, 128 or 256). */
+ * size, 64, 128 or 256). */
 int rtdetr_conv_set_tuning(const char* key, int value);
 
 /* Training-step optimizer (the bench step's AdamW; reference: Ultralytics'

@@ -32,7 +32,7 @@ namespace moe {
 
 constexpr int CV_BM = 128, CV_BN = 128;             // weight-gradient tile
 constexpr int CV_TILE = (CV_BM + CV_BN) * 64 * 2;  // bytes of one weight-gradient ring stage
-static int g_conv_bm = 0;  // moe_set_tuning "conv_bm": 0 = by problem size, else 128 or 256 (forward)
+static int g_conv_bm = 0;  // rtdetr_conv_set_tuning "conv_bm": 0 = by problem size, else 64, 128 or 256 (forward)
 
 struct ConvArgs {
   const uint16_t* x;     // [B H W, C] (fwd: X; dgrad: dY)
@@ -130,18 +130,31 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     const char* cur = smem + (kt % S) * TILE;
     compute_tile<BM, BN, true, true, false>(cur, cur + BM * 128, acc, csum, lane, wm, wn);
   }
-  // lane holds Y[m0 + wm 64 + 16 i + (lane & 15)][n0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3]
+  // Epilogue through LDS: lane holds Y[m0 + wm BM/2 + 16 i + (lane & 15)][n0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3];
+  // the tile goes to a row-major [BM][128] bf16 image (16-B chunk c of row r at chunk c ^ (r & 15):
+  // conflict-free 8-B writes and 16-B reads), then out as whole 256-B rows of 16-B stores
+  // (register-direct 8-B stores at a row stride run at about half that rate)
+  __syncthreads();  // every wave is done reading the ring
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int p = m0 + wm * (BM / 2) + 16 * i + (lane & 15);
-    if (p >= a.P) continue;
-    uint16_t* yrow = a.y + (size_t)p * a.N + n0 + wn * (BN / 2) + 4 * (lane >> 4);
+    const int r = wm * (BM / 2) + 16 * i + (lane & 15);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
+      const int col = wn * (BN / 2) + 16 * j + 4 * (lane >> 4);
       uint2 v;
       v.x = pack2bf(acc[i][j][0], acc[i][j][1]);
       v.y = pack2bf(acc[i][j][2], acc[i][j][3]);
-      *reinterpret_cast<uint2*>(yrow + 16 * j) = v;
+      *reinterpret_cast<uint2*>(smem + r * 256 + (((col >> 3) ^ (r & 15)) << 4) + (col & 7) * 2) = v;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < BM / 16; ++k) {
+    const int r = (tid >> 4) + 16 * k, c = tid & 15;
+    const int p = m0 + r;
+    if (p < a.P) {
+      const uint4 v = *reinterpret_cast<const uint4*>(smem + r * 256 + ((c ^ (r & 15)) << 4));
+      *reinterpret_cast<uint4*>(a.y + (size_t)p * a.N + n0 + c * 8) = v;
     }
   }
 }
@@ -351,13 +364,18 @@ extern "C" int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void
   const double P = a.P;
   ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N) + 2.0 * N * KS * KS * C, false, 0.0,
                  2.0 * P * N * KS * KS * C);
+  // 128-pixel tiles (two workgroups per CU); 64-pixel tiles when 128-pixel
+  // ones would leave the chip under-filled (< 1.5 workgroups per CU); 256
+  // rows (one workgroup per CU) measured slower at every C2 shape
   int bm = g_conv_bm;
-  if (bm != 128 && bm != 256) bm = 128;  // 256 rows: one workgroup per CU, measured slower at every C2 shape
+  if (bm != 64 && bm != 128 && bm != 256) bm = (long long)((a.P + 127) / 128) * (N / 128) < 384 ? 64 : 128;
   if (KS == 3) {
     if (bm == 256) launch_fwd<3, 256>(a, stream, prof);
+    else if (bm == 64) launch_fwd<3, 64>(a, stream, prof);
     else launch_fwd<3, 128>(a, stream, prof);
   } else {
     if (bm == 256) launch_fwd<1, 256>(a, stream, prof);
+    else if (bm == 64) launch_fwd<1, 64>(a, stream, prof);
     else launch_fwd<1, 128>(a, stream, prof);
   }
   return check_launch("rtdetr_conv_fwd");

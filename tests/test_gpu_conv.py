@@ -3,7 +3,7 @@ reference of the same op (F.conv2d on the same bf16 operands, upcast):
 forward, data gradient and weight gradient, 1x1 and 3x3, stride 1 with
 "same" padding, NHWC bf16.
 
-Forward tiles of 128 and 256 pixels (rtdetr_conv_set_tuning "conv_bm") and the
+Forward tiles of 64, 128 and 256 pixels (rtdetr_conv_set_tuning "conv_bm") and the
 automatic choice.  Shapes: the C2 encoder's RepVGG convolutions (256 -> 256 at 23x40, batch 8),
 a ResNet bottleneck shape (128 channels), channel-asymmetric layers
 (512 -> 128, 128 -> 256), odd spatial sizes (7 x 9: the partial 128-pixel
@@ -32,7 +32,7 @@ def _check(got, ref, what):
     assert rel <= 1e-2, f"{what}: relative Frobenius {rel:.3e}"
 
 
-@pytest.mark.parametrize("bm", [0, 128, 256], ids=["bm_auto", "bm128", "bm256"])
+@pytest.mark.parametrize("bm", [0, 64, 128, 256], ids=["bm_auto", "bm64", "bm128", "bm256"])
 @pytest.mark.parametrize("B,C,N,H,W,ks", [(8, 256, 256, 23, 40, 3), (8, 256, 256, 23, 40, 1), (2, 128, 128, 46, 80, 3),
                                           (2, 512, 128, 7, 9, 1), (2, 128, 256, 7, 9, 3), (1, 256, 512, 5, 3, 3)])
 def test_conv_fwd_bwd_vs_fp32(hip_lib, B, C, N, H, W, ks, bm):
