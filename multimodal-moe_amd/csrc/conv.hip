@@ -397,11 +397,11 @@ extern "C" int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int K
   // per CU, each slice >= 8 pixel K-tiles
   const long long tiles = (long long)(N / CV_BM) * (KS * KS * C / CV_BN);
   const long long ktot = ((long long)B * H * W + 63) / 64;
-  long long s = (512 + tiles - 1) / std::max(1ll, tiles);
-  s = std::max(s, 8ll);  // every XCD takes slices
-  s = std::min(s, std::max(1ll, ktot / 8));
-  s = std::min(s, 64ll);
-  if (s >= 8) s = s / 8 * 8;
+  long long s = (512 + tiles - 1) / std::max(1ll, tiles);  // >= 2 workgroups per CU
+  s = (s + 7) / 8 * 8;                                     // every XCD takes the same number of slices
+  s = std::min(s, std::max(1ll, ktot / 4));                // slices of >= 4 pixel K-tiles
+  s = std::min(s, 128ll);
+  if (s > 8) s = s / 8 * 8;
   return (int)std::max(1ll, s);
 }
 
@@ -409,7 +409,7 @@ extern "C" int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int
                                  const void* zero, int B, int H, int W, int C, int N, int KS, hipStream_t stream) {
   const void* ptrs[5] = {dy, x, part, dw, zero};
   if (int rc = conv_check(ptrs, 5, B, H, W, C, N, KS, "rtdetr_conv_wgrad")) return rc;
-  if (nsplit < 1 || nsplit > 64) return fail("rtdetr_conv_wgrad: nsplit must be 1..64");
+  if (nsplit < 1 || nsplit > 128) return fail("rtdetr_conv_wgrad: nsplit must be 1..128");
   ConvWgArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(x), part,
                static_cast<const uint16_t*>(zero), B, H, W, C, N, B * H * W, nsplit, 0};
   const int ktot = (a.P + 63) / 64;
