@@ -531,9 +531,9 @@ int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, 
  * channels_last [N, C, KS, KS] weight); C and N multiples of 128; zero: >= 256
  * zero bytes on the device (read for padding neighbours); pointers 16-B aligned.
  *   rtdetr_conv_fwd         y[B,H,W,N] = conv(x[B,H,W,C], w)   (no im2col buffer)
- *   rtdetr_conv_weight_flip wt[C][KS][KS][N] = w[N][KS-1-ky][KS-1-kx][C]: the
- *                           data gradient is then rtdetr_conv_fwd(dy, wt) with
- *                           C and N exchanged
+ *   rtdetr_conv_dgrad       dx[B,H,W,C] = conv^T(dy[B,H,W,N], w): the forward
+ *                           GEMM over dy with the flipped, transposed weight
+ *                           read in place from w (no transposed copy)
  *   rtdetr_conv_wgrad       dw[N][KS][KS][C] = sum over pixels dy (x) x[neighbour]:
  *                           nsplit pixel slices write fp32 partials to part
  *                           [nsplit][N KS KS C], summed in slice order
@@ -541,7 +541,8 @@ int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, 
  *                           nsplit from rtdetr_conv_wgrad_splits. */
 int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void* zero, int B, int H, int W, int C, int N,
                     int KS, hipStream_t stream);
-int rtdetr_conv_weight_flip(const void* w, void* wt, int N, int C, int KS, hipStream_t stream);
+int rtdetr_conv_dgrad(const void* dy, const void* w, void* dx, const void* zero, int B, int H, int W, int C, int N,
+                      int KS, hipStream_t stream);
 int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
                       const void* zero, int B, int H, int W, int C, int N, int KS, hipStream_t stream);

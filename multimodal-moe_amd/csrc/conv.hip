@@ -11,9 +11,10 @@
 //                      tile's rows are the 64-channel slices of each pixel's
 //                      neighbour for the K-tile's tap, fetched by LDS-DMA with a
 //                      per-row source address (a padding neighbour reads a zero
-//                      row), so no im2col buffer exists.  Used for the data
-//                      gradient too: dX = conv(dY, W') with W' the flipped,
-//                      channel-transposed weight (conv_weight_flip_kernel).
+//                      row), so no im2col buffer exists.  The data gradient
+//                      is the same GEMM over dY with W'[c][tap][n] =
+//                      W[n][KS^2-1-tap][c], read in place from W as an
+//                      MN-contiguous operand image (template flag BT).
 //   conv_wgrad_kernel  dW[n, tap, c] = sum_p dY[p, n] X[nbr(p, tap), c]
 //                      GEMM M = Cout, N = KS^2 Cin, K = pixels, split over S
 //                      slices of the pixels (fp32 partials) and summed in slice
@@ -52,7 +53,7 @@ __device__ __forceinline__ void dma16(const uint16_t* src, char* lds) {
 // ---------------------------------------------------------------------------
 // forward / data gradient
 // ---------------------------------------------------------------------------
-template <int KS, int S, int BM>
+template <int KS, int S, int BM, bool BT>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BN = 128;
@@ -88,11 +89,21 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     px[j] = rem - py[j] * a.W;
     ach[j] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
   }
+  // B rows.  Forward: K-contiguous [BN][64] image of W[n][tap][c0..c0+63].
+  // BT (data gradient, a.w = the ORIGINAL weight [a.C][KS][KS][a.N]): the
+  // operand is W'[n][tap][k] = W[k][KS^2-1-tap][n], read as an MN-contiguous
+  // [64 k-rows][BN] image (k-row = one of W's output channels, BN contiguous
+  // input channels; ds_read_b64_tr_b16 fragments) -- no transposed copy of W.
   const uint16_t* wrow[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int r = (wave + 4 * j) * 8 + (lane >> 3);
-    wrow[j] = a.w + (size_t)(n0 + r) * (KS * KS * a.C) + ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+    if constexpr (BT) {
+      const int kr = (wave + 4 * j) * 4 + (lane >> 4);
+      wrow[j] = a.w + (size_t)kr * (KS * KS * a.N) + n0 + ((lane & 15) ^ mimg_swz<128>(kr)) * 8;
+    } else {
+      const int r = (wave + 4 * j) * 8 + (lane >> 3);
+      wrow[j] = a.w + (size_t)(n0 + r) * (KS * KS * a.C) + ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+    }
   }
   auto issue = [&](int kt) {
     char* buf = smem + (kt % S) * TILE;
@@ -106,7 +117,11 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
       dma16(src, buf + (wave + 4 * j) * 1024);
     }
 #pragma unroll
-    for (int j = 0; j < TN; ++j) dma16(wrow[j] + tap * a.C + c0, buf + BM * 128 + (wave + 4 * j) * 1024);
+    for (int j = 0; j < TN; ++j) {
+      if constexpr (BT) dma16(wrow[j] + (size_t)c0 * (KS * KS * a.N) + (KS * KS - 1 - tap) * a.N,
+                              buf + BM * 128 + (wave + 4 * j) * 1024);
+      else dma16(wrow[j] + tap * a.C + c0, buf + BM * 128 + (wave + 4 * j) * 1024);
+    }
   };
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -128,7 +143,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
     if (kt + S - 1 < nk) issue(kt + S - 1);  // refills the slot consumed in iteration kt - 1
     const char* cur = smem + (kt % S) * TILE;
-    compute_tile<BM, BN, true, true, false>(cur, cur + BM * 128, acc, csum, lane, wm, wn);
+    compute_tile<BM, BN, true, !BT, false>(cur, cur + BM * 128, acc, csum, lane, wm, wn);
   }
   // Epilogue through LDS: lane holds Y[m0 + wm BM/2 + 16 i + (lane & 15)][n0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3];
   // the tile goes to a row-major [BM][128] bf16 image (16-B chunk c of row r at chunk c ^ (r & 15):
@@ -156,21 +171,6 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
       const uint4 v = *reinterpret_cast<const uint4*>(smem + r * 256 + ((c ^ (r & 15)) << 4));
       *reinterpret_cast<uint4*>(a.y + (size_t)p * a.N + n0 + c * 8) = v;
     }
-  }
-}
-
-// W'[c][ky][kx][n] = W[n][KS-1-ky][KS-1-kx][c]: the data gradient's weight
-__global__ __launch_bounds__(256) void conv_weight_flip_kernel(const uint16_t* __restrict__ w,
-                                                               uint16_t* __restrict__ wt, int N, int C, int KS) {
-  const long long total = (long long)N * C * KS * KS;
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    // i indexes the OUTPUT [c][tap'][n] (writes coalesced)
-    const int n = (int)(i % N);
-    const long long q = i / N;
-    const int tap = (int)(q % (KS * KS));
-    const int c = (int)(q / (KS * KS));
-    const int ftap = KS * KS - 1 - tap;
-    wt[i] = w[((long long)n * KS * KS + ftap) * C + c];
   }
 }
 
@@ -331,14 +331,32 @@ static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int 
 
 constexpr int CV_STAGES = 2;
 
-template <int KS, int BM>
+template <int KS, int BM, bool BT>
 static void launch_fwd(ConvArgs a, hipStream_t stream, ProfScope& prof) {
   constexpr size_t lds = CV_STAGES * (BM + 128) * 128;
-  allow_lds_once<conv_fwd_kernel<KS, CV_STAGES, BM>>(lds);
+  allow_lds_once<conv_fwd_kernel<KS, CV_STAGES, BM, BT>>(lds);
   a.mt_n = (a.P + BM - 1) / BM;
   const int NT = a.N / 128;
   const int grid = ((a.mt_n + 7) / 8) * 8 * NT;
-  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, CV_STAGES, BM>), dim3(grid), dim3(256), lds, stream, a);
+  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, CV_STAGES, BM, BT>), dim3(grid), dim3(256), lds, stream, a);
+}
+
+// tile rows: 128 (two workgroups per CU); 64 when 128-row tiles would leave
+// the chip under-filled (< 1.5 workgroups per CU); 256 rows (one workgroup per
+// CU) measured slower at every C2 shape
+template <bool BT>
+static void launch_fwd_any(const ConvArgs& a, int KS, hipStream_t stream, ProfScope& prof) {
+  int bm = g_conv_bm;
+  if (bm != 64 && bm != 128 && bm != 256) bm = (long long)((a.P + 127) / 128) * (a.N / 128) < 384 ? 64 : 128;
+  if (KS == 3) {
+    if (bm == 256) launch_fwd<3, 256, BT>(a, stream, prof);
+    else if (bm == 64) launch_fwd<3, 64, BT>(a, stream, prof);
+    else launch_fwd<3, 128, BT>(a, stream, prof);
+  } else {
+    if (bm == 256) launch_fwd<1, 256, BT>(a, stream, prof);
+    else if (bm == 64) launch_fwd<1, 64, BT>(a, stream, prof);
+    else launch_fwd<1, 128, BT>(a, stream, prof);
+  }
 }
 
 template <int KS>
@@ -364,32 +382,23 @@ extern "C" int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void
   const double P = a.P;
   ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N) + 2.0 * N * KS * KS * C, false, 0.0,
                  2.0 * P * N * KS * KS * C);
-  // 128-pixel tiles (two workgroups per CU); 64-pixel tiles when 128-pixel
-  // ones would leave the chip under-filled (< 1.5 workgroups per CU); 256
-  // rows (one workgroup per CU) measured slower at every C2 shape
-  int bm = g_conv_bm;
-  if (bm != 64 && bm != 128 && bm != 256) bm = (long long)((a.P + 127) / 128) * (N / 128) < 384 ? 64 : 128;
-  if (KS == 3) {
-    if (bm == 256) launch_fwd<3, 256>(a, stream, prof);
-    else if (bm == 64) launch_fwd<3, 64>(a, stream, prof);
-    else launch_fwd<3, 128>(a, stream, prof);
-  } else {
-    if (bm == 256) launch_fwd<1, 256>(a, stream, prof);
-    else if (bm == 64) launch_fwd<1, 64>(a, stream, prof);
-    else launch_fwd<1, 128>(a, stream, prof);
-  }
+  launch_fwd_any<false>(a, KS, stream, prof);
   return check_launch("rtdetr_conv_fwd");
 }
 
-extern "C" int rtdetr_conv_weight_flip(const void* w, void* wt, int N, int C, int KS, hipStream_t stream) {
-  if (w == nullptr || wt == nullptr || N <= 0 || C <= 0 || (KS != 1 && KS != 3))
-    return fail("rtdetr_conv_weight_flip: bad arguments");
-  const long long total = (long long)N * C * KS * KS;
-  const int grid = (int)std::min<long long>((total + 255) / 256, 4096);
-  ProfScope prof(stream, PROF_CONV, 4.0 * total);
-  MOE_LAUNCH(prof, conv_weight_flip_kernel, dim3(grid), dim3(256), 0, stream, static_cast<const uint16_t*>(w),
-             static_cast<uint16_t*>(wt), N, C, KS);
-  return check_launch("rtdetr_conv_weight_flip");
+extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* dx, const void* zero, int B, int H, int W,
+                                 int C, int N, int KS, hipStream_t stream) {
+  const void* ptrs[4] = {dy, w, dx, zero};
+  if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, "rtdetr_conv_dgrad")) return rc;
+  if (B == 0) return 0;
+  // the forward GEMM over dY [P][N] with the flipped, transposed weight, read in place
+  ConvArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(dx),
+             static_cast<const uint16_t*>(zero), B, H, W, N, C, B * H * W, 0};
+  const double P = a.P;
+  ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N) + 2.0 * N * KS * KS * C, false, 0.0,
+                 2.0 * P * N * KS * KS * C);
+  launch_fwd_any<true>(a, KS, stream, prof);
+  return check_launch("rtdetr_conv_dgrad");
 }
 
 extern "C" int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS) {
@@ -397,10 +406,13 @@ extern "C" int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int K
   // per CU, each slice >= 8 pixel K-tiles
   const long long tiles = (long long)(N / CV_BM) * (KS * KS * C / CV_BN);
   const long long ktot = ((long long)B * H * W + 63) / 64;
-  long long s = (512 + tiles - 1) / std::max(1ll, tiles);  // >= 2 workgroups per CU
-  s = (s + 7) / 8 * 8;                                     // every XCD takes the same number of slices
-  s = std::min(s, std::max(1ll, ktot / 4));                // slices of >= 4 pixel K-tiles
-  s = std::min(s, 128ll);
+  // about 2 workgroups per CU, rounded DOWN to a multiple of 8 slices (every
+  // XCD takes the same number) but at least 8: each extra slice costs a full
+  // fp32 partial of the weight (rounding up measured slower at every shape)
+  long long s = (512 + tiles - 1) / std::max(1ll, tiles);
+  s = std::max(s, 8ll);
+  s = std::min(s, std::max(1ll, ktot / 8));  // slices of >= 8 pixel K-tiles
+  s = std::min(s, 64ll);
   if (s > 8) s = s / 8 * 8;
   return (int)std::max(1ll, s);
 }

@@ -1,5 +1,5 @@
 """Convolutions of the RT-DETR body on libmoe_hip's implicit-GEMM kernels
-(csrc/conv.hip: rtdetr_conv_fwd / rtdetr_conv_weight_flip / rtdetr_conv_wgrad).
+(csrc/conv.hip: rtdetr_conv_fwd / rtdetr_conv_dgrad / rtdetr_conv_wgrad).
 
 ``conv2d(x, weight, stride, padding)`` takes the HIP kernels for the
 convolutions they cover -- stride 1, "same" padding, 1x1 or 3x3, no groups,
@@ -7,9 +7,9 @@ channel counts that are multiples of 128, bf16 channels_last activations and
 weights on the GPU (the HybridEncoder's RepVGG / CSP layers and the ResNet
 bottleneck convolutions of 128 / 256 / 512 / 1024 / 2048 channels) -- and
 F.conv2d (MIOpen) for the rest.  Forward: one implicit-GEMM launch (no im2col
-buffer).  Backward: the data gradient is the same kernel over dY with the
-flipped, channel-transposed weight; the weight gradient is split over pixel
-slices with fp32 partials summed in slice order (deterministic).
+buffer).  Backward: the data gradient is the same kernel over dY reading the
+weight flipped and transposed in place; the weight gradient is split over
+pixel slices with fp32 partials summed in slice order (deterministic).
 MOE_HIP_CONV=0 keeps every convolution on MIOpen (A/B switch).
 """
 from __future__ import annotations
@@ -75,12 +75,9 @@ class _ConvHIP(torch.autograd.Function):
         s = L._stream()
         gx = gw = None
         if ctx.needs_input_grad[0]:
-            wt = torch.empty((C, ks, ks, N), dtype=torch.bfloat16, device=x.device)
-            L._check(L.lib().rtdetr_conv_weight_flip(w.data_ptr(), wt.data_ptr(), N, C, ks, s),
-                     "rtdetr_conv_weight_flip")
             gx = torch.empty((B, C, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
-            L._check(L.lib().rtdetr_conv_fwd(gy.data_ptr(), wt.data_ptr(), gx.data_ptr(), z, B, H, W, N, C, ks, s),
-                     "rtdetr_conv_fwd (data gradient)")
+            L._check(L.lib().rtdetr_conv_dgrad(gy.data_ptr(), w.data_ptr(), gx.data_ptr(), z, B, H, W, C, N, ks, s),
+                     "rtdetr_conv_dgrad")
         if ctx.needs_input_grad[1]:
             ns = L.lib().rtdetr_conv_wgrad_splits(B, H, W, C, N, ks)
             part = torch.empty(ns * N * C * ks * ks, dtype=torch.float32, device=x.device)

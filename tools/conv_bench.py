@@ -83,14 +83,9 @@ def main():
         yh = torch.empty_like(gy)
         t_hf = timeit(lambda: lib.rtdetr_conv_fwd(x.data_ptr(), w.data_ptr(), yh.data_ptr(), z, B, H, W, Ci, Co, ks,
                                                   L._stream()))
-        wt = torch.empty((Ci, ks, ks, Co), dtype=torch.bfloat16, device=dev)
         gx = torch.empty_like(x)
-
-        def dgrad():
-            s = L._stream()  # the capture stream
-            lib.rtdetr_conv_weight_flip(w.data_ptr(), wt.data_ptr(), Co, Ci, ks, s)
-            lib.rtdetr_conv_fwd(gy.data_ptr(), wt.data_ptr(), gx.data_ptr(), z, B, H, W, Co, Ci, ks, s)
-        t_hd = timeit(dgrad)
+        t_hd = timeit(lambda: lib.rtdetr_conv_dgrad(gy.data_ptr(), w.data_ptr(), gx.data_ptr(), z, B, H, W, Ci, Co, ks,
+                                                    L._stream()))
         ns = lib.rtdetr_conv_wgrad_splits(B, H, W, Ci, Co, ks)
         part = torch.empty(ns * Co * Ci * ks * ks, dtype=torch.float32, device=dev)
         gw = torch.empty_like(w)
