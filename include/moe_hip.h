@@ -532,8 +532,11 @@ int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, 
  * zero bytes on the device (read for padding neighbours); pointers 16-B aligned.
  *   rtdetr_conv_fwd         y[B,H,W,N] = conv(x[B,H,W,C], w)   (no im2col buffer)
  *   rtdetr_conv_dgrad       dx[B,H,W,C] = conv^T(dy[B,H,W,N], w): the forward
- *                           GEMM over dy with the flipped, transposed weight
- *                           read in place from w (no transposed copy)
+ *                           GEMM over dy with the flipped, transposed weight,
+ *                           written to work first when
+ *                           rtdetr_conv_dgrad_workspace() > 0 (bytes; large
+ *                           problems), else read in place from w (work may be
+ *                           NULL)
  *   rtdetr_conv_wgrad       dw[N][KS][KS][C] = sum over pixels dy (x) x[neighbour]:
  *                           nsplit pixel slices write fp32 partials to part
  *                           [nsplit][N KS KS C], summed in slice order
@@ -541,13 +544,17 @@ int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, 
  *                           nsplit from rtdetr_conv_wgrad_splits. */
 int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void* zero, int B, int H, int W, int C, int N,
                     int KS, hipStream_t stream);
-int rtdetr_conv_dgrad(const void* dy, const void* w, void* dx, const void* zero, int B, int H, int W, int C, int N,
-                      int KS, hipStream_t stream);
+long long rtdetr_conv_dgrad_workspace(int B, int H, int W, int C, int N, int KS);
+int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void* dx, const void* zero, int B, int H, int W,
+                      int C, int N, int KS, hipStream_t stream);
 int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
                       const void* zero, int B, int H, int W, int C, int N, int KS, hipStream_t stream);
-/* Measurement / A-B knob: "conv_bm" = forward pixel-tile rows (0: by problem
- * size, 64, 128 or 256). */
+/* Measurement / A-B knobs (0, or -1 for conv_dgrad_flip, = automatic):
+ * "conv_bm" forward pixel-tile rows 64 / 128 / 256; "conv_wg_stages"
+ * weight-gradient LDS ring depth 2..4; "conv_wg_splits" weight-gradient pixel
+ * slices returned by rtdetr_conv_wgrad_splits; "conv_dgrad_flip" 1 = always
+ * write the flipped weight, 0 = always read it in place. */
 int rtdetr_conv_set_tuning(const char* key, int value);
 
 /* Training-step optimizer (the bench step's AdamW; reference: Ultralytics'

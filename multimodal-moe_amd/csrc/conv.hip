@@ -13,12 +13,14 @@
 //                      per-row source address (a padding neighbour reads a zero
 //                      row), so no im2col buffer exists.  The data gradient
 //                      is the same GEMM over dY with W'[c][tap][n] =
-//                      W[n][KS^2-1-tap][c], read in place from W as an
-//                      MN-contiguous operand image (template flag BT).
+//                      W[n][KS^2-1-tap][c]: large problems write W' once
+//                      (conv_weight_flip_kernel, K-contiguous image), small
+//                      ones read it in place from W as an MN-contiguous
+//                      operand image (template flag BT; no extra launch).
 //   conv_wgrad_kernel  dW[n, tap, c] = sum_p dY[p, n] X[nbr(p, tap), c]
 //                      GEMM M = Cout, N = KS^2 Cin, K = pixels, split over S
-//                      slices of the pixels (fp32 partials) and summed in slice
-//                      order by conv_wgrad_reduce_kernel (deterministic).
+//                      slices of the pixels (fp32 partials) and summed in a
+//                      fixed order by conv_wgrad_reduce_kernel (deterministic).
 // Tiles 128 x 128 x 64, 4 waves (2 x 2), an S-deep LDS-DMA ring (one
 // global_load_lds_dwordx4 per lane per 1 KiB, counted vmcnt waits, raw
 // s_barrier), K-contiguous operand images (fwd) or MN-contiguous ones read by
@@ -33,7 +35,11 @@ namespace moe {
 
 constexpr int CV_BM = 128, CV_BN = 128;             // weight-gradient tile
 constexpr int CV_TILE = (CV_BM + CV_BN) * 64 * 2;  // bytes of one weight-gradient ring stage
-static int g_conv_bm = 0;  // rtdetr_conv_set_tuning "conv_bm": 0 = by problem size, else 64, 128 or 256 (forward)
+// rtdetr_conv_set_tuning knobs (measurement / A-B; 0 or -1 = automatic)
+static int g_conv_bm = 0;          // "conv_bm": forward tile rows 64, 128 or 256
+static int g_conv_wg_stages = 0;   // "conv_wg_stages": weight-gradient ring depth 2..4
+static int g_conv_wg_splits = 0;   // "conv_wg_splits": weight-gradient pixel slices
+static int g_conv_dgrad_flip = -1; // "conv_dgrad_flip": 1 = always write W', 0 = always read in place
 
 struct ConvArgs {
   const uint16_t* x;     // [B H W, C] (fwd: X; dgrad: dY)
@@ -44,6 +50,22 @@ struct ConvArgs {
   int P;                 // B H W
   int mt_n;              // M tiles
 };
+
+// Wait until K-tile kt's DMA has landed for this wave: up to min(S - 2, newer)
+// younger tiles (GW instructions each) may stay in flight.
+template <int S, int GW>
+__device__ __forceinline__ void wait_ring(int newer) {
+  if constexpr (S >= 4) {
+    if (newer >= 2) wait_vm<2 * GW>();
+    else if (newer == 1) wait_vm<GW>();
+    else wait_vm<0>();
+  } else if constexpr (S == 3) {
+    if (newer >= 1) wait_vm<GW>();
+    else wait_vm<0>();
+  } else {
+    wait_vm<0>();
+  }
+}
 
 __device__ __forceinline__ void dma16(const uint16_t* src, char* lds) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -133,13 +155,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) issue(s);
   for (int kt = 0; kt < nk; ++kt) {
-    const int newer = nk - 1 - kt;
-    if constexpr (S == 2) {
-      wait_vm<0>();
-    } else {
-      if (newer >= 1) wait_vm<GW>();
-      else wait_vm<0>();
-    }
+    wait_ring<S, GW>(nk - 1 - kt);
     __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
     if (kt + S - 1 < nk) issue(kt + S - 1);  // refills the slot consumed in iteration kt - 1
     const char* cur = smem + (kt % S) * TILE;
@@ -174,6 +190,27 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   }
 }
 
+// W'[c][tap][n] = W[n][KS^2-1-tap][c]: the data gradient's K-contiguous
+// weight.  One workgroup transposes a 64 x 64 (n, c) block of one tap through
+// LDS: 128-B row reads along c, 128-B row writes along n.
+__global__ __launch_bounds__(256) void conv_weight_flip_kernel(const uint16_t* __restrict__ w,
+                                                               uint16_t* __restrict__ wt, int N, int C, int KS) {
+  __shared__ uint16_t t[64][66];
+  const int c0 = blockIdx.x * 64, n0 = blockIdx.y * 64, tap = blockIdx.z, T = KS * KS;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int n = ty + 4 * r;
+    t[n][tx] = w[((size_t)(n0 + n) * T + (T - 1 - tap)) * C + c0 + tx];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int c = ty + 4 * r;
+    wt[((size_t)(c0 + c) * T + tap) * N + n0 + tx] = t[tx][c];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // weight gradient
 // ---------------------------------------------------------------------------
@@ -197,14 +234,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
   const int wm = wave >> 1, wn = wave & 1;
   const int NN = KS * KS * a.C;      // GEMM N
   const int MT = a.N / CV_BM, NT = NN / CV_BN;
-  // every tile of one pixel slice on one XCD: the slice's dY and X rows are
-  // read by all its output tiles, so they stream through that XCD's L2 once
-  // (slices of one tile spread over XCDs instead made every XCD read all rows)
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  // work units u = split * tiles + tile, a contiguous run of ceil(units / 8)
+  // per XCD: the tiles of one pixel slice share an XCD (its dY and X rows
+  // stream through that L2 once; slices of one tile spread over XCDs made
+  // every XCD read all rows) and every XCD gets the same number of units
   const int tiles = MT * NT;
-  const int tile = slot % tiles;
-  const int split = (slot / tiles) * 8 + xcd;
-  if (split >= a.nsplit) return;
+  const int units = tiles * a.nsplit, per_xcd = (units + 7) / 8;
+  const int local = blockIdx.x >> 3;
+  const int u = (blockIdx.x & 7) * per_xcd + local;
+  if (local >= per_xcd || u >= units) return;
+  const int tile = u % tiles, split = u / tiles;
   const int mt = tile % MT, nt = tile / MT;
   const int m0 = mt * CV_BM, nn0 = nt * CV_BN;
   const int tap = nn0 / a.C, c0 = nn0 - tap * a.C;
@@ -261,13 +300,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) issue(s);
   for (int kt = 0; kt < nk; ++kt) {
-    const int newer = nk - 1 - kt;
-    if constexpr (S == 2) {
-      wait_vm<0>();
-    } else {
-      if (newer >= 1) wait_vm<GW>();
-      else wait_vm<0>();
-    }
+    wait_ring<S, GW>(nk - 1 - kt);
     __builtin_amdgcn_s_barrier();
     if (kt + S - 1 < nk) issue(kt + S - 1);
     const char* cur = smem + (kt % S) * CV_TILE;
@@ -285,14 +318,31 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
   }
 }
 
-// dW = sum over slices in slice order (fp32), written as bf16 or fp32
+// dW = sum of the slices' fp32 partials in a fixed order, written as bf16 or
+// fp32.  A workgroup owns 64 float4 columns; its 4 waves sum the slices
+// k = wave (mod 4) in increasing k, then wave 0 adds the 4 sums in wave order
+// (so a weight with few output tiles still spreads over the whole chip).
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part, int nsplit,
                                                                 long long n, void* __restrict__ dw, int out_bf16) {
-  const long long i = (blockIdx.x * 256ll + threadIdx.x) * 4;
-  if (i >= n) return;
-  float4 s = *reinterpret_cast<const float4*>(part + i);
-  for (int k = 1; k < nsplit; ++k) {
-    const float4 v = *reinterpret_cast<const float4*>(part + (size_t)k * n + i);
+  __shared__ float4 red[3][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long i = (blockIdx.x * 64ll + lane) * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n) {
+    for (int k = wave; k < nsplit; k += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)k * n + i);
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+  }
+  if (wave) red[wave - 1][lane] = s;
+  __syncthreads();
+  if (wave || i >= n) return;
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    const float4 v = red[g][lane];
     s.x += v.x;
     s.y += v.y;
     s.z += v.z;
@@ -359,13 +409,24 @@ static void launch_fwd_any(const ConvArgs& a, int KS, hipStream_t stream, ProfSc
   }
 }
 
+template <int KS, int S>
+static void launch_wgrad_s(const ConvWgArgs& a, hipStream_t stream, ProfScope& prof) {
+  constexpr size_t lds = S * CV_TILE;
+  allow_lds_once<conv_wgrad_kernel<KS, S>>(lds);
+  const int tiles = (a.N / CV_BM) * (KS * KS * a.C / CV_BN);
+  const int grid = (tiles * a.nsplit + 7) / 8 * 8;
+  MOE_LAUNCH(prof, (conv_wgrad_kernel<KS, S>), dim3(grid), dim3(256), lds, stream, a);
+}
+
+// 2-deep ring (64 KiB, two workgroups per CU): deeper rings (1 per CU)
+// measured no faster where the grid fits one round and up to 2x slower where
+// it does not
 template <int KS>
 static void launch_wgrad(const ConvWgArgs& a, hipStream_t stream, ProfScope& prof) {
-  constexpr size_t lds = CV_STAGES * CV_TILE;
-  allow_lds_once<conv_wgrad_kernel<KS, CV_STAGES>>(lds);
-  const int tiles = (a.N / CV_BM) * (KS * KS * a.C / CV_BN);
-  const int grid = tiles * ((a.nsplit + 7) / 8) * 8;
-  MOE_LAUNCH(prof, (conv_wgrad_kernel<KS, CV_STAGES>), dim3(grid), dim3(256), lds, stream, a);
+  const int s = g_conv_wg_stages >= 2 && g_conv_wg_stages <= 4 ? g_conv_wg_stages : 2;
+  if (s == 2) launch_wgrad_s<KS, 2>(a, stream, prof);
+  else if (s == 3) launch_wgrad_s<KS, 3>(a, stream, prof);
+  else launch_wgrad_s<KS, 4>(a, stream, prof);
 }
 
 }  // namespace moe
@@ -386,34 +447,57 @@ extern "C" int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void
   return check_launch("rtdetr_conv_fwd");
 }
 
-extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* dx, const void* zero, int B, int H, int W,
-                                 int C, int N, int KS, hipStream_t stream) {
+extern "C" long long rtdetr_conv_dgrad_workspace(int B, int H, int W, int C, int N, int KS) {
+  // writing W' costs a launch (~2-3 us in a graph) plus 4 B per weight and
+  // buys the K-contiguous operand image, up to ~10 % faster than reading W in
+  // place (MN-contiguous): measured to pay from ~64 Ki pixels, or from
+  // ~25 GFLOP for 3x3 (tools/conv_bench.py conv_dgrad_flip=0/1)
+  const double P = (double)B * H * W;
+  bool flip = P >= 65536 || (KS == 3 && 2.0 * P * N * KS * KS * C >= 2.5e10);
+  if (g_conv_dgrad_flip == 0 || g_conv_dgrad_flip == 1) flip = g_conv_dgrad_flip == 1;
+  return flip ? 2ll * N * KS * KS * C : 0;
+}
+
+extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void* dx, const void* zero, int B, int H,
+                                 int W, int C, int N, int KS, hipStream_t stream) {
   const void* ptrs[4] = {dy, w, dx, zero};
   if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, "rtdetr_conv_dgrad")) return rc;
+  const bool flip = rtdetr_conv_dgrad_workspace(B, H, W, C, N, KS) > 0;
+  if (flip && (work == nullptr || reinterpret_cast<uintptr_t>(work) % 16))
+    return fail("rtdetr_conv_dgrad: this shape needs a 16-B aligned workspace of rtdetr_conv_dgrad_workspace() bytes");
   if (B == 0) return 0;
-  // the forward GEMM over dY [P][N] with the flipped, transposed weight, read in place
+  // the forward GEMM over dY [P][N] with W'
   ConvArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(dx),
              static_cast<const uint16_t*>(zero), B, H, W, N, C, B * H * W, 0};
   const double P = a.P;
+  if (flip) {
+    const long long total = (long long)N * C * KS * KS;
+    {
+      ProfScope prof(stream, PROF_CONV, 4.0 * total);
+      MOE_LAUNCH(prof, conv_weight_flip_kernel, dim3(C / 64, N / 64, KS * KS), dim3(256), 0, stream,
+                 static_cast<const uint16_t*>(w), static_cast<uint16_t*>(work), N, C, KS);
+      if (int rc = check_launch("rtdetr_conv_dgrad (flip)")) return rc;
+    }
+    a.w = static_cast<const uint16_t*>(work);
+  }
   ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N) + 2.0 * N * KS * KS * C, false, 0.0,
                  2.0 * P * N * KS * KS * C);
-  launch_fwd_any<true>(a, KS, stream, prof);
+  if (flip) launch_fwd_any<false>(a, KS, stream, prof);
+  else launch_fwd_any<true>(a, KS, stream, prof);
   return check_launch("rtdetr_conv_dgrad");
 }
 
 extern "C" int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS) {
-  // a multiple of 8 slices (one set per XCD) so that the grid is ~2 workgroups
-  // per CU, each slice >= 8 pixel K-tiles
+  // as many pixel slices as keep tiles x slices <= 512 (every workgroup
+  // resident at once, two per CU: a second round on a few CUs doubles the
+  // time), each slice >= 8 pixel K-tiles, <= 64 (each slice costs an fp32
+  // partial of the weight)
   const long long tiles = (long long)(N / CV_BM) * (KS * KS * C / CV_BN);
   const long long ktot = ((long long)B * H * W + 63) / 64;
-  // about 2 workgroups per CU, rounded DOWN to a multiple of 8 slices (every
-  // XCD takes the same number) but at least 8: each extra slice costs a full
-  // fp32 partial of the weight (rounding up measured slower at every shape)
-  long long s = (512 + tiles - 1) / std::max(1ll, tiles);
-  s = std::max(s, 8ll);
-  s = std::min(s, std::max(1ll, ktot / 8));  // slices of >= 8 pixel K-tiles
+  long long s = 512 / std::max(1ll, tiles);
+  s = std::min(s, std::max(1ll, ktot / 8));
   s = std::min(s, 64ll);
-  if (s > 8) s = s / 8 * 8;
+  if (g_conv_wg_splits > 0) s = std::min<long long>(g_conv_wg_splits, std::max(1ll, ktot));
   return (int)std::max(1ll, s);
 }
 
@@ -435,7 +519,7 @@ extern "C" int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int
     if (int rc = check_launch("rtdetr_conv_wgrad")) return rc;
   }
   ProfScope prof(stream, PROF_CONV, 4.0 * nsplit * nw + (out_bf16 ? 2.0 : 4.0) * nw);
-  MOE_LAUNCH(prof, conv_wgrad_reduce_kernel, dim3((unsigned)((nw / 4 + 255) / 256)), dim3(256), 0, stream, part,
+  MOE_LAUNCH(prof, conv_wgrad_reduce_kernel, dim3((unsigned)((nw / 4 + 63) / 64)), dim3(256), 0, stream, part,
              nsplit, nw, dw, out_bf16);
   return check_launch("rtdetr_conv_wgrad (reduce)");
 }
@@ -444,6 +528,18 @@ extern "C" int rtdetr_conv_set_tuning(const char* key, int value) {
   if (key == nullptr) return fail("rtdetr_conv_set_tuning: key is NULL");
   if (std::string(key) == "conv_bm") {
     g_conv_bm = value;
+    return 0;
+  }
+  if (std::string(key) == "conv_wg_stages") {
+    g_conv_wg_stages = value;
+    return 0;
+  }
+  if (std::string(key) == "conv_wg_splits") {
+    g_conv_wg_splits = value;
+    return 0;
+  }
+  if (std::string(key) == "conv_dgrad_flip") {
+    g_conv_dgrad_flip = value;
     return 0;
   }
   return fail(std::string("rtdetr_conv_set_tuning: unknown key ") + key);

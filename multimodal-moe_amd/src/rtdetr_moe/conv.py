@@ -7,9 +7,10 @@ channel counts that are multiples of 128, bf16 channels_last activations and
 weights on the GPU (the HybridEncoder's RepVGG / CSP layers and the ResNet
 bottleneck convolutions of 128 / 256 / 512 / 1024 / 2048 channels) -- and
 F.conv2d (MIOpen) for the rest.  Forward: one implicit-GEMM launch (no im2col
-buffer).  Backward: the data gradient is the same kernel over dY reading the
-weight flipped and transposed in place; the weight gradient is split over
-pixel slices with fp32 partials summed in slice order (deterministic).
+buffer).  Backward: the data gradient is the same kernel over dY with the
+weight flipped and transposed (written to a workspace for large problems,
+read in place for small ones); the weight gradient is split over pixel slices
+with fp32 partials summed in a fixed order (deterministic).
 MOE_HIP_CONV=0 keeps every convolution on MIOpen (A/B switch).
 """
 from __future__ import annotations
@@ -76,8 +77,10 @@ class _ConvHIP(torch.autograd.Function):
         gx = gw = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty((B, C, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
-            L._check(L.lib().rtdetr_conv_dgrad(gy.data_ptr(), w.data_ptr(), gx.data_ptr(), z, B, H, W, C, N, ks, s),
-                     "rtdetr_conv_dgrad")
+            nb = L.lib().rtdetr_conv_dgrad_workspace(B, H, W, C, N, ks)
+            work = torch.empty(nb // 2, dtype=torch.bfloat16, device=x.device) if nb > 0 else None
+            L._check(L.lib().rtdetr_conv_dgrad(gy.data_ptr(), w.data_ptr(), None if work is None else work.data_ptr(),
+                                               gx.data_ptr(), z, B, H, W, C, N, ks, s), "rtdetr_conv_dgrad")
         if ctx.needs_input_grad[1]:
             ns = L.lib().rtdetr_conv_wgrad_splits(B, H, W, C, N, ks)
             part = torch.empty(ns * N * C * ks * ks, dtype=torch.float32, device=x.device)

@@ -3,8 +3,11 @@ reference of the same op (F.conv2d on the same bf16 operands, upcast):
 forward, data gradient and weight gradient, 1x1 and 3x3, stride 1 with
 "same" padding, NHWC bf16.
 
-Forward tiles of 64, 128 and 256 pixels (rtdetr_conv_set_tuning "conv_bm") and the
-automatic choice.  Shapes: the C2 encoder's RepVGG convolutions (256 -> 256 at 23x40, batch 8),
+Forward tiles of 64, 128 and 256 pixels (rtdetr_conv_set_tuning "conv_bm"),
+weight-gradient rings of 2, 3 and 4 stages ("conv_wg_stages"), 1 / 3 /
+automatic pixel slices ("conv_wg_splits"), the data gradient with the weight
+flipped into a workspace and read in place ("conv_dgrad_flip"), and the
+automatic choices.  Shapes: the C2 encoder's RepVGG convolutions (256 -> 256 at 23x40, batch 8),
 a ResNet bottleneck shape (128 channels), channel-asymmetric layers
 (512 -> 128, 128 -> 256), odd spatial sizes (7 x 9: the partial 128-pixel
 tile and every padding case) and a single image.
@@ -32,17 +35,31 @@ def _check(got, ref, what):
     assert rel <= 1e-2, f"{what}: relative Frobenius {rel:.3e}"
 
 
-@pytest.mark.parametrize("bm", [0, 64, 128, 256], ids=["bm_auto", "bm64", "bm128", "bm256"])
+_KNOBS = {"auto": {}, "bm64_wg2_flip": dict(conv_bm=64, conv_wg_stages=2, conv_dgrad_flip=1),
+          "bm128_wg3_inplace": dict(conv_bm=128, conv_wg_stages=3, conv_dgrad_flip=0, conv_wg_splits=3),
+          "bm256_wg4_flip": dict(conv_bm=256, conv_wg_stages=4, conv_dgrad_flip=1, conv_wg_splits=1)}
+_DEFAULTS = dict(conv_bm=0, conv_wg_stages=0, conv_dgrad_flip=-1, conv_wg_splits=0)
+
+
+@pytest.mark.parametrize("knobs", list(_KNOBS))
 @pytest.mark.parametrize("B,C,N,H,W,ks", [(8, 256, 256, 23, 40, 3), (8, 256, 256, 23, 40, 1), (2, 128, 128, 46, 80, 3),
                                           (2, 512, 128, 7, 9, 1), (2, 128, 256, 7, 9, 3), (1, 256, 512, 5, 3, 3)])
-def test_conv_fwd_bwd_vs_fp32(hip_lib, B, C, N, H, W, ks, bm):
-    from src.rtdetr_moe.conv import _ConvHIP, hip_conv_ok
-
-    assert hip_lib.rtdetr_conv_set_tuning(b"conv_bm", bm) == 0
+def test_conv_fwd_bwd_vs_fp32(hip_lib, B, C, N, H, W, ks, knobs):
+    for k, v in _KNOBS[knobs].items():
+        assert hip_lib.rtdetr_conv_set_tuning(k.encode(), v) == 0
     try:
         _conv_case(B, C, N, H, W, ks)
     finally:
-        hip_lib.rtdetr_conv_set_tuning(b"conv_bm", 0)
+        for k, v in _DEFAULTS.items():
+            hip_lib.rtdetr_conv_set_tuning(k.encode(), v)
+
+
+def test_conv_large_auto_paths(hip_lib):
+    """A stride-8 encoder shape: the automatic choices there (flipped-weight
+    data gradient, a non-multiple-of-8 slice count) against fp32."""
+    assert hip_lib.rtdetr_conv_dgrad_workspace(8, 92, 160, 256, 256, 3) > 0
+    assert hip_lib.rtdetr_conv_dgrad_workspace(8, 23, 40, 256, 256, 3) == 0
+    _conv_case(4, 256, 256, 92, 160, 3)
 
 
 def _conv_case(B, C, N, H, W, ks):

@@ -84,15 +84,17 @@ def main():
         t_hf = timeit(lambda: lib.rtdetr_conv_fwd(x.data_ptr(), w.data_ptr(), yh.data_ptr(), z, B, H, W, Ci, Co, ks,
                                                   L._stream()))
         gx = torch.empty_like(x)
-        t_hd = timeit(lambda: lib.rtdetr_conv_dgrad(gy.data_ptr(), w.data_ptr(), gx.data_ptr(), z, B, H, W, Ci, Co, ks,
-                                                    L._stream()))
+        nb = lib.rtdetr_conv_dgrad_workspace(B, H, W, Ci, Co, ks)
+        wk = torch.empty(max(nb // 2, 8), dtype=torch.bfloat16, device=dev)
+        t_hd = timeit(lambda: lib.rtdetr_conv_dgrad(gy.data_ptr(), w.data_ptr(), wk.data_ptr(), gx.data_ptr(), z, B, H,
+                                                    W, Ci, Co, ks, L._stream()))
         ns = lib.rtdetr_conv_wgrad_splits(B, H, W, Ci, Co, ks)
         part = torch.empty(ns * Co * Ci * ks * ks, dtype=torch.float32, device=dev)
         gw = torch.empty_like(w)
         t_hw = timeit(lambda: lib.rtdetr_conv_wgrad(gy.data_ptr(), x.data_ptr(), part.data_ptr(), ns, gw.data_ptr(), 1,
                                                     z, B, H, W, Ci, Co, ks, L._stream()))
         tf = lambda t: round(flop / t / 1e6, 1)  # noqa: E731  TFLOP/s
-        print(json.dumps({"shape": [B, Ci, Co, H, W, ks], "gflop": round(flop / 1e9, 2), "wgrad_splits": ns,
+        print(json.dumps({"shape": [B, Ci, Co, H, W, ks], "gflop": round(flop / 1e9, 2), "wgrad_splits": ns, "dgrad_flip": nb > 0,
                           "miopen_us": [round(t_mf, 1), round(t_md, 1), round(t_mw, 1)],
                           "hip_us": [round(t_hf, 1), round(t_hd, 1), round(t_hw, 1)],
                           "miopen_tflops": [tf(t_mf), tf(t_md), tf(t_mw)], "hip_tflops": [tf(t_hf), tf(t_hd), tf(t_hw)]}),
