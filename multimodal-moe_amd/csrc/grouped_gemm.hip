@@ -27,6 +27,7 @@
 //      S-deep ring with S-1 K-tiles in flight, counted `s_waitcnt vmcnt` +
 //      raw s_barrier (no vmcnt(0) drain inside the loop).
 #include <algorithm>
+#include <type_traits>
 
 #include "mfma_lds.h"
 #include "moe_common.h"
@@ -102,6 +103,8 @@ static int g_wgrad_bm = 0;  // 0 = by tile count, else 64 or 128
 static int g_xcd_map = 0;   // 0 = default (contiguous chunks), 1 = round-robin, 2 = contiguous chunks
 static int g_ksplit = 0;    // 0 = per-shape choice, else forced split-K factor (1 = off)
 static int g_gemm_pair_off = 0;  // 1: moe_grouped_gemm_bwd_pair issues two launches (A/B)
+static int g_wgrad_dma = 0;      // gathered WGRAD: 0 = default (LDS-DMA ring), 1 = register-staged (A/B)
+static int g_wgrad_stages = 0;   // gathered WGRAD LDS-DMA ring depth: 0 = default (2), else 2 or 3
 
 // split-K workspace registered per device by the caller (moe_set_splitk_workspace)
 struct SplitWs {
@@ -1026,6 +1029,51 @@ __device__ __forceinline__ void dma_tile_rows(const uint16_t* const (&rowp)[R / 
   }
 }
 
+// The same for an MN-contiguous [64][R] tile whose k-rows are gathered: k-row
+// kr is row idx[kr] of `base` (the K-tile's 64 row indices, staged in LDS).
+template <int R>
+__device__ __forceinline__ void dma_tile_krows(const uint16_t* base, int ld, const int32_t* idx, char* lds, int wave,
+                                               int lane) {
+  constexpr int cpr = R / 8, rows_per = 64 / cpr;
+#pragma unroll
+  for (int j = 0; j < R / 32; ++j) {
+    const int ins = wave + 4 * j;
+    const int kr = ins * rows_per + lane / cpr;
+    const int c = (lane % cpr) ^ mimg_swz<R>(kr);
+    const uint16_t* src = base + (size_t)idx[kr] * ld + c * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + ins * 1024), 16, 0, 0);
+  }
+}
+
+// 64 dwords of a K-tile's k-row metadata (row indices or scales) by LDS-DMA:
+// every wave moves 16 of them (one instruction, lanes 0..15), so the four
+// waves' vmcnt counts stay equal.  Rows past `last` read row `last`.
+__device__ __forceinline__ void dma_meta64(const void* src, int row, int last, char* lds, int wave, int lane) {
+  const int r = min(row + wave * 16 + lane, last);
+  if (lane < 16)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(
+                                         static_cast<const int32_t*>(src) + r),
+                                     (__attribute__((address_space(3))) void*)(lds + wave * 64), 4, 0, 0);
+}
+
+// Wait until ring tile kt (and what was issued with it) has landed for this
+// wave: at most min(S - 2, newer) younger issues of PER instructions each may
+// stay in flight.
+template <int S, int PER>
+__device__ __forceinline__ void wait_issue(int newer) {
+  if constexpr (S == 2) {
+    wait_vm<0>();
+  } else if constexpr (S >= 4) {
+    if (newer >= 2) wait_vm<2 * PER>();
+    else if (newer == 1) wait_vm<PER>();
+    else wait_vm<0>();
+  } else {
+    if (newer >= 1) wait_vm<PER>();
+    else wait_vm<0>();
+  }
+}
+
 template <int BM, int BN, int S, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>
 __device__ __forceinline__ void gemm_v2_body(const GemmParams& p, int bid, char* smem) {
   constexpr int A_BYTES = BM * 64 * 2;
@@ -1070,12 +1118,50 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p, int bid, char*
     }
   }
 
+  // WGRAD with gathered k-rows (one operand): k-row r of X is
+  // bf16(x_scale[r] * x[x_gather[r]]) or k-row r of Y is y[b_gather[r]].  The
+  // 64 row indices of K-tile j are DMA'd into an index ring (2S slots, behind
+  // the stage ring: a wave that runs ahead never overwrites indices another
+  // wave is still reading) by issue(j - S + 1), so the K-tile's own DMA reads
+  // them from LDS with no dependent global round trip; its scales travel with
+  // it (one slot per stage) and are applied to the landed X image in LDS.
+  constexpr bool WGG = MODE == MODE_WGRAD && !A_K && !B_K && !(FL & (FL_MX | FL_Y8));
+  const int gop = !WGG ? 0 : (p.x_gather != nullptr ? 1 : (p.b_gather != nullptr ? 2 : 0));  // gathered operand
+  const bool gscale = gop == 1 && p.x_scale != nullptr;
+  char* s_idx = smem + S * BUF;          // [2S][64] int32 row indices
+  char* s_scl = s_idx + 2 * S * 256;     // [S][64] fp32 scales (X gather)
+  const int32_t* gidx = gop == 1 ? p.x_gather : p.b_gather;
+  const int g_last = t.row0 + t.rows_g - 1;
+  if (WGG && gop && t.nk > 0) {
+    // prologue: indices of K-tiles 0 .. S-2 (plain loads; nothing is in flight yet)
+    for (int i = tid; i < (S - 1) * 64; i += 256)
+      reinterpret_cast<int32_t*>(s_idx)[i] = gidx[min(t.row0 + i, g_last)];
+    __syncthreads();
+  }
+
   const int nk = (p.dbg & 2) ? 0 : t.nk;
   auto issue = [&](int kt) {
     char* buf = smem + (kt % S) * BUF;
     const int klim = MODE == MODE_ROWS ? 64 : t.rows_g - kt * 64;
     const uint16_t* ap = A_K ? t.a_base + kt * 64 : t.a_base + (size_t)kt * 64 * p.lda;
     const uint16_t* bp = B_K ? t.b_base + kt * 64 : t.b_base + (size_t)kt * 64 * p.ldb;
+    if constexpr (WGG) {
+      if (gop) {
+        const int32_t* idx = reinterpret_cast<const int32_t*>(s_idx + (kt % (2 * S)) * 256);
+        if (gop == 1) {
+          dma_tile_krows<BM>(p.a + t.m0, p.lda, idx, buf, wave, lane);
+          dma_tile<BN, false>(bp, p.ldb, BN, klim, buf + A_BYTES, wave, lane);
+        } else {
+          dma_tile<BM, false>(ap, p.lda, BM, klim, buf, wave, lane);
+          dma_tile_krows<BN>(p.b + t.n0, p.ldb, idx, buf + A_BYTES, wave, lane);
+        }
+        // the indices of K-tile kt + S - 1 (issued even past the last tile:
+        // every issue moves the same number of instructions), then the scales
+        dma_meta64(gidx, t.row0 + (kt + S - 1) * 64, g_last, s_idx + ((kt + S - 1) % (2 * S)) * 256, wave, lane);
+        if (gscale) dma_meta64(p.x_scale, t.row0 + kt * 64, g_last, s_scl + (kt % S) * 256, wave, lane);
+        return;
+      }
+    }
     if constexpr (GATHER_OK) {
       if (gather) dma_tile_rows<BM>(rowp, sw, kt * 64, buf, wave, lane);
       else dma_tile<BM, A_K>(ap, p.lda, t.a_row_lim, klim, buf, wave, lane);
@@ -1113,19 +1199,34 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p, int bid, char*
 
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt has landed for this wave once at most min(S-2, nk-1-kt) newer tiles are pending
+    // (a gathered WGRAD issue also moves the next indices and the scales: 1 or 2 more)
     const int newer = nk - 1 - kt;
-    if constexpr (S == 2) {
-      wait_vm<0>();  // tile kt+1 is issued after this wait
-    } else if constexpr (S >= 4) {
-      if (newer >= 2) wait_vm<2 * GW>();
-      else if (newer == 1) wait_vm<GW>();
-      else wait_vm<0>();
+    if (WGG && gop) {
+      if (gscale) wait_issue<S, GW + 2>(newer);
+      else wait_issue<S, GW + 1>(newer);
     } else {
-      if (newer >= 1) wait_vm<GW>();
-      else wait_vm<0>();
+      wait_issue<S, GW>(newer);
     }
     __builtin_amdgcn_s_barrier();  // every wave's DMA for tile kt is visible
     char* cur = smem + (kt % S) * BUF;
+    if constexpr (WGG) {
+      if (gscale) {  // X k-rows *= their gate, bf16 RNE (the rows past the group are zeroed below)
+        const int kvalid = min(64, t.rows_g - kt * 64);
+        const float* sc = reinterpret_cast<const float*>(s_scl + (kt % S) * 256);
+        for (int q = tid; q < 64 * (BM / 8); q += 256) {
+          const int kr = q / (BM / 8);
+          if (kr >= kvalid) continue;
+          uint4* ch = reinterpret_cast<uint4*>(cur + kr * (BM * 2) + (q % (BM / 8)) * 16);
+          float f[8];
+          unpack8(*ch, f);
+          const float sv = sc[kr];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] *= sv;
+          *ch = pack8(f);
+        }
+        __syncthreads();
+      }
+    }
     if constexpr (MODE == MODE_WGRAD) {
       const int kvalid = t.rows_g - kt * 64;
       if (kvalid < 64) {  // tail: zero the clamped k-rows of both operands
@@ -1144,6 +1245,8 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p, int bid, char*
     else compute_tile<BM, BN, A_K, B_K, COLSUM>(cur, cur + A_BYTES, acc, csum, lane, wm, wn);
   }
   static_assert(S * (BM + BN) * 64 * 2 >= BM * BN * (MODE == MODE_ROWS ? 2 : 4), "epilogue image exceeds LDS");
+  (void)gidx;
+  (void)g_last;
   if (t.nsplit > 1 && !splitk_merge<TM, TN, COLSUM>(p, t.tile_id, t.split, acc, csum, tid)) return;
   epilogue_lds<BM, BN, MODE, EPI, COLSUM, FL>(p, t.g, t.row0, t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, smem,
                                               tid, lane, wm, wn);
@@ -1201,23 +1304,25 @@ template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, in
 static void launch(const GemmParams& p, dim3 grid, hipStream_t s, const ProfScope& prof, int variant, int stages) {
   // MX: the exponent stage behind the ring ((BM + BN) rows x K/32 bytes)
   const size_t xs = (FL & FL_MX) ? (size_t)(BM + BN) * p.ksb : 0;
+  // (the index / scale rings of a gathered v2 WGRAD: 768 B per stage, added per branch below)
+  const size_t gx = (MODE == MODE_WGRAD && (p.x_gather != nullptr || p.b_gather != nullptr)) ? 768 : 0;
   if (variant == 1 && !(FL & (FL_MX | FL_CQ | FL_AUX8))) {
     constexpr size_t lds = 2 * (BM + BN) * 64 * 2;
     constexpr auto fn = gemm_v1_kernel<BM, BN, A_K, B_K, MODE, EPI, COLSUM, FL & FL_Y8>;
     allow_lds<fn>(lds);
     MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
   } else if (stages == 2) {
-    const size_t lds = 2 * (BM + BN) * 64 * 2 + xs;
+    const size_t lds = 2 * (BM + BN) * 64 * 2 + xs + 2 * gx;
     constexpr auto fn = gemm_v2_kernel<BM, BN, 2, A_K, B_K, MODE, EPI, COLSUM, FL & ~FL_Y8>;
     allow_lds<fn>(lds);
     MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
   } else if (stages >= 4) {
-    const size_t lds = 4 * (BM + BN) * 64 * 2 + xs;
+    const size_t lds = 4 * (BM + BN) * 64 * 2 + xs + 4 * gx;
     constexpr auto fn = gemm_v2_kernel<BM, BN, 4, A_K, B_K, MODE, EPI, COLSUM, FL & ~FL_Y8>;
     allow_lds<fn>(lds);
     MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
   } else {
-    const size_t lds = 3 * (BM + BN) * 64 * 2 + xs;
+    const size_t lds = 3 * (BM + BN) * 64 * 2 + xs + 3 * gx;
     constexpr auto fn = gemm_v2_kernel<BM, BN, 3, A_K, B_K, MODE, EPI, COLSUM, FL & ~FL_Y8>;
     allow_lds<fn>(lds);
     MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
@@ -1378,13 +1483,16 @@ static int plan_wgrad(WgradPlan& pl, const void* x, const void* y, void* c, void
   p.K = 0;
   pl.colsum = colsum != nullptr;
   const int ntn = N / 128;
-  // 64-row tiles, register-staged double buffer (its global_load_dwordx4 path
-  // streams these k-row gathers faster than LDS-DMA)
+  // 64-row tiles.  Gathered k-rows (one operand): the LDS-DMA ring with the
+  // row indices staged in LDS ahead of the tiles (gemm_v2_body); both
+  // operands gathered, or wgrad_dma = 1: the register-staged double buffer
   const bool gath = b_gather != nullptr || x_gather != nullptr;
+  const bool both = b_gather != nullptr && x_gather != nullptr;
   const bool big = M % 128 == 0 && g_wgrad_bm == 128 && !gath;
   pl.bm = big ? 128 : 64;
-  pl.variant = (g_gemm_variant && !gath) ? g_gemm_variant : 1;  // the k-row gathers are in the register path
-  pl.stages = g_gemm_stages ? g_gemm_stages : 2;
+  if (gath) pl.variant = (!both && g_wgrad_dma != 1) ? 2 : 1;
+  else pl.variant = g_gemm_variant ? g_gemm_variant : 1;
+  pl.stages = gath ? (g_wgrad_stages ? g_wgrad_stages : 2) : (g_gemm_stages ? g_gemm_stages : 2);
   int gpad = G >= 8 ? (G + 7) / 8 * 8 : G;
   // split-K over each group's rows: the output (G M N) is too small a grid to
   // fill the chip with K = the whole group; only for long groups: rows_hint / G
@@ -1463,36 +1571,46 @@ static void launch_wgrad(const WgradPlan& pl, hipStream_t s, const ProfScope& pr
 // tile) and each runs the group's whole K loop; dispatched ahead of the
 // dgrad's many short workgroups they overlap them instead of trailing them
 // (kbench: the reverse order ran the two back to back inside the launch).
-template <int S, int EPI, int FLR, int FLW>
+// SW: the weight gradient's body -- 0 = register-staged (v1), 2 / 3 = the
+// LDS-DMA ring of that depth (gathered k-rows, gemm_v2_body).
+template <int S, int SW, int EPI, int FLR, int FLW>
 static void launch_pair_k(const RowsPlan& r, const WgradPlan& w, hipStream_t s, const ProfScope& prof) {
   using R = BodyV2<64, 128, S, true, false, MODE_ROWS, EPI, false, FLR>;
-  using W = BodyV1<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true, FLW>;
+  using W = std::conditional_t<SW == 0, BodyV1<64, 128, false, false, MODE_WGRAD, MOE_EPI_NONE, true, FLW>,
+                               BodyV2<64, 128, (SW ? SW : 2), false, false, MODE_WGRAD, MOE_EPI_NONE, true, FLW>>;
   constexpr auto fn = gemm_pair_kernel<W, R>;
   const size_t lds_r = (size_t)S * (64 + 128) * 64 * 2;
-  const size_t lds_w = 2 * (64 + 128) * 64 * 2;
+  const size_t lds_w = SW == 0 ? 2 * (64 + 128) * 64 * 2 : (size_t)SW * ((64 + 128) * 64 * 2 + 768);
   const size_t lds = lds_r > lds_w ? lds_r : lds_w;
   allow_lds<fn>(lds);
   MOE_LAUNCH(prof, fn, dim3(r.grid + w.grid), dim3(256), lds, s, w.p, r.p, (int)w.grid);
 }
 static bool pair_ok(const RowsPlan& r, const WgradPlan& w) {
   return r.bm == 64 && !r.trans_b && r.variant == 2 && (r.stages == 2 || r.stages == 3) && w.grid % 8 == 0 &&
-         w.bm == 64 && w.variant == 1 && w.colsum &&
+         w.bm == 64 && (w.variant == 1 || (w.variant == 2 && (w.stages == 2 || w.stages == 3))) && w.colsum &&
          (r.epi == MOE_EPI_NONE || r.epi == MOE_EPI_RELU_MASK || r.epi == MOE_EPI_RELU_MASK_MX);
 }
-template <int FLW>
-static void launch_pair(const RowsPlan& r, const WgradPlan& w, hipStream_t s, const ProfScope& prof) {
-#define GG_PAIR(S_)                                                                     \
-  switch (r.epi) {                                                                       \
-    case MOE_EPI_NONE: launch_pair_k<S_, MOE_EPI_NONE, 0, FLW>(r, w, s, prof); break;    \
-    case MOE_EPI_RELU_MASK: launch_pair_k<S_, MOE_EPI_RELU_MASK, 0, FLW>(r, w, s, prof); break; \
-    default: launch_pair_k<S_, MOE_EPI_RELU_MASK, FL_AUX8, FLW>(r, w, s, prof); break;   \
+template <int S, int FLW>
+static void launch_pair_s(const RowsPlan& r, const WgradPlan& w, hipStream_t s, const ProfScope& prof) {
+#define GG_PAIR(SW_)                                                                          \
+  switch (r.epi) {                                                                             \
+    case MOE_EPI_NONE: launch_pair_k<S, SW_, MOE_EPI_NONE, 0, FLW>(r, w, s, prof); break;       \
+    case MOE_EPI_RELU_MASK: launch_pair_k<S, SW_, MOE_EPI_RELU_MASK, 0, FLW>(r, w, s, prof); break; \
+    default: launch_pair_k<S, SW_, MOE_EPI_RELU_MASK, FL_AUX8, FLW>(r, w, s, prof); break;      \
   }
-  if (r.stages == 3) {
+  if (w.variant == 1) {
+    GG_PAIR(0)
+  } else if (w.stages == 3) {
     GG_PAIR(3)
   } else {
     GG_PAIR(2)
   }
 #undef GG_PAIR
+}
+template <int FLW>
+static void launch_pair(const RowsPlan& r, const WgradPlan& w, hipStream_t s, const ProfScope& prof) {
+  if (r.stages == 3) launch_pair_s<3, FLW>(r, w, s, prof);
+  else launch_pair_s<2, FLW>(r, w, s, prof);
 }
 
 }  // namespace moe
@@ -1523,6 +1641,8 @@ extern "C" int moe_set_tuning(const char* key, int value) {
   if (k == "xcd_map" && value >= 0 && value <= 2) { g_xcd_map = value; return 0; }
   if (k == "ksplit" && value >= 0 && value <= 8) { g_ksplit = value; return 0; }
   if (k == "gemm_pair" && value >= 0 && value <= 1) { g_gemm_pair_off = value ? 0 : 1; return 0; }
+  if (k == "wgrad_dma" && value >= 0 && value <= 1) { g_wgrad_dma = value; return 0; }
+  if (k == "wgrad_stages" && (value == 0 || value == 2 || value == 3)) { g_wgrad_stages = value; return 0; }
   if (k == "msda_generic" && value >= 0 && value <= 3) { g_msda_generic = value; return 0; }
   return fail("moe_set_tuning: unknown key or value");
 }

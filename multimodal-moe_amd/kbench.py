@@ -58,6 +58,7 @@ def setup(T, E, k, d, F, seed=0):
     rows = T * k
     xp, pos = L.permute_fwd(x, idx, lrank, rank_base, offsets, E, 0, rows)
     _, tok = L.route_index(idx, lrank, rank_base, offsets, E, 0, rows)
+    _, _, _, _, gate, _, _ = L.route_dispatch(bcnt, idx, lrank, w, auxp, T, E, 0, rows, 1e-2, 1e-3, row_gate=True)
     h = L.grouped_gemm(xp, w1, offsets, E, rows, F, d, 1, L.EPI_BIAS_RELU, bias=b1)
     yp = L.grouped_gemm(h, w2, offsets, E, rows, d, F, 1, L.EPI_BIAS, bias=b2)
     dy = torch.randn((T, d), device="cuda", generator=g).to(torch.bfloat16)
@@ -69,7 +70,7 @@ def setup(T, E, k, d, F, seed=0):
     w1q, w1s = L.quantize_mx(w1)
     w2q, w2s = L.quantize_mx(w2)
     hq, hs = L.grouped_gemm_mx(xq, xs, w1q, w1s, offsets, E, rows, F, d, L.EPI_BIAS_RELU, bias=b1, out_mx=True)
-    return dict(T=T, E=E, k=k, d=d, F=F, x=x, wg=wg, cb=cb, ci=ci, tpi=tpi, w1=w1, w2=w2, b1=b1, b2=b2, idx=idx,
+    return dict(T=T, E=E, k=k, d=d, F=F, x=x, gate=gate, wg=wg, cb=cb, ci=ci, tpi=tpi, w1=w1, w2=w2, b1=b1, b2=b2, idx=idx,
                 auxp=auxp,
                 w=w, probs=probs, lse=lse, lrank=lrank, bcnt=bcnt, rank_base=rank_base, offsets=offsets, rows=rows,
                 xp=xp, pos=pos, tok=tok, h=h, yp=yp, dy=dy, dyp=dyp, dw=dw, dh=dh, dxp=dxp,
@@ -103,8 +104,10 @@ def kernels(c):
          16 * A + 4 * A),
         ("gemm1_fwd_gather", lambda: L.grouped_gemm_gather(c["x"], c["tok"], c["w1"], c["offsets"], E, rows, F, d, 1,
                                                            L.EPI_BIAS_RELU, bias=c["b1"]), 2.0 * A * F * d, 0),
-        ("gemm_pair2", lambda: L.grouped_gemm_bwd_pair(c["dyp"], c["w2"], c["offsets"], E, rows, F, d, L.EPI_RELU_MASK,
-                                                       c["h"], c["dyp"], c["h"]), 4.0 * A * F * d, 0),
+        # as the layer's backward runs it: dY rows gathered by token and scaled by the gate in both halves
+        ("gemm_pair2", lambda: L.grouped_gemm_bwd_pair(c["dy"], c["w2"], c["offsets"], E, rows, F, d, L.EPI_RELU_MASK,
+                                                       c["h"], c["dy"], c["h"], a_gather=c["tok"], row_scale=c["gate"],
+                                                       wx_gather=c["tok"], wx_scale=c["gate"]), 4.0 * A * F * d, 0),
         ("gemm_pair1", lambda: L.grouped_gemm_bwd_pair(c["dh"], c["w1"], c["offsets"], E, rows, d, F, L.EPI_NONE,
                                                        None, c["dh"], c["x"], c["tok"]), 4.0 * A * F * d, 0),
         ("route_dispatch", lambda: L.route_dispatch(c["bcnt"], c["idx"], c["lrank"], c["w"], c["auxp"], T, E, 0,
@@ -151,12 +154,14 @@ def main():
     ap.add_argument("--xcd", default="0", help="comma list of ROWS tile->XCD maps (0 auto, 1 round-robin, 2 contiguous)")
     ap.add_argument("--ksplit", default="0", help="comma list of split-K factors (0 auto, 1 off, 2..8 forced)")
     ap.add_argument("--pair", default="1", help="comma list of gemm_pair modes (1 one launch, 0 two launches)")
+    ap.add_argument("--wg", default="0:0", help="comma list of gathered-wgrad bodies dma:stages (dma 0 auto / 1 "
+                                                "register-staged; stages 0 auto, 2, 3)")
     a = ap.parse_args()
     L.lib()
-    configs = [(v, s, dbg, bm, xm, ks, pr) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
+    configs = [(v, s, dbg, bm, xm, ks, pr, wg) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
                for dbg in map(int, a.debug.split(",")) for bm in map(int, a.bm.split(","))
                for xm in map(int, a.xcd.split(",")) for ks in map(int, a.ksplit.split(","))
-               for pr in map(int, a.pair.split(","))
+               for pr in map(int, a.pair.split(",")) for wg in a.wg.split(",")
                if not (v == 1 and s != int(a.stages.split(",")[0]))]
     if a.config == "c5":  # 32 experts, top-4, bs 16 (no capacity drops here: cf only trims the tail)
         shapes = {"enc": setup(16 * 920, 32, 4, 256, 1024), "dec": setup(16 * 300, 32, 4, 256, 1024, seed=1)}
@@ -164,7 +169,10 @@ def main():
         shapes = {"enc": setup(8 * 920, 8, 2, 256, 1024), "dec": setup(8 * 300, 8, 2, 256, 1024, seed=1)}
     res = {}
     for _ in range(a.rounds):
-        for (v, s, dbg, bm, xm, ks, pr) in configs:
+        for (v, s, dbg, bm, xm, ks, pr, wg) in configs:
+            wd, ws = (int(u) for u in wg.split(":"))
+            L.set_tuning("wgrad_dma", wd)
+            L.set_tuning("wgrad_stages", ws)
             L.set_tuning("gemm_pair", pr)
             L.set_tuning("ksplit", ks)
             L.set_tuning("xcd_map", xm)
@@ -177,21 +185,24 @@ def main():
                 for name, fn, flops, byts in kernels(c):
                     if a.only and a.only not in name:
                         continue
-                    if not name.startswith("gemm") and (v, s, dbg, bm, xm, ks, pr) != configs[0]:
+                    if not name.startswith("gemm") and (v, s, dbg, bm, xm, ks, pr, wg) != configs[0]:
                         continue
                     if pr != 1 and "pair" not in name:
                         continue
-                    res.setdefault((name, sname, v, s, dbg, bm, xm, ks, pr, flops, byts), []).append(timed(fn, a.reps))
+                    res.setdefault((name, sname, v, s, dbg, bm, xm, ks, pr, wg, flops, byts), []).append(
+                        timed(fn, a.reps))
     L.set_tuning("ksplit", 0)
     L.set_tuning("gemm_pair", 1)
     L.set_tuning("gemm_debug", 0)
     L.set_tuning("rows_bm", 0)
     L.set_tuning("wgrad_bm", 0)
     L.set_tuning("xcd_map", 0)
-    for (name, sname, v, s, dbg, bm, xm, ks, pr, flops, byts), ts in res.items():
+    L.set_tuning("wgrad_dma", 0)
+    L.set_tuning("wgrad_stages", 0)
+    for (name, sname, v, s, dbg, bm, xm, ks, pr, wg, flops, byts), ts in res.items():
         us = statistics.median(ts)
         d = {"kernel": name, "config": a.config, "shape": sname, "variant": v, "stages": s, "debug": dbg, "bm": bm,
-             "xcd": xm, "ksplit": ks, "pair": pr, "us": round(us, 2),
+             "xcd": xm, "ksplit": ks, "pair": pr, "wg": wg, "us": round(us, 2),
              "min_us": round(min(ts), 2)}
         if flops:
             d["tflops"] = round(flops / us / 1e6, 1)

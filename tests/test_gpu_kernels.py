@@ -471,6 +471,61 @@ def test_grouped_gemm_bwd_pair_exact(hip_lib, rows_per_group, epi, pair):
         assert int(cnt.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("rows_per_group", [[0, 1, 63, 64, 65, 200, 0, 130], [1500, 40, 0, 1100], [3000] * 4])
+@pytest.mark.parametrize("wg", ["0:0", "0:3", "1:0"], ids=["dma2", "dma3", "regs"])
+def test_grouped_gemm_bwd_pair_gathered(hip_lib, rows_per_group, wg):
+    """The layer backward's pairs with gathered k-rows: (a) dH = gate * (dy[tok]
+    W2) * mask with dW2 = bf16(gate * dy[tok])^T H (X gathered AND scaled), (b)
+    dXp = dH W1 with dW1 = dH^T x[tok] (Y gathered).  The weight gradients
+    equal the plain wgrad of the explicitly gathered (and bf16-scaled) rows
+    bit for bit, for the LDS-DMA ring (2 or 3 stages, indices staged in LDS)
+    and the register-staged body; split-K engages on the 3000-row groups."""
+    from src.moe import _lib as L
+
+    rng = np.random.default_rng(29)
+    G = len(rows_per_group)
+    offsets = np.concatenate([[0], np.cumsum(rows_per_group)]).astype(np.int32)
+    R = int(offsets[-1])
+    d, F = 256, 1024
+    T = max(R, 1) // 2 + 7
+    tok = torch.from_numpy(rng.integers(0, T, size=max(R, 1)).astype(np.int32)).to(DEV)
+    # power-of-two gates: bf16(gate * dy) is exact and every fp32 sum below is exact, so split-K and
+    # the explicit reference agree bit for bit whatever the summation order
+    gate = torch.from_numpy(rng.choice([0.25, 0.5, 1.0, 2.0], size=max(R, 1)).astype(np.float32)).to(DEV)
+    dy = torch.from_numpy(_int_tensor(rng, (T, d), -3, 4)).to(torch.bfloat16).to(DEV)
+    x = torch.from_numpy(_int_tensor(rng, (T, d), -2, 3)).to(torch.bfloat16).to(DEV)
+    h = torch.from_numpy(_int_tensor(rng, (max(R, 1), F), -2, 3)).to(torch.bfloat16).to(DEV)
+    dh = torch.from_numpy(_int_tensor(rng, (max(R, 1), F), -2, 3)).to(torch.bfloat16).to(DEV)
+    w2 = torch.from_numpy(_int_tensor(rng, (G, d, F))).to(torch.bfloat16).to(DEV)
+    w1 = torch.from_numpy(_int_tensor(rng, (G, F, d))).to(torch.bfloat16).to(DEV)
+    off_t = torch.from_numpy(offsets).to(DEV)
+    dma, stages = (int(v) for v in wg.split(":"))
+    L.set_tuning("wgrad_dma", dma)
+    L.set_tuning("wgrad_stages", stages)
+    try:
+        c2, wc2, cs2 = L.grouped_gemm_bwd_pair(dy, w2, off_t, G, R, F, d, L.EPI_RELU_MASK, h, dy, h,
+                                               out_dtype=torch.float32, a_gather=tok, row_scale=gate, wx_gather=tok,
+                                               wx_scale=gate)
+        c1, wc1, cs1 = L.grouped_gemm_bwd_pair(dh, w1, off_t, G, R, d, F, L.EPI_NONE, None, dh, x, tok,
+                                               out_dtype=torch.float32)
+        L.set_tuning("wgrad_dma", 1)
+        L.set_tuning("wgrad_stages", 0)
+        r2 = L.grouped_gemm_bwd_pair(dy, w2, off_t, G, R, F, d, L.EPI_RELU_MASK, h, dy, h, out_dtype=torch.float32,
+                                     a_gather=tok, row_scale=gate, wx_gather=tok, wx_scale=gate)
+    finally:
+        L.set_tuning("wgrad_dma", 0)
+        L.set_tuning("wgrad_stages", 0)
+    dyp = (dy[tok.long()].float() * gate[:, None]).to(torch.bfloat16).contiguous()
+    ref_wc2, ref_cs2 = L.grouped_gemm_wgrad(dyp, h, off_t, G)
+    ref_wc1, ref_cs1 = L.grouped_gemm_wgrad(dh, x[tok.long()].contiguous(), off_t, G)
+    torch.cuda.synchronize()
+    assert torch.equal(wc2, ref_wc2) and torch.equal(cs2, ref_cs2)
+    assert torch.equal(wc1, ref_wc1) and torch.equal(cs1, ref_cs1)
+    assert torch.equal(c2[:R], r2[0][:R]) and torch.equal(wc2, r2[1])  # the dgrad half is unchanged
+    for _ws, cnt in L._SPLIT_WS.values():
+        assert int(cnt.abs().sum()) == 0
+
+
 @pytest.mark.parametrize("T,E,k,cf", [(1000, 8, 2, 0.0), (777, 16, 2, 0.0), (640, 32, 4, 1.25), (1, 4, 1, 0.0)])
 def test_route_index_matches_permute(hip_lib, T, E, k, cf):
     """route_index's pos equals permute_fwd's, and src_tok inverts it: the

@@ -11,7 +11,7 @@ set -u
 X=${BENCH_EXTRA:-}
 TAG=${1:-prof}; shift
 R=$GRAFT_REPO_ROOT
-KRE="gemm_v|gemm_pair|permute_fwd|combine_fwd|combine_bwd|router_topk|route_dispatch|route_index|route_scan|token_bwd|quantize_mx|msda_|linear_wgrad"
+KRE="conv_|attn_|gemm_v|gemm_pair|permute_fwd|combine_fwd|combine_bwd|router_topk|route_dispatch|route_index|route_scan|token_bwd|quantize_mx|msda_|linear_wgrad"
 for WL in "$@"; do
   O=$R/gpurun_out/$TAG/$WL
   mkdir -p $O/prof $O/pmc_fetch $O/pmc_write

@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--marker", default="adamw_step_kernel", help="kernel launched once per step (torch fused AdamW: FusedAdamMathFunctor)")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--skip", type=int, default=0,
+                    help="ignore the last N steps (bench.py's eager kernel-timing steps follow the timed graph replays)")
     ap.add_argument("--full", default=None, help="regex over categories: list those kernels by full name + grid")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
@@ -47,6 +49,8 @@ def main():
     # last marker launch of each step: markers come in bursts (one per param group)
     ends = [marks[j] for j in range(len(marks)) if j + 1 == len(marks) or
             int(rows[marks[j + 1]]["Start_Timestamp"]) - int(rows[marks[j]]["End_Timestamp"]) > 1_000_000]
+    if a.skip:
+        ends = ends[: -a.skip]
     lo, hi = ends[-a.steps - 1] + 1, ends[-1] + 1
     win = rows[lo:hi]
     span = (int(win[-1]["End_Timestamp"]) - int(win[0]["Start_Timestamp"])) / 1e6 / a.steps
