@@ -40,8 +40,8 @@
 extern "C" {
 #endif
 
-/* Number of 64-token router blocks for T tokens (size of the per-block
- * workspaces below). */
+/* Number of router blocks (16 tokens each) for T tokens (size of the
+ * per-block workspaces below). */
 int moe_router_num_blocks(int T);
 
 /* a2+a3: router logits, fp32 softmax, top-k, gates, per-block
@@ -50,13 +50,14 @@ int moe_router_num_blocks(int T);
  *   probs = softmax(logits) (fp32), lse[t] = logsumexp(logits[t])
  *   topk_idx[t,j], j=0..k-1: experts by descending prob, ties -> lower index
  *   topk_w[t,j] = probs[t, idx] (normalize==0 or k==1) or renormalised to sum 1
- *   local_rank[t,j] = #{t' < t in the same 64-token block : idx[t',j] == idx[t,j]}
+ *   local_rank[t,j] = #{t' < t in the same router block : idx[t',j] == idx[t,j]}
  *   block_counts[b, j, e] = #{t in block b : idx[t,j] == e}
  *   aux_partials[b, e] = sum_{t in b} probs[t,e]; aux_partials[b, E] = sum lse^2
- * x: bf16 [T,d]; wg: fp32 [E,d]; ctx_bias: fp32 [C,E] or NULL; ctx_img: int32
- * [T/tokens_per_image] or NULL. Workspaces sized by moe_router_num_blocks(T). */
+ * x: bf16 [T,d]; wg: fp32 [E,d]; ctx_bias: fp32 [n_ctx,E] (n_ctx E <= 4096) or
+ * NULL; ctx_img: int32 [T/tokens_per_image] or NULL. Workspaces sized by
+ * moe_router_num_blocks(T). */
 int moe_router_topk_fwd(const void* x, const float* wg, const float* ctx_bias,
-                        const int32_t* ctx_img, int tokens_per_image,
+                        const int32_t* ctx_img, int n_ctx, int tokens_per_image,
                         int T, int d, int E, int k, int normalize,
                         int32_t* topk_idx, float* topk_w, float* probs, float* lse,
                         int32_t* local_rank, int32_t* block_counts,

@@ -16,7 +16,11 @@ typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWave = 64;
-constexpr int kRouterBlockTokens = 64;  // one wave's ballot covers one block
+// Router block: the tokens of one router workgroup, whose within-block ranks
+// come from one wave's ballots (<= 64).  16 tokens: 4x as many workgroups as
+// 64-token blocks (the decoder's 2,400 tokens were 38 workgroups, a latency
+// chain per workgroup on a mostly idle chip).
+constexpr int kRouterBlockTokens = 16;
 
 // ---- bf16 <-> f32 (round-to-nearest-even; NaN kept NaN via the hw cvt) ----
 __device__ __forceinline__ float bf2f(uint16_t v) {

@@ -1,9 +1,10 @@
 // Router kernels for gfx950.
 //
 //  router_topk_fwd : logits = x.Wg^T + ctx_bias[ctx(t)], fp32 softmax, top-k
-//                    (ties -> lower expert id), gates, per-64-token-block
-//                    routing counts + within-block ranks (wave ballot), aux
-//                    partials.  One block = 64 tokens (16 waves; 4 for E > 32);
+//                    (ties -> lower expert id), gates, per-block routing
+//                    counts + within-block ranks (wave ballot), aux partials.
+//                    One block = kRouterBlockTokens (16) tokens, 4 waves (1
+//                    for E > 32);
 //                    16 lanes per token, each lane owning d/16 channels read as
 //                    16-B chunks (a token row is read by 16 lanes, 4 tokens per
 //                    wave-instruction).
@@ -44,10 +45,10 @@ __device__ __forceinline__ void argmax_stage(float& bv, int& best) {
   if (ov > bv || (ov == bv && oi < best)) { bv = ov; best = oi; }
 }
 
-template <int EMAX, int NW>
+template <int EMAX, int NW, int TPB>
 __global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
     const uint16_t* __restrict__ x, const float* __restrict__ wg,
-    const float* __restrict__ ctx_bias, const int32_t* __restrict__ ctx_img,
+    const float* __restrict__ ctx_bias, const int32_t* __restrict__ ctx_img, int n_ctx,
     int tpi, int T, int d, int E, int k, int normalize,
     int32_t* __restrict__ topk_idx, float* __restrict__ topk_w,
     float* __restrict__ probs_out, float* __restrict__ lse_out,
@@ -55,9 +56,9 @@ __global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
     float* __restrict__ aux_partials) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_wg = reinterpret_cast<float*>(smem);               // [E][d]
-  int32_t* s_idx = reinterpret_cast<int32_t*>(s_wg + E * d);  // [64][k]
-  float* s_aux = reinterpret_cast<float*>(s_idx + 64 * 8);    // [NW][EMAX+1]
-  float* s_cb = s_aux + NW * (EMAX + 1);                       // [64][E] context bias rows
+  int32_t* s_idx = reinterpret_cast<int32_t*>(s_wg + E * d);  // [TPB][8]
+  float* s_aux = reinterpret_cast<float*>(s_idx + TPB * 8);   // [NW][EMAX+1]
+  float* s_cb = s_aux + NW * (EMAX + 1);                       // [n_ctx][E] the context-bias table
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -67,56 +68,40 @@ __global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
   const int blk = blockIdx.x;
 
   // One token per 16-lane group, 4 per wave per iteration; NW waves cover the
-  // block's 64 tokens in 16/NW iterations.  The per-token softmax / top-k is
-  // serial VALU work, so it is spread over 16 waves (one iteration) where the
-  // registers allow (EMAX <= 32).  The x loads (up to PF chunks of the row per
-  // lane; d=256 is fully covered) are issued first, overlapped with the Wg
-  // staging.
+  // block's TPB tokens in TPB/(4 NW) iterations.  Every global load of the
+  // workgroup -- the token rows (up to PF 16-B chunks per lane; d=256 is fully
+  // covered), Wg, the whole [n_ctx][E] context-bias table and each token's
+  // context id -- is independent of the others and issued up front: one
+  // memory round trip before the token loop (the per-token bias row is then
+  // an LDS lookup, and the loop issues no global loads: on gfx9 vmcnt also
+  // counts the loop's stores).
   constexpr int NT = NW * 64;
-  constexpr int ITERS = 16 / NW;
+  constexpr int ITERS = TPB / (4 * NW);
+  static_assert(ITERS >= 1 && ITERS * 4 * NW == TPB, "TPB must be a multiple of 4 NW");
   constexpr int PF = 2;
   const int nchunk = d >> 7;  // 16-B chunks per lane (d / 8 / 16)
+  const bool has_ctx = ctx_bias != nullptr && ctx_img != nullptr;
   uint4 xpre[ITERS][PF];
+  int cid[ITERS];
 #pragma unroll
   for (int it = 0; it < ITERS; ++it) {
-    const int t = blk * 64 + it * NW * 4 + wave * 4 + grp;
+    const int t = blk * TPB + it * NW * 4 + wave * 4 + grp;
     const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)t * d);
 #pragma unroll
     for (int c = 0; c < PF; ++c)
       xpre[it][c] = (t < T && c < nchunk) ? xr[sub + 16 * c] : make_uint4(0u, 0u, 0u, 0u);
+    cid[it] = (has_ctx && t < T) ? ctx_img[t / tpi] : 0;
   }
-
-  // The context id of each (token, expert) element this thread stages below,
-  // loaded together with the x rows: the context-bias gather then waits on
-  // one round trip instead of two (ctx_img, then ctx_bias) after the Wg copy.
-  const bool has_ctx = ctx_bias != nullptr && ctx_img != nullptr;
-  constexpr int CBP = (64 * EMAX + NT - 1) / NT;
-  int cimg[CBP];
-#pragma unroll
-  for (int u = 0; u < CBP; ++u) {
-    const int i = tid + u * NT;
-    const int t = blk * 64 + i / (E > 0 ? E : 1);
-    cimg[u] = (has_ctx && i < 64 * E && t < T) ? ctx_img[t / tpi] : -1;
-  }
-
-  // Stage Wg (fp32 [E][d]) in LDS, 16 B per thread-iteration.
+  // Wg (fp32 [E][d]) and the context-bias table into LDS, 16 B / 4 B per thread-iteration
   {
     const int n4 = (E * d) >> 2;
     const float4* src = reinterpret_cast<const float4*>(wg);
     float4* dst = reinterpret_cast<float4*>(s_wg);
     for (int i = tid; i < n4; i += NT) dst[i] = src[i];
   }
-  for (int i = tid; i < 64 * 8; i += NT) s_idx[i] = -1;
-  // Context-bias row of each of the block's 64 tokens, gathered here so the
-  // token loop below issues no global loads: on gfx9 vmcnt also counts the
-  // loop's stores, so a load inside the loop would wait for them.
-  if (has_ctx) {
-#pragma unroll
-    for (int u = 0; u < CBP; ++u) {
-      const int i = tid + u * NT;
-      if (i < 64 * E) s_cb[i] = cimg[u] >= 0 ? ctx_bias[(size_t)cimg[u] * E + (i - (i / E) * E)] : 0.f;
-    }
-  }
+  if (has_ctx)
+    for (int i = tid; i < n_ctx * E; i += NT) s_cb[i] = ctx_bias[i];
+  for (int i = tid; i < TPB * 8; i += NT) s_idx[i] = -1;
   __syncthreads();
 
   // Expert ownership inside a 16-lane token group: lane `sub` owns experts
@@ -134,7 +119,7 @@ __global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
 #pragma unroll
   for (int it = 0; it < ITERS; ++it) {
     const int tl = it * NW * 4 + wave * 4 + grp;  // token within block
-    const int t = blk * 64 + tl;
+    const int t = blk * TPB + tl;
     const bool valid = t < T;
     float v[EP];
 #pragma unroll
@@ -174,7 +159,7 @@ __global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
     for (int q = 0; q < Q; ++q) {
       const int e = 16 * q + sub;
       own[q] = e < E;
-      logit[q] = v[16 * q] + ((own[q] && has_ctx) ? s_cb[tl * E + e] : 0.f);
+      logit[q] = v[16 * q] + ((own[q] && has_ctx) ? s_cb[cid[it] * E + e] : 0.f);
     }
     float m = -INFINITY;
 #pragma unroll
@@ -254,26 +239,26 @@ __global__ __launch_bounds__(NW * 64) void router_topk_fwd_kernel(
     if (lane == 0) s_aux[wave * (EMAX + 1) + EMAX] = pz;
   }
   __syncthreads();
-  if (tid <= E) {
-    const int src = (tid == E) ? EMAX : tid;
+  for (int i = tid; i <= E; i += NT) {  // E + 1 columns (more than one wave's lanes when NW = 1, E = 64)
+    const int src = (i == E) ? EMAX : i;
     float u = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) u += s_aux[w * (EMAX + 1) + src];
-    aux_partials[(size_t)blk * (E + 1) + tid] = u;
+    aux_partials[(size_t)blk * (E + 1) + i] = u;
   }
 
   // Within-block stable ranks: wave 0, lane l = token l of the block.
   if (wave == 0) {
-    const int t = blk * 64 + lane;
+    const int t = blk * TPB + lane;
     _Pragma("unroll") for (int j = 0; j < 8; ++j) if (j < k) {
-      const int e_l = s_idx[lane * 8 + j];
+      const int e_l = lane < TPB ? s_idx[lane * 8 + j] : -1;
       int rank = 0;
       for (int e = 0; e < E; ++e) {
         const unsigned long long mask = __ballot(e_l == e);
         if (e_l == e) rank = mbcnt(mask);
         if (lane == 0) block_counts[((size_t)blk * k + j) * E + e] = __popcll(mask);
       }
-      if (t < T) local_rank[(size_t)t * k + j] = rank;
+      if (lane < TPB && t < T) local_rank[(size_t)t * k + j] = rank;
     }
   }
 }
@@ -387,11 +372,11 @@ __device__ __forceinline__ float aux_colsum(const float* __restrict__ partials, 
 // ---------------------------------------------------------------------------
 // route dispatch: scan + index + aux loss in one launch (replaces route_scan,
 // route_index and aux_loss_fwd).  Workgroup b owns
-// router block b (64 tokens): it sums the counts of every router block into
+// router block b (kRouterBlockTokens tokens): it sums the counts of every router block into
 // column totals and its own exclusive prefix (coalesced rows, a few KiB read
 // per workgroup from L2: no second launch, no inter-workgroup hand-off),
 // forms the slot bases / hist / kept offsets (one wave), and writes pos,
-// the row -> token map and the row gates of its 64 tokens.  Workgroup 0 also
+// the row -> token map and the row gates of its tokens.  Workgroup 0 also
 // writes hist / offsets and the layer's aux losses.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void route_dispatch_kernel(
@@ -531,8 +516,8 @@ __global__ __launch_bounds__(256) void route_dispatch_kernel(
     }
   }
   // Phase C: this block's assignments
-  for (int a = tid; a < 64 * k; a += 256) {
-    const int t = b * 64 + a / k;
+  for (int a = tid; a < kRouterBlockTokens * k; a += 256) {
+    const int t = b * kRouterBlockTokens + a / k;
     if (t >= T) break;
     const int j = a - (a / k) * k;
     const size_t ai = (size_t)t * k + j;
@@ -749,7 +734,7 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
 // ---------------------------------------------------------------------------
 using namespace moe;
 
-extern "C" int moe_router_num_blocks(int T) { return (T + 63) / 64; }
+extern "C" int moe_router_num_blocks(int T) { return (T + kRouterBlockTokens - 1) / kRouterBlockTokens; }
 
 // Raise the dynamic-LDS cap of a kernel (once, on its first launch) so a
 // launch needing more than 64 KiB succeeds; later launches make no call.
@@ -766,7 +751,7 @@ static void allow_lds(size_t bytes) {
 static int emax_for(int E) { return E <= 8 ? 8 : E <= 16 ? 16 : E <= 32 ? 32 : 64; }
 
 extern "C" int moe_router_topk_fwd(const void* x, const float* wg, const float* ctx_bias,
-                                   const int32_t* ctx_img, int tokens_per_image, int T,
+                                   const int32_t* ctx_img, int n_ctx, int tokens_per_image, int T,
                                    int d, int E, int k, int normalize, int32_t* topk_idx,
                                    float* topk_w, float* probs, float* lse,
                                    int32_t* local_rank, int32_t* block_counts,
@@ -775,25 +760,30 @@ extern "C" int moe_router_topk_fwd(const void* x, const float* wg, const float* 
   if (E < 1 || E > 64 || k < 1 || k > 8 || k > E) return fail("router: need 1<=E<=64, 1<=k<=min(8,E)");
   if ((size_t)E * d * 4 > 64 * 1024) return fail("router: E*d*4 must fit 64 KiB of LDS");
   if (ctx_img != nullptr && tokens_per_image <= 0) return fail("router: tokens_per_image must be > 0");
+  if ((ctx_bias != nullptr) != (ctx_img != nullptr)) return fail("router: ctx_bias and ctx_img go together");
+  if (ctx_bias != nullptr && (n_ctx < 1 || (size_t)n_ctx * E > 4096))
+    return fail("router: need 1 <= n_ctx and n_ctx * E <= 4096 (the context-bias table is staged in LDS)");
   if (T == 0) return 0;
   const int nblk = moe_router_num_blocks(T);
   const int em = emax_for(E);
-  const int nw = em <= 32 ? 16 : 4;
-  const size_t shmem = (size_t)E * d * 4 + 64 * 8 * 4 + nw * (em + 1) * 4 + 64 * (size_t)E * 4;
+  constexpr int TPB = kRouterBlockTokens;
+  const int nw = em <= 32 ? TPB / 4 : 4;
+  const size_t shmem = (size_t)E * d * 4 + TPB * 8 * 4 + nw * (em + 1) * 4 +
+                       (ctx_bias != nullptr ? (size_t)n_ctx * E * 4 : 0);
   const uint16_t* xb = static_cast<const uint16_t*>(x);
   // bytes: x, Wg once, per-token outputs (idx, w, probs, lse, local rank), per-block partials
   ProfScope prof(stream, PROF_ROUTER,
                  2.0 * T * d + 4.0 * E * d + 12.0 * T * k + 4.0 * T * (E + 1) + 4.0 * nblk * (k * E + E + 1));
-#define LAUNCH_R(EM, NW)                                                                       \
-  allow_lds<router_topk_fwd_kernel<EM, NW>>(shmem);                                             \
-  MOE_LAUNCH(prof, (router_topk_fwd_kernel<EM, NW>), dim3(nblk), dim3(NW * 64), shmem, stream, xb, \
-                     wg, ctx_bias, ctx_img, tokens_per_image, T, d, E, k, normalize,       \
-                     topk_idx, topk_w, probs, lse, local_rank, block_counts, aux_partials)
+#define LAUNCH_R(EM, NW)                                                                                    \
+  allow_lds<router_topk_fwd_kernel<EM, NW, TPB>>(shmem);                                                     \
+  MOE_LAUNCH(prof, (router_topk_fwd_kernel<EM, NW, TPB>), dim3(nblk), dim3(NW * 64), shmem, stream, xb, wg,  \
+             ctx_bias, ctx_img, n_ctx, tokens_per_image, T, d, E, k, normalize, topk_idx, topk_w, probs, lse, \
+             local_rank, block_counts, aux_partials)
   switch (em) {
-    case 8: LAUNCH_R(8, 16); break;
-    case 16: LAUNCH_R(16, 16); break;
-    case 32: LAUNCH_R(32, 16); break;
-    default: LAUNCH_R(64, 4); break;
+    case 8: LAUNCH_R(8, TPB / 4); break;
+    case 16: LAUNCH_R(16, TPB / 4); break;
+    case 32: LAUNCH_R(32, TPB / 4); break;
+    default: LAUNCH_R(64, TPB / 16); break;
   }
 #undef LAUNCH_R
   return check_launch("moe_router_topk_fwd");

@@ -29,7 +29,7 @@ _F = ctypes.c_float
 _LL = ctypes.c_longlong
 SIGNATURES = {
     "moe_router_num_blocks": (_I, [_I]),
-    "moe_router_topk_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "moe_router_topk_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "moe_route_scan": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "moe_permute_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "moe_combine_fwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
@@ -279,8 +279,11 @@ def ensure_splitk_workspace(device: torch.device) -> None:
     _SPLIT_WS[idx] = (ws, cnt)
 
 
+ROUTER_BLOCK_TOKENS = 16  # kRouterBlockTokens (csrc/moe_common.h); moe_router_num_blocks agrees (test_capi)
+
+
 def router_num_blocks(T: int) -> int:
-    return (T + 63) // 64
+    return (T + ROUTER_BLOCK_TOKENS - 1) // ROUTER_BLOCK_TOKENS
 
 
 def router_topk_fwd(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize):
@@ -309,7 +312,7 @@ def router_topk_fwd(x, wg, ctx_bias, ctx_img, tokens_per_image, k, normalize):
     aux_partials = torch.empty((nblk, E + 1), dtype=torch.float32, device=dev)
     rc = lib().moe_router_topk_fwd(
         _ptr(x), _ptr(wg), _ptr(ctx_bias), _ptr(ctx_img) if ctx_bias is not None else None,
-        int(tokens_per_image), T, d, E, k, int(normalize),
+        int(ctx_bias.shape[0]) if ctx_bias is not None else 0, int(tokens_per_image), T, d, E, k, int(normalize),
         _ptr(topk_idx), _ptr(topk_w), _ptr(probs), _ptr(lse), _ptr(local_rank),
         _ptr(block_counts), _ptr(aux_partials), _stream())
     _check(rc, "moe_router_topk_fwd")

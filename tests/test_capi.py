@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol():
     assert set(_lib.SIGNATURES) == set(declared_symbols())
     lib = _lib.load_library(lib_path)
     assert lib.moe_version().decode().startswith("moe_hip")
-    assert lib.moe_router_num_blocks(130) == 3
+    assert lib.moe_router_num_blocks(130) == 9 == _lib.router_num_blocks(130)  # 16-token router blocks
 
 
 def test_gpu_path_refuses_cpu_tensors():
