@@ -531,23 +531,29 @@ int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, 
  * x / dy / y: NHWC bf16 [B, H, W, channels]; w: [N][KS][KS][C] bf16 (a
  * channels_last [N, C, KS, KS] weight); C and N multiples of 128; zero: >= 256
  * zero bytes on the device (read for padding neighbours); pointers 16-B aligned.
- *   rtdetr_conv_fwd         y[B,H,W,N] = conv(x[B,H,W,C], w)   (no im2col buffer)
+ *   rtdetr_conv_fwd         y[B,H,W,N] = conv(x[B,H,W,C], w)   (no im2col buffer),
+ *                           with an optional fused epilogue (NULL / 0 = off):
+ *                           y = relu?((y + resid[B,H,W,N]) + bias[N]) (fp32 on
+ *                           the bf16 result: rtdetr_add_bias_relu_nhwc's
+ *                           arithmetic; bias fp32, resid bf16 NHWC)
  *   rtdetr_conv_dgrad       dx[B,H,W,C] = conv^T(dy[B,H,W,N], w): the forward
  *                           GEMM over dy with the flipped, transposed weight,
  *                           written to work first when
  *                           rtdetr_conv_dgrad_workspace() > 0 (bytes; large
  *                           problems), else read in place from w (work may be
- *                           NULL)
+ *                           NULL); relu_mask (bf16 [B,H,W,C] or NULL): dx = 0
+ *                           where relu_mask <= 0 (the ReLU backward of the
+ *                           activation that fed the convolution, fused)
  *   rtdetr_conv_wgrad       dw[N][KS][KS][C] = sum over pixels dy (x) x[neighbour]:
  *                           nsplit pixel slices write fp32 partials to part
  *                           [nsplit][N KS KS C], summed in slice order
  *                           (deterministic) into dw (bf16 if out_bf16 else fp32);
  *                           nsplit from rtdetr_conv_wgrad_splits. */
 int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void* zero, int B, int H, int W, int C, int N,
-                    int KS, hipStream_t stream);
+                    int KS, const float* bias, const void* resid, int relu, hipStream_t stream);
 long long rtdetr_conv_dgrad_workspace(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void* dx, const void* zero, int B, int H, int W,
-                      int C, int N, int KS, hipStream_t stream);
+                      int C, int N, int KS, const void* relu_mask, hipStream_t stream);
 int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
                       const void* zero, int B, int H, int W, int C, int N, int KS, hipStream_t stream);

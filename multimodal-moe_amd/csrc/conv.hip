@@ -49,6 +49,14 @@ struct ConvArgs {
   int B, H, W, C, N;
   int P;                 // B H W
   int mt_n;              // M tiles
+  // fused epilogue on the bf16 result v (each NULL / 0 = off), in this order:
+  //   v = relu?( (v + resid[p][n]) + bias[n] ),  then v = 0 where mask[p][n] <= 0
+  // (the arithmetic of rtdetr_bias_act_nhwc / rtdetr_add_bias_relu_nhwc and of
+  // a ReLU backward on the data gradient, so fused and separate agree bitwise)
+  const float* bias;
+  const uint16_t* resid;
+  const uint16_t* mask;
+  int relu;
 };
 
 // Wait until K-tile kt's DMA has landed for this wave: up to min(S - 2, newer)
@@ -164,7 +172,27 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   // Epilogue through LDS: lane holds Y[m0 + wm BM/2 + 16 i + (lane & 15)][n0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3];
   // the tile goes to a row-major [BM][128] bf16 image (16-B chunk c of row r at chunk c ^ (r & 15):
   // conflict-free 8-B writes and 16-B reads), then out as whole 256-B rows of 16-B stores
-  // (register-direct 8-B stores at a row stride run at about half that rate)
+  // (register-direct 8-B stores at a row stride run at about half that rate).  The fused
+  // epilogue's operands (same 16-B chunks as the stores) are loaded first, behind the image.
+  const int ec = tid & 15;
+  uint4 eres[BM / 16], emask[BM / 16];
+  if (a.resid != nullptr || a.mask != nullptr) {
+#pragma unroll
+    for (int k = 0; k < BM / 16; ++k) {
+      const int p = m0 + (tid >> 4) + 16 * k;
+      const size_t g = (size_t)(p < a.P ? p : 0) * a.N + n0 + ec * 8;
+      if (a.resid != nullptr) eres[k] = *reinterpret_cast<const uint4*>(a.resid + g);
+      if (a.mask != nullptr) emask[k] = *reinterpret_cast<const uint4*>(a.mask + g);
+    }
+  }
+  float eb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (a.bias != nullptr) {
+    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + n0 + ec * 8);
+    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + n0 + ec * 8 + 4);
+    eb[0] = b0.x; eb[1] = b0.y; eb[2] = b0.z; eb[3] = b0.w;
+    eb[4] = b1.x; eb[5] = b1.y; eb[6] = b1.z; eb[7] = b1.w;
+  }
+  const bool efloat = a.resid != nullptr || a.bias != nullptr || a.relu;
   __syncthreads();  // every wave is done reading the ring
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -181,10 +209,39 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < BM / 16; ++k) {
-    const int r = (tid >> 4) + 16 * k, c = tid & 15;
+    const int r = (tid >> 4) + 16 * k, c = ec;
     const int p = m0 + r;
     if (p < a.P) {
-      const uint4 v = *reinterpret_cast<const uint4*>(smem + r * 256 + ((c ^ (r & 15)) << 4));
+      uint4 v = *reinterpret_cast<const uint4*>(smem + r * 256 + ((c ^ (r & 15)) << 4));
+      if (efloat) {
+        float f[8];
+        unpack8(v, f);
+        if (a.resid != nullptr) {
+          float q[8];
+          unpack8(eres[k], q);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] += q[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += eb[e];
+        if (a.relu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+        }
+        v = pack8(f);
+      }
+      if (a.mask != nullptr) {  // keep where the mask element is > 0 (bf16: sign clear, not zero)
+        const uint32_t mw[4] = {emask[k].x, emask[k].y, emask[k].z, emask[k].w};
+        uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t lo = mw[q] & 0xffffu, hi = mw[q] >> 16;
+          const uint32_t keep_lo = ((lo & 0x8000u) || lo == 0) ? 0u : 0xffffu;
+          const uint32_t keep_hi = ((hi & 0x8000u) || hi == 0) ? 0u : 0xffff0000u;
+          vw[q] &= keep_lo | keep_hi;
+        }
+        v = make_uint4(vw[0], vw[1], vw[2], vw[3]);
+      }
       *reinterpret_cast<uint4*>(a.y + (size_t)p * a.N + n0 + c * 8) = v;
     }
   }
@@ -433,15 +490,19 @@ static void launch_wgrad(const ConvWgArgs& a, hipStream_t stream, ProfScope& pro
 
 using namespace moe;
 
+static bool aligned16(const void* p) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+
 extern "C" int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void* zero, int B, int H, int W, int C,
-                               int N, int KS, hipStream_t stream) {
+                               int N, int KS, const float* bias, const void* resid, int relu, hipStream_t stream) {
   const void* ptrs[4] = {x, w, y, zero};
   if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, "rtdetr_conv_fwd")) return rc;
+  if (!aligned16(bias) || !aligned16(resid)) return fail("rtdetr_conv_fwd: bias / resid must be 16-B aligned");
   if (B == 0) return 0;
   ConvArgs a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(y),
-             static_cast<const uint16_t*>(zero), B, H, W, C, N, B * H * W, 0};
+             static_cast<const uint16_t*>(zero), B, H, W, C, N, B * H * W, 0,
+             bias, static_cast<const uint16_t*>(resid), nullptr, relu ? 1 : 0};
   const double P = a.P;
-  ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N) + 2.0 * N * KS * KS * C, false, 0.0,
+  ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N + (resid ? N : 0)) + 2.0 * N * KS * KS * C, false, 0.0,
                  2.0 * P * N * KS * KS * C);
   launch_fwd_any<false>(a, KS, stream, prof);
   return check_launch("rtdetr_conv_fwd");
@@ -459,16 +520,18 @@ extern "C" long long rtdetr_conv_dgrad_workspace(int B, int H, int W, int C, int
 }
 
 extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void* dx, const void* zero, int B, int H,
-                                 int W, int C, int N, int KS, hipStream_t stream) {
+                                 int W, int C, int N, int KS, const void* relu_mask, hipStream_t stream) {
   const void* ptrs[4] = {dy, w, dx, zero};
   if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, "rtdetr_conv_dgrad")) return rc;
+  if (!aligned16(relu_mask)) return fail("rtdetr_conv_dgrad: relu_mask must be 16-B aligned");
   const bool flip = rtdetr_conv_dgrad_workspace(B, H, W, C, N, KS) > 0;
   if (flip && (work == nullptr || reinterpret_cast<uintptr_t>(work) % 16))
     return fail("rtdetr_conv_dgrad: this shape needs a 16-B aligned workspace of rtdetr_conv_dgrad_workspace() bytes");
   if (B == 0) return 0;
   // the forward GEMM over dY [P][N] with W'
   ConvArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(dx),
-             static_cast<const uint16_t*>(zero), B, H, W, N, C, B * H * W, 0};
+             static_cast<const uint16_t*>(zero), B, H, W, N, C, B * H * W, 0,
+             nullptr, nullptr, static_cast<const uint16_t*>(relu_mask), 0};
   const double P = a.P;
   if (flip) {
     const long long total = (long long)N * C * KS * KS;
@@ -480,7 +543,7 @@ extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void
     }
     a.w = static_cast<const uint16_t*>(work);
   }
-  ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N) + 2.0 * N * KS * KS * C, false, 0.0,
+  ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N + (relu_mask ? C : 0)) + 2.0 * N * KS * KS * C, false, 0.0,
                  2.0 * P * N * KS * KS * C);
   if (flip) launch_fwd_any<false>(a, KS, stream, prof);
   else launch_fwd_any<true>(a, KS, stream, prof);

@@ -16,10 +16,13 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
-from .conv import conv2d, conv_module
+from .conv import conv2d, conv2d_add_bias_relu_fork, conv2d_bias_relu, conv_module, hip_conv_ok_for
 from .fused import AddBiasReLU, AddBiasReLUFork, BiasReLU, bn_act, bn_act_ok
 
 _FUSED_BN = os.environ.get("MOE_FUSED_BN", "1") != "0"  # A/B switch: training BN + SiLU in HIP
+# A/B switch: frozen-BN shift + ReLU (+ residual add) in the HIP convolution's
+# epilogue and ReLU backwards in the consumer's data-gradient epilogue
+_FUSED_EPI = os.environ.get("MOE_CONV_EPI", "1") != "0"
 
 _DEPTHS = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3], 50: [3, 4, 6, 3], 101: [3, 4, 23, 3]}
 
@@ -180,14 +183,35 @@ class ConvNormLayer(nn.Module):
         self.act = nn.ReLU(inplace=True) if act == "relu" else (nn.SiLU(inplace=True) if act == "silu" else nn.Identity())
         self.fold = frozen and act in (None, "relu")
 
-    def conv_shift(self, x):
-        """Frozen BN: (conv(x, W * scale), shift) -- the BN output minus its shift."""
+    def folded(self):
+        """Frozen BN: (W * scale, shift); the folded weight PResNet.forward made
+        for this step (one launch for all layers) is consumed."""
         scale, shift = self.norm.scale_shift()
         w = getattr(self, "_w_folded", None)  # set by PResNet.forward (one launch for all)
         self._w_folded = None
         if w is None:
             w = _FoldScale.apply(self.conv.weight, scale)
+        return w, shift
+
+    def conv_shift(self, x, folded=None):
+        """Frozen BN: (conv(x, W * scale), shift) -- the BN output minus its shift."""
+        w, shift = folded if folded is not None else self.folded()
         return conv2d(x, w, self.conv.stride, self.conv.padding), shift
+
+    def hip_ok(self, x_like, cin, w):
+        """Whether this layer's convolution runs on the HIP kernels for an input
+        like x_like with cin channels (the fused epilogues need it)."""
+        return (_FUSED_EPI and self.fold and x_like.shape[0] > 0
+                and hip_conv_ok_for(x_like.is_cuda, x_like.dtype, cin, w, self.conv.stride, self.conv.padding))
+
+    def bias_relu(self, x, folded, mask_input=False, grad_premasked=False):
+        """relu(BN(conv(x))) with the frozen BN folded: one HIP launch when
+        fused (hip_ok), else conv + the BiasReLU kernel."""
+        w, shift = folded
+        if mask_input or grad_premasked or self.hip_ok(x, x.shape[1], w):
+            return conv2d_bias_relu(x, w, shift, mask_input, grad_premasked)
+        y, _ = self.conv_shift(x, folded)
+        return BiasReLU.apply(y, shift)
 
     def forward(self, x):
         if self.fold:
@@ -264,12 +288,21 @@ _NO_FORK = os.environ.get("MOE_BACKBONE_FORK", "1") == "0"
 _NO_FOLD_ALL = os.environ.get("MOE_FOLD_ALL", "1") == "0"
 
 
-def _block_out(last, short, h, x):
+def _block_out(last, short, h, x, folded_last=None, mask_input=False):
     """relu(last(h) + shortcut(x)) as a (main, shortcut) pair of handles on the
     same activation (see fused.AddBiasReLUFork).  With frozen BNs the two BN
-    shifts join the residual add and the ReLU in one fused kernel."""
+    shifts join the residual add and the ReLU in one fused kernel -- the
+    epilogue of last's HIP convolution when it has one (folded_last given and
+    hip_ok; mask_input: h is a ReLU output only last consumes)."""
+    if last.fold and (short is None or short.conv.fold) and folded_last is not None and not _NO_FORK:
+        wl, sl = folded_last
+        if mask_input or last.hip_ok(h, h.shape[1], wl):
+            b, bias = (x, sl) if short is None else short.conv_shift(x)
+            if short is not None:
+                bias = sl + bias
+            return conv2d_add_bias_relu_fork(h, wl, b, bias, mask_input)
     if last.fold and (short is None or short.conv.fold):
-        a, sa = last.conv_shift(h)
+        a, sa = last.conv_shift(h, folded_last)
         b, bias = (x, sa) if short is None else short.conv_shift(x)
         if short is not None:
             bias = sa + bias
@@ -293,7 +326,16 @@ class BasicBlock(nn.Module):
     def forward(self, x, x_short=None):
         """x feeds branch2a, x_short (default x) the shortcut; returns the
         (main, shortcut) handles of the output."""
-        return _block_out(self.branch2b, self.short, self.branch2a(x), x if x_short is None else x_short)
+        xs = x if x_short is None else x_short
+        a, b = self.branch2a, self.branch2b
+        if _FUSED_EPI and a.fold and b.fold and a.act_name == "relu" and x.is_cuda:
+            fa, fb = a.folded(), b.folded()
+            ok_a = a.hip_ok(x, x.shape[1], fa[0])
+            ok_b = b.hip_ok(x, fa[0].shape[0], fb[0])
+            pre_ab = ok_a and ok_b  # branch2b's dgrad masks branch2a's ReLU
+            h = a.bias_relu(x, fa, grad_premasked=pre_ab) if ok_a else a.bias_relu(x, fa)
+            return _block_out(b, self.short, h, xs, fb, mask_input=pre_ab)
+        return _block_out(self.branch2b, self.short, self.branch2a(x), xs)
 
 
 class BottleNeck(nn.Module):
@@ -309,9 +351,23 @@ class BottleNeck(nn.Module):
 
     def forward(self, x, x_short=None):
         """x feeds branch2a, x_short (default x) the shortcut; returns the
-        (main, shortcut) handles of the output."""
-        return _block_out(self.branch2c, self.short, self.branch2b(self.branch2a(x)),
-                          x if x_short is None else x_short)
+        (main, shortcut) handles of the output.  Fused (frozen BNs, HIP
+        convolutions): each branch's shift + ReLU is its convolution's
+        epilogue, the block output's residual add + ReLU is branch2c's, and
+        branch2a's / branch2b's ReLU backwards run in the dgrad epilogue of the
+        next convolution (their only consumer) where that one is HIP too."""
+        xs = x if x_short is None else x_short
+        a, b, c = self.branch2a, self.branch2b, self.branch2c
+        if _FUSED_EPI and a.fold and b.fold and c.fold and x.is_cuda:
+            fa, fb, fc = a.folded(), b.folded(), c.folded()
+            ok_a = a.hip_ok(x, x.shape[1], fa[0])
+            ok_b = b.hip_ok(x, fa[0].shape[0], fb[0])
+            ok_c = c.hip_ok(x, fb[0].shape[0], fc[0])
+            pre_ab, pre_bc = ok_a and ok_b, ok_b and ok_c
+            h1 = a.bias_relu(x, fa, grad_premasked=pre_ab)
+            h2 = b.bias_relu(h1, fb, mask_input=pre_ab, grad_premasked=pre_bc)
+            return _block_out(c, self.short, h2, xs, fc, mask_input=pre_bc)
+        return _block_out(self.branch2c, self.short, self.branch2b(self.branch2a(x)), xs)
 
 
 class PResNet(nn.Module):
@@ -411,9 +467,11 @@ def calibrate_frozen_bn(model: nn.Module, images: torch.Tensor, residual_gain: f
         mod.norm.running_var.copy_(y.var((0, 2, 3), unbiased=False))
         mod._w_folded = None  # refold with the new statistics
 
+    global _FUSED_EPI
+    fused_was, _FUSED_EPI = _FUSED_EPI, False  # the fused blocks bypass ConvNormLayer.forward (no hook would fire)
     hooks = [m.register_forward_pre_hook(pre) for m in layers]
     for m in layers:  # block outputs call conv_shift directly (no forward hook fires there)
-        m.conv_shift = (lambda x, _m=m, _f=m.conv_shift: (pre(_m, (x,)), _f(x))[1])
+        m.conv_shift = (lambda x, folded=None, _m=m, _f=m.conv_shift: (pre(_m, (x,)), _f(x))[1])
     for m in model.modules():
         if isinstance(m, PResNet):
             m._fold_plan = None  # the one-launch fold caches the scales: rebuilt on next use
@@ -428,4 +486,5 @@ def calibrate_frozen_bn(model: nn.Module, images: torch.Tensor, residual_gain: f
         for m in layers:
             del m.conv_shift
             m._w_folded = None
+        _FUSED_EPI = fused_was
     return len(layers)

@@ -37,57 +37,121 @@ def _nhwc(t):
 
 def hip_conv_ok(x, w, stride=1, padding=None, dilation=1, groups=1) -> bool:
     """Whether conv2d(x, w) runs on the HIP implicit-GEMM kernels."""
-    if not (_ENABLED[0] and x.is_cuda and x.dim() == 4 and w.dim() == 4):
+    if not (x.dim() == 4 and x.shape[0] > 0):
+        return False
+    return hip_conv_ok_for(x.is_cuda, x.dtype, x.shape[1], w, stride, padding, dilation, groups)
+
+
+def hip_conv_ok_for(is_cuda, dtype, cin, w, stride=1, padding=None, dilation=1, groups=1) -> bool:
+    """hip_conv_ok for an input of that device kind, dtype and channel count
+    (a consumer's check before its input exists)."""
+    if not (_ENABLED[0] and is_cuda and w.dim() == 4):
         return False
     N, C, kh, kw = w.shape
     ks = kh
     st = stride if isinstance(stride, int) else (stride[0] if stride[0] == stride[1] else -1)
     pd = padding if isinstance(padding, int) else (padding[0] if padding[0] == padding[1] else -1)
     dl = dilation if isinstance(dilation, int) else (dilation[0] if dilation[0] == dilation[1] else -1)
-    return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and kh == kw and ks in (1, 3) and st == 1
-            and pd == (ks - 1) // 2 and dl == 1 and groups == 1 and x.shape[1] == C and C % 128 == 0
-            and N % 128 == 0 and x.shape[0] > 0)
+    return (dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and kh == kw and ks in (1, 3) and st == 1
+            and pd == (ks - 1) // 2 and dl == 1 and groups == 1 and cin == C and C % 128 == 0 and N % 128 == 0)
+
+
+def _fwd(x, w, bias=None, resid=None, relu=False):
+    from ..moe import _lib as L
+
+    B, C, H, W = x.shape
+    N, _, ks, _ = w.shape
+    y = torch.empty((B, N, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    L._check(L.lib().rtdetr_conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), _zero(x.device).data_ptr(),
+                                     B, H, W, C, N, ks, None if bias is None else bias.data_ptr(),
+                                     None if resid is None else resid.data_ptr(), int(relu), L._stream()),
+             "rtdetr_conv_fwd")
+    return y
+
+
+def _bwd(x, w, g, need_x, need_w, mask_input):
+    """(dx, dw) of y = conv(x, w) for the output gradient g; dx is zeroed where
+    x <= 0 when mask_input (the ReLU backward of the activation x, fused)."""
+    from ..moe import _lib as L
+
+    B, C, H, W = x.shape
+    N, _, ks, _ = w.shape
+    g = _nhwc(g.to(torch.bfloat16))
+    z = _zero(x.device).data_ptr()
+    s = L._stream()
+    gx = gw = None
+    if need_x:
+        gx = torch.empty((B, C, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        nb = L.lib().rtdetr_conv_dgrad_workspace(B, H, W, C, N, ks)
+        work = torch.empty(nb // 2, dtype=torch.bfloat16, device=x.device) if nb > 0 else None
+        L._check(L.lib().rtdetr_conv_dgrad(g.data_ptr(), w.data_ptr(), None if work is None else work.data_ptr(),
+                                           gx.data_ptr(), z, B, H, W, C, N, ks,
+                                           x.data_ptr() if mask_input else None, s), "rtdetr_conv_dgrad")
+    if need_w:
+        ns = L.lib().rtdetr_conv_wgrad_splits(B, H, W, C, N, ks)
+        part = torch.empty(ns * N * C * ks * ks, dtype=torch.float32, device=x.device)
+        gw = torch.empty_like(w, memory_format=torch.channels_last)
+        L._check(L.lib().rtdetr_conv_wgrad(g.data_ptr(), x.data_ptr(), part.data_ptr(), ns, gw.data_ptr(), 1,
+                                           z, B, H, W, C, N, ks, s), "rtdetr_conv_wgrad")
+    return gx, gw
 
 
 class _ConvHIP(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, w):
-        from ..moe import _lib as L
+    """y = relu?(conv(x, w) + bias) on the HIP kernels (bias: frozen fp32
+    [N] or None, no gradient).
 
-        B, C, H, W = x.shape
-        N, _, ks, _ = w.shape
+    mask_input: x is a ReLU output whose ONLY consumer is this convolution;
+    the data gradient is then masked by (x > 0) in the dgrad epilogue, so the
+    producer may skip its own ReLU backward.  grad_premasked: this layer's
+    ReLU output feeds only a convolution that does that, so the incoming
+    gradient is already masked (no threshold pass here)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias=None, relu=False, mask_input=False, grad_premasked=False):
         x = _nhwc(x)
         w = _nhwc(w)
-        y = torch.empty((B, N, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
-        L._check(L.lib().rtdetr_conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), _zero(x.device).data_ptr(),
-                                         B, H, W, C, N, ks, L._stream()), "rtdetr_conv_fwd")
-        ctx.save_for_backward(x, w)
+        y = _fwd(x, w, bias, None, relu)
+        ctx.flags = (bool(relu) and not grad_premasked, bool(mask_input))
+        ctx.save_for_backward(x, w, y if ctx.flags[0] else None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
+        x, w, y = ctx.saved_tensors
+        relu_here, mask_input = ctx.flags
+        g = torch.ops.aten.threshold_backward(gy, y, 0) if relu_here else gy
+        gx, gw = _bwd(x, w, g, ctx.needs_input_grad[0], ctx.needs_input_grad[1], mask_input)
+        return gx, gw, None, None, None, None
+
+
+class _ConvHIPFork(torch.autograd.Function):
+    """(y, y') with y = relu((conv(x, w) + resid) + bias) and y' aliasing y: a
+    residual block's output for its two consumers (the next block's branch2a
+    and shortcut), the add and ReLU fused into the convolution's epilogue.
+    Backward: g = (dy + dy') * (y > 0) in one pass (rtdetr_relu_grad2_nhwc),
+    the gradient of both the convolution output and resid."""
+
+    @staticmethod
+    def forward(ctx, x, w, resid, bias, mask_input=False):
+        x = _nhwc(x)
+        w = _nhwc(w)
+        y = _fwd(x, w, bias, _nhwc(resid), True)
+        ctx.mask_input = bool(mask_input)
+        ctx.save_for_backward(x, w, y)
+        return y, y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, dy1, dy2):
         from ..moe import _lib as L
 
-        x, w = ctx.saved_tensors
-        B, C, H, W = x.shape
-        N, _, ks, _ = w.shape
-        gy = _nhwc(gy.to(torch.bfloat16))
-        z = _zero(x.device).data_ptr()
-        s = L._stream()
-        gx = gw = None
-        if ctx.needs_input_grad[0]:
-            gx = torch.empty((B, C, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
-            nb = L.lib().rtdetr_conv_dgrad_workspace(B, H, W, C, N, ks)
-            work = torch.empty(nb // 2, dtype=torch.bfloat16, device=x.device) if nb > 0 else None
-            L._check(L.lib().rtdetr_conv_dgrad(gy.data_ptr(), w.data_ptr(), None if work is None else work.data_ptr(),
-                                               gx.data_ptr(), z, B, H, W, C, N, ks, s), "rtdetr_conv_dgrad")
-        if ctx.needs_input_grad[1]:
-            ns = L.lib().rtdetr_conv_wgrad_splits(B, H, W, C, N, ks)
-            part = torch.empty(ns * N * C * ks * ks, dtype=torch.float32, device=x.device)
-            gw = torch.empty_like(w, memory_format=torch.channels_last)
-            L._check(L.lib().rtdetr_conv_wgrad(gy.data_ptr(), x.data_ptr(), part.data_ptr(), ns, gw.data_ptr(), 1,
-                                               z, B, H, W, C, N, ks, s), "rtdetr_conv_wgrad")
-        return gx, gw
+        x, w, y = ctx.saved_tensors
+        if dy1 is None and dy2 is None:
+            return None, None, None, None, None
+        if dy1 is None:
+            dy1, dy2 = dy2, None
+        g = L.relu_grad2_nhwc(_nhwc(dy1), None if dy2 is None else _nhwc(dy2), y)
+        gx, gw = _bwd(x, w, g, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.mask_input)
+        return gx, gw, g if ctx.needs_input_grad[2] else None, None, None
 
 
 def conv2d(x, weight, stride=1, padding=0):
@@ -96,6 +160,19 @@ def conv2d(x, weight, stride=1, padding=0):
     if hip_conv_ok(x, weight, stride, padding):
         return _ConvHIP.apply(x, weight)
     return F.conv2d(x, weight, None, stride, padding)
+
+
+def conv2d_bias_relu(x, weight, bias, mask_input=False, grad_premasked=False):
+    """relu(conv2d(x, weight) + bias[c]) in one HIP launch (stride 1, "same"
+    padding; the caller checked hip_conv_ok).  bias: fp32 [Cout], no gradient.
+    See _ConvHIP for mask_input / grad_premasked."""
+    return _ConvHIP.apply(x, weight, bias.float().contiguous(), True, mask_input, grad_premasked)
+
+
+def conv2d_add_bias_relu_fork(x, weight, resid, bias, mask_input=False):
+    """(y, y) with y = relu((conv2d(x, weight) + resid) + bias[c]) in one HIP
+    launch -- see _ConvHIPFork."""
+    return _ConvHIPFork.apply(x, weight, resid, None if bias is None else bias.float().contiguous(), mask_input)
 
 
 def conv_module(conv: torch.nn.Conv2d, x):

@@ -98,3 +98,68 @@ def test_conv_dispatch_rules(hip_lib):
     assert not hip_conv_ok(x.float(), w3.float(), 1, 1)
     assert not hip_conv_ok(torch.zeros(1, 64, 8, 8, device=DEV, dtype=torch.bfloat16),
                            torch.zeros(64, 64, 3, 3, device=DEV, dtype=torch.bfloat16), 1, 1)
+
+
+@pytest.mark.parametrize("ks", [1, 3])
+def test_conv_fused_epilogues_match_separate_kernels(hip_lib, ks):
+    """The forward epilogue relu((conv + resid) + bias) and the dgrad's ReLU
+    mask equal the separate kernels they replace (rtdetr_add_bias_relu_nhwc,
+    rtdetr_bias_act_nhwc, threshold_backward) bit for bit."""
+    from src.moe import _lib as L
+    from src.rtdetr_moe import conv as C
+
+    g = torch.Generator(device=DEV).manual_seed(5 + ks)
+    B, Ci, Co, H, W = 2, 256, 128, 11, 13
+    cl = dict(memory_format=torch.channels_last)
+    x = torch.randn(B, Ci, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(**cl)
+    w = (torch.randn(Co, Ci, ks, ks, device=DEV, generator=g) * (Ci * ks * ks) ** -0.5).to(torch.bfloat16).contiguous(**cl)
+    bias = torch.randn(Co, device=DEV, generator=g) * 0.3
+    resid = torch.randn(B, Co, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(**cl)
+    plain = C._fwd(x, w)
+    assert torch.equal(C._fwd(x, w, bias, resid, True), L.add_bias_relu_nhwc(plain, resid, bias))
+    assert torch.equal(C._fwd(x, w, bias, None, True), L.bias_act_nhwc(plain.clone(), bias, True))
+    gy = torch.randn(B, Co, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(**cl)
+    xr = torch.relu(x)  # a ReLU output feeding the convolution
+    gx_m, gw_m = C._bwd(xr, w, gy, True, True, True)
+    gx, gw = C._bwd(xr, w, gy, True, True, False)
+    torch.cuda.synchronize()
+    assert torch.equal(gx_m, torch.ops.aten.threshold_backward(gx, xr, 0)) and torch.equal(gw_m, gw)
+
+
+@pytest.mark.parametrize("cin,width,stride,shortcut", [(512, 128, 1, True), (256, 128, 2, False), (1024, 256, 1, True)])
+def test_bottleneck_fused_matches_unfused(hip_lib, cin, width, stride, shortcut):
+    """A frozen-BN ResNet bottleneck with the fused convolution epilogues
+    (MOE_CONV_EPI, default) against the separate bias / add / ReLU kernels:
+    output handles, input gradient and every weight gradient bitwise equal
+    (stride 2 / projection shortcut: the mixed fused + MIOpen case)."""
+    from src.rtdetr_moe import backbone as BB
+
+    torch.manual_seed(3)
+    blk = BB.BottleNeck(cin, width, stride, shortcut, True).to(DEV)
+    blk = blk.to(torch.bfloat16).to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        for m in blk.modules():
+            if isinstance(m, BB.FrozenBatchNorm2d):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 2.0)
+                m.bias.uniform_(-0.3, 0.3)
+    x0 = torch.randn(2, cin, 24, 40, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g1 = torch.randn(2, width * 4, 24 // stride, 40 // stride, device=DEV).to(torch.bfloat16)
+    g2 = torch.randn_like(g1)
+    res = []
+    for fused in (True, False):
+        BB._FUSED_EPI = fused
+        try:
+            x = x0.clone().requires_grad_(True)
+            y1, y2 = blk(x)
+            params = [p for p in blk.parameters() if p.requires_grad]
+            grads = torch.autograd.grad([y1, y2], [x] + params, [g1.contiguous(memory_format=torch.channels_last),
+                                                               g2.contiguous(memory_format=torch.channels_last)])
+            torch.cuda.synchronize()
+            res.append((y1.detach().clone(), [gg.clone() for gg in grads]))
+        finally:
+            BB._FUSED_EPI = True
+    (ya, ga), (yb, gb) = res
+    assert torch.equal(ya, yb)
+    for u, v in zip(ga, gb):
+        assert torch.equal(u, v)
