@@ -33,8 +33,9 @@
 
 namespace moe {
 
-constexpr int CV_BM = 128, CV_BN = 128;             // weight-gradient tile
-constexpr int CV_TILE = (CV_BM + CV_BN) * 64 * 2;  // bytes of one weight-gradient ring stage
+// weight-gradient tile: 128 x 128, 64 on a side with 64 channels
+static int wg_bm(int N) { return N % 128 == 0 ? 128 : 64; }
+static int wg_bn(int C) { return C % 128 == 0 ? 128 : 64; }
 // rtdetr_conv_set_tuning knobs (measurement / A-B; 0 or -1 = automatic)
 static int g_conv_bm = 0;          // "conv_bm": forward tile rows 64, 128 or 256
 static int g_conv_wg_stages = 0;   // "conv_wg_stages": weight-gradient ring depth 2..4
@@ -83,11 +84,12 @@ __device__ __forceinline__ void dma16(const uint16_t* src, char* lds) {
 // ---------------------------------------------------------------------------
 // forward / data gradient
 // ---------------------------------------------------------------------------
-template <int KS, int S, int BM, bool BT>
+template <int KS, int S, int BM, int BN, bool BT>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int BN = 128;
+  static_assert(BN == 64 || BN == 128, "output-channel tile: 64 or 128");
   constexpr int TILE = (BM + BN) * 128;  // bytes of one ring stage
+  constexpr int CPR = BN / 8;            // 16-B chunks per output row of the tile
   constexpr int TM = BM / 32, TN = BN / 32;
   constexpr int GW = BM / 32 + BN / 32;  // DMA instructions per wave per K-tile
   constexpr int PAD = (KS - 1) / 2;
@@ -127,9 +129,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   const uint16_t* wrow[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    if constexpr (BT) {
-      const int kr = (wave + 4 * j) * 4 + (lane >> 4);
-      wrow[j] = a.w + (size_t)kr * (KS * KS * a.N) + n0 + ((lane & 15) ^ mimg_swz<128>(kr)) * 8;
+    if constexpr (BT) {  // CPR lanes per k-row
+      const int kr = (wave + 4 * j) * (64 / CPR) + lane / CPR;
+      wrow[j] = a.w + (size_t)kr * (KS * KS * a.N) + n0 + ((lane % CPR) ^ mimg_swz<BN>(kr)) * 8;
     } else {
       const int r = (wave + 4 * j) * 8 + (lane >> 3);
       wrow[j] = a.w + (size_t)(n0 + r) * (KS * KS * a.C) + ((lane & 7) ^ ((r >> 1) & 7)) * 8;
@@ -170,16 +172,17 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     compute_tile<BM, BN, true, !BT, false>(cur, cur + BM * 128, acc, csum, lane, wm, wn);
   }
   // Epilogue through LDS: lane holds Y[m0 + wm BM/2 + 16 i + (lane & 15)][n0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3];
-  // the tile goes to a row-major [BM][128] bf16 image (16-B chunk c of row r at chunk c ^ (r & 15):
+  // the tile goes to a row-major [BM][BN] bf16 image (16-B chunk c of row r at chunk c ^ (r % CPR):
   // conflict-free 8-B writes and 16-B reads), then out as whole 256-B rows of 16-B stores
   // (register-direct 8-B stores at a row stride run at about half that rate).  The fused
   // epilogue's operands (same 16-B chunks as the stores) are loaded first, behind the image.
-  const int ec = tid & 15;
-  uint4 eres[BM / 16], emask[BM / 16];
+  constexpr int RPP = 256 / CPR;  // rows per store pass
+  const int ec = tid % CPR;
+  uint4 eres[BM / RPP], emask[BM / RPP];
   if (a.resid != nullptr || a.mask != nullptr) {
 #pragma unroll
-    for (int k = 0; k < BM / 16; ++k) {
-      const int p = m0 + (tid >> 4) + 16 * k;
+    for (int k = 0; k < BM / RPP; ++k) {
+      const int p = m0 + tid / CPR + RPP * k;
       const size_t g = (size_t)(p < a.P ? p : 0) * a.N + n0 + ec * 8;
       if (a.resid != nullptr) eres[k] = *reinterpret_cast<const uint4*>(a.resid + g);
       if (a.mask != nullptr) emask[k] = *reinterpret_cast<const uint4*>(a.mask + g);
@@ -203,16 +206,16 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
       uint2 v;
       v.x = pack2bf(acc[i][j][0], acc[i][j][1]);
       v.y = pack2bf(acc[i][j][2], acc[i][j][3]);
-      *reinterpret_cast<uint2*>(smem + r * 256 + (((col >> 3) ^ (r & 15)) << 4) + (col & 7) * 2) = v;
+      *reinterpret_cast<uint2*>(smem + r * (BN * 2) + (((col >> 3) ^ (r % CPR)) << 4) + (col & 7) * 2) = v;
     }
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < BM / 16; ++k) {
-    const int r = (tid >> 4) + 16 * k, c = ec;
+  for (int k = 0; k < BM / RPP; ++k) {
+    const int r = tid / CPR + RPP * k, c = ec;
     const int p = m0 + r;
     if (p < a.P) {
-      uint4 v = *reinterpret_cast<const uint4*>(smem + r * 256 + ((c ^ (r & 15)) << 4));
+      uint4 v = *reinterpret_cast<const uint4*>(smem + r * (BN * 2) + ((c ^ (r % CPR)) << 4));
       if (efloat) {
         float f[8];
         unpack8(v, f);
@@ -280,17 +283,22 @@ struct ConvWgArgs {
   int nsplit, kt_per;    // pixel K-tiles per slice
 };
 
-template <int KS, int S>
+// Tile WBM (output channels) x WBN (tap-major input channels of one tap):
+// 128 x 128, or 64 on a side with 64 channels (ResNet stage 1).
+template <int KS, int S, int WBM, int WBN>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TM = CV_BM / 32, TN = CV_BN / 32;
-  constexpr int GW = 64 * 2 * (CV_BM + CV_BN) / 1024 / 4;  // DMA instructions per wave per K-tile
+  constexpr int TM = WBM / 32, TN = WBN / 32;
+  constexpr int TILE = (WBM + WBN) * 128;  // bytes of one ring stage
+  // DMA: LA (LB) lanes per 2 WBM- (WBN-) byte k-row, NA (NB) instructions per wave per K-tile
+  constexpr int LA = WBM / 8, LB = WBN / 8, NA = LA / 4, NB = LB / 4;
+  constexpr int GW = NA + NB;
   constexpr int PAD = (KS - 1) / 2;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int NN = KS * KS * a.C;      // GEMM N
-  const int MT = a.N / CV_BM, NT = NN / CV_BN;
+  const int MT = a.N / WBM, NT = NN / WBN;
   // work units u = split * tiles + tile, a contiguous run of ceil(units / 8)
   // per XCD: the tiles of one pixel slice share an XCD (its dY and X rows
   // stream through that L2 once; slices of one tile spread over XCDs made
@@ -302,42 +310,51 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
   if (local >= per_xcd || u >= units) return;
   const int tile = u % tiles, split = u / tiles;
   const int mt = tile % MT, nt = tile / MT;
-  const int m0 = mt * CV_BM, nn0 = nt * CV_BN;
+  const int m0 = mt * WBM, nn0 = nt * WBN;
   const int tap = nn0 / a.C, c0 = nn0 - tap * a.C;
   const int dy_ = tap / KS - PAD, dx_ = tap % KS - PAD;
   const int ktot = (a.P + 63) / 64;
   const int kt0 = split * a.kt_per;
   const int nk = max(0, min(a.kt_per, ktot - kt0));
   const int HW = a.H * a.W;
-  // k-row (pixel) of this lane in DMA instruction j: kr = (wave + 4 j) * 4 + lane / 16 (256-B rows);
-  // its (image, y, x) is kept and advanced by 64 pixels per K-tile (no divisions in the loop)
-  int ach[4], pp[4], py[4], px[4];
+  // A (dY) k-row of this lane in instruction j: (wave + 4 j) (64 / LA) + lane / LA; its pixel
+  // advances by 64 per K-tile.  B (X) k-rows likewise, with the pixel's (y, x) kept and
+  // advanced incrementally (no divisions in the loop) for the neighbour's bounds.
+  int cha[NA], pa[NA], chb[NB], pb[NB], py[NB], px[NB];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int kr = (wave + 4 * j) * 4 + (lane >> 4);
-    ach[j] = ((lane & 15) ^ mimg_swz<128>(kr)) * 8;
+  for (int j = 0; j < NA; ++j) {
+    const int kr = (wave + 4 * j) * (64 / LA) + lane / LA;
+    cha[j] = ((lane % LA) ^ mimg_swz<WBM>(kr)) * 8;
+    pa[j] = kt0 * 64 + kr;
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int kr = (wave + 4 * j) * (64 / LB) + lane / LB;
+    chb[j] = ((lane % LB) ^ mimg_swz<WBN>(kr)) * 8;
     const int p = kt0 * 64 + kr;
-    pp[j] = p;
+    pb[j] = p;
     const int q = p < a.P ? p : 0;
     const int rem = q % HW;
     py[j] = rem / a.W;
     px[j] = rem - py[j] * a.W;
   }
   auto issue = [&](int kt) {
-    char* buf = smem + (kt % S) * CV_TILE;
+    char* buf = smem + (kt % S) * TILE;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int p = pp[j];
-      const bool pv = p < a.P;
+    for (int j = 0; j < NA; ++j) {
+      const int p = pa[j];
+      dma16(p < a.P ? a.dy + (size_t)p * a.N + m0 + cha[j] : a.zero + cha[j], buf + (wave + 4 * j) * 1024);
+      pa[j] = p + 64;
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int p = pb[j];
       const int yy = py[j] + dy_, xx = px[j] + dx_;
-      const bool ok = pv && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+      const bool ok = p < a.P && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
       const long long nb = (long long)p + (long long)dy_ * a.W + dx_;  // the neighbour's flat pixel index
-      const uint16_t* sa = pv ? a.dy + (size_t)p * a.N + m0 + ach[j] : a.zero + ach[j];
-      const uint16_t* sb = ok ? a.x + (size_t)nb * a.C + c0 + ach[j] : a.zero + ach[j];
-      dma16(sa, buf + (wave + 4 * j) * 1024);
-      dma16(sb, buf + CV_BM * 128 + (wave + 4 * j) * 1024);
+      dma16(ok ? a.x + (size_t)nb * a.C + c0 + chb[j] : a.zero + chb[j], buf + WBM * 128 + (wave + 4 * j) * 1024);
       // next K-tile: 64 pixels on (row-major within the image; images are contiguous)
-      pp[j] = p + 64;
+      pb[j] = p + 64;
       int x = px[j] + 64, y = py[j];
       while (x >= a.W) {
         x -= a.W;
@@ -360,15 +377,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
     wait_ring<S, GW>(nk - 1 - kt);
     __builtin_amdgcn_s_barrier();
     if (kt + S - 1 < nk) issue(kt + S - 1);
-    const char* cur = smem + (kt % S) * CV_TILE;
-    compute_tile<CV_BM, CV_BN, false, false, false>(cur, cur + CV_BM * 128, acc, csum, lane, wm, wn);
+    const char* cur = smem + (kt % S) * TILE;
+    compute_tile<WBM, WBN, false, false, false>(cur, cur + WBM * 128, acc, csum, lane, wm, wn);
   }
-  // lane holds dW[m0 + wm 64 + 16 i + (lane & 15)][nn0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3]
+  // lane holds dW[m0 + wm WBM/2 + 16 i + (lane & 15)][nn0 + wn WBN/2 + 16 j + 4 (lane >> 4) + 0..3]
   float* out = a.part + (size_t)split * a.N * NN;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wm * (CV_BM / 2) + 16 * i + (lane & 15);
-    float* row = out + (size_t)m * NN + nn0 + wn * (CV_BN / 2) + 4 * (lane >> 4);
+    const int m = m0 + wm * (WBM / 2) + 16 * i + (lane & 15);
+    float* row = out + (size_t)m * NN + nn0 + wn * (WBN / 2) + 4 * (lane >> 4);
 #pragma unroll
     for (int j = 0; j < TN; ++j)
       *reinterpret_cast<float4*>(row + 16 * j) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
@@ -376,17 +393,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
 }
 
 // dW = sum of the slices' fp32 partials in a fixed order, written as bf16 or
-// fp32.  A workgroup owns 64 float4 columns; its 4 waves sum the slices
-// k = wave (mod 4) in increasing k, then wave 0 adds the 4 sums in wave order
-// (so a weight with few output tiles still spreads over the whole chip).
+// fp32.  A workgroup owns 16 float4 columns; its 16 thread groups sum the
+// slices k = group (mod 16) in increasing k, then group 0 adds the 16 sums in
+// group order (a weight with few output tiles is cut into up to 256 slices;
+// this keeps the sum spread over the chip and short per thread).
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part, int nsplit,
                                                                 long long n, void* __restrict__ dw, int out_bf16) {
-  __shared__ float4 red[3][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long long i = (blockIdx.x * 64ll + lane) * 4;
+  __shared__ float4 red[15][16];
+  const int col = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const long long i = (blockIdx.x * 16ll + col) * 4;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < n) {
-    for (int k = wave; k < nsplit; k += 4) {
+    for (int k = grp; k < nsplit; k += 16) {
       const float4 v = *reinterpret_cast<const float4*>(part + (size_t)k * n + i);
       s.x += v.x;
       s.y += v.y;
@@ -394,12 +412,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __r
       s.w += v.w;
     }
   }
-  if (wave) red[wave - 1][lane] = s;
+  if (grp) red[grp - 1][col] = s;
   __syncthreads();
-  if (wave || i >= n) return;
+  if (grp || i >= n) return;
 #pragma unroll
-  for (int g = 0; g < 3; ++g) {
-    const float4 v = red[g][lane];
+  for (int g = 0; g < 15; ++g) {
+    const float4 v = red[g][col];
     s.x += v.x;
     s.y += v.y;
     s.z += v.z;
@@ -427,8 +445,8 @@ static void allow_lds_once(size_t bytes) {
 static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int C, int N, int KS, const char* what) {
   if (KS != 1 && KS != 3) return fail(std::string(what) + ": kernel size must be 1 or 3");
   if (B < 0 || H <= 0 || W <= 0) return fail(std::string(what) + ": bad B / H / W");
-  if (C % 128 || N % 128 || C <= 0 || N <= 0)
-    return fail(std::string(what) + ": channels must be positive multiples of 128");
+  if (C % 64 || N % 64 || C <= 0 || N <= 0)
+    return fail(std::string(what) + ": channels must be positive multiples of 64");
   if ((long long)B * H * W * (C > N ? C : N) >= (1ll << 31)) return fail(std::string(what) + ": tensor too large");
   for (int i = 0; i < np; ++i)
     if (ptrs[i] == nullptr || reinterpret_cast<uintptr_t>(ptrs[i]) % 16)
@@ -438,14 +456,21 @@ static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int 
 
 constexpr int CV_STAGES = 2;
 
-template <int KS, int BM, bool BT>
-static void launch_fwd(ConvArgs a, hipStream_t stream, ProfScope& prof) {
-  constexpr size_t lds = CV_STAGES * (BM + 128) * 128;
-  allow_lds_once<conv_fwd_kernel<KS, CV_STAGES, BM, BT>>(lds);
+template <int KS, int BM, int BN, bool BT>
+static void launch_fwd_n(ConvArgs a, hipStream_t stream, ProfScope& prof) {
+  constexpr size_t lds = CV_STAGES * (BM + BN) * 128;
+  static_assert(lds >= BM * BN * 2, "epilogue image exceeds the ring");
+  allow_lds_once<conv_fwd_kernel<KS, CV_STAGES, BM, BN, BT>>(lds);
   a.mt_n = (a.P + BM - 1) / BM;
-  const int NT = a.N / 128;
+  const int NT = a.N / BN;
   const int grid = ((a.mt_n + 7) / 8) * 8 * NT;
-  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, CV_STAGES, BM, BT>), dim3(grid), dim3(256), lds, stream, a);
+  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, CV_STAGES, BM, BN, BT>), dim3(grid), dim3(256), lds, stream, a);
+}
+// output-channel tiles of 128, or 64 for 64-channel outputs (ResNet stage 1)
+template <int KS, int BM, bool BT>
+static void launch_fwd(const ConvArgs& a, hipStream_t stream, ProfScope& prof) {
+  if (a.N % 128 == 0) launch_fwd_n<KS, BM, 128, BT>(a, stream, prof);
+  else launch_fwd_n<KS, BM, 64, BT>(a, stream, prof);
 }
 
 // tile rows: 128 (two workgroups per CU); 64 when 128-row tiles would leave
@@ -454,7 +479,8 @@ static void launch_fwd(ConvArgs a, hipStream_t stream, ProfScope& prof) {
 template <bool BT>
 static void launch_fwd_any(const ConvArgs& a, int KS, hipStream_t stream, ProfScope& prof) {
   int bm = g_conv_bm;
-  if (bm != 64 && bm != 128 && bm != 256) bm = (long long)((a.P + 127) / 128) * (a.N / 128) < 384 ? 64 : 128;
+  if (bm != 64 && bm != 128 && bm != 256)
+    bm = (long long)((a.P + 127) / 128) * (a.N / (a.N % 128 == 0 ? 128 : 64)) < 384 ? 64 : 128;
   if (KS == 3) {
     if (bm == 256) launch_fwd<3, 256, BT>(a, stream, prof);
     else if (bm == 64) launch_fwd<3, 64, BT>(a, stream, prof);
@@ -466,13 +492,21 @@ static void launch_fwd_any(const ConvArgs& a, int KS, hipStream_t stream, ProfSc
   }
 }
 
+template <int KS, int S, int WBM, int WBN>
+static void launch_wgrad_t(const ConvWgArgs& a, hipStream_t stream, ProfScope& prof) {
+  constexpr size_t lds = S * (WBM + WBN) * 128;
+  allow_lds_once<conv_wgrad_kernel<KS, S, WBM, WBN>>(lds);
+  const int tiles = (a.N / WBM) * (KS * KS * a.C / WBN);
+  const int grid = (tiles * a.nsplit + 7) / 8 * 8;
+  MOE_LAUNCH(prof, (conv_wgrad_kernel<KS, S, WBM, WBN>), dim3(grid), dim3(256), lds, stream, a);
+}
 template <int KS, int S>
 static void launch_wgrad_s(const ConvWgArgs& a, hipStream_t stream, ProfScope& prof) {
-  constexpr size_t lds = S * CV_TILE;
-  allow_lds_once<conv_wgrad_kernel<KS, S>>(lds);
-  const int tiles = (a.N / CV_BM) * (KS * KS * a.C / CV_BN);
-  const int grid = (tiles * a.nsplit + 7) / 8 * 8;
-  MOE_LAUNCH(prof, (conv_wgrad_kernel<KS, S>), dim3(grid), dim3(256), lds, stream, a);
+  const int bm = wg_bm(a.N), bn = wg_bn(a.C);
+  if (bm == 128 && bn == 128) launch_wgrad_t<KS, S, 128, 128>(a, stream, prof);
+  else if (bm == 128) launch_wgrad_t<KS, S, 128, 64>(a, stream, prof);
+  else if (bn == 128) launch_wgrad_t<KS, S, 64, 128>(a, stream, prof);
+  else launch_wgrad_t<KS, S, 64, 64>(a, stream, prof);
 }
 
 // 2-deep ring (64 KiB, two workgroups per CU): deeper rings (1 per CU)
@@ -553,13 +587,14 @@ extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void
 extern "C" int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS) {
   // as many pixel slices as keep tiles x slices <= 512 (every workgroup
   // resident at once, two per CU: a second round on a few CUs doubles the
-  // time), each slice >= 8 pixel K-tiles, <= 64 (each slice costs an fp32
-  // partial of the weight)
-  const long long tiles = (long long)(N / CV_BM) * (KS * KS * C / CV_BN);
+  // time), each slice >= 8 pixel K-tiles, <= 256 (each slice costs an fp32
+  // partial of the weight; the stage-1 1x1 weights are 1-2 tiles)
+  if (N <= 0 || C <= 0 || N % 64 || C % 64) return 1;
+  const long long tiles = (long long)(N / wg_bm(N)) * (KS * KS * C / wg_bn(C));
   const long long ktot = ((long long)B * H * W + 63) / 64;
   long long s = 512 / std::max(1ll, tiles);
   s = std::min(s, std::max(1ll, ktot / 8));
-  s = std::min(s, 64ll);
+  s = std::min(s, 256ll);
   if (g_conv_wg_splits > 0) s = std::min<long long>(g_conv_wg_splits, std::max(1ll, ktot));
   return (int)std::max(1ll, s);
 }
@@ -568,7 +603,7 @@ extern "C" int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int
                                  const void* zero, int B, int H, int W, int C, int N, int KS, hipStream_t stream) {
   const void* ptrs[5] = {dy, x, part, dw, zero};
   if (int rc = conv_check(ptrs, 5, B, H, W, C, N, KS, "rtdetr_conv_wgrad")) return rc;
-  if (nsplit < 1 || nsplit > 128) return fail("rtdetr_conv_wgrad: nsplit must be 1..128");
+  if (nsplit < 1 || nsplit > 256) return fail("rtdetr_conv_wgrad: nsplit must be 1..256");
   ConvWgArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(x), part,
                static_cast<const uint16_t*>(zero), B, H, W, C, N, B * H * W, nsplit, 0};
   const int ktot = (a.P + 63) / 64;
@@ -582,7 +617,7 @@ extern "C" int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int
     if (int rc = check_launch("rtdetr_conv_wgrad")) return rc;
   }
   ProfScope prof(stream, PROF_CONV, 4.0 * nsplit * nw + (out_bf16 ? 2.0 : 4.0) * nw);
-  MOE_LAUNCH(prof, conv_wgrad_reduce_kernel, dim3((unsigned)((nw / 4 + 63) / 64)), dim3(256), 0, stream, part,
+  MOE_LAUNCH(prof, conv_wgrad_reduce_kernel, dim3((unsigned)((nw / 4 + 15) / 16)), dim3(256), 0, stream, part,
              nsplit, nw, dw, out_bf16);
   return check_launch("rtdetr_conv_wgrad (reduce)");
 }

@@ -3,9 +3,9 @@
 
 ``conv2d(x, weight, stride, padding)`` takes the HIP kernels for the
 convolutions they cover -- stride 1, "same" padding, 1x1 or 3x3, no groups,
-channel counts that are multiples of 128, bf16 channels_last activations and
+channel counts that are multiples of 64, bf16 channels_last activations and
 weights on the GPU (the HybridEncoder's RepVGG / CSP layers and the ResNet
-bottleneck convolutions of 128 / 256 / 512 / 1024 / 2048 channels) -- and
+bottleneck convolutions of 64 .. 2048 channels) -- and
 F.conv2d (MIOpen) for the rest.  Forward: one implicit-GEMM launch (no im2col
 buffer).  Backward: the data gradient is the same kernel over dY with the
 weight flipped and transposed (written to a workspace for large problems,
@@ -53,7 +53,7 @@ def hip_conv_ok_for(is_cuda, dtype, cin, w, stride=1, padding=None, dilation=1, 
     pd = padding if isinstance(padding, int) else (padding[0] if padding[0] == padding[1] else -1)
     dl = dilation if isinstance(dilation, int) else (dilation[0] if dilation[0] == dilation[1] else -1)
     return (dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and kh == kw and ks in (1, 3) and st == 1
-            and pd == (ks - 1) // 2 and dl == 1 and groups == 1 and cin == C and C % 128 == 0 and N % 128 == 0)
+            and pd == (ks - 1) // 2 and dl == 1 and groups == 1 and cin == C and C % 64 == 0 and N % 64 == 0)
 
 
 def _fwd(x, w, bias=None, resid=None, relu=False):

@@ -25,7 +25,9 @@ import torch.nn.functional as F  # noqa: E402
 SHAPES = [(8, 256, 256, 46, 80, 3), (8, 256, 256, 92, 160, 3), (8, 256, 256, 23, 40, 3), (8, 128, 128, 92, 160, 3),
           (8, 512, 512, 23, 40, 3), (8, 256, 256, 46, 80, 1), (8, 256, 256, 92, 160, 1), (8, 1024, 256, 46, 80, 1),
           (8, 256, 1024, 46, 80, 1), (8, 512, 128, 92, 160, 1), (8, 128, 512, 92, 160, 1), (8, 2048, 512, 23, 40, 1),
-          (8, 512, 2048, 23, 40, 1), (8, 512, 256, 92, 160, 1)]
+          (8, 512, 2048, 23, 40, 1), (8, 512, 256, 92, 160, 1),
+          # ResNet stage 1 (64-channel tiles)
+          (8, 64, 64, 184, 320, 3), (8, 256, 64, 184, 320, 1), (8, 64, 256, 184, 320, 1), (8, 64, 64, 184, 320, 1)]
 
 
 def timeit(fn, reps=20):
