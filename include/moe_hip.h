@@ -541,9 +541,12 @@ int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, 
  *                           written to work first when
  *                           rtdetr_conv_dgrad_workspace() > 0 (bytes; large
  *                           problems), else read in place from w (work may be
- *                           NULL); relu_mask (bf16 [B,H,W,C] or NULL): dx = 0
- *                           where relu_mask <= 0 (the ReLU backward of the
- *                           activation that fed the convolution, fused)
+ *                           NULL); add (bf16 [B,H,W,C] or NULL): dx += add
+ *                           (fp32 sum of the two bf16 values); relu_mask (bf16
+ *                           [B,H,W,C] or NULL): then dx = 0 where relu_mask <= 0
+ *                           (the ReLU backward of the activation that fed the
+ *                           convolution, with its other consumer's gradient
+ *                           'add' -- rtdetr_relu_grad2_nhwc's arithmetic, fused)
  *   rtdetr_conv_wgrad       dw[N][KS][KS][C] = sum over pixels dy (x) x[neighbour]:
  *                           nsplit pixel slices write fp32 partials to part
  *                           [nsplit][N KS KS C], summed in slice order
@@ -553,7 +556,7 @@ int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void* zero, int
                     int KS, const float* bias, const void* resid, int relu, hipStream_t stream);
 long long rtdetr_conv_dgrad_workspace(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void* dx, const void* zero, int B, int H, int W,
-                      int C, int N, int KS, const void* relu_mask, hipStream_t stream);
+                      int C, int N, int KS, const void* add, const void* relu_mask, hipStream_t stream);
 int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
                       const void* zero, int B, int H, int W, int C, int N, int KS, hipStream_t stream);

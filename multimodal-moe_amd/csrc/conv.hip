@@ -554,10 +554,11 @@ extern "C" long long rtdetr_conv_dgrad_workspace(int B, int H, int W, int C, int
 }
 
 extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void* dx, const void* zero, int B, int H,
-                                 int W, int C, int N, int KS, const void* relu_mask, hipStream_t stream) {
+                                 int W, int C, int N, int KS, const void* add, const void* relu_mask,
+                                 hipStream_t stream) {
   const void* ptrs[4] = {dy, w, dx, zero};
   if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, "rtdetr_conv_dgrad")) return rc;
-  if (!aligned16(relu_mask)) return fail("rtdetr_conv_dgrad: relu_mask must be 16-B aligned");
+  if (!aligned16(relu_mask) || !aligned16(add)) return fail("rtdetr_conv_dgrad: add / relu_mask must be 16-B aligned");
   const bool flip = rtdetr_conv_dgrad_workspace(B, H, W, C, N, KS) > 0;
   if (flip && (work == nullptr || reinterpret_cast<uintptr_t>(work) % 16))
     return fail("rtdetr_conv_dgrad: this shape needs a 16-B aligned workspace of rtdetr_conv_dgrad_workspace() bytes");
@@ -565,7 +566,7 @@ extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void
   // the forward GEMM over dY [P][N] with W'
   ConvArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(dx),
              static_cast<const uint16_t*>(zero), B, H, W, N, C, B * H * W, 0,
-             nullptr, nullptr, static_cast<const uint16_t*>(relu_mask), 0};
+             nullptr, static_cast<const uint16_t*>(add), static_cast<const uint16_t*>(relu_mask), 0};
   const double P = a.P;
   if (flip) {
     const long long total = (long long)N * C * KS * KS;
@@ -577,7 +578,8 @@ extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void
     }
     a.w = static_cast<const uint16_t*>(work);
   }
-  ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N + (relu_mask ? C : 0)) + 2.0 * N * KS * KS * C, false, 0.0,
+  ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N + (relu_mask ? C : 0) + (add ? C : 0)) + 2.0 * N * KS * KS * C,
+                 false, 0.0,
                  2.0 * P * N * KS * KS * C);
   if (flip) launch_fwd_any<false>(a, KS, stream, prof);
   else launch_fwd_any<true>(a, KS, stream, prof);

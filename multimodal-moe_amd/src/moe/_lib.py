@@ -91,7 +91,7 @@ SIGNATURES = {
                              _I, _I, _I, _I, _F, _P]),
     "rtdetr_conv_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
     "rtdetr_conv_dgrad_workspace": (_LL, [_I, _I, _I, _I, _I, _I]),
-    "rtdetr_conv_dgrad": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "rtdetr_conv_dgrad": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "rtdetr_conv_wgrad_splits": (_I, [_I, _I, _I, _I, _I, _I]),
     "rtdetr_conv_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "rtdetr_conv_wgrad": (_I, [_P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P]),

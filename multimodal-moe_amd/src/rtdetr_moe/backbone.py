@@ -204,12 +204,12 @@ class ConvNormLayer(nn.Module):
         return (_FUSED_EPI and self.fold and x_like.shape[0] > 0
                 and hip_conv_ok_for(x_like.is_cuda, x_like.dtype, cin, w, self.conv.stride, self.conv.padding))
 
-    def bias_relu(self, x, folded, mask_input=False, grad_premasked=False):
+    def bias_relu(self, x, folded, mask_input=False, grad_premasked=False, link=None):
         """relu(BN(conv(x))) with the frozen BN folded: one HIP launch when
         fused (hip_ok), else conv + the BiasReLU kernel."""
         w, shift = folded
         if mask_input or grad_premasked or self.hip_ok(x, x.shape[1], w):
-            return conv2d_bias_relu(x, w, shift, mask_input, grad_premasked)
+            return conv2d_bias_relu(x, w, shift, mask_input, grad_premasked, link)
         y, _ = self.conv_shift(x, folded)
         return BiasReLU.apply(y, shift)
 
@@ -288,7 +288,7 @@ _NO_FORK = os.environ.get("MOE_BACKBONE_FORK", "1") == "0"
 _NO_FOLD_ALL = os.environ.get("MOE_FOLD_ALL", "1") == "0"
 
 
-def _block_out(last, short, h, x, folded_last=None, mask_input=False):
+def _block_out(last, short, h, x, folded_last=None, mask_input=False, link_in=None):
     """relu(last(h) + shortcut(x)) as a (main, shortcut) pair of handles on the
     same activation (see fused.AddBiasReLUFork).  With frozen BNs the two BN
     shifts join the residual add and the ReLU in one fused kernel -- the
@@ -300,7 +300,7 @@ def _block_out(last, short, h, x, folded_last=None, mask_input=False):
             b, bias = (x, sl) if short is None else short.conv_shift(x)
             if short is not None:
                 bias = sl + bias
-            return conv2d_add_bias_relu_fork(h, wl, b, bias, mask_input)
+            return conv2d_add_bias_relu_fork(h, wl, b, bias, mask_input, link_in if short is None else None)
     if last.fold and (short is None or short.conv.fold):
         a, sa = last.conv_shift(h, folded_last)
         b, bias = (x, sa) if short is None else short.conv_shift(x)
@@ -312,6 +312,18 @@ def _block_out(last, short, h, x, folded_last=None, mask_input=False):
         return AddBiasReLUFork.apply(a, b, bias)
     y = F.relu(last(h) + (x if short is None else short(x)))
     return y, y
+
+
+_GRAD_LINK = os.environ.get("MOE_GRAD_LINK", "1") != "0"  # A/B switch for the GradLink hand-off
+
+
+def _link_for(short, x, fused):
+    """The previous block's GradLink when this block's shortcut is the
+    identity and both its first convolution and its output are fused (both
+    ends of the hand-off run: branch2a's dgrad epilogue, this block's fork)."""
+    if short is not None or not fused or not _GRAD_LINK:
+        return None
+    return getattr(x, "grad_link", None)
 
 
 class BasicBlock(nn.Module):
@@ -333,8 +345,9 @@ class BasicBlock(nn.Module):
             ok_a = a.hip_ok(x, x.shape[1], fa[0])
             ok_b = b.hip_ok(x, fa[0].shape[0], fb[0])
             pre_ab = ok_a and ok_b  # branch2b's dgrad masks branch2a's ReLU
-            h = a.bias_relu(x, fa, grad_premasked=pre_ab) if ok_a else a.bias_relu(x, fa)
-            return _block_out(b, self.short, h, xs, fb, mask_input=pre_ab)
+            link = _link_for(self.short, x, ok_a and ok_b)
+            h = a.bias_relu(x, fa, grad_premasked=pre_ab, link=link) if ok_a else a.bias_relu(x, fa)
+            return _block_out(b, self.short, h, xs, fb, mask_input=pre_ab, link_in=link)
         return _block_out(self.branch2b, self.short, self.branch2a(x), xs)
 
 
@@ -364,9 +377,10 @@ class BottleNeck(nn.Module):
             ok_b = b.hip_ok(x, fa[0].shape[0], fb[0])
             ok_c = c.hip_ok(x, fb[0].shape[0], fc[0])
             pre_ab, pre_bc = ok_a and ok_b, ok_b and ok_c
-            h1 = a.bias_relu(x, fa, grad_premasked=pre_ab)
+            link = _link_for(self.short, x, ok_a and ok_c)
+            h1 = a.bias_relu(x, fa, grad_premasked=pre_ab, link=link)
             h2 = b.bias_relu(h1, fb, mask_input=pre_ab, grad_premasked=pre_bc)
-            return _block_out(c, self.short, h2, xs, fc, mask_input=pre_bc)
+            return _block_out(c, self.short, h2, xs, fc, mask_input=pre_bc, link_in=link)
         return _block_out(self.branch2c, self.short, self.branch2b(self.branch2a(x)), xs)
 
 

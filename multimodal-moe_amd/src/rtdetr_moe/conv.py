@@ -69,9 +69,10 @@ def _fwd(x, w, bias=None, resid=None, relu=False):
     return y
 
 
-def _bwd(x, w, g, need_x, need_w, mask_input):
-    """(dx, dw) of y = conv(x, w) for the output gradient g; dx is zeroed where
-    x <= 0 when mask_input (the ReLU backward of the activation x, fused)."""
+def _bwd(x, w, g, need_x, need_w, mask_input, add=None):
+    """(dx, dw) of y = conv(x, w) for the output gradient g; dx += add (x's
+    other consumer's gradient, when given), then dx is zeroed where x <= 0 when
+    mask_input (the ReLU backward of the activation x, fused)."""
     from ..moe import _lib as L
 
     B, C, H, W = x.shape
@@ -86,6 +87,7 @@ def _bwd(x, w, g, need_x, need_w, mask_input):
         work = torch.empty(nb // 2, dtype=torch.bfloat16, device=x.device) if nb > 0 else None
         L._check(L.lib().rtdetr_conv_dgrad(g.data_ptr(), w.data_ptr(), None if work is None else work.data_ptr(),
                                            gx.data_ptr(), z, B, H, W, C, N, ks,
+                                           None if add is None else _nhwc(add).data_ptr(),
                                            x.data_ptr() if mask_input else None, s), "rtdetr_conv_dgrad")
     if need_w:
         ns = L.lib().rtdetr_conv_wgrad_splits(B, H, W, C, N, ks)
@@ -94,6 +96,23 @@ def _bwd(x, w, g, need_x, need_w, mask_input):
         L._check(L.lib().rtdetr_conv_wgrad(g.data_ptr(), x.data_ptr(), part.data_ptr(), ns, gw.data_ptr(), 1,
                                            z, B, H, W, C, N, ks, s), "rtdetr_conv_wgrad")
     return gx, gw
+
+
+class GradLink:
+    """Hand-off between a residual block's output y = relu(s) (made by
+    _ConvHIPFork) and the next block when its shortcut is the identity: y's
+    gradient is mask(y) * (g_a + g_s) with g_a from the next block's branch2a
+    data gradient and g_s the next block's own output gradient (its fork's
+    g, which reaches y through the identity shortcut).  The next fork's
+    backward stores g_s here; branch2a's backward, which autograd runs after
+    it, adds g_s and applies the mask in its dgrad epilogue and marks the
+    result final; y's fork then takes it as is (no rtdetr_relu_grad2 pass)."""
+
+    __slots__ = ("g_short", "final")
+
+    def __init__(self):
+        self.g_short = None
+        self.final = False
 
 
 class _ConvHIP(torch.autograd.Function):
@@ -107,11 +126,12 @@ class _ConvHIP(torch.autograd.Function):
     gradient is already masked (no threshold pass here)."""
 
     @staticmethod
-    def forward(ctx, x, w, bias=None, relu=False, mask_input=False, grad_premasked=False):
+    def forward(ctx, x, w, bias=None, relu=False, mask_input=False, grad_premasked=False, link=None):
         x = _nhwc(x)
         w = _nhwc(w)
         y = _fwd(x, w, bias, None, relu)
         ctx.flags = (bool(relu) and not grad_premasked, bool(mask_input))
+        ctx.link = link  # x is a block output (GradLink): finish its gradient here when the hand-off is there
         ctx.save_for_backward(x, w, y if ctx.flags[0] else None)
         return y
 
@@ -120,8 +140,12 @@ class _ConvHIP(torch.autograd.Function):
         x, w, y = ctx.saved_tensors
         relu_here, mask_input = ctx.flags
         g = torch.ops.aten.threshold_backward(gy, y, 0) if relu_here else gy
-        gx, gw = _bwd(x, w, g, ctx.needs_input_grad[0], ctx.needs_input_grad[1], mask_input)
-        return gx, gw, None, None, None, None
+        link, add = ctx.link, None
+        if link is not None and link.g_short is not None and ctx.needs_input_grad[0]:
+            add, mask_input = link.g_short, True
+            link.g_short, link.final = None, True
+        gx, gw = _bwd(x, w, g, ctx.needs_input_grad[0], ctx.needs_input_grad[1], mask_input, add)
+        return gx, gw, None, None, None, None, None
 
 
 class _ConvHIPFork(torch.autograd.Function):
@@ -132,11 +156,12 @@ class _ConvHIPFork(torch.autograd.Function):
     the gradient of both the convolution output and resid."""
 
     @staticmethod
-    def forward(ctx, x, w, resid, bias, mask_input=False):
+    def forward(ctx, x, w, resid, bias, mask_input=False, link_in=None, link_out=None):
         x = _nhwc(x)
         w = _nhwc(w)
         y = _fwd(x, w, bias, _nhwc(resid), True)
         ctx.mask_input = bool(mask_input)
+        ctx.links = (link_in, link_out)  # link_in: resid is the previous block's output (identity shortcut)
         ctx.save_for_backward(x, w, y)
         return y, y.view_as(y)
 
@@ -145,13 +170,22 @@ class _ConvHIPFork(torch.autograd.Function):
         from ..moe import _lib as L
 
         x, w, y = ctx.saved_tensors
-        if dy1 is None and dy2 is None:
-            return None, None, None, None, None
-        if dy1 is None:
-            dy1, dy2 = dy2, None
-        g = L.relu_grad2_nhwc(_nhwc(dy1), None if dy2 is None else _nhwc(dy2), y)
+        link_in, link_out = ctx.links
+        if link_out is not None and link_out.final:
+            g = dy1  # the next block's branch2a dgrad already added dy2 and masked (GradLink)
+            link_out.final = False
+        else:
+            if link_out is not None:
+                link_out.g_short = None
+            if dy1 is None and dy2 is None:
+                return None, None, None, None, None, None, None
+            if dy1 is None:
+                dy1, dy2 = dy2, None
+            g = L.relu_grad2_nhwc(_nhwc(dy1), None if dy2 is None else _nhwc(dy2), y)
+        if link_in is not None:
+            link_in.g_short = g
         gx, gw = _bwd(x, w, g, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.mask_input)
-        return gx, gw, g if ctx.needs_input_grad[2] else None, None, None
+        return gx, gw, g if ctx.needs_input_grad[2] else None, None, None, None, None
 
 
 def conv2d(x, weight, stride=1, padding=0):
@@ -162,17 +196,24 @@ def conv2d(x, weight, stride=1, padding=0):
     return F.conv2d(x, weight, None, stride, padding)
 
 
-def conv2d_bias_relu(x, weight, bias, mask_input=False, grad_premasked=False):
+def conv2d_bias_relu(x, weight, bias, mask_input=False, grad_premasked=False, link=None):
     """relu(conv2d(x, weight) + bias[c]) in one HIP launch (stride 1, "same"
     padding; the caller checked hip_conv_ok).  bias: fp32 [Cout], no gradient.
-    See _ConvHIP for mask_input / grad_premasked."""
-    return _ConvHIP.apply(x, weight, bias.float().contiguous(), True, mask_input, grad_premasked)
+    See _ConvHIP for mask_input / grad_premasked, GradLink for link (x a
+    block output whose other consumer is the identity shortcut)."""
+    return _ConvHIP.apply(x, weight, bias.float().contiguous(), True, mask_input, grad_premasked, link)
 
 
-def conv2d_add_bias_relu_fork(x, weight, resid, bias, mask_input=False):
+def conv2d_add_bias_relu_fork(x, weight, resid, bias, mask_input=False, link_in=None):
     """(y, y) with y = relu((conv2d(x, weight) + resid) + bias[c]) in one HIP
-    launch -- see _ConvHIPFork."""
-    return _ConvHIPFork.apply(x, weight, resid, None if bias is None else bias.float().contiguous(), mask_input)
+    launch -- see _ConvHIPFork.  link_in: resid is the previous block's output
+    through an identity shortcut (GradLink).  y carries the GradLink for the
+    next block as y.grad_link."""
+    link_out = GradLink()
+    y, y2 = _ConvHIPFork.apply(x, weight, resid, None if bias is None else bias.float().contiguous(), mask_input,
+                               link_in, link_out)
+    y.grad_link = link_out
+    return y, y2
 
 
 def conv_module(conv: torch.nn.Conv2d, x):

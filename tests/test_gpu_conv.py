@@ -172,3 +172,42 @@ def test_bottleneck_fused_matches_unfused(hip_lib, cin, width, stride, shortcut)
     assert torch.equal(ya, yb)
     for u, v in zip(ga, gb):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("cin,width", [(256, 64), (512, 128)])
+def test_block_chain_grad_link_matches_unfused(hip_lib, cin, width):
+    """Two identity-shortcut bottlenecks chained as PResNet chains them: the
+    first block's output gradient is finished in the second block's branch2a
+    dgrad epilogue (GradLink: + the shortcut gradient, ReLU mask) instead of
+    rtdetr_relu_grad2 -- bitwise equal to the unfused chain."""
+    from src.rtdetr_moe import backbone as BB
+
+    torch.manual_seed(4)
+    blks = torch.nn.ModuleList([BB.BottleNeck(cin, width, 1, True, True) for _ in range(2)]).to(DEV)
+    blks = blks.to(torch.bfloat16).to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        for m in blks.modules():
+            if isinstance(m, BB.FrozenBatchNorm2d):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 2.0)
+                m.bias.uniform_(-0.3, 0.3)
+    x0 = torch.randn(2, cin, 16, 24, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g1 = torch.randn(2, cin, 16, 24, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g2 = torch.randn_like(g1)
+    res = []
+    for fused in (True, False):
+        BB._FUSED_EPI = fused
+        try:
+            x = x0.clone().requires_grad_(True)
+            y, ys = blks[0](x)
+            z1, z2 = blks[1](y, ys)
+            params = [p for p in blks.parameters() if p.requires_grad]
+            grads = torch.autograd.grad([z1, z2], [x] + params, [g1, g2])
+            torch.cuda.synchronize()
+            res.append((z1.detach().clone(), [gg.clone() for gg in grads]))
+        finally:
+            BB._FUSED_EPI = True
+    (za, ga), (zb, gb) = res
+    assert torch.equal(za, zb)
+    for u, v in zip(ga, gb):
+        assert torch.equal(u, v)

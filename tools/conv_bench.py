@@ -89,7 +89,7 @@ def main():
         nb = lib.rtdetr_conv_dgrad_workspace(B, H, W, Ci, Co, ks)
         wk = torch.empty(max(nb // 2, 8), dtype=torch.bfloat16, device=dev)
         t_hd = timeit(lambda: lib.rtdetr_conv_dgrad(gy.data_ptr(), w.data_ptr(), wk.data_ptr(), gx.data_ptr(), z, B, H,
-                                                    W, Ci, Co, ks, None, L._stream()))
+                                                    W, Ci, Co, ks, None, None, L._stream()))
         ns = lib.rtdetr_conv_wgrad_splits(B, H, W, Ci, Co, ks)
         part = torch.empty(ns * Co * Ci * ks * ks, dtype=torch.float32, device=dev)
         gw = torch.empty_like(w)
