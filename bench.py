@@ -71,7 +71,9 @@ def load_pmc_traffic(workload):
     """HBM bytes per launch per kernel group from the committed PMC summary of
     the same workload (tools/gpu_round.sh + tools/profile_summary.py:
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected)."""
-    p = ROOT / "profiles" / f"pmc_traffic_{workload}.json"
+    # the newest round's summary (profiles/rNN/pmc_traffic_<wl>.json), else the top-level one
+    cands = sorted((ROOT / "profiles").glob(f"r[0-9][0-9]/pmc_traffic_{workload}.json"))
+    p = cands[-1] if cands else ROOT / "profiles" / f"pmc_traffic_{workload}.json"
     if not p.exists():
         return {}
     try:

@@ -527,17 +527,22 @@ int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, 
 /* Implicit-GEMM convolutions of the RT-DETR body (the
  * backbone and the HybridEncoder's RepVGG / CSP convolutions, which the
  * reference's engine trains inside RTDETR.train, src/models/vision/rtdetr.py:
- * 82-94), bf16 MFMA, stride 1, padding (KS - 1) / 2, KS in {1, 3}, no bias.
+ * 82-94), bf16 MFMA, padding (KS - 1) / 2, KS in {1, 3}, stride 1 (or 2 with
+ * KS = 3: the ResNet-D stage-entry and HybridEncoder downsampling 3x3
+ * convolutions), no bias.  B, H, W are the INPUT x / dx dims; the output y / dy
+ * is [B, Ho, Wo] with Ho = (H - 1) / stride + 1 (W likewise).
  * x / dy / y: NHWC bf16 [B, H, W, channels]; w: [N][KS][KS][C] bf16 (a
- * channels_last [N, C, KS, KS] weight); C and N multiples of 128; zero: >= 256
+ * channels_last [N, C, KS, KS] weight); C and N multiples of 64; zero: >= 256
  * zero bytes on the device (read for padding neighbours); pointers 16-B aligned.
- *   rtdetr_conv_fwd         y[B,H,W,N] = conv(x[B,H,W,C], w)   (no im2col buffer),
+ *   rtdetr_conv_fwd         y[B,Ho,Wo,N] = conv(x[B,H,W,C], w)   (no im2col buffer),
  *                           with an optional fused epilogue (NULL / 0 = off):
  *                           y = relu?((y + resid[B,H,W,N]) + bias[N]) (fp32 on
  *                           the bf16 result: rtdetr_add_bias_relu_nhwc's
  *                           arithmetic; bias fp32, resid bf16 NHWC)
- *   rtdetr_conv_dgrad       dx[B,H,W,C] = conv^T(dy[B,H,W,N], w): the forward
- *                           GEMM over dy with the flipped, transposed weight,
+ *   rtdetr_conv_dgrad       dx[B,H,W,C] = conv^T(dy[B,Ho,Wo,N], w): the forward
+ *                           GEMM over dy with the flipped, transposed weight
+ *                           (stride 2: dx(y, x) reads dy((y+dy)/2, (x+dx)/2)
+ *                           for the taps with both even, a zero row otherwise),
  *                           written to work first when
  *                           rtdetr_conv_dgrad_workspace() > 0 (bytes; large
  *                           problems), else read in place from w (work may be
@@ -551,15 +556,20 @@ int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, 
  *                           nsplit pixel slices write fp32 partials to part
  *                           [nsplit][N KS KS C], summed in slice order
  *                           (deterministic) into dw (bf16 if out_bf16 else fp32);
- *                           nsplit from rtdetr_conv_wgrad_splits. */
+ *                           nsplit from rtdetr_conv_wgrad_splits (called
+ *                           with the OUTPUT dims Ho, Wo: its pixel count is the
+ *                           GEMM's K).
+ * MIOpen, which these replace, zero-fills its atomic split-K weight-gradient
+ * outputs outside a captured hipGraph for some solvers: replays then add onto
+ * the previous step's sums (tools/miopen_graph_probe.py). */
 int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void* zero, int B, int H, int W, int C, int N,
-                    int KS, const float* bias, const void* resid, int relu, hipStream_t stream);
+                    int KS, int stride, const float* bias, const void* resid, int relu, hipStream_t stream);
 long long rtdetr_conv_dgrad_workspace(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void* dx, const void* zero, int B, int H, int W,
-                      int C, int N, int KS, const void* add, const void* relu_mask, hipStream_t stream);
+                      int C, int N, int KS, int stride, const void* add, const void* relu_mask, hipStream_t stream);
 int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
-                      const void* zero, int B, int H, int W, int C, int N, int KS, hipStream_t stream);
+                      const void* zero, int B, int H, int W, int C, int N, int KS, int stride, hipStream_t stream);
 /* Measurement / A-B knobs (0, or -1 for conv_dgrad_flip, = automatic):
  * "conv_bm" forward pixel-tile rows 64 / 128 / 256; "conv_wg_stages"
  * weight-gradient LDS ring depth 2..4; "conv_wg_splits" weight-gradient pixel

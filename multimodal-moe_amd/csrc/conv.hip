@@ -1,6 +1,6 @@
 // Implicit-GEMM convolutions of the RT-DETR body on the bf16 MFMA (gfx950):
-// stride 1, "same" padding (KS - 1) / 2, KS in {1, 3}, NHWC (channels_last)
-// activations and [Cout][KS][KS][Cin] (channels_last) weights.  They replace
+// padding (KS - 1) / 2, KS in {1, 3}, stride 1 or (KS = 3) 2, NHWC
+// (channels_last) activations and [Cout][KS][KS][Cin] (channels_last) weights.  They replace
 // MIOpen for the convolutions that dominate the training step (SURVEY.md 8(f)
 // row 1: "the backbone ... dominate images/sec"; the HybridEncoder's
 // RepVGG 3x3 / 1x1 pairs and the ResNet 3x3 / 1x1 layers): the reference
@@ -17,6 +17,12 @@
 //                      (conv_weight_flip_kernel, K-contiguous image), small
 //                      ones read it in place from W as an MN-contiguous
 //                      operand image (template flag BT; no extra launch).
+//                      Stride 2: the forward's neighbour of output pixel
+//                      (y, x) is input (2y + dy, 2x + dx); the data gradient
+//                      of input pixel (y, x) for tap (dy, dx) reads dY at
+//                      ((y + dy) / 2, (x + dx) / 2) when both are even, else
+//                      the zero row (3 of 4 taps on average: wasted MFMA
+//                      work on a few small layers, no scatter, no atomics).
 //   conv_wgrad_kernel  dW[n, tap, c] = sum_p dY[p, n] X[nbr(p, tap), c]
 //                      GEMM M = Cout, N = KS^2 Cin, K = pixels, split over S
 //                      slices of the pixels (fp32 partials) and summed in a
@@ -43,13 +49,17 @@ static int g_conv_wg_splits = 0;   // "conv_wg_splits": weight-gradient pixel sl
 static int g_conv_dgrad_flip = -1; // "conv_dgrad_flip": 1 = always write W', 0 = always read in place
 
 struct ConvArgs {
-  const uint16_t* x;     // [B H W, C] (fwd: X; dgrad: dY)
+  const uint16_t* x;     // [B Hs Ws, C] (fwd: X; dgrad: dY)
   const uint16_t* w;     // [N][KS][KS][C] (fwd: W; dgrad: W')
   uint16_t* y;           // [B H W, N]
   const uint16_t* zero;  // >= 256 zero bytes (padding rows)
-  int B, H, W, C, N;
+  int B, H, W, C, N;     // H, W: this GEMM's output pixels (fwd: Y, dgrad: dX)
   int P;                 // B H W
   int mt_n;              // M tiles
+  int Hs, Ws;            // the source image x (fwd: X, dgrad: dY)
+  int st, sh;            // neighbour of (y, x) for tap (dy, dx): ((st y + dy) >> sh, (st x + dx) >> sh), valid
+                         // only when sh == 0 or both are even (fwd: st = stride, sh = 0; dgrad: st = 1,
+                         // sh = stride / 2)
   // fused epilogue on the bf16 result v (each NULL / 0 = off), in this order:
   //   v = relu?( (v + resid[p][n]) + bias[n] ),  then v = 0 where mask[p][n] <= 0
   // (the arithmetic of rtdetr_bias_act_nhwc / rtdetr_add_bias_relu_nhwc and of
@@ -105,7 +115,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   const int m0 = mt * BM, n0 = nt * BN;
   const int cpt = a.C / 64;        // K-tiles per tap
   const int nk = KS * KS * cpt;
-  const int HW = a.H * a.W;
+  const int HW = a.H * a.W, HWs = a.Hs * a.Ws;
   // this lane's A rows (one per DMA instruction j): pixel, coordinates, source chunk
   int py[TM], px[TM], pb[TM], ach[TM];
   bool pv[TM];
@@ -143,9 +153,12 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     const int dy = tap / KS - PAD, dx = tap % KS - PAD;
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
-      const int yy = py[j] + dy, xx = px[j] + dx;
-      const bool ok = pv[j] && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
-      const uint16_t* src = ok ? a.x + ((size_t)(pb[j] * HW + yy * a.W + xx)) * a.C + c0 + ach[j] : a.zero + ach[j];
+      int yy = py[j] * a.st + dy, xx = px[j] * a.st + dx;
+      bool ok = pv[j] && !(((yy | xx) & a.sh));  // sh = 1: both even
+      yy >>= a.sh;
+      xx >>= a.sh;
+      ok = ok && yy >= 0 && yy < a.Hs && xx >= 0 && xx < a.Ws;
+      const uint16_t* src = ok ? a.x + ((size_t)(pb[j] * HWs + yy * a.Ws + xx)) * a.C + c0 + ach[j] : a.zero + ach[j];
       dma16(src, buf + (wave + 4 * j) * 1024);
     }
 #pragma unroll
@@ -275,12 +288,13 @@ __global__ __launch_bounds__(256) void conv_weight_flip_kernel(const uint16_t* _
 // weight gradient
 // ---------------------------------------------------------------------------
 struct ConvWgArgs {
-  const uint16_t* dy;    // [P][N]
-  const uint16_t* x;     // [P][C]
+  const uint16_t* dy;    // [P][N], P = B Ho Wo
+  const uint16_t* x;     // [B H W][C]
   float* part;           // [S][N][KS KS C]
   const uint16_t* zero;
   int B, H, W, C, N, P;
   int nsplit, kt_per;    // pixel K-tiles per slice
+  int Ho, Wo, st;        // output pixels (dY) and the stride: x neighbour (st y + dy, st x + dx)
 };
 
 // Tile WBM (output channels) x WBN (tap-major input channels of one tap):
@@ -316,11 +330,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
   const int ktot = (a.P + 63) / 64;
   const int kt0 = split * a.kt_per;
   const int nk = max(0, min(a.kt_per, ktot - kt0));
-  const int HW = a.H * a.W;
+  const int HWo = a.Ho * a.Wo, HW = a.H * a.W;
   // A (dY) k-row of this lane in instruction j: (wave + 4 j) (64 / LA) + lane / LA; its pixel
   // advances by 64 per K-tile.  B (X) k-rows likewise, with the pixel's (y, x) kept and
   // advanced incrementally (no divisions in the loop) for the neighbour's bounds.
-  int cha[NA], pa[NA], chb[NB], pb[NB], py[NB], px[NB];
+  int cha[NA], pa[NA], chb[NB], pb[NB], pi[NB], py[NB], px[NB];
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
     const int kr = (wave + 4 * j) * (64 / LA) + lane / LA;
@@ -334,9 +348,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
     const int p = kt0 * 64 + kr;
     pb[j] = p;
     const int q = p < a.P ? p : 0;
-    const int rem = q % HW;
-    py[j] = rem / a.W;
-    px[j] = rem - py[j] * a.W;
+    pi[j] = q / HWo;
+    const int rem = q - pi[j] * HWo;
+    py[j] = rem / a.Wo;
+    px[j] = rem - py[j] * a.Wo;
   }
   auto issue = [&](int kt) {
     char* buf = smem + (kt % S) * TILE;
@@ -349,19 +364,23 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int p = pb[j];
-      const int yy = py[j] + dy_, xx = px[j] + dx_;
+      const int yy = py[j] * a.st + dy_, xx = px[j] * a.st + dx_;
       const bool ok = p < a.P && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
-      const long long nb = (long long)p + (long long)dy_ * a.W + dx_;  // the neighbour's flat pixel index
+      const long long nb = (long long)pi[j] * HW + (long long)yy * a.W + xx;  // the neighbour's flat pixel index
       dma16(ok ? a.x + (size_t)nb * a.C + c0 + chb[j] : a.zero + chb[j], buf + WBM * 128 + (wave + 4 * j) * 1024);
-      // next K-tile: 64 pixels on (row-major within the image; images are contiguous)
+      // next K-tile: 64 output pixels on (row-major within the image; images are contiguous)
       pb[j] = p + 64;
-      int x = px[j] + 64, y = py[j];
-      while (x >= a.W) {
-        x -= a.W;
-        if (++y == a.H) y = 0;
+      int x = px[j] + 64, y = py[j], im = pi[j];
+      while (x >= a.Wo) {
+        x -= a.Wo;
+        if (++y == a.Ho) {
+          y = 0;
+          ++im;
+        }
       }
       px[j] = x;
       py[j] = y;
+      pi[j] = im;
     }
   };
   f32x4 acc[TM][TN];
@@ -442,8 +461,13 @@ static void allow_lds_once(size_t bytes) {
   }
 }
 
-static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int C, int N, int KS, const char* what) {
+// output size of a padding (KS - 1) / 2 convolution
+static int conv_out(int n, int KS, int stride) { return (n + 2 * ((KS - 1) / 2) - KS) / stride + 1; }
+
+static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int C, int N, int KS, int stride,
+                      const char* what) {
   if (KS != 1 && KS != 3) return fail(std::string(what) + ": kernel size must be 1 or 3");
+  if (stride != 1 && !(stride == 2 && KS == 3)) return fail(std::string(what) + ": stride must be 1 (or 2 with KS 3)");
   if (B < 0 || H <= 0 || W <= 0) return fail(std::string(what) + ": bad B / H / W");
   if (C % 64 || N % 64 || C <= 0 || N <= 0)
     return fail(std::string(what) + ": channels must be positive multiples of 64");
@@ -527,17 +551,19 @@ using namespace moe;
 static bool aligned16(const void* p) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 extern "C" int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void* zero, int B, int H, int W, int C,
-                               int N, int KS, const float* bias, const void* resid, int relu, hipStream_t stream) {
+                               int N, int KS, int stride, const float* bias, const void* resid, int relu,
+                               hipStream_t stream) {
   const void* ptrs[4] = {x, w, y, zero};
-  if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, "rtdetr_conv_fwd")) return rc;
+  if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, stride, "rtdetr_conv_fwd")) return rc;
   if (!aligned16(bias) || !aligned16(resid)) return fail("rtdetr_conv_fwd: bias / resid must be 16-B aligned");
   if (B == 0) return 0;
+  const int Ho = conv_out(H, KS, stride), Wo = conv_out(W, KS, stride);
   ConvArgs a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(y),
-             static_cast<const uint16_t*>(zero), B, H, W, C, N, B * H * W, 0,
+             static_cast<const uint16_t*>(zero), B, Ho, Wo, C, N, B * Ho * Wo, 0, H, W, stride, 0,
              bias, static_cast<const uint16_t*>(resid), nullptr, relu ? 1 : 0};
   const double P = a.P;
-  ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N + (resid ? N : 0)) + 2.0 * N * KS * KS * C, false, 0.0,
-                 2.0 * P * N * KS * KS * C);
+  ProfScope prof(stream, PROF_CONV, 2.0 * ((double)B * H * W * C + P * (N + (resid ? N : 0))) + 2.0 * N * KS * KS * C,
+                 false, 0.0, 2.0 * P * N * KS * KS * C);
   launch_fwd_any<false>(a, KS, stream, prof);
   return check_launch("rtdetr_conv_fwd");
 }
@@ -554,20 +580,23 @@ extern "C" long long rtdetr_conv_dgrad_workspace(int B, int H, int W, int C, int
 }
 
 extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void* dx, const void* zero, int B, int H,
-                                 int W, int C, int N, int KS, const void* add, const void* relu_mask,
+                                 int W, int C, int N, int KS, int stride, const void* add, const void* relu_mask,
                                  hipStream_t stream) {
   const void* ptrs[4] = {dy, w, dx, zero};
-  if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, "rtdetr_conv_dgrad")) return rc;
+  if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, stride, "rtdetr_conv_dgrad")) return rc;
   if (!aligned16(relu_mask) || !aligned16(add)) return fail("rtdetr_conv_dgrad: add / relu_mask must be 16-B aligned");
   const bool flip = rtdetr_conv_dgrad_workspace(B, H, W, C, N, KS) > 0;
   if (flip && (work == nullptr || reinterpret_cast<uintptr_t>(work) % 16))
     return fail("rtdetr_conv_dgrad: this shape needs a 16-B aligned workspace of rtdetr_conv_dgrad_workspace() bytes");
   if (B == 0) return 0;
-  // the forward GEMM over dY [P][N] with W'
+  // the forward GEMM over dY [B Ho Wo][N] with W' (stride 2: dX pixel (y, x) reads dY at ((y + dy) / 2,
+  // (x + dx) / 2) when both are even)
+  const int Ho = conv_out(H, KS, stride), Wo = conv_out(W, KS, stride);
   ConvArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(dx),
-             static_cast<const uint16_t*>(zero), B, H, W, N, C, B * H * W, 0,
+             static_cast<const uint16_t*>(zero), B, H, W, N, C, B * H * W, 0, Ho, Wo, 1, stride == 2 ? 1 : 0,
              nullptr, static_cast<const uint16_t*>(add), static_cast<const uint16_t*>(relu_mask), 0};
   const double P = a.P;
+  const double Pdy = (double)B * Ho * Wo;
   if (flip) {
     const long long total = (long long)N * C * KS * KS;
     {
@@ -578,9 +607,9 @@ extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void
     }
     a.w = static_cast<const uint16_t*>(work);
   }
-  ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N + (relu_mask ? C : 0) + (add ? C : 0)) + 2.0 * N * KS * KS * C,
-                 false, 0.0,
-                 2.0 * P * N * KS * KS * C);
+  // algorithmic flops: the stride-2 zero-row taps are not counted
+  ProfScope prof(stream, PROF_CONV, 2.0 * (P * (C + (relu_mask ? C : 0) + (add ? C : 0)) + Pdy * N) + 2.0 * N * KS * KS * C,
+                 false, 0.0, 2.0 * Pdy * N * KS * KS * C);
   if (flip) launch_fwd_any<false>(a, KS, stream, prof);
   else launch_fwd_any<true>(a, KS, stream, prof);
   return check_launch("rtdetr_conv_dgrad");
@@ -602,18 +631,21 @@ extern "C" int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int K
 }
 
 extern "C" int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
-                                 const void* zero, int B, int H, int W, int C, int N, int KS, hipStream_t stream) {
+                                 const void* zero, int B, int H, int W, int C, int N, int KS, int stride,
+                                 hipStream_t stream) {
   const void* ptrs[5] = {dy, x, part, dw, zero};
-  if (int rc = conv_check(ptrs, 5, B, H, W, C, N, KS, "rtdetr_conv_wgrad")) return rc;
+  if (int rc = conv_check(ptrs, 5, B, H, W, C, N, KS, stride, "rtdetr_conv_wgrad")) return rc;
   if (nsplit < 1 || nsplit > 256) return fail("rtdetr_conv_wgrad: nsplit must be 1..256");
+  const int Ho = conv_out(H, KS, stride), Wo = conv_out(W, KS, stride);
   ConvWgArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(x), part,
-               static_cast<const uint16_t*>(zero), B, H, W, C, N, B * H * W, nsplit, 0};
+               static_cast<const uint16_t*>(zero), B, H, W, C, N, B * Ho * Wo, nsplit, 0, Ho, Wo, stride};
   const int ktot = (a.P + 63) / 64;
   a.kt_per = (ktot + nsplit - 1) / nsplit;
   const long long nw = (long long)N * KS * KS * C;
   {
     const double P = a.P;
-    ProfScope prof(stream, PROF_CONV, 2.0 * P * (C + N) + 4.0 * nsplit * nw, false, 0.0, 2.0 * P * nw);
+    ProfScope prof(stream, PROF_CONV, 2.0 * ((double)B * H * W * C + P * N) + 4.0 * nsplit * nw, false, 0.0,
+                   2.0 * P * nw);
     if (KS == 3) launch_wgrad<3>(a, stream, prof);
     else launch_wgrad<1>(a, stream, prof);
     if (int rc = check_launch("rtdetr_conv_wgrad")) return rc;

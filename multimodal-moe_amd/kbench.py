@@ -22,18 +22,27 @@ import torch  # noqa: E402
 from src.moe import _lib as L  # noqa: E402
 
 
+_FLUSH = None
+
+
 def timed(fn, reps):
     """Median kernel execution time (us) of `fn` over `reps` calls (the sum of
     its launches when it makes several), from the dispatch-stamped event pairs
     of libmoe_hip's profiler (hipExtLaunchKernel): no host overhead or
-    inter-launch gaps included."""
+    inter-launch gaps included.  With --cold every call is preceded by a read
+    of a buffer larger than the Infinity Cache (operands start in HBM, as in a
+    training step where ~GBs pass between a layer's uses of its weights)."""
     fn()
     torch.cuda.synchronize()
     L.lib().moe_profile_enable(1)
     try:
+        if _FLUSH is not None:
+            _FLUSH.sum()
         fn()
         per = max(1, len(L.profile_records()))
         for _ in range(reps):
+            if _FLUSH is not None:
+                _FLUSH.sum()
             fn()
         recs = L.profile_records()
     finally:
@@ -156,8 +165,12 @@ def main():
     ap.add_argument("--pair", default="1", help="comma list of gemm_pair modes (1 one launch, 0 two launches)")
     ap.add_argument("--wg", default="0:0", help="comma list of gathered-wgrad bodies dma:stages (dma 0 auto / 1 "
                                                 "register-staged; stages 0 auto, 2, 3)")
+    ap.add_argument("--cold", action="store_true", help="flush the Infinity Cache (512 MiB read) before every call")
     a = ap.parse_args()
     L.lib()
+    if a.cold:
+        global _FLUSH
+        _FLUSH = torch.zeros(128 << 20, device="cuda", dtype=torch.float32)
     configs = [(v, s, dbg, bm, xm, ks, pr, wg) for v in map(int, a.variants.split(",")) for s in map(int, a.stages.split(","))
                for dbg in map(int, a.debug.split(",")) for bm in map(int, a.bm.split(","))
                for xm in map(int, a.xcd.split(",")) for ks in map(int, a.ksplit.split(","))
@@ -202,7 +215,7 @@ def main():
     for (name, sname, v, s, dbg, bm, xm, ks, pr, wg, flops, byts), ts in res.items():
         us = statistics.median(ts)
         d = {"kernel": name, "config": a.config, "shape": sname, "variant": v, "stages": s, "debug": dbg, "bm": bm,
-             "xcd": xm, "ksplit": ks, "pair": pr, "wg": wg, "us": round(us, 2),
+             "xcd": xm, "ksplit": ks, "pair": pr, "wg": wg, "cold": a.cold, "us": round(us, 2),
              "min_us": round(min(ts), 2)}
         if flops:
             d["tflops"] = round(flops / us / 1e6, 1)

@@ -209,7 +209,7 @@ class ConvNormLayer(nn.Module):
         fused (hip_ok), else conv + the BiasReLU kernel."""
         w, shift = folded
         if mask_input or grad_premasked or self.hip_ok(x, x.shape[1], w):
-            return conv2d_bias_relu(x, w, shift, mask_input, grad_premasked, link)
+            return conv2d_bias_relu(x, w, shift, mask_input, grad_premasked, link, self.conv.stride)
         y, _ = self.conv_shift(x, folded)
         return BiasReLU.apply(y, shift)
 

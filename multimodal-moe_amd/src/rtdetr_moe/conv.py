@@ -2,7 +2,9 @@
 (csrc/conv.hip: rtdetr_conv_fwd / rtdetr_conv_dgrad / rtdetr_conv_wgrad).
 
 ``conv2d(x, weight, stride, padding)`` takes the HIP kernels for the
-convolutions they cover -- stride 1, "same" padding, 1x1 or 3x3, no groups,
+convolutions they cover -- padding (k - 1) / 2, 1x1 or 3x3, stride 1 (or 2
+for 3x3: the ResNet-D stage-entry and HybridEncoder downsampling layers, whose
+MIOpen weight-gradient solvers are not graph-replay safe: DESIGN.md 5), no groups,
 channel counts that are multiples of 64, bf16 channels_last activations and
 weights on the GPU (the HybridEncoder's RepVGG / CSP layers and the ResNet
 bottleneck convolutions of 64 .. 2048 channels) -- and
@@ -42,9 +44,9 @@ def hip_conv_ok(x, w, stride=1, padding=None, dilation=1, groups=1) -> bool:
     return hip_conv_ok_for(x.is_cuda, x.dtype, x.shape[1], w, stride, padding, dilation, groups)
 
 
-def hip_conv_ok_for(is_cuda, dtype, cin, w, stride=1, padding=None, dilation=1, groups=1) -> bool:
+def hip_conv_ok_for(is_cuda, dtype, cin, w, stride=1, padding=None, dilation=1, groups=1, w_dtype=None) -> bool:
     """hip_conv_ok for an input of that device kind, dtype and channel count
-    (a consumer's check before its input exists)."""
+    (a consumer's check before its input exists); w_dtype overrides w.dtype."""
     if not (_ENABLED[0] and is_cuda and w.dim() == 4):
         return False
     N, C, kh, kw = w.shape
@@ -52,24 +54,34 @@ def hip_conv_ok_for(is_cuda, dtype, cin, w, stride=1, padding=None, dilation=1, 
     st = stride if isinstance(stride, int) else (stride[0] if stride[0] == stride[1] else -1)
     pd = padding if isinstance(padding, int) else (padding[0] if padding[0] == padding[1] else -1)
     dl = dilation if isinstance(dilation, int) else (dilation[0] if dilation[0] == dilation[1] else -1)
-    return (dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and kh == kw and ks in (1, 3) and st == 1
-            and pd == (ks - 1) // 2 and dl == 1 and groups == 1 and cin == C and C % 64 == 0 and N % 64 == 0)
+    return (dtype == torch.bfloat16 and (w_dtype or w.dtype) == torch.bfloat16 and kh == kw and ks in (1, 3)
+            and (st == 1 or (st == 2 and ks == 3)) and pd == (ks - 1) // 2 and dl == 1 and groups == 1
+            and cin == C and C % 64 == 0 and N % 64 == 0)
 
 
-def _fwd(x, w, bias=None, resid=None, relu=False):
+def _stride(stride) -> int:
+    return stride if isinstance(stride, int) else stride[0]
+
+
+def _out(n, ks, st):
+    return (n + 2 * ((ks - 1) // 2) - ks) // st + 1
+
+
+def _fwd(x, w, bias=None, resid=None, relu=False, st=1):
     from ..moe import _lib as L
 
     B, C, H, W = x.shape
     N, _, ks, _ = w.shape
-    y = torch.empty((B, N, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    y = torch.empty((B, N, _out(H, ks, st), _out(W, ks, st)), dtype=torch.bfloat16, device=x.device,
+                    memory_format=torch.channels_last)
     L._check(L.lib().rtdetr_conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), _zero(x.device).data_ptr(),
-                                     B, H, W, C, N, ks, None if bias is None else bias.data_ptr(),
+                                     B, H, W, C, N, ks, st, None if bias is None else bias.data_ptr(),
                                      None if resid is None else resid.data_ptr(), int(relu), L._stream()),
              "rtdetr_conv_fwd")
     return y
 
 
-def _bwd(x, w, g, need_x, need_w, mask_input, add=None):
+def _bwd(x, w, g, need_x, need_w, mask_input, add=None, st=1):
     """(dx, dw) of y = conv(x, w) for the output gradient g; dx += add (x's
     other consumer's gradient, when given), then dx is zeroed where x <= 0 when
     mask_input (the ReLU backward of the activation x, fused)."""
@@ -86,15 +98,15 @@ def _bwd(x, w, g, need_x, need_w, mask_input, add=None):
         nb = L.lib().rtdetr_conv_dgrad_workspace(B, H, W, C, N, ks)
         work = torch.empty(nb // 2, dtype=torch.bfloat16, device=x.device) if nb > 0 else None
         L._check(L.lib().rtdetr_conv_dgrad(g.data_ptr(), w.data_ptr(), None if work is None else work.data_ptr(),
-                                           gx.data_ptr(), z, B, H, W, C, N, ks,
+                                           gx.data_ptr(), z, B, H, W, C, N, ks, st,
                                            None if add is None else _nhwc(add).data_ptr(),
                                            x.data_ptr() if mask_input else None, s), "rtdetr_conv_dgrad")
     if need_w:
-        ns = L.lib().rtdetr_conv_wgrad_splits(B, H, W, C, N, ks)
+        ns = L.lib().rtdetr_conv_wgrad_splits(B, _out(H, ks, st), _out(W, ks, st), C, N, ks)
         part = torch.empty(ns * N * C * ks * ks, dtype=torch.float32, device=x.device)
         gw = torch.empty_like(w, memory_format=torch.channels_last)
         L._check(L.lib().rtdetr_conv_wgrad(g.data_ptr(), x.data_ptr(), part.data_ptr(), ns, gw.data_ptr(), 1,
-                                           z, B, H, W, C, N, ks, s), "rtdetr_conv_wgrad")
+                                           z, B, H, W, C, N, ks, st, s), "rtdetr_conv_wgrad")
     return gx, gw
 
 
@@ -126,10 +138,11 @@ class _ConvHIP(torch.autograd.Function):
     gradient is already masked (no threshold pass here)."""
 
     @staticmethod
-    def forward(ctx, x, w, bias=None, relu=False, mask_input=False, grad_premasked=False, link=None):
+    def forward(ctx, x, w, bias=None, relu=False, mask_input=False, grad_premasked=False, link=None, st=1):
         x = _nhwc(x)
         w = _nhwc(w)
-        y = _fwd(x, w, bias, None, relu)
+        y = _fwd(x, w, bias, None, relu, st)
+        ctx.st = st
         ctx.flags = (bool(relu) and not grad_premasked, bool(mask_input))
         ctx.link = link  # x is a block output (GradLink): finish its gradient here when the hand-off is there
         ctx.save_for_backward(x, w, y if ctx.flags[0] else None)
@@ -144,8 +157,8 @@ class _ConvHIP(torch.autograd.Function):
         if link is not None and link.g_short is not None and ctx.needs_input_grad[0]:
             add, mask_input = link.g_short, True
             link.g_short, link.final = None, True
-        gx, gw = _bwd(x, w, g, ctx.needs_input_grad[0], ctx.needs_input_grad[1], mask_input, add)
-        return gx, gw, None, None, None, None, None
+        gx, gw = _bwd(x, w, g, ctx.needs_input_grad[0], ctx.needs_input_grad[1], mask_input, add, ctx.st)
+        return gx, gw, None, None, None, None, None, None
 
 
 class _ConvHIPFork(torch.autograd.Function):
@@ -188,20 +201,37 @@ class _ConvHIPFork(torch.autograd.Function):
         return gx, gw, g if ctx.needs_input_grad[2] else None, None, None, None, None
 
 
+def _autocast_operands(x, w, stride, padding, dilation=1, groups=1):
+    """Under bf16 autocast (TrainStep precision "amp": fp32 weights) a
+    convolution computes on bf16 casts of its input and weight -- autocast's
+    own rule for F.conv2d -- so the cast operands go to the HIP kernels too
+    (MIOpen's atomic weight-gradient solvers are not graph-replay safe:
+    DESIGN.md 5)."""
+    if (x.is_cuda and x.dim() == 4 and x.shape[0] > 0 and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16
+            and x.dtype in (torch.float32, torch.bfloat16) and w.dtype in (torch.float32, torch.bfloat16)
+            and hip_conv_ok_for(True, torch.bfloat16, x.shape[1], w, stride, padding, dilation, groups,
+                                w_dtype=torch.bfloat16)):
+        return x.to(torch.bfloat16), w.to(torch.bfloat16)
+    return x, w
+
+
 def conv2d(x, weight, stride=1, padding=0):
     """F.conv2d(x, weight, None, stride, padding) -- on the HIP kernels when
-    hip_conv_ok, else MIOpen."""
-    if hip_conv_ok(x, weight, stride, padding):
-        return _ConvHIP.apply(x, weight)
+    hip_conv_ok (after autocast's bf16 casts), else MIOpen."""
+    xc, wc = _autocast_operands(x, weight, stride, padding)
+    if hip_conv_ok(xc, wc, stride, padding):
+        return _ConvHIP.apply(xc, wc, None, False, False, False, None, _stride(stride))
     return F.conv2d(x, weight, None, stride, padding)
 
 
-def conv2d_bias_relu(x, weight, bias, mask_input=False, grad_premasked=False, link=None):
-    """relu(conv2d(x, weight) + bias[c]) in one HIP launch (stride 1, "same"
-    padding; the caller checked hip_conv_ok).  bias: fp32 [Cout], no gradient.
+def conv2d_bias_relu(x, weight, bias, mask_input=False, grad_premasked=False, link=None, stride=1):
+    """relu(conv2d(x, weight) + bias[c]) in one HIP launch (padding (k-1)/2;
+    the caller checked hip_conv_ok).  bias: fp32 [Cout], no gradient.
     See _ConvHIP for mask_input / grad_premasked, GradLink for link (x a
     block output whose other consumer is the identity shortcut)."""
-    return _ConvHIP.apply(x, weight, bias.float().contiguous(), True, mask_input, grad_premasked, link)
+    return _ConvHIP.apply(x, weight, bias.float().contiguous(), True, mask_input, grad_premasked, link,
+                          _stride(stride))
 
 
 def conv2d_add_bias_relu_fork(x, weight, resid, bias, mask_input=False, link_in=None):
@@ -218,6 +248,8 @@ def conv2d_add_bias_relu_fork(x, weight, resid, bias, mask_input=False, link_in=
 
 def conv_module(conv: torch.nn.Conv2d, x):
     """A bias-free nn.Conv2d applied through conv2d (falls back to the module)."""
-    if conv.bias is None and hip_conv_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups):
-        return _ConvHIP.apply(x, conv.weight)
+    if conv.bias is None:
+        xc, wc = _autocast_operands(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups)
+        if hip_conv_ok(xc, wc, conv.stride, conv.padding, conv.dilation, conv.groups):
+            return _ConvHIP.apply(xc, wc, None, False, False, False, None, _stride(conv.stride))
     return conv(x)

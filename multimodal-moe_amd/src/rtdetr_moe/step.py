@@ -106,13 +106,17 @@ class GraphedModel:
         torch.cuda.synchronize()
         self.pool = torch.cuda.graph_pool_handle()
         self.g_fwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fwd, pool=self.pool):
+        # captured on the warm-up stream: the autograd nodes the warm-up created
+        # (AccumulateGrad keeps the stream it was made on) then match the capture
+        # stream, so the backward needs no cross-stream syncs -- a single chain,
+        # no fork/join branches for the HIP runtime to spread over parallel streams
+        with torch.cuda.graph(self.g_fwd, pool=self.pool, stream=side):
             out = self._run()
         self.static_out = out
         self.diff = [i for i, o in enumerate(out) if o.requires_grad]
         self.static_gout = [torch.zeros_like(o) for o in out]
         self.g_bwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_bwd, pool=self.pool):
+        with torch.cuda.graph(self.g_bwd, pool=self.pool, stream=side):
             grads = torch.autograd.grad([out[i] for i in self.diff], params,
                                         [self.static_gout[i] for i in self.diff], allow_unused=True)
         self.static_grads = [g if g is not None else torch.zeros_like(p) for g, p in zip(grads, params)]
@@ -191,7 +195,7 @@ class GraphedStep:
         torch.cuda.synchronize()
         self.pool = torch.cuda.graph_pool_handle()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=self.pool):
+        with torch.cuda.graph(self.graph, pool=self.pool, stream=side):  # warm-up stream: see GraphedModel
             loss, losses = self._loss()
             grads = self._grads(loss)
             self.static_loss = loss.detach()

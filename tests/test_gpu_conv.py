@@ -1,7 +1,7 @@
 """HIP implicit-GEMM convolutions (csrc/conv.hip) vs a plain PyTorch fp32
 reference of the same op (F.conv2d on the same bf16 operands, upcast):
 forward, data gradient and weight gradient, 1x1 and 3x3, stride 1 with
-"same" padding, NHWC bf16.
+"same" padding, and 3x3 stride 2 (padding 1), NHWC bf16.
 
 Forward tiles of 64, 128 and 256 pixels (rtdetr_conv_set_tuning "conv_bm"),
 weight-gradient rings of 2, 3 and 4 stages ("conv_wg_stages"), 1 / 3 /
@@ -9,6 +9,8 @@ automatic pixel slices ("conv_wg_splits"), the data gradient with the weight
 flipped into a workspace and read in place ("conv_dgrad_flip"), and the
 automatic choices.  Shapes: the C2 encoder's RepVGG convolutions (256 -> 256 at 23x40, batch 8),
 a ResNet bottleneck shape (128 channels), channel-asymmetric layers
+(stride 2: the ResNet-D stage entries and the encoder's downsampling layers,
+odd input sizes included),
 (512 -> 128, 128 -> 256), 64-channel inputs / outputs (ResNet stage 1: the
 64-wide tiles), odd spatial sizes (7 x 9: the partial 128-pixel tile and every
 padding case) and a single image.
@@ -66,27 +68,43 @@ def test_conv_large_auto_paths(hip_lib):
     _conv_case(4, 256, 256, 92, 160, 3)
 
 
-def _conv_case(B, C, N, H, W, ks):
+@pytest.mark.parametrize("knobs", ["auto", "bm64_wg2_flip", "bm128_wg3_inplace"])
+@pytest.mark.parametrize("B,C,N,H,W", [(2, 128, 128, 46, 80), (8, 256, 256, 23, 40), (2, 64, 128, 11, 13),
+                                       (1, 256, 512, 5, 3), (2, 128, 64, 7, 9), (4, 256, 256, 92, 160)])
+def test_conv_stride2_vs_fp32(hip_lib, B, C, N, H, W, knobs):
+    """3x3 stride-2 convolutions (padding 1, even and odd input sizes):
+    forward, the zero-row data gradient and the strided weight gradient."""
+    for k, v in _KNOBS[knobs].items():
+        assert hip_lib.rtdetr_conv_set_tuning(k.encode(), v) == 0
+    try:
+        _conv_case(B, C, N, H, W, 3, stride=2)
+    finally:
+        for k, v in _DEFAULTS.items():
+            hip_lib.rtdetr_conv_set_tuning(k.encode(), v)
+
+
+def _conv_case(B, C, N, H, W, ks, stride=1):
     from src.rtdetr_moe.conv import _ConvHIP, hip_conv_ok
 
     g = torch.Generator(device=DEV).manual_seed(B + C + N + H + ks)
     x = torch.randn(B, C, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(N, C, ks, ks, device=DEV, generator=g) * (C * ks * ks) ** -0.5).to(torch.bfloat16)
     w = w.contiguous(memory_format=torch.channels_last)
-    gy = torch.randn(B, N, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    assert hip_conv_ok(x, w, 1, (ks - 1) // 2)
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    gy = torch.randn(B, N, Ho, Wo, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert hip_conv_ok(x, w, stride, (ks - 1) // 2)
     xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
-    y = _ConvHIP.apply(xa, wa)
-    assert y.shape == (B, N, H, W) and y.is_contiguous(memory_format=torch.channels_last)
+    y = _ConvHIP.apply(xa, wa, None, False, False, False, None, stride)
+    assert y.shape == (B, N, Ho, Wo) and y.is_contiguous(memory_format=torch.channels_last)
     gx, gw = torch.autograd.grad(y, (xa, wa), gy)
     xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
-    yr = F.conv2d(xr, wr, None, 1, (ks - 1) // 2)
+    yr = F.conv2d(xr, wr, None, stride, (ks - 1) // 2)
     gxr, gwr = torch.autograd.grad(yr, (xr, wr), gy.float())
     torch.cuda.synchronize()
     _check(y, yr, "y")
     _check(gx, gxr, "dx")
     _check(gw, gwr, "dw")
-    y2 = _ConvHIP.apply(xa, wa)
+    y2 = _ConvHIP.apply(xa, wa, None, False, False, False, None, stride)
     gx2, gw2 = torch.autograd.grad(y2, (xa, wa), gy)
     torch.cuda.synchronize()
     assert torch.equal(y, y2) and torch.equal(gx, gx2) and torch.equal(gw, gw2)
@@ -98,7 +116,9 @@ def test_conv_dispatch_rules(hip_lib):
 
     x = torch.zeros(1, 256, 8, 8, device=DEV, dtype=torch.bfloat16)
     w3 = torch.zeros(256, 256, 3, 3, device=DEV, dtype=torch.bfloat16)
-    assert hip_conv_ok(x, w3, 1, 1) and not hip_conv_ok(x, w3, 2, 1) and not hip_conv_ok(x, w3, 1, 0)
+    w1 = torch.zeros(256, 256, 1, 1, device=DEV, dtype=torch.bfloat16)
+    assert hip_conv_ok(x, w3, 1, 1) and hip_conv_ok(x, w3, 2, 1) and not hip_conv_ok(x, w3, 1, 0)
+    assert hip_conv_ok(x, w1, 1, 0) and not hip_conv_ok(x, w1, 2, 0) and not hip_conv_ok(x, w3, 3, 1)
     assert not hip_conv_ok(x.float(), w3.float(), 1, 1)
     assert hip_conv_ok(torch.zeros(1, 64, 8, 8, device=DEV, dtype=torch.bfloat16),
                        torch.zeros(64, 64, 3, 3, device=DEV, dtype=torch.bfloat16), 1, 1)

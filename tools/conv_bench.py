@@ -27,7 +27,10 @@ SHAPES = [(8, 256, 256, 46, 80, 3), (8, 256, 256, 92, 160, 3), (8, 256, 256, 23,
           (8, 256, 1024, 46, 80, 1), (8, 512, 128, 92, 160, 1), (8, 128, 512, 92, 160, 1), (8, 2048, 512, 23, 40, 1),
           (8, 512, 2048, 23, 40, 1), (8, 512, 256, 92, 160, 1),
           # ResNet stage 1 (64-channel tiles)
-          (8, 64, 64, 184, 320, 3), (8, 256, 64, 184, 320, 1), (8, 64, 256, 184, 320, 1), (8, 64, 64, 184, 320, 1)]
+          (8, 64, 64, 184, 320, 3), (8, 256, 64, 184, 320, 1), (8, 64, 256, 184, 320, 1), (8, 64, 64, 184, 320, 1),
+          # stride 2 (ResNet-D stage entries, encoder downsampling): input sizes
+          (8, 128, 128, 184, 320, 3, 2), (8, 256, 256, 92, 160, 3, 2), (8, 512, 512, 46, 80, 3, 2),
+          (8, 256, 256, 46, 80, 3, 2)]
 
 
 def timeit(fn, reps=20):
@@ -68,35 +71,38 @@ def main():
         L._check(L.lib().rtdetr_conv_set_tuning(k.encode(), int(v)), "rtdetr_conv_set_tuning")
     if args:
         shapes = [tuple(int(v) for v in s.split(",")) for s in args]
-    for B, Ci, Co, H, W, ks in shapes:
+    for shape in shapes:
+        B, Ci, Co, H, W, ks = shape[:6]
+        st = shape[6] if len(shape) > 6 else 1  # stride (3x3 only for 2)
+        Ho, Wo = (H - 1) // st + 1, (W - 1) // st + 1
         x = torch.randn(B, Ci, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         w = (torch.randn(Co, Ci, ks, ks, device=dev) * 0.05).to(torch.bfloat16).contiguous(
             memory_format=torch.channels_last)
-        gy = torch.randn(B, Co, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        gy = torch.randn(B, Co, Ho, Wo, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         pad = (ks - 1) // 2
-        flop = 2.0 * B * H * W * Ci * Co * ks * ks
-        t_mf = timeit(lambda: F.conv2d(x, w, None, 1, pad))
-        t_md = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [pad, pad], [1, 1], False,
+        flop = 2.0 * B * Ho * Wo * Ci * Co * ks * ks
+        t_mf = timeit(lambda: F.conv2d(x, w, None, st, pad))
+        t_md = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, [st, st], [pad, pad], [1, 1], False,
                                                                   [0, 0], 1, [True, False, False]))
-        t_mw = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [pad, pad], [1, 1], False,
+        t_mw = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, [st, st], [pad, pad], [1, 1], False,
                                                                   [0, 0], 1, [False, True, False]))
         z = C._zero(dev).data_ptr()
         lib = L.lib()
         yh = torch.empty_like(gy)
         t_hf = timeit(lambda: lib.rtdetr_conv_fwd(x.data_ptr(), w.data_ptr(), yh.data_ptr(), z, B, H, W, Ci, Co, ks,
-                                                  None, None, 0, L._stream()))
+                                                  st, None, None, 0, L._stream()))
         gx = torch.empty_like(x)
         nb = lib.rtdetr_conv_dgrad_workspace(B, H, W, Ci, Co, ks)
         wk = torch.empty(max(nb // 2, 8), dtype=torch.bfloat16, device=dev)
         t_hd = timeit(lambda: lib.rtdetr_conv_dgrad(gy.data_ptr(), w.data_ptr(), wk.data_ptr(), gx.data_ptr(), z, B, H,
-                                                    W, Ci, Co, ks, None, None, L._stream()))
-        ns = lib.rtdetr_conv_wgrad_splits(B, H, W, Ci, Co, ks)
+                                                    W, Ci, Co, ks, st, None, None, L._stream()))
+        ns = lib.rtdetr_conv_wgrad_splits(B, Ho, Wo, Ci, Co, ks)
         part = torch.empty(ns * Co * Ci * ks * ks, dtype=torch.float32, device=dev)
         gw = torch.empty_like(w)
         t_hw = timeit(lambda: lib.rtdetr_conv_wgrad(gy.data_ptr(), x.data_ptr(), part.data_ptr(), ns, gw.data_ptr(), 1,
-                                                    z, B, H, W, Ci, Co, ks, L._stream()))
+                                                    z, B, H, W, Ci, Co, ks, st, L._stream()))
         tf = lambda t: round(flop / t / 1e6, 1)  # noqa: E731  TFLOP/s
-        print(json.dumps({"shape": [B, Ci, Co, H, W, ks], "gflop": round(flop / 1e9, 2), "wgrad_splits": ns, "dgrad_flip": nb > 0,
+        print(json.dumps({"shape": list(shape), "gflop": round(flop / 1e9, 2), "wgrad_splits": ns, "dgrad_flip": nb > 0,
                           "miopen_us": [round(t_mf, 1), round(t_md, 1), round(t_mw, 1)],
                           "hip_us": [round(t_hf, 1), round(t_hd, 1), round(t_hw, 1)],
                           "miopen_tflops": [tf(t_mf), tf(t_md), tf(t_mw)], "hip_tflops": [tf(t_hf), tf(t_hd), tf(t_hw)]}),
