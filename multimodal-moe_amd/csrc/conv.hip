@@ -21,8 +21,10 @@
 //                      (y, x) is input (2y + dy, 2x + dx); the data gradient
 //                      of input pixel (y, x) for tap (dy, dx) reads dY at
 //                      ((y + dy) / 2, (x + dx) / 2) when both are even, else
-//                      the zero row (3 of 4 taps on average: wasted MFMA
-//                      work on a few small layers, no scatter, no atomics).
+//                      the zero row -- or, per parity class of the dX pixel
+//                      (one launch each, template flag PH), only its 1, 2, 2
+//                      or 4 valid taps: the zero-row form's sums without its
+//                      4x MFMA work (no scatter, no atomics either way).
 //   conv_wgrad_kernel  dW[n, tap, c] = sum_p dY[p, n] X[nbr(p, tap), c]
 //                      GEMM M = Cout, N = KS^2 Cin, K = pixels, split over S
 //                      slices of the pixels (fp32 partials) and summed in a
@@ -47,6 +49,7 @@ static int g_conv_bm = 0;          // "conv_bm": forward tile rows 64, 128 or 25
 static int g_conv_wg_stages = 0;   // "conv_wg_stages": weight-gradient ring depth 2..4
 static int g_conv_wg_splits = 0;   // "conv_wg_splits": weight-gradient pixel slices
 static int g_conv_dgrad_flip = -1; // "conv_dgrad_flip": 1 = always write W', 0 = always read in place
+static int g_conv_dgrad_phase = 1; // "conv_dgrad_phase": 0 = stride-2 data gradient over all 9 taps (zero rows; A/B)
 
 struct ConvArgs {
   const uint16_t* x;     // [B Hs Ws, C] (fwd: X; dgrad: dY)
@@ -68,6 +71,11 @@ struct ConvArgs {
   const uint16_t* resid;
   const uint16_t* mask;
   int relu;
+  // PH (stride-2 data gradient by parity class): this launch's output pixels
+  // are dX's (b, 2a + ry, 2c + rx), a < H, c < W; dX is [B, Hd, Wd]; the
+  // class's taps are ky' in {1} (ry = 0) or {0, 2} (ry = 1) (kx' likewise),
+  // reading dY at (a + (ky' == 2), c + (kx' == 2))
+  int ry, rx, Hd, Wd;
 };
 
 // Wait until K-tile kt's DMA has landed for this wave: up to min(S - 2, newer)
@@ -94,7 +102,7 @@ __device__ __forceinline__ void dma16(const uint16_t* src, char* lds) {
 // ---------------------------------------------------------------------------
 // forward / data gradient
 // ---------------------------------------------------------------------------
-template <int KS, int S, int BM, int BN, bool BT>
+template <int KS, int S, int BM, int BN, bool BT, bool PH = false>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   static_assert(BN == 64 || BN == 128, "output-channel tile: 64 or 128");
@@ -114,7 +122,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   if (mt >= a.mt_n) return;
   const int m0 = mt * BM, n0 = nt * BN;
   const int cpt = a.C / 64;        // K-tiles per tap
-  const int nk = KS * KS * cpt;
+  const int nty = PH ? 1 + a.ry : KS, ntx = PH ? 1 + a.rx : KS;  // taps per axis
+  const int nk = nty * ntx * cpt;
   const int HW = a.H * a.W, HWs = a.Hs * a.Ws;
   // this lane's A rows (one per DMA instruction j): pixel, coordinates, source chunk
   int py[TM], px[TM], pb[TM], ach[TM];
@@ -149,8 +158,19 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   }
   auto issue = [&](int kt) {
     char* buf = smem + (kt % S) * TILE;
-    const int tap = kt / cpt, c0 = (kt - tap * cpt) * 64;
-    const int dy = tap / KS - PAD, dx = tap % KS - PAD;
+    const int t = kt / cpt, c0 = (kt - t * cpt) * 64;
+    int tap, dy, dx;
+    if constexpr (PH) {  // class tap (ty, tx) -> flipped-weight tap and dY offset (0 or +1 per axis)
+      const int ty = t / ntx, tx = t - ty * ntx;
+      const int ky = a.ry ? 2 * ty : 1, kx = a.rx ? 2 * tx : 1;
+      tap = ky * KS + kx;
+      dy = ky == 2;
+      dx = kx == 2;
+    } else {
+      tap = t;
+      dy = tap / KS - PAD;
+      dx = tap % KS - PAD;
+    }
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       int yy = py[j] * a.st + dy, xx = px[j] * a.st + dx;
@@ -192,11 +212,20 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   constexpr int RPP = 256 / CPR;  // rows per store pass
   const int ec = tid % CPR;
   uint4 eres[BM / RPP], emask[BM / RPP];
+  // global output row of GEMM row p (PH: the class pixel's dX row)
+  auto grow = [&](int p) -> size_t {
+    if constexpr (PH) {
+      const int b = p / HW, rem = p - b * HW, ya = rem / a.W, xc = rem - ya * a.W;
+      return ((size_t)b * a.Hd + 2 * ya + a.ry) * a.Wd + 2 * xc + a.rx;
+    } else {
+      return (size_t)p;
+    }
+  };
   if (a.resid != nullptr || a.mask != nullptr) {
 #pragma unroll
     for (int k = 0; k < BM / RPP; ++k) {
       const int p = m0 + tid / CPR + RPP * k;
-      const size_t g = (size_t)(p < a.P ? p : 0) * a.N + n0 + ec * 8;
+      const size_t g = grow(p < a.P ? p : 0) * a.N + n0 + ec * 8;
       if (a.resid != nullptr) eres[k] = *reinterpret_cast<const uint4*>(a.resid + g);
       if (a.mask != nullptr) emask[k] = *reinterpret_cast<const uint4*>(a.mask + g);
     }
@@ -258,7 +287,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
         }
         v = make_uint4(vw[0], vw[1], vw[2], vw[3]);
       }
-      *reinterpret_cast<uint4*>(a.y + (size_t)p * a.N + n0 + c * 8) = v;
+      *reinterpret_cast<uint4*>(a.y + grow(p) * a.N + n0 + c * 8) = v;
     }
   }
 }
@@ -480,39 +509,43 @@ static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int 
 
 constexpr int CV_STAGES = 2;
 
-template <int KS, int BM, int BN, bool BT>
+template <int KS, int BM, int BN, bool BT, bool PH>
 static void launch_fwd_n(ConvArgs a, hipStream_t stream, ProfScope& prof) {
   constexpr size_t lds = CV_STAGES * (BM + BN) * 128;
   static_assert(lds >= BM * BN * 2, "epilogue image exceeds the ring");
-  allow_lds_once<conv_fwd_kernel<KS, CV_STAGES, BM, BN, BT>>(lds);
+  allow_lds_once<conv_fwd_kernel<KS, CV_STAGES, BM, BN, BT, PH>>(lds);
   a.mt_n = (a.P + BM - 1) / BM;
   const int NT = a.N / BN;
   const int grid = ((a.mt_n + 7) / 8) * 8 * NT;
-  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, CV_STAGES, BM, BN, BT>), dim3(grid), dim3(256), lds, stream, a);
+  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, CV_STAGES, BM, BN, BT, PH>), dim3(grid), dim3(256), lds, stream, a);
 }
 // output-channel tiles of 128, or 64 for 64-channel outputs (ResNet stage 1)
-template <int KS, int BM, bool BT>
+template <int KS, int BM, bool BT, bool PH>
 static void launch_fwd(const ConvArgs& a, hipStream_t stream, ProfScope& prof) {
-  if (a.N % 128 == 0) launch_fwd_n<KS, BM, 128, BT>(a, stream, prof);
-  else launch_fwd_n<KS, BM, 64, BT>(a, stream, prof);
+  if (a.N % 128 == 0) launch_fwd_n<KS, BM, 128, BT, PH>(a, stream, prof);
+  else launch_fwd_n<KS, BM, 64, BT, PH>(a, stream, prof);
 }
 
 // tile rows: 128 (two workgroups per CU); 64 when 128-row tiles would leave
 // the chip under-filled (< 1.5 workgroups per CU); 256 rows (one workgroup per
 // CU) measured slower at every C2 shape
-template <bool BT>
+template <bool BT, bool PH = false>
 static void launch_fwd_any(const ConvArgs& a, int KS, hipStream_t stream, ProfScope& prof) {
   int bm = g_conv_bm;
   if (bm != 64 && bm != 128 && bm != 256)
     bm = (long long)((a.P + 127) / 128) * (a.N / (a.N % 128 == 0 ? 128 : 64)) < 384 ? 64 : 128;
-  if (KS == 3) {
-    if (bm == 256) launch_fwd<3, 256, BT>(a, stream, prof);
-    else if (bm == 64) launch_fwd<3, 64, BT>(a, stream, prof);
-    else launch_fwd<3, 128, BT>(a, stream, prof);
+  if constexpr (PH) {  // 3x3 only
+    if (bm == 256) launch_fwd<3, 256, BT, true>(a, stream, prof);
+    else if (bm == 64) launch_fwd<3, 64, BT, true>(a, stream, prof);
+    else launch_fwd<3, 128, BT, true>(a, stream, prof);
+  } else if (KS == 3) {
+    if (bm == 256) launch_fwd<3, 256, BT, false>(a, stream, prof);
+    else if (bm == 64) launch_fwd<3, 64, BT, false>(a, stream, prof);
+    else launch_fwd<3, 128, BT, false>(a, stream, prof);
   } else {
-    if (bm == 256) launch_fwd<1, 256, BT>(a, stream, prof);
-    else if (bm == 64) launch_fwd<1, 64, BT>(a, stream, prof);
-    else launch_fwd<1, 128, BT>(a, stream, prof);
+    if (bm == 256) launch_fwd<1, 256, BT, false>(a, stream, prof);
+    else if (bm == 64) launch_fwd<1, 64, BT, false>(a, stream, prof);
+    else launch_fwd<1, 128, BT, false>(a, stream, prof);
   }
 }
 
@@ -607,9 +640,32 @@ extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void
     }
     a.w = static_cast<const uint16_t*>(work);
   }
-  // algorithmic flops: the stride-2 zero-row taps are not counted
-  ProfScope prof(stream, PROF_CONV, 2.0 * (P * (C + (relu_mask ? C : 0) + (add ? C : 0)) + Pdy * N) + 2.0 * N * KS * KS * C,
-                 false, 0.0, 2.0 * Pdy * N * KS * KS * C);
+  // algorithmic bytes / flops (the stride-2 zero-row taps are not counted)
+  const double bytes = 2.0 * (P * (C + (relu_mask ? C : 0) + (add ? C : 0)) + Pdy * N) + 2.0 * N * KS * KS * C;
+  const double flops = 2.0 * Pdy * N * KS * KS * C;
+  if (stride == 2 && g_conv_dgrad_phase != 0) {
+    // one launch per parity class (ry, rx) of the dX pixels, each over its valid taps only
+    for (int ry = 0; ry < 2; ++ry)
+      for (int rx = 0; rx < 2; ++rx) {
+        ConvArgs c = a;
+        c.H = (H - ry + 1) / 2;
+        c.W = (W - rx + 1) / 2;
+        c.P = B * c.H * c.W;
+        c.st = 1;
+        c.sh = 0;
+        c.ry = ry;
+        c.rx = rx;
+        c.Hd = H;
+        c.Wd = W;
+        if (c.P == 0) continue;
+        ProfScope prof(stream, PROF_CONV, bytes * c.P / P, false, 0.0, flops * (1 + ry) * (1 + rx) * c.P / (9.0 * Pdy));
+        if (flip) launch_fwd_any<false, true>(c, KS, stream, prof);
+        else launch_fwd_any<true, true>(c, KS, stream, prof);
+        if (int rc = check_launch("rtdetr_conv_dgrad (class)")) return rc;
+      }
+    return 0;
+  }
+  ProfScope prof(stream, PROF_CONV, bytes, false, 0.0, flops);
   if (flip) launch_fwd_any<false>(a, KS, stream, prof);
   else launch_fwd_any<true>(a, KS, stream, prof);
   return check_launch("rtdetr_conv_dgrad");
@@ -672,6 +728,10 @@ extern "C" int rtdetr_conv_set_tuning(const char* key, int value) {
   }
   if (std::string(key) == "conv_dgrad_flip") {
     g_conv_dgrad_flip = value;
+    return 0;
+  }
+  if (std::string(key) == "conv_dgrad_phase") {
+    g_conv_dgrad_phase = value;
     return 0;
   }
   return fail(std::string("rtdetr_conv_set_tuning: unknown key ") + key);

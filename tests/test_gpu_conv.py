@@ -40,8 +40,9 @@ def _check(got, ref, what):
 
 _KNOBS = {"auto": {}, "bm64_wg2_flip": dict(conv_bm=64, conv_wg_stages=2, conv_dgrad_flip=1),
           "bm128_wg3_inplace": dict(conv_bm=128, conv_wg_stages=3, conv_dgrad_flip=0, conv_wg_splits=3),
-          "bm256_wg4_flip": dict(conv_bm=256, conv_wg_stages=4, conv_dgrad_flip=1, conv_wg_splits=1)}
-_DEFAULTS = dict(conv_bm=0, conv_wg_stages=0, conv_dgrad_flip=-1, conv_wg_splits=0)
+          "bm256_wg4_flip": dict(conv_bm=256, conv_wg_stages=4, conv_dgrad_flip=1, conv_wg_splits=1),
+          "zero_rows": dict(conv_dgrad_phase=0), "zero_rows_inplace": dict(conv_dgrad_phase=0, conv_dgrad_flip=0)}
+_DEFAULTS = dict(conv_bm=0, conv_wg_stages=0, conv_dgrad_flip=-1, conv_wg_splits=0, conv_dgrad_phase=1)
 
 
 @pytest.mark.parametrize("knobs", list(_KNOBS))
@@ -68,12 +69,13 @@ def test_conv_large_auto_paths(hip_lib):
     _conv_case(4, 256, 256, 92, 160, 3)
 
 
-@pytest.mark.parametrize("knobs", ["auto", "bm64_wg2_flip", "bm128_wg3_inplace"])
+@pytest.mark.parametrize("knobs", ["auto", "bm64_wg2_flip", "bm128_wg3_inplace", "zero_rows", "zero_rows_inplace"])
 @pytest.mark.parametrize("B,C,N,H,W", [(2, 128, 128, 46, 80), (8, 256, 256, 23, 40), (2, 64, 128, 11, 13),
                                        (1, 256, 512, 5, 3), (2, 128, 64, 7, 9), (4, 256, 256, 92, 160)])
 def test_conv_stride2_vs_fp32(hip_lib, B, C, N, H, W, knobs):
     """3x3 stride-2 convolutions (padding 1, even and odd input sizes):
-    forward, the zero-row data gradient and the strided weight gradient."""
+    forward, the data gradient (per parity class over its valid taps, or all
+    nine taps with zero rows) and the strided weight gradient."""
     for k, v in _KNOBS[knobs].items():
         assert hip_lib.rtdetr_conv_set_tuning(k.encode(), v) == 0
     try:
@@ -231,3 +233,27 @@ def test_block_chain_grad_link_matches_unfused(hip_lib, cin, width):
     assert torch.equal(za, zb)
     for u, v in zip(ga, gb):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("B,C,N,H,W", [(2, 128, 128, 46, 80), (2, 64, 128, 11, 13), (1, 256, 512, 5, 3)])
+def test_conv_stride2_dgrad_classes_match_zero_rows(hip_lib, B, C, N, H, W):
+    """The parity-class data gradient sums the same nonzero products in the
+    same order as the all-taps zero-row form: bitwise equal, with the fused
+    add + ReLU-mask epilogue scattered to the class pixels."""
+    from src.rtdetr_moe import conv as CV
+
+    g = torch.Generator(device=DEV).manual_seed(H * W + C)
+    cl = dict(memory_format=torch.channels_last)
+    x = torch.relu(torch.randn(B, C, H, W, device=DEV, generator=g)).to(torch.bfloat16).contiguous(**cl)
+    w = (torch.randn(N, C, 3, 3, device=DEV, generator=g) * (9 * C) ** -0.5).to(torch.bfloat16).contiguous(**cl)
+    gy = torch.randn(B, N, (H + 1) // 2, (W + 1) // 2, device=DEV, generator=g).to(torch.bfloat16).contiguous(**cl)
+    add = torch.randn(B, C, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(**cl)
+    outs = []
+    for phase in (1, 0):
+        assert hip_lib.rtdetr_conv_set_tuning(b"conv_dgrad_phase", phase) == 0
+        try:
+            outs.append(CV._bwd(x, w, gy, True, False, True, add, 2)[0])
+        finally:
+            hip_lib.rtdetr_conv_set_tuning(b"conv_dgrad_phase", 1)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
