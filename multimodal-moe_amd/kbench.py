@@ -51,11 +51,17 @@ def timed(fn, reps):
     return 1e3 * statistics.median(sum(ms[i:i + per]) for i in range(0, len(ms) - per + 1, per))
 
 
+SKEW = [0.0]
+
+
 def setup(T, E, k, d, F, seed=0):
     g = torch.Generator(device="cuda").manual_seed(seed)
     x = torch.randn((T, d), device="cuda", generator=g).to(torch.bfloat16)
     wg = (torch.randn((E, d), device="cuda", generator=g) * 0.3).float()
     cb = torch.randn((6, E), device="cuda", generator=g).float() * 0.5
+    # --skew: an expert preference in the context bias, so the routed counts
+    # differ between experts as in a real model (C2 layers: max/mean 1.9-3.2x)
+    cb += SKEW[0] * torch.linspace(0.0, 1.0, E, device="cuda")
     ci = torch.randint(0, 6, (T // 920 if T % 920 == 0 else T // 300,), device="cuda", generator=g).int()
     tpi = 920 if T % 920 == 0 else 300
     w1 = (torch.randn((E, F, d), device="cuda", generator=g) / 16).to(torch.bfloat16)
@@ -165,8 +171,10 @@ def main():
     ap.add_argument("--pair", default="1", help="comma list of gemm_pair modes (1 one launch, 0 two launches)")
     ap.add_argument("--wg", default="0:0", help="comma list of gathered-wgrad bodies dma:stages (dma 0 auto / 1 "
                                                 "register-staged; stages 0 auto, 2, 3)")
+    ap.add_argument("--skew", type=float, default=0.0, help="expert preference added to the context bias")
     ap.add_argument("--cold", action="store_true", help="flush the Infinity Cache (512 MiB read) before every call")
     a = ap.parse_args()
+    SKEW[0] = a.skew
     L.lib()
     if a.cold:
         global _FLUSH
@@ -215,7 +223,7 @@ def main():
     for (name, sname, v, s, dbg, bm, xm, ks, pr, wg, flops, byts), ts in res.items():
         us = statistics.median(ts)
         d = {"kernel": name, "config": a.config, "shape": sname, "variant": v, "stages": s, "debug": dbg, "bm": bm,
-             "xcd": xm, "ksplit": ks, "pair": pr, "wg": wg, "cold": a.cold, "us": round(us, 2),
+             "xcd": xm, "ksplit": ks, "pair": pr, "wg": wg, "skew": a.skew, "cold": a.cold, "us": round(us, 2),
              "min_us": round(min(ts), 2)}
         if flops:
             d["tflops"] = round(flops / us / 1e6, 1)
