@@ -727,6 +727,91 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Router weight gradients (the router's backward after
+// token_bwd): dWg[e][c] = sum_t dlogits[t][e] x[t][c] and the context-bias
+// gradient dcb[ctx][e] = sum over the images b with ctx_img[b] == ctx of
+// sum_{t in b} dlogits[t][e].  Replaces torch's fp32 copy of x, the fp32 GEMM
+// dlogits^T x and the atomic index_add_ (whose arrival order made dcb
+// non-repeatable): two launches, fixed-order sums (bitwise repeatable).
+//   router_wgrad_part_kernel : one workgroup per (image, slice of <= 64
+//     tokens): the slice's x and dlogits rows staged in LDS by loads all
+//     issued up front (one round trip), thread c owns columns
+//     c, c + 256, ... of d and keeps E fp32 sums per column; slice partials
+//     [S][E][d] and [S][E] (dlogits column sums)
+//   router_wgrad_final_kernel: dWg = sum of the slice partials in slice order;
+//     workgroup 0 also forms dcb (contexts in id order, images in order)
+// ---------------------------------------------------------------------------
+constexpr int kRwSlice = 64;  // tokens per slice (at most)
+
+template <int EM>
+__global__ __launch_bounds__(256) void router_wgrad_part_kernel(const float* __restrict__ dlogits,
+                                                                const uint16_t* __restrict__ x, int tpi, int spi,
+                                                                int E, int d, float* __restrict__ part_w,
+                                                                float* __restrict__ part_c) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sdl = reinterpret_cast<float*>(smem);                          // [n][E] dlogits rows
+  uint16_t* sx = reinterpret_cast<uint16_t*>(smem + kRwSlice * EM * 4);  // [n][d] x rows
+  const int s = blockIdx.x, b = s / spi, j = s - b * spi;
+  const int len = (tpi + spi - 1) / spi;
+  const int t0 = b * tpi + j * len, n = max(0, min(len, tpi - j * len));
+  const int tid = threadIdx.x;
+  // every load of the slice issued before any use: one memory round trip
+  const int nch = n * d / 8;  // 16-B chunks of the x rows (contiguous: rows t0 .. t0 + n - 1)
+  const uint4* xs = reinterpret_cast<const uint4*>(x + (size_t)t0 * d);
+  for (int q = tid; q < nch; q += 256) reinterpret_cast<uint4*>(sx)[q] = xs[q];
+  for (int q = tid; q < n * E; q += 256) sdl[q] = dlogits[(size_t)t0 * E + q];
+  __syncthreads();
+  if (tid < E) {  // this slice's dlogits column sum (context-bias gradient), in token order
+    float cs = 0.f;
+    for (int t = 0; t < n; ++t) cs += sdl[t * E + tid];
+    part_c[(size_t)s * E + tid] = cs;
+  }
+  for (int c = tid; c < d; c += 256) {
+    float acc[EM];
+#pragma unroll
+    for (int e = 0; e < EM; ++e) acc[e] = 0.f;
+    for (int t = 0; t < n; ++t) {
+      const float xv = bf2f(sx[t * d + c]);
+#pragma unroll
+      for (int e = 0; e < EM; ++e)
+        if (e < E) acc[e] += sdl[t * E + e] * xv;
+    }
+#pragma unroll
+    for (int e = 0; e < EM; ++e)
+      if (e < E) part_w[((size_t)s * E + e) * d + c] = acc[e];
+  }
+}
+
+__global__ __launch_bounds__(256) void router_wgrad_final_kernel(const float* __restrict__ part_w,
+                                                                 const float* __restrict__ part_c, int S, int spi,
+                                                                 int E, int d, const int32_t* __restrict__ ctx_img,
+                                                                 int C, float* __restrict__ dwg,
+                                                                 float* __restrict__ dcb) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int n = E * d;
+  if (i < n) {
+    float acc = 0.f;
+    for (int s = 0; s < S; ++s) acc += part_w[(size_t)s * n + i];
+    dwg[i] = acc;
+  }
+  if (blockIdx.x == 0 && dcb != nullptr) {
+    const int B = S / spi;
+    for (int q = threadIdx.x; q < C * E; q += 256) {
+      const int cx = q / E, e = q - cx * E;
+      float acc = 0.f;
+      for (int b = 0; b < B; ++b) {
+        if (ctx_img[b] != cx) continue;
+        float sb = 0.f;
+        for (int j = 0; j < spi; ++j) sb += part_c[(size_t)(b * spi + j) * E + e];
+        acc += sb;
+      }
+      dcb[q] = acc;
+    }
+  }
+}
+
 }  // namespace moe
 
 // ---------------------------------------------------------------------------
@@ -897,4 +982,55 @@ extern "C" int moe_aux_loss_fwd(const float* aux_partials, int nblk, int E, cons
   MOE_LAUNCH(prof, aux_loss_fwd_kernel, dim3(1), dim3(256), 0, stream, aux_partials, nblk, E, hist, T, k, lb_coef,
              z_coef, out3, wcoef);
   return check_launch("moe_aux_loss_fwd");
+}
+
+extern "C" int moe_router_wgrad_slices(int tpi) { return tpi <= 0 ? 0 : (tpi + kRwSlice - 1) / kRwSlice; }
+
+extern "C" int moe_router_wgrad(const float* dlogits, const void* x, const int32_t* ctx_img, int B, int tpi, int E,
+                                int d, int C, float* part, float* dwg, float* dcb, hipStream_t stream) {
+  if (B < 0 || tpi < 1 || E < 1 || E > 64 || d < 8 || d > 1024 || d % 8 || C < 0)
+    return fail("router_wgrad: need B >= 0, tpi >= 1, 1 <= E <= 64, d % 8 == 0 in [8, 1024], C >= 0");
+  if (reinterpret_cast<uintptr_t>(x) % 16) return fail("router_wgrad: x must be 16-B aligned");
+  if (dlogits == nullptr || x == nullptr || part == nullptr || dwg == nullptr)
+    return fail("router_wgrad: NULL pointer");
+  if (dcb != nullptr && (ctx_img == nullptr || C < 1)) return fail("router_wgrad: dcb needs ctx_img and C >= 1");
+  const int spi = moe_router_wgrad_slices(tpi);
+  const int S = B * spi;
+  if (S == 0) {  // no tokens: zero gradients
+    if (hipMemsetAsync(dwg, 0, sizeof(float) * E * d, stream) != hipSuccess) return fail("router_wgrad: memset");
+    if (dcb != nullptr && hipMemsetAsync(dcb, 0, sizeof(float) * C * E, stream) != hipSuccess)
+      return fail("router_wgrad: memset");
+    return 0;
+  }
+  float* part_w = part;
+  float* part_c = part + (size_t)S * E * d;
+  const double T = (double)B * tpi;
+  {
+    ProfScope prof(stream, PROF_TOKEN_BWD, 4.0 * T * E + 2.0 * T * d + 4.0 * S * E * (d + 1));
+    const int em = E <= 8 ? 8 : (E <= 16 ? 16 : (E <= 32 ? 32 : 64));
+    const size_t lds = (size_t)kRwSlice * em * 4 + (size_t)kRwSlice * d * 2;
+#define LAUNCH_RW(EM_)                                                                                        \
+  do {                                                                                                        \
+    static bool lds_set = false; /* > 64 KiB of dynamic LDS needs the attribute (d > 384) */                   \
+    if (!lds_set) {                                                                                           \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(router_wgrad_part_kernel<EM_>),                 \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);                      \
+      lds_set = true;                                                                                         \
+    }                                                                                                         \
+    MOE_LAUNCH(prof, router_wgrad_part_kernel<EM_>, dim3(S), dim3(256), lds, stream, dlogits,                 \
+               static_cast<const uint16_t*>(x), tpi, spi, E, d, part_w, part_c);                              \
+  } while (0)
+    switch (em) {
+      case 8: LAUNCH_RW(8); break;
+      case 16: LAUNCH_RW(16); break;
+      case 32: LAUNCH_RW(32); break;
+      default: LAUNCH_RW(64); break;
+    }
+#undef LAUNCH_RW
+    if (int rc = check_launch("moe_router_wgrad (part)")) return rc;
+  }
+  ProfScope prof(stream, PROF_TOKEN_BWD, 4.0 * S * E * (d + 1) + 4.0 * E * d + 4.0 * C * E);
+  MOE_LAUNCH(prof, router_wgrad_final_kernel, dim3((E * d + 255) / 256), dim3(256), 0, stream, part_w, part_c, S,
+             spi, E, d, ctx_img, C, dwg, dcb);
+  return check_launch("moe_router_wgrad");
 }

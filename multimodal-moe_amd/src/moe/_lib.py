@@ -81,6 +81,8 @@ SIGNATURES = {
                                       _P, _I, _P, _P, _P]),
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "moe_set_splitk_workspace": (_I, [_P, ctypes.c_size_t, _P, _I]),
+    "moe_router_wgrad_slices": (_I, [_I]),
+    "moe_router_wgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "rtdetr_hungarian_match": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "rtdetr_set_criterion_match": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "rtdetr_set_criterion_loss": (_I, [_P, _P, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
@@ -518,6 +520,30 @@ def token_bwd_dw(dxp, pos, probs, topk_idx, topk_w, dy, yp, lse, dprob_bias, zc,
                                   _ptr(yp), _ptr(dw), _ptr(lse), _ptr(dprob_bias), _ptr(zc), _ptr(wg), T, d, E, k,
                                   int(normalize), _ptr(dx), _ptr(dlogits), _stream()), "moe_token_bwd_dw")
     return dx, dlogits, dw
+
+
+def router_wgrad(dlogits, x, ctx_img, tokens_per_image, n_ctx):
+    """(dwg fp32 [E, d], dcb fp32 [n_ctx, E] or None): the router weight and
+    context-bias gradients from token_bwd's dlogits (moe_router_wgrad)."""
+    _need(dlogits, torch.float32, "dlogits")
+    _need(x, torch.bfloat16, "x")
+    T, E = dlogits.shape
+    d = x.shape[1]
+    tpi = int(tokens_per_image)
+    if T % tpi:
+        raise MoEKernelError(f"router_wgrad: T = {T} is not a multiple of tokens_per_image = {tpi}")
+    B = T // tpi
+    S = B * int(lib().moe_router_wgrad_slices(tpi))
+    part = torch.empty(max(1, S * E * (d + 1)), dtype=torch.float32, device=x.device)
+    dwg = torch.empty((E, d), dtype=torch.float32, device=x.device)
+    dcb = None
+    if ctx_img is not None and n_ctx > 0:
+        _need(ctx_img, torch.int32, "ctx_img")
+        dcb = torch.empty((n_ctx, E), dtype=torch.float32, device=x.device)
+    _check(lib().moe_router_wgrad(_ptr(dlogits), _ptr(x), _ptr(ctx_img) if dcb is not None else None, B, tpi, E, d,
+                                  int(n_ctx) if dcb is not None else 0, _ptr(part), _ptr(dwg), _ptr(dcb), _stream()),
+           "moe_router_wgrad")
+    return dwg, dcb
 
 
 def aux_loss_fwd(auxp, hist, T, k, lb_coef, z_coef):

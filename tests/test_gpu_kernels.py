@@ -584,3 +584,27 @@ def test_route_dispatch_matches_scan_index_aux(hip_lib, T, E, k, cf):
     assert torch.equal(out, out2) and torch.equal(wcoef, wcoef2)
     keep = pos2 >= 0
     assert torch.equal(gate2[pos2[keep].long()], w[keep])
+
+
+@pytest.mark.parametrize("B,tpi,E,C", [(3, 920, 8, 6), (8, 300, 8, 6), (2, 17, 32, 4), (1, 130, 16, 1)])
+def test_router_wgrad_vs_fp64(hip_lib, B, tpi, E, C):
+    """moe_router_wgrad: dWg = dlogits^T x and the per-context sums of
+    dlogits (contexts repeated across images, one context unused) against an
+    fp64 reference; fixed-order sums, so two launches are bitwise equal."""
+    from src.moe import _lib as L
+
+    g = torch.Generator(device=DEV).manual_seed(B * tpi + E)
+    T, d = B * tpi, 256
+    dl = torch.randn((T, E), device=DEV, generator=g)
+    x = torch.randn((T, d), device=DEV, generator=g).to(torch.bfloat16)
+    ci = torch.randint(0, max(1, C - 1), (B,), device=DEV, generator=g).to(torch.int32)
+    dwg, dcb = L.router_wgrad(dl, x, ci, tpi, C)
+    dwg2, dcb2 = L.router_wgrad(dl, x, ci, tpi, C)
+    dwg0, dcb0 = L.router_wgrad(dl, x, None, tpi, 0)
+    torch.cuda.synchronize()
+    ref = dl.double().t() @ x.double()
+    per_img = dl.double().view(B, tpi, E).sum(1)
+    ref_cb = torch.zeros((C, E), dtype=torch.float64, device=DEV).index_add_(0, ci.long(), per_img)
+    assert ((dwg.double() - ref).norm() / ref.norm()).item() < 1e-5
+    assert (dcb.double() - ref_cb).abs().max().item() <= 1e-4 * max(1.0, ref_cb.abs().max().item())
+    assert torch.equal(dwg, dwg2) and torch.equal(dcb, dcb2) and torch.equal(dwg, dwg0) and dcb0 is None
