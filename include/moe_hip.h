@@ -636,7 +636,9 @@ int train_adamw_step(const void* tensors, const int32_t* chunks, int n_chunks, c
  * back from the device offsets.  Kinds: 0 grouped GEMM, 1 permute/combine row
  * moves, 2 router, 3 route scan, 4 token backward, 5 deformable attention,
  * 6 MXFP8 weight quantizer, 7 backbone convolution epilogues, 8 optimizer,
- * 9 Hungarian matching, 10 fp8 grouped GEMM, 11 dense linear weight gradients.
+ * 9 Hungarian matching, 10 fp8 grouped GEMM, 11 dense linear weight gradients,
+ * 12 self-attention, 13 implicit-GEMM convolutions, 14 router weight /
+ * context-bias gradients.
  * Not thread-safe, not for graph capture.  enable(0|1) also clears; get()
  * waits for the record. */
 enum moe_prof_kind {

@@ -31,7 +31,8 @@ enum ProfKind {
   PROF_GEMM_FP8 = 10,  // grouped GEMM on the fp8 (MXFP8 e4m3) MFMA: priced against the fp8 peak
   PROF_LINEAR = 11,    // dense linear weight + bias gradients (rtdetr_linear_wgrad)
   PROF_ATTN = 12,      // multi-head self-attention (rtdetr_attn_fwd / _bwd)
-  PROF_CONV = 13       // implicit-GEMM convolutions (rtdetr_conv_*)
+  PROF_CONV = 13,      // implicit-GEMM convolutions (rtdetr_conv_*)
+  PROF_ROUTER_WGRAD = 14  // router weight / context-bias gradients (moe_router_wgrad)
 };
 
 class ProfScope {

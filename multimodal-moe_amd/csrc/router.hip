@@ -1006,7 +1006,7 @@ extern "C" int moe_router_wgrad(const float* dlogits, const void* x, const int32
   float* part_c = part + (size_t)S * E * d;
   const double T = (double)B * tpi;
   {
-    ProfScope prof(stream, PROF_TOKEN_BWD, 4.0 * T * E + 2.0 * T * d + 4.0 * S * E * (d + 1));
+    ProfScope prof(stream, PROF_ROUTER_WGRAD, 4.0 * T * E + 2.0 * T * d + 4.0 * S * E * (d + 1));
     const int em = E <= 8 ? 8 : (E <= 16 ? 16 : (E <= 32 ? 32 : 64));
     const size_t lds = (size_t)kRwSlice * em * 4 + (size_t)kRwSlice * d * 2;
 #define LAUNCH_RW(EM_)                                                                                        \
@@ -1029,7 +1029,7 @@ extern "C" int moe_router_wgrad(const float* dlogits, const void* x, const int32
 #undef LAUNCH_RW
     if (int rc = check_launch("moe_router_wgrad (part)")) return rc;
   }
-  ProfScope prof(stream, PROF_TOKEN_BWD, 4.0 * S * E * (d + 1) + 4.0 * E * d + 4.0 * C * E);
+  ProfScope prof(stream, PROF_ROUTER_WGRAD, 4.0 * S * E * (d + 1) + 4.0 * E * d + 4.0 * C * E);
   MOE_LAUNCH(prof, router_wgrad_final_kernel, dim3((E * d + 255) / 256), dim3(256), 0, stream, part_w, part_c, S,
              spi, E, d, ctx_img, C, dwg, dcb);
   return check_launch("moe_router_wgrad");
