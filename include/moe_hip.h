@@ -167,8 +167,10 @@ int moe_router_wgrad_slices(int tpi);
 int moe_router_wgrad(const float* dlogits, const void* x, const int32_t* ctx_img, int B, int tpi, int E, int d,
                      int C, float* part, float* dwg, float* dcb, hipStream_t stream);
 
-/* Grouped GEMM data types / epilogues. */
-enum moe_dtype { MOE_BF16 = 0, MOE_FP8_E4M3 = 1 };
+/* Grouped GEMM data types / epilogues.  MOE_BIAS_BF16 OR'd into the dtype of
+ * moe_grouped_gemm / moe_grouped_gemm_gather: the bias epilogues read a bf16
+ * bias [G][N] (the bf16 parameter itself; no fp32 copy per call). */
+enum moe_dtype { MOE_BF16 = 0, MOE_FP8_E4M3 = 1, MOE_BIAS_BF16 = 0x100 };
 enum moe_epilogue {
   MOE_EPI_NONE = 0,      /* C = A.B                                   */
   MOE_EPI_BIAS = 1,      /* C = A.B + bias[g, n]                      */

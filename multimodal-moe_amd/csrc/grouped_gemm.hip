@@ -91,6 +91,7 @@ struct GemmParams {
   // WGRAD, G = 1 with offsets == nullptr: the group's rows are [0, dense_rows)
   // (a dense linear layer's weight gradient; no device offsets to load)
   int dense_rows;
+  int bias_bf16;  // ROWS bias epilogues: bias is bf16 [G][N] (the bf16 parameter itself, no fp32 copy)
 };
 
 // runtime tuning knobs (moe_set_tuning)
@@ -299,8 +300,15 @@ __device__ __forceinline__ void prefetch_bias(const GemmParams& p, int g, int n0
   if constexpr (MODE == MODE_ROWS && (EPI == MOE_EPI_BIAS || EPI == MOE_EPI_BIAS_RELU)) {
     const int ln = 4 * (lane >> 4);
 #pragma unroll
-    for (int j = 0; j < BN / 32; ++j)
-      bpre[j] = *reinterpret_cast<const float4*>(p.bias + (size_t)g * p.N + n0 + wn * (BN / 2) + 16 * j + ln);
+    for (int j = 0; j < BN / 32; ++j) {
+      const size_t o = (size_t)g * p.N + n0 + wn * (BN / 2) + 16 * j + ln;
+      if (p.bias_bf16) {
+        const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(p.bias) + o);
+        bpre[j] = make_float4(bf2f(v.x & 0xffffu), bf2f(v.x >> 16), bf2f(v.y & 0xffffu), bf2f(v.y >> 16));
+      } else {
+        bpre[j] = *reinterpret_cast<const float4*>(p.bias + o);
+      }
+    }
   }
 }
 
@@ -1650,10 +1658,13 @@ extern "C" int moe_set_tuning(const char* key, int value) {
 extern "C" int moe_grouped_gemm_gather(int dtype, const void* a, const int32_t* a_gather, const void* b, void* c,
                                        const int32_t* offsets, int G, int max_rows, int N, int K, int trans_b,
                                        int epilogue, const float* bias, const void* aux, hipStream_t stream) {
-  if (dtype != MOE_BF16) return fail("grouped_gemm: only MOE_BF16 is implemented");
+  const bool bias16 = (dtype & MOE_BIAS_BF16) != 0;
+  if ((dtype & ~MOE_BIAS_BF16) != MOE_BF16) return fail("grouped_gemm: only MOE_BF16 is implemented");
   RowsPlan pl;
   WsWin win = device_ws();
   if (plan_rows(pl, a, b, c, offsets, G, max_rows, N, K, trans_b, epilogue, bias, aux, a_gather, win)) return -1;
+  pl.p.bias_bf16 = bias16 ? 1 : 0;
+  if (bias16) pl.bytes_fixed -= 2.0 * G * N;  // bias bytes: 2 per element, not 4
   if (max_rows == 0) return 0;
   ProfScope prof(stream, PROF_GEMM, pl.bytes_fixed, true, pl.bytes_row, pl.flops_row);
   pl.p.prof_rows = prof.rows_slot();

@@ -760,7 +760,19 @@ __global__ __launch_bounds__(256) void router_wgrad_part_kernel(const float* __r
   // every load of the slice issued before any use: one memory round trip
   const int nch = n * d / 8;  // 16-B chunks of the x rows (contiguous: rows t0 .. t0 + n - 1)
   const uint4* xs = reinterpret_cast<const uint4*>(x + (size_t)t0 * d);
-  for (int q = tid; q < nch; q += 256) reinterpret_cast<uint4*>(sx)[q] = xs[q];
+  for (int q0 = tid; q0 < nch; q0 += 256 * 8) {  // 8 loads per thread in flight, then their LDS stores
+    uint4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int q = q0 + 256 * u;
+      if (q < nch) v[u] = xs[q];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int q = q0 + 256 * u;
+      if (q < nch) reinterpret_cast<uint4*>(sx)[q] = v[u];
+    }
+  }
   for (int q = tid; q < n * E; q += 256) sdl[q] = dlogits[(size_t)t0 * E + q];
   __syncthreads();
   if (tid < E) {  // this slice's dlogits column sum (context-bias gradient), in token order
@@ -789,26 +801,51 @@ __global__ __launch_bounds__(256) void router_wgrad_final_kernel(const float* __
                                                                  int E, int d, const int32_t* __restrict__ ctx_img,
                                                                  int C, float* __restrict__ dwg,
                                                                  float* __restrict__ dcb) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  // dWg: 64 outputs per workgroup x 4 slice groups; group q sums slices q, q + 4, ... in order, 8 loads in
+  // flight per round, then the 4 group sums are added in group order (fixed order: repeatable)
+  __shared__ float red[4][64];
+  __shared__ float pimg[2048];  // per-image dlogits sums [B][E] (B E <= 2048, host-checked)
+  const int tid = threadIdx.x, q = tid >> 6, l = tid & 63;
   const int n = E * d;
-  if (i < n) {
-    float acc = 0.f;
-    for (int s = 0; s < S; ++s) acc += part_w[(size_t)s * n + i];
-    dwg[i] = acc;
-  }
-  if (blockIdx.x == 0 && dcb != nullptr) {
-    const int B = S / spi;
-    for (int q = threadIdx.x; q < C * E; q += 256) {
-      const int cx = q / E, e = q - cx * E;
-      float acc = 0.f;
-      for (int b = 0; b < B; ++b) {
-        if (ctx_img[b] != cx) continue;
-        float sb = 0.f;
-        for (int j = 0; j < spi; ++j) sb += part_c[(size_t)(b * spi + j) * E + e];
-        acc += sb;
+  const int o = blockIdx.x * 64 + l;
+  float acc = 0.f;
+  if (o < n) {
+    for (int s0 = q; s0 < S; s0 += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int s = s0 + 4 * u;
+        v[u] = s < S ? part_w[(size_t)s * n + o] : 0.f;
       }
-      dcb[q] = acc;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
     }
+  }
+  red[q][l] = acc;
+  __syncthreads();
+  if (q == 0 && o < n) dwg[o] = ((red[0][l] + red[1][l]) + red[2][l]) + red[3][l];
+  if (blockIdx.x != gridDim.x - 1 || dcb == nullptr) return;
+  // dcb (last workgroup): per-image sums of the slice column sums (all loads of a thread issued together),
+  // then per context the images in order
+  const int B = S / spi;
+  for (int be = tid; be < B * E; be += 256) {
+    const int bb = be / E, e = be - bb * E;
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = j < spi ? part_c[(size_t)(bb * spi + j) * E + e] : 0.f;
+    float sb = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) sb += v[j];
+    for (int j = 32; j < spi; ++j) sb += part_c[(size_t)(bb * spi + j) * E + e];
+    pimg[be] = sb;
+  }
+  __syncthreads();
+  for (int ce = tid; ce < C * E; ce += 256) {
+    const int cx = ce / E, e = ce - cx * E;
+    float sum = 0.f;
+    for (int bb = 0; bb < B; ++bb)
+      if (ctx_img[bb] == cx) sum += pimg[bb * E + e];
+    dcb[ce] = sum;
   }
 }
 
@@ -994,6 +1031,7 @@ extern "C" int moe_router_wgrad(const float* dlogits, const void* x, const int32
   if (dlogits == nullptr || x == nullptr || part == nullptr || dwg == nullptr)
     return fail("router_wgrad: NULL pointer");
   if (dcb != nullptr && (ctx_img == nullptr || C < 1)) return fail("router_wgrad: dcb needs ctx_img and C >= 1");
+  if (dcb != nullptr && B * E > 2048) return fail("router_wgrad: B E must be <= 2048 with a context-bias gradient");
   const int spi = moe_router_wgrad_slices(tpi);
   const int S = B * spi;
   if (S == 0) {  // no tokens: zero gradients
@@ -1030,7 +1068,7 @@ extern "C" int moe_router_wgrad(const float* dlogits, const void* x, const int32
     if (int rc = check_launch("moe_router_wgrad (part)")) return rc;
   }
   ProfScope prof(stream, PROF_ROUTER_WGRAD, 4.0 * S * E * (d + 1) + 4.0 * E * d + 4.0 * C * E);
-  MOE_LAUNCH(prof, router_wgrad_final_kernel, dim3((E * d + 255) / 256), dim3(256), 0, stream, part_w, part_c, S,
+  MOE_LAUNCH(prof, router_wgrad_final_kernel, dim3((E * d + 63) / 64), dim3(256), 0, stream, part_w, part_c, S,
              spi, E, d, ctx_img, C, dwg, dcb);
   return check_launch("moe_router_wgrad");
 }

@@ -19,6 +19,7 @@ LIB_PATH = Path(os.environ.get("MOE_HIP_LIB", _PKG / "lib" / "libmoe_hip.so"))
 
 MOE_BF16 = 0
 MOE_FP8_E4M3 = 1
+MOE_BIAS_BF16 = 0x100  # OR into the grouped-GEMM dtype: bf16 bias
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK, EPI_RELU_MASK_MX = 0, 1, 2, 3, 4
 MX_BLOCK = 32  # MXFP8: one E8M0 exponent byte per 32 e4m3 elements of a row
 
@@ -404,10 +405,19 @@ def grouped_gemm(a, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None,
     c = out if out is not None else torch.empty((a.shape[0], N), dtype=torch.bfloat16, device=a.device)
     ensure_splitk_workspace(a.device)
     rc = lib().moe_grouped_gemm(
-        MOE_BF16, _ptr(a), _ptr(b), _ptr(c), _ptr(offsets), G, int(max_rows), N, K, int(trans_b),
+        _gemm_dtype(bias, G, N), _ptr(a), _ptr(b), _ptr(c), _ptr(offsets), G, int(max_rows), N, K, int(trans_b),
         int(epilogue), _ptr(bias), _ptr(aux), None, _stream())
     _check(rc, "moe_grouped_gemm")
     return c
+
+
+def _gemm_dtype(bias, G, N):
+    """MOE_BF16, | MOE_BIAS_BF16 when the bias is a bf16 tensor (read as is)."""
+    if bias is None:
+        return MOE_BF16
+    if bias.dtype not in (torch.float32, torch.bfloat16) or not bias.is_contiguous() or bias.numel() != G * N:
+        raise MoEKernelError(f"grouped_gemm: bias must be a contiguous fp32 / bf16 [G, N] tensor ({G} x {N})")
+    return MOE_BF16 | (MOE_BIAS_BF16 if bias.dtype == torch.bfloat16 else 0)
 
 
 def route_index(topk_idx, local_rank, rank_base, offsets, E, cap, rows_alloc):
@@ -453,7 +463,8 @@ def grouped_gemm_gather(x, src_tok, b, offsets, G, max_rows, N, K, trans_b, epil
         raise MoEKernelError("grouped_gemm_gather: shapes")
     c = torch.empty((max(max_rows, 1), N), dtype=torch.bfloat16, device=x.device)
     ensure_splitk_workspace(x.device)
-    _check(lib().moe_grouped_gemm_gather(MOE_BF16, _ptr(x), _ptr(src_tok), _ptr(b), _ptr(c), _ptr(offsets), G,
+    _check(lib().moe_grouped_gemm_gather(_gemm_dtype(bias, G, N), _ptr(x), _ptr(src_tok), _ptr(b), _ptr(c),
+                                         _ptr(offsets), G,
                                          int(max_rows), N, K, int(trans_b), int(epilogue), _ptr(bias), _ptr(aux),
                                          _stream()), "moe_grouped_gemm_gather")
     return c

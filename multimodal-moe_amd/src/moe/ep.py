@@ -42,6 +42,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from .ops import _bias
+
 
 def _a2a(out, x, group, W):
     if W == 1 and group is None:  # -ep1 without a process group: identity exchange
@@ -137,9 +139,8 @@ class _EPExpertFFN(torch.autograd.Function):
         xb = xr.to(torch.bfloat16).contiguous()
         w1b = w1.to(torch.bfloat16).contiguous()
         w2b = w2.to(torch.bfloat16).contiguous()
-        h = L.grouped_gemm_gather(xb, gather, w1b, offsets, G, R, F, d, 1, L.EPI_BIAS_RELU,
-                                  bias=b1.float().contiguous())
-        ye = L.grouped_gemm(h, w2b, offsets, G, R, d, F, 1, L.EPI_BIAS, bias=b2.float().contiguous())
+        h = L.grouped_gemm_gather(xb, gather, w1b, offsets, G, R, F, d, 1, L.EPI_BIAS_RELU, bias=_bias(b1))
+        ye = L.grouped_gemm(h, w2b, offsets, G, R, d, F, 1, L.EPI_BIAS, bias=_bias(b2))
         ctx.save_for_backward(xb, gather, inv, h, w1b, w2b, offsets)
         ctx.meta = (G, R, float(grad_scale), xr.dtype)
         ctx.wdtype = w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32

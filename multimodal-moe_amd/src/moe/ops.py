@@ -36,6 +36,12 @@ import torch
 from . import _lib as L
 
 
+def _bias(b):
+    """A grouped-GEMM bias operand: bf16 parameters as they are (MOE_BIAS_BF16:
+    the kernel widens them), anything else as fp32."""
+    return b.contiguous() if b.dtype == torch.bfloat16 else b.float().contiguous()
+
+
 def _padded_offsets(E, pad, device):
     """Expert e's rows start at e * pad (the fixed-capacity layout of ep.py)."""
     return (torch.arange(E + 1, dtype=torch.int32, device=device) * int(pad)).contiguous()
@@ -201,8 +207,8 @@ class _ExpertFFNGather(torch.autograd.Function):
         w1b = w1.to(torch.bfloat16).contiguous()
         w2b = w2.to(torch.bfloat16).contiguous()
         h = L.grouped_gemm_gather(xb, tok, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU,
-                                  bias=b1.float().contiguous())
-        yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=b2.float().contiguous())
+                                  bias=_bias(b1))
+        yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=_bias(b2))
         ctx.save_for_backward(xb, tok, h, w1b, w2b, offsets)
         ctx.meta = (G, rows, float(grad_scale))
         ctx.wdtype = w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32
@@ -223,8 +229,8 @@ class _ExpertFFN(torch.autograd.Function):
         G, F, d = w1.shape
         w1b = w1.to(torch.bfloat16).contiguous()
         w2b = w2.to(torch.bfloat16).contiguous()
-        h = L.grouped_gemm(xp, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU, bias=b1.float().contiguous())
-        yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=b2.float().contiguous())
+        h = L.grouped_gemm(xp, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU, bias=_bias(b1))
+        yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=_bias(b2))
         ctx.save_for_backward(xp, h, w1b, w2b, offsets)
         ctx.meta = (G, F, d, rows, float(grad_scale))
         ctx.wdtype = w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32
@@ -383,8 +389,8 @@ class _MoELayer(torch.autograd.Function):
         w1b = w1.to(torch.bfloat16).contiguous()
         w2b = w2.to(torch.bfloat16).contiguous()
         h = L.grouped_gemm_gather(xb, tok, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU,
-                                  bias=b1.float().contiguous())
-        yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=b2.float().contiguous())
+                                  bias=_bias(b1))
+        yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=_bias(b2))
         y = L.combine_fwd(yp, pos, w, T, resid=xb if residual else None)
         ctx.residual = bool(residual)
         ctx.save_for_backward(xb, wg32, idx, w, probs, lse, pos, tok, gate, h, yp, w1b, w2b, offsets, wcoef,
@@ -393,6 +399,7 @@ class _MoELayer(torch.autograd.Function):
                     ctx_bias.shape[0] if ctx_bias is not None else 0, weighted)
         ctx.dtypes = (x.dtype, w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32)
         ctx.mark_non_differentiable(hist)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for raw / hist (backward takes None)
         if weighted:
             raw = out3[:2].clone()
             ctx.mark_non_differentiable(raw)

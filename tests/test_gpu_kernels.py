@@ -608,3 +608,27 @@ def test_router_wgrad_vs_fp64(hip_lib, B, tpi, E, C):
     assert ((dwg.double() - ref).norm() / ref.norm()).item() < 1e-5
     assert (dcb.double() - ref_cb).abs().max().item() <= 1e-4 * max(1.0, ref_cb.abs().max().item())
     assert torch.equal(dwg, dwg2) and torch.equal(dcb, dcb2) and torch.equal(dwg, dwg0) and dcb0 is None
+
+
+@pytest.mark.parametrize("gather", [False, True])
+def test_grouped_gemm_bf16_bias_matches_fp32_bias(hip_lib, gather):
+    """MOE_BIAS_BF16: a bf16 bias read by the kernel gives bitwise the result
+    of the fp32 copy of the same values (the per-call cast it replaces)."""
+    from src.moe import _lib as L
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    G, N, K, R = 4, 1024, 256, 700
+    offsets = torch.tensor([0, 100, 100, 450, R], dtype=torch.int32, device=DEV)
+    x = torch.randn((R, K), device=DEV, generator=g).to(torch.bfloat16)
+    tok = torch.randperm(R, device=DEV, generator=g).to(torch.int32)
+    w = (torch.randn((G, N, K), device=DEV, generator=g) / 16).to(torch.bfloat16)
+    b16 = torch.randn((G, N), device=DEV, generator=g).to(torch.bfloat16)
+    outs = []
+    for b in (b16, b16.float()):
+        for epi in (L.EPI_BIAS, L.EPI_BIAS_RELU):
+            if gather:
+                outs.append(L.grouped_gemm_gather(x, tok, w, offsets, G, R, N, K, 1, epi, bias=b))
+            else:
+                outs.append(L.grouped_gemm(x, w, offsets, G, R, N, K, 1, epi, bias=b))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
