@@ -400,11 +400,12 @@ class _MoELayer(torch.autograd.Function):
         ctx.dtypes = (x.dtype, w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32)
         ctx.mark_non_differentiable(hist)
         ctx.set_materialize_grads(False)  # no zero-filled gradients for raw / hist (backward takes None)
+        # out3's elements leave as views (no copy launches); nothing writes them in place
         if weighted:
-            raw = out3[:2].clone()
+            raw = out3[:2]
             ctx.mark_non_differentiable(raw)
-            return y.to(x.dtype), out3[2].clone(), raw, hist
-        return y.to(x.dtype), out3[0].clone(), out3[1].clone(), hist
+            return y.to(x.dtype), out3[2], raw, hist
+        return y.to(x.dtype), out3[0], out3[1], hist
 
     @staticmethod
     def backward(ctx, dy, g_a, g_b, _h):
