@@ -412,11 +412,21 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int g, int row0, i
 // lines; the register-direct path issues 8-B pieces, which the store path
 // handles at half the rate).  The relu-mask operand is read the same way.
 // Images: 16-B chunk c of row r at c ^ (r % chunks_per_row).
+// Relu-mask operand of the dgrad (EPI_RELU_MASK, bf16): the 16-B chunks this
+// thread's epilogue stores cover, loaded before the K loop (its latency -- an
+// HBM round trip: the forward wrote H long before -- hides behind the loop
+// instead of trailing it) when they fit in 4 registers of 16 B.
+template <int BM, int BN, int MODE, int EPI, int FL>
+struct MaskPre {
+  static constexpr bool ON = MODE == MODE_ROWS && EPI == MOE_EPI_RELU_MASK && !(FL & FL_AUX8) && BM * BN / 2048 <= 4;
+  static constexpr int N = ON ? BM * BN / 2048 : 1;
+};
+
 template <int BM, int BN, int MODE, int EPI, bool COLSUM, int FL>
 __device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row0, int a_row_lim, int m0, int n0,
                                              int nt, f32x4 (&acc)[BM / 32][BN / 32], float (&csum)[BM / 32],
                                              const float4 (&bpre)[BN / 32], char* smem, int tid, int lane, int wm,
-                                             int wn) {
+                                             int wn, const uint4 (&mpre)[MaskPre<BM, BN, MODE, EPI, FL>::N]) {
   constexpr int TM = BM / 32, TN = BN / 32;
   const int lm = lane & 15;
   const int ln = 4 * (lane >> 4);
@@ -473,7 +483,9 @@ __device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row
         }
         v = make_uint4(vw[0], vw[1], vw[2], vw[3]);
       } else if constexpr (EPI == MOE_EPI_RELU_MASK) {  // keep where the forward activation is > 0
-        const uint4 h = *reinterpret_cast<const uint4*>(p.aux + gofs);
+        uint4 h;
+        if constexpr (MaskPre<BM, BN, MODE, EPI, FL>::ON) h = mpre[r0 / RPP];
+        else h = *reinterpret_cast<const uint4*>(p.aux + gofs);
         uint32_t hw[4] = {h.x, h.y, h.z, h.w};
         uint32_t vw[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -1097,6 +1109,19 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p, int bid, char*
   if (!t.init(p, lane, bid)) return;
   float4 bpre[TN];
   prefetch_bias<BN, MODE, EPI>(p, t.g, t.n0, lane, wn, bpre);
+  using MP = MaskPre<BM, BN, MODE, EPI, FL>;
+  uint4 mpre[MP::N];
+  if constexpr (MP::ON) {  // the epilogue's relu-mask chunks (rows as in epilogue_lds' store loop)
+    constexpr int CPR = BN / 8, RPP = 256 / CPR;
+    const int c = tid % CPR;
+#pragma unroll
+    for (int k = 0; k < MP::N; ++k) {
+      const int r = k * RPP + tid / CPR;
+      mpre[k] = r < t.a_row_lim
+                    ? *reinterpret_cast<const uint4*>(p.aux + ((size_t)t.row0 + r) * p.ldc + t.n0 + c * 8)
+                    : make_uint4(0, 0, 0, 0);
+    }
+  }
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -1257,7 +1282,7 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p, int bid, char*
   (void)g_last;
   if (t.nsplit > 1 && !splitk_merge<TM, TN, COLSUM>(p, t.tile_id, t.split, acc, csum, tid)) return;
   epilogue_lds<BM, BN, MODE, EPI, COLSUM, FL>(p, t.g, t.row0, t.a_row_lim, t.m0, t.n0, t.nt, acc, csum, bpre, smem,
-                                              tid, lane, wm, wn);
+                                              tid, lane, wm, wn, mpre);
 }
 
 template <int BM, int BN, int S, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>
