@@ -241,6 +241,17 @@ int rtdetr_linear_wgrad(const void* gy, const void* x, void* dw, void* db, const
 int rtdetr_linear_wgrad_batch(int n, const void* const* gy, const void* const* x, void* const* dw,
                               void* const* db, const int* K, const int* M, const int* N, int out_bf16,
                               hipStream_t stream);
+/* Narrow dense linear gradients (out_features M <= 128, any M; the decoder's
+ * class heads M = 1, box-head last layers M = 4, attention weights M = 96):
+ * dw [M, N] = gy^T x and db [M] = colsum(gy) in out_bf16 ? bf16 : fp32, from
+ * bf16 gy [K, M] and x [K, N] (N even, x 4-byte aligned), deterministic
+ * (fixed-order sum of row-slice partials).  part: fp32 workspace of
+ * rtdetr_linear_wgrad_narrow_parts(K, M, N) floats, 8-byte aligned.  Replaces
+ * torch's gy.t().mm(x) + column sum (linear.py _TokenLinear.backward; the
+ * reference's nn.Linear heads, src/models/vision/rtdetr.py). */
+int rtdetr_linear_wgrad_narrow_parts(int K, int M, int N);
+int rtdetr_linear_wgrad_narrow(const void* gy, const void* x, void* dw, void* db, float* part, int K, int M, int N,
+                               int out_bf16, hipStream_t stream);
 /* a7: one backward step of an expert weight in ONE launch --
  *   dgrad: C[r, n] = epi( s_r sum_k A(r, k) B_g[k][n] )   (trans_b = 0; epilogue
  *          NONE / RELU_MASK / RELU_MASK_MX with aux); A(r, .) = a[a_gather[r]]

@@ -95,9 +95,137 @@ __global__ __launch_bounds__(256) void bias_grad_final_kernel(const float* __res
   }
 }
 
+// Narrow dense linear (out_features M not a multiple of 64: the decoder's
+// class heads M = 1, box-head last layers M = 4, attention weights M = 96):
+//   dW[m, n] = sum_k gy[k, m] x[k, n]     db[m] = sum_k gy[k, m]
+// hipBLASLt ran these few-tile, long-K products on 1-8 workgroups (25-34 us
+// each at K = 2,400 rows).  Here one wave owns 128 columns x 16 outputs x a
+// slice of rows (4 outputs when M <= 4; gy staged in LDS as fp32 and read as broadcasts, x streamed
+// as bf16 pairs, 8 rows in flight), writing fp32 partials [S][M*N + M (+1: even)]; the
+// final kernel sums the S slices in a fixed order (deterministic).
+constexpr int kNwCB = 128;  // columns (n) per wave
+constexpr int kNwU = 8;     // rows per load batch
+
+template <int kNwMT>  // outputs (m) per wave: 4 (M <= 4) or 16
+__global__ __launch_bounds__(64) void narrow_wgrad_part_kernel(const uint16_t* __restrict__ gy,
+                                                               const uint16_t* __restrict__ x, int K, int M, int N,
+                                                               int R, float* __restrict__ part) {
+  __shared__ float s_g[64][kNwMT];
+  const int lane = threadIdx.x;
+  const int n = blockIdx.x * kNwCB + 2 * lane;
+  const int m0 = blockIdx.y * kNwMT;
+  const int s = blockIdx.z;
+  const int k0 = s * R;
+  const int k1 = min(K, k0 + R);
+  const bool ncol = n < N;
+  const size_t Q = ((size_t)M * N + M + 1) & ~(size_t)1;  // slice stride (even: float2 stores)
+  float acc[kNwMT][2];
+#pragma unroll
+  for (int m = 0; m < kNwMT; ++m) acc[m][0] = acc[m][1] = 0.f;
+  float dbs = 0.f;
+  for (int kc = k0; kc < k1; kc += 64) {
+    const int rows = min(64, k1 - kc);
+    for (int i = lane; i < 64 * kNwMT; i += 64) {
+      const int r = i / kNwMT, m = i % kNwMT;
+      s_g[r][m] = (r < rows && m0 + m < M) ? bf2f(gy[(size_t)(kc + r) * M + m0 + m]) : 0.f;
+    }
+    __syncthreads();
+    if (lane < kNwMT)
+      for (int r = 0; r < rows; ++r) dbs += s_g[r][lane];
+    for (int r = 0; r < rows; r += kNwU) {
+      uint32_t xv[kNwU];
+#pragma unroll
+      for (int u = 0; u < kNwU; ++u)
+        xv[u] = (ncol && r + u < rows) ? *reinterpret_cast<const uint32_t*>(x + (size_t)(kc + r + u) * N + n) : 0u;
+#pragma unroll
+      for (int u = 0; u < kNwU; ++u) {
+        const float x0 = bf2f((uint16_t)(xv[u] & 0xffffu)), x1 = bf2f((uint16_t)(xv[u] >> 16));
+        const float4* g4 = reinterpret_cast<const float4*>(s_g[(r + u) & 63]);
+#pragma unroll
+        for (int q = 0; q < kNwMT / 4; ++q) {
+          const float4 g = g4[q];
+          acc[4 * q + 0][0] += g.x * x0; acc[4 * q + 0][1] += g.x * x1;
+          acc[4 * q + 1][0] += g.y * x0; acc[4 * q + 1][1] += g.y * x1;
+          acc[4 * q + 2][0] += g.z * x0; acc[4 * q + 2][1] += g.z * x1;
+          acc[4 * q + 3][0] += g.w * x0; acc[4 * q + 3][1] += g.w * x1;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* ps = part + (size_t)s * Q;
+  if (ncol) {
+#pragma unroll
+    for (int m = 0; m < kNwMT; ++m)
+      if (m0 + m < M) *reinterpret_cast<float2*>(ps + (size_t)(m0 + m) * N + n) = make_float2(acc[m][0], acc[m][1]);
+  }
+  if (blockIdx.x == 0 && lane < kNwMT && m0 + lane < M) ps[(size_t)M * N + m0 + lane] = dbs;
+}
+
+__global__ __launch_bounds__(256) void narrow_wgrad_final_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                                 void* __restrict__ dw, void* __restrict__ db,
+                                                                 int out_bf16) {
+  const size_t MN = (size_t)M * N;
+  const size_t Q = (MN + M + 1) & ~(size_t)1;
+  const size_t c = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= MN + M) return;
+  float t = 0.f;
+  constexpr int U = 16;
+  for (int p = 0; p < S; p += U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = p + u < S ? part[(size_t)(p + u) * Q + c] : 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) t += v[u];
+  }
+  void* out = c < MN ? dw : db;
+  const size_t i = c < MN ? c : c - MN;
+  if (out_bf16) static_cast<uint16_t*>(out)[i] = f2bf(t);
+  else static_cast<float*>(out)[i] = t;
+}
+
 }  // namespace moe
 
 using namespace moe;
+
+static int narrow_slices(int K) {
+  // rows per slice >= 16; at most 32 slices (the final kernel's serial sum)
+  int s = (K + 15) / 16;
+  return s < 1 ? 1 : (s > 32 ? 32 : s);
+}
+
+extern "C" int rtdetr_linear_wgrad_narrow_parts(int K, int M, int N) {
+  if (K <= 0 || M <= 0 || N <= 0) return 0;
+  return narrow_slices(K) * ((M * N + M + 1) & ~1);
+}
+
+extern "C" int rtdetr_linear_wgrad_narrow(const void* gy, const void* x, void* dw, void* db, float* part, int K, int M,
+                                          int N, int out_bf16, hipStream_t stream) {
+  if (gy == nullptr || x == nullptr || dw == nullptr || db == nullptr || part == nullptr)
+    return fail("rtdetr_linear_wgrad_narrow: null pointer");
+  if (K <= 0 || M <= 0 || N <= 0 || M > 128 || N % 2 != 0 || N > 4096)
+    return fail("rtdetr_linear_wgrad_narrow: needs K > 0, 0 < M <= 128, even N <= 4096");
+  if ((reinterpret_cast<uintptr_t>(x) & 3) != 0 || (reinterpret_cast<uintptr_t>(part) & 7) != 0)
+    return fail("rtdetr_linear_wgrad_narrow: x must be 4-byte and part 8-byte aligned");
+  const int S = narrow_slices(K);
+  const int R = (K + S - 1) / S;
+  const double Q = (double)M * N + M;
+  ProfScope prof(stream, PROF_LINEAR, 2.0 * K * (M + N) + 8.0 * S * Q + (out_bf16 ? 2.0 : 4.0) * Q, false, 0.0,
+                 2.0 * K * M * N);
+  const dim3 grid((N + kNwCB - 1) / kNwCB, M <= 4 ? 1 : (M + 15) / 16, S);
+  if (M <= 4)
+    MOE_LAUNCH(prof, narrow_wgrad_part_kernel<4>, grid, dim3(64), 0, stream, static_cast<const uint16_t*>(gy),
+               static_cast<const uint16_t*>(x), K, M, N, R, part);
+  else
+    MOE_LAUNCH(prof, narrow_wgrad_part_kernel<16>, grid, dim3(64), 0, stream, static_cast<const uint16_t*>(gy),
+               static_cast<const uint16_t*>(x), K, M, N, R, part);
+  int rc = check_launch("rtdetr_linear_wgrad_narrow(part)");
+  if (rc != 0) return rc;
+  const size_t Qi = (size_t)M * N + M;
+  hipLaunchKernelGGL(narrow_wgrad_final_kernel, dim3((unsigned)((Qi + 255) / 256)), dim3(256), 0, stream, part, S, M, N,
+                     dw, db, out_bf16);
+  return check_launch("rtdetr_linear_wgrad_narrow(final)");
+}
 
 extern "C" int rtdetr_bias_grad_parts(long long M, int N) {
   if (M <= 0 || N <= 0) return 1;

@@ -41,6 +41,8 @@ SIGNATURES = {
     "moe_grouped_gemm_wgrad_rows": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "rtdetr_linear_wgrad": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "rtdetr_linear_wgrad_batch": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "rtdetr_linear_wgrad_narrow_parts": (_I, [_I, _I, _I]),
+    "rtdetr_linear_wgrad_narrow": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "moe_route_index": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "moe_route_dispatch": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P]),
     "moe_grouped_gemm_gather": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
@@ -627,6 +629,27 @@ def linear_wgrad(gy, x, out_dtype):
     rc = lib().rtdetr_linear_wgrad(_ptr(gy), _ptr(x), _ptr(dw), _ptr(db), _ptr(off), K, M, N,
                                    int(out_dtype == torch.bfloat16), _stream())
     _check(rc, "rtdetr_linear_wgrad")
+    return dw, db
+
+
+def linear_wgrad_narrow(gy, x, out_dtype):
+    """Weight and bias gradients of a narrow dense linear (out_features M <=
+    128, any M: class heads, box-head last layers, attention weights):
+    dW = gy^T x [M, N], db = colsum(gy) [M] in out_dtype, deterministic.  gy
+    bf16 [K, M], x bf16 [K, N] with N even, both contiguous."""
+    _need(gy, torch.bfloat16, "gy")
+    _need(x, torch.bfloat16, "x")
+    if out_dtype not in (torch.float32, torch.bfloat16):
+        raise MoEKernelError("linear_wgrad_narrow: out_dtype must be float32 or bfloat16")
+    K, M, N = int(gy.shape[0]), int(gy.shape[1]), int(x.shape[1])
+    if x.shape[0] != K:
+        raise MoEKernelError("linear_wgrad_narrow: gy and x row counts differ")
+    part = torch.empty((int(lib().rtdetr_linear_wgrad_narrow_parts(K, M, N)),), dtype=torch.float32, device=gy.device)
+    dw = torch.empty((M, N), dtype=out_dtype, device=gy.device)
+    db = torch.empty((M,), dtype=out_dtype, device=gy.device)
+    _check(lib().rtdetr_linear_wgrad_narrow(_ptr(gy), _ptr(x), _ptr(dw), _ptr(db), _ptr(part), K, M, N,
+                                            int(out_dtype == torch.bfloat16), _stream()),
+           "rtdetr_linear_wgrad_narrow")
     return dw, db
 
 

@@ -234,6 +234,17 @@ class _TokenLinear(torch.autograd.Function):
                 return gx, None, None, None
             gw, gb = L.linear_wgrad(g2, x2, odt)
             return gx, gw, gb.to(ctx.bias_dtype), None
+        if (ctx.needs_input_grad[1] and ctx.has_bias and ctx.needs_input_grad[2] and g2.is_cuda
+                and g2.dtype == x2.dtype == torch.bfloat16 and M <= 128 and N % 2 == 0 and 0 < K < BIG_ROWS
+                and x2.is_contiguous()):
+            # narrow heads (M = 1 / 4 / 96): hipBLASLt ran dY^T X on 1-8
+            # workgroups, 25-34 us each; rtdetr_linear_wgrad_narrow splits
+            # the rows over the whole chip and adds the bias column sum
+            from ..moe import _lib as L
+
+            odt = torch.bfloat16 if ctx.weight_dtype == torch.bfloat16 else torch.float32
+            gw, gb = L.linear_wgrad_narrow(g2, x2, odt)
+            return gx, gw, gb.to(ctx.bias_dtype), None
         if ctx.needs_input_grad[1]:
             gw = chunked_wgrad(g2, x2) if x2.shape[0] >= BIG_ROWS else g2.t().mm(x2)
         gb = bias_grad(g2, ctx.bias_dtype) if ctx.has_bias and ctx.needs_input_grad[2] else None

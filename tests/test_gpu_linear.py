@@ -125,6 +125,34 @@ def test_linear_wgrad_dense(hip_lib, K, M, N, out_dtype):
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
 
 
+@pytest.mark.parametrize("K,M,N", [(2400, 1, 256), (2400, 4, 256), (2400, 96, 256), (1, 1, 2), (17, 3, 130),
+                                   (300, 128, 256), (4000, 5, 1024), (2400, 80, 384)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_linear_wgrad_narrow(hip_lib, K, M, N, out_dtype):
+    """rtdetr_linear_wgrad_narrow (class / box / attention-weight heads: M <=
+    128 outputs, any M) vs torch fp64 of the same bf16 operands, same
+    tolerances as the dense kernel; ragged M, N not a multiple of the 128-column
+    wave tile, a single row; deterministic."""
+    from src.moe import _lib as L
+
+    g = torch.Generator().manual_seed(K + 7 * M + N)
+    gy = torch.randn(K, M, generator=g).to(torch.bfloat16).cuda()
+    x = torch.randn(K, N, generator=g).to(torch.bfloat16).cuda()
+    dw, db = L.linear_wgrad_narrow(gy, x, out_dtype)
+    assert dw.shape == (M, N) and db.shape == (M,) and dw.dtype == db.dtype == out_dtype
+    ref_w = gy.double().t().mm(x.double())
+    tol_w = 1e-5 * gy.double().abs().t().mm(x.double().abs()) + 1e-30
+    ref_b = gy.double().sum(0)
+    tol_b = 1e-5 * gy.double().abs().sum(0) + 1e-30
+    if out_dtype == torch.bfloat16:
+        tol_w = tol_w + ref_w.abs() * 2.0 ** -8
+        tol_b = tol_b + ref_b.abs() * 2.0 ** -8
+    assert bool(((dw.double() - ref_w).abs() <= tol_w).all()), float(((dw.double() - ref_w).abs() - tol_w).max())
+    assert bool(((db.double() - ref_b).abs() <= tol_b).all()), float(((db.double() - ref_b).abs() - tol_b).max())
+    dw2, db2 = L.linear_wgrad_narrow(gy, x, out_dtype)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
 def test_linear_wgrad_batch_mixed_shapes(hip_lib, out_dtype):
     """rtdetr_linear_wgrad_batch: 30 problems of mixed shapes (two launches of
