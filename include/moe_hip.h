@@ -241,10 +241,12 @@ int rtdetr_linear_wgrad(const void* gy, const void* x, void* dw, void* db, const
 int rtdetr_linear_wgrad_batch(int n, const void* const* gy, const void* const* x, void* const* dw,
                               void* const* db, const int* K, const int* M, const int* N, int out_bf16,
                               hipStream_t stream);
-/* Narrow dense linear gradients (out_features M <= 128, any M; the decoder's
- * class heads M = 1, box-head last layers M = 4, attention weights M = 96):
- * dw [M, N] = gy^T x and db [M] = colsum(gy) in out_bf16 ? bf16 : fp32, from
- * bf16 gy [K, M] and x [K, N] (N even, x 4-byte aligned), deterministic
+/* Narrow dense linear gradients (out_features M <= 128 with N even: the
+ * decoder's class heads M = 1, box-head last layers M = 4, attention weights
+ * M = 96; or in_features N <= 128 with M even: the query position head's
+ * 4 -> 512 layer): dw [M, N] = gy^T x and db [M] = colsum(gy) in out_bf16 ?
+ * bf16 : fp32, from bf16 gy [K, M] and x [K, N] (the wide one 4-byte
+ * aligned; the other side <= 4096), deterministic
  * (fixed-order sum of row-slice partials).  part: fp32 workspace of
  * rtdetr_linear_wgrad_narrow_parts(K, M, N) floats, 8-byte aligned.  Replaces
  * torch's gy.t().mm(x) + column sum (linear.py _TokenLinear.backward; the

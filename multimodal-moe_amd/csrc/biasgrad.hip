@@ -101,16 +101,21 @@ __global__ __launch_bounds__(256) void bias_grad_final_kernel(const float* __res
 // hipBLASLt ran these few-tile, long-K products on 1-8 workgroups (25-34 us
 // each at K = 2,400 rows).  Here one wave owns 128 columns x 16 outputs x a
 // slice of rows (4 outputs when M <= 4; gy staged in LDS as fp32 and read as broadcasts, x streamed
-// as bf16 pairs, 8 rows in flight), writing fp32 partials [S][M*N + M (+1: even)]; the
+// as bf16 pairs, 16 rows in flight; ~1,024 waves), writing fp32 partials [S][M*N + M (+1: even)]; the
 // final kernel sums the S slices in a fixed order (deterministic).
 constexpr int kNwCB = 128;  // columns (n) per wave
-constexpr int kNwU = 8;     // rows per load batch
+constexpr int kNwU = 16;    // x rows in flight
 
-template <int kNwMT>  // outputs (m) per wave: 4 (M <= 4) or 16
+// TR: the narrow side is the layer's input (N_in <= 128, e.g. the query
+// position head's 4 -> 512 layer): the kernel runs on (gy, x) = (x, dY),
+// stores its [m, n] sums transposed and takes the bias partial from the
+// streamed operand's column sums.
+template <int kNwMT, bool TR>  // outputs (m) per wave: 4 (M <= 4) or 16
 __global__ __launch_bounds__(64) void narrow_wgrad_part_kernel(const uint16_t* __restrict__ gy,
                                                                const uint16_t* __restrict__ x, int K, int M, int N,
                                                                int R, float* __restrict__ part) {
   __shared__ float s_g[64][kNwMT];
+  __shared__ float s_db[64];
   const int lane = threadIdx.x;
   const int n = blockIdx.x * kNwCB + 2 * lane;
   const int m0 = blockIdx.y * kNwMT;
@@ -118,20 +123,23 @@ __global__ __launch_bounds__(64) void narrow_wgrad_part_kernel(const uint16_t* _
   const int k0 = s * R;
   const int k1 = min(K, k0 + R);
   const bool ncol = n < N;
-  const size_t Q = ((size_t)M * N + M + 1) & ~(size_t)1;  // slice stride (even: float2 stores)
+  const size_t Q = ((size_t)M * N + (TR ? N : M) + 1) & ~(size_t)1;  // slice stride (even)
   float acc[kNwMT][2];
+  float xs0 = 0.f, xs1 = 0.f;  // TR: column sums of the streamed operand
 #pragma unroll
   for (int m = 0; m < kNwMT; ++m) acc[m][0] = acc[m][1] = 0.f;
-  float dbs = 0.f;
+  float dbs = 0.f;  // this lane's column of gy is m0 + lane % kNwMT (kNwMT divides 64)
   for (int kc = k0; kc < k1; kc += 64) {
     const int rows = min(64, k1 - kc);
-    for (int i = lane; i < 64 * kNwMT; i += 64) {
+#pragma unroll
+    for (int j = 0; j < kNwMT; ++j) {
+      const int i = lane + 64 * j;
       const int r = i / kNwMT, m = i % kNwMT;
-      s_g[r][m] = (r < rows && m0 + m < M) ? bf2f(gy[(size_t)(kc + r) * M + m0 + m]) : 0.f;
+      const float v = (r < rows && m0 + m < M) ? bf2f(gy[(size_t)(kc + r) * M + m0 + m]) : 0.f;
+      s_g[r][m] = v;
+      dbs += v;
     }
     __syncthreads();
-    if (lane < kNwMT)
-      for (int r = 0; r < rows; ++r) dbs += s_g[r][lane];
     for (int r = 0; r < rows; r += kNwU) {
       uint32_t xv[kNwU];
 #pragma unroll
@@ -140,6 +148,7 @@ __global__ __launch_bounds__(64) void narrow_wgrad_part_kernel(const uint16_t* _
 #pragma unroll
       for (int u = 0; u < kNwU; ++u) {
         const float x0 = bf2f((uint16_t)(xv[u] & 0xffffu)), x1 = bf2f((uint16_t)(xv[u] >> 16));
+        if constexpr (TR) { xs0 += x0; xs1 += x1; }
         const float4* g4 = reinterpret_cast<const float4*>(s_g[(r + u) & 63]);
 #pragma unroll
         for (int q = 0; q < kNwMT / 4; ++q) {
@@ -157,73 +166,124 @@ __global__ __launch_bounds__(64) void narrow_wgrad_part_kernel(const uint16_t* _
   if (ncol) {
 #pragma unroll
     for (int m = 0; m < kNwMT; ++m)
-      if (m0 + m < M) *reinterpret_cast<float2*>(ps + (size_t)(m0 + m) * N + n) = make_float2(acc[m][0], acc[m][1]);
+      if (m0 + m < M) {
+        if constexpr (TR) {
+          ps[(size_t)n * M + m0 + m] = acc[m][0];
+          ps[(size_t)(n + 1) * M + m0 + m] = acc[m][1];
+        } else {
+          *reinterpret_cast<float2*>(ps + (size_t)(m0 + m) * N + n) = make_float2(acc[m][0], acc[m][1]);
+        }
+      }
+    if (TR && blockIdx.y == 0) *reinterpret_cast<float2*>(ps + (size_t)M * N + n) = make_float2(xs0, xs1);
   }
-  if (blockIdx.x == 0 && lane < kNwMT && m0 + lane < M) ps[(size_t)M * N + m0 + lane] = dbs;
+  if (!TR && blockIdx.x == 0) {  // bias partial: the 64 / kNwMT lanes of each column, fixed order
+    s_db[lane] = dbs;
+    __syncthreads();
+    if (lane < kNwMT && m0 + lane < M) {
+      float t = 0.f;
+      for (int j = lane; j < 64; j += kNwMT) t += s_db[j];
+      ps[(size_t)M * N + m0 + lane] = t;
+    }
+  }
 }
 
-__global__ __launch_bounds__(256) void narrow_wgrad_final_kernel(const float* __restrict__ part, int S, int M, int N,
-                                                                 void* __restrict__ dw, void* __restrict__ db,
+// 8 slice lanes x 32 outputs per block (fixed-order sums, as bias_grad_final)
+// (MN dW sums followed by NB bias sums per slice)
+__global__ __launch_bounds__(256) void narrow_wgrad_final_kernel(const float* __restrict__ part, int S, size_t MN,
+                                                                 int NB, void* __restrict__ dw, void* __restrict__ db,
                                                                  int out_bf16) {
-  const size_t MN = (size_t)M * N;
-  const size_t Q = (MN + M + 1) & ~(size_t)1;
-  const size_t c = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (c >= MN + M) return;
+  __shared__ float s_acc[8][32];
+  const size_t M = NB;  // bias entries
+  const size_t Q = (MN + NB + 1) & ~(size_t)1;
+  const int cl = threadIdx.x & 31;
+  const int pl = threadIdx.x >> 5;
+  const size_t c = (size_t)blockIdx.x * 32 + cl;
   float t = 0.f;
-  constexpr int U = 16;
-  for (int p = 0; p < S; p += U) {
-    float v[U];
+  if (c < MN + M) {
+    constexpr int U = 8;
+    for (int p = pl; p < S; p += 8 * U) {
+      float v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = p + u < S ? part[(size_t)(p + u) * Q + c] : 0.f;
+      for (int u = 0; u < U; ++u) v[u] = p + 8 * u < S ? part[(size_t)(p + 8 * u) * Q + c] : 0.f;
 #pragma unroll
-    for (int u = 0; u < U; ++u) t += v[u];
+      for (int u = 0; u < U; ++u) t += v[u];
+    }
   }
-  void* out = c < MN ? dw : db;
-  const size_t i = c < MN ? c : c - MN;
-  if (out_bf16) static_cast<uint16_t*>(out)[i] = f2bf(t);
-  else static_cast<float*>(out)[i] = t;
+  s_acc[pl][cl] = t;
+  __syncthreads();
+  if (pl == 0 && c < MN + M) {
+    float r = 0.f;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) r += s_acc[l][cl];
+    void* out = c < MN ? dw : db;
+    const size_t i = c < MN ? c : c - MN;
+    if (out_bf16) static_cast<uint16_t*>(out)[i] = f2bf(r);
+    else static_cast<float*>(out)[i] = r;
+  }
 }
 
 }  // namespace moe
 
 using namespace moe;
 
-static int narrow_slices(int K) {
-  // rows per slice >= 16; at most 32 slices (the final kernel's serial sum)
-  int s = (K + 15) / 16;
-  return s < 1 ? 1 : (s > 32 ? 32 : s);
+// Row slices: about 1,024 waves over the grid, at most 256 slices, >= 8 rows each.
+static int narrow_rows(int K, int M, int N) {
+  const int wps = ((N + kNwCB - 1) / kNwCB) * (M <= 4 ? 1 : (M + 15) / 16);
+  int s = 1024 / wps;
+  s = s < 1 ? 1 : (s > 256 ? 256 : s);
+  int r = (K + s - 1) / s;
+  return r < 8 ? 8 : r;
 }
+
+static int narrow_slices(int K, int M, int N) {
+  const int r = narrow_rows(K, M, N);
+  return (K + r - 1) / r;
+}
+
+// Kernel orientation of a layer with M outputs and N inputs: direct when M <=
+// 128 and N is even (the kernel's narrow side is M), otherwise transposed (TR).
+static bool narrow_tr(int M, int N) { return !(M <= 128 && N % 2 == 0); }
 
 extern "C" int rtdetr_linear_wgrad_narrow_parts(int K, int M, int N) {
   if (K <= 0 || M <= 0 || N <= 0) return 0;
-  return narrow_slices(K) * ((M * N + M + 1) & ~1);
+  const bool tr = narrow_tr(M, N);
+  return narrow_slices(K, tr ? N : M, tr ? M : N) * ((M * N + M + 1) & ~1);
 }
 
 extern "C" int rtdetr_linear_wgrad_narrow(const void* gy, const void* x, void* dw, void* db, float* part, int K, int M,
                                           int N, int out_bf16, hipStream_t stream) {
   if (gy == nullptr || x == nullptr || dw == nullptr || db == nullptr || part == nullptr)
     return fail("rtdetr_linear_wgrad_narrow: null pointer");
-  if (K <= 0 || M <= 0 || N <= 0 || M > 128 || N % 2 != 0 || N > 4096)
-    return fail("rtdetr_linear_wgrad_narrow: needs K > 0, 0 < M <= 128, even N <= 4096");
-  if ((reinterpret_cast<uintptr_t>(x) & 3) != 0 || (reinterpret_cast<uintptr_t>(part) & 7) != 0)
-    return fail("rtdetr_linear_wgrad_narrow: x must be 4-byte and part 8-byte aligned");
-  const int S = narrow_slices(K);
-  const int R = (K + S - 1) / S;
+  const bool tr = narrow_tr(M, N);
+  const int Mk = tr ? N : M, Nk = tr ? M : N;  // the kernel's narrow and streamed sides
+  const void* gk = tr ? x : gy;
+  const void* xk = tr ? gy : x;
+  if (K <= 0 || Mk <= 0 || Nk <= 0 || Mk > 128 || Nk % 2 != 0 || Nk > 4096)
+    return fail("rtdetr_linear_wgrad_narrow: needs K > 0 and M <= 128 with N even (or N <= 128 with M even), "
+                "the other side <= 4096");
+  if ((reinterpret_cast<uintptr_t>(xk) & 3) != 0 || (reinterpret_cast<uintptr_t>(part) & 7) != 0)
+    return fail("rtdetr_linear_wgrad_narrow: the wide operand must be 4-byte and part 8-byte aligned");
+  const int R = narrow_rows(K, Mk, Nk);
+  const int S = (K + R - 1) / R;
   const double Q = (double)M * N + M;
   ProfScope prof(stream, PROF_LINEAR, 2.0 * K * (M + N) + 8.0 * S * Q + (out_bf16 ? 2.0 : 4.0) * Q, false, 0.0,
                  2.0 * K * M * N);
-  const dim3 grid((N + kNwCB - 1) / kNwCB, M <= 4 ? 1 : (M + 15) / 16, S);
-  if (M <= 4)
-    MOE_LAUNCH(prof, narrow_wgrad_part_kernel<4>, grid, dim3(64), 0, stream, static_cast<const uint16_t*>(gy),
-               static_cast<const uint16_t*>(x), K, M, N, R, part);
+  const dim3 grid((Nk + kNwCB - 1) / kNwCB, Mk <= 4 ? 1 : (Mk + 15) / 16, S);
+  const uint16_t* g16 = static_cast<const uint16_t*>(gk);
+  const uint16_t* x16 = static_cast<const uint16_t*>(xk);
+  if (Mk <= 4 && tr)
+    MOE_LAUNCH(prof, (narrow_wgrad_part_kernel<4, true>), grid, dim3(64), 0, stream, g16, x16, K, Mk, Nk, R, part);
+  else if (Mk <= 4)
+    MOE_LAUNCH(prof, (narrow_wgrad_part_kernel<4, false>), grid, dim3(64), 0, stream, g16, x16, K, Mk, Nk, R, part);
+  else if (tr)
+    MOE_LAUNCH(prof, (narrow_wgrad_part_kernel<16, true>), grid, dim3(64), 0, stream, g16, x16, K, Mk, Nk, R, part);
   else
-    MOE_LAUNCH(prof, narrow_wgrad_part_kernel<16>, grid, dim3(64), 0, stream, static_cast<const uint16_t*>(gy),
-               static_cast<const uint16_t*>(x), K, M, N, R, part);
+    MOE_LAUNCH(prof, (narrow_wgrad_part_kernel<16, false>), grid, dim3(64), 0, stream, g16, x16, K, Mk, Nk, R, part);
   int rc = check_launch("rtdetr_linear_wgrad_narrow(part)");
   if (rc != 0) return rc;
-  const size_t Qi = (size_t)M * N + M;
-  hipLaunchKernelGGL(narrow_wgrad_final_kernel, dim3((unsigned)((Qi + 255) / 256)), dim3(256), 0, stream, part, S, M, N,
-                     dw, db, out_bf16);
+  const size_t MN = (size_t)M * N;
+  hipLaunchKernelGGL(narrow_wgrad_final_kernel, dim3((unsigned)((MN + M + 31) / 32)), dim3(256), 0, stream, part, S,
+                     MN, M, dw, db, out_bf16);
   return check_launch("rtdetr_linear_wgrad_narrow(final)");
 }
 

@@ -634,9 +634,10 @@ def linear_wgrad(gy, x, out_dtype):
 
 def linear_wgrad_narrow(gy, x, out_dtype):
     """Weight and bias gradients of a narrow dense linear (out_features M <=
-    128, any M: class heads, box-head last layers, attention weights):
+    128 with N even: class heads, box-head last layers, attention weights; or
+    in_features N <= 128 with M even: the query position head's first layer):
     dW = gy^T x [M, N], db = colsum(gy) [M] in out_dtype, deterministic.  gy
-    bf16 [K, M], x bf16 [K, N] with N even, both contiguous."""
+    bf16 [K, M], x bf16 [K, N], both contiguous."""
     _need(gy, torch.bfloat16, "gy")
     _need(x, torch.bfloat16, "x")
     if out_dtype not in (torch.float32, torch.bfloat16):

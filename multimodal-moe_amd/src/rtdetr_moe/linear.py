@@ -192,6 +192,11 @@ def bias_grad(g2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     return out
 
 
+def L_narrow_ok(M: int, N: int) -> bool:
+    """Shapes rtdetr_linear_wgrad_narrow takes (M outputs, N inputs)."""
+    return (M <= 128 and N % 2 == 0 and N <= 4096) or (N <= 128 and M % 2 == 0 and M <= 4096)
+
+
 class _TokenLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, dtype):
@@ -235,11 +240,12 @@ class _TokenLinear(torch.autograd.Function):
             gw, gb = L.linear_wgrad(g2, x2, odt)
             return gx, gw, gb.to(ctx.bias_dtype), None
         if (ctx.needs_input_grad[1] and ctx.has_bias and ctx.needs_input_grad[2] and g2.is_cuda
-                and g2.dtype == x2.dtype == torch.bfloat16 and M <= 128 and N % 2 == 0 and 0 < K < BIG_ROWS
+                and g2.dtype == x2.dtype == torch.bfloat16 and L_narrow_ok(M, N) and 0 < K < BIG_ROWS
                 and x2.is_contiguous()):
-            # narrow heads (M = 1 / 4 / 96): hipBLASLt ran dY^T X on 1-8
-            # workgroups, 25-34 us each; rtdetr_linear_wgrad_narrow splits
-            # the rows over the whole chip and adds the bias column sum
+            # narrow heads (M = 1 / 4 / 96 outputs, or the query position
+            # head's 4 inputs): hipBLASLt ran dY^T X on 1-8 workgroups, 25-34
+            # us each; rtdetr_linear_wgrad_narrow splits the rows over the
+            # whole chip and adds the bias column sum
             from ..moe import _lib as L
 
             odt = torch.bfloat16 if ctx.weight_dtype == torch.bfloat16 else torch.float32

@@ -126,11 +126,12 @@ def test_linear_wgrad_dense(hip_lib, K, M, N, out_dtype):
 
 
 @pytest.mark.parametrize("K,M,N", [(2400, 1, 256), (2400, 4, 256), (2400, 96, 256), (1, 1, 2), (17, 3, 130),
-                                   (300, 128, 256), (4000, 5, 1024), (2400, 80, 384)])
+                                   (300, 128, 256), (4000, 5, 1024), (2400, 80, 384),
+                                   (2400, 512, 4), (300, 256, 3), (1000, 130, 20), (64, 4, 3)])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
 def test_linear_wgrad_narrow(hip_lib, K, M, N, out_dtype):
     """rtdetr_linear_wgrad_narrow (class / box / attention-weight heads: M <=
-    128 outputs, any M) vs torch fp64 of the same bf16 operands, same
+    128 outputs, any M; transposed orientation for N <= 128 inputs) vs torch fp64 of the same bf16 operands, same
     tolerances as the dense kernel; ragged M, N not a multiple of the 128-column
     wave tile, a single row; deterministic."""
     from src.moe import _lib as L
