@@ -70,6 +70,7 @@ class _RouteDispatch(torch.autograd.Function):
         ctx.meta = (T, d, E, int(normalize), tokens_per_image, cb is not None, x.dtype,
                     ctx_bias.shape[0] if ctx_bias is not None else 0)
         ctx.mark_non_differentiable(pos, hist, offsets)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the index outputs
         return xp, w, auxp, pos, hist, offsets
 
     @staticmethod
@@ -120,6 +121,7 @@ class _RouteDispatchMX(torch.autograd.Function):
         ctx.meta = (T, d, E, int(normalize), tokens_per_image, cb is not None, x.dtype,
                     ctx_bias.shape[0] if ctx_bias is not None else 0)
         ctx.mark_non_differentiable(pos, hist, offsets, xq, xs)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the index outputs
         return carrier, w, auxp, pos, hist, offsets, xq, xs
 
     @staticmethod
@@ -154,6 +156,7 @@ class _RouteIndex(torch.autograd.Function):
         ctx.meta = (T, d, E, int(normalize), tokens_per_image, cb is not None, x.dtype,
                     ctx_bias.shape[0] if ctx_bias is not None else 0)
         ctx.mark_non_differentiable(pos, hist, offsets, tok, out3, wcoef)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the index outputs
         return carrier, w, auxp, pos, hist, offsets, tok, out3, wcoef
 
     @staticmethod
@@ -172,10 +175,13 @@ class _AuxFused(torch.autograd.Function):
         ctx.nblk = auxp.shape[0]
         raw = out3[:2].clone()
         ctx.mark_non_differentiable(raw)
+        ctx.set_materialize_grads(False)
         return out3[2].clone(), raw
 
     @staticmethod
     def backward(ctx, g, _raw):
+        if g is None:
+            return None, None, None
         (wcoef,) = ctx.saved_tensors
         return (g * wcoef).view(1, -1).expand(ctx.nblk, -1), None, None
 
@@ -308,10 +314,13 @@ class _AuxLoss(torch.autograd.Function):
         ctx.save_for_backward(wcoef)
         ctx.nblk = auxp.shape[0]
         ctx.mark_non_differentiable(out)
+        ctx.set_materialize_grads(False)
         return out[2].clone(), out[:2]
 
     @staticmethod
     def backward(ctx, g, _raw):
+        if g is None:
+            return None, None, None, None, None, None
         (wcoef,) = ctx.saved_tensors
         return (g * wcoef).view(1, -1).expand(ctx.nblk, -1), None, None, None, None, None
 

@@ -106,6 +106,7 @@ class _FoldAll(torch.autograd.Function):
         frozen = [o for o, w in zip(outs, weights) if not w.requires_grad]
         if frozen:  # e.g. the frozen stem: no weight gradient is computed for it
             ctx.mark_non_differentiable(*frozen)
+        ctx.set_materialize_grads(False)  # frozen folds: no zero-filled gradients
         return outs
 
     @staticmethod

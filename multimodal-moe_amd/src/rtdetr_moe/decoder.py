@@ -188,6 +188,7 @@ class _ValueProjAll(torch.autograd.Function):
         ctx.grad_all = grad_all
         ctx.meta = (B, S, d, n, memory.dtype, [w.dtype for w in ws], [b.dtype for b in bs])
         ctx.mark_non_differentiable(v_all, grad_all)
+        ctx.set_materialize_grads(False)  # no zero-filled [B, S, n d] gradients for v_all / grad_all
         return v_all, grad_all, token
 
     @staticmethod
