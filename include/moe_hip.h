@@ -390,6 +390,11 @@ int rtdetr_fold_scale_multi(const void* records, const int32_t* chunks, int n_ch
  * (rtdetr.py:82-94, upstream resnet-d variant). */
 int rtdetr_avgpool2x2_nhwc_fwd(const void* x, int B, int H, int W, int C, void* y, hipStream_t stream);
 int rtdetr_avgpool2x2_nhwc_bwd(const void* gy, int B, int H, int W, int C, void* gx, hipStream_t stream);
+/* The stem's MaxPool2d(3, 2, 1) forward over channels_last bf16 (the stem is
+ * frozen: no backward): y [B, (H-1)/2+1, (W-1)/2+1, C], C % 8 == 0, x and y
+ * 16-B aligned; padding never wins, NaN propagates.  Replaces nn.MaxPool2d in
+ * the reference's ResNet stem (Ultralytics RT-DETR backbone). */
+int rtdetr_maxpool3x3s2_nhwc_fwd(const void* x, int B, int H, int W, int C, void* y, hipStream_t stream);
 
 /* Bias gradient of a linear layer: out[n] = sum_m dy[m, n] over bf16 dy [M, N]
  * (row-major), fp32 accumulation in a fixed order (deterministic, no atomics),

@@ -255,6 +255,25 @@ class _AvgPool2x2(torch.autograd.Function):
         return gx
 
 
+def stem_max_pool(x, pool: nn.MaxPool2d):
+    """The stem's MaxPool2d(3, 2, 1): channels_last bf16 GPU activations that
+    take no gradient (the frozen stem) go through rtdetr_maxpool3x3s2_nhwc_fwd
+    (one 16-B-vector launch; torch's NHWC kernel took 157 us at C2)."""
+    if (x.is_cuda and x.dtype == torch.bfloat16 and not (torch.is_grad_enabled() and x.requires_grad)
+            and pool.kernel_size in (3, (3, 3)) and pool.stride in (2, (2, 2)) and pool.padding in (1, (1, 1))
+            and pool.dilation in (1, (1, 1)) and not pool.ceil_mode and x.shape[1] % 8 == 0
+            and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0):
+        from ..moe import _lib as L
+
+        B, C, H, W = x.shape
+        y = torch.empty((B, C, (H - 1) // 2 + 1, (W - 1) // 2 + 1), dtype=x.dtype, device=x.device,
+                        memory_format=torch.channels_last)
+        L._check(L.lib().rtdetr_maxpool3x3s2_nhwc_fwd(x.data_ptr(), B, H, W, C, y.data_ptr(), L._stream()),
+                 "rtdetr_maxpool3x3s2_nhwc_fwd")
+        return y
+    return pool(x)
+
+
 def avg_pool_2x2(x):
     """AvgPool2d(2, 2, ceil_mode=True).  Even H and W (every RT-DETR input padded
     to a multiple of 32) take a reshape-mean over the channels_last layout, whose
@@ -441,7 +460,7 @@ class PResNet(nn.Module):
 
     def forward(self, x):
         self._fold_all()
-        x = self.pool(self.stem(x))
+        x = stem_max_pool(self.stem(x), self.pool)
         xs = None
         outs = []
         for i, stage in enumerate(self.stages):

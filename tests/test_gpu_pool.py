@@ -33,3 +33,23 @@ def test_avgpool2x2_matches_torch(hip_lib, B, C, H, W):
     assert torch.equal(x2.grad, gref)
     assert x2.grad.is_contiguous(memory_format=torch.channels_last)
     _ = _AvgPool2x2  # the HIP path, not the reshape-mean fallback
+
+
+@pytest.mark.parametrize("B,C,H,W", [(1, 8, 1, 1), (2, 64, 7, 10), (8, 64, 368, 640), (1, 16, 5, 3), (3, 32, 2, 2)])
+def test_stem_maxpool_matches_torch(hip_lib, B, C, H, W):
+    """rtdetr_maxpool3x3s2_nhwc_fwd vs nn.MaxPool2d(3, 2, 1): bit-exact (a max
+    of bf16 values), odd and even sizes, 1x1 input, NaN propagation."""
+    from torch import nn
+
+    from src.rtdetr_moe.backbone import stem_max_pool
+
+    g = torch.Generator().manual_seed(B * C + H * W)
+    x = torch.randn(B, C, H, W, generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=torch.channels_last)
+    if H * W > 4:
+        x[0, 3, H // 2, W // 2] = float("nan")
+    pool = nn.MaxPool2d(3, 2, 1)
+    ref = pool(x)
+    got = stem_max_pool(x, pool)
+    assert got.grad_fn is None and got.is_contiguous(memory_format=torch.channels_last) and got.shape == ref.shape
+    assert torch.equal(torch.isnan(got), torch.isnan(ref))
+    assert torch.equal(got.nan_to_num(0.0), ref.nan_to_num(0.0))
