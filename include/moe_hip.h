@@ -395,6 +395,17 @@ int rtdetr_avgpool2x2_nhwc_bwd(const void* gy, int B, int H, int W, int C, void*
  * 16-B aligned; padding never wins, NaN propagates.  Replaces nn.MaxPool2d in
  * the reference's ResNet stem (Ultralytics RT-DETR backbone). */
 int rtdetr_maxpool3x3s2_nhwc_fwd(const void* x, int B, int H, int W, int C, void* y, hipStream_t stream);
+/* The encoder's FPN top-down concat (HybridEncoder CCFM): out [B, H, W, Ch +
+ * Cl] = cat([nearest x2 upsample of high [B, Hh, Wh, Ch] cropped to H x W,
+ * low [B, H, W, Cl]], channels), channels_last bf16; Ch, Cl % 8 == 0, H/2 <=
+ * Hh <= H and W/2 <= Wh <= W, 16-B aligned.  Backward: dhigh = the 2x2 block
+ * sums of g[.., :Ch] (fp32, one rounding), dlow = g[.., Ch:] dense, one launch.
+ * Replaces F.interpolate(scale 2, nearest) + torch.cat of the reference's
+ * RT-DETR encoder (Ultralytics RTDETRDecoder's HybridEncoder neck). */
+int rtdetr_upcat_nhwc_fwd(const void* high, const void* low, int B, int H, int W, int Hh, int Wh, int Ch, int Cl,
+                          void* out, hipStream_t stream);
+int rtdetr_upcat_nhwc_bwd(const void* g, int B, int H, int W, int Hh, int Wh, int Ch, int Cl, void* dhigh, void* dlow,
+                          hipStream_t stream);
 
 /* Bias gradient of a linear layer: out[n] = sum_m dy[m, n] over bf16 dy [M, N]
  * (row-major), fp32 accumulation in a fixed order (deterministic, no atomics),

@@ -108,9 +108,110 @@ __global__ __launch_bounds__(256) void maxpool3x3s2_fwd_kernel(const uint16_t* _
   reinterpret_cast<uint4*>(y)[i] = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// Encoder FPN top-down step: cat([nearest-upsample x2 of
+// high, low], channels) over channels_last bf16 in one pass, and its
+// transpose.  out [B, H, W, Ch + Cl]:  out[.., :Ch] = high[b, y/2, x/2, :]
+// (2 Hh >= H, 2 Wh >= W: the crop of an odd-sized level), out[.., Ch:] = low.
+// Backward: dhigh[b, i, j] = sum of g over the in-range 2x2 block (fp32, one
+// rounding), dlow = g[.., Ch:] as a dense tensor -- one launch, i < n1 the
+// high role, else the low role.  Replaces F.interpolate + torch.cat and their
+// backward (upsample_nearest2d_backward + the slice copies).
+__global__ __launch_bounds__(256) void upcat_fwd_kernel(const uint4* __restrict__ high, const uint4* __restrict__ low,
+                                                        int H, int W, int Hh, int Wh, int Ch8, int Cl8, long long n,
+                                                        uint4* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int C8 = Ch8 + Cl8;
+  const int cv = (int)(i % C8);
+  const long long p = i / C8;  // b * H * W + y * W + x
+  if (cv < Ch8) {
+    const int x = (int)(p % W);
+    const long long q = p / W;
+    const int y = (int)(q % H);
+    const long long b = q / H;
+    out[i] = high[((b * Hh + (y >> 1)) * Wh + (x >> 1)) * Ch8 + cv];
+  } else {
+    out[i] = low[p * Cl8 + (cv - Ch8)];
+  }
+}
+
+__global__ __launch_bounds__(256) void upcat_bwd_kernel(const uint4* __restrict__ g, int H, int W, int Hh, int Wh,
+                                                        int Ch8, int Cl8, long long n1, long long n,
+                                                        uint4* __restrict__ dhigh, uint4* __restrict__ dlow) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int C8 = Ch8 + Cl8;
+  if (i < n1) {
+    const int cv = (int)(i % Ch8);
+    long long p = i / Ch8;
+    const int j = (int)(p % Wh);
+    p /= Wh;
+    const int r = (int)(p % Hh);
+    const long long b = p / Hh;
+    float acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const int y = 2 * r + dy, x = 2 * j + dx;
+        if (y < H && x < W) {
+          float f[8];
+          unpack8(g[((b * H + y) * W + x) * C8 + cv], f);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) acc[c] += f[c];
+        }
+      }
+    dhigh[i] = pack8(acc);
+  } else {
+    const long long k = i - n1;
+    const int cv = (int)(k % Cl8);
+    const long long p = k / Cl8;
+    dlow[k] = g[p * C8 + Ch8 + cv];
+  }
+}
+
 }  // namespace moe
 
 using namespace moe;
+
+static int upcat_args_ok(const void* a, const void* b, const void* c, int B, int H, int W, int Hh, int Wh, int Ch,
+                         int Cl) {
+  if (a == nullptr || b == nullptr || c == nullptr || B < 0 || H <= 0 || W <= 0 || Hh <= 0 || Wh <= 0) return 0;
+  if ((Ch & 7) || (Cl & 7) || Ch <= 0 || Cl <= 0) return 0;
+  if (2 * Hh < H || 2 * Wh < W || Hh > H || Wh > W) return 0;
+  for (const void* q : {a, b, c})
+    if (reinterpret_cast<uintptr_t>(q) & 15) return 0;
+  return 1;
+}
+
+extern "C" int rtdetr_upcat_nhwc_fwd(const void* high, const void* low, int B, int H, int W, int Hh, int Wh, int Ch,
+                                     int Cl, void* out, hipStream_t stream) {
+  if (!upcat_args_ok(high, low, out, B, H, W, Hh, Wh, Ch, Cl))
+    return fail("upcat_fwd: need Ch, Cl % 8 == 0, H/2 <= Hh <= H (same for W), 16-B aligned pointers");
+  const long long n = (long long)B * H * W * ((Ch + Cl) / 8);
+  if (n == 0) return 0;
+  ProfScope prof(stream, PROF_CONV_EPI, 2.0 * B * ((double)Hh * Wh * Ch + 2.0 * H * W * Cl + (double)H * W * Ch));
+  MOE_LAUNCH(prof, upcat_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+             static_cast<const uint4*>(high), static_cast<const uint4*>(low), H, W, Hh, Wh, Ch / 8, Cl / 8, n,
+             static_cast<uint4*>(out));
+  return check_launch("rtdetr_upcat_nhwc_fwd");
+}
+
+extern "C" int rtdetr_upcat_nhwc_bwd(const void* g, int B, int H, int W, int Hh, int Wh, int Ch, int Cl, void* dhigh,
+                                     void* dlow, hipStream_t stream) {
+  if (!upcat_args_ok(g, dhigh, dlow, B, H, W, Hh, Wh, Ch, Cl))
+    return fail("upcat_bwd: need Ch, Cl % 8 == 0, H/2 <= Hh <= H (same for W), 16-B aligned pointers");
+  const long long n1 = (long long)B * Hh * Wh * (Ch / 8);
+  const long long n = n1 + (long long)B * H * W * (Cl / 8);
+  if (n == 0) return 0;
+  ProfScope prof(stream, PROF_CONV_EPI, 2.0 * B * ((double)H * W * (Ch + 2.0 * Cl) + (double)Hh * Wh * Ch));
+  MOE_LAUNCH(prof, upcat_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+             static_cast<const uint4*>(g), H, W, Hh, Wh, Ch / 8, Cl / 8, n1, n, static_cast<uint4*>(dhigh),
+             static_cast<uint4*>(dlow));
+  return check_launch("rtdetr_upcat_nhwc_bwd");
+}
 
 extern "C" int rtdetr_maxpool3x3s2_nhwc_fwd(const void* x, int B, int H, int W, int C, void* y, hipStream_t stream) {
   if (x == nullptr || y == nullptr || B < 0 || H <= 0 || W <= 0 || (C & 7) || C <= 0 ||

@@ -67,6 +67,8 @@ SIGNATURES = {
     "rtdetr_avgpool2x2_nhwc_fwd": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "rtdetr_avgpool2x2_nhwc_bwd": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "rtdetr_maxpool3x3s2_nhwc_fwd": (_I, [_P, _I, _I, _I, _I, _P, _P]),
+    "rtdetr_upcat_nhwc_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "rtdetr_upcat_nhwc_bwd": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "rtdetr_bias_grad_parts": (_I, [ctypes.c_longlong, _I]),
     "rtdetr_bias_grad": (_I, [_P, ctypes.c_longlong, _I, _P, _I, _P, _I, _P]),
     "rtdetr_add_layer_norm_parts": (_I, [ctypes.c_longlong]),

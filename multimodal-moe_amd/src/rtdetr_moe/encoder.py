@@ -17,6 +17,55 @@ from .fused import bn_act, bn_act_ok
 from .linear import TokenLinear, TokenSelfAttention
 
 
+class _UpCat(torch.autograd.Function):
+    """cat([nearest x2 upsample of high (cropped to low's size), low], dim=1)
+    over channels_last bf16: rtdetr_upcat_nhwc_fwd / _bwd, one launch each way."""
+
+    @staticmethod
+    def forward(ctx, high, low):
+        from ..moe import _lib as L
+
+        B, Ch, Hh, Wh = high.shape
+        Cl, H, W = low.shape[1:]
+        out = torch.empty((B, Ch + Cl, H, W), dtype=low.dtype, device=low.device, memory_format=torch.channels_last)
+        L._check(L.lib().rtdetr_upcat_nhwc_fwd(high.data_ptr(), low.data_ptr(), B, H, W, Hh, Wh, Ch, Cl,
+                                               out.data_ptr(), L._stream()), "rtdetr_upcat_nhwc_fwd")
+        ctx.dims = (B, H, W, Hh, Wh, Ch, Cl)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from ..moe import _lib as L
+
+        B, H, W, Hh, Wh, Ch, Cl = ctx.dims
+        g = g.contiguous(memory_format=torch.channels_last)
+        if g.data_ptr() % 16:
+            g = g.clone(memory_format=torch.channels_last)
+        dhigh = torch.empty((B, Ch, Hh, Wh), dtype=g.dtype, device=g.device, memory_format=torch.channels_last)
+        dlow = torch.empty((B, Cl, H, W), dtype=g.dtype, device=g.device, memory_format=torch.channels_last)
+        L._check(L.lib().rtdetr_upcat_nhwc_bwd(g.data_ptr(), B, H, W, Hh, Wh, Ch, Cl, dhigh.data_ptr(),
+                                               dlow.data_ptr(), L._stream()), "rtdetr_upcat_nhwc_bwd")
+        return dhigh, dlow
+
+
+def up_cat(high, low):
+    """The FPN top-down input: torch.cat([F.interpolate(high, scale_factor=2,
+    mode="nearest") cropped to low, low], dim=1).  channels_last bf16 GPU
+    tensors take the fused HIP pair (_UpCat); anything else the torch ops."""
+    B, Ch, Hh, Wh = high.shape
+    H, W = low.shape[-2:]
+    if (high.is_cuda and high.dtype == low.dtype == torch.bfloat16 and low.shape[0] == B and Ch % 8 == 0
+            and low.shape[1] % 8 == 0 and H <= 2 * Hh and W <= 2 * Wh and Hh <= H and Wh <= W
+            and high.is_contiguous(memory_format=torch.channels_last)
+            and low.is_contiguous(memory_format=torch.channels_last)
+            and high.data_ptr() % 16 == 0 and low.data_ptr() % 16 == 0):
+        return _UpCat.apply(high, low)
+    up = F.interpolate(high, scale_factor=2.0, mode="nearest")
+    if up.shape[-2:] != low.shape[-2:]:
+        up = up[..., :H, :W]
+    return torch.cat([up, low], dim=1)
+
+
 class DenseFFN(nn.Module):
     def __init__(self, d, hidden, act="relu"):
         super().__init__()
@@ -141,11 +190,7 @@ class HybridEncoder(nn.Module):
         for idx in range(n - 1, 0, -1):
             high = self.lateral_convs[n - 1 - idx](inner[0])
             inner[0] = high
-            up = F.interpolate(high, scale_factor=2.0, mode="nearest")
-            low = proj[idx - 1]
-            if up.shape[-2:] != low.shape[-2:]:
-                up = up[..., : low.shape[-2], : low.shape[-1]]
-            inner.insert(0, self.fpn_blocks[n - 1 - idx](torch.cat([up, low], dim=1)))
+            inner.insert(0, self.fpn_blocks[n - 1 - idx](up_cat(high, proj[idx - 1])))
         outs = [inner[0]]
         for idx in range(n - 1):
             down = self.downsample_convs[idx](outs[-1])

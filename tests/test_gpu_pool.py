@@ -53,3 +53,35 @@ def test_stem_maxpool_matches_torch(hip_lib, B, C, H, W):
     assert got.grad_fn is None and got.is_contiguous(memory_format=torch.channels_last) and got.shape == ref.shape
     assert torch.equal(torch.isnan(got), torch.isnan(ref))
     assert torch.equal(got.nan_to_num(0.0), ref.nan_to_num(0.0))
+
+
+@pytest.mark.parametrize("B,Ch,Cl,Hh,Wh,H,W", [(1, 8, 8, 1, 1, 2, 2), (2, 256, 256, 23, 40, 46, 80),
+                                              (8, 256, 256, 46, 80, 92, 160), (2, 16, 24, 3, 5, 5, 9),
+                                              (1, 8, 16, 4, 4, 7, 8)])
+def test_upcat_matches_interpolate_cat(hip_lib, B, Ch, Cl, Hh, Wh, H, W):
+    """rtdetr_upcat_nhwc_fwd / _bwd vs F.interpolate(x2, nearest) + crop +
+    torch.cat: forward and dlow bit-exact, dhigh (2x2 block sums, fp32, one
+    rounding) within one bf16 ulp of the fp32 sums; odd (cropped) levels."""
+    from src.rtdetr_moe.encoder import _UpCat, up_cat
+
+    g = torch.Generator().manual_seed(B * Ch + H * W)
+    cl = torch.channels_last
+    high = torch.randn(B, Ch, Hh, Wh, generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=cl)
+    low = torch.randn(B, Cl, H, W, generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=cl)
+    h1, l1 = high.clone().requires_grad_(True), low.clone().requires_grad_(True)
+    h2, l2 = high.clone().requires_grad_(True), low.clone().requires_grad_(True)
+    up = F.interpolate(h1, scale_factor=2.0, mode="nearest")[..., :H, :W]
+    ref = torch.cat([up, l1], dim=1)
+    got = up_cat(h2, l2)
+    assert "UpCat" in type(got.grad_fn).__name__ and got.is_contiguous(memory_format=cl)
+    assert torch.equal(got, ref)
+    gy = torch.randn(ref.shape, generator=g).to(torch.bfloat16).cuda()
+    ref.backward(gy)
+    got.backward(gy)
+    assert torch.equal(l2.grad, l1.grad)
+    g32 = gy[:, :Ch].float()
+    pad = torch.zeros(B, Ch, 2 * Hh, 2 * Wh, device="cuda")
+    pad[..., :H, :W] = g32
+    sums = pad.view(B, Ch, Hh, 2, Wh, 2).sum((3, 5))
+    assert bool(((h2.grad.float() - sums).abs() <= sums.abs() * 2.0 ** -8 + 1e-30).all())
+    _ = _UpCat
