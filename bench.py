@@ -3,19 +3,24 @@
 
 Metric and configs come from BASELINE.json.  One "step" = one full training
 step of the C2 workload on one batch: RT-DETR-R50 + 8-expert top-2 MoE FFN in
-the AIFI encoder layer and all 6 decoder layers, bf16 autocast, forward,
-Hungarian-matched VFL/L1/GIoU losses + MoE aux losses, backward, grad clip,
-AdamW step.  Synthetic ZOD-shaped batches generated once and
-kept resident in HBM; random-init weights.
+the AIFI encoder layer and all 6 decoder layers, bf16 weights with fp32
+master copies (``--precision amp``: fp32 weights under bf16 autocast),
+forward, Hungarian-matched VFL/L1/GIoU losses + MoE aux losses, backward,
+grad clip, AdamW step; by default forward + criterion + backward replay as
+ONE hipGraph.  Synthetic ZOD-shaped batches generated once
+and kept resident in HBM; random-init weights.
 
   python bench.py                               # N=1, defaults
+  python bench.py --gpus N                      # starts N ranks itself (launch_ranks)
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N         # DP over RCCL (C3), weak scaling
 
 Rank 0 prints ONE JSON line.  Besides the contract keys it carries
 ``roofline`` for the dominant HIP kernel (the grouped expert GEMM: kernel
-times from dispatch-stamped HIP events of every launch inside the timed
-region, recorded by libmoe_hip itself; algorithmic bytes and flops per launch;
+times from dispatch-stamped HIP events recorded by libmoe_hip itself -- in
+graph mode over eager steps right after the timed region, since ROCm 7.2
+stamps no events inside a hipGraph -- next to the rocprofv3-derived average
+of the committed kernel summary; algorithmic bytes and flops per launch;
 bound = HBM, since at d=256, F=1024 every expert GEMM has ~200 flop/B, below
 the MI355X balance of ~312), ``roofline_dispatch`` for the row movers, and
 ``cpu_baseline``: the same model and step in fp32 on the host cores at the
@@ -31,12 +36,71 @@ import argparse
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 from datetime import timedelta
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
+
+
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, script=None, poll_s=0.5):
+    """Start ``n`` worker ranks of ``script`` (default: this file) as fresh
+    child processes, one per GPU, and wait for them (the multi-GPU analogue of
+    the reference's ``device="0,1,..."`` string, rtdetr.py:89).  The parent
+    never touches the GPU: it runs before ``import torch`` and execs nothing,
+    so each child initialises HIP itself.  Each child gets RANK / LOCAL_RANK /
+    WORLD_SIZE / LOCAL_WORLD_SIZE and a 127.0.0.1 rendezvous.  Returns the
+    first non-zero child exit code (the other ranks are then terminated by
+    PID, so a dead rank ends the job instead of hanging it), else 0."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, str(script or Path(__file__).resolve())] + list(argv),
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"[bench] rank {procs.index(p)} exited with {c}; stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(poll_s)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def _requested_gpus(argv):
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    return ap.parse_known_args(argv)[0].gpus
+
+
+if __name__ == "__main__" and "WORLD_SIZE" not in os.environ and _requested_gpus(sys.argv[1:]) > 1:
+    # `python bench.py --gpus N` without a launcher: start the N ranks here,
+    # before anything imports torch or touches a GPU
+    sys.exit(launch_ranks(_requested_gpus(sys.argv[1:]), sys.argv[1:]))
+
 for p in (str(ROOT / "multimodal-moe_amd"), str(ROOT)):
     if p not in sys.path:
         sys.path.insert(0, p)
@@ -87,6 +151,21 @@ def load_pmc_traffic(workload):
             if "mfma_counter_frac" in e:  # rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)
                 out[g]["mfma_counter_frac"] = e["mfma_counter_frac"]
     return out
+
+
+def load_rocprof_summary(workload):
+    """Per-group average launch time of the newest committed rocprofv3
+    kernel-trace summary of the same workload (profiles/rNN/<wl>/
+    kernel_summary.json, tools/profile_summary.py over `rocprofv3
+    --kernel-trace --stats` of this bench command, graph replay included)."""
+    cands = sorted((ROOT / "profiles").glob(f"r[0-9][0-9]/{workload}/kernel_summary.json"))
+    if not cands:
+        return {}, None
+    try:
+        data = json.loads(cands[-1].read_text())
+    except ValueError:
+        return {}, None
+    return data.get("groups", {}), f"{cands[-1].relative_to(ROOT)} ({data.get('source')})"
 
 
 def merge_groups(*ds):
@@ -194,6 +273,8 @@ def setup_dist(n_gpus):
         torch.cuda.set_device(0)
     if n_gpus != world:
         print(f"[bench] warning: --gpus {n_gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    if world > 1:
+        world = dist.get_world_size()  # the process group's (RCCL's) own count, not the env's
     return world, rank, local
 
 
@@ -388,8 +469,17 @@ def main():
         L.TIMER.stop()
         prof_steps = args.profile_steps
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    rccl_world = None
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        one = torch.ones(1, device=device)
+        dist.all_reduce(one)  # the ranks that answer an RCCL all-reduce
+        rccl_world = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                      "all_reduce_ranks": int(one.item())}
+        try:
+            rccl_world["rccl_version"] = ".".join(map(str, torch.cuda.nccl.version()))
+        except Exception:  # noqa: BLE001 (optional detail)
+            pass
     elapsed = float(el.item())
     ksum = L.TIMER.summary() if timing else {}
 
@@ -402,6 +492,18 @@ def main():
         roof = roofline_entry(merge_groups(ksum.get("grouped_gemm"), ksum.get("grouped_gemm_fp8")),
                               pmc.get("grouped_gemm"), prof_elapsed,
                               "grouped GEMM (gemm_v2_kernel: expert fwd, dgrad, wgrad)")
+        rp, rp_src = load_rocprof_summary(args.workload)
+        if roof and rp.get("grouped_gemm", {}).get("avg_us"):
+            # the same algorithmic bytes per launch over rocprof's average
+            # launch duration of the graph-replayed step (the committed summary)
+            g = rp["grouped_gemm"]
+            bpl = roof["algorithmic_bytes_per_launch"]
+            ach = bpl / (g["avg_us"] * 1e-6) / 1e9
+            roof["rocprof"] = {"avg_us": g["avg_us"], "launches": g.get("launches"), "achieved": round(ach, 2),
+                               "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "source": rp_src}
+            if roof.get("flop_per_launch"):
+                tf = roof["flop_per_launch"] / (g["avg_us"] * 1e-6) / 1e12
+                roof["rocprof"]["mfma_tflops"] = round(tf, 1)
         rd = roofline_entry(ksum.get("dispatch"), pmc.get("dispatch"), prof_elapsed,
                             "permute_fwd / combine_fwd / combine_bwd")
         kprof = {}
@@ -425,7 +527,8 @@ def main():
                                      else "hipGraph fwd/bwd") if graphs else "eager",
                        "precision": "bf16 weights + fp32 master" if args.precision == "bf16" else "bf16 autocast",
                        "img": f"{args.img_w}x{args.img_h} (padded to {data.pad_w}x{data.pad_h})",
-                       "parallelism": f"dp{world}" if "ep" not in spec else f"dp{world}+ep{world}"},
+                       "parallelism": f"dp{world}" if "ep" not in spec else f"dp{world}+ep{world}",
+                       "rccl_world": rccl_world},
             "roofline": roof, "roofline_dispatch": rd, "kernel_profile": kprof,
             "kernel_timing": None if not timing else (
                 f"libmoe_hip dispatch-stamped events over the {args.steps} timed steps" if not graphs else

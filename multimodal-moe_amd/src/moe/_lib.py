@@ -545,15 +545,18 @@ def router_wgrad(dlogits, x, ctx_img, tokens_per_image, n_ctx):
     _need(x, torch.bfloat16, "x")
     T, E = dlogits.shape
     d = x.shape[1]
-    tpi = int(tokens_per_image)
-    if T % tpi:
+    has_ctx = ctx_img is not None and n_ctx > 0
+    # without a context bias the image split only shapes the slices: all T
+    # tokens are one "image" then (any tokens_per_image, including 0, works)
+    tpi = int(tokens_per_image) if has_ctx else max(T, 1)
+    if tpi <= 0 or T % tpi:
         raise MoEKernelError(f"router_wgrad: T = {T} is not a multiple of tokens_per_image = {tpi}")
     B = T // tpi
     S = B * int(lib().moe_router_wgrad_slices(tpi))
     part = torch.empty(max(1, S * E * (d + 1)), dtype=torch.float32, device=x.device)
     dwg = torch.empty((E, d), dtype=torch.float32, device=x.device)
     dcb = None
-    if ctx_img is not None and n_ctx > 0:
+    if has_ctx:
         _need(ctx_img, torch.int32, "ctx_img")
         dcb = torch.empty((n_ctx, E), dtype=torch.float32, device=x.device)
     _check(lib().moe_router_wgrad(_ptr(dlogits), _ptr(x), _ptr(ctx_img) if dcb is not None else None, B, tpi, E, d,

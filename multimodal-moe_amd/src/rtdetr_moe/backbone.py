@@ -308,19 +308,29 @@ _NO_FORK = os.environ.get("MOE_BACKBONE_FORK", "1") == "0"
 _NO_FOLD_ALL = os.environ.get("MOE_FOLD_ALL", "1") == "0"
 
 
+def _fork_ok(short):
+    """Whether _block_out takes its fused fork path for a block with this
+    shortcut (given a folded, HIP-eligible last convolution).  Only then does
+    the last convolution's dgrad apply the ReLU mask of its input, so the
+    producer may skip its own ReLU backward (grad_premasked) only then."""
+    return not _NO_FORK and (short is None or short.conv.fold)
+
+
 def _block_out(last, short, h, x, folded_last=None, mask_input=False, link_in=None):
     """relu(last(h) + shortcut(x)) as a (main, shortcut) pair of handles on the
     same activation (see fused.AddBiasReLUFork).  With frozen BNs the two BN
     shifts join the residual add and the ReLU in one fused kernel -- the
     epilogue of last's HIP convolution when it has one (folded_last given and
     hip_ok; mask_input: h is a ReLU output only last consumes)."""
-    if last.fold and (short is None or short.conv.fold) and folded_last is not None and not _NO_FORK:
+    if last.fold and _fork_ok(short) and folded_last is not None:
         wl, sl = folded_last
         if mask_input or last.hip_ok(h, h.shape[1], wl):
             b, bias = (x, sl) if short is None else short.conv_shift(x)
             if short is not None:
                 bias = sl + bias
             return conv2d_add_bias_relu_fork(h, wl, b, bias, mask_input, link_in if short is None else None)
+    if mask_input:  # the producer skipped its ReLU backward for the fork path's dgrad mask
+        raise RuntimeError("_block_out: mask_input set but the fused fork path does not run")
     if last.fold and (short is None or short.conv.fold):
         a, sa = last.conv_shift(h, folded_last)
         b, bias = (x, sa) if short is None else short.conv_shift(x)
@@ -363,8 +373,8 @@ class BasicBlock(nn.Module):
         if _FUSED_EPI and a.fold and b.fold and a.act_name == "relu" and x.is_cuda:
             fa, fb = a.folded(), b.folded()
             ok_a = a.hip_ok(x, x.shape[1], fa[0])
-            ok_b = b.hip_ok(x, fa[0].shape[0], fb[0])
-            pre_ab = ok_a and ok_b  # branch2b's dgrad masks branch2a's ReLU
+            ok_b = b.hip_ok(x, fa[0].shape[0], fb[0]) and _fork_ok(self.short)
+            pre_ab = ok_a and ok_b  # branch2b's dgrad (the fork path of _block_out) masks branch2a's ReLU
             link = _link_for(self.short, x, ok_a and ok_b)
             h = a.bias_relu(x, fa, grad_premasked=pre_ab, link=link) if ok_a else a.bias_relu(x, fa)
             return _block_out(b, self.short, h, xs, fb, mask_input=pre_ab, link_in=link)
@@ -395,8 +405,8 @@ class BottleNeck(nn.Module):
             fa, fb, fc = a.folded(), b.folded(), c.folded()
             ok_a = a.hip_ok(x, x.shape[1], fa[0])
             ok_b = b.hip_ok(x, fa[0].shape[0], fb[0])
-            ok_c = c.hip_ok(x, fb[0].shape[0], fc[0])
-            pre_ab, pre_bc = ok_a and ok_b, ok_b and ok_c
+            ok_c = c.hip_ok(x, fb[0].shape[0], fc[0]) and _fork_ok(self.short)
+            pre_ab, pre_bc = ok_a and ok_b, ok_b and ok_c  # pre_bc: only when _block_out takes its fork path
             link = _link_for(self.short, x, ok_a and ok_c)
             h1 = a.bias_relu(x, fa, grad_premasked=pre_ab, link=link)
             h2 = b.bias_relu(h1, fb, mask_input=pre_ab, grad_premasked=pre_bc)

@@ -358,7 +358,9 @@ class TokenSelfAttention(nn.Module):
         H = self.num_heads
         qk = self._proj(qk_in, 0, 2 * d)
         v = self._proj(v_in, 2 * d, 3 * d)
-        if qk.is_cuda:  # HIP attention (csrc/attn.hip): no Triton-generated SDPA kernels in the step
+        if qk.is_cuda and d % H == 0 and d // H == 32 and d % 8 == 0:
+            # HIP attention (csrc/attn.hip, head_dim 32: RT-DETR's 256 / 8):
+            # no Triton-generated SDPA kernels in the step
             return self.out_proj(self_attention_hip(qk, v, H))
         q, k = qk.split(d, -1)
         heads = lambda t: t.reshape(B, L, H, d // H).transpose(1, 2)  # noqa: E731

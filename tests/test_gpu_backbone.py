@@ -172,3 +172,33 @@ def test_fold_all_matches_per_layer_fold(hip_lib):
     assert not any(k.startswith("stem") for k in res[1][1])
     for k in res[0][1]:
         assert _rel(res[1][1][k], res[0][1][k]) < 2e-2, k
+
+
+@pytest.mark.parametrize("depth", [18, 50])
+def test_no_fork_switch_keeps_relu_backward(hip_lib, monkeypatch, depth):
+    """MOE_BACKBONE_FORK=0 (backbone._NO_FORK) takes _block_out's autograd
+    fallback; the producing convolutions must then keep their own ReLU
+    backward (they skipped it and the gradients came out wrong).
+    Same outputs and weight gradients as the fork path, at bf16 noise."""
+    from src.rtdetr_moe import backbone as bb
+
+    torch.manual_seed(0)
+    m = bb.PResNet(depth).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for mod in m.modules():
+        if hasattr(mod, "running_var") and not isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_var.uniform_(0.5, 2.0)
+            mod.weight.uniform_(0.5, 1.5)
+    x = torch.randn(2, 3, 128, 160, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    for no_fork in (False, True):
+        monkeypatch.setattr(bb, "_NO_FORK", no_fork)
+        m.zero_grad(set_to_none=True)
+        outs = m(x)
+        sum(o.float().square().mean() for o in outs).backward()
+        res.append(([o.detach().clone() for o in outs],
+                    {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert _rel(b, a) < 2e-3
+    assert res[0][1].keys() == res[1][1].keys()
+    for k in res[0][1]:
+        assert _rel(res[1][1][k], res[0][1][k]) < 2e-2, k
