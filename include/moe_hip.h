@@ -91,7 +91,7 @@ int moe_route_index(const int32_t* topk_idx, const int32_t* local_rank, const in
                     hipStream_t stream);
 
 /* a3 + a4 in ONE launch, from the router's outputs: the
- * moe_route_scan totals and prefixes (recomputed per 64-token router block
+ * moe_route_scan totals and prefixes (recomputed per 16-token router block
  * from block_counts, so no second pass), hist / offsets, pos and src_tok as
  * moe_route_index, optionally row_gate[pos[t,j]] = topk_w[t,j] (fp32 [>=
  * offsets[E]]) and the aux losses of moe_aux_loss_fwd (aux_out3 / wcoef /
@@ -217,6 +217,22 @@ int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, void* c
 int moe_grouped_gemm_gather(int dtype, const void* a, const int32_t* a_gather, const void* b, void* c,
                             const int32_t* offsets, int G, int max_rows, int N, int K, int trans_b,
                             int epilogue, const float* bias, const void* aux, hipStream_t stream);
+/* a5: the expert FFN forward in ONE launch,
+ *   h  = relu(x[src_tok[r]] . W1_g^T + b1_g)   bf16 [>= offsets[G], F]
+ *   yp = h . W2_g^T + b2_g                      bf16 [>= offsets[G], d]
+ * for the routed rows r of every expert g (src_tok == NULL: x holds the
+ * routed rows themselves).  Same contract as moe_grouped_gemm_gather(EPI_BIAS_RELU)
+ * followed by moe_grouped_gemm(EPI_BIAS) on h, without h's second pass:
+ * h is written once (the backward's mask / dW2 operand) and never read here.
+ * w1 bf16 [G, F, d], w2 bf16 [G, d, F]; b1 [G, F], b2 [G, d] fp32, or bf16
+ * with MOE_BIAS_BF16 in dtype.  Needs moe_expert_ffn_supported(G, F, d)
+ * (d == 256, F % 128 == 0 and F <= 2048, G <= 64) and 16-B aligned operands.
+ * The reference has no MoE: the expert is "a standard MLP block"
+ * (notes/related_work.md:23). */
+int moe_expert_ffn_supported(int G, int F, int d);
+int moe_expert_ffn_fwd(int dtype, const void* x, const int32_t* src_tok, const void* w1, const void* b1,
+                       const void* w2, const void* b2, const int32_t* offsets, int G, int max_rows, int F, int d,
+                       void* h, void* yp, hipStream_t stream);
 /* moe_grouped_gemm_wgrad_rows with k-row r of Y read as y[y_gather[r]]
  * (dW1 = dH^T Xp from the token rows); y_gather == NULL: contiguous. */
 int moe_grouped_gemm_wgrad_gather(int dtype, const void* x, const void* y, const int32_t* y_gather, void* c,

@@ -115,6 +115,8 @@ def kernels(c):
                                              bias=c["b1"]), 2.0 * A * F * d, 0),
         ("gemm2_fwd", lambda: L.grouped_gemm(c["h"], c["w2"], c["offsets"], E, rows, d, F, 1, L.EPI_BIAS,
                                              bias=c["b2"]), 2.0 * A * F * d, 0),
+        ("ffn_fwd_fused", lambda: L.expert_ffn_fwd(c["x"], c["tok"], c["w1"], c["b1"], c["w2"], c["b2"], c["offsets"],
+                                                   E, rows), 4.0 * A * F * d, 0),
         ("route_index", lambda: L.route_index(c["idx"], c["lrank"], c["rank_base"], c["offsets"], E, 0, rows), 0,
          16 * A + 4 * A),
         ("gemm1_fwd_gather", lambda: L.grouped_gemm_gather(c["x"], c["tok"], c["w1"], c["offsets"], E, rows, F, d, 1,

@@ -46,6 +46,8 @@ SIGNATURES = {
     "moe_route_index": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "moe_route_dispatch": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P]),
     "moe_grouped_gemm_gather": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "moe_expert_ffn_supported": (_I, [_I, _I, _I]),
+    "moe_expert_ffn_fwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "moe_grouped_gemm_wgrad_gather": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "moe_grouped_gemm_bwd_pair": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                        _I, _I, _I, _P]),
@@ -473,6 +475,36 @@ def grouped_gemm_gather(x, src_tok, b, offsets, G, max_rows, N, K, trans_b, epil
                                          int(max_rows), N, K, int(trans_b), int(epilogue), _ptr(bias), _ptr(aux),
                                          _stream()), "moe_grouped_gemm_gather")
     return c
+
+
+def expert_ffn_supported(G, F, d):
+    return bool(lib().moe_expert_ffn_supported(int(G), int(F), int(d)))
+
+
+def expert_ffn_fwd(x, src_tok, w1, b1, w2, b2, offsets, G, max_rows):
+    """One launch (moe_expert_ffn_fwd): h = relu(x[src_tok[r]] W1_g^T + b1_g),
+    yp = h W2_g^T + b2_g for every routed row r (src_tok None: x holds the
+    routed rows).  w1 bf16 [G, F, d], w2 bf16 [G, d, F]; b1 / b2 fp32 or bf16
+    (both the same).  -> (h bf16 [rows, F], yp bf16 [rows, d])."""
+    _need(x, torch.bfloat16, "x")
+    _need(w1, torch.bfloat16, "w1")
+    _need(w2, torch.bfloat16, "w2")
+    if src_tok is not None:
+        _need(src_tok, torch.int32, "src_tok")
+    Gw, F, d = w1.shape
+    if Gw != G or tuple(w2.shape) != (G, d, F) or x.shape[1] != d or b1.numel() != G * F or b2.numel() != G * d:
+        raise MoEKernelError("expert_ffn_fwd: shapes")
+    if b1.dtype != b2.dtype or b1.dtype not in (torch.float32, torch.bfloat16):
+        raise MoEKernelError("expert_ffn_fwd: b1 / b2 must both be fp32 or both bf16")
+    if src_tok is not None and src_tok.numel() < max_rows:
+        raise MoEKernelError("expert_ffn_fwd: src_tok shorter than max_rows")
+    h = torch.empty((max(max_rows, 1), F), dtype=torch.bfloat16, device=x.device)
+    yp = torch.empty((max(max_rows, 1), d), dtype=torch.bfloat16, device=x.device)
+    dt = MOE_BF16 | (MOE_BIAS_BF16 if b1.dtype == torch.bfloat16 else 0)
+    _check(lib().moe_expert_ffn_fwd(dt, _ptr(x), _ptr(src_tok), _ptr(w1), _ptr(b1.contiguous()),
+                                    _ptr(w2), _ptr(b2.contiguous()), _ptr(offsets), G, int(max_rows), F, d,
+                                    _ptr(h), _ptr(yp), _stream()), "moe_expert_ffn_fwd")
+    return h, yp
 
 
 def grouped_gemm_bwd_pair(a, b, offsets, G, max_rows, N, K, epilogue, aux, wx, wy, wy_gather=None,

@@ -7,13 +7,15 @@ for the MXFP8 (C5) and expert-parallel (C4) compositions:
                   scan, K2's index half (pos and the row -> token map; the
                   routed rows are never copied) and the aux losses, one launch
                   backward: token_bwd (dispatch transpose + router backward)
-  _ExpertFFNGather grouped GEMM1 (+b1, ReLU) reading the token rows through
-                  the row map, GEMM2 (+b2)
+  _ExpertFFNGather the expert FFN forward reading the token rows through the
+                  row map: ONE moe_expert_ffn_fwd launch (GEMM1 +b1, ReLU,
+                  H written once, GEMM2 +b2 on H still in registers), or
+                  GEMM1 and GEMM2 as two grouped GEMMs (MOE_FUSED_FFN=0)
                   backward: two paired launches (moe_grouped_gemm_bwd_pair):
                   {dH = dgrad (ReLU mask), dW2 + db2} and {dXp = dgrad, dW1 + db1
                   with the token rows gathered}
   _Combine        gate-weighted combine (K3); backward: combine_bwd
-Single GPU: 5 launches forward (router, route_dispatch, GEMM1, GEMM2,
+Single GPU: 4 launches forward (router, route_dispatch, fused expert FFN,
 combine), 4 backward (combine_bwd, 2 pairs, token_bwd) + 1 torch GEMM for dWg.  The
 expert-parallel path (ep.py) moves real rows through its all-to-alls and runs
 _RouteDispatch (permute) + _ExpertFFN (rows in, same paired backward).  Nothing is synchronised with the host: expert
@@ -40,6 +42,26 @@ def _bias(b):
     """A grouped-GEMM bias operand: bf16 parameters as they are (MOE_BIAS_BF16:
     the kernel widens them), anything else as fp32."""
     return b.contiguous() if b.dtype == torch.bfloat16 else b.float().contiguous()
+
+
+# MOE_FUSED_FFN=0: the expert FFN forward as two grouped GEMMs (A/B switch)
+_FUSED_FFN = os.environ.get("MOE_FUSED_FFN", "1") != "0"
+
+
+def _ffn_forward(xb, tok, w1b, b1, w2b, b2, offsets, G, rows):
+    """(h, yp) of the expert FFN forward: ONE moe_expert_ffn_fwd launch (H
+    written once, never read back) when the shape allows it, else GEMM1
+    (gathering token rows when ``tok`` is given) and GEMM2 as two launches."""
+    F, d = w1b.shape[1], w1b.shape[2]
+    bb1, bb2 = _bias(b1), _bias(b2)
+    if _FUSED_FFN and bb1.dtype == bb2.dtype and L.expert_ffn_supported(G, F, d):
+        return L.expert_ffn_fwd(xb, tok, w1b, bb1, w2b, bb2, offsets, G, rows)
+    if tok is not None:
+        h = L.grouped_gemm_gather(xb, tok, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU, bias=bb1)
+    else:
+        h = L.grouped_gemm(xb, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU, bias=bb1)
+    yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=bb2)
+    return h, yp
 
 
 def _padded_offsets(E, pad, device):
@@ -212,9 +234,7 @@ class _ExpertFFNGather(torch.autograd.Function):
         G, F, d = w1.shape
         w1b = w1.to(torch.bfloat16).contiguous()
         w2b = w2.to(torch.bfloat16).contiguous()
-        h = L.grouped_gemm_gather(xb, tok, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU,
-                                  bias=_bias(b1))
-        yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=_bias(b2))
+        h, yp = _ffn_forward(xb, tok, w1b, b1, w2b, b2, offsets, G, rows)
         ctx.save_for_backward(xb, tok, h, w1b, w2b, offsets)
         ctx.meta = (G, rows, float(grad_scale))
         ctx.wdtype = w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32
@@ -235,8 +255,7 @@ class _ExpertFFN(torch.autograd.Function):
         G, F, d = w1.shape
         w1b = w1.to(torch.bfloat16).contiguous()
         w2b = w2.to(torch.bfloat16).contiguous()
-        h = L.grouped_gemm(xp, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU, bias=_bias(b1))
-        yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=_bias(b2))
+        h, yp = _ffn_forward(xp, None, w1b, b1, w2b, b2, offsets, G, rows)
         ctx.save_for_backward(xp, h, w1b, w2b, offsets)
         ctx.meta = (G, F, d, rows, float(grad_scale))
         ctx.wdtype = w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32
@@ -366,8 +385,9 @@ class _MoELayer(torch.autograd.Function):
     """The whole single-GPU bf16 routed FFN of one layer as ONE autograd node
     (SURVEY 8(a) rows a2-a7), 8 HIP launches forward + backward:
       forward  router_topk_fwd; route_dispatch (scan, index, row gates, aux
-               losses); GEMM1 reading token rows through the row map (+b1,
-               ReLU); GEMM2 (+b2); combine
+               losses); the expert FFN reading token rows through the row
+               map (moe_expert_ffn_fwd: GEMM1 +b1, ReLU, GEMM2 +b2 in one
+               launch); combine
       backward bwd_pair {dH = gate * (dy[token] W2) * (H > 0), dW2 = dYp^T H,
                db2} with dYp = gate * dy[token] formed inside the GEMMs (no
                combine transpose launch); bwd_pair {dXp = dH W1, dW1 = dH^T
@@ -397,9 +417,7 @@ class _MoELayer(torch.autograd.Function):
                                                                       lb_coef, z_coef, row_gate=True)
         w1b = w1.to(torch.bfloat16).contiguous()
         w2b = w2.to(torch.bfloat16).contiguous()
-        h = L.grouped_gemm_gather(xb, tok, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU,
-                                  bias=_bias(b1))
-        yp = L.grouped_gemm(h, w2b, offsets, G, rows, d, F, 1, L.EPI_BIAS, bias=_bias(b2))
+        h, yp = _ffn_forward(xb, tok, w1b, b1, w2b, b2, offsets, G, rows)
         y = L.combine_fwd(yp, pos, w, T, resid=xb if residual else None)
         ctx.residual = bool(residual)
         ctx.save_for_backward(xb, wg32, idx, w, probs, lse, pos, tok, gate, h, yp, w1b, w2b, offsets, wcoef,

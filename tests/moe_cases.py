@@ -106,8 +106,9 @@ G_LB, G_Z = 0.7, 0.3  # loss = <dy, y> + G_LB lb + G_Z z (gradients of both aux 
 
 def run_oracle(c: LayerCase, inp: dict, fused_dgrad: bool = False):
     """fused_dgrad: emulate the single-GPU bf16 layer's gate-in-epilogue dgrad
-    (oracle.moe_backward); the golden fixtures and the EP / MXFP8 paths (which
-    scatter a bf16 dYp) use the plain rounding points."""
+    (oracle.moe_backward) -- the bf16 golden fixtures use it too
+    (tests/golden/make_moe_golden.py); the EP and MXFP8 paths (which scatter a
+    bf16 dYp) use the plain rounding points."""
     st = O.moe_forward(inp["x"], inp["wg"], inp["ctx_bias"], inp["w1"], inp["b1"], inp["w2"], inp["b2"],
                        inp["ctx_img"], c.tpi, c.k, True, c.cap, emulate_bf16=True, mx=c.mx)
     gr = O.moe_backward(st, inp["x"], inp["wg"], inp["w1"], inp["w2"], inp["ctx_img"], c.tpi, 6, inp["dy"],

@@ -129,9 +129,9 @@ def test_whole_step_graph_dp_equals_single_process_mean(hip_lib, tmp_path, preci
         return d2 ** 0.5 / sum(float(ref[n].norm()) ** 2 for n in got) ** 0.5
 
     # Tolerance: the forward is bitwise repeatable, the backward is not (the
-    # deformable-attention value gradients are bf16 atomics and MIOpen's
-    # backward-data / weight convolution solvers sum split-K slices with fp32
-    # atomics, both in arrival order), so two single-process
+    # deformable-attention value gradients are bf16 atomics summed in arrival
+    # order, DESIGN.md 5 -- the convolutions are HIP kernels with fixed-order
+    # sums since round 3, no MIOpen atomic solver runs), so two single-process
     # replays of the same images already differ.  The data-parallel mean must
     # sit within 3x that measured spread (+1e-3) of the single-process mean.
     floor = rel_err({n: ref2[n] for n in r0["g"]})

@@ -1,0 +1,117 @@
+"""The fused expert FFN forward (moe_expert_ffn_fwd, csrc/expert_ffn.hip)
+against the two-launch path it replaces (GEMM1 with the row gather + ReLU,
+GEMM2) and a torch fp32 reference.
+
+Tolerances: with small-integer data every fp32 sum is exact in any order, so
+H and Yp must equal the two-launch outputs bit for bit.  H is bit-exact for
+any data (the same MFMA accumulation order over K = 256 as GEMM1).  Yp on
+random data: the two F halves of every chunk accumulate separately and are
+added once, so it is compared with the fp32 reference (bf16(H) W2^T + b2) at
+1e-2 of max|ref| + 1 bf16 ulp per element, and its relative Frobenius error
+must not exceed 1.5x the two-launch path's + 1e-4.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ints(rng, shape, lo, hi):
+    return torch.from_numpy(rng.integers(lo, hi, size=shape).astype(np.float32))
+
+
+def _two_launch(L, x, tok, w1, b1, w2, b2, off, G, R):
+    F, d = w1.shape[1], w1.shape[2]
+    if tok is not None:
+        h = L.grouped_gemm_gather(x, tok, w1, off, G, R, F, d, 1, L.EPI_BIAS_RELU, bias=b1)
+    else:
+        h = L.grouped_gemm(x, w1, off, G, R, F, d, 1, L.EPI_BIAS_RELU, bias=b1)
+    yp = L.grouped_gemm(h, w2, off, G, R, d, F, 1, L.EPI_BIAS, bias=b2)
+    return h, yp
+
+
+@pytest.mark.parametrize("rows_per_group", [[0, 1, 63, 64, 65, 200, 0, 130], [1500, 40, 0, 1100],
+                                            [7] * 32, [3000]])
+@pytest.mark.parametrize("gather", [True, False])
+@pytest.mark.parametrize("bias_bf16", [False, True])
+@pytest.mark.parametrize("F", [1024, 384])
+def test_expert_ffn_exact_vs_two_launch(hip_lib, rows_per_group, gather, bias_bf16, F):
+    from src.moe import _lib as L
+
+    rng = np.random.default_rng(5)
+    G, d = len(rows_per_group), 256
+    assert L.expert_ffn_supported(G, F, d)
+    offsets = np.concatenate([[0], np.cumsum(rows_per_group)]).astype(np.int32)
+    R = int(offsets[-1])
+    T = max(R // 2, 1) + 3
+    # |H| <= 2 * 256 before the bf16 rounding; |Yp| sums <= 512 * F < 2^24: exact fp32 in any order
+    x = _ints(rng, (T if gather else R + 5, d), -2, 3).to(torch.bfloat16).to(DEV)
+    tok = torch.from_numpy(rng.integers(0, T, size=R + 5).astype(np.int32)).to(DEV) if gather else None
+    w1 = _ints(rng, (G, F, d), -1, 2).to(torch.bfloat16).to(DEV)
+    w2 = _ints(rng, (G, d, F), -1, 2).to(torch.bfloat16).to(DEV)
+    bdt = torch.bfloat16 if bias_bf16 else torch.float32
+    b1 = _ints(rng, (G, F), -8, 9).to(bdt).to(DEV)
+    b2 = _ints(rng, (G, d), -8, 9).to(bdt).to(DEV)
+    off = torch.from_numpy(offsets).to(DEV)
+    h, yp = L.expert_ffn_fwd(x, tok, w1, b1, w2, b2, off, G, R + 5)
+    h_ref, yp_ref = _two_launch(L, x, tok, w1, b1, w2, b2, off, G, R + 5)
+    torch.cuda.synchronize()
+    assert torch.equal(h[:R], h_ref[:R])
+    assert torch.equal(yp[:R], yp_ref[:R])
+    # rows past offsets[G] are never written (the launch's row bound is a host upper bound)
+    assert h.shape == (R + 5, F) and yp.shape == (R + 5, d)
+
+
+@pytest.mark.parametrize("T,E,k", [(8 * 920, 8, 2), (8 * 300, 8, 2), (16 * 300, 32, 4), (2 * 400, 4, 1)])
+def test_expert_ffn_random_vs_fp32(hip_lib, T, E, k):
+    """C2 encoder / decoder, C5 (bf16) and C1 layer shapes with a random
+    expert-major routing of every token k times."""
+    from src.moe import _lib as L
+
+    g = torch.Generator().manual_seed(T + E)
+    d, F = 256, 1024
+    R = T * k
+    counts = torch.distributions.Multinomial(R, torch.ones(E)).sample().long()
+    offsets = torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)]).int()
+    x = torch.randn(T, d, generator=g).to(torch.bfloat16)
+    tok = torch.randint(0, T, (R,), generator=g).int()
+    w1 = (torch.randn(E, F, d, generator=g) / 16).to(torch.bfloat16)
+    w2 = (torch.randn(E, d, F, generator=g) / 32).to(torch.bfloat16)
+    b1 = torch.randn(E, F, generator=g) * 0.1
+    b2 = torch.randn(E, d, generator=g) * 0.1
+    xd, tokd, w1d, w2d, b1d, b2d, offd = (t.to(DEV) for t in (x, tok, w1, w2, b1, b2, offsets))
+    h, yp = L.expert_ffn_fwd(xd, tokd, w1d, b1d, w2d, b2d, offd, E, R)
+    h2, yp2 = _two_launch(L, xd, tokd, w1d, b1d, w2d, b2d, offd, E, R)
+    torch.cuda.synchronize()
+    assert torch.equal(h, h2)
+    ref = torch.empty(R, d)
+    hf = h.float().cpu()
+    off = offsets.tolist()
+    for e in range(E):
+        a, b = off[e], off[e + 1]
+        ref[a:b] = hf[a:b] @ w2[e].float().T + b2[e]
+    got, two = yp.float().cpu(), yp2.float().cpu()
+    tol = 1e-2 * ref.abs().max() + ref.abs() * 2.0 ** -8
+    assert ((got - ref).abs() <= tol).all()
+    rel = float((got - ref).norm() / ref.norm())
+    rel2 = float((two - ref).norm() / ref.norm())
+    assert rel <= 1.5 * rel2 + 1e-4, (rel, rel2)
+
+
+def test_expert_ffn_rejects_bad_shapes(hip_lib):
+    from src.moe import _lib as L
+
+    assert not L.expert_ffn_supported(8, 1000, 256)
+    assert not L.expert_ffn_supported(8, 1024, 128)
+    assert not L.expert_ffn_supported(65, 1024, 256)
+    x = torch.zeros(4, 256, dtype=torch.bfloat16, device=DEV)
+    w1 = torch.zeros(2, 1024, 256, dtype=torch.bfloat16, device=DEV)
+    w2 = torch.zeros(2, 256, 1024, dtype=torch.bfloat16, device=DEV)
+    off = torch.tensor([0, 2, 4], dtype=torch.int32, device=DEV)
+    with pytest.raises(L.MoEKernelError):
+        L.expert_ffn_fwd(x, None, w1, torch.zeros(2, 1024, device=DEV), w2,
+                         torch.zeros(2, 256, device=DEV, dtype=torch.bfloat16), off, 2, 4)
