@@ -232,7 +232,23 @@ int moe_grouped_gemm_gather(int dtype, const void* a, const int32_t* a_gather, c
 int moe_expert_ffn_supported(int G, int F, int d);
 int moe_expert_ffn_fwd(int dtype, const void* x, const int32_t* src_tok, const void* w1, const void* b1,
                        const void* w2, const void* b2, const int32_t* offsets, int G, int max_rows, int F, int d,
-                       void* h, void* yp, hipStream_t stream);
+                       void* h, void* yp, const int32_t* yp_rows, int yp_n, hipStream_t stream);
+/* (yp_rows, yp_n): NULL, ignored -> yp row r is routed row r; else routed row
+ * r is stored at yp row yp_rows[r] of the yp_n-row buffer (the expert-parallel
+ * received layout: moe_ep_compaction's gather map), rows of yp that no routed
+ * row maps to are left untouched. */
+
+/* Expert-parallel receive map (src/moe/ep.py): rank r
+ * received, from source w, recv_cnt[w El + e] rows for local expert e (capped
+ * at S), held at received row (w El + e) S + j.  Writes offsets int32 [El + 1]
+ * (expert-major compact order, sources in rank order inside an expert) and
+ * gather int32 [>= W El S]: compact row -> received row (the expert GEMMs read
+ * the received rows through it and write back through it), and, when
+ * overflow != NULL, *overflow = sum_e max(hist[e] - S, 0) of this rank's send
+ * histogram hist int32 [E] (assignments the fixed-capacity exchange dropped).
+ * One launch, no host sync.  Replaces a chain of torch index ops. */
+int moe_ep_compaction(const int32_t* recv_cnt, const int32_t* hist, int W, int El, int E, int S, int32_t* gather,
+                      int32_t* offsets, int32_t* overflow, hipStream_t stream);
 /* moe_grouped_gemm_wgrad_rows with k-row r of Y read as y[y_gather[r]]
  * (dW1 = dH^T Xp from the token rows); y_gather == NULL: contiguous. */
 int moe_grouped_gemm_wgrad_gather(int dtype, const void* x, const void* y, const int32_t* y_gather, void* c,
@@ -289,6 +305,16 @@ int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather, const floa
                               const void* wy, const int32_t* wy_gather, void* wc, void* wcolsum, int M2, int N2,
                               int out_bf16, hipStream_t stream);
 /* (wc = wcolsum = NULL: the dgrad alone.) */
+/* The same, with dgrad row r stored at C row c_rows[r] (c_rows int32 [>=
+ * offsets[G]], e.g. moe_ep_compaction's gather: dXp lands in the expert-
+ * parallel received layout with no separate row-gather pass); the relu-mask
+ * operand aux stays indexed by r.  c_rows == NULL is moe_grouped_gemm_bwd_pair. */
+int moe_grouped_gemm_bwd_pair_scatter(const void* a, const int32_t* a_gather, const float* row_scale, const void* b,
+                                      void* c, const int32_t* c_rows, const int32_t* offsets, int G, int max_rows,
+                                      int N, int K, int epilogue, const void* aux, const void* wx,
+                                      const int32_t* wx_gather, const float* wx_scale, const void* wy,
+                                      const int32_t* wy_gather, void* wc, void* wcolsum, int M2, int N2,
+                                      int out_bf16, hipStream_t stream);
 
 /* ---- MXFP8 expert path (config C5: 32-expert top-4 fp8 expert GEMMs) ----
  * Format: OCP e4m3 elements with one E8M0 exponent byte per 32 consecutive

@@ -225,3 +225,63 @@ extern "C" int moe_combine_bwd(const void* dy, const void* yp, const int32_t* po
                      topk_w, T, d, k, static_cast<uint16_t*>(dyp), dw);
   return check_launch("moe_combine_bwd");
 }
+
+namespace moe {
+
+// ---------------------------------------------------------------------------
+// Expert-parallel receive map: rank r received, from source
+// w, cnt[w][e] rows for each of its El local experts, held at received row
+// (w El + e) S + j, j < cnt[w][e] (the fixed-capacity layout of src/moe/ep.py).
+// The local experts' GEMMs read them in compact expert-major order (expert e's
+// rows from source 0, then source 1, ...):
+//   offsets[e] = sum_{e' < e} sum_w cnt[w][e'],  offsets[El] = the total
+//   gather[offsets[e] + sum_{w' < w} cnt[w'][e] + j] = (w El + e) S + j
+// One workgroup per (w, e) pair (its prefix recomputed from the <= 1024
+// counts), so the map is one launch with no host sync; workgroup 0 also
+// writes offsets and the overflow of this rank's send histogram,
+// sum_e max(hist[e] - S, 0) (assignments the exchange dropped).
+__global__ __launch_bounds__(256) void ep_compaction_kernel(const int32_t* __restrict__ cnt,
+                                                            const int32_t* __restrict__ hist, int W, int El, int E,
+                                                            int S, int32_t* __restrict__ gather,
+                                                            int32_t* __restrict__ offsets,
+                                                            int32_t* __restrict__ overflow) {
+  __shared__ int s_start;
+  const int b = blockIdx.x, w = b / El, e = b % El;
+  if (threadIdx.x == 0) {
+    int st = 0;
+    for (int ww = 0; ww < W; ++ww)
+      for (int ee = 0; ee < El; ++ee)
+        if (ee < e || (ee == e && ww < w)) st += min(cnt[ww * El + ee], S);
+    s_start = st;
+  }
+  if (b == 0) {
+    for (int ee = threadIdx.x; ee <= El; ee += blockDim.x) {
+      int o = 0;
+      for (int e2 = 0; e2 < ee; ++e2)
+        for (int ww = 0; ww < W; ++ww) o += min(cnt[ww * El + e2], S);
+      offsets[ee] = o;
+    }
+    if (overflow != nullptr && threadIdx.x == 0) {
+      int ov = 0;
+      for (int ee = 0; ee < E; ++ee) ov += max(hist[ee] - S, 0);
+      *overflow = ov;
+    }
+  }
+  __syncthreads();
+  const int n = min(cnt[b], S), st = s_start;
+  const int src0 = b * S;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) gather[st + j] = src0 + j;
+}
+
+}  // namespace moe
+
+extern "C" int moe_ep_compaction(const int32_t* recv_cnt, const int32_t* hist, int W, int El, int E, int S,
+                                 int32_t* gather, int32_t* offsets, int32_t* overflow, hipStream_t stream) {
+  if (W < 1 || El < 1 || W * El > 1024 || S < 1 || E < 0) return fail("ep_compaction: need 1 <= W El <= 1024, S >= 1");
+  if (recv_cnt == nullptr || gather == nullptr || offsets == nullptr || (overflow != nullptr && hist == nullptr))
+    return fail("ep_compaction: NULL pointer");
+  ProfScope prof(stream, PROF_SCAN, 4.0 * W * El + 4.0 * (El + 1) + 4.0 * E);
+  MOE_LAUNCH(prof, ep_compaction_kernel, dim3(W * El), dim3(256), 0, stream, recv_cnt, hist, W, El, E, S, gather,
+             offsets, overflow);
+  return check_launch("moe_ep_compaction");
+}

@@ -60,9 +60,10 @@ struct FfnParams {
   const void* b2;           // [G][256] fp32 or bf16
   const int32_t* offsets;   // [G + 1]
   uint16_t* h;              // [rows][F]
-  uint16_t* yp;             // [rows][256]
+  uint16_t* yp;             // [yp_n][256]
+  const int32_t* yp_rows;   // routed row r -> Yp row yp_rows[r] (expert-parallel received layout), or nullptr
   int32_t* prof_rows;
-  int G, F, bias_bf16;
+  int G, F, bias_bf16, yp_n;
 };
 
 __device__ __forceinline__ void dma16(const void* src, char* lds) {
@@ -243,7 +244,7 @@ __device__ __forceinline__ float4 bias4(const char* lds, int col, int bf) {
 // both halves' sums are the same bits whichever wave adds.
 template <int WF>
 __device__ __forceinline__ void y_out(const f32x4 (&yacc)[2][16], char* smem, const char* lds_b2, int bias_bf16,
-                                      __amdgpu_buffer_rsrc_t yres, int wm, int lane) {
+                                      __amdgpu_buffer_rsrc_t yres, const int (&orow)[2], int wm, int lane) {
   constexpr int kRow = 128 * 4 + 16;  // padded fp32 row of one half (128 columns)
   const int lr = lane & 15, lg = lane >> 4;
   char* mine = smem + (wm * 2 + WF) * 32 * kRow;        // written by the other F half
@@ -256,7 +257,6 @@ __device__ __forceinline__ void y_out(const f32x4 (&yacc)[2][16], char* smem, co
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int rl = 32 * wm + 16 * i + lr;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       constexpr int base = 8 * WF;
@@ -267,7 +267,9 @@ __device__ __forceinline__ void y_out(const f32x4 (&yacc)[2][16], char* smem, co
       u32x2 o;
       o.x = pack2bf((a[0] + o4[0]) + b.x, (a[1] + o4[1]) + b.y);
       o.y = pack2bf((a[2] + o4[2]) + b.z, (a[3] + o4[3]) + b.w);
-      __builtin_amdgcn_raw_buffer_store_b64(o, yres, (rl * kFfD + col) * 2, 0, 0);
+      // (rows past the tile: an offset beyond the descriptor, dropped by the hardware)
+      const uint32_t off = orow[i] >= 0 ? ((uint32_t)orow[i] * kFfD + col) * 2u : 0xfffffff0u;
+      __builtin_amdgcn_raw_buffer_store_b64(o, yres, off, 0, 0);
     }
   }
 }
@@ -422,11 +424,17 @@ void expert_ffn_fwd_kernel(FfnParams p) {
   // ---- Y: sum the two F halves through LDS (ring memory), + b2, bf16 ----
   // (wf is wave-uniform but not a compile-time constant: one branch per half
   // keeps every accumulator index static, so yacc stays in registers)
+  int orow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rl = 32 * wm + 16 * i + lr;
+    orow[i] = rl < nrows ? (p.yp_rows != nullptr ? p.yp_rows[row0 + rl] : row0 + rl) : -1;
+  }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t yres =
-      __builtin_amdgcn_make_buffer_rsrc(p.yp + (size_t)row0 * kFfD, (short)0, nrows * kFfD * 2, 0x00020000);
-  if (wf == 0) y_out<0>(yacc, smem, lds_b2, p.bias_bf16, yres, wm, lane);
-  else y_out<1>(yacc, smem, lds_b2, p.bias_bf16, yres, wm, lane);
+      __builtin_amdgcn_make_buffer_rsrc(p.yp, (short)0, p.yp_n * kFfD * 2, 0x00020000);
+  if (wf == 0) y_out<0>(yacc, smem, lds_b2, p.bias_bf16, yres, orow, wm, lane);
+  else y_out<1>(yacc, smem, lds_b2, p.bias_bf16, yres, orow, wm, lane);
 }
 
 }  // namespace moe
@@ -439,12 +447,14 @@ extern "C" int moe_expert_ffn_supported(int G, int F, int d) {
 
 extern "C" int moe_expert_ffn_fwd(int dtype, const void* x, const int32_t* src_tok, const void* w1, const void* b1,
                                   const void* w2, const void* b2, const int32_t* offsets, int G, int max_rows, int F,
-                                  int d, void* h, void* yp, hipStream_t stream) {
+                                  int d, void* h, void* yp, const int32_t* yp_rows, int yp_n, hipStream_t stream) {
   const bool bias16 = (dtype & MOE_BIAS_BF16) != 0;
   if ((dtype & ~MOE_BIAS_BF16) != MOE_BF16) return fail("expert_ffn_fwd: only MOE_BF16 is implemented");
   if (!moe_expert_ffn_supported(G, F, d))
     return fail("expert_ffn_fwd: need d == 256, F % 128 == 0 in [128, 2048], 1 <= G <= 64");
   if (max_rows < 0) return fail("expert_ffn_fwd: max_rows < 0");
+  if (yp_rows == nullptr) yp_n = max_rows;
+  if (yp_n < 0 || (long long)yp_n * d * 2 > 0x7fffffffLL) return fail("expert_ffn_fwd: bad yp_n");
   if (x == nullptr || w1 == nullptr || b1 == nullptr || w2 == nullptr || b2 == nullptr || offsets == nullptr ||
       (max_rows > 0 && (h == nullptr || yp == nullptr)))
     return fail("expert_ffn_fwd: NULL pointer");
@@ -461,6 +471,8 @@ extern "C" int moe_expert_ffn_fwd(int dtype, const void* x, const int32_t* src_t
   p.offsets = offsets;
   p.h = static_cast<uint16_t*>(h);
   p.yp = static_cast<uint16_t*>(yp);
+  p.yp_rows = yp_rows;
+  p.yp_n = yp_n;
   p.G = G;
   p.F = F;
   p.bias_bf16 = bias16 ? 1 : 0;

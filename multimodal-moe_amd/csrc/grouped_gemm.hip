@@ -92,6 +92,10 @@ struct GemmParams {
   // (a dense linear layer's weight gradient; no device offsets to load)
   int dense_rows;
   int bias_bf16;  // ROWS bias epilogues: bias is bf16 [G][N] (the bf16 parameter itself, no fp32 copy)
+  // ROWS: output row r is stored at C row c_rows[r] (the expert-parallel
+  // received layout, src/moe/ep.py) instead of row r; nullptr = identity.
+  // The epilogue's mask operand (aux) stays indexed by r.
+  const int32_t* c_rows;
 };
 
 // runtime tuning knobs (moe_set_tuning)
@@ -340,6 +344,7 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int g, int row0, i
       const int ml = wm * (BM / 2) + 16 * i + lm;
       if (ml >= a_row_lim) continue;
       const size_t row = (size_t)row0 + ml;
+      const size_t crow = p.c_rows != nullptr ? (size_t)p.c_rows[row] : row;
       const float rs = p.row_scale != nullptr ? p.row_scale[row] : 1.f;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -363,7 +368,7 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int g, int row0, i
         uint2 o;
         o.x = pack2bf(v[0], v[1]);
         o.y = pack2bf(v[2], v[3]);
-        if (!(p.dbg & 1)) *reinterpret_cast<uint2*>(C + row * p.ldc + n) = o;
+        if (!(p.dbg & 1)) *reinterpret_cast<uint2*>(C + crow * p.ldc + n) = o;
       }
     }
   } else {
@@ -470,6 +475,7 @@ __device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row
       if (r >= a_row_lim) continue;
       uint4 v = *reinterpret_cast<const uint4*>(smem + r * (BN * 2) + ((c ^ (r & (CPR - 1))) << 4));
       const size_t gofs = ((size_t)row0 + r) * p.ldc + n0 + c * 8;
+      const size_t cofs = p.c_rows != nullptr ? (size_t)p.c_rows[row0 + r] * p.ldc + n0 + c * 8 : gofs;
       if constexpr (EPI == MOE_EPI_RELU_MASK && (FL & FL_AUX8)) {  // e4m3 activation: keep where byte > +0
         const uint2 h = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(p.aux) + gofs);
         uint32_t vw[4] = {v.x, v.y, v.z, v.w};
@@ -501,11 +507,11 @@ __device__ __forceinline__ void epilogue_lds(const GemmParams& p, int g, int row
         int e;
         const uint2 o = mx_quant_chunk(v, e);
         if (!(p.dbg & 1)) {
-          *reinterpret_cast<uint2*>(static_cast<uint8_t*>(p.c) + gofs) = o;
-          if ((c & 3) == 0) p.cs[((size_t)row0 + r) * (p.ldc / 32) + (n0 + c * 8) / 32] = (uint8_t)(e + 127);
+          *reinterpret_cast<uint2*>(static_cast<uint8_t*>(p.c) + cofs) = o;
+          if ((c & 3) == 0) p.cs[cofs / 32] = (uint8_t)(e + 127);
         }
       } else {
-        if (!(p.dbg & 1)) *reinterpret_cast<uint4*>(C + gofs) = v;
+        if (!(p.dbg & 1)) *reinterpret_cast<uint4*>(C + cofs) = v;
       }
     }
   } else {
@@ -1810,17 +1816,19 @@ extern "C" int rtdetr_linear_wgrad_batch(int n, const void* const* gy, const voi
   return check_launch("rtdetr_linear_wgrad_batch");
 }
 
-extern "C" int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather, const float* row_scale,
-                                         const void* b, void* c, const int32_t* offsets, int G, int max_rows, int N,
-                                         int K, int epilogue, const void* aux, const void* wx,
-                                         const int32_t* wx_gather, const float* wx_scale, const void* wy,
-                                         const int32_t* wy_gather, void* wc, void* wcolsum, int M2, int N2,
-                                         int out_bf16, hipStream_t stream) {
+extern "C" int moe_grouped_gemm_bwd_pair_scatter(const void* a, const int32_t* a_gather, const float* row_scale,
+                                                 const void* b, void* c, const int32_t* c_rows,
+                                                 const int32_t* offsets, int G, int max_rows, int N, int K,
+                                                 int epilogue, const void* aux, const void* wx,
+                                                 const int32_t* wx_gather, const float* wx_scale, const void* wy,
+                                                 const int32_t* wy_gather, void* wc, void* wcolsum, int M2, int N2,
+                                                 int out_bf16, hipStream_t stream) {
   RowsPlan r;
   WgradPlan w;
   WsWin win = device_ws();
   if (plan_rows(r, a, b, c, offsets, G, max_rows, N, K, 0, epilogue, nullptr, aux, a_gather, win, row_scale))
     return -1;
+  r.p.c_rows = c_rows;
   if (wc == nullptr) {  // dgrad only (the caller computes the weight gradient elsewhere)
     if (wcolsum != nullptr) return fail("grouped_gemm_bwd_pair: wcolsum without wc");
     if (max_rows == 0) return 0;
@@ -1855,6 +1863,17 @@ extern "C" int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather,
   r.p.prof_rows = prof.rows_slot();
   launch_pair<0>(r, w, stream, prof);
   return check_launch("moe_grouped_gemm_bwd_pair");
+}
+
+extern "C" int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather, const float* row_scale,
+                                         const void* b, void* c, const int32_t* offsets, int G, int max_rows, int N,
+                                         int K, int epilogue, const void* aux, const void* wx,
+                                         const int32_t* wx_gather, const float* wx_scale, const void* wy,
+                                         const int32_t* wy_gather, void* wc, void* wcolsum, int M2, int N2,
+                                         int out_bf16, hipStream_t stream) {
+  return moe_grouped_gemm_bwd_pair_scatter(a, a_gather, row_scale, b, c, nullptr, offsets, G, max_rows, N, K,
+                                           epilogue, aux, wx, wx_gather, wx_scale, wy, wy_gather, wc, wcolsum, M2,
+                                           N2, out_bf16, stream);
 }
 
 // ---------------------------------------------------------------------------

@@ -47,7 +47,10 @@ SIGNATURES = {
     "moe_route_dispatch": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P]),
     "moe_grouped_gemm_gather": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "moe_expert_ffn_supported": (_I, [_I, _I, _I]),
-    "moe_expert_ffn_fwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "moe_expert_ffn_fwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _P]),
+    "moe_ep_compaction": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "moe_grouped_gemm_bwd_pair_scatter": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P,
+                                               _P, _P, _P, _I, _I, _I, _P]),
     "moe_grouped_gemm_wgrad_gather": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "moe_grouped_gemm_bwd_pair": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                        _I, _I, _I, _P]),
@@ -481,11 +484,13 @@ def expert_ffn_supported(G, F, d):
     return bool(lib().moe_expert_ffn_supported(int(G), int(F), int(d)))
 
 
-def expert_ffn_fwd(x, src_tok, w1, b1, w2, b2, offsets, G, max_rows):
+def expert_ffn_fwd(x, src_tok, w1, b1, w2, b2, offsets, G, max_rows, yp_rows=None, yp_n=0):
     """One launch (moe_expert_ffn_fwd): h = relu(x[src_tok[r]] W1_g^T + b1_g),
     yp = h W2_g^T + b2_g for every routed row r (src_tok None: x holds the
     routed rows).  w1 bf16 [G, F, d], w2 bf16 [G, d, F]; b1 / b2 fp32 or bf16
-    (both the same).  -> (h bf16 [rows, F], yp bf16 [rows, d])."""
+    (both the same).  yp_rows (int32): routed row r is stored at row
+    yp_rows[r] of a yp_n-row yp (the EP received layout; unmapped rows are
+    left uninitialised).  -> (h bf16 [rows, F], yp bf16 [rows or yp_n, d])."""
     _need(x, torch.bfloat16, "x")
     _need(w1, torch.bfloat16, "w1")
     _need(w2, torch.bfloat16, "w2")
@@ -498,17 +503,39 @@ def expert_ffn_fwd(x, src_tok, w1, b1, w2, b2, offsets, G, max_rows):
         raise MoEKernelError("expert_ffn_fwd: b1 / b2 must both be fp32 or both bf16")
     if src_tok is not None and src_tok.numel() < max_rows:
         raise MoEKernelError("expert_ffn_fwd: src_tok shorter than max_rows")
+    if yp_rows is not None:
+        _need(yp_rows, torch.int32, "yp_rows")
+        if yp_rows.numel() < max_rows:
+            raise MoEKernelError("expert_ffn_fwd: yp_rows shorter than max_rows")
     h = torch.empty((max(max_rows, 1), F), dtype=torch.bfloat16, device=x.device)
-    yp = torch.empty((max(max_rows, 1), d), dtype=torch.bfloat16, device=x.device)
+    n_out = int(yp_n) if yp_rows is not None else max(max_rows, 1)
+    yp = torch.empty((max(n_out, 1), d), dtype=torch.bfloat16, device=x.device)
     dt = MOE_BF16 | (MOE_BIAS_BF16 if b1.dtype == torch.bfloat16 else 0)
     _check(lib().moe_expert_ffn_fwd(dt, _ptr(x), _ptr(src_tok), _ptr(w1), _ptr(b1.contiguous()),
                                     _ptr(w2), _ptr(b2.contiguous()), _ptr(offsets), G, int(max_rows), F, d,
-                                    _ptr(h), _ptr(yp), _stream()), "moe_expert_ffn_fwd")
+                                    _ptr(h), _ptr(yp), _ptr(yp_rows), n_out, _stream()), "moe_expert_ffn_fwd")
     return h, yp
 
 
+def ep_compaction(recv_cnt, hist, S):
+    """recv_cnt int32 [W, El] (rows received per source and local expert,
+    capped at S), hist int32 [E] (this rank's send histogram) -> (gather
+    int32 [W El S], offsets int32 [El + 1], overflow int32 [1]) in one launch
+    (moe_ep_compaction)."""
+    _need(recv_cnt, torch.int32, "recv_cnt")
+    _need(hist, torch.int32, "hist")
+    W, El = recv_cnt.shape
+    gather = torch.zeros(W * El * S, dtype=torch.int32, device=recv_cnt.device)
+    offsets = torch.empty(El + 1, dtype=torch.int32, device=recv_cnt.device)
+    overflow = torch.empty(1, dtype=torch.int32, device=recv_cnt.device)
+    _check(lib().moe_ep_compaction(_ptr(recv_cnt), _ptr(hist), W, El, hist.numel(), int(S), _ptr(gather),
+                                   _ptr(offsets), _ptr(overflow), _stream()), "moe_ep_compaction")
+    return gather, offsets, overflow
+
+
 def grouped_gemm_bwd_pair(a, b, offsets, G, max_rows, N, K, epilogue, aux, wx, wy, wy_gather=None,
-                          out_dtype=torch.bfloat16, a_gather=None, row_scale=None, wx_gather=None, wx_scale=None):
+                          out_dtype=torch.bfloat16, a_gather=None, row_scale=None, wx_gather=None, wx_scale=None,
+                          c_rows=None, c_n=0):
     """One launch: C = epi(s_r A(r) . B_g) (dgrad, B stored [K][N] per group;
     A(r) = a[a_gather[r]] when given, s_r = row_scale[r]) and the weight
     gradient WC_g = WX_g^T WY_g with colsum (WX(r) = bf16(wx_scale[r] *
@@ -532,14 +559,20 @@ def grouped_gemm_bwd_pair(a, b, offsets, G, max_rows, N, K, epilogue, aux, wx, w
     if (wy_gather is None and wy.shape[0] < max_rows) or (wx_gather is None and wx.shape[0] < max_rows):
         raise MoEKernelError("grouped_gemm_bwd_pair: wgrad shapes")
     rows_out = max(max_rows, 1) if a_gather is not None else a.shape[0]
+    if c_rows is not None:  # dgrad row r lands at C row c_rows[r] of a c_n-row C (the rest uninitialised)
+        _need(c_rows, torch.int32, "c_rows")
+        if c_rows.numel() < max_rows:
+            raise MoEKernelError("grouped_gemm_bwd_pair: c_rows shorter than max_rows")
+        rows_out = max(int(c_n), 1)
     c = torch.empty((rows_out, N), dtype=torch.bfloat16, device=a.device)
     wc = torch.empty((G, M2, N2), dtype=out_dtype, device=a.device)
     cs = torch.empty((G, M2), dtype=out_dtype, device=a.device)
     ensure_splitk_workspace(a.device)
-    _check(lib().moe_grouped_gemm_bwd_pair(_ptr(a), _ptr(a_gather), _ptr(row_scale), _ptr(b), _ptr(c), _ptr(offsets),
-                                           G, int(max_rows), N, K, int(epilogue), _ptr(aux), _ptr(wx),
-                                           _ptr(wx_gather), _ptr(wx_scale), _ptr(wy), _ptr(wy_gather), _ptr(wc),
-                                           _ptr(cs), M2, N2, int(out_dtype == torch.bfloat16), _stream()),
+    _check(lib().moe_grouped_gemm_bwd_pair_scatter(_ptr(a), _ptr(a_gather), _ptr(row_scale), _ptr(b), _ptr(c),
+                                                   _ptr(c_rows), _ptr(offsets), G, int(max_rows), N, K,
+                                                   int(epilogue), _ptr(aux), _ptr(wx), _ptr(wx_gather),
+                                                   _ptr(wx_scale), _ptr(wy), _ptr(wy_gather), _ptr(wc), _ptr(cs), M2,
+                                                   N2, int(out_dtype == torch.bfloat16), _stream()),
            "moe_grouped_gemm_bwd_pair")
     return c, wc, cs
 

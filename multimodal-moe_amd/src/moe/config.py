@@ -34,10 +34,12 @@ class MoEConfig:
     expert_parallel: bool = False  # route through ep.py (set by an -ep<n> spec token, n >= 1)
     # rows each rank may send to one expert in the fixed-capacity all-to-all, as
     # a factor of the mean T k / E (layers with capacity_factor > 0 use their
-    # own capacity instead).  0 (default) = lossless: T slots, the worst case,
-    # so the EP layer equals the single-process layer; an explicit -epcf<f>
-    # spec token opts into smaller exchanges that drop (and count) overflow
-    ep_capacity_factor: float = 0.0
+    # own capacity instead).  2.0 (default): each all-to-all carries 2x the
+    # mean rows (SURVEY 8(e)'s budget); assignments beyond it are dropped like
+    # capacity drops and counted (MoEFFN.last_ep_overflow, bench ep_overflow).
+    # 0 (spec token -epcf0) = lossless: T slots, the worst case, so the EP
+    # layer equals the single-process layer (8x the bytes at C4)
+    ep_capacity_factor: float = 2.0
     router_init_std: float = 0.02
     ctx_init_scale: float = 0.5
 

@@ -8,8 +8,9 @@ the flat all-reduce of TrainStep).
 
 The exchange is FIXED-CAPACITY: every (source rank, expert) pair owns S rows
 of the all-to-all buffers (S = ``MoEConfig.ep_slot_rows(T)``: the layer's
-capacity when it has one, else T -- lossless, the default -- or, with an
-explicit ep_capacity_factor f > 0, ceil(f T k / E)), so every split size is
+capacity when it has one, else ceil(f T k / E) with f = ep_capacity_factor,
+2.0 by default (every all-to-all then carries 2x the mean rows), or T --
+lossless, the worst case -- with ``-epcf0``), so every split size is
 static and nothing about the routing is read on the host.  Per MoE layer:
 
   route + dispatch      router + scan + permute into the padded send layout:
@@ -19,12 +20,16 @@ static and nothing about the routing is read on the host.  Per MoE layer:
                         so nothing changes)
   counts exchange       all_to_all of the kept counts [W, E/W] (device ints)
   dispatch a2a          all_to_all_single of the [E S, d] rows, equal splits
-  compaction map        on the device from the received counts: compact
-                        expert-major row -> received row (``gather``), its
-                        inverse (``inv``) and the local expert offsets
-  expert FFN            grouped GEMM1 reads the received rows through
-                        ``gather`` (no compaction copy), GEMM2; the output is
-                        put back in the received layout (one row gather)
+  compaction map        on the device from the received counts, ONE HIP
+                        launch (moe_ep_compaction): compact expert-major row
+                        -> received row (``gather``), the local expert offsets
+                        and this rank's overflow count
+  expert FFN            the fused expert FFN reads the received rows through
+                        ``gather`` (no compaction copy) and writes each output
+                        row straight back to its received row (no row-gather
+                        pass); the backward's dXp lands the same way
+                        (torch index maps + two-launch GEMMs remain for the
+                        MXFP8 experts and the CPU path)
   combine a2a           the reverse all_to_all_single, then the gate-weighted
                         combine at the padded positions
 Backward mirrors it; the transposes of the two row maps are the maps
@@ -165,6 +170,64 @@ class _EPExpertFFN(torch.autograd.Function):
         return dxe.index_select(0, inv).to(xdtype), None, None, dW1, db1, dW2, db2, None, None
 
 
+class _EPExpertFFNScatter(torch.autograd.Function):
+    """The local experts over the received rows, in the received layout, with
+    no row-gather passes: the fused expert FFN (moe_expert_ffn_fwd) reads
+    received row gather[r] for compact row r and writes its output row back
+    to received row gather[r]; the backward's first paired launch reads dYp =
+    dyr[gather] inside the GEMMs, the second gathers xr[gather] for dW1 and
+    stores dXp row r at received row gather[r] (moe_grouped_gemm_bwd_pair_
+    scatter).  Received rows no expert row maps to (the slots' padding) are
+    left uninitialised both ways: no one reads them (the sender's combine and
+    token backward read kept positions only)."""
+
+    @staticmethod
+    def forward(ctx, xr, gather, w1, b1, w2, b2, offsets, grad_scale):
+        from . import _lib as L
+        from .ops import _bias
+
+        G, F, d = w1.shape
+        R = xr.shape[0]
+        xb = xr.to(torch.bfloat16).contiguous()
+        w1b = w1.to(torch.bfloat16).contiguous()
+        w2b = w2.to(torch.bfloat16).contiguous()
+        h, yr = L.expert_ffn_fwd(xb, gather, w1b, _bias(b1), w2b, _bias(b2), offsets, G, R, yp_rows=gather, yp_n=R)
+        ctx.save_for_backward(xb, gather, h, w1b, w2b, offsets)
+        ctx.meta = (G, R, float(grad_scale), xr.dtype)
+        ctx.wdtype = w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32
+        return yr
+
+    @staticmethod
+    def backward(ctx, dyr):
+        from . import _lib as L
+
+        xb, gather, h, w1b, w2b, offsets = ctx.saved_tensors
+        G, R, s, xdtype = ctx.meta
+        F, d = w1b.shape[1], w1b.shape[2]
+        odt = torch.bfloat16 if ctx.wdtype == torch.bfloat16 else torch.float32
+        dyb = dyr.to(torch.bfloat16).contiguous()
+        dh, dW2, db2 = L.grouped_gemm_bwd_pair(dyb, w2b, offsets, G, R, F, d, L.EPI_RELU_MASK, h, dyb, h,
+                                               out_dtype=odt, a_gather=gather, wx_gather=gather)
+        dxr, dW1, db1 = L.grouped_gemm_bwd_pair(dh, w1b, offsets, G, R, d, F, L.EPI_NONE, None, dh, xb, gather,
+                                                out_dtype=odt, c_rows=gather, c_n=R)
+        if s != 1.0:
+            for t in (dW1, db1, dW2, db2):
+                t.mul_(s)
+        return dxr.to(xdtype), None, dW1, db1, dW2, db2, None, None
+
+
+def _fused_ep_ok(layer, x, fp8):
+    """The HIP receive path (moe_ep_compaction + the scattering fused FFN):
+    bf16 experts of a shape the fused FFN takes (ops.MOE_FUSED_FFN on)."""
+    if not x.is_cuda or fp8:
+        return False
+    from . import _lib as L
+    from .ops import _FUSED_FFN
+
+    G, F, d = layer.w1.shape
+    return _FUSED_FFN and L.expert_ffn_supported(G, F, d)
+
+
 class _CarrierExchange(torch.autograd.Function):
     """MXFP8 path: the routed rows cross as e4m3 + exponents (non-differentiable
     uint8); this node stands for them in the autograd graph.  Forward: a
@@ -232,6 +295,7 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap):
     fp8 = cfg.expert_dtype == "fp8"
     gs = getattr(layer, "ep_grad_scale", 1.0 / W)  # 1.0 when the optimizer applies 1/W (graph-mode TrainStep)
     if x.is_cuda:
+        from . import _lib as L
         from .ops import aux_losses, combine_hip as combine
         from .ops import expert_ffn_mx_hip, route_dispatch_hip, route_dispatch_mx_hip
 
@@ -247,6 +311,17 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap):
 
         xp, w, lb, z, pos, hist = _route_padded_eager(x, layer.wg, ctx_bias, ctx_img, tokens_per_image, k,
                                                       cfg.normalize, S)
+    if _fused_ep_ok(layer, x, fp8):
+        # counts exchange (int32), then the receive map, the local expert
+        # offsets and this rank's overflow in ONE launch (moe_ep_compaction)
+        kept = hist.clamp(max=S).view(W, El).contiguous()
+        recv_cnt = _a2a(torch.empty_like(kept), kept, group, W)
+        gather, offs, overflow = L.ep_compaction(recv_cnt, hist, S)
+        layer.last_ep_overflow = overflow[0] if cap <= 0 else None
+        xr = _Exchange.apply(xp, group, W)
+        yr = _EPExpertFFNScatter.apply(xr, gather, layer.w1, layer.b1, layer.w2, layer.b2, offs, gs)
+        yp = _Exchange.apply(yr, group, W)
+        return combine(yp, w, pos, T), lb, z, hist
     recv_cnt = _exchange_counts(hist.clamp(max=S).view(W, El), group, W)
     gather, inv, offs = compaction_map(recv_cnt, S)
     layer.last_ep_overflow = (hist.to(torch.int64) - S).clamp(min=0).sum() if cap <= 0 else None

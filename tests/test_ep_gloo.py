@@ -133,8 +133,10 @@ def test_compaction_map_is_a_bijection_on_valid_rows():
 def test_ep_slot_rows():
     from src.moe.config import MoEConfig, parse_moe_spec
 
-    assert MoEConfig(num_experts=16, top_k=2).ep_slot_rows(7360) == 7360  # default: lossless (T slots)
-    assert parse_moe_spec("rtdetr-r50-moe16-top2-ep1").moe.ep_slot_rows(2400) == 2400
+    assert MoEConfig(num_experts=16, top_k=2).ep_slot_rows(7360) == 1840  # default: 2x the mean rows
+    assert MoEConfig(num_experts=16, top_k=2, ep_capacity_factor=0.0).ep_slot_rows(7360) == 7360  # lossless
+    assert parse_moe_spec("rtdetr-r50-moe16-top2-ep1-epcf0").moe.ep_slot_rows(7360) == 7360
+    assert parse_moe_spec("rtdetr-r50-moe16-top2-ep1").moe.ep_slot_rows(2400) == 600
     c = MoEConfig(num_experts=16, top_k=2, ep_capacity_factor=2.0)
     assert c.ep_slot_rows(7360) == 1840        # 2 x mean 920
     c.ep_capacity_factor = 8.0                 # f k >= E: worst case, T

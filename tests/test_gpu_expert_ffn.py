@@ -115,3 +115,58 @@ def test_expert_ffn_rejects_bad_shapes(hip_lib):
     with pytest.raises(L.MoEKernelError):
         L.expert_ffn_fwd(x, None, w1, torch.zeros(2, 1024, device=DEV), w2,
                          torch.zeros(2, 256, device=DEV, dtype=torch.bfloat16), off, 2, 4)
+
+
+@pytest.mark.parametrize("W,El,S", [(1, 16, 1840), (4, 2, 37), (8, 4, 5), (2, 1, 1)])
+def test_ep_compaction_matches_torch_map(hip_lib, W, El, S):
+    """moe_ep_compaction == ep.compaction_map (the torch index chain it
+    replaces) on random received counts, incl. counts above S (capped)."""
+    from src.moe import _lib as L
+    from src.moe.ep import compaction_map
+
+    g = torch.Generator().manual_seed(W * 100 + El)
+    cnt = torch.randint(0, S + 3, (W, El), generator=g).int()
+    E = W * El
+    hist = torch.randint(0, 2 * S + 1, (E,), generator=g).int()
+    gather, offs, ovf = L.ep_compaction(cnt.to(DEV), hist.to(DEV), S)
+    g_ref, _inv, o_ref = compaction_map(cnt.clamp(max=S).to(torch.int64), S)
+    torch.cuda.synchronize()
+    n = int(o_ref[-1])
+    assert torch.equal(offs.cpu(), o_ref.int())
+    assert torch.equal(gather[:n].cpu(), g_ref[:n].cpu())
+    assert int(ovf[0]) == int((hist - S).clamp(min=0).sum())
+
+
+@pytest.mark.parametrize("rows_per_group", [[0, 1, 63, 64, 65, 200, 0, 130], [1500, 40, 0, 1100]])
+def test_scatter_outputs_match_gather_after(hip_lib, rows_per_group):
+    """Output-row scatter (EP received layout): the fused FFN's Yp and the
+    paired dgrad's C written through c_rows equal the unscattered outputs
+    moved by index, bit for bit."""
+    from src.moe import _lib as L
+
+    rng = np.random.default_rng(9)
+    G, d, F = len(rows_per_group), 256, 1024
+    offsets = np.concatenate([[0], np.cumsum(rows_per_group)]).astype(np.int32)
+    R = int(offsets[-1])
+    n_out = 2 * R + 16
+    rows = torch.from_numpy(rng.permutation(n_out)[:R].astype(np.int32)).to(DEV)
+    x = _ints(rng, (n_out, d), -2, 3).to(torch.bfloat16).to(DEV)
+    w1 = _ints(rng, (G, F, d), -1, 2).to(torch.bfloat16).to(DEV)
+    w2 = _ints(rng, (G, d, F), -1, 2).to(torch.bfloat16).to(DEV)
+    b1 = _ints(rng, (G, F), -8, 9).to(DEV)
+    b2 = _ints(rng, (G, d), -8, 9).to(DEV)
+    off = torch.from_numpy(offsets).to(DEV)
+    h, ys = L.expert_ffn_fwd(x, rows, w1, b1, w2, b2, off, G, R, yp_rows=rows, yp_n=n_out)
+    h2, y2 = L.expert_ffn_fwd(x, rows, w1, b1, w2, b2, off, G, R)
+    dy = _ints(rng, (n_out, d), -2, 3).to(torch.bfloat16).to(DEV)
+    dh, _, _ = L.grouped_gemm_bwd_pair(dy, w2, off, G, R, F, d, L.EPI_RELU_MASK, h, dy, h, a_gather=rows,
+                                       wx_gather=rows)
+    dxs, _, _ = L.grouped_gemm_bwd_pair(dh, w1, off, G, R, d, F, L.EPI_NONE, None, dh, x, rows, c_rows=rows,
+                                        c_n=n_out)
+    dx2, _, _ = L.grouped_gemm_bwd_pair(dh, w1, off, G, R, d, F, L.EPI_NONE, None, dh, x, rows)
+    torch.cuda.synchronize()
+    assert torch.equal(h, h2)
+    idx = rows.long()
+    assert ys.shape == (n_out, d) and dxs.shape == (n_out, d)
+    assert torch.equal(ys[idx], y2[:R])
+    assert torch.equal(dxs[idx], dx2[:R])
