@@ -310,6 +310,35 @@ def build_model(spec, device, world):
     return model
 
 
+def expert_parallel_stats(model, spec, world):
+    """C4 exchange accounting of the last step (rank-local): the slot rows S
+    per (source, expert), the bytes of one all-to-all per MoE layer (E S d bf16
+    rows: the fixed-capacity buffer; (W-1)/W of it leaves the rank), and the
+    assignments the fixed-capacity exchange dropped (ep_overflow), against
+    SURVEY 8(e)'s lossless-exchange budget A (W-1)/W 512 B per direction."""
+    layers = [m for m in model.moe_layers() if getattr(m, "last_tokens", 0)]
+    if not layers:
+        return None
+    cfg = layers[0].cfg
+    per_layer, over, assign, a2a = [], 0, 0, 0.0
+    for m in layers:
+        T = m.last_tokens
+        S = cfg.ep_slot_rows(T)
+        b = cfg.num_experts * S * m.d_model * 2
+        ov = int(m.last_ep_overflow) if m.last_ep_overflow is not None else 0
+        over += ov
+        assign += T * cfg.top_k
+        a2a += 4 * b  # forward dispatch + combine, backward both transposes
+        per_layer.append({"T": T, "slots": S, "bytes_per_a2a": b,
+                          "survey_bytes_per_a2a": round(T * cfg.top_k * 512 * (max(world, 8) - 1) / max(world, 8)),
+                          "overflow": ov})
+    return {"slot_factor": cfg.ep_capacity_factor if cfg.ep_capacity_factor > 0 else "lossless",
+            "ep_overflow": over, "assignments": assign, "overflow_frac": round(over / max(assign, 1), 5),
+            "a2a_bytes_per_step_per_rank": round(a2a), "layers": per_layer,
+            "note": "survey_bytes_per_a2a: SURVEY 8(e)'s off-rank bytes of a lossless exchange at W=8; "
+                    "bytes_per_a2a: this build's fixed-capacity buffer (its (W-1)/W leaves the rank)"}
+
+
 def host_threads():
     """(threads used, CPUs in this process's affinity set): the affinity set,
     capped by OMP_NUM_THREADS when the box sets it (the GPU box exports the
@@ -483,6 +512,7 @@ def main():
     elapsed = float(el.item())
     ksum = L.TIMER.summary() if timing else {}
 
+    ep_stats = expert_parallel_stats(model, spec, world) if "-ep" in spec else None
     result = None
     if rank == 0:
         images_total = world * batch * args.steps
@@ -535,6 +565,7 @@ def main():
                 f"libmoe_hip dispatch-stamped events over {args.profile_steps} eager steps right after the "
                 f"timed region (same shapes; the timed steps replay hipGraphs, which carry no timing events)"),
             **({"phases_gpu_host_ms": phases} if phases else {}),
+            **({"expert_parallel": ep_stats} if ep_stats else {}),
         }
     if world > 1:
         dist.barrier()

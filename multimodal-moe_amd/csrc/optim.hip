@@ -26,7 +26,7 @@ struct OptTensor {        // 48 B, mirrored by src/rtdetr_moe/optim.py
   long long moff;         // offset of the tensor in the flat master / moment buffers (multiple of 8)
   int gdtype;             // 0 bf16, 1 fp32, 2 no gradient this step (tensor skipped, as torch.optim does)
   int group;              // lr group
-  int pad0, pad1;
+  float* hi_out;          // fp32 weight to write (a sharded master's parameter), or nullptr
 };
 static_assert(sizeof(OptTensor) == 48, "OptTensor layout");
 
@@ -209,6 +209,11 @@ __global__ __launch_bounds__(256) void adamw_step_kernel(const OptTensor* __rest
       o.w = pack2bf(p[6], p[7]);
       *reinterpret_cast<uint4*>(t.lowp + e) = o;
     }
+    if (t.hi_out != nullptr) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        reinterpret_cast<float4*>(t.hi_out + e)[h] = make_float4(p[4 * h], p[4 * h + 1], p[4 * h + 2], p[4 * h + 3]);
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -217,6 +222,7 @@ __global__ __launch_bounds__(256) void adamw_step_kernel(const OptTensor* __rest
         m1[i] = v1[i];
         m2[i] = v2[i];
         if (t.lowp != nullptr) t.lowp[e + i] = f2bf(p[i]);
+        if (t.hi_out != nullptr) t.hi_out[e + i] = p[i];
       }
     }
   }

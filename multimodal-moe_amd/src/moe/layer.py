@@ -53,6 +53,7 @@ class MoEFFN(nn.Module):
         self.last_aux_weighted = None  # lb_coef lb + z_coef z (GPU path: fused kernel, differentiable)
         self.last_hist = None  # int32 [E] expert histogram of the last forward
         self.last_ep_overflow = None  # EP without capacity: assignments beyond the a2a slots (device)
+        self.last_tokens = 0   # T of the last forward (bench: EP exchange bytes)
 
     def forward(self, x: torch.Tensor, ctx_img: torch.Tensor | None, residual: bool = False) -> torch.Tensor:
         """x [B, L, d] (image-major tokens), ctx_img int [B] -> [B, L, d].
@@ -62,6 +63,7 @@ class MoEFFN(nn.Module):
         cfg = self.cfg
         flat = x.reshape(B * L, d)
         T = B * L
+        self.last_tokens = T
         cap = cfg.capacity(T)
         cb = self.ctx_bias if (self.ctx_bias is not None and ctx_img is not None) else None
         ci = ctx_img.to(torch.int32).contiguous() if cb is not None else None

@@ -359,7 +359,9 @@ def _train_worker(a: TrainArgs, rank: int, world: int, local: int | str) -> Trai
         if rank == 0 or ep:
             metrics = _evaluate(core, a.data, "val", a.imgsz, a.batch, device, a.workers, a.seed)
         # checkpoint state: fp32 masters; expert shards gathered to [E, ...] (collective)
-        sd = gather_expert_shards(core, _master_state_dict(core, step)) if (rank == 0 or ep) else None
+        # (a sharded data-parallel optimizer gathers masters collectively: every rank joins)
+        collective = ep or getattr(getattr(step, "opt", None), "W", 1) > 1
+        sd = gather_expert_shards(core, _master_state_dict(core, step)) if (rank == 0 or collective) else None
         if rank == 0:
             last_metrics = metrics
             fit = _results_dict(metrics)["fitness"]

@@ -10,9 +10,10 @@ computes torch.autograd.grad of the forward outputs w.r.t. every trainable
 parameter into static gradient buffers that the optimizer reads directly (no
 per-parameter AccumulateGrad copies).  What stays eager: the Hungarian
 matching (host linear_sum_assignment, one device->host copy of all cost
-matrices), the batched set criterion, the gradient all-reduce (one flat RCCL
-all_reduce over xGMI when world > 1), gradient clipping and the fused AdamW
-update.
+matrices), the batched set criterion, and the optimizer: when world > 1
+the data-parallel reduction (one fp32 reduce-scatter over RCCL, AdamW on this
+rank's slice, one all-gather of the weights: optim.ShardedDPAdamW), gradient
+clipping and the fused AdamW update.
 
 The captured forward keeps the MoE aux losses as an explicit graph output so
 their gradients reach the router through the captured backward.
@@ -30,6 +31,9 @@ from .linear import TokenSelfAttention, deferred_weight_grads, merge_deferred
 from .model import RTDETRMoE
 
 _FUSED_CRIT = os.environ.get("MOE_FUSED_CRITERION", "1") != "0"  # A/B switch
+# MOE_ZERO=0: GPU data parallelism through the flat fp32 all-reduce + replicated
+# FlatAdamW (optim.DPGradReducer) instead of the sharded optimizer (A/B switch)
+_ZERO = os.environ.get("MOE_ZERO", "1") != "0"
 
 
 class FlatOutputs(nn.Module):
@@ -327,10 +331,18 @@ class TrainStep:
             # their master segment -- before any graph capture bakes addresses.
             # Expert-parallel shards enter the clip norm through a sum over the
             # EP group (the same global norm on every rank)
-            from .optim import FlatAdamW
+            from .optim import FlatAdamW, ShardedDPAdamW
 
-            self.opt = FlatAdamW([(bb, lr_backbone), (rest, lr)], weight_decay=weight_decay, clip_norm=clip_norm,
-                                 sharded=self.ep_params, shard_group=self.ep_group)
+            if world > 1 and _ZERO:
+                # C3 data parallelism: reduce-scatter of the fp32 gradients,
+                # AdamW on this rank's 1/world slice, all-gather of the weights
+                # (optim.ShardedDPAdamW); the replicated parameters become views
+                # of its flat spaces here, before any graph capture
+                self.opt = ShardedDPAdamW([(bb, lr_backbone), (rest, lr)], weight_decay=weight_decay,
+                                          clip_norm=clip_norm, sharded=self.ep_params)
+            else:
+                self.opt = FlatAdamW([(bb, lr_backbone), (rest, lr)], weight_decay=weight_decay,
+                                     clip_norm=clip_norm, sharded=self.ep_params, shard_group=self.ep_group)
             self.opt_params = None
         else:
             self.opt_params = bb + rest
@@ -339,19 +351,20 @@ class TrainStep:
         self.flat = FlatOutputs(model)
         self.reducer = None
         if world > 1 and images.is_cuda:
-            # GPU data parallelism (graph or eager): the replicated gradients are
-            # summed in fp32 by ONE all-reduce after the backward
-            # (optim.DPGradReducer) and the optimizer applies 1/world to EVERY
-            # gradient (FlatAdamW inv_world); expert-parallel weights are not
-            # all-reduced (their gradients already hold every rank's tokens), so
-            # their layers must not pre-scale by 1/world
             from ..moe.layer import MoEFFN
-            from .optim import DPGradReducer
 
-            self.reducer = DPGradReducer(self.dp_params)
+            # expert-parallel weights are not reduced (their gradients already
+            # hold every rank's tokens), so their layers must not pre-scale by
+            # 1/world: the optimizer applies 1/world to every gradient
             for m in model.modules():
                 if isinstance(m, MoEFFN) and m.ep_size > 1:
                     m.ep_grad_scale = 1.0
+        if world > 1 and images.is_cuda and not _ZERO:
+            # (A/B) the replicated gradients summed in fp32 by ONE all-reduce
+            # after the backward (optim.DPGradReducer), a replicated FlatAdamW
+            from .optim import DPGradReducer
+
+            self.reducer = DPGradReducer(self.dp_params)
         images = self._cast_in(images)
         self.runner = None
         self.stepper = None
@@ -447,7 +460,7 @@ class TrainStep:
         return loss.detach()
 
     def _optimizer_step(self):
-        if self.opt_params is None:  # GPU: FlatAdamW (clip inside)
+        if self.opt_params is None:  # GPU: FlatAdamW / ShardedDPAdamW (reduction + clip inside)
             if self.reducer is not None:
                 self.opt.step(self._allreduce_grads(), inv_world=1.0 / self.world)
             else:

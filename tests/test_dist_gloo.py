@@ -81,3 +81,31 @@ def test_ddp_gloo_world2_matches_single_process(tmp_path):
     for n in g0:
         assert torch.equal(g0[n], g1[n]), f"ranks disagree on {n}"
         torch.testing.assert_close(g0[n], ref[n], rtol=2e-4, atol=2e-5, msg=lambda m: f"{n}: {m}")
+
+
+def test_sharded_optimizer_layout():
+    """optim.ShardedDPAdamW.layout (host side of the ZeRO-1 data-parallel
+    optimizer): every element of every tensor lands in exactly one piece,
+    pieces never cross a rank slice, every piece and slice starts at a
+    multiple of 8 elements (16-B bf16 / 32-B fp32 vectors), and the slices
+    cover each parameter space with at most 8 W - 1 padding elements."""
+    from src.rtdetr_moe.optim import ShardedDPAdamW
+
+    rng = __import__("random").Random(3)
+    for W in (1, 2, 3, 8):
+        tensors = {i: (rng.randint(0, 1), rng.choice([1, 7, 8, 255, 256, 4096, 65537, 262144])) for i in range(40)}
+        space_of, poff, S, pieces = ShardedDPAdamW.layout(tensors, W)
+        assert all(s % 8 == 0 and s >= 8 for s in S)
+        for sp in (0, 1):
+            need = sum((n + 7) // 8 * 8 for (s, n) in tensors.values() if s == sp)
+            assert need <= S[sp] * W < need + 8 * W + 8
+        cover = {i: [] for i in tensors}
+        for (i, i0, n, r, s) in pieces:
+            a = poff[i] + i0
+            assert s == space_of[i] and n > 0 and a % 8 == 0 and i0 % 8 == 0
+            assert r * S[s] <= a and a + n <= (r + 1) * S[s] and 0 <= r < W
+            cover[i].append((i0, n))
+        for i, (s, n) in tensors.items():
+            segs = sorted(cover[i])
+            assert segs[0][0] == 0 and sum(m for _, m in segs) == n
+            assert all(segs[k][0] + segs[k][1] == segs[k + 1][0] for k in range(len(segs) - 1))

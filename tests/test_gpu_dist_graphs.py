@@ -69,7 +69,8 @@ def _model(spec, dev):
 DP_SPEC = "rtdetr-r18-moe4-top2-dec2"
 
 
-def _dp_worker(rank, world, port, out, precision):
+def _dp_worker(rank, world, port, out, precision, zero):
+    os.environ["MOE_ZERO"] = "1" if zero else "0"  # read when step.py is imported (below)
     _init(rank, world, port)
     from src.rtdetr_moe.criterion import SetCriterion
     from src.rtdetr_moe.step import TrainStep
@@ -79,11 +80,16 @@ def _dp_worker(rank, world, port, out, precision):
     images, targets, ctx = _data(rank, dev)
     step = TrainStep(model, SetCriterion(num_classes=1), images, ctx, graphs=True, world=world, lr=1e-3,
                      precision=precision, targets=targets, num_boxes=NB)
-    assert step.stepper is not None and step.reducer is not None
+    assert step.stepper is not None
+    assert (step.reducer is None) == zero and (type(step.opt).__name__ == "ShardedDPAdamW") == zero
     step(images, ctx, targets, NB)
     torch.cuda.synchronize()
     names = {id(p): n for n, p in model.named_parameters()}
-    mean = {names[id(p)]: (v.float() / world).cpu() for p, v in zip(step.dp_params, step.reducer.views)}
+    if zero:  # the reduce-scattered slices, gathered (test helper)
+        red = step.opt.reduced_grads()
+        mean = {names[id(step.opt.params[i])]: (v.float() / world).cpu() for i, v in red.items()}
+    else:
+        mean = {names[id(p)]: (v.float() / world).cpu() for p, v in zip(step.dp_params, step.reducer.views)}
     coef = step.opt.coef.cpu().clone()  # [norm of the mean gradient, applied scale] of step 1
     losses = [float(step(images, ctx, targets, NB))]
     torch.cuda.synchronize()
@@ -93,12 +99,15 @@ def _dp_worker(rank, world, port, out, precision):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("precision", ["bf16", "amp"])
-def test_whole_step_graph_dp_equals_single_process_mean(hip_lib, tmp_path, precision):
+@pytest.mark.parametrize("precision,zero", [("bf16", True), ("amp", True), ("bf16", False)])
+def test_whole_step_graph_dp_equals_single_process_mean(hip_lib, tmp_path, precision, zero):
+    """zero: the sharded optimizer (reduce-scatter, AdamW on 1/world of the
+    state, all-gather; optim.ShardedDPAdamW, the default); else the flat
+    all-reduce + replicated FlatAdamW (MOE_ZERO=0)."""
     from src.rtdetr_moe.criterion import SetCriterion
     from src.rtdetr_moe.step import TrainStep
 
-    mp.start_processes(_dp_worker, args=(2, _port(), tmp_path, precision), nprocs=2, join=True,
+    mp.start_processes(_dp_worker, args=(2, _port(), tmp_path, precision, zero), nprocs=2, join=True,
                        start_method="spawn")
     r0, r1 = torch.load(tmp_path / "r0.pt"), torch.load(tmp_path / "r1.pt")
     assert torch.equal(r0["w"], r1["w"]), "ranks diverged after the graph-mode all-reduce"
