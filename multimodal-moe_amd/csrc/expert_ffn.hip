@@ -312,6 +312,7 @@ void expert_ffn_fwd_kernel(FfnParams p) {
   const int g = __builtin_amdgcn_readfirstlane(__builtin_ctzll(hit));
   const int row0 = __builtin_amdgcn_readfirstlane(__shfl(lo, g, 64) + (t - __shfl(incl - tg, g, 64)) * kFfBM);
   const int nrows = __builtin_amdgcn_readfirstlane(min(kFfBM, __shfl(hi, g, 64) - row0));
+  MOE_DASSERT(nrows >= 1 && nrows <= kFfBM && row0 >= 0);
 
   char* lds_b1 = s_bias;
   char* lds_b2 = s_bias + kFfB1Bytes;
@@ -333,6 +334,7 @@ void expert_ffn_fwd_kernel(FfnParams p) {
       int r = (wave + 4 * q) * 8 + (lane >> 3);
       r = min(r, nrows - 1);
       rs[q] = p.gather != nullptr ? p.gather[row0 + r] : row0 + r;
+      MOE_DASSERT(rs[q] >= 0);
     }
 #pragma unroll
     for (int j = 0; j < kFfG; ++j) {
@@ -429,6 +431,7 @@ void expert_ffn_fwd_kernel(FfnParams p) {
   for (int i = 0; i < 2; ++i) {
     const int rl = 32 * wm + 16 * i + lr;
     orow[i] = rl < nrows ? (p.yp_rows != nullptr ? p.yp_rows[row0 + rl] : row0 + rl) : -1;
+    MOE_DASSERT(orow[i] < p.yp_n);
   }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t yres =

@@ -270,6 +270,7 @@ struct Tile {
     }
     m0 = mt * BM;
     n0 = nt * BN;
+    MOE_DASSERT(rows_g >= 0 && row0 >= 0);  // expert offsets non-decreasing
     if constexpr (MODE == MODE_ROWS) {
       a_base = p.a + (size_t)row0 * p.lda;
       a_row_lim = rows_g < BM ? rows_g : BM;
@@ -609,6 +610,7 @@ __device__ __forceinline__ bool splitk_merge(const GemmParams& p, int tile_id, i
   __syncthreads();
   if (tid == 0) {
     const int old = __hip_atomic_fetch_add(p.cnt + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    MOE_DASSERT(old >= 0 && old < p.ksplit);  // split-K arrival counter (reset by the previous launch's last slice)
     if (old == p.ksplit - 1)  // ready for the next launch
       __hip_atomic_store(p.cnt + tile_id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_arrived = old;
@@ -1152,6 +1154,7 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p, int bid, char*
         const int r = (wave + 4 * j) * 8 + (lane >> 3);
         sw[j] = (lane & 7) ^ ((r >> 1) & 7);
         const int rc = r < t.a_row_lim ? r : t.a_row_lim - 1;
+        MOE_DASSERT(p.a_gather[t.row0 + rc] >= 0);  // a gather index of a kept row
         rowp[j] = p.a + (size_t)p.a_gather[t.row0 + rc] * p.lda + kofs0;
       }
     }

@@ -7,6 +7,15 @@
 
 #include "../../include/moe_hip.h"
 
+// Device-side asserts of the debug build (build_ext.py --debug: -DMOE_DEBUG);
+// compiled out otherwise.  A failing assert traps the wave.
+#ifdef MOE_DEBUG
+#include <cassert>
+#define MOE_DASSERT(c) assert(c)
+#else
+#define MOE_DASSERT(c) ((void)0)
+#endif
+
 namespace moe {
 
 extern int g_msda_generic;  // msda.hip: 1 = generic fused MSDA kernels (moe_set_tuning "msda_generic")
