@@ -498,12 +498,18 @@ __global__ __launch_bounds__(256) void msda_fused_fwd_lp_kernel(
   }
 }
 
-template <int LPG, int LL, int PP>
+// REC: instead of the value-gradient atomics, every corner contribution is
+// RECORDED as (row within its level or -1, weight a * w_c) at its natural
+// position ((b H + h) LL + l) [Q PP 4] + (q PP + p) 4 + c of `rec`; the
+// deterministic value gradient (msda_vgrad_sort_kernel + msda_vgrad_tile_kernel
+// below) sums them in that order in fp32.
+template <int LPG, int LL, int PP, bool REC = false>
 __global__ __launch_bounds__(256) void msda_fused_bwd_lp_kernel(
     const uint16_t* __restrict__ value, const int32_t* __restrict__ shapes, const int32_t* __restrict__ starts,
     const uint16_t* __restrict__ off, const float* __restrict__ ref, const uint16_t* __restrict__ logits,
     float offset_scale, const uint16_t* __restrict__ grad_out, int B, int S, int Q, int H, long long ldv,
-    uint16_t* __restrict__ grad_value, uint16_t* __restrict__ grad_off, uint16_t* __restrict__ grad_logits) {
+    uint16_t* __restrict__ grad_value, uint16_t* __restrict__ grad_off, uint16_t* __restrict__ grad_logits,
+    int2* __restrict__ rec) {
   constexpr int D = 2 * LPG;
   constexpr int LP = LL * PP;
   constexpr float invP = 1.f / (float)PP;
@@ -582,16 +588,38 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_lp_kernel(
         const uint16_t* vbn = value + ((size_t)b * S + lv.start[l + 1]) * ldv + h * D + 2 * sub;
         msda_level_geo<LPG, LL, PP>(lv, l + 1, pr, offw, offset_scale, vbn, ldv, valid, geo[(l + 1) & 1]);
       }
+      if constexpr (REC) {
+        // lane 4 p + c of the group records corner (p, c) of this level
+        if (valid && sub < 4 * PP) {
+          const int p = sub >> 2, c = sub & 3;
+          float fxp = 0.f, fyp = 0.f, ap = 0.f;
+          int x0p = 0, y0p = 0;
 #pragma unroll
-      for (int p = 0; p < PP; ++p)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          if (!(cur.in & (1u << (4 * p + c)))) continue;
-          const int xi = cur.x0[p] + (c & 1), yi = cur.y0[p] + (c >> 1);
-          bf16x2_t t = *reinterpret_cast<const bf16x2_t*>(&pv[p][c]);
-          __builtin_amdgcn_global_atomic_fadd_v2bf16(
-              (__attribute__((address_space(1))) bf16x2_t*)(grad_value + gofs + (size_t)(yi * Wl + xi) * ldv), t);
+          for (int pp = 0; pp < PP; ++pp)
+            if (pp == p) {
+              fxp = cur.fx[pp]; fyp = cur.fy[pp]; x0p = cur.x0[pp]; y0p = cur.y0[pp];
+              ap = pr.a[l * PP + pp];
+            }
+          const float wcn = ((c & 1) ? fxp : 1.f - fxp) * ((c >> 1) ? fyp : 1.f - fyp);
+          const int row = (cur.in & (1u << sub)) ? (y0p + (c >> 1)) * Wl + x0p + (c & 1) : -1;
+          const int q = (gi / H) % Q;
+          const size_t at = ((size_t)(b * H + h) * LL + l) * ((size_t)Q * PP * 4) + (size_t)q * PP * 4 + sub;
+          rec[at] = make_int2(row, __float_as_int(ap * wcn));
         }
+        (void)pv;
+        (void)gofs;
+      } else {
+#pragma unroll
+        for (int p = 0; p < PP; ++p)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (!(cur.in & (1u << (4 * p + c)))) continue;
+            const int xi = cur.x0[p] + (c & 1), yi = cur.y0[p] + (c >> 1);
+            bf16x2_t t = *reinterpret_cast<const bf16x2_t*>(&pv[p][c]);
+            __builtin_amdgcn_global_atomic_fadd_v2bf16(
+                (__attribute__((address_space(1))) bf16x2_t*)(grad_value + gofs + (size_t)(yi * Wl + xi) * ldv), t);
+          }
+      }
     }
     // softmax backward: d logit_sp = a_sp (ga_sp - sum_j a_j ga_j); lane `sub` writes sample sub
     if (valid && sub < LP) {
@@ -599,6 +627,145 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_lp_kernel(
       grad_logits[(size_t)gi * LP + sub] = f2bf(a * (my_ga - dot));
       *reinterpret_cast<uint32_t*>(grad_off + ((size_t)gi * LP + sub) * 2) = my_goff;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic value gradient (REC mode).  The recorded corner contributions
+// of every (b, h, level) group -- n = Q PP 4 of them, in (q, p, c) order --
+// are bucketed by destination tile of R value rows (stable counting sort, one
+// workgroup per group: thread t owns the contiguous entries [t k, (t+1) k),
+// per-thread tile counts in LDS, one exclusive scan, then an in-order
+// scatter), and each tile's workgroup sums its entries into an fp32 LDS image
+// of the tile's rows in that order, rounding once to bf16.  Every element of
+// the gradient is written (untouched rows get zeros: no memset), every sum
+// has a fixed order (bitwise repeatable), and the accumulation is fp32 -- the
+// atomic path added bf16 pairs in arrival order.
+// ---------------------------------------------------------------------------
+constexpr int kVgTilesMax = 64;
+constexpr int kVgSortThreads = 128;
+
+__global__ __launch_bounds__(kVgSortThreads) void msda_vgrad_sort_kernel(const int2* __restrict__ rec,
+                                                              const int32_t* __restrict__ shapes, int H, int L, int n,
+                                                              int R, int4* __restrict__ sorted,
+                                                              int32_t* __restrict__ toff) {
+  constexpr int NTH = kVgSortThreads;
+  __shared__ int cnt[kVgTilesMax * NTH];  // [tile][thread]
+  __shared__ int part[NTH];
+  const int grp = blockIdx.x, l = grp % L, tid = threadIdx.x;
+  const int hw = shapes[2 * l] * shapes[2 * l + 1];
+  const int nt = (hw + R - 1) / R;
+  const int k = (n + NTH - 1) / NTH, e0 = tid * k, e1 = min(n, e0 + k);
+  const int2* src = rec + (size_t)grp * n;
+  for (int t = 0; t < nt; ++t) cnt[t * NTH + tid] = 0;
+  for (int e = e0; e < e1; ++e) {
+    const int row = src[e].x;
+    if (row >= 0) cnt[(row / R) * NTH + tid] += 1;
+  }
+  __syncthreads();
+  // exclusive scan of cnt in (tile, thread) order, i.e. memory order: thread t
+  // takes the nt consecutive elements [t nt, (t+1) nt) (nt NTH in all)
+  int loc = 0;
+  for (int i = 0; i < nt; ++i) loc += cnt[tid * nt + i];
+  part[tid] = loc;
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int i = 0; i < NTH; ++i) {
+      const int v = part[i];
+      part[i] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  int run = part[tid];
+  for (int i = 0; i < nt; ++i) {
+    const int v = cnt[tid * nt + i];
+    cnt[tid * nt + i] = run;
+    run += v;
+  }
+  __syncthreads();
+  int32_t* to = toff + (size_t)grp * (kVgTilesMax + 1);
+  for (int t = tid; t < nt; t += NTH) to[t] = cnt[t * NTH];
+  if (tid == NTH - 1) to[nt] = run;  // the total: the last thread's running sum
+  int4* dst = sorted + (size_t)grp * n;
+  for (int e = e0; e < e1; ++e) {  // in entry order: stable
+    const int2 v = src[e];
+    if (v.x < 0) continue;
+    const int slot = (v.x / R) * NTH + tid;
+    const int pos = cnt[slot];
+    cnt[slot] = pos + 1;
+    dst[pos] = make_int4(v.x, v.y, e, 0);
+  }
+}
+
+// One workgroup per (b, h, level, tile of R rows).  Threads: 8 groups of 32
+// lanes; group k owns the tile rows r with r % 8 == k (so two entries of one
+// row are always added by the same lanes, in entry order); a lane owns D / 32
+// channels.  Entries and their grad_out rows are staged in LDS by chunks.
+template <int D>
+__global__ __launch_bounds__(256) void msda_vgrad_tile_kernel(const int4* __restrict__ sorted,
+                                                              const int32_t* __restrict__ toff,
+                                                              const int32_t* __restrict__ shapes,
+                                                              const int32_t* __restrict__ starts,
+                                                              const uint16_t* __restrict__ grad_out, int B, int S,
+                                                              int Q, int H, int L, int P, int R, int tiles_bh,
+                                                              long long ldv, uint16_t* __restrict__ grad_value) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int CH = 256;          // entries per staged chunk
+  constexpr int DL = D / 32;       // channels per lane
+  float* acc = reinterpret_cast<float*>(smem);                     // [R][D]
+  int4* sent = reinterpret_cast<int4*>(smem + (size_t)R * D * 4);  // [CH]
+  uint16_t* sg = reinterpret_cast<uint16_t*>(sent + CH);            // [CH][D]
+  const int tid = threadIdx.x, gk = tid >> 5, ln = tid & 31;
+  const int bh = blockIdx.x / tiles_bh;
+  int rem = blockIdx.x - bh * tiles_bh, l = 0, hw = 0;
+  for (; l < L; ++l) {
+    hw = shapes[2 * l] * shapes[2 * l + 1];
+    const int nt = (hw + R - 1) / R;
+    if (rem < nt) break;
+    rem -= nt;
+  }
+  const int t = rem, b = bh / H, h = bh - b * H;
+  const int grp = bh * L + l, n = Q * P * 4;
+  const int32_t* to = toff + (size_t)grp * (kVgTilesMax + 1);
+  const int j0 = to[t], j1 = to[t + 1];
+  const int r0 = t * R, rows = min(R, hw - r0);
+  for (int i = tid; i < R * D; i += 256) acc[i] = 0.f;
+  const int4* ent = sorted + (size_t)grp * n;
+  for (int c0 = j0; c0 < j1; c0 += CH) {
+    const int cn = min(CH, j1 - c0);
+    __syncthreads();  // (previous chunk consumed; acc zeroed)
+    for (int i = tid; i < cn; i += 256) sent[i] = ent[c0 + i];
+    __syncthreads();
+    // grad_out rows of the chunk's entries: D bf16 = D / 8 16-B pieces each
+    constexpr int PPR = D / 8;
+    for (int i = tid; i < cn * PPR; i += 256) {
+      const int j = i / PPR, pc = i - j * PPR;
+      const int q = sent[j].z / (P * 4);
+      reinterpret_cast<uint4*>(sg + (size_t)j * D)[pc] =
+          reinterpret_cast<const uint4*>(grad_out + (((size_t)b * Q + q) * H + h) * D)[pc];
+    }
+    __syncthreads();
+    for (int j = 0; j < cn; ++j) {
+      const int4 e = sent[j];
+      const int r = e.x - r0;
+      if ((r & 7) != gk) continue;
+      const float w = __int_as_float(e.y);
+#pragma unroll
+      for (int u = 0; u < DL; ++u) {
+        const int dch = ln * DL + u;
+        acc[r * D + dch] += w * bf2f(sg[(size_t)j * D + dch]);
+      }
+    }
+  }
+  __syncthreads();
+  // the tile's rows out as bf16 (16-B pieces), zeros where nothing landed
+  constexpr int PPR = D / 8;
+  uint16_t* gv = grad_value + ((size_t)b * S + starts[l] + r0) * ldv + (size_t)h * D;
+  for (int i = tid; i < rows * PPR; i += 256) {
+    const int r = i / PPR, pc = i - r * PPR;
+    *reinterpret_cast<uint4*>(gv + (size_t)r * ldv + pc * 8) = pack8(acc + r * D + pc * 8);
   }
 }
 
@@ -743,10 +910,10 @@ extern "C" int rtdetr_msda_fused_bwd_ld(const void* value, long long ldv, const 
   const bool lp34 = L == 3 && P == 4 && !(g_msda_generic & 2);
   if (D == 32 && lp34)
     MOE_LAUNCH(prof, (msda_fused_bwd_lp_kernel<16, 3, 4>), dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v,
-               shapes, starts, o, ref, lg, offset_scale, go, B, S, Q, H, ldv, gv, gof, glg);
+               shapes, starts, o, ref, lg, offset_scale, go, B, S, Q, H, ldv, gv, gof, glg, static_cast<int2*>(nullptr));
   else if (D == 64 && lp34)
     MOE_LAUNCH(prof, (msda_fused_bwd_lp_kernel<32, 3, 4>), dim3(msda_grid(groups, 32)), dim3(256), 0, stream, v,
-               shapes, starts, o, ref, lg, offset_scale, go, B, S, Q, H, ldv, gv, gof, glg);
+               shapes, starts, o, ref, lg, offset_scale, go, B, S, Q, H, ldv, gv, gof, glg, static_cast<int2*>(nullptr));
   else if (D == 32)
     MOE_LAUNCH(prof, msda_fused_bwd_kernel<16>, dim3(msda_grid(groups, 16)), dim3(256), 0, stream, v, shapes, starts,
                o, ref, lg, offset_scale, go, B, S, Q, H, L, P, ldv, gv, gof, glg);
@@ -769,4 +936,94 @@ extern "C" int rtdetr_msda_fused_bwd(const void* value, const int32_t* shapes, c
                                      void* grad_off, void* grad_logits, hipStream_t stream) {
   return rtdetr_msda_fused_bwd_ld(value, (long long)H * D, shapes, starts, off, ref, logits, offset_scale, grad_out,
                                   B, S, Q, H, D, L, P, grad_value, 1, grad_off, grad_logits, stream);
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic decoder MSDA backward (L = 3, P = 4): the fused backward in
+// REC mode, then the per-group tile sort and the per-tile fp32 sums.  Writes
+// EVERY element of its grad_value column slice (no zeroing needed).
+// hw_host: the L level sizes h_l w_l in HOST memory (they size the tile grid).
+// ---------------------------------------------------------------------------
+static int vg_rows_per_tile(const int32_t* hw_host, int L) {
+  int mx = 1;
+  for (int l = 0; l < L; ++l) mx = std::max(mx, (int)hw_host[l]);
+  return 256 * ((mx + 256 * kVgTilesMax - 1) / (256 * kVgTilesMax));
+}
+
+extern "C" long long rtdetr_msda_vgrad_workspace(int B, int Q, int H, int L, int P) {
+  const long long n = (long long)B * H * L * Q * P * 4;
+  return n * 8 + n * 16 + (long long)B * H * L * (kVgTilesMax + 1) * 4 + 256;
+}
+
+extern "C" int rtdetr_msda_fused_bwd_det(const void* value, long long ldv, const int32_t* shapes,
+                                         const int32_t* starts, const int32_t* hw_host, const void* off,
+                                         const float* ref, const void* logits, float offset_scale,
+                                         const void* grad_out, int B, int S, int Q, int H, int D, int L, int P,
+                                         void* grad_value, void* grad_off, void* grad_logits, void* work,
+                                         long long work_bytes, hipStream_t stream) {
+  if (msda_check(B, S, Q, H, D, L, P)) return -1;
+  if (L != 3 || P != 4) return fail("msda_fused_bwd_det: needs L = 3, P = 4 (the RT-DETR decoder)");
+  if (ldv < (long long)H * D || ldv % 8 != 0) return fail("msda_fused_bwd_det: ldv must be >= H * D, a multiple of 8");
+  if (hw_host == nullptr || work == nullptr) return fail("msda_fused_bwd_det: NULL hw_host / work");
+  if (work_bytes < rtdetr_msda_vgrad_workspace(B, Q, H, L, P)) return fail("msda_fused_bwd_det: workspace too small");
+  if (reinterpret_cast<uintptr_t>(work) % 16 || reinterpret_cast<uintptr_t>(grad_value) % 16)
+    return fail("msda_fused_bwd_det: work and grad_value must be 16-B aligned");
+  if (Q == 0) return 0;  // (no samples: the caller's slice stays as it was)
+  const int R = vg_rows_per_tile(hw_host, L);
+  int tiles_bh = 0;
+  for (int l = 0; l < L; ++l) tiles_bh += (hw_host[l] + R - 1) / R;
+  const long long n = (long long)Q * P * 4, n_all = n * B * H * L;
+  int2* rec = static_cast<int2*>(work);
+  int4* sorted = reinterpret_cast<int4*>(static_cast<char*>(work) + n_all * 8);
+  int32_t* toff = reinterpret_cast<int32_t*>(static_cast<char*>(work) + n_all * 24);
+  const long long groups = (long long)B * Q * H;
+  const uint16_t* v = static_cast<const uint16_t*>(value);
+  const uint16_t* o = static_cast<const uint16_t*>(off);
+  const uint16_t* lg = static_cast<const uint16_t*>(logits);
+  const uint16_t* go = static_cast<const uint16_t*>(grad_out);
+  uint16_t* gv = static_cast<uint16_t*>(grad_value);
+  {
+    const double samples = (double)groups * L * P;
+    ProfScope prof(stream, PROF_MSDA, samples * (8.0 * D + 32.0 + 10.0) + groups * (2.0 * D + 16.0 / H));
+    if (D == 32)
+      MOE_LAUNCH(prof, (msda_fused_bwd_lp_kernel<16, 3, 4, true>), dim3(msda_grid(groups, 16)), dim3(256), 0, stream,
+                 v, shapes, starts, o, ref, lg, offset_scale, go, B, S, Q, H, ldv, gv,
+                 static_cast<uint16_t*>(grad_off), static_cast<uint16_t*>(grad_logits), rec);
+    else
+      MOE_LAUNCH(prof, (msda_fused_bwd_lp_kernel<32, 3, 4, true>), dim3(msda_grid(groups, 32)), dim3(256), 0, stream,
+                 v, shapes, starts, o, ref, lg, offset_scale, go, B, S, Q, H, ldv, gv,
+                 static_cast<uint16_t*>(grad_off), static_cast<uint16_t*>(grad_logits), rec);
+    if (int rc = check_launch("rtdetr_msda_fused_bwd_det (samples)")) return rc;
+  }
+  {
+    ProfScope prof(stream, PROF_MSDA, (double)n_all * (8.0 + 16.0) + (double)B * H * L * (kVgTilesMax + 1) * 4);
+    MOE_LAUNCH(prof, msda_vgrad_sort_kernel, dim3(B * H * L), dim3(kVgSortThreads), 0, stream, rec, shapes, H, L,
+               (int)n, R, sorted, toff);
+    if (int rc = check_launch("rtdetr_msda_fused_bwd_det (sort)")) return rc;
+  }
+  const size_t lds = (size_t)R * D * 4 + 256 * 16 + (size_t)256 * D * 2;
+  if (lds > 159 * 1024) return fail("msda_fused_bwd_det: level too large for the LDS tile");
+  double rows = 0;
+  for (int l = 0; l < L; ++l) rows += hw_host[l];
+  ProfScope prof(stream, PROF_MSDA, (double)n_all * (16.0 + 2.0 * D) + rows * B * H * D * 2.0);
+  if (D == 32) {
+    static bool a32 = false;
+    if (!a32) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(msda_vgrad_tile_kernel<32>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+      a32 = true;
+    }
+    MOE_LAUNCH(prof, msda_vgrad_tile_kernel<32>, dim3(B * H * tiles_bh), dim3(256), lds, stream, sorted, toff, shapes,
+               starts, go, B, S, Q, H, L, P, R, tiles_bh, ldv, gv);
+  } else {
+    static bool a64 = false;
+    if (!a64) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(msda_vgrad_tile_kernel<64>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+      a64 = true;
+    }
+    MOE_LAUNCH(prof, msda_vgrad_tile_kernel<64>, dim3(B * H * tiles_bh), dim3(256), lds, stream, sorted, toff, shapes,
+               starts, go, B, S, Q, H, L, P, R, tiles_bh, ldv, gv);
+  }
+  return check_launch("rtdetr_msda_fused_bwd_det");
 }

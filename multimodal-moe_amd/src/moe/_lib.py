@@ -86,6 +86,9 @@ SIGNATURES = {
     "rtdetr_msda_bwd_bf16": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "rtdetr_msda_fused_fwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_msda_fused_bwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "rtdetr_msda_vgrad_workspace": (_LL, [_I, _I, _I, _I, _I]),
+    "rtdetr_msda_fused_bwd_det": (_I, [_P, _LL, _P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P,
+                                       _P, _LL, _P]),
     "rtdetr_msda_fused_fwd_ld": (_I, [_P, ctypes.c_longlong, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _I, _I,
                                       _P, _P]),
     "rtdetr_msda_fused_bwd_ld": (_I, [_P, ctypes.c_longlong, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _I, _I,
@@ -1007,6 +1010,35 @@ def msda_fused_bwd_slice(value_all, grad_all, col0, H, D, shapes, starts, off, r
                                           _ptr(ref), _ptr(logits), float(offset_scale), _ptr(grad_out), B, S, Q, H, D,
                                           L, P, grad_all.data_ptr() + 2 * col0, 0, _ptr(go), _ptr(gl), _stream()),
            "rtdetr_msda_fused_bwd_ld")
+    return go, gl
+
+
+def msda_det_ok(L, P, D):
+    """Shapes the deterministic MSDA backward takes (the RT-DETR decoder's)."""
+    return L == 3 and P == 4 and D in (32, 64)
+
+
+def msda_fused_bwd_slice_det(value_all, grad_all, col0, H, D, shapes, starts, hw, off, ref, logits, offset_scale, L,
+                             P, grad_out):
+    """Deterministic backward of msda_fused_fwd_slice (rtdetr_msda_fused_bwd_det):
+    the value gradient of the column slice is WRITTEN (every element; fp32
+    sums in a fixed order, one bf16 rounding) -- grad_all needs no zeroing.
+    hw: the L level sizes h_l w_l (host ints).  -> (grad_off, grad_logits)."""
+    B, S, C = value_all.shape
+    Q = off.shape[1]
+    _need(grad_out, torch.bfloat16, "grad_out")
+    _need(grad_all, torch.bfloat16, "grad_all")
+    if grad_all.shape != value_all.shape or len(hw) != L:
+        raise MoEKernelError("msda_fused_bwd_slice_det: shapes")
+    go = torch.empty_like(off)
+    gl = torch.empty_like(logits)
+    nbytes = int(lib().rtdetr_msda_vgrad_workspace(B, Q, H, L, P))
+    work = torch.empty(nbytes, dtype=torch.uint8, device=value_all.device)
+    hw_c = (ctypes.c_int32 * L)(*[int(v) for v in hw])
+    _check(lib().rtdetr_msda_fused_bwd_det(value_all.data_ptr() + 2 * col0, C, _ptr(shapes), _ptr(starts), hw_c,
+                                           _ptr(off), _ptr(ref), _ptr(logits), float(offset_scale), _ptr(grad_out),
+                                           B, S, Q, H, D, L, P, grad_all.data_ptr() + 2 * col0, _ptr(go), _ptr(gl),
+                                           _ptr(work), nbytes, _stream()), "rtdetr_msda_fused_bwd_det")
     return go, gl
 
 

@@ -174,7 +174,7 @@ class _ValueProjAll(torch.autograd.Function):
     column sums of G, split back per layer."""
 
     @staticmethod
-    def forward(ctx, memory, dtype, *wb):
+    def forward(ctx, memory, dtype, det, *wb):
         n = len(wb) // 2
         ws, bs = wb[0::2], wb[1::2]
         B, S, d = memory.shape
@@ -182,7 +182,10 @@ class _ValueProjAll(torch.autograd.Function):
         W = torch.cat([w.to(dtype) for w in ws], 0)  # [n d, d]
         bias = torch.cat([b.to(dtype) for b in bs], 0)
         v_all = F.linear(m2, W, bias).view(B, S, n * d)
-        grad_all = torch.zeros_like(v_all)
+        # det: every layer's deterministic MSDA backward writes its whole
+        # column slice (no zero fill of the [B, S, n d] buffer); else the
+        # atomic backward accumulates into a zeroed buffer
+        grad_all = torch.empty_like(v_all) if det else torch.zeros_like(v_all)
         token = torch.zeros((), dtype=torch.float32, device=memory.device)
         ctx.save_for_backward(m2, W)
         ctx.grad_all = grad_all
@@ -203,7 +206,7 @@ class _ValueProjAll(torch.autograd.Function):
         grads = []
         for i in range(n):
             grads += [dW[i * d:(i + 1) * d].to(wdt[i]), db[i * d:(i + 1) * d].to(bdt[i])]
-        return (dmem, None, *grads)
+        return (dmem, None, None, *grads)
 
 
 class _MSDAFusedSlot(torch.autograd.Function):
@@ -211,7 +214,8 @@ class _MSDAFusedSlot(torch.autograd.Function):
     gradient is accumulated into the same slice of its shared buffer."""
 
     @staticmethod
-    def forward(ctx, token, v_all, grad_all, col0, H, D, shapes_t, starts_t, off, ref, logits, offset_scale, L, P):
+    def forward(ctx, token, v_all, grad_all, col0, H, D, shapes_t, starts_t, off, ref, logits, offset_scale, L, P,
+                hw=None):
         from ..moe import _lib as L_
 
         o, lg = off.contiguous(), logits.contiguous()
@@ -219,7 +223,7 @@ class _MSDAFusedSlot(torch.autograd.Function):
         out = L_.msda_fused_fwd_slice(v_all, col0, H, D, shapes_t, starts_t, o, r, lg, offset_scale, L, P)
         ctx.save_for_backward(v_all, shapes_t, starts_t, o, r, lg)
         ctx.grad_all = grad_all
-        ctx.cfg = (col0, H, D, offset_scale, L, P)
+        ctx.cfg = (col0, H, D, offset_scale, L, P, hw)
         return out
 
     @staticmethod
@@ -227,17 +231,33 @@ class _MSDAFusedSlot(torch.autograd.Function):
         from ..moe import _lib as L_
 
         v_all, shapes_t, starts_t, o, r, lg = ctx.saved_tensors
-        col0, H, D, offset_scale, L, P = ctx.cfg
-        go, gl = L_.msda_fused_bwd_slice(v_all, ctx.grad_all, col0, H, D, shapes_t, starts_t, o, r, lg, offset_scale,
-                                         L, P, grad_out.to(torch.bfloat16).contiguous())
+        col0, H, D, offset_scale, L, P, hw = ctx.cfg
+        g = grad_out.to(torch.bfloat16).contiguous()
+        if hw is not None:  # deterministic: writes the slice (fixed-order fp32 sums)
+            go, gl = L_.msda_fused_bwd_slice_det(v_all, ctx.grad_all, col0, H, D, shapes_t, starts_t, hw, o, r, lg,
+                                                 offset_scale, L, P, g)
+        else:  # atomic: accumulates into the zeroed slice
+            go, gl = L_.msda_fused_bwd_slice(v_all, ctx.grad_all, col0, H, D, shapes_t, starts_t, o, r, lg,
+                                             offset_scale, L, P, g)
         ctx.grad_all = None
-        return (torch.zeros((), dtype=torch.float32, device=go.device),) + (None,) * 7 + (go, None, gl) + (None,) * 3
+        return (torch.zeros((), dtype=torch.float32, device=go.device),) + (None,) * 7 + (go, None, gl) + (None,) * 4
 
 
 _LEVEL_CACHE = {}
 _FUSED_MSDA = os.environ.get("MOE_FUSED_MSDA", "1") != "0"  # A/B switch
 _BATCHED_VALUE = os.environ.get("MOE_BATCHED_VALUE", "1") != "0"  # A/B switch: one value projection for all layers
 _FUSED_BOXES = os.environ.get("MOE_FUSED_BOXES", "1") != "0"  # A/B switch
+# MOE_DET_MSDA=0: the decoder's MSDA value gradients by packed bf16 atomics
+# (arrival order) instead of the deterministic fixed-order fp32 sums (A/B)
+_DET_MSDA = os.environ.get("MOE_DET_MSDA", "1") != "0"
+
+
+def _det_msda(L, P, D):
+    """Whether the decoder's fused MSDA backward runs deterministically
+    (_lib.msda_det_ok shapes, MOE_DET_MSDA on)."""
+    from ..moe import _lib as L_
+
+    return _DET_MSDA and L_.msda_det_ok(L, P, D)
 
 
 def _level_tensors(shapes, device):
@@ -300,8 +320,10 @@ class MSDeformableAttention(nn.Module):
             if not (off.dtype == logits.dtype == torch.bfloat16 and not ref_boxes.requires_grad and L * P <= 16):
                 raise RuntimeError("the batched value projection needs the fused bf16 MSDA path")
             st, so = _level_tensors(shapes, v_all.device)
+            det = _det_msda(L, P, self.d // H)  # (the same rule _value_slots applied to every layer)
+            hw = tuple(int(h) * int(w) for h, w in shapes) if det else None
             out = _MSDAFusedSlot.apply(token, v_all, g_all, col0, H, self.d // H, st, so, off, ref_boxes, logits,
-                                       float(self.offset_scale), L, P)
+                                       float(self.offset_scale), L, P, hw)
             return self.output_proj(out)
         v = self.value_proj(value).view(B, value.shape[1], H, self.d // H)
         off = self.sampling_offsets(query)
@@ -397,8 +419,11 @@ class RTDETRDecoder(nn.Module):
         if not (_BATCHED_VALUE and _FUSED_MSDA and memory.is_cuda and dtype == torch.bfloat16 and n > 1):
             return [None] * n
         vps = [layer.cross_attn.value_proj for layer in self.layers]
+        det = all(_det_msda(la.cross_attn.nlevels, la.cross_attn.npoints, la.cross_attn.d // la.cross_attn.nhead)
+                  for la in self.layers)
         with torch.autocast("cuda", enabled=False):
-            v_all, g_all, token = _ValueProjAll.apply(memory, dtype, *[t for m in vps for t in (m.weight, m.bias)])
+            v_all, g_all, token = _ValueProjAll.apply(memory, dtype, det,
+                                                      *[t for m in vps for t in (m.weight, m.bias)])
         return [(v_all, g_all, token, i * self.hidden) for i in range(n)]
 
     def forward(self, feats, ctx):
