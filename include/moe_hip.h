@@ -405,6 +405,22 @@ int rtdetr_msda_fused_bwd_ld(const void* value, long long ldv, const int32_t* sh
                              const void* off, const float* ref, const void* logits, float offset_scale,
                              const void* grad_out, int B, int S, int Q, int H, int D, int L, int P, void* grad_value,
                              int zero_grad_value, void* grad_off, void* grad_logits, hipStream_t stream);
+/* Deterministic variant of rtdetr_msda_fused_bwd_ld for the decoder's L = 3,
+ * P = 4 (D = 32 or 64): the value gradient of the column slice is WRITTEN,
+ * every element (rows no sample touches get zeros), as fp32 sums in a fixed
+ * order rounded once to bf16 -- the corner contributions are recorded by the
+ * per-sample kernel, bucketed by tile of value rows (stable counting sort) and
+ * summed per tile -- instead of packed bf16 atomics in arrival order.
+ * grad_off / grad_logits as rtdetr_msda_fused_bwd_ld.  hw_host: the L level
+ * sizes h_l w_l in HOST memory (they size the tile grid); work: a device
+ * workspace of rtdetr_msda_vgrad_workspace(B, Q, H, L, P) bytes, 16-B aligned.
+ * Three launches, no host sync. */
+long long rtdetr_msda_vgrad_workspace(int B, int Q, int H, int L, int P);
+int rtdetr_msda_fused_bwd_det(const void* value, long long ldv, const int32_t* shapes, const int32_t* starts,
+                              const int32_t* hw_host, const void* off, const float* ref, const void* logits,
+                              float offset_scale, const void* grad_out, int B, int S, int Q, int H, int D, int L,
+                              int P, void* grad_value, void* grad_off, void* grad_logits, void* work,
+                              long long work_bytes, hipStream_t stream);
 
 /* ---- frozen-BatchNorm convolution epilogues of the backbone ----
  * With frozen BN statistics, conv + BN = conv with per-channel scaled weights
