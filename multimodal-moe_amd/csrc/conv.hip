@@ -46,6 +46,7 @@ static int wg_bm(int N) { return N % 128 == 0 ? 128 : 64; }
 static int wg_bn(int C) { return C % 128 == 0 ? 128 : 64; }
 // rtdetr_conv_set_tuning knobs (measurement / A-B; 0 or -1 = automatic)
 static int g_conv_bm = 0;          // "conv_bm": forward tile rows 64, 128 or 256
+static int g_conv_big = 0;         // "conv_big": 1 = the 8-wave 256 x 128 forward / data-gradient tile
 static int g_conv_wg_stages = 0;   // "conv_wg_stages": weight-gradient ring depth 2..4
 static int g_conv_wg_splits = 0;   // "conv_wg_splits": weight-gradient pixel slices
 static int g_conv_dgrad_flip = -1; // "conv_dgrad_flip": 1 = always write W', 0 = always read in place
@@ -102,18 +103,24 @@ __device__ __forceinline__ void dma16(const uint16_t* src, char* lds) {
 // ---------------------------------------------------------------------------
 // forward / data gradient
 // ---------------------------------------------------------------------------
-template <int KS, int S, int BM, int BN, bool BT, bool PH = false>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
+// WGM x WGN waves (2 x 2: 256 threads; the big tiles 256 x 128 / 256 x 256
+// run 4 x 2 / 2 x 4 = 8 waves, 512 threads, two per SIMD): wave (wm, wn)
+// computes rows wm BM/WGM .. and columns wn BN/WGN .. of the tile.
+template <int KS, int S, int BM, int BN, bool BT, bool PH = false, int WGM = 2, int WGN = 2>
+__global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  static_assert(BN == 64 || BN == 128, "output-channel tile: 64 or 128");
+  static_assert(BN == 64 || BN == 128 || BN == 256, "output-channel tile: 64, 128 or 256");
+  constexpr int NW = WGM * WGN, NTH = 64 * NW;
   constexpr int TILE = (BM + BN) * 128;  // bytes of one ring stage
   constexpr int CPR = BN / 8;            // 16-B chunks per output row of the tile
-  constexpr int TM = BM / 32, TN = BN / 32;
-  constexpr int GW = BM / 32 + BN / 32;  // DMA instructions per wave per K-tile
+  constexpr int TM = BM / (16 * WGM), TN = BN / (16 * WGN);  // 16 x 16 blocks per wave
+  constexpr int AP = BM / (8 * NW), BP = BN / (8 * NW);       // DMA instructions per wave per K-tile (A, B)
+  static_assert(AP >= 1 && BP >= 1 && AP * 8 * NW == BM && BP * 8 * NW == BN, "tile / wave split");
+  constexpr int GW = AP + BP;            // DMA instructions per wave per K-tile
   constexpr int PAD = (KS - 1) / 2;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
   // XCD-aware map: the N tiles of one M tile run on one XCD (they share the A panel)
   const int NT = a.N / BN;
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
@@ -126,11 +133,11 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   const int nk = nty * ntx * cpt;
   const int HW = a.H * a.W, HWs = a.Hs * a.Ws;
   // this lane's A rows (one per DMA instruction j): pixel, coordinates, source chunk
-  int py[TM], px[TM], pb[TM], ach[TM];
-  bool pv[TM];
+  int py[AP], px[AP], pb[AP], ach[AP];
+  bool pv[AP];
 #pragma unroll
-  for (int j = 0; j < TM; ++j) {
-    const int r = (wave + 4 * j) * 8 + (lane >> 3);
+  for (int j = 0; j < AP; ++j) {
+    const int r = (wave + NW * j) * 8 + (lane >> 3);
     const int p = m0 + r;
     pv[j] = p < a.P;
     const int pp = pv[j] ? p : 0;
@@ -145,14 +152,14 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   // operand is W'[n][tap][k] = W[k][KS^2-1-tap][n], read as an MN-contiguous
   // [64 k-rows][BN] image (k-row = one of W's output channels, BN contiguous
   // input channels; ds_read_b64_tr_b16 fragments) -- no transposed copy of W.
-  const uint16_t* wrow[TN];
+  const uint16_t* wrow[BP];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
+  for (int j = 0; j < BP; ++j) {
     if constexpr (BT) {  // CPR lanes per k-row
-      const int kr = (wave + 4 * j) * (64 / CPR) + lane / CPR;
+      const int kr = (wave + NW * j) * (64 / CPR) + lane / CPR;
       wrow[j] = a.w + (size_t)kr * (KS * KS * a.N) + n0 + ((lane % CPR) ^ mimg_swz<BN>(kr)) * 8;
     } else {
-      const int r = (wave + 4 * j) * 8 + (lane >> 3);
+      const int r = (wave + NW * j) * 8 + (lane >> 3);
       wrow[j] = a.w + (size_t)(n0 + r) * (KS * KS * a.C) + ((lane & 7) ^ ((r >> 1) & 7)) * 8;
     }
   }
@@ -172,20 +179,20 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
       dx = tap % KS - PAD;
     }
 #pragma unroll
-    for (int j = 0; j < TM; ++j) {
+    for (int j = 0; j < AP; ++j) {
       int yy = py[j] * a.st + dy, xx = px[j] * a.st + dx;
       bool ok = pv[j] && !(((yy | xx) & a.sh));  // sh = 1: both even
       yy >>= a.sh;
       xx >>= a.sh;
       ok = ok && yy >= 0 && yy < a.Hs && xx >= 0 && xx < a.Ws;
       const uint16_t* src = ok ? a.x + ((size_t)(pb[j] * HWs + yy * a.Ws + xx)) * a.C + c0 + ach[j] : a.zero + ach[j];
-      dma16(src, buf + (wave + 4 * j) * 1024);
+      dma16(src, buf + (wave + NW * j) * 1024);
     }
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
+    for (int j = 0; j < BP; ++j) {
       if constexpr (BT) dma16(wrow[j] + (size_t)c0 * (KS * KS * a.N) + (KS * KS - 1 - tap) * a.N,
-                              buf + BM * 128 + (wave + 4 * j) * 1024);
-      else dma16(wrow[j] + tap * a.C + c0, buf + BM * 128 + (wave + 4 * j) * 1024);
+                              buf + BM * 128 + (wave + NW * j) * 1024);
+      else dma16(wrow[j] + tap * a.C + c0, buf + BM * 128 + (wave + NW * j) * 1024);
     }
   };
   f32x4 acc[TM][TN];
@@ -193,7 +200,6 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float csum[TM];
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) issue(s);
@@ -202,14 +208,14 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
     if (kt + S - 1 < nk) issue(kt + S - 1);  // refills the slot consumed in iteration kt - 1
     const char* cur = smem + (kt % S) * TILE;
-    compute_tile<BM, BN, true, !BT, false>(cur, cur + BM * 128, acc, csum, lane, wm, wn);
+    compute_tile_w<BM, BN, WGM, WGN, true, !BT>(cur, cur + BM * 128, acc, lane, wm, wn);
   }
   // Epilogue through LDS: lane holds Y[m0 + wm BM/2 + 16 i + (lane & 15)][n0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3];
   // the tile goes to a row-major [BM][BN] bf16 image (16-B chunk c of row r at chunk c ^ (r % CPR):
   // conflict-free 8-B writes and 16-B reads), then out as whole 256-B rows of 16-B stores
   // (register-direct 8-B stores at a row stride run at about half that rate).  The fused
   // epilogue's operands (same 16-B chunks as the stores) are loaded first, behind the image.
-  constexpr int RPP = 256 / CPR;  // rows per store pass
+  constexpr int RPP = NTH / CPR;  // rows per store pass
   const int ec = tid % CPR;
   uint4 eres[BM / RPP], emask[BM / RPP];
   // global output row of GEMM row p (PH: the class pixel's dX row)
@@ -241,10 +247,10 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   __syncthreads();  // every wave is done reading the ring
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int r = wm * (BM / 2) + 16 * i + (lane & 15);
+    const int r = wm * (BM / WGM) + 16 * i + (lane & 15);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int col = wn * (BN / 2) + 16 * j + 4 * (lane >> 4);
+      const int col = wn * (BN / WGN) + 16 * j + 4 * (lane >> 4);
       uint2 v;
       v.x = pack2bf(acc[i][j][0], acc[i][j][1]);
       v.y = pack2bf(acc[i][j][2], acc[i][j][3]);
@@ -509,16 +515,35 @@ static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int 
 
 constexpr int CV_STAGES = 2;
 
-template <int KS, int BM, int BN, bool BT, bool PH>
+template <int KS, int BM, int BN, bool BT, bool PH, int WGM = 2, int WGN = 2>
 static void launch_fwd_n(ConvArgs a, hipStream_t stream, ProfScope& prof) {
   constexpr size_t lds = CV_STAGES * (BM + BN) * 128;
   static_assert(lds >= BM * BN * 2, "epilogue image exceeds the ring");
-  allow_lds_once<conv_fwd_kernel<KS, CV_STAGES, BM, BN, BT, PH>>(lds);
+  static_assert(!(BT && BN > 128), "the in-place (MN-contiguous) weight image takes 64 or 128 columns");
+  allow_lds_once<conv_fwd_kernel<KS, CV_STAGES, BM, BN, BT, PH, WGM, WGN>>(lds);
   a.mt_n = (a.P + BM - 1) / BM;
   const int NT = a.N / BN;
   const int grid = ((a.mt_n + 7) / 8) * 8 * NT;
-  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, CV_STAGES, BM, BN, BT, PH>), dim3(grid), dim3(256), lds, stream, a);
+  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, CV_STAGES, BM, BN, BT, PH, WGM, WGN>), dim3(grid), dim3(64 * WGM * WGN), lds,
+             stream, a);
 }
+
+// The 8-wave big tile: 256 x 128, 4 x 2 waves of 64 x 64 (the 128 x 128
+// tile's wave tile), one workgroup (two waves per SIMD) per CU with a 96 KiB
+// ring.  Per 64-deep K-tile it stages 25 % fewer LDS bytes per flop than the
+// 128 x 128 tile (the L2 -> LDS stream bounds the 3x3 layers).  (A 256 x 256
+// tile of 2 x 4 waves needs 128 x 64 accumulators per wave: it spills at the
+// 256 registers two waves per SIMD leave.)  Returns false when the shape does
+// not take it.
+template <int KS, bool BT, bool PH>
+static bool launch_fwd_big(const ConvArgs& a, hipStream_t stream, ProfScope& prof, int mode) {
+  if (mode >= 1 && a.N % 128 == 0) {
+    launch_fwd_n<KS, 256, 128, BT, PH, 4, 2>(a, stream, prof);
+    return true;
+  }
+  return false;
+}
+
 // output-channel tiles of 128, or 64 for 64-channel outputs (ResNet stage 1)
 template <int KS, int BM, bool BT, bool PH>
 static void launch_fwd(const ConvArgs& a, hipStream_t stream, ProfScope& prof) {
@@ -527,10 +552,19 @@ static void launch_fwd(const ConvArgs& a, hipStream_t stream, ProfScope& prof) {
 }
 
 // tile rows: 128 (two workgroups per CU); 64 when 128-row tiles would leave
-// the chip under-filled (< 1.5 workgroups per CU); 256 rows (one workgroup per
-// CU) measured slower at every C2 shape
+// the chip under-filled (< 1.5 workgroups per CU); 256 rows of 4 waves (one
+// workgroup per CU) measured slower at every C2 shape
 template <bool BT, bool PH = false>
 static void launch_fwd_any(const ConvArgs& a, int KS, hipStream_t stream, ProfScope& prof) {
+  if (g_conv_big > 0) {  // "conv_big" 1: the 8-wave 256 x 128 tile where N % 128 == 0
+    if constexpr (PH) {
+      if (launch_fwd_big<3, BT, true>(a, stream, prof, g_conv_big)) return;
+    } else {
+      if (KS == 3 ? launch_fwd_big<3, BT, false>(a, stream, prof, g_conv_big)
+                  : launch_fwd_big<1, BT, false>(a, stream, prof, g_conv_big))
+        return;
+    }
+  }
   int bm = g_conv_bm;
   if (bm != 64 && bm != 128 && bm != 256)
     bm = (long long)((a.P + 127) / 128) * (a.N / (a.N % 128 == 0 ? 128 : 64)) < 384 ? 64 : 128;
@@ -716,6 +750,10 @@ extern "C" int rtdetr_conv_set_tuning(const char* key, int value) {
   if (key == nullptr) return fail("rtdetr_conv_set_tuning: key is NULL");
   if (std::string(key) == "conv_bm") {
     g_conv_bm = value;
+    return 0;
+  }
+  if (std::string(key) == "conv_big") {
+    g_conv_big = value;
     return 0;
   }
   if (std::string(key) == "conv_wg_stages") {

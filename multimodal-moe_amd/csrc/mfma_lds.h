@@ -91,6 +91,28 @@ __device__ __forceinline__ void compute_tile(const char* abuf, const char* bbuf,
   }
 }
 
+// The same for WGM x WGN waves: wave (wm, wn) owns rows wm BM/WGM + 16 i and
+// columns wn BN/WGN + 16 j of the tile (compute_tile is the 2 x 2 case).
+template <int BM, int BN, int WGM, int WGN, bool A_K, bool B_K>
+__device__ __forceinline__ void compute_tile_w(const char* abuf, const char* bbuf,
+                                               f32x4 (&acc)[BM / (16 * WGM)][BN / (16 * WGN)], int lane, int wm,
+                                               int wn) {
+  constexpr int TM = BM / (16 * WGM), TN = BN / (16 * WGN);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    bf16x8 af[TM], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = read_frag<BM, A_K>(abuf, wm * (BM / WGM) + 16 * i, ks, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = read_frag<BN, B_K>(bbuf, wn * (BN / WGN) + 16 * j, ks, lane);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

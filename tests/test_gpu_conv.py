@@ -41,8 +41,9 @@ def _check(got, ref, what):
 _KNOBS = {"auto": {}, "bm64_wg2_flip": dict(conv_bm=64, conv_wg_stages=2, conv_dgrad_flip=1),
           "bm128_wg3_inplace": dict(conv_bm=128, conv_wg_stages=3, conv_dgrad_flip=0, conv_wg_splits=3),
           "bm256_wg4_flip": dict(conv_bm=256, conv_wg_stages=4, conv_dgrad_flip=1, conv_wg_splits=1),
-          "zero_rows": dict(conv_dgrad_phase=0), "zero_rows_inplace": dict(conv_dgrad_phase=0, conv_dgrad_flip=0)}
-_DEFAULTS = dict(conv_bm=0, conv_wg_stages=0, conv_dgrad_flip=-1, conv_wg_splits=0, conv_dgrad_phase=1)
+          "zero_rows": dict(conv_dgrad_phase=0), "zero_rows_inplace": dict(conv_dgrad_phase=0, conv_dgrad_flip=0),
+          "big8w_flip": dict(conv_big=1, conv_dgrad_flip=1), "big8w_inplace": dict(conv_big=1, conv_dgrad_flip=0)}
+_DEFAULTS = dict(conv_bm=0, conv_wg_stages=0, conv_dgrad_flip=-1, conv_wg_splits=0, conv_dgrad_phase=1, conv_big=0)
 
 
 @pytest.mark.parametrize("knobs", list(_KNOBS))
@@ -69,7 +70,8 @@ def test_conv_large_auto_paths(hip_lib):
     _conv_case(4, 256, 256, 92, 160, 3)
 
 
-@pytest.mark.parametrize("knobs", ["auto", "bm64_wg2_flip", "bm128_wg3_inplace", "zero_rows", "zero_rows_inplace"])
+@pytest.mark.parametrize("knobs", ["auto", "bm64_wg2_flip", "bm128_wg3_inplace", "zero_rows", "zero_rows_inplace",
+                                   "big8w_flip", "big8w_inplace"])
 @pytest.mark.parametrize("B,C,N,H,W", [(2, 128, 128, 46, 80), (8, 256, 256, 23, 40), (2, 64, 128, 11, 13),
                                        (1, 256, 512, 5, 3), (2, 128, 64, 7, 9), (4, 256, 256, 92, 160)])
 def test_conv_stride2_vs_fp32(hip_lib, B, C, N, H, W, knobs):
@@ -257,3 +259,35 @@ def test_conv_stride2_dgrad_classes_match_zero_rows(hip_lib, B, C, N, H, W):
             hip_lib.rtdetr_conv_set_tuning(b"conv_dgrad_phase", 1)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+@pytest.mark.parametrize("flip", [1, 0])
+def test_conv_big_tile_bit_exact(hip_lib, stride, flip):
+    """The 8-wave 256 x 128 tile ("conv_big") runs every output element's
+    K loop in the same order as the 4-wave 128 x 128 tile: forward and data
+    gradient bit for bit equal (128-channel shapes; 64-channel outputs keep
+    the 64-wide tiles)."""
+    from src.rtdetr_moe.conv import _ConvHIP
+
+    g = torch.Generator(device=DEV).manual_seed(11 + stride)
+    B, C, N, H, W = 4, 256, 256, 46, 80
+    x = torch.randn(B, C, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(N, C, 3, 3, device=DEV, generator=g) * (C * 9) ** -0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    gy = torch.randn(B, N, Ho, Wo, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    try:
+        assert hip_lib.rtdetr_conv_set_tuning(b"conv_dgrad_flip", flip) == 0
+        for big in (0, 1):
+            assert hip_lib.rtdetr_conv_set_tuning(b"conv_big", big) == 0
+            xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+            y = _ConvHIP.apply(xa, wa, None, False, False, False, None, stride)
+            gx, = torch.autograd.grad(y, (xa,), gy)
+            torch.cuda.synchronize()
+            res.append((y, gx))
+    finally:
+        for k, v in _DEFAULTS.items():
+            hip_lib.rtdetr_conv_set_tuning(k.encode(), v)
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
