@@ -482,10 +482,13 @@ extern "C" int moe_expert_ffn_fwd(int dtype, const void* x, const int32_t* src_t
   const long long tiles = (max_rows + kFfBM - 1) / kFfBM + G;
   const long long grid = (tiles + 7) / 8 * 8;
   const size_t lds = 4 * kFfSlot;  // (+ the static bias array)
+  // exactly the dynamic bytes: static (bias) + dynamic must stay within the 160 KB a CU has, or the
+  // attribute is refused and the launch fails
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(expert_ffn_fwd_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(expert_ffn_fwd_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return fail("expert_ffn_fwd: LDS attribute refused");
     attr = true;
   }
   // algorithmic bytes: both weights + biases once; per routed row X (d), H (F) and Yp (d)

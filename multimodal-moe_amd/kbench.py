@@ -85,7 +85,8 @@ def setup(T, E, k, d, F, seed=0):
     w1q, w1s = L.quantize_mx(w1)
     w2q, w2s = L.quantize_mx(w2)
     hq, hs = L.grouped_gemm_mx(xq, xs, w1q, w1s, offsets, E, rows, F, d, L.EPI_BIAS_RELU, bias=b1, out_mx=True)
-    return dict(T=T, E=E, k=k, d=d, F=F, x=x, gate=gate, wg=wg, cb=cb, ci=ci, tpi=tpi, w1=w1, w2=w2, b1=b1, b2=b2, idx=idx,
+    _, dlogits = L.token_bwd(dxp, pos, probs, idx, w, dw, lse, None, None, wg, True)
+    return dict(dlogits=dlogits, T=T, E=E, k=k, d=d, F=F, x=x, gate=gate, wg=wg, cb=cb, ci=ci, tpi=tpi, w1=w1, w2=w2, b1=b1, b2=b2, idx=idx,
                 auxp=auxp,
                 w=w, probs=probs, lse=lse, lrank=lrank, bcnt=bcnt, rank_base=rank_base, offsets=offsets, rows=rows,
                 xp=xp, pos=pos, tok=tok, h=h, yp=yp, dy=dy, dyp=dyp, dw=dw, dh=dh, dxp=dxp,
@@ -152,6 +153,8 @@ def kernels(c):
          2.0 * A * F * d, 0),
         ("gemm_wgrad1_mx", lambda: L.grouped_gemm_wgrad_mx(c["dh"], c["xq"], c["xs"], c["offsets"], E),
          2.0 * A * F * d, 0),
+        ("router_wgrad", lambda: L.router_wgrad(c["dlogits"], c["x"], c["ci"], c["tpi"], 6), 0,
+         4 * T * E + 512 * T + 4 * (E * d + 6 * E)),
         ("token_bwd", lambda: L.token_bwd(c["dxp"], c["pos"], c["probs"], c["idx"], c["w"], c["dw"], c["lse"],
                                           None, None, c["wg"], True), 0, 512 * (A + T) + 4 * (2 * E + 3 * k) * T),
     ]

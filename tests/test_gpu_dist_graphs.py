@@ -179,7 +179,8 @@ def _ep_layer_worker(rank, world, port, out):
 
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    layer = MoEFFN(256, MoEConfig(num_experts=E_EP, top_k=K_EP, ep_size=world, expert_parallel=True)).to(dev)
+    layer = MoEFFN(256, MoEConfig(num_experts=E_EP, top_k=K_EP, ep_size=world, expert_parallel=True,
+                                   ep_capacity_factor=0.0)).to(dev)  # lossless slots
     x, ctx, dy = _ep_inputs(rank, dev)
     x.requires_grad_(True)
     y = layer(x, ctx)
@@ -216,7 +217,7 @@ def test_hip_ep_layer_two_ranks_matches_single_gpu(hip_lib, tmp_path):
     El = E_EP // W
     for r in range(W):
         got = torch.load(tmp_path / f"ep{r}.pt")
-        assert got["overflow"] == 0  # lossless exchange (default)
+        assert got["overflow"] == 0  # lossless exchange (ep_capacity_factor 0)
         x, ctx, dy = _ep_inputs(r, dev)
         x.requires_grad_(True)
         ref.zero_grad(set_to_none=True)
