@@ -157,11 +157,12 @@ int moe_token_bwd_res(const void* dxp, const int32_t* pos, const float* probs,
 
 /* Router weight gradients after moe_token_bwd_*: dwg fp32 [E,d] = dlogits^T x
  * (dlogits fp32 [T,E] from token_bwd, x bf16 [T,d] the router input, T = B
- * tpi image-major, d % 8 == 0, x 16-B aligned) and, when dcb is not NULL, the
- * context-bias gradient dcb fp32 [C,E]: row c = the sum of dlogits over the
- * tokens of the images with ctx_img[b] == c.  Two launches, fixed-order sums
- * (bitwise repeatable; replaces a torch fp32 GEMM and an atomic index_add).
- * part: fp32 scratch of B moe_router_wgrad_slices(tpi) (E d + E) floats.
+ * tpi image-major, d % 8 == 0, x and dlogits 16-B aligned) and, when dcb is
+ * not NULL, the context-bias gradient dcb fp32 [C,E]: row c = the sum of
+ * dlogits over the tokens of the images with ctx_img[b] == c.  One launch,
+ * fixed-order sums (bitwise repeatable; replaces a torch fp32 GEMM and an
+ * atomic index_add).  part is unused (may be NULL) and
+ * moe_router_wgrad_slices returns 0: both stay for the C-ABI.
  * Reference: the router backward of SURVEY 8(a) row a7. */
 int moe_router_wgrad_slices(int tpi);
 int moe_router_wgrad(const float* dlogits, const void* x, const int32_t* ctx_img, int B, int tpi, int E, int d,

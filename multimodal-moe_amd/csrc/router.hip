@@ -731,121 +731,124 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
 // ---------------------------------------------------------------------------
 // Router weight gradients (the router's backward after
 // token_bwd): dWg[e][c] = sum_t dlogits[t][e] x[t][c] and the context-bias
-// gradient dcb[ctx][e] = sum over the images b with ctx_img[b] == ctx of
-// sum_{t in b} dlogits[t][e].  Replaces torch's fp32 copy of x, the fp32 GEMM
-// dlogits^T x and the atomic index_add_ (whose arrival order made dcb
-// non-repeatable): two launches, fixed-order sums (bitwise repeatable).
-//   router_wgrad_part_kernel : one workgroup per (image, slice of <= 64
-//     tokens): the slice's x and dlogits rows staged in LDS by loads all
-//     issued up front (one round trip), thread c owns columns
-//     c, c + 256, ... of d and keeps E fp32 sums per column; slice partials
-//     [S][E][d] and [S][E] (dlogits column sums)
-//   router_wgrad_final_kernel: dWg = sum of the slice partials in slice order;
-//     workgroup 0 also forms dcb (contexts in id order, images in order)
+// gradient dcb[ctx][e] = sum of dlogits[t][e] over the tokens t of the images
+// with ctx_img[t / tpi] == ctx.  Replaces torch's fp32 copy of x, the fp32
+// GEMM dlogits^T x and the atomic index_add_ (whose arrival order made dcb
+// non-repeatable).
+//
+// One launch, no workspace: workgroup j owns the CW columns [j CW, j CW + CW)
+// of dWg for every expert (CW = 32 / EM, EM the expert count rounded up) and
+// context j of dcb.  Its 256 threads stride over ALL T tokens (thread i:
+// tokens i, i + 256, ...), U tokens' loads in flight per round (dlogits row,
+// CW x columns, the token's context), keeping E x CW + E fp32 sums; the
+// 256 per-thread sums are then added in LDS in a fixed order.  Every sum has a
+// fixed association: bitwise repeatable, and dWg does not depend on whether
+// dcb is formed.  dlogits (T E 4 B) is re-read by every workgroup from L2;
+// x is read once in total (each workgroup its own columns).
 // ---------------------------------------------------------------------------
-constexpr int kRwSlice = 64;  // tokens per slice (at most)
+template <int EM>
+struct RwCfg {
+  static constexpr int CW = EM >= 32 ? 1 : 32 / EM;        // dWg columns per workgroup
+  static constexpr int U = EM <= 16 ? 16 : (EM == 32 ? 4 : 2);  // tokens per round in flight
+  static constexpr int NV = EM * CW + EM;                  // per-thread sums: dWg block + dcb row
+  static constexpr int NVP = NV <= 64 ? 64 : 128;          // outputs rounded to a power of two
+  static constexpr int TPO = 256 / NVP;                    // threads per output in the final sum
+  static constexpr int RS = 260;                           // LDS row stride (floats): conflict-free reads
+  static constexpr size_t lds() { return (size_t)NV * RS * 4 + (size_t)NVP * TPO * 4; }
+};
 
 template <int EM>
-__global__ __launch_bounds__(256) void router_wgrad_part_kernel(const float* __restrict__ dlogits,
-                                                                const uint16_t* __restrict__ x, int tpi, int spi,
-                                                                int E, int d, float* __restrict__ part_w,
-                                                                float* __restrict__ part_c) {
+__global__ __launch_bounds__(256) void router_wgrad_kernel(const float* __restrict__ dlogits,
+                                                           const uint16_t* __restrict__ x,
+                                                           const int32_t* __restrict__ ctx_img, int T, int tpi,
+                                                           int E, int d, int C, float* __restrict__ dwg,
+                                                           float* __restrict__ dcb) {
+  using K = RwCfg<EM>;
+  constexpr int CW = K::CW, U = K::U, NV = K::NV, TPO = K::TPO, RS = K::RS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* sdl = reinterpret_cast<float*>(smem);                          // [n][E] dlogits rows
-  uint16_t* sx = reinterpret_cast<uint16_t*>(smem + kRwSlice * EM * 4);  // [n][d] x rows
-  const int s = blockIdx.x, b = s / spi, j = s - b * spi;
-  const int len = (tpi + spi - 1) / spi;
-  const int t0 = b * tpi + j * len, n = max(0, min(len, tpi - j * len));
-  const int tid = threadIdx.x;
-  // every load of the slice issued before any use: one memory round trip
-  const int nch = n * d / 8;  // 16-B chunks of the x rows (contiguous: rows t0 .. t0 + n - 1)
-  const uint4* xs = reinterpret_cast<const uint4*>(x + (size_t)t0 * d);
-  for (int q0 = tid; q0 < nch; q0 += 256 * 8) {  // 8 loads per thread in flight, then their LDS stores
-    uint4 v[8];
+  float* red = reinterpret_cast<float*>(smem);  // [NV][RS]
+  float* red2 = red + NV * RS;                   // [NVP][TPO]
+  const int tid = threadIdx.x, j = blockIdx.x;
+  const bool has_w = j * CW < d;
+  const bool has_c = dcb != nullptr && j < C;
+  const bool vec = (E & 3) == 0;
+  const int c0 = has_w ? j * CW : 0;
+  float acc[EM * CW], accb[EM];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int q = q0 + 256 * u;
-      if (q < nch) v[u] = xs[q];
-    }
+  for (int i = 0; i < EM * CW; ++i) acc[i] = 0.f;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int q = q0 + 256 * u;
-      if (q < nch) reinterpret_cast<uint4*>(sx)[q] = v[u];
-    }
-  }
-  for (int q = tid; q < n * E; q += 256) sdl[q] = dlogits[(size_t)t0 * E + q];
-  __syncthreads();
-  if (tid < E) {  // this slice's dlogits column sum (context-bias gradient), in token order
-    float cs = 0.f;
-    for (int t = 0; t < n; ++t) cs += sdl[t * E + tid];
-    part_c[(size_t)s * E + tid] = cs;
-  }
-  for (int c = tid; c < d; c += 256) {
-    float acc[EM];
+  for (int e = 0; e < EM; ++e) accb[e] = 0.f;
+  for (int t0 = tid; t0 < T; t0 += 256 * U) {
+    float dl[U][EM];
+    float xv[U][CW];
+    bool in_c[U];
+    // every load of the round first (one memory round trip per U tokens)
 #pragma unroll
-    for (int e = 0; e < EM; ++e) acc[e] = 0.f;
-    for (int t = 0; t < n; ++t) {
-      const float xv = bf2f(sx[t * d + c]);
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + 256 * u;
+      const bool ok = t < T;
+      const float* row = dlogits + (size_t)(ok ? t : 0) * E;
+      if (vec) {
 #pragma unroll
-      for (int e = 0; e < EM; ++e)
-        if (e < E) acc[e] += sdl[t * E + e] * xv;
-    }
+        for (int q = 0; q < EM / 4; ++q) {
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ok && 4 * q < E) v = reinterpret_cast<const float4*>(row)[q];
+          dl[u][4 * q] = v.x; dl[u][4 * q + 1] = v.y; dl[u][4 * q + 2] = v.z; dl[u][4 * q + 3] = v.w;
+        }
+      } else {
 #pragma unroll
-    for (int e = 0; e < EM; ++e)
-      if (e < E) part_w[((size_t)s * E + e) * d + c] = acc[e];
-  }
-}
-
-__global__ __launch_bounds__(256) void router_wgrad_final_kernel(const float* __restrict__ part_w,
-                                                                 const float* __restrict__ part_c, int S, int spi,
-                                                                 int E, int d, const int32_t* __restrict__ ctx_img,
-                                                                 int C, float* __restrict__ dwg,
-                                                                 float* __restrict__ dcb) {
-  // dWg: 64 outputs per workgroup x 4 slice groups; group q sums slices q, q + 4, ... in order, 8 loads in
-  // flight per round, then the 4 group sums are added in group order (fixed order: repeatable)
-  __shared__ float red[4][64];
-  __shared__ float pimg[2048];  // per-image dlogits sums [B][E] (B E <= 2048, host-checked)
-  const int tid = threadIdx.x, q = tid >> 6, l = tid & 63;
-  const int n = E * d;
-  const int o = blockIdx.x * 64 + l;
-  float acc = 0.f;
-  if (o < n) {
-    for (int s0 = q; s0 < S; s0 += 32) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int s = s0 + 4 * u;
-        v[u] = s < S ? part_w[(size_t)s * n + o] : 0.f;
+        for (int e = 0; e < EM; ++e) dl[u][e] = (ok && e < E) ? row[e] : 0.f;
       }
+      const uint16_t* xr = x + (size_t)(ok ? t : 0) * d + c0;
+      if constexpr (CW == 4) {
+        uint2 v = make_uint2(0u, 0u);
+        if (ok && has_w) v = *reinterpret_cast<const uint2*>(xr);
+        xv[u][0] = __uint_as_float(v.x << 16); xv[u][1] = __uint_as_float(v.x & 0xffff0000u);
+        xv[u][2] = __uint_as_float(v.y << 16); xv[u][3] = __uint_as_float(v.y & 0xffff0000u);
+      } else if constexpr (CW == 2) {
+        uint32_t v = 0u;
+        if (ok && has_w) v = *reinterpret_cast<const uint32_t*>(xr);
+        xv[u][0] = __uint_as_float(v << 16); xv[u][1] = __uint_as_float(v & 0xffff0000u);
+      } else {
+        xv[u][0] = (ok && has_w) ? bf2f(*xr) : 0.f;
+      }
+      in_c[u] = has_c && ok && ctx_img[t / tpi] == j;
+    }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u];
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int e = 0; e < EM; ++e) {
+#pragma unroll
+        for (int w = 0; w < CW; ++w) acc[e * CW + w] += dl[u][e] * xv[u][w];
+        accb[e] += in_c[u] ? dl[u][e] : 0.f;
+      }
     }
   }
-  red[q][l] = acc;
+  // fixed-order sum over the 256 threads: output o is split over TPO threads
+  // (thread p takes the sums of threads p, p + TPO, ... in order), then the TPO
+  // partials are added in order
+#pragma unroll
+  for (int i = 0; i < EM * CW; ++i) red[i * RS + tid] = acc[i];
+#pragma unroll
+  for (int e = 0; e < EM; ++e) red[(EM * CW + e) * RS + tid] = accb[e];
   __syncthreads();
-  if (q == 0 && o < n) dwg[o] = ((red[0][l] + red[1][l]) + red[2][l]) + red[3][l];
-  if (blockIdx.x != gridDim.x - 1 || dcb == nullptr) return;
-  // dcb (last workgroup): per-image sums of the slice column sums (all loads of a thread issued together),
-  // then per context the images in order
-  const int B = S / spi;
-  for (int be = tid; be < B * E; be += 256) {
-    const int bb = be / E, e = be - bb * E;
-    float v[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) v[j] = j < spi ? part_c[(size_t)(bb * spi + j) * E + e] : 0.f;
-    float sb = 0.f;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) sb += v[j];
-    for (int j = 32; j < spi; ++j) sb += part_c[(size_t)(bb * spi + j) * E + e];
-    pimg[be] = sb;
+  const int o = tid / TPO, part = tid - o * TPO;
+  if (o < NV) {
+    float s = 0.f;
+    for (int i = part; i < 256; i += TPO) s += red[o * RS + i];
+    red2[o * TPO + part] = s;
   }
   __syncthreads();
-  for (int ce = tid; ce < C * E; ce += 256) {
-    const int cx = ce / E, e = ce - cx * E;
-    float sum = 0.f;
-    for (int bb = 0; bb < B; ++bb)
-      if (ctx_img[bb] == cx) sum += pimg[bb * E + e];
-    dcb[ce] = sum;
+  if (part != 0 || o >= NV) return;
+  float s = red2[o * TPO];
+#pragma unroll
+  for (int q = 1; q < TPO; ++q) s += red2[o * TPO + q];
+  if (o < EM * CW) {
+    const int e = o / CW, w = o - e * CW;
+    if (has_w && e < E) dwg[(size_t)e * d + c0 + w] = s;
+  } else {
+    const int e = o - EM * CW;
+    if (has_c && e < E) dcb[(size_t)j * E + e] = s;
   }
 }
 
@@ -1021,54 +1024,50 @@ extern "C" int moe_aux_loss_fwd(const float* aux_partials, int nblk, int E, cons
   return check_launch("moe_aux_loss_fwd");
 }
 
-extern "C" int moe_router_wgrad_slices(int tpi) { return tpi <= 0 ? 0 : (tpi + kRwSlice - 1) / kRwSlice; }
+// (the one-launch kernel needs no workspace: kept for the C-ABI, always 0)
+extern "C" int moe_router_wgrad_slices(int tpi) { (void)tpi; return 0; }
 
 extern "C" int moe_router_wgrad(const float* dlogits, const void* x, const int32_t* ctx_img, int B, int tpi, int E,
                                 int d, int C, float* part, float* dwg, float* dcb, hipStream_t stream) {
+  (void)part;
   if (B < 0 || tpi < 1 || E < 1 || E > 64 || d < 8 || d > 1024 || d % 8 || C < 0)
     return fail("router_wgrad: need B >= 0, tpi >= 1, 1 <= E <= 64, d % 8 == 0 in [8, 1024], C >= 0");
-  if (reinterpret_cast<uintptr_t>(x) % 16) return fail("router_wgrad: x must be 16-B aligned");
-  if (dlogits == nullptr || x == nullptr || part == nullptr || dwg == nullptr)
-    return fail("router_wgrad: NULL pointer");
+  if (reinterpret_cast<uintptr_t>(x) % 16 || reinterpret_cast<uintptr_t>(dlogits) % 16)
+    return fail("router_wgrad: x and dlogits must be 16-B aligned");
+  if (dlogits == nullptr || x == nullptr || dwg == nullptr) return fail("router_wgrad: NULL pointer");
   if (dcb != nullptr && (ctx_img == nullptr || C < 1)) return fail("router_wgrad: dcb needs ctx_img and C >= 1");
-  if (dcb != nullptr && B * E > 2048) return fail("router_wgrad: B E must be <= 2048 with a context-bias gradient");
-  const int spi = moe_router_wgrad_slices(tpi);
-  const int S = B * spi;
-  if (S == 0) {  // no tokens: zero gradients
+  if ((long long)B * tpi > 0x7fffffffLL / 1024) return fail("router_wgrad: too many tokens");
+  const int T = B * tpi;
+  if (T == 0) {  // no tokens: zero gradients
     if (hipMemsetAsync(dwg, 0, sizeof(float) * E * d, stream) != hipSuccess) return fail("router_wgrad: memset");
     if (dcb != nullptr && hipMemsetAsync(dcb, 0, sizeof(float) * C * E, stream) != hipSuccess)
       return fail("router_wgrad: memset");
     return 0;
   }
-  float* part_w = part;
-  float* part_c = part + (size_t)S * E * d;
-  const double T = (double)B * tpi;
-  {
-    ProfScope prof(stream, PROF_ROUTER_WGRAD, 4.0 * T * E + 2.0 * T * d + 4.0 * S * E * (d + 1));
-    const int em = E <= 8 ? 8 : (E <= 16 ? 16 : (E <= 32 ? 32 : 64));
-    const size_t lds = (size_t)kRwSlice * em * 4 + (size_t)kRwSlice * d * 2;
+  // bytes: dlogits and x once, dWg and dcb written (+ one context id per token)
+  ProfScope prof(stream, PROF_ROUTER_WGRAD,
+                 4.0 * T * E + 2.0 * T * d + 4.0 * E * d + (dcb != nullptr ? 4.0 * C * E + 4.0 * B : 0.0));
 #define LAUNCH_RW(EM_)                                                                                        \
   do {                                                                                                        \
-    static bool lds_set = false; /* > 64 KiB of dynamic LDS needs the attribute (d > 384) */                   \
+    using K = RwCfg<EM_>;                                                                                     \
+    const int ncb = d / K::CW;                                                                                \
+    const int grid = dcb != nullptr && C > ncb ? C : ncb;                                                     \
+    static bool lds_set = false; /* > 64 KiB of dynamic LDS at E > 32 */                                      \
     if (!lds_set) {                                                                                           \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(router_wgrad_part_kernel<EM_>),                 \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);                      \
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(router_wgrad_kernel<EM_>),                        \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::lds()) != hipSuccess)       \
+        return fail("router_wgrad: LDS attribute refused");                                                   \
       lds_set = true;                                                                                         \
     }                                                                                                         \
-    MOE_LAUNCH(prof, router_wgrad_part_kernel<EM_>, dim3(S), dim3(256), lds, stream, dlogits,                 \
-               static_cast<const uint16_t*>(x), tpi, spi, E, d, part_w, part_c);                              \
+    MOE_LAUNCH(prof, router_wgrad_kernel<EM_>, dim3(grid), dim3(256), K::lds(), stream, dlogits,              \
+               static_cast<const uint16_t*>(x), ctx_img, T, tpi, E, d, C, dwg, dcb);                          \
   } while (0)
-    switch (em) {
-      case 8: LAUNCH_RW(8); break;
-      case 16: LAUNCH_RW(16); break;
-      case 32: LAUNCH_RW(32); break;
-      default: LAUNCH_RW(64); break;
-    }
-#undef LAUNCH_RW
-    if (int rc = check_launch("moe_router_wgrad (part)")) return rc;
+  switch (emax_for(E)) {
+    case 8: LAUNCH_RW(8); break;
+    case 16: LAUNCH_RW(16); break;
+    case 32: LAUNCH_RW(32); break;
+    default: LAUNCH_RW(64); break;
   }
-  ProfScope prof(stream, PROF_ROUTER_WGRAD, 4.0 * S * E * (d + 1) + 4.0 * E * d + 4.0 * C * E);
-  MOE_LAUNCH(prof, router_wgrad_final_kernel, dim3((E * d + 63) / 64), dim3(256), 0, stream, part_w, part_c, S,
-             spi, E, d, ctx_img, C, dwg, dcb);
+#undef LAUNCH_RW
   return check_launch("moe_router_wgrad");
 }

@@ -620,15 +620,13 @@ def router_wgrad(dlogits, x, ctx_img, tokens_per_image, n_ctx):
     if tpi <= 0 or T % tpi:
         raise MoEKernelError(f"router_wgrad: T = {T} is not a multiple of tokens_per_image = {tpi}")
     B = T // tpi
-    S = B * int(lib().moe_router_wgrad_slices(tpi))
-    part = torch.empty(max(1, S * E * (d + 1)), dtype=torch.float32, device=x.device)
     dwg = torch.empty((E, d), dtype=torch.float32, device=x.device)
     dcb = None
     if has_ctx:
         _need(ctx_img, torch.int32, "ctx_img")
         dcb = torch.empty((n_ctx, E), dtype=torch.float32, device=x.device)
     _check(lib().moe_router_wgrad(_ptr(dlogits), _ptr(x), _ptr(ctx_img) if dcb is not None else None, B, tpi, E, d,
-                                  int(n_ctx) if dcb is not None else 0, _ptr(part), _ptr(dwg), _ptr(dcb), _stream()),
+                                  int(n_ctx) if dcb is not None else 0, None, _ptr(dwg), _ptr(dcb), _stream()),
            "moe_router_wgrad")
     return dwg, dcb
 

@@ -113,7 +113,7 @@ class _RouteDispatch(torch.autograd.Function):
         else:
             dprob_bias, zc = None, None
         dx, dlogits = L.token_bwd(d_xp, pos_use, probs, idx, w, d_w, lse, dprob_bias, zc, wg32, normalize)
-        # router weight + context-bias gradients: two HIP launches, fixed-order sums
+        # router weight + context-bias gradients: one HIP launch, fixed-order sums
         dwg, dcb = L.router_wgrad(dlogits, xb, ctx_img if has_ctx else None, tpi, C if has_ctx else 0)
         return dx.to(xdtype), dwg, dcb, None, None, None, None, None, None, None
 
@@ -393,8 +393,8 @@ class _MoELayer(torch.autograd.Function):
                combine transpose launch); bwd_pair {dXp = dH W1, dW1 = dH^T
                x[token], db1}; token_bwd_dw (gate gradient <dy, Yp>, router
                softmax / top-k / aux / z-loss backward, dx)
-    plus the router weight and context-bias gradients (moe_router_wgrad: two
-    launches, fixed-order sums).  Outputs: y, then (weighted=True) the
+    plus the router weight and context-bias gradients (moe_router_wgrad: one
+    launch, fixed-order sums).  Outputs: y, then (weighted=True) the
     layer's lb_coef lb + z_coef z and the detached raw (lb, z), or
     (weighted=False) lb and z as separate differentiable outputs; hist.
     residual=True (x in bf16): y = x + FFN(x) -- the caller's residual add
@@ -464,7 +464,7 @@ class _MoELayer(torch.autograd.Function):
             zc = (2.0 * g_b.float() * wcoef[E:E + 1]).contiguous() if g_b is not None else None
         dx, dlogits, _ = L.token_bwd_dw(dxp, pos, probs, idx, w, dyb, yp, lse, dprob_bias, zc, wg32, normalize,
                                         dres=dyb if ctx.residual else None)
-        # router weight + context-bias gradients: two HIP launches, fixed-order sums
+        # router weight + context-bias gradients: one HIP launch, fixed-order sums
         dwg, dcb = L.router_wgrad(dlogits, xb, ctx_img if has_ctx else None, tpi, C if has_ctx else 0)
         return (dx.to(xdtype), dwg, dcb, dW1, db1, dW2, db2) + (None,) * 9
 
