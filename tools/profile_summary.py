@@ -23,14 +23,15 @@ import sys
 from pathlib import Path
 
 GROUPS = [
-    ("grouped_gemm", re.compile(r"gemm_v\d_kernel|gemm_pair_kernel")),
+    ("grouped_gemm", re.compile(r"gemm_v\d_kernel|gemm_pair_kernel|expert_ffn_fwd_kernel")),
     ("linear_wgrad", re.compile(r"linear_wgrad_kernel")),
     ("dispatch", re.compile(r"permute_fwd(_mx)?_kernel|combine_fwd_kernel|combine_bwd_kernel")),
     ("router", re.compile(r"router_topk_fwd_kernel")),
     ("route_scan", re.compile(r"route_scan_kernel|route_dispatch_kernel|route_index_kernel")),
     ("quantize_mx", re.compile(r"quantize_mx_kernel")),
     ("token_bwd", re.compile(r"token_bwd_kernel")),
-    ("msda", re.compile(r"msda_(fwd|bwd)_kernel")),
+    ("router_wgrad", re.compile(r"router_wgrad_kernel")),
+    ("msda", re.compile(r"msda_(fused_)?(fwd|bwd)(_lp)?_kernel|msda_vgrad_(sort|tile)_kernel")),
 ]
 
 
