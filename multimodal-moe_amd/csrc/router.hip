@@ -772,7 +772,7 @@ __global__ __launch_bounds__(256) void router_wgrad_kernel(const float* __restri
   const bool has_w = j * CW < d;
   const bool has_c = dcb != nullptr && j < C;
   const bool vec = (E & 3) == 0;
-  const int c0 = has_w ? j * CW : 0;
+  const int c0 = has_w ? j * CW : 0;  // (a context-only workgroup reads column 0, unused)
   float acc[EM * CW], accb[EM];
 #pragma unroll
   for (int i = 0; i < EM * CW; ++i) acc[i] = 0.f;
@@ -781,46 +781,47 @@ __global__ __launch_bounds__(256) void router_wgrad_kernel(const float* __restri
   for (int t0 = tid; t0 < T; t0 += 256 * U) {
     float dl[U][EM];
     float xv[U][CW];
-    bool in_c[U];
-    // every load of the round first (one memory round trip per U tokens)
+    int ci[U];
+    // every load of the round first, from clamped (always valid) addresses, with
+    // no use in between -- one memory round trip per U tokens (a use of any one
+    // load waits for all loads issued before it)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int t = t0 + 256 * u;
-      const bool ok = t < T;
-      const float* row = dlogits + (size_t)(ok ? t : 0) * E;
+      const int tc = min(t0 + 256 * u, T - 1);
+      const float* row = dlogits + (size_t)tc * E;
       if (vec) {
 #pragma unroll
         for (int q = 0; q < EM / 4; ++q) {
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (ok && 4 * q < E) v = reinterpret_cast<const float4*>(row)[q];
+          const float4 v = reinterpret_cast<const float4*>(row)[min(q, (E >> 2) - 1)];
           dl[u][4 * q] = v.x; dl[u][4 * q + 1] = v.y; dl[u][4 * q + 2] = v.z; dl[u][4 * q + 3] = v.w;
         }
       } else {
 #pragma unroll
-        for (int e = 0; e < EM; ++e) dl[u][e] = (ok && e < E) ? row[e] : 0.f;
+        for (int e = 0; e < EM; ++e) dl[u][e] = row[min(e, E - 1)];
       }
-      const uint16_t* xr = x + (size_t)(ok ? t : 0) * d + c0;
+      const uint16_t* xr = x + (size_t)tc * d + c0;
       if constexpr (CW == 4) {
-        uint2 v = make_uint2(0u, 0u);
-        if (ok && has_w) v = *reinterpret_cast<const uint2*>(xr);
+        const uint2 v = *reinterpret_cast<const uint2*>(xr);
         xv[u][0] = __uint_as_float(v.x << 16); xv[u][1] = __uint_as_float(v.x & 0xffff0000u);
         xv[u][2] = __uint_as_float(v.y << 16); xv[u][3] = __uint_as_float(v.y & 0xffff0000u);
       } else if constexpr (CW == 2) {
-        uint32_t v = 0u;
-        if (ok && has_w) v = *reinterpret_cast<const uint32_t*>(xr);
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(xr);
         xv[u][0] = __uint_as_float(v << 16); xv[u][1] = __uint_as_float(v & 0xffff0000u);
       } else {
-        xv[u][0] = (ok && has_w) ? bf2f(*xr) : 0.f;
+        xv[u][0] = bf2f(*xr);
       }
-      in_c[u] = has_c && ok && ctx_img[t / tpi] == j;
+      ci[u] = has_c ? ctx_img[tc / tpi] : -1;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      const bool ok = t0 + 256 * u < T;
+      const bool in_c = ok && ci[u] == j;
 #pragma unroll
       for (int e = 0; e < EM; ++e) {
+        const float g = (ok && e < E) ? dl[u][e] : 0.f;
 #pragma unroll
-        for (int w = 0; w < CW; ++w) acc[e * CW + w] += dl[u][e] * xv[u][w];
-        accb[e] += in_c[u] ? dl[u][e] : 0.f;
+        for (int w = 0; w < CW; ++w) acc[e * CW + w] += g * xv[u][w];
+        accb[e] += in_c ? g : 0.f;
       }
     }
   }

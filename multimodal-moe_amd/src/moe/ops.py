@@ -46,6 +46,7 @@ def _bias(b):
 
 # MOE_FUSED_FFN=0: the expert FFN forward as two grouped GEMMs (A/B switch)
 _FUSED_FFN = os.environ.get("MOE_FUSED_FFN", "1") != "0"
+_FUSED_MIN_ROWS = int(os.environ.get("MOE_FUSED_FFN_MIN_ROWS", "1536"))
 
 
 def _ffn_forward(xb, tok, w1b, b1, w2b, b2, offsets, G, rows):
@@ -54,7 +55,11 @@ def _ffn_forward(xb, tok, w1b, b1, w2b, b2, offsets, G, rows):
     (gathering token rows when ``tok`` is given) and GEMM2 as two launches."""
     F, d = w1b.shape[1], w1b.shape[2]
     bb1, bb2 = _bias(b1), _bias(b2)
-    if _FUSED_FFN and bb1.dtype == bb2.dtype and L.expert_ffn_supported(G, F, d):
+    # fused only for >= 1,536 rows per expert on average: every workgroup streams its expert's whole
+    # W1 and W2, so at the C2 decoder's 600 rows / expert the one-round grid is latency-bound (kbench
+    # cold, profiles/r04/kbench: decoder 41.0 us fused vs 11.8 + 14.1 us; encoder 45.6 vs 25.9 + 21.5)
+    if (_FUSED_FFN and bb1.dtype == bb2.dtype and L.expert_ffn_supported(G, F, d)
+            and rows >= _FUSED_MIN_ROWS * G):
         return L.expert_ffn_fwd(xb, tok, w1b, bb1, w2b, bb2, offsets, G, rows)
     if tok is not None:
         h = L.grouped_gemm_gather(xb, tok, w1b, offsets, G, rows, F, d, 1, L.EPI_BIAS_RELU, bias=bb1)
