@@ -738,47 +738,48 @@ __global__ __launch_bounds__(256) void token_bwd_kernel(
 //
 // One launch, no workspace: workgroup j owns the CW columns [j CW, j CW + CW)
 // of dWg for every expert (CW = 32 / EM, EM the expert count rounded up) and
-// context j of dcb.  Its 256 threads stride over ALL T tokens (thread i:
-// tokens i, i + 256, ...), U tokens' loads in flight per round (dlogits row,
-// CW x columns, the token's context), keeping E x CW + E fp32 sums; the
-// 256 per-thread sums are then added in LDS in a fixed order.  Every sum has a
-// fixed association: bitwise repeatable, and dWg does not depend on whether
-// dcb is formed.  dlogits (T E 4 B) is re-read by every workgroup from L2;
-// x is read once in total (each workgroup its own columns).
+// context j of dcb.  Its NT threads (1,024 for E <= 16, else 256) stride over
+// ALL T tokens (thread i: tokens i, i + NT, ...), U tokens' loads in flight
+// per round (dlogits row, CW x columns, the token's context), keeping
+// E x CW + E fp32 sums; the per-thread sums are then added in LDS in a fixed
+// order.  Every sum has a fixed association: bitwise repeatable, and dWg does
+// not depend on whether dcb is formed.  dlogits (T E 4 B) is re-read by every
+// workgroup from L2; x is read once in total (each workgroup its own columns).
 // ---------------------------------------------------------------------------
 template <int EM>
 struct RwCfg {
-  static constexpr int CW = EM >= 32 ? 1 : 32 / EM;        // dWg columns per workgroup
-  static constexpr int U = EM <= 16 ? 16 : (EM == 32 ? 4 : 2);  // tokens per round in flight
-  static constexpr int NV = EM * CW + EM;                  // per-thread sums: dWg block + dcb row
-  static constexpr int NVP = NV <= 64 ? 64 : 128;          // outputs rounded to a power of two
-  static constexpr int TPO = 256 / NVP;                    // threads per output in the final sum
-  static constexpr int RS = 260;                           // LDS row stride (floats): conflict-free reads
+  static constexpr int CW = EM >= 32 ? 1 : 32 / EM;          // dWg columns per workgroup
+  static constexpr int NT = EM <= 16 ? 1024 : 256;            // threads (16 waves: 4 per SIMD at <= 128 VGPRs)
+  static constexpr int U = EM == 8 ? 4 : (EM == 16 ? 2 : (EM == 32 ? 4 : 2));  // tokens per round in flight
+  static constexpr int NV = EM * CW + EM;                    // per-thread sums: dWg block + dcb row
+  static constexpr int NVP = NV <= 64 ? 64 : 128;            // outputs rounded to a power of two
+  static constexpr int TPO = 256 / NVP;                      // threads per output in the final sum
+  static constexpr int RS = 260;                             // LDS row stride (floats): conflict-free reads
   static constexpr size_t lds() { return (size_t)NV * RS * 4 + (size_t)NVP * TPO * 4; }
 };
 
-template <int EM>
-__global__ __launch_bounds__(256) void router_wgrad_kernel(const float* __restrict__ dlogits,
-                                                           const uint16_t* __restrict__ x,
-                                                           const int32_t* __restrict__ ctx_img, int T, int tpi,
-                                                           int E, int d, int C, float* __restrict__ dwg,
-                                                           float* __restrict__ dcb) {
+template <int EM, bool VEC>
+__global__ __launch_bounds__(RwCfg<EM>::NT) void router_wgrad_kernel(const float* __restrict__ dlogits,
+                                                                     const uint16_t* __restrict__ x,
+                                                                     const int32_t* __restrict__ ctx_img, int T,
+                                                                     int tpi, int E, int d, int C,
+                                                                     float* __restrict__ dwg,
+                                                                     float* __restrict__ dcb) {
   using K = RwCfg<EM>;
-  constexpr int CW = K::CW, U = K::U, NV = K::NV, TPO = K::TPO, RS = K::RS;
+  constexpr int CW = K::CW, NT = K::NT, U = K::U, NV = K::NV, TPO = K::TPO, RS = K::RS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem);  // [NV][RS]
+  float* red = reinterpret_cast<float*>(smem);  // [NV][RS]: slot i holds the sum of threads i, i + 256, ...
   float* red2 = red + NV * RS;                   // [NVP][TPO]
   const int tid = threadIdx.x, j = blockIdx.x;
   const bool has_w = j * CW < d;
   const bool has_c = dcb != nullptr && j < C;
-  const bool vec = (E & 3) == 0;
   const int c0 = has_w ? j * CW : 0;  // (a context-only workgroup reads column 0, unused)
   float acc[EM * CW], accb[EM];
 #pragma unroll
   for (int i = 0; i < EM * CW; ++i) acc[i] = 0.f;
 #pragma unroll
   for (int e = 0; e < EM; ++e) accb[e] = 0.f;
-  for (int t0 = tid; t0 < T; t0 += 256 * U) {
+  for (int t0 = tid; t0 < T; t0 += NT * U) {
     float dl[U][EM];
     float xv[U][CW];
     int ci[U];
@@ -787,9 +788,9 @@ __global__ __launch_bounds__(256) void router_wgrad_kernel(const float* __restri
     // load waits for all loads issued before it)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int tc = min(t0 + 256 * u, T - 1);
+      const int tc = min(t0 + NT * u, T - 1);
       const float* row = dlogits + (size_t)tc * E;
-      if (vec) {
+      if constexpr (VEC) {  // E % 4 == 0: 16-B loads (a runtime branch here was merged into dword loads)
 #pragma unroll
         for (int q = 0; q < EM / 4; ++q) {
           const float4 v = reinterpret_cast<const float4*>(row)[min(q, (E >> 2) - 1)];
@@ -814,7 +815,7 @@ __global__ __launch_bounds__(256) void router_wgrad_kernel(const float* __restri
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool ok = t0 + 256 * u < T;
+      const bool ok = t0 + NT * u < T;
       const bool in_c = ok && ci[u] == j;
 #pragma unroll
       for (int e = 0; e < EM; ++e) {
@@ -825,31 +826,43 @@ __global__ __launch_bounds__(256) void router_wgrad_kernel(const float* __restri
       }
     }
   }
-  // fixed-order sum over the 256 threads: output o is split over TPO threads
-  // (thread p takes the sums of threads p, p + TPO, ... in order), then the TPO
-  // partials are added in order
+  // fixed-order sum over the NT threads: the groups of 256 threads add their
+  // sums into the 256 slots one group after another (slot i = thread i +
+  // thread i + 256 + ...); output o is then split over TPO threads (thread p
+  // takes slots p, p + TPO, ... in order) and the TPO partials added in order
 #pragma unroll
-  for (int i = 0; i < EM * CW; ++i) red[i * RS + tid] = acc[i];
+  for (int q = 0; q < NT / 256; ++q) {
+    if (tid / 256 == q) {
+      const int sl = tid & 255;
 #pragma unroll
-  for (int e = 0; e < EM; ++e) red[(EM * CW + e) * RS + tid] = accb[e];
-  __syncthreads();
-  const int o = tid / TPO, part = tid - o * TPO;
-  if (o < NV) {
-    float s = 0.f;
-    for (int i = part; i < 256; i += TPO) s += red[o * RS + i];
-    red2[o * TPO + part] = s;
+      for (int i = 0; i < EM * CW; ++i) red[i * RS + sl] = q == 0 ? acc[i] : red[i * RS + sl] + acc[i];
+#pragma unroll
+      for (int e = 0; e < EM; ++e)
+        red[(EM * CW + e) * RS + sl] = q == 0 ? accb[e] : red[(EM * CW + e) * RS + sl] + accb[e];
+    }
+    __syncthreads();
+  }
+  const int o = tid / TPO, part = tid - o * TPO;  // (threads 256 .. NT - 1 only pass the barrier)
+  if (tid < 256 && o < NV) {
+    float v[256 / TPO];  // all reads first, then the fixed-order sum
+#pragma unroll
+    for (int i = 0; i < 256 / TPO; ++i) v[i] = red[o * RS + part + TPO * i];
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 256 / TPO; ++i) sum += v[i];
+    red2[o * TPO + part] = sum;
   }
   __syncthreads();
-  if (part != 0 || o >= NV) return;
-  float s = red2[o * TPO];
+  if (tid >= 256 || part != 0 || o >= NV) return;
+  float sum = red2[o * TPO];
 #pragma unroll
-  for (int q = 1; q < TPO; ++q) s += red2[o * TPO + q];
+  for (int q = 1; q < TPO; ++q) sum += red2[o * TPO + q];
   if (o < EM * CW) {
     const int e = o / CW, w = o - e * CW;
-    if (has_w && e < E) dwg[(size_t)e * d + c0 + w] = s;
+    if (has_w && e < E) dwg[(size_t)e * d + c0 + w] = sum;
   } else {
     const int e = o - EM * CW;
-    if (has_c && e < E) dcb[(size_t)j * E + e] = s;
+    if (has_c && e < E) dcb[(size_t)j * E + e] = sum;
   }
 }
 
@@ -1055,13 +1068,19 @@ extern "C" int moe_router_wgrad(const float* dlogits, const void* x, const int32
     const int grid = dcb != nullptr && C > ncb ? C : ncb;                                                     \
     static bool lds_set = false; /* > 64 KiB of dynamic LDS at E > 32 */                                      \
     if (!lds_set) {                                                                                           \
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(router_wgrad_kernel<EM_>),                        \
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(router_wgrad_kernel<EM_, true>),                  \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::lds()) != hipSuccess ||     \
+          hipFuncSetAttribute(reinterpret_cast<const void*>(router_wgrad_kernel<EM_, false>),                 \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::lds()) != hipSuccess)       \
         return fail("router_wgrad: LDS attribute refused");                                                   \
       lds_set = true;                                                                                         \
     }                                                                                                         \
-    MOE_LAUNCH(prof, router_wgrad_kernel<EM_>, dim3(grid), dim3(256), K::lds(), stream, dlogits,              \
-               static_cast<const uint16_t*>(x), ctx_img, T, tpi, E, d, C, dwg, dcb);                          \
+    if (E % 4 == 0)                                                                                           \
+      MOE_LAUNCH(prof, (router_wgrad_kernel<EM_, true>), dim3(grid), dim3(K::NT), K::lds(), stream, dlogits,    \
+                 static_cast<const uint16_t*>(x), ctx_img, T, tpi, E, d, C, dwg, dcb);                        \
+    else                                                                                                      \
+      MOE_LAUNCH(prof, (router_wgrad_kernel<EM_, false>), dim3(grid), dim3(K::NT), K::lds(), stream, dlogits,   \
+                 static_cast<const uint16_t*>(x), ctx_img, T, tpi, E, d, C, dwg, dcb);                        \
   } while (0)
   switch (emax_for(E)) {
     case 8: LAUNCH_RW(8); break;
