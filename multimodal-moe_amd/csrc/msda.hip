@@ -633,139 +633,248 @@ __global__ __launch_bounds__(256) void msda_fused_bwd_lp_kernel(
 // ---------------------------------------------------------------------------
 // Deterministic value gradient (REC mode).  The recorded corner contributions
 // of every (b, h, level) group -- n = Q PP 4 of them, in (q, p, c) order --
-// are bucketed by destination tile of R value rows (stable counting sort, one
-// workgroup per group: thread t owns the contiguous entries [t k, (t+1) k),
-// per-thread tile counts in LDS, one exclusive scan, then an in-order
-// scatter), and each tile's workgroup sums its entries into an fp32 LDS image
-// of the tile's rows in that order, rounding once to bf16.  Every element of
-// the gradient is written (untouched rows get zeros: no memset), every sum
-// has a fixed order (bitwise repeatable), and the accumulation is fp32 -- the
+// are bucketed by destination tile of kVgRows value rows (a stable counting
+// sort, one workgroup per group, ballot ranks per round of 256 entries).  Each tile's workgroup then takes its entries in chunks
+// of kVgChunk (in entry order): sorts the chunk by (row, entry) in LDS
+// (ballot peer ranks + a row scan: the order is a pure function of the
+// entries), forms every entry's fp32 product w x grad_out[q] in parallel (all loads of
+// a thread issued together), and each 32-lane group adds the products of its
+// rows (rows r % 8 == group) in sorted order into registers -- row-parallel,
+// with no dependent memory access inside a row's sum.  Every element of the
+// gradient is written (untouched rows get zeros: no memset), every sum has a
+// fixed order (bitwise repeatable), and the accumulation is fp32 -- the
 // atomic path added bf16 pairs in arrival order.
 // ---------------------------------------------------------------------------
-constexpr int kVgTilesMax = 64;
-constexpr int kVgSortThreads = 128;
+constexpr int kVgTilesMax = 128;  // tiles per level (levels up to kVgRows x 128 = 32,768 rows)
+constexpr int kVgRows = 256;      // value rows per tile, at most (levels of < 16 x 256 rows take fewer)
+constexpr int kVgChunk = 256;     // entries per sorted chunk
 
-__global__ __launch_bounds__(kVgSortThreads) void msda_vgrad_sort_kernel(const int2* __restrict__ rec,
-                                                              const int32_t* __restrict__ shapes, int H, int L, int n,
-                                                              int R, int4* __restrict__ sorted,
+// Per-level tiling, by value (kernel arguments: no memory load to find a
+// tile): every level holds the same Q P 4 entries per (b, h), so the small
+// levels get smaller tiles (R = 16 .. 256 rows, at least 16 tiles where the
+// level allows), spreading their many entries per row over more workgroups.
+struct VgLevels {
+  int hw[4], R[4], nt[4], start[4];
+};
+
+// Stable bucketing of a group's entries by tile: 256 entries per round, one
+// per thread; within a wave the lanes of one tile are found from 7 ballots of
+// the tile bits (rank = peers below the lane).  Pass 1 records every (round,
+// wave, tile) count, a per-tile walk over (round, wave) turns them into
+// offsets, a scan over tiles gives the tile bases, and pass 2 recomputes the
+// ranks and scatters -- entry order kept within a tile, no serial chain per
+// thread (each thread's rec loads are issued four rounds at a time).
+__global__ __launch_bounds__(256) void msda_vgrad_sort_kernel(const int2* __restrict__ rec, VgLevels lv, int L,
+                                                              int n, int4* __restrict__ sorted,
                                                               int32_t* __restrict__ toff) {
-  constexpr int NTH = kVgSortThreads;
-  __shared__ int cnt[kVgTilesMax * NTH];  // [tile][thread]
-  __shared__ int part[NTH];
-  const int grp = blockIdx.x, l = grp % L, tid = threadIdx.x;
-  const int hw = shapes[2 * l] * shapes[2 * l + 1];
-  const int nt = (hw + R - 1) / R;
-  const int k = (n + NTH - 1) / NTH, e0 = tid * k, e1 = min(n, e0 + k);
+  extern __shared__ __attribute__((aligned(16))) int vsm[];
+  const int grp = blockIdx.x, l = grp % L, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int R = lv.R[l], nt = lv.nt[l], NR = (n + 255) / 256;
+  int* cnt = vsm;                  // [NR][4][nt]: counts, then offsets within the tile
+  int* base = vsm + NR * 4 * nt;   // [nt]
+  int* wtot = base + kVgTilesMax;  // [4]
   const int2* src = rec + (size_t)grp * n;
-  for (int t = 0; t < nt; ++t) cnt[t * NTH + tid] = 0;
-  for (int e = e0; e < e1; ++e) {
-    const int row = src[e].x;
-    if (row >= 0) cnt[(row / R) * NTH + tid] += 1;
-  }
+  for (int i = tid; i < NR * 4 * nt; i += 256) cnt[i] = 0;
   __syncthreads();
-  // exclusive scan of cnt in (tile, thread) order, i.e. memory order: thread t
-  // takes the nt consecutive elements [t nt, (t+1) nt) (nt NTH in all)
-  int loc = 0;
-  for (int i = 0; i < nt; ++i) loc += cnt[tid * nt + i];
-  part[tid] = loc;
-  __syncthreads();
-  if (tid == 0) {
-    int run = 0;
-    for (int i = 0; i < NTH; ++i) {
-      const int v = part[i];
-      part[i] = run;
-      run += v;
+  // one round: the tile of this thread's entry and its rank among the wave's lanes of that tile
+  auto rank_of = [&](int row, bool valid, int& tile, uint64_t& peers) {
+    tile = valid ? row / R : 0;
+    peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 7; ++bit) {
+      const bool on = (tile >> bit) & 1;
+      const uint64_t bb = __ballot(valid && on);
+      peers &= on ? bb : ~bb;
     }
-  }
-  __syncthreads();
-  int run = part[tid];
-  for (int i = 0; i < nt; ++i) {
-    const int v = cnt[tid * nt + i];
-    cnt[tid * nt + i] = run;
-    run += v;
-  }
-  __syncthreads();
-  int32_t* to = toff + (size_t)grp * (kVgTilesMax + 1);
-  for (int t = tid; t < nt; t += NTH) to[t] = cnt[t * NTH];
-  if (tid == NTH - 1) to[nt] = run;  // the total: the last thread's running sum
-  int4* dst = sorted + (size_t)grp * n;
-  for (int e = e0; e < e1; ++e) {  // in entry order: stable
-    const int2 v = src[e];
-    if (v.x < 0) continue;
-    const int slot = (v.x / R) * NTH + tid;
-    const int pos = cnt[slot];
-    cnt[slot] = pos + 1;
-    dst[pos] = make_int4(v.x, v.y, e, 0);
+    return __popcll(peers & ((1ull << lane) - 1ull));
+  };
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int rd0 = 0; rd0 < NR; rd0 += 4) {
+      int2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // four rounds' loads in flight
+        const int e = (rd0 + u) * 256 + tid;
+        v[u] = (rd0 + u < NR && e < n) ? src[e] : make_int2(-1, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (rd0 + u >= NR) break;
+        const bool valid = v[u].x >= 0;
+        int tile;
+        uint64_t peers;
+        const int rank = rank_of(v[u].x, valid, tile, peers);
+        int* c = cnt + ((rd0 + u) * 4 + wave) * nt + tile;
+        if (pass == 0) {
+          if (valid && rank == 0) *c = __popcll(peers);
+        } else if (valid) {
+          sorted[(size_t)grp * n + base[tile] + *c + rank] = make_int4(v[u].x, v[u].y, (rd0 + u) * 256 + tid, 0);
+        }
+      }
+    }
+    if (pass == 1) break;
+    __syncthreads();
+    // per tile (thread = tile): offsets over (round, wave) in order, then the scan over tiles
+    int tot = 0;
+    if (tid < nt) {
+      for (int i = 0; i < NR * 4; ++i) {
+        const int c = cnt[i * nt + tid];
+        cnt[i * nt + tid] = tot;
+        tot += c;
+      }
+    }
+    int inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int x = __shfl_up(inc, o);
+      if (lane >= o) inc += x;
+    }
+    if (lane == 63) wtot[wave] = inc;
+    __syncthreads();
+    int b0 = 0;
+    for (int w = 0; w < wave; ++w) b0 += wtot[w];
+    int32_t* to = toff + (size_t)grp * (kVgTilesMax + 1);
+    if (tid < nt) {
+      base[tid] = b0 + inc - tot;
+      to[tid] = b0 + inc - tot;
+    }
+    if (tid == nt - 1) to[nt] = b0 + inc;
+    __syncthreads();
   }
 }
 
-// One workgroup per (b, h, level, tile of R rows).  Threads: 8 groups of 32
-// lanes; group k owns the tile rows r with r % 8 == k (so two entries of one
-// row are always added by the same lanes, in entry order); a lane owns D / 32
-// channels.  Entries and their grad_out rows are staged in LDS by chunks.
+// One workgroup per (b, h, level, tile of R <= 256 rows); 8 groups of 32
+// lanes, group g owns the tile rows r % 8 == g (up to 32 row sums per lane of
+// D / 32 channels each, in registers across chunks).  A chunk holds one entry
+// per thread and is sorted by (row, entry) with no comparison sort: each wave
+// finds the lanes holding the same row from 8 ballots of the row bits (rank =
+// the peers below the lane), the per-wave row counts are scanned over the
+// rows, and every entry lands at rowstart + earlier waves' count + rank.  The
+// grad_out rows of the sorted chunk are staged in LDS (bf16) with their
+// weights, so a row's sum reads only LDS; the next chunk's entries are loaded
+// before this chunk is summed.
 template <int D>
 __global__ __launch_bounds__(256) void msda_vgrad_tile_kernel(const int4* __restrict__ sorted,
-                                                              const int32_t* __restrict__ toff,
-                                                              const int32_t* __restrict__ shapes,
-                                                              const int32_t* __restrict__ starts,
-                                                              const uint16_t* __restrict__ grad_out, int B, int S,
-                                                              int Q, int H, int L, int P, int R, int tiles_bh,
-                                                              long long ldv, uint16_t* __restrict__ grad_value) {
+                                                              const int32_t* __restrict__ toff, VgLevels lv,
+                                                              const uint16_t* __restrict__ grad_out, int S, int Q,
+                                                              int H, int L, int P, int tiles_bh, long long ldv,
+                                                              uint16_t* __restrict__ grad_value) {
+  constexpr int CH = kVgChunk, RPG = kVgRows / 8;
+  constexpr int DL = D / 32;   // channels per lane
+  constexpr int PPR = D / 8;   // 16-B pieces per grad_out row
+  static_assert(CH == 256 && kVgRows == 256, "one entry per thread, one row per thread in the scan");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int CH = 256;          // entries per staged chunk
-  constexpr int DL = D / 32;       // channels per lane
-  float* acc = reinterpret_cast<float*>(smem);                     // [R][D]
-  int4* sent = reinterpret_cast<int4*>(smem + (size_t)R * D * 4);  // [CH]
-  uint16_t* sg = reinterpret_cast<uint16_t*>(sent + CH);            // [CH][D]
-  const int tid = threadIdx.x, gk = tid >> 5, ln = tid & 31;
+  uint16_t* sg = reinterpret_cast<uint16_t*>(smem);                   // [CH][D] grad_out rows, sorted order
+  int4* sent = reinterpret_cast<int4*>(sg + CH * D);                  // [CH] the chunk's entries (entry order)
+  float* sw = reinterpret_cast<float*>(sent + CH);                    // [CH] weights, sorted order
+  int* sidx = reinterpret_cast<int*>(sw + CH);                        // [CH] sorted position -> chunk index
+  int* wcnt = sidx + CH;                                              // [4][256] per-wave row counts -> offsets
+  int* rs = wcnt + 4 * 256;                                           // [256] first sorted position of a row
+  int* re = rs + 256;                                                 // [256] one past its last
+  int* wtot = re + 256;                                               // [4] scan: wave totals
+  const int tid = threadIdx.x, gk = tid >> 5, ln = tid & 31, wave = tid >> 6, lane = tid & 63;
   const int bh = blockIdx.x / tiles_bh;
-  int rem = blockIdx.x - bh * tiles_bh, l = 0, hw = 0;
-  for (; l < L; ++l) {
-    hw = shapes[2 * l] * shapes[2 * l + 1];
-    const int nt = (hw + R - 1) / R;
-    if (rem < nt) break;
-    rem -= nt;
-  }
-  const int t = rem, b = bh / H, h = bh - b * H;
+  int rem = blockIdx.x - bh * tiles_bh, l = 0;
+  while (l < L - 1 && rem >= lv.nt[l]) rem -= lv.nt[l++];
+  const int R = lv.R[l], t = rem, b = bh / H, h = bh - b * H;
   const int grp = bh * L + l, n = Q * P * 4;
   const int32_t* to = toff + (size_t)grp * (kVgTilesMax + 1);
   const int j0 = to[t], j1 = to[t + 1];
-  const int r0 = t * R, rows = min(R, hw - r0);
-  for (int i = tid; i < R * D; i += 256) acc[i] = 0.f;
+  const int r0 = t * R, rows = min(R, lv.hw[l] - r0);
   const int4* ent = sorted + (size_t)grp * n;
+  const uint16_t* gob = grad_out + ((size_t)b * Q * H + h) * D;  // + q H D: the query's row for head h
+  float acc[RPG][DL];
+#pragma unroll
+  for (int i = 0; i < RPG; ++i)
+#pragma unroll
+    for (int u = 0; u < DL; ++u) acc[i][u] = 0.f;
+  int4 e = make_int4(0, 0, 0, 0);
+  if (j0 + tid < j1) e = ent[j0 + tid];
   for (int c0 = j0; c0 < j1; c0 += CH) {
     const int cn = min(CH, j1 - c0);
-    __syncthreads();  // (previous chunk consumed; acc zeroed)
-    for (int i = tid; i < cn; i += 256) sent[i] = ent[c0 + i];
+    const bool valid = tid < cn;
+    const int row = valid ? e.x - r0 : 0;
+    __syncthreads();  // (the previous chunk's sums are done)
+    sent[tid] = e;
+    if (c0 + CH + tid < j1) e = ent[c0 + CH + tid];  // the next chunk's entry, in flight meanwhile
+#pragma unroll
+    for (int w = 0; w < 4; ++w) wcnt[w * 256 + tid] = 0;
+    // the wave's lanes holding this lane's row, and this lane's rank among them
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const bool on = (row >> bit) & 1;
+      const uint64_t bb = __ballot(valid && on);
+      peers &= on ? bb : ~bb;
+    }
+    const int rank = __popcll(peers & ((1ull << lane) - 1ull));
     __syncthreads();
-    // grad_out rows of the chunk's entries: D bf16 = D / 8 16-B pieces each
-    constexpr int PPR = D / 8;
-    for (int i = tid; i < cn * PPR; i += 256) {
-      const int j = i / PPR, pc = i - j * PPR;
-      const int q = sent[j].z / (P * 4);
-      reinterpret_cast<uint4*>(sg + (size_t)j * D)[pc] =
-          reinterpret_cast<const uint4*>(grad_out + (((size_t)b * Q + q) * H + h) * D)[pc];
+    if (valid && rank == 0) wcnt[wave * 256 + row] = __popcll(peers);
+    __syncthreads();
+    {  // thread = row: earlier waves' counts, the row total, and its exclusive scan over rows
+      const int c0w = wcnt[tid], c1w = wcnt[256 + tid], c2w = wcnt[512 + tid], c3w = wcnt[768 + tid];
+      wcnt[256 + tid] = c0w;
+      wcnt[512 + tid] = c0w + c1w;
+      wcnt[768 + tid] = c0w + c1w + c2w;
+      wcnt[tid] = 0;
+      const int tot = c0w + c1w + c2w + c3w;
+      int inc = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int x = __shfl_up(inc, o);
+        if (lane >= o) inc += x;
+      }
+      if (lane == 63) wtot[wave] = inc;
+      __syncthreads();
+      int base = 0;
+      for (int w = 0; w < wave; ++w) base += wtot[w];
+      rs[tid] = base + inc - tot;
+      re[tid] = base + inc;
     }
     __syncthreads();
-    for (int j = 0; j < cn; ++j) {
-      const int4 e = sent[j];
-      const int r = e.x - r0;
-      if ((r & 7) != gk) continue;
-      const float w = __int_as_float(e.y);
+    if (valid) sidx[rs[row] + wcnt[wave * 256 + row] + rank] = tid;
+    __syncthreads();
+    // stage the sorted chunk's grad_out rows (bf16) and weights: all loads of a thread first
+    for (int i0 = tid; i0 < cn * PPR; i0 += 256 * 4) {
+      uint4 g[4];
 #pragma unroll
-      for (int u = 0; u < DL; ++u) {
-        const int dch = ln * DL + u;
-        acc[r * D + dch] += w * bf2f(sg[(size_t)j * D + dch]);
+      for (int u = 0; u < 4; ++u) {
+        const int i = min(i0 + 256 * u, cn * PPR - 1);
+        const int p = i / PPR, pc = i - p * PPR;
+        g[u] = reinterpret_cast<const uint4*>(gob + (size_t)(sent[sidx[p]].z / (P * 4)) * H * D)[pc];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 256 * u;
+        if (i < cn * PPR) reinterpret_cast<uint4*>(sg)[i] = g[u];
+      }
+    }
+    if (valid) sw[tid] = __int_as_float(sent[sidx[tid]].y);
+    __syncthreads();
+    // each group adds its rows' terms in sorted order (fp32 fma, as the atomic path's products)
+#pragma unroll
+    for (int i = 0; i < RPG; ++i) {
+      const int r = gk + 8 * i;
+      const int p1 = re[r];
+      for (int p = rs[r]; p < p1; ++p) {
+        const float w = sw[p];
+#pragma unroll
+        for (int u = 0; u < DL; ++u) acc[i][u] = fmaf(w, bf2f(sg[p * D + ln * DL + u]), acc[i][u]);
       }
     }
   }
-  __syncthreads();
-  // the tile's rows out as bf16 (16-B pieces), zeros where nothing landed
-  constexpr int PPR = D / 8;
-  uint16_t* gv = grad_value + ((size_t)b * S + starts[l] + r0) * ldv + (size_t)h * D;
-  for (int i = tid; i < rows * PPR; i += 256) {
-    const int r = i / PPR, pc = i - r * PPR;
-    *reinterpret_cast<uint4*>(gv + (size_t)r * ldv + pc * 8) = pack8(acc + r * D + pc * 8);
+  // the tile's rows out as bf16 straight from the sums (a row's D channels: one 64/128-B segment per group),
+  // zeros where nothing landed
+  uint16_t* gv = grad_value + ((size_t)b * S + lv.start[l] + r0) * ldv + (size_t)h * D;
+#pragma unroll
+  for (int i = 0; i < RPG; ++i) {
+    const int r = gk + 8 * i;
+    if (r < rows) {
+      if constexpr (DL == 1) {
+        gv[(size_t)r * ldv + ln] = f2bf(acc[i][0]);
+      } else {
+        *reinterpret_cast<uint32_t*>(gv + (size_t)r * ldv + 2 * ln) = pack2bf(acc[i][0], acc[i][1]);
+      }
+    }
   }
 }
 
@@ -944,12 +1053,6 @@ extern "C" int rtdetr_msda_fused_bwd(const void* value, const int32_t* shapes, c
 // EVERY element of its grad_value column slice (no zeroing needed).
 // hw_host: the L level sizes h_l w_l in HOST memory (they size the tile grid).
 // ---------------------------------------------------------------------------
-static int vg_rows_per_tile(const int32_t* hw_host, int L) {
-  int mx = 1;
-  for (int l = 0; l < L; ++l) mx = std::max(mx, (int)hw_host[l]);
-  return 256 * ((mx + 256 * kVgTilesMax - 1) / (256 * kVgTilesMax));
-}
-
 extern "C" long long rtdetr_msda_vgrad_workspace(int B, int Q, int H, int L, int P) {
   const long long n = (long long)B * H * L * Q * P * 4;
   return n * 8 + n * 16 + (long long)B * H * L * (kVgTilesMax + 1) * 4 + 256;
@@ -969,9 +1072,23 @@ extern "C" int rtdetr_msda_fused_bwd_det(const void* value, long long ldv, const
   if (reinterpret_cast<uintptr_t>(work) % 16 || reinterpret_cast<uintptr_t>(grad_value) % 16)
     return fail("msda_fused_bwd_det: work and grad_value must be 16-B aligned");
   if (Q == 0) return 0;  // (no samples: the caller's slice stays as it was)
-  const int R = vg_rows_per_tile(hw_host, L);
-  int tiles_bh = 0;
-  for (int l = 0; l < L; ++l) tiles_bh += (hw_host[l] + R - 1) / R;
+  VgLevels lv{};
+  int tiles_bh = 0, ntmax = 0, start = 0;
+  for (int l = 0; l < L; ++l) {
+    const int hw = hw_host[l];
+    if (hw < 1 || hw > kVgRows * kVgTilesMax)
+      return fail("msda_fused_bwd_det: every level needs 1 .. 32,768 value rows");
+    int R = kVgRows;
+    while (R > 16 && (hw + R - 1) / R < 16) R >>= 1;  // at least 16 tiles where rows allow, R >= 16
+    lv.hw[l] = hw;
+    lv.R[l] = R;
+    lv.nt[l] = (hw + R - 1) / R;
+    lv.start[l] = start;
+    start += hw;
+    tiles_bh += lv.nt[l];
+    ntmax = std::max(ntmax, lv.nt[l]);
+  }
+  if (start > S) return fail("msda_fused_bwd_det: level sizes exceed S");
   const long long n = (long long)Q * P * 4, n_all = n * B * H * L;
   int2* rec = static_cast<int2*>(work);
   int4* sorted = reinterpret_cast<int4*>(static_cast<char*>(work) + n_all * 8);
@@ -997,33 +1114,43 @@ extern "C" int rtdetr_msda_fused_bwd_det(const void* value, long long ldv, const
   }
   {
     ProfScope prof(stream, PROF_MSDA, (double)n_all * (8.0 + 16.0) + (double)B * H * L * (kVgTilesMax + 1) * 4);
-    MOE_LAUNCH(prof, msda_vgrad_sort_kernel, dim3(B * H * L), dim3(kVgSortThreads), 0, stream, rec, shapes, H, L,
-               (int)n, R, sorted, toff);
+    const size_t slds = ((size_t)((n + 255) / 256) * 4 * ntmax + kVgTilesMax + 4) * 4;
+    if (slds > 150 * 1024) return fail("msda_fused_bwd_det: too many samples per group for the tile sort");
+    static bool sset = false;
+    if (!sset) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(msda_vgrad_sort_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
+        return fail("msda_fused_bwd_det: LDS attribute refused");
+      sset = true;
+    }
+    MOE_LAUNCH(prof, msda_vgrad_sort_kernel, dim3(B * H * L), dim3(256), slds, stream, rec, lv, L, (int)n, sorted,
+               toff);
     if (int rc = check_launch("rtdetr_msda_fused_bwd_det (sort)")) return rc;
   }
-  const size_t lds = (size_t)R * D * 4 + 256 * 16 + (size_t)256 * D * 2;
-  if (lds > 159 * 1024) return fail("msda_fused_bwd_det: level too large for the LDS tile");
+  const size_t lds = (size_t)kVgChunk * (D * 2 + 16 + 4 + 4) + 256 * 24 + 16;
   double rows = 0;
   for (int l = 0; l < L; ++l) rows += hw_host[l];
   ProfScope prof(stream, PROF_MSDA, (double)n_all * (16.0 + 2.0 * D) + rows * B * H * D * 2.0);
   if (D == 32) {
     static bool a32 = false;
     if (!a32) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(msda_vgrad_tile_kernel<32>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(msda_vgrad_tile_kernel<32>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return fail("msda_fused_bwd_det: LDS attribute refused");
       a32 = true;
     }
-    MOE_LAUNCH(prof, msda_vgrad_tile_kernel<32>, dim3(B * H * tiles_bh), dim3(256), lds, stream, sorted, toff, shapes,
-               starts, go, B, S, Q, H, L, P, R, tiles_bh, ldv, gv);
+    MOE_LAUNCH(prof, msda_vgrad_tile_kernel<32>, dim3(B * H * tiles_bh), dim3(256), lds, stream, sorted, toff, lv, go,
+               S, Q, H, L, P, tiles_bh, ldv, gv);
   } else {
     static bool a64 = false;
     if (!a64) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(msda_vgrad_tile_kernel<64>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(msda_vgrad_tile_kernel<64>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return fail("msda_fused_bwd_det: LDS attribute refused");
       a64 = true;
     }
-    MOE_LAUNCH(prof, msda_vgrad_tile_kernel<64>, dim3(B * H * tiles_bh), dim3(256), lds, stream, sorted, toff, shapes,
-               starts, go, B, S, Q, H, L, P, R, tiles_bh, ldv, gv);
+    MOE_LAUNCH(prof, msda_vgrad_tile_kernel<64>, dim3(B * H * tiles_bh), dim3(256), lds, stream, sorted, toff, lv, go,
+               S, Q, H, L, P, tiles_bh, ldv, gv);
   }
   return check_launch("rtdetr_msda_fused_bwd_det");
 }

@@ -1,7 +1,7 @@
 """Probe: the fused deformable-attention kernels at the C2 decoder shape
 (B 8, Q 300, H 8, D 32, L 3, P 4, levels 92x160 / 46x80 / 23x40), forward and
 backward time per call (eager loop between events), level-batched kernels vs
-the generic ones (moe_set_tuning msda_generic), and their agreement.
+the generic ones and the deterministic backward (moe_set_tuning msda_generic), and their agreement.
 
     python tools/msda_probe.py > gpurun_out/ms/probe.jsonl
 """
@@ -64,6 +64,10 @@ def main():
         outs[generic] = (fwd().float(), grad_all[..., col0:col0 + H * D].float().clone(), go.float(), gl.float())
         grad_all.zero_()
     L.set_tuning("msda_generic", 0)
+    hw = [h * w for h, w in shapes]
+    det = lambda: L.msda_fused_bwd_slice_det(value_all, grad_all, col0, H, D, st, so, hw, off, ref, logits, 0.5,  # noqa: E731
+                                             Lv, P, gout)
+    res["det_bwd_us"] = round(timed(det), 2)
     for name, a, b in zip(("out", "dvalue", "doff", "dlogits"), outs[3], outs[0]):
         res[f"{name}_max_abs_diff"] = float((a - b).abs().max())
         res[f"{name}_rel"] = float((a - b).norm() / a.norm().clamp_min(1e-12))
