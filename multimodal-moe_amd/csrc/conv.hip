@@ -216,8 +216,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
   // (register-direct 8-B stores at a row stride run at about half that rate).  The fused
   // epilogue's operands (same 16-B chunks as the stores) are loaded first, behind the image.
   constexpr int RPP = NTH / CPR;  // rows per store pass
+  constexpr bool PRE = BM / RPP <= 16;  // epilogue operands loaded up front (else per store pass: registers)
+  constexpr int NPRE = PRE ? BM / RPP : 1;
   const int ec = tid % CPR;
-  uint4 eres[BM / RPP], emask[BM / RPP];
+  uint4 eres[NPRE], emask[NPRE];
   // global output row of GEMM row p (PH: the class pixel's dX row)
   auto grow = [&](int p) -> size_t {
     if constexpr (PH) {
@@ -227,9 +229,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
       return (size_t)p;
     }
   };
-  if (a.resid != nullptr || a.mask != nullptr) {
+  if (PRE && (a.resid != nullptr || a.mask != nullptr)) {
 #pragma unroll
-    for (int k = 0; k < BM / RPP; ++k) {
+    for (int k = 0; k < NPRE; ++k) {
       const int p = m0 + tid / CPR + RPP * k;
       const size_t g = grow(p < a.P ? p : 0) * a.N + n0 + ec * 8;
       if (a.resid != nullptr) eres[k] = *reinterpret_cast<const uint4*>(a.resid + g);
@@ -264,12 +266,21 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
     const int p = m0 + r;
     if (p < a.P) {
       uint4 v = *reinterpret_cast<const uint4*>(smem + r * (BN * 2) + ((c ^ (r % CPR)) << 4));
+      uint4 er, em;
+      if constexpr (PRE) {
+        er = eres[k];
+        em = emask[k];
+      } else {
+        const size_t g = grow(p) * a.N + n0 + ec * 8;
+        if (a.resid != nullptr) er = *reinterpret_cast<const uint4*>(a.resid + g);
+        if (a.mask != nullptr) em = *reinterpret_cast<const uint4*>(a.mask + g);
+      }
       if (efloat) {
         float f[8];
         unpack8(v, f);
         if (a.resid != nullptr) {
           float q[8];
-          unpack8(eres[k], q);
+          unpack8(er, q);
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] += q[e];
         }
@@ -282,7 +293,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
         v = pack8(f);
       }
       if (a.mask != nullptr) {  // keep where the mask element is > 0 (bf16: sign clear, not zero)
-        const uint32_t mw[4] = {emask[k].x, emask[k].y, emask[k].z, emask[k].w};
+        const uint32_t mw[4] = {em.x, em.y, em.z, em.w};
         uint32_t vw[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -537,7 +548,15 @@ static void launch_fwd_n(ConvArgs a, hipStream_t stream, ProfScope& prof) {
 // not take it.
 template <int KS, bool BT, bool PH>
 static bool launch_fwd_big(const ConvArgs& a, hipStream_t stream, ProfScope& prof, int mode) {
-  if (mode >= 1 && a.N % 128 == 0) {
+  if constexpr (!BT) {
+    // mode 2: 256 x 256 of 2 x 2 waves, each wave 128 x 128 (one workgroup per CU, 128 KiB ring): a
+    // quarter of the 128 x 128 tile's LDS-DMA pieces and half its LDS reads per flop
+    if (mode == 2 && a.N % 256 == 0) {
+      launch_fwd_n<KS, 256, 256, BT, PH, 2, 2>(a, stream, prof);
+      return true;
+    }
+  }
+  if (mode == 1 && a.N % 128 == 0) {
     launch_fwd_n<KS, 256, 128, BT, PH, 4, 2>(a, stream, prof);
     return true;
   }

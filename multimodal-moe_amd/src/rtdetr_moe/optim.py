@@ -211,11 +211,17 @@ class DPGradReducer:
     zeros) and summed over the ranks with ONE all-reduce, so no ring hop
     rounds a partial sum to bf16.  ``__call__`` returns fp32 views of the
     summed gradients in the parameters' own layouts; FlatAdamW reads them in
-    place and applies the 1/world mean (``inv_world``) inside its kernels."""
+    place and applies the 1/world mean (``inv_world``) inside its kernels.
+    A parameter without a gradient on EVERY rank comes back as None (agreed
+    over the group on the first call; torch.optim then skips it: no decay, no
+    moment update), and ``broadcast_params`` gives every replica rank 0's
+    weights at the start, as DDP does."""
 
     def __init__(self, params, group=None):
         self.params = list(params)
         self.group = group
+        self._has_grad = None
+        self._local_pattern = None
         self.offsets, off = [], 0
         for p in self.params:
             self.offsets.append(off)
@@ -244,9 +250,44 @@ class DPGradReducer:
             return buf
         return g
 
+    def _world(self):
+        return dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
+
+    @torch.no_grad()
+    def broadcast_params(self):
+        """Rank 0's values of every replicated parameter on every rank (staged
+        through the host on gloo); call before the optimizer copies its masters."""
+        if self._world() <= 1:
+            return
+        gloo = dist.get_backend(self.group) == "gloo"
+        for p in self.params:
+            if gloo:
+                h = p.detach().cpu()
+                dist.broadcast(h, 0, group=self.group)
+                p.copy_(h.to(p.device))
+            else:
+                dist.broadcast(p.data, 0, group=self.group)
+
+    def _agree_has_grad(self, srcs):
+        local = [0 if s is None else 1 for s in srcs]
+        if self._has_grad is None:
+            agg = torch.tensor(local, dtype=torch.int32)
+            if self._world() > 1:
+                if dist.get_backend(self.group) == "gloo":
+                    dist.all_reduce(agg, group=self.group)
+                else:
+                    d = agg.to(self.flat.device)
+                    dist.all_reduce(d, group=self.group)
+                    agg = d.cpu()
+            self._has_grad = (agg > 0).tolist()
+            self._local_pattern = local
+        elif local != self._local_pattern:
+            raise RuntimeError("DPGradReducer: the set of parameters with a gradient changed after the first step")
+
     @torch.no_grad()
     def __call__(self, grads):
         srcs = [self._source(i, p, g) for i, (p, g) in enumerate(zip(self.params, grads))]
+        self._agree_has_grad(srcs)
         ptrs = tuple(s.data_ptr() if s is not None else 0 for s in srcs)
         if ptrs != self._ptrs:
             rec = np.zeros(len(self.params), dtype=_REC)
@@ -259,9 +300,9 @@ class DPGradReducer:
             self._ptrs = ptrs
         L._check(L.lib().train_grad_pack(self._table.data_ptr(), self.chunks.data_ptr(), self.n_chunks,
                                          self.flat.data_ptr(), L._stream()), "train_grad_pack")
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
+        if self._world() > 1:
             dist.all_reduce(self.flat, group=self.group)
-        return self.views
+        return [v if h else None for v, h in zip(self.views, self._has_grad)]
 
 
 def _collective(kind, out, inp, group):

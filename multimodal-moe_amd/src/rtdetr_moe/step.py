@@ -333,6 +333,13 @@ class TrainStep:
             # EP group (the same global norm on every rank)
             from .optim import FlatAdamW, ShardedDPAdamW
 
+            if world > 1 and not _ZERO:
+                # (A/B flat path) every replica starts from rank 0's weights, as DDP
+                # does, before FlatAdamW copies its masters
+                from .optim import DPGradReducer
+
+                self.reducer = DPGradReducer(self.dp_params)
+                self.reducer.broadcast_params()
             if world > 1 and _ZERO:
                 # C3 data parallelism: reduce-scatter of the fp32 gradients,
                 # AdamW on this rank's 1/world slice, all-gather of the weights
@@ -349,7 +356,7 @@ class TrainStep:
             self.opt = torch.optim.AdamW([{"params": bb, "lr": lr_backbone}, {"params": rest, "lr": lr}], lr=lr,
                                          weight_decay=weight_decay)
         self.flat = FlatOutputs(model)
-        self.reducer = None
+        self.reducer = getattr(self, "reducer", None)
         if world > 1 and images.is_cuda:
             from ..moe.layer import MoEFFN
 
@@ -359,12 +366,6 @@ class TrainStep:
             for m in model.modules():
                 if isinstance(m, MoEFFN) and m.ep_size > 1:
                     m.ep_grad_scale = 1.0
-        if world > 1 and images.is_cuda and not _ZERO:
-            # (A/B) the replicated gradients summed in fp32 by ONE all-reduce
-            # after the backward (optim.DPGradReducer), a replicated FlatAdamW
-            from .optim import DPGradReducer
-
-            self.reducer = DPGradReducer(self.dp_params)
         images = self._cast_in(images)
         self.runner = None
         self.stepper = None
