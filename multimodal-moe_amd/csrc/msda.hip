@@ -688,13 +688,34 @@ __global__ __launch_bounds__(256) void msda_vgrad_sort_kernel(const int2* __rest
     }
     return __popcll(peers & ((1ull << lane) - 1ull));
   };
+  // up to kVgRegRounds rounds (6,144 entries: Q <= 384 at L 3, P 4) are loaded ONCE, all together, and kept
+  // in registers for both passes; larger groups reload four rounds at a time
+  constexpr int kVgRegRounds = 24;
+  int2 vr[kVgRegRounds];
+  const bool in_regs = NR <= kVgRegRounds;
+  if (in_regs) {
+#pragma unroll
+    for (int u = 0; u < kVgRegRounds; ++u) {
+      const int e = u * 256 + tid;
+      vr[u] = (u < NR && e < n) ? src[e] : make_int2(-1, 0);
+    }
+  }
   for (int pass = 0; pass < 2; ++pass) {
     for (int rd0 = 0; rd0 < NR; rd0 += 4) {
       int2 v[4];
+      if (in_regs) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {  // four rounds' loads in flight
-        const int e = (rd0 + u) * 256 + tid;
-        v[u] = (rd0 + u < NR && e < n) ? src[e] : make_int2(-1, 0);
+        for (int q = 0; q < kVgRegRounds / 4; ++q)  // (static register indices: select the four rounds)
+          if (4 * q == rd0) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = vr[4 * q + u];
+          }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {  // four rounds' loads in flight
+          const int e = (rd0 + u) * 256 + tid;
+          v[u] = (rd0 + u < NR && e < n) ? src[e] : make_int2(-1, 0);
+        }
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
