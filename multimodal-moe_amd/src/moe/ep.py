@@ -312,15 +312,18 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap):
         xp, w, lb, z, pos, hist = _route_padded_eager(x, layer.wg, ctx_bias, ctx_img, tokens_per_image, k,
                                                       cfg.normalize, S)
     if _fused_ep_ok(layer, x, fp8):
-        # counts exchange (int32), then the receive map, the local expert
-        # offsets and this rank's overflow in ONE launch (moe_ep_compaction)
-        kept = hist.clamp(max=S).view(W, El).contiguous()
-        recv_cnt = _a2a(torch.empty_like(kept), kept, group, W)
+        # counts exchange (int32; the compaction caps them at S), then the
+        # receive map, the local expert offsets and this rank's overflow in ONE
+        # launch (moe_ep_compaction).  -ep1 without a process group: the
+        # exchanges are identities and are skipped (no copies)
+        ident = W == 1 and group is None
+        sent = hist.view(W, El)
+        recv_cnt = sent if ident else _a2a(torch.empty_like(sent), sent.contiguous(), group, W)
         gather, offs, overflow = L.ep_compaction(recv_cnt, hist, S)
         layer.last_ep_overflow = overflow[0] if cap <= 0 else None
-        xr = _Exchange.apply(xp, group, W)
+        xr = xp if ident else _Exchange.apply(xp, group, W)
         yr = _EPExpertFFNScatter.apply(xr, gather, layer.w1, layer.b1, layer.w2, layer.b2, offs, gs)
-        yp = _Exchange.apply(yr, group, W)
+        yp = yr if ident else _Exchange.apply(yr, group, W)
         return combine(yp, w, pos, T), lb, z, hist
     recv_cnt = _exchange_counts(hist.clamp(max=S).view(W, El), group, W)
     gather, inv, offs = compaction_map(recv_cnt, S)
