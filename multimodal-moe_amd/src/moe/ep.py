@@ -282,8 +282,11 @@ def _route_padded_eager(x, wg, ctx_bias, ctx_img, tpi, k, normalize, S):
     return xp, w, lb, z, pos, hist.to(torch.int32)
 
 
-def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap):
-    """-> (y [T, d], lb, z, hist [E]) of one expert-parallel MoE layer."""
+def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=False):
+    """-> (y [T, d], lb, z, hist [E]) of one expert-parallel MoE layer;
+    residual=True: y = x + FFN(x), on the HIP bf16 path folded into the
+    combine (returned with ``y_has_residual`` set on the layer)."""
+    layer.y_has_residual = False
     cfg = layer.cfg
     E, W, k = cfg.num_experts, layer.ep_size, cfg.top_k
     El = E // W
@@ -324,6 +327,9 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap):
         xr = xp if ident else _Exchange.apply(xp, group, W)
         yr = _EPExpertFFNScatter.apply(xr, gather, layer.w1, layer.b1, layer.w2, layer.b2, offs, gs)
         yp = yr if ident else _Exchange.apply(yr, group, W)
+        if residual and x.dtype == torch.bfloat16:
+            layer.y_has_residual = True
+            return combine(yp, w, pos, T, resid=x), lb, z, hist
         return combine(yp, w, pos, T), lb, z, hist
     recv_cnt = _exchange_counts(hist.clamp(max=S).view(W, El), group, W)
     gather, inv, offs = compaction_map(recv_cnt, S)

@@ -54,6 +54,7 @@ class MoEFFN(nn.Module):
         self.last_hist = None  # int32 [E] expert histogram of the last forward
         self.last_ep_overflow = None  # EP without capacity: assignments beyond the a2a slots (device)
         self.last_tokens = 0   # T of the last forward (bench: EP exchange bytes)
+        self.y_has_residual = False  # EP: the residual was folded into the combine
 
     def forward(self, x: torch.Tensor, ctx_img: torch.Tensor | None, residual: bool = False) -> torch.Tensor:
         """x [B, L, d] (image-major tokens), ctx_img int [B] -> [B, L, d].
@@ -70,7 +71,12 @@ class MoEFFN(nn.Module):
         if self.ep_size > 1 or cfg.expert_parallel:  # C4: experts sharded over ranks, all-to-all exchange
             from .ep import moe_ffn_ep
 
-            y, lb, z, hist = moe_ffn_ep(self, flat, cb, ci, L, cap)
+            y, lb, z, hist = moe_ffn_ep(self, flat, cb, ci, L, cap, residual=residual)
+            if residual and self.y_has_residual:  # folded into the combine
+                self.last_aux = (lb, z)
+                self.last_aux_weighted = None
+                self.last_hist = hist
+                return y.to(x.dtype).view(B, L, d)
         elif flat.is_cuda:
             from .ops import moe_ffn_hip
 

@@ -513,7 +513,27 @@ def expert_ffn_mx_hip(carrier, xq, xs, w1, b1, w2, b2, offsets, rows, grad_scale
     return _ExpertFFNMX.apply(carrier, xq, xs, w1, b1, w2, b2, offsets, int(rows), grad_scale)
 
 
-def combine_hip(yp, w, pos, T):
+class _CombineRes(torch.autograd.Function):
+    """y = resid + combine (one bf16 rounding, moe_combine_res_fwd): the EP
+    layer's residual branch without a separate add; backward: dresid = dy."""
+
+    @staticmethod
+    def forward(ctx, yp, w, pos, T, resid):
+        y = L.combine_fwd(yp.to(torch.bfloat16).contiguous(), pos, w, T, resid=resid.to(torch.bfloat16).contiguous())
+        ctx.save_for_backward(yp, w, pos)
+        ctx.rdtype = resid.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        yp, w, pos = ctx.saved_tensors
+        dyp, dw = L.combine_bwd(dy.to(torch.bfloat16).contiguous(), yp.to(torch.bfloat16).contiguous(), pos, w)
+        return dyp, dw, None, None, dy.to(ctx.rdtype)
+
+
+def combine_hip(yp, w, pos, T, resid=None):
+    if resid is not None:
+        return _CombineRes.apply(yp, w, pos, int(T), resid)
     return _Combine.apply(yp, w, pos, int(T))
 
 
