@@ -285,8 +285,11 @@ def _route_padded_eager(x, wg, ctx_bias, ctx_img, tpi, k, normalize, S):
 def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=False):
     """-> (y [T, d], lb, z, hist [E]) of one expert-parallel MoE layer;
     residual=True: y = x + FFN(x), on the HIP bf16 path folded into the
-    combine (returned with ``y_has_residual`` set on the layer)."""
+    combine (returned with ``y_has_residual`` set on the layer).  On the GPU
+    lb and z are detached (logging) and ``layer.ep_aux_weighted`` carries the
+    differentiable lb_coef lb + z_coef z (moe_aux_loss_fwd)."""
     layer.y_has_residual = False
+    layer.ep_aux_weighted = None
     cfg = layer.cfg
     E, W, k = cfg.num_experts, layer.ep_size, cfg.top_k
     El = E // W
@@ -299,7 +302,7 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=Fals
     gs = getattr(layer, "ep_grad_scale", 1.0 / W)  # 1.0 when the optimizer applies 1/W (graph-mode TrainStep)
     if x.is_cuda:
         from . import _lib as L
-        from .ops import aux_losses, combine_hip as combine
+        from .ops import aux_loss_weighted, combine_hip as combine
         from .ops import expert_ffn_mx_hip, route_dispatch_hip, route_dispatch_mx_hip
 
         if fp8:
@@ -308,7 +311,10 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=Fals
         else:
             xp, w, auxp, pos, hist, _, _ = route_dispatch_hip(x, layer.wg, ctx_bias, ctx_img, tokens_per_image, k,
                                                               cfg.normalize, cap, pad=S)
-        lb, z = aux_losses(auxp, hist, T, k)
+        # lb_coef lb + z_coef z in one HIP launch each way (the single-GPU path's
+        # aux kernel); the raw (lb, z) come back detached, for logging
+        layer.ep_aux_weighted, raw = aux_loss_weighted(auxp, hist, T, k, cfg.lb_coef, cfg.z_coef)
+        lb, z = raw[0], raw[1]
     else:
         from .eager import combine_eager as combine, expert_ffn_eager, expert_ffn_mx_eager
 

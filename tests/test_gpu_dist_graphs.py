@@ -169,11 +169,8 @@ def _ep_inputs(rank, dev):
 
 
 def _ep_loss(layer, y, dy, ep):
-    if ep:
-        aux = layer.cfg.lb_coef * layer.last_aux[0] + layer.cfg.z_coef * layer.last_aux[1]
-    else:
-        aux = layer.aux_loss()
-    return (y.float() * dy).sum() + 10.0 * aux
+    # both paths: the aux-loss kernel's weighted term (last_aux holds the detached raw lb, z)
+    return (y.float() * dy).sum() + 10.0 * layer.aux_loss()
 
 
 def _ep_layer_worker(rank, world, port, out):
