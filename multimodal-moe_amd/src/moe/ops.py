@@ -69,9 +69,17 @@ def _ffn_forward(xb, tok, w1b, b1, w2b, b2, offsets, G, rows):
     return h, yp
 
 
+_PADDED_OFFSETS: dict = {}
+
+
 def _padded_offsets(E, pad, device):
-    """Expert e's rows start at e * pad (the fixed-capacity layout of ep.py)."""
-    return (torch.arange(E + 1, dtype=torch.int32, device=device) * int(pad)).contiguous()
+    """Expert e's rows start at e * pad (the fixed-capacity layout of ep.py);
+    cached per (E, pad, device): read-only, so no launches per layer call."""
+    key = (int(E), int(pad), str(device))
+    t = _PADDED_OFFSETS.get(key)
+    if t is None:
+        t = _PADDED_OFFSETS[key] = (torch.arange(E + 1, dtype=torch.int32, device=device) * int(pad)).contiguous()
+    return t
 
 
 class _RouteDispatch(torch.autograd.Function):
