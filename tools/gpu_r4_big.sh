@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-4 bundle: conv A/B of the 256 x 256 tile, MSDA probe under rocprof, C4 + C5 bench lines.
+set -u
+R=$GRAFT_REPO_ROOT; cd $R
+bash tools/gpu_conv_ab.sh r4n_conv conv_big=2; rc=$?
+[ $rc -eq 0 ] || exit $rc
+bash tools/gpu_msda_prof.sh r4n_msda; rc=$?
+[ $rc -eq 0 ] || exit $rc
+mkdir -p gpurun_out/r4n
+for WL in c4 c5; do
+  timeout -k 10 420 python bench.py --workload $WL > gpurun_out/r4n/bench_$WL.json 2> gpurun_out/r4n/bench_$WL.err; rc=$?
+  echo "BENCH $WL $rc"; tail -c 300 gpurun_out/r4n/bench_$WL.json
+  [ $rc -eq 0 ] || exit $rc
+done
