@@ -12,3 +12,6 @@ for WL in c4 c5; do
   echo "BENCH $WL $rc"; tail -c 300 gpurun_out/r4n/bench_$WL.json
   [ $rc -eq 0 ] || exit $rc
 done
+timeout -k 10 400 python tools/torch_prof.py --stacks --steps 2 --out gpurun_out/r4n/tprof_stacks.txt > gpurun_out/r4n/tprof.log 2>&1; rc=$?
+echo "TPROF $rc"
+exit $rc
