@@ -13,7 +13,7 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
-from .linear import TokenLinear, TokenSelfAttention, bias_grad, chunked_wgrad
+from .linear import TokenLinear, TokenSelfAttention, _MLPHip, bias_grad, chunked_wgrad, mlp_hip_ok
 from ..moe.config import MoEConfig
 from .encoder import HybridEncoder, make_ffn
 from .norm import AddLayerNorm
@@ -80,6 +80,11 @@ class MLP(nn.Module):
         self.layers = nn.ModuleList(TokenLinear(a, b) for a, b in zip(dims, dims[1:] + [dout]))
 
     def forward(self, x):
+        if _FUSED_MLP and mlp_hip_ok(x, self.layers):
+            # one autograd node: bias + ReLU in the GEMM epilogue, the ReLU mask in the
+            # next layer's data-gradient epilogue (linear._MLPHip)
+            wb = [t for m in self.layers for t in (m.weight, m.bias)]
+            return _MLPHip.apply(x, len(self.layers), *wb)
         for i, layer in enumerate(self.layers):
             x = layer(x)
             if i < len(self.layers) - 1:
@@ -247,6 +252,7 @@ _LEVEL_CACHE = {}
 _FUSED_MSDA = os.environ.get("MOE_FUSED_MSDA", "1") != "0"  # A/B switch
 _BATCHED_VALUE = os.environ.get("MOE_BATCHED_VALUE", "1") != "0"  # A/B switch: one value projection for all layers
 _FUSED_BOXES = os.environ.get("MOE_FUSED_BOXES", "1") != "0"  # A/B switch
+_FUSED_MLP = os.environ.get("MOE_FUSED_MLP", "1") != "0"  # A/B switch: ReLU MLP heads as one node (linear._MLPHip)
 # MOE_DET_MSDA=0: the decoder's MSDA value gradients by packed bf16 atomics
 # (arrival order) instead of the deterministic fixed-order fp32 sums (A/B)
 _DET_MSDA = os.environ.get("MOE_DET_MSDA", "1") != "0"

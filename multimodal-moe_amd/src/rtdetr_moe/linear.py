@@ -197,6 +197,54 @@ def L_narrow_ok(M: int, N: int) -> bool:
     return (M <= 128 and N % 2 == 0 and N <= 4096) or (N <= 128 and M % 2 == 0 and M <= 4096)
 
 
+def _defer_targets(weight, bias, x):
+    """Where a deferred weight gradient would land (the leaf parameters), or
+    None; the backward decides whether to defer (GraphedStep's forward runs
+    outside the collecting context)."""
+    if DEFER_WGRAD[0] and bias is not None and bias.dtype == weight.dtype and x.is_cuda:
+        wt, bt = _row_target(weight), _row_target(bias)
+        if wt is not None and bt is not None:
+            return (wt, bt)
+    return None
+
+
+def _linear_wgrad(g2, x2, weight_dtype, bias_dtype, has_bias, need_w, need_b, targets):
+    """(gw, gb) of one dense linear from its 2-D output gradient and input, or
+    (None, None) when deferred (linear.DeferredWgrad collects them)."""
+    K, M = g2.shape
+    N = x2.shape[1]
+    if (need_w and has_bias and need_b and g2.is_cuda and g2.dtype == x2.dtype == torch.bfloat16
+            and M % 64 == 0 and N % 128 == 0 and DENSE_WGRAD_ROWS[0] <= K < BIG_ROWS and x2.is_contiguous()):
+        # weight + bias gradient in one libmoe_hip launch (split over rows):
+        # hipBLASLt's dY^T X on these few-tile outputs plus the bias column
+        # sum took ~31 us at 2,400 rows, this ~14 us (tools/mm_probe_small.py)
+        from ..moe import _lib as L
+
+        odt = torch.bfloat16 if weight_dtype == torch.bfloat16 else torch.float32
+        if _ACTIVE[0] is not None and targets is not None and weight_dtype == odt:
+            _ACTIVE[0].add(g2, x2, odt, *targets)  # computed after the backward, batched
+            return None, None
+        gw, gb = L.linear_wgrad(g2, x2, odt)
+        return gw, gb.to(bias_dtype)
+    if (need_w and has_bias and need_b and g2.is_cuda and g2.dtype == x2.dtype == torch.bfloat16
+            and L_narrow_ok(M, N) and 0 < K < BIG_ROWS and x2.is_contiguous()):
+        # narrow heads (M = 1 / 4 / 96 outputs, or the query position
+        # head's 4 inputs): hipBLASLt ran dY^T X on 1-8 workgroups, 25-34
+        # us each; rtdetr_linear_wgrad_narrow splits the rows over the
+        # whole chip and adds the bias column sum
+        from ..moe import _lib as L
+
+        odt = torch.bfloat16 if weight_dtype == torch.bfloat16 else torch.float32
+        gw, gb = L.linear_wgrad_narrow(g2, x2, odt)
+        return gw, gb.to(bias_dtype)
+    gw = gb = None
+    if need_w:
+        gw = chunked_wgrad(g2, x2) if x2.shape[0] >= BIG_ROWS else g2.t().mm(x2)
+    if has_bias and need_b:
+        gb = bias_grad(g2, bias_dtype)
+    return gw, gb
+
+
 class _TokenLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, dtype):
@@ -206,14 +254,7 @@ class _TokenLinear(torch.autograd.Function):
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.weight_dtype = weight.dtype
-        # where a deferred weight gradient would land (the leaf parameters; the
-        # backward decides whether to defer: GraphedStep's forward runs outside
-        # the collecting context)
-        ctx.targets = None
-        if DEFER_WGRAD[0] and bias is not None and bias.dtype == weight.dtype and x.is_cuda:
-            wt, bt = _row_target(weight), _row_target(bias)
-            if wt is not None and bt is not None:
-                ctx.targets = (wt, bt)
+        ctx.targets = _defer_targets(weight, bias, x)
         return F.linear(xc, wc, bc)
 
     @staticmethod
@@ -222,39 +263,109 @@ class _TokenLinear(torch.autograd.Function):
         g2 = gy.reshape(-1, gy.shape[-1]).to(wc.dtype).contiguous()
         x2 = xc.reshape(-1, xc.shape[-1])
         gx = g2.mm(wc).view(xc.shape) if ctx.needs_input_grad[0] else None
-        gw = gb = None
-        K, M = g2.shape
-        N = x2.shape[1]
-        if (ctx.needs_input_grad[1] and ctx.has_bias and ctx.needs_input_grad[2] and g2.is_cuda
-                and g2.dtype == x2.dtype == torch.bfloat16 and M % 64 == 0 and N % 128 == 0
-                and DENSE_WGRAD_ROWS[0] <= K < BIG_ROWS and x2.is_contiguous()):
-            # weight + bias gradient in one libmoe_hip launch (split over rows):
-            # hipBLASLt's dY^T X on these few-tile outputs plus the bias column
-            # sum took ~31 us at 2,400 rows, this ~14 us (tools/mm_probe_small.py)
-            from ..moe import _lib as L
-
-            odt = torch.bfloat16 if ctx.weight_dtype == torch.bfloat16 else torch.float32
-            if _ACTIVE[0] is not None and ctx.targets is not None and ctx.weight_dtype == odt:
-                _ACTIVE[0].add(g2, x2, odt, *ctx.targets)  # computed after the backward, batched
-                return gx, None, None, None
-            gw, gb = L.linear_wgrad(g2, x2, odt)
-            return gx, gw, gb.to(ctx.bias_dtype), None
-        if (ctx.needs_input_grad[1] and ctx.has_bias and ctx.needs_input_grad[2] and g2.is_cuda
-                and g2.dtype == x2.dtype == torch.bfloat16 and L_narrow_ok(M, N) and 0 < K < BIG_ROWS
-                and x2.is_contiguous()):
-            # narrow heads (M = 1 / 4 / 96 outputs, or the query position
-            # head's 4 inputs): hipBLASLt ran dY^T X on 1-8 workgroups, 25-34
-            # us each; rtdetr_linear_wgrad_narrow splits the rows over the
-            # whole chip and adds the bias column sum
-            from ..moe import _lib as L
-
-            odt = torch.bfloat16 if ctx.weight_dtype == torch.bfloat16 else torch.float32
-            gw, gb = L.linear_wgrad_narrow(g2, x2, odt)
-            return gx, gw, gb.to(ctx.bias_dtype), None
-        if ctx.needs_input_grad[1]:
-            gw = chunked_wgrad(g2, x2) if x2.shape[0] >= BIG_ROWS else g2.t().mm(x2)
-        gb = bias_grad(g2, ctx.bias_dtype) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        gw, gb = _linear_wgrad(g2, x2, ctx.weight_dtype, ctx.bias_dtype, ctx.has_bias, ctx.needs_input_grad[1],
+                               ctx.needs_input_grad[2], ctx.targets)
         return gx, gw, gb, None
+
+
+_ROW_OFFSETS: dict = {}
+
+
+def _row_offsets(rows, device):
+    """[0, rows] int32 on the device (one group for the grouped GEMM), cached."""
+    key = (int(rows), str(device))
+    t = _ROW_OFFSETS.get(key)
+    if t is None:
+        t = _ROW_OFFSETS[key] = torch.tensor([0, int(rows)], dtype=torch.int32, device=device)
+    return t
+
+
+def _gemm_ok(N, K):
+    return N % 128 == 0 and K % 64 == 0
+
+
+class _MLPHip(torch.autograd.Function):
+    """The detector's ReLU MLP heads (box heads, query-position head) in bf16
+    as ONE autograd node: a hidden layer whose shape the grouped GEMM takes
+    (N % 128 == 0, K % 64 == 0) runs on it with the bias + ReLU epilogue (no
+    separate ReLU launch); in the backward the ReLU mask of layer i-1's output
+    is applied in layer i's data-gradient epilogue (EPI_RELU_MASK, no
+    threshold_backward launch); the weight gradients go through the same
+    kernels as TokenLinear's (and the same deferral).  Other layers fall back
+    to F.linear / torch ops inside the node."""
+
+    @staticmethod
+    def forward(ctx, x, n, *wb):
+        from ..moe import _lib as L
+
+        ws, bs = wb[0::2], wb[1::2]
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        rows = x2.shape[0]
+        offs = _row_offsets(rows, x.device)
+        ins = []
+        h = x2
+        for i in range(n):
+            w, b = ws[i], bs[i]
+            relu = i < n - 1
+            ins.append(h)
+            N, K = w.shape
+            if _gemm_ok(N, K):
+                h = L.grouped_gemm(h, w.contiguous(), offs, 1, rows, N, K, 1,
+                                   L.EPI_BIAS_RELU if relu else L.EPI_BIAS, bias=b if b.dtype == torch.bfloat16 else b.float())
+            else:
+                h = F.linear(h, w, b)
+                if relu:
+                    h = F.relu(h)
+        ctx.save_for_backward(*ins, *ws)
+        ctx.n = n
+        ctx.meta = [(b.dtype, w.dtype, _defer_targets(w, b, x)) for w, b in zip(ws, bs)]
+        ctx.xshape = x.shape
+        return h.view(*x.shape[:-1], h.shape[-1])
+
+    @staticmethod
+    def backward(ctx, gy):
+        from ..moe import _lib as L
+
+        n = ctx.n
+        saved = ctx.saved_tensors
+        ins, ws = saved[:n], saved[n:]
+        g = gy.reshape(-1, gy.shape[-1]).to(torch.bfloat16).contiguous()
+        rows = g.shape[0]
+        offs = _row_offsets(rows, g.device)
+        grads = [None] * (2 * n)
+        gx = None
+        for i in range(n - 1, -1, -1):
+            w, xin = ws[i], ins[i]
+            bdt, wdt, tg = ctx.meta[i]
+            need_w = ctx.needs_input_grad[2 + 2 * i]
+            need_b = ctx.needs_input_grad[3 + 2 * i]
+            # data gradient first (the weight gradient may be deferred, and reads g as is)
+            gin = None
+            if i > 0 or ctx.needs_input_grad[0]:
+                N_in = w.shape[1]
+                if i > 0 and _gemm_ok(N_in, w.shape[0]):
+                    # g_in = (g W) * (x_i > 0): the previous layer's ReLU mask in the epilogue
+                    gin = L.grouped_gemm(g, w.contiguous(), offs, 1, rows, N_in, w.shape[0], 0, L.EPI_RELU_MASK,
+                                         aux=xin)
+                else:
+                    gin = g.mm(w)
+                    if i > 0:
+                        gin = gin * (xin > 0).to(gin.dtype)
+            gw, gb = _linear_wgrad(g, xin, wdt, bdt, True, need_w, need_b, tg)
+            grads[2 * i], grads[2 * i + 1] = gw, gb
+            g = gin
+        if ctx.needs_input_grad[0]:
+            gx = g.view(ctx.xshape)
+        return (gx, None, *grads)
+
+
+def mlp_hip_ok(x, layers) -> bool:
+    """_MLPHip takes bf16 CUDA inputs with bf16 weights and biases (the bench
+    precision; under autocast / fp32 weights the per-layer path runs)."""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.numel() > 0) or torch.is_autocast_enabled("cuda"):
+        return False
+    return all(m.weight.dtype == torch.bfloat16 and m.bias is not None and m.bias.dtype == torch.bfloat16
+               for m in layers)
 
 
 class TokenLinear(nn.Linear):
