@@ -548,14 +548,8 @@ static void launch_fwd_n(ConvArgs a, hipStream_t stream, ProfScope& prof) {
 // not take it.
 template <int KS, bool BT, bool PH>
 static bool launch_fwd_big(const ConvArgs& a, hipStream_t stream, ProfScope& prof, int mode) {
-  if constexpr (!BT) {
-    // mode 2: 256 x 256 of 2 x 2 waves, each wave 128 x 128 (one workgroup per CU, 128 KiB ring): a
-    // quarter of the 128 x 128 tile's LDS-DMA pieces and half its LDS reads per flop
-    if (mode == 2 && a.N % 256 == 0) {
-      launch_fwd_n<KS, 256, 256, BT, PH, 2, 2>(a, stream, prof);
-      return true;
-    }
-  }
+  // (a 256 x 256 tile of 2 x 2 waves, 128 x 128 per wave at one workgroup per CU, measured 1.2-4x
+  // slower at every C2 shape: profiles/r04/conv/conv_bench_256x256_ab.jsonl)
   if (mode == 1 && a.N % 128 == 0) {
     launch_fwd_n<KS, 256, 128, BT, PH, 4, 2>(a, stream, prof);
     return true;

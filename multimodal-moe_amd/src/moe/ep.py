@@ -285,11 +285,8 @@ def _route_padded_eager(x, wg, ctx_bias, ctx_img, tpi, k, normalize, S):
 def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=False):
     """-> (y [T, d], lb, z, hist [E]) of one expert-parallel MoE layer;
     residual=True: y = x + FFN(x), on the HIP bf16 path folded into the
-    combine (returned with ``y_has_residual`` set on the layer).  On the GPU
-    lb and z are detached (logging) and ``layer.ep_aux_weighted`` carries the
-    differentiable lb_coef lb + z_coef z (moe_aux_loss_fwd)."""
+    combine (returned with ``y_has_residual`` set on the layer)."""
     layer.y_has_residual = False
-    layer.ep_aux_weighted = None
     cfg = layer.cfg
     E, W, k = cfg.num_experts, layer.ep_size, cfg.top_k
     El = E // W
@@ -302,7 +299,7 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=Fals
     gs = getattr(layer, "ep_grad_scale", 1.0 / W)  # 1.0 when the optimizer applies 1/W (graph-mode TrainStep)
     if x.is_cuda:
         from . import _lib as L
-        from .ops import aux_loss_weighted, combine_hip as combine
+        from .ops import aux_losses_hip, combine_hip as combine
         from .ops import expert_ffn_mx_hip, route_dispatch_hip, route_dispatch_mx_hip
 
         if fp8:
@@ -311,10 +308,9 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=Fals
         else:
             xp, w, auxp, pos, hist, _, _ = route_dispatch_hip(x, layer.wg, ctx_bias, ctx_img, tokens_per_image, k,
                                                               cfg.normalize, cap, pad=S)
-        # lb_coef lb + z_coef z in one HIP launch each way (the single-GPU path's
-        # aux kernel); the raw (lb, z) come back detached, for logging
-        layer.ep_aux_weighted, raw = aux_loss_weighted(auxp, hist, T, k, cfg.lb_coef, cfg.z_coef)
-        lb, z = raw[0], raw[1]
+        # lb and z (differentiable) from the single-GPU path's aux-loss kernel:
+        # one HIP launch each way instead of ~20 torch ops
+        lb, z = aux_losses_hip(auxp, hist, T, k)
     else:
         from .eager import combine_eager as combine, expert_ffn_eager, expert_ffn_mx_eager
 

@@ -357,6 +357,34 @@ class _AuxLoss(torch.autograd.Function):
         return (g * wcoef).view(1, -1).expand(ctx.nblk, -1), None, None, None, None, None
 
 
+class _AuxLossRaw(torch.autograd.Function):
+    """(lb, z) of one layer as separate differentiable scalars from ONE HIP
+    launch (moe_aux_loss_fwd with unit coefficients: wcoef = d(lb, z)/d auxp
+    per column); backward = (g_lb wcoef[:E], g_z wcoef[E]) broadcast over the
+    router blocks (one small op)."""
+
+    @staticmethod
+    def forward(ctx, auxp, hist, T, k):
+        out, wcoef = L.aux_loss_fwd(auxp.contiguous(), hist, T, k, 1.0, 1.0)
+        ctx.save_for_backward(wcoef)
+        ctx.nblk = auxp.shape[0]
+        ctx.set_materialize_grads(False)
+        return out[0].clone(), out[1].clone()
+
+    @staticmethod
+    def backward(ctx, g_lb, g_z):
+        (wcoef,) = ctx.saved_tensors
+        E = wcoef.numel() - 1
+        zero = torch.zeros((), dtype=wcoef.dtype, device=wcoef.device)
+        scale = torch.cat([(g_lb if g_lb is not None else zero).expand(E), (g_z if g_z is not None else zero).view(1)])
+        return (scale * wcoef).view(1, -1).expand(ctx.nblk, -1), None, None, None
+
+
+def aux_losses_hip(auxp, hist, T, k):
+    """-> (lb, z), differentiable, in one launch each way (moe_aux_loss_fwd)."""
+    return _AuxLossRaw.apply(auxp, hist, int(T), int(k))
+
+
 def aux_loss_weighted(auxp, hist, T, k, lb_coef, z_coef):
     """-> (lb_coef lb + z_coef z (differentiable), detached (lb, z) [2])."""
     return _AuxLoss.apply(auxp, hist, int(T), int(k), float(lb_coef), float(z_coef))

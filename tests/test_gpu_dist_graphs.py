@@ -169,7 +169,6 @@ def _ep_inputs(rank, dev):
 
 
 def _ep_loss(layer, y, dy, ep):
-    # both paths: the aux-loss kernel's weighted term (last_aux holds the detached raw lb, z)
     return (y.float() * dy).sum() + 10.0 * layer.aux_loss()
 
 

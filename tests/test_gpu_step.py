@@ -126,7 +126,7 @@ def test_ep_world1_matches_single_gpu_layer(hip_lib, dtype, cf, epcf, rccl):
             if ep:
                 layer.cfg, layer.ep_group = ecfg, (dist.group.WORLD if rccl else None)
                 y = layer(xi, ctx)
-                aux = layer.aux_loss()  # the EP layer's aux-loss kernel (lb, z in last_aux are detached)
+                aux = layer.aux_loss()
                 if cf <= 0:
                     over = int(layer.last_ep_overflow)
                     assert (over > 0) == (epcf * k < E), over
