@@ -171,7 +171,11 @@ int moe_router_wgrad(const float* dlogits, const void* x, const int32_t* ctx_img
 /* Grouped GEMM data types / epilogues.  MOE_BIAS_BF16 OR'd into the dtype of
  * moe_grouped_gemm / moe_grouped_gemm_gather: the bias epilogues read a bf16
  * bias [G][N] (the bf16 parameter itself; no fp32 copy per call). */
-enum moe_dtype { MOE_BF16 = 0, MOE_FP8_E4M3 = 1, MOE_BIAS_BF16 = 0x100 };
+enum moe_dtype { MOE_BF16 = 0, MOE_FP8_E4M3 = 1, MOE_BIAS_BF16 = 0x100, MOE_DENSE_LAYER = 0x200 };
+/* MOE_DENSE_LAYER OR'd into moe_grouped_gemm / _gather's dtype: the call is a
+ * dense (non-expert) layer run on the grouped GEMM with G = 1 (the detector's
+ * MLP heads); same arithmetic, counted by the library profiler with the dense
+ * linears (kind 11) instead of the expert GEMMs. */
 enum moe_epilogue {
   MOE_EPI_NONE = 0,      /* C = A.B                                   */
   MOE_EPI_BIAS = 1,      /* C = A.B + bias[g, n]                      */

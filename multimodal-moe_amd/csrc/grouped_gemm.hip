@@ -1693,14 +1693,15 @@ extern "C" int moe_grouped_gemm_gather(int dtype, const void* a, const int32_t* 
                                        const int32_t* offsets, int G, int max_rows, int N, int K, int trans_b,
                                        int epilogue, const float* bias, const void* aux, hipStream_t stream) {
   const bool bias16 = (dtype & MOE_BIAS_BF16) != 0;
-  if ((dtype & ~MOE_BIAS_BF16) != MOE_BF16) return fail("grouped_gemm: only MOE_BF16 is implemented");
+  const bool dense = (dtype & MOE_DENSE_LAYER) != 0;  // a dense layer on this kernel: profiled apart from the experts
+  if ((dtype & ~(MOE_BIAS_BF16 | MOE_DENSE_LAYER)) != MOE_BF16) return fail("grouped_gemm: only MOE_BF16 is implemented");
   RowsPlan pl;
   WsWin win = device_ws();
   if (plan_rows(pl, a, b, c, offsets, G, max_rows, N, K, trans_b, epilogue, bias, aux, a_gather, win)) return -1;
   pl.p.bias_bf16 = bias16 ? 1 : 0;
   if (bias16) pl.bytes_fixed -= 2.0 * G * N;  // bias bytes: 2 per element, not 4
   if (max_rows == 0) return 0;
-  ProfScope prof(stream, PROF_GEMM, pl.bytes_fixed, true, pl.bytes_row, pl.flops_row);
+  ProfScope prof(stream, dense ? PROF_LINEAR : PROF_GEMM, pl.bytes_fixed, true, pl.bytes_row, pl.flops_row);
   pl.p.prof_rows = prof.rows_slot();
   launch_rows(pl, stream, prof);
   return check_launch("moe_grouped_gemm");

@@ -20,6 +20,7 @@ LIB_PATH = Path(os.environ.get("MOE_HIP_LIB", _PKG / "lib" / "libmoe_hip.so"))
 MOE_BF16 = 0
 MOE_FP8_E4M3 = 1
 MOE_BIAS_BF16 = 0x100  # OR into the grouped-GEMM dtype: bf16 bias
+MOE_DENSE_LAYER = 0x200  # OR into the grouped-GEMM dtype: a dense layer (profiled with the dense linears)
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK, EPI_RELU_MASK_MX = 0, 1, 2, 3, 4
 MX_BLOCK = 32  # MXFP8: one E8M0 exponent byte per 32 e4m3 elements of a row
 
@@ -406,7 +407,7 @@ def token_bwd(dxp, pos, probs, topk_idx, topk_w, dw, lse, dprob_bias, zc, wg, no
 
 
 def grouped_gemm(a, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None, aux=None,
-                 out=None):
+                 out=None, dense=False):
     _need(a, torch.bfloat16, "a")
     _need(b, torch.bfloat16, "b")
     if aux is not None:
@@ -418,7 +419,8 @@ def grouped_gemm(a, b, offsets, G, max_rows, N, K, trans_b, epilogue, bias=None,
     c = out if out is not None else torch.empty((a.shape[0], N), dtype=torch.bfloat16, device=a.device)
     ensure_splitk_workspace(a.device)
     rc = lib().moe_grouped_gemm(
-        _gemm_dtype(bias, G, N), _ptr(a), _ptr(b), _ptr(c), _ptr(offsets), G, int(max_rows), N, K, int(trans_b),
+        _gemm_dtype(bias, G, N) | (MOE_DENSE_LAYER if dense else 0), _ptr(a), _ptr(b), _ptr(c), _ptr(offsets), G,
+        int(max_rows), N, K, int(trans_b),
         int(epilogue), _ptr(bias), _ptr(aux), None, _stream())
     _check(rc, "moe_grouped_gemm")
     return c

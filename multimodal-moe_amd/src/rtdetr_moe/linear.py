@@ -311,7 +311,8 @@ class _MLPHip(torch.autograd.Function):
             N, K = w.shape
             if _gemm_ok(N, K):
                 h = L.grouped_gemm(h, w.contiguous(), offs, 1, rows, N, K, 1,
-                                   L.EPI_BIAS_RELU if relu else L.EPI_BIAS, bias=b if b.dtype == torch.bfloat16 else b.float())
+                                   L.EPI_BIAS_RELU if relu else L.EPI_BIAS, bias=b if b.dtype == torch.bfloat16 else b.float(),
+                                   dense=True)
             else:
                 h = F.linear(h, w, b)
                 if relu:
@@ -346,7 +347,7 @@ class _MLPHip(torch.autograd.Function):
                 if i > 0 and _gemm_ok(N_in, w.shape[0]):
                     # g_in = (g W) * (x_i > 0): the previous layer's ReLU mask in the epilogue
                     gin = L.grouped_gemm(g, w.contiguous(), offs, 1, rows, N_in, w.shape[0], 0, L.EPI_RELU_MASK,
-                                         aux=xin)
+                                         aux=xin, dense=True)
                 else:
                     gin = g.mm(w)
                     if i > 0:
