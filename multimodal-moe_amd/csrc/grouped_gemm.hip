@@ -42,7 +42,9 @@ enum {
   FL_MX = 1,    // ROWS: A and B are MXFP8 (e4m3 + E8M0 per 32 along K): v_mfma_scale_f32_16x16x128_f8f6f4
   FL_CQ = 2,    // ROWS: C is written as MXFP8 (e4m3 [rows][N] + exponents [rows][N/32])
   FL_AUX8 = 4,  // ROWS, EPI_RELU_MASK: the mask operand is e4m3 (keep where the byte is > +0)
-  FL_Y8 = 8     // WGRAD: Y is MXFP8, dequantised to bf16 while staging (v1)
+  FL_Y8 = 8,    // WGRAD: Y is MXFP8, dequantised to bf16 while staging (v1)
+  FL_DENSE = 16  // ROWS: a dense (non-expert) layer (MOE_DENSE_LAYER): same code, its own kernel name, so
+                 // rocprof summaries keep it apart from the expert GEMMs
 };
 
 struct GemmParams {
@@ -1350,7 +1352,7 @@ static void launch(const GemmParams& p, dim3 grid, hipStream_t s, const ProfScop
   const size_t gx = (MODE == MODE_WGRAD && (p.x_gather != nullptr || p.b_gather != nullptr)) ? 768 : 0;
   if (variant == 1 && !(FL & (FL_MX | FL_CQ | FL_AUX8))) {
     constexpr size_t lds = 2 * (BM + BN) * 64 * 2;
-    constexpr auto fn = gemm_v1_kernel<BM, BN, A_K, B_K, MODE, EPI, COLSUM, FL & FL_Y8>;
+    constexpr auto fn = gemm_v1_kernel<BM, BN, A_K, B_K, MODE, EPI, COLSUM, FL & (FL_Y8 | FL_DENSE)>;
     allow_lds<fn>(lds);
     MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
   } else if (stages == 2) {
@@ -1422,7 +1424,7 @@ struct RowsPlan {
   GemmParams p{};
   long long grid = 0;  // workgroups (tiles x split)
   int bm = 64, variant = 2, stages = 2, epi = 0;
-  bool trans_b = true;
+  bool trans_b = true, dense = false;
   double bytes_fixed = 0, bytes_row = 0, flops_row = 0;
 };
 struct WgradPlan {
@@ -1586,7 +1588,21 @@ static void launch_rows_epi(const RowsPlan& pl, hipStream_t s, const ProfScope& 
     default: launch_rows_bm<BM, MOE_EPI_RELU_MASK, BK, FL_AUX8>(pl, s, prof); break;
   }
 }
+template <bool BK>
+static void launch_rows_dense(const RowsPlan& pl, hipStream_t s, const ProfScope& prof) {
+  switch (pl.epi) {
+    case MOE_EPI_BIAS: launch_rows_bm<64, MOE_EPI_BIAS, BK, FL_DENSE>(pl, s, prof); break;
+    case MOE_EPI_BIAS_RELU: launch_rows_bm<64, MOE_EPI_BIAS_RELU, BK, FL_DENSE>(pl, s, prof); break;
+    case MOE_EPI_RELU_MASK: launch_rows_bm<64, MOE_EPI_RELU_MASK, BK, FL_DENSE>(pl, s, prof); break;
+    default: launch_rows_bm<64, MOE_EPI_NONE, BK, FL_DENSE>(pl, s, prof); break;
+  }
+}
 static void launch_rows(const RowsPlan& pl, hipStream_t s, const ProfScope& prof) {
+  if (pl.dense && pl.bm == 64 && pl.epi <= MOE_EPI_RELU_MASK) {
+    if (pl.trans_b) launch_rows_dense<true>(pl, s, prof);
+    else launch_rows_dense<false>(pl, s, prof);
+    return;
+  }
   if (pl.bm == 128) {
     if (pl.trans_b) launch_rows_epi<128, true>(pl, s, prof);
     else launch_rows_epi<128, false>(pl, s, prof);
@@ -1699,6 +1715,7 @@ extern "C" int moe_grouped_gemm_gather(int dtype, const void* a, const int32_t* 
   WsWin win = device_ws();
   if (plan_rows(pl, a, b, c, offsets, G, max_rows, N, K, trans_b, epilogue, bias, aux, a_gather, win)) return -1;
   pl.p.bias_bf16 = bias16 ? 1 : 0;
+  pl.dense = dense;
   if (bias16) pl.bytes_fixed -= 2.0 * G * N;  // bias bytes: 2 per element, not 4
   if (max_rows == 0) return 0;
   ProfScope prof(stream, dense ? PROF_LINEAR : PROF_GEMM, pl.bytes_fixed, true, pl.bytes_row, pl.flops_row);
