@@ -350,8 +350,8 @@ class _MLPHip(torch.autograd.Function):
                                          aux=xin, dense=True)
                 else:
                     gin = g.mm(w)
-                    if i > 0:
-                        gin = gin * (xin > 0).to(gin.dtype)
+                    if i > 0:  # ReLU backward of layer i-1's output: one launch
+                        gin = torch.ops.aten.threshold_backward(gin, xin, 0.0)
             gw, gb = _linear_wgrad(g, xin, wdt, bdt, True, need_w, need_b, tg)
             grads[2 * i], grads[2 * i + 1] = gw, gb
             g = gin
