@@ -673,6 +673,16 @@ int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void* zero, int
 long long rtdetr_conv_dgrad_workspace(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void* dx, const void* zero, int B, int H, int W,
                       int C, int N, int KS, int stride, const void* add, const void* relu_mask, hipStream_t stream);
+/* Batched weight flip (round 4): rtdetr_conv_weight_flip_multi writes W' for
+ * every weight of a device table of n descriptors {const bf16* w; bf16* wt;
+ * int N, C, KS, block0} (32 B each, block0 = the prefix sum of (C/64)(N/64)KS^2
+ * blocks; total_blocks their sum) in ONE launch; rtdetr_conv_dgrad_preflipped
+ * is rtdetr_conv_dgrad for a shape that flips (workspace > 0) reading W' from
+ * wflip instead of writing it (w is still checked, not read). */
+int rtdetr_conv_weight_flip_multi(const void* table, int n, int total_blocks, hipStream_t stream);
+int rtdetr_conv_dgrad_preflipped(const void* dy, const void* w, const void* wflip, void* dx, const void* zero, int B,
+                                 int H, int W, int C, int N, int KS, int stride, const void* add, const void* relu_mask,
+                                 hipStream_t stream);
 int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
                       const void* zero, int B, int H, int W, int C, int N, int KS, int stride, hipStream_t stream);

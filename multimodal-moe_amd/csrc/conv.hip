@@ -330,6 +330,41 @@ __global__ __launch_bounds__(256) void conv_weight_flip_kernel(const uint16_t* _
   }
 }
 
+// Every registered convolution weight of a step flipped in ONE launch (the
+// data gradients then read their W' from persistent buffers): descriptor i
+// owns blocks [block0_i, block0_{i+1}), one 64 x 64 (n, c) block of one tap
+// each, as conv_weight_flip_kernel.
+struct FlipDesc {
+  const uint16_t* w;
+  uint16_t* wt;
+  int N, C, KS, block0;
+};
+
+__global__ __launch_bounds__(256) void conv_weight_flip_multi_kernel(const FlipDesc* __restrict__ d, int n) {
+  __shared__ uint16_t t[64][66];
+  int i = 0;
+  while (i + 1 < n && d[i + 1].block0 <= (int)blockIdx.x) ++i;  // (n is small: a uniform scan)
+  const uint16_t* w = d[i].w;
+  uint16_t* wt = d[i].wt;
+  const int N = d[i].N, C = d[i].C, T = d[i].KS * d[i].KS;
+  const int cb = C / 64, nbk = N / 64;
+  const int local = blockIdx.x - d[i].block0;
+  const int tap = local / (cb * nbk), rem = local - tap * cb * nbk;
+  const int n0 = (rem / cb) * 64, c0 = (rem - (rem / cb) * cb) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int nn = ty + 4 * r;
+    t[nn][tx] = w[((size_t)(n0 + nn) * T + (T - 1 - tap)) * C + c0 + tx];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int c = ty + 4 * r;
+    wt[((size_t)(c0 + c) * T + tap) * N + n0 + tx] = t[tx][c];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // weight gradient
 // ---------------------------------------------------------------------------
@@ -659,13 +694,14 @@ extern "C" long long rtdetr_conv_dgrad_workspace(int B, int H, int W, int C, int
   return flip ? 2ll * N * KS * KS * C : 0;
 }
 
-extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void* dx, const void* zero, int B, int H,
-                                 int W, int C, int N, int KS, int stride, const void* add, const void* relu_mask,
-                                 hipStream_t stream) {
+static int conv_dgrad_impl(const void* dy, const void* w, void* work, bool preflipped, void* dx, const void* zero,
+                           int B, int H, int W, int C, int N, int KS, int stride, const void* add,
+                           const void* relu_mask, hipStream_t stream) {
   const void* ptrs[4] = {dy, w, dx, zero};
   if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, stride, "rtdetr_conv_dgrad")) return rc;
   if (!aligned16(relu_mask) || !aligned16(add)) return fail("rtdetr_conv_dgrad: add / relu_mask must be 16-B aligned");
   const bool flip = rtdetr_conv_dgrad_workspace(B, H, W, C, N, KS) > 0;
+  if (preflipped && !flip) return fail("rtdetr_conv_dgrad_preflipped: this shape reads W in place (no flip)");
   if (flip && (work == nullptr || reinterpret_cast<uintptr_t>(work) % 16))
     return fail("rtdetr_conv_dgrad: this shape needs a 16-B aligned workspace of rtdetr_conv_dgrad_workspace() bytes");
   if (B == 0) return 0;
@@ -677,7 +713,7 @@ extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void
              nullptr, static_cast<const uint16_t*>(add), static_cast<const uint16_t*>(relu_mask), 0};
   const double P = a.P;
   const double Pdy = (double)B * Ho * Wo;
-  if (flip) {
+  if (flip && !preflipped) {
     const long long total = (long long)N * C * KS * KS;
     {
       ProfScope prof(stream, PROF_CONV, 4.0 * total);
@@ -685,8 +721,8 @@ extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void
                  static_cast<const uint16_t*>(w), static_cast<uint16_t*>(work), N, C, KS);
       if (int rc = check_launch("rtdetr_conv_dgrad (flip)")) return rc;
     }
-    a.w = static_cast<const uint16_t*>(work);
   }
+  if (flip) a.w = static_cast<const uint16_t*>(work);
   // algorithmic bytes / flops (the stride-2 zero-row taps are not counted)
   const double bytes = 2.0 * (P * (C + (relu_mask ? C : 0) + (add ? C : 0)) + Pdy * N) + 2.0 * N * KS * KS * C;
   const double flops = 2.0 * Pdy * N * KS * KS * C;
@@ -716,6 +752,31 @@ extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void
   if (flip) launch_fwd_any<false>(a, KS, stream, prof);
   else launch_fwd_any<true>(a, KS, stream, prof);
   return check_launch("rtdetr_conv_dgrad");
+}
+
+extern "C" int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void* dx, const void* zero, int B, int H,
+                                 int W, int C, int N, int KS, int stride, const void* add, const void* relu_mask,
+                                 hipStream_t stream) {
+  return conv_dgrad_impl(dy, w, work, false, dx, zero, B, H, W, C, N, KS, stride, add, relu_mask, stream);
+}
+
+extern "C" int rtdetr_conv_dgrad_preflipped(const void* dy, const void* w, const void* wflip, void* dx,
+                                            const void* zero, int B, int H, int W, int C, int N, int KS, int stride,
+                                            const void* add, const void* relu_mask, hipStream_t stream) {
+  if (wflip == nullptr) return fail("rtdetr_conv_dgrad_preflipped: NULL flipped weight");
+  return conv_dgrad_impl(dy, w, const_cast<void*>(wflip), true, dx, zero, B, H, W, C, N, KS, stride, add, relu_mask,
+                         stream);
+}
+
+extern "C" int rtdetr_conv_weight_flip_multi(const void* table, int n, int total_blocks, hipStream_t stream) {
+  if (n < 0 || total_blocks < 0) return fail("rtdetr_conv_weight_flip_multi: n, total_blocks must be >= 0");
+  if (n == 0 || total_blocks == 0) return 0;
+  if (table == nullptr || reinterpret_cast<uintptr_t>(table) % 16)
+    return fail("rtdetr_conv_weight_flip_multi: table must be a 16-B aligned device array");
+  ProfScope prof(stream, PROF_CONV, 64.0 * 64.0 * 4.0 * total_blocks);
+  MOE_LAUNCH(prof, conv_weight_flip_multi_kernel, dim3(total_blocks), dim3(256), 0, stream,
+             static_cast<const FlipDesc*>(table), n);
+  return check_launch("rtdetr_conv_weight_flip_multi");
 }
 
 extern "C" int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS) {

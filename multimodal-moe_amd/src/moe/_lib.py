@@ -109,6 +109,8 @@ SIGNATURES = {
     "rtdetr_conv_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
     "rtdetr_conv_dgrad_workspace": (_LL, [_I, _I, _I, _I, _I, _I]),
     "rtdetr_conv_dgrad": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "rtdetr_conv_dgrad_preflipped": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "rtdetr_conv_weight_flip_multi": (_I, [_P, _I, _I, _P]),
     "rtdetr_conv_wgrad_splits": (_I, [_I, _I, _I, _I, _I, _I]),
     "rtdetr_conv_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "rtdetr_conv_wgrad": (_I, [_P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P]),

@@ -81,6 +81,75 @@ def _fwd(x, w, bias=None, resid=None, relu=False, st=1):
     return y
 
 
+# Batched weight flips (GraphedStep): the data gradients of the flipping
+# shapes read W' from persistent per-weight buffers, all written by ONE
+# rtdetr_conv_weight_flip_multi launch right before the backward (49 flip
+# launches per C2 step before).  Entries are keyed by (weight address, shape):
+# the flip runs after the forward, so whatever bf16 weight lives at a key's
+# address then is the one its data gradient reads (captured graphs keep every
+# address); an unregistered weight takes the per-call flip and registers.
+_FLIP_ON = [False]     # inside batched_flips(): register, and use W' buffers flipped at entry
+_FLIP_VALID = [False]  # the W' buffers hold this backward's weights
+_FLIP_REG: dict = {}
+_FLIP_TABLE = [None, 0, 0, 0]  # (device table, n, total blocks, registry size it was built for)
+
+
+def _flip_entry(w, nb):
+    key = (w.data_ptr(), tuple(w.shape))
+    e = _FLIP_REG.get(key)
+    if e is None and _FLIP_ON[0]:
+        e = _FLIP_REG[key] = torch.empty(nb // 2, dtype=torch.bfloat16, device=w.device)
+    return e
+
+
+def _flip_all(dev):
+    import numpy as np
+
+    from ..moe import _lib as L
+
+    if not _FLIP_REG:
+        return
+    if _FLIP_TABLE[3] != len(_FLIP_REG):
+        dt = np.dtype([("w", np.uint64), ("wt", np.uint64), ("N", np.int32), ("C", np.int32), ("KS", np.int32),
+                       ("block0", np.int32)])
+        rec = np.zeros(len(_FLIP_REG), dtype=dt)
+        b0 = 0
+        for i, ((ptr, shape), buf) in enumerate(_FLIP_REG.items()):
+            N, C, ks = shape[0], shape[1], shape[2]
+            rec[i] = (ptr, buf.data_ptr(), N, C, ks, b0)
+            b0 += (C // 64) * (N // 64) * ks * ks
+        _FLIP_TABLE[:] = [torch.from_numpy(rec.view(np.uint8).copy()).to(dev), len(_FLIP_REG), b0, len(_FLIP_REG)]
+    t, n, blocks, _ = _FLIP_TABLE
+    L._check(L.lib().rtdetr_conv_weight_flip_multi(t.data_ptr(), n, blocks, L._stream()),
+             "rtdetr_conv_weight_flip_multi")
+
+
+class batched_flips:
+    """Context for a backward (GraphedStep): every registered weight flipped in
+    one launch at entry, the data gradients then read the flipped buffers."""
+
+    def __init__(self, device):
+        self.device = device
+
+    def __enter__(self):
+        if _BATCHED_FLIPS:
+            _FLIP_ON[0] = True
+            if _FLIP_TABLE[3] != len(_FLIP_REG) and torch.cuda.is_current_stream_capturing():
+                return self  # (a table rebuild copies from the host: not inside a capture) register only
+            _flip_all(self.device)
+            _FLIP_VALID[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _FLIP_ON[0] = False
+        _FLIP_VALID[0] = False
+        return False
+
+
+# MOE_BATCHED_FLIPS=0: every flipping data gradient writes its own W' (A/B switch)
+_BATCHED_FLIPS = os.environ.get("MOE_BATCHED_FLIPS", "1") != "0"
+
+
 def _bwd(x, w, g, need_x, need_w, mask_input, add=None, st=1):
     """(dx, dw) of y = conv(x, w) for the output gradient g; dx += add (x's
     other consumer's gradient, when given), then dx is zeroed where x <= 0 when
@@ -96,11 +165,24 @@ def _bwd(x, w, g, need_x, need_w, mask_input, add=None, st=1):
     if need_x:
         gx = torch.empty((B, C, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         nb = L.lib().rtdetr_conv_dgrad_workspace(B, H, W, C, N, ks)
-        work = torch.empty(nb // 2, dtype=torch.bfloat16, device=x.device) if nb > 0 else None
-        L._check(L.lib().rtdetr_conv_dgrad(g.data_ptr(), w.data_ptr(), None if work is None else work.data_ptr(),
-                                           gx.data_ptr(), z, B, H, W, C, N, ks, st,
-                                           None if add is None else _nhwc(add).data_ptr(),
-                                           x.data_ptr() if mask_input else None, s), "rtdetr_conv_dgrad")
+        pre = None
+        if nb > 0 and _FLIP_ON[0] and w.dtype == torch.bfloat16:
+            key = (w.data_ptr(), tuple(w.shape))
+            if _FLIP_VALID[0] and key in _FLIP_REG:
+                pre = _FLIP_REG[key]  # flipped at the backward's entry
+            work = _flip_entry(w, nb)  # (registers it: flipped in place by this call, batched from then on)
+        else:
+            work = torch.empty(nb // 2, dtype=torch.bfloat16, device=x.device) if nb > 0 else None
+        addp = None if add is None else _nhwc(add).data_ptr()
+        maskp = x.data_ptr() if mask_input else None
+        if pre is not None:
+            L._check(L.lib().rtdetr_conv_dgrad_preflipped(g.data_ptr(), w.data_ptr(), pre.data_ptr(), gx.data_ptr(), z,
+                                                          B, H, W, C, N, ks, st, addp, maskp, s),
+                     "rtdetr_conv_dgrad_preflipped")
+        else:
+            L._check(L.lib().rtdetr_conv_dgrad(g.data_ptr(), w.data_ptr(), None if work is None else work.data_ptr(),
+                                               gx.data_ptr(), z, B, H, W, C, N, ks, st, addp, maskp, s),
+                     "rtdetr_conv_dgrad")
     if need_w:
         ns = L.lib().rtdetr_conv_wgrad_splits(B, _out(H, ks, st), _out(W, ks, st), C, N, ks)
         part = torch.empty(ns * N * C * ks * ks, dtype=torch.float32, device=x.device)

@@ -182,7 +182,13 @@ class GraphedStep:
     def _grads(self, loss):
         """Gradients of every parameter: autograd for most, the conforming dense
         layers' weight + bias gradients batched after it (linear.DeferredWgrad)."""
-        with deferred_weight_grads() as deferred:
+        from .conv import batched_flips
+        from contextlib import nullcontext
+
+        # bf16 weights live at fixed addresses: the convolutions' flipped weights in one launch
+        # (conv.batched_flips); autocast's per-step weight casts would not
+        flips = nullcontext() if self.autocast else batched_flips(loss.device)
+        with deferred_weight_grads() as deferred, flips:
             grads = torch.autograd.grad(loss, self.params, allow_unused=True)
         self.deferred_layers = 0 if deferred is None else len(deferred.items)
         return merge_deferred(self.params, grads, deferred)

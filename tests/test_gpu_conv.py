@@ -291,3 +291,38 @@ def test_conv_big_tile_bit_exact(hip_lib, stride, flip):
         for k, v in _DEFAULTS.items():
             hip_lib.rtdetr_conv_set_tuning(k.encode(), v)
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+def test_batched_flip_matches_per_call_flip(hip_lib):
+    """rtdetr_conv_weight_flip_multi + rtdetr_conv_dgrad_preflipped (conv.batched_flips, GraphedStep) give
+    bitwise the data gradient of the per-call flip, for two weights of different shapes in one table."""
+    from src.moe import _lib as L
+    from src.rtdetr_moe import conv as Cv
+
+    dev = torch.device("cuda")
+    torch.manual_seed(3)
+    cases = [(8, 256, 256, 92, 160, 3), (8, 1024, 256, 46, 80, 1)]
+    ws, gs, xs = [], [], []
+    for B, C, N, H, W, ks in cases:
+        assert L.lib().rtdetr_conv_dgrad_workspace(B, H, W, C, N, ks) > 0  # shapes that flip
+        ws.append((torch.randn(N, C, ks, ks, device=dev) * 0.05).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last))
+        xs.append(torch.randn(B, C, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        gs.append(torch.randn(B, N, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+    ref = [Cv._bwd(x, w, g, True, False, False)[0] for x, w, g in zip(xs, ws, gs)]
+    Cv._FLIP_REG.clear()
+    Cv._FLIP_TABLE[:] = [None, 0, 0, 0]
+    try:
+        with Cv.batched_flips(dev):  # registers (per-call flips into the persistent buffers)
+            first = [Cv._bwd(x, w, g, True, False, False)[0] for x, w, g in zip(xs, ws, gs)]
+        assert len(Cv._FLIP_REG) == 2
+        for bufs in Cv._FLIP_REG.values():
+            bufs.zero_()  # the batched flip must rewrite them
+        with Cv.batched_flips(dev):  # one multi-flip launch, then the preflipped data gradients
+            second = [Cv._bwd(x, w, g, True, False, False)[0] for x, w, g in zip(xs, ws, gs)]
+        torch.cuda.synchronize()
+        for r, a, b in zip(ref, first, second):
+            assert torch.equal(r, a) and torch.equal(r, b)
+    finally:
+        Cv._FLIP_REG.clear()
+        Cv._FLIP_TABLE[:] = [None, 0, 0, 0]
