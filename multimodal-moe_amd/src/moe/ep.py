@@ -282,10 +282,14 @@ def _route_padded_eager(x, wg, ctx_bias, ctx_img, tpi, k, normalize, S):
     return xp, w, lb, z, pos, hist.to(torch.int32)
 
 
-def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=False):
+def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=False, aux_coefs=None):
     """-> (y [T, d], lb, z, hist [E]) of one expert-parallel MoE layer;
     residual=True: y = x + FFN(x), on the HIP bf16 path folded into the
-    combine (returned with ``y_has_residual`` set on the layer)."""
+    combine (returned with ``y_has_residual`` set on the layer).
+    aux_coefs=(lb_coef, z_coef) on the GPU: lb and z come back detached and
+    ``layer.ep_aux_weighted`` holds the differentiable lb_coef lb + z_coef z
+    from the fused aux-loss kernel (MoEFFN; one launch each way)."""
+    layer.ep_aux_weighted = None
     layer.y_has_residual = False
     cfg = layer.cfg
     E, W, k = cfg.num_experts, layer.ep_size, cfg.top_k
@@ -299,7 +303,7 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=Fals
     gs = getattr(layer, "ep_grad_scale", 1.0 / W)  # 1.0 when the optimizer applies 1/W (graph-mode TrainStep)
     if x.is_cuda:
         from . import _lib as L
-        from .ops import aux_losses_hip, combine_hip as combine
+        from .ops import aux_loss_weighted, aux_losses_hip, combine_hip as combine
         from .ops import expert_ffn_mx_hip, route_dispatch_hip, route_dispatch_mx_hip
 
         if fp8:
@@ -308,9 +312,14 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=Fals
         else:
             xp, w, auxp, pos, hist, _, _ = route_dispatch_hip(x, layer.wg, ctx_bias, ctx_img, tokens_per_image, k,
                                                               cfg.normalize, cap, pad=S)
-        # lb and z (differentiable) from the single-GPU path's aux-loss kernel:
-        # one HIP launch each way instead of ~20 torch ops
-        lb, z = aux_losses_hip(auxp, hist, T, k)
+        # lb and z from the single-GPU path's aux-loss kernel: one HIP launch each
+        # way instead of ~20 torch ops (differentiable, or the weighted sum when
+        # the caller passes its coefficients)
+        if aux_coefs is not None:
+            layer.ep_aux_weighted, raw = aux_loss_weighted(auxp, hist, T, k, *aux_coefs)
+            lb, z = raw[0], raw[1]
+        else:
+            lb, z = aux_losses_hip(auxp, hist, T, k)
     else:
         from .eager import combine_eager as combine, expert_ffn_eager, expert_ffn_mx_eager
 

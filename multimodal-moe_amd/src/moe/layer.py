@@ -55,6 +55,7 @@ class MoEFFN(nn.Module):
         self.last_ep_overflow = None  # EP without capacity: assignments beyond the a2a slots (device)
         self.last_tokens = 0   # T of the last forward (bench: EP exchange bytes)
         self.y_has_residual = False  # EP: the residual was folded into the combine
+        self.ep_aux_weighted = None  # EP on the GPU: lb_coef lb + z_coef z from the fused kernel
 
     def forward(self, x: torch.Tensor, ctx_img: torch.Tensor | None, residual: bool = False) -> torch.Tensor:
         """x [B, L, d] (image-major tokens), ctx_img int [B] -> [B, L, d].
@@ -71,10 +72,11 @@ class MoEFFN(nn.Module):
         if self.ep_size > 1 or cfg.expert_parallel:  # C4: experts sharded over ranks, all-to-all exchange
             from .ep import moe_ffn_ep
 
-            y, lb, z, hist = moe_ffn_ep(self, flat, cb, ci, L, cap, residual=residual)
+            y, lb, z, hist = moe_ffn_ep(self, flat, cb, ci, L, cap, residual=residual,
+                                        aux_coefs=(cfg.lb_coef, cfg.z_coef))
             if residual and self.y_has_residual:  # folded into the combine
                 self.last_aux = (lb, z)
-                self.last_aux_weighted = None
+                self.last_aux_weighted = self.ep_aux_weighted
                 self.last_hist = hist
                 return y.to(x.dtype).view(B, L, d)
         elif flat.is_cuda:
@@ -96,7 +98,7 @@ class MoEFFN(nn.Module):
         if residual:
             y = flat + y
         self.last_aux = (lb, z)
-        self.last_aux_weighted = None
+        self.last_aux_weighted = getattr(self, "ep_aux_weighted", None)
         self.last_hist = hist
         return y.view(B, L, d)
 

@@ -369,14 +369,19 @@ class _AuxLossRaw(torch.autograd.Function):
         ctx.save_for_backward(wcoef)
         ctx.nblk = auxp.shape[0]
         ctx.set_materialize_grads(False)
-        return out[0].clone(), out[1].clone()
+        return out[0], out[1]  # (views of the kernel's output: no copies)
 
     @staticmethod
     def backward(ctx, g_lb, g_z):
         (wcoef,) = ctx.saved_tensors
         E = wcoef.numel() - 1
-        zero = torch.zeros((), dtype=wcoef.dtype, device=wcoef.device)
-        scale = torch.cat([(g_lb if g_lb is not None else zero).expand(E), (g_z if g_z is not None else zero).view(1)])
+        if g_lb is None and g_z is None:
+            return None, None, None, None
+        if g_lb is None or g_z is None:
+            zero = torch.zeros((), dtype=wcoef.dtype, device=wcoef.device)
+            g_lb = zero if g_lb is None else g_lb
+            g_z = zero if g_z is None else g_z
+        scale = torch.cat([g_lb.reshape(1).expand(E), g_z.reshape(1)])
         return (scale * wcoef).view(1, -1).expand(ctx.nblk, -1), None, None, None
 
 
