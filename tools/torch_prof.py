@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--out", default="gpurun_out/tprof.txt")
     ap.add_argument("--spec", default="rtdetr-r50-moe8-top2")
     ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--single-ctx", action="store_true", help="single-context batches (bench.py c4)")
+    ap.add_argument("--glue-shapes", action="store_true",
+                    help="record shapes: glue ops (adds, casts, fills) grouped by input shape")
     ap.add_argument("--stacks", action="store_true",
                     help="also attribute glue ops (casts, adds, fills, ReLU backward) to source lines")
     a = ap.parse_args()
@@ -42,7 +45,7 @@ def main():
     torch.backends.cudnn.benchmark = True  # as bench.py (--conv-search)
     dev = torch.device("cuda", 0)
     model = bench.build_model(a.spec, dev, 1)
-    data = SyntheticZOD(batch=a.batch, img_h=720, img_w=1280, seed=1000)
+    data = SyntheticZOD(batch=a.batch, img_h=720, img_w=1280, seed=1000, single_context=0 if a.single_ctx else None)
     images, targets, ctx = data.sample()
     images = images.to(dev).contiguous(memory_format=torch.channels_last)
     ctx = ctx.to(dev)
@@ -54,7 +57,7 @@ def main():
     torch.cuda.synchronize()
     acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
     cfg = torch._C._profiler._ExperimentalConfig(verbose=True) if a.stacks else None
-    with torch.profiler.profile(activities=acts, record_shapes=not a.stacks, with_stack=a.stacks,
+    with torch.profiler.profile(activities=acts, record_shapes=a.glue_shapes or not a.stacks, with_stack=a.stacks,
                                 experimental_config=cfg) as prof:
         for _ in range(a.steps):
             step(images, ctx, targets, nb)
@@ -68,6 +71,12 @@ def main():
                          max_shapes_column_width=100))
         f.write("\n\n# by op name\n")
         f.write(prof.key_averages().table(sort_by="device_time_total", row_limit=80, max_name_column_width=60))
+        if a.glue_shapes:
+            f.write("\n\n# glue ops by input shape (count per step, device ms per step)\n")
+            rows = [(e.device_time_total / 1e3 / a.steps, e.count / a.steps, e.key, str(e.input_shapes)[:150])
+                    for e in ka if e.key in GLUE]
+            rows.sort(key=lambda r: -r[0])
+            f.write("\n".join(f"{t:8.3f} ms {c:7.1f}/step  {n:26s} {sh}" for t, c, n, sh in rows[:80]) + "\n")
         if a.stacks:
             f.write("\n\n# glue ops by source line (count per step, device ms per step)\n")
             f.write(glue_by_line(prof, a.steps))
