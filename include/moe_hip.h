@@ -161,10 +161,15 @@ int moe_token_bwd_res(const void* dxp, const int32_t* pos, const float* probs,
  * not NULL, the context-bias gradient dcb fp32 [C,E]: row c = the sum of
  * dlogits over the tokens of the images with ctx_img[b] == c.  One launch,
  * fixed-order sums (bitwise repeatable; replaces a torch fp32 GEMM and an
- * atomic index_add).  part is unused (may be NULL) and
- * moe_router_wgrad_slices returns 0: both stay for the C-ABI.
+ * atomic index_add).  part: a 16-B aligned fp32 workspace of
+ * moe_router_wgrad_workspace(B, tpi, E, d) bytes (no initialisation needed):
+ * the chunked kernel (token chunks x column slices, per-chunk partials summed
+ * in chunk order by the last workgroup of each slice; its arrival counters are
+ * the tail of moe_set_splitk_workspace's counter array); when that returns 0
+ * (no counters registered, d % 64 != 0, or tuning router_wgrad_chunked=0) or
+ * part is NULL the per-column one-pass kernel runs and part is unused.
  * Reference: the router backward of SURVEY 8(a) row a7. */
-int moe_router_wgrad_slices(int tpi);
+long long moe_router_wgrad_workspace(int B, int tpi, int E, int d);
 int moe_router_wgrad(const float* dlogits, const void* x, const int32_t* ctx_img, int B, int tpi, int E, int d,
                      int C, float* part, float* dwg, float* dcb, hipStream_t stream);
 

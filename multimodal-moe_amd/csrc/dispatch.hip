@@ -236,6 +236,7 @@ namespace moe {
 // rows from source 0, then source 1, ...):
 //   offsets[e] = sum_{e' < e} sum_w cnt[w][e'],  offsets[El] = the total
 //   gather[offsets[e] + sum_{w' < w} cnt[w'][e] + j] = (w El + e) S + j
+//   gather[offsets[El] ...] = 0 (every one of the W El S entries is written)
 // One workgroup per (w, e) pair (its prefix recomputed from the <= 1024
 // counts), so the map is one launch with no host sync; workgroup 0 also
 // writes offsets and the overflow of this rank's send histogram,
@@ -245,14 +246,20 @@ __global__ __launch_bounds__(256) void ep_compaction_kernel(const int32_t* __res
                                                             int S, int32_t* __restrict__ gather,
                                                             int32_t* __restrict__ offsets,
                                                             int32_t* __restrict__ overflow) {
-  __shared__ int s_start;
+  __shared__ int s_start, s_pad;
   const int b = blockIdx.x, w = b / El, e = b % El;
   if (threadIdx.x == 0) {
-    int st = 0;
+    int st = 0, tot = 0;
     for (int ww = 0; ww < W; ++ww)
-      for (int ee = 0; ee < El; ++ee)
-        if (ee < e || (ee == e && ww < w)) st += min(cnt[ww * El + ee], S);
+      for (int ee = 0; ee < El; ++ee) {
+        const int c = min(cnt[ww * El + ee], S);
+        tot += c;
+        if (ee < e || (ee == e && ww < w)) st += c;
+      }
     s_start = st;
+    // this pair's S - n padding entries of the tail [tot, W El S), in compact
+    // pair order: (pairs before it) S - st entries precede them
+    s_pad = tot + (e * W + w) * S - st;
   }
   if (b == 0) {
     for (int ee = threadIdx.x; ee <= El; ee += blockDim.x) {
@@ -271,6 +278,9 @@ __global__ __launch_bounds__(256) void ep_compaction_kernel(const int32_t* __res
   const int n = min(cnt[b], S), st = s_start;
   const int src0 = b * S;
   for (int j = threadIdx.x; j < n; j += blockDim.x) gather[st + j] = src0 + j;
+  // the tail past the received rows points at received row 0 (a valid row for
+  // any reader that loads a whole tile's indices): no memset of the map
+  for (int j = n + threadIdx.x; j < S; j += blockDim.x) gather[s_pad + (j - n)] = 0;
 }
 
 }  // namespace moe

@@ -168,6 +168,7 @@ def main():
     ap.add_argument("--variants", default="0")
     ap.add_argument("--stages", default="0")
     ap.add_argument("--only", default="")
+    ap.add_argument("--tune", action="append", default=[], help="key=value for moe_set_tuning (repeatable)")
     ap.add_argument("--config", choices=["c2", "c5"], default="c2", help="layer shapes (C2: E8 k2 bs8; C5: E32 k4 bs16)")
     ap.add_argument("--debug", default="0", help="comma list of gemm_debug modes (1 no C stores, 2 no main loop)")
     ap.add_argument("--bm", default="0", help="comma list of forced row-tile heights (0 = auto) for rows and wgrad")
@@ -181,6 +182,9 @@ def main():
     a = ap.parse_args()
     SKEW[0] = a.skew
     L.lib()
+    for kv in a.tune:
+        key, val = kv.split("=", 1)
+        L.set_tuning(key, int(val))
     if a.cold:
         global _FLUSH
         _FLUSH = torch.zeros(128 << 20, device="cuda", dtype=torch.float32)

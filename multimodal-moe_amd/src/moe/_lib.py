@@ -96,7 +96,7 @@ SIGNATURES = {
                                       _P, _I, _P, _P, _P]),
     "moe_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "moe_set_splitk_workspace": (_I, [_P, ctypes.c_size_t, _P, _I]),
-    "moe_router_wgrad_slices": (_I, [_I]),
+    "moe_router_wgrad_workspace": (_LL, [_I, _I, _I, _I]),
     "moe_router_wgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "rtdetr_hungarian_match": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "rtdetr_set_criterion_match": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
@@ -532,7 +532,7 @@ def ep_compaction(recv_cnt, hist, S):
     _need(recv_cnt, torch.int32, "recv_cnt")
     _need(hist, torch.int32, "hist")
     W, El = recv_cnt.shape
-    gather = torch.zeros(W * El * S, dtype=torch.int32, device=recv_cnt.device)
+    gather = torch.empty(W * El * S, dtype=torch.int32, device=recv_cnt.device)  # (all entries written)
     offsets = torch.empty(El + 1, dtype=torch.int32, device=recv_cnt.device)
     overflow = torch.empty(1, dtype=torch.int32, device=recv_cnt.device)
     _check(lib().moe_ep_compaction(_ptr(recv_cnt), _ptr(hist), W, El, hist.numel(), int(S), _ptr(gather),
@@ -618,19 +618,25 @@ def router_wgrad(dlogits, x, ctx_img, tokens_per_image, n_ctx):
     T, E = dlogits.shape
     d = x.shape[1]
     has_ctx = ctx_img is not None and n_ctx > 0
-    # without a context bias the image split only shapes the slices: all T
-    # tokens are one "image" then (any tokens_per_image, including 0, works)
-    tpi = int(tokens_per_image) if has_ctx else max(T, 1)
-    if tpi <= 0 or T % tpi:
+    # the image split shapes the token chunks (the same with or without dcb, so
+    # dWg does not depend on it); without a context bias any tokens_per_image
+    # works: one "image" of all T tokens when it does not divide T
+    tpi = int(tokens_per_image) if tokens_per_image else 0
+    if has_ctx and (tpi <= 0 or T % tpi):
         raise MoEKernelError(f"router_wgrad: T = {T} is not a multiple of tokens_per_image = {tpi}")
+    if tpi <= 0 or T % tpi:
+        tpi = max(T, 1)
     B = T // tpi
     dwg = torch.empty((E, d), dtype=torch.float32, device=x.device)
     dcb = None
     if has_ctx:
         _need(ctx_img, torch.int32, "ctx_img")
         dcb = torch.empty((n_ctx, E), dtype=torch.float32, device=x.device)
+    ensure_splitk_workspace(x.device)  # (registers the chunked kernel's arrival counters)
+    nbytes = lib().moe_router_wgrad_workspace(B, tpi, E, d) if T > 0 else 0
+    part = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=x.device) if nbytes > 0 else None
     _check(lib().moe_router_wgrad(_ptr(dlogits), _ptr(x), _ptr(ctx_img) if dcb is not None else None, B, tpi, E, d,
-                                  int(n_ctx) if dcb is not None else 0, None, _ptr(dwg), _ptr(dcb), _stream()),
+                                  int(n_ctx) if dcb is not None else 0, _ptr(part), _ptr(dwg), _ptr(dcb), _stream()),
            "moe_router_wgrad")
     return dwg, dcb
 

@@ -345,9 +345,10 @@ class _AuxLoss(torch.autograd.Function):
         out, wcoef = L.aux_loss_fwd(auxp.contiguous(), hist, T, k, lb_coef, z_coef)
         ctx.save_for_backward(wcoef)
         ctx.nblk = auxp.shape[0]
-        ctx.mark_non_differentiable(out)
+        raw = out[:2]
+        ctx.mark_non_differentiable(raw)
         ctx.set_materialize_grads(False)
-        return out[2].clone(), out[:2]
+        return out[2], raw  # (views of the kernel's output: no copy)
 
     @staticmethod
     def backward(ctx, g, _raw):

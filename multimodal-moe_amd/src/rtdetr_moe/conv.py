@@ -283,6 +283,50 @@ class _ConvHIPFork(torch.autograd.Function):
         return gx, gw, g if ctx.needs_input_grad[2] else None, None, None, None, None
 
 
+class _ConvHIPPair(torch.autograd.Function):
+    """(conv(x, w1), conv(x, w2)): two stride-1 convolutions of the same input
+    (RT-DETR's RepVgg 3x3 + 1x1 branches, CSPRep's two 1x1 entry layers).
+    Backward: the second data gradient adds the first in its epilogue (the
+    `add` operand of rtdetr_conv_dgrad), so x's gradient needs no separate
+    accumulation launch by autograd."""
+
+    @staticmethod
+    def forward(ctx, x, w1, w2):
+        x = _nhwc(x)
+        w1, w2 = _nhwc(w1), _nhwc(w2)
+        ctx.save_for_backward(x, w1, w2)
+        ctx.set_materialize_grads(False)
+        return _fwd(x, w1), _fwd(x, w2)
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        x, w1, w2 = ctx.saved_tensors
+        nx, nw1, nw2 = ctx.needs_input_grad
+        gx = gw1 = gw2 = None
+        if g1 is not None:
+            gx, gw1 = _bwd(x, w1, g1, nx, nw1, False)
+        if g2 is not None:
+            gx, gw2 = _bwd(x, w2, g2, nx, nw2, False, add=gx)
+        return gx, gw1, gw2
+
+
+def conv_pair(conv1: torch.nn.Conv2d, conv2: torch.nn.Conv2d, x):
+    """(conv1(x), conv2(x)) for two bias-free stride-1 nn.Conv2d on the same
+    input: one autograd node on the HIP kernels (_ConvHIPPair) when both take
+    them (after autocast's casts), else conv_module twice."""
+    if (_PAIR_ON and conv1.bias is None and conv2.bias is None and _stride(conv1.stride) == 1
+            and _stride(conv2.stride) == 1):
+        xc, w1 = _autocast_operands(x, conv1.weight, conv1.stride, conv1.padding, conv1.dilation, conv1.groups)
+        _, w2 = _autocast_operands(x, conv2.weight, conv2.stride, conv2.padding, conv2.dilation, conv2.groups)
+        if (hip_conv_ok(xc, w1, conv1.stride, conv1.padding, conv1.dilation, conv1.groups)
+                and hip_conv_ok(xc, w2, conv2.stride, conv2.padding, conv2.dilation, conv2.groups)):
+            return _ConvHIPPair.apply(xc, w1, w2)
+    return conv_module(conv1, x), conv_module(conv2, x)
+
+
+_PAIR_ON = os.environ.get("MOE_CONV_PAIR", "1") != "0"
+
+
 def _autocast_operands(x, w, stride, padding, dilation=1, groups=1):
     """Under bf16 autocast (TrainStep precision "amp": fp32 weights) a
     convolution computes on bf16 casts of its input and weight -- autocast's

@@ -12,7 +12,7 @@ from ..moe.config import MoEConfig
 from ..moe.layer import MoEFFN
 from .norm import AddLayerNorm
 from .backbone import _FUSED_BN, ConvNormLayer
-from .conv import conv_module
+from .conv import conv_module, conv_pair
 from .fused import bn_act, bn_act_ok
 from .linear import TokenLinear, TokenSelfAttention
 
@@ -107,7 +107,7 @@ class RepVggBlock(nn.Module):
 
     def forward(self, x):
         if _FUSED_BN:
-            y1, y2 = conv_module(self.conv1.conv, x), conv_module(self.conv2.conv, x)
+            y1, y2 = conv_pair(self.conv1.conv, self.conv2.conv, x)  # one node: dx accumulated in the dgrad
             if bn_act_ok([y1, y2], [self.conv1.norm, self.conv2.norm]):  # both BNs + sum + SiLU in HIP
                 return bn_act([y1, y2], [self.conv1.norm, self.conv2.norm], "silu")
             return F.silu(self.conv1.norm(y1) + self.conv2.norm(y2))
@@ -124,6 +124,14 @@ class CSPRepLayer(nn.Module):
         self.conv3 = ConvNormLayer(hidden, cout, 1, 1, "silu") if hidden != cout else nn.Identity()
 
     def forward(self, x):
+        c1, c2 = self.conv1, self.conv2
+        if _FUSED_BN and not c1.fold and not c2.fold:
+            y1, y2 = conv_pair(c1.conv, c2.conv, x)  # one node: dx accumulated in the dgrad
+            if bn_act_ok([y1], [c1.norm]) and bn_act_ok([y2], [c2.norm]):
+                a1, a2 = bn_act([y1], [c1.norm], "silu"), bn_act([y2], [c2.norm], "silu")
+            else:
+                a1, a2 = c1.act(c1.norm(y1)), c2.act(c2.norm(y2))
+            return self.conv3(self.bottlenecks(a1) + a2)
         return self.conv3(self.bottlenecks(self.conv1(x)) + self.conv2(x))
 
 

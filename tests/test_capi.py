@@ -22,7 +22,7 @@ def test_header_declares_the_expected_entry_points():
               "moe_token_bwd", "moe_grouped_gemm", "moe_grouped_gemm_wgrad", "moe_last_error",
               "moe_quantize_mx", "moe_permute_fwd_mx", "moe_grouped_gemm_mx", "moe_grouped_gemm_wgrad_mx",
               "moe_set_splitk_workspace", "train_grad_pack", "rtdetr_attn_fwd", "rtdetr_attn_bwd", "rtdetr_conv_fwd", "rtdetr_conv_dgrad", "rtdetr_conv_dgrad_workspace", "rtdetr_conv_wgrad_splits", "rtdetr_conv_set_tuning", "rtdetr_conv_wgrad", "train_grad_sqnorm", "train_grad_norm_finalize", "train_adamw_step",
-              "moe_router_wgrad", "moe_router_wgrad_slices",
+              "moe_router_wgrad", "moe_router_wgrad_workspace",
               "rtdetr_linear_wgrad_narrow", "rtdetr_linear_wgrad_narrow_parts",
               "rtdetr_maxpool3x3s2_nhwc_fwd", "rtdetr_upcat_nhwc_fwd", "rtdetr_upcat_nhwc_bwd"]:
         assert s in syms

@@ -326,3 +326,32 @@ def test_batched_flip_matches_per_call_flip(hip_lib):
     finally:
         Cv._FLIP_REG.clear()
         Cv._FLIP_TABLE[:] = [None, 0, 0, 0]
+
+
+@pytest.mark.parametrize("C,N,H,W", [(256, 256, 46, 80), (256, 128, 23, 40)])
+def test_conv_pair_matches_two_convolutions(hip_lib, C, N, H, W):
+    """conv.conv_pair (RepVgg 3x3 + 1x1 on one input, one autograd node whose
+    second data gradient adds the first in its epilogue) == two separate HIP
+    convolutions: outputs and weight gradients bitwise, the input gradient
+    within one bf16 rounding of autograd's bf16 sum of the two."""
+    from src.rtdetr_moe import conv as Cv
+
+    torch.manual_seed(5)
+    dev = torch.device("cuda")
+    c1 = torch.nn.Conv2d(C, N, 3, 1, 1, bias=False).to(dev, torch.bfloat16).to(memory_format=torch.channels_last)
+    c2 = torch.nn.Conv2d(C, N, 1, 1, 0, bias=False).to(dev, torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(4, C, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g1, g2 = (torch.randn(4, N, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+              for _ in range(2))
+    outs = []
+    for pair in (True, False):
+        xa = x.clone().requires_grad_(True)
+        y1, y2 = Cv.conv_pair(c1, c2, xa) if pair else (Cv.conv_module(c1, xa), Cv.conv_module(c2, xa))
+        assert (y1.grad_fn.name() == y2.grad_fn.name()) == pair
+        grads = torch.autograd.grad((y1, y2), (xa, c1.weight, c2.weight), (g1, g2))
+        outs.append((y1, y2) + grads)
+    torch.cuda.synchronize()
+    (a1, a2, ax, aw1, aw2), (b1, b2, bx, bw1, bw2) = outs
+    assert torch.equal(a1, b1) and torch.equal(a2, b2) and torch.equal(aw1, bw1) and torch.equal(aw2, bw2)
+    d = (ax.float() - bx.float()).abs()
+    assert d.max().item() <= 2 ** -7 * bx.float().abs().max().item()

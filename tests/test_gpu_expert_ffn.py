@@ -128,12 +128,16 @@ def test_ep_compaction_matches_torch_map(hip_lib, W, El, S):
     cnt = torch.randint(0, S + 3, (W, El), generator=g).int()
     E = W * El
     hist = torch.randint(0, 2 * S + 1, (E,), generator=g).int()
+    g0 = L.ep_compaction(cnt.to(DEV), hist.to(DEV), S)[0]
+    g0.fill_(-7)  # every entry must be (re)written: the map is allocated uninitialised (the
+    del g0        # caching allocator hands this block back to the next call)
     gather, offs, ovf = L.ep_compaction(cnt.to(DEV), hist.to(DEV), S)
     g_ref, _inv, o_ref = compaction_map(cnt.clamp(max=S).to(torch.int64), S)
     torch.cuda.synchronize()
     n = int(o_ref[-1])
     assert torch.equal(offs.cpu(), o_ref.int())
     assert torch.equal(gather[:n].cpu(), g_ref[:n].cpu())
+    assert bool((gather[n:] == 0).all())  # the tail points at received row 0
     assert int(ovf[0]) == int((hist - S).clamp(min=0).sum())
 
 
