@@ -166,8 +166,9 @@ int moe_token_bwd_res(const void* dxp, const int32_t* pos, const float* probs,
  * the chunked kernel (token chunks x column slices, per-chunk partials summed
  * in chunk order by the last workgroup of each slice; its arrival counters are
  * the tail of moe_set_splitk_workspace's counter array); when that returns 0
- * (no counters registered, d % 64 != 0, or tuning router_wgrad_chunked=0) or
- * part is NULL the per-column one-pass kernel runs and part is unused.
+ * (the default: tuning router_wgrad_chunked=0 -- measured no faster at C2 --,
+ * no counters registered, or d % 64 != 0) or part is NULL the per-column
+ * one-pass kernel runs and part is unused.
  * Reference: the router backward of SURVEY 8(a) row a7. */
 long long moe_router_wgrad_workspace(int B, int tpi, int E, int d);
 int moe_router_wgrad(const float* dlogits, const void* x, const int32_t* ctx_img, int B, int tpi, int E, int d,

@@ -185,5 +185,5 @@ int check_launch(const char* what);        // returns 0 or -(1000 + err)
 // of the split-K counter array registered by moe_set_splitk_workspace
 constexpr int kRouterWgradCounters = 64;
 void router_wgrad_set_counters(int dev, int32_t* cnt);
-extern int g_router_wgrad_chunked;  // moe_set_tuning("router_wgrad_chunked"): 1 (default) / 0 = per-column kernel
+extern int g_router_wgrad_chunked;  // moe_set_tuning("router_wgrad_chunked"): 1 = chunked kernel / 0 (default) = per-column kernel
 }  // namespace moe

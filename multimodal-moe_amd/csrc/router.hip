@@ -1056,7 +1056,7 @@ __global__ __launch_bounds__(256) void router_wgrad_chunk_kernel(
 }
 
 static int32_t* g_rw_cnt[64];
-int g_router_wgrad_chunked = 1;
+int g_router_wgrad_chunked = 0;  // A/B: not faster than the per-column kernel at C2
 
 void router_wgrad_set_counters(int dev, int32_t* cnt) {
   if (dev >= 0 && dev < 64) g_rw_cnt[dev] = cnt;

@@ -592,7 +592,7 @@ def test_route_dispatch_matches_scan_index_aux(hip_lib, T, E, k, cf):
 def test_router_wgrad_vs_fp64(hip_lib, B, tpi, E, C, chunked):
     """moe_router_wgrad: dWg = dlogits^T x and the per-context sums of
     dlogits (contexts repeated across images, one context unused) against an
-    fp64 reference, chunked kernel (default) and per-column kernel; fixed-order
+    fp64 reference, chunked kernel and per-column kernel (default); fixed-order
     sums, so two launches are bitwise equal and dWg does not depend on whether
     dcb is formed."""
     from src.moe import _lib as L
@@ -611,7 +611,7 @@ def test_router_wgrad_vs_fp64(hip_lib, B, tpi, E, C, chunked):
         dwg0, dcb0 = L.router_wgrad(dl, x, None, tpi, 0)
         torch.cuda.synchronize()
     finally:
-        L.set_tuning("router_wgrad_chunked", 1)
+        L.set_tuning("router_wgrad_chunked", 0)
     ref = dl.double().t() @ x.double()
     per_img = dl.double().view(B, tpi, E).sum(1)
     ref_cb = torch.zeros((C, E), dtype=torch.float64, device=DEV).index_add_(0, ci.long(), per_img)
