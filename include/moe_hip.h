@@ -543,6 +543,14 @@ int rtdetr_bn_act_fwd(const void* const* x, const float* const* gamma, const flo
 int rtdetr_bn_act_bwd(const void* dy, const void* const* x, const float* const* gamma, int nb, long long M, int C,
                       int act, const float* saved, float* ws, float* coef, void* const* dx, float* dgb,
                       hipStream_t stream);
+/* rtdetr_bn_act_fwd with the batch statistics already summed per row block
+ * by the producing convolution (rtdetr_conv_fwd_stats): part fp32
+ * [nb][part_blocks][2][C] (sum, sum of squares of the bf16 x_i),
+ * 1 <= part_blocks <= 2048; no statistics pass, no workspace. */
+int rtdetr_bn_act_fwd_part(const void* const* x, const float* const* gamma, const float* const* beta,
+                           float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act,
+                           float eps, float momentum, const float* part, int part_blocks, float* saved, void* y,
+                           hipStream_t stream);
 
 /* Process-wide tuning overrides (not thread-safe; set before launching).  By
  * default (0) every launch picks its own kernel variant, ring depth and tile
@@ -676,6 +684,14 @@ int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, 
  * the previous step's sums (tools/miopen_graph_probe.py). */
 int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void* zero, int B, int H, int W, int C, int N,
                     int KS, int stride, const float* bias, const void* resid, int relu, hipStream_t stream);
+/* rtdetr_conv_fwd (no epilogue) that also writes the BatchNorm statistics of
+ * its bf16 output: part fp32 [ceil(B Ho Wo / rows)][2][N], row block r = the
+ * column sums and sums of squares over output pixels [r rows, (r + 1) rows),
+ * rows = rtdetr_conv_fwd_stats_rows(...) (the forward's M-tile height).  For
+ * rtdetr_bn_act_fwd_part (the encoder's ConvNormLayer / RepVgg BatchNorms). */
+int rtdetr_conv_fwd_stats_rows(int B, int H, int W, int C, int N, int KS, int stride);
+int rtdetr_conv_fwd_stats(const void* x, const void* w, void* y, const void* zero, int B, int H, int W, int C,
+                          int N, int KS, int stride, float* part, hipStream_t stream);
 long long rtdetr_conv_dgrad_workspace(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_dgrad(const void* dy, const void* w, void* work, void* dx, const void* zero, int B, int H, int W,
                       int C, int N, int KS, int stride, const void* add, const void* relu_mask, hipStream_t stream);

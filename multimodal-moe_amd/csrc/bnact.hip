@@ -30,7 +30,8 @@ struct BnArgs {
   int nb;  // branches: 1 or 2
 };
 
-constexpr int BN_MAX_BLOCKS = 1024;  // partial-sum blocks of a reduction (4 per CU)
+constexpr int BN_MAX_BLOCKS = 2048;  // partial rows a finalize reduces (the convolution-epilogue statistics: one per M tile)
+constexpr int BN_BLOCKS = 1024;      // partial-sum blocks of bn_stats / bn_bwd_reduce (4 per CU)
 constexpr int BN_FIN_T = 1024;        // finalize threads: 8 channels x 128 block lanes
 
 __device__ __forceinline__ void load8f(const float* p, float* v) {
@@ -324,7 +325,7 @@ static int bn_grid(long long nchunk) {
 // rows per block and block count of the reductions: a function of M only
 static void bn_blocks(long long M, int* nblk, int* rpb) {
   long long n = (M + 63) / 64;
-  if (n > BN_MAX_BLOCKS) n = BN_MAX_BLOCKS;
+  if (n > BN_BLOCKS) n = BN_BLOCKS;
   if (n < 1) n = 1;
   *rpb = (int)((M + n - 1) / n);
   *nblk = (int)((M + *rpb - 1) / *rpb);
@@ -344,14 +345,17 @@ using namespace moe;
 
 extern "C" size_t rtdetr_bn_act_workspace(long long M, int C, int nb) {
   (void)M;
-  return (size_t)BN_MAX_BLOCKS * 3 * C * (nb > 1 ? 2 : 1) * sizeof(float);
+  return (size_t)BN_BLOCKS * 3 * C * (nb > 1 ? 2 : 1) * sizeof(float);
 }
 
-extern "C" int rtdetr_bn_act_fwd(const void* const* x, const float* const* gamma, const float* const* beta,
-                                 float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act,
-                                 float eps, float momentum, float* saved, float* ws, void* y, hipStream_t stream) {
+static int bn_act_fwd_impl(const void* const* x, const float* const* gamma, const float* const* beta,
+                           float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act,
+                           float eps, float momentum, float* saved, float* ws, const float* part, int part_blocks,
+                           void* y, hipStream_t stream) {
   if (int rc = bn_check(nb, M, C, act)) return rc;
-  if (!x || !gamma || !beta || !saved || !ws || !y) return fail("bn_act_fwd: NULL argument");
+  if (!x || !gamma || !beta || !saved || !y || (!ws && !part)) return fail("bn_act_fwd: NULL argument");
+  if (part != nullptr && (part_blocks < 1 || part_blocks > BN_MAX_BLOCKS))
+    return fail("bn_act_fwd_part: need 1 <= part_blocks <= 2048");
   BnArgs a{};
   a.nb = nb;
   for (int i = 0; i < nb; ++i) {
@@ -366,12 +370,14 @@ extern "C" int rtdetr_bn_act_fwd(const void* const* x, const float* const* gamma
   int nblk, rpb;
   bn_blocks(M, &nblk, &rpb);
   const long long nchunk = M * (C / 8);
-  {
+  if (part == nullptr) {
     ProfScope prof(stream, PROF_CONV_EPI, 2.0 * nb * M * C);
     MOE_LAUNCH(prof, bn_stats_kernel, dim3(nblk, nb), dim3(256), 2 * 2048 * sizeof(float), stream, a, M, C, rpb, ws);
+  } else {
+    nblk = part_blocks;  // the producing convolution's epilogue wrote them (rtdetr_conv_fwd_stats)
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8, nb), dim3(BN_FIN_T), 0, stream, a, ws, nblk, M, C, eps, momentum,
-                   saved);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8, nb), dim3(BN_FIN_T), 0, stream, a, part ? part : ws, nblk, M, C,
+                     eps, momentum, saved);
   {
     ProfScope prof(stream, PROF_CONV_EPI, 2.0 * (nb + 1) * M * C);
 #define BN_APPLY(A, N)                                                                                  \
@@ -385,6 +391,22 @@ extern "C" int rtdetr_bn_act_fwd(const void* const* x, const float* const* gamma
 #undef BN_APPLY
   }
   return check_launch("rtdetr_bn_act_fwd");
+}
+
+extern "C" int rtdetr_bn_act_fwd(const void* const* x, const float* const* gamma, const float* const* beta,
+                                 float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act,
+                                 float eps, float momentum, float* saved, float* ws, void* y, hipStream_t stream) {
+  return bn_act_fwd_impl(x, gamma, beta, run_mean, run_var, nb, M, C, act, eps, momentum, saved, ws, nullptr, 0, y,
+                         stream);
+}
+
+extern "C" int rtdetr_bn_act_fwd_part(const void* const* x, const float* const* gamma, const float* const* beta,
+                                      float* const* run_mean, float* const* run_var, int nb, long long M, int C,
+                                      int act, float eps, float momentum, const float* part, int part_blocks,
+                                      float* saved, void* y, hipStream_t stream) {
+  if (part == nullptr) return fail("bn_act_fwd_part: part is NULL");
+  return bn_act_fwd_impl(x, gamma, beta, run_mean, run_var, nb, M, C, act, eps, momentum, saved, nullptr, part,
+                         part_blocks, y, stream);
 }
 
 extern "C" int rtdetr_bn_act_bwd(const void* dy, const void* const* x, const float* const* gamma, int nb,

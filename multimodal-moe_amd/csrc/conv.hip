@@ -77,6 +77,10 @@ struct ConvArgs {
   // class's taps are ky' in {1} (ry = 0) or {0, 2} (ry = 1) (kx' likewise),
   // reading dY at (a + (ky' == 2), c + (kx' == 2))
   int ry, rx, Hd, Wd;
+  // forward only (rtdetr_conv_fwd_stats): per-tile column sums of the stored
+  // bf16 output and of its square, stats[(m0 / BM) * 2 + {0, 1}][n] (the
+  // partial layout of the BatchNorm statistics, csrc/bnact.hip)
+  float* stats;
 };
 
 // Wait until K-tile kt's DMA has landed for this wave: up to min(S - 2, newer)
@@ -246,6 +250,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
     eb[4] = b1.x; eb[5] = b1.y; eb[6] = b1.z; eb[7] = b1.w;
   }
   const bool efloat = a.resid != nullptr || a.bias != nullptr || a.relu;
+  float st_s[8], st_q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) st_s[e] = st_q[e] = 0.f;
   __syncthreads();  // every wave is done reading the ring
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -305,6 +312,40 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
         v = make_uint4(vw[0], vw[1], vw[2], vw[3]);
       }
       *reinterpret_cast<uint4*>(a.y + grow(p) * a.N + n0 + c * 8) = v;
+      if constexpr (!PH) {
+        if (a.stats != nullptr) {  // BatchNorm statistics of the stored values
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            st_s[e] += f[e];
+            st_q[e] = fmaf(f[e], f[e], st_q[e]);
+          }
+        }
+      }
+    }
+  }
+  if constexpr (!PH) {
+    if (a.stats != nullptr) {  // the RPP row groups' sums added in row order
+      __syncthreads();  // every thread is done reading the output image
+      float* red = reinterpret_cast<float*>(smem);  // [2][RPP][BN]
+      const int rg = tid / CPR;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[rg * BN + ec * 8 + e] = st_s[e];
+        red[(RPP + rg) * BN + ec * 8 + e] = st_q[e];
+      }
+      __syncthreads();
+      for (int c = tid; c < BN; c += NTH) {
+        float s1 = 0.f, s2 = 0.f;
+        for (int r = 0; r < RPP; ++r) {
+          s1 += red[r * BN + c];
+          s2 += red[(RPP + r) * BN + c];
+        }
+        float* pp = a.stats + (size_t)(m0 / BM) * 2 * a.N + n0 + c;
+        pp[0] = s1;
+        pp[a.N] = s2;
+      }
     }
   }
 }
@@ -602,6 +643,14 @@ static void launch_fwd(const ConvArgs& a, hipStream_t stream, ProfScope& prof) {
 // tile rows: 128 (two workgroups per CU); 64 when 128-row tiles would leave
 // the chip under-filled (< 1.5 workgroups per CU); 256 rows of 4 waves (one
 // workgroup per CU) measured slower at every C2 shape
+// rows per partial of rtdetr_conv_fwd_stats (the forward's M-tile height): the
+// statistics come as ceil(B Ho Wo / rows) partial rows of [2][N]
+static int fwd_bm(long long P, int N) {
+  int bm = g_conv_bm;
+  if (bm != 64 && bm != 128 && bm != 256) bm = (long long)((P + 127) / 128) * (N / (N % 128 == 0 ? 128 : 64)) < 384 ? 64 : 128;
+  return bm;
+}
+
 template <bool BT, bool PH = false>
 static void launch_fwd_any(const ConvArgs& a, int KS, hipStream_t stream, ProfScope& prof) {
   if (g_conv_big > 0) {  // "conv_big" 1: the 8-wave 256 x 128 tile where N % 128 == 0
@@ -613,9 +662,7 @@ static void launch_fwd_any(const ConvArgs& a, int KS, hipStream_t stream, ProfSc
         return;
     }
   }
-  int bm = g_conv_bm;
-  if (bm != 64 && bm != 128 && bm != 256)
-    bm = (long long)((a.P + 127) / 128) * (a.N / (a.N % 128 == 0 ? 128 : 64)) < 384 ? 64 : 128;
+  const int bm = fwd_bm(a.P, a.N);
   if constexpr (PH) {  // 3x3 only
     if (bm == 256) launch_fwd<3, 256, BT, true>(a, stream, prof);
     else if (bm == 64) launch_fwd<3, 64, BT, true>(a, stream, prof);
@@ -681,6 +728,39 @@ extern "C" int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void
                  false, 0.0, 2.0 * P * N * KS * KS * C);
   launch_fwd_any<false>(a, KS, stream, prof);
   return check_launch("rtdetr_conv_fwd");
+}
+
+extern "C" int rtdetr_conv_fwd_stats_rows(int B, int H, int W, int C, int N, int KS, int stride) {
+  (void)C;
+  if (B <= 0 || H <= 0 || W <= 0 || N <= 0 || (KS != 1 && KS != 3) || (stride != 1 && stride != 2)) return 0;
+  return fwd_bm((long long)B * conv_out(H, KS, stride) * conv_out(W, KS, stride), N);
+}
+
+extern "C" int rtdetr_conv_fwd_stats(const void* x, const void* w, void* y, const void* zero, int B, int H, int W,
+                                     int C, int N, int KS, int stride, float* part, hipStream_t stream) {
+  const void* ptrs[4] = {x, w, y, zero};
+  if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, stride, "rtdetr_conv_fwd_stats")) return rc;
+  if (part == nullptr || !aligned16(part)) return fail("rtdetr_conv_fwd_stats: part must be 16-B aligned");
+  if (B == 0) return 0;
+  const int Ho = conv_out(H, KS, stride), Wo = conv_out(W, KS, stride);
+  ConvArgs a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(y),
+             static_cast<const uint16_t*>(zero), B, Ho, Wo, C, N, B * Ho * Wo, 0, H, W, stride, 0,
+             nullptr, nullptr, nullptr, 0};
+  a.stats = part;
+  const double P = a.P;
+  ProfScope prof(stream, PROF_CONV, 2.0 * ((double)B * H * W * C + P * N) + 2.0 * N * KS * KS * C, false, 0.0,
+                 2.0 * P * N * KS * KS * C);
+  const int bm = fwd_bm(a.P, N);  // (the default tiles: never the A/B "conv_big" shapes)
+  if (KS == 3) {
+    if (bm == 256) launch_fwd<3, 256, false, false>(a, stream, prof);
+    else if (bm == 64) launch_fwd<3, 64, false, false>(a, stream, prof);
+    else launch_fwd<3, 128, false, false>(a, stream, prof);
+  } else {
+    if (bm == 256) launch_fwd<1, 256, false, false>(a, stream, prof);
+    else if (bm == 64) launch_fwd<1, 64, false, false>(a, stream, prof);
+    else launch_fwd<1, 128, false, false>(a, stream, prof);
+  }
+  return check_launch("rtdetr_conv_fwd_stats");
 }
 
 extern "C" long long rtdetr_conv_dgrad_workspace(int B, int H, int W, int C, int N, int KS) {

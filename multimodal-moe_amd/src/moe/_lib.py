@@ -107,6 +107,9 @@ SIGNATURES = {
     "rtdetr_attn_bwd": (_I, [_P, _LL, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _P, _P, _P, _LL, _P, _LL, _P, _LL,
                              _I, _I, _I, _I, _F, _P]),
     "rtdetr_conv_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
+    "rtdetr_conv_fwd_stats_rows": (_I, [_I, _I, _I, _I, _I, _I, _I]),
+    "rtdetr_conv_fwd_stats": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "rtdetr_bn_act_fwd_part": (_I, [_P, _P, _P, _P, _P, _I, ctypes.c_longlong, _I, _I, _F, _F, _P, _I, _P, _P, _P]),
     "rtdetr_conv_dgrad_workspace": (_LL, [_I, _I, _I, _I, _I, _I]),
     "rtdetr_conv_dgrad": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "rtdetr_conv_dgrad_preflipped": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
@@ -919,6 +922,33 @@ def bn_act_fwd(xs, gammas, betas, run_means, run_vars, act, eps, momentum):
     pv, kv = _ptrs(run_vars) if has_run else (None, None)
     _check(lib().rtdetr_bn_act_fwd(px, pg, pb, pm, pv, nb, M, C, int(act), float(eps), float(momentum),
                                    _ptr(saved), _ptr(ws), _ptr(y), _stream()), "rtdetr_bn_act_fwd")
+    return y, saved
+
+
+def bn_act_fwd_part(xs, gammas, betas, run_means, run_vars, act, eps, momentum, part):
+    """bn_act_fwd with the statistics partials of rtdetr_conv_fwd_stats:
+    part fp32 [nb, nblk, 2, C]."""
+    M, C = _nhwc_rows(xs[0], "x0")
+    nb = len(xs)
+    for i, x in enumerate(xs[1:], 1):
+        if _nhwc_rows(x, f"x{i}") != (M, C):
+            raise MoEKernelError("bn_act: branches differ in shape")
+    _need(part, torch.float32, "part")
+    if part.dim() != 4 or part.shape[0] != nb or part.shape[2] != 2 or part.shape[3] != C:
+        raise MoEKernelError(f"bn_act_fwd_part: part must be [{nb}, nblk, 2, {C}], got {tuple(part.shape)}")
+    for t in list(gammas) + list(betas) + [r for r in run_means + run_vars if r is not None]:
+        _need(t, torch.float32, "bn affine/statistics")
+    y = torch.empty_like(xs[0])
+    saved = torch.empty((nb, 4, C), dtype=torch.float32, device=y.device)
+    px, kx = _ptrs(xs)
+    pg, kg = _ptrs(gammas)
+    pb, kb = _ptrs(betas)
+    has_run = all(r is not None for r in run_means + run_vars)
+    pm, km = _ptrs(run_means) if has_run else (None, None)
+    pv, kv = _ptrs(run_vars) if has_run else (None, None)
+    _check(lib().rtdetr_bn_act_fwd_part(px, pg, pb, pm, pv, nb, M, C, int(act), float(eps), float(momentum),
+                                        _ptr(part), int(part.shape[1]), _ptr(saved), _ptr(y), _stream()),
+           "rtdetr_bn_act_fwd_part")
     return y, saved
 
 

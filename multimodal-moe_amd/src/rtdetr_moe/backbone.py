@@ -16,7 +16,7 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
-from .conv import conv2d, conv2d_add_bias_relu_fork, conv2d_bias_relu, conv_module, hip_conv_ok_for
+from .conv import conv2d, conv2d_add_bias_relu_fork, conv2d_bias_relu, conv_module, conv_module_stats, hip_conv_ok_for
 from .fused import AddBiasReLU, AddBiasReLUFork, BiasReLU, bn_act, bn_act_ok
 
 _FUSED_BN = os.environ.get("MOE_FUSED_BN", "1") != "0"  # A/B switch: training BN + SiLU in HIP
@@ -220,9 +220,12 @@ class ConvNormLayer(nn.Module):
             if self.act_name == "relu":
                 return BiasReLU.apply(y, shift)
             return y + shift.view(1, -1, 1, 1).to(y.dtype)
+        if self.act_name in (None, "silu") and _FUSED_BN:
+            y, part = conv_module_stats(self.conv, x)  # (the BN statistics from the conv epilogue)
+            if bn_act_ok([y], [self.norm]):
+                return bn_act([y], [self.norm], self.act_name, part)  # BN + SiLU in HIP (training statistics)
+            return self.act(self.norm(y))
         y = conv_module(self.conv, x)
-        if self.act_name in (None, "silu") and _FUSED_BN and bn_act_ok([y], [self.norm]):
-            return bn_act([y], [self.norm], self.act_name)  # BN + SiLU in HIP (training statistics)
         return self.act(self.norm(y))
 
 

@@ -81,6 +81,35 @@ def _fwd(x, w, bias=None, resid=None, relu=False, st=1):
     return y
 
 
+def _stats_blocks(x, w, st=1):
+    """Row blocks of rtdetr_conv_fwd_stats' BatchNorm partials for y =
+    conv(x, w) (0: too many for the BatchNorm finalize -- take bn_stats)."""
+    from ..moe import _lib as L
+
+    B, C, H, W = x.shape
+    N, _, ks, _ = w.shape
+    rows = L.lib().rtdetr_conv_fwd_stats_rows(B, H, W, C, N, ks, st)
+    if rows <= 0:
+        return 0
+    nblk = -(-(B * _out(H, ks, st) * _out(W, ks, st)) // rows)
+    return nblk if nblk <= 2048 else 0
+
+
+def _fwd_stats(x, w, part, st=1):
+    """conv(x, w) that also writes its output's BatchNorm partials into part
+    (fp32 [nblk, 2, N], rtdetr_conv_fwd_stats)."""
+    from ..moe import _lib as L
+
+    B, C, H, W = x.shape
+    N, _, ks, _ = w.shape
+    y = torch.empty((B, N, _out(H, ks, st), _out(W, ks, st)), dtype=torch.bfloat16, device=x.device,
+                    memory_format=torch.channels_last)
+    L._check(L.lib().rtdetr_conv_fwd_stats(x.data_ptr(), w.data_ptr(), y.data_ptr(), _zero(x.device).data_ptr(),
+                                           B, H, W, C, N, ks, st, part.data_ptr(), L._stream()),
+             "rtdetr_conv_fwd_stats")
+    return y
+
+
 # Batched weight flips (GraphedStep): the data gradients of the flipping
 # shapes read W' from persistent per-weight buffers, all written by ONE
 # rtdetr_conv_weight_flip_multi launch right before the backward (49 flip
@@ -283,48 +312,104 @@ class _ConvHIPFork(torch.autograd.Function):
         return gx, gw, g if ctx.needs_input_grad[2] else None, None, None, None, None
 
 
+class _ConvHIPStats(torch.autograd.Function):
+    """(conv(x, w), BatchNorm partials fp32 [1, nblk, 2, N] of its output) for
+    a training BatchNorm that follows (fused.bn_act(parts=...)): the
+    statistics pass over y is folded into the convolution's epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, w, nblk, st):
+        x = _nhwc(x)
+        w = _nhwc(w)
+        part = torch.empty((1, nblk, 2, w.shape[0]), dtype=torch.float32, device=x.device)
+        y = _fwd_stats(x, w, part[0], st)
+        ctx.st = st
+        ctx.save_for_backward(x, w)
+        ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, gy, _gpart):
+        x, w = ctx.saved_tensors
+        if gy is None:
+            return None, None, None, None
+        gx, gw = _bwd(x, w, gy, ctx.needs_input_grad[0], ctx.needs_input_grad[1], False, None, ctx.st)
+        return gx, gw, None, None
+
+
+def conv_module_stats(conv: torch.nn.Conv2d, x):
+    """(conv(x), BatchNorm partials or None): `conv_module` whose HIP forward
+    also sums its output's BatchNorm statistics (_ConvHIPStats) when that
+    applies (MOE_CONV_BN_STATS=0: never)."""
+    if _STATS_ON and conv.bias is None:
+        xc, wc = _autocast_operands(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups)
+        if hip_conv_ok(xc, wc, conv.stride, conv.padding, conv.dilation, conv.groups):
+            st = _stride(conv.stride)
+            nblk = _stats_blocks(xc, wc, st)
+            if nblk > 0:
+                return _ConvHIPStats.apply(xc, wc, nblk, st)
+            return _ConvHIP.apply(xc, wc, None, False, False, False, None, st), None
+    return conv_module(conv, x), None
+
+
 class _ConvHIPPair(torch.autograd.Function):
     """(conv(x, w1), conv(x, w2)): two stride-1 convolutions of the same input
     (RT-DETR's RepVgg 3x3 + 1x1 branches, CSPRep's two 1x1 entry layers).
     Backward: the second data gradient adds the first in its epilogue (the
     `add` operand of rtdetr_conv_dgrad), so x's gradient needs no separate
-    accumulation launch by autograd."""
+    accumulation launch by autograd.  nblk > 0: the forwards also write their
+    outputs' BatchNorm partials, returned as a third output [2, nblk, 2, N]."""
 
     @staticmethod
-    def forward(ctx, x, w1, w2):
+    def forward(ctx, x, w1, w2, nblk=0):
         x = _nhwc(x)
         w1, w2 = _nhwc(w1), _nhwc(w2)
         ctx.save_for_backward(x, w1, w2)
         ctx.set_materialize_grads(False)
+        if nblk > 0:
+            part = torch.empty((2, nblk, 2, w1.shape[0]), dtype=torch.float32, device=x.device)
+            ctx.mark_non_differentiable(part)
+            return _fwd_stats(x, w1, part[0]), _fwd_stats(x, w2, part[1]), part
         return _fwd(x, w1), _fwd(x, w2)
 
     @staticmethod
-    def backward(ctx, g1, g2):
+    def backward(ctx, g1, g2, _gpart=None):
         x, w1, w2 = ctx.saved_tensors
-        nx, nw1, nw2 = ctx.needs_input_grad
+        nx, nw1, nw2 = ctx.needs_input_grad[:3]
         gx = gw1 = gw2 = None
         if g1 is not None:
             gx, gw1 = _bwd(x, w1, g1, nx, nw1, False)
         if g2 is not None:
             gx, gw2 = _bwd(x, w2, g2, nx, nw2, False, add=gx)
-        return gx, gw1, gw2
+        return gx, gw1, gw2, None
 
 
-def conv_pair(conv1: torch.nn.Conv2d, conv2: torch.nn.Conv2d, x):
-    """(conv1(x), conv2(x)) for two bias-free stride-1 nn.Conv2d on the same
-    input: one autograd node on the HIP kernels (_ConvHIPPair) when both take
-    them (after autocast's casts), else conv_module twice."""
+def conv_pair(conv1: torch.nn.Conv2d, conv2: torch.nn.Conv2d, x, stats=False):
+    """(conv1(x), conv2(x)[, parts]) for two bias-free stride-1 nn.Conv2d on
+    the same input: one autograd node on the HIP kernels (_ConvHIPPair) when
+    both take them (after autocast's casts), else conv_module twice.
+    stats=True: a third element, the outputs' BatchNorm partials
+    [2, nblk, 2, N] for fused.bn_act(parts=...), or None."""
     if (_PAIR_ON and conv1.bias is None and conv2.bias is None and _stride(conv1.stride) == 1
-            and _stride(conv2.stride) == 1):
+            and _stride(conv2.stride) == 1 and conv1.out_channels == conv2.out_channels):
         xc, w1 = _autocast_operands(x, conv1.weight, conv1.stride, conv1.padding, conv1.dilation, conv1.groups)
         _, w2 = _autocast_operands(x, conv2.weight, conv2.stride, conv2.padding, conv2.dilation, conv2.groups)
         if (hip_conv_ok(xc, w1, conv1.stride, conv1.padding, conv1.dilation, conv1.groups)
                 and hip_conv_ok(xc, w2, conv2.stride, conv2.padding, conv2.dilation, conv2.groups)):
-            return _ConvHIPPair.apply(xc, w1, w2)
+            if not stats:
+                return _ConvHIPPair.apply(xc, w1, w2)
+            nblk = _stats_blocks(xc, w1) if _STATS_ON else 0
+            if nblk > 0 and nblk == _stats_blocks(xc, w2):
+                return _ConvHIPPair.apply(xc, w1, w2, nblk)
+            return _ConvHIPPair.apply(xc, w1, w2) + (None,)
+    if stats:
+        return conv_module(conv1, x), conv_module(conv2, x), None
     return conv_module(conv1, x), conv_module(conv2, x)
 
 
 _PAIR_ON = os.environ.get("MOE_CONV_PAIR", "1") != "0"
+_STATS_ON = os.environ.get("MOE_CONV_BN_STATS", "1") != "0"
 
 
 def _autocast_operands(x, w, stride, padding, dilation=1, groups=1):

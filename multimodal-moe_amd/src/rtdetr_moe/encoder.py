@@ -107,9 +107,10 @@ class RepVggBlock(nn.Module):
 
     def forward(self, x):
         if _FUSED_BN:
-            y1, y2 = conv_pair(self.conv1.conv, self.conv2.conv, x)  # one node: dx accumulated in the dgrad
+            # one node: dx accumulated in the dgrad, the BN statistics in the forward epilogues
+            y1, y2, parts = conv_pair(self.conv1.conv, self.conv2.conv, x, stats=True)
             if bn_act_ok([y1, y2], [self.conv1.norm, self.conv2.norm]):  # both BNs + sum + SiLU in HIP
-                return bn_act([y1, y2], [self.conv1.norm, self.conv2.norm], "silu")
+                return bn_act([y1, y2], [self.conv1.norm, self.conv2.norm], "silu", parts)
             return F.silu(self.conv1.norm(y1) + self.conv2.norm(y2))
         return F.silu(self.conv1(x) + self.conv2(x))
 
@@ -126,9 +127,10 @@ class CSPRepLayer(nn.Module):
     def forward(self, x):
         c1, c2 = self.conv1, self.conv2
         if _FUSED_BN and not c1.fold and not c2.fold:
-            y1, y2 = conv_pair(c1.conv, c2.conv, x)  # one node: dx accumulated in the dgrad
+            y1, y2, parts = conv_pair(c1.conv, c2.conv, x, stats=True)  # (as RepVggBlock)
             if bn_act_ok([y1], [c1.norm]) and bn_act_ok([y2], [c2.norm]):
-                a1, a2 = bn_act([y1], [c1.norm], "silu"), bn_act([y2], [c2.norm], "silu")
+                p1, p2 = (None, None) if parts is None else (parts[0:1], parts[1:2])
+                a1, a2 = bn_act([y1], [c1.norm], "silu", p1), bn_act([y2], [c2.norm], "silu", p2)
             else:
                 a1, a2 = c1.act(c1.norm(y1)), c2.act(c2.norm(y2))
             return self.conv3(self.bottlenecks(a1) + a2)

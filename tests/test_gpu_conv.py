@@ -355,3 +355,74 @@ def test_conv_pair_matches_two_convolutions(hip_lib, C, N, H, W):
     assert torch.equal(a1, b1) and torch.equal(a2, b2) and torch.equal(aw1, bw1) and torch.equal(aw2, bw2)
     d = (ax.float() - bx.float()).abs()
     assert d.max().item() <= 2 ** -7 * bx.float().abs().max().item()
+
+
+@pytest.mark.parametrize("B,C,N,H,W,ks,st", [(8, 256, 256, 92, 160, 1, 1), (8, 256, 256, 46, 80, 3, 2),
+                                             (2, 128, 256, 23, 40, 3, 1), (1, 64, 128, 7, 9, 1, 1)])
+def test_conv_fwd_stats_partials(hip_lib, B, C, N, H, W, ks, st):
+    """rtdetr_conv_fwd_stats: the output equals rtdetr_conv_fwd's bit for bit,
+    and its per-row-block partials are the column sums and sums of squares of
+    that bf16 output (fp64 reference; ragged last block, 64- and 128-row
+    tiles, stride 2)."""
+    from src.rtdetr_moe import conv as Cv
+
+    torch.manual_seed(B + C + H)
+    dev = torch.device("cuda")
+    x = torch.randn(B, C, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(N, C, ks, ks, device=dev) * 0.05).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    nblk = Cv._stats_blocks(x, w, st)
+    assert nblk > 0
+    part = torch.full((nblk, 2, N), float("nan"), device=dev)
+    y = Cv._fwd_stats(x, w, part, st)
+    y0 = Cv._fwd(x, w, st=st)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
+    rows = -(-y.shape[0] * y.shape[2] * y.shape[3] // nblk)
+    yf = y.permute(0, 2, 3, 1).reshape(-1, N).double()
+    for blk in (0, nblk - 1):
+        seg = yf[blk * rows:(blk + 1) * rows]
+        assert torch.allclose(part[blk, 0].double(), seg.sum(0), rtol=1e-5, atol=1e-3)
+        assert torch.allclose(part[blk, 1].double(), (seg * seg).sum(0), rtol=1e-5, atol=1e-3)
+    tot = part.double().sum(0)
+    assert torch.allclose(tot[0], yf.sum(0), rtol=1e-5, atol=1e-2)
+    assert torch.allclose(tot[1], (yf * yf).sum(0), rtol=1e-5, atol=1e-2)
+
+
+def test_bn_act_with_conv_stats_matches_stats_pass(hip_lib):
+    """ConvNormLayer / RepVgg with the BatchNorm statistics from the conv
+    epilogue (MOE_CONV_BN_STATS, default) vs the separate statistics pass:
+    the same outputs up to the statistics' summation order, the same running
+    statistics and gradients to fp32 rounding."""
+    import copy
+
+    from src.rtdetr_moe import conv as Cv
+    from src.rtdetr_moe.encoder import RepVggBlock
+
+    torch.manual_seed(11)
+    dev = torch.device("cuda")
+    blk = RepVggBlock(256, 256).to(dev).to(memory_format=torch.channels_last)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.Conv2d):
+            m.to(torch.bfloat16)
+    blk.train()
+    x = torch.randn(4, 256, 46, 80, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(4, 256, 46, 80, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    for on in (True, False):
+        b = copy.deepcopy(blk)
+        Cv._STATS_ON = on
+        try:
+            xa = x.clone().requires_grad_(True)
+            y = b(xa)
+            g = torch.autograd.grad(y, [xa] + [p for p in b.parameters()], gy)
+        finally:
+            Cv._STATS_ON = True
+        res.append((y, g, [t.clone() for t in (b.conv1.norm.running_mean, b.conv1.norm.running_var,
+                                                   b.conv2.norm.running_mean, b.conv2.norm.running_var)]))
+    torch.cuda.synchronize()
+    (ya, ga, ra), (yb, gb, rb) = res
+    assert (ya.float() - yb.float()).abs().max().item() <= 2 ** -6 * yb.float().abs().max().item()
+    for a, b in zip(ra, rb):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
+    for a, b in zip(ga, gb):
+        assert ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item() < 1e-2
