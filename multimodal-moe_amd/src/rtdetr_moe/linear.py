@@ -95,8 +95,29 @@ class DeferredWgrad:
         grads, acc = {}, {}
         direct = {torch.bfloat16: [], torch.float32: []}
         summed = []
+        # a shared layer whose every use covers its whole weight and bias (a
+        # head applied once per decoder layer): each use's fp32 gradient goes
+        # to its own slot of a stacked buffer, summed once over the uses
+        # (one reduction instead of a zero fill and one add per use)
+        uses = {}
+        for gy, x, odt, (wp, wr), (bp, br) in self.items:
+            key = (id(wp), id(bp))
+            full = wr == 0 and br == 0 and gy.shape[1] == wp.shape[0] == bp.shape[0]
+            u = uses.setdefault(key, [0, True, wp, bp, odt])
+            u[0] += 1
+            u[1] = u[1] and full and id(wp) in shared and id(bp) in shared
+        stacked = {}
+        for key, (n, ok, wp, bp, odt) in uses.items():
+            if ok and n > 1 and sum(1 for k2 in uses if id(wp) in k2 or id(bp) in k2) == 1:
+                stacked[key] = [torch.empty((n,) + tuple(wp.shape), dtype=torch.float32, device=wp.device),
+                                torch.empty((n,) + tuple(bp.shape), dtype=torch.float32, device=wp.device), 0, odt]
         for gy, x, odt, (wp, wr), (bp, br) in self.items:
             M, N = gy.shape[1], x.shape[1]
+            st = stacked.get((id(wp), id(bp)))
+            if st is not None:
+                direct[torch.float32].append((gy, x, st[0][st[2]], st[1][st[2]]))
+                st[2] += 1
+                continue
             for p_ in (wp, bp):
                 if id(p_) in shared:
                     if id(p_) not in acc:
@@ -122,6 +143,9 @@ class DeferredWgrad:
                     grads[id(p_)][r0:r0 + part.shape[0]] += part.to(odt)
         for k, (a, odt) in acc.items():
             grads[k] = a.to(odt)
+        for (kw, kb), (bw, bb, _, odt) in stacked.items():
+            grads[kw] = bw.sum(0).to(odt)
+            grads[kb] = bb.sum(0).to(odt)
         self.items.clear()
         return grads
 
