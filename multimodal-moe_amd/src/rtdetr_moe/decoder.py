@@ -441,7 +441,7 @@ class RTDETRDecoder(nn.Module):
         memory = torch.cat([f.flatten(2).permute(0, 2, 1) for f in proj], 1).contiguous()  # [B, S, d]
         B = memory.shape[0]
         anchors, valid = self._anchors(shapes, memory.device, torch.float32)
-        mem_v = valid.to(memory.dtype) * memory
+        vmask = valid.to(memory.dtype)  # [1, S, 1]
         # Query selection.  Only the top-k rows of the encoder-output heads are
         # used downstream (their logits/boxes and the detached decoder targets),
         # so the heads run over all S tokens once without autograd, to rank
@@ -452,10 +452,14 @@ class RTDETRDecoder(nn.Module):
             topk = self.query_override.to(memory.device)
         else:
             with torch.no_grad():
-                enc_rank = self.enc_score_head(self.enc_output(mem_v)).float().max(-1).values
+                enc_rank = self.enc_score_head(self.enc_output(vmask * memory)).float().max(-1).values
             topk = torch.topk(enc_rank, self.num_queries, dim=1).indices
         self.last_topk = topk
-        sel = self.enc_output(mem_v.gather(1, topk[..., None].expand(-1, -1, mem_v.shape[-1])))
+        # (valid * memory) at the selected rows: the mask applied after the
+        # gather (same products), so the backward multiplies [B, Q, d], not [B, S, d]
+        sel_in = memory.gather(1, topk[..., None].expand(-1, -1, memory.shape[-1])) * \
+            vmask.expand(B, -1, -1).gather(1, topk[..., None])
+        sel = self.enc_output(sel_in)
         enc_topk_logits = self.enc_score_head(sel)
         ref_unact = self.enc_bbox_head(sel).float() + anchors.expand(B, -1, -1).gather(
             1, topk[..., None].expand(-1, -1, 4))
