@@ -228,6 +228,13 @@ int moe_grouped_gemm_wgrad_rows(int dtype, const void* x, const void* y, void* c
 int moe_grouped_gemm_gather(int dtype, const void* a, const int32_t* a_gather, const void* b, void* c,
                             const int32_t* offsets, int G, int max_rows, int N, int K, int trans_b,
                             int epilogue, const float* bias, const void* aux, hipStream_t stream);
+/* moe_grouped_gemm_gather whose output row r is stored at row c_rows[r] of c
+ * (the expert-parallel received layout, like moe_expert_ffn_fwd's yp_rows):
+ * the second expert GEMM of the two-launch EP forward for layers with few rows
+ * per expert (src/moe/ep.py).  Rows of c no r maps to are left untouched. */
+int moe_grouped_gemm_scatter(int dtype, const void* a, const int32_t* a_gather, const void* b, void* c,
+                             const int32_t* c_rows, const int32_t* offsets, int G, int max_rows, int N, int K,
+                             int trans_b, int epilogue, const float* bias, const void* aux, hipStream_t stream);
 /* a5: the expert FFN forward in ONE launch,
  *   h  = relu(x[src_tok[r]] . W1_g^T + b1_g)   bf16 [>= offsets[G], F]
  *   yp = h . W2_g^T + b2_g                      bf16 [>= offsets[G], d]

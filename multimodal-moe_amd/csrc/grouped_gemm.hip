@@ -1732,6 +1732,25 @@ extern "C" int moe_grouped_gemm_gather(int dtype, const void* a, const int32_t* 
   return check_launch("moe_grouped_gemm");
 }
 
+extern "C" int moe_grouped_gemm_scatter(int dtype, const void* a, const int32_t* a_gather, const void* b, void* c,
+                                        const int32_t* c_rows, const int32_t* offsets, int G, int max_rows, int N,
+                                        int K, int trans_b, int epilogue, const float* bias, const void* aux,
+                                        hipStream_t stream) {
+  if ((dtype & ~MOE_BIAS_BF16) != MOE_BF16) return fail("grouped_gemm_scatter: only MOE_BF16 is implemented");
+  if (c_rows == nullptr) return fail("grouped_gemm_scatter: c_rows is NULL");
+  RowsPlan pl;
+  WsWin win = device_ws();
+  if (plan_rows(pl, a, b, c, offsets, G, max_rows, N, K, trans_b, epilogue, bias, aux, a_gather, win)) return -1;
+  pl.p.bias_bf16 = (dtype & MOE_BIAS_BF16) ? 1 : 0;
+  pl.p.c_rows = c_rows;
+  if (pl.p.bias_bf16) pl.bytes_fixed -= 2.0 * G * N;
+  if (max_rows == 0) return 0;
+  ProfScope prof(stream, PROF_GEMM, pl.bytes_fixed, true, pl.bytes_row, pl.flops_row);
+  pl.p.prof_rows = prof.rows_slot();
+  launch_rows(pl, stream, prof);
+  return check_launch("moe_grouped_gemm_scatter");
+}
+
 extern "C" int moe_grouped_gemm(int dtype, const void* a, const void* b, void* c,
                                 const int32_t* offsets, int G, int max_rows, int N, int K,
                                 int trans_b, int epilogue, const float* bias, const void* aux,

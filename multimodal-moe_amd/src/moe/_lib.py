@@ -47,6 +47,7 @@ SIGNATURES = {
     "moe_route_index": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "moe_route_dispatch": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P]),
     "moe_grouped_gemm_gather": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "moe_grouped_gemm_scatter": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "moe_expert_ffn_supported": (_I, [_I, _I, _I]),
     "moe_expert_ffn_fwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _P]),
     "moe_ep_compaction": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
@@ -492,6 +493,24 @@ def grouped_gemm_gather(x, src_tok, b, offsets, G, max_rows, N, K, trans_b, epil
 
 def expert_ffn_supported(G, F, d):
     return bool(lib().moe_expert_ffn_supported(int(G), int(F), int(d)))
+
+
+def grouped_gemm_scatter(a, b, offsets, G, max_rows, N, K, trans_b, epilogue, c_rows, out, bias=None, aux=None):
+    """grouped_gemm whose output row r goes to row c_rows[r] of out (bf16
+    [>= max c_rows + 1, N]; rows no r maps to are left as they are)."""
+    _need(a, torch.bfloat16, "a")
+    _need(b, torch.bfloat16, "b")
+    _need(c_rows, torch.int32, "c_rows")
+    _need(out, torch.bfloat16, "out")
+    if b.numel() != G * N * K or a.shape[1] != K or a.shape[0] < max_rows or c_rows.numel() < max_rows:
+        raise MoEKernelError("grouped_gemm_scatter: shapes")
+    if out.dim() != 2 or out.shape[1] != N or not out.is_contiguous():
+        raise MoEKernelError("grouped_gemm_scatter: out must be a contiguous [rows, N] tensor")
+    ensure_splitk_workspace(a.device)
+    _check(lib().moe_grouped_gemm_scatter(_gemm_dtype(bias, G, N), _ptr(a), None, _ptr(b), _ptr(out), _ptr(c_rows),
+                                          _ptr(offsets), G, int(max_rows), N, K, int(trans_b), int(epilogue),
+                                          _ptr(bias), _ptr(aux), _stream()), "moe_grouped_gemm_scatter")
+    return out
 
 
 def expert_ffn_fwd(x, src_tok, w1, b1, w2, b2, offsets, G, max_rows, yp_rows=None, yp_n=0):

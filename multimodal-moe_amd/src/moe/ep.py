@@ -172,9 +172,10 @@ class _EPExpertFFN(torch.autograd.Function):
 
 class _EPExpertFFNScatter(torch.autograd.Function):
     """The local experts over the received rows, in the received layout, with
-    no row-gather passes: the fused expert FFN (moe_expert_ffn_fwd) reads
-    received row gather[r] for compact row r and writes its output row back
-    to received row gather[r]; the backward's first paired launch reads dYp =
+    no row-gather passes: the fused expert FFN (moe_expert_ffn_fwd) -- or, at
+    few rows per expert, GEMM1 gathering + GEMM2 scattering
+    (moe_grouped_gemm_scatter) -- reads received row gather[r] for compact
+    row r and writes its output row back to received row gather[r]; the backward's first paired launch reads dYp =
     dyr[gather] inside the GEMMs, the second gathers xr[gather] for dW1 and
     stores dXp row r at received row gather[r] (moe_grouped_gemm_bwd_pair_
     scatter).  Received rows no expert row maps to (the slots' padding) are
@@ -182,7 +183,7 @@ class _EPExpertFFNScatter(torch.autograd.Function):
     token backward read kept positions only)."""
 
     @staticmethod
-    def forward(ctx, xr, gather, w1, b1, w2, b2, offsets, grad_scale):
+    def forward(ctx, xr, gather, w1, b1, w2, b2, offsets, grad_scale, fused=True):
         from . import _lib as L
         from .ops import _bias
 
@@ -191,7 +192,13 @@ class _EPExpertFFNScatter(torch.autograd.Function):
         xb = xr.to(torch.bfloat16).contiguous()
         w1b = w1.to(torch.bfloat16).contiguous()
         w2b = w2.to(torch.bfloat16).contiguous()
-        h, yr = L.expert_ffn_fwd(xb, gather, w1b, _bias(b1), w2b, _bias(b2), offsets, G, R, yp_rows=gather, yp_n=R)
+        if fused:
+            h, yr = L.expert_ffn_fwd(xb, gather, w1b, _bias(b1), w2b, _bias(b2), offsets, G, R, yp_rows=gather,
+                                     yp_n=R)
+        else:  # few rows per expert: two launches (the fused FFN streams every expert's weights per row tile)
+            h = L.grouped_gemm_gather(xb, gather, w1b, offsets, G, R, F, d, 1, L.EPI_BIAS_RELU, bias=_bias(b1))
+            yr = L.grouped_gemm_scatter(h, w2b, offsets, G, R, d, F, 1, L.EPI_BIAS, gather,
+                                        torch.empty((R, d), dtype=torch.bfloat16, device=xb.device), bias=_bias(b2))
         ctx.save_for_backward(xb, gather, h, w1b, w2b, offsets)
         ctx.meta = (G, R, float(grad_scale), xr.dtype)
         ctx.wdtype = w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32
@@ -213,7 +220,7 @@ class _EPExpertFFNScatter(torch.autograd.Function):
         if s != 1.0:
             for t in (dW1, db1, dW2, db2):
                 t.mul_(s)
-        return dxr.to(xdtype), None, dW1, db1, dW2, db2, None, None
+        return dxr.to(xdtype), None, dW1, db1, dW2, db2, None, None, None
 
 
 def _fused_ep_ok(layer, x, fp8):
@@ -336,7 +343,11 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=Fals
         gather, offs, overflow = L.ep_compaction(recv_cnt, hist, S)
         layer.last_ep_overflow = overflow[0] if cap <= 0 else None
         xr = xp if ident else _Exchange.apply(xp, group, W)
-        yr = _EPExpertFFNScatter.apply(xr, gather, layer.w1, layer.b1, layer.w2, layer.b2, offs, gs)
+        # the one-launch FFN where each local expert receives enough rows (the
+        # single-GPU path's threshold, ops._FUSED_MIN_ROWS), else two launches
+        from .ops import _FUSED_MIN_ROWS
+        fused = T * k * W >= _FUSED_MIN_ROWS * E
+        yr = _EPExpertFFNScatter.apply(xr, gather, layer.w1, layer.b1, layer.w2, layer.b2, offs, gs, fused)
         yp = yr if ident else _Exchange.apply(yr, group, W)
         if residual and x.dtype == torch.bfloat16:
             layer.y_has_residual = True

@@ -174,3 +174,10 @@ def test_scatter_outputs_match_gather_after(hip_lib, rows_per_group):
     assert ys.shape == (n_out, d) and dxs.shape == (n_out, d)
     assert torch.equal(ys[idx], y2[:R])
     assert torch.equal(dxs[idx], dx2[:R])
+    # the two-launch EP forward: GEMM1 gathering, GEMM2 scattering (moe_grouped_gemm_scatter)
+    hg = L.grouped_gemm_gather(x, rows, w1, off, G, R, F, d, 1, L.EPI_BIAS_RELU, bias=b1)
+    yg = L.grouped_gemm_scatter(hg, w2, off, G, R, d, F, 1, L.EPI_BIAS, rows,
+                                torch.empty((n_out, d), dtype=torch.bfloat16, device=DEV), bias=b2)
+    torch.cuda.synchronize()
+    assert torch.equal(hg[:R], h[:R])
+    assert torch.equal(yg[idx], y2[:R])
