@@ -514,6 +514,16 @@ int rtdetr_add_layer_norm_fwd(const void* a, const void* b, const void* gamma, c
 int rtdetr_add_layer_norm_bwd(const void* dout, const void* a, const void* b, const void* gamma, int w_bf16,
                               const float* mean, const float* rstd, long long T, int d, void* ds, float* partials,
                               int P, void* dgamma_dbeta, hipStream_t stream);
+/* The decoder's `t = LN(a + b); q = t + pos` in one pass: out2 = bf16(out +
+ * pos) (pos, out2 bf16 [T, d], both or neither).  bwd2: the gradient of out
+ * is dout + dout2 (summed in bf16 per element, as autograd's accumulation of
+ * the two consumers'; dout2 may be NULL); pos's gradient is dout2 itself. */
+int rtdetr_add_layer_norm_pos_fwd(const void* a, const void* b, const void* gamma, const void* beta, int w_bf16,
+                                  long long T, int d, float eps, const void* pos, void* out, void* out2, float* mean,
+                                  float* rstd, hipStream_t stream);
+int rtdetr_add_layer_norm_bwd2(const void* dout, const void* dout2, const void* a, const void* b, const void* gamma,
+                               int w_bf16, const float* mean, const float* rstd, long long T, int d, void* ds,
+                               float* partials, int P, void* dgamma_dbeta, hipStream_t stream);
 
 /* Decoder box refinement (one launch each way), over n = B*Q*4 elements:
  *   y = sigmoid(delta + log(max(x', eps) / max(1 - x', eps))), x' = clamp(ref, 0, 1)

@@ -61,7 +61,9 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const uint16_t* __restr
                                                          const uint16_t* __restrict__ b, const void* gamma,
                                                          const void* beta, int T, float eps,
                                                          uint16_t* __restrict__ out, float* __restrict__ mean_out,
-                                                         float* __restrict__ rstd_out) {
+                                                         float* __restrict__ rstd_out,
+                                                         const uint16_t* __restrict__ pos = nullptr,
+                                                         uint16_t* __restrict__ out2 = nullptr) {
   constexpr int d = NC * 128;
   const int tid = threadIdx.x, sub = tid & 15;
   float gm[NC][8], bt[NC][8];
@@ -93,7 +95,16 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const uint16_t* __restr
       float o[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mean) * rstd * gm[c][i] + bt[c][i];
-      reinterpret_cast<uint4*>(out + (size_t)t * d)[sub + 16 * c] = pack8(o);
+      const uint4 ob = pack8(o);
+      reinterpret_cast<uint4*>(out + (size_t)t * d)[sub + 16 * c] = ob;
+      if (out2 != nullptr) {  // out2 = out + pos, the bf16 add of the rounded output (torch's `out + pos`)
+        float f[8], q2[8];
+        unpack8(ob, f);
+        unpack8(reinterpret_cast<const uint4*>(pos + (size_t)t * d)[sub + 16 * c], q2);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f[i] += q2[i];
+        reinterpret_cast<uint4*>(out2 + (size_t)t * d)[sub + 16 * c] = pack8(f);
+      }
     }
     if (sub == 0) {
       mean_out[t] = mean;
@@ -108,7 +119,8 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(const uint16_t* __restr
                                                          const uint16_t* __restrict__ b, const void* gamma,
                                                          const float* __restrict__ mean_in,
                                                          const float* __restrict__ rstd_in, int T,
-                                                         uint16_t* __restrict__ ds, float* __restrict__ partials) {
+                                                         uint16_t* __restrict__ ds, float* __restrict__ partials,
+                                                         const uint16_t* __restrict__ dout2 = nullptr) {
   constexpr int d = NC * 128;
   __shared__ float s_red[16][2 * d];
   const int tid = threadIdx.x, sub = tid & 15, rg = tid >> 4;
@@ -124,6 +136,20 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(const uint16_t* __restr
     uint4 rd[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) rd[c] = reinterpret_cast<const uint4*>(dout + (size_t)t * d)[sub + 16 * c];
+    if (dout2 != nullptr) {  // the output's second consumer (out + pos): its gradient summed in bf16 as autograd would
+      uint4 r2[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) r2[c] = reinterpret_cast<const uint4*>(dout2 + (size_t)t * d)[sub + 16 * c];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        float f[8], g2[8];
+        unpack8(rd[c], f);
+        unpack8(r2[c], g2);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f[i] += g2[i];
+        rd[c] = pack8(f);
+      }
+    }
     load_sum<NC>(a, b, t, d, sub, v);
     const float mean = mean_in[t], rstd = rstd_in[t];
     float s1 = 0.f, s2 = 0.f;
@@ -219,25 +245,29 @@ extern "C" int rtdetr_add_layer_norm_parts(long long T) {
   return (int)(p < 1 ? 1 : p > 256 ? 256 : p);
 }
 
-extern "C" int rtdetr_add_layer_norm_fwd(const void* a, const void* b, const void* gamma, const void* beta,
-                                         int w_bf16, long long T, int d, float eps, void* out, float* mean,
-                                         float* rstd, hipStream_t stream) {
-  const void* fwd_ops[2] = {beta, out};
-  if (add_ln_check(a, b, gamma, T, d, "add_layer_norm_fwd", fwd_ops, 2)) return -1;
+extern "C" int rtdetr_add_layer_norm_pos_fwd(const void* a, const void* b, const void* gamma, const void* beta,
+                                             int w_bf16, long long T, int d, float eps, const void* pos, void* out,
+                                             void* out2, float* mean, float* rstd, hipStream_t stream) {
+  const void* fwd_ops[4] = {beta, out, pos, out2};
+  if (add_ln_check(a, b, gamma, T, d, "add_layer_norm_fwd", fwd_ops, 4)) return -1;
+  if ((pos == nullptr) != (out2 == nullptr)) return fail("add_layer_norm_pos_fwd: pos and out2 go together");
   if (beta == nullptr || out == nullptr || mean == nullptr || rstd == nullptr)
     return fail("add_layer_norm_fwd: beta, out, mean and rstd are required");
   if (T == 0) return 0;
   long long grid = (T + 15) / 16;
   if (grid > 2048) grid = 2048;
-  // bytes: a (+ b) read, out written, mean / rstd written, weights once
+  // bytes: a (+ b) read, out written, mean / rstd written, weights once (+ pos read, out2 written)
   ProfScope prof(stream, PROF_CONV_EPI,
-                 2.0 * T * d * (b != nullptr ? 3.0 : 2.0) + 8.0 * T + (w_bf16 ? 4.0 : 8.0) * d);
+                 2.0 * T * d * ((b != nullptr ? 3.0 : 2.0) + (pos != nullptr ? 2.0 : 0.0)) + 8.0 * T +
+                     (w_bf16 ? 4.0 : 8.0) * d);
+  const auto* pb = static_cast<const uint16_t*>(pos);
+  auto* o2 = static_cast<uint16_t*>(out2);
   const auto* ab = static_cast<const uint16_t*>(a);
   const auto* bb = static_cast<const uint16_t*>(b);
   auto* ob = static_cast<uint16_t*>(out);
 #define LNF(NC, WB) \
   MOE_LAUNCH(prof, (add_ln_fwd_kernel<NC, WB>), dim3((unsigned)grid), dim3(256), 0, stream, ab, bb, gamma, beta, \
-             (int)T, eps, ob, mean, rstd)
+             (int)T, eps, ob, mean, rstd, pb, o2)
   if (w_bf16) {
     if (d == 128) { LNF(1, true); } else if (d == 256) { LNF(2, true); } else { LNF(4, true); }
   } else {
@@ -247,26 +277,35 @@ extern "C" int rtdetr_add_layer_norm_fwd(const void* a, const void* b, const voi
   return check_launch("rtdetr_add_layer_norm_fwd");
 }
 
-extern "C" int rtdetr_add_layer_norm_bwd(const void* dout, const void* a, const void* b, const void* gamma,
-                                         int w_bf16, const float* mean, const float* rstd, long long T, int d,
-                                         void* ds, float* partials, int P, void* dgamma_dbeta,
-                                         hipStream_t stream) {
-  const void* bwd_ops[4] = {dout, ds, partials, dgamma_dbeta};
-  if (add_ln_check(a, b, gamma, T, d, "add_layer_norm_bwd", bwd_ops, 4)) return -1;
+extern "C" int rtdetr_add_layer_norm_fwd(const void* a, const void* b, const void* gamma, const void* beta,
+                                         int w_bf16, long long T, int d, float eps, void* out, float* mean,
+                                         float* rstd, hipStream_t stream) {
+  return rtdetr_add_layer_norm_pos_fwd(a, b, gamma, beta, w_bf16, T, d, eps, nullptr, out, nullptr, mean, rstd,
+                                       stream);
+}
+
+extern "C" int rtdetr_add_layer_norm_bwd2(const void* dout, const void* dout2, const void* a, const void* b,
+                                          const void* gamma, int w_bf16, const float* mean, const float* rstd,
+                                          long long T, int d, void* ds, float* partials, int P, void* dgamma_dbeta,
+                                          hipStream_t stream) {
+  const void* bwd_ops[5] = {dout, ds, partials, dgamma_dbeta, dout2};
+  if (add_ln_check(a, b, gamma, T, d, "add_layer_norm_bwd", bwd_ops, 5)) return -1;
   if (dout == nullptr || mean == nullptr || rstd == nullptr || ds == nullptr || partials == nullptr ||
       dgamma_dbeta == nullptr)
     return fail("add_layer_norm_bwd: dout, mean, rstd, ds, partials and dgamma_dbeta are required");
   if (P != rtdetr_add_layer_norm_parts(T)) return fail("add_layer_norm_bwd: P must be rtdetr_add_layer_norm_parts(T)");
   // bytes: dout, a (+ b) read, ds written, per-row statistics, partials out and back, [dgamma; dbeta]
   ProfScope prof(stream, PROF_CONV_EPI,
-                 2.0 * T * d * (b != nullptr ? 4.0 : 3.0) + 8.0 * T + 16.0 * P * d + (w_bf16 ? 6.0 : 12.0) * d);
+                 2.0 * T * d * ((b != nullptr ? 4.0 : 3.0) + (dout2 != nullptr ? 1.0 : 0.0)) + 8.0 * T + 16.0 * P * d +
+                     (w_bf16 ? 6.0 : 12.0) * d);
+  const auto* d2 = static_cast<const uint16_t*>(dout2);
   const auto* db = static_cast<const uint16_t*>(dout);
   const auto* ab = static_cast<const uint16_t*>(a);
   const auto* bb = static_cast<const uint16_t*>(b);
   auto* sb = static_cast<uint16_t*>(ds);
 #define LNB(NC, WB) \
   MOE_LAUNCH(prof, (add_ln_bwd_kernel<NC, WB>), dim3(P), dim3(256), 0, stream, db, ab, bb, gamma, mean, rstd, \
-             (int)T, sb, partials)
+             (int)T, sb, partials, d2)
   if (w_bf16) {
     if (d == 128) { LNB(1, true); } else if (d == 256) { LNB(2, true); } else { LNB(4, true); }
   } else {
@@ -278,4 +317,12 @@ extern "C" int rtdetr_add_layer_norm_bwd(const void* dout, const void* a, const 
   hipLaunchKernelGGL(add_ln_final_kernel, dim3((2 * d + 15) / 16), dim3(256), 0, stream, partials, P, 2 * d,
                      dgamma_dbeta, w_bf16);
   return check_launch("rtdetr_add_layer_norm_bwd(final)");
+}
+
+extern "C" int rtdetr_add_layer_norm_bwd(const void* dout, const void* a, const void* b, const void* gamma,
+                                         int w_bf16, const float* mean, const float* rstd, long long T, int d,
+                                         void* ds, float* partials, int P, void* dgamma_dbeta,
+                                         hipStream_t stream) {
+  return rtdetr_add_layer_norm_bwd2(dout, nullptr, a, b, gamma, w_bf16, mean, rstd, T, d, ds, partials, P,
+                                    dgamma_dbeta, stream);
 }

@@ -81,6 +81,8 @@ SIGNATURES = {
     "rtdetr_add_layer_norm_parts": (_I, [ctypes.c_longlong]),
     "rtdetr_add_layer_norm_fwd": (_I, [_P, _P, _P, _P, _I, ctypes.c_longlong, _I, _F, _P, _P, _P, _P]),
     "rtdetr_add_layer_norm_bwd": (_I, [_P, _P, _P, _P, _I, _P, _P, ctypes.c_longlong, _I, _P, _P, _I, _P, _P]),
+    "rtdetr_add_layer_norm_pos_fwd": (_I, [_P, _P, _P, _P, _I, ctypes.c_longlong, _I, _F, _P, _P, _P, _P, _P, _P]),
+    "rtdetr_add_layer_norm_bwd2": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, ctypes.c_longlong, _I, _P, _P, _I, _P, _P]),
     "rtdetr_box_refine_fwd": (_I, [_P, _I, _P, ctypes.c_longlong, _F, _P, _P]),
     "rtdetr_box_refine_bwd": (_I, [_P, _P, _P, _P, ctypes.c_longlong, _F, _P, _I, _P, _P]),
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),

@@ -357,8 +357,9 @@ class TransformerDecoderLayer(nn.Module):
         self.norm3 = AddLayerNorm(d)
 
     def forward(self, tgt, ref_boxes, memory, shapes, query_pos, ctx, vslot=None):
-        tgt = self.norm1(tgt, self.self_attn(tgt + query_pos, tgt))
-        tgt = self.norm2(tgt, self.cross_attn(tgt + query_pos, ref_boxes, memory, shapes, vslot))
+        # t1 and the cross-attention query t1 + query_pos from one LayerNorm launch
+        tgt, q = self.norm1.with_pos(tgt, self.self_attn(tgt + query_pos, tgt), query_pos)
+        tgt = self.norm2(tgt, self.cross_attn(q, ref_boxes, memory, shapes, vslot))
         tgt = self.norm3(self.ffn(tgt, ctx, residual=True))  # tgt + FFN(tgt)
         return tgt
 

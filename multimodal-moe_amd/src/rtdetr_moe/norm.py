@@ -72,6 +72,58 @@ class _AddLayerNorm(torch.autograd.Function):
         return ds, (ds if ctx.has_b else None), dwb[0], dwb[1], None
 
 
+class _AddLayerNormPos(torch.autograd.Function):
+    """(t, t + pos) with t = LayerNorm(a + b) in one launch (the decoder's
+    cross-attention query); backward: t's two gradients summed inside the
+    LayerNorm backward (no autograd accumulation launch), pos's gradient is
+    the second one itself."""
+
+    @staticmethod
+    def forward(ctx, a, b, weight, bias, pos, eps):
+        d = a.shape[-1]
+        T = a.numel() // d
+        w = weight.contiguous()
+        bb = bias.contiguous()
+        out = torch.empty_like(a)
+        out2 = torch.empty_like(a)
+        mean = torch.empty(T, dtype=torch.float32, device=a.device)
+        rstd = torch.empty(T, dtype=torch.float32, device=a.device)
+        L._check(L.lib().rtdetr_add_layer_norm_pos_fwd(a.data_ptr(), b.data_ptr(), w.data_ptr(), bb.data_ptr(),
+                                                       int(w.dtype == torch.bfloat16), T, d, float(eps),
+                                                       pos.data_ptr(), out.data_ptr(), out2.data_ptr(),
+                                                       mean.data_ptr(), rstd.data_ptr(), L._stream()),
+                 "rtdetr_add_layer_norm_pos_fwd")
+        ctx.save_for_backward(a, b, w, mean, rstd)
+        ctx.set_materialize_grads(False)
+        return out, out2
+
+    @staticmethod
+    def backward(ctx, dout, dout2):
+        a, b, w, mean, rstd = ctx.saved_tensors
+        if dout is None and dout2 is None:
+            return None, None, None, None, None, None
+        d = a.shape[-1]
+        T = a.numel() // d
+        g1 = (dout if dout is not None else dout2).to(torch.bfloat16).contiguous()
+        g2 = dout2.to(torch.bfloat16).contiguous() if (dout is not None and dout2 is not None) else None
+        ds = torch.empty_like(a)
+        lib = L.lib()
+        P = int(lib.rtdetr_add_layer_norm_parts(T))
+        parts = torch.empty((P, 2 * d), dtype=torch.float32, device=a.device)
+        dwb = torch.empty((2, d), dtype=w.dtype, device=a.device)
+        L._check(lib.rtdetr_add_layer_norm_bwd2(g1.data_ptr(), g2.data_ptr() if g2 is not None else None,
+                                                a.data_ptr(), b.data_ptr(), w.data_ptr(),
+                                                int(w.dtype == torch.bfloat16), mean.data_ptr(), rstd.data_ptr(),
+                                                T, d, ds.data_ptr(), parts.data_ptr(), P, dwb.data_ptr(),
+                                                L._stream()),
+                 "rtdetr_add_layer_norm_bwd2")
+        return ds, ds, dwb[0], dwb[1], dout2, None
+
+
+# MOE_LN_POS=0: the decoder's t + pos as a separate add (A/B switch)
+_LN_POS = os.environ.get("MOE_LN_POS", "1") != "0"
+
+
 def add_layer_norm(a: torch.Tensor, b: torch.Tensor | None, weight: torch.Tensor, bias: torch.Tensor,
                    eps: float = 1e-5) -> torch.Tensor:
     """LayerNorm(a + b) over the last dimension (b may be None)."""
@@ -83,6 +135,16 @@ def add_layer_norm(a: torch.Tensor, b: torch.Tensor | None, weight: torch.Tensor
 
 class AddLayerNorm(nn.LayerNorm):
     """nn.LayerNorm whose forward(a, b=None) is LayerNorm(a + b) (fused on the GPU)."""
+
+    def with_pos(self, a: torch.Tensor, b: torch.Tensor, pos: torch.Tensor):
+        """(t, t + pos) with t = LayerNorm(a + b): one launch each way on the
+        GPU (_AddLayerNormPos) when the fused path applies."""
+        if (_LN_POS and len(self.normalized_shape) == 1 and self.weight is not None
+                and _fused_ok(a, b, self.weight, self.bias) and pos.dtype == torch.bfloat16
+                and pos.shape == a.shape and pos.is_contiguous()):
+            return _AddLayerNormPos.apply(a, b, self.weight, self.bias, pos, self.eps)
+        t = self(a, b)
+        return t, t + pos
 
     def forward(self, a: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:  # type: ignore[override]
         if len(self.normalized_shape) != 1 or self.weight is None:

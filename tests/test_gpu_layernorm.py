@@ -105,3 +105,34 @@ def test_add_layer_norm_rejects_bad_shapes(hip_lib):
     rc = lib.rtdetr_add_layer_norm_fwd(x.data_ptr(), None, w.data_ptr(), w.data_ptr(), 1, 4, 192, 1e-5,
                                        out.data_ptr(), st.data_ptr(), st.data_ptr(), L._stream())
     assert rc != 0 and b"d must be" in lib.moe_last_error()
+
+
+@pytest.mark.parametrize("wdtype", [torch.float32, torch.bfloat16])
+def test_add_layer_norm_with_pos_matches_separate_add(hip_lib, wdtype):
+    """AddLayerNorm.with_pos (t and t + pos from one launch, the two gradients
+    of t summed inside the LayerNorm backward) == LayerNorm(a + b) followed by
+    a separate `t + pos`, outputs and every gradient bit for bit (the kernel
+    sums the two bf16 gradients in bf16 exactly as autograd's accumulation)."""
+    from src.rtdetr_moe import norm as N
+
+    torch.manual_seed(4)
+    ln = N.AddLayerNorm(256).cuda().to(wdtype)
+    with torch.no_grad():
+        ln.weight.add_(torch.randn_like(ln.weight) * 0.1)
+        ln.bias.add_(torch.randn_like(ln.bias) * 0.1)
+    a, b, pos = (torch.randn(8, 300, 256, device="cuda").to(torch.bfloat16) for _ in range(3))
+    g1, g2 = (torch.randn(8, 300, 256, device="cuda").to(torch.bfloat16) for _ in range(2))
+    res = []
+    for fused in (True, False):
+        aa, bb, pp = (t.clone().requires_grad_(True) for t in (a, b, pos))
+        if fused:
+            t, q = ln.with_pos(aa, bb, pp)
+            assert q.grad_fn.name() == "_AddLayerNormPosBackward"
+        else:
+            t = ln(aa, bb)
+            q = t + pp
+        grads = torch.autograd.grad((t, q), (aa, bb, pp, ln.weight, ln.bias), (g1, g2))
+        res.append((t, q) + grads)
+    torch.cuda.synchronize()
+    for x, y in zip(*res):
+        assert torch.equal(x, y)
