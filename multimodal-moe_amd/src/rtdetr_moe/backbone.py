@@ -234,7 +234,7 @@ class _AvgPool2x2(torch.autograd.Function):
     / _bwd (one launch each way, 16-B channel vectors)."""
 
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, link=None):
         from ..moe import _lib as L
 
         B, C, H, W = x.shape
@@ -242,6 +242,7 @@ class _AvgPool2x2(torch.autograd.Function):
         L._check(L.lib().rtdetr_avgpool2x2_nhwc_fwd(x.data_ptr(), B, H, W, C, y.data_ptr(), L._stream()),
                  "rtdetr_avgpool2x2_nhwc_fwd")
         ctx.shape = (B, C, H, W)
+        ctx.link = link  # x is a block output whose other consumer is branch2a (GradLink, downsampling shortcut)
         return y
 
     @staticmethod
@@ -255,7 +256,9 @@ class _AvgPool2x2(torch.autograd.Function):
         gx = torch.empty((B, C, H, W), dtype=gy.dtype, device=gy.device, memory_format=torch.channels_last)
         L._check(L.lib().rtdetr_avgpool2x2_nhwc_bwd(gy.data_ptr(), B, H, W, C, gx.data_ptr(), L._stream()),
                  "rtdetr_avgpool2x2_nhwc_bwd")
-        return gx
+        if ctx.link is not None:  # handed to branch2a's dgrad epilogue (which autograd runs after this)
+            ctx.link.g_short = gx
+        return gx, None
 
 
 def stem_max_pool(x, pool: nn.MaxPool2d):
@@ -277,7 +280,7 @@ def stem_max_pool(x, pool: nn.MaxPool2d):
     return pool(x)
 
 
-def avg_pool_2x2(x):
+def avg_pool_2x2(x, link=None):
     """AvgPool2d(2, 2, ceil_mode=True).  Even H and W (every RT-DETR input padded
     to a multiple of 32) take a reshape-mean over the channels_last layout, whose
     backward is one broadcast kernel (ROCm's NHWC avg_pool2d backward took
@@ -287,7 +290,7 @@ def avg_pool_2x2(x):
     if H % 2 or W % 2 or not x.is_contiguous(memory_format=torch.channels_last):
         return F.avg_pool2d(x, 2, 2, 0, ceil_mode=True)
     if x.is_cuda and x.dtype == torch.bfloat16 and C % 8 == 0 and x.data_ptr() % 16 == 0:
-        return _AvgPool2x2.apply(x)
+        return _AvgPool2x2.apply(x, link)
     y = x.permute(0, 2, 3, 1).reshape(B, H // 2, 2, W // 2, 2, C).mean(dim=(2, 4))
     return y.permute(0, 3, 1, 2)
 
@@ -303,8 +306,8 @@ class _Shortcut(nn.Module):
     def forward(self, x):
         return self.conv(avg_pool_2x2(x) if self.down else x)
 
-    def conv_shift(self, x):
-        return self.conv.conv_shift(avg_pool_2x2(x) if self.down else x)
+    def conv_shift(self, x, link=None):
+        return self.conv.conv_shift(avg_pool_2x2(x, link) if self.down else x)
 
 
 _NO_FORK = os.environ.get("MOE_BACKBONE_FORK", "1") == "0"
@@ -319,7 +322,7 @@ def _fork_ok(short):
     return not _NO_FORK and (short is None or short.conv.fold)
 
 
-def _block_out(last, short, h, x, folded_last=None, mask_input=False, link_in=None):
+def _block_out(last, short, h, x, folded_last=None, mask_input=False, link_in=None, short_link=None):
     """relu(last(h) + shortcut(x)) as a (main, shortcut) pair of handles on the
     same activation (see fused.AddBiasReLUFork).  With frozen BNs the two BN
     shifts join the residual add and the ReLU in one fused kernel -- the
@@ -328,7 +331,7 @@ def _block_out(last, short, h, x, folded_last=None, mask_input=False, link_in=No
     if last.fold and _fork_ok(short) and folded_last is not None:
         wl, sl = folded_last
         if mask_input or last.hip_ok(h, h.shape[1], wl):
-            b, bias = (x, sl) if short is None else short.conv_shift(x)
+            b, bias = (x, sl) if short is None else short.conv_shift(x, short_link)
             if short is not None:
                 bias = sl + bias
             return conv2d_add_bias_relu_fork(h, wl, b, bias, mask_input, link_in if short is None else None)
@@ -350,11 +353,18 @@ def _block_out(last, short, h, x, folded_last=None, mask_input=False, link_in=No
 _GRAD_LINK = os.environ.get("MOE_GRAD_LINK", "1") != "0"  # A/B switch for the GradLink hand-off
 
 
+_DOWN_LINK = os.environ.get("MOE_DOWN_LINK", "1") != "0"  # A/B switch: GradLink through downsampling shortcuts
+
+
 def _link_for(short, x, fused):
     """The previous block's GradLink when this block's shortcut is the
-    identity and both its first convolution and its output are fused (both
-    ends of the hand-off run: branch2a's dgrad epilogue, this block's fork)."""
-    if short is not None or not fused or not _GRAD_LINK:
+    identity -- or (round 4) the ResNet-D downsampling shortcut, whose
+    average-pool backward hands its gradient over -- and both its first
+    convolution and its output are fused (both ends of the hand-off run:
+    branch2a's dgrad epilogue, this block's fork / shortcut)."""
+    if not fused or not _GRAD_LINK:
+        return None
+    if short is not None and not (_DOWN_LINK and short.down and short.conv.fold):
         return None
     return getattr(x, "grad_link", None)
 
@@ -413,7 +423,8 @@ class BottleNeck(nn.Module):
             link = _link_for(self.short, x, ok_a and ok_c)
             h1 = a.bias_relu(x, fa, grad_premasked=pre_ab, link=link)
             h2 = b.bias_relu(h1, fb, mask_input=pre_ab, grad_premasked=pre_bc)
-            return _block_out(c, self.short, h2, xs, fc, mask_input=pre_bc, link_in=link)
+            return _block_out(c, self.short, h2, xs, fc, mask_input=pre_bc, link_in=link,
+                              short_link=link if self.short is not None else None)
         return _block_out(self.branch2c, self.short, self.branch2b(self.branch2a(x)), xs)
 
 

@@ -202,3 +202,32 @@ def test_no_fork_switch_keeps_relu_backward(hip_lib, monkeypatch, depth):
     assert res[0][1].keys() == res[1][1].keys()
     for k in res[0][1]:
         assert _rel(res[1][1][k], res[0][1][k]) < 2e-2, k
+
+
+def test_down_link_matches_relu_grad2(hip_lib, monkeypatch):
+    """GradLink through the ResNet-D downsampling shortcuts (backbone._DOWN_LINK:
+    the average-pool backward hands its gradient to branch2a's dgrad epilogue,
+    which adds it and applies the block input's ReLU mask -- no relu_grad2 pass
+    at the stage boundaries) == the relu_grad2 path, at bf16 noise."""
+    from src.rtdetr_moe import backbone as bb
+
+    torch.manual_seed(1)
+    m = bb.PResNet(50).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for mod in m.modules():
+        if hasattr(mod, "running_var") and not isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_var.uniform_(0.5, 2.0)
+            mod.weight.uniform_(0.5, 1.5)
+    x = torch.randn(2, 3, 128, 160, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    for down in (True, False):
+        monkeypatch.setattr(bb, "_DOWN_LINK", down)
+        m.zero_grad(set_to_none=True)
+        outs = m(x)
+        sum(o.float().square().mean() for o in outs).backward()
+        res.append(([o.detach().clone() for o in outs],
+                    {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert torch.equal(a, b)
+    assert res[0][1].keys() == res[1][1].keys()
+    for k in res[0][1]:
+        assert _rel(res[0][1][k], res[1][1][k]) < 2e-2, k
