@@ -153,19 +153,31 @@ def load_pmc_traffic(workload):
     return out
 
 
+def lib_build_id():
+    """sha256 (first 16 hex digits) of the libmoe_hip.so this process loaded:
+    ties a committed rocprof summary to the build it was taken of."""
+    import hashlib
+
+    from src.moe import _lib as L
+
+    return hashlib.sha256(Path(L.LIB_PATH).read_bytes()).hexdigest()[:16]
+
+
 def load_rocprof_summary(workload):
-    """Per-group average launch time of the newest committed rocprofv3
-    kernel-trace summary of the same workload (profiles/rNN/<wl>/
-    kernel_summary.json, tools/profile_summary.py over `rocprofv3
-    --kernel-trace --stats` of this bench command, graph replay included)."""
+    """(groups, source, meta) of the newest committed rocprofv3 kernel-trace
+    summary of the same workload (profiles/rNN/<wl>/kernel_summary.json,
+    tools/profile_summary.py over `rocprofv3 --kernel-trace --stats` of this
+    bench command, graph replay included); meta holds the build id and the
+    bench configuration of the profiled run (tools/profile_summary.py copies
+    them from that run's own bench line)."""
     cands = sorted((ROOT / "profiles").glob(f"r[0-9][0-9]/{workload}/kernel_summary.json"))
     if not cands:
-        return {}, None
+        return {}, None, {}
     try:
         data = json.loads(cands[-1].read_text())
     except ValueError:
-        return {}, None
-    return data.get("groups", {}), f"{cands[-1].relative_to(ROOT)} ({data.get('source')})"
+        return {}, None, {}
+    return data.get("groups", {}), f"{cands[-1].relative_to(ROOT)} ({data.get('source')})", data.get("bench", {})
 
 
 def merge_groups(*ds):
@@ -221,6 +233,45 @@ def roofline_entry(d, pmc, elapsed, kernel):
     return e
 
 
+def rocprof_headline(e, g, src, match):
+    """Put the graph-replay timing of a kernel group on the headline.
+
+    ``e`` is the live roofline entry (dispatch-stamped HIP events of eager
+    steps right after the timed region: hipGraphs carry no events on ROCm
+    7.2); ``g`` the group in the committed rocprofv3 summary of this bench
+    command, whose average launch duration covers the replayed step graph.
+    When that summary belongs to this build (``match``), achieved / frac /
+    avg_us become the rocprof figures -- algorithmic bytes per launch (this
+    run's library profiler) / rocprof's average duration / peak -- and the
+    live event figures move to ``eager_events``; otherwise the headline stays
+    live and the summary is reported as ``rocprof`` with ``matches_build``
+    false."""
+    if not e or not g or not g.get("avg_us"):
+        return e
+    bpl = e["algorithmic_bytes_per_launch"]
+    sec = g["avg_us"] * 1e-6
+    ach = bpl / sec / 1e9
+    rp = {"avg_us": g["avg_us"], "launches": g.get("launches"), "achieved": round(ach, 2), "unit": "GB/s",
+          "frac": round(ach / PEAK_HBM_GBS, 4), "source": src, "matches_build": bool(match)}
+    if e.get("flop_per_launch"):
+        rp["mfma_tflops"] = round(e["flop_per_launch"] / sec / 1e12, 1)
+    if not match or e["bound"] != "hbm":
+        e["rocprof"] = rp
+        e["timing_source"] = "libmoe_hip dispatch-stamped HIP events (eager steps after the timed region)"
+        return e
+    live = {k: e[k] for k in ("avg_us", "launches", "achieved", "frac")}
+    if "mfma" in e:
+        live["mfma_tflops"] = e["mfma"]["achieved"]
+    live["source"] = "libmoe_hip dispatch-stamped HIP events over the eager steps after the timed region"
+    e.update({"avg_us": g["avg_us"], "launches": g.get("launches"), "achieved": rp["achieved"], "frac": rp["frac"],
+              "eager_events": live,
+              "timing_source": f"rocprofv3 --kernel-trace of this build's bench command (graph replay): {src}"})
+    if "mfma" in e and e.get("flop_per_launch"):
+        e["mfma"]["achieved"] = rp["mfma_tflops"]
+        e["mfma"]["frac"] = round(e["flop_per_launch"] / sec / 1e12 / e["mfma"]["peak"], 4)
+    return e
+
+
 def parse_args():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -257,6 +308,9 @@ def parse_args():
                          "criterion")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="graph mode: eager steps after the timed region that carry the kernel events")
+    ap.add_argument("--eval-steps", type=int, default=10,
+                    help="eval leg after the training measurement: timed inference forwards of the same batch "
+                         "(engine._evaluate's forward: model.eval(), no_grad, bf16 autocast); 0 skips it")
     return ap.parse_args()
 
 
@@ -323,16 +377,19 @@ def expert_parallel_stats(model, spec, world):
     per_layer, over, assign, a2a = [], 0, 0, 0.0
     for m in layers:
         T = m.last_tokens
-        S = cfg.ep_slot_rows(T)
+        S = cfg.ep_slot_rows(T, m.d_model)
         b = cfg.num_experts * S * m.d_model * 2
         ov = int(m.last_ep_overflow) if m.last_ep_overflow is not None else 0
         over += ov
         assign += T * cfg.top_k
         a2a += 4 * b  # forward dispatch + combine, backward both transposes
-        per_layer.append({"T": T, "slots": S, "bytes_per_a2a": b,
+        per_layer.append({"T": T, "slots": S, "lossless": S >= T,
+                          "slot_factor": round(S * cfg.num_experts / (T * cfg.top_k), 3), "bytes_per_a2a": b,
                           "survey_bytes_per_a2a": round(T * cfg.top_k * 512 * (max(world, 8) - 1) / max(world, 8)),
-                          "overflow": ov})
+                          "overflow": ov, "overflow_frac": round(ov / max(T * cfg.top_k, 1), 5)})
     return {"slot_factor": cfg.ep_capacity_factor if cfg.ep_capacity_factor > 0 else "lossless",
+            "lossless_budget_mb": cfg.ep_lossless_mb,
+            "max_layer_overflow_frac": max(p["overflow_frac"] for p in per_layer),
             "ep_overflow": over, "assignments": assign, "overflow_frac": round(over / max(assign, 1), 5),
             "a2a_bytes_per_step_per_rank": round(a2a), "layers": per_layer,
             "note": "survey_bytes_per_a2a: SURVEY 8(e)'s off-rank bytes of a lossless exchange at W=8; "
@@ -415,6 +472,33 @@ def cpu_baseline(spec, batch_img, img_h, img_w, target_s):
                       f"src/moe/eager.py (fp32 torch ops{', MXFP8 expert GEMMs emulated' if 'fp8' in spec else ''})"}
 
 
+def eval_leg(model, images, ctx, steps, warmup=3):
+    """Inference speed of the trained model on the workload's batch: the
+    forward engine._evaluate times for ``speed_inference_ms_per_img`` (reference
+    scripts/eval_detector.py:99-116 derives fps_inference_only from it):
+    model.eval(), no_grad, bf16 autocast, the batch resident in HBM, timed
+    between synchronizes.  Returns the eval block of the bench line."""
+    was_training = model.training
+    model.eval()
+    try:
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            for _ in range(warmup):
+                model(images, ctx)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                model(images, ctx)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+    finally:
+        model.train(was_training)
+    n = steps * images.shape[0]
+    return {"speed_inference_ms_per_img": round(1e3 * dt / n, 4), "fps_inference_only": round(n / dt, 2),
+            "images_per_sec": round(n / dt, 2), "batch": int(images.shape[0]), "steps": steps, "warmup": warmup,
+            "mode": "eager forward, model.eval(), torch.no_grad, bf16 autocast (engine._evaluate's forward), "
+                    "batch resident in HBM, postprocess excluded"}
+
+
 def main():
     args = parse_args()
     world, rank, local = setup_dist(args.gpus)
@@ -431,6 +515,7 @@ def main():
     from src.rtdetr_moe.data import SyntheticZOD
 
     L.lib()  # fail loudly if the HIP extension is missing
+    build_id = lib_build_id()
     for kv in args.tune:
         key, val = kv.split("=", 1)
         L.set_tuning(key, int(val))
@@ -497,6 +582,10 @@ def main():
         L.TIMER.harvest()
         L.TIMER.stop()
         prof_steps = args.profile_steps
+    ev = None
+    if args.eval_steps > 0:
+        log(rank, f"eval leg: {args.eval_steps} inference forwards")
+        ev = eval_leg(model, images, ctx, args.eval_steps)
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
     rccl_world = None
     if world > 1:
@@ -522,20 +611,17 @@ def main():
         roof = roofline_entry(merge_groups(ksum.get("grouped_gemm"), ksum.get("grouped_gemm_fp8")),
                               pmc.get("grouped_gemm"), prof_elapsed,
                               "grouped GEMM (gemm_v2_kernel: expert fwd, dgrad, wgrad)")
-        rp, rp_src = load_rocprof_summary(args.workload)
-        if roof and rp.get("grouped_gemm", {}).get("avg_us"):
-            # the same algorithmic bytes per launch over rocprof's average
-            # launch duration of the graph-replayed step (the committed summary)
-            g = rp["grouped_gemm"]
-            bpl = roof["algorithmic_bytes_per_launch"]
-            ach = bpl / (g["avg_us"] * 1e-6) / 1e9
-            roof["rocprof"] = {"avg_us": g["avg_us"], "launches": g.get("launches"), "achieved": round(ach, 2),
-                               "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "source": rp_src}
-            if roof.get("flop_per_launch"):
-                tf = roof["flop_per_launch"] / (g["avg_us"] * 1e-6) / 1e12
-                roof["rocprof"]["mfma_tflops"] = round(tf, 1)
+        rp, rp_src, rp_meta = load_rocprof_summary(args.workload)
+        # the committed rocprof summary is THIS build's when its profiled bench
+        # line carries the same library hash and configuration (else it is
+        # reported, labelled stale, and the headline stays on the live events)
+        rp_match = (rp_meta.get("libmoe_hip_sha16") == build_id and rp_meta.get("workload") == wl["desc"]
+                    and rp_meta.get("precision") == args.precision and rp_meta.get("graphs") == bool(graphs)
+                    and rp_meta.get("batch") == batch)
+        roof = rocprof_headline(roof, rp.get("grouped_gemm"), rp_src, rp_match)
         rd = roofline_entry(ksum.get("dispatch"), pmc.get("dispatch"), prof_elapsed,
                             "permute_fwd / combine_fwd / combine_bwd")
+        rd = rocprof_headline(rd, rp.get("dispatch"), rp_src, rp_match)
         kprof = {}
         for name, d in ksum.items():
             if d["total_ms"] <= 0:
@@ -558,12 +644,14 @@ def main():
                        "precision": "bf16 weights + fp32 master" if args.precision == "bf16" else "bf16 autocast",
                        "img": f"{args.img_w}x{args.img_h} (padded to {data.pad_w}x{data.pad_h})",
                        "parallelism": f"dp{world}" if "ep" not in spec else f"dp{world}+ep{world}",
-                       "rccl_world": rccl_world},
+                       "rccl_world": rccl_world, "batch": batch},
+            "build": {"libmoe_hip_sha16": build_id, "precision": args.precision, "graphs": bool(graphs)},
             "roofline": roof, "roofline_dispatch": rd, "kernel_profile": kprof,
             "kernel_timing": None if not timing else (
                 f"libmoe_hip dispatch-stamped events over the {args.steps} timed steps" if not graphs else
                 f"libmoe_hip dispatch-stamped events over {args.profile_steps} eager steps right after the "
                 f"timed region (same shapes; the timed steps replay hipGraphs, which carry no timing events)"),
+            **({"eval": ev} if ev else {}),
             **({"phases_gpu_host_ms": phases} if phases else {}),
             **({"expert_parallel": ep_stats} if ep_stats else {}),
         }

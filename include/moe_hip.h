@@ -161,14 +161,9 @@ int moe_token_bwd_res(const void* dxp, const int32_t* pos, const float* probs,
  * not NULL, the context-bias gradient dcb fp32 [C,E]: row c = the sum of
  * dlogits over the tokens of the images with ctx_img[b] == c.  One launch,
  * fixed-order sums (bitwise repeatable; replaces a torch fp32 GEMM and an
- * atomic index_add).  part: a 16-B aligned fp32 workspace of
- * moe_router_wgrad_workspace(B, tpi, E, d) bytes (no initialisation needed):
- * the chunked kernel (token chunks x column slices, per-chunk partials summed
- * in chunk order by the last workgroup of each slice; its arrival counters are
- * the tail of moe_set_splitk_workspace's counter array); when that returns 0
- * (the default: tuning router_wgrad_chunked=0 -- measured no faster at C2 --,
- * no counters registered, or d % 64 != 0) or part is NULL the per-column
- * one-pass kernel runs and part is unused.
+ * atomic index_add).  part: reserved, pass NULL (moe_router_wgrad_workspace
+ * returns 0; a chunked variant that used it was measured no faster at C2 and
+ * removed in round 5).
  * Reference: the router backward of SURVEY 8(a) row a7. */
 long long moe_router_wgrad_workspace(int B, int tpi, int E, int d);
 int moe_router_wgrad(const float* dlogits, const void* x, const int32_t* ctx_img, int B, int tpi, int E, int d,
@@ -798,12 +793,22 @@ enum moe_prof_kind {
   MOE_PROF_GEMM_FP8 = 10, /* grouped GEMM on the fp8 (MXFP8) MFMA: priced at the fp8 peak */
   MOE_PROF_LINEAR = 11,   /* dense linear weight + bias gradients (rtdetr_linear_wgrad) */
   MOE_PROF_ATTN = 12,     /* multi-head self-attention (rtdetr_attn_fwd / rtdetr_attn_bwd) */
-  MOE_PROF_CONV = 13      /* implicit-GEMM convolutions (rtdetr_conv_*) */
+  MOE_PROF_CONV = 13,     /* implicit-GEMM convolutions (rtdetr_conv_*) */
+  MOE_PROF_ROUTER_WGRAD = 14 /* router weight / context-bias gradients (moe_router_wgrad) */
 };
 int moe_profile_enable(int on);
 int moe_profile_count(void);
 int moe_profile_get(int i, int* kind, float* ms, double* flops, double* bytes);
 int moe_profile_clear(void);
+
+/* Host-side launch counts per moe_prof_kind (MOE_PROF_*): every kernel launch
+ * the library issues increments its kind's count, profiling on or off and
+ * inside hipGraph capture (a captured launch counts once, when captured).
+ * out[i] = count of kind i for i < n (0 past the last kind).  How a caller
+ * proves the HIP path ran (tests/test_gpu_dropin.py).  reset() zeroes them.
+ * Not thread-safe. */
+int moe_launch_counts(long long* out, int n);
+int moe_launch_counts_reset(void);
 
 /* Thread-local message for the last non-zero return code. */
 const char* moe_last_error(void);

@@ -71,12 +71,18 @@ struct Profiler {
   }
 };
 Profiler g_prof;
+// host-side launch counts per profiler kind: every launch through a ProfScope,
+// profiling on or off and inside hipGraph capture (a captured launch counts
+// once, at capture) -- how a caller checks that the HIP path ran
+constexpr int kKinds = 32;
+long long g_launches[kKinds] = {};
 }  // namespace
 
 ProfScope::ProfScope(hipStream_t s, int kind, double bytes_fixed, bool per_row, double bytes_per_row,
                      double flops_per_row)
     : active_(g_prof.on), idx_(-1) {
   (void)s;
+  if (kind >= 0 && kind < kKinds) ++g_launches[kind];
   if (!active_) return;
   Record r{kind, g_prof.ev(), g_prof.ev(), bytes_fixed, bytes_per_row, flops_per_row, -1, per_row};
   if (per_row && g_prof.rows_dev != nullptr && g_prof.rows_used < kRowSlots) r.rows_slot = g_prof.rows_used++;
@@ -141,5 +147,16 @@ extern "C" int moe_profile_get(int i, int* kind, float* ms, double* flops, doubl
 
 extern "C" int moe_profile_clear(void) {
   moe::g_prof.clear();
+  return 0;
+}
+
+extern "C" int moe_launch_counts(long long* out, int n) {
+  if (out == nullptr || n < 0) return moe::fail("moe_launch_counts: NULL out or n < 0");
+  for (int i = 0; i < n; ++i) out[i] = i < moe::kKinds ? moe::g_launches[i] : 0;
+  return 0;
+}
+
+extern "C" int moe_launch_counts_reset(void) {
+  for (auto& c : moe::g_launches) c = 0;
   return 0;
 }

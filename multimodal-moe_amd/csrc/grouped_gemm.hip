@@ -1686,20 +1686,12 @@ extern "C" int moe_set_splitk_workspace(void* ws, size_t ws_bytes, int32_t* coun
   g_split_ws[dev].ws_bytes = ws ? ws_bytes : 0;
   g_split_ws[dev].cnt = counters;
   g_split_ws[dev].n_cnt = counters ? n_counters : 0;
-  // the last kRouterWgradCounters counters belong to the chunked router weight gradient
-  if (counters != nullptr && n_counters >= 4 * kRouterWgradCounters) {
-    g_split_ws[dev].n_cnt = n_counters - kRouterWgradCounters;
-    router_wgrad_set_counters(dev, counters + g_split_ws[dev].n_cnt);
-  } else {
-    router_wgrad_set_counters(dev, nullptr);
-  }
   return 0;
 }
 
 extern "C" int moe_set_tuning(const char* key, int value) {
   const std::string k = key ? key : "";
   if (k == "gemm_variant" && value >= 0 && value <= 2) { g_gemm_variant = value; return 0; }
-  if (k == "router_wgrad_chunked" && (value == 0 || value == 1)) { g_router_wgrad_chunked = value; return 0; }
   if (k == "gemm_stages" && (value == 0 || (value >= 2 && value <= 4))) { g_gemm_stages = value; return 0; }
   if (k == "gemm_debug" && value >= 0 && value <= 3) { g_gemm_debug = value; return 0; }
   if (k == "rows_bm" && (value == 0 || value == 64 || value == 128)) { g_rows_bm = value; return 0; }

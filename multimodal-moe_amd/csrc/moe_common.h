@@ -181,9 +181,4 @@ namespace moe {
 void set_error(const std::string& msg);
 int fail(const std::string& msg);          // returns -1
 int check_launch(const char* what);        // returns 0 or -(1000 + err)
-// arrival counters of the chunked router weight gradient (router.hip): the tail
-// of the split-K counter array registered by moe_set_splitk_workspace
-constexpr int kRouterWgradCounters = 64;
-void router_wgrad_set_counters(int dev, int32_t* cnt);
-extern int g_router_wgrad_chunked;  // moe_set_tuning("router_wgrad_chunked"): 1 = chunked kernel / 0 (default) = per-column kernel
 }  // namespace moe

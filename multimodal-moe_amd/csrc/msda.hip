@@ -1092,7 +1092,6 @@ extern "C" int rtdetr_msda_fused_bwd_det(const void* value, long long ldv, const
   if (work_bytes < rtdetr_msda_vgrad_workspace(B, Q, H, L, P)) return fail("msda_fused_bwd_det: workspace too small");
   if (reinterpret_cast<uintptr_t>(work) % 16 || reinterpret_cast<uintptr_t>(grad_value) % 16)
     return fail("msda_fused_bwd_det: work and grad_value must be 16-B aligned");
-  if (Q == 0) return 0;  // (no samples: the caller's slice stays as it was)
   VgLevels lv{};
   int tiles_bh = 0, ntmax = 0, start = 0;
   for (int l = 0; l < L; ++l) {
@@ -1109,7 +1108,14 @@ extern "C" int rtdetr_msda_fused_bwd_det(const void* value, long long ldv, const
     tiles_bh += lv.nt[l];
     ntmax = std::max(ntmax, lv.nt[l]);
   }
-  if (start > S) return fail("msda_fused_bwd_det: level sizes exceed S");
+  // every row of the slice must belong to a level: the tile kernel writes
+  // exactly the level rows, and the caller's buffer is not zeroed
+  if (start != S) return fail("msda_fused_bwd_det: the level sizes must sum to S");
+  if (Q == 0) {  // no samples: the value gradient is zero (written, not left as it was)
+    if (hipMemset2DAsync(grad_value, (size_t)ldv * 2, 0, (size_t)H * D * 2, (size_t)B * S, stream) != hipSuccess)
+      return fail("msda_fused_bwd_det: zero fill failed");
+    return 0;
+  }
   const long long n = (long long)Q * P * 4, n_all = n * B * H * L;
   int2* rec = static_cast<int2*>(work);
   int4* sorted = reinterpret_cast<int4*>(static_cast<char*>(work) + n_all * 8);

@@ -869,221 +869,6 @@ __global__ __launch_bounds__(RwCfg<EM>::NT) void router_wgrad_kernel(const float
   }
 }
 
-// ---------------------------------------------------------------------------
-// Chunked router weight gradient (round 4): the same sums as router_wgrad_kernel
-// with every load coalesced and the whole chip busy.  Workgroup (c, s) takes
-// token chunk c (chunks never straddle an image: chunk c lies in image
-// c / CPI) and the SW-column slice s of x: 16 threads cover one token's slice
-// (CWT columns each, one 16-64 B run per token row), 16 token rows per pass,
-// U passes' loads in flight.  Each thread keeps EM x CWT sums; the workgroup
-// adds its 16 row groups in LDS in a fixed order and stores its [EM][SW]
-// partial (and, in slice 0, the chunk's dlogits column sums for dcb) with
-// agent-coherent stores.  The last workgroup of slice s to arrive (per-slice
-// arrival counter, reset by it for the next launch) sums the NC partials in
-// chunk order: dWg and dcb are bitwise repeatable and independent of arrival
-// order.  The per-token loads of router_wgrad_kernel (one 8 B piece of a
-// different row per lane, 64 rows per wave instruction) were address-bound in
-// the texture units with only d / CW workgroups.
-// ---------------------------------------------------------------------------
-template <int EM>
-struct Rw2Cfg {
-  static constexpr int SW = EM <= 16 ? 64 : (EM == 32 ? 32 : 16);  // dWg columns per slice
-  static constexpr int CWT = SW / 16;                               // columns per thread
-  static constexpr int RPP = 16;                                    // token rows per pass
-  static constexpr int NA = EM * CWT;                               // sums per thread
-  static constexpr int NO = EM * SW;                                // partial outputs per workgroup
-  static constexpr int U = EM == 8 ? 8 : (EM == 64 ? 2 : 4);        // passes in flight
-  static constexpr int NB = EM <= 16 ? 1 : EM / 16;                 // dlogits columns per lane (dcb)
-  static constexpr size_t lds() { return (size_t)(NA + NB) * 256 * 4; }
-};
-
-__device__ __forceinline__ void rw_st(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float rw_ld(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int EM, bool VEC>
-__global__ __launch_bounds__(256) void router_wgrad_chunk_kernel(
-    const float* __restrict__ dlogits, const uint16_t* __restrict__ x, const int32_t* __restrict__ ctx_img,
-    int tpi, int E, int d, int C, int CPI, int CH, int NC, float* __restrict__ part, int32_t* __restrict__ cnt,
-    float* __restrict__ dwg, float* __restrict__ dcb) {
-  using K = Rw2Cfg<EM>;
-  constexpr int SW = K::SW, CWT = K::CWT, RPP = K::RPP, NA = K::NA, NO = K::NO, U = K::U, NB = K::NB;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem);  // [NA][256]
-  float* redb = red + NA * 256;                 // [NB][256]: dlogits column sums (slice 0, dcb)
-  __shared__ int s_old;
-  const int c = blockIdx.x, s = blockIdx.y, NS = gridDim.y;
-  const int tid = threadIdx.x, r = tid >> 4, q = tid & 15;
-  const int img = c / CPI, kc = c - img * CPI;
-  const int t_lo = img * tpi + min(tpi, kc * CH), t_hi = img * tpi + min(tpi, (kc + 1) * CH);
-  const int col = s * SW + q * CWT;
-  const bool do_b = dcb != nullptr && s == 0;
-  float acc[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) acc[i] = 0.f;
-  float accb[NB];
-#pragma unroll
-  for (int j = 0; j < NB; ++j) accb[j] = 0.f;
-  for (int t0 = t_lo + r; t0 < t_hi; t0 += RPP * U) {
-    float dl[U][EM];
-    float xv[U][CWT];
-    // every load of the round first (clamped, always valid addresses), then the sums
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int tc = min(t0 + RPP * u, t_hi - 1);
-      const float* row = dlogits + (size_t)tc * E;
-      if constexpr (VEC) {
-#pragma unroll
-        for (int qq = 0; qq < EM / 4; ++qq) {
-          const float4 v = reinterpret_cast<const float4*>(row)[min(qq, (E >> 2) - 1)];
-          dl[u][4 * qq] = v.x; dl[u][4 * qq + 1] = v.y; dl[u][4 * qq + 2] = v.z; dl[u][4 * qq + 3] = v.w;
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < EM; ++e) dl[u][e] = row[min(e, E - 1)];
-      }
-      const uint16_t* xr = x + (size_t)tc * d + col;
-      if constexpr (CWT == 4) {
-        const uint2 v = *reinterpret_cast<const uint2*>(xr);
-        xv[u][0] = __uint_as_float(v.x << 16); xv[u][1] = __uint_as_float(v.x & 0xffff0000u);
-        xv[u][2] = __uint_as_float(v.y << 16); xv[u][3] = __uint_as_float(v.y & 0xffff0000u);
-      } else if constexpr (CWT == 2) {
-        const uint32_t v = *reinterpret_cast<const uint32_t*>(xr);
-        xv[u][0] = __uint_as_float(v << 16); xv[u][1] = __uint_as_float(v & 0xffff0000u);
-      } else {
-        xv[u][0] = bf2f(*xr);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool ok = t0 + RPP * u < t_hi;
-#pragma unroll
-      for (int e = 0; e < EM; ++e) {
-        const float g = (ok && e < E) ? dl[u][e] : 0.f;
-#pragma unroll
-        for (int w = 0; w < CWT; ++w) acc[e * CWT + w] += g * xv[u][w];
-      }
-      if (do_b) {  // lane q of each row group sums dlogits columns q, q + 16, ...
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          float sel = 0.f;
-#pragma unroll
-          for (int e = 16 * j; e < (16 * j + 16 < EM ? 16 * j + 16 : EM); ++e) sel = (e == 16 * j + q) ? dl[u][e] : sel;
-          accb[j] += (ok && 16 * j + q < E) ? sel : 0.f;
-        }
-      }
-    }
-  }
-  // the 16 row groups' sums added in row order
-#pragma unroll
-  for (int i = 0; i < NA; ++i) red[i * 256 + tid] = acc[i];
-#pragma unroll
-  for (int j = 0; j < NB; ++j) redb[j * 256 + tid] = accb[j];
-  __syncthreads();
-  const int NO_ = NO;
-  float* mine = part + ((size_t)s * NC + c) * NO_;
-  for (int o = tid; o < NO; o += 256) {  // o = i * 16 + lane: sum i of lane q' over the row groups
-    const int i = o >> 4, ql = o & 15;
-    float v = 0.f;
-#pragma unroll
-    for (int rr = 0; rr < RPP; ++rr) v += red[i * 256 + rr * 16 + ql];
-    rw_st(mine + o, v);
-  }
-  float* dsum = part + (size_t)NS * NC * NO;  // [NC][EM]
-  if (do_b && tid < EM) {  // column tid = 16 j + lane
-    const int j = tid >> 4, ql = tid & 15;
-    float v = 0.f;
-#pragma unroll
-    for (int rr = 0; rr < RPP; ++rr) v += redb[j * 256 + rr * 16 + ql];
-    rw_st(dsum + (size_t)c * EM + tid, v);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial stores have completed
-  __syncthreads();
-  if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(cnt + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    MOE_DASSERT(old >= 0 && old < NC);  // reset by the previous launch's last workgroup
-    if (old == NC - 1) __hip_atomic_store(cnt + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_old = old;
-  }
-  __syncthreads();
-  if (s_old != NC - 1) return;
-  // last of slice s: the NC partials in chunk order; each thread's MO outputs
-  // x 64 / MO chunks of loads in flight per round trip
-  constexpr int MO = NO / 256, CB = 64 / MO;
-  {
-    const float* src = part + (size_t)s * NC * NO + tid;
-    float sum[MO];
-#pragma unroll
-    for (int m = 0; m < MO; ++m) sum[m] = 0.f;
-    for (int c0 = 0; c0 < NC; c0 += CB) {
-      float v[MO][CB];
-#pragma unroll
-      for (int j = 0; j < CB; ++j)
-#pragma unroll
-        for (int m = 0; m < MO; ++m) v[m][j] = rw_ld(src + (size_t)min(c0 + j, NC - 1) * NO + 256 * m);
-#pragma unroll
-      for (int j = 0; j < CB; ++j)
-#pragma unroll
-        for (int m = 0; m < MO; ++m) sum[m] += (c0 + j < NC) ? v[m][j] : 0.f;
-    }
-#pragma unroll
-    for (int m = 0; m < MO; ++m) {
-      const int o = tid + 256 * m, i = o >> 4, ql = o & 15;
-      const int e = i / CWT, w = i - e * CWT;
-      if (e < E) dwg[(size_t)e * d + s * SW + ql * CWT + w] = sum[m];
-    }
-  }
-  if (do_b) {
-    int* s_ctx = reinterpret_cast<int*>(red);  // (the row-group sums are dead)
-    for (int cc = tid; cc < NC; cc += 256) s_ctx[cc] = ctx_img[cc / CPI];
-    __syncthreads();
-    for (int o = tid; o < C * E; o += 256) {
-      const int ctx = o / E, e = o - ctx * E;
-      float sum = 0.f;
-      for (int c0 = 0; c0 < NC; c0 += 32) {
-        float v[32];
-#pragma unroll
-        for (int j = 0; j < 32; ++j) v[j] = rw_ld(dsum + (size_t)min(c0 + j, NC - 1) * EM + e);
-#pragma unroll
-        for (int j = 0; j < 32; ++j) sum += (c0 + j < NC && s_ctx[min(c0 + j, NC - 1)] == ctx) ? v[j] : 0.f;
-      }
-      dcb[o] = sum;
-    }
-  }
-}
-
-static int32_t* g_rw_cnt[64];
-int g_router_wgrad_chunked = 0;  // A/B: not faster than the per-column kernel at C2
-
-void router_wgrad_set_counters(int dev, int32_t* cnt) {
-  if (dev >= 0 && dev < 64) g_rw_cnt[dev] = cnt;
-}
-
-// chunk geometry of router_wgrad_chunk_kernel: NC = B CPI chunks of CH tokens,
-// NC ~ sqrt(T 63 256 / (NO 16 U)) balances the chunk loop's load rounds against
-// the final sum's (NO / 256 outputs x NC loads per thread)
-struct RwGeom {
-  int em, sw, no, cpi, ch, nc, ns;
-};
-static RwGeom rw_geom(int B, int tpi, int E, int d) {
-  RwGeom g{};
-  g.em = E <= 8 ? 8 : E <= 16 ? 16 : E <= 32 ? 32 : 64;
-  g.sw = g.em <= 16 ? 64 : (g.em == 32 ? 32 : 16);
-  const int u = g.em == 8 ? 8 : (g.em == 64 ? 2 : 4);
-  g.no = g.em * g.sw;
-  const double T = (double)B * tpi;
-  int nc = (int)(std::sqrt(T * 63.0 * 256.0 / ((double)g.no * 16.0 * u)) + 0.5);
-  nc = std::max(1, std::min(nc, 256));
-  g.cpi = std::max(1, (nc + B - 1) / std::max(B, 1));
-  g.ch = (tpi + g.cpi - 1) / g.cpi;
-  g.nc = B * g.cpi;
-  g.ns = d / g.sw;
-  return g;
-}
-
 }  // namespace moe
 
 // ---------------------------------------------------------------------------
@@ -1256,14 +1041,11 @@ extern "C" int moe_aux_loss_fwd(const float* aux_partials, int nblk, int E, cons
   return check_launch("moe_aux_loss_fwd");
 }
 
-// workspace of the chunked kernel (0: the per-column kernel runs, part unused)
+// Reserved workspace query (the chunked variant that used it was measured no
+// faster and removed in round 5): always 0, so callers pass part = NULL.
 extern "C" long long moe_router_wgrad_workspace(int B, int tpi, int E, int d) {
-  if (B <= 0 || tpi <= 0 || E < 1 || E > 64 || d % 64 || d > 1024 || g_router_wgrad_chunked == 0) return 0;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || g_rw_cnt[dev] == nullptr) return 0;
-  const RwGeom g = rw_geom(B, tpi, E, d);
-  if (g.nc > 256 * 64 || (long long)B * g.cpi > 65535) return 0;
-  return 4ll * ((long long)g.ns * g.nc * g.no + (long long)g.nc * g.em);
+  (void)B, (void)tpi, (void)E, (void)d;
+  return 0;
 }
 
 extern "C" int moe_router_wgrad(const float* dlogits, const void* x, const int32_t* ctx_img, int B, int tpi, int E,
@@ -1285,41 +1067,7 @@ extern "C" int moe_router_wgrad(const float* dlogits, const void* x, const int32
   // bytes: dlogits and x once, dWg and dcb written (+ one context id per token)
   ProfScope prof(stream, PROF_ROUTER_WGRAD,
                  4.0 * T * E + 2.0 * T * d + 4.0 * E * d + (dcb != nullptr ? 4.0 * C * E + 4.0 * B : 0.0));
-  if (part != nullptr && moe_router_wgrad_workspace(B, tpi, E, d) > 0) {
-    if (reinterpret_cast<uintptr_t>(part) % 16) return fail("router_wgrad: part must be 16-B aligned");
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const RwGeom g = rw_geom(B, tpi, E, d);
-#define LAUNCH_RC(EM_)                                                                                        \
-  do {                                                                                                        \
-    using K = Rw2Cfg<EM_>;                                                                                    \
-    static bool lds_set = false; /* 64 KiB + 1 KiB of dynamic LDS */                                          \
-    if (!lds_set) {                                                                                           \
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(router_wgrad_chunk_kernel<EM_, true>),            \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::lds()) != hipSuccess ||     \
-          hipFuncSetAttribute(reinterpret_cast<const void*>(router_wgrad_chunk_kernel<EM_, false>),           \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::lds()) != hipSuccess)       \
-        return fail("router_wgrad: LDS attribute refused");                                                   \
-      lds_set = true;                                                                                         \
-    }                                                                                                         \
-    if (E % 4 == 0)                                                                                           \
-      MOE_LAUNCH(prof, (router_wgrad_chunk_kernel<EM_, true>), dim3(g.nc, g.ns), dim3(256), K::lds(), stream,  \
-                 dlogits, static_cast<const uint16_t*>(x), ctx_img, tpi, E, d, C, g.cpi, g.ch, g.nc, part,      \
-                 g_rw_cnt[dev], dwg, dcb);                                                                    \
-    else                                                                                                      \
-      MOE_LAUNCH(prof, (router_wgrad_chunk_kernel<EM_, false>), dim3(g.nc, g.ns), dim3(256), K::lds(), stream, \
-                 dlogits, static_cast<const uint16_t*>(x), ctx_img, tpi, E, d, C, g.cpi, g.ch, g.nc, part,      \
-                 g_rw_cnt[dev], dwg, dcb);                                                                    \
-  } while (0)
-    switch (g.em) {
-      case 8: LAUNCH_RC(8); break;
-      case 16: LAUNCH_RC(16); break;
-      case 32: LAUNCH_RC(32); break;
-      default: LAUNCH_RC(64); break;
-    }
-#undef LAUNCH_RC
-    return check_launch("moe_router_wgrad");
-  }
+  (void)part;  // reserved (moe_router_wgrad_workspace is 0)
 #define LAUNCH_RW(EM_)                                                                                        \
   do {                                                                                                        \
     using K = RwCfg<EM_>;                                                                                     \

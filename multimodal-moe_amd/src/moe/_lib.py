@@ -128,6 +128,8 @@ SIGNATURES = {
     "moe_profile_count": (_I, []),
     "moe_profile_get": (_I, [_I, _P, _P, _P, _P]),
     "moe_profile_clear": (_I, []),
+    "moe_launch_counts": (_I, [_P, _I]),
+    "moe_launch_counts_reset": (_I, []),
     "moe_last_error": (ctypes.c_char_p, []),
     "moe_version": (ctypes.c_char_p, []),
 }
@@ -248,6 +250,17 @@ def profile_records(clear=True):
     if clear:
         lib().moe_profile_clear()
     return out
+
+
+def launch_counts(reset=False) -> dict:
+    """{kind name: launches} the library has issued since the last reset
+    (host-side counts, graph capture included: moe_launch_counts)."""
+    n = max(PROF_KINDS) + 1
+    buf = (ctypes.c_longlong * n)()
+    _check(lib().moe_launch_counts(ctypes.cast(buf, ctypes.c_void_p), n), "moe_launch_counts")
+    if reset:
+        lib().moe_launch_counts_reset()
+    return {PROF_KINDS[i]: int(buf[i]) for i in range(n) if buf[i]}
 
 
 def _ptr(t: torch.Tensor | None) -> int | None:
@@ -656,11 +669,8 @@ def router_wgrad(dlogits, x, ctx_img, tokens_per_image, n_ctx):
     if has_ctx:
         _need(ctx_img, torch.int32, "ctx_img")
         dcb = torch.empty((n_ctx, E), dtype=torch.float32, device=x.device)
-    ensure_splitk_workspace(x.device)  # (registers the chunked kernel's arrival counters)
-    nbytes = lib().moe_router_wgrad_workspace(B, tpi, E, d) if T > 0 else 0
-    part = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=x.device) if nbytes > 0 else None
     _check(lib().moe_router_wgrad(_ptr(dlogits), _ptr(x), _ptr(ctx_img) if dcb is not None else None, B, tpi, E, d,
-                                  int(n_ctx) if dcb is not None else 0, _ptr(part), _ptr(dwg), _ptr(dcb), _stream()),
+                                  int(n_ctx) if dcb is not None else 0, None, _ptr(dwg), _ptr(dcb), _stream()),
            "moe_router_wgrad")
     return dwg, dcb
 

@@ -6,8 +6,9 @@ local architecture spec (no network fetch), e.g.::
 
     rtdetr-r50-moe8-top2          C2/C3: R50, 8 experts, top-2, bf16
     rtdetr-r18-moe4-top1          C1: R18, 4 experts, top-1 (CPU plumbing)
-    rtdetr-r50-moe16-top2-ep8     C4: 16 experts sharded over 8 ranks (lossless exchange)
-    rtdetr-r50-moe16-top2-ep8-epcf2    same, all-to-all slots at 2x the mean load (overflow dropped + counted)
+    rtdetr-r50-moe16-top2-ep8     C4: 16 experts sharded over 8 ranks (slots sized per layer, below)
+    rtdetr-r50-moe16-top2-ep8-epcf0    same, every layer lossless (T slots per source and expert)
+    rtdetr-r50-moe16-top2-ep8-epmb0    same, every layer at ep_capacity_factor (no lossless budget)
     rtdetr-r50-moe32-top4-cf1.25-fp8   C5: capacity factor 1.25, fp8 experts
     rtdetr-r50                    dense FFN (no MoE)
 """
@@ -32,14 +33,22 @@ class MoEConfig:
     use_context: bool = True
     ep_size: int = 1              # expert-parallel group size (C4)
     expert_parallel: bool = False  # route through ep.py (set by an -ep<n> spec token, n >= 1)
-    # rows each rank may send to one expert in the fixed-capacity all-to-all, as
-    # a factor of the mean T k / E (layers with capacity_factor > 0 use their
-    # own capacity instead).  2.0 (default): each all-to-all carries 2x the
-    # mean rows (SURVEY 8(e)'s budget); assignments beyond it are dropped like
-    # capacity drops and counted (MoEFFN.last_ep_overflow, bench ep_overflow).
-    # 0 (spec token -epcf0) = lossless: T slots, the worst case, so the EP
-    # layer equals the single-process layer (8x the bytes at C4)
+    # rows each rank may send to one expert in the fixed-capacity all-to-all
+    # (layers with capacity_factor > 0 use their own capacity instead), sized
+    # PER LAYER from its token count T:
+    #  * lossless (S = T, the worst case: the EP layer equals the single-process
+    #    layer) when that exchange buffer, E T d 2 bytes, fits ep_lossless_mb
+    #    (default 32 MB: every C4 decoder layer, 16 x 2,400 x 512 B = 19.7 MB,
+    #    where single-context batches skew the experts most -- round 4 measured
+    #    22.7 % drops there at 2x the mean);
+    #  * else ceil(ep_capacity_factor T k / E) (default 2.0, SURVEY 8(e)'s
+    #    budget: the C4 encoder, 60 MB lossless -> 15 MB); assignments beyond it
+    #    are dropped like capacity drops and counted (MoEFFN.last_ep_overflow,
+    #    bench ep_overflow).
+    # Spec tokens: -epcf<f> sets the factor (-epcf0: every layer lossless),
+    # -epmb<MB> the lossless budget (-epmb0: every layer at the factor).
     ep_capacity_factor: float = 2.0
+    ep_lossless_mb: float = 32.0
     router_init_std: float = 0.02
     ctx_init_scale: float = 0.5
 
@@ -48,15 +57,18 @@ class MoEConfig:
             return 0
         return int(math.ceil(self.capacity_factor * tokens * self.top_k / self.num_experts))
 
-    def ep_slot_rows(self, tokens: int) -> int:
+    def ep_slot_rows(self, tokens: int, d_model: int = 256) -> int:
         """Rows per (source rank, expert) of the expert-parallel exchange: the
-        layer capacity when it has one, else ceil(ep_capacity_factor T k / E),
-        never more than T (a token sends at most one row to an expert)."""
+        layer capacity when it has one; T (lossless) when the factor is 0, or
+        when the lossless buffer E T d 2 bytes fits ep_lossless_mb; else
+        ceil(ep_capacity_factor T k / E) -- never more than T (a token sends at
+        most one row to an expert)."""
         cap = self.capacity(tokens)
         if cap > 0:
             return cap
         f = self.ep_capacity_factor
-        if f <= 0 or f * self.top_k >= self.num_experts:
+        lossless_bytes = self.num_experts * tokens * d_model * 2
+        if f <= 0 or f * self.top_k >= self.num_experts or lossless_bytes <= self.ep_lossless_mb * 1e6:
             return max(1, tokens)
         return max(1, min(tokens, int(math.ceil(f * tokens * self.top_k / self.num_experts))))
 
@@ -103,6 +115,9 @@ def parse_moe_spec(spec: str) -> ModelSpec:
         elif tok.startswith("epcf"):
             moe = moe or MoEConfig()
             moe.ep_capacity_factor = float(tok[4:])
+        elif tok.startswith("epmb"):
+            moe = moe or MoEConfig()
+            moe.ep_lossless_mb = float(tok[4:])
         elif tok.startswith("ep"):
             moe = moe or MoEConfig()
             moe.ep_size = int(tok[2:])

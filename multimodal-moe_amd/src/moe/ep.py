@@ -183,24 +183,25 @@ class _EPExpertFFNScatter(torch.autograd.Function):
     token backward read kept positions only)."""
 
     @staticmethod
-    def forward(ctx, xr, gather, w1, b1, w2, b2, offsets, grad_scale, fused=True):
+    def forward(ctx, xr, gather, w1, b1, w2, b2, offsets, grad_scale, fused=True, rows=None):
         from . import _lib as L
         from .ops import _bias
 
         G, F, d = w1.shape
-        R = xr.shape[0]
+        Rn = xr.shape[0]  # received layout rows (W El S)
+        R = Rn if rows is None else min(int(rows), Rn)  # compact row bound
         xb = xr.to(torch.bfloat16).contiguous()
         w1b = w1.to(torch.bfloat16).contiguous()
         w2b = w2.to(torch.bfloat16).contiguous()
         if fused:
             h, yr = L.expert_ffn_fwd(xb, gather, w1b, _bias(b1), w2b, _bias(b2), offsets, G, R, yp_rows=gather,
-                                     yp_n=R)
+                                     yp_n=Rn)
         else:  # few rows per expert: two launches (the fused FFN streams every expert's weights per row tile)
             h = L.grouped_gemm_gather(xb, gather, w1b, offsets, G, R, F, d, 1, L.EPI_BIAS_RELU, bias=_bias(b1))
             yr = L.grouped_gemm_scatter(h, w2b, offsets, G, R, d, F, 1, L.EPI_BIAS, gather,
-                                        torch.empty((R, d), dtype=torch.bfloat16, device=xb.device), bias=_bias(b2))
+                                        torch.empty((Rn, d), dtype=torch.bfloat16, device=xb.device), bias=_bias(b2))
         ctx.save_for_backward(xb, gather, h, w1b, w2b, offsets)
-        ctx.meta = (G, R, float(grad_scale), xr.dtype)
+        ctx.meta = (G, R, Rn, float(grad_scale), xr.dtype)
         ctx.wdtype = w1.dtype if (w1.dtype == b1.dtype == w2.dtype == b2.dtype) else torch.float32
         return yr
 
@@ -209,18 +210,18 @@ class _EPExpertFFNScatter(torch.autograd.Function):
         from . import _lib as L
 
         xb, gather, h, w1b, w2b, offsets = ctx.saved_tensors
-        G, R, s, xdtype = ctx.meta
+        G, R, Rn, s, xdtype = ctx.meta
         F, d = w1b.shape[1], w1b.shape[2]
         odt = torch.bfloat16 if ctx.wdtype == torch.bfloat16 else torch.float32
         dyb = dyr.to(torch.bfloat16).contiguous()
         dh, dW2, db2 = L.grouped_gemm_bwd_pair(dyb, w2b, offsets, G, R, F, d, L.EPI_RELU_MASK, h, dyb, h,
                                                out_dtype=odt, a_gather=gather, wx_gather=gather)
         dxr, dW1, db1 = L.grouped_gemm_bwd_pair(dh, w1b, offsets, G, R, d, F, L.EPI_NONE, None, dh, xb, gather,
-                                                out_dtype=odt, c_rows=gather, c_n=R)
+                                                out_dtype=odt, c_rows=gather, c_n=Rn)
         if s != 1.0:
             for t in (dW1, db1, dW2, db2):
                 t.mul_(s)
-        return dxr.to(xdtype), None, dW1, db1, dW2, db2, None, None, None
+        return dxr.to(xdtype), None, dW1, db1, dW2, db2, None, None, None, None
 
 
 def _fused_ep_ok(layer, x, fp8):
@@ -229,10 +230,13 @@ def _fused_ep_ok(layer, x, fp8):
     if not x.is_cuda or fp8:
         return False
     from . import _lib as L
-    from .ops import _FUSED_FFN
+    from .ops import _FUSED_FFN, _bias
 
     G, F, d = layer.w1.shape
-    return _FUSED_FFN and L.expert_ffn_supported(G, F, d)
+    # the fused FFN reads both biases in one dtype (ops._ffn_forward's rule);
+    # mixed fp32 / bf16 biases take the grouped-GEMM gather / scatter branch
+    same = _bias(layer.b1).dtype == _bias(layer.b2).dtype
+    return _FUSED_FFN and same and L.expert_ffn_supported(G, F, d)
 
 
 class _CarrierExchange(torch.autograd.Function):
@@ -303,7 +307,7 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=Fals
     El = E // W
     group = layer.ep_group
     T, d = x.shape
-    S = cfg.ep_slot_rows(T)
+    S = cfg.ep_slot_rows(T, d)
     if cap > 0 and S != cap:
         raise ValueError(f"EP slot rows {S} must equal the layer capacity {cap}")
     fp8 = cfg.expert_dtype == "fp8"
@@ -347,7 +351,10 @@ def moe_ffn_ep(layer, x, ctx_bias, ctx_img, tokens_per_image, cap, residual=Fals
         # single-GPU path's threshold, ops._FUSED_MIN_ROWS), else two launches
         from .ops import _FUSED_MIN_ROWS
         fused = T * k * W >= _FUSED_MIN_ROWS * E
-        yr = _EPExpertFFNScatter.apply(xr, gather, layer.w1, layer.b1, layer.w2, layer.b2, offs, gs, fused)
+        # compact rows: every source sends at most T k rows (equal T on every
+        # rank: static shapes), so the GEMM grids and H need min(W El S, W T k)
+        rows = min(W * El * S, W * T * k)
+        yr = _EPExpertFFNScatter.apply(xr, gather, layer.w1, layer.b1, layer.w2, layer.b2, offs, gs, fused, rows)
         yp = yr if ident else _Exchange.apply(yr, group, W)
         if residual and x.dtype == torch.bfloat16:
             layer.y_has_residual = True

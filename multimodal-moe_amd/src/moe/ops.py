@@ -15,8 +15,10 @@ for the MXFP8 (C5) and expert-parallel (C4) compositions:
                   {dH = dgrad (ReLU mask), dW2 + db2} and {dXp = dgrad, dW1 + db1
                   with the token rows gathered}
   _Combine        gate-weighted combine (K3); backward: combine_bwd
-Single GPU: 4 launches forward (router, route_dispatch, fused expert FFN,
-combine), 4 backward (combine_bwd, 2 pairs, token_bwd) + 1 torch GEMM for dWg.  The
+Single GPU (_MoELayer): 4 launches forward (router, route_dispatch, the fused
+expert FFN -- or GEMM1 + GEMM2 below 1,536 rows per expert --, combine with
+the residual), 4 backward (2 pairs with the combine transpose folded in,
+token_bwd, router_wgrad: dWg and the context-bias gradient in one launch).  The
 expert-parallel path (ep.py) moves real rows through its all-to-alls and runs
 _RouteDispatch (permute) + _ExpertFFN (rows in, same paired backward).  Nothing is synchronised with the host: expert
 offsets stay on the device, grids are sized from host upper bounds, and the

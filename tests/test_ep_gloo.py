@@ -25,8 +25,10 @@ E, K, D, F, TPI = 4, 2, 32, 64, 12  # D, F multiples of the 32-element MX block
 def _cfg(ep, dtype="bf16", epcf=2.0, cf=0.0):
     from src.moe.config import MoEConfig
 
+    # ep_lossless_mb=0: slots at the factor at every size (these tiny layers
+    # would otherwise fit the default lossless budget and never overflow)
     return MoEConfig(num_experts=E, top_k=K, hidden=F, ep_size=ep, capacity_factor=cf, expert_dtype=dtype,
-                     ep_capacity_factor=epcf, expert_parallel=ep > 1)
+                     ep_capacity_factor=epcf, ep_lossless_mb=0.0, expert_parallel=ep > 1)
 
 
 def _inputs(rank):
@@ -133,11 +135,17 @@ def test_compaction_map_is_a_bijection_on_valid_rows():
 def test_ep_slot_rows():
     from src.moe.config import MoEConfig, parse_moe_spec
 
-    assert MoEConfig(num_experts=16, top_k=2).ep_slot_rows(7360) == 1840  # default: 2x the mean rows
+    # default, per layer: the C4 encoder (lossless buffer 16 x 7,360 x 512 B = 60 MB > 32 MB) at 2x the
+    # mean rows, every C4 decoder layer (19.7 MB) lossless
+    assert MoEConfig(num_experts=16, top_k=2).ep_slot_rows(7360) == 1840
+    assert MoEConfig(num_experts=16, top_k=2).ep_slot_rows(2400) == 2400
     assert MoEConfig(num_experts=16, top_k=2, ep_capacity_factor=0.0).ep_slot_rows(7360) == 7360  # lossless
     assert parse_moe_spec("rtdetr-r50-moe16-top2-ep1-epcf0").moe.ep_slot_rows(7360) == 7360
-    assert parse_moe_spec("rtdetr-r50-moe16-top2-ep1").moe.ep_slot_rows(2400) == 600
-    c = MoEConfig(num_experts=16, top_k=2, ep_capacity_factor=2.0)
+    assert parse_moe_spec("rtdetr-r50-moe16-top2-ep1").moe.ep_slot_rows(2400) == 2400
+    assert parse_moe_spec("rtdetr-r50-moe16-top2-ep1-epmb0").moe.ep_slot_rows(2400) == 600  # no lossless budget
+    assert parse_moe_spec("rtdetr-r50-moe16-top2-ep1-epmb100").moe.ep_slot_rows(7360) == 7360
+    assert MoEConfig(num_experts=16, top_k=2).ep_slot_rows(2400, d_model=512) == 600  # 39 MB > 32 MB
+    c = MoEConfig(num_experts=16, top_k=2, ep_capacity_factor=2.0, ep_lossless_mb=0.0)
     assert c.ep_slot_rows(7360) == 1840        # 2 x mean 920
     c.ep_capacity_factor = 8.0                 # f k >= E: worst case, T
     assert c.ep_slot_rows(7360) == 7360

@@ -4,7 +4,10 @@ gloo (the flat gradient all-reduce and the norm partials on device tensors;
 the expert-parallel all-to-all staged through the host, src/moe/ep.py).
 
 * C3 data parallelism, bench.py's default execution (the whole step as ONE
-  hipGraph, fp32 flat all-reduce, FlatAdamW with inv_world): after one step
+  hipGraph; ZeRO-1 by default -- optim.ShardedDPAdamW: one fp32
+  reduce-scatter, AdamW on the rank's 1/W slice, one bf16 all-gather -- and
+  the flat fp32 all-reduce + FlatAdamW with inv_world as the MOE_ZERO=0
+  A/B path; both are tested): after one step
   the reduced gradient equals the mean of single-process graph-mode gradients
   of the two ranks' images, the clip norm is the norm of that mean, and both
   ranks hold identical weights.  The comparison is with the per-rank mean, not
@@ -12,7 +15,9 @@ the expert-parallel all-to-all staged through the host, src/moe/ep.py).
   BatchNorm and the MoE load-balance loss are per-rank batch statistics under
   data parallelism (no SyncBN), exactly as in DDP.
 * C4 expert parallelism: the HIP EP layer at world 2 (16 experts, 8 per rank)
-  reproduces the single-GPU 16-expert layer on each rank's tokens, and an
+  reproduces the single-GPU 16-expert layer on each rank's tokens -- with
+  lossless slots, and with slots below the skewed load (the capacity-factor
+  layer's drops, the overflow count) --, and an
   ``-ep2`` model trained for two steps keeps its replicated weights
   bit-identical across ranks (the clip norm sums the expert shards over the
   EP group).
@@ -172,15 +177,17 @@ def _ep_loss(layer, y, dy, ep):
     return (y.float() * dy).sum() + 10.0 * layer.aux_loss()
 
 
-def _ep_layer_worker(rank, world, port, out):
+def _ep_layer_worker(rank, world, port, out, epcf=0.0):
     _init(rank, world, port)
     from src.moe.config import MoEConfig
     from src.moe.layer import MoEFFN
 
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
+    # epcf 0: lossless slots; epcf 1: S = T k / E rows per (source, expert),
+    # below the skewed load, with no lossless budget: the receive path drops
     layer = MoEFFN(256, MoEConfig(num_experts=E_EP, top_k=K_EP, ep_size=world, expert_parallel=True,
-                                   ep_capacity_factor=0.0)).to(dev)  # lossless slots
+                                   ep_capacity_factor=epcf, ep_lossless_mb=0.0)).to(dev)
     x, ctx, dy = _ep_inputs(rank, dev)
     x.requires_grad_(True)
     y = layer(x, ctx)
@@ -204,20 +211,30 @@ def _close(a, b, what):
 
 
 @pytest.mark.gpu
-def test_hip_ep_layer_two_ranks_matches_single_gpu(hip_lib, tmp_path):
+@pytest.mark.parametrize("epcf", [0.0, 1.0], ids=["lossless", "overflow"])
+def test_hip_ep_layer_two_ranks_matches_single_gpu(hip_lib, tmp_path, epcf):
+    """The HIP expert-parallel layer over 2 ranks (moe_ep_compaction, the
+    scattering FFN, the paired backward writing the received layout) against
+    the single-GPU 16-expert layer on each rank's tokens: lossless slots, and
+    slots of T k / E rows per (source, expert) -- the lossy layout the C4
+    encoder runs -- where the reference layer has capacity factor 1.0 on the
+    rank's own tokens (the same slot-major drops) and the reported overflow is
+    sum_e max(hist_e - S, 0)."""
     from src.moe.config import MoEConfig
     from src.moe.layer import MoEFFN
 
     W = 2
-    mp.start_processes(_ep_layer_worker, args=(W, _port(), tmp_path), nprocs=W, join=True, start_method="spawn")
+    mp.start_processes(_ep_layer_worker, args=(W, _port(), tmp_path, epcf), nprocs=W, join=True,
+                       start_method="spawn")
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    ref = MoEFFN(256, MoEConfig(num_experts=E_EP, top_k=K_EP)).to(dev)  # all 16 experts, fused single-GPU path
+    # all 16 experts, fused single-GPU path; capacity factor epcf emulates the slots
+    ref = MoEFFN(256, MoEConfig(num_experts=E_EP, top_k=K_EP, capacity_factor=epcf)).to(dev)
     sums = None
     El = E_EP // W
+    overflow = 0
     for r in range(W):
         got = torch.load(tmp_path / f"ep{r}.pt")
-        assert got["overflow"] == 0  # lossless exchange (ep_capacity_factor 0)
         x, ctx, dy = _ep_inputs(r, dev)
         x.requires_grad_(True)
         ref.zero_grad(set_to_none=True)
@@ -225,10 +242,15 @@ def test_hip_ep_layer_two_ranks_matches_single_gpu(hip_lib, tmp_path):
         _ep_loss(ref, y, dy, False).backward()
         torch.cuda.synchronize()
         assert torch.equal(got["hist"], ref.last_hist.cpu())
+        T = x.shape[0] * x.shape[1]
+        S = ref.cfg.capacity(T) if epcf > 0 else T
+        assert got["overflow"] == int((ref.last_hist.long().cpu() - S).clamp(min=0).sum())
+        overflow += got["overflow"]
         _close(got["y"], y.detach().float().cpu(), f"rank {r} y")
         _close(got["dx"], x.grad.float().cpu(), f"rank {r} dx")
         g = {n: getattr(ref, n).grad.float().cpu().clone() for n in ("wg", "ctx_bias", "w1", "b1", "w2", "b2")}
         sums = g if sums is None else {n: sums[n] + g[n] for n in g}
+    assert (overflow > 0) == (epcf > 0), overflow  # the skewed single-context batches overflow T k / E slots
     for r in range(W):
         got = torch.load(tmp_path / f"ep{r}.pt")
         for n in ("wg", "ctx_bias"):

@@ -78,10 +78,13 @@ def gpu_layer(c: MC.LayerCase, inp: dict):
                 db2=_np(b2.grad))
 
 
-def gpu_layer_ep(c: MC.LayerCase, inp: dict):
+def gpu_layer_ep(c: MC.LayerCase, inp: dict, default_slots=False, dy_scale=1.0):
     """The expert-parallel layer (src/moe/ep.py: fixed-capacity padded dispatch,
     device row maps, GEMM1 over the gathered received rows) at W = 1 (identity
-    exchange), slots covering the worst case (no overflow drops)."""
+    exchange): slots covering the worst case (no overflow drops), or with
+    ``default_slots`` the default per-layer slot sizing (MoEConfig
+    ep_capacity_factor / ep_lossless_mb), whose drops the caller checks.
+    dy_scale 0: the loss is the aux terms alone."""
     from types import SimpleNamespace
 
     from src.moe.config import MoEConfig
@@ -90,21 +93,27 @@ def gpu_layer_ep(c: MC.LayerCase, inp: dict):
     def P(a):
         return torch.from_numpy(np.asarray(a)).float().to(DEV).requires_grad_(True)
 
-    cfg = MoEConfig(num_experts=c.E, top_k=c.k, capacity_factor=0.0 if c.cap <= 0 else 1.25,
-                    expert_dtype="fp8" if c.mx else "bf16", ep_capacity_factor=float(c.E) / c.k,
-                    expert_parallel=True)
-    assert cfg.capacity(c.T) == c.cap
+    if default_slots:
+        cfg = MoEConfig(num_experts=c.E, top_k=c.k, expert_dtype="fp8" if c.mx else "bf16", expert_parallel=True)
+    else:
+        cfg = MoEConfig(num_experts=c.E, top_k=c.k, capacity_factor=0.0 if c.cap <= 0 else 1.25,
+                        expert_dtype="fp8" if c.mx else "bf16", ep_capacity_factor=float(c.E) / c.k,
+                        expert_parallel=True)
+        assert cfg.capacity(c.T) == c.cap
     layer = SimpleNamespace(cfg=cfg, ep_size=1, ep_group=None, wg=P(inp["wg"]), w1=P(inp["w1"]), b1=P(inp["b1"]),
                             w2=P(inp["w2"]), b2=P(inp["b2"]))
     cb = P(inp["ctx_bias"])
     x = torch.from_numpy(np.asarray(inp["x"], np.float32)).to(torch.bfloat16).to(DEV).requires_grad_(True)
     ci = torch.from_numpy(inp["ctx_img"]).to(DEV)
-    y, lb, z, hist = moe_ffn_ep(layer, x, cb, ci, c.tpi, c.cap)
-    dy = torch.from_numpy(np.asarray(inp["dy"], np.float32)).to(torch.bfloat16).to(DEV)
+    y, lb, z, hist = moe_ffn_ep(layer, x, cb, ci, c.tpi, 0 if default_slots else c.cap)
+    dy = torch.from_numpy(np.asarray(inp["dy"], np.float32) * dy_scale).to(torch.bfloat16).to(DEV)
     ((y.float() * dy.float()).sum() + MC.G_LB * lb + MC.G_Z * z).backward()
     torch.cuda.synchronize()
-    assert layer.last_ep_overflow is None or int(layer.last_ep_overflow) == 0
+    over = 0 if layer.last_ep_overflow is None else int(layer.last_ep_overflow)
+    if not default_slots:
+        assert over == 0
     return dict(hist=hist.cpu().numpy(), y=_np(y), lb=float(lb.detach()), z=float(z.detach()), dx=_np(x.grad),
+                overflow=over, slots=cfg.ep_slot_rows(c.T, x.shape[1]),
                 dwg=_np(layer.wg.grad), dctx_bias=_np(cb.grad), dw1=_np(layer.w1.grad), db1=_np(layer.b1.grad),
                 dw2=_np(layer.w2.grad), db2=_np(layer.b2.grad))
 
@@ -186,6 +195,61 @@ def test_full_size_ep_layer_vs_oracle(hip_lib, name):
     assert all(v <= gtol for v in gerr.values()), gerr
     _REPORT[f"ep/{name}"] = dict(T=c.T, E=c.E, k=c.k, cap=c.cap, mx=c.mx, y_max_err_over_scale=y_err,
                                  dx_max_err_over_scale=dx_err, grad_rel_fro=gerr)
+
+
+@pytest.mark.parametrize("name", ["c4_enc", "c4_dec"])
+def test_full_size_ep_default_slots_vs_oracle(hip_lib, name):
+    """C4 through the expert-parallel layer with the DEFAULT slot sizing the
+    C4 bench runs (MoEConfig: the encoder at S = 2 T k / E rows per (source,
+    expert) -- 60 MB lossless exceeds the 32 MB budget --, every decoder layer
+    lossless) against the oracle with the same drops: at W = 1 a (source,
+    expert) slot block is the expert's capacity, so the oracle runs with
+    capacity S.  The overflow the layer reports is sum_e max(hist_e - S, 0)."""
+    import dataclasses
+
+    c0 = MC.FULL[name]
+    inp = MC.make_inputs(c0)
+    g = gpu_layer_ep(c0, inp, default_slots=True)
+    S = g["slots"]
+    assert S == (1840 if name == "c4_enc" else c0.T), S
+    # the oracle's capacity ceil(cf T k / E) = S
+    c = dataclasses.replace(c0, cf=(S * c0.E / (c0.T * c0.k)) if S < c0.T else 0.0)
+    assert c.cap == (S if S < c0.T else 0)
+    st, gr = MC.run_oracle(c, inp)
+    np.testing.assert_array_equal(g["hist"], st.hist)
+    assert g["overflow"] == int(np.maximum(st.hist - S, 0).sum()) == int((st.pos < 0).sum())
+    y_err = _elem_check(g["y"], st.y, f"{name} ep-default y")
+    dx_err = _elem_check(g["dx"], gr["dx"], f"{name} ep-default dx")
+    assert abs(g["lb"] - st.lb) <= 1e-5 * max(1.0, abs(st.lb))
+    assert abs(g["z"] - st.z) <= 1e-5 * max(1.0, abs(st.z))
+    gerr = {k: _rel_fro(g[k], gr[k]) for k in ("dwg", "dctx_bias", "dw1", "db1", "dw2", "db2")}
+    assert all(v <= 5e-3 for v in gerr.values()), gerr
+    _REPORT[f"ep_default/{name}"] = dict(T=c0.T, E=c0.E, k=c0.k, slots=S, overflow=g["overflow"],
+                                         overflow_frac=g["overflow"] / (c0.T * c0.k), y_max_err_over_scale=y_err,
+                                         dx_max_err_over_scale=dx_err, grad_rel_fro=gerr)
+
+
+@pytest.mark.parametrize("name", ["c4_enc", "c4_dec"])
+def test_ep_aux_loss_router_gradients_vs_oracle(hip_lib, name):
+    """The EP layer's aux-loss path in isolation: loss = G_LB lb + G_Z z only
+    (dy = 0), so every router-weight and context-bias gradient comes from the
+    load-balance and z losses through the fused aux-loss kernel (round 4 lost
+    the context-bias term there once, 2340c1c -> 58cb520)."""
+    c = MC.FULL[name]
+    inp = MC.make_inputs(c)
+    g = gpu_layer_ep(c, inp, dy_scale=0.0)
+    st = MC.O.moe_forward(inp["x"], inp["wg"], inp["ctx_bias"], inp["w1"], inp["b1"], inp["w2"], inp["b2"],
+                          inp["ctx_img"], c.tpi, c.k, True, c.cap, emulate_bf16=True)
+    gr = MC.O.moe_backward(st, inp["x"], inp["wg"], inp["w1"], inp["w2"], inp["ctx_img"], c.tpi, 6,
+                           np.zeros_like(inp["dy"]), g_lb=MC.G_LB, g_z=MC.G_Z, normalize=True, emulate_bf16=True)
+    np.testing.assert_array_equal(g["hist"], st.hist)
+    used = np.unique(inp["ctx_img"])
+    assert np.abs(gr["dctx_bias"][used]).max() > 0  # the aux terms do reach the context bias
+    for k in ("dwg", "dctx_bias"):
+        err = _rel_fro(g[k], gr[k])
+        assert err <= 1e-4, f"{name} {k}: relative Frobenius {err:.2e}"
+    assert np.abs(g["dw1"]).max() == 0 and np.abs(g["dw2"]).max() == 0  # no expert gradient without dy
+    assert _rel_fro(g["dx"], gr["dx"]) <= 1e-2
 
 
 @pytest.mark.parametrize("name", list(MC.GOLDEN))

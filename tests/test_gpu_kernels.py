@@ -586,15 +586,13 @@ def test_route_dispatch_matches_scan_index_aux(hip_lib, T, E, k, cf):
     assert torch.equal(gate2[pos2[keep].long()], w[keep])
 
 
-@pytest.mark.parametrize("chunked", [1, 0])
 @pytest.mark.parametrize("B,tpi,E,C", [(3, 920, 8, 6), (8, 300, 8, 6), (2, 17, 32, 4), (1, 130, 16, 1),
                                        (16, 920, 32, 5), (4, 333, 6, 3), (2, 2500, 64, 2), (8, 1, 8, 3)])
-def test_router_wgrad_vs_fp64(hip_lib, B, tpi, E, C, chunked):
+def test_router_wgrad_vs_fp64(hip_lib, B, tpi, E, C):
     """moe_router_wgrad: dWg = dlogits^T x and the per-context sums of
     dlogits (contexts repeated across images, one context unused) against an
-    fp64 reference, chunked kernel and per-column kernel (default); fixed-order
-    sums, so two launches are bitwise equal and dWg does not depend on whether
-    dcb is formed."""
+    fp64 reference; fixed-order sums, so two launches are bitwise equal and dWg
+    does not depend on whether dcb is formed."""
     from src.moe import _lib as L
 
     g = torch.Generator(device=DEV).manual_seed(B * tpi + E)
@@ -602,16 +600,11 @@ def test_router_wgrad_vs_fp64(hip_lib, B, tpi, E, C, chunked):
     dl = torch.randn((T, E), device=DEV, generator=g)
     x = torch.randn((T, d), device=DEV, generator=g).to(torch.bfloat16)
     ci = torch.randint(0, max(1, C - 1), (B,), device=DEV, generator=g).to(torch.int32)
-    L.set_tuning("router_wgrad_chunked", chunked)
-    try:
-        L.ensure_splitk_workspace(x.device)
-        assert (L.lib().moe_router_wgrad_workspace(B, tpi, E, d) > 0) == bool(chunked)
-        dwg, dcb = L.router_wgrad(dl, x, ci, tpi, C)
-        dwg2, dcb2 = L.router_wgrad(dl, x, ci, tpi, C)
-        dwg0, dcb0 = L.router_wgrad(dl, x, None, tpi, 0)
-        torch.cuda.synchronize()
-    finally:
-        L.set_tuning("router_wgrad_chunked", 0)
+    assert L.lib().moe_router_wgrad_workspace(B, tpi, E, d) == 0  # reserved since round 5
+    dwg, dcb = L.router_wgrad(dl, x, ci, tpi, C)
+    dwg2, dcb2 = L.router_wgrad(dl, x, ci, tpi, C)
+    dwg0, dcb0 = L.router_wgrad(dl, x, None, tpi, 0)
+    torch.cuda.synchronize()
     ref = dl.double().t() @ x.double()
     per_img = dl.double().view(B, tpi, E).sum(1)
     ref_cb = torch.zeros((C, E), dtype=torch.float64, device=DEV).index_add_(0, ci.long(), per_img)

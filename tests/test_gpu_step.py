@@ -115,7 +115,7 @@ def test_ep_world1_matches_single_gpu_layer(hip_lib, dtype, cf, epcf, rccl):
         cfg = MoEConfig(num_experts=E, top_k=k, capacity_factor=ref_cf, expert_dtype=dtype)
         layer = MoEFFN(256, cfg).to(DEV)
         ecfg = MoEConfig(num_experts=E, top_k=k, capacity_factor=cf, expert_dtype=dtype, ep_capacity_factor=epcf,
-                         expert_parallel=True)
+                         ep_lossless_mb=0.0, expert_parallel=True)
         x = torch.randn(4, 150, 256, device=DEV).to(torch.bfloat16)
         ctx = torch.tensor([0, 1, 2, 3], dtype=torch.int32, device=DEV)
         dy = torch.randn(4, 150, 256, device=DEV)

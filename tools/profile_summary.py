@@ -136,6 +136,19 @@ def main(src: str, dst: str):
     mp = src_p / "pmc_mfma" / "p_counter_collection.csv"
     mfma = mfma_summary(mp) if mp.exists() else {}
     res = {"source": str(src_p), "all_kernels_total_ms": round(total_ns / 1e6, 3), "groups": {}}
+    # the profiled bench line: its build id and configuration let bench.py tell
+    # whether this summary belongs to the build it runs (bench.rocprof_headline)
+    bj = src_p / "prof" / "bench.json"
+    if bj.exists():
+        lines = [ln for ln in bj.read_text().splitlines() if ln.startswith("{")]
+        if lines:
+            b = json.loads(lines[-1])
+            res["bench"] = {"libmoe_hip_sha16": b.get("build", {}).get("libmoe_hip_sha16"),
+                            "precision": b.get("build", {}).get("precision"),
+                            "graphs": b.get("build", {}).get("graphs"),
+                            "workload": b.get("config", {}).get("workload"),
+                            "batch": b.get("config", {}).get("batch"),
+                            "steps": b.get("steps"), "warmup": b.get("warmup"), "value": b.get("value")}
     for g, _ in GROUPS:
         e = dict(stats.get(g, {}))
         if g in fetch and g in write:
