@@ -279,6 +279,8 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the workload's)")
+    ap.add_argument("--spec-extra", default="", help="model-spec tokens appended to the workload's spec (A/B, "
+                                                      "e.g. -epmb0 or -epcf0 for C4)")
     ap.add_argument("--img-h", type=int, default=720)
     ap.add_argument("--img-w", type=int, default=1280)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -506,7 +508,7 @@ def main():
         heartbeat()
     device = torch.device("cuda", local)
     wl = WORKLOADS[args.workload]
-    spec = wl["spec"].format(N=world)
+    spec = wl["spec"].format(N=world) + args.spec_extra
     torch.backends.cudnn.benchmark = bool(args.conv_search)
     torch.backends.cudnn.deterministic = bool(args.deterministic)
     batch = args.batch or wl["batch"]
@@ -582,6 +584,9 @@ def main():
         L.TIMER.harvest()
         L.TIMER.stop()
         prof_steps = args.profile_steps
+    # the exchange accounting of the last TRAINING step (the eval leg's
+    # forwards below run eval-mode BatchNorm: different activations, routing)
+    ep_stats = expert_parallel_stats(model, spec, world) if "-ep" in spec else None
     ev = None
     if args.eval_steps > 0:
         log(rank, f"eval leg: {args.eval_steps} inference forwards")
@@ -601,7 +606,6 @@ def main():
     elapsed = float(el.item())
     ksum = L.TIMER.summary() if timing else {}
 
-    ep_stats = expert_parallel_stats(model, spec, world) if "-ep" in spec else None
     result = None
     if rank == 0:
         images_total = world * batch * args.steps

@@ -602,16 +602,17 @@ static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int 
 
 constexpr int CV_STAGES = 2;
 
-template <int KS, int BM, int BN, bool BT, bool PH, int WGM = 2, int WGN = 2>
+template <int KS, int BM, int BN, bool BT, bool PH, int WGM = 2, int WGN = 2, int ST = CV_STAGES>
 static void launch_fwd_n(ConvArgs a, hipStream_t stream, ProfScope& prof) {
-  constexpr size_t lds = CV_STAGES * (BM + BN) * 128;
+  constexpr size_t lds = ST * (BM + BN) * 128;
   static_assert(lds >= BM * BN * 2, "epilogue image exceeds the ring");
+  static_assert(lds <= 160 * 1024, "ring exceeds the CU's LDS");
   static_assert(!(BT && BN > 128), "the in-place (MN-contiguous) weight image takes 64 or 128 columns");
-  allow_lds_once<conv_fwd_kernel<KS, CV_STAGES, BM, BN, BT, PH, WGM, WGN>>(lds);
+  allow_lds_once<conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN>>(lds);
   a.mt_n = (a.P + BM - 1) / BM;
   const int NT = a.N / BN;
   const int grid = ((a.mt_n + 7) / 8) * 8 * NT;
-  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, CV_STAGES, BM, BN, BT, PH, WGM, WGN>), dim3(grid), dim3(64 * WGM * WGN), lds,
+  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN>), dim3(grid), dim3(64 * WGM * WGN), lds,
              stream, a);
 }
 
@@ -626,11 +627,16 @@ template <int KS, bool BT, bool PH>
 static bool launch_fwd_big(const ConvArgs& a, hipStream_t stream, ProfScope& prof, int mode) {
   // (a 256 x 256 tile of 2 x 2 waves, 128 x 128 per wave at one workgroup per CU, measured 1.2-4x
   // slower at every C2 shape: profiles/r04/conv/conv_bench_256x256_ab.jsonl)
-  if (mode == 1 && a.N % 128 == 0) {
-    launch_fwd_n<KS, 256, 128, BT, PH, 4, 2>(a, stream, prof);
-    return true;
+  if (a.N % 128 != 0) return false;
+  switch (mode) {
+    case 1: launch_fwd_n<KS, 256, 128, BT, PH, 4, 2>(a, stream, prof); return true;
+    // deeper rings (round 5): K-tiles in flight per CU, not the tile shape, bound these layers
+    case 2: launch_fwd_n<KS, 256, 128, BT, PH, 4, 2, 3>(a, stream, prof); return true;    // 144 KiB, 1 WG / CU
+    case 3: launch_fwd_n<KS, 128, 128, BT, PH, 2, 2, 3>(a, stream, prof); return true;    //  96 KiB, 1 WG / CU
+    case 4: launch_fwd_n<KS, 128, 128, BT, PH, 2, 2, 4>(a, stream, prof); return true;    // 128 KiB, 1 WG / CU
+    case 5: launch_fwd_n<KS, 128, 128, BT, PH, 4, 2, 4>(a, stream, prof); return true;    // 8 waves of 32 x 64
+    default: return false;
   }
-  return false;
 }
 
 // output-channel tiles of 128, or 64 for 64-channel outputs (ResNet stage 1)

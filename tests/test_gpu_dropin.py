@@ -89,7 +89,7 @@ def test_scripts_train_then_eval_on_gpu(hip_lib, tmp_path, monkeypatch):
             assert m.dtype == torch.float32 and m.shape == g.shape
             assert torch.equal(m.to(torch.bfloat16), g.to("cpu", torch.bfloat16)), f"{name}.{attr}"
             n_exp += 1
-    assert n_exp >= 2 * 7  # AIFI + 6 decoder layers
+    assert n_exp == 2 * len(gpu_model.moe_layers()) >= 2 * 4  # AIFI + the R18 spec's 3 decoder layers
     # at least one master differs from its bf16 rounding: fp32 state, not a widened bf16 copy
     w = sd[f"{next(n for n, m in gpu_model.named_modules() if isinstance(m, MoEFFN))}.w1"]
     assert not torch.equal(w, w.to(torch.bfloat16).float())

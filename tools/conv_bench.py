@@ -101,11 +101,21 @@ def main():
         gw = torch.empty_like(w)
         t_hw = timeit(lambda: lib.rtdetr_conv_wgrad(gy.data_ptr(), x.data_ptr(), part.data_ptr(), ns, gw.data_ptr(), 1,
                                                     z, B, H, W, Ci, Co, ks, st, L._stream()))
+        # correctness of the variant under test (HIP vs MIOpen, bf16 outputs)
+        yref = F.conv2d(x, w, None, st, pad)
+        xref = torch.ops.aten.convolution_backward(gy, x, w, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
+                                                   [True, False, False])[0]
+        wref = torch.ops.aten.convolution_backward(gy, x, w, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
+                                                   [False, True, False])[1]
+        rel = lambda a, b: round(float((a.float() - b.float()).norm() / b.float().norm().clamp(min=1e-12)), 5)  # noqa: E731
+        errs = [rel(yh, yref), rel(gx, xref), rel(gw, wref)]
         tf = lambda t: round(flop / t / 1e6, 1)  # noqa: E731  TFLOP/s
         print(json.dumps({"shape": list(shape), "gflop": round(flop / 1e9, 2), "wgrad_splits": ns, "dgrad_flip": nb > 0,
                           "miopen_us": [round(t_mf, 1), round(t_md, 1), round(t_mw, 1)],
                           "hip_us": [round(t_hf, 1), round(t_hd, 1), round(t_hw, 1)],
-                          "miopen_tflops": [tf(t_mf), tf(t_md), tf(t_mw)], "hip_tflops": [tf(t_hf), tf(t_hd), tf(t_hw)]}),
+                          "miopen_tflops": [tf(t_mf), tf(t_md), tf(t_mw)], "hip_tflops": [tf(t_hf), tf(t_hd), tf(t_hw)],
+                          "rel_err_vs_miopen": errs,
+                          "tuning": [a for a in sys.argv[1:] if "=" in a]}),
               flush=True)
 
 
