@@ -112,6 +112,12 @@ static int g_ksplit = 0;    // 0 = per-shape choice, else forced split-K factor 
 static int g_gemm_pair_off = 0;  // 1: moe_grouped_gemm_bwd_pair issues two launches (A/B)
 static int g_wgrad_dma = 0;      // gathered WGRAD: 0 = default (LDS-DMA ring), 1 = register-staged (A/B)
 static int g_wgrad_stages = 0;   // gathered WGRAD LDS-DMA ring depth: 0 = default (2), else 2 or 3
+// split-K of the HEAVY groups of a weight gradient that is otherwise unsplit
+// (the decoder's ~600-row experts): groups of at least this many K-tiles (64
+// rows) run as two slices merged in slice order; 0 = off.  In the training
+// step the routed counts are skewed (largest expert 2-3x the mean early on):
+// the heaviest group's K loop is the launch's tail.
+static int g_wgrad_split_hot = 0;
 
 // split-K workspace registered per device by the caller (moe_set_splitk_workspace)
 struct SplitWs {
@@ -1550,9 +1556,13 @@ static int plan_wgrad(WgradPlan& pl, const void* x, const void* y, void* c, void
   // against 21.1 us for hipBLASLt's dY^T X without the bias column sum
   const long long nkt = (rows_hint + 63) / 64;
   const int dense_want = (int)std::max(1LL, std::min({8LL, 256 / std::max(1LL, tiles), nkt / 4}));
-  const int want = g_ksplit ? g_ksplit
-                            : (G == 1 ? dense_want : ((tiles <= 512 && rows_hint >= 1024LL * G) ? 2 : 1));
+  int want = g_ksplit ? g_ksplit
+                      : (G == 1 ? dense_want : ((tiles <= 512 && rows_hint >= 1024LL * G) ? 2 : 1));
   p.split_min_kt = 0;
+  if (want == 1 && g_wgrad_split_hot > 0 && G > 1 && !g_ksplit) {
+    want = 2;
+    p.split_min_kt = g_wgrad_split_hot;
+  }
   if (want > 1 && tiles % 8 != 0) {  // split grids map 8-slot XCD rows: pad the group count
     gpad = (G + 7) / 8 * 8;
     tiles = tpg * gpad;
@@ -1701,6 +1711,7 @@ extern "C" int moe_set_tuning(const char* key, int value) {
   if (k == "gemm_pair" && value >= 0 && value <= 1) { g_gemm_pair_off = value ? 0 : 1; return 0; }
   if (k == "wgrad_dma" && value >= 0 && value <= 1) { g_wgrad_dma = value; return 0; }
   if (k == "wgrad_stages" && (value == 0 || value == 2 || value == 3)) { g_wgrad_stages = value; return 0; }
+  if (k == "wgrad_split_hot" && value >= 0 && value <= 1024) { g_wgrad_split_hot = value; return 0; }
   if (k == "msda_generic" && value >= 0 && value <= 3) { g_msda_generic = value; return 0; }
   return fail("moe_set_tuning: unknown key or value");
 }

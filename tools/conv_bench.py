@@ -109,12 +109,19 @@ def main():
                                                    [False, True, False])[1]
         rel = lambda a, b: round(float((a.float() - b.float()).norm() / b.float().norm().clamp(min=1e-12)), 5)  # noqa: E731
         errs = [rel(yh, yref), rel(gx, xref), rel(gw, wref)]
+        # the same GEMM (M = output pixels, N = Cout, K = KS^2 Cin) on hipBLASLt
+        # (torch.mm, bf16): what a library GEMM reaches at this shape
+        am = torch.randn(B * Ho * Wo, ks * ks * Ci, device=dev).to(torch.bfloat16)
+        bm = torch.randn(ks * ks * Ci, Co, device=dev).to(torch.bfloat16)
+        t_mm = timeit(lambda: torch.mm(am, bm))
+        del am, bm
         tf = lambda t: round(flop / t / 1e6, 1)  # noqa: E731  TFLOP/s
         print(json.dumps({"shape": list(shape), "gflop": round(flop / 1e9, 2), "wgrad_splits": ns, "dgrad_flip": nb > 0,
                           "miopen_us": [round(t_mf, 1), round(t_md, 1), round(t_mw, 1)],
                           "hip_us": [round(t_hf, 1), round(t_hd, 1), round(t_hw, 1)],
                           "miopen_tflops": [tf(t_mf), tf(t_md), tf(t_mw)], "hip_tflops": [tf(t_hf), tf(t_hd), tf(t_hw)],
-                          "rel_err_vs_miopen": errs,
+                          "rel_err_vs_miopen": errs, "hipblaslt_gemm_us": round(t_mm, 1),
+                          "hipblaslt_gemm_tflops": tf(t_mm),
                           "tuning": [a for a in sys.argv[1:] if "=" in a]}),
               flush=True)
 
