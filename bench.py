@@ -478,27 +478,40 @@ def eval_leg(model, images, ctx, steps, warmup=3):
     """Inference speed of the trained model on the workload's batch: the
     forward engine._evaluate times for ``speed_inference_ms_per_img`` (reference
     scripts/eval_detector.py:99-116 derives fps_inference_only from it):
-    model.eval(), no_grad, bf16 autocast, the batch resident in HBM, timed
-    between synchronizes.  Returns the eval block of the bench line."""
+    engine.EvalForward -- model.eval(), no_grad, bf16 autocast, replayed as a
+    hipGraph per input shape -- with the batch resident in HBM, timed between
+    synchronizes; the same forward run eagerly is reported beside it.  Returns
+    the eval block of the bench line."""
+    from src.rtdetr_moe.engine import EvalForward
+
+    def timed(fwd):
+        for _ in range(warmup):
+            fwd(images, ctx)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fwd(images, ctx)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
     was_training = model.training
     model.eval()
     try:
-        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
-            for _ in range(warmup):
-                model(images, ctx)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                model(images, ctx)
-            torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
+        graphed = EvalForward(model)
+        graphed.prepare(images, ctx)
+        dt = timed(graphed)
+        eager = EvalForward(model)
+        eager.enabled = False
+        dt_eager = timed(eager)
+        del graphed
     finally:
         model.train(was_training)
     n = steps * images.shape[0]
     return {"speed_inference_ms_per_img": round(1e3 * dt / n, 4), "fps_inference_only": round(n / dt, 2),
             "images_per_sec": round(n / dt, 2), "batch": int(images.shape[0]), "steps": steps, "warmup": warmup,
-            "mode": "eager forward, model.eval(), torch.no_grad, bf16 autocast (engine._evaluate's forward), "
-                    "batch resident in HBM, postprocess excluded"}
+            "eager_images_per_sec": round(n / dt_eager, 2),
+            "mode": "engine.EvalForward (engine._evaluate's forward): model.eval(), torch.no_grad, bf16 autocast, "
+                    "hipGraph replay per input shape; batch resident in HBM, postprocess excluded"}
 
 
 def main():

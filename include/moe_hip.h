@@ -329,6 +329,22 @@ int moe_grouped_gemm_bwd_pair_scatter(const void* a, const int32_t* a_gather, co
                                       const int32_t* wy_gather, void* wc, void* wcolsum, int M2, int N2,
                                       int out_bf16, hipStream_t stream);
 
+/* The routed expert FFN backward of the single-GPU bf16 layer in TWO launches
+ * (replaces the two moe_grouped_gemm_bwd_pair calls): launch 1 the dgrad
+ * dH = relu'(H) * (gate[r] dy[tok[r]] . W2_g) into dh bf16 [max_rows, F];
+ * launch 2 ONE grid of dXp = dH . W1_g (dxp bf16 [max_rows, d]), dW2_g =
+ * dYp^T H + db2 (dYp = bf16(gate * dy[tok]) formed while staging) and dW1_g =
+ * dH^T x[tok] + db1 -- the two weight gradients' K loops (the routed counts)
+ * run beside each other instead of in two launches.  dy, x bf16 [T, d]; h bf16
+ * [max_rows, F] (the forward's H); w1 bf16 [G, F, d], w2 bf16 [G, d, F]; tok,
+ * gate [max_rows] (row -> token, gate); dw1/db1/dw2/db2 bf16 (out_bf16 = 1) or
+ * fp32 [G, F, d] / [G, F] / [G, d, F] / [G, d].  Same sums, in the same order,
+ * as the paired calls (bitwise equal).  Reference: SURVEY 8(a) row a7. */
+int moe_expert_ffn_bwd(const void* dy, const int32_t* tok, const float* gate, const void* x, const void* h,
+                       const void* w1, const void* w2, const int32_t* offsets, int G, int max_rows, int F, int d,
+                       void* dh, void* dxp, void* dw1, void* db1, void* dw2, void* db2, int out_bf16,
+                       hipStream_t stream);
+
 /* ---- MXFP8 expert path (config C5: 32-expert top-4 fp8 expert GEMMs) ----
  * Format: OCP e4m3 elements with one E8M0 exponent byte per 32 consecutive
  * elements of a row ("MXFP8"); the block exponent e is the smallest with

@@ -1320,6 +1320,18 @@ void gemm_pair_kernel(GemmParams p1, GemmParams p2, int n1) {
   if ((int)blockIdx.x < n1) P1::run(p1, blockIdx.x, smem);
   else P2::run(p2, (int)blockIdx.x - n1, smem);
 }
+// Three independent grouped GEMMs in ONE launch (the expert FFN backward's
+// second half, moe_expert_ffn_bwd): workgroups [0, n1) problem 1, [n1, n12)
+// problem 2, the rest problem 3; n1 and n12 are multiples of 8 (XCD maps).
+template <class P1, class P2, class P3>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+void gemm_triple_kernel(GemmParams p1, GemmParams p2, GemmParams p3, int n1, int n12) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x;
+  if (b < n1) P1::run(p1, b, smem);
+  else if (b < n12) P2::run(p2, b - n1, smem);
+  else P3::run(p3, b - n12, smem);
+}
 template <int BM, int BN, int S, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL>
 struct BodyV2 {
   static __device__ __forceinline__ void run(const GemmParams& p, int bid, char* smem) {
@@ -1681,6 +1693,40 @@ static void launch_pair(const RowsPlan& r, const WgradPlan& w, hipStream_t s, co
   else launch_pair_s<2, FLW>(r, w, s, prof);
 }
 
+// The expert FFN backward's second launch: dW2 (+ db2) and dW1 (+ db1) as
+// gathered-k-row LDS-DMA weight gradients and dXp as the dgrad, all three in
+// one grid.  The caller checks triple_ok.
+static bool triple_ok(const RowsPlan& r, const WgradPlan& w2, const WgradPlan& w1) {
+  auto wok = [](const WgradPlan& w) {
+    return w.bm == 64 && w.variant == 2 && (w.stages == 2 || w.stages == 3) && w.colsum && w.grid % 8 == 0;
+  };
+  return r.bm == 64 && !r.trans_b && r.variant == 2 && (r.stages == 2 || r.stages == 3) && r.epi == MOE_EPI_NONE &&
+         r.grid % 8 == 0 && wok(w2) && wok(w1) && w2.stages == w1.stages;
+}
+template <int S, int SW>
+static void launch_triple_k(const RowsPlan& r, const WgradPlan& w2, const WgradPlan& w1, hipStream_t s,
+                            const ProfScope& prof) {
+  using R = BodyV2<64, 128, S, true, false, MODE_ROWS, MOE_EPI_NONE, false, 0>;
+  using W = BodyV2<64, 128, SW, false, false, MODE_WGRAD, MOE_EPI_NONE, true, 0>;
+  constexpr auto fn = gemm_triple_kernel<W, W, R>;
+  const size_t lds_r = (size_t)S * (64 + 128) * 64 * 2;
+  const size_t lds_w = (size_t)SW * ((64 + 128) * 64 * 2 + 768);
+  const size_t lds = lds_r > lds_w ? lds_r : lds_w;
+  allow_lds<fn>(lds);
+  const int n1 = (int)w2.grid, n12 = (int)(w2.grid + w1.grid);
+  MOE_LAUNCH(prof, fn, dim3(r.grid + w2.grid + w1.grid), dim3(256), lds, s, w2.p, w1.p, r.p, n1, n12);
+}
+static void launch_triple(const RowsPlan& r, const WgradPlan& w2, const WgradPlan& w1, hipStream_t s,
+                          const ProfScope& prof) {
+  if (r.stages == 3) {
+    if (w2.stages == 3) launch_triple_k<3, 3>(r, w2, w1, s, prof);
+    else launch_triple_k<3, 2>(r, w2, w1, s, prof);
+  } else {
+    if (w2.stages == 3) launch_triple_k<2, 3>(r, w2, w1, s, prof);
+    else launch_triple_k<2, 2>(r, w2, w1, s, prof);
+  }
+}
+
 }  // namespace moe
 
 using namespace moe;
@@ -1914,6 +1960,69 @@ extern "C" int moe_grouped_gemm_bwd_pair_scatter(const void* a, const int32_t* a
   r.p.prof_rows = prof.rows_slot();
   launch_pair<0>(r, w, stream, prof);
   return check_launch("moe_grouped_gemm_bwd_pair");
+}
+
+// The routed expert FFN backward in TWO launches (single-GPU bf16 layer):
+//   1. dH = relu'(H) * (gate[r] dy[tok[r]] . W2_g)                     (dgrad)
+//   2. dXp = dH . W1_g,  dW2 = dYp^T H (+ db2),  dW1 = dH^T x[tok] (+ db1) (one grid)
+// where dYp = bf16(gate * dy[tok]) is formed while staging.  The paired form
+// ({dH, dW2} then {dXp, dW1}) runs the two weight gradients -- the long K
+// loops, skewed by the routed counts -- one after the other; here they run
+// beside each other and beside dXp, after the short dH launch.
+extern "C" int moe_expert_ffn_bwd(const void* dy, const int32_t* tok, const float* gate, const void* x, const void* h,
+                                  const void* w1, const void* w2, const int32_t* offsets, int G, int max_rows, int F,
+                                  int d, void* dh, void* dxp, void* dw1, void* db1, void* dw2, void* db2, int out_bf16,
+                                  hipStream_t stream) {
+  if (dy == nullptr || tok == nullptr || gate == nullptr || x == nullptr || h == nullptr || w1 == nullptr ||
+      w2 == nullptr || dh == nullptr || dxp == nullptr || dw1 == nullptr || db1 == nullptr || dw2 == nullptr ||
+      db2 == nullptr || offsets == nullptr)
+    return fail("expert_ffn_bwd: NULL pointer");
+  if (max_rows <= 0 || g_gemm_pair_off) {  // (no rows: the paired path writes the zero weight gradients)
+    if (moe_grouped_gemm_bwd_pair_scatter(dy, tok, gate, w2, dh, nullptr, offsets, G, max_rows, F, d,
+                                          MOE_EPI_RELU_MASK, h, dy, tok, gate, h, nullptr, dw2, db2, d, F, out_bf16,
+                                          stream))
+      return -1;
+    return moe_grouped_gemm_bwd_pair_scatter(dh, nullptr, nullptr, w1, dxp, nullptr, offsets, G, max_rows, d, F,
+                                             MOE_EPI_NONE, nullptr, dh, nullptr, nullptr, x, tok, dw1, db1, F, d,
+                                             out_bf16, stream);
+  }
+  WsWin win = device_ws();
+  RowsPlan r2, r1;
+  WgradPlan wg2, wg1;
+  if (plan_rows(r2, dy, w2, dh, offsets, G, max_rows, F, d, 0, MOE_EPI_RELU_MASK, nullptr, h, tok, win, gate))
+    return -1;
+  {  // launch 1: dH (its split-K window, if any, is free again after this launch)
+    ProfScope prof(stream, PROF_GEMM, r2.bytes_fixed, true, r2.bytes_row, r2.flops_row);
+    r2.p.prof_rows = prof.rows_slot();
+    launch_rows(r2, stream, prof);
+    if (check_launch("moe_expert_ffn_bwd (dH)")) return -1;
+  }
+  win = device_ws();
+  if (plan_wgrad(wg2, dy, h, dw2, db2, offsets, G, d, F, max_rows, out_bf16, nullptr, win, tok, gate)) return -1;
+  if (plan_wgrad(wg1, dh, x, dw1, db1, offsets, G, F, d, max_rows, out_bf16, tok, win)) return -1;
+  if (plan_rows(r1, dh, w1, dxp, offsets, G, max_rows, d, F, 0, MOE_EPI_NONE, nullptr, nullptr, nullptr, win))
+    return -1;
+  if (!triple_ok(r1, wg2, wg1)) {  // separate launches (shapes the one-grid form does not take)
+    {
+      ProfScope prof(stream, PROF_GEMM, r1.bytes_fixed, true, r1.bytes_row, r1.flops_row);
+      r1.p.prof_rows = prof.rows_slot();
+      launch_rows(r1, stream, prof);
+    }
+    if (check_launch("moe_expert_ffn_bwd (dXp)")) return -1;
+    ProfScope p2(stream, PROF_GEMM, wg2.bytes_fixed, true, wg2.bytes_row, wg2.flops_row);
+    wg2.p.prof_rows = p2.rows_slot();
+    launch_wgrad<0>(wg2, stream, p2);
+    if (check_launch("moe_expert_ffn_bwd (dW2)")) return -1;
+    ProfScope p1(stream, PROF_GEMM, wg1.bytes_fixed, true, wg1.bytes_row, wg1.flops_row);
+    wg1.p.prof_rows = p1.rows_slot();
+    launch_wgrad<0>(wg1, stream, p1);
+    return check_launch("moe_expert_ffn_bwd (dW1)");
+  }
+  ProfScope prof(stream, PROF_GEMM, r1.bytes_fixed + wg2.bytes_fixed + wg1.bytes_fixed, true,
+                 r1.bytes_row + wg2.bytes_row + wg1.bytes_row, r1.flops_row + wg2.flops_row + wg1.flops_row);
+  r1.p.prof_rows = prof.rows_slot();
+  launch_triple(r1, wg2, wg1, stream, prof);
+  return check_launch("moe_expert_ffn_bwd");
 }
 
 extern "C" int moe_grouped_gemm_bwd_pair(const void* a, const int32_t* a_gather, const float* row_scale,

@@ -128,6 +128,7 @@ SIGNATURES = {
     "moe_profile_count": (_I, []),
     "moe_profile_get": (_I, [_I, _P, _P, _P, _P]),
     "moe_profile_clear": (_I, []),
+    "moe_expert_ffn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
     "moe_launch_counts": (_I, [_P, _I]),
     "moe_launch_counts_reset": (_I, []),
     "moe_last_error": (ctypes.c_char_p, []),
@@ -575,6 +576,36 @@ def ep_compaction(recv_cnt, hist, S):
     _check(lib().moe_ep_compaction(_ptr(recv_cnt), _ptr(hist), W, El, hist.numel(), int(S), _ptr(gather),
                                    _ptr(offsets), _ptr(overflow), _stream()), "moe_ep_compaction")
     return gather, offsets, overflow
+
+
+def expert_ffn_bwd(dy, tok, gate, x, h, w1, w2, offsets, G, max_rows, out_dtype=torch.bfloat16):
+    """The expert FFN backward in two launches (moe_expert_ffn_bwd): dy, x bf16
+    [T, d] token rows, tok / gate [>= max_rows] row -> token map and gate, h
+    bf16 [max_rows, F] the forward's H, w1 bf16 [G, F, d], w2 bf16 [G, d, F].
+    -> (dh [max_rows, F], dxp [max_rows, d], dW1, db1, dW2, db2)."""
+    for t, n in ((dy, "dy"), (x, "x"), (h, "h"), (w1, "w1"), (w2, "w2")):
+        _need(t, torch.bfloat16, n)
+    _need(tok, torch.int32, "tok")
+    _need(gate, torch.float32, "gate")
+    Gw, F, d = w1.shape
+    if Gw != G or tuple(w2.shape) != (G, d, F) or dy.shape[1] != d or x.shape[1] != d or h.shape[1] != F:
+        raise MoEKernelError("expert_ffn_bwd: shapes")
+    if tok.numel() < max_rows or gate.numel() < max_rows or h.shape[0] < max_rows:
+        raise MoEKernelError("expert_ffn_bwd: tok / gate / h shorter than max_rows")
+    dev = dy.device
+    rows = max(int(max_rows), 1)
+    dh = torch.empty((rows, F), dtype=torch.bfloat16, device=dev)
+    dxp = torch.empty((rows, d), dtype=torch.bfloat16, device=dev)
+    dw1 = torch.empty((G, F, d), dtype=out_dtype, device=dev)
+    db1 = torch.empty((G, F), dtype=out_dtype, device=dev)
+    dw2 = torch.empty((G, d, F), dtype=out_dtype, device=dev)
+    db2 = torch.empty((G, d), dtype=out_dtype, device=dev)
+    ensure_splitk_workspace(dev)
+    _check(lib().moe_expert_ffn_bwd(_ptr(dy), _ptr(tok), _ptr(gate), _ptr(x), _ptr(h), _ptr(w1), _ptr(w2),
+                                    _ptr(offsets), G, int(max_rows), F, d, _ptr(dh), _ptr(dxp), _ptr(dw1), _ptr(db1),
+                                    _ptr(dw2), _ptr(db2), int(out_dtype == torch.bfloat16), _stream()),
+           "moe_expert_ffn_bwd")
+    return dh, dxp, dw1, db1, dw2, db2
 
 
 def grouped_gemm_bwd_pair(a, b, offsets, G, max_rows, N, K, epilogue, aux, wx, wy, wy_gather=None,

@@ -48,6 +48,9 @@ def _bias(b):
 
 # MOE_FUSED_FFN=0: the expert FFN forward as two grouped GEMMs (A/B switch)
 _FUSED_FFN = os.environ.get("MOE_FUSED_FFN", "1") != "0"
+# MOE_FFN_BWD2=0: the single-GPU expert FFN backward as the two paired launches
+# {dH, dW2}, {dXp, dW1} instead of moe_expert_ffn_bwd's dH, {dXp, dW2, dW1} (A/B)
+_FFN_BWD2 = os.environ.get("MOE_FFN_BWD2", "1") != "0"
 _FUSED_MIN_ROWS = int(os.environ.get("MOE_FUSED_FFN_MIN_ROWS", "1536"))
 
 
@@ -494,11 +497,15 @@ class _MoELayer(torch.autograd.Function):
         if dy is None:
             dy = torch.zeros((T, d), dtype=torch.bfloat16, device=xb.device)
         dyb = dy.to(torch.bfloat16).contiguous()
-        dh, dW2, db2 = L.grouped_gemm_bwd_pair(dyb, w2b, offsets, G, rows, F, d, L.EPI_RELU_MASK, h, dyb, h,
-                                               out_dtype=odt, a_gather=tok, row_scale=gate, wx_gather=tok,
-                                               wx_scale=gate)
-        dxp, dW1, db1 = L.grouped_gemm_bwd_pair(dh, w1b, offsets, G, rows, d, F, L.EPI_NONE, None, dh, xb, tok,
-                                                out_dtype=odt)
+        if _FFN_BWD2:  # two launches: dH, then {dXp, dW2, dW1} in one grid
+            _, dxp, dW1, db1, dW2, db2 = L.expert_ffn_bwd(dyb, tok, gate, xb, h, w1b, w2b, offsets, G, rows,
+                                                          out_dtype=odt)
+        else:  # paired launches {dH, dW2}, {dXp, dW1} (A/B)
+            dh, dW2, db2 = L.grouped_gemm_bwd_pair(dyb, w2b, offsets, G, rows, F, d, L.EPI_RELU_MASK, h, dyb, h,
+                                                   out_dtype=odt, a_gather=tok, row_scale=gate, wx_gather=tok,
+                                                   wx_scale=gate)
+            dxp, dW1, db1 = L.grouped_gemm_bwd_pair(dh, w1b, offsets, G, rows, d, F, L.EPI_NONE, None, dh, xb, tok,
+                                                    out_dtype=odt)
         # aux-loss gradients as device tensors (no host sync): the router
         # partials' gradient is uniform over blocks (moe_route_dispatch wcoef)
         if weighted:

@@ -452,11 +452,71 @@ def train(a: TrainArgs) -> TrainResults:
 # ---------------------------------------------------------------------------
 # validation
 # ---------------------------------------------------------------------------
+class EvalForward:
+    """The inference forward of ``_evaluate`` (no_grad, bf16 autocast on the
+    GPU).  On the GPU each input shape is captured once as a hipGraph and
+    replayed (static input buffers refreshed by device copies; the outputs are
+    the graph's static tensors, valid until the next call) -- the eval forward
+    is ~400 kernel launches, which eager PyTorch issues slower than the GPU
+    runs them.  MOE_EVAL_GRAPHS=0 keeps it eager; at most ``max_shapes``
+    shapes are captured (later ones run eagerly)."""
+
+    def __init__(self, model: RTDETRMoE, max_shapes: int = 2):
+        self.model = model
+        self.graphs = {}
+        self.max_shapes = max_shapes
+        self.enabled = os.environ.get("MOE_EVAL_GRAPHS", "1") != "0"
+
+    def _run(self, images, ctx):
+        with torch.autocast(images.device.type, dtype=torch.bfloat16, enabled=images.is_cuda, cache_enabled=False):
+            return self.model(images, ctx)
+
+    @staticmethod
+    def _key(images, ctx):
+        return (tuple(images.shape), images.dtype, tuple(images.stride()), tuple(ctx.shape), ctx.dtype)
+
+    @torch.no_grad()
+    def prepare(self, images, ctx):
+        """Capture the graph for this input shape now (outside any timed span)."""
+        if images.is_cuda and self.enabled and self._key(images, ctx) not in self.graphs \
+                and len(self.graphs) < self.max_shapes:
+            self(images, ctx)
+
+    @torch.no_grad()
+    def __call__(self, images, ctx):
+        if not (images.is_cuda and self.enabled):
+            return self._run(images, ctx)
+        key = self._key(images, ctx)
+        ent = self.graphs.get(key)
+        if ent is None:
+            if len(self.graphs) >= self.max_shapes:
+                return self._run(images, ctx)
+            si, sc = images.clone(), ctx.clone()
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):  # warm-up: convolution search, lazy library state, allocator
+                for _ in range(2):
+                    self._run(si, sc)
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side):
+                out = self._run(si, sc)
+            torch.cuda.synchronize()
+            ent = self.graphs[key] = (g, si, sc, out)
+        g, si, sc, out = ent
+        si.copy_(images)
+        sc.copy_(ctx)
+        g.replay()
+        return out
+
+
 @torch.no_grad()
 def _evaluate(model: RTDETRMoE, data, split, imgsz, batch, device, workers, seed, speed: dict | None = None,
               ev_out: list | None = None):
     model.eval()
     on_gpu = device.type == "cuda"
+    fwd = EvalForward(model)
     ev = DetectionEvaluator()
     if ev_out is not None:
         ev_out.append(ev)
@@ -465,12 +525,16 @@ def _evaluate(model: RTDETRMoE, data, split, imgsz, batch, device, workers, seed
     for images, targets, ctx in _batches(data, split, imgsz, batch, workers, seed, 0, 1, 0):
         t0 = time.perf_counter()
         images = images.to(device, non_blocking=True)
+        ctx = ctx.to(device)
+        t_cap = 0.0
         if on_gpu:
             images = images.contiguous(memory_format=torch.channels_last)
+            tc = time.perf_counter()
+            fwd.prepare(images, ctx)  # first batch of a shape: graph capture, untimed
+            t_cap = time.perf_counter() - tc
             torch.cuda.synchronize()
         t1 = time.perf_counter()
-        with torch.autocast(device.type, dtype=torch.bfloat16, enabled=on_gpu):
-            out = model(images, ctx.to(device))
+        out = fwd(images, ctx)
         if on_gpu:
             torch.cuda.synchronize()
         t2 = time.perf_counter()
@@ -484,7 +548,7 @@ def _evaluate(model: RTDETRMoE, data, split, imgsz, batch, device, workers, seed
             ev.update(det["boxes"].float().cpu().numpy(), det["scores"].float().cpu().numpy(),
                       det["labels"].cpu().numpy(), gt_xyxy, t["labels"].numpy())
         t3 = time.perf_counter()
-        t_pre += t1 - t0
+        t_pre += t1 - t0 - t_cap
         t_inf += t2 - t1
         t_post += t3 - t2
         n_img += images.shape[0]

@@ -113,3 +113,27 @@ def test_scripts_train_then_eval_on_gpu(hip_lib, tmp_path, monkeypatch):
     assert (out / "metrics_table.csv").exists()
     em = json.loads((out / "run_metadata.json").read_text())
     assert em["split"] == "val" and em["cuda_available"] is True and em["model_family"] == "rtdetr"
+
+
+@pytest.mark.gpu
+def test_eval_forward_graph_matches_eager(hip_lib):
+    """engine.EvalForward (the inference forward of eval_rtdetr_detector,
+    replayed as a hipGraph per input shape) returns what the eager forward
+    returns, on two different batches through the same captured graph."""
+    from src.rtdetr_moe.data import SyntheticZOD
+    from src.rtdetr_moe.engine import EvalForward
+    from src.rtdetr_moe.model import RTDETRMoE
+
+    torch.manual_seed(0)
+    model = RTDETRMoE("rtdetr-r18-moe4-top2").cuda().to(memory_format=torch.channels_last).eval()
+    graphed, eager = EvalForward(model), EvalForward(model)
+    eager.enabled = False
+    for seed in (1, 2):
+        images, _, ctx = SyntheticZOD(batch=2, img_h=320, img_w=384, seed=seed).sample("cuda")
+        images = images.contiguous(memory_format=torch.channels_last)
+        ref = {k: v.clone() for k, v in eager(images, ctx).items() if torch.is_tensor(v)}
+        got = graphed(images, ctx)
+        torch.cuda.synchronize()
+        assert len(graphed.graphs) == 1
+        for k, v in ref.items():
+            torch.testing.assert_close(got[k].float(), v.float(), rtol=1e-3, atol=1e-3, msg=lambda m: f"{k}: {m}")

@@ -181,3 +181,50 @@ def test_scatter_outputs_match_gather_after(hip_lib, rows_per_group):
     torch.cuda.synchronize()
     assert torch.equal(hg[:R], h[:R])
     assert torch.equal(yg[idx], y2[:R])
+
+
+@pytest.mark.parametrize("rows_per_group", [[600] * 8, [1840] * 8, [1900, 300, 0, 650, 1, 64, 1200, 85],
+                                            [0, 0, 0, 5], [3000, 10, 10, 10, 10, 10, 10, 10]],
+                         ids=["dec", "enc", "skew", "sparse", "hot"])
+@pytest.mark.parametrize("out_bf16", [True, False])
+def test_expert_ffn_bwd_equals_paired_launches(hip_lib, rows_per_group, out_bf16):
+    """moe_expert_ffn_bwd (dH, then {dXp, dW2, dW1} in one grid) against the
+    two paired launches it replaces ({dH, dW2}, {dXp, dW1}): the same bodies
+    summing in the same order, so every output is bitwise equal -- at the C2
+    decoder / encoder shapes (the encoder's weight gradients split-K), skewed
+    and empty experts."""
+    from src.moe import _lib as L
+
+    g = torch.Generator().manual_seed(sum(rows_per_group) + len(rows_per_group))
+    G, d, F = len(rows_per_group), 256, 1024
+    offsets = torch.tensor(np.concatenate([[0], np.cumsum(rows_per_group)]).astype(np.int32), device=DEV)
+    R = int(offsets[-1])
+    T = max(R // 2, 1)
+    dy = (torch.randn(T, d, generator=g) * 0.05).to(torch.bfloat16).to(DEV)
+    x = torch.randn(T, d, generator=g).to(torch.bfloat16).to(DEV)
+    tok = torch.randint(0, T, (R,), generator=g, dtype=torch.int32).to(DEV)
+    gate = torch.rand(R, generator=g).to(DEV)
+    h = torch.relu(torch.randn(R, F, generator=g)).to(torch.bfloat16).to(DEV)
+    w1 = (torch.randn(G, F, d, generator=g) * 0.05).to(torch.bfloat16).to(DEV)
+    w2 = (torch.randn(G, d, F, generator=g) * 0.03).to(torch.bfloat16).to(DEV)
+    odt = torch.bfloat16 if out_bf16 else torch.float32
+    dh, dxp, dW1, db1, dW2, db2 = L.expert_ffn_bwd(dy, tok, gate, x, h, w1, w2, offsets, G, R, out_dtype=odt)
+    rdh, rdW2, rdb2 = L.grouped_gemm_bwd_pair(dy, w2, offsets, G, R, F, d, L.EPI_RELU_MASK, h, dy, h, out_dtype=odt,
+                                              a_gather=tok, row_scale=gate, wx_gather=tok, wx_scale=gate)
+    rdxp, rdW1, rdb1 = L.grouped_gemm_bwd_pair(rdh, w1, offsets, G, R, d, F, L.EPI_NONE, None, rdh, x, tok,
+                                               out_dtype=odt)
+    torch.cuda.synchronize()
+    assert torch.equal(dh[:R], rdh[:R])
+    assert torch.equal(dxp[:R], rdxp[:R])
+    for got, ref, n in ((dW1, rdW1, "dW1"), (db1, rdb1, "db1"), (dW2, rdW2, "dW2"), (db2, rdb2, "db2")):
+        assert torch.equal(got, ref), n
+    # and against fp32 torch: dYp = bf16(gate dy[tok]); dH = relu'(H) (dYp W2); dXp = dH W1
+    lo = offsets.cpu().tolist()
+    dyp = (gate[:, None] * dy[tok.long()].float()).to(torch.bfloat16).float()
+    for e in range(G):
+        a, b = lo[e], lo[e + 1]
+        if b <= a:
+            assert float(dW1[e].float().abs().max()) == 0.0 and float(dW2[e].float().abs().max()) == 0.0
+            continue
+        ref_w2 = dyp[a:b].t() @ h[a:b].float()
+        assert (dW2[e].float() - ref_w2).norm() <= 5e-3 * ref_w2.norm() + 1e-6
