@@ -662,7 +662,8 @@ def main():
                        "img": f"{args.img_w}x{args.img_h} (padded to {data.pad_w}x{data.pad_h})",
                        "parallelism": f"dp{world}" if "ep" not in spec else f"dp{world}+ep{world}",
                        "rccl_world": rccl_world, "batch": batch},
-            "build": {"libmoe_hip_sha16": build_id, "precision": args.precision, "graphs": bool(graphs)},
+            "build": {"libmoe_hip_sha16": build_id, "precision": args.precision, "graphs": bool(graphs),
+                      "tune": list(args.tune), "spec_extra": args.spec_extra},
             "roofline": roof, "roofline_dispatch": rd, "kernel_profile": kprof,
             "kernel_timing": None if not timing else (
                 f"libmoe_hip dispatch-stamped events over the {args.steps} timed steps" if not graphs else

@@ -118,6 +118,9 @@ static int g_wgrad_stages = 0;   // gathered WGRAD LDS-DMA ring depth: 0 = defau
 // step the routed counts are skewed (largest expert 2-3x the mean early on):
 // the heaviest group's K loop is the launch's tail.
 static int g_wgrad_split_hot = 0;
+// split-K factor of an under-filled forward GEMM (K-contiguous B, e.g. the
+// decoder's GEMM2: 150 tiles of K = 1,024); 0 = off (A/B)
+static int g_fwd_ksplit = 0;
 
 // split-K workspace registered per device by the caller (moe_set_splitk_workspace)
 struct SplitWs {
@@ -1501,6 +1504,7 @@ static int plan_rows(RowsPlan& pl, const void* a, const void* b, void* c, const 
   // (MN-contiguous B; kbench: decoder dX 15.0 -> 11.5 us with the map above;
   // the K-contiguous forward GEMM2 only loses to the merge latency)
   int want = g_ksplit ? g_ksplit : ((!trans_b && tiles < 256 && K / 64 >= 16) ? 2 : 1);
+  if (!g_ksplit && trans_b && g_fwd_ksplit > 1 && tiles < 256 && K / 64 >= 16) want = g_fwd_ksplit;
   if (want > K / 64) want = K / 64;
   const long long part = 256LL * (pl.bm / 32) * (128 / 32) * 4;
   const int S = pick_split(want, tiles, part, win);
@@ -1758,6 +1762,7 @@ extern "C" int moe_set_tuning(const char* key, int value) {
   if (k == "wgrad_dma" && value >= 0 && value <= 1) { g_wgrad_dma = value; return 0; }
   if (k == "wgrad_stages" && (value == 0 || value == 2 || value == 3)) { g_wgrad_stages = value; return 0; }
   if (k == "wgrad_split_hot" && value >= 0 && value <= 1024) { g_wgrad_split_hot = value; return 0; }
+  if (k == "fwd_ksplit" && value >= 0 && value <= 8) { g_fwd_ksplit = value; return 0; }
   if (k == "msda_generic" && value >= 0 && value <= 3) { g_msda_generic = value; return 0; }
   return fail("moe_set_tuning: unknown key or value");
 }

@@ -128,6 +128,9 @@ def kernels(c):
                                                        wx_gather=c["tok"], wx_scale=c["gate"]), 4.0 * A * F * d, 0),
         ("gemm_pair1", lambda: L.grouped_gemm_bwd_pair(c["dh"], c["w1"], c["offsets"], E, rows, d, F, L.EPI_NONE,
                                                        None, c["dh"], c["x"], c["tok"]), 4.0 * A * F * d, 0),
+        # the layer's backward since round 5: dH, then {dXp, dW2, dW1} in one grid (moe_expert_ffn_bwd)
+        ("ffn_bwd2", lambda: L.expert_ffn_bwd(c["dy"], c["tok"], c["gate"], c["x"], c["h"], c["w1"], c["w2"],
+                                              c["offsets"], E, rows), 8.0 * A * F * d, 0),
         ("route_dispatch", lambda: L.route_dispatch(c["bcnt"], c["idx"], c["lrank"], c["w"], c["auxp"], T, E, 0,
                                                     rows, 1e-2, 1e-3, row_gate=True), 0, 24 * A),
         ("moe_layer_fwd_bwd", lambda: layer_fwd_bwd(c), 6.0 * A * F * d, 0),
@@ -179,6 +182,9 @@ def main():
                                                 "register-staged; stages 0 auto, 2, 3)")
     ap.add_argument("--skew", type=float, default=0.0, help="expert preference added to the context bias")
     ap.add_argument("--cold", action="store_true", help="flush the Infinity Cache (512 MiB read) before every call")
+    ap.add_argument("--sweep", action="append", default=[],
+                    help="key=v1,v2,... moe_set_tuning values interleaved per round (one knob; repeat the flag "
+                         "for a cross product)")
     a = ap.parse_args()
     SKEW[0] = a.skew
     L.lib()
@@ -197,8 +203,16 @@ def main():
         shapes = {"enc": setup(16 * 920, 32, 4, 256, 1024), "dec": setup(16 * 300, 32, 4, 256, 1024, seed=1)}
     else:
         shapes = {"enc": setup(8 * 920, 8, 2, 256, 1024), "dec": setup(8 * 300, 8, 2, 256, 1024, seed=1)}
+    sweeps = [[]]
+    for sw in a.sweep:
+        key, vals = sw.split("=", 1)
+        sweeps = [prev + [(key, int(v))] for prev in sweeps for v in vals.split(",")]
     res = {}
     for _ in range(a.rounds):
+      for swv in sweeps:
+        for key, val in swv:
+            L.set_tuning(key, val)
+        tag = ",".join(f"{k}={v}" for k, v in swv)
         for (v, s, dbg, bm, xm, ks, pr, wg) in configs:
             wd, ws = (int(u) for u in wg.split(":"))
             L.set_tuning("wgrad_dma", wd)
@@ -219,8 +233,10 @@ def main():
                         continue
                     if pr != 1 and "pair" not in name:
                         continue
-                    res.setdefault((name, sname, v, s, dbg, bm, xm, ks, pr, wg, flops, byts), []).append(
+                    res.setdefault((name, sname, v, s, dbg, bm, xm, ks, pr, wg, flops, byts, tag), []).append(
                         timed(fn, a.reps))
+        for key, _ in swv:
+            L.set_tuning(key, 0)
     L.set_tuning("ksplit", 0)
     L.set_tuning("gemm_pair", 1)
     L.set_tuning("gemm_debug", 0)
@@ -229,9 +245,10 @@ def main():
     L.set_tuning("xcd_map", 0)
     L.set_tuning("wgrad_dma", 0)
     L.set_tuning("wgrad_stages", 0)
-    for (name, sname, v, s, dbg, bm, xm, ks, pr, wg, flops, byts), ts in res.items():
+    for (name, sname, v, s, dbg, bm, xm, ks, pr, wg, flops, byts, tag), ts in res.items():
         us = statistics.median(ts)
-        d = {"kernel": name, "config": a.config, "shape": sname, "variant": v, "stages": s, "debug": dbg, "bm": bm,
+        d = {"kernel": name, "config": a.config, "shape": sname, "sweep": tag, "variant": v, "stages": s, "debug": dbg,
+             "bm": bm,
              "xcd": xm, "ksplit": ks, "pair": pr, "wg": wg, "skew": a.skew, "cold": a.cold, "us": round(us, 2),
              "min_us": round(min(ts), 2)}
         if flops:
