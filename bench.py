@@ -398,6 +398,29 @@ def expert_parallel_stats(model, spec, world):
                     "bytes_per_a2a: this build's fixed-capacity buffer (its (W-1)/W leaves the rank)"}
 
 
+def dp_exchange_bytes(model, world):
+    """C3's gradient / weight exchange per rank per step for this
+    model's replicated parameters (expert-parallel shards excluded), as ZeRO-1
+    (optim.ShardedDPAdamW: fp32 reduce-scatter + bf16 / fp32 all-gather) and
+    as the flat fp32 all-reduce (MOE_ZERO=0), ring algorithm, at this run's
+    world size and at W = 8 (the driver's scaling run)."""
+    nb = sum(p.numel() for p in model.parameters()
+             if p.requires_grad and not getattr(p, "expert_parallel", False) and p.dtype == torch.bfloat16)
+    nf = sum(p.numel() for p in model.parameters()
+             if p.requires_grad and not getattr(p, "expert_parallel", False) and p.dtype != torch.bfloat16)
+
+    def at(w):
+        f = (w - 1) / w
+        return {"zero1_reduce_scatter": round(f * 4 * (nb + nf)), "zero1_all_gather": round(f * (2 * nb + 4 * nf)),
+                "zero1_total": round(f * (4 * (nb + nf) + 2 * nb + 4 * nf)),
+                "flat_all_reduce": round(2 * f * 4 * (nb + nf))}
+
+    return {"replicated_bf16_params": nb, "replicated_fp32_params": nf, "world": world, "bytes_per_rank": at(world),
+            "bytes_per_rank_at_w8": at(8),
+            "note": "ring collectives: each rank sends (W-1)/W of the buffer per reduce-scatter / all-gather, "
+                    "2 (W-1)/W per all-reduce; issued after the step graph's replay (not overlapped)"}
+
+
 def host_threads():
     """(threads used, CPUs in this process's affinity set): the affinity set,
     capped by OMP_NUM_THREADS when the box sets it (the GPU box exports the
@@ -670,6 +693,7 @@ def main():
                 f"libmoe_hip dispatch-stamped events over {args.profile_steps} eager steps right after the "
                 f"timed region (same shapes; the timed steps replay hipGraphs, which carry no timing events)"),
             **({"eval": ev} if ev else {}),
+            "dp_exchange": dp_exchange_bytes(model, world),
             **({"phases_gpu_host_ms": phases} if phases else {}),
             **({"expert_parallel": ep_stats} if ep_stats else {}),
         }

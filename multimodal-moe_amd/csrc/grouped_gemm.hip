@@ -121,6 +121,13 @@ static int g_wgrad_split_hot = 0;
 // split-K factor of an under-filled forward GEMM (K-contiguous B, e.g. the
 // decoder's GEMM2: 150 tiles of K = 1,024); 0 = off (A/B)
 static int g_fwd_ksplit = 0;
+// moe_expert_ffn_bwd: the largest mean rows per expert that take the two-launch
+// form (dH, then {dXp, dW2, dW1}); above it the two paired launches run (the
+// C2 encoder's 1,840 rows per expert: the one-grid form needs two rounds of
+// the chip, in-step 110 us vs 98 us paired; the decoder's 600: 49 vs 56 us)
+static int g_bwd2_max_rows = 1024;
+// split-K of the dXp body inside that grid: 0 = the per-shape choice, 1 = off
+static int g_bwd2_dx_split = 0;
 
 // split-K workspace registered per device by the caller (moe_set_splitk_workspace)
 struct SplitWs {
@@ -1763,6 +1770,8 @@ extern "C" int moe_set_tuning(const char* key, int value) {
   if (k == "wgrad_stages" && (value == 0 || value == 2 || value == 3)) { g_wgrad_stages = value; return 0; }
   if (k == "wgrad_split_hot" && value >= 0 && value <= 1024) { g_wgrad_split_hot = value; return 0; }
   if (k == "fwd_ksplit" && value >= 0 && value <= 8) { g_fwd_ksplit = value; return 0; }
+  if (k == "bwd2_max_rows" && value >= 0) { g_bwd2_max_rows = value; return 0; }
+  if (k == "bwd2_dx_split" && value >= 0 && value <= 1) { g_bwd2_dx_split = value; return 0; }
   if (k == "msda_generic" && value >= 0 && value <= 3) { g_msda_generic = value; return 0; }
   return fail("moe_set_tuning: unknown key or value");
 }
@@ -1982,7 +1991,9 @@ extern "C" int moe_expert_ffn_bwd(const void* dy, const int32_t* tok, const floa
       w2 == nullptr || dh == nullptr || dxp == nullptr || dw1 == nullptr || db1 == nullptr || dw2 == nullptr ||
       db2 == nullptr || offsets == nullptr)
     return fail("expert_ffn_bwd: NULL pointer");
-  if (max_rows <= 0 || g_gemm_pair_off) {  // (no rows: the paired path writes the zero weight gradients)
+  if (max_rows <= 0 || g_gemm_pair_off || (long long)max_rows > (long long)g_bwd2_max_rows * G) {
+    // paired launches: no rows (they write the zero weight gradients), the A/B
+    // switch, or experts long enough that the one-grid form needs two rounds
     if (moe_grouped_gemm_bwd_pair_scatter(dy, tok, gate, w2, dh, nullptr, offsets, G, max_rows, F, d,
                                           MOE_EPI_RELU_MASK, h, dy, tok, gate, h, nullptr, dw2, db2, d, F, out_bf16,
                                           stream))
@@ -2005,8 +2016,14 @@ extern "C" int moe_expert_ffn_bwd(const void* dy, const int32_t* tok, const floa
   win = device_ws();
   if (plan_wgrad(wg2, dy, h, dw2, db2, offsets, G, d, F, max_rows, out_bf16, nullptr, win, tok, gate)) return -1;
   if (plan_wgrad(wg1, dh, x, dw1, db1, offsets, G, F, d, max_rows, out_bf16, tok, win)) return -1;
-  if (plan_rows(r1, dh, w1, dxp, offsets, G, max_rows, d, F, 0, MOE_EPI_NONE, nullptr, nullptr, nullptr, win))
-    return -1;
+  {
+    const int ks_saved = g_ksplit;
+    if (g_bwd2_dx_split == 1) g_ksplit = 1;  // (plan-time override: the dXp body unsplit)
+    const int rc = plan_rows(r1, dh, w1, dxp, offsets, G, max_rows, d, F, 0, MOE_EPI_NONE, nullptr, nullptr, nullptr,
+                             win);
+    g_ksplit = ks_saved;
+    if (rc) return -1;
+  }
   if (!triple_ok(r1, wg2, wg1)) {  // separate launches (shapes the one-grid form does not take)
     {
       ProfScope prof(stream, PROF_GEMM, r1.bytes_fixed, true, r1.bytes_row, r1.flops_row);

@@ -26,7 +26,7 @@ GROUPS = [
     # the detector's MLP heads on the grouped GEMM (MOE_DENSE_LAYER: FL_DENSE = 16 in the template) are
     # not expert GEMMs -- matched first, kept out of the roofline group
     ("dense_gemm", re.compile(r"gemm_v\d_kernel<[^>]*, 16>")),
-    ("grouped_gemm", re.compile(r"gemm_v\d_kernel|gemm_pair_kernel|expert_ffn_fwd_kernel")),
+    ("grouped_gemm", re.compile(r"gemm_v\d_kernel|gemm_pair_kernel|gemm_triple_kernel|expert_ffn_fwd_kernel")),
     ("linear_wgrad", re.compile(r"linear_wgrad_kernel")),
     ("dispatch", re.compile(r"permute_fwd(_mx)?_kernel|combine_fwd_kernel|combine_bwd_kernel")),
     ("router", re.compile(r"router_topk_fwd_kernel")),
