@@ -477,6 +477,12 @@ int rtdetr_fold_scale_multi(const void* records, const int32_t* chunks, int n_ch
  * (rtdetr.py:82-94, upstream resnet-d variant). */
 int rtdetr_avgpool2x2_nhwc_fwd(const void* x, int B, int H, int W, int C, void* y, hipStream_t stream);
 int rtdetr_avgpool2x2_nhwc_bwd(const void* gy, int B, int H, int W, int C, void* gx, hipStream_t stream);
+/* the same, plus an addend of gx's shape: gx = (pool backward) + add (add may
+ * be NULL).  The backbone's stage outputs: the encoder's gradient of a stage
+ * output joins the ResNet-D shortcut's gradient here, before branch2a's dgrad
+ * epilogue adds both and applies the ReLU mask (GradLink, backbone.stage_taps). */
+int rtdetr_avgpool2x2_nhwc_bwd_add(const void* gy, const void* add, int B, int H, int W, int C, void* gx,
+                                   hipStream_t stream);
 /* The stem's MaxPool2d(3, 2, 1) forward over channels_last bf16 (the stem is
  * frozen: no backward): y [B, (H-1)/2+1, (W-1)/2+1, C], C % 8 == 0, x and y
  * 16-B aligned; padding never wins, NaN propagates.  Replaces nn.MaxPool2d in
@@ -579,6 +585,20 @@ int rtdetr_bn_act_fwd_part(const void* const* x, const float* const* gamma, cons
                            float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act,
                            float eps, float momentum, const float* part, int part_blocks, float* saved, void* y,
                            hipStream_t stream);
+/* The same with y (forward) / dy (backward) a batch-strided slice of a wider
+ * row-major tensor: row r of the [M, C] layout is row (r / hw) * bstride +
+ * r % hw of y / dy (hw = 0: contiguous).  The decoder's memory [B, S, C]:
+ * level l's BatchNorm output written straight into its rows (y = memory +
+ * start_l C, hw = h_l w_l, bstride = S) and its gradient read from d memory
+ * in place -- no concatenation forward, no strided copy backward.  fwd_rows:
+ * part (conv-epilogue statistics, ws unused) or ws (a statistics pass). */
+int rtdetr_bn_act_fwd_rows(const void* const* x, const float* const* gamma, const float* const* beta,
+                           float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act,
+                           float eps, float momentum, const float* part, int part_blocks, float* ws, float* saved,
+                           void* y, long long y_hw, long long y_bstride, hipStream_t stream);
+int rtdetr_bn_act_bwd_rows(const void* dy, long long dy_hw, long long dy_bstride, const void* const* x,
+                           const float* const* gamma, int nb, long long M, int C, int act, const float* saved,
+                           float* ws, float* coef, void* const* dx, float* dgb, hipStream_t stream);
 
 /* Process-wide tuning overrides (not thread-safe; set before launching).  By
  * default (0) every launch picks its own kernel variant, ring depth and tile

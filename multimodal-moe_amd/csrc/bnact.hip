@@ -28,7 +28,16 @@ struct BnArgs {
   float* run_mean[2];
   float* run_var[2];
   int nb;  // branches: 1 or 2
+  // row map of y (forward) / dy (backward): row r of the [M, C] layout lives
+  // at row (r / rhw) * rbs + r % rhw -- a batch-strided slice of a wider
+  // tensor (the decoder's memory [B, S, C], one level's rows per image);
+  // rhw == 0: contiguous (row r at row r)
+  long long rhw, rbs;
 };
+
+__device__ __forceinline__ long long map_row(const BnArgs& a, long long r) {
+  return a.rhw ? (r / a.rhw) * a.rbs + r % a.rhw : r;
+}
 
 constexpr int BN_MAX_BLOCKS = 2048;  // partial rows a finalize reduces (the convolution-epilogue statistics: one per M tile)
 constexpr int BN_BLOCKS = 1024;      // partial-sum blocks of bn_stats / bn_bwd_reduce (4 per CU)
@@ -183,14 +192,14 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(BnArgs a, const float* __
                                                        int C, uint4* __restrict__ y) {
   const int cch = C >> 3;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nchunk; i += (long long)gridDim.x * 256) {
-    const int c0 = (int)(i % cch) * 8;
+    const int cc = (int)(i % cch), c0 = cc * 8;
     float z[8], xs[NB][8];
     bn_z<NB>(a, saved, C, i, c0, z, xs);
     if constexpr (ACT == 1) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) z[j] = z[j] * sigmoidf_(z[j]);
     }
-    y[i] = pack8(z);
+    y[a.rhw ? map_row(a, i / cch) * cch + cc : i] = pack8(z);
   }
 }
 
@@ -211,11 +220,11 @@ __device__ __forceinline__ void bn_grad_in(const uint4* __restrict__ dy, long lo
 // finalize: sum g xhat = invstd (sum g x - mean sum g))
 template <int ACT, int NB>
 __device__ __forceinline__ void bn_bwd_row(const BnArgs& a, const uint4* __restrict__ dy,
-                                           const float* __restrict__ saved, int C, long long i, int c0, float* sg,
-                                           float (*sgx)[8]) {
+                                           const float* __restrict__ saved, int C, long long i, long long idy, int c0,
+                                           float* sg, float (*sgx)[8]) {
   float z[8], xs[NB][8], gv[8];
   bn_z<NB>(a, saved, C, i, c0, z, xs);
-  bn_grad_in<ACT>(dy, i, z, gv);
+  bn_grad_in<ACT>(dy, idy, z, gv);
 #pragma unroll
   for (int j = 0; j < 8; ++j) sg[j] += gv[j];
 #pragma unroll
@@ -242,10 +251,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a, const uint
   }
   long long r = r0 + g;
   for (; r + groups < r1; r += 2 * groups) {
-    bn_bwd_row<ACT, NB>(a, dy, saved, C, r * cch + cc, c0, sg, sgx);
-    bn_bwd_row<ACT, NB>(a, dy, saved, C, (r + groups) * cch + cc, c0, sg, sgx);
+    bn_bwd_row<ACT, NB>(a, dy, saved, C, r * cch + cc, map_row(a, r) * cch + cc, c0, sg, sgx);
+    bn_bwd_row<ACT, NB>(a, dy, saved, C, (r + groups) * cch + cc, map_row(a, r + groups) * cch + cc, c0, sg, sgx);
   }
-  if (r < r1) bn_bwd_row<ACT, NB>(a, dy, saved, C, r * cch + cc, c0, sg, sgx);
+  if (r < r1) bn_bwd_row<ACT, NB>(a, dy, saved, C, r * cch + cc, map_row(a, r) * cch + cc, c0, sg, sgx);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sm[g * C + c0 + j] = sg[j];
@@ -299,10 +308,10 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(BnArgs a, const uint4* _
                                                         uint4* __restrict__ dx0, uint4* __restrict__ dx1) {
   const int cch = C >> 3;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nchunk; i += (long long)gridDim.x * 256) {
-    const int c0 = (int)(i % cch) * 8;
+    const int cc = (int)(i % cch), c0 = cc * 8;
     float z[8], xs[NB][8], gv[8];
     bn_z<NB>(a, saved, C, i, c0, z, xs);
-    bn_grad_in<ACT>(dy, i, z, gv);
+    bn_grad_in<ACT>(dy, a.rhw ? map_row(a, i / cch) * cch + cc : i, z, gv);
 #pragma unroll
     for (int br = 0; br < NB; ++br) {
       float A[8], B[8], D[8], o[8];
@@ -348,16 +357,25 @@ extern "C" size_t rtdetr_bn_act_workspace(long long M, int C, int nb) {
   return (size_t)BN_BLOCKS * 3 * C * (nb > 1 ? 2 : 1) * sizeof(float);
 }
 
+static int bn_rows_check(long long M, long long hw, long long bs) {
+  if (hw == 0) return 0;
+  if (hw < 0 || bs < hw || M % hw) return fail("bn_act rows: need 0 < hw <= bstride and M a multiple of hw");
+  return 0;
+}
+
 static int bn_act_fwd_impl(const void* const* x, const float* const* gamma, const float* const* beta,
                            float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act,
                            float eps, float momentum, float* saved, float* ws, const float* part, int part_blocks,
-                           void* y, hipStream_t stream) {
+                           void* y, long long y_hw, long long y_bstride, hipStream_t stream) {
   if (int rc = bn_check(nb, M, C, act)) return rc;
+  if (int rc = bn_rows_check(M, y_hw, y_bstride)) return rc;
   if (!x || !gamma || !beta || !saved || !y || (!ws && !part)) return fail("bn_act_fwd: NULL argument");
   if (part != nullptr && (part_blocks < 1 || part_blocks > BN_MAX_BLOCKS))
     return fail("bn_act_fwd_part: need 1 <= part_blocks <= 2048");
   BnArgs a{};
   a.nb = nb;
+  a.rhw = y_hw;
+  a.rbs = y_bstride;
   for (int i = 0; i < nb; ++i) {
     if (!x[i] || !gamma[i] || !beta[i]) return fail("bn_act_fwd: NULL branch pointer");
     a.x[i] = static_cast<const uint4*>(x[i]);
@@ -397,7 +415,7 @@ extern "C" int rtdetr_bn_act_fwd(const void* const* x, const float* const* gamma
                                  float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act,
                                  float eps, float momentum, float* saved, float* ws, void* y, hipStream_t stream) {
   return bn_act_fwd_impl(x, gamma, beta, run_mean, run_var, nb, M, C, act, eps, momentum, saved, ws, nullptr, 0, y,
-                         stream);
+                         0, 0, stream);
 }
 
 extern "C" int rtdetr_bn_act_fwd_part(const void* const* x, const float* const* gamma, const float* const* beta,
@@ -406,16 +424,29 @@ extern "C" int rtdetr_bn_act_fwd_part(const void* const* x, const float* const* 
                                       float* saved, void* y, hipStream_t stream) {
   if (part == nullptr) return fail("bn_act_fwd_part: part is NULL");
   return bn_act_fwd_impl(x, gamma, beta, run_mean, run_var, nb, M, C, act, eps, momentum, saved, nullptr, part,
-                         part_blocks, y, stream);
+                         part_blocks, y, 0, 0, stream);
 }
 
-extern "C" int rtdetr_bn_act_bwd(const void* dy, const void* const* x, const float* const* gamma, int nb,
-                                 long long M, int C, int act, const float* saved, float* ws, float* coef,
-                                 void* const* dx, float* dgb, hipStream_t stream) {
+extern "C" int rtdetr_bn_act_fwd_rows(const void* const* x, const float* const* gamma, const float* const* beta,
+                                      float* const* run_mean, float* const* run_var, int nb, long long M, int C,
+                                      int act, float eps, float momentum, const float* part, int part_blocks,
+                                      float* ws, float* saved, void* y, long long y_hw, long long y_bstride,
+                                      hipStream_t stream) {
+  return bn_act_fwd_impl(x, gamma, beta, run_mean, run_var, nb, M, C, act, eps, momentum, saved,
+                         part ? nullptr : ws, part, part_blocks, y, y_hw, y_bstride, stream);
+}
+
+extern "C" int rtdetr_bn_act_bwd_rows(const void* dy, long long dy_hw, long long dy_bstride, const void* const* x,
+                                      const float* const* gamma, int nb, long long M, int C, int act,
+                                      const float* saved, float* ws, float* coef, void* const* dx, float* dgb,
+                                      hipStream_t stream) {
   if (int rc = bn_check(nb, M, C, act)) return rc;
+  if (int rc = bn_rows_check(M, dy_hw, dy_bstride)) return rc;
   if (!dy || !x || !gamma || !saved || !ws || !coef || !dx || !dgb) return fail("bn_act_bwd: NULL argument");
   BnArgs a{};
   a.nb = nb;
+  a.rhw = dy_hw;
+  a.rbs = dy_bstride;
   for (int i = 0; i < nb; ++i) {
     if (!x[i] || !dx[i]) return fail("bn_act_bwd: NULL branch pointer");
     a.x[i] = static_cast<const uint4*>(x[i]);
@@ -458,4 +489,10 @@ extern "C" int rtdetr_bn_act_bwd(const void* dy, const void* const* x, const flo
 #undef BN_DX
   }
   return check_launch("rtdetr_bn_act_bwd");
+}
+
+extern "C" int rtdetr_bn_act_bwd(const void* dy, const void* const* x, const float* const* gamma, int nb,
+                                 long long M, int C, int act, const float* saved, float* ws, float* coef,
+                                 void* const* dx, float* dgb, hipStream_t stream) {
+  return rtdetr_bn_act_bwd_rows(dy, 0, 0, x, gamma, nb, M, C, act, saved, ws, coef, dx, dgb, stream);
 }

@@ -35,7 +35,8 @@ __global__ __launch_bounds__(256) void avgpool2x2_fwd_kernel(const uint16_t* __r
   reinterpret_cast<uint4*>(y)[i] = pack8(o);
 }
 
-__global__ __launch_bounds__(256) void avgpool2x2_bwd_kernel(const uint16_t* __restrict__ gy, int H, int W, int C8,
+__global__ __launch_bounds__(256) void avgpool2x2_bwd_kernel(const uint16_t* __restrict__ gy,
+                                                             const uint16_t* __restrict__ add, int H, int W, int C8,
                                                              long long n, uint16_t* __restrict__ gx) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
@@ -50,14 +51,32 @@ __global__ __launch_bounds__(256) void avgpool2x2_bwd_kernel(const uint16_t* __r
   unpack8(reinterpret_cast<const uint4*>(gy)[i], v);
 #pragma unroll
   for (int k = 0; k < 8; ++k) v[k] *= 0.25f;
-  const uint4 q = pack8(v);
   uint4* xr = reinterpret_cast<uint4*>(gx);
   const long long row0 = ((b * H + 2 * oh) * W + 2 * ow) * C8 + cv;
   const long long row1 = row0 + (long long)W * C8;
-  xr[row0] = q;
-  xr[row0 + C8] = q;
-  xr[row1] = q;
-  xr[row1 + C8] = q;
+  if (add == nullptr) {
+    const uint4 q = pack8(v);
+    xr[row0] = q;
+    xr[row0 + C8] = q;
+    xr[row1] = q;
+    xr[row1 + C8] = q;
+    return;
+  }
+  // gx = (gy / 4 upsampled) + add: the quarter rounded to bf16 first, as the
+  // separate pool backward + add would, then the fp32 sum rounded once
+  const uint4 q = pack8(v);
+  float qv[8];
+  unpack8(q, qv);
+  const uint4* ar = reinterpret_cast<const uint4*>(add);
+  const long long rows[4] = {row0, row0 + C8, row1, row1 + C8};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float a[8];
+    unpack8(ar[rows[r]], a);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] += qv[k];
+    xr[rows[r]] = pack8(a);
+  }
 }
 
 // Stem max pool (MaxPool2d(3, 2, 1), forward only: the stem is frozen, so
@@ -243,12 +262,19 @@ extern "C" int rtdetr_avgpool2x2_nhwc_fwd(const void* x, int B, int H, int W, in
   return check_launch("rtdetr_avgpool2x2_nhwc_fwd");
 }
 
-extern "C" int rtdetr_avgpool2x2_nhwc_bwd(const void* gy, int B, int H, int W, int C, void* gx, hipStream_t stream) {
-  if (!pool_args_ok(gy, gx, B, H, W, C)) return fail("avgpool2x2_bwd: need even H, W, C % 8 == 0, 16-B aligned");
+extern "C" int rtdetr_avgpool2x2_nhwc_bwd_add(const void* gy, const void* add, int B, int H, int W, int C, void* gx,
+                                              hipStream_t stream) {
+  if (!pool_args_ok(gy, gx, B, H, W, C) || reinterpret_cast<uintptr_t>(add) % 16)
+    return fail("avgpool2x2_bwd: need even H, W, C % 8 == 0, 16-B aligned");
   const long long n = (long long)B * (H / 2) * (W / 2) * (C / 8);
   if (n == 0) return 0;
-  ProfScope prof(stream, PROF_CONV_EPI, 2.0 * B * H * W * C * 1.25);
+  ProfScope prof(stream, PROF_CONV_EPI, 2.0 * B * H * W * C * (add ? 2.25 : 1.25));
   MOE_LAUNCH(prof, avgpool2x2_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-             static_cast<const uint16_t*>(gy), H, W, C / 8, n, static_cast<uint16_t*>(gx));
+             static_cast<const uint16_t*>(gy), static_cast<const uint16_t*>(add), H, W, C / 8, n,
+             static_cast<uint16_t*>(gx));
   return check_launch("rtdetr_avgpool2x2_nhwc_bwd");
+}
+
+extern "C" int rtdetr_avgpool2x2_nhwc_bwd(const void* gy, int B, int H, int W, int C, void* gx, hipStream_t stream) {
+  return rtdetr_avgpool2x2_nhwc_bwd_add(gy, nullptr, B, H, W, C, gx, stream);
 }

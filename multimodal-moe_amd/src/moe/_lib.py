@@ -73,6 +73,7 @@ SIGNATURES = {
     "rtdetr_bn_act_bwd": (_I, [_P, _P, _P, _I, ctypes.c_longlong, _I, _I, _P, _P, _P, _P, _P, _P]),
     "rtdetr_avgpool2x2_nhwc_fwd": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "rtdetr_avgpool2x2_nhwc_bwd": (_I, [_P, _I, _I, _I, _I, _P, _P]),
+    "rtdetr_avgpool2x2_nhwc_bwd_add": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "rtdetr_maxpool3x3s2_nhwc_fwd": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "rtdetr_upcat_nhwc_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_upcat_nhwc_bwd": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
@@ -113,6 +114,10 @@ SIGNATURES = {
     "rtdetr_conv_fwd_stats_rows": (_I, [_I, _I, _I, _I, _I, _I, _I]),
     "rtdetr_conv_fwd_stats": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_bn_act_fwd_part": (_I, [_P, _P, _P, _P, _P, _I, ctypes.c_longlong, _I, _I, _F, _F, _P, _I, _P, _P, _P]),
+    "rtdetr_bn_act_fwd_rows": (_I, [_P, _P, _P, _P, _P, _I, ctypes.c_longlong, _I, _I, _F, _F, _P, _I, _P, _P, _P,
+                                    ctypes.c_longlong, ctypes.c_longlong, _P]),
+    "rtdetr_bn_act_bwd_rows": (_I, [_P, ctypes.c_longlong, ctypes.c_longlong, _P, _P, _I, ctypes.c_longlong, _I, _I,
+                                    _P, _P, _P, _P, _P, _P]),
     "rtdetr_conv_dgrad_workspace": (_LL, [_I, _I, _I, _I, _I, _I]),
     "rtdetr_conv_dgrad": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "rtdetr_conv_dgrad_preflipped": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
@@ -1030,6 +1035,56 @@ def bn_act_bwd(dy, xs, gammas, saved, act):
     _check(lib().rtdetr_bn_act_bwd(_ptr(dy), px, pg, nb, M, C, int(act), _ptr(saved), _ptr(ws), _ptr(coef), pd,
                                    _ptr(dgb), _stream()), "rtdetr_bn_act_bwd")
     return dxs, dgb
+
+
+def bn_act_fwd_rows(x, gamma, beta, run_mean, run_var, act, eps, momentum, part, y, row0, hw, bstride):
+    """One-branch bn_act_fwd whose output goes to rows of a wider tensor: y
+    bf16 [B', S, C] contiguous, x's row r (image r // hw, pixel r % hw) to y's
+    flat row (r // hw) * bstride + row0 + r % hw.  part: conv-epilogue
+    statistics fp32 [1, nblk, 2, C] or None (a statistics pass).  -> saved."""
+    M, C = _nhwc_rows(x, "x")
+    _need(y, torch.bfloat16, "y")
+    if not y.is_contiguous() or y.shape[-1] != C or M % hw or (M // hw - 1) * bstride + row0 + hw > y.numel() // C:
+        raise MoEKernelError("bn_act_fwd_rows: y layout")
+    for t in [gamma, beta] + [r for r in (run_mean, run_var) if r is not None]:
+        _need(t, torch.float32, "bn affine/statistics")
+    saved = torch.empty((1, 4, C), dtype=torch.float32, device=x.device)
+    ws = None if part is not None else _bn_ws(M, C, 1, x.device)
+    if part is not None:
+        _need(part, torch.float32, "part")
+        if part.dim() != 4 or part.shape[0] != 1 or part.shape[2] != 2 or part.shape[3] != C:
+            raise MoEKernelError("bn_act_fwd_rows: part must be [1, nblk, 2, C]")
+    px, kx = _ptrs([x])
+    pg, kg = _ptrs([gamma])
+    pb, kb = _ptrs([beta])
+    has_run = run_mean is not None and run_var is not None
+    pm, km = _ptrs([run_mean]) if has_run else (None, None)
+    pv, kv = _ptrs([run_var]) if has_run else (None, None)
+    _check(lib().rtdetr_bn_act_fwd_rows(px, pg, pb, pm, pv, 1, M, C, int(act), float(eps), float(momentum),
+                                        _ptr(part), int(part.shape[1]) if part is not None else 0, _ptr(ws),
+                                        _ptr(saved), y.data_ptr() + row0 * C * 2, hw, bstride, _stream()),
+           "rtdetr_bn_act_fwd_rows")
+    return saved
+
+
+def bn_act_bwd_rows(dy, row0, hw, bstride, x, gamma, saved, act):
+    """One-branch bn_act_bwd reading dy from rows of a wider tensor (the
+    layout of bn_act_fwd_rows).  -> (dx bf16 like x, dgb fp32 [1, 2, C])."""
+    M, C = _nhwc_rows(x, "x")
+    _need(dy, torch.bfloat16, "dy")
+    if not dy.is_contiguous() or dy.shape[-1] != C or M % hw or (M // hw - 1) * bstride + row0 + hw > dy.numel() // C:
+        raise MoEKernelError("bn_act_bwd_rows: dy layout")
+    dx = torch.empty_like(x)
+    coef = torch.empty((1, 3, C), dtype=torch.float32, device=x.device)
+    dgb = torch.empty((1, 2, C), dtype=torch.float32, device=x.device)
+    ws = _bn_ws(M, C, 1, x.device)
+    px, kx = _ptrs([x])
+    pg, kg = _ptrs([gamma])
+    pd, kd = _ptrs([dx])
+    _check(lib().rtdetr_bn_act_bwd_rows(dy.data_ptr() + row0 * C * 2, hw, bstride, px, pg, 1, M, C, int(act),
+                                        _ptr(saved), _ptr(ws), _ptr(coef), pd, _ptr(dgb), _stream()),
+           "rtdetr_bn_act_bwd_rows")
+    return dx, dgb
 
 
 def msda_fwd(value, shapes, starts, loc, attn):

@@ -254,11 +254,77 @@ class _AvgPool2x2(torch.autograd.Function):
         if gy.data_ptr() % 16:
             gy = gy.clone(memory_format=torch.channels_last)
         gx = torch.empty((B, C, H, W), dtype=gy.dtype, device=gy.device, memory_format=torch.channels_last)
-        L._check(L.lib().rtdetr_avgpool2x2_nhwc_bwd(gy.data_ptr(), B, H, W, C, gx.data_ptr(), L._stream()),
+        link = ctx.link
+        ext = None
+        if link is not None and link.g_ext is not None and not link.ext_used and _ext_ok(link.g_ext, gx):
+            ext = link.g_ext  # the encoder's gradient of this stage output (stage_taps), added in the same pass
+            link.ext_used = True
+        L._check(L.lib().rtdetr_avgpool2x2_nhwc_bwd_add(gy.data_ptr(), None if ext is None else ext.data_ptr(),
+                                                         B, H, W, C, gx.data_ptr(), L._stream()),
                  "rtdetr_avgpool2x2_nhwc_bwd")
-        if ctx.link is not None:  # handed to branch2a's dgrad epilogue (which autograd runs after this)
-            ctx.link.g_short = gx
+        if link is not None:  # handed to branch2a's dgrad epilogue (which autograd runs after this)
+            link.g_short = gx
         return gx, None
+
+
+def _ext_ok(ext, like):
+    return (ext.dtype == like.dtype and ext.shape == like.shape and ext.data_ptr() % 16 == 0
+            and ext.is_contiguous(memory_format=torch.channels_last))
+
+
+class _StageTap(torch.autograd.Function):
+    """Identity on a returned stage output (C3 / C4 / C5) for its external
+    consumer (the encoder).  The output's other consumer, the next stage's
+    first block, finishes its gradient through a GradLink (branch2a's dgrad
+    epilogue adds the shortcut gradient and applies the ReLU mask); the
+    external gradient must be masked too.  Backward: the gradient is parked on
+    the link (no gradient returned, so autograd issues no accumulation add);
+    the shortcut's average-pool backward adds it in the same pass, or the
+    producing fork adds it (rtdetr_relu_grad2 / a masked add) when the link
+    path does not run.  Autograd runs this right after the consumer's own
+    backward (a node created after the whole backbone), before any node of
+    the next stage -- when the consumer taps again (HybridEncoder.forward);
+    PResNet's own tap on its outputs runs just before the producing fork."""
+
+    @staticmethod
+    def forward(ctx, x, link):
+        ctx.link = link
+        ctx.set_materialize_grads(False)
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is not None:
+            g = g.contiguous(memory_format=torch.channels_last)
+            if g.data_ptr() % 16:
+                g = g.clone(memory_format=torch.channels_last)
+            link = ctx.link
+            link.g_ext = g if link.g_ext is None else link.g_ext + g
+            link.ext_used = False
+        return None, None
+
+
+# MOE_STAGE_TAP=0: no taps (A/B: the round-4 behaviour, where an external
+# consumer's gradient of C3 / C4 was summed by autograd and, on the GradLink
+# path, never masked -- tests/test_gpu_backbone.py::test_stage_outputs_with_external_consumer)
+_STAGE_TAP = os.environ.get("MOE_STAGE_TAP", "1") != "0"
+
+
+def stage_taps(feats):
+    """The backbone outputs as the encoder should consume them: a block output
+    that carries a GradLink goes through _StageTap (gradient handed over on the
+    link); anything else as is."""
+    if not (_STAGE_TAP and torch.is_grad_enabled()):
+        return list(feats)
+    out = []
+    for f in feats:
+        link = getattr(f, "grad_link", None)
+        if link is not None and f.requires_grad:
+            t = _StageTap.apply(f, link)
+            t.grad_link = link  # (a consumer may tap again: the later tap hands over first)
+            f = t
+        out.append(f)
+    return out
 
 
 def stem_max_pool(x, pool: nn.MaxPool2d):
@@ -492,7 +558,10 @@ class PResNet(nn.Module):
                 x, xs = blk(x, xs)
             if i in self.return_idx:
                 outs.append(x)
-        return outs
+        # returned outputs whose gradient the next stage finishes through a
+        # GradLink: any external consumer's gradient reaches the link (masked
+        # there), never an unmasked autograd sum (stage_taps)
+        return stage_taps(outs)
 
 
 @torch.no_grad()

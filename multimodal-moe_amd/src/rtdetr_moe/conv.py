@@ -231,11 +231,17 @@ class GradLink:
     it, adds g_s and applies the mask in its dgrad epilogue and marks the
     result final; y's fork then takes it as is (no rtdetr_relu_grad2 pass)."""
 
-    __slots__ = ("g_short", "final")
+    __slots__ = ("g_short", "final", "g_ext", "ext_used")
 
     def __init__(self):
         self.g_short = None
         self.final = False
+        # a returned stage output's gradient from its external consumer (the
+        # encoder), handed over by backbone.stage_taps instead of autograd's
+        # accumulation; ext_used: the average-pool backward folded it into the
+        # shortcut gradient (so branch2a's dgrad epilogue adds and masks it)
+        self.g_ext = None
+        self.ext_used = False
 
 
 class _ConvHIP(torch.autograd.Function):
@@ -284,6 +290,7 @@ class _ConvHIPFork(torch.autograd.Function):
         x = _nhwc(x)
         w = _nhwc(w)
         y = _fwd(x, w, bias, _nhwc(resid), True)
+        ctx.set_materialize_grads(False)  # an unused handle: no zero-filled gradient
         ctx.mask_input = bool(mask_input)
         ctx.links = (link_in, link_out)  # link_in: resid is the previous block's output (identity shortcut)
         ctx.save_for_backward(x, w, y)
@@ -295,12 +302,21 @@ class _ConvHIPFork(torch.autograd.Function):
 
         x, w, y = ctx.saved_tensors
         link_in, link_out = ctx.links
+        ext = None  # the encoder's gradient of this output (stage_taps), unless already folded in
+        if link_out is not None:
+            if link_out.g_ext is not None and not link_out.ext_used:
+                ext = link_out.g_ext
+            link_out.g_ext, link_out.ext_used = None, False
         if link_out is not None and link_out.final:
             g = dy1  # the next block's branch2a dgrad already added dy2 and masked (GradLink)
             link_out.final = False
+            if ext is not None:  # (not folded in by the shortcut's pool backward: masked here)
+                g = g + torch.where(y > 0, ext, torch.zeros_like(ext))
         else:
             if link_out is not None:
                 link_out.g_short = None
+            if ext is not None:
+                dy1 = ext if dy1 is None else dy1 + ext
             if dy1 is None and dy2 is None:
                 return None, None, None, None, None, None, None
             if dy1 is None:

@@ -17,6 +17,9 @@ from .linear import TokenLinear, TokenSelfAttention, _MLPHip, bias_grad, chunked
 from ..moe.config import MoEConfig
 from .encoder import HybridEncoder, make_ffn
 from .norm import AddLayerNorm
+from .backbone import _FUSED_BN
+from .conv import conv_module_stats
+from .fused import bn_act_ok
 
 
 def inverse_sigmoid(x, eps=1e-5):
@@ -166,6 +169,54 @@ class _MSDAFusedHip(torch.autograd.Function):
         return gv, None, None, go, None, gl, None, None, None
 
 
+class _LevelMemory(torch.autograd.Function):
+    """The decoder's memory [B, S, d]: the input projections' training
+    BatchNorms (act none) of the n levels, each written straight into its rows
+    of memory (rtdetr_bn_act_fwd_rows: image b, level l at rows
+    [b S + start_l, b S + start_l + h_l w_l)), instead of n BatchNorm outputs
+    concatenated (a copy of all of memory) whose backward hands every level a
+    strided slice of d memory to copy back to channels_last.  Backward reads
+    each level's rows of d memory in place (rtdetr_bn_act_bwd_rows).  Inputs:
+    the conv outputs y_l (channels_last bf16), their conv-epilogue statistics
+    partials (or None), then gammas and betas."""
+
+    @staticmethod
+    def forward(ctx, bns, parts, *args):
+        from ..moe import _lib as L
+
+        n = len(bns)
+        ys, gammas, betas = args[:n], args[n:2 * n], args[2 * n:3 * n]
+        B, C = ys[0].shape[:2]
+        hws = [int(y.shape[2] * y.shape[3]) for y in ys]
+        S = sum(hws)
+        mem = torch.empty((B, S, C), dtype=torch.bfloat16, device=ys[0].device)
+        saved, row0 = [], 0
+        for y, g, b, bn, part, hw in zip(ys, gammas, betas, bns, parts, hws):
+            saved.append(L.bn_act_fwd_rows(y, g, b, bn.running_mean, bn.running_var, 0, bn.eps, bn.momentum, part,
+                                           mem, row0, hw, S))
+            row0 += hw
+        ctx.save_for_backward(*ys, *gammas, *saved)
+        ctx.meta = (n, hws, S)
+        return mem
+
+    @staticmethod
+    def backward(ctx, dmem):
+        from ..moe import _lib as L
+
+        n, hws, S = ctx.meta
+        t = ctx.saved_tensors
+        ys, gammas, saved = t[:n], t[n:2 * n], t[2 * n:]
+        dmem = dmem.contiguous()
+        dxs, dgs, dbs, row0 = [], [], [], 0
+        for y, g, sv, hw in zip(ys, gammas, saved, hws):
+            dx, dgb = L.bn_act_bwd_rows(dmem, row0, hw, S, y, g, sv, 0)
+            dxs.append(dx)
+            dgs.append(dgb[0, 0])
+            dbs.append(dgb[0, 1])
+            row0 += hw
+        return (None, None, *dxs, *dgs, *dbs)
+
+
 class _ValueProjAll(torch.autograd.Function):
     """The decoder layers' value projections over the encoder memory as ONE
     GEMM, [B*S, d] x [d, n d] with the n layers' weights concatenated per call
@@ -176,10 +227,14 @@ class _ValueProjAll(torch.autograd.Function):
     `token` every layer takes as an input (its zero gradient makes autograd run
     this backward after all of them).  Backward: d memory = G W (one GEMM, no
     per-layer gradient adds), dW = G^T memory (one row-chunked GEMM), db = the
-    column sums of G, split back per layer."""
+    column sums of G, split back per layer.
+    Also returns the query selection's rows, sel = memory[b, topk[b, q]] *
+    vsel[b, q] (the encoder-output heads' input): its gradient is added into
+    the rows of d memory in place (one scatter-add over the B Q selected rows)
+    instead of autograd's zero-filled [B, S, d] scatter and full-size add."""
 
     @staticmethod
-    def forward(ctx, memory, dtype, det, *wb):
+    def forward(ctx, memory, dtype, det, topk, vsel, *wb):
         n = len(wb) // 2
         ws, bs = wb[0::2], wb[1::2]
         B, S, d = memory.shape
@@ -192,26 +247,30 @@ class _ValueProjAll(torch.autograd.Function):
         # atomic backward accumulates into a zeroed buffer
         grad_all = torch.empty_like(v_all) if det else torch.zeros_like(v_all)
         token = torch.zeros((), dtype=torch.float32, device=memory.device)
-        ctx.save_for_backward(m2, W)
+        idx = topk[..., None].expand(-1, -1, d)
+        sel = memory.gather(1, idx) * vsel
+        ctx.save_for_backward(m2, W, idx, vsel)
         ctx.grad_all = grad_all
         ctx.meta = (B, S, d, n, memory.dtype, [w.dtype for w in ws], [b.dtype for b in bs])
         ctx.mark_non_differentiable(v_all, grad_all)
         ctx.set_materialize_grads(False)  # no zero-filled [B, S, n d] gradients for v_all / grad_all
-        return v_all, grad_all, token
+        return v_all, grad_all, token, sel
 
     @staticmethod
-    def backward(ctx, _gv, _gg, _gt):
-        m2, W = ctx.saved_tensors
+    def backward(ctx, _gv, _gg, _gt, gsel):
+        m2, W, idx, vsel = ctx.saved_tensors
         B, S, d, n, mdtype, wdt, bdt = ctx.meta
         G = ctx.grad_all.view(B * S, n * d)
         ctx.grad_all = None
         dmem = G.mm(W).view(B, S, d).to(mdtype) if ctx.needs_input_grad[0] else None
+        if dmem is not None and gsel is not None:  # (top-k rows are distinct per image: one add per row)
+            dmem.scatter_add_(1, idx, (gsel * vsel).to(mdtype))
         dW = chunked_wgrad(G, m2)  # fp32 [n d, d]
         db = bias_grad(G, torch.float32)
         grads = []
         for i in range(n):
             grads += [dW[i * d:(i + 1) * d].to(wdt[i]), db[i * d:(i + 1) * d].to(bdt[i])]
-        return (dmem, None, None, *grads)
+        return (dmem, None, None, None, None, *grads)
 
 
 class _MSDAFusedSlot(torch.autograd.Function):
@@ -256,6 +315,9 @@ _FUSED_MLP = os.environ.get("MOE_FUSED_MLP", "1") != "0"  # A/B switch: ReLU MLP
 # MOE_DET_MSDA=0: the decoder's MSDA value gradients by packed bf16 atomics
 # (arrival order) instead of the deterministic fixed-order fp32 sums (A/B)
 _DET_MSDA = os.environ.get("MOE_DET_MSDA", "1") != "0"
+# MOE_LEVEL_MEMORY=0: the input projections' BatchNorm outputs concatenated
+# into memory by torch.cat (A/B switch for _LevelMemory)
+_LEVEL_MEMORY = os.environ.get("MOE_LEVEL_MEMORY", "1") != "0"
 
 
 def _det_msda(L, P, D):
@@ -418,28 +480,49 @@ class RTDETRDecoder(nn.Module):
             self._anchor_cache[key] = (a.to(dtype), valid.to(dtype))
         return self._anchor_cache[key]
 
-    def _value_slots(self, memory):
+    def _value_slots(self, memory, topk, vsel):
         """GPU bf16 path: all layers' value projections as one GEMM
-        (_ValueProjAll); elsewhere each layer projects its own values."""
+        (_ValueProjAll, which also gathers the selected rows) -> (slots, sel);
+        elsewhere None (each layer projects its own values)."""
         n = len(self.layers)
         dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else memory.dtype
         if not (_BATCHED_VALUE and _FUSED_MSDA and memory.is_cuda and dtype == torch.bfloat16 and n > 1):
-            return [None] * n
+            return None
         vps = [layer.cross_attn.value_proj for layer in self.layers]
         det = all(_det_msda(la.cross_attn.nlevels, la.cross_attn.npoints, la.cross_attn.d // la.cross_attn.nhead)
                   for la in self.layers)
         with torch.autocast("cuda", enabled=False):
-            v_all, g_all, token = _ValueProjAll.apply(memory, dtype, det,
-                                                      *[t for m in vps for t in (m.weight, m.bias)])
-        return [(v_all, g_all, token, i * self.hidden) for i in range(n)]
+            v_all, g_all, token, sel = _ValueProjAll.apply(memory, dtype, det, topk, vsel,
+                                                           *[t for m in vps for t in (m.weight, m.bias)])
+        return [(v_all, g_all, token, i * self.hidden) for i in range(n)], sel
+
+    def _memory(self, feats):
+        """(memory [B, S, d], level shapes): the input projections (1x1 conv +
+        training BatchNorm) of every level, flattened and concatenated over
+        the levels.  GPU bf16 with the fused BatchNorm: each level's
+        BatchNorm writes its rows of memory directly (_LevelMemory), its
+        statistics summed in the convolution's epilogue."""
+        if _FUSED_BN and _LEVEL_MEMORY and feats[0].is_cuda:
+            ys, parts, bns = [], [], []
+            for p, f in zip(self.input_proj, feats):
+                y, part = conv_module_stats(p[0], f)
+                ys.append(y)
+                parts.append(part)
+                bns.append(p[1])
+            if all(bn_act_ok([y], [bn]) for y, bn in zip(ys, bns)) and len({y.shape[:2] for y in ys}) == 1:
+                mem = _LevelMemory.apply(bns, parts, *ys, *[bn.weight for bn in bns], *[bn.bias for bn in bns])
+                return mem, [tuple(y.shape[-2:]) for y in ys]
+            proj = [bn(y) for y, bn in zip(ys, bns)]
+        else:
+            # conv + training BatchNorm through libmoe_hip's bn_act (as the encoder's
+            # input projections): MIOpen's BN backward at batch 1 lost the gradient
+            # (relative error 1.4 vs 0.09 for a bf16 CPU run, tools/grad_flow_diag.py)
+            proj = [HybridEncoder._proj(p, f) for p, f in zip(self.input_proj, feats)]
+        shapes = [tuple(f.shape[-2:]) for f in proj]
+        return torch.cat([f.flatten(2).permute(0, 2, 1) for f in proj], 1).contiguous(), shapes  # [B, S, d]
 
     def forward(self, feats, ctx):
-        # conv + training BatchNorm through libmoe_hip's bn_act (as the encoder's
-        # input projections): MIOpen's BN backward at batch 1 lost the gradient
-        # (relative error 1.4 vs 0.09 for a bf16 CPU run, tools/grad_flow_diag.py)
-        proj = [HybridEncoder._proj(p, f) for p, f in zip(self.input_proj, feats)]
-        shapes = [tuple(f.shape[-2:]) for f in proj]
-        memory = torch.cat([f.flatten(2).permute(0, 2, 1) for f in proj], 1).contiguous()  # [B, S, d]
+        memory, shapes = self._memory(feats)
         B = memory.shape[0]
         anchors, valid = self._anchors(shapes, memory.device, torch.float32)
         vmask = valid.to(memory.dtype)  # [1, S, 1]
@@ -458,8 +541,13 @@ class RTDETRDecoder(nn.Module):
         self.last_topk = topk
         # (valid * memory) at the selected rows: the mask applied after the
         # gather (same products), so the backward multiplies [B, Q, d], not [B, S, d]
-        sel_in = memory.gather(1, topk[..., None].expand(-1, -1, memory.shape[-1])) * \
-            vmask.expand(B, -1, -1).gather(1, topk[..., None])
+        vsel = vmask.expand(B, -1, -1).gather(1, topk[..., None])
+        vs = self._value_slots(memory, topk, vsel)
+        if vs is not None:
+            vslots, sel_in = vs
+        else:
+            vslots = [None] * len(self.layers)
+            sel_in = memory.gather(1, topk[..., None].expand(-1, -1, memory.shape[-1])) * vsel
         sel = self.enc_output(sel_in)
         enc_topk_logits = self.enc_score_head(sel)
         ref_unact = self.enc_bbox_head(sel).float() + anchors.expand(B, -1, -1).gather(
@@ -468,7 +556,6 @@ class RTDETRDecoder(nn.Module):
         tgt = sel.detach()
         ref_detach = ref_unact.detach().sigmoid()
         ref = ref_detach
-        vslots = self._value_slots(memory)
         dec_logits, dec_boxes = [], []
         for i, layer in enumerate(self.layers):
             query_pos = self.query_pos_head(ref_detach.to(tgt.dtype))

@@ -11,7 +11,7 @@ import torch.nn.functional as F
 from ..moe.config import MoEConfig
 from ..moe.layer import MoEFFN
 from .norm import AddLayerNorm
-from .backbone import _FUSED_BN, ConvNormLayer
+from .backbone import _FUSED_BN, ConvNormLayer, stage_taps
 from .conv import conv_module, conv_pair
 from .fused import bn_act, bn_act_ok
 from .linear import TokenLinear, TokenSelfAttention
@@ -187,6 +187,7 @@ class HybridEncoder(nn.Module):
         return p(f)
 
     def forward(self, feats, ctx):
+        feats = stage_taps(feats)  # backbone outputs with a GradLink: gradient handed over, not accumulated
         proj = [self._proj(p, f) for p, f in zip(self.input_proj, feats)]
         for i, enc_ind in enumerate(self.use_encoder_idx):
             B, C, h, w = proj[enc_ind].shape

@@ -231,3 +231,47 @@ def test_down_link_matches_relu_grad2(hip_lib, monkeypatch):
     assert res[0][1].keys() == res[1][1].keys()
     for k in res[0][1]:
         assert _rel(res[0][1][k], res[1][1][k]) < 2e-2, k
+
+
+@pytest.mark.parametrize("tap", [False, True])
+def test_stage_outputs_with_external_consumer(hip_lib, monkeypatch, tap):
+    """The backbone's returned stage outputs (C3, C4) also feed the next stage,
+    whose first block finishes their gradient through a GradLink (the average
+    pool of the ResNet-D shortcut hands its gradient to branch2a's dgrad
+    epilogue, which adds it and applies the ReLU mask).  The encoder's
+    gradient for those outputs must be masked too: with a general consumer
+    (a 1x1 HIP convolution, as the encoder's input projections, then a random
+    linear functional, which -- unlike a square loss -- is non-zero where the
+    ReLU output is zero) the parameter gradients with the links on equal the
+    link-free path (every gradient summed by autograd, one relu_grad2 pass) at
+    bf16 noise.  tap: the outputs go through backbone.stage_taps (the
+    encoder's hand-off of its gradient into the link, no autograd add)."""
+    from src.rtdetr_moe import backbone as bb
+    from src.rtdetr_moe.conv import conv_module
+
+    torch.manual_seed(3)
+    m = bb.PResNet(50).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for mod in m.modules():
+        if hasattr(mod, "running_var") and not isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_var.uniform_(0.5, 2.0)
+            mod.weight.uniform_(0.5, 1.5)
+    projs = [torch.nn.Conv2d(c, 64, 1, bias=False).to(DEV).to(torch.bfloat16) for c in m.out_channels]
+    x = torch.randn(2, 3, 128, 160, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    rs = None
+    res = []
+    for links in (True, False):
+        monkeypatch.setattr(bb, "_GRAD_LINK", links)
+        monkeypatch.setattr(bb, "_DOWN_LINK", links)
+        m.zero_grad(set_to_none=True)
+        outs = m(x)
+        if tap:
+            outs = bb.stage_taps(outs)
+        ys = [conv_module(p, o) for p, o in zip(projs, outs)]
+        if rs is None:
+            g = torch.Generator(device=DEV).manual_seed(7)
+            rs = [torch.randn(y.shape, device=DEV, generator=g).to(torch.bfloat16) for y in ys]
+        sum((y.float() * r.float()).sum() for y, r in zip(ys, rs)).backward()
+        res.append({n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None})
+    assert res[0].keys() == res[1].keys() and len(res[0]) > 0
+    bad = {k: round(_rel(res[0][k], res[1][k]), 4) for k in res[0] if _rel(res[0][k], res[1][k]) >= 2e-2}
+    assert not bad, bad
