@@ -591,11 +591,15 @@ int rtdetr_bn_act_fwd_part(const void* const* x, const float* const* gamma, cons
  * level l's BatchNorm output written straight into its rows (y = memory +
  * start_l C, hw = h_l w_l, bstride = S) and its gradient read from d memory
  * in place -- no concatenation forward, no strided copy backward.  fwd_rows:
- * part (conv-epilogue statistics, ws unused) or ws (a statistics pass). */
+ * part (conv-epilogue statistics, ws unused) or ws (a statistics pass);
+ * resid (bf16 [M, C] in x's layout, or NULL): y = act(z) + resid, act(z)
+ * rounded to bf16 before the add (the bits of a bf16 activation then a bf16
+ * add) -- the CSPRep layer's bottleneck output + shortcut branch, whose
+ * gradient is dy for both (no separate add either way). */
 int rtdetr_bn_act_fwd_rows(const void* const* x, const float* const* gamma, const float* const* beta,
                            float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act,
                            float eps, float momentum, const float* part, int part_blocks, float* ws, float* saved,
-                           void* y, long long y_hw, long long y_bstride, hipStream_t stream);
+                           const void* resid, void* y, long long y_hw, long long y_bstride, hipStream_t stream);
 int rtdetr_bn_act_bwd_rows(const void* dy, long long dy_hw, long long dy_bstride, const void* const* x,
                            const float* const* gamma, int nb, long long M, int C, int act, const float* saved,
                            float* ws, float* coef, void* const* dx, float* dgb, hipStream_t stream);

@@ -33,6 +33,10 @@ struct BnArgs {
   // tensor (the decoder's memory [B, S, C], one level's rows per image);
   // rhw == 0: contiguous (row r at row r)
   long long rhw, rbs;
+  // forward: y = act(z) + resid (resid bf16 [M, C] in x's layout, or NULL);
+  // act(z) is rounded to bf16 first, then the fp32 sum rounded once -- the
+  // same bits as a bf16 activation followed by torch's bf16 add
+  const uint4* resid;
 };
 
 __device__ __forceinline__ long long map_row(const BnArgs& a, long long r) {
@@ -199,7 +203,16 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(BnArgs a, const float* __
 #pragma unroll
       for (int j = 0; j < 8; ++j) z[j] = z[j] * sigmoidf_(z[j]);
     }
-    y[a.rhw ? map_row(a, i / cch) * cch + cc : i] = pack8(z);
+    uint4 o = pack8(z);
+    if (a.resid != nullptr) {
+      float r[8];
+      unpack8(o, z);
+      unpack8(a.resid[i], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] += r[j];
+      o = pack8(z);
+    }
+    y[a.rhw ? map_row(a, i / cch) * cch + cc : i] = o;
   }
 }
 
@@ -366,7 +379,7 @@ static int bn_rows_check(long long M, long long hw, long long bs) {
 static int bn_act_fwd_impl(const void* const* x, const float* const* gamma, const float* const* beta,
                            float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act,
                            float eps, float momentum, float* saved, float* ws, const float* part, int part_blocks,
-                           void* y, long long y_hw, long long y_bstride, hipStream_t stream) {
+                           const void* resid, void* y, long long y_hw, long long y_bstride, hipStream_t stream) {
   if (int rc = bn_check(nb, M, C, act)) return rc;
   if (int rc = bn_rows_check(M, y_hw, y_bstride)) return rc;
   if (!x || !gamma || !beta || !saved || !y || (!ws && !part)) return fail("bn_act_fwd: NULL argument");
@@ -376,6 +389,8 @@ static int bn_act_fwd_impl(const void* const* x, const float* const* gamma, cons
   a.nb = nb;
   a.rhw = y_hw;
   a.rbs = y_bstride;
+  a.resid = static_cast<const uint4*>(resid);
+  if (reinterpret_cast<uintptr_t>(resid) % 16) return fail("bn_act_fwd: resid must be 16-B aligned");
   for (int i = 0; i < nb; ++i) {
     if (!x[i] || !gamma[i] || !beta[i]) return fail("bn_act_fwd: NULL branch pointer");
     a.x[i] = static_cast<const uint4*>(x[i]);
@@ -414,8 +429,8 @@ static int bn_act_fwd_impl(const void* const* x, const float* const* gamma, cons
 extern "C" int rtdetr_bn_act_fwd(const void* const* x, const float* const* gamma, const float* const* beta,
                                  float* const* run_mean, float* const* run_var, int nb, long long M, int C, int act,
                                  float eps, float momentum, float* saved, float* ws, void* y, hipStream_t stream) {
-  return bn_act_fwd_impl(x, gamma, beta, run_mean, run_var, nb, M, C, act, eps, momentum, saved, ws, nullptr, 0, y,
-                         0, 0, stream);
+  return bn_act_fwd_impl(x, gamma, beta, run_mean, run_var, nb, M, C, act, eps, momentum, saved, ws, nullptr, 0,
+                         nullptr, y, 0, 0, stream);
 }
 
 extern "C" int rtdetr_bn_act_fwd_part(const void* const* x, const float* const* gamma, const float* const* beta,
@@ -424,16 +439,16 @@ extern "C" int rtdetr_bn_act_fwd_part(const void* const* x, const float* const* 
                                       float* saved, void* y, hipStream_t stream) {
   if (part == nullptr) return fail("bn_act_fwd_part: part is NULL");
   return bn_act_fwd_impl(x, gamma, beta, run_mean, run_var, nb, M, C, act, eps, momentum, saved, nullptr, part,
-                         part_blocks, y, 0, 0, stream);
+                         part_blocks, nullptr, y, 0, 0, stream);
 }
 
 extern "C" int rtdetr_bn_act_fwd_rows(const void* const* x, const float* const* gamma, const float* const* beta,
                                       float* const* run_mean, float* const* run_var, int nb, long long M, int C,
                                       int act, float eps, float momentum, const float* part, int part_blocks,
-                                      float* ws, float* saved, void* y, long long y_hw, long long y_bstride,
-                                      hipStream_t stream) {
+                                      float* ws, float* saved, const void* resid, void* y, long long y_hw,
+                                      long long y_bstride, hipStream_t stream) {
   return bn_act_fwd_impl(x, gamma, beta, run_mean, run_var, nb, M, C, act, eps, momentum, saved,
-                         part ? nullptr : ws, part, part_blocks, y, y_hw, y_bstride, stream);
+                         part ? nullptr : ws, part, part_blocks, resid, y, y_hw, y_bstride, stream);
 }
 
 extern "C" int rtdetr_bn_act_bwd_rows(const void* dy, long long dy_hw, long long dy_bstride, const void* const* x,

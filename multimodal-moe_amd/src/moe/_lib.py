@@ -115,7 +115,7 @@ SIGNATURES = {
     "rtdetr_conv_fwd_stats": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_bn_act_fwd_part": (_I, [_P, _P, _P, _P, _P, _I, ctypes.c_longlong, _I, _I, _F, _F, _P, _I, _P, _P, _P]),
     "rtdetr_bn_act_fwd_rows": (_I, [_P, _P, _P, _P, _P, _I, ctypes.c_longlong, _I, _I, _F, _F, _P, _I, _P, _P, _P,
-                                    ctypes.c_longlong, ctypes.c_longlong, _P]),
+                                    _P, ctypes.c_longlong, ctypes.c_longlong, _P]),
     "rtdetr_bn_act_bwd_rows": (_I, [_P, ctypes.c_longlong, ctypes.c_longlong, _P, _P, _I, ctypes.c_longlong, _I, _I,
                                     _P, _P, _P, _P, _P, _P]),
     "rtdetr_conv_dgrad_workspace": (_LL, [_I, _I, _I, _I, _I, _I]),
@@ -968,9 +968,11 @@ def _bn_ws(M, C, nb, dev):
     return torch.empty(n, dtype=torch.float32, device=dev)
 
 
-def bn_act_fwd(xs, gammas, betas, run_means, run_vars, act, eps, momentum):
+def bn_act_fwd(xs, gammas, betas, run_means, run_vars, act, eps, momentum, resid=None):
     """Training BatchNorm of 1-2 channels_last bf16 branches, summed, act
-    (0 none / 1 silu) -> (y, saved fp32 [nb, 4, C])."""
+    (0 none / 1 silu) [+ resid, bf16 like x] -> (y, saved fp32 [nb, 4, C])."""
+    if resid is not None:
+        return _bn_act_fwd_resid(xs, gammas, betas, run_means, run_vars, act, eps, momentum, None, resid)
     M, C = _nhwc_rows(xs[0], "x0")
     nb = len(xs)
     for i, x in enumerate(xs[1:], 1):
@@ -992,9 +994,42 @@ def bn_act_fwd(xs, gammas, betas, run_means, run_vars, act, eps, momentum):
     return y, saved
 
 
-def bn_act_fwd_part(xs, gammas, betas, run_means, run_vars, act, eps, momentum, part):
+def _bn_act_fwd_resid(xs, gammas, betas, run_means, run_vars, act, eps, momentum, part, resid):
+    """bn_act_fwd / bn_act_fwd_part with y = act(z) + resid
+    (rtdetr_bn_act_fwd_rows, contiguous rows)."""
+    M, C = _nhwc_rows(xs[0], "x0")
+    nb = len(xs)
+    for i, x in enumerate(xs[1:], 1):
+        if _nhwc_rows(x, f"x{i}") != (M, C):
+            raise MoEKernelError("bn_act: branches differ in shape")
+    if _nhwc_rows(resid, "resid") != (M, C) or resid.data_ptr() % 16:
+        raise MoEKernelError("bn_act: resid must be a 16-B aligned channels_last bf16 tensor like x")
+    if part is not None:
+        _need(part, torch.float32, "part")
+        if part.dim() != 4 or part.shape[0] != nb or part.shape[2] != 2 or part.shape[3] != C:
+            raise MoEKernelError(f"bn_act_fwd_part: part must be [{nb}, nblk, 2, {C}], got {tuple(part.shape)}")
+    for t in list(gammas) + list(betas) + [r for r in run_means + run_vars if r is not None]:
+        _need(t, torch.float32, "bn affine/statistics")
+    y = torch.empty_like(xs[0])
+    saved = torch.empty((nb, 4, C), dtype=torch.float32, device=y.device)
+    ws = None if part is not None else _bn_ws(M, C, nb, y.device)
+    px, kx = _ptrs(xs)
+    pg, kg = _ptrs(gammas)
+    pb, kb = _ptrs(betas)
+    has_run = all(r is not None for r in run_means + run_vars)
+    pm, km = _ptrs(run_means) if has_run else (None, None)
+    pv, kv = _ptrs(run_vars) if has_run else (None, None)
+    _check(lib().rtdetr_bn_act_fwd_rows(px, pg, pb, pm, pv, nb, M, C, int(act), float(eps), float(momentum),
+                                        _ptr(part), int(part.shape[1]) if part is not None else 0, _ptr(ws),
+                                        _ptr(saved), _ptr(resid), _ptr(y), 0, 0, _stream()), "rtdetr_bn_act_fwd_rows")
+    return y, saved
+
+
+def bn_act_fwd_part(xs, gammas, betas, run_means, run_vars, act, eps, momentum, part, resid=None):
     """bn_act_fwd with the statistics partials of rtdetr_conv_fwd_stats:
     part fp32 [nb, nblk, 2, C]."""
+    if resid is not None:
+        return _bn_act_fwd_resid(xs, gammas, betas, run_means, run_vars, act, eps, momentum, part, resid)
     M, C = _nhwc_rows(xs[0], "x0")
     nb = len(xs)
     for i, x in enumerate(xs[1:], 1):
@@ -1062,7 +1097,7 @@ def bn_act_fwd_rows(x, gamma, beta, run_mean, run_var, act, eps, momentum, part,
     pv, kv = _ptrs([run_var]) if has_run else (None, None)
     _check(lib().rtdetr_bn_act_fwd_rows(px, pg, pb, pm, pv, 1, M, C, int(act), float(eps), float(momentum),
                                         _ptr(part), int(part.shape[1]) if part is not None else 0, _ptr(ws),
-                                        _ptr(saved), y.data_ptr() + row0 * C * 2, hw, bstride, _stream()),
+                                        _ptr(saved), None, y.data_ptr() + row0 * C * 2, hw, bstride, _stream()),
            "rtdetr_bn_act_fwd_rows")
     return saved
 

@@ -328,18 +328,38 @@ class _ConvHIPFork(torch.autograd.Function):
         return gx, gw, g if ctx.needs_input_grad[2] else None, None, None, None, None
 
 
+class GradSlot:
+    """Hand-off of an activation's gradient between its two convolution
+    consumers (the encoder's PAN inputs P3 / P4: the encoder's downsampling
+    convolution and the decoder's input projection).  The first consumer
+    created (collector) runs its backward LAST (autograd runs later-created
+    nodes first); the later one (depositor) parks its data gradient here and
+    returns none, and the collector's dgrad epilogue adds it (the `add`
+    operand) -- no autograd accumulation launch.  A depositor that runs after
+    the collector (closed slot) returns its gradient to autograd as usual."""
+
+    __slots__ = ("g", "closed", "has_collector")
+
+    def __init__(self):
+        self.g = None
+        self.closed = False
+        self.has_collector = False
+
+
 class _ConvHIPStats(torch.autograd.Function):
     """(conv(x, w), BatchNorm partials fp32 [1, nblk, 2, N] of its output) for
     a training BatchNorm that follows (fused.bn_act(parts=...)): the
-    statistics pass over y is folded into the convolution's epilogue."""
+    statistics pass over y is folded into the convolution's epilogue.
+    slot / collect: see GradSlot (collect True: this is the collector)."""
 
     @staticmethod
-    def forward(ctx, x, w, nblk, st):
+    def forward(ctx, x, w, nblk, st, slot=None, collect=False):
         x = _nhwc(x)
         w = _nhwc(w)
         part = torch.empty((1, nblk, 2, w.shape[0]), dtype=torch.float32, device=x.device)
         y = _fwd_stats(x, w, part[0], st)
         ctx.st = st
+        ctx.slot, ctx.collect = slot, collect
         ctx.save_for_backward(x, w)
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)
@@ -348,10 +368,18 @@ class _ConvHIPStats(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, _gpart):
         x, w = ctx.saved_tensors
+        slot = ctx.slot
+        add = None
+        if slot is not None and ctx.collect:
+            add, slot.g, slot.closed = slot.g, None, True
         if gy is None:
-            return None, None, None, None
-        gx, gw = _bwd(x, w, gy, ctx.needs_input_grad[0], ctx.needs_input_grad[1], False, None, ctx.st)
-        return gx, gw, None, None
+            if add is not None:
+                return add, None, None, None, None, None
+            return None, None, None, None, None, None
+        gx, gw = _bwd(x, w, gy, ctx.needs_input_grad[0], ctx.needs_input_grad[1], False, add, ctx.st)
+        if slot is not None and not ctx.collect and not slot.closed and gx is not None and slot.g is None:
+            slot.g, gx = gx, None  # parked for the collector's dgrad epilogue
+        return gx, gw, None, None, None, None
 
 
 def conv_module_stats(conv: torch.nn.Conv2d, x):
@@ -364,7 +392,11 @@ def conv_module_stats(conv: torch.nn.Conv2d, x):
             st = _stride(conv.stride)
             nblk = _stats_blocks(xc, wc, st)
             if nblk > 0:
-                return _ConvHIPStats.apply(xc, wc, nblk, st)
+                slot = getattr(x, "grad_slot", None) if xc is x and torch.is_grad_enabled() else None
+                collect = False
+                if slot is not None and not slot.has_collector:
+                    slot.has_collector = collect = True
+                return _ConvHIPStats.apply(xc, wc, nblk, st, slot, collect)
             return _ConvHIP.apply(xc, wc, None, False, False, False, None, st), None
     return conv_module(conv, x), None
 

@@ -13,7 +13,7 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
-from .linear import TokenLinear, TokenSelfAttention, _MLPHip, bias_grad, chunked_wgrad, mlp_hip_ok
+from .linear import TokenLinear, TokenSelfAttention, _MLPHip, bias_grad, chunked_wgrad, dual_linear, mlp_hip_ok
 from ..moe.config import MoEConfig
 from .encoder import HybridEncoder, make_ffn
 from .norm import AddLayerNorm
@@ -383,8 +383,7 @@ class MSDeformableAttention(nn.Module):
         H, L, P = self.nhead, self.nlevels, self.npoints
         if vslot is not None:
             v_all, g_all, token, col0 = vslot
-            off = self.sampling_offsets(query)
-            logits = self.attention_weights(query)
+            off, logits = dual_linear(query, self.sampling_offsets, self.attention_weights)
             if not (off.dtype == logits.dtype == torch.bfloat16 and not ref_boxes.requires_grad and L * P <= 16):
                 raise RuntimeError("the batched value projection needs the fused bf16 MSDA path")
             st, so = _level_tensors(shapes, v_all.device)
@@ -394,8 +393,7 @@ class MSDeformableAttention(nn.Module):
                                        float(self.offset_scale), L, P, hw)
             return self.output_proj(out)
         v = self.value_proj(value).view(B, value.shape[1], H, self.d // H)
-        off = self.sampling_offsets(query)
-        logits = self.attention_weights(query)
+        off, logits = dual_linear(query, self.sampling_offsets, self.attention_weights)
         if (_FUSED_MSDA and v.is_cuda and v.dtype == off.dtype == logits.dtype == torch.bfloat16
                 and not ref_boxes.requires_grad and L * P <= 16):
             st, so = _level_tensors(shapes, v.device)

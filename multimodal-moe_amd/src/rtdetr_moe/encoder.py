@@ -12,7 +12,7 @@ from ..moe.config import MoEConfig
 from ..moe.layer import MoEFFN
 from .norm import AddLayerNorm
 from .backbone import _FUSED_BN, ConvNormLayer, stage_taps
-from .conv import conv_module, conv_pair
+from .conv import GradSlot, conv_module, conv_pair
 from .fused import bn_act, bn_act_ok
 from .linear import TokenLinear, TokenSelfAttention
 
@@ -105,14 +105,18 @@ class RepVggBlock(nn.Module):
         self.conv1 = ConvNormLayer(cin, cout, 3, 1)
         self.conv2 = ConvNormLayer(cin, cout, 1, 1)
 
-    def forward(self, x):
+    def forward(self, x, resid=None):
+        """silu(BN1(conv3x3 x) + BN2(conv1x1 x)) [+ resid: the CSPRep
+        shortcut branch, added in the same pass on the fused path]."""
         if _FUSED_BN:
             # one node: dx accumulated in the dgrad, the BN statistics in the forward epilogues
             y1, y2, parts = conv_pair(self.conv1.conv, self.conv2.conv, x, stats=True)
             if bn_act_ok([y1, y2], [self.conv1.norm, self.conv2.norm]):  # both BNs + sum + SiLU in HIP
-                return bn_act([y1, y2], [self.conv1.norm, self.conv2.norm], "silu", parts)
-            return F.silu(self.conv1.norm(y1) + self.conv2.norm(y2))
-        return F.silu(self.conv1(x) + self.conv2(x))
+                return bn_act([y1, y2], [self.conv1.norm, self.conv2.norm], "silu", parts, resid=resid)
+            y = F.silu(self.conv1.norm(y1) + self.conv2.norm(y2))
+        else:
+            y = F.silu(self.conv1(x) + self.conv2(x))
+        return y if resid is None else y + resid
 
 
 class CSPRepLayer(nn.Module):
@@ -133,8 +137,18 @@ class CSPRepLayer(nn.Module):
                 a1, a2 = bn_act([y1], [c1.norm], "silu", p1), bn_act([y2], [c2.norm], "silu", p2)
             else:
                 a1, a2 = c1.act(c1.norm(y1)), c2.act(c2.norm(y2))
-            return self.conv3(self.bottlenecks(a1) + a2)
+            return self.conv3(self._bottlenecks_plus(a1, a2))
         return self.conv3(self.bottlenecks(self.conv1(x)) + self.conv2(x))
+
+    def _bottlenecks_plus(self, h, a2):
+        """bottlenecks(h) + a2, the add in the last RepVgg block's BatchNorm
+        pass (RepVggBlock resid)."""
+        blocks = list(self.bottlenecks)
+        if not blocks or not all(isinstance(b, RepVggBlock) for b in blocks):
+            return self.bottlenecks(h) + a2
+        for b in blocks[:-1]:
+            h = b(h)
+        return blocks[-1](h, resid=a2)
 
 
 def sincos_pos_embed_2d(w, h, dim=256, temperature=10000.0, device=None, dtype=torch.float32):
@@ -204,6 +218,12 @@ class HybridEncoder(nn.Module):
             inner.insert(0, self.fpn_blocks[n - 1 - idx](up_cat(high, proj[idx - 1])))
         outs = [inner[0]]
         for idx in range(n - 1):
-            down = self.downsample_convs[idx](outs[-1])
+            src = outs[-1]
+            if torch.is_grad_enabled() and src.requires_grad and src.is_cuda:
+                # src is also an encoder output (the decoder's input projection
+                # consumes it): its gradient from there joins this convolution's
+                # dgrad epilogue (GradSlot), not an autograd add
+                src.grad_slot = GradSlot()
+            down = self.downsample_convs[idx](src)
             outs.append(self.pan_blocks[idx](torch.cat([down, inner[idx + 1]], dim=1)))
         return outs

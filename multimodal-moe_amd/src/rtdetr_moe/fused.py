@@ -111,15 +111,16 @@ class AddBiasReLUFork(torch.autograd.Function):
 # ---------------------------------------------------------------------------
 class _BatchNormAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, act, eps, momentum, bns, parts, *args):
+    def forward(ctx, act, eps, momentum, bns, parts, resid, *args):
         nb = len(bns)
         xs, gammas, betas = args[:nb], args[nb:2 * nb], args[2 * nb:3 * nb]
         rms = [bn.running_mean for bn in bns]
         rvs = [bn.running_var for bn in bns]
         if parts is not None:  # statistics summed by the producing convolution (conv.conv_module_stats)
-            y, saved = L.bn_act_fwd_part(list(xs), list(gammas), list(betas), rms, rvs, act, eps, momentum, parts)
+            y, saved = L.bn_act_fwd_part(list(xs), list(gammas), list(betas), rms, rvs, act, eps, momentum, parts,
+                                         resid=resid)
         else:
-            y, saved = L.bn_act_fwd(list(xs), list(gammas), list(betas), rms, rvs, act, eps, momentum)
+            y, saved = L.bn_act_fwd(list(xs), list(gammas), list(betas), rms, rvs, act, eps, momentum, resid=resid)
         ctx.act, ctx.nb = act, nb
         ctx.save_for_backward(*xs, *gammas, saved)
         return y
@@ -131,7 +132,8 @@ class _BatchNormAct(torch.autograd.Function):
         xs, gammas, saved = list(t[:nb]), list(t[nb:2 * nb]), t[2 * nb]
         dy = dy.contiguous(memory_format=torch.channels_last)
         dxs, dgb = L.bn_act_bwd(dy, xs, gammas, saved, ctx.act)
-        return (None, None, None, None, None, *dxs, *[dgb[i, 0] for i in range(nb)],
+        dres = dy if ctx.needs_input_grad[5] else None  # y = act(z) + resid: resid's gradient is dy itself
+        return (None, None, None, None, None, dres, *dxs, *[dgb[i, 0] for i in range(nb)],
                 *[dgb[i, 1] for i in range(nb)])
 
 
@@ -153,13 +155,19 @@ def bn_act_ok(xs, bns) -> bool:
     return True
 
 
-def bn_act(xs, bns, act: str | None, parts=None):
-    """act(sum_i BN_i(x_i)) through libmoe_hip (callers check bn_act_ok).
-    parts: the branches' batch-statistics partials fp32 [nb, nblk, 2, C]
-    from their convolutions' epilogues (conv.conv_module_stats / conv_pair),
-    or None (a statistics pass over x).  num_batches_tracked is not advanced
-    (it only matters with momentum=None)."""
+def bn_act(xs, bns, act: str | None, parts=None, resid=None):
+    """act(sum_i BN_i(x_i)) [+ resid] through libmoe_hip (callers check
+    bn_act_ok).  parts: the branches' batch-statistics partials fp32
+    [nb, nblk, 2, C] from their convolutions' epilogues
+    (conv.conv_module_stats / conv_pair), or None (a statistics pass over x).
+    resid: a tensor like x added after the activation in the same pass (the
+    CSPRep layer's shortcut branch; bits of the bf16 activation then a bf16
+    add).  num_batches_tracked is not advanced (it only matters with
+    momentum=None)."""
     bns = list(bns)
     a = 1 if act == "silu" else 0
-    return _BatchNormAct.apply(a, float(bns[0].eps), float(bns[0].momentum), bns, parts, *xs,
+    if resid is not None and not (_gpu_ok(resid) and resid.shape == xs[0].shape and resid.data_ptr() % 16 == 0):
+        return _BatchNormAct.apply(a, float(bns[0].eps), float(bns[0].momentum), bns, parts, None, *xs,
+                                   *[bn.weight for bn in bns], *[bn.bias for bn in bns]) + resid
+    return _BatchNormAct.apply(a, float(bns[0].eps), float(bns[0].momentum), bns, parts, resid, *xs,
                                *[bn.weight for bn in bns], *[bn.bias for bn in bns])

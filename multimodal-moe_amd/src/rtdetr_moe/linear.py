@@ -292,6 +292,53 @@ class _TokenLinear(torch.autograd.Function):
         return gx, gw, gb, None
 
 
+class _DualTokenLinear(torch.autograd.Function):
+    """(x W1^T + b1, x W2^T + b2): two linears of the same input as one node
+    (the deformable attention's sampling-offset and attention-weight heads on
+    the query).  Forward: the two GEMMs TokenLinear issues.  Backward: x's
+    gradient g1 W1 + g2 W2 with the second product accumulated in place by its
+    GEMM (addmm_, beta = 1; fp32 sum, one rounding) instead of two products
+    and autograd's add; the weight gradients as TokenLinear's (deferred)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, dtype):
+        xc = x.to(dtype)
+        w1c, w2c = w1.to(dtype), w2.to(dtype)
+        y1 = F.linear(xc, w1c, b1.to(dtype))
+        y2 = F.linear(xc, w2c, b2.to(dtype))
+        ctx.save_for_backward(xc, w1c, w2c)
+        ctx.meta = ((w1.dtype, b1.dtype, _defer_targets(w1, b1, x)), (w2.dtype, b2.dtype, _defer_targets(w2, b2, x)))
+        ctx.set_materialize_grads(False)
+        return y1, y2
+
+    @staticmethod
+    def backward(ctx, gy1, gy2):
+        xc, w1c, w2c = ctx.saved_tensors
+        x2 = xc.reshape(-1, xc.shape[-1])
+        gx = None
+        grads = [None] * 4
+        for i, (gy, wc) in enumerate(((gy1, w1c), (gy2, w2c))):
+            if gy is None:
+                continue
+            g2 = gy.reshape(-1, gy.shape[-1]).to(wc.dtype).contiguous()
+            if ctx.needs_input_grad[0]:
+                gx = g2.mm(wc) if gx is None else gx.addmm_(g2, wc)
+            wdt, bdt, tg = ctx.meta[i]
+            grads[2 * i], grads[2 * i + 1] = _linear_wgrad(g2, x2, wdt, bdt, True, ctx.needs_input_grad[1 + 2 * i],
+                                                           ctx.needs_input_grad[2 + 2 * i], tg)
+        return (None if gx is None else gx.view(xc.shape), *grads, None)
+
+
+def dual_linear(x, lin1: nn.Linear, lin2: nn.Linear):
+    """(lin1(x), lin2(x)): one autograd node on the GPU (_DualTokenLinear),
+    the two modules elsewhere."""
+    if x.is_cuda and x.numel() > 0 and lin1.bias is not None and lin2.bias is not None:
+        dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+        with torch.autocast("cuda", enabled=False):
+            return _DualTokenLinear.apply(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias, dtype)
+    return lin1(x), lin2(x)
+
+
 _ROW_OFFSETS: dict = {}
 
 

@@ -83,3 +83,86 @@ def test_value_proj_selection_rows(hip_lib):
         res.append((sel.detach().clone(), m.grad.clone()))
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("nb", [1, 2])
+def test_bn_act_resid_equals_add(hip_lib, nb):
+    """fused.bn_act(..., resid=r) == bn_act(...) + r, forward and backward, bitwise
+    (the CSPRep layer's bottleneck output + shortcut branch)."""
+    from src.rtdetr_moe.fused import bn_act
+
+    torch.manual_seed(2)
+    shape = (2, 128, 20, 24)
+    xs0 = [torch.randn(shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+           for _ in range(nb)]
+    r0 = torch.randn(shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    bns = [torch.nn.BatchNorm2d(shape[1]).to(DEV) for _ in range(nb)]
+    res = []
+    for fused in (True, False):
+        xs = [x.clone().requires_grad_(True) for x in xs0]
+        r = r0.clone().requires_grad_(True)
+        for bn in bns:
+            bn.weight.grad = bn.bias.grad = None
+        y = bn_act(xs, bns, "silu", resid=r) if fused else bn_act(xs, bns, "silu") + r
+        y.backward(dy)
+        res.append([y.detach().clone(), r.grad.clone()] + [x.grad.clone() for x in xs] +
+                   [t.grad.clone() for bn in bns for t in (bn.weight, bn.bias)])
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+
+
+def test_dual_linear_matches_two_linears(hip_lib):
+    """linear.dual_linear (one node; x's gradient accumulated by the second
+    GEMM) == two TokenLinears: outputs and weight gradients bitwise, x's
+    gradient at one bf16 rounding (fp32 sum, rounded once)."""
+    from src.rtdetr_moe.linear import TokenLinear, dual_linear
+
+    torch.manual_seed(4)
+    l1 = TokenLinear(256, 192).to(DEV).to(torch.bfloat16)
+    l2 = TokenLinear(256, 96).to(DEV).to(torch.bfloat16)
+    x0 = torch.randn(4, 300, 256, device=DEV).to(torch.bfloat16)
+    g1 = torch.randn(4, 300, 192, device=DEV).to(torch.bfloat16)
+    g2 = torch.randn(4, 300, 96, device=DEV).to(torch.bfloat16)
+    res = []
+    for fused in (True, False):
+        x = x0.clone().requires_grad_(True)
+        for p in list(l1.parameters()) + list(l2.parameters()):
+            p.grad = None
+        y1, y2 = dual_linear(x, l1, l2) if fused else (l1(x), l2(x))
+        torch.autograd.backward([y1, y2], [g1, g2])
+        res.append((y1.detach().clone(), y2.detach().clone(), x.grad.float().clone(),
+                    [p.grad.clone() for p in list(l1.parameters()) + list(l2.parameters())]))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert float((res[0][2] - res[1][2]).norm() / res[1][2].norm()) < 4e-3
+    for a, b in zip(res[0][3], res[1][3]):
+        assert torch.equal(a, b)
+
+
+def test_grad_slot_two_conv_consumers(hip_lib):
+    """conv.GradSlot: an activation consumed by two stats convolutions (the
+    encoder's downsampling conv, then the decoder's input projection): the
+    later consumer parks its data gradient, the earlier one adds it in its
+    dgrad epilogue -- the input gradient equals autograd's sum at one bf16
+    rounding, the weight gradients bitwise."""
+    from src.rtdetr_moe.conv import GradSlot, conv_module_stats
+
+    torch.manual_seed(5)
+    ca = torch.nn.Conv2d(256, 256, 3, 2, 1, bias=False).to(DEV).to(torch.bfloat16)
+    cb = torch.nn.Conv2d(256, 256, 1, bias=False).to(DEV).to(torch.bfloat16)
+    x0 = torch.randn(2, 256, 46, 80, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res, rs = [], None
+    for slot in (True, False):
+        x = x0.clone().requires_grad_(True)
+        ca.weight.grad = cb.weight.grad = None
+        if slot:
+            x.grad_slot = GradSlot()
+        ya, pa = conv_module_stats(ca, x)
+        yb, pb = conv_module_stats(cb, x)
+        assert pa is not None and pb is not None
+        if rs is None:
+            rs = [torch.randn(y.shape, device=DEV).to(torch.bfloat16) for y in (ya, yb)]
+        ((ya.float() * rs[0].float()).sum() + (yb.float() * rs[1].float()).sum()).backward()
+        res.append((x.grad.float().clone(), ca.weight.grad.clone(), cb.weight.grad.clone()))
+    assert float((res[0][0] - res[1][0]).norm() / res[1][0].norm()) < 4e-3
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
