@@ -104,6 +104,9 @@ struct GemmParams {
 // runtime tuning overrides (moe_set_tuning); 0 = the per-shape choice below
 static int g_gemm_variant = 0;
 static int g_gemm_stages = 0;
+// ring depth of the long-K (>= 1024) row GEMMs whose grid is under one
+// workgroup per CU (the decoder's GEMM2: 176 workgroups, 16 K-tiles each)
+static int g_deep_stages = 3;
 static int g_gemm_debug = 0;
 static int g_rows_bm = 0;   // 0 = by tile count, else 64 or 128
 static int g_wgrad_bm = 0;  // 0 = by tile count, else 64 or 128
@@ -1106,17 +1109,14 @@ __device__ __forceinline__ void dma_meta64(const void* src, int row, int last, c
 // Wait until ring tile kt (and what was issued with it) has landed for this
 // wave: at most min(S - 2, newer) younger issues of PER instructions each may
 // stay in flight.
-template <int S, int PER>
+template <int S, int PER, int Y = S - 2>
 __device__ __forceinline__ void wait_issue(int newer) {
-  if constexpr (S == 2) {
+  if constexpr (Y <= 0) {
     wait_vm<0>();
-  } else if constexpr (S >= 4) {
-    if (newer >= 2) wait_vm<2 * PER>();
-    else if (newer == 1) wait_vm<PER>();
-    else wait_vm<0>();
   } else {
-    if (newer >= 1) wait_vm<PER>();
-    else wait_vm<0>();
+    static_assert(Y * PER < 64, "vmcnt");
+    if (newer >= Y) wait_vm<Y * PER>();
+    else wait_issue<S, PER, Y - 1>(newer);
   }
 }
 
@@ -1372,6 +1372,12 @@ static void allow_lds(size_t bytes) {
   }
 }
 
+// the 6-deep ring is instantiated for the 64-row bf16 row GEMMs only
+template <int BM, int MODE, int FL>
+constexpr bool deep_ring_ok() {
+  return MODE == MODE_ROWS && BM == 64 && !(FL & (FL_MX | FL_CQ | FL_AUX8));
+}
+
 template <int BM, int BN, bool A_K, bool B_K, int MODE, int EPI, bool COLSUM, int FL = 0>
 static void launch(const GemmParams& p, dim3 grid, hipStream_t s, const ProfScope& prof, int variant, int stages) {
   // MX: the exponent stage behind the ring ((BM + BN) rows x K/32 bytes)
@@ -1388,6 +1394,14 @@ static void launch(const GemmParams& p, dim3 grid, hipStream_t s, const ProfScop
     constexpr auto fn = gemm_v2_kernel<BM, BN, 2, A_K, B_K, MODE, EPI, COLSUM, FL & ~FL_Y8>;
     allow_lds<fn>(lds);
     MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
+  } else if (stages >= 6 && deep_ring_ok<BM, MODE, FL>()) {
+    // (one workgroup per CU: the deep ring of the long-K, sub-chip grids)
+    if constexpr (deep_ring_ok<BM, MODE, FL>()) {
+      const size_t lds = 6 * (BM + BN) * 64 * 2 + 6 * gx;
+      constexpr auto fn = gemm_v2_kernel<BM, BN, 6, A_K, B_K, MODE, EPI, COLSUM, FL & ~FL_Y8>;
+      allow_lds<fn>(lds);
+      MOE_LAUNCH(prof, fn, grid, dim3(256), lds, s, p);
+    }
   } else if (stages >= 4) {
     const size_t lds = 4 * (BM + BN) * 64 * 2 + xs + 4 * gx;
     constexpr auto fn = gemm_v2_kernel<BM, BN, 4, A_K, B_K, MODE, EPI, COLSUM, FL & ~FL_Y8>;
@@ -1518,7 +1532,7 @@ static int plan_rows(RowsPlan& pl, const void* a, const void* b, void* c, const 
   win = bind_split(p, S, tiles, part, win);
   pl.grid = tiles * S;
   pl.variant = (g_gemm_variant && !a_gather) ? g_gemm_variant : 2;  // the row gather needs the LDS-DMA ring
-  pl.stages = g_gemm_stages ? g_gemm_stages : ((K >= 1024 && pl.grid < 256) ? 3 : 2);
+  pl.stages = g_gemm_stages ? g_gemm_stages : ((K >= 1024 && pl.grid < 256) ? g_deep_stages : 2);
   // algorithmic bytes: weights + bias once; per routed row A (K), C (N) and the relu-mask operand (N)
   const bool has_bias = epilogue == MOE_EPI_BIAS || epilogue == MOE_EPI_BIAS_RELU;
   const double mask_bytes = epilogue == MOE_EPI_RELU_MASK ? 2.0 * N : (epilogue == MOE_EPI_RELU_MASK_MX ? 1.0 * N : 0.0);
@@ -1760,6 +1774,10 @@ extern "C" int moe_set_tuning(const char* key, int value) {
   const std::string k = key ? key : "";
   if (k == "gemm_variant" && value >= 0 && value <= 2) { g_gemm_variant = value; return 0; }
   if (k == "gemm_stages" && (value == 0 || (value >= 2 && value <= 4))) { g_gemm_stages = value; return 0; }
+  if (k == "deep_stages" && (value == 0 || value == 2 || value == 3 || value == 4 || value == 6)) {
+    g_deep_stages = value ? value : 3;  // (0: the default)
+    return 0;
+  }
   if (k == "gemm_debug" && value >= 0 && value <= 3) { g_gemm_debug = value; return 0; }
   if (k == "rows_bm" && (value == 0 || value == 64 || value == 128)) { g_rows_bm = value; return 0; }
   if (k == "wgrad_bm" && (value == 0 || value == 64 || value == 128)) { g_wgrad_bm = value; return 0; }

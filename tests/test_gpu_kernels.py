@@ -83,23 +83,26 @@ def _int_tensor(rng, shape, lo=-3, hi=4):
     return rng.integers(lo, hi, size=shape).astype(np.float64)
 
 
-# (gemm_variant, gemm_stages, ksplit); 0 = per-shape choice, ksplit 1 = no split-K
+# (gemm_variant, gemm_stages, ksplit[, deep_stages]); 0 = per-shape choice, ksplit 1 = no split-K;
+# deep_stages: the ring depth of long-K sub-chip row GEMMs (default 3)
 GEMM_CFGS = [(0, 0, 0), (0, 0, 1), (1, 2, 1), (2, 2, 1), (2, 3, 1), (2, 4, 1),
-             (1, 2, 2), (2, 2, 3), (2, 3, 4), (1, 2, 5)]
+             (1, 2, 2), (2, 2, 3), (2, 3, 4), (1, 2, 5), (0, 0, 1, 4), (0, 0, 1, 6)]
 
 
 @pytest.fixture
 def gemm_cfg(request, hip_lib):
     from src.moe import _lib as L
 
-    v, s, ks = request.param
+    v, s, ks, *deep = request.param
     L.set_tuning("gemm_variant", v)
     L.set_tuning("gemm_stages", s)
     L.set_tuning("ksplit", ks)
+    L.set_tuning("deep_stages", deep[0] if deep else 3)
     yield request.param
     L.set_tuning("gemm_variant", 0)  # back to the per-shape choice
     L.set_tuning("gemm_stages", 0)
     L.set_tuning("ksplit", 0)
+    L.set_tuning("deep_stages", 3)
     # split-K arrival counters are left at zero by every launch
     torch.cuda.synchronize()
     for _ws, cnt in L._SPLIT_WS.values():
