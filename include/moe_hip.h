@@ -299,6 +299,19 @@ int rtdetr_linear_wgrad_batch(int n, const void* const* gy, const void* const* x
 int rtdetr_linear_wgrad_narrow_parts(int K, int M, int N);
 int rtdetr_linear_wgrad_narrow(const void* gy, const void* x, void* dw, void* db, float* part, int K, int M, int N,
                                int out_bf16, hipStream_t stream);
+/* Batched (linear.DeferredWgrad, after the backward): n <= 32 narrow problems
+ * q = (gy[q] [K[q], M[q]], x[q] [K[q], N[q]]) in n_groups consecutive groups
+ * (group g = the next group_count[g] problems, one shape), each group's dW /
+ * db the fixed-order sum over its problems (a head applied several times, the
+ * query position head once per decoder layer, gets its single gradient) into
+ * dw[g] / db[g].  Two launches for all (26 per C2 step before, two per head).
+ * part: rtdetr_linear_wgrad_narrow_batch_parts(n, K, M, N) floats (-1: a
+ * problem outside the narrow shapes), 8-byte aligned. */
+long long rtdetr_linear_wgrad_narrow_batch_parts(int n, const int* K, const int* M, const int* N);
+int rtdetr_linear_wgrad_narrow_batch(int n, const void* const* gy, const void* const* x, const int* K, const int* M,
+                                     const int* N, int n_groups, const int* group_count, void* const* dw,
+                                     void* const* db, float* part, long long part_floats, int out_bf16,
+                                     hipStream_t stream);
 /* a7: one backward step of an expert weight in ONE launch --
  *   dgrad: C[r, n] = epi( s_r sum_k A(r, k) B_g[k][n] )   (trans_b = 0; epilogue
  *          NONE / RELU_MASK / RELU_MASK_MX with aux); A(r, .) = a[a_gather[r]]

@@ -111,15 +111,15 @@ constexpr int kNwU = 16;    // x rows in flight
 // stores its [m, n] sums transposed and takes the bias partial from the
 // streamed operand's column sums.
 template <int kNwMT, bool TR>  // outputs (m) per wave: 4 (M <= 4) or 16
-__global__ __launch_bounds__(64) void narrow_wgrad_part_kernel(const uint16_t* __restrict__ gy,
-                                                               const uint16_t* __restrict__ x, int K, int M, int N,
-                                                               int R, float* __restrict__ part) {
+__device__ __forceinline__ void narrow_wgrad_part_body(const uint16_t* __restrict__ gy,
+                                                       const uint16_t* __restrict__ x, int K, int M, int N, int R,
+                                                       float* __restrict__ part, int bx, int by, int bz) {
   __shared__ float s_g[64][kNwMT];
   __shared__ float s_db[64];
   const int lane = threadIdx.x;
-  const int n = blockIdx.x * kNwCB + 2 * lane;
-  const int m0 = blockIdx.y * kNwMT;
-  const int s = blockIdx.z;
+  const int n = bx * kNwCB + 2 * lane;
+  const int m0 = by * kNwMT;
+  const int s = bz;
   const int k0 = s * R;
   const int k1 = min(K, k0 + R);
   const bool ncol = n < N;
@@ -174,9 +174,9 @@ __global__ __launch_bounds__(64) void narrow_wgrad_part_kernel(const uint16_t* _
           *reinterpret_cast<float2*>(ps + (size_t)(m0 + m) * N + n) = make_float2(acc[m][0], acc[m][1]);
         }
       }
-    if (TR && blockIdx.y == 0) *reinterpret_cast<float2*>(ps + (size_t)M * N + n) = make_float2(xs0, xs1);
+    if (TR && by == 0) *reinterpret_cast<float2*>(ps + (size_t)M * N + n) = make_float2(xs0, xs1);
   }
-  if (!TR && blockIdx.x == 0) {  // bias partial: the 64 / kNwMT lanes of each column, fixed order
+  if (!TR && bx == 0) {  // bias partial: the 64 / kNwMT lanes of each column, fixed order
     s_db[lane] = dbs;
     __syncthreads();
     if (lane < kNwMT && m0 + lane < M) {
@@ -184,6 +184,84 @@ __global__ __launch_bounds__(64) void narrow_wgrad_part_kernel(const uint16_t* _
       for (int j = lane; j < 64; j += kNwMT) t += s_db[j];
       ps[(size_t)M * N + m0 + lane] = t;
     }
+  }
+}
+
+template <int kNwMT, bool TR>
+__global__ __launch_bounds__(64) void narrow_wgrad_part_kernel(const uint16_t* __restrict__ gy,
+                                                               const uint16_t* __restrict__ x, int K, int M, int N,
+                                                               int R, float* __restrict__ part) {
+  narrow_wgrad_part_body<kNwMT, TR>(gy, x, K, M, N, R, part, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// Batched narrow weight gradients (the decoder's score / box / query-position
+// heads after the backward, linear.DeferredWgrad): problem q (the kernel's
+// orientation: narrow side Mk, streamed side Nk) owns blocks [base[q],
+// base[q+1]) of one launch; groups g sum the partial slices of their member
+// problems (a weight applied several times -- the shared query-position head
+// -- gets one gradient, fixed problem then slice order: deterministic).
+constexpr int kNbMax = 32;
+struct NarrowBatch {
+  const uint16_t* g[kNbMax];  // the kernel's narrow operand (gy, or x when transposed)
+  const uint16_t* x[kNbMax];  // the streamed operand
+  long long poff[kNbMax];     // float offset of the problem's slices in part
+  int K[kNbMax], Mk[kNbMax], Nk[kNbMax], R[kNbMax], S[kNbMax], base[kNbMax + 1];
+  unsigned char mt4[kNbMax], tr[kNbMax];
+  int n;
+};
+struct NarrowGroups {
+  void* dw[kNbMax];
+  void* db[kNbMax];
+  int M[kNbMax], N[kNbMax];  // the layer's outputs / inputs (dW [M][N], db [M])
+  int first[kNbMax], count[kNbMax], base[kNbMax + 1];
+  int n, out_bf16;
+};
+
+__global__ __launch_bounds__(64) void narrow_wgrad_part_batch_kernel(NarrowBatch b, float* __restrict__ part) {
+  int q = 0;
+  while (q + 1 < b.n && (int)blockIdx.x >= b.base[q + 1]) ++q;
+  const int local = blockIdx.x - b.base[q];
+  const int gx = (b.Nk[q] + kNwCB - 1) / kNwCB, gy = b.mt4[q] ? 1 : (b.Mk[q] + 15) / 16;
+  const int bx = local % gx, by = (local / gx) % gy, bz = local / (gx * gy);
+  float* pp = part + b.poff[q];
+  if (b.mt4[q]) {
+    if (b.tr[q]) narrow_wgrad_part_body<4, true>(b.g[q], b.x[q], b.K[q], b.Mk[q], b.Nk[q], b.R[q], pp, bx, by, bz);
+    else narrow_wgrad_part_body<4, false>(b.g[q], b.x[q], b.K[q], b.Mk[q], b.Nk[q], b.R[q], pp, bx, by, bz);
+  } else {
+    if (b.tr[q]) narrow_wgrad_part_body<16, true>(b.g[q], b.x[q], b.K[q], b.Mk[q], b.Nk[q], b.R[q], pp, bx, by, bz);
+    else narrow_wgrad_part_body<16, false>(b.g[q], b.x[q], b.K[q], b.Mk[q], b.Nk[q], b.R[q], pp, bx, by, bz);
+  }
+}
+
+// one block per 32 outputs of a group: 8 slice lanes, the group's problems in
+// order, each problem's slices in order, then a fixed 8-lane sum
+__global__ __launch_bounds__(256) void narrow_wgrad_final_batch_kernel(NarrowBatch b, NarrowGroups gr,
+                                                                       const float* __restrict__ part) {
+  __shared__ float s_acc[8][32];
+  int g = 0;
+  while (g + 1 < gr.n && (int)blockIdx.x >= gr.base[g + 1]) ++g;
+  const size_t MN = (size_t)gr.M[g] * gr.N[g], NB = gr.M[g];
+  const size_t Q = (MN + NB + 1) & ~(size_t)1;
+  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
+  const size_t c = (size_t)(blockIdx.x - gr.base[g]) * 32 + cl;
+  float t = 0.f;
+  if (c < MN + NB) {
+    for (int j = 0; j < gr.count[g]; ++j) {
+      const int q = gr.first[g] + j;
+      const float* pp = part + b.poff[q];
+      for (int p = pl; p < b.S[q]; p += 8) t += pp[(size_t)p * Q + c];
+    }
+  }
+  s_acc[pl][cl] = t;
+  __syncthreads();
+  if (pl == 0 && c < MN + NB) {
+    float r = 0.f;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) r += s_acc[l][cl];
+    void* out = c < MN ? gr.dw[g] : gr.db[g];
+    const size_t i = c < MN ? c : c - MN;
+    if (gr.out_bf16) static_cast<uint16_t*>(out)[i] = f2bf(r);
+    else static_cast<float*>(out)[i] = r;
   }
 }
 
@@ -285,6 +363,97 @@ extern "C" int rtdetr_linear_wgrad_narrow(const void* gy, const void* x, void* d
   hipLaunchKernelGGL(narrow_wgrad_final_kernel, dim3((unsigned)((MN + M + 31) / 32)), dim3(256), 0, stream, part, S,
                      MN, M, dw, db, out_bf16);
   return check_launch("rtdetr_linear_wgrad_narrow(final)");
+}
+
+// Batched: problems q = (gy [K][M], x [K][N]) in groups (consecutive problems
+// of one group share M, N and the outputs dw [M][N], db [M]).  part: at least
+// rtdetr_linear_wgrad_narrow_batch_parts floats.  Two launches for all.
+static int narrow_batch_setup(int n, const int* K, const int* M, const int* N, const void* const* gy,
+                              const void* const* x, NarrowBatch& b, long long& floats) {
+  if (n < 1 || n > kNbMax) return fail("rtdetr_linear_wgrad_narrow_batch: 1..32 problems");
+  b = NarrowBatch{};
+  b.n = n;
+  floats = 0;
+  int blocks = 0;
+  for (int q = 0; q < n; ++q) {
+    const bool tr = narrow_tr(M[q], N[q]);
+    const int Mk = tr ? N[q] : M[q], Nk = tr ? M[q] : N[q];
+    if (K[q] <= 0 || Mk <= 0 || Nk <= 0 || Mk > 128 || Nk % 2 != 0 || Nk > 4096)
+      return fail("rtdetr_linear_wgrad_narrow_batch: a problem outside the narrow shapes");
+    b.tr[q] = tr;
+    b.mt4[q] = Mk <= 4;
+    b.Mk[q] = Mk;
+    b.Nk[q] = Nk;
+    b.K[q] = K[q];
+    b.R[q] = narrow_rows(K[q], Mk, Nk);
+    b.S[q] = (K[q] + b.R[q] - 1) / b.R[q];
+    if (gy != nullptr) {
+      b.g[q] = static_cast<const uint16_t*>(tr ? x[q] : gy[q]);
+      b.x[q] = static_cast<const uint16_t*>(tr ? gy[q] : x[q]);
+      if (b.g[q] == nullptr || b.x[q] == nullptr || (reinterpret_cast<uintptr_t>(b.x[q]) & 3))
+        return fail("rtdetr_linear_wgrad_narrow_batch: null or misaligned operand");
+    }
+    b.poff[q] = floats;
+    floats += (long long)b.S[q] * (((long long)M[q] * N[q] + M[q] + 1) & ~1LL);
+    floats = (floats + 1) & ~1LL;
+    b.base[q] = blocks;
+    blocks += ((Nk + kNwCB - 1) / kNwCB) * (Mk <= 4 ? 1 : (Mk + 15) / 16) * b.S[q];
+  }
+  b.base[n] = blocks;
+  return 0;
+}
+
+extern "C" long long rtdetr_linear_wgrad_narrow_batch_parts(int n, const int* K, const int* M, const int* N) {
+  NarrowBatch b;
+  long long floats = 0;
+  if (narrow_batch_setup(n, K, M, N, nullptr, nullptr, b, floats)) return -1;
+  return floats;
+}
+
+extern "C" int rtdetr_linear_wgrad_narrow_batch(int n, const void* const* gy, const void* const* x, const int* K,
+                                                const int* M, const int* N, int n_groups, const int* group_count,
+                                                void* const* dw, void* const* db, float* part, long long part_floats,
+                                                int out_bf16, hipStream_t stream) {
+  if (gy == nullptr || x == nullptr || K == nullptr || M == nullptr || N == nullptr || group_count == nullptr ||
+      dw == nullptr || db == nullptr || part == nullptr || (reinterpret_cast<uintptr_t>(part) & 7))
+    return fail("rtdetr_linear_wgrad_narrow_batch: null pointer or misaligned part");
+  NarrowBatch b;
+  long long floats = 0;
+  if (int rc = narrow_batch_setup(n, K, M, N, gy, x, b, floats)) return rc;
+  if (floats > part_floats) return fail("rtdetr_linear_wgrad_narrow_batch: part too small");
+  if (n_groups < 1 || n_groups > n) return fail("rtdetr_linear_wgrad_narrow_batch: bad group count");
+  NarrowGroups gr{};
+  gr.n = n_groups;
+  gr.out_bf16 = out_bf16;
+  int q = 0, blocks = 0;
+  double bytes = 0.0, flops = 0.0;
+  for (int g = 0; g < n_groups; ++g) {
+    if (group_count[g] < 1 || q + group_count[g] > n) return fail("rtdetr_linear_wgrad_narrow_batch: bad groups");
+    for (int j = 1; j < group_count[g]; ++j)
+      if (M[q + j] != M[q] || N[q + j] != N[q]) return fail("rtdetr_linear_wgrad_narrow_batch: group shapes differ");
+    if (dw[g] == nullptr || db[g] == nullptr) return fail("rtdetr_linear_wgrad_narrow_batch: null output");
+    gr.dw[g] = dw[g];
+    gr.db[g] = db[g];
+    gr.M[g] = M[q];
+    gr.N[g] = N[q];
+    gr.first[g] = q;
+    gr.count[g] = group_count[g];
+    gr.base[g] = blocks;
+    blocks += (int)(((size_t)M[q] * N[q] + M[q] + 31) / 32);
+    for (int j = 0; j < group_count[g]; ++j) {
+      bytes += 2.0 * K[q + j] * (M[q + j] + N[q + j]);
+      flops += 2.0 * K[q + j] * M[q + j] * N[q + j];
+    }
+    q += group_count[g];
+  }
+  if (q != n) return fail("rtdetr_linear_wgrad_narrow_batch: groups do not cover the problems");
+  gr.base[n_groups] = blocks;
+  ProfScope prof(stream, PROF_LINEAR, bytes + 8.0 * floats, false, 0.0, flops);
+  MOE_LAUNCH(prof, narrow_wgrad_part_batch_kernel, dim3((unsigned)b.base[n]), dim3(64), 0, stream, b, part);
+  if (int rc = check_launch("rtdetr_linear_wgrad_narrow_batch(part)")) return rc;
+  hipLaunchKernelGGL(narrow_wgrad_final_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, b, gr,
+                     static_cast<const float*>(part));
+  return check_launch("rtdetr_linear_wgrad_narrow_batch(final)");
 }
 
 extern "C" int rtdetr_bias_grad_parts(long long M, int N) {

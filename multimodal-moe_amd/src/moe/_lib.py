@@ -44,6 +44,9 @@ SIGNATURES = {
     "rtdetr_linear_wgrad_batch": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "rtdetr_linear_wgrad_narrow_parts": (_I, [_I, _I, _I]),
     "rtdetr_linear_wgrad_narrow": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "rtdetr_linear_wgrad_narrow_batch_parts": (ctypes.c_longlong, [_I, _P, _P, _P]),
+    "rtdetr_linear_wgrad_narrow_batch": (_I, [_I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, ctypes.c_longlong, _I,
+                                              _P]),
     "moe_route_index": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "moe_route_dispatch": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P]),
     "moe_grouped_gemm_gather": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
@@ -807,6 +810,59 @@ def linear_wgrad_narrow(gy, x, out_dtype):
 
 
 LINEAR_WGRAD_BATCH = 24  # problems per rtdetr_linear_wgrad_batch launch
+
+
+NARROW_BATCH = 32  # problems per rtdetr_linear_wgrad_narrow_batch launch pair
+
+
+def linear_wgrad_narrow_batch(groups, out_dtype):
+    """Narrow dense weight + bias gradients, batched: groups = [([(gy bf16
+    [K, M], x bf16 [K, N]), ...], dw [M, N], db [M])] -- each group's outputs
+    the sum over its problems (contiguous out_dtype tensors)."""
+    if out_dtype not in (torch.float32, torch.bfloat16):
+        raise MoEKernelError("linear_wgrad_narrow_batch: out_dtype must be float32 or bfloat16")
+    chunk, n = [], 0
+    for grp in groups + [None]:
+        if grp is None or n + len(grp[0]) > NARROW_BATCH:
+            if chunk:
+                _narrow_batch_launch(chunk, out_dtype)
+            chunk, n = [], 0
+            if grp is None:
+                break
+        if len(grp[0]) > NARROW_BATCH:
+            raise MoEKernelError("linear_wgrad_narrow_batch: a group of more than 32 problems")
+        chunk.append(grp)
+        n += len(grp[0])
+
+
+def _narrow_batch_launch(groups, out_dtype):
+    probs = [pr for g in groups for pr in g[0]]
+    n, ng = len(probs), len(groups)
+    gys, xs = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)()
+    Ks, Ms, Ns = (ctypes.c_int * n)(), (ctypes.c_int * n)(), (ctypes.c_int * n)()
+    for q, (gy, x) in enumerate(probs):
+        _need(gy, torch.bfloat16, "gy")
+        _need(x, torch.bfloat16, "x")
+        if gy.dim() != 2 or x.dim() != 2 or gy.shape[0] != x.shape[0] or not (gy.is_contiguous() and x.is_contiguous()):
+            raise MoEKernelError("linear_wgrad_narrow_batch: gy [K, M] and x [K, N] contiguous")
+        gys[q], xs[q] = gy.data_ptr(), x.data_ptr()
+        Ks[q], Ms[q], Ns[q] = int(gy.shape[0]), int(gy.shape[1]), int(x.shape[1])
+    cnt = (ctypes.c_int * ng)(*[len(g[0]) for g in groups])
+    dws, dbs = (ctypes.c_void_p * ng)(), (ctypes.c_void_p * ng)()
+    for g, (_, dw, db) in enumerate(groups):
+        if dw.dtype != out_dtype or db.dtype != out_dtype or not (dw.is_contiguous() and db.is_contiguous()):
+            raise MoEKernelError("linear_wgrad_narrow_batch: dw / db must be contiguous out_dtype tensors")
+        dws[g], dbs[g] = dw.data_ptr(), db.data_ptr()
+    floats = int(lib().rtdetr_linear_wgrad_narrow_batch_parts(n, ctypes.cast(Ks, ctypes.c_void_p),
+                                                               ctypes.cast(Ms, ctypes.c_void_p),
+                                                               ctypes.cast(Ns, ctypes.c_void_p)))
+    if floats < 0:
+        raise MoEKernelError("linear_wgrad_narrow_batch: a problem outside the narrow shapes")
+    part = torch.empty(max(floats, 2), dtype=torch.float32, device=probs[0][0].device)
+    c = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+    _check(lib().rtdetr_linear_wgrad_narrow_batch(n, c(gys), c(xs), c(Ks), c(Ms), c(Ns), ng, c(cnt), c(dws), c(dbs),
+                                                  part.data_ptr(), floats, int(out_dtype == torch.bfloat16),
+                                                  _stream()), "rtdetr_linear_wgrad_narrow_batch")
 
 
 def linear_wgrad_batch(jobs, out_dtype):

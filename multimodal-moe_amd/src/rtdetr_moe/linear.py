@@ -26,6 +26,9 @@ DENSE_WGRAD_ROWS = [512]  # from this many rows, conforming shapes use libmoe_hi
 # GraphedStep defers conforming dense weight gradients to one batched launch
 # after the backward (MOE_DEFER_WGRAD=0: one launch per layer, as before)
 DEFER_WGRAD = [os.environ.get("MOE_DEFER_WGRAD", "1") != "0"]
+# the narrow heads' gradients deferred too, batched into one launch pair
+# (MOE_NARROW_DEFER=0: one launch pair per head, as before)
+NARROW_DEFER = [os.environ.get("MOE_NARROW_DEFER", "1") != "0"]
 _ACTIVE: list = [None]  # the DeferredWgrad collecting during a backward, or None
 
 
@@ -58,15 +61,43 @@ class DeferredWgrad:
 
     def __init__(self):
         self.items = []  # (gy, x, out dtype, (weight leaf, row), (bias leaf, row))
+        self.narrow = []  # the same for narrow heads (rtdetr_linear_wgrad_narrow_batch)
 
     def add(self, gy, x, odt, wt, bt):
         self.items.append((gy, x, odt, wt, bt))
+
+    def add_narrow(self, gy, x, odt, wt, bt):
+        self.narrow.append((gy, x, odt, wt, bt))
+
+    def _flush_narrow(self):
+        """The narrow heads' gradients in one launch pair per 32 problems: a
+        head applied several times (the query position head, once per decoder
+        layer) is one group whose gradient sums its uses in fp32 (rounded
+        once), instead of one gradient per use summed by autograd."""
+        from ..moe import _lib as L
+
+        keys = {}
+        for gy, x, odt, (wp, _), (bp, _) in self.narrow:
+            k = (id(wp), id(bp), odt)
+            if k not in keys:
+                keys[k] = [wp, bp, odt, []]
+            keys[k][3].append((gy, x))
+        self.narrow = []
+        out, by_dtype = {}, {}
+        for wp, bp, odt, probs in keys.values():
+            dw = torch.empty(wp.shape, dtype=odt, device=wp.device)
+            db = torch.empty(bp.shape, dtype=odt, device=wp.device)
+            by_dtype.setdefault(odt, []).append((probs, dw, db))
+            out[id(wp)], out[id(bp)] = dw, db
+        for odt, groups in by_dtype.items():
+            L.linear_wgrad_narrow_batch(groups, odt)
+        return out
 
     def flush(self):
         from ..moe import _lib as L
 
         if not self.items:
-            return {}
+            return self._flush_narrow() if self.narrow else {}
         # a parameter whose rows receive more than one layer's gradient (a
         # layer applied several times, e.g. a shared head) is summed in fp32
         # and rounded once; the others are written in place, in their dtype
@@ -147,6 +178,9 @@ class DeferredWgrad:
             grads[kw] = bw.sum(0).to(odt)
             grads[kb] = bb.sum(0).to(odt)
         self.items.clear()
+        if self.narrow:
+            for k, g in self._flush_narrow().items():
+                grads[k] = g if k not in grads else grads[k] + g.to(grads[k].dtype)
         return grads
 
 
@@ -259,6 +293,11 @@ def _linear_wgrad(g2, x2, weight_dtype, bias_dtype, has_bias, need_w, need_b, ta
         from ..moe import _lib as L
 
         odt = torch.bfloat16 if weight_dtype == torch.bfloat16 else torch.float32
+        if (_ACTIVE[0] is not None and targets is not None and weight_dtype == odt and NARROW_DEFER[0]
+                and targets[0][1] == 0 and targets[1][1] == 0 and M == targets[0][0].shape[0]
+                and M == targets[1][0].shape[0] and g2.is_contiguous()):
+            _ACTIVE[0].add_narrow(g2, x2, odt, *targets)  # batched after the backward
+            return None, None
         gw, gb = L.linear_wgrad_narrow(g2, x2, odt)
         return gw, gb.to(bias_dtype)
     gw = gb = None

@@ -166,3 +166,36 @@ def test_grad_slot_two_conv_consumers(hip_lib):
         res.append((x.grad.float().clone(), ca.weight.grad.clone(), cb.weight.grad.clone()))
     assert float((res[0][0] - res[1][0]).norm() / res[1][0].norm()) < 4e-3
     assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+
+
+def test_narrow_heads_batched_after_backward(hip_lib, monkeypatch):
+    """linear.DeferredWgrad's narrow heads (score head M = 1, box-head last
+    layer M = 4, the query-position head's 4 -> 512 layer applied three times)
+    in one rtdetr_linear_wgrad_narrow_batch launch pair == one
+    rtdetr_linear_wgrad_narrow call per use summed by autograd, at bf16
+    rounding (the batched sum is fp32, rounded once)."""
+    from src.rtdetr_moe import linear as lin
+    from src.rtdetr_moe.decoder import MLP
+
+    torch.manual_seed(6)
+    score = lin.TokenLinear(256, 1).to(DEV).to(torch.bfloat16)
+    box = MLP(256, 256, 4, 3).to(DEV).to(torch.bfloat16)
+    qpos = MLP(4, 512, 256, 2).to(DEV).to(torch.bfloat16)
+    for m in list(box.layers) + list(qpos.layers):
+        torch.nn.init.normal_(m.weight, std=0.05)
+    params = list(score.parameters()) + list(box.parameters()) + list(qpos.parameters())
+    t0 = torch.randn(2400, 256, device=DEV).to(torch.bfloat16)
+    refs = [torch.rand(2400, 4, device=DEV).to(torch.bfloat16) for _ in range(3)]
+    res = []
+    for defer in (True, False):
+        monkeypatch.setattr(lin, "NARROW_DEFER", [defer])
+        t = t0.clone().requires_grad_(True)
+        loss = (score(t).float() ** 2).sum() + (box(t).float() ** 2).sum()
+        for r in refs:
+            loss = loss + (qpos(r).float() * t.float()).sum()
+        with lin.deferred_weight_grads() as d:
+            grads = torch.autograd.grad(loss, params, allow_unused=True)
+        grads = lin.merge_deferred(params, grads, d)
+        res.append([g.float() for g in grads])
+    for a, b in zip(res[0], res[1]):
+        assert float((a - b).norm() / b.norm().clamp_min(1e-12)) < 1e-2

@@ -331,8 +331,9 @@ def test_whole_step_deferred_weight_grads(hip_lib, precision):
     loss, _ = gs._loss()
     with linear.deferred_weight_grads() as d:
         grads = torch.autograd.grad(loss, gs.params, allow_unused=True)
-    items = list(d.items)
-    assert len(items) == gs.deferred_layers
+    assert len(d.items) == gs.deferred_layers
+    items = list(d.items) + list(d.narrow)  # (+ the narrow heads, batched by rtdetr_linear_wgrad_narrow_batch)
+    assert len(d.narrow) > 0
     merged = linear.merge_deferred(gs.params, grads, d)
     # per element: fp32 accumulation (1e-5 of sum |terms|) plus, for bf16
     # outputs, one rounding of each layer's partial and one of their sum (a
