@@ -554,6 +554,13 @@ int rtdetr_add_layer_norm_pos_fwd(const void* a, const void* b, const void* gamm
 int rtdetr_add_layer_norm_bwd2(const void* dout, const void* dout2, const void* a, const void* b, const void* gamma,
                                int w_bf16, const float* mean, const float* rstd, long long T, int d, void* ds,
                                float* partials, int P, void* dgamma_dbeta, hipStream_t stream);
+/* bwd / bwd2 with dgamma_dbeta NULL stop after the row pass (partials
+ * written, no final); the finals of many LayerNorms then run as ONE launch
+ * after the backward (linear.DeferredWgrad): problem q sums its P[q] <= 256
+ * partial rows of N[q] = 2d columns into out[q] ([dgamma; dbeta], bf16 when
+ * out_bf16[q]), the same fixed order as the single final.  n <= 48. */
+int rtdetr_add_layer_norm_final_batch(int n, const float* const* partials, const int* P, const int* N,
+                                      void* const* out, const int* out_bf16, hipStream_t stream);
 
 /* Decoder box refinement (one launch each way), over n = B*Q*4 elements:
  *   y = sigmoid(delta + log(max(x', eps) / max(1 - x', eps))), x' = clamp(ref, 0, 1)

@@ -222,6 +222,44 @@ __global__ __launch_bounds__(256) void add_ln_final_kernel(const float* __restri
   }
 }
 
+// Batched finals (linear.DeferredWgrad after the backward): problem q sums its
+// P[q] partial rows of N[q] columns into out[q]; blocks [base[q], base[q+1]).
+constexpr int kLnFinMax = 48;
+struct LnFinalBatch {
+  const float* part[kLnFinMax];
+  void* out[kLnFinMax];
+  int P[kLnFinMax], N[kLnFinMax], bf16[kLnFinMax], base[kLnFinMax + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void add_ln_final_batch_kernel(LnFinalBatch b) {
+  __shared__ float s_acc[16][17];
+  int q = 0;
+  while (q + 1 < b.n && (int)blockIdx.x >= b.base[q + 1]) ++q;
+  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  const int n = (blockIdx.x - b.base[q]) * 16 + cl;
+  const int P = b.P[q], N = b.N[q];
+  const float* partials = b.part[q];
+  float v[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int p = pl + 16 * u;
+    v[u] = (n < N && p < P) ? partials[(size_t)p * N + n] : 0.f;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) s += v[u];
+  s_acc[pl][cl] = s;
+  __syncthreads();
+  if (pl == 0 && n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) t += s_acc[l][cl];
+    if (b.bf16[q]) static_cast<uint16_t*>(b.out[q])[n] = f2bf(t);
+    else static_cast<float*>(b.out[q])[n] = t;
+  }
+}
+
 }  // namespace moe
 
 using namespace moe;
@@ -290,9 +328,8 @@ extern "C" int rtdetr_add_layer_norm_bwd2(const void* dout, const void* dout2, c
                                           hipStream_t stream) {
   const void* bwd_ops[5] = {dout, ds, partials, dgamma_dbeta, dout2};
   if (add_ln_check(a, b, gamma, T, d, "add_layer_norm_bwd", bwd_ops, 5)) return -1;
-  if (dout == nullptr || mean == nullptr || rstd == nullptr || ds == nullptr || partials == nullptr ||
-      dgamma_dbeta == nullptr)
-    return fail("add_layer_norm_bwd: dout, mean, rstd, ds, partials and dgamma_dbeta are required");
+  if (dout == nullptr || mean == nullptr || rstd == nullptr || ds == nullptr || partials == nullptr)
+    return fail("add_layer_norm_bwd: dout, mean, rstd, ds and partials are required");
   if (P != rtdetr_add_layer_norm_parts(T)) return fail("add_layer_norm_bwd: P must be rtdetr_add_layer_norm_parts(T)");
   // bytes: dout, a (+ b) read, ds written, per-row statistics, partials out and back, [dgamma; dbeta]
   ProfScope prof(stream, PROF_CONV_EPI,
@@ -313,10 +350,34 @@ extern "C" int rtdetr_add_layer_norm_bwd2(const void* dout, const void* dout2, c
   }
 #undef LNB
   int rc = check_launch("rtdetr_add_layer_norm_bwd");
-  if (rc != 0) return rc;
+  if (rc != 0 || dgamma_dbeta == nullptr) return rc;  // (NULL: the partials stay for a batched final)
   hipLaunchKernelGGL(add_ln_final_kernel, dim3((2 * d + 15) / 16), dim3(256), 0, stream, partials, P, 2 * d,
                      dgamma_dbeta, w_bf16);
   return check_launch("rtdetr_add_layer_norm_bwd(final)");
+}
+
+extern "C" int rtdetr_add_layer_norm_final_batch(int n, const float* const* partials, const int* P, const int* N,
+                                                 void* const* out, const int* out_bf16, hipStream_t stream) {
+  if (n < 1 || n > kLnFinMax || partials == nullptr || P == nullptr || N == nullptr || out == nullptr ||
+      out_bf16 == nullptr)
+    return fail("rtdetr_add_layer_norm_final_batch: 1..48 problems, non-NULL arrays");
+  LnFinalBatch b{};
+  b.n = n;
+  int blocks = 0;
+  for (int q = 0; q < n; ++q) {
+    if (partials[q] == nullptr || out[q] == nullptr || P[q] < 1 || P[q] > 256 || N[q] < 1)
+      return fail("rtdetr_add_layer_norm_final_batch: bad problem");
+    b.part[q] = partials[q];
+    b.out[q] = out[q];
+    b.P[q] = P[q];
+    b.N[q] = N[q];
+    b.bf16[q] = out_bf16[q];
+    b.base[q] = blocks;
+    blocks += (N[q] + 15) / 16;
+  }
+  b.base[n] = blocks;
+  hipLaunchKernelGGL(add_ln_final_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, b);
+  return check_launch("rtdetr_add_layer_norm_final_batch");
 }
 
 extern "C" int rtdetr_add_layer_norm_bwd(const void* dout, const void* a, const void* b, const void* gamma,

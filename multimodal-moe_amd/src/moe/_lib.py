@@ -87,6 +87,7 @@ SIGNATURES = {
     "rtdetr_add_layer_norm_bwd": (_I, [_P, _P, _P, _P, _I, _P, _P, ctypes.c_longlong, _I, _P, _P, _I, _P, _P]),
     "rtdetr_add_layer_norm_pos_fwd": (_I, [_P, _P, _P, _P, _I, ctypes.c_longlong, _I, _F, _P, _P, _P, _P, _P, _P]),
     "rtdetr_add_layer_norm_bwd2": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, ctypes.c_longlong, _I, _P, _P, _I, _P, _P]),
+    "rtdetr_add_layer_norm_final_batch": (_I, [_I, _P, _P, _P, _P, _P, _P]),
     "rtdetr_box_refine_fwd": (_I, [_P, _I, _P, ctypes.c_longlong, _F, _P, _P]),
     "rtdetr_box_refine_bwd": (_I, [_P, _P, _P, _P, ctypes.c_longlong, _F, _P, _I, _P, _P]),
     "rtdetr_msda_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
@@ -810,6 +811,29 @@ def linear_wgrad_narrow(gy, x, out_dtype):
 
 
 LINEAR_WGRAD_BATCH = 24  # problems per rtdetr_linear_wgrad_batch launch
+
+
+LN_FINAL_BATCH = 48  # problems per rtdetr_add_layer_norm_final_batch launch
+
+
+def add_layer_norm_final_batch(jobs):
+    """[(partials fp32 [P, 2d], out [2, d] bf16 / fp32 contiguous)]: the
+    LayerNorms' [dgamma; dbeta] from their row-pass partials, batched."""
+    for i in range(0, len(jobs), LN_FINAL_BATCH):
+        part = jobs[i:i + LN_FINAL_BATCH]
+        n = len(part)
+        ps, outs = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)()
+        Ps, Ns, bf = (ctypes.c_int * n)(), (ctypes.c_int * n)(), (ctypes.c_int * n)()
+        for q, (pt, out) in enumerate(part):
+            _need(pt, torch.float32, "partials")
+            if out.dtype not in (torch.float32, torch.bfloat16) or not out.is_contiguous() or pt.dim() != 2 \
+                    or out.numel() != pt.shape[1] or not pt.is_contiguous():
+                raise MoEKernelError("add_layer_norm_final_batch: partials [P, 2d] and out [2, d] contiguous")
+            ps[q], outs[q] = pt.data_ptr(), out.data_ptr()
+            Ps[q], Ns[q], bf[q] = int(pt.shape[0]), int(pt.shape[1]), int(out.dtype == torch.bfloat16)
+        c = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+        _check(lib().rtdetr_add_layer_norm_final_batch(n, c(ps), c(Ps), c(Ns), c(outs), c(bf), _stream()),
+               "rtdetr_add_layer_norm_final_batch")
 
 
 NARROW_BATCH = 32  # problems per rtdetr_linear_wgrad_narrow_batch launch pair

@@ -62,9 +62,29 @@ class DeferredWgrad:
     def __init__(self):
         self.items = []  # (gy, x, out dtype, (weight leaf, row), (bias leaf, row))
         self.narrow = []  # the same for narrow heads (rtdetr_linear_wgrad_narrow_batch)
+        self.ln = []  # (row-pass partials fp32 [P, 2d], weight leaf, bias leaf): LayerNorm finals
 
     def add(self, gy, x, odt, wt, bt):
         self.items.append((gy, x, odt, wt, bt))
+
+    def add_ln(self, parts, w, b):
+        self.ln.append((parts, w, b))
+
+    def _flush_ln(self):
+        """Every deferred LayerNorm's [dgamma; dbeta] in one launch
+        (rtdetr_add_layer_norm_final_batch) instead of one final per norm."""
+        from ..moe import _lib as L
+
+        out, jobs = {}, []
+        for parts, w, b in self.ln:
+            dwb = torch.empty((2, w.shape[0]), dtype=w.dtype, device=parts.device)
+            jobs.append((parts, dwb))
+            for p_, g in ((w, dwb[0]), (b, dwb[1])):
+                out[id(p_)] = g if id(p_) not in out else out[id(p_)] + g  # (a norm applied twice)
+        self.ln = []
+        if jobs:
+            L.add_layer_norm_final_batch(jobs)
+        return out
 
     def add_narrow(self, gy, x, odt, wt, bt):
         self.narrow.append((gy, x, odt, wt, bt))
@@ -97,7 +117,10 @@ class DeferredWgrad:
         from ..moe import _lib as L
 
         if not self.items:
-            return self._flush_narrow() if self.narrow else {}
+            out = self._flush_narrow() if self.narrow else {}
+            if self.ln:
+                out.update(self._flush_ln())
+            return out
         # a parameter whose rows receive more than one layer's gradient (a
         # layer applied several times, e.g. a shared head) is summed in fp32
         # and rounded once; the others are written in place, in their dtype
@@ -178,9 +201,13 @@ class DeferredWgrad:
             grads[kw] = bw.sum(0).to(odt)
             grads[kb] = bb.sum(0).to(odt)
         self.items.clear()
+        extra = {}
         if self.narrow:
-            for k, g in self._flush_narrow().items():
-                grads[k] = g if k not in grads else grads[k] + g.to(grads[k].dtype)
+            extra.update(self._flush_narrow())
+        if self.ln:
+            extra.update(self._flush_ln())
+        for k, g in extra.items():
+            grads[k] = g if k not in grads else grads[k] + g.to(grads[k].dtype)
         return grads
 
 

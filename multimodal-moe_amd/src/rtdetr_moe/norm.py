@@ -19,6 +19,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..moe import _lib as L
+from . import linear as _LIN
 
 # MOE_FUSED_LN=0: torch's add + layer_norm instead (A/B switch)
 _FUSED_LN = os.environ.get("MOE_FUSED_LN", "1") != "0"
@@ -50,6 +51,7 @@ class _AddLayerNorm(torch.autograd.Function):
                  "rtdetr_add_layer_norm_fwd")
         ctx.save_for_backward(a, b if b is not None else torch.empty(0, device=a.device), w, mean, rstd)
         ctx.has_b = b is not None
+        ctx.leaves = (weight, bias)
         return out
 
     @staticmethod
@@ -63,12 +65,16 @@ class _AddLayerNorm(torch.autograd.Function):
         lib = L.lib()
         P = int(lib.rtdetr_add_layer_norm_parts(T))
         parts = torch.empty((P, 2 * d), dtype=torch.float32, device=a.device)
-        dwb = torch.empty((2, d), dtype=w.dtype, device=a.device)
+        defer = _defer_ln(ctx.leaves, w)
+        dwb = None if defer else torch.empty((2, d), dtype=w.dtype, device=a.device)
         L._check(lib.rtdetr_add_layer_norm_bwd(dout.data_ptr(), a.data_ptr(), b.data_ptr() if b is not None else None,
                                                w.data_ptr(), int(w.dtype == torch.bfloat16), mean.data_ptr(),
                                                rstd.data_ptr(), T, d, ds.data_ptr(), parts.data_ptr(), P,
-                                               dwb.data_ptr(), L._stream()),
+                                               None if defer else dwb.data_ptr(), L._stream()),
                  "rtdetr_add_layer_norm_bwd")
+        if defer:  # [dgamma; dbeta] from the partials after the backward, batched
+            _LIN._ACTIVE[0].add_ln(parts, *ctx.leaves)
+            return ds, (ds if ctx.has_b else None), None, None, None
         return ds, (ds if ctx.has_b else None), dwb[0], dwb[1], None
 
 
@@ -95,6 +101,7 @@ class _AddLayerNormPos(torch.autograd.Function):
                  "rtdetr_add_layer_norm_pos_fwd")
         ctx.save_for_backward(a, b, w, mean, rstd)
         ctx.set_materialize_grads(False)
+        ctx.leaves = (weight, bias)
         return out, out2
 
     @staticmethod
@@ -110,14 +117,32 @@ class _AddLayerNormPos(torch.autograd.Function):
         lib = L.lib()
         P = int(lib.rtdetr_add_layer_norm_parts(T))
         parts = torch.empty((P, 2 * d), dtype=torch.float32, device=a.device)
-        dwb = torch.empty((2, d), dtype=w.dtype, device=a.device)
+        defer = _defer_ln(ctx.leaves, w)
+        dwb = None if defer else torch.empty((2, d), dtype=w.dtype, device=a.device)
         L._check(lib.rtdetr_add_layer_norm_bwd2(g1.data_ptr(), g2.data_ptr() if g2 is not None else None,
                                                 a.data_ptr(), b.data_ptr(), w.data_ptr(),
                                                 int(w.dtype == torch.bfloat16), mean.data_ptr(), rstd.data_ptr(),
-                                                T, d, ds.data_ptr(), parts.data_ptr(), P, dwb.data_ptr(),
-                                                L._stream()),
+                                                T, d, ds.data_ptr(), parts.data_ptr(), P,
+                                                None if defer else dwb.data_ptr(), L._stream()),
                  "rtdetr_add_layer_norm_bwd2")
+        if defer:
+            _LIN._ACTIVE[0].add_ln(parts, *ctx.leaves)
+            return ds, ds, None, None, dout2, None
         return ds, ds, dwb[0], dwb[1], dout2, None
+
+
+# MOE_DEFER_LN=0: each LayerNorm's [dgamma; dbeta] final right after its row
+# pass (A/B switch; default: deferred into linear.DeferredWgrad's batched flush)
+_DEFER_LN = os.environ.get("MOE_DEFER_LN", "1") != "0"
+
+
+def _defer_ln(leaves, w) -> bool:
+    """Whether this backward parks its LayerNorm partials for the batched
+    final: inside a collecting backward (linear.deferred_weight_grads), leaf
+    gamma / beta of one dtype."""
+    wl, bl = leaves
+    return (_DEFER_LN and _LIN._ACTIVE[0] is not None and wl is not None and bl is not None and wl.is_leaf
+            and bl.is_leaf and wl.dtype == bl.dtype == w.dtype and wl.requires_grad and bl.requires_grad)
 
 
 # MOE_LN_POS=0: the decoder's t + pos as a separate add (A/B switch)

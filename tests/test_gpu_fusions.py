@@ -199,3 +199,63 @@ def test_narrow_heads_batched_after_backward(hip_lib, monkeypatch):
         res.append([g.float() for g in grads])
     for a, b in zip(res[0], res[1]):
         assert float((a - b).norm() / b.norm().clamp_min(1e-12)) < 1e-2
+
+
+@pytest.mark.parametrize("pos", [False, True])
+def test_layer_norm_finals_batched(hip_lib, pos):
+    """LayerNorm [dgamma; dbeta] deferred to rtdetr_add_layer_norm_final_batch
+    (one launch for every norm of the backward) == the per-norm final,
+    bitwise (same fixed-order sum); the row gradients unchanged."""
+    from src.rtdetr_moe import linear as lin
+    from src.rtdetr_moe import norm
+
+    torch.manual_seed(7)
+    lns = [norm.AddLayerNorm(256).to(DEV).to(torch.bfloat16) for _ in range(3)]
+    for m in lns:
+        m.weight.data.uniform_(0.5, 1.5)
+        m.bias.data.uniform_(-0.5, 0.5)
+    a0 = torch.randn(2400, 256, device=DEV).to(torch.bfloat16)
+    b0 = torch.randn(2400, 256, device=DEV).to(torch.bfloat16)
+    p0 = torch.randn(2400, 256, device=DEV).to(torch.bfloat16)
+    params = [t for m in lns for t in (m.weight, m.bias)]
+    res = []
+    for defer in (True, False):
+        a = a0.clone().requires_grad_(True)
+        x = a
+        for m in lns:
+            if pos:
+                t, q = m.with_pos(x, b0, p0)
+                x = t.float().sin().to(torch.bfloat16) + q
+            else:
+                x = m(x, b0)
+        loss = (x.float() ** 2).sum()
+        if defer:
+            with lin.deferred_weight_grads() as d:
+                grads = torch.autograd.grad(loss, params + [a], allow_unused=True)
+            assert len(d.ln) == 3 and all(g is None for g in grads[:-1])
+            grads = lin.merge_deferred(params + [a], grads, d)
+        else:
+            grads = torch.autograd.grad(loss, params + [a])
+        res.append([g.clone() for g in grads])
+    for g1, g2 in zip(res[0], res[1]):
+        assert torch.equal(g1, g2)
+
+
+def test_ranking_rows_overwrite_equals_mask(hip_lib):
+    """RTDETRDecoder._enc_output_masked (linear on memory, invalid-anchor rows
+    overwritten with the bias) == enc_output(valid * memory), bitwise."""
+    from src.rtdetr_moe.decoder import RTDETRDecoder
+
+    torch.manual_seed(8)
+    dec = RTDETRDecoder(num_layers=1).to(DEV).to(torch.bfloat16)
+    shapes = [(92, 160), (46, 80), (23, 40)]
+    S = sum(h * w for h, w in shapes)
+    anchors, valid = dec._anchors(shapes, torch.device(DEV), torch.float32)
+    inv = dec._anchor_cache[("inv", tuple(shapes), torch.device(DEV), torch.float32)]
+    assert 0 < inv.numel() < S
+    memory = torch.randn(2, S, 256, device=DEV).to(torch.bfloat16)
+    vmask = valid.to(memory.dtype)
+    with torch.no_grad():
+        ref = dec.enc_output(vmask * memory)
+        got = dec._enc_output_masked(memory, inv, vmask)
+    assert torch.equal(got, ref)

@@ -333,6 +333,7 @@ def test_whole_step_deferred_weight_grads(hip_lib, precision):
         grads = torch.autograd.grad(loss, gs.params, allow_unused=True)
     assert len(d.items) == gs.deferred_layers
     items = list(d.items) + list(d.narrow)  # (+ the narrow heads, batched by rtdetr_linear_wgrad_narrow_batch)
+    d.ln_saved = list(d.ln)
     assert len(d.narrow) > 0
     merged = linear.merge_deferred(gs.params, grads, d)
     # per element: fp32 accumulation (1e-5 of sum |terms|) plus, for bf16
@@ -347,7 +348,12 @@ def test_whole_step_deferred_weight_grads(hip_lib, precision):
             ref.setdefault(id(p_), z(p_, gy.device))[r0:r0 + M] += val
             tol.setdefault(id(p_), z(p_, gy.device))[r0:r0 + M] += bound
             mag.setdefault(id(p_), z(p_, gy.device))[r0:r0 + M] += val.abs()
+    ln_ids = {id(t) for _, w, b in d.ln_saved for t in (w, b)}  # (the LayerNorm finals, batched too)
+    assert len(ln_ids) > 0
     for p, g, m in zip(gs.params, grads, merged):
+        if id(p) in ln_ids:
+            assert g is None and m is not None and m.shape == p.shape and bool(torch.isfinite(m).all())
+            continue
         if id(p) not in ref:
             assert m is g
             continue

@@ -30,7 +30,7 @@ import bench  # noqa: E402  (WORKLOADS, build_model)
 WATCH = ("add", "add_", "cat", "copy_", "mul", "mul_", "fill_", "zero_", "clone", "_to_copy", "index_add_",
          "scatter_add_", "scatter_add", "index_put_", "sub", "where", "threshold_backward", "new_zeros", "zeros_like",
          "sum", "div", "neg", "slice_backward", "select_backward", "masked_fill_", "gather", "scatter")
-MIN_NUMEL = 100_000
+MIN_NUMEL = int(os.environ.get("CENSUS_MIN_NUMEL", "100000"))
 
 
 def _where():
