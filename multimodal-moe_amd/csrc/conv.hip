@@ -51,6 +51,7 @@ static int g_conv_wg_stages = 0;   // "conv_wg_stages": weight-gradient ring dep
 static int g_conv_wg_splits = 0;   // "conv_wg_splits": weight-gradient pixel slices
 static int g_conv_dgrad_flip = -1; // "conv_dgrad_flip": 1 = always write W', 0 = always read in place
 static int g_conv_dgrad_phase = 1; // "conv_dgrad_phase": 0 = stride-2 data gradient over all 9 taps (zero rows; A/B)
+static int g_conv_areg = 0;        // "conv_areg": 1 = forward / data-gradient A operand in registers (AR)
 
 struct ConvArgs {
   const uint16_t* x;     // [B Hs Ws, C] (fwd: X; dgrad: dY)
@@ -110,17 +111,27 @@ __device__ __forceinline__ void dma16(const uint16_t* src, char* lds) {
 // WGM x WGN waves (2 x 2: 256 threads; the big tiles 256 x 128 / 256 x 256
 // run 4 x 2 / 2 x 4 = 8 waves, 512 threads, two per SIMD): wave (wm, wn)
 // computes rows wm BM/WGM .. and columns wn BN/WGN .. of the tile.
-template <int KS, int S, int BM, int BN, bool BT, bool PH = false, int WGM = 2, int WGN = 2>
+// AR (the A operand in registers): each wave loads its own A fragments --
+// rows wm BM/WGM + 16 i + (lane & 15), 16 B of k per lane, straight from the
+// pixel's neighbour row -- with plain vector loads into a two-deep register
+// buffer, and only B goes through the LDS-DMA ring.  The conv's K-tile needs
+// (BM + BN) x 128 B per workgroup through the LDS-DMA fill path, the bound of
+// the 128 x 128 tile (~46 GB/s per CU against a measured LDS-DMA fill ceiling
+// of ~70-90 GB/s per CU, MI355X_MICROARCH.md ldsdma-fill); with A on the
+// vector-load path the ring carries half the bytes and the LDS serves B's
+// fragment reads only.  One K-tile in flight (S = 2).
+template <int KS, int S, int BM, int BN, bool BT, bool PH = false, int WGM = 2, int WGN = 2, bool AR = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   static_assert(BN == 64 || BN == 128 || BN == 256, "output-channel tile: 64, 128 or 256");
+  static_assert(!AR || S == 2, "AR: one K-tile in flight");
   constexpr int NW = WGM * WGN, NTH = 64 * NW;
-  constexpr int TILE = (BM + BN) * 128;  // bytes of one ring stage
+  constexpr int TILE = (AR ? BN : BM + BN) * 128;  // bytes of one ring stage
   constexpr int CPR = BN / 8;            // 16-B chunks per output row of the tile
   constexpr int TM = BM / (16 * WGM), TN = BN / (16 * WGN);  // 16 x 16 blocks per wave
   constexpr int AP = BM / (8 * NW), BP = BN / (8 * NW);       // DMA instructions per wave per K-tile (A, B)
   static_assert(AP >= 1 && BP >= 1 && AP * 8 * NW == BM && BP * 8 * NW == BN, "tile / wave split");
-  constexpr int GW = AP + BP;            // DMA instructions per wave per K-tile
+  constexpr int GW = (AR ? 0 : AP) + BP;  // DMA instructions per wave per K-tile
   constexpr int PAD = (KS - 1) / 2;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -167,10 +178,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
       wrow[j] = a.w + (size_t)(n0 + r) * (KS * KS * a.C) + ((lane & 7) ^ ((r >> 1) & 7)) * 8;
     }
   }
-  auto issue = [&](int kt) {
-    char* buf = smem + (kt % S) * TILE;
-    const int t = kt / cpt, c0 = (kt - t * cpt) * 64;
-    int tap, dy, dx;
+  // K-tile kt -> (input-channel offset c0, weight tap, neighbour offset dy, dx)
+  auto tapinfo = [&](int kt, int& c0, int& tap, int& dy, int& dx) {
+    const int t = kt / cpt;
+    c0 = (kt - t * cpt) * 64;
     if constexpr (PH) {  // class tap (ty, tx) -> flipped-weight tap and dY offset (0 or +1 per axis)
       const int ty = t / ntx, tx = t - ty * ntx;
       const int ky = a.ry ? 2 * ty : 1, kx = a.rx ? 2 * tx : 1;
@@ -182,8 +193,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
       dy = tap / KS - PAD;
       dx = tap % KS - PAD;
     }
+  };
+  auto issue = [&](int kt) {
+    char* buf = smem + (kt % S) * TILE;
+    int c0, tap, dy, dx;
+    tapinfo(kt, c0, tap, dy, dx);
 #pragma unroll
-    for (int j = 0; j < AP; ++j) {
+    for (int j = 0; j < (AR ? 0 : AP); ++j) {
       int yy = py[j] * a.st + dy, xx = px[j] * a.st + dx;
       bool ok = pv[j] && !(((yy | xx) & a.sh));  // sh = 1: both even
       yy >>= a.sh;
@@ -192,11 +208,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
       const uint16_t* src = ok ? a.x + ((size_t)(pb[j] * HWs + yy * a.Ws + xx)) * a.C + c0 + ach[j] : a.zero + ach[j];
       dma16(src, buf + (wave + NW * j) * 1024);
     }
+    constexpr int BOFF = AR ? 0 : BM * 128;  // the B image's offset in the stage
 #pragma unroll
     for (int j = 0; j < BP; ++j) {
       if constexpr (BT) dma16(wrow[j] + (size_t)c0 * (KS * KS * a.N) + (KS * KS - 1 - tap) * a.N,
-                              buf + BM * 128 + (wave + NW * j) * 1024);
-      else dma16(wrow[j] + tap * a.C + c0, buf + BM * 128 + (wave + NW * j) * 1024);
+                              buf + BOFF + (wave + NW * j) * 1024);
+      else dma16(wrow[j] + tap * a.C + c0, buf + BOFF + (wave + NW * j) * 1024);
     }
   };
   f32x4 acc[TM][TN];
@@ -204,15 +221,90 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (AR) {
+    // this lane's A rows (one per 16-row block i): pixel coordinates
+    int qy[TM], qx[TM], qb[TM];
+    bool qv[TM];
 #pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < nk) issue(s);
-  for (int kt = 0; kt < nk; ++kt) {
-    wait_ring<S, GW>(nk - 1 - kt);
-    __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
-    if (kt + S - 1 < nk) issue(kt + S - 1);  // refills the slot consumed in iteration kt - 1
-    const char* cur = smem + (kt % S) * TILE;
-    compute_tile_w<BM, BN, WGM, WGN, true, !BT>(cur, cur + BM * 128, acc, lane, wm, wn);
+    for (int i = 0; i < TM; ++i) {
+      const int p = m0 + wm * (BM / WGM) + 16 * i + (lane & 15);
+      qv[i] = p < a.P;
+      const int pp = qv[i] ? p : 0;
+      qb[i] = pp / HW;
+      const int rem = pp - qb[i] * HW;
+      qy[i] = rem / a.W;
+      qx[i] = rem - qy[i] * a.W;
+    }
+    const int kch = (lane >> 4) * 8;  // this lane's 8 k of each 32-k step
+    auto load_a = [&](int kt, bf16x8 (&dst)[TM][2]) {
+      int c0, tap, dy, dx;
+      tapinfo(kt, c0, tap, dy, dx);
+      (void)tap;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        int yy = qy[i] * a.st + dy, xx = qx[i] * a.st + dx;
+        bool ok = qv[i] && !(((yy | xx) & a.sh));
+        yy >>= a.sh;
+        xx >>= a.sh;
+        ok = ok && yy >= 0 && yy < a.Hs && xx >= 0 && xx < a.Ws;
+        const uint16_t* src = ok ? a.x + ((size_t)(qb[i] * HWs + yy * a.Ws + xx)) * a.C + c0 + kch : a.zero + kch;
+        dst[i][0] = *reinterpret_cast<const bf16x8*>(src);
+        dst[i][1] = *reinterpret_cast<const bf16x8*>(src + 32);
+      }
+    };
+    auto compute = [&](const char* bbuf, const bf16x8 (&af)[TM][2]) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 bfr[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = read_frag<BN, !BT>(bbuf, wn * (BN / WGN) + 16 * j, ks, lane);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i][ks], acc[i][j], 0, 0, 0);
+      }
+    };
+    // s_waitcnt vmcnt(0) as a builtin (the compiler's waitcnt pass sees it)
+    auto drain = [] {
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0x70 | 0xF00);
+      asm volatile("" ::: "memory");
+    };
+    bf16x8 A0[TM][2], A1[TM][2];
+    if (nk > 0) {
+      issue(0);
+      load_a(0, A0);
+    }
+    for (int kt = 0; kt < nk; kt += 2) {
+      drain();  // B DMA and A loads of tile kt have landed (this wave)
+      __builtin_amdgcn_s_barrier();  // ... for every wave; slot (kt + 1) % 2 is free
+      if (kt + 1 < nk) {
+        issue(kt + 1);
+        load_a(kt + 1, A1);
+      }
+      compute(smem + (kt % 2) * TILE, A0);
+      if (kt + 1 < nk) {
+        drain();
+        __builtin_amdgcn_s_barrier();
+        if (kt + 2 < nk) {
+          issue(kt + 2);
+          load_a(kt + 2, A0);
+        }
+        compute(smem + ((kt + 1) % 2) * TILE, A1);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+      if (s < nk) issue(s);
+    for (int kt = 0; kt < nk; ++kt) {
+      wait_ring<S, GW>(nk - 1 - kt);
+      __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
+      if (kt + S - 1 < nk) issue(kt + S - 1);  // refills the slot consumed in iteration kt - 1
+      const char* cur = smem + (kt % S) * TILE;
+      compute_tile_w<BM, BN, WGM, WGN, true, !BT>(cur, cur + BM * 128, acc, lane, wm, wn);
+    }
   }
   // Epilogue through LDS: lane holds Y[m0 + wm BM/2 + 16 i + (lane & 15)][n0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3];
   // the tile goes to a row-major [BM][BN] bf16 image (16-B chunk c of row r at chunk c ^ (r % CPR):
@@ -602,17 +694,17 @@ static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int 
 
 constexpr int CV_STAGES = 2;
 
-template <int KS, int BM, int BN, bool BT, bool PH, int WGM = 2, int WGN = 2, int ST = CV_STAGES>
+template <int KS, int BM, int BN, bool BT, bool PH, int WGM = 2, int WGN = 2, int ST = CV_STAGES, bool AR = false>
 static void launch_fwd_n(ConvArgs a, hipStream_t stream, ProfScope& prof) {
-  constexpr size_t lds = ST * (BM + BN) * 128;
+  constexpr size_t lds = ST * (AR ? BN : BM + BN) * 128;
   static_assert(lds >= BM * BN * 2, "epilogue image exceeds the ring");
   static_assert(lds <= 160 * 1024, "ring exceeds the CU's LDS");
   static_assert(!(BT && BN > 128), "the in-place (MN-contiguous) weight image takes 64 or 128 columns");
-  allow_lds_once<conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN>>(lds);
+  allow_lds_once<conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN, AR>>(lds);
   a.mt_n = (a.P + BM - 1) / BM;
   const int NT = a.N / BN;
   const int grid = ((a.mt_n + 7) / 8) * 8 * NT;
-  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN>), dim3(grid), dim3(64 * WGM * WGN), lds,
+  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN, AR>), dim3(grid), dim3(64 * WGM * WGN), lds,
              stream, a);
 }
 
@@ -639,9 +731,17 @@ static bool launch_fwd_big(const ConvArgs& a, hipStream_t stream, ProfScope& pro
   }
 }
 
-// output-channel tiles of 128, or 64 for 64-channel outputs (ResNet stage 1)
+// output-channel tiles of 128, or 64 for 64-channel outputs (ResNet stage 1);
+// "conv_areg" 1: the 128-row tiles with the A operand in registers (AR)
 template <int KS, int BM, bool BT, bool PH>
 static void launch_fwd(const ConvArgs& a, hipStream_t stream, ProfScope& prof) {
+  if constexpr (BM == 128) {
+    if (g_conv_areg == 1) {
+      if (a.N % 128 == 0) launch_fwd_n<KS, BM, 128, BT, PH, 2, 2, 2, true>(a, stream, prof);
+      else launch_fwd_n<KS, BM, 64, BT, PH, 2, 2, 2, true>(a, stream, prof);
+      return;
+    }
+  }
   if (a.N % 128 == 0) launch_fwd_n<KS, BM, 128, BT, PH>(a, stream, prof);
   else launch_fwd_n<KS, BM, 64, BT, PH>(a, stream, prof);
 }
@@ -930,6 +1030,10 @@ extern "C" int rtdetr_conv_set_tuning(const char* key, int value) {
   }
   if (std::string(key) == "conv_dgrad_phase") {
     g_conv_dgrad_phase = value;
+    return 0;
+  }
+  if (std::string(key) == "conv_areg") {
+    g_conv_areg = value;
     return 0;
   }
   return fail(std::string("rtdetr_conv_set_tuning: unknown key ") + key);

@@ -302,6 +302,11 @@ def _need(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
 # thin typed wrappers (tensors in, tensors out; shapes checked on the host)
 # ---------------------------------------------------------------------------
 def set_tuning(key: str, value: int) -> None:
+    """A libmoe_hip tuning override: conv_* keys go to rtdetr_conv_set_tuning
+    (the convolutions), the rest to moe_set_tuning (the grouped GEMMs)."""
+    if key.startswith("conv_"):
+        _check(lib().rtdetr_conv_set_tuning(key.encode(), int(value)), f"rtdetr_conv_set_tuning({key}={value})")
+        return
     _check(lib().moe_set_tuning(key.encode(), int(value)), f"moe_set_tuning({key}={value})")
 
 

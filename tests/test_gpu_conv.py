@@ -42,8 +42,13 @@ _KNOBS = {"auto": {}, "bm64_wg2_flip": dict(conv_bm=64, conv_wg_stages=2, conv_d
           "bm128_wg3_inplace": dict(conv_bm=128, conv_wg_stages=3, conv_dgrad_flip=0, conv_wg_splits=3),
           "bm256_wg4_flip": dict(conv_bm=256, conv_wg_stages=4, conv_dgrad_flip=1, conv_wg_splits=1),
           "zero_rows": dict(conv_dgrad_phase=0), "zero_rows_inplace": dict(conv_dgrad_phase=0, conv_dgrad_flip=0),
-          "big8w_flip": dict(conv_big=1, conv_dgrad_flip=1), "big8w_inplace": dict(conv_big=1, conv_dgrad_flip=0)}
-_DEFAULTS = dict(conv_bm=0, conv_wg_stages=0, conv_dgrad_flip=-1, conv_wg_splits=0, conv_dgrad_phase=1, conv_big=0)
+          "big8w_flip": dict(conv_big=1, conv_dgrad_flip=1), "big8w_inplace": dict(conv_big=1, conv_dgrad_flip=0),
+          # the A operand in registers (128-row tiles), flipped / in-place weights, zero-row stride-2 dgrad
+          "areg_flip": dict(conv_areg=1, conv_bm=128, conv_dgrad_flip=1),
+          "areg_inplace": dict(conv_areg=1, conv_bm=128, conv_dgrad_flip=0),
+          "areg_zero_rows": dict(conv_areg=1, conv_bm=128, conv_dgrad_phase=0)}
+_DEFAULTS = dict(conv_bm=0, conv_wg_stages=0, conv_dgrad_flip=-1, conv_wg_splits=0, conv_dgrad_phase=1, conv_big=0,
+                 conv_areg=0)
 
 
 @pytest.mark.parametrize("knobs", list(_KNOBS))
@@ -71,7 +76,7 @@ def test_conv_large_auto_paths(hip_lib):
 
 
 @pytest.mark.parametrize("knobs", ["auto", "bm64_wg2_flip", "bm128_wg3_inplace", "zero_rows", "zero_rows_inplace",
-                                   "big8w_flip", "big8w_inplace"])
+                                   "big8w_flip", "big8w_inplace", "areg_flip", "areg_inplace", "areg_zero_rows"])
 @pytest.mark.parametrize("B,C,N,H,W", [(2, 128, 128, 46, 80), (8, 256, 256, 23, 40), (2, 64, 128, 11, 13),
                                        (1, 256, 512, 5, 3), (2, 128, 64, 7, 9), (4, 256, 256, 92, 160)])
 def test_conv_stride2_vs_fp32(hip_lib, B, C, N, H, W, knobs):
