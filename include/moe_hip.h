@@ -482,6 +482,13 @@ int rtdetr_add_bias_relu_nhwc(const void* a, const void* b, const float* bias, l
  * output channel, a multiple of 8; 16-B aligned tensors); `chunks` device
  * int32 pairs {record, chunk of 2048 elements}.  out = RNE(float(w) * scale). */
 int rtdetr_fold_scale_multi(const void* records, const int32_t* chunks, int n_chunks, hipStream_t stream);
+/* The same product for n <= 64 tensors given as host pointer arrays (the
+ * table goes in the kernel argument: the folds' backward dW_l = dW'_l *
+ * scale_l on gradients allocated during the backward, graph-capture safe):
+ * out_q[r, :] = bf16(in_q[r, :] * scale_q[r]), bf16 [rows_q, inner_q], inner a
+ * multiple of 8.  One launch for every backbone convolution (52 at C2). */
+int rtdetr_fold_scale_batch(int n, const void* const* in, const float* const* scale, void* const* out,
+                            const int* rows, const int* inner, hipStream_t stream);
 
 /* ResNet-D shortcut AvgPool2d(2, 2) over channels_last bf16 [B, H, W, C]
  * (even H, W; C % 8 == 0; 16-B aligned): y = RNE(0.25 * window sum, fp32);

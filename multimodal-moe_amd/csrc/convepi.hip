@@ -103,6 +103,33 @@ __global__ __launch_bounds__(256) void fold_scale_multi_kernel(const FoldRec* __
   *reinterpret_cast<uint4*>(r.out + e) = pack8(v);
 }
 
+// The same product for up to 64 tensors whose addresses are only known at
+// launch time (the folds' backward, dW_l = dW'_l * scale_l, on gradients
+// autograd allocates): the table travels as the kernel argument; tensor q
+// owns blocks [base[q], base[q+1]) of 2048 elements each.
+constexpr int kFoldBatch = 64;
+struct FoldBatch {
+  const uint16_t* in[kFoldBatch];
+  const float* scale[kFoldBatch];
+  uint16_t* out[kFoldBatch];
+  int rows[kFoldBatch], inner[kFoldBatch], base[kFoldBatch + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void fold_scale_batch_kernel(FoldBatch b) {
+  int q = 0;
+  while (q + 1 < b.n && (int)blockIdx.x >= b.base[q + 1]) ++q;
+  const long long e = (long long)(blockIdx.x - b.base[q]) * 2048 + threadIdx.x * 8;
+  const long long n = (long long)b.rows[q] * b.inner[q];
+  if (e >= n) return;
+  const float s = b.scale[q][e / b.inner[q]];
+  float v[8];
+  unpack8(*reinterpret_cast<const uint4*>(b.in[q] + e), v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] *= s;
+  *reinterpret_cast<uint4*>(b.out[q] + e) = pack8(v);
+}
+
 }  // namespace moe
 
 using namespace moe;
@@ -162,4 +189,33 @@ extern "C" int rtdetr_fold_scale_multi(const void* records, const int32_t* chunk
   MOE_LAUNCH(prof, fold_scale_multi_kernel, dim3(n_chunks), dim3(256), 0, stream,
              static_cast<const FoldRec*>(records), reinterpret_cast<const int2*>(chunks));
   return check_launch("rtdetr_fold_scale_multi");
+}
+
+extern "C" int rtdetr_fold_scale_batch(int n, const void* const* in, const float* const* scale, void* const* out,
+                                       const int* rows, const int* inner, hipStream_t stream) {
+  if (n < 1 || n > kFoldBatch || in == nullptr || scale == nullptr || out == nullptr || rows == nullptr ||
+      inner == nullptr)
+    return fail("fold_scale_batch: 1..64 tensors, non-NULL arrays");
+  FoldBatch b{};
+  b.n = n;
+  int blocks = 0;
+  double bytes = 0.0;
+  for (int q = 0; q < n; ++q) {
+    if (in[q] == nullptr || scale[q] == nullptr || out[q] == nullptr || rows[q] < 1 || inner[q] < 8 ||
+        inner[q] % 8 || (reinterpret_cast<uintptr_t>(in[q]) | reinterpret_cast<uintptr_t>(out[q])) % 16)
+      return fail("fold_scale_batch: bad tensor (inner a multiple of 8, 16-B aligned bf16)");
+    b.in[q] = static_cast<const uint16_t*>(in[q]);
+    b.scale[q] = scale[q];
+    b.out[q] = static_cast<uint16_t*>(out[q]);
+    b.rows[q] = rows[q];
+    b.inner[q] = inner[q];
+    b.base[q] = blocks;
+    const long long numel = (long long)rows[q] * inner[q];
+    blocks += (int)((numel + 2047) / 2048);
+    bytes += 4.0 * numel + 4.0 * rows[q];
+  }
+  b.base[n] = blocks;
+  ProfScope prof(stream, PROF_CONV_EPI, bytes);
+  MOE_LAUNCH(prof, fold_scale_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, b);
+  return check_launch("rtdetr_fold_scale_batch");
 }

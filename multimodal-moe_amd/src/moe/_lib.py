@@ -71,6 +71,7 @@ SIGNATURES = {
     "rtdetr_add_bias_relu_nhwc": (_I, [_P, _P, _P, ctypes.c_longlong, _I, _P, _P]),
     "rtdetr_relu_grad2_nhwc": (_I, [_P, _P, _P, ctypes.c_longlong, _I, _P, _P]),
     "rtdetr_fold_scale_multi": (_I, [_P, _P, _I, _P]),
+    "rtdetr_fold_scale_batch": (_I, [_I, _P, _P, _P, _P, _P, _P]),
     "rtdetr_bn_act_workspace": (ctypes.c_size_t, [ctypes.c_longlong, _I, _I]),
     "rtdetr_bn_act_fwd": (_I, [_P, _P, _P, _P, _P, _I, ctypes.c_longlong, _I, _I, _F, _F, _P, _P, _P, _P]),
     "rtdetr_bn_act_bwd": (_I, [_P, _P, _P, _I, ctypes.c_longlong, _I, _I, _P, _P, _P, _P, _P, _P]),

@@ -10,6 +10,7 @@ convolutions); nothing here is on the MoE hot path.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
@@ -112,15 +113,42 @@ class _FoldAll(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *grads):
         plan = ctx.plan
-        out = []
+        out, jobs = [], []
         for g, sc in zip(grads, plan.scales):
             if g is None:
                 out.append(None)
                 continue
             gw = torch.empty_like(g)
-            torch.mul(g, sc.view(-1, *([1] * (g.dim() - 1))), out=gw)
+            if _FOLD_BWD_BATCH and _fold_batch_ok(g, gw):
+                jobs.append((g, sc, gw))  # bf16(g * scale[row]): one launch for all of them below
+            else:
+                torch.mul(g, sc.view(-1, *([1] * (g.dim() - 1))), out=gw)
             out.append(gw)
+        if jobs:
+            from ..moe import _lib as L
+
+            for i in range(0, len(jobs), 64):
+                part = jobs[i:i + 64]
+                n = len(part)
+                arr = [(ctypes.c_void_p * n)(*[t.data_ptr() for t in col]) for col in zip(*part)]
+                rows = (ctypes.c_int * n)(*[g.shape[0] for g, _, _ in part])
+                inner = (ctypes.c_int * n)(*[g.numel() // g.shape[0] for g, _, _ in part])
+                c = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+                L._check(L.lib().rtdetr_fold_scale_batch(n, c(arr[0]), c(arr[1]), c(arr[2]), c(rows), c(inner),
+                                                         L._stream()), "rtdetr_fold_scale_batch")
         return (None, *out)
+
+
+# MOE_FOLD_BWD_BATCH=0: one torch.mul per folded weight's gradient (A/B switch)
+_FOLD_BWD_BATCH = os.environ.get("MOE_FOLD_BWD_BATCH", "1") != "0"
+
+
+def _fold_batch_ok(g, gw):
+    """rtdetr_fold_scale_batch takes the gradient (bf16, dense in the weight's
+    layout: output channel outermost, 16-B aligned, whole 8-element groups)."""
+    return (g.is_cuda and g.dtype == torch.bfloat16 and gw.stride() == g.stride() and g.data_ptr() % 16 == 0
+            and gw.data_ptr() % 16 == 0 and (g.numel() // g.shape[0]) % 8 == 0 and g.numel() > 0
+            and (g.is_contiguous() or g.is_contiguous(memory_format=torch.channels_last)))
 
 
 class FoldPlan:

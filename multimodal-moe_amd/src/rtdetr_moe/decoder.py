@@ -266,10 +266,18 @@ class _ValueProjAll(torch.autograd.Function):
         if dmem is not None and gsel is not None:  # (top-k rows are distinct per image: one add per row)
             dmem.scatter_add_(1, idx, (gsel * vsel).to(mdtype))
         dW = chunked_wgrad(G, m2)  # fp32 [n d, d]
-        db = bias_grad(G, torch.float32)
         grads = []
-        for i in range(n):
-            grads += [dW[i * d:(i + 1) * d].to(wdt[i]), db[i * d:(i + 1) * d].to(bdt[i])]
+        if len(set(wdt)) == 1 and len(set(bdt)) == 1:
+            # one cast of all layers' weights and the bias sums in their dtype:
+            # 2 launches instead of 2 n (per-layer slices are views)
+            dWc = dW.to(wdt[0])
+            dbc = bias_grad(G, bdt[0])
+            for i in range(n):
+                grads += [dWc[i * d:(i + 1) * d], dbc[i * d:(i + 1) * d]]
+        else:
+            db = bias_grad(G, torch.float32)
+            for i in range(n):
+                grads += [dW[i * d:(i + 1) * d].to(wdt[i]), db[i * d:(i + 1) * d].to(bdt[i])]
         return (dmem, None, None, None, None, *grads)
 
 
@@ -304,7 +312,8 @@ class _MSDAFusedSlot(torch.autograd.Function):
             go, gl = L_.msda_fused_bwd_slice(v_all, ctx.grad_all, col0, H, D, shapes_t, starts_t, o, r, lg,
                                              offset_scale, L, P, g)
         ctx.grad_all = None
-        return (torch.zeros((), dtype=torch.float32, device=go.device),) + (None,) * 7 + (go, None, gl) + (None,) * 4
+        # (no gradient for `token`: it only orders _ValueProjAll's backward after this one)
+        return (None,) * 8 + (go, None, gl) + (None,) * 4
 
 
 _LEVEL_CACHE = {}

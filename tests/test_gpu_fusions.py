@@ -259,3 +259,27 @@ def test_ranking_rows_overwrite_equals_mask(hip_lib):
         ref = dec.enc_output(vmask * memory)
         got = dec._enc_output_masked(memory, inv, vmask)
     assert torch.equal(got, ref)
+
+
+def test_fold_backward_batched_equals_per_tensor(hip_lib, monkeypatch):
+    """backbone._FoldAll's backward (dW_l = dW'_l * scale_l for every folded
+    convolution) as one rtdetr_fold_scale_batch launch == one torch.mul per
+    tensor, bitwise."""
+    from src.rtdetr_moe import backbone as bb
+
+    torch.manual_seed(9)
+    m = bb.PResNet(50).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for mod in m.modules():
+        if hasattr(mod, "running_var") and not isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_var.uniform_(0.5, 2.0)
+            mod.weight.uniform_(0.5, 1.5)
+    x = torch.randn(2, 3, 64, 96, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    for batched in (True, False):
+        monkeypatch.setattr(bb, "_FOLD_BWD_BATCH", batched)
+        m.zero_grad(set_to_none=True)
+        sum(o.float().sum() for o in m(x)).backward()
+        res.append({n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None})
+    assert res[0].keys() == res[1].keys() and len(res[0]) > 40
+    for k in res[0]:
+        assert torch.equal(res[0][k], res[1][k]), k
