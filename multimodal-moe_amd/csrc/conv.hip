@@ -52,6 +52,8 @@ static int g_conv_wg_splits = 0;   // "conv_wg_splits": weight-gradient pixel sl
 static int g_conv_dgrad_flip = -1; // "conv_dgrad_flip": 1 = always write W', 0 = always read in place
 static int g_conv_dgrad_phase = 1; // "conv_dgrad_phase": 0 = stride-2 data gradient over all 9 taps (zero rows; A/B)
 static int g_conv_areg = 0;        // "conv_areg": 1 = forward / data-gradient A operand in registers (AR)
+static int g_conv_k32 = -1;        // "conv_k32": 1-3 = forward / data-gradient 32-deep K-tiles, ring depth 2-4;
+                                   // 0 = never; -1 = automatic (k32_auto)
 
 struct ConvArgs {
   const uint16_t* x;     // [B Hs Ws, C] (fwd: X; dgrad: dY)
@@ -120,17 +122,27 @@ __device__ __forceinline__ void dma16(const uint16_t* src, char* lds) {
 // of ~70-90 GB/s per CU, MI355X_MICROARCH.md ldsdma-fill); with A on the
 // vector-load path the ring carries half the bytes and the LDS serves B's
 // fragment reads only.  One K-tile in flight (S = 2).
-template <int KS, int S, int BM, int BN, bool BT, bool PH = false, int WGM = 2, int WGN = 2, bool AR = false>
+// KT: K-tile depth, 64 (128-B operand rows, 2 MFMA k-steps per barrier) or
+// 32 (64-B rows, one k-step: half the ring bytes per stage, so more
+// workgroups per CU at the same depth -- "conv_k32"); the 32-deep
+// K-contiguous image swizzles chunk c of row r to c ^ ((r >> 2) & 3).
+template <int KS, int S, int BM, int BN, bool BT, bool PH = false, int WGM = 2, int WGN = 2, bool AR = false,
+          int KT = 64>
 __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   static_assert(BN == 64 || BN == 128 || BN == 256, "output-channel tile: 64, 128 or 256");
   static_assert(!AR || S == 2, "AR: one K-tile in flight");
+  static_assert(KT == 64 || (KT == 32 && !AR), "K-tile 64, or 32 without AR");
   constexpr int NW = WGM * WGN, NTH = 64 * NW;
-  constexpr int TILE = (AR ? BN : BM + BN) * 128;  // bytes of one ring stage
+  constexpr int RB = KT * 2;              // bytes per operand row of a K-contiguous K-tile image
+  constexpr int CH = KT / 8;              // 16-B chunks per such row
+  constexpr int RPI = 1024 / RB;          // rows per DMA instruction (64 lanes x 16 B)
+  constexpr int TILE = (AR ? BN : BM + BN) * RB;  // bytes of one ring stage
   constexpr int CPR = BN / 8;            // 16-B chunks per output row of the tile
   constexpr int TM = BM / (16 * WGM), TN = BN / (16 * WGN);  // 16 x 16 blocks per wave
-  constexpr int AP = BM / (8 * NW), BP = BN / (8 * NW);       // DMA instructions per wave per K-tile (A, B)
-  static_assert(AP >= 1 && BP >= 1 && AP * 8 * NW == BM && BP * 8 * NW == BN, "tile / wave split");
+  constexpr int AP = BM / (RPI * NW), BP = BN / (RPI * NW);   // DMA instructions per wave per K-tile (A, B)
+  static_assert(AP >= 1 && BP >= 1 && AP * RPI * NW == BM && BP * RPI * NW == BN, "tile / wave split");
+  auto kswz = [](int r) { return KT == 64 ? ((r >> 1) & 7) : ((r >> 2) & 3); };
   constexpr int GW = (AR ? 0 : AP) + BP;  // DMA instructions per wave per K-tile
   constexpr int PAD = (KS - 1) / 2;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -143,7 +155,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
   const int mt = (slot / NT) * 8 + xcd;
   if (mt >= a.mt_n) return;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int cpt = a.C / 64;        // K-tiles per tap
+  const int cpt = a.C / KT;        // K-tiles per tap
   const int nty = PH ? 1 + a.ry : KS, ntx = PH ? 1 + a.rx : KS;  // taps per axis
   const int nk = nty * ntx * cpt;
   const int HW = a.H * a.W, HWs = a.Hs * a.Ws;
@@ -152,7 +164,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
   bool pv[AP];
 #pragma unroll
   for (int j = 0; j < AP; ++j) {
-    const int r = (wave + NW * j) * 8 + (lane >> 3);
+    const int r = (wave + NW * j) * RPI + lane / CH;
     const int p = m0 + r;
     pv[j] = p < a.P;
     const int pp = pv[j] ? p : 0;
@@ -160,7 +172,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
     const int rem = pp - pb[j] * HW;
     py[j] = rem / a.W;
     px[j] = rem - py[j] * a.W;
-    ach[j] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+    ach[j] = ((lane % CH) ^ kswz(r)) * 8;
   }
   // B rows.  Forward: K-contiguous [BN][64] image of W[n][tap][c0..c0+63].
   // BT (data gradient, a.w = the ORIGINAL weight [a.C][KS][KS][a.N]): the
@@ -174,14 +186,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
       const int kr = (wave + NW * j) * (64 / CPR) + lane / CPR;
       wrow[j] = a.w + (size_t)kr * (KS * KS * a.N) + n0 + ((lane % CPR) ^ mimg_swz<BN>(kr)) * 8;
     } else {
-      const int r = (wave + NW * j) * 8 + (lane >> 3);
-      wrow[j] = a.w + (size_t)(n0 + r) * (KS * KS * a.C) + ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+      const int r = (wave + NW * j) * RPI + lane / CH;
+      wrow[j] = a.w + (size_t)(n0 + r) * (KS * KS * a.C) + ((lane % CH) ^ kswz(r)) * 8;
     }
   }
   // K-tile kt -> (input-channel offset c0, weight tap, neighbour offset dy, dx)
   auto tapinfo = [&](int kt, int& c0, int& tap, int& dy, int& dx) {
     const int t = kt / cpt;
-    c0 = (kt - t * cpt) * 64;
+    c0 = (kt - t * cpt) * KT;
     if constexpr (PH) {  // class tap (ty, tx) -> flipped-weight tap and dY offset (0 or +1 per axis)
       const int ty = t / ntx, tx = t - ty * ntx;
       const int ky = a.ry ? 2 * ty : 1, kx = a.rx ? 2 * tx : 1;
@@ -208,7 +220,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
       const uint16_t* src = ok ? a.x + ((size_t)(pb[j] * HWs + yy * a.Ws + xx)) * a.C + c0 + ach[j] : a.zero + ach[j];
       dma16(src, buf + (wave + NW * j) * 1024);
     }
-    constexpr int BOFF = AR ? 0 : BM * 128;  // the B image's offset in the stage
+    constexpr int BOFF = AR ? 0 : BM * RB;  // the B image's offset in the stage
 #pragma unroll
     for (int j = 0; j < BP; ++j) {
       if constexpr (BT) dma16(wrow[j] + (size_t)c0 * (KS * KS * a.N) + (KS * KS - 1 - tap) * a.N,
@@ -303,7 +315,28 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
       __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
       if (kt + S - 1 < nk) issue(kt + S - 1);  // refills the slot consumed in iteration kt - 1
       const char* cur = smem + (kt % S) * TILE;
-      compute_tile_w<BM, BN, WGM, WGN, true, !BT>(cur, cur + BM * 128, acc, lane, wm, wn);
+      if constexpr (KT == 64) {
+        compute_tile_w<BM, BN, WGM, WGN, true, !BT>(cur, cur + BM * 128, acc, lane, wm, wn);
+      } else {  // one 32-deep k-step
+        auto rd32 = [&](const char* img, int row_base) {
+          const int r = row_base + (lane & 15), c = lane >> 4;
+          return *reinterpret_cast<const bf16x8*>(img + r * 64 + ((c ^ ((r >> 2) & 3)) << 4));
+        };
+        const char* bimg = cur + BM * 64;
+        bf16x8 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = rd32(cur, wm * (BM / WGM) + 16 * i);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (BT) bfr[j] = read_frag<BN, false>(bimg, wn * (BN / WGN) + 16 * j, 0, lane);
+          else bfr[j] = rd32(bimg, wn * (BN / WGN) + 16 * j);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
     }
   }
   // Epilogue through LDS: lane holds Y[m0 + wm BM/2 + 16 i + (lane & 15)][n0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3];
@@ -312,7 +345,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
   // (register-direct 8-B stores at a row stride run at about half that rate).  The fused
   // epilogue's operands (same 16-B chunks as the stores) are loaded first, behind the image.
   constexpr int RPP = NTH / CPR;  // rows per store pass
-  constexpr bool PRE = BM / RPP <= 16;  // epilogue operands loaded up front (else per store pass: registers)
+  // epilogue operands loaded up front (else per store pass: registers; the
+  // 32-deep variant keeps its register budget for 4 waves per SIMD)
+  constexpr bool PRE = BM / RPP <= 16 && KT == 64;
   constexpr int NPRE = PRE ? BM / RPP : 1;
   const int ec = tid % CPR;
   uint4 eres[NPRE], emask[NPRE];
@@ -694,18 +729,21 @@ static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int 
 
 constexpr int CV_STAGES = 2;
 
-template <int KS, int BM, int BN, bool BT, bool PH, int WGM = 2, int WGN = 2, int ST = CV_STAGES, bool AR = false>
+template <int KS, int BM, int BN, bool BT, bool PH, int WGM = 2, int WGN = 2, int ST = CV_STAGES, bool AR = false,
+          int KT = 64>
 static void launch_fwd_n(ConvArgs a, hipStream_t stream, ProfScope& prof) {
-  constexpr size_t lds = ST * (AR ? BN : BM + BN) * 128;
-  static_assert(lds >= BM * BN * 2, "epilogue image exceeds the ring");
+  constexpr size_t ring = ST * (AR ? BN : BM + BN) * KT * 2;
+  // the epilogue's output image (and statistics rows) reuse the ring's LDS
+  constexpr size_t lds = ring > (size_t)BM * BN * 2 ? ring : (size_t)BM * BN * 2;
+  static_assert(2 * (64 * WGM * WGN / (BN / 8)) * BN * 4 <= lds, "statistics rows exceed the LDS");
   static_assert(lds <= 160 * 1024, "ring exceeds the CU's LDS");
   static_assert(!(BT && BN > 128), "the in-place (MN-contiguous) weight image takes 64 or 128 columns");
-  allow_lds_once<conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN, AR>>(lds);
+  allow_lds_once<conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN, AR, KT>>(lds);
   a.mt_n = (a.P + BM - 1) / BM;
   const int NT = a.N / BN;
   const int grid = ((a.mt_n + 7) / 8) * 8 * NT;
-  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN, AR>), dim3(grid), dim3(64 * WGM * WGN), lds,
-             stream, a);
+  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN, AR, KT>), dim3(grid), dim3(64 * WGM * WGN),
+             lds, stream, a);
 }
 
 // The 8-wave big tile: 256 x 128, 4 x 2 waves of 64 x 64 (the 128 x 128
@@ -731,6 +769,18 @@ static bool launch_fwd_big(const ConvArgs& a, hipStream_t stream, ProfScope& pro
   }
 }
 
+// The 32-deep K-tile with a 2-deep ring (32 KiB of LDS, 4 workgroups per CU
+// against 2) pays where the K loop is short and the grid long: 1x1
+// convolutions with at most 512 input channels over >= 16 M outputs, where
+// the epilogues of some workgroups overlap the main loops of others
+// (tools/conv_bench.py, gpurun_out/r5v: e.g. 128 -> 512 at 92 x 160 43.6 ->
+// 35.7 us, the 64 -> 256 stage-1 data gradient 80.8 -> 69.0 us).  The 3x3
+// layers (K = 9 C) and 1x1 layers with 1024+ input channels are slower with
+// it (the per-barrier work halves): they keep the 64-deep tile.
+static int k32_auto(int KS, const ConvArgs& a) {
+  return KS == 1 && a.C <= 512 && (long long)a.P * a.N >= 16000000LL ? 1 : 0;
+}
+
 // output-channel tiles of 128, or 64 for 64-channel outputs (ResNet stage 1);
 // "conv_areg" 1: the 128-row tiles with the A operand in registers (AR)
 template <int KS, int BM, bool BT, bool PH>
@@ -739,6 +789,21 @@ static void launch_fwd(const ConvArgs& a, hipStream_t stream, ProfScope& prof) {
     if (g_conv_areg == 1) {
       if (a.N % 128 == 0) launch_fwd_n<KS, BM, 128, BT, PH, 2, 2, 2, true>(a, stream, prof);
       else launch_fwd_n<KS, BM, 64, BT, PH, 2, 2, 2, true>(a, stream, prof);
+      return;
+    }
+  }
+  if constexpr (BM == 128 || BM == 64) {
+    const int k32 = g_conv_k32 >= 0 ? g_conv_k32 : k32_auto(KS, a);
+    if (k32 >= 1 && k32 <= 3) {  // 32-deep K-tiles, ring depth 2-4
+      const bool w = a.N % 128 == 0;
+      switch (k32) {
+        case 1: w ? launch_fwd_n<KS, BM, 128, BT, PH, 2, 2, 2, false, 32>(a, stream, prof)
+                  : launch_fwd_n<KS, BM, 64, BT, PH, 2, 2, 2, false, 32>(a, stream, prof); break;
+        case 2: w ? launch_fwd_n<KS, BM, 128, BT, PH, 2, 2, 3, false, 32>(a, stream, prof)
+                  : launch_fwd_n<KS, BM, 64, BT, PH, 2, 2, 3, false, 32>(a, stream, prof); break;
+        default: w ? launch_fwd_n<KS, BM, 128, BT, PH, 2, 2, 4, false, 32>(a, stream, prof)
+                   : launch_fwd_n<KS, BM, 64, BT, PH, 2, 2, 4, false, 32>(a, stream, prof); break;
+      }
       return;
     }
   }
@@ -1034,6 +1099,11 @@ extern "C" int rtdetr_conv_set_tuning(const char* key, int value) {
   }
   if (std::string(key) == "conv_areg") {
     g_conv_areg = value;
+    return 0;
+  }
+  if (std::string(key) == "conv_k32") {
+    if (value < -1 || value > 3) return fail("rtdetr_conv_set_tuning: conv_k32 takes -1 (auto) or 0-3");
+    g_conv_k32 = value;
     return 0;
   }
   return fail(std::string("rtdetr_conv_set_tuning: unknown key ") + key);

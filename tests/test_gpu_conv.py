@@ -46,9 +46,13 @@ _KNOBS = {"auto": {}, "bm64_wg2_flip": dict(conv_bm=64, conv_wg_stages=2, conv_d
           # the A operand in registers (128-row tiles), flipped / in-place weights, zero-row stride-2 dgrad
           "areg_flip": dict(conv_areg=1, conv_bm=128, conv_dgrad_flip=1),
           "areg_inplace": dict(conv_areg=1, conv_bm=128, conv_dgrad_flip=0),
-          "areg_zero_rows": dict(conv_areg=1, conv_bm=128, conv_dgrad_phase=0)}
+          "areg_zero_rows": dict(conv_areg=1, conv_bm=128, conv_dgrad_phase=0),
+          # 32-deep K-tiles, ring depth 2 / 3 / 4 (128- and 64-row tiles)
+          "k32_s2_flip": dict(conv_k32=1, conv_dgrad_flip=1), "k32_s3_inplace": dict(conv_k32=2, conv_dgrad_flip=0),
+          "k32_s4_bm64": dict(conv_k32=3, conv_bm=64), "k32_s2_zero_rows": dict(conv_k32=1, conv_dgrad_phase=0),
+          "k32_off": dict(conv_k32=0)}
 _DEFAULTS = dict(conv_bm=0, conv_wg_stages=0, conv_dgrad_flip=-1, conv_wg_splits=0, conv_dgrad_phase=1, conv_big=0,
-                 conv_areg=0)
+                 conv_areg=0, conv_k32=-1)
 
 
 @pytest.mark.parametrize("knobs", list(_KNOBS))
@@ -76,7 +80,8 @@ def test_conv_large_auto_paths(hip_lib):
 
 
 @pytest.mark.parametrize("knobs", ["auto", "bm64_wg2_flip", "bm128_wg3_inplace", "zero_rows", "zero_rows_inplace",
-                                   "big8w_flip", "big8w_inplace", "areg_flip", "areg_inplace", "areg_zero_rows"])
+                                   "big8w_flip", "big8w_inplace", "areg_flip", "areg_inplace", "areg_zero_rows",
+                                   "k32_s2_flip", "k32_s3_inplace", "k32_s4_bm64", "k32_s2_zero_rows"])
 @pytest.mark.parametrize("B,C,N,H,W", [(2, 128, 128, 46, 80), (8, 256, 256, 23, 40), (2, 64, 128, 11, 13),
                                        (1, 256, 512, 5, 3), (2, 128, 64, 7, 9), (4, 256, 256, 92, 160)])
 def test_conv_stride2_vs_fp32(hip_lib, B, C, N, H, W, knobs):
@@ -266,27 +271,33 @@ def test_conv_stride2_dgrad_classes_match_zero_rows(hip_lib, B, C, N, H, W):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("alt", ["conv_big:1", "conv_k32:1", "conv_k32:2", "conv_k32:3"])
+@pytest.mark.parametrize("ks", [3, 1])
 @pytest.mark.parametrize("stride", [1, 2])
 @pytest.mark.parametrize("flip", [1, 0])
-def test_conv_big_tile_bit_exact(hip_lib, stride, flip):
-    """The 8-wave 256 x 128 tile ("conv_big") runs every output element's
-    K loop in the same order as the 4-wave 128 x 128 tile: forward and data
-    gradient bit for bit equal (128-channel shapes; 64-channel outputs keep
-    the 64-wide tiles)."""
+def test_conv_big_tile_bit_exact(hip_lib, stride, flip, alt, ks):
+    """The 8-wave 256 x 128 tile ("conv_big") and the 32-deep K-tiles
+    ("conv_k32", one k-step per stage) run every output element's K loop in
+    the same order as the 4-wave 128 x 128 tile: forward and data gradient bit
+    for bit equal (128-channel shapes; 64-channel outputs keep the 64-wide
+    tiles)."""
+    knob, val = alt.split(":")
+    if ks == 1 and stride == 2:
+        pytest.skip("1x1 convolutions run at stride 1")
     from src.rtdetr_moe.conv import _ConvHIP
 
     g = torch.Generator(device=DEV).manual_seed(11 + stride)
     B, C, N, H, W = 4, 256, 256, 46, 80
     x = torch.randn(B, C, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    w = (torch.randn(N, C, 3, 3, device=DEV, generator=g) * (C * 9) ** -0.5).to(torch.bfloat16)
+    w = (torch.randn(N, C, ks, ks, device=DEV, generator=g) * (C * ks * ks) ** -0.5).to(torch.bfloat16)
     w = w.contiguous(memory_format=torch.channels_last)
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     gy = torch.randn(B, N, Ho, Wo, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     res = []
     try:
         assert hip_lib.rtdetr_conv_set_tuning(b"conv_dgrad_flip", flip) == 0
-        for big in (0, 1):
-            assert hip_lib.rtdetr_conv_set_tuning(b"conv_big", big) == 0
+        for v in (0, int(val)):
+            assert hip_lib.rtdetr_conv_set_tuning(knob.encode(), v) == 0
             xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
             y = _ConvHIP.apply(xa, wa, None, False, False, False, None, stride)
             gx, = torch.autograd.grad(y, (xa,), gy)
