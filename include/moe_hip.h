@@ -312,6 +312,25 @@ int rtdetr_linear_wgrad_narrow_batch(int n, const void* const* gy, const void* c
                                      const int* N, int n_groups, const int* group_count, void* const* dw,
                                      void* const* db, float* part, long long part_floats, int out_bf16,
                                      hipStream_t stream);
+/* Narrow dense linears (csrc/narrow.hip), bf16 rows, fp32 accumulation, the
+ * bias (bf16 when b_bf16, else fp32; NULL = none) added in fp32, one rounding:
+ *   fwd:   y [M, N] = act(x [M, K] w[N, K]^T + b), act = ReLU when relu; for
+ *          N <= 8 with K % 8 == 0 (the score heads, the box heads' 256 -> 4
+ *          layers, the query ranking's head over all memory tokens) or K <= 8
+ *          with N % 8 == 0 (the query position head's 4 -> 512 layer);
+ *   dgrad: gx [M, K] = g [M, N] w [N, K], N <= 8, K % 8 == 0, then zeroed
+ *          where mask [M, K] (bf16, e.g. the layer's input: the previous
+ *          layer's ReLU) is <= 0 (mask NULL: no mask) -- threshold_backward
+ *          fused.
+ * Replace hipBLASLt's 1-8 column GEMMs (+ a ReLU / ReLU-backward launch) in
+ * linear.py's _TokenLinear / _MLPHip (the reference's nn.Linear heads,
+ * src/models/vision/rtdetr.py).  rtdetr_linear_narrow_supported(K, N): 1
+ * when fwd takes the shape. */
+int rtdetr_linear_narrow_supported(int K, int N);
+int rtdetr_linear_narrow_fwd(const void* x, const void* w, const void* b, int b_bf16, void* y, long long M, int K,
+                             int N, int relu, hipStream_t stream);
+int rtdetr_linear_narrow_dgrad(const void* g, const void* w, const void* mask, void* gx, long long M, int K, int N,
+                               hipStream_t stream);
 /* a7: one backward step of an expert weight in ONE launch --
  *   dgrad: C[r, n] = epi( s_r sum_k A(r, k) B_g[k][n] )   (trans_b = 0; epilogue
  *          NONE / RELU_MASK / RELU_MASK_MX with aux); A(r, .) = a[a_gather[r]]

@@ -47,6 +47,9 @@ SIGNATURES = {
     "rtdetr_linear_wgrad_narrow_batch_parts": (ctypes.c_longlong, [_I, _P, _P, _P]),
     "rtdetr_linear_wgrad_narrow_batch": (_I, [_I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, ctypes.c_longlong, _I,
                                               _P]),
+    "rtdetr_linear_narrow_supported": (_I, [_I, _I]),
+    "rtdetr_linear_narrow_fwd": (_I, [_P, _P, _P, _I, _P, _LL, _I, _I, _I, _P]),
+    "rtdetr_linear_narrow_dgrad": (_I, [_P, _P, _P, _P, _LL, _I, _I, _P]),
     "moe_route_index": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "moe_route_dispatch": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P]),
     "moe_grouped_gemm_gather": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
@@ -814,6 +817,47 @@ def linear_wgrad_narrow(gy, x, out_dtype):
                                             int(out_dtype == torch.bfloat16), _stream()),
            "rtdetr_linear_wgrad_narrow")
     return dw, db
+
+
+def linear_narrow_ok(K, N):
+    """Shapes rtdetr_linear_narrow_fwd takes (N <= 8 with K % 8 == 0, or K <= 8 with N % 8 == 0)."""
+    return (1 <= N <= 8 and K >= 8 and K % 8 == 0) or (1 <= K <= 8 and N >= 8 and N % 8 == 0)
+
+
+def linear_narrow_fwd(x, w, b, relu=False):
+    """y = act(x w^T + b) for a narrow layer (rtdetr_linear_narrow_fwd): x bf16
+    [M, K] contiguous, w bf16 [N, K], b bf16 / fp32 [N] or None -> bf16 [M, N]."""
+    _need(x, torch.bfloat16, "x")
+    _need(w, torch.bfloat16, "w")
+    M, K = x.shape
+    N = w.shape[0]
+    if w.shape[1] != K or not x.is_contiguous() or not w.is_contiguous():
+        raise MoEKernelError("linear_narrow_fwd: x [M, K] and w [N, K] contiguous")
+    if b is not None and (b.dtype not in (torch.bfloat16, torch.float32) or b.numel() != N or not b.is_contiguous()):
+        raise MoEKernelError("linear_narrow_fwd: b must be a contiguous bf16 / fp32 [N] tensor")
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    _check(lib().rtdetr_linear_narrow_fwd(_ptr(x), _ptr(w), _ptr(b), int(b is not None and b.dtype == torch.bfloat16),
+                                          _ptr(y), M, K, N, int(bool(relu)), _stream()), "rtdetr_linear_narrow_fwd")
+    return y
+
+
+def linear_narrow_dgrad(g, w, mask=None):
+    """gx = (g w) * [mask > 0] through a narrow layer (rtdetr_linear_narrow_dgrad):
+    g bf16 [M, N <= 8] contiguous, w bf16 [N, K], mask bf16 [M, K] or None."""
+    _need(g, torch.bfloat16, "g")
+    _need(w, torch.bfloat16, "w")
+    M, N = g.shape
+    K = w.shape[1]
+    if w.shape[0] != N or not g.is_contiguous() or not w.is_contiguous():
+        raise MoEKernelError("linear_narrow_dgrad: g [M, N] and w [N, K] contiguous")
+    if mask is not None:
+        _need(mask, torch.bfloat16, "mask")
+        if tuple(mask.shape) != (M, K) or not mask.is_contiguous():
+            raise MoEKernelError("linear_narrow_dgrad: mask must be a contiguous [M, K] tensor")
+    gx = torch.empty((M, K), dtype=torch.bfloat16, device=g.device)
+    _check(lib().rtdetr_linear_narrow_dgrad(_ptr(g), _ptr(w), _ptr(mask), _ptr(gx), M, K, N, _stream()),
+           "rtdetr_linear_narrow_dgrad")
+    return gx
 
 
 LINEAR_WGRAD_BATCH = 24  # problems per rtdetr_linear_wgrad_batch launch

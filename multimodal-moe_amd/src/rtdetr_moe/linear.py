@@ -29,6 +29,21 @@ DEFER_WGRAD = [os.environ.get("MOE_DEFER_WGRAD", "1") != "0"]
 # the narrow heads' gradients deferred too, batched into one launch pair
 # (MOE_NARROW_DEFER=0: one launch pair per head, as before)
 NARROW_DEFER = [os.environ.get("MOE_NARROW_DEFER", "1") != "0"]
+# narrow heads (N <= 8 outputs, or K <= 8 inputs) through rtdetr_linear_narrow_fwd /
+# _dgrad instead of hipBLASLt's 1-8-column GEMMs + a ReLU (backward) launch
+NARROW_LINEAR = [os.environ.get("MOE_NARROW_LINEAR", "1") != "0"]
+
+
+def _narrow_fwd_ok(x, w, b):
+    from ..moe import _lib as L
+
+    return (NARROW_LINEAR[0] and x.is_cuda and x.dtype == w.dtype == torch.bfloat16 and x.numel() > 0
+            and (b is None or b.dtype in (torch.bfloat16, torch.float32)) and L.linear_narrow_ok(w.shape[1], w.shape[0]))
+
+
+def _narrow_dgrad_ok(g2, w):
+    return (NARROW_LINEAR[0] and g2.is_cuda and g2.dtype == w.dtype == torch.bfloat16 and w.shape[0] <= 8
+            and w.shape[1] % 8 == 0 and g2.shape[0] > 0)
 _ACTIVE: list = [None]  # the DeferredWgrad collecting during a backward, or None
 
 
@@ -345,6 +360,11 @@ class _TokenLinear(torch.autograd.Function):
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.weight_dtype = weight.dtype
         ctx.targets = _defer_targets(weight, bias, x)
+        if _narrow_fwd_ok(xc, wc, bc) and wc.shape[0] <= 8:
+            from ..moe import _lib as L
+
+            y = L.linear_narrow_fwd(xc.reshape(-1, xc.shape[-1]).contiguous(), wc.contiguous(), bc)
+            return y.view(*xc.shape[:-1], wc.shape[0])
         return F.linear(xc, wc, bc)
 
     @staticmethod
@@ -352,7 +372,14 @@ class _TokenLinear(torch.autograd.Function):
         xc, wc = ctx.saved_tensors
         g2 = gy.reshape(-1, gy.shape[-1]).to(wc.dtype).contiguous()
         x2 = xc.reshape(-1, xc.shape[-1])
-        gx = g2.mm(wc).view(xc.shape) if ctx.needs_input_grad[0] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            if _narrow_dgrad_ok(g2, wc):
+                from ..moe import _lib as L
+
+                gx = L.linear_narrow_dgrad(g2, wc.contiguous()).view(xc.shape)
+            else:
+                gx = g2.mm(wc).view(xc.shape)
         gw, gb = _linear_wgrad(g2, x2, ctx.weight_dtype, ctx.bias_dtype, ctx.has_bias, ctx.needs_input_grad[1],
                                ctx.needs_input_grad[2], ctx.targets)
         return gx, gw, gb, None
@@ -450,6 +477,8 @@ class _MLPHip(torch.autograd.Function):
                 h = L.grouped_gemm(h, w.contiguous(), offs, 1, rows, N, K, 1,
                                    L.EPI_BIAS_RELU if relu else L.EPI_BIAS, bias=b if b.dtype == torch.bfloat16 else b.float(),
                                    dense=True)
+            elif _narrow_fwd_ok(h, w, b):  # the box heads' 256 -> 4, the query position head's 4 -> 512 (+ ReLU)
+                h = L.linear_narrow_fwd(h.contiguous(), w.contiguous(), b, relu)
             else:
                 h = F.linear(h, w, b)
                 if relu:
@@ -485,6 +514,8 @@ class _MLPHip(torch.autograd.Function):
                     # g_in = (g W) * (x_i > 0): the previous layer's ReLU mask in the epilogue
                     gin = L.grouped_gemm(g, w.contiguous(), offs, 1, rows, N_in, w.shape[0], 0, L.EPI_RELU_MASK,
                                          aux=xin, dense=True)
+                elif _narrow_dgrad_ok(g, w):  # a narrow layer: the same, one elementwise-shaped pass
+                    gin = L.linear_narrow_dgrad(g, w.contiguous(), xin.contiguous() if i > 0 else None)
                 else:
                     gin = g.mm(w)
                     if i > 0:  # ReLU backward of layer i-1's output: one launch

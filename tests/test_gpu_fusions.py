@@ -283,3 +283,87 @@ def test_fold_backward_batched_equals_per_tensor(hip_lib, monkeypatch):
     assert res[0].keys() == res[1].keys() and len(res[0]) > 40
     for k in res[0]:
         assert torch.equal(res[0][k], res[1][k]), k
+
+
+def _close_bf16(got, ref, what):
+    """Within bf16 rounding of an fp32 reference (one rounding of a sum taken
+    in another order)."""
+    got, ref = got.float(), ref.float()
+    assert torch.isfinite(got).all(), what
+    tol = 1e-2 * ref.abs().max().item() + 1e-3
+    err = (got - ref).abs().max().item()
+    assert err <= tol, f"{what}: max err {err:.3e} > {tol:.3e}"
+
+
+@pytest.mark.parametrize("M,K,N,relu,bias", [(2400, 256, 1, False, "bf16"), (2400, 256, 4, False, "bf16"),
+                                             (5003, 256, 1, False, "fp32"), (37, 512, 8, True, None),
+                                             (9, 1024, 3, False, "bf16"), (2400, 4, 512, True, "bf16"),
+                                             (11, 8, 64, False, "fp32"), (0, 256, 4, False, "bf16")])
+def test_linear_narrow_fwd_vs_fp32(hip_lib, M, K, N, relu, bias):
+    """rtdetr_linear_narrow_fwd (N <= 8 outputs: lanes per row + butterfly; K
+    <= 8 inputs: 8 outputs per thread) against an fp32 linear."""
+    from src.moe import _lib as L
+
+    torch.manual_seed(M + K + N)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    b = None if bias is None else torch.randn(N, device=DEV).to(torch.bfloat16 if bias == "bf16" else torch.float32)
+    y = L.linear_narrow_fwd(x, w, b, relu)
+    ref = torch.nn.functional.linear(x.float(), w.float(), None if b is None else b.float())
+    if relu:
+        ref = ref.relu()
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    if M:
+        _close_bf16(y, ref, "narrow fwd")
+
+
+@pytest.mark.parametrize("M,K,N,masked", [(2400, 256, 4, True), (2400, 256, 1, False), (333, 512, 8, True),
+                                          (7, 64, 3, False)])
+def test_linear_narrow_dgrad_vs_fp32(hip_lib, M, K, N, masked):
+    """rtdetr_linear_narrow_dgrad: g w, zeroed where the mask is <= 0 (the
+    previous layer's ReLU), against fp32 (exact zeros where masked)."""
+    from src.moe import _lib as L
+
+    torch.manual_seed(M + K)
+    g = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    mask = torch.randn(M, K, device=DEV).relu().to(torch.bfloat16) if masked else None
+    gx = L.linear_narrow_dgrad(g, w, mask)
+    ref = g.float() @ w.float()
+    if masked:
+        ref = ref * (mask.float() > 0)
+        assert torch.all(gx[mask <= 0] == 0)
+    _close_bf16(gx, ref, "narrow dgrad")
+
+
+def test_narrow_heads_match_library_path(hip_lib, monkeypatch):
+    """A decoder box head (MLP 256 -> 256 -> 256 -> 4), the query position
+    head (4 -> 512 -> 256) and a score head (TokenLinear 256 -> 1) with the
+    narrow kernels against the hipBLASLt + torch-ReLU composition: outputs
+    and every gradient within bf16 rounding."""
+    from src.rtdetr_moe import linear as lin
+    from src.rtdetr_moe.decoder import MLP
+
+    torch.manual_seed(5)
+    box = MLP(256, 256, 4, 3).to(DEV).to(torch.bfloat16)
+    qpos = MLP(4, 512, 256, 2).to(DEV).to(torch.bfloat16)
+    score = lin.TokenLinear(256, 1).to(DEV).to(torch.bfloat16)
+    x = torch.randn(8, 300, 256, device=DEV).to(torch.bfloat16)
+    ref_pts = torch.rand(8, 300, 4, device=DEV).to(torch.bfloat16)
+    gy = [torch.randn(8, 300, n, device=DEV).to(torch.bfloat16) for n in (4, 256, 1)]
+    mods = [box, qpos, score]
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(lin, "NARROW_LINEAR", [on])
+        for m in mods:
+            m.zero_grad(set_to_none=True)
+        xa = x.clone().requires_grad_(True)
+        outs = [box(xa), qpos(ref_pts), score(xa)]
+        torch.autograd.backward(outs, gy)
+        res.append(([o.detach() for o in outs], xa.grad.clone(),
+                    [p.grad.clone() for m in mods for p in m.parameters()]))
+    for a, b in zip(res[0][0], res[1][0]):
+        _close_bf16(a, b, "head output")
+    _close_bf16(res[0][1], res[1][1], "input gradient")
+    for a, b in zip(res[0][2], res[1][2]):
+        _close_bf16(a, b, "parameter gradient")
