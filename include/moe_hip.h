@@ -312,6 +312,16 @@ int rtdetr_linear_wgrad_narrow_batch(int n, const void* const* gy, const void* c
                                      const int* N, int n_groups, const int* group_count, void* const* dw,
                                      void* const* db, float* part, long long part_floats, int out_bf16,
                                      hipStream_t stream);
+/* The ResNet-D stem's first convolution, relu?(conv3x3(x, w, pad 1, stride) +
+ * bias) for C = 3 -> N = 32 (the frozen BatchNorm folded into w / bias): x
+ * bf16 NHWC [B, H, W, 3]; wf fp32 [9 C][N] (row (ky 3 + kx) C + c holds
+ * w[:, c, ky, kx]); bias fp32 [N] or NULL; y bf16 NHWC [B, Ho, Wo, N], 16-B
+ * aligned.  One thread per output pixel on the vector ALU (3 input channels
+ * are too shallow for the implicit GEMM's K-tiles), the weights through
+ * scalar loads; fp32 sums, one rounding.  Replaces MIOpen's convolution + a
+ * bias/ReLU pass (backbone.PResNet's stem; the reference's RT-DETR backbone). */
+int rtdetr_conv3x3_direct_fwd(const void* x, const float* wf, const float* bias, void* y, int B, int H, int W, int C,
+                              int N, int stride, int relu, hipStream_t stream);
 /* Narrow dense linears (csrc/narrow.hip), bf16 rows, fp32 accumulation, the
  * bias (bf16 when b_bf16, else fp32; NULL = none) added in fp32, one rounding:
  *   fwd:   y [M, N] = act(x [M, K] w[N, K]^T + b), act = ReLU when relu; for
@@ -750,7 +760,9 @@ int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, 
  * convolutions), no bias.  B, H, W are the INPUT x / dx dims; the output y / dy
  * is [B, Ho, Wo] with Ho = (H - 1) / stride + 1 (W likewise).
  * x / dy / y: NHWC bf16 [B, H, W, channels]; w: [N][KS][KS][C] bf16 (a
- * channels_last [N, C, KS, KS] weight); C and N multiples of 64; zero: >= 256
+ * channels_last [N, C, KS, KS] weight); C and N multiples of 64 (the forward
+ * also takes multiples of 32: 32-deep K-tiles, a partial last output-channel
+ * tile -- the stem's 32 -> 32 / 32 -> 64 layers); zero: >= 256
  * zero bytes on the device (read for padding neighbours); pointers 16-B aligned.
  *   rtdetr_conv_fwd         y[B,Ho,Wo,N] = conv(x[B,H,W,C], w)   (no im2col buffer),
  *                           with an optional fused epilogue (NULL / 0 = off):

@@ -148,8 +148,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WGN, wn = wave % WGN;
-  // XCD-aware map: the N tiles of one M tile run on one XCD (they share the A panel)
-  const int NT = a.N / BN;
+  // XCD-aware map: the N tiles of one M tile run on one XCD (they share the A panel);
+  // a partial last N tile (N % BN, forward only: the stem's 32-channel layers) reads
+  // zero weight rows and stores only its valid columns
+  const int NT = (a.N + BN - 1) / BN;
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
   const int nt = slot % NT;
   const int mt = (slot / NT) * 8 + xcd;
@@ -180,14 +182,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
   // [64 k-rows][BN] image (k-row = one of W's output channels, BN contiguous
   // input channels; ds_read_b64_tr_b16 fragments) -- no transposed copy of W.
   const uint16_t* wrow[BP];
+  bool bv[BP];  // this lane's weight row exists (n0 + r < N)
 #pragma unroll
   for (int j = 0; j < BP; ++j) {
     if constexpr (BT) {  // CPR lanes per k-row
       const int kr = (wave + NW * j) * (64 / CPR) + lane / CPR;
       wrow[j] = a.w + (size_t)kr * (KS * KS * a.N) + n0 + ((lane % CPR) ^ mimg_swz<BN>(kr)) * 8;
+      bv[j] = true;
     } else {
       const int r = (wave + NW * j) * RPI + lane / CH;
-      wrow[j] = a.w + (size_t)(n0 + r) * (KS * KS * a.C) + ((lane % CH) ^ kswz(r)) * 8;
+      bv[j] = n0 + r < a.N;
+      wrow[j] = bv[j] ? a.w + (size_t)(n0 + r) * (KS * KS * a.C) + ((lane % CH) ^ kswz(r)) * 8
+                      : a.zero + ((lane % CH) ^ kswz(r)) * 8;
     }
   }
   // K-tile kt -> (input-channel offset c0, weight tap, neighbour offset dy, dx)
@@ -225,7 +231,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
     for (int j = 0; j < BP; ++j) {
       if constexpr (BT) dma16(wrow[j] + (size_t)c0 * (KS * KS * a.N) + (KS * KS - 1 - tap) * a.N,
                               buf + BOFF + (wave + NW * j) * 1024);
-      else dma16(wrow[j] + tap * a.C + c0, buf + BOFF + (wave + NW * j) * 1024);
+      else dma16(bv[j] ? wrow[j] + tap * a.C + c0 : wrow[j], buf + BOFF + (wave + NW * j) * 1024);
     }
   };
   f32x4 acc[TM][TN];
@@ -360,7 +366,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
       return (size_t)p;
     }
   };
-  if (PRE && (a.resid != nullptr || a.mask != nullptr)) {
+  const bool ecol = n0 + ec * 8 < a.N;  // this thread's 8 output columns exist
+  if (PRE && ecol && (a.resid != nullptr || a.mask != nullptr)) {
 #pragma unroll
     for (int k = 0; k < NPRE; ++k) {
       const int p = m0 + tid / CPR + RPP * k;
@@ -370,7 +377,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
     }
   }
   float eb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (a.bias != nullptr) {
+  if (a.bias != nullptr && ecol) {
     const float4 b0 = *reinterpret_cast<const float4*>(a.bias + n0 + ec * 8);
     const float4 b1 = *reinterpret_cast<const float4*>(a.bias + n0 + ec * 8 + 4);
     eb[0] = b0.x; eb[1] = b0.y; eb[2] = b0.z; eb[3] = b0.w;
@@ -398,7 +405,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
   for (int k = 0; k < BM / RPP; ++k) {
     const int r = tid / CPR + RPP * k, c = ec;
     const int p = m0 + r;
-    if (p < a.P) {
+    if (p < a.P && ecol) {
       uint4 v = *reinterpret_cast<const uint4*>(smem + r * (BN * 2) + ((c ^ (r % CPR)) << 4));
       uint4 er, em;
       if constexpr (PRE) {
@@ -474,6 +481,68 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
         pp[a.N] = s2;
       }
     }
+  }
+}
+
+// The ResNet-D stem's first convolution (3 -> 32 channels, 3x3, stride 2,
+// pad 1, the frozen BatchNorm folded: bias + ReLU) -- 3 input channels are too
+// shallow for the implicit GEMM's K-tiles (MIOpen ran it at ~110 us plus a
+// bias + ReLU pass).  One thread per output pixel computes all NO outputs on
+// the vector ALU: its 9 CI input values loaded first (independent loads in
+// flight), the weights fp32 [9 CI][NO] read with uniform addresses (scalar
+// loads into SGPRs, operands of packed fp32 FMAs: two output channels per
+// v_pk_fma_f32; weights staged in LDS instead cost a waited ds_read per two
+// FMAs), fp32 sums + bias, ReLU, one rounding, 16-B stores of the NHWC row.
+template <int NO, int CI>
+__global__ __launch_bounds__(256) void conv_direct_kernel(const uint16_t* __restrict__ x, const float* __restrict__ wf,
+                                                          const float* __restrict__ bias, uint16_t* __restrict__ y,
+                                                          int B, int H, int W, int Ho, int Wo, int st, int relu) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const long long P = (long long)B * Ho * Wo;
+  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  const int HWo = Ho * Wo;
+  const int b = (int)(p / HWo), rem = (int)(p - (long long)b * HWo), yo = rem / Wo, xo = rem - yo * Wo;
+  // all 9 CI input loads issued first (one latency, not nine); the tap loop
+  // kept rolled (unrolled, the compiler hoists all 9 CI NO weight loads and
+  // spills SGPRs) over a shifting register window: tap t reads raw[0 .. CI)
+  // and moves the rest down
+  uint16_t raw[9 * CI];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int yy = yo * st + t / 3 - 1, xx = xo * st + t % 3 - 1;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    const uint16_t* src = x + (((size_t)b * H + (ok ? yy : 0)) * W + (ok ? xx : 0)) * CI;
+#pragma unroll
+    for (int c = 0; c < CI; ++c) raw[t * CI + c] = ok ? src[c] : (uint16_t)0;
+  }
+  f32x2 acc[NO / 2];
+#pragma unroll
+  for (int n = 0; n < NO / 2; ++n) acc[n] = f32x2{0.f, 0.f};
+#pragma unroll 1
+  for (int t = 0; t < 9; ++t) {
+    const float* wt = wf + (size_t)t * CI * NO;
+#pragma unroll
+    for (int c = 0; c < CI; ++c) {
+      const float v = bf2f(raw[c]);
+      const f32x2 vv = f32x2{v, v};
+#pragma unroll
+      for (int n = 0; n < NO; n += 2)
+        acc[n / 2] = __builtin_elementwise_fma(vv, f32x2{wt[c * NO + n], wt[c * NO + n + 1]}, acc[n / 2]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8 * CI; ++i) raw[i] = raw[i + CI];
+  }
+  uint4* out = reinterpret_cast<uint4*>(y + (size_t)p * NO);
+#pragma unroll
+  for (int n = 0; n < NO; n += 8) {
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float t = acc[(n + j) / 2][(n + j) % 2] + (bias ? bias[n + j] : 0.f);
+      o[j] = relu ? fmaxf(t, 0.f) : t;
+    }
+    out[n / 8] = pack8(o);
   }
 }
 
@@ -714,12 +783,12 @@ static void allow_lds_once(size_t bytes) {
 static int conv_out(int n, int KS, int stride) { return (n + 2 * ((KS - 1) / 2) - KS) / stride + 1; }
 
 static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int C, int N, int KS, int stride,
-                      const char* what) {
+                      const char* what, int cmul = 64) {
   if (KS != 1 && KS != 3) return fail(std::string(what) + ": kernel size must be 1 or 3");
   if (stride != 1 && !(stride == 2 && KS == 3)) return fail(std::string(what) + ": stride must be 1 (or 2 with KS 3)");
   if (B < 0 || H <= 0 || W <= 0) return fail(std::string(what) + ": bad B / H / W");
-  if (C % 64 || N % 64 || C <= 0 || N <= 0)
-    return fail(std::string(what) + ": channels must be positive multiples of 64");
+  if (C % cmul || N % cmul || C <= 0 || N <= 0)
+    return fail(std::string(what) + ": channels must be positive multiples of " + std::to_string(cmul));
   if ((long long)B * H * W * (C > N ? C : N) >= (1ll << 31)) return fail(std::string(what) + ": tensor too large");
   for (int i = 0; i < np; ++i)
     if (ptrs[i] == nullptr || reinterpret_cast<uintptr_t>(ptrs[i]) % 16)
@@ -740,7 +809,7 @@ static void launch_fwd_n(ConvArgs a, hipStream_t stream, ProfScope& prof) {
   static_assert(!(BT && BN > 128), "the in-place (MN-contiguous) weight image takes 64 or 128 columns");
   allow_lds_once<conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN, AR, KT>>(lds);
   a.mt_n = (a.P + BM - 1) / BM;
-  const int NT = a.N / BN;
+  const int NT = (a.N + BN - 1) / BN;
   const int grid = ((a.mt_n + 7) / 8) * 8 * NT;
   MOE_LAUNCH(prof, (conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN, AR, KT>), dim3(grid), dim3(64 * WGM * WGN),
              lds, stream, a);
@@ -786,14 +855,14 @@ static int k32_auto(int KS, const ConvArgs& a) {
 template <int KS, int BM, bool BT, bool PH>
 static void launch_fwd(const ConvArgs& a, hipStream_t stream, ProfScope& prof) {
   if constexpr (BM == 128) {
-    if (g_conv_areg == 1) {
+    if (g_conv_areg == 1 && a.C % 64 == 0 && a.N % 64 == 0) {
       if (a.N % 128 == 0) launch_fwd_n<KS, BM, 128, BT, PH, 2, 2, 2, true>(a, stream, prof);
       else launch_fwd_n<KS, BM, 64, BT, PH, 2, 2, 2, true>(a, stream, prof);
       return;
     }
   }
   if constexpr (BM == 128 || BM == 64) {
-    const int k32 = g_conv_k32 >= 0 ? g_conv_k32 : k32_auto(KS, a);
+    const int k32 = a.C % 64 ? (g_conv_k32 >= 2 ? g_conv_k32 : 1) : (g_conv_k32 >= 0 ? g_conv_k32 : k32_auto(KS, a));
     if (k32 >= 1 && k32 <= 3) {  // 32-deep K-tiles, ring depth 2-4
       const bool w = a.N % 128 == 0;
       switch (k32) {
@@ -824,7 +893,8 @@ static int fwd_bm(long long P, int N) {
 
 template <bool BT, bool PH = false>
 static void launch_fwd_any(const ConvArgs& a, int KS, hipStream_t stream, ProfScope& prof) {
-  if (g_conv_big > 0) {  // "conv_big" 1: the 8-wave 256 x 128 tile where N % 128 == 0
+  const bool c32 = a.C % 64 != 0 || a.N % 64 != 0;  // 32-channel multiples: the 32-deep, 64-wide tiles only
+  if (g_conv_big > 0 && !c32) {  // "conv_big" 1: the 8-wave 256 x 128 tile where N % 128 == 0
     if constexpr (PH) {
       if (launch_fwd_big<3, BT, true>(a, stream, prof, g_conv_big)) return;
     } else {
@@ -833,7 +903,8 @@ static void launch_fwd_any(const ConvArgs& a, int KS, hipStream_t stream, ProfSc
         return;
     }
   }
-  const int bm = fwd_bm(a.P, a.N);
+  int bm = fwd_bm(a.P, a.N);
+  if (c32 && bm == 256) bm = 128;
   if constexpr (PH) {  // 3x3 only
     if (bm == 256) launch_fwd<3, 256, BT, true>(a, stream, prof);
     else if (bm == 64) launch_fwd<3, 64, BT, true>(a, stream, prof);
@@ -887,7 +958,8 @@ extern "C" int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void
                                int N, int KS, int stride, const float* bias, const void* resid, int relu,
                                hipStream_t stream) {
   const void* ptrs[4] = {x, w, y, zero};
-  if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, stride, "rtdetr_conv_fwd")) return rc;
+  // (the forward alone also takes 32-channel multiples: 32-deep K-tiles, a partial N tile)
+  if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, stride, "rtdetr_conv_fwd", 32)) return rc;
   if (!aligned16(bias) || !aligned16(resid)) return fail("rtdetr_conv_fwd: bias / resid must be 16-B aligned");
   if (B == 0) return 0;
   const int Ho = conv_out(H, KS, stride), Wo = conv_out(W, KS, stride);
@@ -1069,6 +1141,24 @@ extern "C" int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int
   MOE_LAUNCH(prof, conv_wgrad_reduce_kernel, dim3((unsigned)((nw / 4 + 15) / 16)), dim3(256), 0, stream, part,
              nsplit, nw, dw, out_bf16);
   return check_launch("rtdetr_conv_wgrad (reduce)");
+}
+
+extern "C" int rtdetr_conv3x3_direct_fwd(const void* x, const float* wf, const float* bias, void* y, int B, int H,
+                                         int W, int C, int N, int stride, int relu, hipStream_t stream) {
+  if (C != 3 || N != 32) return fail("rtdetr_conv3x3_direct_fwd: takes C = 3 -> N = 32 (the ResNet-D stem)");
+  if (stride != 1 && stride != 2) return fail("rtdetr_conv3x3_direct_fwd: stride 1 or 2");
+  if (B < 0 || H <= 0 || W <= 0) return fail("rtdetr_conv3x3_direct_fwd: bad B / H / W");
+  if (B == 0) return 0;
+  if (x == nullptr || wf == nullptr || y == nullptr || reinterpret_cast<uintptr_t>(y) % 16)
+    return fail("rtdetr_conv3x3_direct_fwd: x, wf non-NULL, y 16-B aligned");
+  const int Ho = conv_out(H, 3, stride), Wo = conv_out(W, 3, stride);
+  const long long P = (long long)B * Ho * Wo;
+  const long long blocks = (P + 255) / 256;
+  if (blocks > 0x7fffffffLL) return fail("rtdetr_conv3x3_direct_fwd: too many pixels");
+  ProfScope prof(stream, PROF_CONV, 2.0 * ((double)B * H * W * C + P * N), false, 0.0, 2.0 * P * N * 9 * C);
+  MOE_LAUNCH(prof, (conv_direct_kernel<32, 3>), dim3((unsigned)blocks), dim3(256), 0, stream,
+             static_cast<const uint16_t*>(x), wf, bias, static_cast<uint16_t*>(y), B, H, W, Ho, Wo, stride, relu);
+  return check_launch("rtdetr_conv3x3_direct_fwd");
 }
 
 extern "C" int rtdetr_conv_set_tuning(const char* key, int value) {

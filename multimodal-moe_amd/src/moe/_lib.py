@@ -47,6 +47,7 @@ SIGNATURES = {
     "rtdetr_linear_wgrad_narrow_batch_parts": (ctypes.c_longlong, [_I, _P, _P, _P]),
     "rtdetr_linear_wgrad_narrow_batch": (_I, [_I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, ctypes.c_longlong, _I,
                                               _P]),
+    "rtdetr_conv3x3_direct_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rtdetr_linear_narrow_supported": (_I, [_I, _I]),
     "rtdetr_linear_narrow_fwd": (_I, [_P, _P, _P, _I, _P, _LL, _I, _I, _I, _P]),
     "rtdetr_linear_narrow_dgrad": (_I, [_P, _P, _P, _P, _LL, _I, _I, _P]),
@@ -817,6 +818,29 @@ def linear_wgrad_narrow(gy, x, out_dtype):
                                             int(out_dtype == torch.bfloat16), _stream()),
            "rtdetr_linear_wgrad_narrow")
     return dw, db
+
+
+def conv3x3_direct_fwd(x, w, bias, stride=1, relu=True):
+    """relu(conv3x3(x, w, pad 1) + bias) for the stem's 3 -> 32 layer
+    (rtdetr_conv3x3_direct_fwd): x bf16 [B, 3, H, W] channels_last, w bf16
+    [32, 3, 3, 3] (any strides), bias fp32 [32] or None -> bf16 channels_last."""
+    for t, name in ((x, "x"), (w, "w")):
+        if not t.is_cuda or t.dtype != torch.bfloat16:
+            raise MoEKernelError(f"conv3x3_direct_fwd: {name} must be a bf16 GPU tensor (no CPU fallback)")
+    B, C, H, W = x.shape
+    N = w.shape[0]
+    if not x.is_contiguous(memory_format=torch.channels_last) or tuple(w.shape[1:]) != (C, 3, 3):
+        raise MoEKernelError("conv3x3_direct_fwd: x channels_last [B, C, H, W], w [N, C, 3, 3]")
+    if bias is not None:
+        _need(bias, torch.float32, "bias")
+        if bias.numel() != N or not bias.is_contiguous():
+            raise MoEKernelError("conv3x3_direct_fwd: bias fp32 [N]")
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    wf = w.permute(2, 3, 1, 0).reshape(9 * C, N).float().contiguous()  # [(ky 3 + kx) C + c][n]
+    y = torch.empty((B, N, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    _check(lib().rtdetr_conv3x3_direct_fwd(_ptr(x), _ptr(wf), _ptr(bias), _ptr(y), B, H, W, C, N, int(stride),
+                                           int(bool(relu)), _stream()), "rtdetr_conv3x3_direct_fwd")
+    return y
 
 
 def linear_narrow_ok(K, N):

@@ -141,6 +141,9 @@ class _FoldAll(torch.autograd.Function):
 
 # MOE_FOLD_BWD_BATCH=0: one torch.mul per folded weight's gradient (A/B switch)
 _FOLD_BWD_BATCH = os.environ.get("MOE_FOLD_BWD_BATCH", "1") != "0"
+# the frozen stem on libmoe_hip: 1 = the direct 3 -> 32 kernel, 2 = also the
+# 32 -> 32 / 32 -> 64 layers on the implicit GEMM; 0: modules (MIOpen)
+_STEM_HIP = int(os.environ.get("MOE_STEM_HIP", "2"))
 
 
 def _fold_batch_ok(g, gw):
@@ -576,9 +579,41 @@ class PResNet(nn.Module):
         for l, w in zip(plan.layers, outs):
             l._w_folded = w
 
+    def _stem_hip_ok(self, x):
+        return (_STEM_HIP and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[0] > 0
+                and x.shape[1] == 3 and not x.requires_grad and x.is_contiguous(memory_format=torch.channels_last)
+                and len(self.stem) == 3 and all(isinstance(l, ConvNormLayer) and l.fold and l.act_name == "relu"
+                                                and l.conv.kernel_size == (3, 3) for l in self.stem)
+                and [l.conv.out_channels for l in self.stem] == [32, 32, 64]
+                and not any(p.requires_grad for p in self.stem.parameters())
+                and all(l.conv.weight.dtype == torch.bfloat16 for l in self.stem))
+
+    def _stem(self, x):
+        """The frozen ResNet-D stem (three 3x3 conv + folded BN + ReLU).  GPU
+        bf16 without gradients: the 3 -> 32 layer on the direct kernel
+        (rtdetr_conv3x3_direct_fwd, bias + ReLU fused); with MOE_STEM_HIP=2
+        also the 32 -> 32 / 32 -> 64 layers on the implicit-GEMM forward
+        (32-deep K-tiles, bias + ReLU in its epilogue).  Elsewhere the
+        modules."""
+        if not self._stem_hip_ok(x):
+            return self.stem(x)
+        from ..moe import _lib as L
+        from .conv import _fwd, _nhwc
+
+        l1, l2, l3 = self.stem
+        w, shift = l1.folded()
+        y = L.conv3x3_direct_fwd(x, w, shift.float().contiguous(), l1.conv.stride[0], True)
+        for l in (l2, l3):
+            if _STEM_HIP >= 2:
+                w, shift = l.folded()
+                y = _fwd(y, _nhwc(w), shift.float().contiguous(), None, True, l.conv.stride[0])
+            else:
+                y = l(y)
+        return y
+
     def forward(self, x):
         self._fold_all()
-        x = stem_max_pool(self.stem(x), self.pool)
+        x = stem_max_pool(self._stem(x), self.pool)
         xs = None
         outs = []
         for i, stage in enumerate(self.stages):

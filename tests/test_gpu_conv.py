@@ -442,3 +442,61 @@ def test_bn_act_with_conv_stats_matches_stats_pass(hip_lib):
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
     for a, b in zip(ga, gb):
         assert ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item() < 1e-2
+
+
+@pytest.mark.parametrize("B,H,W,st", [(2, 64, 96, 2), (1, 37, 50, 2), (2, 20, 24, 1)])
+def test_conv3x3_direct_stem_vs_fp32(hip_lib, B, H, W, st):
+    """rtdetr_conv3x3_direct_fwd (the stem's 3 -> 32 layer, bias + ReLU, odd
+    sizes, NCHW- and channels_last-strided weights) against fp32."""
+    from src.moe import _lib as L
+
+    g = torch.Generator(device=DEV).manual_seed(H + W)
+    x = torch.randn(B, 3, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(32, 3, 3, 3, device=DEV, generator=g) * 0.3).to(torch.bfloat16)
+    b = torch.randn(32, device=DEV, generator=g)
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), b, st, 1).relu()
+    for wl in (w, w.contiguous(memory_format=torch.channels_last)):
+        y = L.conv3x3_direct_fwd(x, wl, b, st, True)
+        assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+        _check(y, ref, "direct stem conv")
+
+
+@pytest.mark.parametrize("C,N,ks,st", [(32, 32, 3, 1), (32, 64, 3, 1), (32, 96, 1, 1), (64, 32, 3, 2), (96, 64, 3, 1)])
+def test_conv_fwd_32_channel_multiples(hip_lib, C, N, ks, st):
+    """The implicit-GEMM forward on 32-channel multiples (32-deep K-tiles, a
+    partial last output-channel tile), with the bias + ReLU epilogue, against
+    fp32."""
+    from src.rtdetr_moe.conv import _fwd
+
+    g = torch.Generator(device=DEV).manual_seed(C + N + ks)
+    B, H, W = 2, 23, 41
+    x = torch.randn(B, C, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(N, C, ks, ks, device=DEV, generator=g) * (C * ks * ks) ** -0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    b = torch.randn(N, device=DEV, generator=g)
+    y = _fwd(x, w, b, None, True, st)
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), b, st, (ks - 1) // 2).relu()
+    _check(y, ref, "32-channel conv fwd")
+
+
+def test_stem_hip_matches_modules(hip_lib, monkeypatch):
+    """PResNet's frozen stem on libmoe_hip (direct 3 -> 32, implicit GEMMs
+    for 32 -> 32 -> 64 with the folded shift + ReLU in the epilogue) against
+    the modules (MIOpen + the bias/ReLU kernel): within bf16 rounding."""
+    from src.rtdetr_moe import backbone as bb
+
+    torch.manual_seed(3)
+    m = bb.PResNet(50).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for mod in m.stem.modules():
+        if hasattr(mod, "running_var") and not isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_var.uniform_(0.5, 2.0)
+            mod.running_mean.uniform_(-0.2, 0.2)
+    x = torch.randn(2, 3, 96, 160, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    with torch.no_grad():
+        for mode in (2, 1, 0):
+            monkeypatch.setattr(bb, "_STEM_HIP", mode)
+            assert m._stem_hip_ok(x) == (mode > 0)
+            outs.append(m._stem(x))
+    _check(outs[0], outs[2], "stem (all HIP)")
+    _check(outs[1], outs[2], "stem (direct first layer)")
