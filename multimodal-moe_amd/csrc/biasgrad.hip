@@ -29,7 +29,11 @@ __global__ __launch_bounds__(256) void bias_grad_part_kernel(const uint16_t* __r
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
   if (rl < RL) {
-    constexpr int U = 4;  // loads in flight per thread
+    // loads in flight per thread: with 16-B row vectors a wide gradient has few
+    // row lanes per block (N = 1,536: one, 192 threads), so 8 rows per thread
+    // keep ~50 KB per CU in flight (4: the value projection's 475 MB column sum
+    // ran at 3.7 TB/s)
+    constexpr int U = VEC == 8 ? 8 : 4;
     for (long long r = r0 + rl; r < r1; r += (long long)U * RL) {
       if constexpr (VEC == 8) {
         uint4 raw[U];
@@ -458,9 +462,9 @@ extern "C" int rtdetr_linear_wgrad_narrow_batch(int n, const void* const* gy, co
 
 extern "C" int rtdetr_bias_grad_parts(long long M, int N) {
   if (M <= 0 || N <= 0) return 1;
-  // ~128 rows per block at small M, at most 256 blocks (one per CU) at large M
+  // ~128 rows per block at small M, at most 512 blocks (two per CU) at large M
   long long p = (M + 127) / 128;
-  return (int)(p > 256 ? 256 : p);
+  return (int)(p > 512 ? 512 : p);
 }
 
 extern "C" int rtdetr_bias_grad(const void* dy, long long M, int N, float* partials, int P, void* out, int out_bf16,
