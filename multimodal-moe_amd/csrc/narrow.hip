@@ -14,6 +14,8 @@
 //                 previous layer's ReLU mask applied in the same pass
 // fp32 accumulation, the bias added in fp32, one rounding to bf16 (as the
 // library GEMM's bias epilogue); the sum order is fixed (deterministic).
+#include <algorithm>
+
 #include "moe_common.h"
 #include "prof.h"
 
@@ -67,15 +69,28 @@ __global__ __launch_bounds__(256) void linear_narrow_out_kernel(const uint16_t* 
   }
 }
 
+// A thread keeps one 8-output chunk (its 8 K weights and biases in registers,
+// loaded once) and walks the rows with a stride of the rows in flight: the
+// per-row work is one x row load and one 16-B store (loading the weights per
+// output per row made this 15 us for the 2,400 x 4 -> 512 layer).
 __global__ __launch_bounds__(256) void linear_smallk_kernel(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ w, const void* b, int b_bf16,
                                                             uint16_t* __restrict__ y, long long M, int K, int N,
                                                             int relu) {
   const int nc = N >> 3;
-  const long long total = M * nc;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const long long r = i / nc;
-    const int n0 = (int)(i - r * nc) * 8;
+  const long long lanes = (long long)gridDim.x * 256;
+  const long long rows_in_flight = lanes / nc;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows_in_flight * nc) return;
+  const int n0 = (int)(i % nc) * 8;
+  float wr[8][8], bs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bs[j] = bias_at(b, b_bf16, n0 + j);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wr[j][k] = k < K ? bf2f(w[(size_t)(n0 + j) * K + k]) : 0.f;
+  }
+  for (long long r = i / nc; r < M; r += rows_in_flight) {
     float xv[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) xv[k] = k < K ? bf2f(x[r * K + k]) : 0.f;
@@ -85,8 +100,8 @@ __global__ __launch_bounds__(256) void linear_smallk_kernel(const uint16_t* __re
       float s = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        if (k < K) s = fmaf(xv[k], bf2f(w[(size_t)(n0 + j) * K + k]), s);
-      s += bias_at(b, b_bf16, n0 + j);
+        if (k < K) s = fmaf(xv[k], wr[j][k], s);
+      s += bs[j];
       o[j] = relu ? fmaxf(s, 0.f) : s;
     }
     reinterpret_cast<uint4*>(y + r * N)[n0 >> 3] = pack8(o);
@@ -178,8 +193,10 @@ extern "C" int rtdetr_linear_narrow_fwd(const void* x, const void* w, const void
                  N, lg, relu);
   } else {
     if (!al16(y)) return fail("rtdetr_linear_narrow_fwd: y must be 16-B aligned");
-    MOE_LAUNCH(prof, linear_smallk_kernel, dim3(ew_grid(M * (N / 8))), dim3(256), 0, stream, x16, w16, b, b_bf16,
-               y16, M, K, N, relu);
+    // ~8 rows per thread (at least one chunk of rows per 256 threads), <= 2,048 workgroups
+    const long long want = (M * (N / 8) + 8 * 256 - 1) / (8 * 256);
+    const int grid = (int)std::max(1LL, std::min(2048LL, std::max(want, (long long)(N / 8 + 255) / 256)));
+    MOE_LAUNCH(prof, linear_smallk_kernel, dim3(grid), dim3(256), 0, stream, x16, w16, b, b_bf16, y16, M, K, N, relu);
   }
   return check_launch("rtdetr_linear_narrow_fwd");
 }
