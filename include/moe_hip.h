@@ -312,6 +312,15 @@ int rtdetr_linear_wgrad_narrow_batch(int n, const void* const* gy, const void* c
                                      const int* N, int n_groups, const int* group_count, void* const* dw,
                                      void* const* db, float* part, long long part_floats, int out_bf16,
                                      hipStream_t stream);
+/* Row-wise top-k of fp32 scores (RT-DETR query selection: k = 300 of the S
+ * memory tokens per image): x fp32 [rows][n], n <= 32768, 0 < k <= min(n,
+ * 1024); idx int64 [rows][k] sorted by value descending (equal values: the
+ * lower index first; at the cut the lowest indices among equal values are
+ * kept); val fp32 [rows][k] or NULL.  One 1,024-thread workgroup per row:
+ * radix select over LDS-staged keys, ordered compaction, bitonic sort.
+ * Replaces torch.topk (decoder.RTDETRDecoder.forward; the reference's
+ * RT-DETR query selection). */
+int rtdetr_topk_rows(const float* x, int rows, int n, int k, long long* idx, float* val, hipStream_t stream);
 /* The ResNet-D stem's first convolution, relu?(conv3x3(x, w, pad 1, stride) +
  * bias) for C = 3 -> N = 32 (the frozen BatchNorm folded into w / bias): x
  * bf16 NHWC [B, H, W, 3]; wf fp32 [9 C][N] (row (ky 3 + kx) C + c holds

@@ -47,6 +47,7 @@ SIGNATURES = {
     "rtdetr_linear_wgrad_narrow_batch_parts": (ctypes.c_longlong, [_I, _P, _P, _P]),
     "rtdetr_linear_wgrad_narrow_batch": (_I, [_I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, ctypes.c_longlong, _I,
                                               _P]),
+    "rtdetr_topk_rows": (_I, [_P, _I, _I, _I, _P, _P, _P]),
     "rtdetr_conv3x3_direct_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rtdetr_linear_narrow_supported": (_I, [_I, _I]),
     "rtdetr_linear_narrow_fwd": (_I, [_P, _P, _P, _I, _P, _LL, _I, _I, _I, _P]),
@@ -818,6 +819,24 @@ def linear_wgrad_narrow(gy, x, out_dtype):
                                             int(out_dtype == torch.bfloat16), _stream()),
            "rtdetr_linear_wgrad_narrow")
     return dw, db
+
+
+TOPK_MAX_N, TOPK_MAX_K = 32768, 1024
+
+
+def topk_rows(x, k, values=False):
+    """Top-k of each row of fp32 x [rows, n] (rtdetr_topk_rows: radix select +
+    bitonic sort in LDS, n <= 32768, k <= 1024) -> int64 indices [rows, k],
+    sorted by value descending (equal values: lower index first; and the
+    lowest indices among equal values at the cut), plus the values when asked."""
+    if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 2:
+        raise MoEKernelError("topk_rows: x must be an fp32 [rows, n] GPU tensor (no CPU fallback)")
+    x = x.contiguous()
+    rows, n = x.shape
+    idx = torch.empty((rows, k), dtype=torch.int64, device=x.device)
+    val = torch.empty((rows, k), dtype=torch.float32, device=x.device) if values else None
+    _check(lib().rtdetr_topk_rows(_ptr(x), rows, n, int(k), _ptr(idx), _ptr(val), _stream()), "rtdetr_topk_rows")
+    return (idx, val) if values else idx
 
 
 def conv3x3_direct_fwd(x, w, bias, stride=1, relu=True):

@@ -217,6 +217,18 @@ class _LevelMemory(torch.autograd.Function):
         return (None, None, *dxs, *dgs, *dbs)
 
 
+def _select_queries(rank, k):
+    """Indices of the k best-ranked memory tokens per image, best first:
+    libmoe_hip's rtdetr_topk_rows on the GPU (torch.topk ran one
+    single-workgroup sort per image, ~128 us at C2), torch.topk elsewhere."""
+    from ..moe import _lib as L
+
+    if (_HIP_TOPK and rank.is_cuda and rank.dtype == torch.float32 and rank.dim() == 2
+            and rank.shape[1] <= L.TOPK_MAX_N and 0 < k <= min(L.TOPK_MAX_K, rank.shape[1])):
+        return L.topk_rows(rank, k)
+    return torch.topk(rank, k, dim=1).indices
+
+
 class _ValueProjAll(torch.autograd.Function):
     """The decoder layers' value projections over the encoder memory as ONE
     GEMM, [B*S, d] x [d, n d] with the n layers' weights concatenated per call
@@ -329,6 +341,8 @@ _DET_MSDA = os.environ.get("MOE_DET_MSDA", "1") != "0"
 _LEVEL_MEMORY = os.environ.get("MOE_LEVEL_MEMORY", "1") != "0"
 # MOE_MASK_ROWS=0: the ranking's valid * memory as a full multiply (A/B switch)
 _MASK_ROWS = os.environ.get("MOE_MASK_ROWS", "1") != "0"
+# query selection top-k on libmoe_hip (rtdetr_topk_rows); 0: torch.topk
+_HIP_TOPK = os.environ.get("MOE_HIP_TOPK", "1") != "0"
 
 
 def _det_msda(L, P, D):
@@ -565,7 +579,7 @@ class RTDETRDecoder(nn.Module):
             with torch.no_grad():
                 inv = self._anchor_cache[("inv", tuple(shapes), memory.device, torch.float32)]
                 enc_rank = self.enc_score_head(self._enc_output_masked(memory, inv, vmask)).float().max(-1).values
-            topk = torch.topk(enc_rank, self.num_queries, dim=1).indices
+            topk = _select_queries(enc_rank, self.num_queries)
         self.last_topk = topk
         # (valid * memory) at the selected rows: the mask applied after the
         # gather (same products), so the backward multiplies [B, Q, d], not [B, S, d]

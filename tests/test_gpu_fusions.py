@@ -367,3 +367,37 @@ def test_narrow_heads_match_library_path(hip_lib, monkeypatch):
     _close_bf16(res[0][1], res[1][1], "input gradient")
     for a, b in zip(res[0][2], res[1][2]):
         _close_bf16(a, b, "parameter gradient")
+
+
+@pytest.mark.parametrize("rows,n,k,ties", [(8, 19320, 300, False), (8, 19320, 300, True), (3, 8400, 300, True),
+                                           (2, 1000, 1000, True), (5, 700, 1, False), (1, 32768, 1024, True)])
+def test_topk_rows_vs_torch(hip_lib, rows, n, k, ties):
+    """rtdetr_topk_rows: the same sorted values as torch.topk; without ties the
+    same indices; with ties (bf16-quantised scores) a valid top-k whose equal
+    values are ordered by index and cut at the lowest indices."""
+    from src.moe import _lib as L
+
+    g = torch.Generator(device=DEV).manual_seed(n + k)
+    x = torch.randn(rows, n, device=DEV, generator=g)
+    if ties:
+        x = x.to(torch.bfloat16).float()
+    idx, val = L.topk_rows(x, k, values=True)
+    ref_v, ref_i = torch.topk(x, k, dim=1)
+    assert torch.equal(val, ref_v)
+    assert torch.equal(torch.gather(x, 1, idx), val)
+    srt = idx.sort(1).values
+    assert torch.all(srt[:, 1:] != srt[:, :-1])  # distinct indices per row
+    if not ties:
+        assert torch.equal(idx, ref_i)
+    else:
+        kth = val[:, -1:]
+        # every value above the cut is taken; at the cut the lowest indices are
+        for r in range(rows):
+            above = (x[r] > kth[r]).nonzero().flatten()
+            assert set(above.tolist()) <= set(idx[r].tolist())
+            eq_all = (x[r] == kth[r]).nonzero().flatten().sort().values
+            eq_taken = idx[r][val[r] == kth[r]].sort().values
+            assert torch.equal(eq_taken, eq_all[:eq_taken.numel()])
+        # equal values ordered by index
+        same = val[:, 1:] == val[:, :-1]
+        assert torch.all(idx[:, 1:][same] > idx[:, :-1][same])
