@@ -11,14 +11,17 @@ for the MXFP8 (C5) and expert-parallel (C4) compositions:
                   row map: ONE moe_expert_ffn_fwd launch (GEMM1 +b1, ReLU,
                   H written once, GEMM2 +b2 on H still in registers), or
                   GEMM1 and GEMM2 as two grouped GEMMs (MOE_FUSED_FFN=0)
-                  backward: two paired launches (moe_grouped_gemm_bwd_pair):
-                  {dH = dgrad (ReLU mask), dW2 + db2} and {dXp = dgrad, dW1 + db1
-                  with the token rows gathered}
+                  backward: up to 1,024 rows per expert (the decoder)
+                  moe_expert_ffn_bwd -- dH = dgrad (ReLU mask), then {dW2 +
+                  db2, dW1 + db1, dXp} in ONE grid --; above (the encoder)
+                  two paired launches (moe_grouped_gemm_bwd_pair): {dH, dW2 +
+                  db2} and {dXp = dgrad, dW1 + db1 with the token rows gathered}
   _Combine        gate-weighted combine (K3); backward: combine_bwd
 Single GPU (_MoELayer): 4 launches forward (router, route_dispatch, the fused
 expert FFN -- or GEMM1 + GEMM2 below 1,536 rows per expert --, combine with
-the residual), 4 backward (2 pairs with the combine transpose folded in,
-token_bwd, router_wgrad: dWg and the context-bias gradient in one launch).  The
+the residual), 4 backward (the expert FFN backward in two launches with the
+combine transpose folded in, token_bwd, router_wgrad: dWg and the
+context-bias gradient in one launch).  The
 expert-parallel path (ep.py) moves real rows through its all-to-alls and runs
 _RouteDispatch (permute) + _ExpertFFN (rows in, same paired backward).  Nothing is synchronised with the host: expert
 offsets stay on the device, grids are sized from host upper bounds, and the
