@@ -16,7 +16,8 @@ tokens whose CPU top-(k+1) logit margin exceeds EPS_MARGIN), next to the
 router kernel's agreement with the fp64 oracle on the GPU's own activations.
 
 Configs: C1's model (R18 + 4-expert top-1) at 640x640, batch 2, and C2's
-(R50 + 8-expert top-2) at 1280x720 (padded to 736), batch 2, random-init
+(R50 + 8-expert top-2) at 1280x720 (padded to 736), batch 2 and -- in bf16,
+the bench precision -- C2's own batch 8, random-init
 weights with the frozen backbone BatchNorm statistics calibrated on the batch
 (backbone.calibrate_frozen_bn: the default mean-0 / var-1 statistics of a
 random backbone let its features vanish, which amplifies any rounding
@@ -145,8 +146,11 @@ def _sets(out):
 
 
 @pytest.mark.parametrize("precision", ["bf16", "amp"])
-@pytest.mark.parametrize("spec,B,h,w", [("rtdetr-r18-moe4-top1", 2, 640, 640), ("rtdetr-r50-moe8-top2", 2, 720, 1280)])
+@pytest.mark.parametrize("spec,B,h,w", [("rtdetr-r18-moe4-top1", 2, 640, 640), ("rtdetr-r50-moe8-top2", 2, 720, 1280),
+                                        ("rtdetr-r50-moe8-top2", 8, 720, 1280)])
 def test_detector_gpu_vs_cpu(hip_lib, spec, B, h, w, precision):
+    if B == 8 and precision != "bf16":
+        pytest.skip("C2's batch 8 at the bench precision (bf16) only: the CPU runs take ~1 min")
     from oracle import moe_oracle as O
     from src.moe import _lib as L
     from src.moe import eager
