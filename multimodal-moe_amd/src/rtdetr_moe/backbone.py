@@ -579,14 +579,23 @@ class PResNet(nn.Module):
         for l, w in zip(plan.layers, outs):
             l._w_folded = w
 
+    @staticmethod
+    def _stem_amp():
+        return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
     def _stem_hip_ok(self, x):
-        return (_STEM_HIP and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[0] > 0
+        """bf16 input and weights -- or fp32 ones under bf16 autocast (the
+        evaluation forward, precision "amp"), cast as autocast would for the
+        convolutions."""
+        amp = self._stem_amp()
+        ok_dt = (torch.bfloat16, torch.float32) if amp else (torch.bfloat16,)
+        return (_STEM_HIP and x.is_cuda and x.dtype in ok_dt and x.dim() == 4 and x.shape[0] > 0
                 and x.shape[1] == 3 and not x.requires_grad and x.is_contiguous(memory_format=torch.channels_last)
                 and len(self.stem) == 3 and all(isinstance(l, ConvNormLayer) and l.fold and l.act_name == "relu"
                                                 and l.conv.kernel_size == (3, 3) for l in self.stem)
                 and [l.conv.out_channels for l in self.stem] == [32, 32, 64]
                 and not any(p.requires_grad for p in self.stem.parameters())
-                and all(l.conv.weight.dtype == torch.bfloat16 for l in self.stem))
+                and all(l.conv.weight.dtype in ok_dt for l in self.stem))
 
     def _stem(self, x):
         """The frozen ResNet-D stem (three 3x3 conv + folded BN + ReLU).  GPU
@@ -601,12 +610,14 @@ class PResNet(nn.Module):
         from .conv import _fwd, _nhwc
 
         l1, l2, l3 = self.stem
+        if x.dtype != torch.bfloat16:  # bf16 autocast: the convolution's own input cast
+            x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         w, shift = l1.folded()
-        y = L.conv3x3_direct_fwd(x, w, shift.float().contiguous(), l1.conv.stride[0], True)
+        y = L.conv3x3_direct_fwd(x, w.to(torch.bfloat16), shift.float().contiguous(), l1.conv.stride[0], True)
         for l in (l2, l3):
             if _STEM_HIP >= 2:
                 w, shift = l.folded()
-                y = _fwd(y, _nhwc(w), shift.float().contiguous(), None, True, l.conv.stride[0])
+                y = _fwd(y, _nhwc(w.to(torch.bfloat16)), shift.float().contiguous(), None, True, l.conv.stride[0])
             else:
                 y = l(y)
         return y

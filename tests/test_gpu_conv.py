@@ -500,3 +500,15 @@ def test_stem_hip_matches_modules(hip_lib, monkeypatch):
             outs.append(m._stem(x))
     _check(outs[0], outs[2], "stem (all HIP)")
     _check(outs[1], outs[2], "stem (direct first layer)")
+    # the evaluation forward's case: fp32 input (and fp32 weights) under bf16 autocast
+    m32 = bb.PResNet(50).to(DEV).to(memory_format=torch.channels_last)
+    m32.load_state_dict(m.state_dict())
+    x32 = x.float().contiguous(memory_format=torch.channels_last)
+    outs = []
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        for mode in (2, 0):
+            monkeypatch.setattr(bb, "_STEM_HIP", mode)
+            assert m32._stem_hip_ok(x32) == (mode > 0)
+            outs.append(m32._stem(x32))
+    assert outs[0].dtype == torch.bfloat16
+    _check(outs[0], outs[1], "stem under autocast")
