@@ -642,6 +642,17 @@ int rtdetr_bn_act_fwd(const void* const* x, const float* const* gamma, const flo
 int rtdetr_bn_act_bwd(const void* dy, const void* const* x, const float* const* gamma, int nb, long long M, int C,
                       int act, const float* saved, float* ws, float* coef, void* const* dx, float* dgb,
                       hipStream_t stream);
+/* Inference-mode (running statistics) BatchNorm of nb = 1 or 2 branches +
+ * their sum + act (0 none, 1 SiLU) [+ resid, added after the activation] in
+ * ONE pass: y = act(sum_i x_i scale_i + shift_i), scale = gamma *
+ * rsqrt(running_var + eps), shift = beta - running_mean * scale (fp32 affine
+ * and statistics [C]; x_i / y / resid NHWC bf16 [M, C], 16-B aligned; C a
+ * power of two in [8, 2048]).  The HybridEncoder's / decoder input
+ * projections' BatchNorms in the evaluation forward (torch: batch_norm, then
+ * SiLU and the branch add as separate passes). */
+int rtdetr_bn_act_eval(const void* const* x, const float* const* gamma, const float* const* beta,
+                       const float* const* run_mean, const float* const* run_var, int nb, long long M, int C, int act,
+                       float eps, const void* resid, void* y, hipStream_t stream);
 /* rtdetr_bn_act_fwd with the batch statistics already summed per row block
  * by the producing convolution (rtdetr_conv_fwd_stats): part fp32
  * [nb][part_blocks][2][C] (sum, sum of squares of the bf16 x_i),

@@ -216,6 +216,52 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(BnArgs a, const float* __
   }
 }
 
+// Inference-mode BatchNorm (running statistics) + branch sum + act (+ resid):
+// scale = gamma * rsqrt(running_var + eps), shift = beta - running_mean *
+// scale per channel, computed by every workgroup into LDS, then the apply
+// pass -- one launch per BatchNorm (torch: a batch_norm kernel, then SiLU and
+// the branch add as separate passes).
+template <int ACT, int NB>
+__global__ __launch_bounds__(256) void bn_eval_kernel(BnArgs a, float eps, long long nchunk, int C,
+                                                      uint4* __restrict__ y) {
+  extern __shared__ float ss[];  // [NB][2][C]
+  for (int i = threadIdx.x; i < NB * C; i += 256) {
+    const int br = i / C, c = i - br * C;
+    const float sc = a.gamma[br][c] * rsqrtf(a.run_var[br][c] + eps);
+    ss[(br * 2) * C + c] = sc;
+    ss[(br * 2 + 1) * C + c] = a.beta[br][c] - a.run_mean[br][c] * sc;
+  }
+  __syncthreads();
+  const int cch = C >> 3;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nchunk; i += (long long)gridDim.x * 256) {
+    const int c0 = (int)(i % cch) * 8;
+    float z[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = 0.f;
+#pragma unroll
+    for (int br = 0; br < NB; ++br) {
+      float xs[8];
+      unpack8(a.x[br][i], xs);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] += fmaf(xs[j], ss[(br * 2) * C + c0 + j], ss[(br * 2 + 1) * C + c0 + j]);
+    }
+    if constexpr (ACT == 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = z[j] * sigmoidf_(z[j]);
+    }
+    uint4 o = pack8(z);
+    if (a.resid != nullptr) {  // act rounded to bf16 first, then the fp32 sum rounded once (as bn_apply)
+      float r[8];
+      unpack8(o, z);
+      unpack8(a.resid[i], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] += r[j];
+      o = pack8(z);
+    }
+    y[i] = o;
+  }
+}
+
 // g = dy * act'(z)
 template <int ACT>
 __device__ __forceinline__ void bn_grad_in(const uint4* __restrict__ dy, long long i, const float* z, float* g) {
@@ -504,6 +550,40 @@ extern "C" int rtdetr_bn_act_bwd_rows(const void* dy, long long dy_hw, long long
 #undef BN_DX
   }
   return check_launch("rtdetr_bn_act_bwd");
+}
+
+extern "C" int rtdetr_bn_act_eval(const void* const* x, const float* const* gamma, const float* const* beta,
+                                  const float* const* run_mean, const float* const* run_var, int nb, long long M,
+                                  int C, int act, float eps, const void* resid, void* y, hipStream_t stream) {
+  if (int rc = bn_check(nb, M, C, act)) return rc;
+  if (!x || !gamma || !beta || !run_mean || !run_var || !y) return fail("bn_act_eval: NULL argument");
+  if (reinterpret_cast<uintptr_t>(resid) % 16 || reinterpret_cast<uintptr_t>(y) % 16)
+    return fail("bn_act_eval: y / resid must be 16-B aligned");
+  BnArgs a{};
+  a.nb = nb;
+  a.resid = static_cast<const uint4*>(resid);
+  for (int i = 0; i < nb; ++i) {
+    if (!x[i] || !gamma[i] || !beta[i] || !run_mean[i] || !run_var[i]) return fail("bn_act_eval: NULL branch pointer");
+    if (reinterpret_cast<uintptr_t>(x[i]) % 16) return fail("bn_act_eval: x must be 16-B aligned");
+    a.x[i] = static_cast<const uint4*>(x[i]);
+    a.gamma[i] = gamma[i];
+    a.beta[i] = beta[i];
+    a.run_mean[i] = const_cast<float*>(run_mean[i]);  // (read only here)
+    a.run_var[i] = const_cast<float*>(run_var[i]);
+  }
+  const long long nchunk = M * (C / 8);
+  const size_t shm = (size_t)nb * 2 * C * sizeof(float);
+  ProfScope prof(stream, PROF_CONV_EPI, 2.0 * (nb + 1 + (resid ? 1 : 0)) * M * C);
+#define BN_EVAL(A, N)                                                                                  \
+  MOE_LAUNCH(prof, (bn_eval_kernel<A, N>), dim3(bn_grid(nchunk)), dim3(256), shm, stream, a, eps, nchunk, C, \
+             static_cast<uint4*>(y))
+  if (act == 1) {
+    if (nb == 2) BN_EVAL(1, 2); else BN_EVAL(1, 1);
+  } else {
+    if (nb == 2) BN_EVAL(0, 2); else BN_EVAL(0, 1);
+  }
+#undef BN_EVAL
+  return check_launch("rtdetr_bn_act_eval");
 }
 
 extern "C" int rtdetr_bn_act_bwd(const void* dy, const void* const* x, const float* const* gamma, int nb,

@@ -79,6 +79,7 @@ SIGNATURES = {
     "rtdetr_fold_scale_batch": (_I, [_I, _P, _P, _P, _P, _P, _P]),
     "rtdetr_bn_act_workspace": (ctypes.c_size_t, [ctypes.c_longlong, _I, _I]),
     "rtdetr_bn_act_fwd": (_I, [_P, _P, _P, _P, _P, _I, ctypes.c_longlong, _I, _I, _F, _F, _P, _P, _P, _P]),
+    "rtdetr_bn_act_eval": (_I, [_P, _P, _P, _P, _P, _I, ctypes.c_longlong, _I, _I, _F, _P, _P, _P]),
     "rtdetr_bn_act_bwd": (_I, [_P, _P, _P, _I, ctypes.c_longlong, _I, _I, _P, _P, _P, _P, _P, _P]),
     "rtdetr_avgpool2x2_nhwc_fwd": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "rtdetr_avgpool2x2_nhwc_bwd": (_I, [_P, _I, _I, _I, _I, _P, _P]),
@@ -1165,6 +1166,30 @@ def bn_act_fwd(xs, gammas, betas, run_means, run_vars, act, eps, momentum, resid
     _check(lib().rtdetr_bn_act_fwd(px, pg, pb, pm, pv, nb, M, C, int(act), float(eps), float(momentum),
                                    _ptr(saved), _ptr(ws), _ptr(y), _stream()), "rtdetr_bn_act_fwd")
     return y, saved
+
+
+def bn_act_eval(xs, gammas, betas, run_means, run_vars, act, eps, resid=None):
+    """Inference-mode BatchNorm (running statistics) of 1-2 channels_last bf16
+    branches, summed, act (0 none / 1 silu) [+ resid after the act], one pass
+    (rtdetr_bn_act_eval) -> y."""
+    M, C = _nhwc_rows(xs[0], "x0")
+    nb = len(xs)
+    for i, x in enumerate(xs[1:], 1):
+        if _nhwc_rows(x, f"x{i}") != (M, C):
+            raise MoEKernelError("bn_act_eval: branches differ in shape")
+    if resid is not None and (_nhwc_rows(resid, "resid") != (M, C) or resid.data_ptr() % 16):
+        raise MoEKernelError("bn_act_eval: resid must be a 16-B aligned channels_last bf16 tensor like x")
+    for t in list(gammas) + list(betas) + list(run_means) + list(run_vars):
+        _need(t, torch.float32, "bn affine/statistics")
+    y = torch.empty_like(xs[0])
+    px, kx = _ptrs(xs)
+    pg, kg = _ptrs(gammas)
+    pb, kb = _ptrs(betas)
+    pm, km = _ptrs(run_means)
+    pv, kv = _ptrs(run_vars)
+    _check(lib().rtdetr_bn_act_eval(px, pg, pb, pm, pv, nb, M, C, int(act), float(eps), _ptr(resid), _ptr(y),
+                                    _stream()), "rtdetr_bn_act_eval")
+    return y
 
 
 def _bn_act_fwd_resid(xs, gammas, betas, run_means, run_vars, act, eps, momentum, part, resid):

@@ -18,7 +18,7 @@ from torch import nn
 import torch.nn.functional as F
 
 from .conv import conv2d, conv2d_add_bias_relu_fork, conv2d_bias_relu, conv_module, conv_module_stats, hip_conv_ok_for
-from .fused import AddBiasReLU, AddBiasReLUFork, BiasReLU, bn_act, bn_act_ok
+from .fused import AddBiasReLU, AddBiasReLUFork, BiasReLU, bn_act, bn_act_eval, bn_act_ok, bn_eval_ok
 
 _FUSED_BN = os.environ.get("MOE_FUSED_BN", "1") != "0"  # A/B switch: training BN + SiLU in HIP
 # A/B switch: frozen-BN shift + ReLU (+ residual add) in the HIP convolution's
@@ -252,6 +252,11 @@ class ConvNormLayer(nn.Module):
                 return BiasReLU.apply(y, shift)
             return y + shift.view(1, -1, 1, 1).to(y.dtype)
         if self.act_name in (None, "silu") and _FUSED_BN:
+            if not self.norm.training and not torch.is_grad_enabled():  # inference: running statistics
+                y = conv_module(self.conv, x)
+                if bn_eval_ok([y], [self.norm]):
+                    return bn_act_eval([y], [self.norm], self.act_name)  # BN + SiLU in one HIP pass
+                return self.act(self.norm(y))
             y, part = conv_module_stats(self.conv, x)  # (the BN statistics from the conv epilogue)
             if bn_act_ok([y], [self.norm]):
                 return bn_act([y], [self.norm], self.act_name, part)  # BN + SiLU in HIP (training statistics)

@@ -19,7 +19,7 @@ from .encoder import HybridEncoder, make_ffn
 from .norm import AddLayerNorm
 from .backbone import _FUSED_BN
 from .conv import conv_module_stats
-from .fused import bn_act_ok
+from .fused import bn_act_eval, bn_act_ok, bn_eval_ok
 
 
 def inverse_sigmoid(x, eps=1e-5):
@@ -553,7 +553,8 @@ class RTDETRDecoder(nn.Module):
             if all(bn_act_ok([y], [bn]) for y, bn in zip(ys, bns)) and len({y.shape[:2] for y in ys}) == 1:
                 mem = _LevelMemory.apply(bns, parts, *ys, *[bn.weight for bn in bns], *[bn.bias for bn in bns])
                 return mem, [tuple(y.shape[-2:]) for y in ys]
-            proj = [bn(y) for y, bn in zip(ys, bns)]
+            # inference: running statistics in one HIP pass per level
+            proj = [bn_act_eval([y], [bn], None) if bn_eval_ok([y], [bn]) else bn(y) for y, bn in zip(ys, bns)]
         else:
             # conv + training BatchNorm through libmoe_hip's bn_act (as the encoder's
             # input projections): MIOpen's BN backward at batch 1 lost the gradient

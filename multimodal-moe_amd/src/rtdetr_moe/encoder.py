@@ -13,7 +13,7 @@ from ..moe.layer import MoEFFN
 from .norm import AddLayerNorm
 from .backbone import _FUSED_BN, ConvNormLayer, stage_taps
 from .conv import GradSlot, conv_module, conv_pair
-from .fused import bn_act, bn_act_ok
+from .fused import bn_act, bn_act_eval, bn_act_ok, bn_eval_ok
 from .linear import TokenLinear, TokenSelfAttention
 
 
@@ -109,10 +109,17 @@ class RepVggBlock(nn.Module):
         """silu(BN1(conv3x3 x) + BN2(conv1x1 x)) [+ resid: the CSPRep
         shortcut branch, added in the same pass on the fused path]."""
         if _FUSED_BN:
+            norms = [self.conv1.norm, self.conv2.norm]
+            if not self.conv1.norm.training and not torch.is_grad_enabled():  # inference: running statistics
+                y1, y2 = conv_pair(self.conv1.conv, self.conv2.conv, x)
+                if bn_eval_ok([y1, y2], norms):  # both BNs + sum + SiLU (+ shortcut) in one HIP pass
+                    return bn_act_eval([y1, y2], norms, "silu", resid=resid)
+                y = F.silu(self.conv1.norm(y1) + self.conv2.norm(y2))
+                return y if resid is None else y + resid
             # one node: dx accumulated in the dgrad, the BN statistics in the forward epilogues
             y1, y2, parts = conv_pair(self.conv1.conv, self.conv2.conv, x, stats=True)
-            if bn_act_ok([y1, y2], [self.conv1.norm, self.conv2.norm]):  # both BNs + sum + SiLU in HIP
-                return bn_act([y1, y2], [self.conv1.norm, self.conv2.norm], "silu", parts, resid=resid)
+            if bn_act_ok([y1, y2], norms):  # both BNs + sum + SiLU in HIP
+                return bn_act([y1, y2], norms, "silu", parts, resid=resid)
             y = F.silu(self.conv1.norm(y1) + self.conv2.norm(y2))
         else:
             y = F.silu(self.conv1(x) + self.conv2(x))
@@ -131,6 +138,13 @@ class CSPRepLayer(nn.Module):
     def forward(self, x):
         c1, c2 = self.conv1, self.conv2
         if _FUSED_BN and not c1.fold and not c2.fold:
+            if not c1.norm.training and not torch.is_grad_enabled():  # inference: running statistics
+                y1, y2 = conv_pair(c1.conv, c2.conv, x)
+                if bn_eval_ok([y1], [c1.norm]) and bn_eval_ok([y2], [c2.norm]):
+                    a1, a2 = bn_act_eval([y1], [c1.norm], "silu"), bn_act_eval([y2], [c2.norm], "silu")
+                else:
+                    a1, a2 = c1.act(c1.norm(y1)), c2.act(c2.norm(y2))
+                return self.conv3(self._bottlenecks_plus(a1, a2))
             y1, y2, parts = conv_pair(c1.conv, c2.conv, x, stats=True)  # (as RepVggBlock)
             if bn_act_ok([y1], [c1.norm]) and bn_act_ok([y2], [c2.norm]):
                 p1, p2 = (None, None) if parts is None else (parts[0:1], parts[1:2])
@@ -197,6 +211,8 @@ class HybridEncoder(nn.Module):
         conv, bn = p[0], p[1]
         if _FUSED_BN:
             y = conv_module(conv, f)
+            if bn_eval_ok([y], [bn]):  # inference: running statistics, one HIP pass
+                return bn_act_eval([y], [bn], None)
             return bn_act([y], [bn], None) if bn_act_ok([y], [bn]) else bn(y)
         return p(f)
 

@@ -19,6 +19,8 @@ CPU tensors (config C1 plumbing) take the same math in torch ops.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..moe import _lib as L
@@ -153,6 +155,38 @@ def bn_act_ok(xs, bns) -> bool:
                 and bn.weight.dtype == torch.float32 and bn.eps == bns[0].eps and bn.momentum == bns[0].momentum):
             return False
     return True
+
+
+# MOE_BN_EVAL=0: inference-mode BatchNorms through torch (A/B switch)
+_BN_EVAL = os.environ.get("MOE_BN_EVAL", "1") != "0"
+
+
+def bn_eval_ok(xs, bns) -> bool:
+    """Inference-mode BatchNorms (running statistics, no gradient wanted) that
+    rtdetr_bn_act_eval takes: GPU channels_last bf16 branches of one shape, C
+    a power of two in [8, 2048], fp32 affine and statistics."""
+    if not _BN_EVAL or torch.is_grad_enabled():
+        return False
+    x = xs[0]
+    if not (x.is_cuda and x.dim() == 4 and all(_gpu_ok(t) and t.shape == x.shape for t in xs)):
+        return False
+    C = x.shape[1]
+    if C < 8 or C > 2048 or C & (C - 1):
+        return False
+    return all(isinstance(bn, torch.nn.BatchNorm2d) and not bn.training and bn.affine and bn.track_running_stats
+               and bn.running_mean is not None and bn.weight.dtype == torch.float32
+               and bn.running_var.dtype == torch.float32 and bn.eps == bns[0].eps for bn in bns)
+
+
+def bn_act_eval(xs, bns, act: str | None, resid=None):
+    """act(sum_i BN_i(x_i)) [+ resid] with running statistics in one HIP pass
+    (callers check bn_eval_ok)."""
+    bns = list(bns)
+    if resid is not None and not (_gpu_ok(resid) and resid.shape == xs[0].shape and resid.data_ptr() % 16 == 0):
+        return bn_act_eval(xs, bns, act) + resid
+    return L.bn_act_eval(list(xs), [bn.weight for bn in bns], [bn.bias for bn in bns],
+                         [bn.running_mean for bn in bns], [bn.running_var for bn in bns],
+                         1 if act == "silu" else 0, float(bns[0].eps), resid)
 
 
 def bn_act(xs, bns, act: str | None, parts=None, resid=None):

@@ -115,3 +115,48 @@ def test_encoder_fused_bn_matches_unfused(hip_lib, monkeypatch):
     assert rel(ga, gb) < 5e-2
     for a, b in zip(pa, pb):
         assert rel(a, b) < 5e-2
+
+
+@pytest.mark.parametrize("nb,act,resid", [(1, "silu", False), (2, "silu", True), (1, None, False), (2, "silu", False)])
+def test_bn_act_eval_matches_torch(hip_lib, nb, act, resid):
+    """rtdetr_bn_act_eval (running statistics, branch sum, SiLU, shortcut after
+    the activation) against torch's inference BatchNorm in fp32."""
+    from src.rtdetr_moe.fused import bn_act_eval, bn_eval_ok
+
+    g = torch.Generator().manual_seed(nb * 7 + int(resid))
+    shape = (4, 256, 23, 40)
+    xs = [_cl(torch.randn(shape, generator=g) * 1.5 + 0.3) for _ in range(nb)]
+    bns = [bn.eval() for bn in _bns(nb, shape[1], g)]
+    r = _cl(torch.randn(shape, generator=g)) if resid else None
+    with torch.no_grad():
+        assert bn_eval_ok(xs, bns)
+        y = bn_act_eval(xs, bns, act, resid=r)
+        z = sum(bn(x.float()) for bn, x in zip(bns, xs))
+        ref = F.silu(z) if act == "silu" else z
+        if resid:
+            ref = ref + r.float()
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=2e-2 * ref.abs().max().item())
+
+
+def test_encoder_eval_bn_matches_torch_bn(hip_lib, monkeypatch):
+    """The HybridEncoder's inference forward with the one-pass HIP BatchNorms
+    against torch's batch_norm + SiLU + adds: within bf16 rounding."""
+    from src.rtdetr_moe import encoder, fused
+
+    torch.manual_seed(2)
+    enc = encoder.HybridEncoder().to(DEV).to(memory_format=torch.channels_last)
+    for m in enc.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.3, 0.3)
+            m.running_var.uniform_(0.5, 2.0)
+    enc.eval()
+    feats = [_cl(torch.randn(2, c, h, w)) for c, h, w in ((512, 46, 80), (1024, 23, 40), (2048, 12, 20))]
+    ctx = torch.zeros(2, dtype=torch.long, device=DEV)
+    outs = []
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        for on in (True, False):
+            monkeypatch.setattr(fused, "_BN_EVAL", on)
+            outs.append([o.float() for o in enc(feats, ctx)])
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * b.abs().max().item())
