@@ -698,7 +698,11 @@ def main():
             **({"expert_parallel": ep_stats} if ep_stats else {}),
         }
     if world > 1:
+        from src.rtdetr_moe.step import release_graphs
+
         dist.barrier()
+        step = None  # its captured graphs (C4: RCCL all-to-alls inside) go before the communicator
+        release_graphs()
         dist.destroy_process_group()
     if rank == 0:
         if not args.no_e2e_roofline:

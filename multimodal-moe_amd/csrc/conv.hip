@@ -770,13 +770,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __r
   }
 }
 
+// (per device; a failure is reported through moe_last_error and the launch
+// that follows fails its check_launch)
 template <auto FN>
 static void allow_lds_once(size_t bytes) {
-  static bool done = false;
-  if (!done) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(FN), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    done = true;
-  }
+  static unsigned long long done = 0;
+  (void)allow_dyn_lds(reinterpret_cast<const void*>(FN), (int)bytes, &done, "conv: dynamic LDS");
 }
 
 // output size of a padding (KS - 1) / 2 convolution

@@ -1364,12 +1364,10 @@ template <auto FN>
 static void allow_lds(size_t bytes) {
   // (raised to 159 KiB at once -- the MX exponent stage makes the size depend
   // on K; 1 KiB is left for the kernels' static LDS, e.g. the split-K flag)
-  static bool done = false;
-  if (!done && bytes > 65536) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(FN), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              159 * 1024);
-    done = true;
-  }
+  // (per device; a failure is reported through moe_last_error and the launch
+  // that follows fails its check_launch)
+  static unsigned long long done = 0;
+  if (bytes > 65536) (void)allow_dyn_lds(reinterpret_cast<const void*>(FN), 159 * 1024, &done, "grouped_gemm: dynamic LDS");
 }
 
 // the 6-deep ring is instantiated for the 64-row bf16 row GEMMs only

@@ -181,4 +181,18 @@ namespace moe {
 void set_error(const std::string& msg);
 int fail(const std::string& msg);          // returns -1
 int check_launch(const char* what);        // returns 0 or -(1000 + err)
+
+// Raise a kernel's dynamic-LDS limit once per device (the attribute is
+// per-device state in HIP).  Returns 0, or fail() with the HIP error when the
+// attribute cannot be set.  `done` is the kernel's own per-device bitmask.
+inline int allow_dyn_lds(const void* fn, int bytes, unsigned long long* done, const char* what) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail(std::string(what) + ": no device");
+  const unsigned long long bit = 1ull << dev;
+  if (__atomic_load_n(done, __ATOMIC_ACQUIRE) & bit) return 0;
+  const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e != hipSuccess) return fail(std::string(what) + ": hipFuncSetAttribute failed: " + hipGetErrorString(e));
+  __atomic_fetch_or(done, bit, __ATOMIC_RELEASE);
+  return 0;
+}
 }  // namespace moe

@@ -58,14 +58,17 @@ __global__ __launch_bounds__(256) void linear_narrow_out_kernel(const uint16_t* 
   for (int off = lpr >> 1; off > 0; off >>= 1)
 #pragma unroll
     for (int n = 0; n < NO; ++n) acc[n] += __shfl_xor(acc[n], off);
-  if (r < M && sub < N) {
-    float v = 0.f;
+  // after the butterfly every lane of the group holds all N sums: lane sub
+  // writes the columns n with n % lpr == sub (all of them when lpr < N)
+  if (r < M) {
 #pragma unroll
-    for (int n = 0; n < NO; ++n)
-      if (n == sub) v = acc[n];
-    v += bias_at(b, b_bf16, sub);
-    if (relu) v = fmaxf(v, 0.f);
-    y[r * N + sub] = f2bf(v);
+    for (int n = 0; n < NO; ++n) {
+      if (n < N && (n & (lpr - 1)) == sub) {
+        float v = acc[n] + bias_at(b, b_bf16, n);
+        if (relu) v = fmaxf(v, 0.f);
+        y[r * N + n] = f2bf(v);
+      }
+    }
   }
 }
 

@@ -882,11 +882,10 @@ extern "C" int moe_router_num_blocks(int T) { return (T + kRouterBlockTokens - 1
 // launch needing more than 64 KiB succeeds; later launches make no call.
 template <auto FN>
 static void allow_lds(size_t bytes) {
-  static bool done = false;
-  if (!done)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(FN), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              96 * 1024);
-  done = true;
+  // (per device; a failure is reported through moe_last_error and the launch
+  // that follows fails its check_launch)
+  static unsigned long long done = 0;
+  (void)allow_dyn_lds(reinterpret_cast<const void*>(FN), 96 * 1024, &done, "router: dynamic LDS");
   (void)bytes;
 }
 

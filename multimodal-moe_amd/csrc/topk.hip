@@ -148,13 +148,11 @@ extern "C" int rtdetr_topk_rows(const float* x, int rows, int n, int k, long lon
     return fail("rtdetr_topk_rows: needs 0 < k <= min(n, 1024) and n <= 32768");
   if (rows == 0) return 0;
   if (x == nullptr || idx == nullptr) return fail("rtdetr_topk_rows: null pointer");
-  static bool attr = false;
+  static unsigned long long attr_done = 0;  // per-device bitmask
   const size_t lds = (size_t)n * sizeof(uint32_t);
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topk_rows_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kTopkMaxN * sizeof(uint32_t)));
-    attr = true;
-  }
+  if (int rc = allow_dyn_lds(reinterpret_cast<const void*>(topk_rows_kernel), (int)(kTopkMaxN * sizeof(uint32_t)),
+                             &attr_done, "rtdetr_topk_rows"))
+    return rc;
   ProfScope prof(stream, PROF_ROUTER, 4.0 * rows * n + 8.0 * rows * k);
   MOE_LAUNCH(prof, topk_rows_kernel, dim3(rows), dim3(kTopkThreads), lds, stream, x, n, k, idx, val);
   return check_launch("rtdetr_topk_rows");

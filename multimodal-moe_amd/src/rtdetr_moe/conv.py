@@ -338,12 +338,32 @@ class GradSlot:
     operand) -- no autograd accumulation launch.  A depositor that runs after
     the collector (closed slot) returns its gradient to autograd as usual."""
 
-    __slots__ = ("g", "closed", "has_collector")
+    __slots__ = ("g", "closed", "has_collector", "__weakref__")
 
     def __init__(self):
         self.g = None
         self.closed = False
         self.has_collector = False
+        _OPEN_SLOTS.append(self)
+        if len(_OPEN_SLOTS) > 256:  # forwards whose backward never ran (no check after them)
+            del _OPEN_SLOTS[:128]
+
+
+_OPEN_SLOTS: list = []
+
+
+def check_grad_slots():
+    """After a backward: every GradSlot created since the last check must have
+    handed its parked gradient to the collector.  A gradient still parked means
+    the collector's backward never ran (its output did not reach the loss) and
+    the depositor's data gradient would be lost silently -- raise instead."""
+    pending = [s for s in _OPEN_SLOTS if s.g is not None]
+    _OPEN_SLOTS.clear()
+    if pending:
+        for s in pending:
+            s.g = None
+        raise RuntimeError(f"{len(pending)} GradSlot gradient(s) were parked but never collected: the collecting "
+                           "convolution's output did not reach the loss")
 
 
 class _ConvHIPStats(torch.autograd.Function):

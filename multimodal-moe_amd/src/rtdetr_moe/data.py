@@ -134,6 +134,8 @@ class YoloDataset(torch.utils.data.Dataset):
         root = Path(cfg.get("path", self.yaml_path.parent))
         if not root.is_absolute():
             root = (self.yaml_path.parent / root).resolve()
+        if not root.exists():  # an export moved since write_yolo_dataset_yaml wrote its absolute path
+            root = self.yaml_path.parent.resolve()
         rel = cfg.get(split)
         if rel is None:
             raise KeyError(f"split {split!r} missing in {data_yaml}")

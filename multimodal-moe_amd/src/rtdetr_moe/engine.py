@@ -420,6 +420,9 @@ def _mp_entry(local_idx, a, devices, port, out_file):
             Path(out_file).write_text(json.dumps({"results_dict": res.results_dict, "epochs_run": res.epochs_run,
                                                   "moe": res.moe}))
     finally:
+        from .step import release_graphs
+
+        release_graphs()  # the rank's step / evaluation graphs, before the communicator goes
         dist.destroy_process_group()
 
 
@@ -500,7 +503,9 @@ class EvalForward:
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=side):
+            from .step import CAPTURE_MODE
+
+            with torch.cuda.graph(g, stream=side, capture_error_mode=CAPTURE_MODE):
                 out = self._run(si, sc)
             torch.cuda.synchronize()
             ent = self.graphs[key] = (g, si, sc, out)

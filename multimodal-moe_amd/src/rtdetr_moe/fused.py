@@ -174,8 +174,9 @@ def bn_eval_ok(xs, bns) -> bool:
     if C < 8 or C > 2048 or C & (C - 1):
         return False
     return all(isinstance(bn, torch.nn.BatchNorm2d) and not bn.training and bn.affine and bn.track_running_stats
-               and bn.running_mean is not None and bn.weight.dtype == torch.float32
-               and bn.running_var.dtype == torch.float32 and bn.eps == bns[0].eps for bn in bns)
+               and bn.running_mean is not None and bn.running_var is not None
+               and all(t.dtype == torch.float32 for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var))
+               and bn.eps == bns[0].eps for bn in bns)
 
 
 def bn_act_eval(xs, bns, act: str | None, resid=None):

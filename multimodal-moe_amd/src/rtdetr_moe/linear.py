@@ -390,8 +390,9 @@ class _DualTokenLinear(torch.autograd.Function):
     (the deformable attention's sampling-offset and attention-weight heads on
     the query).  Forward: the two GEMMs TokenLinear issues.  Backward: x's
     gradient g1 W1 + g2 W2 with the second product accumulated in place by its
-    GEMM (addmm_, beta = 1; fp32 sum, one rounding) instead of two products
-    and autograd's add; the weight gradients as TokenLinear's (deferred)."""
+    GEMM (addmm_, beta = 1) instead of two products and autograd's add -- the
+    first product is already rounded to bf16, so the sum is rounded twice,
+    bitwise what the autograd add gave; the weight gradients as TokenLinear's (deferred)."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, dtype):

@@ -27,6 +27,7 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
+from .conv import check_grad_slots
 from .linear import TokenSelfAttention, deferred_weight_grads, merge_deferred
 from .model import RTDETRMoE
 
@@ -34,6 +35,26 @@ _FUSED_CRIT = os.environ.get("MOE_FUSED_CRITERION", "1") != "0"  # A/B switch
 # MOE_ZERO=0: GPU data parallelism through the flat fp32 all-reduce + replicated
 # FlatAdamW (optim.DPGradReducer) instead of the sharded optimizer (A/B switch)
 _ZERO = os.environ.get("MOE_ZERO", "1") != "0"
+
+# Stream-capture mode of every hipGraph capture (step graphs, the evaluation
+# forward): "thread_local".  Under the default "global" mode the RCCL process
+# group's watchdog thread, which polls the events of recent collectives, gets
+# hipErrorCapturedEvent while a capture that holds collectives (the C4
+# expert-parallel all-to-alls) is open, and terminates the process
+# (tools/rccl_capture_probe.py, gpurun_out/r6b); thread_local confines the
+# capture's restrictions to the capturing thread (gpurun_out/r6d).
+CAPTURE_MODE = "thread_local"
+
+
+def release_graphs():
+    """Before ``dist.destroy_process_group()``: free every unreachable captured
+    graph (their captured RCCL kernels keep the communicator busy: the destroy
+    then hangs, gpurun_out/r6c) and drain the device."""
+    import gc
+
+    gc.collect()
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
 
 
 class FlatOutputs(nn.Module):
@@ -105,6 +126,7 @@ class GraphedModel:
                 grads = torch.autograd.grad([o for o in out if o.requires_grad],
                                             params, [torch.ones_like(o) for o in out if o.requires_grad],
                                             allow_unused=True)
+                check_grad_slots()
                 del out, grads
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
@@ -114,15 +136,16 @@ class GraphedModel:
         # (AccumulateGrad keeps the stream it was made on) then match the capture
         # stream, so the backward needs no cross-stream syncs -- a single chain,
         # no fork/join branches for the HIP runtime to spread over parallel streams
-        with torch.cuda.graph(self.g_fwd, pool=self.pool, stream=side):
+        with torch.cuda.graph(self.g_fwd, pool=self.pool, stream=side, capture_error_mode=CAPTURE_MODE):
             out = self._run()
         self.static_out = out
         self.diff = [i for i, o in enumerate(out) if o.requires_grad]
         self.static_gout = [torch.zeros_like(o) for o in out]
         self.g_bwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_bwd, pool=self.pool, stream=side):
+        with torch.cuda.graph(self.g_bwd, pool=self.pool, stream=side, capture_error_mode=CAPTURE_MODE):
             grads = torch.autograd.grad([out[i] for i in self.diff], params,
                                         [self.static_gout[i] for i in self.diff], allow_unused=True)
+            check_grad_slots()
         self.static_grads = [g if g is not None else torch.zeros_like(p) for g, p in zip(grads, params)]
         self.anchor = torch.zeros((), device=images.device, requires_grad=True)
         torch.cuda.synchronize()
@@ -190,6 +213,7 @@ class GraphedStep:
         flips = nullcontext() if self.autocast else batched_flips(loss.device)
         with deferred_weight_grads() as deferred, flips:
             grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+        check_grad_slots()
         self.deferred_layers = 0 if deferred is None else len(deferred.items)
         return merge_deferred(self.params, grads, deferred)
 
@@ -205,7 +229,8 @@ class GraphedStep:
         torch.cuda.synchronize()
         self.pool = torch.cuda.graph_pool_handle()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=self.pool, stream=side):  # warm-up stream: see GraphedModel
+        with torch.cuda.graph(self.graph, pool=self.pool, stream=side,
+                              capture_error_mode=CAPTURE_MODE):  # warm-up stream: see GraphedModel
             loss, losses = self._loss()
             grads = self._grads(loss)
             self.static_loss = loss.detach()
@@ -313,7 +338,10 @@ class TrainStep:
 
     def __init__(self, model: RTDETRMoE, criterion, images, ctx, *, lr=1e-4, lr_backbone=1e-5,
                  weight_decay=1e-4, clip_norm=0.1, graphs=True, ddp_local=None, world=1, precision="bf16",
-                 targets=None, num_boxes=1.0):
+                 targets=None, num_boxes=1.0, zero=None):
+        """zero: the ZeRO-1 optimizer (optim.ShardedDPAdamW) -- default: at
+        world > 1 unless MOE_ZERO=0; True also at world 1 (a world-1 process
+        group: the RCCL reduce-scatter / all-gather branch on one GPU, tests)."""
         self.model = model
         self.criterion = criterion
         self.clip_norm = clip_norm
@@ -339,14 +367,15 @@ class TrainStep:
             # EP group (the same global norm on every rank)
             from .optim import FlatAdamW, ShardedDPAdamW
 
-            if world > 1 and not _ZERO:
+            use_zero = (world > 1 and _ZERO) if zero is None else bool(zero)
+            if world > 1 and not use_zero:
                 # (A/B flat path) every replica starts from rank 0's weights, as DDP
                 # does, before FlatAdamW copies its masters
                 from .optim import DPGradReducer
 
                 self.reducer = DPGradReducer(self.dp_params)
                 self.reducer.broadcast_params()
-            if world > 1 and _ZERO:
+            if use_zero:
                 # C3 data parallelism: reduce-scatter of the fp32 gradients,
                 # AdamW on this rank's 1/world slice, all-gather of the weights
                 # (optim.ShardedDPAdamW); the replicated parameters become views
@@ -461,6 +490,7 @@ class TrainStep:
                     p.grad = g
         else:
             loss.backward()
+        check_grad_slots()
         self._mark("backward")
         self._optimizer_step()
         self._mark("optimizer")

@@ -156,6 +156,7 @@ def main(argv=None) -> int:
     workers = int(cfg.get("train_dataloader", {}).get("num_workers", 0))
     ncls = int(cfg.get("num_classes", 1))
     device = _device(a.device)
+    print(f"engine device: {'cpu' if device == 'cpu' else 'cuda:' + device}", flush=True)
     if a.test_only:
         if not a.resume:
             raise SystemExit("--test-only needs -r WEIGHTS")

@@ -298,7 +298,10 @@ def _close_bf16(got, ref, what):
 @pytest.mark.parametrize("M,K,N,relu,bias", [(2400, 256, 1, False, "bf16"), (2400, 256, 4, False, "bf16"),
                                              (5003, 256, 1, False, "fp32"), (37, 512, 8, True, None),
                                              (9, 1024, 3, False, "bf16"), (2400, 4, 512, True, "bf16"),
-                                             (11, 8, 64, False, "fp32"), (0, 256, 4, False, "bf16")])
+                                             (11, 8, 64, False, "fp32"), (0, 256, 4, False, "bf16"),
+                                             # fewer lanes per row than outputs (K / 8 < N)
+                                             (37, 8, 4, True, "bf16"), (9, 16, 8, False, "fp32"),
+                                             (5, 8, 8, False, None), (13, 24, 7, True, "bf16")])
 def test_linear_narrow_fwd_vs_fp32(hip_lib, M, K, N, relu, bias):
     """rtdetr_linear_narrow_fwd (N <= 8 outputs: lanes per row + butterfly; K
     <= 8 inputs: 8 outputs per thread) against an fp32 linear."""
