@@ -814,6 +814,18 @@ int rtdetr_attn_bwd(const void* q, long long ldq, const void* k, long long ldk, 
  * the previous step's sums (tools/miopen_graph_probe.py). */
 int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void* zero, int B, int H, int W, int C, int N,
                     int KS, int stride, const float* bias, const void* resid, int relu, hipStream_t stream);
+/* rtdetr_conv_fwd with the activation named (act 0 none, 1 ReLU, 2 SiLU) and,
+ * with resid_post, the residual added AFTER the activation in bf16:
+ * y = bf16(bf16(act(conv + bias)) + resid) (round 6: the evaluation forward's
+ * re-parameterised RepVgg blocks -- 3x3 + 1x1 + both running-statistics
+ * BatchNorms folded into one 3x3 weight and bias -- and the folded
+ * ConvNormLayers of the HybridEncoder; torch's SiLU-then-add order).
+ * y_img_rows > 0: image b's output rows (and resid rows) are written at rows
+ * b y_img_rows + y_row_off + pixel of y (the decoder's input projections
+ * writing their level of the memory [B, S, N] in place); 0 = dense. */
+int rtdetr_conv_fwd_act(const void* x, const void* w, void* y, const void* zero, int B, int H, int W, int C, int N,
+                        int KS, int stride, const float* bias, const void* resid, int act, int resid_post,
+                        long long y_img_rows, long long y_row_off, hipStream_t stream);
 /* rtdetr_conv_fwd (no epilogue) that also writes the BatchNorm statistics of
  * its bf16 output: part fp32 [ceil(B Ho Wo / rows)][2][N], row block r = the
  * column sums and sums of squares over output pixels [r rows, (r + 1) rows),

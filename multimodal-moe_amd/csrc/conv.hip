@@ -52,6 +52,11 @@ static int g_conv_wg_splits = 0;   // "conv_wg_splits": weight-gradient pixel sl
 static int g_conv_dgrad_flip = -1; // "conv_dgrad_flip": 1 = always write W', 0 = always read in place
 static int g_conv_dgrad_phase = 1; // "conv_dgrad_phase": 0 = stride-2 data gradient over all 9 taps (zero rows; A/B)
 static int g_conv_areg = 0;        // "conv_areg": 1 = forward / data-gradient A operand in registers (AR)
+static int g_conv_halo = -1;       // "conv_halo": 3x3 stride-1 forward / data gradient on conv3x3_halo_kernel:
+                                   // 0 = never, 1 = BM 256 (8 waves), 2 = BM 128 (4 waves) where eligible,
+                                   // -1 = automatic
+static int g_conv_8ph = -1;        // "conv_8ph": the 256 x 256 eight-phase kernel (conv_8ph_kernel): 0 never,
+                                   // 1 wherever it applies, -1 automatic (3x3, >= 256 tiles)
 static int g_conv_k32 = -1;        // "conv_k32": 1-3 = forward / data-gradient 32-deep K-tiles, ring depth 2-4;
                                    // 0 = never; -1 = automatic (k32_auto)
 
@@ -68,13 +73,15 @@ struct ConvArgs {
                          // only when sh == 0 or both are even (fwd: st = stride, sh = 0; dgrad: st = 1,
                          // sh = stride / 2)
   // fused epilogue on the bf16 result v (each NULL / 0 = off), in this order:
-  //   v = relu?( (v + resid[p][n]) + bias[n] ),  then v = 0 where mask[p][n] <= 0
+  //   v = act( (v + resid[p][n]) + bias[n] ),  then v = 0 where mask[p][n] <= 0
   // (the arithmetic of rtdetr_bias_act_nhwc / rtdetr_add_bias_relu_nhwc and of
-  // a ReLU backward on the data gradient, so fused and separate agree bitwise)
+  // a ReLU backward on the data gradient, so fused and separate agree bitwise);
+  // resid_post (the evaluation forward's folded RepVgg block + CSP shortcut):
+  //   v = bf16( bf16(act(v + bias[n])) + resid[p][n] )  -- torch's SiLU then add
   const float* bias;
   const uint16_t* resid;
   const uint16_t* mask;
-  int relu;
+  int relu;              // act: 0 none, 1 ReLU, 2 SiLU
   // PH (stride-2 data gradient by parity class): this launch's output pixels
   // are dX's (b, 2a + ry, 2c + rx), a < H, c < W; dX is [B, Hd, Wd]; the
   // class's taps are ky' in {1} (ry = 0) or {0, 2} (ry = 1) (kx' likewise),
@@ -84,6 +91,11 @@ struct ConvArgs {
   // bf16 output and of its square, stats[(m0 / BM) * 2 + {0, 1}][n] (the
   // partial layout of the BatchNorm statistics, csrc/bnact.hip)
   float* stats;
+  int resid_post;        // resid added after the activation (see above)
+  // output rows (and resid rows) of image b at b yS + yoff + pixel when yS > 0
+  // (forward only: the evaluation forward's input projections write their level
+  // of the decoder memory [B, S, N] in place); 0 = dense [B H W, N]
+  long long yS, yoff;
 };
 
 // Wait until K-tile kt's DMA has landed for this wave: up to min(S - 2, newer)
@@ -107,6 +119,209 @@ __device__ __forceinline__ void dma16(const uint16_t* src, char* lds) {
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
+// s_waitcnt vmcnt(n) for a run-time n (0..15; a larger n waits for 15, which
+// is only stricter), as the builtin so the compiler's waitcnt pass sees it
+template <int N>
+__device__ __forceinline__ void vm_wait_b() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void vm_wait_dyn(int n) {
+  switch (n < 0 ? 0 : (n > 15 ? 15 : n)) {
+    case 0: vm_wait_b<0>(); break;
+    case 1: vm_wait_b<1>(); break;
+    case 2: vm_wait_b<2>(); break;
+    case 3: vm_wait_b<3>(); break;
+    case 4: vm_wait_b<4>(); break;
+    case 5: vm_wait_b<5>(); break;
+    case 6: vm_wait_b<6>(); break;
+    case 7: vm_wait_b<7>(); break;
+    case 8: vm_wait_b<8>(); break;
+    case 9: vm_wait_b<9>(); break;
+    case 10: vm_wait_b<10>(); break;
+    case 11: vm_wait_b<11>(); break;
+    case 12: vm_wait_b<12>(); break;
+    case 13: vm_wait_b<13>(); break;
+    case 14: vm_wait_b<14>(); break;
+    default: vm_wait_b<15>(); break;
+  }
+}
+
+// Epilogue of the implicit-GEMM convolutions (conv_fwd_kernel and
+// conv3x3_halo_kernel): the fused bias / residual / activation / ReLU-mask
+// operations and the BatchNorm statistics of ConvArgs, on the accumulator tile
+// of WGM x WGN waves (wave (wm, wn) owns rows wm BM/WGM + 16 i and columns
+// wn BN/WGN + 16 j).  PRE_OK: the epilogue operands may be loaded up front.
+// EXT: the evaluation forward's extensions (SiLU, the residual after the
+// activation, output rows at an image stride -- rtdetr_conv_fwd_act); a
+// compile-time switch, so that the training kernels keep their register budget
+// (the run-time branches cost the 32-deep tiles a workgroup per CU).
+template <int BM, int BN, int WGM, int WGN, bool PH, bool PRE_OK, bool EXT = false>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[BM / (16 * WGM)][BN / (16 * WGN)],
+                                              char* smem, int m0, int n0, int tid, int lane, int wm, int wn) {
+  constexpr int NTH = 64 * WGM * WGN;
+  constexpr int CPR = BN / 8;
+  constexpr int TM = BM / (16 * WGM), TN = BN / (16 * WGN);
+  const int HW = a.H * a.W;
+  // Epilogue through LDS: lane holds Y[m0 + wm BM/2 + 16 i + (lane & 15)][n0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3];
+  // the tile goes to a row-major [BM][BN] bf16 image (16-B chunk c of row r at chunk c ^ (r % CPR):
+  // conflict-free 8-B writes and 16-B reads), then out as whole 256-B rows of 16-B stores
+  // (register-direct 8-B stores at a row stride run at about half that rate).  The fused
+  // epilogue's operands (same 16-B chunks as the stores) are loaded first, behind the image.
+  constexpr int RPP = NTH / CPR;  // rows per store pass
+  // epilogue operands loaded up front (else per store pass: registers; the
+  // 32-deep variant keeps its register budget for 4 waves per SIMD)
+  constexpr bool PRE = BM / RPP <= 16 && PRE_OK;
+  constexpr int NPRE = PRE ? BM / RPP : 1;
+  const int ec = tid % CPR;
+  uint4 eres[NPRE], emask[NPRE];
+  // global output row of GEMM row p (PH: the class pixel's dX row)
+  auto grow = [&](int p) -> size_t {
+    if constexpr (PH) {
+      const int b = p / HW, rem = p - b * HW, ya = rem / a.W, xc = rem - ya * a.W;
+      return ((size_t)b * a.Hd + 2 * ya + a.ry) * a.Wd + 2 * xc + a.rx;
+    } else if constexpr (EXT) {
+      if (a.yS == 0) return (size_t)p;
+      const int b = p / HW;  // rows of image b start at b yS + yoff (a level block of [B, S, N])
+      return (size_t)b * a.yS + a.yoff + (p - b * HW);
+    } else {
+      return (size_t)p;
+    }
+  };
+  const bool ecol = n0 + ec * 8 < a.N;  // this thread's 8 output columns exist
+  if (PRE && ecol && (a.resid != nullptr || a.mask != nullptr)) {
+#pragma unroll
+    for (int k = 0; k < NPRE; ++k) {
+      const int p = m0 + tid / CPR + RPP * k;
+      const size_t g = grow(p < a.P ? p : 0) * a.N + n0 + ec * 8;
+      if (a.resid != nullptr) eres[k] = *reinterpret_cast<const uint4*>(a.resid + g);
+      if (a.mask != nullptr) emask[k] = *reinterpret_cast<const uint4*>(a.mask + g);
+    }
+  }
+  float eb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (a.bias != nullptr && ecol) {
+    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + n0 + ec * 8);
+    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + n0 + ec * 8 + 4);
+    eb[0] = b0.x; eb[1] = b0.y; eb[2] = b0.z; eb[3] = b0.w;
+    eb[4] = b1.x; eb[5] = b1.y; eb[6] = b1.z; eb[7] = b1.w;
+  }
+  const bool efloat = a.resid != nullptr || a.bias != nullptr || a.relu;
+  float st_s[8], st_q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) st_s[e] = st_q[e] = 0.f;
+  __syncthreads();  // every wave is done reading the ring
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * (BM / WGM) + 16 * i + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * (BN / WGN) + 16 * j + 4 * (lane >> 4);
+      uint2 v;
+      v.x = pack2bf(acc[i][j][0], acc[i][j][1]);
+      v.y = pack2bf(acc[i][j][2], acc[i][j][3]);
+      *reinterpret_cast<uint2*>(smem + r * (BN * 2) + (((col >> 3) ^ (r % CPR)) << 4) + (col & 7) * 2) = v;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < BM / RPP; ++k) {
+    const int r = tid / CPR + RPP * k, c = ec;
+    const int p = m0 + r;
+    if (p < a.P && ecol) {
+      uint4 v = *reinterpret_cast<const uint4*>(smem + r * (BN * 2) + ((c ^ (r % CPR)) << 4));
+      uint4 er, em;
+      if constexpr (PRE) {
+        er = eres[k];
+        em = emask[k];
+      } else {
+        const size_t g = grow(p) * a.N + n0 + ec * 8;
+        if (a.resid != nullptr) er = *reinterpret_cast<const uint4*>(a.resid + g);
+        if (a.mask != nullptr) em = *reinterpret_cast<const uint4*>(a.mask + g);
+      }
+      if (efloat) {
+        float f[8];
+        unpack8(v, f);
+        if (a.resid != nullptr && !(EXT && a.resid_post)) {
+          float q[8];
+          unpack8(er, q);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] += q[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += eb[e];
+        if (!EXT || a.relu == 1) {
+          if (a.relu) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+          }
+        } else if (a.relu == 2) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = f[e] / (1.f + __expf(-f[e]));
+        }
+        v = pack8(f);
+        if constexpr (EXT) {
+          if (a.resid != nullptr && a.resid_post) {
+            float q[8];
+            unpack8(v, f);
+            unpack8(er, q);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] += q[e];
+            v = pack8(f);
+          }
+        }
+      }
+      if (a.mask != nullptr) {  // keep where the mask element is > 0 (bf16: sign clear, not zero)
+        const uint32_t mw[4] = {em.x, em.y, em.z, em.w};
+        uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t lo = mw[q] & 0xffffu, hi = mw[q] >> 16;
+          const uint32_t keep_lo = ((lo & 0x8000u) || lo == 0) ? 0u : 0xffffu;
+          const uint32_t keep_hi = ((hi & 0x8000u) || hi == 0) ? 0u : 0xffff0000u;
+          vw[q] &= keep_lo | keep_hi;
+        }
+        v = make_uint4(vw[0], vw[1], vw[2], vw[3]);
+      }
+      *reinterpret_cast<uint4*>(a.y + grow(p) * a.N + n0 + c * 8) = v;
+      if constexpr (!PH) {
+        if (a.stats != nullptr) {  // BatchNorm statistics of the stored values
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            st_s[e] += f[e];
+            st_q[e] = fmaf(f[e], f[e], st_q[e]);
+          }
+        }
+      }
+    }
+  }
+  if constexpr (!PH) {
+    if (a.stats != nullptr) {  // the RPP row groups' sums added in row order
+      __syncthreads();  // every thread is done reading the output image
+      float* red = reinterpret_cast<float*>(smem);  // [2][RPP][BN]
+      const int rg = tid / CPR;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[rg * BN + ec * 8 + e] = st_s[e];
+        red[(RPP + rg) * BN + ec * 8 + e] = st_q[e];
+      }
+      __syncthreads();
+      for (int c = tid; c < BN; c += NTH) {
+        float s1 = 0.f, s2 = 0.f;
+        for (int r = 0; r < RPP; ++r) {
+          s1 += red[r * BN + c];
+          s2 += red[(RPP + r) * BN + c];
+        }
+        float* pp = a.stats + (size_t)(m0 / BM) * 2 * a.N + n0 + c;
+        pp[0] = s1;
+        pp[a.N] = s2;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // forward / data gradient
 // ---------------------------------------------------------------------------
@@ -127,7 +342,7 @@ __device__ __forceinline__ void dma16(const uint16_t* src, char* lds) {
 // workgroups per CU at the same depth -- "conv_k32"); the 32-deep
 // K-contiguous image swizzles chunk c of row r to c ^ ((r >> 2) & 3).
 template <int KS, int S, int BM, int BN, bool BT, bool PH = false, int WGM = 2, int WGN = 2, bool AR = false,
-          int KT = 64>
+          int KT = 64, bool EXT = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   static_assert(BN == 64 || BN == 128 || BN == 256, "output-channel tile: 64, 128 or 256");
@@ -345,143 +560,407 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_fwd_kernel(ConvArgs a) {
       }
     }
   }
-  // Epilogue through LDS: lane holds Y[m0 + wm BM/2 + 16 i + (lane & 15)][n0 + wn 64 + 16 j + 4 (lane >> 4) + 0..3];
-  // the tile goes to a row-major [BM][BN] bf16 image (16-B chunk c of row r at chunk c ^ (r % CPR):
-  // conflict-free 8-B writes and 16-B reads), then out as whole 256-B rows of 16-B stores
-  // (register-direct 8-B stores at a row stride run at about half that rate).  The fused
-  // epilogue's operands (same 16-B chunks as the stores) are loaded first, behind the image.
-  constexpr int RPP = NTH / CPR;  // rows per store pass
-  // epilogue operands loaded up front (else per store pass: registers; the
-  // 32-deep variant keeps its register budget for 4 waves per SIMD)
-  constexpr bool PRE = BM / RPP <= 16 && KT == 64;
-  constexpr int NPRE = PRE ? BM / RPP : 1;
-  const int ec = tid % CPR;
-  uint4 eres[NPRE], emask[NPRE];
-  // global output row of GEMM row p (PH: the class pixel's dX row)
-  auto grow = [&](int p) -> size_t {
-    if constexpr (PH) {
-      const int b = p / HW, rem = p - b * HW, ya = rem / a.W, xc = rem - ya * a.W;
-      return ((size_t)b * a.Hd + 2 * ya + a.ry) * a.Wd + 2 * xc + a.rx;
-    } else {
-      return (size_t)p;
-    }
-  };
-  const bool ecol = n0 + ec * 8 < a.N;  // this thread's 8 output columns exist
-  if (PRE && ecol && (a.resid != nullptr || a.mask != nullptr)) {
-#pragma unroll
-    for (int k = 0; k < NPRE; ++k) {
-      const int p = m0 + tid / CPR + RPP * k;
-      const size_t g = grow(p < a.P ? p : 0) * a.N + n0 + ec * 8;
-      if (a.resid != nullptr) eres[k] = *reinterpret_cast<const uint4*>(a.resid + g);
-      if (a.mask != nullptr) emask[k] = *reinterpret_cast<const uint4*>(a.mask + g);
-    }
-  }
-  float eb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (a.bias != nullptr && ecol) {
-    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + n0 + ec * 8);
-    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + n0 + ec * 8 + 4);
-    eb[0] = b0.x; eb[1] = b0.y; eb[2] = b0.z; eb[3] = b0.w;
-    eb[4] = b1.x; eb[5] = b1.y; eb[6] = b1.z; eb[7] = b1.w;
-  }
-  const bool efloat = a.resid != nullptr || a.bias != nullptr || a.relu;
-  float st_s[8], st_q[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) st_s[e] = st_q[e] = 0.f;
-  __syncthreads();  // every wave is done reading the ring
+  conv_epilogue<BM, BN, WGM, WGN, PH, KT == 64, EXT>(a, acc, smem, m0, n0, tid, lane, wm, wn);
+}
+
+// ---------------------------------------------------------------------------
+// 3x3 stride-1 convolutions with a halo-staged A operand (round 6)
+// ---------------------------------------------------------------------------
+// conv_fwd_kernel stages, for every (tap, 64-channel slice) K-tile, the BM
+// neighbour rows of its output pixels: 9 x BM rows per slice, each through a
+// per-row computed LDS-DMA source (tap offsets, bounds) -- the issue cost of
+// those DMAs and their address arithmetic, not the bytes, left the MFMA pipe
+// busy 0.33 of the time (r05 PMC).  Here the M-tile is BM consecutive output
+// pixels in raster order, and for each 64-channel slice three halo groups are
+// staged once:
+//   group g (dy = g - 1): pixels m0 + dy W - 1 .. m0 + dy W + BM  (BM + 2 rows)
+// as plain contiguous rows (a row outside [0, P) reads the zero row).  Tap
+// (dy, dx)'s A fragment for output row r is halo row r + dx + 1 of group
+// dy + 1; a lane whose pixel has no such neighbour (y + dy or x + dx outside
+// the image -- which includes every row that wrapped into another image row
+// or image) reads a zero row of LDS instead.  So a slice costs 3 (BM + 2) A
+// rows instead of 9 BM, with no per-tap address work, and the B operand (the
+// weight K-tile of the tap) streams through a BS-deep ring as before.
+// Schedule, per K-step kt = (slice cs, tap t), t = 3 g + (dx + 1):
+//   wait (this wave's B(kt) and halo(g, cs) landed) -> barrier ->
+//   issue B(kt + BS - 1); at t = 3 the group-0 halo of slice cs + 1, at t = 6
+//   group 1 of cs + 1, at t = 0 group 2 of cs (each group's previous contents
+//   were last read before this barrier) -> MFMA on (cs, t).
+// Each group reload has six K-steps to land.  The per-wave vmcnt waits are
+// counted at run time from the wave's own issue sequence.
+// BM x BN tile, WGM x WGN waves of 64 x 64; the same K order for every output
+// (slice-major, tap-minor) and the shared epilogue (conv_epilogue).
+template <int BM, int BN, int WGM, int WGN, int BS>
+__global__ __launch_bounds__(64 * WGM * WGN) void conv3x3_halo_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NW = WGM * WGN;
+  constexpr int HR = BM + 2;                      // halo rows per group
+  constexpr int GI = (HR + 7) / 8;                // 1-KiB DMA instructions per group (8 rows each)
+  constexpr int GS = GI * 1024;                   // group stride (bytes)
+  constexpr int HALO = 3 * GS;
+  constexpr int BT_BYTES = BN * 128;              // one B K-tile image
+  constexpr int BP = BN / (8 * NW);               // B DMA instructions per wave per K-step
+  constexpr int ZOFF = HALO + BS * BT_BYTES;      // the 128-B zero row
+  constexpr int TM = BM / (16 * WGM), TN = BN / (16 * WGN);
+  static_assert(BP >= 1 && BP * 8 * NW == BN, "B tile / wave split");
+  static_assert(BM / WGM == 64 && BN / WGN == 64, "64 x 64 wave tiles");
+  static_assert(ZOFF + 128 <= 160 * 1024 && BM * BN * 2 <= ZOFF, "LDS budget");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int NT = a.N / BN;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int nt = slot % NT;
+  const int mt = (slot / NT) * 8 + xcd;
+  if (mt >= a.mt_n) return;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int ncs = a.C / 64;
+  const int nk = 9 * ncs;
+  const int HW = a.H * a.W;
+  if (tid < 8) *reinterpret_cast<uint4*>(smem + ZOFF + tid * 16) = make_uint4(0, 0, 0, 0);
+  // tap validity of this lane's output rows (bit t: tap t = 3 (dy + 1) + dx + 1 has its neighbour)
+  uint32_t tv[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int r = wm * (BM / WGM) + 16 * i + (lane & 15);
+    const int p = m0 + wm * 64 + 16 * i + (lane & 15);
+    const int rem = p % HW, y = rem / a.W, x = rem - y * a.W;
+    const uint32_t ym = y > 0, yp = y < a.H - 1, xm = x > 0, xp = x < a.W - 1;
+    const uint32_t rows[3] = {ym, 1u, yp}, cols[3] = {xm, 1u, xp};
+    uint32_t m = 0;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * (BN / WGN) + 16 * j + 4 * (lane >> 4);
-      uint2 v;
-      v.x = pack2bf(acc[i][j][0], acc[i][j][1]);
-      v.y = pack2bf(acc[i][j][2], acc[i][j][3]);
-      *reinterpret_cast<uint2*>(smem + r * (BN * 2) + (((col >> 3) ^ (r % CPR)) << 4) + (col & 7) * 2) = v;
+    for (int t = 0; t < 9; ++t) m |= (rows[t / 3] & cols[t % 3]) << t;
+    tv[i] = m;
+  }
+  // halo group g of slice cs: GI instructions j = wave + NW u (rows 8 j .. 8 j + 7)
+  const int hc = (GI - wave + NW - 1) / NW;  // this wave's instructions per group
+  auto issue_halo = [&](int g, int cs) {
+    const long long q0 = (long long)m0 + (long long)(g - 1) * a.W - 1;
+    char* gbase = smem + g * GS;
+    for (int j = wave; j < GI; j += NW) {
+      const int hr = 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ ((hr >> 1) & 7);
+      const long long q = q0 + hr;
+      const bool ok = hr < HR && q >= 0 && q < a.P;
+      const uint16_t* src = ok ? a.x + (size_t)q * a.C + cs * 64 + c * 8 : a.zero + c * 8;
+      dma16(src, gbase + j * 1024);
+    }
+  };
+  // B K-tile kt = (cs, t): W[n0 + r][t][cs 64 ..], rows 8 j .. 8 j + 7 for j = wave + NW b
+  auto issue_b = [&](int kt) {
+    const int cs = kt / 9, t = kt - cs * 9;
+    char* bbase = smem + HALO + (kt % BS) * BT_BYTES;
+#pragma unroll
+    for (int b = 0; b < BP; ++b) {
+      const int j = wave + NW * b;
+      const int r = 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      dma16(a.w + (size_t)(n0 + r) * (9 * a.C) + t * a.C + cs * 64 + c * 8, bbase + j * 1024);
+    }
+  };
+  // per-wave issue bookkeeping (scalars, constant indices only): cumulative DMA
+  // instruction count after the B tiles kt .. kt + BS - 2 (bq[]) and after the
+  // latest issue of each halo group (h0, h1, h2)
+  static_assert(BS >= 2 && BS <= 4, "B ring depth");
+  int cnt = 0;
+  int bq[BS - 1];
+  issue_halo(0, 0);
+  cnt += hc;
+  int h0 = cnt;
+  issue_halo(1, 0);
+  cnt += hc;
+  int h1 = cnt;
+  issue_halo(2, 0);
+  cnt += hc;
+  int h2 = cnt;
+#pragma unroll
+  for (int s = 0; s < BS - 1; ++s) {
+    if (s < nk) {
+      issue_b(s);
+      cnt += BP;
+    }
+    bq[s] = cnt;
+  }
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int zrow = ZOFF;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cs = kt / 9, t = kt - cs * 9, g = t / 3, dx = t - 3 * g - 1;
+    vm_wait_dyn(cnt - max(bq[0], g == 0 ? h0 : (g == 1 ? h1 : h2)));
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + BS - 1 < nk) {
+      issue_b(kt + BS - 1);
+      cnt += BP;
+    }
+#pragma unroll
+    for (int s = 0; s + 1 < BS - 1; ++s) bq[s] = bq[s + 1];
+    bq[BS - 2] = cnt;
+    if (t == 3 && cs + 1 < ncs) {
+      issue_halo(0, cs + 1);
+      cnt += hc;
+      h0 = cnt;
+    } else if (t == 6 && cs + 1 < ncs) {
+      issue_halo(1, cs + 1);
+      cnt += hc;
+      h1 = cnt;
+    } else if (t == 0 && cs > 0) {
+      issue_halo(2, cs);
+      cnt += hc;
+      h2 = cnt;
+    }
+    const char* gbase = smem + g * GS;
+    const char* bimg = smem + HALO + (kt % BS) * BT_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+      const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int h = wm * 64 + 16 * i + (lane & 15) + dx + 1;
+        const int off = ((tv[i] >> t) & 1) ? (int)(gbase - smem) + h * 128 + ((c ^ ((h >> 1) & 7)) << 4)
+                                            : zrow + (c << 4);
+        af[i] = *reinterpret_cast<const bf16x8*>(smem + off);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = read_frag<BN, true>(bimg, wn * 64 + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
   }
-  __syncthreads();
+  vm_wait_b<0>();  // (nothing is in flight here; the epilogue reuses the halo LDS)
+  conv_epilogue<BM, BN, WGM, WGN, false, true>(a, acc, smem, m0, n0, tid, lane, wm, wn);
+}
+
+// ---------------------------------------------------------------------------
+// 256 x 256 tiles in 8 phases (round 6)
+// ---------------------------------------------------------------------------
+// The 2-barrier-per-K-tile structure of conv_fwd_kernel (and of the halo
+// kernel above, which cut the A staging ~2.5x and ran no faster) sits at the
+// ~750 TFLOP/s ceiling cdna_hip_programming.md section 5 describes for that
+// structure; its 256 x 256 eight-phase schedule is the way past it.  Here:
+// 8 waves as 2 (M) x 4 (N), 128 x 64 outputs per wave (acc 8 x 4 blocks),
+// 64-deep K-tiles double-buffered in LDS (A [256][64] + B [256][64] = 64 KiB
+// per buffer), each K-tile computed in 4 phases -- one 64 x 32 quadrant of the
+// wave tile per phase, 16 MFMA -- in the order (0,0) (0,1) (1,1) (1,0), so a
+// phase reads 8 A fragments, 4 B fragments, or both.  The staging unit is the
+// half-tile: H0 = A rows {0..63, 128..191} (both wave rows' first quarters),
+// H1 = A rows {64..127, 192..255}, H2 = B rows (output channels) {64 c + 0..31},
+// H3 = {64 c + 32..63}; 16 KiB, two LDS-DMA instructions per wave each.  A
+// half-tile is re-staged (for the K-tile two ahead, same buffer) in the phase
+// after its last read: H0 in phase 1, H3 in 2, H1 in 3, H2 in 4 (phases 0-3
+// compute the even buffer, 4-7 the odd one: the odd buffer's half-tiles go out
+// in phases 5, 6, 7 and 0).  Three half-tiles stay in flight across the
+// barriers: vmcnt(6) at phases 3 and 7 retires the other buffer, whose reads
+// start one phase later.  Phase body: fragment reads -> half-tile issue ->
+// [wait] -> barrier -> lgkmcnt(0) -> setprio(1), 16 MFMA, setprio(0) ->
+// barrier.  A rows are gathered per tap like conv_fwd_kernel's (any
+// KS / stride / dgrad geometry of ConvArgs, PH excluded); every output's K loop
+// runs in conv_fwd_kernel's order (tap-major, channel slice minor, k-steps of
+// 32 in order), so the two kernels agree bit for bit.
+template <int KS>
+__global__ __launch_bounds__(512, 1) void conv_8ph_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BM = 256, BN = 256, NW = 8;
+  constexpr int IMG = 256 * 128;  // one [256][64] bf16 operand image
+  constexpr int BUF = 2 * IMG;    // A + B of one K-tile
+  constexpr int PAD = (KS - 1) / 2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int NT = a.N / BN;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int nt = slot % NT;
+  const int mt = (slot / NT) * 8 + xcd;
+  if (mt >= a.mt_n) return;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int cpt = a.C / 64;
+  const int nk = KS * KS * cpt;
+  const int HW = a.H * a.W, HWs = a.Hs * a.Ws;
+  // A staging: half h, instruction u (0, 1): half-rows 8 j .. 8 j + 7, j = wave + 8 u;
+  // lane's half-row hr = 8 j + lane / 8 -> tile row r = (hr & 63) + 128 (hr >> 6) + 64 h
+  int py[2][2], px[2][2], pb[2][2], ach[2][2];
+  bool pv[2][2];
 #pragma unroll
-  for (int k = 0; k < BM / RPP; ++k) {
-    const int r = tid / CPR + RPP * k, c = ec;
-    const int p = m0 + r;
-    if (p < a.P && ecol) {
-      uint4 v = *reinterpret_cast<const uint4*>(smem + r * (BN * 2) + ((c ^ (r % CPR)) << 4));
-      uint4 er, em;
-      if constexpr (PRE) {
-        er = eres[k];
-        em = emask[k];
-      } else {
-        const size_t g = grow(p) * a.N + n0 + ec * 8;
-        if (a.resid != nullptr) er = *reinterpret_cast<const uint4*>(a.resid + g);
-        if (a.mask != nullptr) em = *reinterpret_cast<const uint4*>(a.mask + g);
-      }
-      if (efloat) {
-        float f[8];
-        unpack8(v, f);
-        if (a.resid != nullptr) {
-          float q[8];
-          unpack8(er, q);
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] += q[e];
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] += eb[e];
-        if (a.relu) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
-        }
-        v = pack8(f);
-      }
-      if (a.mask != nullptr) {  // keep where the mask element is > 0 (bf16: sign clear, not zero)
-        const uint32_t mw[4] = {em.x, em.y, em.z, em.w};
-        uint32_t vw[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t lo = mw[q] & 0xffffu, hi = mw[q] >> 16;
-          const uint32_t keep_lo = ((lo & 0x8000u) || lo == 0) ? 0u : 0xffffu;
-          const uint32_t keep_hi = ((hi & 0x8000u) || hi == 0) ? 0u : 0xffff0000u;
-          vw[q] &= keep_lo | keep_hi;
-        }
-        v = make_uint4(vw[0], vw[1], vw[2], vw[3]);
-      }
-      *reinterpret_cast<uint4*>(a.y + grow(p) * a.N + n0 + c * 8) = v;
-      if constexpr (!PH) {
-        if (a.stats != nullptr) {  // BatchNorm statistics of the stored values
-          float f[8];
-          unpack8(v, f);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            st_s[e] += f[e];
-            st_q[e] = fmaf(f[e], f[e], st_q[e]);
-          }
-        }
-      }
+    for (int u = 0; u < 2; ++u) {
+      const int hr = 8 * (wave + 8 * u) + (lane >> 3);
+      const int r = (hr & 63) + 128 * (hr >> 6) + 64 * h;
+      const int p = m0 + r;
+      pv[h][u] = p < a.P;
+      const int pp = pv[h][u] ? p : 0;
+      pb[h][u] = pp / HW;
+      const int rem = pp - pb[h][u] * HW;
+      py[h][u] = rem / a.W;
+      px[h][u] = rem - py[h][u] * a.W;
+      ach[h][u] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
     }
-  }
-  if constexpr (!PH) {
-    if (a.stats != nullptr) {  // the RPP row groups' sums added in row order
-      __syncthreads();  // every thread is done reading the output image
-      float* red = reinterpret_cast<float*>(smem);  // [2][RPP][BN]
-      const int rg = tid / CPR;
+  auto tapinfo = [&](int kt, int& c0, int& tap, int& dy, int& dx) __attribute__((always_inline)) {
+    const int t = kt / cpt;
+    c0 = (kt - t * cpt) * 64;
+    tap = t;
+    dy = t / KS - PAD;
+    dx = t % KS - PAD;
+  };
+  auto issue_a = [&](int h, int kt) __attribute__((always_inline)) {
+    char* img = smem + (kt & 1) * BUF;
+    int c0, tap, dy, dx;
+    tapinfo(kt, c0, tap, dy, dx);
+    (void)tap;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        red[rg * BN + ec * 8 + e] = st_s[e];
-        red[(RPP + rg) * BN + ec * 8 + e] = st_q[e];
-      }
-      __syncthreads();
-      for (int c = tid; c < BN; c += NTH) {
-        float s1 = 0.f, s2 = 0.f;
-        for (int r = 0; r < RPP; ++r) {
-          s1 += red[r * BN + c];
-          s2 += red[(RPP + r) * BN + c];
-        }
-        float* pp = a.stats + (size_t)(m0 / BM) * 2 * a.N + n0 + c;
-        pp[0] = s1;
-        pp[a.N] = s2;
-      }
+    for (int u = 0; u < 2; ++u) {
+      const int hr0 = 8 * (wave + 8 * u);
+      const int r0 = (hr0 & 63) + 128 * (hr0 >> 6) + 64 * h;
+      int yy = py[h][u] * a.st + dy, xx = px[h][u] * a.st + dx;
+      bool ok = pv[h][u] && !(((yy | xx) & a.sh));
+      yy >>= a.sh;
+      xx >>= a.sh;
+      ok = ok && yy >= 0 && yy < a.Hs && xx >= 0 && xx < a.Ws;
+      const uint16_t* src = ok ? a.x + ((size_t)(pb[h][u] * HWs + yy * a.Ws + xx)) * a.C + c0 + ach[h][u]
+                               : a.zero + ach[h][u];
+      dma16(src, img + r0 * 128);
     }
+  };
+  // B staging: half h (H2 = 0, H3 = 1): half-row hr -> channel row n = 64 (hr >> 5) + (hr & 31) + 32 h
+  auto issue_b = [&](int h, int kt) __attribute__((always_inline)) {
+    char* img = smem + (kt & 1) * BUF + IMG;
+    int c0, tap, dy, dx;
+    tapinfo(kt, c0, tap, dy, dx);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int hr0 = 8 * (wave + 8 * u);
+      const int hr = hr0 + (lane >> 3);
+      const int n = 64 * (hr >> 5) + (hr & 31) + 32 * h;
+      const int n0r = 64 * (hr0 >> 5) + (hr0 & 31) + 32 * h;
+      const int c = (lane & 7) ^ ((n >> 1) & 7);
+      dma16(a.w + (size_t)(n0 + n) * (KS * KS * a.C) + tap * a.C + c0 + c * 8, img + n0r * 128);
+    }
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bfr[2][2];
+  // fragment addresses: the K-contiguous image's swizzle (r >> 1) & 7 depends only on lane & 15 for
+  // 16-aligned row blocks, so every fragment of a k-step is one per-lane base + a constant offset
+  // (ds_read_b128's immediate): two bases per operand instead of one address register per fragment
+  const int fr = lane & 15, fc = lane >> 4;
+  const int abase0 = kimg_off(wr * 128 + fr, fc), abase1 = kimg_off(wr * 128 + fr, 4 + fc);
+  const int bbase0 = IMG + kimg_off(wc * 64 + fr, fc), bbase1 = IMG + kimg_off(wc * 64 + fr, 4 + fc);
+  auto read_a = [&](int kt, int qa) __attribute__((always_inline)) {
+    const char* img = smem + (kt & 1) * BUF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      af[i][0] = *reinterpret_cast<const bf16x8*>(img + abase0 + (qa * 64 + 16 * i) * 128);
+      af[i][1] = *reinterpret_cast<const bf16x8*>(img + abase1 + (qa * 64 + 16 * i) * 128);
+    }
+  };
+  auto read_b = [&](int kt, int qb) __attribute__((always_inline)) {
+    const char* img = smem + (kt & 1) * BUF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bfr[j][0] = *reinterpret_cast<const bf16x8*>(img + bbase0 + (qb * 32 + 16 * j) * 128);
+      bfr[j][1] = *reinterpret_cast<const bf16x8*>(img + bbase1 + (qb * 32 + 16 * j) * 128);
+    }
+  };
+  auto mfma = [&](int qa, int qb) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qa * 4 + i][qb * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][ks], af[i][ks], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = []() __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // prologue: K-tile 0 (even buffer) whole, K-tile 1's H0, H3, H1 (its H2 goes out in phase 0);
+  // nk is even (ph8_ok), so every loop trip computes two whole K-tiles and has one exit
+  issue_a(0, 0);
+  issue_b(1, 0);
+  issue_a(1, 0);
+  issue_b(0, 0);
+  issue_a(0, 1);
+  issue_b(1, 1);
+  issue_a(1, 1);
+  vm_wait_b<6>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  bar();
+  for (int kt = 0; kt < nk; kt += 2) {
+    const bool nx0 = kt + 2 < nk;  // (then kt + 3 < nk as well)
+    // phase 0: quadrant (0,0) of the even tile
+    read_a(kt, 0);
+    read_b(kt, 0);
+    issue_b(0, kt + 1);
+    bar();
+    mfma(0, 0);
+    bar();
+    // phase 1: (0,1)
+    read_b(kt, 1);
+    if (nx0) issue_a(0, kt + 2);
+    bar();
+    mfma(0, 1);
+    bar();
+    // phase 2: (1,1)
+    read_a(kt, 1);
+    if (nx0) issue_b(1, kt + 2);
+    bar();
+    mfma(1, 1);
+    bar();
+    // phase 3: (1,0); retire the odd tile
+    read_b(kt, 0);
+    if (nx0) {
+      issue_a(1, kt + 2);
+      vm_wait_b<6>();
+    } else {
+      vm_wait_b<0>();
+    }
+    bar();
+    mfma(1, 0);
+    bar();
+    // phases 4-7: the odd tile kt + 1
+    read_a(kt + 1, 0);
+    read_b(kt + 1, 0);
+    if (nx0) issue_b(0, kt + 2);
+    bar();
+    mfma(0, 0);
+    bar();
+    read_b(kt + 1, 1);
+    if (nx0) issue_a(0, kt + 3);
+    bar();
+    mfma(0, 1);
+    bar();
+    read_a(kt + 1, 1);
+    if (nx0) issue_b(1, kt + 3);
+    bar();
+    mfma(1, 1);
+    bar();
+    read_b(kt + 1, 0);
+    if (nx0) {
+      issue_a(1, kt + 3);
+      vm_wait_b<6>();
+    } else {
+      vm_wait_b<0>();
+    }
+    bar();
+    mfma(1, 0);
+    bar();
   }
+  vm_wait_b<0>();
+  conv_epilogue<BM, BN, 2, 4, false, false, true>(a, acc, smem, m0, n0, tid, lane, wr, wc);
 }
 
 // The ResNet-D stem's first convolution (3 -> 32 channels, 3x3, stride 2,
@@ -798,7 +1277,7 @@ static int conv_check(const void* const* ptrs, int np, int B, int H, int W, int 
 constexpr int CV_STAGES = 2;
 
 template <int KS, int BM, int BN, bool BT, bool PH, int WGM = 2, int WGN = 2, int ST = CV_STAGES, bool AR = false,
-          int KT = 64>
+          int KT = 64, bool EXT = false>
 static void launch_fwd_n(ConvArgs a, hipStream_t stream, ProfScope& prof) {
   constexpr size_t ring = ST * (AR ? BN : BM + BN) * KT * 2;
   // the epilogue's output image (and statistics rows) reuse the ring's LDS
@@ -806,12 +1285,12 @@ static void launch_fwd_n(ConvArgs a, hipStream_t stream, ProfScope& prof) {
   static_assert(2 * (64 * WGM * WGN / (BN / 8)) * BN * 4 <= lds, "statistics rows exceed the LDS");
   static_assert(lds <= 160 * 1024, "ring exceeds the CU's LDS");
   static_assert(!(BT && BN > 128), "the in-place (MN-contiguous) weight image takes 64 or 128 columns");
-  allow_lds_once<conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN, AR, KT>>(lds);
+  allow_lds_once<conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN, AR, KT, EXT>>(lds);
   a.mt_n = (a.P + BM - 1) / BM;
   const int NT = (a.N + BN - 1) / BN;
   const int grid = ((a.mt_n + 7) / 8) * 8 * NT;
-  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN, AR, KT>), dim3(grid), dim3(64 * WGM * WGN),
-             lds, stream, a);
+  MOE_LAUNCH(prof, (conv_fwd_kernel<KS, ST, BM, BN, BT, PH, WGM, WGN, AR, KT, EXT>), dim3(grid),
+             dim3(64 * WGM * WGN), lds, stream, a);
 }
 
 // The 8-wave big tile: 256 x 128, 4 x 2 waves of 64 x 64 (the 128 x 128
@@ -890,8 +1369,61 @@ static int fwd_bm(long long P, int N) {
   return bm;
 }
 
+template <int BM, int BN, int WGM, int WGN, int BS>
+static void launch_halo(ConvArgs a, hipStream_t stream, ProfScope& prof) {
+  constexpr int GI = (BM + 2 + 7) / 8;
+  constexpr size_t lds = 3 * GI * 1024 + BS * BN * 128 + 128;
+  allow_lds_once<conv3x3_halo_kernel<BM, BN, WGM, WGN, BS>>(lds);
+  a.mt_n = (a.P + BM - 1) / BM;
+  const int NT = a.N / BN;
+  const int grid = ((a.mt_n + 7) / 8) * 8 * NT;
+  MOE_LAUNCH(prof, (conv3x3_halo_kernel<BM, BN, WGM, WGN, BS>), dim3(grid), dim3(64 * WGM * WGN), lds, stream, a);
+}
+
+static void launch_8ph(ConvArgs a, int KS, hipStream_t stream, ProfScope& prof) {
+  constexpr size_t lds = 2 * 2 * 256 * 128;  // 128 KiB (the epilogue's 256 x 256 bf16 image fits)
+  a.mt_n = (a.P + 255) / 256;
+  const int grid = ((a.mt_n + 7) / 8) * 8 * (a.N / 256);
+  if (KS == 3) {
+    allow_lds_once<conv_8ph_kernel<3>>(lds);
+    MOE_LAUNCH(prof, conv_8ph_kernel<3>, dim3(grid), dim3(512), lds, stream, a);
+  } else {
+    allow_lds_once<conv_8ph_kernel<1>>(lds);
+    MOE_LAUNCH(prof, conv_8ph_kernel<1>, dim3(grid), dim3(512), lds, stream, a);
+  }
+}
+
+// the 8-phase 256 x 256 kernel's operands: whole 256-column N tiles, 64-channel
+// slices, no statistics epilogue; "conv_8ph" 1 forces it where eligible, -1
+// (automatic) takes it for grids of at least one wave of the chip
+static bool ph8_ok(int C, int N, int KS) { return N % 256 == 0 && C % 64 == 0 && (KS * KS * (C / 64)) % 2 == 0; }
+static bool ph8_auto(long long P, int N, int KS) { return KS == 3 && ((P + 255) / 256) * (N / 256) >= 256; }
+// whether a forward (not PH / BT) of these operands takes conv_8ph_kernel
+static bool ph8_takes(long long P, int C, int N, int KS) {
+  return g_conv_8ph != 0 && ph8_ok(C, N, KS) && (g_conv_8ph > 0 || ph8_auto(P, N, KS));
+}
+
+// the halo kernel's operands: 3x3, stride 1 (forward, or the stride-1 data
+// gradient with the K-contiguous flipped weight), 64-channel multiples, whole
+// 128-column N tiles
+static bool halo_ok(const ConvArgs& a, int KS) {
+  return KS == 3 && a.st == 1 && a.sh == 0 && a.Hs == a.H && a.Ws == a.W && a.C % 64 == 0 && a.N % 128 == 0 &&
+         a.stats == nullptr;
+}
+
 template <bool BT, bool PH = false>
 static void launch_fwd_any(const ConvArgs& a, int KS, hipStream_t stream, ProfScope& prof) {
+  if constexpr (!BT && !PH) {
+    if (ph8_takes(a.P, a.C, a.N, KS)) {
+      launch_8ph(a, KS, stream, prof);
+      return;
+    }
+    if (g_conv_halo > 0 && halo_ok(a, KS)) {
+      if (g_conv_halo == 2) launch_halo<128, 128, 2, 2, 2>(a, stream, prof);
+      else launch_halo<256, 128, 4, 2, 3>(a, stream, prof);
+      return;
+    }
+  }
   const bool c32 = a.C % 64 != 0 || a.N % 64 != 0;  // 32-channel multiples: the 32-deep, 64-wide tiles only
   if (g_conv_big > 0 && !c32) {  // "conv_big" 1: the 8-wave 256 x 128 tile where N % 128 == 0
     if constexpr (PH) {
@@ -916,6 +1448,31 @@ static void launch_fwd_any(const ConvArgs& a, int KS, hipStream_t stream, ProfSc
     if (bm == 256) launch_fwd<1, 256, BT, false>(a, stream, prof);
     else if (bm == 64) launch_fwd<1, 64, BT, false>(a, stream, prof);
     else launch_fwd<1, 128, BT, false>(a, stream, prof);
+  }
+}
+
+// The forward with the extended epilogue (rtdetr_conv_fwd_act: the evaluation
+// forward's folded layers): the 8-phase kernel where it applies, else the
+// default tiles -- 64 / 128 rows (fwd_bm), 32-deep K-tiles where k32_auto takes
+// them -- instantiated with EXT; the A/B tuning knobs are not consulted.
+template <int KS>
+static void launch_fwd_ext(const ConvArgs& a, hipStream_t stream, ProfScope& prof) {
+  if (ph8_takes(a.P, a.C, a.N, KS)) {
+    launch_8ph(a, KS, stream, prof);
+    return;
+  }
+  const bool w = a.N % 128 == 0;
+  const bool k32 = a.C % 64 != 0 || a.N % 64 != 0 || k32_auto(KS, a);
+  if (fwd_bm(a.P, a.N) == 64) {
+    if (k32) w ? launch_fwd_n<KS, 64, 128, false, false, 2, 2, 2, false, 32, true>(a, stream, prof)
+             : launch_fwd_n<KS, 64, 64, false, false, 2, 2, 2, false, 32, true>(a, stream, prof);
+    else w ? launch_fwd_n<KS, 64, 128, false, false, 2, 2, CV_STAGES, false, 64, true>(a, stream, prof)
+           : launch_fwd_n<KS, 64, 64, false, false, 2, 2, CV_STAGES, false, 64, true>(a, stream, prof);
+  } else {
+    if (k32) w ? launch_fwd_n<KS, 128, 128, false, false, 2, 2, 2, false, 32, true>(a, stream, prof)
+             : launch_fwd_n<KS, 128, 64, false, false, 2, 2, 2, false, 32, true>(a, stream, prof);
+    else w ? launch_fwd_n<KS, 128, 128, false, false, 2, 2, CV_STAGES, false, 64, true>(a, stream, prof)
+           : launch_fwd_n<KS, 128, 64, false, false, 2, 2, CV_STAGES, false, 64, true>(a, stream, prof);
   }
 }
 
@@ -972,10 +1529,37 @@ extern "C" int rtdetr_conv_fwd(const void* x, const void* w, void* y, const void
   return check_launch("rtdetr_conv_fwd");
 }
 
+extern "C" int rtdetr_conv_fwd_act(const void* x, const void* w, void* y, const void* zero, int B, int H, int W,
+                                   int C, int N, int KS, int stride, const float* bias, const void* resid, int act,
+                                   int resid_post, long long y_img_rows, long long y_row_off, hipStream_t stream) {
+  const void* ptrs[4] = {x, w, y, zero};
+  if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, stride, "rtdetr_conv_fwd_act", 32)) return rc;
+  if (!aligned16(bias) || !aligned16(resid)) return fail("rtdetr_conv_fwd_act: bias / resid must be 16-B aligned");
+  if (act < 0 || act > 2) return fail("rtdetr_conv_fwd_act: act must be 0 (none), 1 (ReLU) or 2 (SiLU)");
+  if (resid_post && resid == nullptr) return fail("rtdetr_conv_fwd_act: resid_post without resid");
+  if (B == 0) return 0;
+  const int Ho = conv_out(H, KS, stride), Wo = conv_out(W, KS, stride);
+  ConvArgs a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(y),
+             static_cast<const uint16_t*>(zero), B, Ho, Wo, C, N, B * Ho * Wo, 0, H, W, stride, 0,
+             bias, static_cast<const uint16_t*>(resid), nullptr, act};
+  a.resid_post = resid_post ? 1 : 0;
+  if (y_img_rows != 0 && (y_img_rows < (long long)Ho * Wo || y_row_off < 0 || y_row_off + (long long)Ho * Wo > y_img_rows))
+    return fail("rtdetr_conv_fwd_act: the output rows [y_row_off, y_row_off + Ho Wo) must lie within y_img_rows");
+  a.yS = y_img_rows;
+  a.yoff = y_row_off;
+  const double P = a.P;
+  ProfScope prof(stream, PROF_CONV, 2.0 * ((double)B * H * W * C + P * (N + (resid ? N : 0))) + 2.0 * N * KS * KS * C,
+                 false, 0.0, 2.0 * P * N * KS * KS * C);
+  if (KS == 3) launch_fwd_ext<3>(a, stream, prof);
+  else launch_fwd_ext<1>(a, stream, prof);
+  return check_launch("rtdetr_conv_fwd_act");
+}
+
 extern "C" int rtdetr_conv_fwd_stats_rows(int B, int H, int W, int C, int N, int KS, int stride) {
-  (void)C;
   if (B <= 0 || H <= 0 || W <= 0 || N <= 0 || (KS != 1 && KS != 3) || (stride != 1 && stride != 2)) return 0;
-  return fwd_bm((long long)B * conv_out(H, KS, stride) * conv_out(W, KS, stride), N);
+  const long long P = (long long)B * conv_out(H, KS, stride) * conv_out(W, KS, stride);
+  if (ph8_takes(P, C, N, KS)) return 256;  // the 8-phase kernel's 256-row M-tiles
+  return fwd_bm(P, N);
 }
 
 extern "C" int rtdetr_conv_fwd_stats(const void* x, const void* w, void* y, const void* zero, int B, int H, int W,
@@ -992,6 +1576,10 @@ extern "C" int rtdetr_conv_fwd_stats(const void* x, const void* w, void* y, cons
   const double P = a.P;
   ProfScope prof(stream, PROF_CONV, 2.0 * ((double)B * H * W * C + P * N) + 2.0 * N * KS * KS * C, false, 0.0,
                  2.0 * P * N * KS * KS * C);
+  if (ph8_takes(a.P, C, N, KS)) {  // 256-row partials (rtdetr_conv_fwd_stats_rows says so)
+    launch_8ph(a, KS, stream, prof);
+    return check_launch("rtdetr_conv_fwd_stats");
+  }
   const int bm = fwd_bm(a.P, N);  // (the default tiles: never the A/B "conv_big" shapes)
   if (KS == 3) {
     if (bm == 256) launch_fwd<3, 256, false, false>(a, stream, prof);
@@ -1164,6 +1752,14 @@ extern "C" int rtdetr_conv_set_tuning(const char* key, int value) {
   if (key == nullptr) return fail("rtdetr_conv_set_tuning: key is NULL");
   if (std::string(key) == "conv_bm") {
     g_conv_bm = value;
+    return 0;
+  }
+  if (std::string(key) == "conv_8ph") {
+    g_conv_8ph = value;
+    return 0;
+  }
+  if (std::string(key) == "conv_halo") {
+    g_conv_halo = value;
     return 0;
   }
   if (std::string(key) == "conv_big") {

@@ -122,6 +122,7 @@ SIGNATURES = {
     "rtdetr_attn_bwd": (_I, [_P, _LL, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _P, _P, _P, _LL, _P, _LL, _P, _LL,
                              _I, _I, _I, _I, _F, _P]),
     "rtdetr_conv_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
+    "rtdetr_conv_fwd_act": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _I, _I, _LL, _LL, _P]),
     "rtdetr_conv_fwd_stats_rows": (_I, [_I, _I, _I, _I, _I, _I, _I]),
     "rtdetr_conv_fwd_stats": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rtdetr_bn_act_fwd_part": (_I, [_P, _P, _P, _P, _P, _I, ctypes.c_longlong, _I, _I, _F, _F, _P, _I, _P, _P, _P]),

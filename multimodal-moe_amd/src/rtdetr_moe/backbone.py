@@ -253,6 +253,11 @@ class ConvNormLayer(nn.Module):
             return y + shift.view(1, -1, 1, 1).to(y.dtype)
         if self.act_name in (None, "silu") and _FUSED_BN:
             if not self.norm.training and not torch.is_grad_enabled():  # inference: running statistics
+                from . import evalfold
+
+                y = evalfold.conv_folded(self, x)  # BN (+ SiLU) folded into the convolution
+                if y is not None:
+                    return y
                 y = conv_module(self.conv, x)
                 if bn_eval_ok([y], [self.norm]):
                     return bn_act_eval([y], [self.norm], self.act_name)  # BN + SiLU in one HIP pass

@@ -81,6 +81,44 @@ def _fwd(x, w, bias=None, resid=None, relu=False, st=1):
     return y
 
 
+def conv_act_eval(x, w, bias, act, resid=None, st=1, out=None, out_row=0):
+    """Inference only (no autograd): act(conv(x, w) + bias) [+ resid after the
+    activation, bf16 SiLU-then-add] in one rtdetr_conv_fwd_act launch
+    (act 0 none, 1 ReLU, 2 SiLU): the folded BatchNorm / RepVgg layers of
+    evalfold.py.  out ([B, S, N] bf16, contiguous): write image b's Ho Wo
+    output rows at out[b, out_row:out_row + Ho Wo] instead (returns out)."""
+    from ..moe import _lib as L
+
+    x = _nhwc(x)
+    if x.data_ptr() % 16:
+        x = x.clone(memory_format=torch.channels_last)
+    if resid is not None:
+        resid = _nhwc(resid)
+        if resid.data_ptr() % 16:
+            resid = resid.clone(memory_format=torch.channels_last)
+    B, C, H, W = x.shape
+    N, _, ks, _ = w.shape
+    Ho, Wo = _out(H, ks, st), _out(W, ks, st)
+    if out is not None:
+        if resid is not None or not (out.dim() == 3 and out.shape[0] == B and out.shape[2] == N
+                                     and out.dtype == torch.bfloat16 and out.is_contiguous()
+                                     and 0 <= out_row and out_row + Ho * Wo <= out.shape[1]):
+            raise ValueError("conv_act_eval: out must be a contiguous bf16 [B, S, N] holding the rows")
+        y, rows = out, out.shape[1]
+    else:
+        y = torch.empty((B, N, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        rows = 0
+    if resid is not None and resid.shape != y.shape:
+        raise ValueError(f"conv_act_eval: resid {tuple(resid.shape)} vs output {tuple(y.shape)}")
+    L._check(L.lib().rtdetr_conv_fwd_act(x.data_ptr(), w.data_ptr(), y.data_ptr(), _zero(x.device).data_ptr(),
+                                         B, H, W, C, N, ks, st, bias.data_ptr(),
+                                         None if resid is None else resid.data_ptr(), int(act),
+                                         1 if resid is not None else 0, rows, int(out_row) if rows else 0,
+                                         L._stream()),
+             "rtdetr_conv_fwd_act")
+    return y
+
+
 def _stats_blocks(x, w, st=1):
     """Row blocks of rtdetr_conv_fwd_stats' BatchNorm partials for y =
     conv(x, w) (0: too many for the BatchNorm finalize -- take bn_stats)."""

@@ -543,6 +543,22 @@ class RTDETRDecoder(nn.Module):
         the levels.  GPU bf16 with the fused BatchNorm: each level's
         BatchNorm writes its rows of memory directly (_LevelMemory), its
         statistics summed in the convolution's epilogue."""
+        if _FUSED_BN and feats[0].is_cuda and not torch.is_grad_enabled():
+            from . import evalfold
+
+            # inference: each level's 1x1 conv with its BN folded writes its rows of the memory in place
+            if all(evalfold.folded(p, f) is not None and evalfold.folded(p, f)[3] == 1
+                   for p, f in zip(self.input_proj, feats)):
+                shapes = [tuple(f.shape[-2:]) for f in feats]
+                S = sum(h * w for h, w in shapes)
+                B = feats[0].shape[0]
+                mem = torch.empty((B, S, self.input_proj[0][0].out_channels), dtype=torch.bfloat16,
+                                  device=feats[0].device)
+                row = 0
+                for p, f, (h, w) in zip(self.input_proj, feats, shapes):
+                    evalfold.conv_folded(p, f, out=mem, out_row=row)
+                    row += h * w
+                return mem, shapes
         if _FUSED_BN and _LEVEL_MEMORY and feats[0].is_cuda:
             ys, parts, bns = [], [], []
             for p, f in zip(self.input_proj, feats):

@@ -12,6 +12,7 @@ from ..moe.config import MoEConfig
 from ..moe.layer import MoEFFN
 from .norm import AddLayerNorm
 from .backbone import _FUSED_BN, ConvNormLayer, stage_taps
+from . import evalfold
 from .conv import GradSlot, conv_module, conv_pair
 from .fused import bn_act, bn_act_eval, bn_act_ok, bn_eval_ok
 from .linear import TokenLinear, TokenSelfAttention
@@ -111,6 +112,9 @@ class RepVggBlock(nn.Module):
         if _FUSED_BN:
             norms = [self.conv1.norm, self.conv2.norm]
             if not self.conv1.norm.training and not torch.is_grad_enabled():  # inference: running statistics
+                y = evalfold.conv_folded(self, x, resid)  # both branches + BNs folded: one 3x3 conv + SiLU (+ r)
+                if y is not None:
+                    return y
                 y1, y2 = conv_pair(self.conv1.conv, self.conv2.conv, x)
                 if bn_eval_ok([y1, y2], norms):  # both BNs + sum + SiLU (+ shortcut) in one HIP pass
                     return bn_act_eval([y1, y2], norms, "silu", resid=resid)
@@ -139,6 +143,9 @@ class CSPRepLayer(nn.Module):
         c1, c2 = self.conv1, self.conv2
         if _FUSED_BN and not c1.fold and not c2.fold:
             if not c1.norm.training and not torch.is_grad_enabled():  # inference: running statistics
+                a1, a2 = evalfold.conv_folded(c1, x), evalfold.conv_folded(c2, x)  # BN + SiLU folded
+                if a1 is not None and a2 is not None:
+                    return self.conv3(self._bottlenecks_plus(a1, a2))
                 y1, y2 = conv_pair(c1.conv, c2.conv, x)
                 if bn_eval_ok([y1], [c1.norm]) and bn_eval_ok([y2], [c2.norm]):
                     a1, a2 = bn_act_eval([y1], [c1.norm], "silu"), bn_act_eval([y2], [c2.norm], "silu")
@@ -210,6 +217,9 @@ class HybridEncoder(nn.Module):
     def _proj(p, f):
         conv, bn = p[0], p[1]
         if _FUSED_BN:
+            y = evalfold.conv_folded(p, f)  # inference: the BN folded into the convolution
+            if y is not None:
+                return y
             y = conv_module(conv, f)
             if bn_eval_ok([y], [bn]):  # inference: running statistics, one HIP pass
                 return bn_act_eval([y], [bn], None)

@@ -72,6 +72,20 @@ class RTDETRMoE(nn.Module):
     def flops(self):
         return self.GFLOPs
 
+    def train(self, mode: bool = True):
+        """nn.Module.train, plus the inference re-parameterisation: entering
+        eval mode folds the running-statistics BatchNorms (and each RepVgg
+        block's 1x1 branch) into the convolutions (evalfold.refresh); entering
+        training marks the folds stale."""
+        super().train(mode)
+        from . import evalfold
+
+        if mode:
+            evalfold.invalidate(self)
+        else:
+            evalfold.refresh(self)
+        return self
+
     def moe_layers(self):
         return [m for m in self.modules() if isinstance(m, MoEFFN)]
 

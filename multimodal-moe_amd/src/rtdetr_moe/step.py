@@ -46,6 +46,34 @@ _ZERO = os.environ.get("MOE_ZERO", "1") != "0"
 CAPTURE_MODE = "thread_local"
 
 
+def _drop_autograd_graphs(model=None):
+    """Release the autograd graphs of the warm-up / capture passes now.  Two
+    things keep such a graph -- and the parameters' AccumulateGrad nodes in
+    it, which remember the side stream they were created on -- alive past the
+    capture: the MoE layers' cached aux-loss tensors (``last_aux``,
+    ``last_aux_weighted``: differentiable, they reach every parameter upstream
+    of the router) and the custom Functions' ctx reference cycles.  A later
+    pass on another stream (the re-capture's new side stream, bench.py's eager
+    profile steps) would then re-use the stale nodes and synchronise across
+    streams in every step (torch's "AccumulateGrad node's stream does not
+    match" warning).  The cached tensors are detached (same storage: their
+    values still follow graph replays) and the cycles collected."""
+    import gc
+
+    from ..moe.layer import MoEFFN
+
+    if model is not None:
+        for m in model.modules():
+            if isinstance(m, MoEFFN):
+                if m.last_aux is not None:
+                    m.last_aux = tuple(t.detach() if torch.is_tensor(t) else t for t in m.last_aux)
+                for name in ("last_aux_weighted", "ep_aux_weighted"):
+                    t = getattr(m, name, None)
+                    if torch.is_tensor(t):
+                        setattr(m, name, t.detach())
+    gc.collect()
+
+
 def release_graphs():
     """Before ``dist.destroy_process_group()``: free every unreachable captured
     graph (their captured RCCL kernels keep the communicator busy: the destroy
@@ -148,6 +176,8 @@ class GraphedModel:
             check_grad_slots()
         self.static_grads = [g if g is not None else torch.zeros_like(p) for g, p in zip(grads, params)]
         self.anchor = torch.zeros((), device=images.device, requires_grad=True)
+        del grads
+        _drop_autograd_graphs(self.fn if isinstance(self.fn, nn.Module) else None)
         torch.cuda.synchronize()
 
     def _run(self):
@@ -236,6 +266,8 @@ class GraphedStep:
             self.static_loss = loss.detach()
             self.static_losses = {k: v.detach() for k, v in losses.items()}
         self.static_grads = [g if g is not None else torch.zeros_like(p) for g, p in zip(grads, self.params)]
+        del loss, losses, grads
+        _drop_autograd_graphs(self.fn if isinstance(self.fn, nn.Module) else None)
         torch.cuda.synchronize()
         self.captures += 1
         if self.on_capture is not None:
@@ -444,6 +476,7 @@ class TrainStep:
             self.graphs = False
             for p in self.params:
                 p.grad = None
+            _drop_autograd_graphs(self.model)  # the captures' AccumulateGrad nodes (side stream) go too
 
     def _allreduce_grads(self):
         """Data-parallel gradient sum (GPU, world > 1): the replicated

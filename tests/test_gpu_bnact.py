@@ -160,3 +160,80 @@ def test_encoder_eval_bn_matches_torch_bn(hip_lib, monkeypatch):
             outs.append([o.float() for o in enc(feats, ctx)])
     for a, b in zip(*outs):
         torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * b.abs().max().item())
+
+
+@pytest.mark.parametrize("ks,st,act,resid", [(3, 1, 2, True), (3, 1, 2, False), (1, 1, 0, False), (3, 2, 2, False),
+                                             (1, 1, 1, False), (3, 1, 0, True)])
+def test_conv_act_eval_matches_torch(hip_lib, ks, st, act, resid):
+    """rtdetr_conv_fwd_act (the folded inference layers: conv + bias, ReLU /
+    SiLU, the shortcut added after the activation) against fp32 torch on the
+    same bf16 operands (one bf16 rounding of the conv, one of the activation,
+    one of the add: rtol 1e-2, atol 2e-2 x scale)."""
+    from src.rtdetr_moe.conv import conv_act_eval
+
+    g = torch.Generator().manual_seed(ks * 10 + st + act)
+    x = _cl(torch.randn(2, 256, 23, 40, generator=g))
+    w = _cl(torch.randn(128, 256, ks, ks, generator=g) * (256 * ks * ks) ** -0.5)
+    b = (torch.randn(128, generator=g) * 0.5).to(DEV)
+    Ho, Wo = (23 - 1) // st + 1, (40 - 1) // st + 1
+    r = _cl(torch.randn(2, 128, Ho, Wo, generator=g)) if resid else None
+    with torch.no_grad():
+        y = conv_act_eval(x, w, b, act, resid=r, st=st)
+        z = F.conv2d(x.float(), w.float(), b, stride=st, padding=(ks - 1) // 2)
+        ref = F.silu(z) if act == 2 else (z.relu() if act == 1 else z)
+        if resid:
+            ref = ref + r.float()
+    assert y.shape == ref.shape and y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=2e-2 * ref.abs().max().item())
+
+
+def test_encoder_eval_fold_matches_unfolded(hip_lib, monkeypatch):
+    """The HybridEncoder's inference forward with every running-statistics
+    BatchNorm folded into its convolution and each RepVgg block as ONE 3x3
+    convolution (evalfold: the 1x1 branch in the centre tap, SiLU and the CSP
+    shortcut in the epilogue) against the unfolded inference path (conv + the
+    one-pass BatchNorm kernel): within bf16 rounding (the folded weights are
+    rounded once to bf16)."""
+    from src.rtdetr_moe import encoder, evalfold
+
+    torch.manual_seed(3)
+    enc = encoder.HybridEncoder().to(DEV).to(memory_format=torch.channels_last)
+    for m in enc.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.3, 0.3)
+            m.running_var.uniform_(0.5, 2.0)
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    enc.eval()
+    evalfold.refresh(enc)
+    n_fold = sum(hasattr(m, "_eval_fold") for m in enc.modules())
+    assert n_fold == 3 + 2 + 2 + 4 * (2 + 3), n_fold  # proj, lateral, downsample, CSP entries + RepVgg blocks
+    feats = [_cl(torch.randn(2, c, h, w)) for c, h, w in ((512, 46, 80), (1024, 23, 40), (2048, 12, 20))]
+    ctx = torch.zeros(2, dtype=torch.long, device=DEV)
+    outs = []
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        for on in (True, False):
+            monkeypatch.setattr(evalfold, "_ON", on)
+            outs.append([o.float() for o in enc(feats, ctx)])
+    for a, b in zip(*outs):
+        assert torch.isfinite(a).all()
+        torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * b.abs().max().item())
+
+
+def test_conv_act_eval_rows_into_memory(hip_lib):
+    """rtdetr_conv_fwd_act writing image b's output rows at out[b, row:row + Ho Wo]
+    (the folded input projections filling the decoder memory [B, S, N] in
+    place): bitwise the dense output, other rows untouched."""
+    from src.rtdetr_moe.conv import conv_act_eval
+
+    g = torch.Generator().manual_seed(5)
+    x = _cl(torch.randn(3, 512, 12, 20, generator=g))
+    w = _cl(torch.randn(256, 512, 1, 1, generator=g) * 512 ** -0.5)
+    b = torch.randn(256, generator=g).to(DEV)
+    dense = conv_act_eval(x, w, b, 0)
+    mem = torch.full((3, 300, 256), 7.0, dtype=torch.bfloat16, device=DEV)
+    got = conv_act_eval(x, w, b, 0, out=mem, out_row=40)
+    assert got is mem
+    ref = dense.flatten(2).permute(0, 2, 1)
+    assert torch.equal(mem[:, 40:280], ref)
+    assert (mem[:, :40] == 7).all() and (mem[:, 280:] == 7).all()

@@ -50,9 +50,14 @@ _KNOBS = {"auto": {}, "bm64_wg2_flip": dict(conv_bm=64, conv_wg_stages=2, conv_d
           # 32-deep K-tiles, ring depth 2 / 3 / 4 (128- and 64-row tiles)
           "k32_s2_flip": dict(conv_k32=1, conv_dgrad_flip=1), "k32_s3_inplace": dict(conv_k32=2, conv_dgrad_flip=0),
           "k32_s4_bm64": dict(conv_k32=3, conv_bm=64), "k32_s2_zero_rows": dict(conv_k32=1, conv_dgrad_phase=0),
-          "k32_off": dict(conv_k32=0)}
+          "k32_off": dict(conv_k32=0),
+          # the halo-staged 3x3 stride-1 kernel (256 x 128 / 128 x 128 tiles; the flipped-weight data gradient)
+          "halo256_flip": dict(conv_halo=1, conv_dgrad_flip=1), "halo128_flip": dict(conv_halo=2, conv_dgrad_flip=1),
+          "halo256_inplace": dict(conv_halo=1, conv_dgrad_flip=0), "halo_off": dict(conv_halo=0),
+          # the 256 x 256 eight-phase kernel (N % 256 == 0 and an even K-tile count; else the default tiles)
+          "ph8_flip": dict(conv_8ph=1, conv_dgrad_flip=1), "ph8_off": dict(conv_8ph=0)}
 _DEFAULTS = dict(conv_bm=0, conv_wg_stages=0, conv_dgrad_flip=-1, conv_wg_splits=0, conv_dgrad_phase=1, conv_big=0,
-                 conv_areg=0, conv_k32=-1)
+                 conv_areg=0, conv_k32=-1, conv_halo=-1, conv_8ph=-1)
 
 
 @pytest.mark.parametrize("knobs", list(_KNOBS))
@@ -60,7 +65,9 @@ _DEFAULTS = dict(conv_bm=0, conv_wg_stages=0, conv_dgrad_flip=-1, conv_wg_splits
                                           (2, 512, 128, 7, 9, 1), (2, 128, 256, 7, 9, 3), (1, 256, 512, 5, 3, 3),
                                           # 64-channel tiles (ResNet stage 1): output, input and both
                                           (2, 64, 64, 23, 40, 3), (2, 256, 64, 7, 9, 1), (2, 64, 256, 11, 13, 1),
-                                          (1, 64, 128, 5, 3, 3), (2, 128, 64, 9, 7, 3)])
+                                          (1, 64, 128, 5, 3, 3), (2, 128, 64, 9, 7, 3),
+                                          # one-row / one-column images, a row wider than the halo tile
+                                          (2, 64, 128, 1, 7, 3), (3, 64, 128, 6, 1, 3), (2, 128, 128, 3, 300, 3)])
 def test_conv_fwd_bwd_vs_fp32(hip_lib, B, C, N, H, W, ks, knobs):
     for k, v in _KNOBS[knobs].items():
         assert hip_lib.rtdetr_conv_set_tuning(k.encode(), v) == 0
@@ -140,8 +147,8 @@ def test_conv_dispatch_rules(hip_lib):
                            torch.zeros(64, 32, 3, 3, device=DEV, dtype=torch.bfloat16), 1, 1)
 
 
-@pytest.mark.parametrize("ks", [1, 3])
-def test_conv_fused_epilogues_match_separate_kernels(hip_lib, ks):
+@pytest.mark.parametrize("ks,halo", [(1, 0), (3, 0), (3, 1), (3, 2)])
+def test_conv_fused_epilogues_match_separate_kernels(hip_lib, ks, halo):
     """The forward epilogue relu((conv + resid) + bias) and the dgrad's ReLU
     mask equal the separate kernels they replace (rtdetr_add_bias_relu_nhwc,
     rtdetr_bias_act_nhwc, threshold_backward) bit for bit."""
@@ -155,15 +162,19 @@ def test_conv_fused_epilogues_match_separate_kernels(hip_lib, ks):
     w = (torch.randn(Co, Ci, ks, ks, device=DEV, generator=g) * (Ci * ks * ks) ** -0.5).to(torch.bfloat16).contiguous(**cl)
     bias = torch.randn(Co, device=DEV, generator=g) * 0.3
     resid = torch.randn(B, Co, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(**cl)
-    plain = C._fwd(x, w)
-    assert torch.equal(C._fwd(x, w, bias, resid, True), L.add_bias_relu_nhwc(plain, resid, bias))
-    assert torch.equal(C._fwd(x, w, bias, None, True), L.bias_act_nhwc(plain.clone(), bias, True))
-    gy = torch.randn(B, Co, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(**cl)
-    xr = torch.relu(x)  # a ReLU output feeding the convolution
-    gx_m, gw_m = C._bwd(xr, w, gy, True, True, True)
-    gx, gw = C._bwd(xr, w, gy, True, True, False)
-    torch.cuda.synchronize()
-    assert torch.equal(gx_m, torch.ops.aten.threshold_backward(gx, xr, 0)) and torch.equal(gw_m, gw)
+    assert hip_lib.rtdetr_conv_set_tuning(b"conv_halo", halo) == 0
+    try:
+        plain = C._fwd(x, w)
+        assert torch.equal(C._fwd(x, w, bias, resid, True), L.add_bias_relu_nhwc(plain, resid, bias))
+        assert torch.equal(C._fwd(x, w, bias, None, True), L.bias_act_nhwc(plain.clone(), bias, True))
+        gy = torch.randn(B, Co, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(**cl)
+        xr = torch.relu(x)  # a ReLU output feeding the convolution
+        gx_m, gw_m = C._bwd(xr, w, gy, True, True, True)
+        gx, gw = C._bwd(xr, w, gy, True, True, False)
+        torch.cuda.synchronize()
+        assert torch.equal(gx_m, torch.ops.aten.threshold_backward(gx, xr, 0)) and torch.equal(gw_m, gw)
+    finally:
+        hip_lib.rtdetr_conv_set_tuning(b"conv_halo", -1)
 
 
 @pytest.mark.parametrize("cin,width,stride,shortcut", [(512, 128, 1, True), (256, 128, 2, False), (1024, 256, 1, True),
@@ -271,13 +282,14 @@ def test_conv_stride2_dgrad_classes_match_zero_rows(hip_lib, B, C, N, H, W):
     assert torch.equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("alt", ["conv_big:1", "conv_k32:1", "conv_k32:2", "conv_k32:3"])
+@pytest.mark.parametrize("alt", ["conv_big:1", "conv_k32:1", "conv_k32:2", "conv_k32:3", "conv_8ph:1"])
 @pytest.mark.parametrize("ks", [3, 1])
 @pytest.mark.parametrize("stride", [1, 2])
 @pytest.mark.parametrize("flip", [1, 0])
 def test_conv_big_tile_bit_exact(hip_lib, stride, flip, alt, ks):
-    """The 8-wave 256 x 128 tile ("conv_big") and the 32-deep K-tiles
-    ("conv_k32", one k-step per stage) run every output element's K loop in
+    """The 8-wave 256 x 128 tile ("conv_big"), the 32-deep K-tiles
+    ("conv_k32", one k-step per stage) and the 256 x 256 eight-phase kernel
+    ("conv_8ph") run every output element's K loop in
     the same order as the 4-wave 128 x 128 tile: forward and data gradient bit
     for bit equal (128-channel shapes; 64-channel outputs keep the 64-wide
     tiles)."""
@@ -374,6 +386,7 @@ def test_conv_pair_matches_two_convolutions(hip_lib, C, N, H, W):
 
 
 @pytest.mark.parametrize("B,C,N,H,W,ks,st", [(8, 256, 256, 92, 160, 1, 1), (8, 256, 256, 46, 80, 3, 2),
+                                             (8, 256, 256, 92, 160, 3, 1),  # the 8-phase kernel: 256-row partials
                                              (2, 128, 256, 23, 40, 3, 1), (1, 64, 128, 7, 9, 1, 1)])
 def test_conv_fwd_stats_partials(hip_lib, B, C, N, H, W, ks, st):
     """rtdetr_conv_fwd_stats: the output equals rtdetr_conv_fwd's bit for bit,

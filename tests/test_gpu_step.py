@@ -361,3 +361,52 @@ def test_whole_step_deferred_weight_grads(hip_lib, precision):
         r = ref[id(p)]
         t = 1e-5 * tol[id(p)] + (2.0 ** -8 * (mag[id(p)] + r.abs()) if m.dtype == torch.bfloat16 else 0.0) + 1e-30
         assert bool(((m.double() - r).abs() <= t).all()), (tuple(p.shape), float(((m.double() - r).abs() - t).max()))
+
+
+_MISMATCH_CHILD = r"""
+import sys
+sys.path[:0] = [sys.argv[1] + "/multimodal-moe_amd", sys.argv[1]]
+import torch
+from tests.test_gpu_step import _setup, DEV
+from src.rtdetr_moe.step import TrainStep
+
+model, crit, images, targets, ctx = _setup(seed=6)
+nb = max(1.0, float(sum(len(t["boxes"]) for t in targets)))
+g = torch.Generator(device=DEV).manual_seed(9)
+big = [{"boxes": torch.rand(20, 4, device=DEV, generator=g) * 0.2 + 0.3,
+        "labels": torch.zeros(20, dtype=torch.int64, device=DEV)},
+       {"boxes": torch.rand(2, 4, device=DEV, generator=g) * 0.2 + 0.3,
+        "labels": torch.zeros(2, dtype=torch.int64, device=DEV)}]
+step = TrainStep(model, crit, images, ctx, graphs=True, world=1, precision="bf16", lr=1e-3,
+                 targets=targets, num_boxes=nb)
+step(images, ctx, targets, nb)
+step(images, ctx, big, 22.0)  # re-capture on a new side stream
+assert step.stepper.captures == 2
+step.use_eager()  # bench.py's eager profiling steps
+for _ in range(2):
+    step(images, ctx, targets, nb)
+torch.cuda.synchronize()
+print("CHILD_OK")
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_no_accumulate_grad_stream_mismatch(hip_lib):
+    """The warm-up / capture passes' autograd graphs are released right after
+    the capture (the MoE layers' cached aux-loss tensors detached, ctx cycles
+    collected): neither a re-capture on a new side stream nor bench.py's eager
+    profiling steps after ``use_eager()`` re-use an AccumulateGrad node created
+    on the capture stream (torch's "AccumulateGrad node's stream does not
+    match" warning: a hidden cross-stream synchronisation in every eager step).
+    Run in a fresh process: torch emits that warning once per process."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = str(Path(__file__).resolve().parents[1])
+    r = subprocess.run([sys.executable, "-c", _MISMATCH_CHILD, root], capture_output=True, text=True, timeout=280,
+                       cwd=root, env=dict(os.environ, PYTHONWARNINGS="always"))
+    assert r.returncode == 0 and "CHILD_OK" in r.stdout, r.stderr[-3000:]
+    assert "AccumulateGrad" not in r.stderr, r.stderr[-2000:]
