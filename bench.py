@@ -660,7 +660,11 @@ def main():
                     and rp_meta.get("batch") == batch)
         roof = rocprof_headline(roof, rp.get("grouped_gemm"), rp_src, rp_match)
         rd = roofline_entry(ksum.get("dispatch"), pmc.get("dispatch"), prof_elapsed,
-                            "permute_fwd / combine_fwd / combine_bwd")
+                            "dispatch kernels of this workload: combine_fwd (gate-weighted combine + residual) at "
+                            "C2 / C5; permute_fwd + combine_fwd / _bwd where rows are copied (the EP send layout, "
+                            "C4). The scatter half of the C2 dispatch has no kernel of its own: GEMM1 gathers the "
+                            "token rows through the row map in its LDS-DMA loads (its bytes are in the grouped-GEMM "
+                            "entry)")
         rd = rocprof_headline(rd, rp.get("dispatch"), rp_src, rp_match)
         kprof = {}
         for name, d in ksum.items():

@@ -484,13 +484,10 @@ extern "C" int moe_expert_ffn_fwd(int dtype, const void* x, const int32_t* src_t
   const size_t lds = 4 * kFfSlot;  // (+ the static bias array)
   // exactly the dynamic bytes: static (bias) + dynamic must stay within the 160 KB a CU has, or the
   // attribute is refused and the launch fails
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(expert_ffn_fwd_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-      return fail("expert_ffn_fwd: LDS attribute refused");
-    attr = true;
-  }
+  static unsigned long long attr = 0;  // per-device bitmask
+  if (int rc = allow_dyn_lds(reinterpret_cast<const void*>(expert_ffn_fwd_kernel), (int)lds, &attr,
+                             "expert_ffn_fwd: LDS attribute"))
+    return rc;
   // algorithmic bytes: both weights + biases once; per routed row X (d), H (F) and Yp (d)
   const double bb = bias16 ? 2.0 : 4.0;
   ProfScope prof(stream, PROF_GEMM, 4.0 * G * F * d + bb * G * (F + d), true, 2.0 * (2 * d + F), 4.0 * F * d);

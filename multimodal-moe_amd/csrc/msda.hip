@@ -1143,13 +1143,10 @@ extern "C" int rtdetr_msda_fused_bwd_det(const void* value, long long ldv, const
     ProfScope prof(stream, PROF_MSDA, (double)n_all * (8.0 + 16.0) + (double)B * H * L * (kVgTilesMax + 1) * 4);
     const size_t slds = ((size_t)((n + 255) / 256) * 4 * ntmax + kVgTilesMax + 4) * 4;
     if (slds > 150 * 1024) return fail("msda_fused_bwd_det: too many samples per group for the tile sort");
-    static bool sset = false;
-    if (!sset) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(msda_vgrad_sort_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
-        return fail("msda_fused_bwd_det: LDS attribute refused");
-      sset = true;
-    }
+    static unsigned long long sset = 0;  // per-device bitmask
+    if (int rc = allow_dyn_lds(reinterpret_cast<const void*>(msda_vgrad_sort_kernel), 150 * 1024, &sset,
+                               "msda_fused_bwd_det: LDS attribute"))
+      return rc;
     MOE_LAUNCH(prof, msda_vgrad_sort_kernel, dim3(B * H * L), dim3(256), slds, stream, rec, lv, L, (int)n, sorted,
                toff);
     if (int rc = check_launch("rtdetr_msda_fused_bwd_det (sort)")) return rc;
@@ -1159,23 +1156,17 @@ extern "C" int rtdetr_msda_fused_bwd_det(const void* value, long long ldv, const
   for (int l = 0; l < L; ++l) rows += hw_host[l];
   ProfScope prof(stream, PROF_MSDA, (double)n_all * (16.0 + 2.0 * D) + rows * B * H * D * 2.0);
   if (D == 32) {
-    static bool a32 = false;
-    if (!a32) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(msda_vgrad_tile_kernel<32>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return fail("msda_fused_bwd_det: LDS attribute refused");
-      a32 = true;
-    }
+    static unsigned long long a32 = 0;  // per-device bitmask
+    if (int rc = allow_dyn_lds(reinterpret_cast<const void*>(msda_vgrad_tile_kernel<32>), (int)lds, &a32,
+                               "msda_fused_bwd_det: LDS attribute"))
+      return rc;
     MOE_LAUNCH(prof, msda_vgrad_tile_kernel<32>, dim3(B * H * tiles_bh), dim3(256), lds, stream, sorted, toff, lv, go,
                S, Q, H, L, P, tiles_bh, ldv, gv);
   } else {
-    static bool a64 = false;
-    if (!a64) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(msda_vgrad_tile_kernel<64>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return fail("msda_fused_bwd_det: LDS attribute refused");
-      a64 = true;
-    }
+    static unsigned long long a64 = 0;  // per-device bitmask
+    if (int rc = allow_dyn_lds(reinterpret_cast<const void*>(msda_vgrad_tile_kernel<64>), (int)lds, &a64,
+                               "msda_fused_bwd_det: LDS attribute"))
+      return rc;
     MOE_LAUNCH(prof, msda_vgrad_tile_kernel<64>, dim3(B * H * tiles_bh), dim3(256), lds, stream, sorted, toff, lv, go,
                S, Q, H, L, P, tiles_bh, ldv, gv);
   }

@@ -1072,15 +1072,13 @@ extern "C" int moe_router_wgrad(const float* dlogits, const void* x, const int32
     using K = RwCfg<EM_>;                                                                                     \
     const int ncb = d / K::CW;                                                                                \
     const int grid = dcb != nullptr && C > ncb ? C : ncb;                                                     \
-    static bool lds_set = false; /* > 64 KiB of dynamic LDS at E > 32 */                                      \
-    if (!lds_set) {                                                                                           \
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(router_wgrad_kernel<EM_, true>),                  \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::lds()) != hipSuccess ||     \
-          hipFuncSetAttribute(reinterpret_cast<const void*>(router_wgrad_kernel<EM_, false>),                 \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::lds()) != hipSuccess)       \
-        return fail("router_wgrad: LDS attribute refused");                                                   \
-      lds_set = true;                                                                                         \
-    }                                                                                                         \
+    static unsigned long long lds_v = 0, lds_s = 0; /* per device; > 64 KiB of dynamic LDS at E > 32 */      \
+    if (int rc = allow_dyn_lds(reinterpret_cast<const void*>(router_wgrad_kernel<EM_, true>), (int)K::lds(),  \
+                               &lds_v, "router_wgrad"))                                                       \
+      return rc;                                                                                              \
+    if (int rc = allow_dyn_lds(reinterpret_cast<const void*>(router_wgrad_kernel<EM_, false>), (int)K::lds(), \
+                               &lds_s, "router_wgrad"))                                                       \
+      return rc;                                                                                              \
     if (E % 4 == 0)                                                                                           \
       MOE_LAUNCH(prof, (router_wgrad_kernel<EM_, true>), dim3(grid), dim3(K::NT), K::lds(), stream, dlogits,    \
                  static_cast<const uint16_t*>(x), ctx_img, T, tpi, E, d, C, dwg, dcb);                        \

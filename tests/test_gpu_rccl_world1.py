@@ -42,7 +42,10 @@ def _port():
 
 @contextmanager
 def _world1(backend):
+    from src.rtdetr_moe.step import release_graphs
+
     kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
+    release_graphs()  # earlier tests' unreachable graphs go before the communicator exists
     dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1, **kw)
     try:
         yield dist.group.WORLD
