@@ -322,6 +322,9 @@ def setup_dist(n_gpus):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
+        from src.rtdetr_moe.step import rccl_env
+
+        rccl_env()
         # a rank that never arrives fails the job instead of hanging it
         dist.init_process_group("nccl", device_id=torch.device("cuda", local),
                                 timeout=timedelta(seconds=float(os.environ.get("MOE_DIST_TIMEOUT_S", "600"))))

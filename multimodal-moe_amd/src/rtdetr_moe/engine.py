@@ -411,6 +411,9 @@ def _mp_entry(local_idx, a, devices, port, out_file):
                        "WORLD_SIZE": str(len(devices)), "LOCAL_RANK": str(local_idx)})
     dev = devices[local_idx]
     torch.cuda.set_device(dev)
+    from .step import rccl_env
+
+    rccl_env()
     # collective timeout: a dead rank fails the run instead of hanging it
     dist.init_process_group("nccl", device_id=torch.device("cuda", dev),
                             timeout=timedelta(seconds=float(os.environ.get("MOE_DIST_TIMEOUT_S", "1800"))))
@@ -502,8 +505,10 @@ class EvalForward:
                     self._run(si, sc)
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
+            from .step import CAPTURE_MODE, quiesce_collectives
+
+            quiesce_collectives()  # training's eager collectives retired before the capture opens
             g = torch.cuda.CUDAGraph()
-            from .step import CAPTURE_MODE
 
             with torch.cuda.graph(g, stream=side, capture_error_mode=CAPTURE_MODE):
                 out = self._run(si, sc)

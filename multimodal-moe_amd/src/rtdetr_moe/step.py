@@ -37,13 +37,43 @@ _FUSED_CRIT = os.environ.get("MOE_FUSED_CRITERION", "1") != "0"  # A/B switch
 _ZERO = os.environ.get("MOE_ZERO", "1") != "0"
 
 # Stream-capture mode of every hipGraph capture (step graphs, the evaluation
-# forward): "thread_local".  Under the default "global" mode the RCCL process
-# group's watchdog thread, which polls the events of recent collectives, gets
-# hipErrorCapturedEvent while a capture that holds collectives (the C4
-# expert-parallel all-to-alls) is open, and terminates the process
-# (tools/rccl_capture_probe.py, gpurun_out/r6b); thread_local confines the
-# capture's restrictions to the capturing thread (gpurun_out/r6d).
+# forward): "thread_local", so that only the capturing thread is restricted.
+# It is NOT what keeps a capture that holds RCCL collectives (the C4
+# expert-parallel all-to-alls) alive -- quiesce_collectives is: the process
+# group's watchdog thread polls the end events of recent eager collectives,
+# and a poll that lands while the capture is open, with the RCCL stream joined
+# into it, fails with hipErrorCapturedEvent and terminates the process (in
+# either mode: tools/rccl_capture_probe.py, gpurun_out/r6b global, r6p
+# thread_local; with the drain: r6c).
 CAPTURE_MODE = "thread_local"
+# Seconds to let the RCCL watchdog retire the warm-up's eager collectives
+# before a capture opens (quiesce_collectives; its poll period is ~100 ms).
+_DRAIN_S = float(os.environ.get("MOE_CAPTURE_DRAIN_S", "0.5"))
+
+
+def rccl_env():
+    """Call before every ``init_process_group("nccl")``: one CUDA event per
+    collective instead of torch's recycled event cache, so that no event a
+    capture recorded (captured collectives' end events) is ever handed to an
+    eager collective that the watchdog then polls.  Together with
+    quiesce_collectives this leaves the watchdog only eagerly recorded,
+    completed events to look at."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+
+
+def quiesce_collectives():
+    """Before opening a capture while an RCCL group is live: drain the device,
+    then give the group's watchdog time to retire every completed eager
+    collective, so that none of their events is polled while the capture is
+    open (see CAPTURE_MODE).  No eager collective may be issued between this
+    call and the end of the capture."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    if "nccl" not in str(dist.get_backend()).lower():
+        return
+    torch.cuda.synchronize()
+    if _DRAIN_S > 0:
+        time.sleep(_DRAIN_S)
 
 
 def _drop_autograd_graphs(model=None):
@@ -158,6 +188,7 @@ class GraphedModel:
                 del out, grads
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        quiesce_collectives()
         self.pool = torch.cuda.graph_pool_handle()
         self.g_fwd = torch.cuda.CUDAGraph()
         # captured on the warm-up stream: the autograd nodes the warm-up created
@@ -257,6 +288,7 @@ class GraphedStep:
                 del loss, grads
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        quiesce_collectives()
         self.pool = torch.cuda.graph_pool_handle()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, pool=self.pool, stream=side,

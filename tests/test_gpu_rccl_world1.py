@@ -42,16 +42,15 @@ def _port():
 
 @contextmanager
 def _world1(backend):
-    from src.rtdetr_moe.step import release_graphs
+    from src.rtdetr_moe.step import rccl_env, release_graphs
 
     kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
     release_graphs()  # earlier tests' unreachable graphs go before the communicator exists
+    rccl_env()
     dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1, **kw)
     try:
         yield dist.group.WORLD
     finally:
-        from src.rtdetr_moe.step import release_graphs
-
         release_graphs()  # graphs holding captured RCCL kernels must go before the communicator
         dist.destroy_process_group()
 

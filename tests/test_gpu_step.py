@@ -107,6 +107,9 @@ def test_ep_world1_matches_single_gpu_layer(hip_lib, dtype, cf, epcf, rccl):
         with socket.socket() as s:
             s.bind(("127.0.0.1", 0))
             port = s.getsockname()[1]
+        from src.rtdetr_moe.step import rccl_env
+
+        rccl_env()
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     try:
         torch.manual_seed(0)
