@@ -289,6 +289,9 @@ def parse_args():
                          "<= 20 s, BASELINE.md 2)")
     ap.add_argument("--no-e2e-roofline", action="store_true", help="skip the model-FLOP count (roofline_e2e)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip per-launch HIP events")
+    ap.add_argument("--dump-prof-records", default=None, metavar="PATH",
+                    help="with --no-graphs: write the timed steps' per-launch library records (kind, ms, flops, "
+                         "algorithmic bytes, in launch order) as JSON (tools/gemm_traffic.py joins them with PMC)")
     ap.add_argument("--precision", choices=["bf16", "amp"], default="bf16",
                     help="bf16: bf16 GEMM/conv weights + fp32 master weights; amp: fp32 weights under bf16 autocast")
     ap.add_argument("--phase-timing", action="store_true",
@@ -611,6 +614,9 @@ def main():
         step.phases = None
     prof_steps = args.steps
     if timing and not graphs:
+        if args.dump_prof_records and rank == 0:
+            recs = [(L.PROF_KINDS.get(k, str(k)), ms, fl, by) for k, ms, fl, by in L.profile_records(clear=False)]
+            Path(args.dump_prof_records).write_text(json.dumps({"steps": args.steps, "records": recs}))
         L.TIMER.harvest()  # the K steps' launch records, read after the timed region
         L.TIMER.stop()
     elif timing:
