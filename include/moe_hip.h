@@ -850,6 +850,17 @@ int rtdetr_conv_dgrad_preflipped(const void* dy, const void* w, const void* wfli
 int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int KS);
 int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
                       const void* zero, int B, int H, int W, int C, int N, int KS, int stride, hipStream_t stream);
+/* rtdetr_conv_wgrad in two halves (round 6): rtdetr_conv_wgrad_part writes
+ * only the nsplit fp32 slices to part; rtdetr_conv_wgrad_reduce_batch sums
+ * the slices of n <= 48 weights (parts[q] [nsplits[q]][nws[q]] -> dws[q],
+ * bf16 if out_bf16 else fp32) in ONE launch, each exactly as
+ * rtdetr_conv_wgrad's own reduction (bitwise).  The training step defers the
+ * reductions of a whole backward to one or two such launches instead of one
+ * launch per convolution. */
+int rtdetr_conv_wgrad_part(const void* dy, const void* x, float* part, int nsplit, const void* zero, int B, int H,
+                           int W, int C, int N, int KS, int stride, hipStream_t stream);
+int rtdetr_conv_wgrad_reduce_batch(int n, const float* const* parts, const int* nsplits, const long long* nws,
+                                   void* const* dws, int out_bf16, hipStream_t stream);
 /* Measurement / A-B knobs (0, or -1 for conv_dgrad_flip, = automatic):
  * "conv_bm" forward pixel-tile rows 64 / 128 / 256; "conv_wg_stages"
  * weight-gradient LDS ring depth 2..4; "conv_wg_splits" weight-gradient pixel

@@ -1213,11 +1213,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgArgs a) {
 // slices k = group (mod 16) in increasing k, then group 0 adds the 16 sums in
 // group order (a weight with few output tiles is cut into up to 256 slices;
 // this keeps the sum spread over the chip and short per thread).
-__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part, int nsplit,
-                                                                long long n, void* __restrict__ dw, int out_bf16) {
-  __shared__ float4 red[15][16];
+__device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part, int nsplit, long long n,
+                                                  void* __restrict__ dw, int out_bf16, long long blk,
+                                                  float4 (&red)[15][16]) {
   const int col = threadIdx.x & 15, grp = threadIdx.x >> 4;
-  const long long i = (blockIdx.x * 16ll + col) * 4;
+  const long long i = (blk * 16ll + col) * 4;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < n) {
     for (int k = grp; k < nsplit; k += 16) {
@@ -1247,6 +1247,40 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __r
   } else {
     *reinterpret_cast<float4*>(static_cast<float*>(dw) + i) = s;
   }
+}
+
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part, int nsplit,
+                                                                long long n, void* __restrict__ dw, int out_bf16) {
+  __shared__ float4 red[15][16];
+  wgrad_reduce_body(part, nsplit, n, dw, out_bf16, blockIdx.x, red);
+}
+
+// The slice sums of up to kWgRedBatch weight gradients in ONE launch (round 6:
+// the training step defers every convolution's reduction to the end of the
+// backward, src/rtdetr_moe/conv.py deferred_wgrads): descriptor q owns blocks
+// [base[q], base[q + 1]); each block runs conv_wgrad_reduce_kernel's body, so
+// every dW is bitwise what its own reduction launch writes.  The table
+// travels as the kernel argument (no host-to-device copy inside a capture).
+constexpr int kWgRedBatch = 48;
+struct WgRedBatch {
+  const float* part[kWgRedBatch];
+  void* dw[kWgRedBatch];
+  long long n[kWgRedBatch];
+  int nsplit[kWgRedBatch];
+  int base[kWgRedBatch + 1];
+  int count, out_bf16;
+};
+
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_batch_kernel(WgRedBatch b) {
+  __shared__ float4 red[15][16];
+  const int bid = blockIdx.x;
+  int lo = 0, hi = b.count - 1;  // the last q with base[q] <= bid (uniform binary search)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (b.base[mid] <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  wgrad_reduce_body(b.part[lo], b.nsplit[lo], b.n[lo], b.dw[lo], b.out_bf16, bid - b.base[lo], red);
 }
 
 // (per device; a failure is reported through moe_last_error and the launch
@@ -1704,11 +1738,10 @@ extern "C" int rtdetr_conv_wgrad_splits(int B, int H, int W, int C, int N, int K
   return (int)std::max(1ll, s);
 }
 
-extern "C" int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
-                                 const void* zero, int B, int H, int W, int C, int N, int KS, int stride,
-                                 hipStream_t stream) {
-  const void* ptrs[5] = {dy, x, part, dw, zero};
-  if (int rc = conv_check(ptrs, 5, B, H, W, C, N, KS, stride, "rtdetr_conv_wgrad")) return rc;
+extern "C" int rtdetr_conv_wgrad_part(const void* dy, const void* x, float* part, int nsplit, const void* zero,
+                                      int B, int H, int W, int C, int N, int KS, int stride, hipStream_t stream) {
+  const void* ptrs[4] = {dy, x, part, zero};
+  if (int rc = conv_check(ptrs, 4, B, H, W, C, N, KS, stride, "rtdetr_conv_wgrad")) return rc;
   if (nsplit < 1 || nsplit > 256) return fail("rtdetr_conv_wgrad: nsplit must be 1..256");
   const int Ho = conv_out(H, KS, stride), Wo = conv_out(W, KS, stride);
   ConvWgArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(x), part,
@@ -1716,18 +1749,53 @@ extern "C" int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int
   const int ktot = (a.P + 63) / 64;
   a.kt_per = (ktot + nsplit - 1) / nsplit;
   const long long nw = (long long)N * KS * KS * C;
-  {
-    const double P = a.P;
-    ProfScope prof(stream, PROF_CONV, 2.0 * ((double)B * H * W * C + P * N) + 4.0 * nsplit * nw, false, 0.0,
-                   2.0 * P * nw);
-    if (KS == 3) launch_wgrad<3>(a, stream, prof);
-    else launch_wgrad<1>(a, stream, prof);
-    if (int rc = check_launch("rtdetr_conv_wgrad")) return rc;
-  }
+  const double P = a.P;
+  ProfScope prof(stream, PROF_CONV, 2.0 * ((double)B * H * W * C + P * N) + 4.0 * nsplit * nw, false, 0.0,
+                 2.0 * P * nw);
+  if (KS == 3) launch_wgrad<3>(a, stream, prof);
+  else launch_wgrad<1>(a, stream, prof);
+  return check_launch("rtdetr_conv_wgrad");
+}
+
+extern "C" int rtdetr_conv_wgrad(const void* dy, const void* x, float* part, int nsplit, void* dw, int out_bf16,
+                                 const void* zero, int B, int H, int W, int C, int N, int KS, int stride,
+                                 hipStream_t stream) {
+  if (dw == nullptr || reinterpret_cast<uintptr_t>(dw) % 16) return fail("rtdetr_conv_wgrad: dw NULL or unaligned");
+  if (int rc = rtdetr_conv_wgrad_part(dy, x, part, nsplit, zero, B, H, W, C, N, KS, stride, stream)) return rc;
+  const long long nw = (long long)N * KS * KS * C;
   ProfScope prof(stream, PROF_CONV, 4.0 * nsplit * nw + (out_bf16 ? 2.0 : 4.0) * nw);
   MOE_LAUNCH(prof, conv_wgrad_reduce_kernel, dim3((unsigned)((nw / 4 + 15) / 16)), dim3(256), 0, stream, part,
              nsplit, nw, dw, out_bf16);
   return check_launch("rtdetr_conv_wgrad (reduce)");
+}
+
+extern "C" int rtdetr_conv_wgrad_reduce_batch(int n, const float* const* parts, const int* nsplits,
+                                              const long long* nws, void* const* dws, int out_bf16,
+                                              hipStream_t stream) {
+  if (n < 1 || n > kWgRedBatch || parts == nullptr || nsplits == nullptr || nws == nullptr || dws == nullptr)
+    return fail("rtdetr_conv_wgrad_reduce_batch: 1..48 weights, non-NULL arrays");
+  WgRedBatch b{};
+  b.count = n;
+  b.out_bf16 = out_bf16 ? 1 : 0;
+  long long blocks = 0;
+  double bytes = 0.0;
+  for (int q = 0; q < n; ++q) {
+    if (parts[q] == nullptr || dws[q] == nullptr || nsplits[q] < 1 || nsplits[q] > 256 || nws[q] < 4 ||
+        nws[q] % 4 || (reinterpret_cast<uintptr_t>(parts[q]) | reinterpret_cast<uintptr_t>(dws[q])) % 16)
+      return fail("rtdetr_conv_wgrad_reduce_batch: bad descriptor (16-B aligned, nsplit 1..256, n % 4 == 0)");
+    b.part[q] = parts[q];
+    b.dw[q] = dws[q];
+    b.n[q] = nws[q];
+    b.nsplit[q] = nsplits[q];
+    b.base[q] = (int)blocks;
+    blocks += (nws[q] / 4 + 15) / 16;
+    bytes += 4.0 * nsplits[q] * nws[q] + (out_bf16 ? 2.0 : 4.0) * nws[q];
+  }
+  if (blocks > 0x7fffffffLL) return fail("rtdetr_conv_wgrad_reduce_batch: too many blocks");
+  b.base[n] = (int)blocks;
+  ProfScope prof(stream, PROF_CONV, bytes);
+  MOE_LAUNCH(prof, conv_wgrad_reduce_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, b);
+  return check_launch("rtdetr_conv_wgrad_reduce_batch");
 }
 
 extern "C" int rtdetr_conv3x3_direct_fwd(const void* x, const float* wf, const float* bias, void* y, int B, int H,

@@ -137,6 +137,8 @@ SIGNATURES = {
     "rtdetr_conv_wgrad_splits": (_I, [_I, _I, _I, _I, _I, _I]),
     "rtdetr_conv_set_tuning": (_I, [ctypes.c_char_p, _I]),
     "rtdetr_conv_wgrad": (_I, [_P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "rtdetr_conv_wgrad_part": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "rtdetr_conv_wgrad_reduce_batch": (_I, [_I, _P, _P, _P, _P, _I, _P]),
     "train_grad_pack": (_I, [_P, _P, _I, _P, _P]),
     "train_grad_sqnorm": (_I, [_P, _P, _I, _P, _P]),
     "train_grad_norm_finalize": (_I, [_P, _I, _F, _F, _P, _P, _I, _P, _P]),

@@ -84,6 +84,9 @@ class _FoldScale(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        from .conv import flush_wgrads
+
+        flush_wgrads()  # g may be a deferred convolution weight gradient (conv.deferred_wgrads)
         (scale,) = ctx.saved_tensors
         s = scale.view(-1, *([1] * (g.dim() - 1)))
         gw = torch.empty_like(g)
@@ -112,6 +115,9 @@ class _FoldAll(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
+        from .conv import flush_wgrads
+
+        flush_wgrads()  # the convolutions' deferred weight-gradient sums land before they are scaled
         plan = ctx.plan
         out, jobs = [], []
         for g, sc in zip(grads, plan.scales):

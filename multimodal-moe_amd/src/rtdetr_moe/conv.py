@@ -254,9 +254,80 @@ def _bwd(x, w, g, need_x, need_w, mask_input, add=None, st=1):
         ns = L.lib().rtdetr_conv_wgrad_splits(B, _out(H, ks, st), _out(W, ks, st), C, N, ks)
         part = torch.empty(ns * N * C * ks * ks, dtype=torch.float32, device=x.device)
         gw = torch.empty_like(w, memory_format=torch.channels_last)
-        L._check(L.lib().rtdetr_conv_wgrad(g.data_ptr(), x.data_ptr(), part.data_ptr(), ns, gw.data_ptr(), 1,
-                                           z, B, H, W, C, N, ks, st, s), "rtdetr_conv_wgrad")
+        pend = _WG_PENDING[0]
+        if pend is not None:  # the slice sum runs in the scope's batched reduction (deferred_wgrads)
+            L._check(L.lib().rtdetr_conv_wgrad_part(g.data_ptr(), x.data_ptr(), part.data_ptr(), ns, z, B, H, W,
+                                                    C, N, ks, st, s), "rtdetr_conv_wgrad_part")
+            pend.append((part, ns, N * C * ks * ks, gw))
+        else:
+            L._check(L.lib().rtdetr_conv_wgrad(g.data_ptr(), x.data_ptr(), part.data_ptr(), ns, gw.data_ptr(), 1,
+                                               z, B, H, W, C, N, ks, st, s), "rtdetr_conv_wgrad")
     return gx, gw
+
+
+# MOE_CONV_WG_DEFER=0: one slice-sum launch per convolution weight gradient
+# instead of the batched reduction at the end of the backward (A/B switch)
+_WG_DEFER_ON = os.environ.get("MOE_CONV_WG_DEFER", "1") != "0"
+# (part, nsplit, numel, gw) of the weight gradients whose slice sums are
+# pending, while a deferred_wgrads scope is open; None otherwise
+_WG_PENDING: list = [None]
+_WG_BATCH = 48  # descriptors per rtdetr_conv_wgrad_reduce_batch launch
+
+
+class deferred_wgrads:
+    """Scope of one backward pass (GraphedStep._grads): every HIP convolution's
+    weight gradient writes only its fp32 pixel slices (rtdetr_conv_wgrad_part)
+    and the slice sums of all of them run as one or two
+    rtdetr_conv_wgrad_reduce_batch launches -- bitwise the per-convolution
+    reductions -- when the scope closes, or earlier at flush_wgrads() (a
+    consumer of the gradients inside the backward: backbone._FoldAll).  Until
+    then the returned gradient tensors hold no values, so the scope is only
+    opened where nothing else reads them first: bf16 weights (no autocast
+    cast node between the parameter and the convolution), torch.autograd.grad
+    (no AccumulateGrad).  The ~94 small reduction launches of a C2 step were
+    0.62 ms of it (profiles/r05/c2/step_breakdown.txt)."""
+
+    def __init__(self, enabled=True):
+        self.on = bool(enabled) and _WG_DEFER_ON
+
+    def __enter__(self):
+        if self.on:
+            if _WG_PENDING[0] is not None:
+                raise RuntimeError("deferred_wgrads: scopes do not nest")
+            _WG_PENDING[0] = []
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        if self.on:
+            try:
+                if exc_type is None:
+                    flush_wgrads()
+            finally:
+                _WG_PENDING[0] = None
+        return False
+
+
+def flush_wgrads():
+    """Run the pending slice sums now (no-op outside a deferred_wgrads scope)."""
+    pend = _WG_PENDING[0]
+    if not pend:
+        return
+    import ctypes
+
+    from ..moe import _lib as L
+
+    s = L._stream()
+    for i in range(0, len(pend), _WG_BATCH):
+        chunk = pend[i:i + _WG_BATCH]
+        n = len(chunk)
+        parts = (ctypes.c_void_p * n)(*[c[0].data_ptr() for c in chunk])
+        nsplit = (ctypes.c_int * n)(*[c[1] for c in chunk])
+        numel = (ctypes.c_longlong * n)(*[c[2] for c in chunk])
+        dws = (ctypes.c_void_p * n)(*[c[3].data_ptr() for c in chunk])
+        cv = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+        L._check(L.lib().rtdetr_conv_wgrad_reduce_batch(n, cv(parts), cv(nsplit), cv(numel), cv(dws), 1, s),
+                 "rtdetr_conv_wgrad_reduce_batch")
+    pend.clear()
 
 
 class GradLink:

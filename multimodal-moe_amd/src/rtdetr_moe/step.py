@@ -266,13 +266,15 @@ class GraphedStep:
     def _grads(self, loss):
         """Gradients of every parameter: autograd for most, the conforming dense
         layers' weight + bias gradients batched after it (linear.DeferredWgrad)."""
-        from .conv import batched_flips
+        from .conv import batched_flips, deferred_wgrads
         from contextlib import nullcontext
 
         # bf16 weights live at fixed addresses: the convolutions' flipped weights in one launch
-        # (conv.batched_flips); autocast's per-step weight casts would not
+        # (conv.batched_flips); autocast's per-step weight casts would not.  The convolutions'
+        # weight-gradient slice sums batched at the end of the backward (conv.deferred_wgrads;
+        # under autocast the weight casts' backward reads each gradient at once)
         flips = nullcontext() if self.autocast else batched_flips(loss.device)
-        with deferred_weight_grads() as deferred, flips:
+        with deferred_weight_grads() as deferred, flips, deferred_wgrads(enabled=not self.autocast):
             grads = torch.autograd.grad(loss, self.params, allow_unused=True)
         check_grad_slots()
         self.deferred_layers = 0 if deferred is None else len(deferred.items)

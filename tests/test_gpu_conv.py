@@ -525,3 +525,72 @@ def test_stem_hip_matches_modules(hip_lib, monkeypatch):
             outs.append(m32._stem(x32))
     assert outs[0].dtype == torch.bfloat16
     _check(outs[0], outs[1], "stem under autocast")
+
+
+def test_wgrad_reduce_batch_matches_per_call(hip_lib):
+    """rtdetr_conv_wgrad_part + ONE rtdetr_conv_wgrad_reduce_batch over weights of different shapes and slice
+    counts (conv.deferred_wgrads) == rtdetr_conv_wgrad per weight, bitwise; a batch of 1..48, 16-B checks."""
+    from src.moe import _lib as L
+    from src.rtdetr_moe import conv as Cv
+
+    dev = torch.device("cuda")
+    torch.manual_seed(5)
+    cases = [(8, 128, 128, 92, 160, 3, 1), (8, 512, 256, 23, 40, 1, 1), (2, 64, 64, 46, 80, 3, 2),
+             (4, 256, 128, 23, 40, 3, 1), (1, 64, 128, 9, 7, 1, 1)]
+    xs, ws, gs = [], [], []
+    for B, C, N, H, W, ks, st in cases:
+        Ho, Wo = (H + 2 * (ks // 2) - ks) // st + 1, (W + 2 * (ks // 2) - ks) // st + 1
+        xs.append(torch.randn(B, C, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        ws.append((torch.randn(N, C, ks, ks, device=dev) * 0.05).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last))
+        gs.append(torch.randn(B, N, Ho, Wo, device=dev).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last))
+    ref = [Cv._bwd(x, w, g, False, True, False, st=c[6])[1] for x, w, g, c in zip(xs, ws, gs, cases)]
+    with Cv.deferred_wgrads():
+        got = [Cv._bwd(x, w, g, False, True, False, st=c[6])[1] for x, w, g, c in zip(xs, ws, gs, cases)]
+        assert len(Cv._WG_PENDING[0]) == len(cases)
+    assert Cv._WG_PENDING[0] is None
+    torch.cuda.synchronize()
+    for c, r, a in zip(cases, ref, got):
+        assert torch.equal(r, a), c
+    # argument checks (no launch)
+    import ctypes
+
+    one = (ctypes.c_void_p * 1)(None)
+    ns = (ctypes.c_int * 1)(1)
+    nw = (ctypes.c_longlong * 1)(4)
+    cv = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+    assert L.lib().rtdetr_conv_wgrad_reduce_batch(1, cv(one), cv(ns), cv(nw), cv(one), 1, None) != 0
+    assert L.lib().rtdetr_conv_wgrad_reduce_batch(49, cv(one), cv(ns), cv(nw), cv(one), 1, None) != 0
+
+
+def test_deferred_wgrads_backbone_bitwise(hip_lib):
+    """A PResNet-50 backward (frozen-BN folds: _FoldAll's backward flushes the pending sums first) with every
+    convolution's weight-gradient reduction deferred and batched == the per-convolution reductions, bitwise,
+    for every parameter gradient."""
+    from src.rtdetr_moe import conv as Cv
+    from src.rtdetr_moe.backbone import PResNet
+
+    torch.manual_seed(0)
+    m = PResNet(50).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for mod in m.modules():
+        if hasattr(mod, "running_var") and not isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_var.uniform_(0.5, 2.0)
+            mod.weight.uniform_(0.5, 1.5)
+    x = torch.randn(2, 3, 128, 160, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    params = [p for p in m.parameters() if p.requires_grad]
+    res = []
+    for defer in (False, True):
+        outs = m(x)
+        loss = sum((o.float() * torch.linspace(-1, 1, o.numel(), device=DEV).view_as(o)).sum() for o in outs)
+        with Cv.deferred_wgrads(enabled=defer):
+            grads = torch.autograd.grad(loss, params, allow_unused=True)
+        torch.cuda.synchronize()
+        res.append([None if g is None else g.clone() for g in grads])
+    n = 0
+    for p, a, b in zip(params, res[0], res[1]):
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert torch.equal(a, b)
+            n += 1
+    assert n > 20, n
